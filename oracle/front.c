@@ -1,0 +1,363 @@
+/*
+ * front.c -- ORACLE (test infrastructure).  Per-8x8-block front end of the
+ * VarDCT encode: block DC, adaptive quantization, AC-strategy choice among the
+ * 8x8-class transforms (with the thesis hooks P and F), forward transforms,
+ * chroma-from-luma residual and quantization.
+ *
+ * [ext] libjxl stages restated (enc_ac_strategy.cc, enc_adaptive_quantization.cc,
+ * enc_transforms-inl.h, quant_weights.cc); not in /root/reference -> parity
+ * unpinned against libjxl.  The thesis hooks follow
+ * /root/reference/proposals/combined.diff:247-253 (F) and :270-274 (P).
+ * Every float operation order here is the contract the HIP kernel mirrors.
+ */
+#include <float.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "jxo_internal.h"
+
+/* ---------- default dequantization weights [ext quant_weights.cc] ---------- */
+static double mult_band(double v) { return v > 0 ? 1.0 + v : 1.0 / (1.0 - v); }
+
+static void get_quant_weights(int rows, int cols, const double bands_in[3][6],
+                              int nb, double out[3][64]) {
+  for (int c = 0; c < 3; c++) {
+    double bands[6];
+    bands[0] = bands_in[c][0];
+    for (int i = 1; i < nb; i++) bands[i] = bands[i - 1] * mult_band(bands_in[c][i]);
+    double scale = (nb - 1) / (1.4142135623730951 + 1e-6);
+    double rcpcol = scale / (cols - 1), rcprow = scale / (rows - 1);
+    for (int y = 0; y < rows; y++) {
+      double dy = y * rcprow;
+      for (int x = 0; x < cols; x++) {
+        double dx = x * rcpcol;
+        double pos = sqrt(dx * dx + dy * dy);
+        int idx = (int)pos;
+        if (idx > nb - 2) idx = nb - 2;
+        double frac = pos - idx;
+        double a = bands[idx], b = bands[idx + 1];
+        out[c][y * cols + x] = a * pow(b / a, frac);
+      }
+    }
+  }
+}
+
+void jxo_quant_weights(int kind, float out[3][64]) {
+  static const double dct8[3][6] = {{3150.0, 0.0, -0.4, -0.4, -0.4, -2.0},
+                                    {560.0, 0.0, -0.3, -0.3, -0.3, -0.3},
+                                    {512.0, -2.0, -1.0, 0.0, -1.0, -2.0}};
+  static const double dct4[3][6] = {{2200.0, 0.0, 0.0, 0.0},
+                                    {392.0, 0.0, 0.0, 0.0},
+                                    {112.0, -0.25, -0.25, -0.5}};
+  static const double dct4x8[3][6] = {
+      {2198.050556016380522, -0.96269623020744692, -0.76194253026666783, -0.6551140670773547},
+      {764.3655248643528689, -0.92630200888366945, -0.9675229603596517, -0.27845290869168118},
+      {527.107573587542228, -1.4594385811273854, -1.450082094097871593, -1.5843722511996204}};
+  double w[3][64];
+  if (kind == JXO_QK_DCT8) {
+    get_quant_weights(8, 8, dct8, 6, w);
+    for (int c = 0; c < 3; c++)
+      for (int i = 0; i < 64; i++) out[c][i] = (float)w[c][i];
+  } else if (kind == JXO_QK_DCT4) {
+    get_quant_weights(4, 4, dct4, 4, w);
+    for (int c = 0; c < 3; c++)
+      for (int y = 0; y < 8; y++)
+        for (int x = 0; x < 8; x++) out[c][y * 8 + x] = (float)w[c][(y / 2) * 4 + x / 2];
+  } else {
+    get_quant_weights(4, 8, dct4x8, 4, w);
+    for (int c = 0; c < 3; c++)
+      for (int y = 0; y < 8; y++)
+        for (int x = 0; x < 8; x++) out[c][y * 8 + x] = (float)w[c][(y / 2) * 8 + x];
+  }
+}
+
+/* [ext] natural coefficient order of an 8x8 varblock (zigzag) */
+void jxo_natural_order8(uint8_t order[64]) {
+  int cur = 1;
+  order[0] = 0;
+  for (int i = 0; i < 8; i++)
+    for (int j = 0; j <= i; j++) {
+      int x = j, y = i - j;
+      if (i & 1) {
+        int t = x;
+        x = y;
+        y = t;
+      }
+      if (x == 0 && y == 0) continue;
+      order[cur++] = (uint8_t)(y * 8 + x);
+    }
+  for (int ip = 7; ip > 0; ip--) {
+    int i = ip - 1;
+    for (int j = 0; j <= i; j++) {
+      int x = 7 - (i - j), y = 7 - j;
+      if (i & 1) {
+        int t = x;
+        x = y;
+        y = t;
+      }
+      order[cur++] = (uint8_t)(y * 8 + x);
+    }
+  }
+}
+
+/* ---------- frame scalars (host-side, double precision) ---------- */
+void jxo_frame_init(jxo_frame* f, uint32_t w, uint32_t h, const jxo_params* p) {
+  memset(f, 0, sizeof(*f));
+  f->w = w;
+  f->h = h;
+  f->bxs = (w + 7) / 8;
+  f->bys = (h + 7) / 8;
+  f->xp = f->bxs * 8;
+  f->yp = f->bys * 8;
+  f->gxs = (w + 255) / 256;
+  f->gys = (h + 255) / 256;
+  f->ngroups = f->gxs * f->gys;
+  f->lfxs = (w + 2047) / 2048;
+  f->lfys = (h + 2047) / 2048;
+  f->nlf = f->lfxs * f->lfys;
+  f->distance = p->distance;
+  f->effort = p->effort;
+  f->proposals = p->proposals;
+  double d = p->distance;
+  double qfb = 0.79 / d;
+  f->qf_base = (float)qfb;
+  long G = (long)floor(qfb * 1024.0 + 0.5);
+  if (G < 1) G = 1;
+  if (G > 73727) G = 73727;
+  f->G = (uint32_t)G;
+  f->inv_g = (float)(65536.0 / (double)G);
+  double t = 0.3 * pow(d / 0.3, 0.66);
+  if (t > d) t = d;
+  if (t < 0.5 * d) t = 0.5 * d;
+  double qdc_f = 1.12 / t;
+  if (qdc_f > 50.0) qdc_f = 50.0;
+  long qdc = (long)floor(qdc_f * 65536.0 / (double)G + 0.5);
+  if (qdc < 1) qdc = 1;
+  if (qdc > 65536) qdc = 65536;
+  f->qdc = (uint32_t)qdc;
+  static const double m_lf[3] = {1.0 / 4096.0, 1.0 / 512.0, 1.0 / 256.0};
+  for (int c = 0; c < 3; c++) {
+    f->dc_mul[c] = (float)((double)G * (double)qdc / 65536.0 / m_lf[c]);
+    f->dc_step[c] = (float)(65536.0 / (double)G / (double)qdc * m_lf[c]);
+  }
+  for (int k = 0; k < 3; k++) jxo_quant_weights(k, f->wts[k]);
+}
+
+/* ---------- transforms (fmaf chains, fixed order) ---------- */
+static float T8[8][8], T4[4][4];
+static int tables_ready = 0;
+static void init_tables(void) {
+  if (tables_ready) return;
+  for (int k = 0; k < 8; k++)
+    for (int n = 0; n < 8; n++)
+      T8[k][n] = (float)((k == 0 ? 1.0 : 1.4142135623730951) / 8.0 *
+                         cos(3.14159265358979323846 * (2 * n + 1) * k / 16.0));
+  for (int k = 0; k < 4; k++)
+    for (int n = 0; n < 4; n++)
+      T4[k][n] = (float)((k == 0 ? 1.0 : 1.4142135623730951) / 4.0 *
+                         cos(3.14159265358979323846 * (2 * n + 1) * k / 8.0));
+  tables_ready = 1;
+}
+
+/* 2D DCT of an R x C region (row stride 8) -> out[R][C]; rows first */
+static void dct2d(const float* in, int R, int C, float* out) {
+  float tmp[8][8];
+  const float* TC = C == 8 ? &T8[0][0] : &T4[0][0];
+  const float* TR = R == 8 ? &T8[0][0] : &T4[0][0];
+  for (int r = 0; r < R; r++)
+    for (int k = 0; k < C; k++) {
+      float acc = 0.0f;
+      for (int n = 0; n < C; n++) acc = fmaf(in[r * 8 + n], TC[k * C + n], acc);
+      tmp[r][k] = acc;
+    }
+  for (int k = 0; k < R; k++)
+    for (int c = 0; c < C; c++) {
+      float acc = 0.0f;
+      for (int n = 0; n < R; n++) acc = fmaf(tmp[n][c], TR[k * R + n], acc);
+      out[k * C + c] = acc;
+    }
+}
+
+/* forward transform of one channel of an 8x8 block into the coefficient
+ * layout of raw strategy t [ext enc_transforms-inl.h].  Slot 0 is unused by
+ * the AC coder (DC travels in the LF image). */
+void jxo_transform(int t, const float* px /* 8x8, stride 8 */, float* co) {
+  init_tables();
+  float o[64];
+  if (t == JXO_DCT8) {
+    dct2d(px, 8, 8, co);
+  } else if (t == JXO_DCT4X4) {
+    for (int sy = 0; sy < 2; sy++)
+      for (int sx = 0; sx < 2; sx++) {
+        dct2d(px + sy * 32 + sx * 4, 4, 4, o);
+        for (int iy = 0; iy < 4; iy++)
+          for (int ix = 0; ix < 4; ix++) co[(sy + 2 * iy) * 8 + sx + 2 * ix] = o[iy * 4 + ix];
+      }
+    float A = co[0], B = co[1], C = co[8], D = co[9];
+    co[0] = (((A + B) + C) + D) * 0.25f;
+    co[1] = (((A + B) - C) - D) * 0.25f;
+    co[8] = (((A - B) + C) - D) * 0.25f;
+    co[9] = (((A - B) - C) + D) * 0.25f;
+  } else if (t == JXO_DCT8X4) { /* two 4-row x 8-col halves stacked */
+    for (int sy = 0; sy < 2; sy++) {
+      dct2d(px + sy * 32, 4, 8, o);
+      for (int iy = 0; iy < 4; iy++)
+        for (int ix = 0; ix < 8; ix++) co[(sy + 2 * iy) * 8 + ix] = o[iy * 8 + ix];
+    }
+    float A = co[0], B = co[8];
+    co[0] = (A + B) * 0.5f;
+    co[8] = (A - B) * 0.5f;
+  } else { /* JXO_DCT4X8: two 8-row x 4-col halves side by side, stored transposed */
+    for (int sx = 0; sx < 2; sx++) {
+      dct2d(px + sx * 4, 8, 4, o);
+      for (int ry = 0; ry < 8; ry++)
+        for (int cx = 0; cx < 4; cx++) co[(sx + 2 * cx) * 8 + ry] = o[ry * 4 + cx];
+    }
+    float A = co[0], B = co[8];
+    co[0] = (A + B) * 0.5f;
+    co[8] = (A - B) * 0.5f;
+  }
+}
+
+/* [ext] default quant biases (decoder side, OpsinInverseMatrix defaults) */
+static const float kBias[4] = {1.0f - 0.05465007330715401f, 1.0f - 0.07005449891748593f,
+                               1.0f - 0.049935103337343655f, 0.145f};
+static inline float adjust_bias(int c, int q) {
+  if (q == 0) return 0.0f;
+  if (q == 1) return kBias[c];
+  if (q == -1) return -kBias[c];
+  return (float)q - kBias[3] / (float)q;
+}
+static inline int quant1(float v) {
+  float a = fabsf(v);
+  if (a < 0.58f) return 0;
+  int q = (int)(a + 0.5f);
+  if (q > (1 << 24)) q = 1 << 24;
+  return v < 0.0f ? -q : q;
+}
+static inline int bitlen(uint32_t v) {
+  int n = 0;
+  while (v) {
+    n++;
+    v >>= 1;
+  }
+  return n;
+}
+
+static int qkind(int t) {
+  return t == JXO_DCT8 ? JXO_QK_DCT8 : (t == JXO_DCT4X4 ? JXO_QK_DCT4 : JXO_QK_DCT4X8);
+}
+
+/* Quantize one block under strategy t.  Channel order Y, X, B (Y first: X/B
+ * subtract the dequantized Y -- CfL with ytox=0, ytob base 1.0).  Returns the
+ * rate/distortion cost; writes q[3][64] (X,Y,B order) if q != NULL. */
+float jxo_quantize_block(const jxo_frame* f, int t, const float px[3][64],
+                         float scale, int32_t q[3][64]) {
+  float co[3][64];
+  for (int c = 0; c < 3; c++) jxo_transform(t, px[c], co[c]);
+  const int qk = qkind(t);
+  float yd[64];
+  int bits = 0;
+  float dist = 0.0f;
+  static const int corder[3] = {1, 0, 2};
+  for (int ci = 0; ci < 3; ci++) {
+    const int c = corder[ci];
+    int nz = 0;
+    for (int k = 1; k < 64; k++) {
+      const float ws = f->wts[qk][c][k] * scale;
+      float r = co[c][k];
+      if (c == 2) r = r - yd[k];
+      const float v = r * ws;
+      const int qq = quant1(v);
+      if (c == 1) yd[k] = adjust_bias(1, qq) / ws;
+      const uint32_t aq = (uint32_t)(qq < 0 ? -qq : qq);
+      const float e = fabsf(v) - (float)aq;
+      dist += e * e;
+      if (aq) {
+        bits += 2 + 2 * bitlen(aq);
+        nz++;
+      }
+      if (q) q[c][k] = qq;
+    }
+    bits += bitlen((uint32_t)nz);
+    if (q) q[c][0] = 0;
+  }
+  static const float tmul[14] = {1.0f, 0, 0, 1.05f, 0, 0, 0, 0, 0, 0, 0, 0, 1.02f, 1.02f};
+  return ((float)bits + 8.0f * dist) * tmul[t];
+}
+
+/* block-level front end: pixels px[c][64] (X,Y,B), returns chosen strategy,
+ * writes qf raw (1..256), quantized AC and DC. */
+int jxo_front_block(const jxo_frame* f, const float px[3][64], const float* homog,
+                    int32_t q[3][64], int32_t dcq[3], int* qf_raw) {
+  /* block DC = mean (row-major float sum) */
+  float dc[3];
+  for (int c = 0; c < 3; c++) {
+    float s = 0.0f;
+    for (int i = 0; i < 64; i++) s += px[c][i];
+    dc[c] = s * (1.0f / 64.0f);
+  }
+  /* DC quantization: Y first, B residual against dequantized Y (base
+   * correlation b = 1.0, x = 0.0) */
+  int qy = dc[1] * f->dc_mul[1] >= 0.0f ? (int)(dc[1] * f->dc_mul[1] + 0.5f)
+                                        : -(int)(-(dc[1] * f->dc_mul[1]) + 0.5f);
+  float ydq = (float)qy * f->dc_step[1];
+  float xv = dc[0] * f->dc_mul[0];
+  float bv = (dc[2] - ydq) * f->dc_mul[2];
+  dcq[1] = qy;
+  dcq[0] = xv >= 0.0f ? (int)(xv + 0.5f) : -(int)(-xv + 0.5f);
+  dcq[2] = bv >= 0.0f ? (int)(bv + 0.5f) : -(int)(-bv + 0.5f);
+
+  /* adaptive quantization: mean absolute gradient of Y inside the block */
+  const float* Y = px[1];
+  float act = 0.0f;
+  for (int y = 0; y < 8; y++)
+    for (int x = 0; x < 7; x++) act += fabsf(Y[y * 8 + x + 1] - Y[y * 8 + x]);
+  for (int y = 0; y < 7; y++)
+    for (int x = 0; x < 8; x++) act += fabsf(Y[(y + 1) * 8 + x] - Y[y * 8 + x]);
+  float am = act * (1.0f / 112.0f);
+  float mult = 1.5f / sqrtf(1.0f + am * 40.0f);
+  if (mult < 0.45f) mult = 0.45f;
+  if (mult > 1.5f) mult = 1.5f;
+  float qff = f->qf_base * mult;
+  int raw = (int)(qff * f->inv_g + 0.5f);
+  if (raw < 1) raw = 1;
+  if (raw > 256) raw = 256;
+  *qf_raw = raw;
+  const float scale = (float)f->G * (float)raw / 65536.0f;
+
+  /* AC strategy search over the 8x8-class candidates [ext
+   * FindBest8x8Transform], hook F on every estimate, hook P on a DCT8 win */
+  static const int cand[4] = {JXO_DCT8, JXO_DCT4X4, JXO_DCT4X8, JXO_DCT8X4};
+  const int ncand = f->effort >= 5 ? 4 : 1;
+  int best_t = JXO_DCT8;
+  if (ncand > 1) {
+    float best = FLT_MAX;
+    for (int i = 0; i < ncand; i++) {
+      float e = jxo_quantize_block(f, cand[i], px, scale, NULL);
+      if (f->proposals & 2) e = jxo_hook_f(e, homog[0], homog[1], homog[2]);
+      if (e < best) {
+        best = e;
+        best_t = cand[i];
+      }
+    }
+  }
+  if ((f->proposals & 1) && best_t == JXO_DCT8) {
+    /* HomogeneityPartition thresholds, combined.diff:219-234 */
+    float T = 1.60f;
+    if ((double)f->distance > 10.0)
+      T = 1.80f;
+    else if ((double)f->distance <= 3.0)
+      T = 1.50f;
+    const float rh = homog[0], rv = homog[1], rd = homog[2];
+    if (rd > T)
+      best_t = JXO_DCT4X4;
+    else if (rh > rv && rh > T)
+      best_t = JXO_DCT8X4;
+    else if (rv > rh && rv > T)
+      best_t = JXO_DCT4X8;
+  }
+  jxo_quantize_block(f, best_t, px, scale, q);
+  return best_t;
+}

@@ -1,0 +1,1012 @@
+"""ORACLE decoder (test infrastructure only -- never part of the product path).
+
+A minimal JPEG XL codestream decoder for the subset the encoder writes:
+bare codestream (0xFF0A), SizeHeader, all-default ImageMetadata (8-bit sRGB,
+xyb_encoded), one VarDCT frame with 8x8-class AC strategies, default
+quantization tables / block context map / coefficient orders, modular LF
+groups with local MA trees, prefix-code or ANS entropy streams, no LZ77, no
+loop filters.
+
+It is written from the decoder's side of the format ([ext] ISO/IEC 18181-1 /
+libjxl dec_*.cc; neither is in /root/reference, so parity with djxl is
+unpinned) and is the independent read-back that pins the encoder's bitstream
+layout: every test decodes the produced bytes, checks that the recovered
+AC strategies / quant field / quantized coefficients equal the encoder's, and
+measures PSNR with the reference harness formula
+(benchmark-jpegxl/src/image_reader.rs:555-606).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+
+class JxlError(Exception):
+    pass
+
+
+# ----------------------------------------------------------------------------
+# bit reader
+# ----------------------------------------------------------------------------
+class BitReader:
+    def __init__(self, data: bytes, start_bit: int = 0, end_bit: int | None = None):
+        self.data = bytes(data) + b"\0" * 16
+        self.pos = start_bit
+        self.end = len(data) * 8 if end_bit is None else end_bit
+
+    def read(self, n: int) -> int:
+        if n == 0:
+            return 0
+        p = self.pos >> 3
+        v = int.from_bytes(self.data[p:p + 9], "little") >> (self.pos & 7)
+        self.pos += n
+        if self.pos > self.end:
+            raise JxlError("read past end of section")
+        return v & ((1 << n) - 1)
+
+    def peek(self, n: int) -> int:
+        p = self.pos >> 3
+        v = int.from_bytes(self.data[p:p + 9], "little") >> (self.pos & 7)
+        return v & ((1 << n) - 1)
+
+    def skip(self, n: int):
+        self.pos += n
+        if self.pos > self.end:
+            raise JxlError("read past end of section")
+
+    def bool(self) -> bool:
+        return self.read(1) == 1
+
+    def pad(self):
+        self.pos = (self.pos + 7) & ~7
+
+    def u32(self, *dists):
+        sel = self.read(2)
+        d = dists[sel]
+        if d[0] == "v":
+            return d[1]
+        return self.read(d[1]) + d[2]
+
+    def u64(self) -> int:
+        sel = self.read(2)
+        if sel == 0:
+            return 0
+        if sel == 1:
+            return 1 + self.read(4)
+        if sel == 2:
+            return 17 + self.read(8)
+        v = self.read(12)
+        shift = 12
+        while self.read(1):
+            if shift == 60:
+                v |= self.read(4) << 60
+                break
+            v |= self.read(8) << shift
+            shift += 8
+        return v
+
+    def f16(self) -> float:
+        bits = self.read(16)
+        return float(np.frombuffer(np.uint16(bits).tobytes(), dtype=np.float16)[0])
+
+
+def ceil_log2(x: int) -> int:
+    n = 0
+    while (1 << n) < x:
+        n += 1
+    return n
+
+
+def unpack_signed(u: int) -> int:
+    return (u >> 1) ^ -(u & 1)
+
+
+# ----------------------------------------------------------------------------
+# entropy decoding
+# ----------------------------------------------------------------------------
+class PrefixCode:
+    """Brotli-style canonical prefix code read LSB-first."""
+
+    def __init__(self, lengths):
+        self.single = None
+        used = [(l, s) for s, l in enumerate(lengths) if l]
+        if len(used) == 0:
+            self.single = 0
+            return
+        if len(used) == 1 and used[0][0] == 0:
+            self.single = used[0][1]
+            return
+        maxlen = max(l for l, _ in used)
+        self.maxlen = maxlen
+        bl = [0] * 16
+        for l, _ in used:
+            bl[l] += 1
+        nxt = [0] * 17
+        c = 0
+        for b in range(1, 16):
+            c = (c + bl[b - 1]) << 1
+            nxt[b] = c
+        table_sym = np.zeros(1 << maxlen, dtype=np.int32)
+        table_len = np.zeros(1 << maxlen, dtype=np.int32)
+        filled = np.zeros(1 << maxlen, dtype=bool)
+        for s, l in enumerate(lengths):
+            if not l:
+                continue
+            code = nxt[l]
+            nxt[l] += 1
+            rev = int(format(code, "0%db" % l)[::-1], 2)
+            idx = np.arange(rev, 1 << maxlen, 1 << l)
+            if filled[idx].any():
+                raise JxlError("overlapping prefix code")
+            table_sym[idx] = s
+            table_len[idx] = l
+            filled[idx] = True
+        if not filled.all():
+            raise JxlError("incomplete prefix code")
+        self.sym = table_sym.tolist()
+        self.len = table_len.tolist()
+
+    def read(self, br: BitReader) -> int:
+        if self.single is not None:
+            return self.single
+        idx = br.peek(self.maxlen)
+        br.skip(self.len[idx])
+        return self.sym[idx]
+
+
+def read_simple_prefix(br: BitReader, alphabet: int):
+    max_bits = (alphabet - 1).bit_length() if alphabet > 1 else 0
+    nsym = br.read(2) + 1
+    syms = [br.read(max_bits) for _ in range(nsym)]
+    for s in syms:
+        if s >= alphabet:
+            raise JxlError("simple code symbol out of range")
+    if len(set(syms)) != len(syms):
+        raise JxlError("duplicate simple code symbols")
+    lengths = [0] * alphabet
+    if nsym == 1:
+        return _single(syms[0])
+    if nsym == 2:
+        for s in syms:
+            lengths[s] = 1
+    elif nsym == 3:
+        lengths[syms[0]] = 1
+        lengths[syms[1]] = 2
+        lengths[syms[2]] = 2
+    else:
+        if br.read(1):  # tree_select
+            lengths[syms[0]] = 1
+            lengths[syms[1]] = 2
+            lengths[syms[2]] = 3
+            lengths[syms[3]] = 3
+        else:
+            for s in syms:
+                lengths[s] = 2
+    return PrefixCode(lengths)
+
+
+def _single(sym):
+    p = PrefixCode([])
+    p.single = sym
+    return p
+
+
+K_CL_ORDER = [1, 2, 3, 4, 0, 5, 17, 6, 16, 7, 8, 9, 10, 11, 12, 13, 14, 15]
+# static code for code-length code lengths (4-bit peek -> (bits, value))
+K_CLCL = [(2, 0), (2, 4), (2, 3), (3, 2), (2, 0), (2, 4), (2, 3), (4, 1),
+          (2, 0), (2, 4), (2, 3), (3, 2), (2, 0), (2, 4), (2, 3), (4, 5)]
+
+
+def read_prefix_code(br: BitReader, alphabet: int) -> PrefixCode:
+    if alphabet == 1:
+        return _single(0)
+    hskip = br.read(2)
+    if hskip == 1:
+        return read_simple_prefix(br, alphabet)
+    cl = [0] * 18
+    space = 32
+    ncodes = 0
+    i = hskip
+    while i < 18 and space > 0:
+        b, v = K_CLCL[br.peek(4)]
+        br.skip(b)
+        cl[K_CL_ORDER[i]] = v
+        if v:
+            space -= 32 >> v
+            ncodes += 1
+        i += 1
+    if not (ncodes == 1 or space == 0):
+        raise JxlError("invalid code-length code")
+    if ncodes == 1:
+        only = [s for s in range(18) if cl[s]][0]
+        clcode = _single(only)
+    else:
+        clcode = PrefixCode(cl)
+    lengths = [0] * alphabet
+    sym = 0
+    prev_len = 8
+    repeat = 0
+    repeat_len = 0
+    space = 32768
+    while sym < alphabet and space > 0:
+        v = clcode.read(br)
+        if v < 16:
+            repeat = 0
+            lengths[sym] = v
+            sym += 1
+            if v:
+                prev_len = v
+                space -= 32768 >> v
+        else:
+            extra = 2 if v == 16 else 3
+            new_len = prev_len if v == 16 else 0
+            if repeat_len != new_len:
+                repeat = 0
+                repeat_len = new_len
+            old = repeat
+            if repeat > 0:
+                repeat = (repeat - 2) << extra
+            repeat += br.read(extra) + 3
+            delta = repeat - old
+            if sym + delta > alphabet:
+                raise JxlError("code length repeat overflow")
+            for k in range(delta):
+                lengths[sym + k] = repeat_len
+            sym += delta
+            if repeat_len:
+                space -= delta << (15 - repeat_len)
+    if space != 0:
+        raise JxlError("incomplete prefix code lengths")
+    return PrefixCode(lengths)
+
+
+class UintConfig:
+    def __init__(self, split_exp, msb, lsb):
+        self.split_exp, self.msb, self.lsb = split_exp, msb, lsb
+        self.split = 1 << split_exp
+
+    def read(self, token: int, br: BitReader) -> int:
+        if token < self.split:
+            return token
+        ml = self.msb + self.lsb
+        nbits = self.split_exp - ml + ((token - self.split) >> ml)
+        low = token & ((1 << self.lsb) - 1)
+        token >>= self.lsb
+        bits = br.read(nbits)
+        hi = (token & ((1 << self.msb) - 1)) | (1 << self.msb)
+        return (((hi << nbits) | bits) << self.lsb) | low
+
+
+def read_uint_config(br: BitReader, log_alpha: int) -> UintConfig:
+    split_exp = br.read(ceil_log2(log_alpha + 1))
+    msb = lsb = 0
+    if split_exp != log_alpha:
+        msb = br.read(ceil_log2(split_exp + 1))
+        if msb > split_exp:
+            raise JxlError("bad uint config")
+        lsb = br.read(ceil_log2(split_exp - msb + 1))
+        if msb + lsb > split_exp:
+            raise JxlError("bad uint config")
+    return UintConfig(split_exp, msb, lsb)
+
+
+def read_varlen_u8(br: BitReader) -> int:
+    if br.read(1):
+        n = br.read(3)
+        if n == 0:
+            return 1
+        return br.read(n) + (1 << n)
+    return 0
+
+
+def read_varlen_u16(br: BitReader) -> int:
+    if br.read(1):
+        n = br.read(4)
+        if n == 0:
+            return 1
+        return br.read(n) + (1 << n)
+    return 0
+
+
+# ANS: 12-bit precision, alias tables [ext dec_ans.cc]
+ANS_LOG_TAB = 12
+LOGCOUNT_CODE = {0: (5, 17), 1: (4, 11), 2: (4, 15), 3: (4, 3), 4: (4, 9), 5: (4, 7),
+                 6: (3, 4), 7: (3, 2), 8: (3, 5), 9: (3, 6), 10: (3, 0), 11: (6, 33),
+                 12: (7, 1), 13: (7, 65)}
+_LOGCOUNT_TABLE = {}
+for _sym, (_l, _c) in LOGCOUNT_CODE.items():
+    for _hi in range(1 << (7 - _l)):
+        _LOGCOUNT_TABLE[_c | (_hi << _l)] = (_l, _sym)
+
+
+def pop_count_precision(logcount: int, shift: int) -> int:
+    r = min(logcount, shift - ((ANS_LOG_TAB - logcount) >> 1))
+    return max(r, 0)
+
+
+def read_ans_histogram(br: BitReader):
+    total = 1 << ANS_LOG_TAB
+    if br.read(1):  # simple
+        nsym = br.read(1) + 1
+        syms = [read_varlen_u8(br) for _ in range(nsym)]
+        counts = [0] * (max(syms) + 1)
+        if nsym == 1:
+            counts[syms[0]] = total
+        else:
+            if syms[0] == syms[1]:
+                raise JxlError("bad simple ANS histogram")
+            counts[syms[0]] = br.read(ANS_LOG_TAB)
+            counts[syms[1]] = total - counts[syms[0]]
+        return counts
+    if br.read(1):  # flat
+        alpha = read_varlen_u8(br) + 1
+        base, rem = divmod(total, alpha)
+        return [base + (1 if i < rem else 0) for i in range(alpha)]
+    upper = (ANS_LOG_TAB + 1).bit_length() - 1
+    log = 0
+    while log < upper and br.read(1):
+        log += 1
+    shift = (br.read(log) | (1 << log)) - 1
+    if shift > ANS_LOG_TAB + 1:
+        raise JxlError("bad shift")
+    length = read_varlen_u8(br) + 3
+    logcounts = [0] * length
+    same = [0] * length
+    omit_log, omit_pos = -1, -1
+    i = 0
+    while i < length:
+        nb, v = _LOGCOUNT_TABLE[br.peek(7)]
+        br.skip(nb)
+        logcounts[i] = v
+        if v == ANS_LOG_TAB + 1:
+            rle = read_varlen_u8(br)
+            same[i] = rle + 5
+            i += rle + 4
+            continue
+        if v > omit_log:
+            omit_log, omit_pos = v, i
+        i += 1
+    if omit_pos < 0:
+        raise JxlError("bad histogram")
+    if omit_pos + 1 < length and logcounts[omit_pos + 1] == ANS_LOG_TAB + 1:
+        raise JxlError("bad histogram")
+    counts = [0] * length
+    prev = 0
+    numsame = 0
+    tot = 0
+    for i in range(length):
+        if same[i]:
+            numsame = same[i] - 1
+            prev = counts[i - 1] if i > 0 else 0
+        if numsame > 0:
+            counts[i] = prev
+            numsame -= 1
+        else:
+            code = logcounts[i]
+            if i == omit_pos or code == 0:
+                continue
+            if code == 1:
+                counts[i] = 1
+            else:
+                bc = pop_count_precision(code - 1, shift)
+                counts[i] = (1 << (code - 1)) + (br.read(bc) << (code - 1 - bc))
+        tot += counts[i]
+    counts[omit_pos] = total - tot
+    if counts[omit_pos] <= 0:
+        raise JxlError("bad histogram sum")
+    return counts
+
+
+def alias_table(counts, log_alpha):
+    table_size = 1 << log_alpha
+    entry = (1 << ANS_LOG_TAB) >> log_alpha
+    counts = list(counts) + [0] * (table_size - len(counts))
+    if len(counts) > table_size:
+        raise JxlError("histogram larger than alphabet")
+    nz = [i for i, c in enumerate(counts) if c]
+    cutoff = [0] * table_size
+    right = [0] * table_size
+    offset = [0] * table_size
+    if len(nz) == 1:
+        s = nz[0]
+        for i in range(table_size):
+            right[i] = s
+            offset[i] = i * entry
+            cutoff[i] = 0
+        return cutoff, right, offset, entry
+    cut = counts[:]
+    under, over = [], []
+    for i in range(table_size):
+        if cut[i] > entry:
+            over.append(i)
+        elif cut[i] < entry:
+            under.append(i)
+    while over:
+        o = over[-1]
+        u = under.pop()
+        by = entry - cut[u]
+        cut[o] -= by
+        right[u] = o
+        offset[u] = cut[o]
+        if cut[o] < entry:
+            over.pop()
+            under.append(o)
+        elif cut[o] == entry:
+            over.pop()
+    for i in range(table_size):
+        if cut[i] == entry:
+            right[i] = i
+            offset[i] = 0
+            cutoff[i] = 0
+        else:
+            offset[i] -= cut[i]
+            cutoff[i] = cut[i]
+    return cutoff, right, offset, entry
+
+
+class EntropyStream:
+    """DecodeHistograms + a symbol reader (prefix or ANS)."""
+
+    def __init__(self, br: BitReader, nctx: int):
+        if br.read(1):
+            raise JxlError("LZ77 streams are not produced by this encoder")
+        if nctx > 1:
+            self.ctxmap = read_context_map(br, nctx)
+        else:
+            self.ctxmap = [0]
+        nh = max(self.ctxmap) + 1
+        self.prefix = br.bool()
+        log_alpha = 15 if self.prefix else 5 + br.read(2)
+        self.cfgs = [read_uint_config(br, log_alpha) for _ in range(nh)]
+        if self.prefix:
+            alphas = [read_varlen_u16(br) + 1 for _ in range(nh)]
+            self.codes = [read_prefix_code(br, a) for a in alphas]
+        else:
+            self.tables = []
+            self.freqs = []
+            for _ in range(nh):
+                counts = read_ans_histogram(br)
+                if len(counts) > (1 << log_alpha):
+                    raise JxlError("ANS histogram too large")
+                self.freqs.append(counts + [0] * ((1 << log_alpha) - len(counts)))
+                self.tables.append(alias_table(counts, log_alpha))
+            self.log_alpha = log_alpha
+        self.state = None
+
+    def begin(self, br: BitReader):
+        if not self.prefix:
+            self.state = br.read(32)
+
+    def read_symbol(self, br: BitReader, h: int) -> int:
+        if self.prefix:
+            return self.codes[h].read(br)
+        cutoff, right, offset, entry = self.tables[h]
+        res = self.state & 0xFFF
+        i = res // entry
+        pos = res % entry
+        if pos >= cutoff[i]:
+            sym = right[i]
+            off = offset[i] + pos
+        else:
+            sym = i
+            off = pos
+        self.state = self.freqs[h][sym] * (self.state >> 12) + off
+        if self.state < (1 << 16):
+            self.state = ((self.state << 16) | br.read(16)) & 0xFFFFFFFF
+        return sym
+
+    def read(self, br: BitReader, ctx: int) -> int:
+        h = self.ctxmap[ctx]
+        tok = self.read_symbol(br, h)
+        return self.cfgs[h].read(tok, br)
+
+    def end(self):
+        if not self.prefix and self.state != 0x130000:
+            raise JxlError("ANS final state mismatch: %x" % self.state)
+
+
+def read_context_map(br: BitReader, n: int):
+    if br.read(1):  # simple
+        bits = br.read(2)
+        cm = [br.read(bits) for _ in range(n)]
+    else:
+        use_mtf = br.read(1)
+        es = EntropyStream(br, 1)
+        es.begin(br)
+        cm = [es.read(br, 0) for _ in range(n)]
+        es.end()
+        if use_mtf:
+            mtf = list(range(256))
+            out = []
+            for v in cm:
+                s = mtf[v]
+                out.append(s)
+                if v:
+                    mtf.pop(v)
+                    mtf.insert(0, s)
+            cm = out
+    nh = max(cm) + 1
+    if len(set(cm)) != nh:
+        raise JxlError("incomplete context map")
+    return cm
+
+
+# ----------------------------------------------------------------------------
+# modular sub-bitstreams
+# ----------------------------------------------------------------------------
+def read_tree(br: BitReader):
+    es = EntropyStream(br, 6)
+    es.begin(br)
+    nodes = []
+    to_decode = 1
+    leaf_id = 0
+    while to_decode > 0:
+        to_decode -= 1
+        prop = es.read(br, 1)
+        if prop > 256:
+            raise JxlError("bad tree property")
+        if prop == 0:
+            pred = es.read(br, 2)
+            off = unpack_signed(es.read(br, 3))
+            mlog = es.read(br, 4)
+            mbits = es.read(br, 5)
+            if pred > 13:
+                raise JxlError("bad predictor")
+            nodes.append(("leaf", leaf_id, pred, off, (mbits + 1) << mlog))
+            leaf_id += 1
+        else:
+            sv = unpack_signed(es.read(br, 0))
+            p = len(nodes)
+            nodes.append(("split", prop - 1, sv, p + to_decode + 1, p + to_decode + 2))
+            to_decode += 2
+    es.end()
+    return nodes, leaf_id
+
+
+def _predict(pred, img, x, y, w):
+    W = img[y][x - 1] if x > 0 else (img[y - 1][x] if y > 0 else 0)
+    if pred == 1:
+        return W
+    N = img[y - 1][x] if y > 0 else W
+    if pred == 2:
+        return N
+    NW = img[y - 1][x - 1] if (x > 0 and y > 0) else W
+    if pred == 3:
+        return (W + N) // 2
+    if pred == 5:
+        g = W + N - NW
+        lo, hi = min(W, N), max(W, N)
+        return min(max(g, lo), hi)
+    if pred == 8:
+        return NW
+    raise JxlError("predictor %d not supported by the test decoder" % pred)
+
+
+def read_modular(br: BitReader, channels):
+    """channels: list of (w, h).  Returns list of 2-D int lists."""
+    if br.read(1):
+        raise JxlError("global tree not produced by this encoder")
+    if not br.read(1):
+        raise JxlError("custom weighted-predictor header not produced")
+    ntr = br.u32(("v", 0), ("v", 1), ("b", 4, 2), ("b", 8, 18))
+    if ntr:
+        raise JxlError("modular transforms not produced")
+    nodes, nleaves = read_tree(br)
+    es = EntropyStream(br, nleaves)
+    es.begin(br)
+    out = []
+    for ci, (w, h) in enumerate(channels):
+        img = [[0] * w for _ in range(h)]
+        if w and h:
+            for y in range(h):
+                for x in range(w):
+                    n = nodes[0]
+                    i = 0
+                    while n[0] == "split":
+                        prop = n[1]
+                        if prop == 0:
+                            v = ci
+                        elif prop == 2:
+                            v = y
+                        elif prop == 3:
+                            v = x
+                        else:
+                            raise JxlError("property %d unsupported" % prop)
+                        i = n[3] if v > n[2] else n[4]
+                        n = nodes[i]
+                    _, leaf, pred, off, mul = n
+                    r = unpack_signed(es.read(br, leaf))
+                    p = 0 if pred == 0 else _predict(pred, img, x, y, w)
+                    img[y][x] = r * mul + off + p
+        out.append(img)
+    es.end()
+    return out
+
+
+# ----------------------------------------------------------------------------
+# VarDCT constants (decoder view)
+# ----------------------------------------------------------------------------
+STRATEGY_ORDER = [0, 1, 1, 1, 2, 3, 4, 4, 5, 5, 6, 6, 1, 1, 1, 1, 1, 1, 7, 8, 8, 9, 10, 10, 11, 12, 12]
+DEFAULT_CTX_MAP = [0, 1, 2, 2, 3, 3, 4, 5, 6, 6, 6, 6, 6,
+                   7, 8, 9, 9, 10, 11, 12, 13, 14, 14, 14, 14, 14,
+                   7, 8, 9, 9, 10, 11, 12, 13, 14, 14, 14, 14, 14]
+FREQ_CTX = [0, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 15, 16, 16, 17, 17, 18, 18,
+            19, 19, 20, 20, 21, 21, 22, 22, 23, 23, 23, 23, 24, 24, 24, 24, 25, 25, 25, 25, 26,
+            26, 26, 26, 27, 27, 27, 27, 28, 28, 28, 28, 29, 29, 29, 29, 30, 30, 30, 30]
+NNZ_CTX = [0, 0, 31, 62, 62, 93, 93, 93, 93, 123, 123, 123, 123, 152, 152, 152, 152, 152,
+           152, 152, 152, 180, 180, 180, 180, 180, 180, 180, 180, 180, 180, 180, 180] + [206] * 31
+QUANT_BIAS = (1.0 - 0.05465007330715401, 1.0 - 0.07005449891748593,
+              1.0 - 0.049935103337343655, 0.145)
+M_LF = (1.0 / 4096, 1.0 / 512, 1.0 / 256)
+OPSIN_BIAS = 0.0037930732552754493
+OPSIN_M = np.array([[0.30, 0.622, 0.078], [0.23, 0.692, 0.078],
+                    [0.24342268924547819, 0.20476744424496821, 0.55180986650955360]])
+
+
+def natural_order8():
+    order = [0]
+    for i in range(8):
+        for j in range(i + 1):
+            x, y = j, i - j
+            if i % 2:
+                x, y = y, x
+            if x == 0 and y == 0:
+                continue
+            order.append(y * 8 + x)
+    for ip in range(7, 0, -1):
+        i = ip - 1
+        for j in range(i + 1):
+            x, y = 7 - (i - j), 7 - j
+            if i % 2:
+                x, y = y, x
+            order.append(y * 8 + x)
+    return order
+
+
+def _weights(rows, cols, bands_in, nb):
+    out = np.zeros((3, rows * cols))
+    for c in range(3):
+        bands = [bands_in[c][0]]
+        for i in range(1, nb):
+            v = bands_in[c][i]
+            bands.append(bands[-1] * (1 + v if v > 0 else 1 / (1 - v)))
+        scale = (nb - 1) / (math.sqrt(2) + 1e-6)
+        for y in range(rows):
+            for x in range(cols):
+                pos = math.hypot(x * scale / (cols - 1), y * scale / (rows - 1))
+                idx = min(int(pos), nb - 2)
+                frac = pos - idx
+                a, b = bands[idx], bands[idx + 1]
+                out[c, y * cols + x] = a * (b / a) ** frac
+    return out
+
+
+def default_dequant():
+    """[kind] -> (3,64) dequant multipliers (1/weight) in coefficient layout."""
+    w8 = _weights(8, 8, [[3150.0, 0.0, -0.4, -0.4, -0.4, -2.0], [560.0, 0.0, -0.3, -0.3, -0.3, -0.3],
+                         [512.0, -2.0, -1.0, 0.0, -1.0, -2.0]], 6)
+    w4 = _weights(4, 4, [[2200.0, 0.0, 0.0, 0.0], [392.0, 0.0, 0.0, 0.0], [112.0, -0.25, -0.25, -0.5]], 4)
+    w48 = _weights(4, 8, [[2198.050556016380522, -0.96269623020744692, -0.76194253026666783, -0.6551140670773547],
+                          [764.3655248643528689, -0.92630200888366945, -0.9675229603596517, -0.27845290869168118],
+                          [527.107573587542228, -1.4594385811273854, -1.450082094097871593, -1.5843722511996204]], 4)
+    k4 = np.zeros((3, 64))
+    k48 = np.zeros((3, 64))
+    for y in range(8):
+        for x in range(8):
+            k4[:, y * 8 + x] = w4[:, (y // 2) * 4 + x // 2]
+            k48[:, y * 8 + x] = w48[:, (y // 2) * 8 + x]
+    return {0: 1.0 / w8, 3: 1.0 / k4, 12: 1.0 / k48, 13: 1.0 / k48}
+
+
+def _idct_mat(n):
+    m = np.zeros((n, n))
+    for k in range(n):
+        for x in range(n):
+            m[x, k] = (1.0 if k == 0 else math.sqrt(2)) * math.cos(math.pi * (2 * x + 1) * k / (2 * n))
+    return m  # pixels = m @ coeffs
+
+
+_I8, _I4 = _idct_mat(8), _idct_mat(4)
+
+
+def inverse_transform(t, co):
+    """co: 64 coefficients (layout of strategy t) -> 8x8 pixels."""
+    c = co.reshape(8, 8)
+    if t == 0:
+        return _I8 @ c @ _I8.T
+    out = np.zeros((8, 8))
+    if t == 3:
+        A, B, C, D = c[0, 0], c[0, 1], c[1, 0], c[1, 1]
+        dcs = [A + B + C + D, A + B - C - D, A - B + C - D, A - B - C + D]
+        for sy in range(2):
+            for sx in range(2):
+                blk = np.zeros((4, 4))
+                for iy in range(4):
+                    for ix in range(4):
+                        blk[iy, ix] = c[sy + 2 * iy, sx + 2 * ix]
+                blk[0, 0] = dcs[sy * 2 + sx]
+                out[4 * sy:4 * sy + 4, 4 * sx:4 * sx + 4] = _I4 @ blk @ _I4.T
+        return out
+    d0, d1 = c[0, 0], c[1, 0]
+    dcs = [d0 + d1, d0 - d1]
+    if t == 13:  # DCT8X4: two 4x8 (rows x cols) halves stacked
+        for sy in range(2):
+            blk = np.zeros((4, 8))
+            for iy in range(4):
+                blk[iy, :] = c[sy + 2 * iy, :]
+            blk[0, 0] = dcs[sy]
+            out[4 * sy:4 * sy + 4, :] = _I4 @ blk @ _I8.T
+        return out
+    if t == 12:  # DCT4X8: two 8x4 halves side by side, coefficients transposed
+        for sx in range(2):
+            blk = np.zeros((8, 4))  # [row freq][col freq]
+            for cx in range(4):
+                blk[:, cx] = c[sx + 2 * cx, :]
+            blk[0, 0] = dcs[sx]
+            out[:, 4 * sx:4 * sx + 4] = _I8 @ blk @ _I4.T
+        return out
+    raise JxlError("AC strategy %d not supported by the test decoder" % t)
+
+
+def xyb_to_srgb8(X, Y, B):
+    cb = OPSIN_BIAS ** (1.0 / 3.0)
+    L = Y + X + cb
+    M = Y - X + cb
+    S = B + cb
+    mixed = np.stack([L ** 3 - OPSIN_BIAS, M ** 3 - OPSIN_BIAS, S ** 3 - OPSIN_BIAS], axis=-1)
+    lin = mixed @ np.linalg.inv(OPSIN_M).T
+    lin = np.clip(lin, 0.0, 1.0)
+    srgb = np.where(lin <= 0.0031308, lin * 12.92, 1.055 * np.power(lin, 1 / 2.4) - 0.055)
+    return np.clip(np.floor(srgb * 255.0 + 0.5), 0, 255).astype(np.uint8)
+
+
+# ----------------------------------------------------------------------------
+# frame decoding
+# ----------------------------------------------------------------------------
+def _read_size(br):
+    return br.u32(("b", 9, 1), ("b", 13, 1), ("b", 18, 1), ("b", 30, 1))
+
+
+class Decoded:
+    pass
+
+
+def decode(data: bytes, want_pixels: bool = True) -> Decoded:
+    br = BitReader(data)
+    if br.read(16) != 0x0AFF:
+        raise JxlError("not a JPEG XL codestream")
+    if br.bool():
+        ys = (br.read(5) + 1) * 8
+        ratio = br.read(3)
+        if ratio:
+            raise JxlError("ratio sizes not produced")
+        xs = (br.read(5) + 1) * 8
+    else:
+        ys = _read_size(br)
+        if br.read(3):
+            raise JxlError("ratio sizes not produced")
+        xs = _read_size(br)
+    if not br.bool():
+        raise JxlError("only all-default ImageMetadata is produced")
+    br.pad()
+    # FrameHeader
+    if br.bool():
+        raise JxlError("all-default frame header not produced")
+    ftype = br.read(2)
+    enc = br.read(1)
+    flags = br.u64()
+    if ftype != 0 or enc != 0:
+        raise JxlError("only regular VarDCT frames")
+    if flags != 128:
+        raise JxlError("unexpected frame flags %d" % flags)
+    if br.u32(("v", 1), ("v", 2), ("v", 4), ("v", 8)) != 1:
+        raise JxlError("upsampling")
+    x_qm = br.read(3)
+    b_qm = br.read(3)
+    if br.u32(("v", 1), ("v", 2), ("v", 3), ("b", 3, 4)) != 1:
+        raise JxlError("passes")
+    if br.bool():
+        raise JxlError("crop")
+    if br.u32(("v", 0), ("v", 1), ("v", 2), ("b", 2, 3)) != 0:
+        raise JxlError("blending")
+    if not br.bool():
+        raise JxlError("is_last")
+    nlen = br.u32(("v", 0), ("b", 4, 0), ("b", 5, 16), ("b", 10, 48))
+    br.skip(8 * nlen)
+    if br.bool():
+        gab, epf = True, 1
+    else:
+        gab = br.bool()
+        if gab:
+            raise JxlError("gaborish not produced")
+        epf = br.read(2)
+        if epf:
+            raise JxlError("EPF not produced")
+        if br.u64():
+            raise JxlError("loop filter extensions")
+    if br.u64():
+        raise JxlError("frame extensions")
+    if gab or epf:
+        raise JxlError("default loop filters not produced")
+    bxs, bys = (xs + 7) // 8, (ys + 7) // 8
+    gxs, gys = (xs + 255) // 256, (ys + 255) // 256
+    ng = gxs * gys
+    lfxs, lfys = (xs + 2047) // 2048, (ys + 2047) // 2048
+    nlf = lfxs * lfys
+    # TOC
+    if br.bool():
+        raise JxlError("permuted TOC not produced")
+    br.pad()
+    nent = 1 if ng == 1 else 2 + nlf + ng
+    sizes = [br.u32(("b", 10, 0), ("b", 14, 1024), ("b", 22, 17408), ("b", 30, 4211712)) for _ in range(nent)]
+    br.pad()
+    base = br.pos >> 3
+    if base + sum(sizes) > len(data):
+        raise JxlError("truncated codestream: need %d bytes, have %d" % (base + sum(sizes), len(data)))
+    offs = []
+    o = base
+    for s in sizes:
+        offs.append(o)
+        o += s
+
+    def sec(i):
+        if nent == 1:
+            return shared
+        return BitReader(data, offs[i] * 8, (offs[i] + sizes[i]) * 8)
+
+    shared = BitReader(data, base * 8, (base + sizes[0]) * 8) if nent == 1 else None
+    d = Decoded()
+    d.xsize, d.ysize, d.bxs, d.bys = xs, ys, bxs, bys
+    d.section_sizes = sizes
+    # LfGlobal
+    s = sec(0)
+    if not s.bool():
+        raise JxlError("custom LF dequant not produced")
+    G = s.u32(("b", 11, 1), ("b", 11, 2049), ("b", 12, 4097), ("b", 16, 8193))
+    qdc = s.u32(("v", 16), ("b", 5, 1), ("b", 8, 1), ("b", 16, 1))
+    if not s.bool():
+        raise JxlError("custom block ctx map not produced")
+    if not s.bool():
+        raise JxlError("custom colour correlation not produced")
+    if s.bool():
+        raise JxlError("global tree not produced")
+    d.global_scale, d.quant_dc = G, qdc
+    d.dc = np.zeros((3, bys, bxs), dtype=np.int64)
+    d.acs = np.zeros((bys, bxs), dtype=np.int32)
+    d.qf = np.zeros((bys, bxs), dtype=np.int32)
+    for lg in range(nlf):
+        s = sec(1 + lg)
+        lgx, lgy = lg % lfxs, lg // lfxs
+        bx0, by0 = lgx * 256, lgy * 256
+        bw, bh = min(256, bxs - bx0), min(256, bys - by0)
+        if s.read(2):
+            raise JxlError("extra_precision not produced")
+        ch = read_modular(s, [(bw, bh)] * 3)
+        for mi, c in enumerate((1, 0, 2)):
+            d.dc[c, by0:by0 + bh, bx0:bx0 + bw] = np.array(ch[mi], dtype=np.int64)
+        count = s.read(ceil_log2(bw * bh)) + 1
+        cw, chh = (bw + 7) // 8, (bh + 7) // 8
+        meta = read_modular(s, [(cw, chh), (cw, chh), (count, 2), (bw, bh)])
+        if any(v for row in meta[0] for v in row) or any(v for row in meta[1] for v in row):
+            raise JxlError("non-zero CfL map not produced")
+        k = 0
+        covered = np.zeros((bh, bw), dtype=bool)
+        for y in range(bh):
+            for x in range(bw):
+                if covered[y, x]:
+                    continue
+                if k >= count:
+                    raise JxlError("too few varblocks")
+                t = meta[2][0][k]
+                if t not in (0, 3, 12, 13):
+                    raise JxlError("AC strategy %d not produced" % t)
+                d.acs[by0 + y, bx0 + x] = t
+                d.qf[by0 + y, bx0 + x] = 1 + min(max(meta[2][1][k], 0), 255)
+                covered[y, x] = True
+                k += 1
+        if k != count:
+            raise JxlError("varblock count mismatch")
+    # HfGlobal
+    s = sec(1 + nlf)
+    if not s.bool():
+        raise JxlError("custom dequant matrices not produced")
+    npresets = s.read(ceil_log2(ng)) + 1
+    used_orders = s.u32(("v", 0x5F), ("v", 0x13), ("v", 0), ("b", 13, 0))
+    if used_orders:
+        raise JxlError("custom coefficient orders not produced")
+    nctx_ac = 15 * (37 + 458)
+    hf = EntropyStream(s, npresets * nctx_ac)
+    order = natural_order8()
+    d.ac = np.zeros((bys, bxs, 3, 64), dtype=np.int64)
+    d.ac_tokens = np.zeros((ng, 3), dtype=np.int64)
+    for g in range(ng):
+        s = sec(2 + nlf + g)
+        gx, gy = g % gxs, g // gxs
+        bx0, by0 = gx * 32, gy * 32
+        gw, gh = min(32, bxs - bx0), min(32, bys - by0)
+        preset = s.read(ceil_log2(npresets))
+        off = preset * nctx_ac
+        hf.begin(s)
+        nzs = np.zeros((3, gh, gw), dtype=np.int64)
+        for by in range(gh):
+            for bx in range(gw):
+                t = int(d.acs[by0 + by, bx0 + bx])
+                ordi = STRATEGY_ORDER[t]
+                for c in (1, 0, 2):
+                    if bx == 0:
+                        pred = 32 if by == 0 else nzs[c, by - 1, bx]
+                    elif by == 0:
+                        pred = nzs[c, by, bx - 1]
+                    else:
+                        pred = (nzs[c, by - 1, bx] + nzs[c, by, bx - 1] + 1) // 2
+                    bctx = DEFAULT_CTX_MAP[(c ^ 1 if c < 2 else 2) * 13 + ordi]
+                    pp = min(int(pred), 64)
+                    bucket = pp if pp < 8 else 4 + pp // 2
+                    nz = hf.read(s, off + bucket * 15 + bctx)
+                    ntok = 1
+                    if nz + 1 > 64:
+                        raise JxlError("nzeros too large")
+                    nzs[c, by, bx] = nz
+                    zoff = off + 15 * 37 + 458 * bctx
+                    prev = 0 if nz > 4 else 1
+                    k = 1
+                    left = nz
+                    while k < 64 and left > 0:
+                        u = hf.read(s, zoff + (NNZ_CTX[left] + FREQ_CTX[k]) * 2 + prev)
+                        ntok += 1
+                        v = unpack_signed(u)
+                        d.ac[by0 + by, bx0 + bx, c, order[k]] = v
+                        prev = 1 if u else 0
+                        left -= prev
+                        k += 1
+                    if left:
+                        raise JxlError("nzeros not exhausted")
+                    d.ac_tokens[g, c] += ntok
+        hf.end()
+    d.x_qm, d.b_qm = x_qm, b_qm
+    if want_pixels:
+        d.rgb = reconstruct(d)
+    return d
+
+
+def reconstruct(d: Decoded) -> np.ndarray:
+    deq = default_dequant()
+    inv_gs = 65536.0 / d.global_scale
+    x_mul = 1.25 ** (2 - d.x_qm)  # scale 2 -> 1.0
+    b_mul = 1.25 ** (2 - d.b_qm)
+    dc_step = [M_LF[c] * inv_gs / d.quant_dc for c in range(3)]
+    X = np.zeros((d.bys * 8, d.bxs * 8))
+    Y = np.zeros_like(X)
+    B = np.zeros_like(X)
+    ac = d.ac.astype(np.float64)
+    # AdjustQuantBias
+    adj = np.where(np.abs(ac) == 1, np.sign(ac) * np.array(QUANT_BIAS[:3])[None, None, :, None],
+                   np.where(ac == 0, 0.0, ac - QUANT_BIAS[3] / np.where(ac == 0, 1, ac)))
+    for by in range(d.bys):
+        for bx in range(d.bxs):
+            t = int(d.acs[by, bx])
+            qf = d.qf[by, bx]
+            mul = deq[t] * (inv_gs / qf)
+            cy = adj[by, bx, 1] * mul[1]
+            cx = adj[by, bx, 0] * mul[0] * x_mul
+            cb = adj[by, bx, 2] * mul[2] * b_mul + cy  # ytob base 1.0
+            dcy = d.dc[1, by, bx] * dc_step[1]
+            dcx = d.dc[0, by, bx] * dc_step[0]
+            dcb = d.dc[2, by, bx] * dc_step[2] + dcy
+            for arr, co, dcv in ((X, cx, dcx), (Y, cy, dcy), (B, cb, dcb)):
+                co = co.copy()
+                co[0] = dcv
+                arr[by * 8:by * 8 + 8, bx * 8:bx * 8 + 8] = inverse_transform(t, co)
+    rgb = xyb_to_srgb8(X, Y, B)
+    return rgb[:d.ysize, :d.xsize]
+
+
+def mse_psnr(orig: np.ndarray, comp: np.ndarray):
+    """benchmark-jpegxl/src/image_reader.rs:555-606: f64 sum of squared sample
+    differences over W*H*3 / count; PSNR = 10*log10(255^2/MSE)."""
+    o = orig.astype(np.float64).ravel()
+    c = comp.astype(np.float64).ravel()
+    mse = float(np.sum((o - c) ** 2) / o.size)
+    psnr = float("inf") if mse == 0 else 10.0 * math.log10(255.0 * 255.0 / mse)
+    return mse, psnr

@@ -1,0 +1,137 @@
+"""ctypes binding of the CPU oracle (test infrastructure only).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module, and only as the checker.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+
+
+def build(force: bool = False):
+    if force or not os.path.exists(LIB) or any(
+            os.path.getmtime(os.path.join(HERE, f)) > os.path.getmtime(LIB)
+            for f in os.listdir(HERE) if f.endswith((".c", ".h"))):
+        subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+class _Params(ctypes.Structure):
+    _fields_ = [("distance", ctypes.c_float), ("effort", ctypes.c_int),
+                ("proposals", ctypes.c_uint32), ("coder", ctypes.c_int)]
+
+
+class _Result(ctypes.Structure):
+    _fields_ = [("xsize", ctypes.c_uint32), ("ysize", ctypes.c_uint32),
+                ("bxs", ctypes.c_uint32), ("bys", ctypes.c_uint32),
+                ("acs", ctypes.POINTER(ctypes.c_uint8)), ("qf", ctypes.POINTER(ctypes.c_uint8)),
+                ("dc", ctypes.POINTER(ctypes.c_int32)), ("ac", ctypes.POINTER(ctypes.c_int32)),
+                ("ac_tokens", ctypes.POINTER(ctypes.c_uint32)), ("homog", ctypes.POINTER(ctypes.c_float)),
+                ("global_scale", ctypes.c_uint32), ("quant_dc", ctypes.c_uint32),
+                ("bytes", ctypes.POINTER(ctypes.c_uint8)), ("nbytes", ctypes.c_size_t)]
+
+
+class _Xyb(ctypes.Structure):
+    _fields_ = [("plane", ctypes.c_void_p * 3), ("xsize", ctypes.c_size_t),
+                ("ysize", ctypes.c_size_t), ("stride", ctypes.c_size_t)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        _lib = ctypes.CDLL(LIB)
+        _lib.jxo_encode_rgb8.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                         ctypes.c_size_t, ctypes.POINTER(_Params), ctypes.POINTER(_Result)]
+        _lib.jxo_result_free.argtypes = [ctypes.POINTER(_Result)]
+        _lib.jxo_homog_map.argtypes = [ctypes.POINTER(_Xyb), ctypes.c_float, ctypes.c_int,
+                                       ctypes.c_void_p, ctypes.c_void_p]
+        _lib.jxo_homogeneity.argtypes = [ctypes.POINTER(_Xyb), ctypes.c_size_t, ctypes.c_size_t,
+                                         ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
+                                         ctypes.c_size_t, ctypes.c_float, ctypes.c_int]
+        _lib.jxo_homogeneity.restype = ctypes.c_float
+        _lib.jxo_hook_f.argtypes = [ctypes.c_float] * 4
+        _lib.jxo_hook_f.restype = ctypes.c_float
+        _lib.jxo_srgb8_to_xyb.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_size_t,
+                                          ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+        _lib.jxo_cbrtf.argtypes = [ctypes.c_float]
+        _lib.jxo_cbrtf.restype = ctypes.c_float
+    return _lib
+
+
+class OracleResult:
+    pass
+
+
+def encode(rgb: np.ndarray, distance=1.0, effort=7, proposals=0, coder=0) -> OracleResult:
+    rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
+    h, w, _ = rgb.shape
+    p = _Params(distance, effort, proposals, coder)
+    r = _Result()
+    st = lib().jxo_encode_rgb8(rgb.ctypes.data, w, h, w * 3, ctypes.byref(p), ctypes.byref(r))
+    if st != 0:
+        raise RuntimeError("oracle encode failed: %d" % st)
+    try:
+        o = OracleResult()
+        nb = r.bxs * r.bys
+        o.bxs, o.bys = r.bxs, r.bys
+        o.acs = np.ctypeslib.as_array(r.acs, (nb,)).copy().reshape(r.bys, r.bxs)
+        o.qf = np.ctypeslib.as_array(r.qf, (nb,)).copy().reshape(r.bys, r.bxs)
+        o.dc = np.ctypeslib.as_array(r.dc, (3 * nb,)).copy().reshape(3, r.bys, r.bxs)
+        o.ac = np.ctypeslib.as_array(r.ac, (nb * 192,)).copy().reshape(r.bys, r.bxs, 3, 64)
+        ng = ((w + 255) // 256) * ((h + 255) // 256)
+        o.ac_tokens = np.ctypeslib.as_array(r.ac_tokens, (ng * 3,)).copy().reshape(ng, 3)
+        o.homog = (np.ctypeslib.as_array(r.homog, (nb * 3,)).copy().reshape(r.bys, r.bxs, 3)
+                   if r.homog else None)
+        o.global_scale, o.quant_dc = r.global_scale, r.quant_dc
+        o.bytes = bytes(np.ctypeslib.as_array(r.bytes, (r.nbytes,)))
+        return o
+    finally:
+        lib().jxo_result_free(ctypes.byref(r))
+
+
+def _xyb_struct(planes: np.ndarray):
+    planes = np.ascontiguousarray(planes, dtype=np.float32)
+    _, ys, xs = planes.shape
+    s = _Xyb()
+    for c in range(3):
+        s.plane[c] = planes[c].ctypes.data
+    s.xsize, s.ysize, s.stride = xs, ys, xs
+    return s, planes
+
+
+def homog_map(planes: np.ndarray, distance: float, h1_mode: int = 0):
+    """planes: (3, Hp, Wp) float32 XYB.  Returns (r3 (bys,bxs,3), type (bys,bxs))."""
+    s, planes = _xyb_struct(planes)
+    _, ys, xs = planes.shape
+    r3 = np.zeros((ys // 8, xs // 8, 3), dtype=np.float32)
+    t = np.zeros((ys // 8, xs // 8), dtype=np.uint8)
+    lib().jxo_homog_map(ctypes.byref(s), distance, h1_mode, r3.ctypes.data, t.ctypes.data)
+    return r3, t
+
+
+def homogeneity(planes, x, y, xs, ys, bx, by, distance, h1_mode=0):
+    s, planes = _xyb_struct(planes)
+    return lib().jxo_homogeneity(ctypes.byref(s), x, y, xs, ys, bx, by, distance, h1_mode)
+
+
+def hook_f(ret, rh, rv, rd):
+    return lib().jxo_hook_f(ret, rh, rv, rd)
+
+
+def srgb8_to_xyb(rgb: np.ndarray) -> np.ndarray:
+    rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
+    h, w, _ = rgb.shape
+    xp, yp = (w + 7) // 8 * 8, (h + 7) // 8 * 8
+    out = np.zeros((3, yp, xp), dtype=np.float32)
+    lib().jxo_srgb8_to_xyb(rgb.ctypes.data, w, h, w * 3, xp, yp, out.ctypes.data)
+    return out
