@@ -1,0 +1,100 @@
+/*
+ * jxg.h -- C ABI of the MI355X-native JPEG XL VarDCT encode path.
+ *
+ * Drop-in boundary: this library replaces what the benchmark harness reaches
+ * through `docker exec ... /libjxl/build/tools/cjxl IN OUT --distance=D
+ * --effort=E` (pscoro/JPEG-XL-Lossy-Image-Compression-Thesis,
+ * benchmark-jpegxl/src/docker_manager.rs:100-137 DockerManager::execute_cjxl,
+ * called from benchmark-jpegxl/src/benchmark.rs:654-677).  The encoder
+ * internals it re-implements are libjxl's VarDCT heuristics with the thesis
+ * hooks of proposals/combined.diff (HomogeneityPartition :213-235 hooked into
+ * FindBest8x8Transform :270-274; EstimateEntropy factor :247-253).
+ *
+ * Conventions: status 0 = OK, negative on error (never aborts); one context
+ * per host thread; device memory is owned by the context; output buffers are
+ * allocated by the library and released with jxg_buffer_free.
+ */
+#ifndef JXG_H_
+#define JXG_H_
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  JXG_OK = 0,
+  JXG_ERR_INVALID_ARG = -1,
+  JXG_ERR_NO_DEVICE = -2,
+  JXG_ERR_HIP = -3,
+  JXG_ERR_OOM = -4,
+  JXG_ERR_UNSUPPORTED = -5,
+  JXG_ERR_INTERNAL = -6
+} jxg_status;
+
+/* proposals bitmask: the thesis patches (proposals/ directory) */
+#define JXG_PROPOSAL_P 1u /* homogeneity-partitioning.diff:272-276 */
+#define JXG_PROPOSAL_F 2u /* homogeneity-factored-entropy.diff:247-253 */
+
+/* flags */
+#define JXG_FLAG_H1_INT_ABS 1u /* thesis SML with int abs(int) */
+#define JXG_FLAG_KEEP_MAPS 2u  /* keep per-block maps for jxg_get_stats */
+
+typedef struct {
+  float distance;      /* cjxl --distance (butteraugli target), (0, 25] */
+  int effort;          /* cjxl --effort 1..9 (>=5: 8x8-class ACS search) */
+  uint32_t proposals;  /* JXG_PROPOSAL_* */
+  int num_devices;     /* informative; multi-GPU runs one context per rank */
+  uint32_t flags;      /* JXG_FLAG_* */
+  int device;          /* HIP device ordinal */
+} jxg_params;
+
+typedef struct {
+  uint8_t* data;
+  size_t size;
+} jxg_buffer;
+
+typedef struct {
+  uint32_t xsize, ysize, xsize_blocks, ysize_blocks;
+  uint32_t num_groups, num_lf_groups;
+  uint32_t global_scale, quant_dc;
+  size_t bytes;
+  /* valid until the next encode on this context (JXG_FLAG_KEEP_MAPS) */
+  const uint8_t* ac_strategy;  /* [ysize_blocks][xsize_blocks] raw strategy */
+  const uint8_t* quant_field;  /* raw quant field - 1 */
+  const int32_t* dc;           /* [3][blocks] quantized DC (X, Y, B) */
+  const int32_t* ac;           /* [blocks][3][64] quantized AC, natural order */
+  const uint32_t* ac_tokens;   /* [num_groups][3] AC token counts (X, Y, B) */
+  const float* homogeneity;    /* [blocks][3] r_h r_v r_d (if P|F) */
+  /* device time per stage, milliseconds (last encode) */
+  float ms_front, ms_histogram, ms_emit, ms_assemble, ms_total;
+} jxg_stats;
+
+const char* jxg_status_str(jxg_status s);
+jxg_status jxg_create(const jxg_params* params, void** ctx);
+void jxg_destroy(void* ctx);
+
+/* host RGB8 (interleaved, row_stride bytes per row) -> codestream */
+jxg_status jxg_encode_rgb8(void* ctx, const uint8_t* rgb, uint32_t xsize, uint32_t ysize,
+                           size_t row_stride, jxg_buffer* out);
+/* device-resident RGB8 (same layout, device pointer) -> codestream */
+jxg_status jxg_encode_rgb8_device(void* ctx, const void* d_rgb, uint32_t xsize,
+                                  uint32_t ysize, size_t row_stride, jxg_buffer* out);
+/* n frames of equal size (benchmark config 3: 64 x 1080p) */
+jxg_status jxg_encode_batch_rgb8(void* ctx, const uint8_t* const* rgbs, uint32_t n,
+                                 uint32_t xsize, uint32_t ysize, size_t row_stride,
+                                 jxg_buffer* outs);
+jxg_status jxg_get_stats(void* ctx, jxg_stats* stats);
+void jxg_buffer_free(jxg_buffer* buf);
+
+/* thesis selector alone over a host XYB frame [3][ysize][xsize] (xsize, ysize
+ * multiples of 8): r3 = (r_h, r_v, r_d) per block, type = raw strategy
+ * (combined.diff:183-235) */
+jxg_status jxg_homogeneity_map(void* ctx, const float* xyb, uint32_t xsize, uint32_t ysize,
+                               float distance, uint32_t flags, float* r3, uint8_t* type);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,343 @@
+// jxg_bitstream.cpp -- see jxg_bitstream.h.
+#include "jxg_bitstream.h"
+
+#include <algorithm>
+#include <cstring>
+
+namespace jxg {
+
+void hybrid_encode(uint32_t v, const UintCfg& c, uint32_t* tok, uint32_t* nb, uint32_t* bits) {
+  const uint32_t split = 1u << c.split_exp;
+  if (v < split) {
+    *tok = v;
+    *nb = 0;
+    *bits = 0;
+    return;
+  }
+  const uint32_t n = 31u - (uint32_t)__builtin_clz(v);
+  const uint32_t m = v - (1u << n);
+  *tok = split + ((n - c.split_exp) << (c.msb + c.lsb)) + ((m >> (n - c.msb)) << c.lsb) +
+         (v & ((1u << c.lsb) - 1));
+  *nb = n - c.msb - c.lsb;
+  *bits = (v >> c.lsb) & (*nb >= 32 ? 0xFFFFFFFFu : ((1u << *nb) - 1));
+}
+
+namespace {
+
+// Huffman code lengths.  Leaves ordered by (count, symbol); two-queue merge
+// that prefers the leaf queue on ties; if the deepest leaf exceeds maxlen the
+// counts become (c >> 1) | 1 and the construction repeats.
+void huffman_lengths(const uint32_t* counts_in, int n, int maxlen, uint8_t* len) {
+  std::vector<uint32_t> counts(counts_in, counts_in + n);
+  for (;;) {
+    std::vector<int> leaves;
+    for (int i = 0; i < n; i++) {
+      len[i] = 0;
+      if (counts[i]) leaves.push_back(i);
+    }
+    const int k = (int)leaves.size();
+    if (k == 0) return;
+    if (k == 1) {
+      len[leaves[0]] = 1;
+      return;
+    }
+    std::stable_sort(leaves.begin(), leaves.end(), [&](int a, int b) {
+      return counts[a] != counts[b] ? counts[a] < counts[b] : a < b;
+    });
+    std::vector<uint64_t> weight(2 * k);
+    std::vector<int> parent(2 * k, -1);
+    for (int i = 0; i < k; i++) weight[i] = counts[leaves[i]];
+    int next_leaf = 0, next_node = k, end = k;
+    while ((k - next_leaf) + (end - next_node) > 1) {
+      int pick[2];
+      for (int& p : pick) {
+        if (next_leaf < k && (next_node >= end || weight[next_leaf] <= weight[next_node]))
+          p = next_leaf++;
+        else
+          p = next_node++;
+      }
+      weight[end] = weight[pick[0]] + weight[pick[1]];
+      parent[pick[0]] = parent[pick[1]] = end;
+      end++;
+    }
+    std::vector<int> depth(end, 0);
+    for (int i = end - 2; i >= 0; i--) depth[i] = depth[parent[i]] + 1;
+    int deepest = 0;
+    for (int i = 0; i < k; i++) {
+      len[leaves[i]] = (uint8_t)depth[i];
+      deepest = std::max(deepest, depth[i]);
+    }
+    if (deepest <= maxlen) return;
+    for (auto& c : counts)
+      if (c) c = (c >> 1) | 1u;
+  }
+}
+
+// canonical codes (shorter first, then by symbol), bit-reversed for LSB-first
+void canonical(const uint8_t* len, int n, uint16_t* code) {
+  int count[16] = {0};
+  for (int i = 0; i < n; i++)
+    if (len[i]) count[len[i]]++;
+  int next[16] = {0};
+  int c = 0;
+  for (int b = 1; b < 16; b++) {
+    c = (c + count[b - 1]) << 1;
+    next[b] = c;
+  }
+  for (int i = 0; i < n; i++) {
+    code[i] = 0;
+    if (!len[i]) continue;
+    const int v = next[len[i]]++;
+    int r = 0;
+    for (int b = 0; b < len[i]; b++) r |= ((v >> b) & 1) << (len[i] - 1 - b);
+    code[i] = (uint16_t)r;
+  }
+}
+
+}  // namespace
+
+PrefixCode build_prefix_code(const uint32_t* counts, int n) {
+  PrefixCode p;
+  int last = -1;
+  for (int i = 0; i < n; i++)
+    if (counts[i]) {
+      last = i;
+      p.nsym++;
+    }
+  if (last <= 0) return p;  // alphabet 1: every symbol costs 0 bits
+  p.alphabet = (uint32_t)last + 1;
+  huffman_lengths(counts, last + 1, 15, p.len.data());
+  if (p.nsym == 1) {
+    p.len[last] = 0;
+    p.simple = 1;
+    p.ssyms[0] = (uint16_t)last;
+    return p;
+  }
+  if (p.nsym <= 4) {
+    std::vector<int> s;
+    for (int i = 0; i <= last; i++)
+      if (counts[i]) s.push_back(i);
+    std::stable_sort(s.begin(), s.end(), [&](int a, int b) {
+      return p.len[a] != p.len[b] ? p.len[a] < p.len[b] : a < b;
+    });
+    p.simple = p.nsym;
+    for (int i = 0; i < p.nsym; i++) p.ssyms[i] = (uint16_t)s[i];
+    if (p.nsym == 4 && p.len[s[0]] == 1) p.tree_select = 1;
+  }
+  canonical(p.len.data(), last + 1, p.code.data());
+  return p;
+}
+
+void write_prefix_code(BitWriter& w, const PrefixCode& p) {
+  if (p.alphabet <= 1) return;
+  if (p.simple) {
+    uint32_t max_bits = 0;
+    while ((1u << max_bits) < p.alphabet) max_bits++;
+    w.put(2, 1);
+    w.put(2, (uint32_t)p.simple - 1);
+    for (int i = 0; i < p.simple; i++) w.put(max_bits, p.ssyms[i]);
+    if (p.simple == 4) w.put(1, (uint32_t)p.tree_select);
+    return;
+  }
+  // code-length code (RFC 7932 §3.5) over the used length values 0..15
+  static const uint8_t kOrder[18] = {1, 2, 3, 4, 0, 5, 17, 6, 16, 7, 8, 9, 10, 11, 12, 13, 14, 15};
+  static const uint8_t kStaticCode[6] = {0, 7, 3, 2, 1, 15};
+  static const uint8_t kStaticLen[6] = {2, 4, 3, 2, 2, 4};
+  const int n = (int)p.alphabet;
+  uint32_t hist[18] = {0};
+  for (int i = 0; i < n; i++) hist[p.len[i]]++;
+  uint8_t cl_len[18];
+  uint16_t cl_code[18];
+  huffman_lengths(hist, 18, 5, cl_len);
+  canonical(cl_len, 18, cl_code);
+  int used = 0;
+  for (int i = 0; i < 18; i++) used += cl_len[i] != 0;
+  w.put(2, 0);  // HSKIP
+  int space = 32;
+  for (int i = 0; i < 18 && space > 0; i++) {
+    const int v = cl_len[kOrder[i]];
+    w.put(kStaticLen[v], kStaticCode[v]);
+    if (v) space -= 32 >> v;
+  }
+  if (used == 1) return;  // one code-length symbol: every length costs 0 bits
+  for (int i = 0; i < n; i++) w.put(cl_len[p.len[i]], cl_code[p.len[i]]);
+}
+
+void write_token(BitWriter& w, const PrefixCode& p, const UintCfg& c, uint32_t v) {
+  uint32_t tok, nb, bits;
+  hybrid_encode(v, c, &tok, &nb, &bits);
+  w.put(p.len[tok], p.code[tok]);
+  w.put(nb, bits);
+}
+
+void write_u32_sel(BitWriter& w, uint32_t sel, uint32_t nbits, uint32_t v) {
+  w.put(2, sel);
+  w.put(nbits, v);
+}
+
+namespace {
+void write_varlen16(BitWriter& w, uint32_t v) {
+  if (v == 0) {
+    w.put(1, 0);
+    return;
+  }
+  const uint32_t n = 31u - (uint32_t)__builtin_clz(v);
+  w.put(1, 1);
+  w.put(4, n);
+  w.put(n, v - (1u << n));
+}
+void write_uint_config(BitWriter& w, const UintCfg& c) {  // log_alpha_size 15
+  w.put(4, c.split_exp);
+  if (c.split_exp != 15) {
+    w.put(ceil_log2(c.split_exp + 1), c.msb);
+    w.put(ceil_log2(c.split_exp - c.msb + 1), c.lsb);
+  }
+}
+void write_context_map(BitWriter& w, const std::vector<uint8_t>& map, int nhist) {
+  const int n = (int)map.size();
+  if (nhist == 1) {
+    w.put(1, 1);
+    w.put(2, 0);
+    return;
+  }
+  if (nhist <= 8 && n <= 16) {
+    const uint32_t bits = ceil_log2((uint32_t)nhist);
+    w.put(1, 1);
+    w.put(2, bits);
+    for (uint8_t v : map) w.put(bits, v);
+    return;
+  }
+  w.put(1, 0);  // entropy coded
+  w.put(1, 0);  // no move-to-front
+  uint32_t counts[256] = {0};
+  for (uint8_t v : map) counts[v]++;
+  std::vector<PrefixCode> code{build_prefix_code(counts, 256)};
+  write_histograms(w, std::vector<uint8_t>{0}, 1, code, kCfgMap);
+  for (uint8_t v : map) write_token(w, code[0], kCfgMap, v);
+}
+}  // namespace
+
+void write_histograms(BitWriter& w, const std::vector<uint8_t>& ctxmap, int nhist,
+                      const std::vector<PrefixCode>& codes, const UintCfg& cfg) {
+  w.put(1, 0);  // lz77.enabled
+  if (ctxmap.size() > 1) write_context_map(w, ctxmap, nhist);
+  w.put(1, 1);  // use_prefix_code
+  for (int h = 0; h < nhist; h++) write_uint_config(w, cfg);
+  for (int h = 0; h < nhist; h++) write_varlen16(w, codes[h].alphabet - 1);
+  for (int h = 0; h < nhist; h++) write_prefix_code(w, codes[h]);
+}
+
+// DC: split on channel -> leaves (Y), (B), (X); clamped gradient predictor
+const TreeNode kDcTree[5] = {{0, 0, 1, 2, 0, -1},
+                             {0, 1, 3, 4, 0, -1},
+                             {-1, 0, 0, 0, 5, 0},
+                             {-1, 0, 0, 0, 5, 1},
+                             {-1, 0, 0, 0, 5, 2}};
+// AC metadata: cmap (zero) | epf (zero) | qf row (west) | acs row (zero)
+const TreeNode kMetaTree[7] = {{0, 1, 1, 2, 0, -1},  {0, 2, 3, 4, 0, -1},
+                               {-1, 0, 0, 0, 0, 0},  {-1, 0, 0, 0, 0, 1},
+                               {2, 0, 5, 6, 0, -1},  {-1, 0, 0, 0, 1, 2},
+                               {-1, 0, 0, 0, 0, 3}};
+
+void write_modular_prelude(BitWriter& w, const TreeNode* tree, int nnodes, int nleaves,
+                           const std::vector<PrefixCode>& leaf_codes) {
+  w.put(1, 0);  // use_global_tree
+  w.put(1, 1);  // wp_header.all_default
+  w.put(2, 0);  // nb_transforms = 0
+  // tree tokens (context, value) breadth-first; one histogram for 6 contexts
+  std::vector<std::pair<int, uint32_t>> toks;
+  for (int i = 0; i < nnodes; i++) {
+    const TreeNode& t = tree[i];
+    if (t.prop < 0) {
+      toks.push_back({1, 0});
+      toks.push_back({2, (uint32_t)t.predictor});
+      toks.push_back({3, 0});
+      toks.push_back({4, 0});
+      toks.push_back({5, 0});
+    } else {
+      toks.push_back({1, (uint32_t)t.prop + 1});
+      const int32_t sv = t.splitval;
+      toks.push_back({0, sv >= 0 ? (uint32_t)sv * 2u : (uint32_t)(-sv) * 2u - 1u});
+    }
+  }
+  uint32_t counts[128] = {0};
+  for (auto& t : toks) {
+    uint32_t tok, nb, bits;
+    hybrid_encode(t.second, kCfg420, &tok, &nb, &bits);
+    counts[tok]++;
+  }
+  std::vector<PrefixCode> tc{build_prefix_code(counts, 128)};
+  write_histograms(w, std::vector<uint8_t>(6, 0), 1, tc, kCfg420);
+  for (auto& t : toks) write_token(w, tc[0], kCfg420, t.second);
+  std::vector<uint8_t> map(nleaves);
+  for (int l = 0; l < nleaves; l++) map[l] = (uint8_t)l;
+  write_histograms(w, map, nleaves, leaf_codes, kCfg420);
+}
+
+namespace {
+void write_size(BitWriter& w, uint32_t v) {
+  const uint32_t m = v - 1;
+  if (m < (1u << 9))
+    write_u32_sel(w, 0, 9, m);
+  else if (m < (1u << 13))
+    write_u32_sel(w, 1, 13, m);
+  else if (m < (1u << 18))
+    write_u32_sel(w, 2, 18, m);
+  else
+    write_u32_sel(w, 3, 30, m);
+}
+}  // namespace
+
+void write_headers(BitWriter& w, uint32_t xs, uint32_t ys) {
+  w.put(8, 0xFF);
+  w.put(8, 0x0A);
+  if (xs % 8 == 0 && ys % 8 == 0 && xs <= 256 && ys <= 256) {
+    w.put(1, 1);
+    w.put(5, ys / 8 - 1);
+    w.put(3, 0);
+    w.put(5, xs / 8 - 1);
+  } else {
+    w.put(1, 0);
+    write_size(w, ys);
+    w.put(3, 0);
+    write_size(w, xs);
+  }
+  w.put(1, 1);  // ImageMetadata.all_default (8-bit sRGB, xyb_encoded)
+  w.pad_to_byte();
+  // FrameHeader
+  w.put(1, 0);                      // all_default
+  w.put(2, 0);                      // frame_type: regular
+  w.put(1, 0);                      // encoding: VarDCT
+  write_u32_sel(w, 2, 8, 128 - 17); // flags = kSkipAdaptiveDCSmoothing
+  w.put(2, 0);                      // upsampling 1
+  w.put(3, 2);                      // x_qm_scale
+  w.put(3, 2);                      // b_qm_scale
+  w.put(2, 0);                      // num_passes 1
+  w.put(1, 0);                      // no crop
+  w.put(2, 0);                      // blending: replace
+  w.put(1, 1);                      // is_last
+  w.put(2, 0);                      // name length 0
+  w.put(1, 0);                      // loop filter not all_default
+  w.put(1, 0);                      //   no gaborish
+  w.put(2, 0);                      //   epf_iters 0
+  w.put(2, 0);                      //   loop filter extensions
+  w.put(2, 0);                      // frame extensions
+}
+
+void write_toc(BitWriter& w, const std::vector<uint32_t>& sizes) {
+  w.put(1, 0);  // not permuted
+  w.pad_to_byte();
+  for (uint32_t s : sizes) {
+    if (s < 1024)
+      write_u32_sel(w, 0, 10, s);
+    else if (s < 17408)
+      write_u32_sel(w, 1, 14, s - 1024);
+    else if (s < 4211712)
+      write_u32_sel(w, 2, 22, s - 17408);
+    else
+      write_u32_sel(w, 3, 30, s - 4211712);
+  }
+  w.pad_to_byte();
+}
+
+}  // namespace jxg

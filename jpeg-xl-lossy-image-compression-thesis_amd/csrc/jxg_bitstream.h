@@ -1,0 +1,106 @@
+// jxg_bitstream.h -- host-side codestream writing: bit writer, prefix-code
+// construction and serialisation, entropy-code headers, modular trees,
+// image / frame headers and TOC.  [ext] JPEG XL codestream layout
+// (ISO/IEC 18181-1); the byte-level contract is shared with the CPU oracle
+// (oracle/encode.c, oracle/entropy.c) and checked bit-for-bit by the tests.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include <array>
+#include <vector>
+
+namespace jxg {
+
+class BitWriter {
+ public:
+  void put(uint32_t nbits, uint64_t v) {
+    if (nbits == 0) return;
+    v &= (nbits >= 64) ? ~0ull : ((1ull << nbits) - 1);
+    while (nbits) {
+      const size_t word = bits_ >> 6;
+      const uint32_t off = (uint32_t)(bits_ & 63);
+      if (word >= words_.size()) words_.push_back(0);
+      const uint32_t take = nbits < 64 - off ? nbits : 64 - off;
+      words_[word] |= (v & (take == 64 ? ~0ull : ((1ull << take) - 1))) << off;
+      v = take == 64 ? 0 : v >> take;
+      nbits -= take;
+      bits_ += take;
+    }
+  }
+  void pad_to_byte() { bits_ = (bits_ + 7) & ~(size_t)7; }
+  size_t bits() const { return bits_; }
+  // little-endian 32-bit words holding the bits (tail zero)
+  std::vector<uint32_t> words32() const {
+    std::vector<uint32_t> w((bits_ + 31) / 32, 0);
+    for (size_t i = 0; i < w.size(); i++) w[i] = (uint32_t)(words_[i / 2] >> (32 * (i & 1)));
+    return w;
+  }
+  std::vector<uint8_t> bytes() const {
+    std::vector<uint8_t> b((bits_ + 7) / 8);
+    for (size_t i = 0; i < b.size(); i++) b[i] = (uint8_t)(words_[i / 8] >> (8 * (i & 7)));
+    return b;
+  }
+  void append(const BitWriter& o) {
+    for (size_t i = 0; i < o.bits_; i += 64) {
+      const uint32_t n = (uint32_t)(o.bits_ - i < 64 ? o.bits_ - i : 64);
+      put(n, o.words_[i / 64]);
+    }
+  }
+
+ private:
+  std::vector<uint64_t> words_;
+  size_t bits_ = 0;
+};
+
+struct UintCfg {
+  uint32_t split_exp, msb, lsb;
+};
+constexpr UintCfg kCfg420{4, 2, 0};
+constexpr UintCfg kCfgMap{8, 0, 0};
+
+void hybrid_encode(uint32_t v, const UintCfg& c, uint32_t* tok, uint32_t* nb, uint32_t* bits);
+
+// A Brotli-style prefix code over at most 256 symbols.
+struct PrefixCode {
+  uint32_t alphabet = 1;  // serialised alphabet size
+  int nsym = 0;           // used symbols
+  int simple = 0;         // simple-code NSYM (1..4) or 0 for a complex code
+  int tree_select = 0;
+  std::array<uint16_t, 4> ssyms{};
+  std::array<uint8_t, 256> len{};
+  std::array<uint16_t, 256> code{};  // bit-reversed canonical code
+  // packed (code | len << 16) for device tables
+  uint32_t packed(uint32_t sym) const { return code[sym] | ((uint32_t)len[sym] << 16); }
+};
+PrefixCode build_prefix_code(const uint32_t* counts, int n);
+void write_prefix_code(BitWriter& w, const PrefixCode& p);
+
+void write_token(BitWriter& w, const PrefixCode& p, const UintCfg& c, uint32_t v);
+// DecodeHistograms: lz77 off, context map (ctxmap[nctx] dense ids), prefix codes
+void write_histograms(BitWriter& w, const std::vector<uint8_t>& ctxmap, int nhist,
+                      const std::vector<PrefixCode>& codes, const UintCfg& cfg);
+
+// Modular MA trees used by the LF-group streams (local trees, no transforms)
+struct TreeNode {
+  int prop, splitval, lchild, rchild, predictor, leaf;  // prop < 0: leaf
+};
+extern const TreeNode kDcTree[5];
+extern const TreeNode kMetaTree[7];
+// GroupHeader + tree + data histograms (leaf codes); the residual tokens are
+// emitted on the GPU
+void write_modular_prelude(BitWriter& w, const TreeNode* tree, int nnodes, int nleaves,
+                           const std::vector<PrefixCode>& leaf_codes);
+
+// SizeHeader + all-default ImageMetadata + byte padding + FrameHeader
+void write_headers(BitWriter& w, uint32_t xsize, uint32_t ysize);
+void write_toc(BitWriter& w, const std::vector<uint32_t>& section_bytes);
+void write_u32_sel(BitWriter& w, uint32_t sel, uint32_t nbits, uint32_t v);
+
+inline uint32_t ceil_log2(uint32_t x) {
+  uint32_t n = 0;
+  while ((1u << n) < x) n++;
+  return n;
+}
+
+}  // namespace jxg

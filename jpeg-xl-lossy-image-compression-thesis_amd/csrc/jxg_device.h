@@ -1,0 +1,175 @@
+// jxg_device.h -- gfx950 device math for the VarDCT encode path.
+//
+// Every float operation here follows the op order fixed in DESIGN.md §3 (and
+// restated by oracle/front.c, oracle/homog.c, oracle/xyb.c) so the HIP path is
+// bit-identical to the CPU oracle.  Built with -ffp-contract=off; fmaf is
+// used only where written explicitly; division/sqrt are IEEE (hipcc default
+// correctly-rounded f32 div/sqrt).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace jxg {
+
+// raw AcStrategy ids returned by the thesis selector
+// (proposals/combined.diff:227-233)
+enum : int { kDCT8 = 0, kDCT4X4 = 3, kDCT4X8 = 12, kDCT8X4 = 13 };
+
+// opsin absorbance [ext libjxl opsin_params.h]
+constexpr float kM00 = 0.30f, kM01 = 0.622f, kM02 = 0.078f;
+constexpr float kM10 = 0.23f, kM11 = 0.692f, kM12 = 0.078f;
+constexpr float kM20 = 0.24342268924547819f, kM21 = 0.20476744424496821f,
+                kM22 = 0.55180986650955360f;
+constexpr float kOpsinBias = 0.0037930732552754493f;
+
+__device__ __forceinline__ float cbrt_det(float x) {
+  if (!(x > 0.0f)) return 0.0f;
+  uint32_t i = __float_as_uint(x) / 3u + 0x2a514067u;
+  float y = __uint_as_float(i);
+#pragma unroll
+  for (int it = 0; it < 4; it++) {
+    float t = y * y;
+    y = (y + y + x / t) / 3.0f;
+  }
+  return y;
+}
+
+__device__ __forceinline__ void pixel_xyb(const float* lut, float cb, uint32_t r8,
+                                          uint32_t g8, uint32_t b8, float& X,
+                                          float& Y, float& B) {
+  const float r = lut[r8], g = lut[g8], b = lut[b8];
+  float m0 = ((kM00 * r + kM01 * g) + kM02 * b) + kOpsinBias;
+  float m1 = ((kM10 * r + kM11 * g) + kM12 * b) + kOpsinBias;
+  float m2 = ((kM20 * r + kM21 * g) + kM22 * b) + kOpsinBias;
+  m0 = cbrt_det(m0) - cb;
+  m1 = cbrt_det(m1) - cb;
+  m2 = cbrt_det(m2) - cb;
+  X = 0.5f * (m0 - m1);
+  Y = 0.5f * (m0 + m1);
+  B = m2;
+}
+
+// [ext] AC context model tables (libjxl ac_context.h)
+__device__ __constant__ static const uint8_t kStrategyOrder[27] = {
+    0, 1, 1, 1, 2, 3, 4, 4, 5, 5, 6, 6, 1, 1, 1, 1, 1, 1, 7, 8, 8, 9, 10, 10, 11, 12, 12};
+__device__ __constant__ static const uint8_t kDefaultCtxMap[39] = {
+    0, 1, 2, 2, 3,  3,  4,  5,  6,  6,  6,  6,  6,  7, 8, 9, 9, 10, 11, 12,
+    13, 14, 14, 14, 14, 14, 7, 8, 9, 9, 10, 11, 12, 13, 14, 14, 14, 14, 14};
+__device__ __constant__ static const uint8_t kFreqCtx[64] = {
+    0,  0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15, 15, 16, 16, 17, 17,
+    18, 18, 19, 19, 20, 20, 21, 21, 22, 22, 23, 23, 23, 23, 24, 24, 24, 24, 25, 25, 25, 25,
+    26, 26, 26, 26, 27, 27, 27, 27, 28, 28, 28, 28, 29, 29, 29, 29, 30, 30, 30, 30};
+__device__ __constant__ static const uint16_t kNnzCtx[64] = {
+    0,   0,   31,  62,  62,  93,  93,  93,  93,  123, 123, 123, 123, 152, 152, 152,
+    152, 152, 152, 152, 152, 180, 180, 180, 180, 180, 180, 180, 180, 180, 180, 180,
+    180, 206, 206, 206, 206, 206, 206, 206, 206, 206, 206, 206, 206, 206, 206, 206,
+    206, 206, 206, 206, 206, 206, 206, 206, 206, 206, 206, 206, 206, 206, 206, 206};
+
+constexpr int kBlockCtx = 15, kNzBuckets = 37, kZdCtx = 458;
+constexpr int kAcCtx = kBlockCtx * (kNzBuckets + kZdCtx);  // 7425
+constexpr int kMaxClusters = 132;
+constexpr int kAlpha = 128;
+
+__host__ __device__ __forceinline__ int bclass(int bctx) {
+  if (bctx < 7) return bctx == 0 ? 0 : (bctx == 1 ? 1 : 2);
+  return bctx == 7 ? 3 : (bctx == 8 ? 4 : 5);
+}
+// static clustering of the 7425 AC contexts (the map is transmitted)
+__host__ __device__ __forceinline__ int ac_cluster(int ctx) {
+  if (ctx < kBlockCtx * kNzBuckets) {
+    int bucket = ctx / kBlockCtx, bctx = ctx % kBlockCtx;
+    int nb = bucket == 0 ? 0 : (bucket <= 2 ? 1 : (bucket <= 8 ? 2 : 3));
+    return bclass(bctx) * 4 + nb;
+  }
+  int z = ctx - kBlockCtx * kNzBuckets;
+  int bctx = z / kZdCtx, zz = z % kZdCtx;
+  int prev = zz & 1, base = zz >> 1;
+  int bi = base >= 206 ? 7 : base >= 180 ? 6 : base >= 152 ? 5 : base >= 123 ? 4
+         : base >= 93 ? 3 : base >= 62 ? 2 : base >= 31 ? 1 : 0;
+  const int nzb_base = bi == 7 ? 206 : bi == 6 ? 180 : bi == 5 ? 152 : bi == 4 ? 123
+                     : bi == 3 ? 93 : bi == 2 ? 62 : bi == 1 ? 31 : 0;
+  int fc = base - nzb_base;
+  int nzg = bi < 2 ? 0 : (bi < 4 ? 1 : 2);
+  int fg = fc < 4 ? 0 : (fc < 12 ? 1 : 2);
+  return 24 + ((bclass(bctx) * 3 + nzg) * 3 + fg) * 2 + prev;
+}
+
+__host__ __device__ __forceinline__ uint32_t pack_signed(int32_t v) {
+  return v >= 0 ? (uint32_t)v * 2u : (uint32_t)(-(int64_t)v) * 2u - 1u;
+}
+
+// hybrid-uint (split_exponent 4, msb_in_token 2, lsb_in_token 0)
+__host__ __device__ __forceinline__ void hybrid420(uint32_t v, uint32_t& tok, uint32_t& nb,
+                                                   uint32_t& bits) {
+  if (v < 16u) {
+    tok = v;
+    nb = 0;
+    bits = 0;
+    return;
+  }
+#ifdef __HIP_DEVICE_COMPILE__
+  uint32_t n = 31u - (uint32_t)__clz(v);
+#else
+  uint32_t n = 31u - (uint32_t)__builtin_clz(v);
+#endif
+  uint32_t m = v - (1u << n);
+  tok = 16u + ((n - 4u) << 2) + (m >> (n - 2u));
+  nb = n - 2u;
+  bits = v & ((1u << nb) - 1u);
+}
+
+// natural coefficient order of an 8x8 varblock [ext coeff_order.cc]:
+// zigzag index -> raster position, computable at compile time
+struct Order64 {
+  uint8_t v[64];
+};
+__host__ __device__ constexpr Order64 make_order64() {
+  Order64 o{};
+  int cur = 1;
+  o.v[0] = 0;
+  for (int i = 0; i < 8; i++)
+    for (int j = 0; j <= i; j++) {
+      int x = j, y = i - j;
+      if (i & 1) {
+        int t = x;
+        x = y;
+        y = t;
+      }
+      if (x == 0 && y == 0) continue;
+      o.v[cur++] = (uint8_t)(y * 8 + x);
+    }
+  for (int ip = 7; ip > 0; ip--) {
+    int i = ip - 1;
+    for (int j = 0; j <= i; j++) {
+      int x = 7 - (i - j), y = 7 - j;
+      if (i & 1) {
+        int t = x;
+        x = y;
+        y = t;
+      }
+      o.v[cur++] = (uint8_t)(y * 8 + x);
+    }
+  }
+  return o;
+}
+__host__ __device__ constexpr int c_order_h(int j) { return make_order64().v[j]; }
+__host__ __device__ constexpr int c_inv_order_h(int k) {
+  const Order64 o = make_order64();
+  for (int j = 0; j < 64; j++)
+    if (o.v[j] == k) return j;
+  return 0;
+}
+// coefficient slab addressing: block (bx, by) -> 64x64-pixel tile and lane
+__host__ __device__ __forceinline__ size_t coef_index(uint32_t bx, uint32_t by, uint32_t tiles_x,
+                                                      int c, int j) {
+  const size_t tile = (size_t)(by >> 3) * tiles_x + (bx >> 3);
+  const uint32_t lane = (by & 7) * 8 + (bx & 7);
+  return ((tile * 3 + c) * 64 + j) * 64 + lane;
+}
+
+__device__ __forceinline__ int nz_bucket(int n) {
+  if (n >= 64) n = 64;
+  return n < 8 ? n : 4 + n / 2;
+}
+
+}  // namespace jxg

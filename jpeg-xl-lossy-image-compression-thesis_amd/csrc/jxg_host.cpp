@@ -1,0 +1,718 @@
+// jxg_host.cpp -- host orchestration and the C ABI (include/jxg.h).
+//
+// One encode = one stream-ordered pipeline on the context's HIP stream:
+//   front (RGB8 -> ACS/QF/DC/AC)            [jxg_front.hip]
+//   ac_hist + lf_hist (token statistics)     [jxg_entropy.hip]
+//   -> D2H histograms; host builds prefix codes, LfGlobal/HfGlobal and the
+//      LF-group stream preludes (a few KB of header bits)
+//   ac_emit + lf_rowbits/lf_scan/lf_emit (bit emission into scratch)
+//   -> D2H section sizes; host writes headers + TOC and the piece list
+//   concat (bit-exact assembly) -> D2H codestream
+// The byte stream equals the CPU oracle's (oracle/encode.c) bit for bit.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <vector>
+
+#include "../../include/jxg.h"
+#include "jxg_bitstream.h"
+#include "jxg_device.h"
+#include "jxg_kernels.h"
+
+namespace jxg {
+
+#define JXG_HIP(expr)                                                          \
+  do {                                                                         \
+    hipError_t e_ = (expr);                                                    \
+    if (e_ != hipSuccess) {                                                    \
+      std::fprintf(stderr, "jxg: %s failed: %s\n", #expr, hipGetErrorString(e_)); \
+      return JXG_ERR_HIP;                                                      \
+    }                                                                          \
+  } while (0)
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  hipError_t ensure(size_t count) {
+    if (count <= n && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    size_t want = std::max<size_t>(count, 1);
+    hipError_t e = hipMalloc((void**)&p, want * sizeof(T));
+    if (e == hipSuccess) n = want;
+    return e;
+  }
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+template <class T>
+struct PinBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  hipError_t ensure(size_t count) {
+    if (count <= n && p) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    n = 0;
+    size_t want = std::max<size_t>(count, 1);
+    hipError_t e = hipHostMalloc((void**)&p, want * sizeof(T), hipHostMallocDefault);
+    if (e == hipSuccess) n = want;
+    return e;
+  }
+  ~PinBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+};
+
+// frame-level scalars: same formulas as oracle jxo_frame_init (host, double)
+struct Frame {
+  uint32_t w, h, bxs, bys, xp, yp, tiles_x, tiles_y;
+  uint32_t gxs, gys, ngroups, lfxs, lfys, nlf;
+  float qf_base, inv_g;
+  uint32_t G, qdc;
+  float dc_mul[3], dc_step[3];
+};
+
+static Frame make_frame(uint32_t w, uint32_t h, float distance) {
+  Frame f{};
+  f.w = w;
+  f.h = h;
+  f.bxs = (w + 7) / 8;
+  f.bys = (h + 7) / 8;
+  f.xp = f.bxs * 8;
+  f.yp = f.bys * 8;
+  f.tiles_x = (f.bxs + 7) / 8;
+  f.tiles_y = (f.bys + 7) / 8;
+  f.gxs = (w + 255) / 256;
+  f.gys = (h + 255) / 256;
+  f.ngroups = f.gxs * f.gys;
+  f.lfxs = (w + 2047) / 2048;
+  f.lfys = (h + 2047) / 2048;
+  f.nlf = f.lfxs * f.lfys;
+  const double d = distance;
+  const double qfb = 0.79 / d;
+  f.qf_base = (float)qfb;
+  long G = (long)std::floor(qfb * 1024.0 + 0.5);
+  G = std::min<long>(std::max<long>(G, 1), 73727);
+  f.G = (uint32_t)G;
+  f.inv_g = (float)(65536.0 / (double)G);
+  double t = 0.3 * std::pow(d / 0.3, 0.66);
+  if (t > d) t = d;
+  if (t < 0.5 * d) t = 0.5 * d;
+  double qdc_f = 1.12 / t;
+  if (qdc_f > 50.0) qdc_f = 50.0;
+  long qdc = (long)std::floor(qdc_f * 65536.0 / (double)G + 0.5);
+  qdc = std::min<long>(std::max<long>(qdc, 1), 65536);
+  f.qdc = (uint32_t)qdc;
+  const double m_lf[3] = {1.0 / 4096.0, 1.0 / 512.0, 1.0 / 256.0};
+  for (int c = 0; c < 3; c++) {
+    f.dc_mul[c] = (float)((double)G * (double)qdc / 65536.0 / m_lf[c]);
+    f.dc_step[c] = (float)(65536.0 / (double)G / (double)qdc * m_lf[c]);
+  }
+  return f;
+}
+
+// default dequantization weights (inverse steps) [ext libjxl quant_weights.cc]
+static void quant_weights(float out[3][3][64]) {
+  static const double dct8[3][6] = {{3150.0, 0.0, -0.4, -0.4, -0.4, -2.0},
+                                    {560.0, 0.0, -0.3, -0.3, -0.3, -0.3},
+                                    {512.0, -2.0, -1.0, 0.0, -1.0, -2.0}};
+  static const double dct4[3][6] = {
+      {2200.0, 0.0, 0.0, 0.0}, {392.0, 0.0, 0.0, 0.0}, {112.0, -0.25, -0.25, -0.5}};
+  static const double dct4x8[3][6] = {
+      {2198.050556016380522, -0.96269623020744692, -0.76194253026666783, -0.6551140670773547},
+      {764.3655248643528689, -0.92630200888366945, -0.9675229603596517, -0.27845290869168118},
+      {527.107573587542228, -1.4594385811273854, -1.450082094097871593, -1.5843722511996204}};
+  auto weights = [](int rows, int cols, const double (*bands_in)[6], int nb, double* out3) {
+    for (int c = 0; c < 3; c++) {
+      double bands[6];
+      bands[0] = bands_in[c][0];
+      for (int i = 1; i < nb; i++) {
+        const double v = bands_in[c][i];
+        bands[i] = bands[i - 1] * (v > 0 ? 1.0 + v : 1.0 / (1.0 - v));
+      }
+      const double scale = (nb - 1) / (1.4142135623730951 + 1e-6);
+      const double rc = scale / (cols - 1), rr = scale / (rows - 1);
+      for (int y = 0; y < rows; y++) {
+        const double dy = y * rr;
+        for (int x = 0; x < cols; x++) {
+          const double dx = x * rc;
+          const double pos = std::sqrt(dx * dx + dy * dy);
+          int idx = (int)pos;
+          if (idx > nb - 2) idx = nb - 2;
+          const double frac = pos - idx;
+          const double a = bands[idx], b = bands[idx + 1];
+          out3[c * 64 + y * cols + x] = a * std::pow(b / a, frac);
+        }
+      }
+    }
+  };
+  double w[3 * 64];
+  weights(8, 8, dct8, 6, w);
+  for (int c = 0; c < 3; c++)
+    for (int i = 0; i < 64; i++) out[0][c][i] = (float)w[c * 64 + i];
+  weights(4, 4, dct4, 4, w);
+  for (int c = 0; c < 3; c++)
+    for (int y = 0; y < 8; y++)
+      for (int x = 0; x < 8; x++) out[1][c][y * 8 + x] = (float)w[c * 64 + (y / 2) * 4 + x / 2];
+  weights(4, 8, dct4x8, 4, w);
+  for (int c = 0; c < 3; c++)
+    for (int y = 0; y < 8; y++)
+      for (int x = 0; x < 8; x++) out[2][c][y * 8 + x] = (float)w[c * 64 + (y / 2) * 8 + x];
+}
+
+static void srgb_lut(float lut[256]) {
+  for (int u = 0; u < 256; u++) {
+    const double v = u / 255.0;
+    lut[u] = (float)(v <= 0.04045 ? v / 12.92 : std::pow((v + 0.055) / 1.055, 2.4));
+  }
+}
+
+struct Ctx {
+  jxg_params params{};
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[6] = {};
+  bool constants_ready = false;
+  // device
+  DevBuf<uint8_t> rgb, acs, qf, cluster_map_dummy;
+  DevBuf<int32_t> dc, ac;
+  DevBuf<float> homog, xyb, r3;
+  DevBuf<uint8_t> type;
+  DevBuf<uint32_t> hist_ac, bound, ntok, codes_ac, gbits, lfhist, sbound, lfcodes, rowbits,
+      stream_rows, stream_bits, scratch, chunks, out;
+  DevBuf<uint64_t> gbase, rowoff, stream_base;
+  DevBuf<LfRow> rows;
+  DevBuf<ConcatPiece> pieces;
+  // host
+  PinBuf<uint32_t> h_hist_ac, h_bound, h_ntok, h_lfhist, h_sbound, h_gbits, h_sbits;
+  PinBuf<uint32_t> h_out;
+  std::vector<uint8_t> m_acs, m_qf;
+  std::vector<int32_t> m_dc, m_ac;
+  std::vector<uint32_t> m_ntok;
+  std::vector<float> m_homog;
+  jxg_stats stats{};
+};
+
+static jxg_status init_constants(Ctx* c) {
+  if (c->constants_ready) return JXG_OK;
+  float lut[256];
+  srgb_lut(lut);
+  static float wts[3][3][64];
+  quant_weights(wts);
+  set_front_constants(lut, wts, c->stream);
+  uint8_t tab[kAcCtx];
+  for (int i = 0; i < kAcCtx; i++) tab[i] = (uint8_t)ac_cluster(i);
+  set_cluster_table(tab, c->stream);
+  JXG_HIP(hipGetLastError());
+  c->constants_ready = true;
+  return JXG_OK;
+}
+
+// LF-group rows: (lf group, stream, channel, y) in stream order
+static void build_rows(const Frame& f, std::vector<LfRow>& rows, std::vector<uint32_t>& srows) {
+  rows.clear();
+  srows.clear();
+  for (uint32_t lg = 0; lg < f.nlf; lg++) {
+    const uint32_t bx0 = (lg % f.lfxs) * 256, by0 = (lg / f.lfxs) * 256;
+    const uint32_t bw = std::min(256u, f.bxs - bx0), bh = std::min(256u, f.bys - by0);
+    srows.push_back((uint32_t)rows.size());
+    for (uint16_t ch = 0; ch < 3; ch++)
+      for (uint32_t y = 0; y < bh; y++) rows.push_back({lg, 0, ch, y, bw, lg * 2});
+    srows.push_back((uint32_t)rows.size());
+    const uint32_t cw = (bw + 7) / 8, chh = (bh + 7) / 8;
+    for (uint16_t ch = 0; ch < 2; ch++)
+      for (uint32_t y = 0; y < chh; y++) rows.push_back({lg, 1, ch, y, cw, lg * 2 + 1});
+    for (uint32_t y = 0; y < 2; y++) rows.push_back({lg, 1, 2, y, bw * bh, lg * 2 + 1});
+    for (uint32_t y = 0; y < bh; y++) rows.push_back({lg, 1, 3, y, bw, lg * 2 + 1});
+  }
+  srows.push_back((uint32_t)rows.size());
+}
+
+static float elapsed(hipEvent_t a, hipEvent_t b) {
+  float ms = 0.0f;
+  (void)hipEventElapsedTime(&ms, a, b);
+  return ms;
+}
+
+static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32_t h,
+                                size_t stride, jxg_buffer* out) {
+  hipStream_t s = c->stream;
+  const jxg_params& P = c->params;
+  const Frame f = make_frame(w, h, P.distance);
+  const size_t nb = (size_t)f.bxs * f.bys;
+  const bool homog = (P.proposals & 3u) != 0;
+  jxg_status st = init_constants(c);
+  if (st) return st;
+  JXG_HIP(c->acs.ensure(nb));
+  JXG_HIP(c->qf.ensure(nb));
+  JXG_HIP(c->dc.ensure(nb * 3));
+  JXG_HIP(c->ac.ensure(nb * 192));
+  if (homog) JXG_HIP(c->homog.ensure(nb * 3));
+  JXG_HIP(c->hist_ac.ensure(kMaxClusters * kAlpha));
+  JXG_HIP(c->codes_ac.ensure(kMaxClusters * kAlpha));
+  JXG_HIP(c->bound.ensure(f.ngroups));
+  JXG_HIP(c->ntok.ensure(f.ngroups * 3));
+  JXG_HIP(c->gbits.ensure(f.ngroups));
+  JXG_HIP(c->gbase.ensure(f.ngroups));
+  const uint32_t nstreams = f.nlf * 2;
+  std::vector<LfRow> rows;
+  std::vector<uint32_t> srows;
+  build_rows(f, rows, srows);
+  const uint32_t nrows = (uint32_t)rows.size();
+  JXG_HIP(c->rows.ensure(nrows));
+  JXG_HIP(c->lfhist.ensure(nstreams * 4 * kAlpha));
+  JXG_HIP(c->lfcodes.ensure(nstreams * 4 * kAlpha));
+  JXG_HIP(c->sbound.ensure(nstreams));
+  JXG_HIP(c->rowbits.ensure(nrows));
+  JXG_HIP(c->rowoff.ensure(nrows));
+  JXG_HIP(c->stream_rows.ensure(nstreams + 1));
+  JXG_HIP(c->stream_base.ensure(nstreams));
+  JXG_HIP(c->stream_bits.ensure(nstreams));
+  JXG_HIP(c->h_hist_ac.ensure(kMaxClusters * kAlpha));
+  JXG_HIP(c->h_bound.ensure(f.ngroups));
+  JXG_HIP(c->h_ntok.ensure(f.ngroups * 3));
+  JXG_HIP(c->h_lfhist.ensure(nstreams * 4 * kAlpha));
+  JXG_HIP(c->h_sbound.ensure(nstreams));
+  JXG_HIP(c->h_gbits.ensure(f.ngroups));
+  JXG_HIP(c->h_sbits.ensure(nstreams));
+  JXG_HIP(hipMemcpyAsync(c->rows.p, rows.data(), nrows * sizeof(LfRow), hipMemcpyHostToDevice, s));
+  JXG_HIP(hipMemcpyAsync(c->stream_rows.p, srows.data(), srows.size() * 4, hipMemcpyHostToDevice, s));
+
+  // ---------------- stage 1: front end ----------------
+  JXG_HIP(hipEventRecord(c->ev[0], s));
+  FrontArgs fa{};
+  fa.rgb = d_rgb;
+  fa.w = w;
+  fa.h = h;
+  fa.stride = stride;
+  fa.bxs = f.bxs;
+  fa.bys = f.bys;
+  fa.xp = f.xp;
+  fa.yp = f.yp;
+  fa.tiles_x = f.tiles_x;
+  fa.distance = P.distance;
+  fa.effort = P.effort;
+  fa.proposals = P.proposals;
+  fa.h1_int = (P.flags & JXG_FLAG_H1_INT_ABS) ? 1 : 0;
+  fa.qf_base = f.qf_base;
+  fa.inv_g = f.inv_g;
+  fa.G = f.G;
+  for (int i = 0; i < 3; i++) {
+    fa.dc_mul[i] = f.dc_mul[i];
+    fa.dc_step[i] = f.dc_step[i];
+  }
+  fa.acs = c->acs.p;
+  fa.qf = c->qf.p;
+  fa.dc = c->dc.p;
+  fa.ac = c->ac.p;
+  fa.homog = homog ? c->homog.p : nullptr;
+  launch_front(fa, f.tiles_x, f.tiles_y, s);
+  JXG_HIP(hipGetLastError());
+  JXG_HIP(hipEventRecord(c->ev[1], s));
+
+  // ---------------- stage 2: statistics ----------------
+  JXG_HIP(hipMemsetAsync(c->hist_ac.p, 0, kMaxClusters * kAlpha * 4, s));
+  JXG_HIP(hipMemsetAsync(c->lfhist.p, 0, (size_t)nstreams * 4 * kAlpha * 4, s));
+  JXG_HIP(hipMemsetAsync(c->sbound.p, 0, nstreams * 4, s));
+  AcArgs aa{};
+  aa.acs = c->acs.p;
+  aa.ac = c->ac.p;
+  aa.bxs = f.bxs;
+  aa.bys = f.bys;
+  aa.gxs = f.gxs;
+  aa.hist = c->hist_ac.p;
+  aa.bound = c->bound.p;
+  aa.ntok = c->ntok.p;
+  aa.codes = c->codes_ac.p;
+  aa.base = c->gbase.p;
+  aa.bits = c->gbits.p;
+  launch_ac_hist(aa, f.ngroups, s);
+  LfArgs la{};
+  la.rows = c->rows.p;
+  la.dc = c->dc.p;
+  la.acs = c->acs.p;
+  la.qf = c->qf.p;
+  la.bxs = f.bxs;
+  la.bys = f.bys;
+  la.lfxs = f.lfxs;
+  la.hist = c->lfhist.p;
+  la.sbound = c->sbound.p;
+  la.codes = c->lfcodes.p;
+  la.row_bits = c->rowbits.p;
+  la.row_off = c->rowoff.p;
+  la.stream_rows = c->stream_rows.p;
+  la.stream_base = c->stream_base.p;
+  la.stream_bits = c->stream_bits.p;
+  launch_lf_hist(la, nrows, s);
+  JXG_HIP(hipGetLastError());
+  JXG_HIP(hipMemcpyAsync(c->h_hist_ac.p, c->hist_ac.p, kMaxClusters * kAlpha * 4, hipMemcpyDeviceToHost, s));
+  JXG_HIP(hipMemcpyAsync(c->h_bound.p, c->bound.p, f.ngroups * 4, hipMemcpyDeviceToHost, s));
+  JXG_HIP(hipMemcpyAsync(c->h_ntok.p, c->ntok.p, f.ngroups * 12, hipMemcpyDeviceToHost, s));
+  JXG_HIP(hipMemcpyAsync(c->h_lfhist.p, c->lfhist.p, (size_t)nstreams * 4 * kAlpha * 4, hipMemcpyDeviceToHost, s));
+  JXG_HIP(hipMemcpyAsync(c->h_sbound.p, c->sbound.p, nstreams * 4, hipMemcpyDeviceToHost, s));
+  JXG_HIP(hipEventRecord(c->ev[2], s));
+  JXG_HIP(hipStreamSynchronize(s));
+
+  // ---------------- host: codes and header sections ----------------
+  int dense[kMaxClusters];
+  std::fill(dense, dense + kMaxClusters, -1);
+  int nhist = 0;
+  std::vector<uint8_t> ctxmap(kAcCtx);
+  for (int ctx = 0; ctx < kAcCtx; ctx++) {
+    const int cl = ac_cluster(ctx);
+    uint64_t tot = 0;
+    for (int k = 0; k < kAlpha; k++) tot += c->h_hist_ac.p[cl * kAlpha + k];
+    if (tot && dense[cl] < 0) dense[cl] = nhist++;
+    ctxmap[ctx] = (uint8_t)(dense[cl] < 0 ? 0 : dense[cl]);
+  }
+  std::vector<PrefixCode> codes(std::max(nhist, 1));
+  std::vector<uint32_t> packed(kMaxClusters * kAlpha, 0);
+  for (int cl = 0; cl < kMaxClusters; cl++) {
+    if (dense[cl] < 0) continue;
+    codes[dense[cl]] = build_prefix_code(c->h_hist_ac.p + cl * kAlpha, kAlpha);
+    for (int k = 0; k < kAlpha; k++) packed[cl * kAlpha + k] = codes[dense[cl]].packed(k);
+  }
+  // LF-group stream codes and preludes
+  std::vector<uint32_t> lfpacked((size_t)nstreams * 4 * kAlpha, 0);
+  std::vector<BitWriter> preA(f.nlf), preB(f.nlf);
+  for (uint32_t lg = 0; lg < f.nlf; lg++) {
+    const uint32_t bx0 = (lg % f.lfxs) * 256, by0 = (lg / f.lfxs) * 256;
+    const uint32_t bw = std::min(256u, f.bxs - bx0), bh = std::min(256u, f.bys - by0);
+    for (int sidx = 0; sidx < 2; sidx++) {
+      const uint32_t sid = lg * 2 + sidx;
+      const int nleaves = sidx == 0 ? 3 : 4;
+      std::vector<PrefixCode> lc(nleaves);
+      for (int l = 0; l < nleaves; l++) {
+        lc[l] = build_prefix_code(c->h_lfhist.p + ((size_t)sid * 4 + l) * kAlpha, kAlpha);
+        for (int k = 0; k < kAlpha; k++) lfpacked[((size_t)sid * 4 + l) * kAlpha + k] = lc[l].packed(k);
+      }
+      if (sidx == 0) {
+        preA[lg].put(2, 0);  // extra_precision
+        write_modular_prelude(preA[lg], kDcTree, 5, 3, lc);
+      } else {
+        preB[lg].put(ceil_log2(bw * bh), bw * bh - 1);  // varblock count - 1
+        write_modular_prelude(preB[lg], kMetaTree, 7, 4, lc);
+      }
+    }
+  }
+  BitWriter lfglobal, hfglobal;
+  lfglobal.put(1, 1);  // LfChannelDequantization.all_default
+  if (f.G <= 2048)
+    write_u32_sel(lfglobal, 0, 11, f.G - 1);
+  else if (f.G <= 4096)
+    write_u32_sel(lfglobal, 1, 11, f.G - 2049);
+  else if (f.G <= 8192)
+    write_u32_sel(lfglobal, 2, 12, f.G - 4097);
+  else
+    write_u32_sel(lfglobal, 3, 16, f.G - 8193);
+  if (f.qdc == 16)
+    lfglobal.put(2, 0);
+  else if (f.qdc <= 32)
+    write_u32_sel(lfglobal, 1, 5, f.qdc - 1);
+  else if (f.qdc <= 256)
+    write_u32_sel(lfglobal, 2, 8, f.qdc - 1);
+  else
+    write_u32_sel(lfglobal, 3, 16, f.qdc - 1);
+  lfglobal.put(1, 1);  // BlockCtxMap default
+  lfglobal.put(1, 1);  // colour correlation default
+  lfglobal.put(1, 0);  // GlobalModular: no tree, no channels
+  hfglobal.put(1, 1);  // DequantMatrices all_default
+  hfglobal.put(ceil_log2(f.ngroups), 0);  // num_hf_presets - 1
+  write_u32_sel(hfglobal, 2, 0, 0);        // used_orders = 0
+  write_histograms(hfglobal, ctxmap, nhist, codes, kCfg420);
+
+  // scratch layout: AC groups then LF streams (32-bit aligned regions)
+  std::vector<uint64_t> gbase(f.ngroups), sbase(nstreams);
+  uint64_t cursor = 0;
+  for (uint32_t g = 0; g < f.ngroups; g++) {
+    gbase[g] = cursor;
+    cursor += ((uint64_t)c->h_bound.p[g] + 63) & ~31ull;
+  }
+  for (uint32_t i = 0; i < nstreams; i++) {
+    sbase[i] = cursor;
+    cursor += ((uint64_t)c->h_sbound.p[i] + 63) & ~31ull;
+  }
+  const uint64_t scratch_words = cursor / 32 + 2;
+  JXG_HIP(c->scratch.ensure(scratch_words));
+  JXG_HIP(hipMemcpyAsync(c->codes_ac.p, packed.data(), packed.size() * 4, hipMemcpyHostToDevice, s));
+  JXG_HIP(hipMemcpyAsync(c->lfcodes.p, lfpacked.data(), lfpacked.size() * 4, hipMemcpyHostToDevice, s));
+  JXG_HIP(hipMemcpyAsync(c->gbase.p, gbase.data(), gbase.size() * 8, hipMemcpyHostToDevice, s));
+  JXG_HIP(hipMemcpyAsync(c->stream_base.p, sbase.data(), sbase.size() * 8, hipMemcpyHostToDevice, s));
+  JXG_HIP(hipMemsetAsync(c->scratch.p, 0, scratch_words * 4, s));
+
+  // ---------------- stage 3: emission ----------------
+  aa.scratch = c->scratch.p;
+  la.scratch = c->scratch.p;
+  launch_ac_emit(aa, f.ngroups, s);
+  launch_lf_rowbits(la, nrows, s);
+  launch_lf_scan(la, nstreams, s);
+  launch_lf_emit(la, nrows, s);
+  JXG_HIP(hipGetLastError());
+  JXG_HIP(hipMemcpyAsync(c->h_gbits.p, c->gbits.p, f.ngroups * 4, hipMemcpyDeviceToHost, s));
+  JXG_HIP(hipMemcpyAsync(c->h_sbits.p, c->stream_bits.p, nstreams * 4, hipMemcpyDeviceToHost, s));
+  JXG_HIP(hipEventRecord(c->ev[3], s));
+  JXG_HIP(hipStreamSynchronize(s));
+
+  // ---------------- host: layout, TOC, pieces ----------------
+  struct Piece {
+    int arena;  // 0 scratch, 1 host chunk
+    uint64_t src, nbits;
+  };
+  std::vector<std::vector<Piece>> sections;
+  std::vector<uint32_t> chunk_words;
+  auto add_chunk = [&](const BitWriter& bw) -> Piece {
+    Piece p{1, (uint64_t)chunk_words.size() * 32, bw.bits()};
+    auto wv = bw.words32();
+    chunk_words.insert(chunk_words.end(), wv.begin(), wv.end());
+    return p;
+  };
+  sections.push_back({add_chunk(lfglobal)});
+  for (uint32_t lg = 0; lg < f.nlf; lg++) {
+    sections.push_back({add_chunk(preA[lg]), Piece{0, sbase[lg * 2], c->h_sbits.p[lg * 2]},
+                        add_chunk(preB[lg]), Piece{0, sbase[lg * 2 + 1], c->h_sbits.p[lg * 2 + 1]}});
+  }
+  sections.push_back({add_chunk(hfglobal)});
+  for (uint32_t g = 0; g < f.ngroups; g++) sections.push_back({Piece{0, gbase[g], c->h_gbits.p[g]}});
+  const bool single = f.ngroups == 1;
+  std::vector<uint32_t> sizes;
+  if (single) {
+    uint64_t total = 0;
+    for (auto& sec : sections)
+      for (auto& p : sec) total += p.nbits;
+    sizes.push_back((uint32_t)((total + 7) / 8));
+  } else {
+    for (auto& sec : sections) {
+      uint64_t t = 0;
+      for (auto& p : sec) t += p.nbits;
+      sizes.push_back((uint32_t)((t + 7) / 8));
+    }
+  }
+  BitWriter head;
+  write_headers(head, w, h);
+  write_toc(head, sizes);
+  const Piece head_piece = add_chunk(head);
+  std::vector<ConcatPiece> cps;
+  uint64_t dst = 0, max_words = 0;
+  auto emit_piece = [&](const Piece& p) {
+    if (p.nbits) {
+      cps.push_back({p.src, dst, p.nbits, (uint32_t)p.arena, 0});
+      max_words = std::max<uint64_t>(max_words, (p.nbits + 31) / 32);
+    }
+    dst += p.nbits;
+  };
+  emit_piece(head_piece);
+  for (auto& sec : sections) {
+    for (auto& p : sec) emit_piece(p);
+    if (!single) dst = (dst + 7) & ~7ull;
+  }
+  dst = (dst + 7) & ~7ull;
+  const size_t out_bytes = (size_t)(dst / 8);
+  const size_t out_words = (out_bytes + 3) / 4 + 1;
+  chunk_words.push_back(0);  // read-ahead guard
+  JXG_HIP(c->chunks.ensure(chunk_words.size()));
+  JXG_HIP(c->pieces.ensure(cps.size()));
+  JXG_HIP(c->out.ensure(out_words));
+  JXG_HIP(c->h_out.ensure(out_words));
+  JXG_HIP(hipMemcpyAsync(c->chunks.p, chunk_words.data(), chunk_words.size() * 4, hipMemcpyHostToDevice, s));
+  JXG_HIP(hipMemcpyAsync(c->pieces.p, cps.data(), cps.size() * sizeof(ConcatPiece), hipMemcpyHostToDevice, s));
+  JXG_HIP(hipMemsetAsync(c->out.p, 0, out_words * 4, s));
+  launch_concat(c->pieces.p, (uint32_t)cps.size(), max_words, c->scratch.p, c->chunks.p, c->out.p, s);
+  JXG_HIP(hipGetLastError());
+  JXG_HIP(hipMemcpyAsync(c->h_out.p, c->out.p, out_words * 4, hipMemcpyDeviceToHost, s));
+  JXG_HIP(hipEventRecord(c->ev[4], s));
+  if (P.flags & JXG_FLAG_KEEP_MAPS) {
+    c->m_acs.resize(nb);
+    c->m_qf.resize(nb);
+    c->m_dc.resize(nb * 3);
+    c->m_ac.resize(nb * 192);
+    JXG_HIP(hipMemcpyAsync(c->m_acs.data(), c->acs.p, nb, hipMemcpyDeviceToHost, s));
+    JXG_HIP(hipMemcpyAsync(c->m_qf.data(), c->qf.p, nb, hipMemcpyDeviceToHost, s));
+    JXG_HIP(hipMemcpyAsync(c->m_dc.data(), c->dc.p, nb * 12, hipMemcpyDeviceToHost, s));
+    JXG_HIP(hipMemcpyAsync(c->m_ac.data(), c->ac.p, nb * 192 * 4, hipMemcpyDeviceToHost, s));
+    if (homog) {
+      c->m_homog.resize(nb * 3);
+      JXG_HIP(hipMemcpyAsync(c->m_homog.data(), c->homog.p, nb * 12, hipMemcpyDeviceToHost, s));
+    }
+  }
+  JXG_HIP(hipStreamSynchronize(s));
+  out->data = (uint8_t*)std::malloc(out_bytes);
+  if (!out->data) return JXG_ERR_OOM;
+  std::memcpy(out->data, c->h_out.p, out_bytes);
+  out->size = out_bytes;
+
+  // stats
+  jxg_stats& S = c->stats;
+  S = jxg_stats{};
+  S.xsize = w;
+  S.ysize = h;
+  S.xsize_blocks = f.bxs;
+  S.ysize_blocks = f.bys;
+  S.num_groups = f.ngroups;
+  S.num_lf_groups = f.nlf;
+  S.global_scale = f.G;
+  S.quant_dc = f.qdc;
+  S.bytes = out_bytes;
+  c->m_ntok.assign(c->h_ntok.p, c->h_ntok.p + f.ngroups * 3);
+  S.ac_tokens = c->m_ntok.data();
+  if (P.flags & JXG_FLAG_KEEP_MAPS) {
+    // AC back to natural (raster) order for the caller
+    static const Order64 ord = make_order64();
+    std::vector<int32_t> nat(nb * 192);
+    for (size_t b = 0; b < nb * 3; b++)
+      for (int j = 0; j < 64; j++) nat[b * 64 + ord.v[j]] = c->m_ac[b * 64 + j];
+    c->m_ac.swap(nat);
+    S.ac_strategy = c->m_acs.data();
+    S.quant_field = c->m_qf.data();
+    S.dc = c->m_dc.data();
+    S.ac = c->m_ac.data();
+    S.homogeneity = homog ? c->m_homog.data() : nullptr;
+  }
+  S.ms_front = elapsed(c->ev[0], c->ev[1]);
+  S.ms_histogram = elapsed(c->ev[1], c->ev[2]);
+  S.ms_emit = elapsed(c->ev[2], c->ev[3]);
+  S.ms_assemble = elapsed(c->ev[3], c->ev[4]);
+  S.ms_total = elapsed(c->ev[0], c->ev[4]);
+  return JXG_OK;
+}
+
+}  // namespace jxg
+
+using namespace jxg;
+
+extern "C" {
+
+const char* jxg_status_str(jxg_status s) {
+  switch (s) {
+    case JXG_OK: return "ok";
+    case JXG_ERR_INVALID_ARG: return "invalid argument";
+    case JXG_ERR_NO_DEVICE: return "no HIP device";
+    case JXG_ERR_HIP: return "HIP runtime error";
+    case JXG_ERR_OOM: return "out of memory";
+    case JXG_ERR_UNSUPPORTED: return "unsupported";
+    default: return "internal error";
+  }
+}
+
+jxg_status jxg_create(const jxg_params* params, void** out) {
+  if (!params || !out) return JXG_ERR_INVALID_ARG;
+  *out = nullptr;
+  if (!(params->distance > 0.0f) || params->distance > 25.0f) return JXG_ERR_INVALID_ARG;
+  if (params->effort < 1 || params->effort > 10) return JXG_ERR_INVALID_ARG;
+  if (params->proposals & ~3u) return JXG_ERR_INVALID_ARG;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return JXG_ERR_NO_DEVICE;
+  if (params->device < 0 || params->device >= ndev) return JXG_ERR_INVALID_ARG;
+  if (hipSetDevice(params->device) != hipSuccess) return JXG_ERR_HIP;
+  Ctx* c = new (std::nothrow) Ctx();
+  if (!c) return JXG_ERR_OOM;
+  c->params = *params;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return JXG_ERR_HIP;
+  }
+  for (auto& e : c->ev)
+    if (hipEventCreate(&e) != hipSuccess) {
+      delete c;
+      return JXG_ERR_HIP;
+    }
+  *out = c;
+  return JXG_OK;
+}
+
+void jxg_destroy(void* ctx) {
+  if (!ctx) return;
+  Ctx* c = static_cast<Ctx*>(ctx);
+  (void)hipSetDevice(c->params.device);
+  (void)hipStreamSynchronize(c->stream);
+  for (auto& e : c->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+jxg_status jxg_encode_rgb8_device(void* ctx, const void* d_rgb, uint32_t w, uint32_t h,
+                                  size_t stride, jxg_buffer* out) {
+  if (!ctx || !d_rgb || !out || w == 0 || h == 0 || w > (1u << 18) || h > (1u << 18) ||
+      stride < (size_t)w * 3)
+    return JXG_ERR_INVALID_ARG;
+  Ctx* c = static_cast<Ctx*>(ctx);
+  out->data = nullptr;
+  out->size = 0;
+  if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
+  return encode_device(c, static_cast<const uint8_t*>(d_rgb), w, h, stride, out);
+}
+
+jxg_status jxg_encode_rgb8(void* ctx, const uint8_t* rgb, uint32_t w, uint32_t h, size_t stride,
+                           jxg_buffer* out) {
+  if (!ctx || !rgb || !out || w == 0 || h == 0 || w > (1u << 18) || h > (1u << 18) ||
+      stride < (size_t)w * 3)
+    return JXG_ERR_INVALID_ARG;
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
+  const size_t bytes = stride * (h - 1) + (size_t)w * 3;
+  if (c->rgb.ensure(bytes) != hipSuccess) return JXG_ERR_OOM;
+  if (hipMemcpyAsync(c->rgb.p, rgb, bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+    return JXG_ERR_HIP;
+  out->data = nullptr;
+  out->size = 0;
+  return encode_device(c, c->rgb.p, w, h, stride, out);
+}
+
+jxg_status jxg_encode_batch_rgb8(void* ctx, const uint8_t* const* rgbs, uint32_t n, uint32_t w,
+                                 uint32_t h, size_t stride, jxg_buffer* outs) {
+  if (!ctx || !rgbs || !outs) return JXG_ERR_INVALID_ARG;
+  for (uint32_t i = 0; i < n; i++) {
+    jxg_status st = jxg_encode_rgb8(ctx, rgbs[i], w, h, stride, &outs[i]);
+    if (st != JXG_OK) {
+      for (uint32_t j = 0; j < i; j++) jxg_buffer_free(&outs[j]);
+      return st;
+    }
+  }
+  return JXG_OK;
+}
+
+jxg_status jxg_get_stats(void* ctx, jxg_stats* stats) {
+  if (!ctx || !stats) return JXG_ERR_INVALID_ARG;
+  *stats = static_cast<Ctx*>(ctx)->stats;
+  return JXG_OK;
+}
+
+void jxg_buffer_free(jxg_buffer* buf) {
+  if (!buf) return;
+  std::free(buf->data);
+  buf->data = nullptr;
+  buf->size = 0;
+}
+
+jxg_status jxg_homogeneity_map(void* ctx, const float* xyb, uint32_t xsize, uint32_t ysize,
+                               float distance, uint32_t flags, float* r3, uint8_t* type) {
+  if (!ctx || !xyb || !r3 || !type || xsize == 0 || ysize == 0 || xsize % 8 || ysize % 8)
+    return JXG_ERR_INVALID_ARG;
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
+  const size_t plane = (size_t)xsize * ysize, nb = plane / 64;
+  JXG_HIP(c->xyb.ensure(plane * 3));
+  JXG_HIP(c->r3.ensure(nb * 3));
+  JXG_HIP(c->type.ensure(nb));
+  hipStream_t s = c->stream;
+  JXG_HIP(hipMemcpyAsync(c->xyb.p, xyb, plane * 12, hipMemcpyHostToDevice, s));
+  HomogArgs a{c->xyb.p, xsize, ysize, xsize, plane, distance,
+              (flags & JXG_FLAG_H1_INT_ABS) ? 1 : 0, c->r3.p, c->type.p};
+  launch_homog(a, (xsize / 8 + 7) / 8, (ysize / 8 + 7) / 8, s);
+  JXG_HIP(hipGetLastError());
+  JXG_HIP(hipMemcpyAsync(r3, c->r3.p, nb * 12, hipMemcpyDeviceToHost, s));
+  JXG_HIP(hipMemcpyAsync(type, c->type.p, nb, hipMemcpyDeviceToHost, s));
+  JXG_HIP(hipStreamSynchronize(s));
+  return JXG_OK;
+}
+
+}  // extern "C"

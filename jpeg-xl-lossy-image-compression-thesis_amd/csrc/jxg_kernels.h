@@ -1,0 +1,100 @@
+// jxg_kernels.h -- kernel argument blocks and device-symbol setup shared by
+// the HIP translation units and the host orchestrator (jxg_host.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace jxg {
+
+struct FrontArgs {
+  const uint8_t* rgb;
+  uint32_t w, h;
+  size_t stride;
+  uint32_t bxs, bys, xp, yp, tiles_x;
+  float distance;
+  int effort;
+  uint32_t proposals;
+  int h1_int;
+  float qf_base, inv_g;
+  uint32_t G;
+  float dc_mul[3], dc_step[3];
+  uint8_t* acs;   // [nb] raw strategy
+  uint8_t* qf;    // [nb] raw-1
+  int32_t* dc;    // [3][nb] X,Y,B
+  int32_t* ac;    // [nb][3 X,Y,B][64 zigzag]
+  float* homog;   // [nb][3] or null
+};
+
+struct HomogArgs {
+  const float* xyb;  // [3][ysize][stride]
+  uint32_t xsize, ysize;
+  size_t stride, plane;
+  float distance;
+  int h1_int;
+  float* r3;
+  uint8_t* type;
+};
+
+// AC (pass group) token kernels
+struct AcArgs {
+  const uint8_t* acs;
+  const int32_t* ac;
+  uint32_t bxs, bys, gxs;
+  uint32_t* hist;        // [kMaxClusters][kAlpha]      (hist pass)
+  uint32_t* bound;       // [ngroups] bit upper bound   (hist pass)
+  uint32_t* ntok;        // [ngroups][3] token counts   (hist pass)
+  const uint32_t* codes; // [kMaxClusters][kAlpha] (code | len << 16)  (emit pass)
+  const uint64_t* base;  // [ngroups] scratch bit offset (emit pass)
+  uint32_t* scratch;     // bit buffer (emit pass, zeroed)
+  uint32_t* bits;        // [ngroups] exact bits (emit pass)
+};
+
+// LF-group modular streams: rows of (lf group, stream, channel, y)
+struct LfRow {
+  uint32_t lg;      // LF group
+  uint16_t stream;  // 0 = DC, 1 = AC metadata
+  uint16_t chan;
+  uint32_t y, width;
+  uint32_t sid;     // stream index = lg*2 + stream
+};
+struct LfArgs {
+  const LfRow* rows;
+  const int32_t* dc;  // [3][nb]
+  const uint8_t* acs;
+  const uint8_t* qf;
+  uint32_t bxs, bys, lfxs;
+  uint32_t* hist;         // [nstreams][4 leaves][kAlpha]  (hist)
+  uint32_t* sbound;       // [nstreams] (hist)
+  const uint32_t* codes;  // [nstreams][4][kAlpha] (emit)
+  uint32_t* row_bits;     // [nrows]
+  uint64_t* row_off;      // [nrows] absolute scratch bit offset (scan -> emit)
+  const uint32_t* stream_rows;  // [nstreams+1] first row of each stream
+  const uint64_t* stream_base;  // [nstreams] scratch bit offset of each stream
+  uint32_t* stream_bits;        // [nstreams] exact bits (scan)
+  uint32_t* scratch;
+};
+
+struct ConcatPiece {
+  uint64_t src_bit;  // bit offset into the source arena
+  uint64_t dst_bit;  // bit offset into the output
+  uint64_t nbits;
+  uint32_t arena;    // 0 = device scratch, 1 = host-chunk upload
+  uint32_t pad;
+};
+
+void set_front_constants(const float lut[256], const float wts[3][3][64], hipStream_t s);
+void launch_front(const FrontArgs& a, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s);
+void launch_homog(const HomogArgs& a, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s);
+void launch_ac_hist(const AcArgs& a, uint32_t ngroups, hipStream_t s);
+void launch_ac_emit(const AcArgs& a, uint32_t ngroups, hipStream_t s);
+void launch_lf_hist(const LfArgs& a, uint32_t nrows, hipStream_t s);
+void launch_lf_rowbits(const LfArgs& a, uint32_t nrows, hipStream_t s);
+void launch_lf_scan(const LfArgs& a, uint32_t nstreams, hipStream_t s);
+void launch_lf_emit(const LfArgs& a, uint32_t nrows, hipStream_t s);
+void set_cluster_table(const uint8_t* tab, hipStream_t s);
+void launch_concat(const ConcatPiece* pieces, uint32_t npieces, uint64_t max_words,
+                   const uint32_t* scratch, const uint32_t* chunks, uint32_t* out,
+                   hipStream_t s);
+
+}  // namespace jxg

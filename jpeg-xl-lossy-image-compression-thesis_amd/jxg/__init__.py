@@ -1,0 +1,232 @@
+"""jxg -- Python host mirror of the MI355X JPEG XL VarDCT encode path.
+
+Thin ctypes layer over the C ABI in include/jxg.h (libjxg.so, built in-tree
+for gfx950).  It mirrors the reference harness's encoder boundary:
+
+* ``execute_cjxl(input, output, distance, effort)`` follows
+  ``DockerManager::execute_cjxl`` (benchmark-jpegxl/src/docker_manager.rs:
+  100-137): ``mkdir -p dirname(output)``, run the encoder with
+  ``--distance=D --effort=E``, return ``(True, stdout)`` on exit 0 and
+  ``(False, stderr-or-stdout)`` otherwise;
+* ``comp_image_name`` is the ``{stem}-{distance}-{effort}.jxl`` naming of
+  benchmark.rs:644-650 (Rust ``{}`` formatting of f64);
+* ``calculate_mse`` / ``calculate_psnr`` restate image_reader.rs:555-606.
+
+There is no CPU fallback: importing works anywhere, but every encode goes
+through libjxg.so on a HIP device and raises if either is missing.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libjxg.so")
+CLI_PATH = os.path.join(HERE, "jxg_cjxl")
+
+PROPOSAL_P = 1
+PROPOSAL_F = 2
+FLAG_H1_INT_ABS = 1
+FLAG_KEEP_MAPS = 2
+
+
+class JxgError(RuntimeError):
+    pass
+
+
+class _Params(ctypes.Structure):
+    _fields_ = [("distance", ctypes.c_float), ("effort", ctypes.c_int),
+                ("proposals", ctypes.c_uint32), ("num_devices", ctypes.c_int),
+                ("flags", ctypes.c_uint32), ("device", ctypes.c_int)]
+
+
+class _Buffer(ctypes.Structure):
+    _fields_ = [("data", ctypes.POINTER(ctypes.c_uint8)), ("size", ctypes.c_size_t)]
+
+
+class _Stats(ctypes.Structure):
+    _fields_ = [("xsize", ctypes.c_uint32), ("ysize", ctypes.c_uint32),
+                ("xsize_blocks", ctypes.c_uint32), ("ysize_blocks", ctypes.c_uint32),
+                ("num_groups", ctypes.c_uint32), ("num_lf_groups", ctypes.c_uint32),
+                ("global_scale", ctypes.c_uint32), ("quant_dc", ctypes.c_uint32),
+                ("bytes", ctypes.c_size_t),
+                ("ac_strategy", ctypes.POINTER(ctypes.c_uint8)),
+                ("quant_field", ctypes.POINTER(ctypes.c_uint8)),
+                ("dc", ctypes.POINTER(ctypes.c_int32)),
+                ("ac", ctypes.POINTER(ctypes.c_int32)),
+                ("ac_tokens", ctypes.POINTER(ctypes.c_uint32)),
+                ("homogeneity", ctypes.POINTER(ctypes.c_float)),
+                ("ms_front", ctypes.c_float), ("ms_histogram", ctypes.c_float),
+                ("ms_emit", ctypes.c_float), ("ms_assemble", ctypes.c_float),
+                ("ms_total", ctypes.c_float)]
+
+
+# every symbol declared in include/jxg.h
+EXPORTS = ("jxg_status_str", "jxg_create", "jxg_destroy", "jxg_encode_rgb8",
+           "jxg_encode_rgb8_device", "jxg_encode_batch_rgb8", "jxg_get_stats",
+           "jxg_buffer_free", "jxg_homogeneity_map")
+
+_lib = None
+
+
+def load():
+    """Load libjxg.so (raises JxgError if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise JxgError("libjxg.so not built at %s (run __graft_entry__.build())" % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    vp = ctypes.c_void_p
+    lib.jxg_status_str.restype = ctypes.c_char_p
+    lib.jxg_status_str.argtypes = [ctypes.c_int]
+    lib.jxg_create.argtypes = [ctypes.POINTER(_Params), ctypes.POINTER(vp)]
+    lib.jxg_destroy.argtypes = [vp]
+    lib.jxg_destroy.restype = None
+    lib.jxg_encode_rgb8.argtypes = [vp, vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_size_t,
+                                    ctypes.POINTER(_Buffer)]
+    lib.jxg_encode_rgb8_device.argtypes = [vp, vp, ctypes.c_uint32, ctypes.c_uint32,
+                                           ctypes.c_size_t, ctypes.POINTER(_Buffer)]
+    lib.jxg_get_stats.argtypes = [vp, ctypes.POINTER(_Stats)]
+    lib.jxg_buffer_free.argtypes = [ctypes.POINTER(_Buffer)]
+    lib.jxg_buffer_free.restype = None
+    lib.jxg_homogeneity_map.argtypes = [vp, vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_float,
+                                        ctypes.c_uint32, vp, vp]
+    _lib = lib
+    return lib
+
+
+def _check(st):
+    if st != 0:
+        raise JxgError("jxg: %s (%d)" % (load().jxg_status_str(st).decode(), st))
+
+
+class Encoder:
+    """One encoder context (= one HIP stream + device buffers) on one GPU."""
+
+    def __init__(self, distance=1.0, effort=7, proposals=0, device=0, flags=0, num_devices=1):
+        lib = load()
+        self.params = _Params(distance, effort, proposals, num_devices, flags, device)
+        self._ctx = ctypes.c_void_p()
+        _check(lib.jxg_create(ctypes.byref(self.params), ctypes.byref(self._ctx)))
+
+    def close(self):
+        if self._ctx:
+            load().jxg_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def _take(buf):
+        try:
+            return ctypes.string_at(buf.data, buf.size)
+        finally:
+            load().jxg_buffer_free(ctypes.byref(buf))
+
+    def encode(self, rgb: np.ndarray) -> bytes:
+        """Host (H, W, 3) uint8 -> codestream bytes."""
+        rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
+        h, w, c = rgb.shape
+        if c != 3:
+            raise ValueError("expected (H, W, 3) uint8")
+        buf = _Buffer()
+        _check(load().jxg_encode_rgb8(self._ctx, rgb.ctypes.data, w, h, w * 3, ctypes.byref(buf)))
+        return self._take(buf)
+
+    def encode_device(self, ptr: int, width: int, height: int, row_stride: int | None = None) -> bytes:
+        """Device-resident RGB8 (e.g. ``tensor.data_ptr()`` of a uint8 CUDA tensor)."""
+        buf = _Buffer()
+        _check(load().jxg_encode_rgb8_device(self._ctx, ctypes.c_void_p(ptr), width, height,
+                                             row_stride or width * 3, ctypes.byref(buf)))
+        return self._take(buf)
+
+    def stats(self) -> dict:
+        s = _Stats()
+        _check(load().jxg_get_stats(self._ctx, ctypes.byref(s)))
+        nb = s.xsize_blocks * s.ysize_blocks
+        out = {k: getattr(s, k) for k in ("xsize", "ysize", "xsize_blocks", "ysize_blocks",
+                                          "num_groups", "num_lf_groups", "global_scale",
+                                          "quant_dc", "bytes", "ms_front", "ms_histogram",
+                                          "ms_emit", "ms_assemble", "ms_total")}
+        if s.ac_tokens:
+            out["ac_tokens"] = np.ctypeslib.as_array(s.ac_tokens, (s.num_groups * 3,)).reshape(-1, 3).copy()
+        if s.ac_strategy:
+            shp = (s.ysize_blocks, s.xsize_blocks)
+            out["acs"] = np.ctypeslib.as_array(s.ac_strategy, (nb,)).reshape(shp).copy()
+            out["qf"] = np.ctypeslib.as_array(s.quant_field, (nb,)).reshape(shp).copy()
+            out["dc"] = np.ctypeslib.as_array(s.dc, (3 * nb,)).reshape((3,) + shp).copy()
+            out["ac"] = np.ctypeslib.as_array(s.ac, (nb * 192,)).reshape(shp + (3, 64)).copy()
+            if s.homogeneity:
+                out["homog"] = np.ctypeslib.as_array(s.homogeneity, (nb * 3,)).reshape(shp + (3,)).copy()
+        return out
+
+    def homogeneity_map(self, xyb: np.ndarray, distance: float, flags: int = 0):
+        """Thesis selector over a (3, H, W) float32 XYB frame (H, W multiples of 8)."""
+        xyb = np.ascontiguousarray(xyb, dtype=np.float32)
+        _, ys, xs = xyb.shape
+        r3 = np.zeros((ys // 8, xs // 8, 3), dtype=np.float32)
+        t = np.zeros((ys // 8, xs // 8), dtype=np.uint8)
+        _check(load().jxg_homogeneity_map(self._ctx, xyb.ctypes.data, xs, ys, distance, flags,
+                                          r3.ctypes.data, t.ctypes.data))
+        return r3, t
+
+
+# ---------------------------------------------------------------------------
+# harness mirror (benchmark-jpegxl)
+# ---------------------------------------------------------------------------
+def rust_f64(v: float) -> str:
+    """Rust ``format!("{}", f64)``: 1.0 -> "1", 0.5 -> "0.5"."""
+    if float(v).is_integer():
+        return str(int(v))
+    return repr(float(v))
+
+
+def comp_image_name(stem: str, distance: float, effort: int) -> str:
+    """benchmark.rs:644-650: ``{stem}-{distance}-{effort}.jxl``."""
+    return "%s-%s-%d.jxl" % (stem, rust_f64(distance), effort)
+
+
+def execute_cjxl(input_file: str, output_file: str, distance: float, effort: int,
+                 proposals: str = "none", device: int = 0):
+    """DockerManager::execute_cjxl (docker_manager.rs:100-137) with the GPU
+    encoder in place of ``/libjxl/build/tools/cjxl``."""
+    d = os.path.dirname(output_file)
+    if d:
+        os.makedirs(d, exist_ok=True)
+    if not os.path.exists(CLI_PATH):
+        raise JxgError("jxg_cjxl not built at %s" % CLI_PATH)
+    args = [CLI_PATH, input_file, output_file, "--distance=%s" % rust_f64(distance),
+            "--effort=%d" % effort, "--proposals=%s" % proposals, "--device=%d" % device]
+    p = subprocess.run(args, capture_output=True, text=True)
+    if p.returncode == 0:
+        return True, p.stdout
+    return False, p.stderr or p.stdout
+
+
+def calculate_mse(orig: np.ndarray, comp: np.ndarray) -> float:
+    """image_reader.rs:569-593: f64 sum of squared sample differences / count."""
+    o = np.asarray(orig, dtype=np.float64).ravel()
+    c = np.asarray(comp, dtype=np.float64).ravel()
+    if o.size != c.size:
+        raise ValueError("sample count mismatch")
+    return float(np.sum((o - c) ** 2) / o.size)
+
+
+def calculate_psnr(mse: float, max_value: float = 255.0) -> float:
+    """image_reader.rs:604-606."""
+    return 10.0 * math.log10((max_value * max_value) / mse) if mse > 0 else float("inf")

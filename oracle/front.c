@@ -144,46 +144,65 @@ void jxo_frame_init(jxo_frame* f, uint32_t w, uint32_t h, const jxo_params* p) {
   for (int k = 0; k < 3; k++) jxo_quant_weights(k, f->wts[k]);
 }
 
-/* ---------- transforms (fmaf chains, fixed order) ---------- */
-static float T8[8][8], T4[4][4];
-static int tables_ready = 0;
-static void init_tables(void) {
-  if (tables_ready) return;
-  for (int k = 0; k < 8; k++)
-    for (int n = 0; n < 8; n++)
-      T8[k][n] = (float)((k == 0 ? 1.0 : 1.4142135623730951) / 8.0 *
-                         cos(3.14159265358979323846 * (2 * n + 1) * k / 16.0));
-  for (int k = 0; k < 4; k++)
-    for (int n = 0; n < 4; n++)
-      T4[k][n] = (float)((k == 0 ? 1.0 : 1.4142135623730951) / 4.0 *
-                         cos(3.14159265358979323846 * (2 * n + 1) * k / 8.0));
-  tables_ready = 1;
+/* ---------- transforms ----------
+ * DCT-II scaled so that out[0] is the mean (out[k] = a_k/N sum x_n
+ * cos(pi(2n+1)k/2N), a_0 = 1, a_k = sqrt 2), computed by a fixed even/odd
+ * butterfly with explicit fmaf chains.  The constants are float(sqrt2/N *
+ * cos(...)) written as hex literals; the HIP kernel uses the same sequence. */
+#define K_A 0x1.63150cp-3f  /* sqrt2/8 cos(pi/16)  */
+#define K_B 0x1.2d062ep-3f  /* sqrt2/8 cos(3pi/16) */
+#define K_C 0x1.92469cp-4f  /* sqrt2/8 cos(5pi/16) */
+#define K_D 0x1.1a855ep-5f  /* sqrt2/8 cos(7pi/16) */
+#define K_E1 0x1.4e7aeap-3f /* sqrt2/8 cos(pi/8)   */
+#define K_E3 0x1.1517a8p-4f /* sqrt2/8 cos(3pi/8)  */
+#define K_F1 0x1.4e7aeap-2f /* sqrt2/4 cos(pi/8)   */
+#define K_F3 0x1.1517a8p-3f /* sqrt2/4 cos(3pi/8)  */
+
+static void dct8_1d(float* v, int st) {
+  const float x0 = v[0], x1 = v[st], x2 = v[2 * st], x3 = v[3 * st], x4 = v[4 * st],
+              x5 = v[5 * st], x6 = v[6 * st], x7 = v[7 * st];
+  const float s0 = x0 + x7, s1 = x1 + x6, s2 = x2 + x5, s3 = x3 + x4;
+  const float d0 = x0 - x7, d1 = x1 - x6, d2 = x2 - x5, d3 = x3 - x4;
+  const float a0 = s0 + s3, a1 = s1 + s2, b0 = s0 - s3, b1 = s1 - s2;
+  v[0] = (a0 + a1) * 0.125f;
+  v[4 * st] = (a0 - a1) * 0.125f;
+  v[2 * st] = fmaf(b1, K_E3, b0 * K_E1);
+  v[6 * st] = fmaf(b1, -K_E1, b0 * K_E3);
+  v[1 * st] = fmaf(d3, K_D, fmaf(d2, K_C, fmaf(d1, K_B, d0 * K_A)));
+  v[3 * st] = fmaf(d3, -K_C, fmaf(d2, -K_A, fmaf(d1, -K_D, d0 * K_B)));
+  v[5 * st] = fmaf(d3, K_B, fmaf(d2, K_D, fmaf(d1, -K_A, d0 * K_C)));
+  v[7 * st] = fmaf(d3, -K_A, fmaf(d2, K_B, fmaf(d1, -K_C, d0 * K_D)));
+}
+static void dct4_1d(float* v, int st) {
+  const float x0 = v[0], x1 = v[st], x2 = v[2 * st], x3 = v[3 * st];
+  const float s0 = x0 + x3, s1 = x1 + x2, d0 = x0 - x3, d1 = x1 - x2;
+  v[0] = (s0 + s1) * 0.25f;
+  v[2 * st] = (s0 - s1) * 0.25f;
+  v[st] = fmaf(d1, K_F3, d0 * K_F1);
+  v[3 * st] = fmaf(d1, -K_F1, d0 * K_F3);
 }
 
 /* 2D DCT of an R x C region (row stride 8) -> out[R][C]; rows first */
 static void dct2d(const float* in, int R, int C, float* out) {
-  float tmp[8][8];
-  const float* TC = C == 8 ? &T8[0][0] : &T4[0][0];
-  const float* TR = R == 8 ? &T8[0][0] : &T4[0][0];
+  float t[64];
   for (int r = 0; r < R; r++)
-    for (int k = 0; k < C; k++) {
-      float acc = 0.0f;
-      for (int n = 0; n < C; n++) acc = fmaf(in[r * 8 + n], TC[k * C + n], acc);
-      tmp[r][k] = acc;
-    }
-  for (int k = 0; k < R; k++)
-    for (int c = 0; c < C; c++) {
-      float acc = 0.0f;
-      for (int n = 0; n < R; n++) acc = fmaf(tmp[n][c], TR[k * R + n], acc);
-      out[k * C + c] = acc;
-    }
+    for (int c = 0; c < C; c++) t[r * 8 + c] = in[r * 8 + c];
+  for (int r = 0; r < R; r++) {
+    if (C == 8) dct8_1d(t + r * 8, 1);
+    else dct4_1d(t + r * 8, 1);
+  }
+  for (int c = 0; c < C; c++) {
+    if (R == 8) dct8_1d(t + c, 8);
+    else dct4_1d(t + c, 8);
+  }
+  for (int r = 0; r < R; r++)
+    for (int c = 0; c < C; c++) out[r * C + c] = t[r * 8 + c];
 }
 
 /* forward transform of one channel of an 8x8 block into the coefficient
  * layout of raw strategy t [ext enc_transforms-inl.h].  Slot 0 is unused by
  * the AC coder (DC travels in the LF image). */
 void jxo_transform(int t, const float* px /* 8x8, stride 8 */, float* co) {
-  init_tables();
   float o[64];
   if (t == JXO_DCT8) {
     dct2d(px, 8, 8, co);
@@ -252,6 +271,22 @@ static int qkind(int t) {
 /* Quantize one block under strategy t.  Channel order Y, X, B (Y first: X/B
  * subtract the dequantized Y -- CfL with ytox=0, ytob base 1.0).  Returns the
  * rate/distortion cost; writes q[3][64] (X,Y,B order) if q != NULL. */
+/* raster position (in the coefficient layout of t) of the transform's
+ * working-array element p = prow*8 + pcol (inverse of the layout permutation
+ * applied in jxo_transform). */
+static int co_index(int t, int p) {
+  const int prow = p >> 3, pcol = p & 7;
+  if (t == JXO_DCT8) return p;
+  if (t == JXO_DCT4X4)
+    return ((prow >> 2) + 2 * (prow & 3)) * 8 + (pcol >> 2) + 2 * (pcol & 3);
+  if (t == JXO_DCT8X4) return ((prow >> 2) + 2 * (prow & 3)) * 8 + pcol;
+  return ((pcol >> 2) + 2 * (pcol & 3)) * 8 + prow; /* JXO_DCT4X8 */
+}
+
+/* The distortion sum follows the GPU decomposition (8 lanes per block, lane r
+ * owns working-array column r after the column pass): per channel, lane
+ * partials over rows k = 0..7 (skipping the DC slot), then the 8 partials
+ * summed in lane order; channels in order Y, X, B. */
 float jxo_quantize_block(const jxo_frame* f, int t, const float px[3][64],
                          float scale, int32_t q[3][64]) {
   float co[3][64];
@@ -264,22 +299,30 @@ float jxo_quantize_block(const jxo_frame* f, int t, const float px[3][64],
   for (int ci = 0; ci < 3; ci++) {
     const int c = corder[ci];
     int nz = 0;
-    for (int k = 1; k < 64; k++) {
-      const float ws = f->wts[qk][c][k] * scale;
-      float r = co[c][k];
-      if (c == 2) r = r - yd[k];
-      const float v = r * ws;
-      const int qq = quant1(v);
-      if (c == 1) yd[k] = adjust_bias(1, qq) / ws;
-      const uint32_t aq = (uint32_t)(qq < 0 ? -qq : qq);
-      const float e = fabsf(v) - (float)aq;
-      dist += e * e;
-      if (aq) {
-        bits += 2 + 2 * bitlen(aq);
-        nz++;
+    float dch = 0.0f;
+    for (int r = 0; r < 8; r++) {
+      float part = 0.0f;
+      for (int k = 0; k < 8; k++) {
+        const int ci_ = co_index(t, k * 8 + r);
+        if (ci_ == 0) continue;
+        const float ws = f->wts[qk][c][ci_] * scale;
+        float rv = co[c][ci_];
+        if (c == 2) rv = rv - yd[ci_];
+        const float v = rv * ws;
+        const int qq = quant1(v);
+        if (c == 1) yd[ci_] = adjust_bias(1, qq) / ws;
+        const uint32_t aq = (uint32_t)(qq < 0 ? -qq : qq);
+        const float e = fabsf(v) - (float)aq;
+        part += e * e;
+        if (aq) {
+          bits += 2 + 2 * bitlen(aq);
+          nz++;
+        }
+        if (q) q[c][ci_] = qq;
       }
-      if (q) q[c][k] = qq;
+      dch += part;
     }
+    dist += dch;
     bits += bitlen((uint32_t)nz);
     if (q) q[c][0] = 0;
   }

@@ -1,0 +1,87 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle.
+
+Bit-exact on everything integer: codestream bytes, AC strategy map, quant
+field, quantized DC/AC, per-group AC token counts; bit-exact (IEEE bit
+patterns, NaN/inf included) on the thesis similarity indices.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+# (width, height, distance, effort, proposals)
+CASES = [
+    (64, 64, 1.0, 7, 0),
+    (200, 136, 1.0, 7, 3),
+    (256, 256, 1.0, 7, 0),
+    (300, 200, 2.0, 5, 1),
+    (512, 512, 1.0, 7, 2),
+    (777, 333, 0.5, 7, 3),
+    (1, 1, 1.0, 7, 3),
+    (9, 7, 3.0, 7, 3),
+    (2100, 72, 1.0, 7, 0),
+    (520, 2050, 12.0, 4, 1),
+    (640, 480, 25.0, 7, 3),
+    (640, 480, 0.1, 3, 0),
+]
+
+
+@pytest.mark.parametrize("w,h,d,e,p", CASES)
+def test_encode_matches_oracle(jxg_mod, oracle, decoder, w, h, d, e, p):
+    from jxg.synth import synth_rgb8
+
+    img = synth_rgb8(w, h, 0x4A584C00 + w * 7 + h)
+    with jxg_mod.Encoder(distance=d, effort=e, proposals=p, flags=jxg_mod.FLAG_KEEP_MAPS) as enc:
+        got = enc.encode(img)
+        st = enc.stats()
+    ref = oracle.encode(img, d, e, p)
+    assert np.array_equal(st["acs"], ref.acs)
+    assert np.array_equal(st["qf"], ref.qf)
+    assert np.array_equal(st["dc"], ref.dc)
+    assert np.array_equal(st["ac"], ref.ac)
+    assert np.array_equal(st["ac_tokens"], ref.ac_tokens)
+    if p:
+        assert np.array_equal(st["homog"].view(np.uint32), ref.homog.view(np.uint32))
+    assert got == ref.bytes
+    if w * h <= 300 * 200:
+        dec = decoder.decode(got)
+        assert np.array_equal(dec.acs, ref.acs)
+        assert np.array_equal(dec.ac, ref.ac)
+
+
+def test_device_resident_input(jxg_mod):
+    torch = pytest.importorskip("torch")
+    from jxg.synth import synth_rgb8
+
+    img = synth_rgb8(480, 320, 7)
+    t = torch.from_numpy(img).cuda()
+    with jxg_mod.Encoder(distance=1.0, effort=7) as enc:
+        a = enc.encode(img)
+        b = enc.encode_device(t.data_ptr(), 480, 320)
+    assert a == b
+
+
+@pytest.mark.parametrize("d,h1", [(1.0, 0), (2.5, 0), (12.0, 0), (1.0, 1)])
+def test_homogeneity_map_bitexact(jxg_mod, oracle, d, h1):
+    rng = np.random.default_rng(int(d * 10) + h1)
+    xyb = np.stack([rng.uniform(-0.03, 0.03, (136, 200)),
+                    rng.uniform(0.0, 0.85, (136, 200)),
+                    rng.uniform(0.0, 0.85, (136, 200))]).astype(np.float32)
+    xyb[:, :, 96:] = np.repeat(xyb[:, :, 96:97], 104, axis=2)  # flat region
+    xyb[:, 40:96, :64] = 0.0                                     # all-zero: 0/0 -> NaN
+    with jxg_mod.Encoder() as enc:
+        r3, t = enc.homogeneity_map(xyb, d, h1)
+    rr, tt = oracle.homog_map(xyb, d, h1)
+    assert np.array_equal(r3.view(np.uint32), rr.view(np.uint32))
+    assert np.array_equal(t, tt)
+    assert np.isnan(r3).any()
+
+
+def test_4k_matches_oracle(jxg_mod, oracle):
+    from jxg.synth import config_image
+
+    img = config_image(1)
+    with jxg_mod.Encoder(distance=1.0, effort=7) as enc:
+        got = enc.encode(img)
+    ref = oracle.encode(img, 1.0, 7, 0)
+    assert got == ref.bytes
