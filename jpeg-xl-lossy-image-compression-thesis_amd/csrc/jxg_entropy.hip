@@ -1,6 +1,6 @@
 // jxg_entropy.hip -- token statistics and bit emission on gfx950.
 //
-// Pass groups (256x256 px, 32x32 blocks): one 256-thread workgroup per group.
+// Pass groups (256x256 px, 32x32 blocks): one 1024-thread workgroup per group.
 //   ac_hist : non-zero counts -> tokens -> clustered histograms (LDS, then one
 //             global atomic per non-empty bin) + exact per-group token counts
 //             and a bit upper bound used to place the group's scratch region.
@@ -79,7 +79,9 @@ __device__ void fill_nz(const AcArgs& a, const GroupGeom& G, uint8_t (*sNz)[1024
   }
 }
 
-__global__ __launch_bounds__(256) void ac_hist_kernel(AcArgs a) {
+constexpr int kAcThreads = 1024;
+
+__global__ __launch_bounds__(kAcThreads) void ac_hist_kernel(AcArgs a) {
   __shared__ uint32_t sHist[kMaxClusters * kAlpha];
   __shared__ uint8_t sNz[3][1024];
   __shared__ uint8_t sClu[kAcCtx];
@@ -154,11 +156,11 @@ struct BitSink {
   __device__ __forceinline__ void finish() { flush_word((uint32_t)acc, n); }
 };
 
-__global__ __launch_bounds__(256) void ac_emit_kernel(AcArgs a) {
+__global__ __launch_bounds__(kAcThreads) void ac_emit_kernel(AcArgs a) {
   __shared__ uint8_t sNz[3][1024];
   __shared__ uint8_t sClu[kAcCtx];
   __shared__ uint32_t sOff[3 * 1024];
-  __shared__ uint32_t sScan[256];
+  __shared__ uint32_t sScan[kAcThreads];
   const int g = blockIdx.x;
   const GroupGeom G = group_geom(a, g);
   for (int i = threadIdx.x; i < kAcCtx; i += blockDim.x) sClu[i] = c_cluster[i];
@@ -182,13 +184,13 @@ __global__ __launch_bounds__(256) void ac_emit_kernel(AcArgs a) {
   }
   __syncthreads();
   // exclusive scan over tasks in stream order: thread i owns [i*per, (i+1)*per)
-  const int per = (ntask + 255) / 256;
+  const int per = (ntask + kAcThreads - 1) / kAcThreads;
   const int t0 = threadIdx.x * per;
   uint32_t local = 0;
   for (int t = t0; t < t0 + per && t < ntask; t++) local += sOff[t];
   sScan[threadIdx.x] = local;
   __syncthreads();
-  for (int d = 1; d < 256; d <<= 1) {
+  for (int d = 1; d < kAcThreads; d <<= 1) {
     uint32_t v = threadIdx.x >= d ? sScan[threadIdx.x - d] : 0;
     __syncthreads();
     sScan[threadIdx.x] += v;
@@ -218,7 +220,7 @@ __global__ __launch_bounds__(256) void ac_emit_kernel(AcArgs a) {
                  });
     s.finish();
   }
-  if (threadIdx.x == 255) a.bits[g] = sScan[255];
+  if (threadIdx.x == kAcThreads - 1) a.bits[g] = sScan[kAcThreads - 1];
 }
 
 // ----------------------------- LF groups -----------------------------------
@@ -285,10 +287,10 @@ __global__ __launch_bounds__(256) void lf_hist_kernel(LfArgs a) {
   if (threadIdx.x == 0) sBound = 0;
   __syncthreads();
   uint32_t bound = 0;
-  for (uint32_t x = threadIdx.x; x < r.width; x += blockDim.x) {
+  for (uint32_t i = threadIdx.x; i < r.width; i += blockDim.x) {
     uint32_t u, tok, nb, bits;
     int leaf;
-    lf_residual(a, r, L, (int)x, u, leaf);
+    lf_residual(a, r, L, (int)(r.x0 + i), u, leaf);
     hybrid420(u, tok, nb, bits);
     atomicAdd(&sHist[leaf * kAlpha + tok], 1u);
     bound += 15u + nb;
@@ -321,9 +323,9 @@ __global__ __launch_bounds__(256) void lf_rowbits_kernel(LfArgs a) {
   if (threadIdx.x == 0) sSum = 0;
   __syncthreads();
   uint32_t s = 0;
-  for (uint32_t x = threadIdx.x; x < r.width; x += blockDim.x) {
+  for (uint32_t i = threadIdx.x; i < r.width; i += blockDim.x) {
     uint32_t code, clen, nb, bits;
-    s += lf_sample_bits(a, r, L, (int)x, code, clen, nb, bits);
+    s += lf_sample_bits(a, r, L, (int)(r.x0 + i), code, clen, nb, bits);
   }
   atomicAdd(&sSum, s);
   __syncthreads();
@@ -363,7 +365,7 @@ __global__ __launch_bounds__(256) void lf_emit_kernel(LfArgs a) {
   for (uint32_t x0 = 0; x0 < r.width; x0 += blockDim.x) {
     const uint32_t x = x0 + threadIdx.x;
     uint32_t code = 0, clen = 0, nb = 0, bits = 0, tot = 0;
-    if (x < r.width) tot = lf_sample_bits(a, r, L, (int)x, code, clen, nb, bits);
+    if (x < r.width) tot = lf_sample_bits(a, r, L, (int)(r.x0 + x), code, clen, nb, bits);
     sScan[threadIdx.x] = tot;
     __syncthreads();
     for (int d = 1; d < 256; d <<= 1) {
@@ -412,10 +414,10 @@ __global__ __launch_bounds__(256) void concat_kernel(const ConcatPiece* pieces,
 
 // ------------------------------- launchers ---------------------------------
 void launch_ac_hist(const AcArgs& a, uint32_t ngroups, hipStream_t s) {
-  hipLaunchKernelGGL(ac_hist_kernel, dim3(ngroups), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(ac_hist_kernel, dim3(ngroups), dim3(kAcThreads), 0, s, a);
 }
 void launch_ac_emit(const AcArgs& a, uint32_t ngroups, hipStream_t s) {
-  hipLaunchKernelGGL(ac_emit_kernel, dim3(ngroups), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(ac_emit_kernel, dim3(ngroups), dim3(kAcThreads), 0, s, a);
 }
 void launch_lf_hist(const LfArgs& a, uint32_t nrows, hipStream_t s) {
   hipLaunchKernelGGL(lf_hist_kernel, dim3(nrows), dim3(256), 0, s, a);

@@ -217,22 +217,26 @@ static jxg_status init_constants(Ctx* c) {
   return JXG_OK;
 }
 
-// LF-group rows: (lf group, stream, channel, y) in stream order
+// LF-group row segments: (lf group, stream, channel, y, x0) in stream order
 static void build_rows(const Frame& f, std::vector<LfRow>& rows, std::vector<uint32_t>& srows) {
   rows.clear();
   srows.clear();
+  auto add = [&](uint32_t lg, uint16_t stream, uint16_t ch, uint32_t y, uint32_t width) {
+    for (uint32_t x0 = 0; x0 < width; x0 += kLfSeg)
+      rows.push_back({lg, stream, ch, y, x0, std::min(kLfSeg, width - x0), lg * 2 + stream});
+  };
   for (uint32_t lg = 0; lg < f.nlf; lg++) {
     const uint32_t bx0 = (lg % f.lfxs) * 256, by0 = (lg / f.lfxs) * 256;
     const uint32_t bw = std::min(256u, f.bxs - bx0), bh = std::min(256u, f.bys - by0);
     srows.push_back((uint32_t)rows.size());
     for (uint16_t ch = 0; ch < 3; ch++)
-      for (uint32_t y = 0; y < bh; y++) rows.push_back({lg, 0, ch, y, bw, lg * 2});
+      for (uint32_t y = 0; y < bh; y++) add(lg, 0, ch, y, bw);
     srows.push_back((uint32_t)rows.size());
     const uint32_t cw = (bw + 7) / 8, chh = (bh + 7) / 8;
     for (uint16_t ch = 0; ch < 2; ch++)
-      for (uint32_t y = 0; y < chh; y++) rows.push_back({lg, 1, ch, y, cw, lg * 2 + 1});
-    for (uint32_t y = 0; y < 2; y++) rows.push_back({lg, 1, 2, y, bw * bh, lg * 2 + 1});
-    for (uint32_t y = 0; y < bh; y++) rows.push_back({lg, 1, 3, y, bw, lg * 2 + 1});
+      for (uint32_t y = 0; y < chh; y++) add(lg, 1, ch, y, cw);
+    for (uint32_t y = 0; y < 2; y++) add(lg, 1, 2, y, bw * bh);
+    for (uint32_t y = 0; y < bh; y++) add(lg, 1, 3, y, bw);
   }
   srows.push_back((uint32_t)rows.size());
 }

@@ -51,12 +51,16 @@ struct AcArgs {
 };
 
 // LF-group modular streams: rows of (lf group, stream, channel, y)
+// One segment of <= kLfSeg samples of a channel row (long rows -- the
+// 2 x count AC-strategy/quant-field channel -- are split so every workgroup
+// does one pass).
+constexpr uint32_t kLfSeg = 256;
 struct LfRow {
   uint32_t lg;      // LF group
   uint16_t stream;  // 0 = DC, 1 = AC metadata
   uint16_t chan;
-  uint32_t y, width;
-  uint32_t sid;     // stream index = lg*2 + stream
+  uint32_t y, x0, width;  // samples [x0, x0 + width) of row y
+  uint32_t sid;           // stream index = lg*2 + stream
 };
 struct LfArgs {
   const LfRow* rows;

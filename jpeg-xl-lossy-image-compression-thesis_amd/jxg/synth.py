@@ -4,8 +4,8 @@
 (seed ^ tile index) picks one of {flat, horizontal gradient, vertical
 gradient, horizontal stripes, vertical stripes, diagonal checker, quadrant
 edge, uniform noise, smooth-plus-noise} and its two colours; per-pixel noise is
-splitmix64(seed, x, y, c).  One tile in five of the flat kind is all-black,
-which drives the thesis selector's 0/0 -> NaN -> DCT path
+one splitmix64(seed, x, y) whose low three bytes feed R, G, B.  One flat tile in
+five is all-black, which drives the thesis selector's 0/0 -> NaN -> DCT path
 (proposals/combined.diff:209-211).  Seeds: 0x4A584C00 + config index.
 """
 from __future__ import annotations
@@ -13,16 +13,13 @@ from __future__ import annotations
 import numpy as np
 
 SEED_BASE = 0x4A584C00
-_M = np.uint64(0xFFFFFFFFFFFFFFFF)
 
 
 def _splitmix64(x: np.ndarray) -> np.ndarray:
-    with np.errstate(over="ignore"):
-        x = x.astype(np.uint64) + np.uint64(0x9E3779B97F4A7C15)
-        z = x
-        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
-        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
-        return z ^ (z >> np.uint64(31))
+    x = x.astype(np.uint64) + np.uint64(0x9E3779B97F4A7C15)
+    z = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
 
 
 def synth_rgb8(w: int, h: int, seed: int) -> np.ndarray:
@@ -32,26 +29,27 @@ def synth_rgb8(w: int, h: int, seed: int) -> np.ndarray:
 
 
 def _synth(w: int, h: int, seed: int) -> np.ndarray:
-    seed = np.uint64(seed & 0xFFFFFFFFFFFFFFFF)
-    ys, xs = np.mgrid[0:h, 0:w]
-    ys = ys.astype(np.int64)
-    xs = xs.astype(np.int64)
-    ntx = (w + 63) // 64
-    tile = (ys // 64) * ntx + (xs // 64)
-    th = _splitmix64(np.uint64(seed) ^ tile.astype(np.uint64))
-    kind = (th % np.uint64(9)).astype(np.int64)
-    lx = xs % 64
-    ly = ys % 64
-    out = np.zeros((h, w, 3), dtype=np.int64)
-    pix_key = (ys.astype(np.uint64) << np.uint64(32)) | (xs.astype(np.uint64) << np.uint64(2))
+    s = np.uint64(seed & 0xFFFFFFFFFFFFFFFF)
+    ntx, nty = (w + 63) // 64, (h + 63) // 64
+    th = _splitmix64(s ^ np.arange(ntx * nty, dtype=np.uint64)).reshape(nty, ntx)
+    kind_t = (th % np.uint64(9)).astype(np.int8)
+    period_t = (2 + (th >> np.uint64(56)) % np.uint64(14)).astype(np.int32)
+    black_t = ((th >> np.uint64(40)) % np.uint64(5)) == 0
+    ty = np.arange(h) // 64
+    tx = np.arange(w) // 64
+    kind = kind_t[ty][:, tx]
+    period = period_t[ty][:, tx]
+    ly = (np.arange(h, dtype=np.int32) % 64)[:, None]
+    lx = (np.arange(w, dtype=np.int32) % 64)[None, :]
+    key = (np.arange(h, dtype=np.uint64)[:, None] << np.uint64(32)) | np.arange(w, dtype=np.uint64)[None, :]
+    noise64 = _splitmix64((s * np.uint64(0x100000001B3)) ^ key)
+    out = np.empty((h, w, 3), dtype=np.uint8)
+    cond = [kind == k for k in range(9)]
     for c in range(3):
-        c0 = ((th >> np.uint64(8 + 8 * c)) & np.uint64(0xFF)).astype(np.int64)
-        c1 = ((th >> np.uint64(32 + 8 * c)) & np.uint64(0xFF)).astype(np.int64)
-        noise = (_splitmix64(seed * np.uint64(0x100000001B3) ^ pix_key ^ np.uint64(c))
-                 & np.uint64(0xFF)).astype(np.int64)
-        period = 2 + ((th >> np.uint64(56)) % np.uint64(14)).astype(np.int64)
-        black = ((th >> np.uint64(40)) % np.uint64(5)) == 0
-        flat = np.where(black, 0, c0)
+        c0 = ((th >> np.uint64(8 + 8 * c)) & np.uint64(0xFF)).astype(np.int32)[ty][:, tx]
+        c1 = ((th >> np.uint64(32 + 8 * c)) & np.uint64(0xFF)).astype(np.int32)[ty][:, tx]
+        noise = ((noise64 >> np.uint64(8 * c)) & np.uint64(0xFF)).astype(np.int32)
+        flat = np.where(black_t[ty][:, tx], 0, c0)
         hgrad = c0 + (c1 - c0) * lx // 63
         vgrad = c0 + (c1 - c0) * ly // 63
         hstripe = np.where((ly // period) % 2 == 0, c0, c1)
@@ -59,12 +57,9 @@ def _synth(w: int, h: int, seed: int) -> np.ndarray:
         checker = np.where(((lx // period + ly // period) % 2) == 0, c0, c1)
         quad = np.where((lx < 32) ^ (ly < 32), c0, c1)
         smooth = (hgrad + vgrad) // 2 + (noise % 17) - 8
-        choices = [flat, hgrad, vgrad, hstripe, vstripe, checker, quad, noise, smooth]
-        v = np.zeros_like(xs)
-        for k, arr in enumerate(choices):
-            v = np.where(kind == k, arr, v)
+        v = np.select(cond, [flat, hgrad, vgrad, hstripe, vstripe, checker, quad, noise, smooth])
         out[..., c] = np.clip(v, 0, 255)
-    return out.astype(np.uint8)
+    return out
 
 
 # SURVEY.md §8(d) workload shapes: (name, width, height, frames)
