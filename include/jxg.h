@@ -69,6 +69,8 @@ typedef struct {
   const float* homogeneity;    /* [blocks][3] r_h r_v r_d (if P|F) */
   /* device time per stage, milliseconds (last encode) */
   float ms_front, ms_histogram, ms_emit, ms_assemble, ms_total;
+  /* host wall clock of the whole call and of the host-side code/header work */
+  float ms_host_call, ms_host_codes, ms_host_layout;
 } jxg_stats;
 
 const char* jxg_status_str(jxg_status s);

@@ -172,4 +172,31 @@ __device__ __forceinline__ int nz_bucket(int n) {
   return n < 8 ? n : 4 + n / 2;
 }
 
+// bit sink writing into a zero-initialised word buffer with atomicOr
+struct BitSink {
+  uint32_t* buf;
+  uint64_t pos;  // absolute bit position of acc's bit 0
+  uint64_t acc;
+  int n;
+  __device__ __forceinline__ void flush_word(uint32_t lo, int nb) {
+    if (nb == 0) return;
+    const uint64_t w = pos >> 5;
+    const int sh = (int)(pos & 31);
+    atomicOr(&buf[w], lo << sh);
+    if (sh && (sh + nb > 32)) atomicOr(&buf[w + 1], lo >> (32 - sh));
+  }
+  __device__ __forceinline__ void put(uint32_t nbits, uint32_t v) {
+    if (nbits == 0) return;
+    acc |= (uint64_t)v << n;
+    n += (int)nbits;
+    if (n >= 32) {
+      flush_word((uint32_t)acc, 32);
+      pos += 32;
+      acc >>= 32;
+      n -= 32;
+    }
+  }
+  __device__ __forceinline__ void finish() { flush_word((uint32_t)acc, n); }
+};
+
 }  // namespace jxg

@@ -1,12 +1,6 @@
 // jxg_entropy.hip -- token statistics and bit emission on gfx950.
 //
-// Pass groups (256x256 px, 32x32 blocks): one 1024-thread workgroup per group.
-//   ac_hist : non-zero counts -> tokens -> clustered histograms (LDS, then one
-//             global atomic per non-empty bin) + exact per-group token counts
-//             and a bit upper bound used to place the group's scratch region.
-//   ac_emit : same token walk with the prefix codes: per-(block,channel) bit
-//             lengths -> workgroup exclusive scan -> every task writes its bits
-//             at its offset with atomicOr into the zeroed scratch region.
+// (pass-group AC kernels: jxg_ac.hip)
 // LF groups (modular streams of quantized DC and AC metadata) are processed
 // one row per workgroup: lf_hist -> lf_rowbits -> lf_scan -> lf_emit.
 // concat  : bit-exact assembly of all sections (device scratch + host chunks)
@@ -17,211 +11,6 @@
 #include "jxg_kernels.h"
 
 namespace jxg {
-
-__constant__ uint8_t c_cluster[kAcCtx];  // context -> static cluster id
-
-struct GroupGeom {
-  int bx0, by0, gw, gh;
-};
-__device__ __forceinline__ GroupGeom group_geom(const AcArgs& a, int g) {
-  GroupGeom r;
-  const int gx = g % (int)a.gxs, gy = g / (int)a.gxs;
-  r.bx0 = gx * 32;
-  r.by0 = gy * 32;
-  r.gw = min(32, (int)a.bxs - r.bx0);
-  r.gh = min(32, (int)a.bys - r.by0);
-  return r;
-}
-
-__device__ __forceinline__ int count_nz(const int32_t* q) {
-  const int4* q4 = reinterpret_cast<const int4*>(q);
-  int nz = 0;
-#pragma unroll
-  for (int i = 0; i < 16; i++) {
-    const int4 v = q4[i];
-    nz += (i > 0 && v.x != 0) + (v.y != 0) + (v.z != 0) + (v.w != 0);
-  }
-  return nz;
-}
-
-// Walk the tokens of one (block, channel): f(ctx, value).
-template <class F>
-__device__ __forceinline__ void block_tokens(const int32_t* q, int nz, int pred, int bctx, F&& f) {
-  f(nz_bucket(pred) * kBlockCtx + bctx, (uint32_t)nz);
-  const int zoff = kBlockCtx * kNzBuckets + kZdCtx * bctx;
-  int prev = nz > 4 ? 0 : 1;
-  int left = nz;
-  for (int k = 1; k < 64 && left > 0; k++) {
-    const int32_t v = q[k];
-    f(zoff + (kNnzCtx[left] + kFreqCtx[k]) * 2 + prev, pack_signed(v));
-    prev = v != 0;
-    left -= prev;
-  }
-}
-
-__device__ __forceinline__ int predict_nz(const uint8_t* nzc, int bx, int by) {
-  if (bx == 0) return by == 0 ? 32 : nzc[(by - 1) * 32 + bx];
-  if (by == 0) return nzc[by * 32 + bx - 1];
-  return (nzc[(by - 1) * 32 + bx] + nzc[by * 32 + bx - 1] + 1) / 2;
-}
-
-__device__ __forceinline__ int block_ctx_of(int c, int acs) {
-  return kDefaultCtxMap[(c < 2 ? c ^ 1 : 2) * 13 + kStrategyOrder[acs]];
-}
-
-__device__ void fill_nz(const AcArgs& a, const GroupGeom& G, uint8_t (*sNz)[1024]) {
-  const int ntask = G.gw * G.gh * 3;
-  for (int t = threadIdx.x; t < ntask; t += blockDim.x) {
-    const int b = t / 3, c = t - b * 3;
-    const int bx = b % G.gw, by = b / G.gw;
-    const size_t gb = (size_t)(G.by0 + by) * a.bxs + G.bx0 + bx;
-    sNz[c][by * 32 + bx] = (uint8_t)count_nz(a.ac + (gb * 3 + c) * 64);
-  }
-}
-
-constexpr int kAcThreads = 1024;
-
-__global__ __launch_bounds__(kAcThreads) void ac_hist_kernel(AcArgs a) {
-  __shared__ uint32_t sHist[kMaxClusters * kAlpha];
-  __shared__ uint8_t sNz[3][1024];
-  __shared__ uint8_t sClu[kAcCtx];
-  __shared__ uint32_t sBound, sNtok[3];
-  const int g = blockIdx.x;
-  const GroupGeom G = group_geom(a, g);
-  for (int i = threadIdx.x; i < kMaxClusters * kAlpha; i += blockDim.x) sHist[i] = 0;
-  for (int i = threadIdx.x; i < kAcCtx; i += blockDim.x) sClu[i] = c_cluster[i];
-  if (threadIdx.x < 3) sNtok[threadIdx.x] = 0;
-  if (threadIdx.x == 0) sBound = 0;
-  fill_nz(a, G, sNz);
-  __syncthreads();
-  const int ntask = G.gw * G.gh * 3;
-  uint32_t bound = 0, nt[3] = {0, 0, 0};
-  for (int t = threadIdx.x; t < ntask; t += blockDim.x) {
-    const int b = t / 3, ci = t - b * 3;
-    const int c = ci == 0 ? 1 : (ci == 1 ? 0 : 2);
-    const int bx = b % G.gw, by = b / G.gw;
-    const size_t gb = (size_t)(G.by0 + by) * a.bxs + G.bx0 + bx;
-    const int32_t* q = a.ac + (gb * 3 + c) * 64;
-    const int nz = sNz[c][by * 32 + bx];
-    uint32_t cnt = 0;
-    block_tokens(q, nz, predict_nz(sNz[c], bx, by), block_ctx_of(c, a.acs[gb]),
-                 [&](int ctx, uint32_t v) {
-                   uint32_t tok, nb, bits;
-                   hybrid420(v, tok, nb, bits);
-                   atomicAdd(&sHist[sClu[ctx] * kAlpha + tok], 1u);
-                   bound += 15u + nb;
-                   cnt++;
-                 });
-    nt[c] += cnt;
-  }
-  atomicAdd(&sBound, bound);
-  atomicAdd(&sNtok[0], nt[0]);
-  atomicAdd(&sNtok[1], nt[1]);
-  atomicAdd(&sNtok[2], nt[2]);
-  __syncthreads();
-  for (int i = threadIdx.x; i < kMaxClusters * kAlpha; i += blockDim.x)
-    if (sHist[i]) atomicAdd(&a.hist[i], sHist[i]);
-  if (threadIdx.x == 0) {
-    a.bound[g] = sBound;
-    a.ntok[g * 3 + 0] = sNtok[0];
-    a.ntok[g * 3 + 1] = sNtok[1];
-    a.ntok[g * 3 + 2] = sNtok[2];
-  }
-}
-
-// bit sink writing into a zero-initialised word buffer with atomicOr
-struct BitSink {
-  uint32_t* buf;
-  uint64_t pos;  // absolute bit position of acc's bit 0
-  uint64_t acc;
-  int n;
-  __device__ __forceinline__ void flush_word(uint32_t lo, int nb) {
-    if (nb == 0) return;
-    const uint64_t w = pos >> 5;
-    const int sh = (int)(pos & 31);
-    atomicOr(&buf[w], lo << sh);
-    if (sh && (sh + nb > 32)) atomicOr(&buf[w + 1], lo >> (32 - sh));
-  }
-  __device__ __forceinline__ void put(uint32_t nbits, uint32_t v) {
-    if (nbits == 0) return;
-    acc |= (uint64_t)v << n;
-    n += (int)nbits;
-    if (n >= 32) {
-      flush_word((uint32_t)acc, 32);
-      pos += 32;
-      acc >>= 32;
-      n -= 32;
-    }
-  }
-  __device__ __forceinline__ void finish() { flush_word((uint32_t)acc, n); }
-};
-
-__global__ __launch_bounds__(kAcThreads) void ac_emit_kernel(AcArgs a) {
-  __shared__ uint8_t sNz[3][1024];
-  __shared__ uint8_t sClu[kAcCtx];
-  __shared__ uint32_t sOff[3 * 1024];
-  __shared__ uint32_t sScan[kAcThreads];
-  const int g = blockIdx.x;
-  const GroupGeom G = group_geom(a, g);
-  for (int i = threadIdx.x; i < kAcCtx; i += blockDim.x) sClu[i] = c_cluster[i];
-  fill_nz(a, G, sNz);
-  __syncthreads();
-  const int ntask = G.gw * G.gh * 3;
-  // pass 1: bits per task
-  for (int t = threadIdx.x; t < ntask; t += blockDim.x) {
-    const int b = t / 3, ci = t - b * 3;
-    const int c = ci == 0 ? 1 : (ci == 1 ? 0 : 2);
-    const int bx = b % G.gw, by = b / G.gw;
-    const size_t gb = (size_t)(G.by0 + by) * a.bxs + G.bx0 + bx;
-    uint32_t bits_t = 0;
-    block_tokens(a.ac + (gb * 3 + c) * 64, sNz[c][by * 32 + bx], predict_nz(sNz[c], bx, by),
-                 block_ctx_of(c, a.acs[gb]), [&](int ctx, uint32_t v) {
-                   uint32_t tok, nb, bits;
-                   hybrid420(v, tok, nb, bits);
-                   bits_t += (a.codes[sClu[ctx] * kAlpha + tok] >> 16) + nb;
-                 });
-    sOff[t] = bits_t;
-  }
-  __syncthreads();
-  // exclusive scan over tasks in stream order: thread i owns [i*per, (i+1)*per)
-  const int per = (ntask + kAcThreads - 1) / kAcThreads;
-  const int t0 = threadIdx.x * per;
-  uint32_t local = 0;
-  for (int t = t0; t < t0 + per && t < ntask; t++) local += sOff[t];
-  sScan[threadIdx.x] = local;
-  __syncthreads();
-  for (int d = 1; d < kAcThreads; d <<= 1) {
-    uint32_t v = threadIdx.x >= d ? sScan[threadIdx.x - d] : 0;
-    __syncthreads();
-    sScan[threadIdx.x] += v;
-    __syncthreads();
-  }
-  uint32_t run = sScan[threadIdx.x] - local;
-  for (int t = t0; t < t0 + per && t < ntask; t++) {
-    const uint32_t v = sOff[t];
-    sOff[t] = run;
-    run += v;
-  }
-  __syncthreads();
-  const uint64_t base = a.base[g];
-  for (int t = threadIdx.x; t < ntask; t += blockDim.x) {
-    const int b = t / 3, ci = t - b * 3;
-    const int c = ci == 0 ? 1 : (ci == 1 ? 0 : 2);
-    const int bx = b % G.gw, by = b / G.gw;
-    const size_t gb = (size_t)(G.by0 + by) * a.bxs + G.bx0 + bx;
-    BitSink s{a.scratch, base + sOff[t], 0, 0};
-    block_tokens(a.ac + (gb * 3 + c) * 64, sNz[c][by * 32 + bx], predict_nz(sNz[c], bx, by),
-                 block_ctx_of(c, a.acs[gb]), [&](int ctx, uint32_t v) {
-                   uint32_t tok, nb, bits;
-                   hybrid420(v, tok, nb, bits);
-                   const uint32_t cl = a.codes[sClu[ctx] * kAlpha + tok];
-                   s.put(cl >> 16, cl & 0xFFFFu);
-                   s.put(nb, bits);
-                 });
-    s.finish();
-  }
-  if (threadIdx.x == kAcThreads - 1) a.bits[g] = sScan[kAcThreads - 1];
-}
 
 // ----------------------------- LF groups -----------------------------------
 struct LfGeom {
@@ -413,12 +202,6 @@ __global__ __launch_bounds__(256) void concat_kernel(const ConcatPiece* pieces,
 }
 
 // ------------------------------- launchers ---------------------------------
-void launch_ac_hist(const AcArgs& a, uint32_t ngroups, hipStream_t s) {
-  hipLaunchKernelGGL(ac_hist_kernel, dim3(ngroups), dim3(kAcThreads), 0, s, a);
-}
-void launch_ac_emit(const AcArgs& a, uint32_t ngroups, hipStream_t s) {
-  hipLaunchKernelGGL(ac_emit_kernel, dim3(ngroups), dim3(kAcThreads), 0, s, a);
-}
 void launch_lf_hist(const LfArgs& a, uint32_t nrows, hipStream_t s) {
   hipLaunchKernelGGL(lf_hist_kernel, dim3(nrows), dim3(256), 0, s, a);
 }
@@ -440,8 +223,5 @@ void launch_concat(const ConcatPiece* pieces, uint32_t npieces, uint64_t max_wor
                      chunks, out);
 }
 
-void set_cluster_table(const uint8_t* tab, hipStream_t s) {
-  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_cluster), tab, kAcCtx, 0, hipMemcpyHostToDevice, s);
-}
 
 }  // namespace jxg

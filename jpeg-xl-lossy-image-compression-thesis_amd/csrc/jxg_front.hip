@@ -4,16 +4,17 @@
 //   -> block DC + adaptive quantization
 //   -> AC-strategy search over the 8x8-class transforms with hooks F
 //      (combined.diff:247-253) and P (:270-274)
-//   -> forward transform, CfL residual, quantization -> int32 coefficients
+//   -> forward transform, CfL residual, quantization -> int16 coefficients
 //      ([block][X,Y,B][64 zigzag]), quantized DC, strategy, quant field.
 //
-// One 256-thread workgroup per 64x64 pixel tile (8x8 blocks).
-// Transform/quantization work is done by 8-lane groups: lane r of a group owns
-// pixel row r for the row pass and working-array column r for the column pass
-// (transpose through a per-group LDS scratch), so each lane carries 8 values
-// per channel instead of a whole block.  A wave runs 8 blocks of one block
-// row with one (wave-uniform) candidate strategy at a time.
-// Float op order == oracle/front.c (see jxo_quantize_block's sum order).
+// One 512-thread workgroup (8 waves) per 64x64 pixel tile; wave w owns block
+// row w.  Within a wave, 8-lane group g owns block column g and lane r owns
+// pixel row r for the row butterfly, then (after an in-register XOR-butterfly
+// transpose) working-array column r for the column butterfly and the
+// quantization of its 8 coefficients.  The candidate strategy is
+// wave-uniform.  The LDS tile uses a one-dword skew per 8-pixel block column
+// (row stride 75) so both the lane = block phase and the lane = row phase are
+// (nearly) bank-conflict free.  Float op order == oracle/front.c.
 #include <float.h>
 
 #include "jxg_device.h"
@@ -25,10 +26,14 @@ __constant__ float c_lut[256];
 __constant__ float c_wts[3][3][64];  // [quant kind][channel X,Y,B][raster k]
 
 constexpr int kTile = 64;
-constexpr int kRows = 66;  // 64 + halo above/below
-constexpr int kW = 72;     // LDS row stride; pixel column gx maps to gx - (tile_x0 - kOff)
-constexpr int kOff = 4;    // interior column 0 at LDS column 4 (16-B aligned)
-constexpr int kXbuf = 8 * 9;  // per-group transpose scratch (8 x 9 floats)
+constexpr int kRows = 66;           // 64 + halo above/below
+constexpr int kS = 75;              // LDS row stride (floats)
+constexpr int kPlane = kRows * kS;  // floats per XYB plane
+constexpr int kThreads = 512;
+
+// LDS offset of tile-local pixel (lx, ly), lx/ly in [0, 66): one dword of
+// skew per interior 8-pixel block column
+__device__ __forceinline__ int lds_at(int lx, int ly) { return ly * kS + lx + ((lx + 7) >> 3); }
 
 // ---------------------------------------------------------------------------
 // thesis homogeneity (combined.diff:17-181) on the LDS tile
@@ -37,9 +42,9 @@ struct Tile {
   const float* X;
   const float* Y;
   const float* B;
-  int ox, oy;  // padded-frame coordinate of LDS (0,0)
+  int ox, oy;  // padded-frame coordinate of tile-local (0,0)
   __device__ __forceinline__ float at(const float* p, int gx, int gy) const {
-    return p[(gy - oy) * kW + (gx - ox)];
+    return p[lds_at(gx - ox, gy - oy)];
   }
 };
 
@@ -58,7 +63,7 @@ __device__ __forceinline__ float lap(const Tile& t, int px, int py) {
 // The Laplacian is recomputed for the column walk instead of being kept in a
 // per-lane array (identical values; keeps the function register-light).
 template <int XS, int YS>
-__device__ float homogeneity(const Tile& t, int x, int y, int bx, int by, float dist,
+__device__ __forceinline__ float homogeneity(const Tile& t, int x, int y, int bx, int by, float dist,
                              int ysize, int h1_int) {
   float thr = 0.25f;
   if ((double)dist > 10.0)
@@ -104,7 +109,7 @@ __device__ float homogeneity(const Tile& t, int x, int y, int bx, int by, float 
   for (int i = 0; i < YS; i++)
 #pragma unroll
     for (int j = 0; j < XS; j++) {
-      const int px = x + bx + j, py = y + by + i;
+      const int px = x0 + j, py = y0 + i;
       if (py + 1 >= ysize) continue;
       const float p = t.at(t.Y, px, py);
       const float l = t.at(t.Y, px - 1, py);
@@ -125,19 +130,19 @@ __device__ float homogeneity(const Tile& t, int x, int y, int bx, int by, float 
 #pragma unroll 1
   for (int i = 0; i < YS; i++)
 #pragma unroll
-    for (int j = 0; j < XS; j++) mx += t.at(t.X, x + bx + j, y + by + i);
+    for (int j = 0; j < XS; j++) mx += t.at(t.X, x0 + j, y0 + i);
   mx /= n;
 #pragma unroll 1
   for (int i = 0; i < YS; i++)
 #pragma unroll
-    for (int j = 0; j < XS; j++) mb += t.at(t.B, x + bx + j, y + by + i);
+    for (int j = 0; j < XS; j++) mb += t.at(t.B, x0 + j, y0 + i);
   mb /= n;
   float vx = 0.0f, vb = 0.0f;
 #pragma unroll 1
   for (int i = 0; i < YS; i++)
 #pragma unroll
     for (int j = 0; j < XS; j++) {
-      const float diff = t.at(t.X, x + bx + j, y + by + i) - mx;
+      const float diff = t.at(t.X, x0 + j, y0 + i) - mx;
       vx += diff * diff;
     }
   vx /= n;
@@ -145,7 +150,7 @@ __device__ float homogeneity(const Tile& t, int x, int y, int bx, int by, float 
   for (int i = 0; i < YS; i++)
 #pragma unroll
     for (int j = 0; j < XS; j++) {
-      const float diff = t.at(t.B, x + bx + j, y + by + i) - mb;
+      const float diff = t.at(t.B, x0 + j, y0 + i) - mb;
       vb += diff * diff;
     }
   vb /= n;
@@ -158,7 +163,7 @@ __device__ float homogeneity(const Tile& t, int x, int y, int bx, int by, float 
 // region r of CalculateHomogeneitySimilarityIndices (combined.diff:189-204):
 // 0 h1(8,4,0,0) 1 h2(8,4,0,4) 2 v1(4,8,0,0) 3 v2(4,8,4,0)
 // 4 (4,4,0,0) 5 (4,4,4,4) 6 (4,4,0,4) 7 (4,4,4,0)
-__device__ float homog_region(const Tile& t, int r, int x, int y, float dist, int ysize,
+__device__ __forceinline__ float homog_region(const Tile& t, int r, int x, int y, float dist, int ysize,
                               int h1) {
   switch (r) {
     case 0: return homogeneity<8, 4>(t, x, y, 0, 0, dist, ysize, h1);
@@ -195,6 +200,11 @@ __device__ __forceinline__ uint8_t partition_of(float rh, float rv, float rd, fl
   return kDCT8;
 }
 
+__device__ __forceinline__ float hook_f(float ret, float rh, float rv, float rd) {
+  const float avg_r = (rh + rv + rd) / 3.0f;
+  return (float)((double)ret * 0.8 * (double)avg_r);
+}
+
 // ---------------------------------------------------------------------------
 // 1-D DCT-II (out[0] = mean), fixed even/odd butterfly; op sequence and hex
 // constants are those of oracle/front.c (dct8_1d / dct4_1d).
@@ -227,8 +237,29 @@ __device__ __forceinline__ void dct4_1d(float* v) {
   v[3] = fmaf(d1, -kF1, d0 * kF3);
 }
 
-// working-array element p = prow*8 + pcol -> raster position in the
-// coefficient layout of strategy T (oracle co_index)
+// 8x8 transpose across the 8 lanes of a group (lane r: row r -> column r)
+// by three XOR butterflies; pure data movement.  The lane-dependent choice is
+// made with bit masks: a select between two array elements would be folded
+// into a dynamically indexed (scratch) array access.
+__device__ __forceinline__ void transpose8(float* v, int r) {
+#pragma unroll
+  for (int d = 4; d >= 1; d >>= 1) {
+    const uint32_t m = (r & d) ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      if (i & d) continue;
+      const int j = i | d;
+      const uint32_t a = __float_as_uint(v[i]), b = __float_as_uint(v[j]);
+      const uint32_t send = (a & m) | (b & ~m);
+      const uint32_t recv = (uint32_t)__shfl_xor((int)send, d);
+      v[i] = __uint_as_float((recv & m) | (a & ~m));
+      v[j] = __uint_as_float((b & m) | (recv & ~m));
+    }
+  }
+}
+
+// working-array element (prow, pcol) -> raster position in the coefficient
+// layout of strategy T (oracle co_index)
 template <int T>
 __device__ __forceinline__ int co_index(int prow, int pcol) {
   if (T == kDCT8) return prow * 8 + pcol;
@@ -252,8 +283,8 @@ __device__ __forceinline__ float adjust_bias_y(int q) {
 __device__ __forceinline__ int quant1(float v) {
   const float a = fabsf(v);
   if (a < 0.58f) return 0;
-  int q = (int)(a + 0.5f);
-  if (q > (1 << 24)) q = 1 << 24;
+  int q = a < 32767.0f ? (int)(a + 0.5f) : 32767;
+  if (q > 32767) q = 32767;
   return v < 0.0f ? -q : q;
 }
 __device__ __forceinline__ int bitlen(uint32_t v) { return v ? 32 - __clz(v) : 0; }
@@ -263,32 +294,41 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-// One 8-lane group quantizes one block under strategy T (channels Y, X, B).
-//   src   : LDS address of the block's top-left pixel in plane X (planes are
-//           kPlane floats apart), row stride kW
-//   r     : lane within the group (0..7), g0 = lane index of the group's lane 0
-//   xb    : the group's transpose scratch (kXbuf floats)
-//   wts   : LDS copy of c_wts
-//   out   : [X,Y,B][64 zigzag] ints of this block, or nullptr
-// Returns the rate/distortion cost (identical in all 8 lanes).
-constexpr int kPlane = kRows * kW;
+// sum of a per-lane value over the 8 lanes of the group, in lane order
+__device__ __forceinline__ float group_sum_ordered(float v, int g0) {
+  float s = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 8; i++) s += __shfl(v, g0 + i);
+  return s;
+}
+
+struct GroupCtx {
+  const float* pix;  // LDS planes X, Y, B (kPlane apart)
+  int ly0;           // tile-local row of the block's pixel row 0 (= lby*8 + 1)
+  int lx0;           // tile-local column of pixel column 0 (= lbx*8 + 1)
+  int r, g0;
+  const float* wts;  // LDS copy of c_wts
+  const uint8_t* inv_order;
+  int16_t* stage;    // this group's 64-entry LDS staging (int16)
+};
+
+// One 8-lane group quantizes one block under strategy T (channels Y, X, B)
+// and returns the rate/distortion cost (same in all 8 lanes).  With out !=
+// nullptr the zigzag-ordered int16 coefficients [X,Y,B][64] are written.
 template <int T>
-__device__ float quantize_group(const float* src, int r, int g0, float* xb,
-                                const float* wts, float scale, int32_t* out,
-                                const uint8_t* inv_order) {
+__device__ __forceinline__ float quantize_group(const GroupCtx& G, float scale, int16_t* out) {
   constexpr int qk = qkind<T>();
   float yd[8];
   int bits = 0;
   float dist = 0.0f;
-#pragma unroll
+#pragma unroll 1  // one channel live at a time (keeps 4 waves/SIMD)
   for (int ci = 0; ci < 3; ci++) {
     const int c = ci == 0 ? 1 : (ci == 1 ? 0 : 2);
+    const float* plane = G.pix + c * kPlane;
+    const int base = lds_at(G.lx0, G.ly0 + G.r);  // 8 contiguous dwords (same skew)
     float v[8];
-    const float* row = src + c * kPlane + r * kW;
-    const float4 lo = *reinterpret_cast<const float4*>(row);
-    const float4 hi = *reinterpret_cast<const float4*>(row + 4);
-    v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
-    v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+#pragma unroll
+    for (int x = 0; x < 8; x++) v[x] = plane[base + x];
     // row pass
     if (T == kDCT8 || T == kDCT8X4) {
       dct8_1d(v);
@@ -296,13 +336,7 @@ __device__ float quantize_group(const float* src, int r, int g0, float* xb,
       dct4_1d(v);
       dct4_1d(v + 4);
     }
-    // transpose: lane r gets working-array column r
-#pragma unroll
-    for (int x = 0; x < 8; x++) xb[r * 9 + x] = v[x];
-    wave_lds_sync();
-#pragma unroll
-    for (int k = 0; k < 8; k++) v[k] = xb[k * 9 + r];
-    wave_lds_sync();
+    transpose8(v, G.r);
     // column pass
     if (T == kDCT8 || T == kDCT4X8) {
       dct8_1d(v);
@@ -312,89 +346,92 @@ __device__ float quantize_group(const float* src, int r, int g0, float* xb,
     }
     // lowest-frequency combine (enc_transforms [ext]); slots per oracle
     if (T == kDCT4X4) {
-      const float A = __shfl(v[0], g0), C = __shfl(v[4], g0);
-      const float B = __shfl(v[0], g0 + 4), D = __shfl(v[4], g0 + 4);
-      if (r == 0) {
+      const float A = __shfl(v[0], G.g0), C = __shfl(v[4], G.g0);
+      const float B = __shfl(v[0], G.g0 + 4), D = __shfl(v[4], G.g0 + 4);
+      if (G.r == 0) {
         v[0] = (((A + B) + C) + D) * 0.25f;
         v[4] = (((A - B) + C) - D) * 0.25f;
-      } else if (r == 4) {
+      } else if (G.r == 4) {
         v[0] = (((A + B) - C) - D) * 0.25f;
         v[4] = (((A - B) - C) + D) * 0.25f;
       }
     } else if (T == kDCT8X4) {
-      if (r == 0) {
+      if (G.r == 0) {
         const float A = v[0], B = v[4];
         v[0] = (A + B) * 0.5f;
         v[4] = (A - B) * 0.5f;
       }
     } else if (T == kDCT4X8) {
-      const float A = __shfl(v[0], g0), B = __shfl(v[0], g0 + 4);
-      if (r == 0) v[0] = (A + B) * 0.5f;
-      if (r == 4) v[0] = (A - B) * 0.5f;
+      const float A = __shfl(v[0], G.g0), B = __shfl(v[0], G.g0 + 4);
+      if (G.r == 0) v[0] = (A + B) * 0.5f;
+      if (G.r == 4) v[0] = (A - B) * 0.5f;
     }
-    // quantize the 8 coefficients of working column r
     int nz = 0;
     float part = 0.0f;
-    int32_t q[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-      const int co = co_index<T>(k, r);
-      q[k] = 0;
-      if (co == 0) continue;
-      const float ws = wts[(qk * 3 + c) * 64 + co] * scale;
-      float rv = v[k];
-      if (c == 2) rv = rv - yd[k];
-      const float vq = rv * ws;
-      const int qq = quant1(vq);
-      if (c == 1) yd[k] = adjust_bias_y(qq) / ws;
-      const uint32_t aq = (uint32_t)(qq < 0 ? -qq : qq);
-      const float e = fabsf(vq) - (float)aq;
-      part += e * e;
-      if (aq) {
-        bits += 2 + 2 * bitlen(aq);
-        nz++;
+      const int co = co_index<T>(k, G.r);
+      int qq = 0;
+      if (co != 0) {
+        const float ws = G.wts[(qk * 3 + c) * 64 + co] * scale;
+        float rv = v[k];
+        if (c == 2) rv = rv - yd[k];
+        const float vq = rv * ws;
+        qq = quant1(vq);
+        if (c == 1) yd[k] = adjust_bias_y(qq) / ws;
+        const uint32_t aq = (uint32_t)(qq < 0 ? -qq : qq);
+        const float e = fabsf(vq) - (float)aq;
+        part += e * e;
+        if (aq) {
+          bits += 2 + 2 * bitlen(aq);
+          nz++;
+        }
       }
-      q[k] = qq;
+      if (out) G.stage[G.inv_order[co]] = (int16_t)qq;
     }
-    // lane partials in lane order (oracle: dch += part for r = 0..7)
-    float dch = 0.0f;
-#pragma unroll
-    for (int i = 0; i < 8; i++) dch += __shfl(part, g0 + i);
-    dist += dch;
+    dist += group_sum_ordered(part, G.g0);
     int nzc = nz;
 #pragma unroll
     for (int i = 1; i < 8; i <<= 1) nzc += __shfl_xor(nzc, i);
-    bits += bitlen((uint32_t)nzc) * (r == 0 ? 1 : 0);
+    bits += G.r == 0 ? bitlen((uint32_t)nzc) : 0;
     if (out) {
-#pragma unroll
-      for (int k = 0; k < 8; k++) out[c * 64 + inv_order[co_index<T>(k, r)]] = q[k];
+      wave_lds_sync();
+      const uint4 w = *reinterpret_cast<const uint4*>(G.stage + 8 * G.r);
+      *reinterpret_cast<uint4*>(out + c * 64 + 8 * G.r) = w;
+      wave_lds_sync();
     }
   }
-  // bits: per-lane coefficient terms + lane 0's nz terms -> group total
 #pragma unroll
   for (int i = 1; i < 8; i <<= 1) bits += __shfl_xor(bits, i);
   const float tmul = T == kDCT8 ? 1.0f : (T == kDCT4X4 ? 1.05f : 1.02f);
   return ((float)bits + 8.0f * dist) * tmul;
 }
 
-__device__ float hook_f(float ret, float rh, float rv, float rd) {
-  const float avg_r = (rh + rv + rd) / 3.0f;
-  return (float)((double)ret * 0.8 * (double)avg_r);
+__device__ __forceinline__ void load_xyb_tile(const FrontArgs& a, const float* lut, float* sPix,
+                                              int ox, int oy) {
+  const float cb = cbrt_det(kOpsinBias);
+  for (int i = threadIdx.x; i < kRows * 66; i += kThreads) {
+    const int ly = i / 66, lx = i - ly * 66;
+    const int gx = ox + lx, gy = oy + ly;
+    float X = 0.0f, Y = 0.0f, B = 0.0f;
+    if (gx >= 0 && gy >= 0 && gx < (int)a.xp && gy < (int)a.yp) {
+      const int sx = gx < (int)a.w ? gx : (int)a.w - 1;
+      const int sy = gy < (int)a.h ? gy : (int)a.h - 1;
+      const uint8_t* p = a.rgb + (size_t)sy * a.stride + 3 * (size_t)sx;
+      pixel_xyb(lut, cb, p[0], p[1], p[2], X, Y, B);
+    }
+    const int o = lds_at(lx, ly);
+    sPix[o] = X;
+    sPix[kPlane + o] = Y;
+    sPix[2 * kPlane + o] = B;
+  }
 }
 
-template <int T>
-__device__ __forceinline__ float run_group(const float* sPix, int lbx, int lby, int r, int g0,
-                                           float* xb, const float* wts, float scale,
-                                           int32_t* out, const uint8_t* inv_order) {
-  const float* src = sPix + (lby * 8 + 1) * kW + kOff + lbx * 8;
-  return quantize_group<T>(src, r, g0, xb, wts, scale, out, inv_order);
-}
-
-__global__ __launch_bounds__(256) void front_kernel(FrontArgs a) {
-  __shared__ __attribute__((aligned(16))) float sPix[3 * kPlane];  // X, Y, B planes
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void front_kernel(FrontArgs a) {
+  __shared__ __attribute__((aligned(16))) float sPix[3 * kPlane];
+  __shared__ __attribute__((aligned(16))) int16_t sStage[8][8][64];
   __shared__ float sLut[256];
   __shared__ float sWts[3 * 3 * 64];
-  __shared__ float sXb[32][kXbuf];  // one transpose scratch per 8-lane group
   __shared__ uint8_t sInv[64];
   __shared__ float sH[8][64];
   __shared__ float sR[64][3];
@@ -403,46 +440,25 @@ __global__ __launch_bounds__(256) void front_kernel(FrontArgs a) {
   __shared__ int sAcs[64];
   const int tid = threadIdx.x;
   const int tx = blockIdx.x, ty = blockIdx.y;
-  const int ox = tx * kTile - kOff, oy = ty * kTile - 1;
-  sLut[tid] = c_lut[tid];
-  for (int i = tid; i < 576; i += 256) sWts[i] = (&c_wts[0][0][0])[i];
+  const int ox = tx * kTile - 1, oy = ty * kTile - 1;
+  if (tid < 256) sLut[tid] = c_lut[tid];
+  for (int i = tid; i < 576; i += kThreads) sWts[i] = (&c_wts[0][0][0])[i];
   if (tid < 64) sInv[tid] = (uint8_t)c_inv_order_h(tid);
   __syncthreads();
-  float* const sX = sPix;
-  float* const sY = sPix + kPlane;
-  float* const sB = sPix + 2 * kPlane;
-  const float cb = cbrt_det(kOpsinBias);
-  for (int i = tid; i < kRows * 66; i += 256) {
-    const int ly = i / 66, lx = i - ly * 66 + (kOff - 1);
-    const int gx = ox + lx, gy = oy + ly;
-    float X = 0.0f, Y = 0.0f, B = 0.0f;
-    if (gx >= 0 && gy >= 0 && gx < (int)a.xp && gy < (int)a.yp) {
-      const int sx = gx < (int)a.w ? gx : (int)a.w - 1;
-      const int sy = gy < (int)a.h ? gy : (int)a.h - 1;
-      const uint8_t* p = a.rgb + (size_t)sy * a.stride + 3 * (size_t)sx;
-      pixel_xyb(sLut, cb, p[0], p[1], p[2], X, Y, B);
-    }
-    sX[ly * kW + lx] = X;
-    sY[ly * kW + lx] = Y;
-    sB[ly * kW + lx] = B;
-  }
+  load_xyb_tile(a, sLut, sPix, ox, oy);
   __syncthreads();
   const int nbx = min(8, (int)a.bxs - tx * 8), nby = min(8, (int)a.bys - ty * 8);
   const int wave = tid >> 6, lane = tid & 63;
   const size_t nb = (size_t)a.bxs * a.bys;
-  const Tile tile{sX, sY, sB, ox, oy};
-  // ---- phase A: thesis homogeneity (lane = block, wave-uniform region) ----
+  const Tile tile{sPix, sPix + kPlane, sPix + 2 * kPlane, ox, oy};
+  // ---- phase A: thesis homogeneity; wave w = region w, lane = block ----
   if (a.proposals & 3u) {
     const int lbx = lane & 7, lby = lane >> 3;
-    const bool valid = lbx < nbx && lby < nby;
-    const int gx0 = tx * kTile + lbx * 8, gy0 = ty * kTile + lby * 8;
-#pragma unroll 1
-    for (int rr = 0; rr < 2; rr++) {
-      const int r = wave + rr * 4;
-      if (valid) sH[r][lane] = homog_region(tile, r, gx0, gy0, a.distance, (int)a.yp, a.h1_int);
-    }
+    if (lbx < nbx && lby < nby)
+      sH[wave][lane] = homog_region(tile, wave, tx * kTile + lbx * 8, ty * kTile + lby * 8,
+                                    a.distance, (int)a.yp, a.h1_int);
     __syncthreads();
-    if (tid < 64 && valid) {
+    if (tid < 64 && lbx < nbx && lby < nby) {
       float h[8];
 #pragma unroll
       for (int r = 0; r < 8; r++) h[r] = sH[r][lane];
@@ -459,23 +475,43 @@ __global__ __launch_bounds__(256) void front_kernel(FrontArgs a) {
       }
     }
   }
-  // ---- phase B: block DC and adaptive quantization (lane = block) ----
-  if (tid < 64) {
-    const int lbx = lane & 7, lby = lane >> 3;
-    if (lbx < nbx && lby < nby) {
-      const size_t gb = (size_t)(ty * 8 + lby) * a.bxs + tx * 8 + lbx;
-      const int base = (lby * 8 + 1) * kW + kOff + lbx * 8;
-      float dc[3];
+  // ---- phases B + C: wave w = block row, group g = block column ----
+  const int g = lane >> 3, r = lane & 7, g0 = lane & ~7;
+  const int lbx = g, lby = wave;
+  const bool valid = lbx < nbx && lby < nby;
+  const int b = lby * 8 + lbx;
+  const size_t gb = (size_t)(ty * 8 + lby) * a.bxs + tx * 8 + lbx;
+  GroupCtx G{sPix, lby * 8 + 1, lbx * 8 + 1, r, g0, sWts, sInv, &sStage[wave][g][0]};
+  int raw = 1;
+  if (valid) {
+    // block DC (row partials in lane order) and AQ activity
+    float dc[3];
 #pragma unroll
-      for (int c = 0; c < 3; c++) {
-        const float* pl = sPix + c * kPlane + base;
-        float s = 0.0f;
+    for (int c = 0; c < 3; c++) {
+      const float* pl = sPix + c * kPlane + lds_at(G.lx0, G.ly0 + r);
+      float rs = 0.0f;
 #pragma unroll
-        for (int y = 0; y < 8; y++)
+      for (int x = 0; x < 8; x++) rs += pl[x];
+      dc[c] = group_sum_ordered(rs, g0) * (1.0f / 64.0f);
+    }
+    const float* Yr = sPix + kPlane + lds_at(G.lx0, G.ly0 + r);
+    const float* Yn = sPix + kPlane + lds_at(G.lx0, G.ly0 + r + 1);
+    float hr = 0.0f, vr = 0.0f;
 #pragma unroll
-          for (int x = 0; x < 8; x++) s += pl[y * kW + x];
-        dc[c] = s * (1.0f / 64.0f);
-      }
+    for (int x = 0; x < 7; x++) hr += fabsf(Yr[x + 1] - Yr[x]);
+    if (r < 7) {
+#pragma unroll
+      for (int x = 0; x < 8; x++) vr += fabsf(Yn[x] - Yr[x]);
+    }
+    const float act = group_sum_ordered(hr + vr, g0);
+    const float am = act * (1.0f / 112.0f);
+    float mult = 1.5f / sqrtf(1.0f + am * 40.0f);
+    if (mult < 0.45f) mult = 0.45f;
+    if (mult > 1.5f) mult = 1.5f;
+    const float qff = a.qf_base * mult;
+    raw = (int)(qff * a.inv_g + 0.5f);
+    raw = raw < 1 ? 1 : (raw > 256 ? 256 : raw);
+    if (r == 0) {
       const float vy = dc[1] * a.dc_mul[1];
       const int qy = vy >= 0.0f ? (int)(vy + 0.5f) : -(int)(-vy + 0.5f);
       const float ydq = (float)qy * a.dc_step[1];
@@ -484,48 +520,21 @@ __global__ __launch_bounds__(256) void front_kernel(FrontArgs a) {
       a.dc[nb + gb] = qy;
       a.dc[gb] = xv >= 0.0f ? (int)(xv + 0.5f) : -(int)(-xv + 0.5f);
       a.dc[2 * nb + gb] = bv >= 0.0f ? (int)(bv + 0.5f) : -(int)(-bv + 0.5f);
-      const float* Yp = sY + base;
-      float act = 0.0f;
-#pragma unroll
-      for (int y = 0; y < 8; y++)
-#pragma unroll
-        for (int x = 0; x < 7; x++) act += fabsf(Yp[y * kW + x + 1] - Yp[y * kW + x]);
-#pragma unroll
-      for (int y = 0; y < 7; y++)
-#pragma unroll
-        for (int x = 0; x < 8; x++) act += fabsf(Yp[(y + 1) * kW + x] - Yp[y * kW + x]);
-      const float am = act * (1.0f / 112.0f);
-      float mult = 1.5f / sqrtf(1.0f + am * 40.0f);
-      if (mult < 0.45f) mult = 0.45f;
-      if (mult > 1.5f) mult = 1.5f;
-      const float qff = a.qf_base * mult;
-      int raw = (int)(qff * a.inv_g + 0.5f);
-      raw = raw < 1 ? 1 : (raw > 256 ? 256 : raw);
-      sRaw[lane] = raw;
+      sRaw[b] = raw;
     }
   }
-  __syncthreads();
-  // ---- phase C: candidate costs.  8-lane groups: group gi (0..7) of a wave
-  // handles block column lbx = gi; the wave walks block rows. ----
-  const int gi = lane >> 3, r = lane & 7, g0 = lane & ~7;
-  float* xb = sXb[wave * 8 + gi];
+  const float scale = (float)a.G * (float)raw / 65536.0f;
   const int ncand = a.effort >= 5 ? 4 : 1;
-  const int lbx = gi;
-  // DCT8 is always evaluated; its coefficients are written right away (most
-  // blocks keep it) and overwritten below for blocks that switch.
-#pragma unroll 1
-  for (int lby = wave; lby < 8; lby += 4) {
-    const bool valid = lbx < nbx && lby < nby;
-    if (!valid) continue;
-    const int b = lby * 8 + lbx;
-    const float scale = (float)a.G * (float)sRaw[b] / 65536.0f;
-    const size_t gb = (size_t)(ty * 8 + lby) * a.bxs + tx * 8 + lbx;
-    const float e = run_group<kDCT8>(sPix, lbx, lby, r, g0, xb, sWts, scale, a.ac + gb * 192, sInv);
-    if (r == 0) sCost[0][b] = e;
+  int16_t* out = a.ac + gb * 192;
+  if (valid) {
+    // DCT8 is always evaluated; its coefficients are written right away (most
+    // blocks keep it) and overwritten below for blocks that switch.
+    const float e0 = quantize_group<kDCT8>(G, scale, out);
+    if (r == 0) sCost[0][b] = e0;
     if (ncand > 1) {
-      const float e1 = run_group<kDCT4X4>(sPix, lbx, lby, r, g0, xb, sWts, scale, nullptr, sInv);
-      const float e2 = run_group<kDCT4X8>(sPix, lbx, lby, r, g0, xb, sWts, scale, nullptr, sInv);
-      const float e3 = run_group<kDCT8X4>(sPix, lbx, lby, r, g0, xb, sWts, scale, nullptr, sInv);
+      const float e1 = quantize_group<kDCT4X4>(G, scale, nullptr);
+      const float e2 = quantize_group<kDCT4X8>(G, scale, nullptr);
+      const float e3 = quantize_group<kDCT8X4>(G, scale, nullptr);
       if (r == 0) {
         sCost[1][b] = e1;
         sCost[2][b] = e2;
@@ -538,61 +547,52 @@ __global__ __launch_bounds__(256) void front_kernel(FrontArgs a) {
   if (tid < 64) {
     const int bx_ = lane & 7, by_ = lane >> 3;
     if (bx_ < nbx && by_ < nby) {
-      const int cand[4] = {kDCT8, kDCT4X4, kDCT4X8, kDCT8X4};
       int best_t = kDCT8;
       if (ncand > 1) {
         float best = FLT_MAX;
-        for (int i = 0; i < ncand; i++) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const int cand = i == 0 ? kDCT8 : (i == 1 ? kDCT4X4 : (i == 2 ? kDCT4X8 : kDCT8X4));
           float e = sCost[i][lane];
           if (a.proposals & 2u) e = hook_f(e, sR[lane][0], sR[lane][1], sR[lane][2]);
           if (e < best) {
             best = e;
-            best_t = cand[i];
+            best_t = cand;
           }
         }
       }
       if ((a.proposals & 1u) && best_t == kDCT8)
         best_t = partition_of(sR[lane][0], sR[lane][1], sR[lane][2], a.distance);
       sAcs[lane] = best_t;
-      const size_t gb = (size_t)(ty * 8 + by_) * a.bxs + tx * 8 + bx_;
-      a.acs[gb] = (uint8_t)best_t;
-      a.qf[gb] = (uint8_t)(sRaw[lane] - 1);
+      const size_t gbl = (size_t)(ty * 8 + by_) * a.bxs + tx * 8 + bx_;
+      a.acs[gbl] = (uint8_t)best_t;
+      a.qf[gbl] = (uint8_t)(sRaw[lane] - 1);
     }
   }
   __syncthreads();
   // ---- phase E: final coefficients for blocks that left DCT8 ----
-#pragma unroll 1
-  for (int lby = wave; lby < 8; lby += 4) {
-    const bool valid = lbx < nbx && lby < nby;
-    const int b = lby * 8 + lbx;
-    const int t = valid ? sAcs[b] : kDCT8;
-    if (t == kDCT8) continue;
-    const float scale = (float)a.G * (float)sRaw[b] / 65536.0f;
-    int32_t* out = a.ac + ((size_t)(ty * 8 + lby) * a.bxs + tx * 8 + lbx) * 192;
-    if (t == kDCT4X4)
-      run_group<kDCT4X4>(sPix, lbx, lby, r, g0, xb, sWts, scale, out, sInv);
-    else if (t == kDCT4X8)
-      run_group<kDCT4X8>(sPix, lbx, lby, r, g0, xb, sWts, scale, out, sInv);
-    else
-      run_group<kDCT8X4>(sPix, lbx, lby, r, g0, xb, sWts, scale, out, sInv);
-  }
+  const int t = valid ? sAcs[b] : kDCT8;
+  if (t == kDCT4X4) quantize_group<kDCT4X4>(G, scale, out);
+  if (t == kDCT4X8) quantize_group<kDCT4X8>(G, scale, out);
+  if (t == kDCT8X4) quantize_group<kDCT8X4>(G, scale, out);
 }
 
 // standalone thesis selector over a given XYB frame (parity entry point)
-__global__ __launch_bounds__(256) void homog_kernel(HomogArgs a) {
+__global__ __launch_bounds__(kThreads) void homog_kernel(HomogArgs a) {
   __shared__ float sPix[3 * kPlane];
   __shared__ float sH[8][64];
   const int tid = threadIdx.x;
   const int tx = blockIdx.x, ty = blockIdx.y;
-  const int ox = tx * kTile - kOff, oy = ty * kTile - 1;
-  for (int i = tid; i < kRows * 66; i += 256) {
-    const int ly = i / 66, lx = i - ly * 66 + (kOff - 1);
+  const int ox = tx * kTile - 1, oy = ty * kTile - 1;
+  for (int i = tid; i < kRows * 66; i += kThreads) {
+    const int ly = i / 66, lx = i - ly * 66;
     const int gx = ox + lx, gy = oy + ly;
     const bool in = gx >= 0 && gy >= 0 && gx < (int)a.xsize && gy < (int)a.ysize;
     const size_t o = (size_t)gy * a.stride + gx;
-    sPix[ly * kW + lx] = in ? a.xyb[o] : 0.0f;
-    sPix[kPlane + ly * kW + lx] = in ? a.xyb[a.plane + o] : 0.0f;
-    sPix[2 * kPlane + ly * kW + lx] = in ? a.xyb[2 * a.plane + o] : 0.0f;
+    const int l = lds_at(lx, ly);
+    sPix[l] = in ? a.xyb[o] : 0.0f;
+    sPix[kPlane + l] = in ? a.xyb[a.plane + o] : 0.0f;
+    sPix[2 * kPlane + l] = in ? a.xyb[2 * a.plane + o] : 0.0f;
   }
   __syncthreads();
   const int bxs = (int)a.xsize / 8, bys = (int)a.ysize / 8;
@@ -600,12 +600,9 @@ __global__ __launch_bounds__(256) void homog_kernel(HomogArgs a) {
   const int lbx = lane & 7, lby = lane >> 3;
   const bool valid = tx * 8 + lbx < bxs && ty * 8 + lby < bys;
   const Tile tile{sPix, sPix + kPlane, sPix + 2 * kPlane, ox, oy};
-  const int gx0 = tx * kTile + lbx * 8, gy0 = ty * kTile + lby * 8;
-#pragma unroll 1
-  for (int rr = 0; rr < 2; rr++) {
-    const int r = wave + rr * 4;
-    if (valid) sH[r][lane] = homog_region(tile, r, gx0, gy0, a.distance, (int)a.ysize, a.h1_int);
-  }
+  if (valid)
+    sH[wave][lane] = homog_region(tile, wave, tx * kTile + lbx * 8, ty * kTile + lby * 8,
+                                  a.distance, (int)a.ysize, a.h1_int);
   __syncthreads();
   if (tid < 64 && valid) {
     float h[8];
@@ -628,10 +625,10 @@ void set_front_constants(const float lut[256], const float wts[3][3][64], hipStr
                                hipMemcpyHostToDevice, s);
 }
 void launch_front(const FrontArgs& a, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s) {
-  hipLaunchKernelGGL(front_kernel, dim3(tiles_x, tiles_y), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(front_kernel, dim3(tiles_x, tiles_y), dim3(kThreads), 0, s, a);
 }
 void launch_homog(const HomogArgs& a, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s) {
-  hipLaunchKernelGGL(homog_kernel, dim3(tiles_x, tiles_y), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(homog_kernel, dim3(tiles_x, tiles_y), dim3(kThreads), 0, s, a);
 }
 
 }  // namespace jxg

@@ -12,10 +12,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <new>
 #include <vector>
 
@@ -72,6 +74,62 @@ struct PinBuf {
     if (p) (void)hipHostFree(p);
   }
 };
+
+// Output codestreams live in pinned host blocks so the final D2H copy lands
+// in the caller's buffer directly (no bounce copy, no first-touch page
+// faults).  Blocks carry a small header and are recycled through a
+// process-wide pool by jxg_buffer_free.
+struct OutHeader {
+  uint64_t magic;
+  size_t cap;  // usable bytes after the header
+};
+constexpr uint64_t kOutMagic = 0x6a78674f75744275ull;  // "jxgOutBu"
+constexpr size_t kOutHdr = 64;
+static std::mutex g_pool_mu;
+static std::vector<uint8_t*> g_pool;  // free blocks (header addresses)
+
+static uint8_t* out_alloc(size_t bytes) {
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    size_t best = g_pool.size();
+    for (size_t i = 0; i < g_pool.size(); i++) {
+      const size_t cap = reinterpret_cast<OutHeader*>(g_pool[i])->cap;
+      if (cap >= bytes && (best == g_pool.size() ||
+                           cap < reinterpret_cast<OutHeader*>(g_pool[best])->cap))
+        best = i;
+    }
+    if (best < g_pool.size()) {
+      uint8_t* b = g_pool[best];
+      g_pool.erase(g_pool.begin() + best);
+      return b + kOutHdr;
+    }
+  }
+  const size_t cap = std::max<size_t>(bytes + bytes / 8, 1 << 16);
+  void* p = nullptr;
+  if (hipHostMalloc(&p, cap + kOutHdr, hipHostMallocDefault) != hipSuccess) return nullptr;
+  OutHeader* hd = static_cast<OutHeader*>(p);
+  hd->magic = kOutMagic;
+  hd->cap = cap;
+  return static_cast<uint8_t*>(p) + kOutHdr;
+}
+
+static void out_release(uint8_t* data) {
+  if (!data) return;
+  uint8_t* b = data - kOutHdr;
+  if (reinterpret_cast<OutHeader*>(b)->magic != kOutMagic) return;  // not ours
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  if (g_pool.size() < 8) {
+    g_pool.push_back(b);
+    return;
+  }
+  reinterpret_cast<OutHeader*>(b)->magic = 0;
+  (void)hipHostFree(b);
+}
+
+using Clock = std::chrono::steady_clock;
+static float ms_since(Clock::time_point t0) {
+  return std::chrono::duration<float, std::milli>(Clock::now() - t0).count();
+}
 
 // frame-level scalars: same formulas as oracle jxo_frame_init (host, double)
 struct Frame {
@@ -184,7 +242,8 @@ struct Ctx {
   bool constants_ready = false;
   // device
   DevBuf<uint8_t> rgb, acs, qf, cluster_map_dummy;
-  DevBuf<int32_t> dc, ac;
+  DevBuf<int32_t> dc;
+  DevBuf<int16_t> ac;
   DevBuf<float> homog, xyb, r3;
   DevBuf<uint8_t> type;
   DevBuf<uint32_t> hist_ac, bound, ntok, codes_ac, gbits, lfhist, sbound, lfcodes, rowbits,
@@ -194,9 +253,13 @@ struct Ctx {
   DevBuf<ConcatPiece> pieces;
   // host
   PinBuf<uint32_t> h_hist_ac, h_bound, h_ntok, h_lfhist, h_sbound, h_gbits, h_sbits;
-  PinBuf<uint32_t> h_out;
+  // LF row segments cached per frame size
+  uint32_t rows_w = 0, rows_h = 0;
+  std::vector<LfRow> rows_h_cache;
+  std::vector<uint32_t> srows_cache;
   std::vector<uint8_t> m_acs, m_qf;
   std::vector<int32_t> m_dc, m_ac;
+  std::vector<int16_t> m_ac16;
   std::vector<uint32_t> m_ntok;
   std::vector<float> m_homog;
   jxg_stats stats{};
@@ -248,7 +311,7 @@ static float elapsed(hipEvent_t a, hipEvent_t b) {
 }
 
 static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32_t h,
-                                size_t stride, jxg_buffer* out) {
+                                size_t stride, jxg_buffer* out, Clock::time_point t_call) {
   hipStream_t s = c->stream;
   const jxg_params& P = c->params;
   const Frame f = make_frame(w, h, P.distance);
@@ -268,9 +331,14 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   JXG_HIP(c->gbits.ensure(f.ngroups));
   JXG_HIP(c->gbase.ensure(f.ngroups));
   const uint32_t nstreams = f.nlf * 2;
-  std::vector<LfRow> rows;
-  std::vector<uint32_t> srows;
-  build_rows(f, rows, srows);
+  const bool new_rows = c->rows_w != w || c->rows_h != h;
+  if (new_rows) {
+    build_rows(f, c->rows_h_cache, c->srows_cache);
+    c->rows_w = w;
+    c->rows_h = h;
+  }
+  const std::vector<LfRow>& rows = c->rows_h_cache;
+  const std::vector<uint32_t>& srows = c->srows_cache;
   const uint32_t nrows = (uint32_t)rows.size();
   JXG_HIP(c->rows.ensure(nrows));
   JXG_HIP(c->lfhist.ensure(nstreams * 4 * kAlpha));
@@ -288,8 +356,10 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   JXG_HIP(c->h_sbound.ensure(nstreams));
   JXG_HIP(c->h_gbits.ensure(f.ngroups));
   JXG_HIP(c->h_sbits.ensure(nstreams));
-  JXG_HIP(hipMemcpyAsync(c->rows.p, rows.data(), nrows * sizeof(LfRow), hipMemcpyHostToDevice, s));
-  JXG_HIP(hipMemcpyAsync(c->stream_rows.p, srows.data(), srows.size() * 4, hipMemcpyHostToDevice, s));
+  if (new_rows) {
+    JXG_HIP(hipMemcpyAsync(c->rows.p, rows.data(), nrows * sizeof(LfRow), hipMemcpyHostToDevice, s));
+    JXG_HIP(hipMemcpyAsync(c->stream_rows.p, srows.data(), srows.size() * 4, hipMemcpyHostToDevice, s));
+  }
 
   // ---------------- stage 1: front end ----------------
   JXG_HIP(hipEventRecord(c->ev[0], s));
@@ -367,15 +437,20 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   JXG_HIP(hipStreamSynchronize(s));
 
   // ---------------- host: codes and header sections ----------------
+  const Clock::time_point t_codes = Clock::now();
   int dense[kMaxClusters];
   std::fill(dense, dense + kMaxClusters, -1);
+  bool used[kMaxClusters];
+  for (int cl = 0; cl < kMaxClusters; cl++) {
+    uint64_t tot = 0;
+    for (int k = 0; k < kAlpha; k++) tot += c->h_hist_ac.p[cl * kAlpha + k];
+    used[cl] = tot != 0;
+  }
   int nhist = 0;
   std::vector<uint8_t> ctxmap(kAcCtx);
   for (int ctx = 0; ctx < kAcCtx; ctx++) {
     const int cl = ac_cluster(ctx);
-    uint64_t tot = 0;
-    for (int k = 0; k < kAlpha; k++) tot += c->h_hist_ac.p[cl * kAlpha + k];
-    if (tot && dense[cl] < 0) dense[cl] = nhist++;
+    if (used[cl] && dense[cl] < 0) dense[cl] = nhist++;
     ctxmap[ctx] = (uint8_t)(dense[cl] < 0 ? 0 : dense[cl]);
   }
   std::vector<PrefixCode> codes(std::max(nhist, 1));
@@ -446,6 +521,7 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
     cursor += ((uint64_t)c->h_sbound.p[i] + 63) & ~31ull;
   }
   const uint64_t scratch_words = cursor / 32 + 2;
+  const float ms_codes = ms_since(t_codes);
   JXG_HIP(c->scratch.ensure(scratch_words));
   JXG_HIP(hipMemcpyAsync(c->codes_ac.p, packed.data(), packed.size() * 4, hipMemcpyHostToDevice, s));
   JXG_HIP(hipMemcpyAsync(c->lfcodes.p, lfpacked.data(), lfpacked.size() * 4, hipMemcpyHostToDevice, s));
@@ -467,6 +543,7 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   JXG_HIP(hipStreamSynchronize(s));
 
   // ---------------- host: layout, TOC, pieces ----------------
+  const Clock::time_point t_layout = Clock::now();
   struct Piece {
     int arena;  // 0 scratch, 1 host chunk
     uint64_t src, nbits;
@@ -525,32 +602,38 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   JXG_HIP(c->chunks.ensure(chunk_words.size()));
   JXG_HIP(c->pieces.ensure(cps.size()));
   JXG_HIP(c->out.ensure(out_words));
-  JXG_HIP(c->h_out.ensure(out_words));
+  uint8_t* host_out = out_alloc(out_words * 4);
+  if (!host_out) return JXG_ERR_OOM;
+  const float ms_layout = ms_since(t_layout);
   JXG_HIP(hipMemcpyAsync(c->chunks.p, chunk_words.data(), chunk_words.size() * 4, hipMemcpyHostToDevice, s));
   JXG_HIP(hipMemcpyAsync(c->pieces.p, cps.data(), cps.size() * sizeof(ConcatPiece), hipMemcpyHostToDevice, s));
   JXG_HIP(hipMemsetAsync(c->out.p, 0, out_words * 4, s));
   launch_concat(c->pieces.p, (uint32_t)cps.size(), max_words, c->scratch.p, c->chunks.p, c->out.p, s);
   JXG_HIP(hipGetLastError());
-  JXG_HIP(hipMemcpyAsync(c->h_out.p, c->out.p, out_words * 4, hipMemcpyDeviceToHost, s));
+  if (hipMemcpyAsync(host_out, c->out.p, out_words * 4, hipMemcpyDeviceToHost, s) != hipSuccess) {
+    out_release(host_out);
+    return JXG_ERR_HIP;
+  }
   JXG_HIP(hipEventRecord(c->ev[4], s));
   if (P.flags & JXG_FLAG_KEEP_MAPS) {
     c->m_acs.resize(nb);
     c->m_qf.resize(nb);
     c->m_dc.resize(nb * 3);
-    c->m_ac.resize(nb * 192);
+    c->m_ac16.resize(nb * 192);
     JXG_HIP(hipMemcpyAsync(c->m_acs.data(), c->acs.p, nb, hipMemcpyDeviceToHost, s));
     JXG_HIP(hipMemcpyAsync(c->m_qf.data(), c->qf.p, nb, hipMemcpyDeviceToHost, s));
     JXG_HIP(hipMemcpyAsync(c->m_dc.data(), c->dc.p, nb * 12, hipMemcpyDeviceToHost, s));
-    JXG_HIP(hipMemcpyAsync(c->m_ac.data(), c->ac.p, nb * 192 * 4, hipMemcpyDeviceToHost, s));
+    JXG_HIP(hipMemcpyAsync(c->m_ac16.data(), c->ac.p, nb * 192 * 2, hipMemcpyDeviceToHost, s));
     if (homog) {
       c->m_homog.resize(nb * 3);
       JXG_HIP(hipMemcpyAsync(c->m_homog.data(), c->homog.p, nb * 12, hipMemcpyDeviceToHost, s));
     }
   }
-  JXG_HIP(hipStreamSynchronize(s));
-  out->data = (uint8_t*)std::malloc(out_bytes);
-  if (!out->data) return JXG_ERR_OOM;
-  std::memcpy(out->data, c->h_out.p, out_bytes);
+  if (hipStreamSynchronize(s) != hipSuccess) {
+    out_release(host_out);
+    return JXG_ERR_HIP;
+  }
+  out->data = host_out;
   out->size = out_bytes;
 
   // stats
@@ -570,10 +653,9 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   if (P.flags & JXG_FLAG_KEEP_MAPS) {
     // AC back to natural (raster) order for the caller
     static const Order64 ord = make_order64();
-    std::vector<int32_t> nat(nb * 192);
+    c->m_ac.assign(nb * 192, 0);
     for (size_t b = 0; b < nb * 3; b++)
-      for (int j = 0; j < 64; j++) nat[b * 64 + ord.v[j]] = c->m_ac[b * 64 + j];
-    c->m_ac.swap(nat);
+      for (int j = 0; j < 64; j++) c->m_ac[b * 64 + ord.v[j]] = c->m_ac16[b * 64 + j];
     S.ac_strategy = c->m_acs.data();
     S.quant_field = c->m_qf.data();
     S.dc = c->m_dc.data();
@@ -585,6 +667,9 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   S.ms_emit = elapsed(c->ev[2], c->ev[3]);
   S.ms_assemble = elapsed(c->ev[3], c->ev[4]);
   S.ms_total = elapsed(c->ev[0], c->ev[4]);
+  S.ms_host_codes = ms_codes;
+  S.ms_host_layout = ms_layout;
+  S.ms_host_call = ms_since(t_call);
   return JXG_OK;
 }
 
@@ -649,10 +734,11 @@ jxg_status jxg_encode_rgb8_device(void* ctx, const void* d_rgb, uint32_t w, uint
       stride < (size_t)w * 3)
     return JXG_ERR_INVALID_ARG;
   Ctx* c = static_cast<Ctx*>(ctx);
+  const Clock::time_point t0 = Clock::now();
   out->data = nullptr;
   out->size = 0;
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
-  return encode_device(c, static_cast<const uint8_t*>(d_rgb), w, h, stride, out);
+  return encode_device(c, static_cast<const uint8_t*>(d_rgb), w, h, stride, out, t0);
 }
 
 jxg_status jxg_encode_rgb8(void* ctx, const uint8_t* rgb, uint32_t w, uint32_t h, size_t stride,
@@ -660,6 +746,7 @@ jxg_status jxg_encode_rgb8(void* ctx, const uint8_t* rgb, uint32_t w, uint32_t h
   if (!ctx || !rgb || !out || w == 0 || h == 0 || w > (1u << 18) || h > (1u << 18) ||
       stride < (size_t)w * 3)
     return JXG_ERR_INVALID_ARG;
+  const Clock::time_point t0 = Clock::now();
   Ctx* c = static_cast<Ctx*>(ctx);
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
   const size_t bytes = stride * (h - 1) + (size_t)w * 3;
@@ -668,7 +755,7 @@ jxg_status jxg_encode_rgb8(void* ctx, const uint8_t* rgb, uint32_t w, uint32_t h
     return JXG_ERR_HIP;
   out->data = nullptr;
   out->size = 0;
-  return encode_device(c, c->rgb.p, w, h, stride, out);
+  return encode_device(c, c->rgb.p, w, h, stride, out, t0);
 }
 
 jxg_status jxg_encode_batch_rgb8(void* ctx, const uint8_t* const* rgbs, uint32_t n, uint32_t w,
@@ -692,7 +779,7 @@ jxg_status jxg_get_stats(void* ctx, jxg_stats* stats) {
 
 void jxg_buffer_free(jxg_buffer* buf) {
   if (!buf) return;
-  std::free(buf->data);
+  out_release(buf->data);
   buf->data = nullptr;
   buf->size = 0;
 }

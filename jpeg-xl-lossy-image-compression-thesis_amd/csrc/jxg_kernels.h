@@ -22,7 +22,7 @@ struct FrontArgs {
   uint8_t* acs;   // [nb] raw strategy
   uint8_t* qf;    // [nb] raw-1
   int32_t* dc;    // [3][nb] X,Y,B
-  int32_t* ac;    // [nb][3 X,Y,B][64 zigzag]
+  int16_t* ac;    // [nb][3 X,Y,B][64 zigzag]
   float* homog;   // [nb][3] or null
 };
 
@@ -39,7 +39,7 @@ struct HomogArgs {
 // AC (pass group) token kernels
 struct AcArgs {
   const uint8_t* acs;
-  const int32_t* ac;
+  const int16_t* ac;  // [nb][3][64 zigzag]
   uint32_t bxs, bys, gxs;
   uint32_t* hist;        // [kMaxClusters][kAlpha]      (hist pass)
   uint32_t* bound;       // [ngroups] bit upper bound   (hist pass)

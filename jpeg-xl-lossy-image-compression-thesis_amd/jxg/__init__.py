@@ -62,7 +62,8 @@ class _Stats(ctypes.Structure):
                 ("homogeneity", ctypes.POINTER(ctypes.c_float)),
                 ("ms_front", ctypes.c_float), ("ms_histogram", ctypes.c_float),
                 ("ms_emit", ctypes.c_float), ("ms_assemble", ctypes.c_float),
-                ("ms_total", ctypes.c_float)]
+                ("ms_total", ctypes.c_float), ("ms_host_call", ctypes.c_float),
+                ("ms_host_codes", ctypes.c_float), ("ms_host_layout", ctypes.c_float)]
 
 
 # every symbol declared in include/jxg.h
@@ -103,6 +104,34 @@ def load():
 def _check(st):
     if st != 0:
         raise JxgError("jxg: %s (%d)" % (load().jxg_status_str(st).decode(), st))
+
+
+class Codestream:
+    """Zero-copy view of a jxg_buffer; released with jxg_buffer_free."""
+
+    def __init__(self, buf):
+        self._buf = buf
+        self.size = buf.size
+
+    def memoryview(self):
+        return memoryview((ctypes.c_uint8 * self.size).from_address(self._buf.data)).cast("B")
+
+    def tobytes(self) -> bytes:
+        return ctypes.string_at(self._buf.data, self.size)
+
+    def __len__(self):
+        return self.size
+
+    def release(self):
+        if self._buf is not None and self._buf.data:
+            load().jxg_buffer_free(ctypes.byref(self._buf))
+        self._buf = None
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:
+            pass
 
 
 class Encoder:
@@ -148,12 +177,16 @@ class Encoder:
         _check(load().jxg_encode_rgb8(self._ctx, rgb.ctypes.data, w, h, w * 3, ctypes.byref(buf)))
         return self._take(buf)
 
-    def encode_device(self, ptr: int, width: int, height: int, row_stride: int | None = None) -> bytes:
-        """Device-resident RGB8 (e.g. ``tensor.data_ptr()`` of a uint8 CUDA tensor)."""
+    def encode_device(self, ptr: int, width: int, height: int, row_stride: int | None = None,
+                      copy: bool = True):
+        """Device-resident RGB8 (e.g. ``tensor.data_ptr()`` of a uint8 CUDA tensor).
+
+        copy=False returns a :class:`Codestream` that owns the library's
+        (pinned) output buffer instead of copying it into ``bytes``."""
         buf = _Buffer()
         _check(load().jxg_encode_rgb8_device(self._ctx, ctypes.c_void_p(ptr), width, height,
                                              row_stride or width * 3, ctypes.byref(buf)))
-        return self._take(buf)
+        return self._take(buf) if copy else Codestream(buf)
 
     def stats(self) -> dict:
         s = _Stats()
@@ -162,7 +195,9 @@ class Encoder:
         out = {k: getattr(s, k) for k in ("xsize", "ysize", "xsize_blocks", "ysize_blocks",
                                           "num_groups", "num_lf_groups", "global_scale",
                                           "quant_dc", "bytes", "ms_front", "ms_histogram",
-                                          "ms_emit", "ms_assemble", "ms_total")}
+                                          "ms_emit", "ms_assemble", "ms_total",
+                                          "ms_host_call", "ms_host_codes",
+                                          "ms_host_layout")}
         if s.ac_tokens:
             out["ac_tokens"] = np.ctypeslib.as_array(s.ac_tokens, (s.num_groups * 3,)).reshape(-1, 3).copy()
         if s.ac_strategy:

@@ -248,11 +248,13 @@ static inline float adjust_bias(int c, int q) {
   if (q == -1) return -kBias[c];
   return (float)q - kBias[3] / (float)q;
 }
+/* dead zone 0.58, round half up, clamp to int16 (the coefficient storage
+ * type of the GPU path; |q| <= 32767 holds for distance >= ~0.05) */
 static inline int quant1(float v) {
   float a = fabsf(v);
   if (a < 0.58f) return 0;
-  int q = (int)(a + 0.5f);
-  if (q > (1 << 24)) q = 1 << 24;
+  int q = a < 32767.0f ? (int)(a + 0.5f) : 32767;
+  if (q > 32767) q = 32767;
   return v < 0.0f ? -q : q;
 }
 static inline int bitlen(uint32_t v) {
@@ -334,11 +336,16 @@ float jxo_quantize_block(const jxo_frame* f, int t, const float px[3][64],
  * writes qf raw (1..256), quantized AC and DC. */
 int jxo_front_block(const jxo_frame* f, const float px[3][64], const float* homog,
                     int32_t q[3][64], int32_t dcq[3], int* qf_raw) {
-  /* block DC = mean (row-major float sum) */
+  /* block DC = mean: row partial sums (left to right), then the 8 row sums
+   * top to bottom -- the 8-lane order of the GPU path (lane = row) */
   float dc[3];
   for (int c = 0; c < 3; c++) {
     float s = 0.0f;
-    for (int i = 0; i < 64; i++) s += px[c][i];
+    for (int y = 0; y < 8; y++) {
+      float rs = 0.0f;
+      for (int x = 0; x < 8; x++) rs += px[c][y * 8 + x];
+      s += rs;
+    }
     dc[c] = s * (1.0f / 64.0f);
   }
   /* DC quantization: Y first, B residual against dequantized Y (base
@@ -352,13 +359,18 @@ int jxo_front_block(const jxo_frame* f, const float px[3][64], const float* homo
   dcq[0] = xv >= 0.0f ? (int)(xv + 0.5f) : -(int)(-xv + 0.5f);
   dcq[2] = bv >= 0.0f ? (int)(bv + 0.5f) : -(int)(-bv + 0.5f);
 
-  /* adaptive quantization: mean absolute gradient of Y inside the block */
+  /* adaptive quantization: mean absolute gradient of Y inside the block;
+   * per row y: horizontal diffs of row y plus vertical diffs to row y+1,
+   * the 8 row partials summed top to bottom (lane order) */
   const float* Y = px[1];
   float act = 0.0f;
-  for (int y = 0; y < 8; y++)
-    for (int x = 0; x < 7; x++) act += fabsf(Y[y * 8 + x + 1] - Y[y * 8 + x]);
-  for (int y = 0; y < 7; y++)
-    for (int x = 0; x < 8; x++) act += fabsf(Y[(y + 1) * 8 + x] - Y[y * 8 + x]);
+  for (int y = 0; y < 8; y++) {
+    float hr = 0.0f, vr = 0.0f;
+    for (int x = 0; x < 7; x++) hr += fabsf(Y[y * 8 + x + 1] - Y[y * 8 + x]);
+    if (y < 7)
+      for (int x = 0; x < 8; x++) vr += fabsf(Y[(y + 1) * 8 + x] - Y[y * 8 + x]);
+    act += hr + vr;
+  }
   float am = act * (1.0f / 112.0f);
   float mult = 1.5f / sqrtf(1.0f + am * 40.0f);
   if (mult < 0.45f) mult = 0.45f;
