@@ -22,16 +22,18 @@ constexpr float kM20 = 0.24342268924547819f, kM21 = 0.20476744424496821f,
                 kM22 = 0.55180986650955360f;
 constexpr float kOpsinBias = 0.0037930732552754493f;
 
+// multiply/fma-only cube root == oracle/xyb.c jxo_cbrtf (bit-identical)
 __device__ __forceinline__ float cbrt_det(float x) {
   if (!(x > 0.0f)) return 0.0f;
-  uint32_t i = __float_as_uint(x) / 3u + 0x2a514067u;
-  float y = __uint_as_float(i);
+  const uint32_t i = 0x54a2fa8cu - __float_as_uint(x) / 3u;
+  float r = __uint_as_float(i);
 #pragma unroll
-  for (int it = 0; it < 4; it++) {
-    float t = y * y;
-    y = (y + y + x / t) / 3.0f;
+  for (int it = 0; it < 3; it++) {
+    const float r3 = (r * r) * r;
+    const float e = fmaf(-x, r3, 1.0f);
+    r = fmaf(r * e, 0x1.555556p-2f, r);
   }
-  return y;
+  return (x * r) * r;
 }
 
 __device__ __forceinline__ void pixel_xyb(const float* lut, float cb, uint32_t r8,
@@ -159,12 +161,14 @@ __host__ __device__ constexpr int c_inv_order_h(int k) {
     if (o.v[j] == k) return j;
   return 0;
 }
-// coefficient slab addressing: block (bx, by) -> 64x64-pixel tile and lane
-__host__ __device__ __forceinline__ size_t coef_index(uint32_t bx, uint32_t by, uint32_t tiles_x,
-                                                      int c, int j) {
-  const size_t tile = (size_t)(by >> 3) * tiles_x + (bx >> 3);
-  const uint32_t lane = (by & 7) * 8 + (bx & 7);
-  return ((tile * 3 + c) * 64 + j) * 64 + lane;
+// transform working-array element (prow, pcol) -> raster position in the
+// 8x8 coefficient layout of strategy T (oracle/front.c co_index); only
+// (0, 0) maps to the DC slot
+__host__ __device__ __forceinline__ int co_index_rt(int T, int prow, int pcol) {
+  if (T == kDCT8) return prow * 8 + pcol;
+  if (T == kDCT4X4) return ((prow >> 2) + 2 * (prow & 3)) * 8 + (pcol >> 2) + 2 * (pcol & 3);
+  if (T == kDCT8X4) return ((prow >> 2) + 2 * (prow & 3)) * 8 + pcol;
+  return ((pcol >> 2) + 2 * (pcol & 3)) * 8 + prow;  // kDCT4X8
 }
 
 __device__ __forceinline__ int nz_bucket(int n) {

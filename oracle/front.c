@@ -248,6 +248,11 @@ static inline float adjust_bias(int c, int q) {
   if (q == -1) return -kBias[c];
   return (float)q - kBias[3] / (float)q;
 }
+/* pairwise (tree) sum of 8 lane partials: ((0+1)+(2+3))+((4+5)+(6+7)) -- the
+ * order an XOR-butterfly reduction over the 8 lanes of a GPU group yields */
+static inline float tree8(const float* v) {
+  return ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+}
 /* dead zone 0.58, round half up, clamp to int16 (the coefficient storage
  * type of the GPU path; |q| <= 32767 holds for distance >= ~0.05) */
 static inline int quant1(float v) {
@@ -286,24 +291,25 @@ static int co_index(int t, int p) {
 }
 
 /* The distortion sum follows the GPU decomposition (8 lanes per block, lane r
- * owns working-array column r after the column pass): per channel, lane
- * partials over rows k = 0..7 (skipping the DC slot), then the 8 partials
- * summed in lane order; channels in order Y, X, B. */
+ * owns working-array column r after the column pass): lane r accumulates
+ * e*e with fmaf over channels Y, X, B and rows k = 0..7 (skipping the DC
+ * slot); the 8 lane partials are then tree-summed (tree8).  The Y dequant
+ * used for the B residual multiplies by the inverse weight (1/w) and the
+ * inverse scale (1/scale), like libjxl's dequantization [ext]. */
 float jxo_quantize_block(const jxo_frame* f, int t, const float px[3][64],
                          float scale, int32_t q[3][64]) {
   float co[3][64];
   for (int c = 0; c < 3; c++) jxo_transform(t, px[c], co[c]);
   const int qk = qkind(t);
+  const float inv_scale = 1.0f / scale;
   float yd[64];
+  float part[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   int bits = 0;
-  float dist = 0.0f;
   static const int corder[3] = {1, 0, 2};
   for (int ci = 0; ci < 3; ci++) {
     const int c = corder[ci];
     int nz = 0;
-    float dch = 0.0f;
     for (int r = 0; r < 8; r++) {
-      float part = 0.0f;
       for (int k = 0; k < 8; k++) {
         const int ci_ = co_index(t, k * 8 + r);
         if (ci_ == 0) continue;
@@ -312,22 +318,21 @@ float jxo_quantize_block(const jxo_frame* f, int t, const float px[3][64],
         if (c == 2) rv = rv - yd[ci_];
         const float v = rv * ws;
         const int qq = quant1(v);
-        if (c == 1) yd[ci_] = adjust_bias(1, qq) / ws;
+        if (c == 1) yd[ci_] = adjust_bias(1, qq) * ((1.0f / f->wts[qk][c][ci_]) * inv_scale);
         const uint32_t aq = (uint32_t)(qq < 0 ? -qq : qq);
         const float e = fabsf(v) - (float)aq;
-        part += e * e;
+        part[r] = fmaf(e, e, part[r]);
         if (aq) {
           bits += 2 + 2 * bitlen(aq);
           nz++;
         }
         if (q) q[c][ci_] = qq;
       }
-      dch += part;
     }
-    dist += dch;
     bits += bitlen((uint32_t)nz);
     if (q) q[c][0] = 0;
   }
+  const float dist = tree8(part);
   static const float tmul[14] = {1.0f, 0, 0, 1.05f, 0, 0, 0, 0, 0, 0, 0, 0, 1.02f, 1.02f};
   return ((float)bits + 8.0f * dist) * tmul[t];
 }
@@ -337,16 +342,15 @@ float jxo_quantize_block(const jxo_frame* f, int t, const float px[3][64],
 int jxo_front_block(const jxo_frame* f, const float px[3][64], const float* homog,
                     int32_t q[3][64], int32_t dcq[3], int* qf_raw) {
   /* block DC = mean: row partial sums (left to right), then the 8 row sums
-   * top to bottom -- the 8-lane order of the GPU path (lane = row) */
+   * tree-summed -- the 8-lane order of the GPU path (lane = row) */
   float dc[3];
   for (int c = 0; c < 3; c++) {
-    float s = 0.0f;
+    float rs[8];
     for (int y = 0; y < 8; y++) {
-      float rs = 0.0f;
-      for (int x = 0; x < 8; x++) rs += px[c][y * 8 + x];
-      s += rs;
+      rs[y] = 0.0f;
+      for (int x = 0; x < 8; x++) rs[y] += px[c][y * 8 + x];
     }
-    dc[c] = s * (1.0f / 64.0f);
+    dc[c] = tree8(rs) * (1.0f / 64.0f);
   }
   /* DC quantization: Y first, B residual against dequantized Y (base
    * correlation b = 1.0, x = 0.0) */
@@ -361,16 +365,17 @@ int jxo_front_block(const jxo_frame* f, const float px[3][64], const float* homo
 
   /* adaptive quantization: mean absolute gradient of Y inside the block;
    * per row y: horizontal diffs of row y plus vertical diffs to row y+1,
-   * the 8 row partials summed top to bottom (lane order) */
+   * the 8 row partials tree-summed (lane order of the GPU path) */
   const float* Y = px[1];
-  float act = 0.0f;
+  float ra[8];
   for (int y = 0; y < 8; y++) {
     float hr = 0.0f, vr = 0.0f;
     for (int x = 0; x < 7; x++) hr += fabsf(Y[y * 8 + x + 1] - Y[y * 8 + x]);
     if (y < 7)
       for (int x = 0; x < 8; x++) vr += fabsf(Y[(y + 1) * 8 + x] - Y[y * 8 + x]);
-    act += hr + vr;
+    ra[y] = hr + vr;
   }
+  const float act = tree8(ra);
   float am = act * (1.0f / 112.0f);
   float mult = 1.5f / sqrtf(1.0f + am * 40.0f);
   if (mult < 0.45f) mult = 0.45f;

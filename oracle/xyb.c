@@ -11,19 +11,24 @@
 
 #include "jxo_internal.h"
 
-/* deterministic cube root: bit-hack seed + 4 Newton steps, each op IEEE */
+/* deterministic cube root, multiply/fma only (no division): bit-hack seed of
+ * x^(-1/3), three Newton steps r <- r + (r*(1 - x*r^3))/3 written with
+ * explicit fmaf, then cbrt = x*r*r.  Every op is a correctly rounded IEEE
+ * mul/fma, so the GPU (jxg_device.h cbrt_det) reproduces it bit for bit.
+ * Max relative error vs cbrt() ~1e-7 over the opsin range [bias, 1.1]. */
 float jxo_cbrtf(float x) {
   if (!(x > 0.0f)) return 0.0f;
   uint32_t i;
   memcpy(&i, &x, 4);
-  i = i / 3u + 0x2a514067u;
-  float y;
-  memcpy(&y, &i, 4);
-  for (int it = 0; it < 4; it++) {
-    float t = y * y;
-    y = (y + y + x / t) / 3.0f;
+  i = 0x54a2fa8cu - i / 3u;
+  float r;
+  memcpy(&r, &i, 4);
+  for (int it = 0; it < 3; it++) {
+    const float r3 = (r * r) * r;
+    const float e = fmaf(-x, r3, 1.0f);
+    r = fmaf(r * e, 0x1.555556p-2f, r);
   }
-  return y;
+  return (x * r) * r;
 }
 
 void jxo_srgb_lut(float lut[256]) {
