@@ -50,12 +50,6 @@ __device__ __forceinline__ void load_coefs(const int16_t* q, uint32_t* w) {
 __device__ __forceinline__ int32_t coef(const uint32_t* w, int k) {
   return (int32_t)(int16_t)(w[k >> 1] >> ((k & 1) * 16));
 }
-__device__ __forceinline__ int count_nz(const uint32_t* w) {
-  int nz = 0;
-#pragma unroll
-  for (int k = 1; k < 64; k++) nz += coef(w, k) != 0;
-  return nz;
-}
 
 // Tokens of one (block, channel): f(ctx, value) in bitstream order.
 template <class F>
@@ -111,13 +105,13 @@ __device__ __forceinline__ Task task_of(const AcArgs& a, const GroupGeom& G, int
   return k;
 }
 
+// non-zero counts of the group's blocks (written by the front kernel)
 __device__ void fill_nz(const AcArgs& a, const GroupGeom& G, uint8_t (*sNz)[1024]) {
-  const int ntask = G.gw * G.gh * 3;
-  for (int t = threadIdx.x; t < ntask; t += blockDim.x) {
-    const Task k = task_of(a, G, t);
-    uint32_t w[32];
-    load_coefs(a.ac + (k.gb * 3 + k.c) * 64, w);
-    sNz[k.c][k.by * 32 + k.bx] = (uint8_t)count_nz(w);
+  const size_t nb = (size_t)a.bxs * a.bys;
+  for (int i = threadIdx.x; i < 3 * 1024; i += blockDim.x) {
+    const int c = i >> 10, by = (i >> 5) & 31, bx = i & 31;
+    if (bx < G.gw && by < G.gh)
+      sNz[c][by * 32 + bx] = a.nz[c * nb + (size_t)(G.by0 + by) * a.bxs + G.bx0 + bx];
   }
 }
 

@@ -2,7 +2,8 @@
 //
 // (pass-group AC kernels: jxg_ac.hip)
 // LF groups (modular streams of quantized DC and AC metadata) are processed
-// one row per workgroup: lf_hist -> lf_rowbits -> lf_scan -> lf_emit.
+// in chunks of <= 4096 samples of one stream per workgroup, 16 consecutive
+// samples per thread: lf_hist -> lf_bits -> lf_scan -> lf_emit.
 // concat  : bit-exact assembly of all sections (device scratch + host chunks)
 //           into the final codestream, one word per lane.
 // Token order, contexts and hybrid-uint split are those of oracle/encode.c
@@ -67,70 +68,101 @@ __device__ __forceinline__ void lf_residual(const LfArgs& a, const LfRow& r, con
   u = pack_signed(v - pred);
 }
 
+// Chunk bookkeeping in LDS: segment starts (sample index within the chunk)
+struct LfChunkLds {
+  LfRow row[kLfChunkRows];
+  uint32_t start[kLfChunkRows + 1];
+};
+
+__device__ __forceinline__ LfChunk load_chunk(const LfArgs& a, LfChunkLds& S) {
+  const LfChunk ch = a.chunks[blockIdx.x];
+  if (threadIdx.x < ch.nrows) S.row[threadIdx.x] = a.rows[ch.row0 + threadIdx.x];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (uint32_t i = 0; i < ch.nrows; i++) {
+      S.start[i] = acc;
+      acc += S.row[i].width;
+    }
+    S.start[ch.nrows] = acc;
+  }
+  __syncthreads();
+  return ch;
+}
+
+// Visit this thread's samples [t*kLfPer, ...) of the chunk in stream order:
+// f(j, u, leaf) for j = 0..cnt-1.
+template <class F>
+__device__ __forceinline__ void for_my_samples(const LfArgs& a, const LfChunk& ch,
+                                               const LfChunkLds& S, F&& f) {
+  const uint32_t first = threadIdx.x * kLfPer;
+  if (first >= ch.nsamp) return;
+  uint32_t seg = 0;
+  while (S.start[seg + 1] <= first) seg++;
+  uint32_t pos = first;
+#pragma unroll
+  for (uint32_t j = 0; j < kLfPer; j++) {
+    if (pos < ch.nsamp) {
+      while (S.start[seg + 1] <= pos) seg++;
+      const LfRow& r = S.row[seg];
+      const LfGeom L = lf_geom(a, r.lg);
+      uint32_t u;
+      int leaf;
+      lf_residual(a, r, L, (int)(r.x0 + pos - S.start[seg]), u, leaf);
+      f(j, u, leaf);
+    }
+    pos++;
+  }
+}
+
 __global__ __launch_bounds__(256) void lf_hist_kernel(LfArgs a) {
   __shared__ uint32_t sHist[4 * kAlpha];
   __shared__ uint32_t sBound;
-  const LfRow r = a.rows[blockIdx.x];
-  const LfGeom L = lf_geom(a, r.lg);
+  __shared__ LfChunkLds S;
   for (int i = threadIdx.x; i < 4 * kAlpha; i += blockDim.x) sHist[i] = 0;
   if (threadIdx.x == 0) sBound = 0;
-  __syncthreads();
+  const LfChunk ch = load_chunk(a, S);
   uint32_t bound = 0;
-  for (uint32_t i = threadIdx.x; i < r.width; i += blockDim.x) {
-    uint32_t u, tok, nb, bits;
-    int leaf;
-    lf_residual(a, r, L, (int)(r.x0 + i), u, leaf);
+  for_my_samples(a, ch, S, [&](uint32_t, uint32_t u, int leaf) {
+    uint32_t tok, nb, bits;
     hybrid420(u, tok, nb, bits);
     atomicAdd(&sHist[leaf * kAlpha + tok], 1u);
     bound += 15u + nb;
-  }
+  });
   atomicAdd(&sBound, bound);
   __syncthreads();
   for (int i = threadIdx.x; i < 4 * kAlpha; i += blockDim.x)
-    if (sHist[i]) atomicAdd(&a.hist[(size_t)r.sid * 4 * kAlpha + i], sHist[i]);
-  if (threadIdx.x == 0) atomicAdd(&a.sbound[r.sid], sBound);
+    if (sHist[i]) atomicAdd(&a.hist[(size_t)ch.sid * 4 * kAlpha + i], sHist[i]);
+  if (threadIdx.x == 0) atomicAdd(&a.sbound[ch.sid], sBound);
 }
 
-__device__ __forceinline__ uint32_t lf_sample_bits(const LfArgs& a, const LfRow& r,
-                                                   const LfGeom& L, int x, uint32_t& code,
-                                                   uint32_t& clen, uint32_t& nb,
-                                                   uint32_t& bits) {
-  uint32_t u, tok;
-  int leaf;
-  lf_residual(a, r, L, x, u, leaf);
-  hybrid420(u, tok, nb, bits);
-  const uint32_t cl = a.codes[((size_t)r.sid * 4 + leaf) * kAlpha + tok];
-  code = cl & 0xFFFFu;
-  clen = cl >> 16;
-  return clen + nb;
-}
-
-__global__ __launch_bounds__(256) void lf_rowbits_kernel(LfArgs a) {
+// exact bits of each chunk
+__global__ __launch_bounds__(256) void lf_bits_kernel(LfArgs a) {
   __shared__ uint32_t sSum;
-  const LfRow r = a.rows[blockIdx.x];
-  const LfGeom L = lf_geom(a, r.lg);
+  __shared__ LfChunkLds S;
   if (threadIdx.x == 0) sSum = 0;
+  const LfChunk ch = load_chunk(a, S);
+  uint32_t sum = 0;
+  for_my_samples(a, ch, S, [&](uint32_t, uint32_t u, int leaf) {
+    uint32_t tok, nb, bits;
+    hybrid420(u, tok, nb, bits);
+    sum += (a.codes[((size_t)ch.sid * 4 + leaf) * kAlpha + tok] >> 16) + nb;
+  });
+  atomicAdd(&sSum, sum);
   __syncthreads();
-  uint32_t s = 0;
-  for (uint32_t i = threadIdx.x; i < r.width; i += blockDim.x) {
-    uint32_t code, clen, nb, bits;
-    s += lf_sample_bits(a, r, L, (int)(r.x0 + i), code, clen, nb, bits);
-  }
-  atomicAdd(&sSum, s);
-  __syncthreads();
-  if (threadIdx.x == 0) a.row_bits[blockIdx.x] = sSum;
+  if (threadIdx.x == 0) a.chunk_bits[blockIdx.x] = sSum;
 }
 
-// per-stream exclusive scan of row bits -> absolute row offsets
+// per-stream exclusive scan of chunk bits -> absolute chunk offsets
 __global__ __launch_bounds__(256) void lf_scan_kernel(LfArgs a) {
   __shared__ uint32_t sScan[256];
   const uint32_t sid = blockIdx.x;
-  const uint32_t r0 = a.stream_rows[sid], r1 = a.stream_rows[sid + 1];
+  const uint32_t r0 = a.stream_chunks[sid], r1 = a.stream_chunks[sid + 1];
   uint64_t run = a.stream_base[sid];
   const uint64_t start = run;
   for (uint32_t c0 = r0; c0 < r1; c0 += blockDim.x) {
     const uint32_t r = c0 + threadIdx.x;
-    const uint32_t v = r < r1 ? a.row_bits[r] : 0;
+    const uint32_t v = r < r1 ? a.chunk_bits[r] : 0;
     sScan[threadIdx.x] = v;
     __syncthreads();
     for (int d = 1; d < 256; d <<= 1) {
@@ -139,39 +171,51 @@ __global__ __launch_bounds__(256) void lf_scan_kernel(LfArgs a) {
       sScan[threadIdx.x] += t;
       __syncthreads();
     }
-    if (r < r1) a.row_off[r] = run + sScan[threadIdx.x] - v;
+    if (r < r1) a.chunk_off[r] = run + sScan[threadIdx.x] - v;
     run += sScan[255];
     __syncthreads();
   }
   if (threadIdx.x == 0) a.stream_bits[sid] = (uint32_t)(run - start);
 }
 
-__global__ __launch_bounds__(256) void lf_emit_kernel(LfArgs a) {
-  __shared__ uint32_t sScan[256];
-  const LfRow r = a.rows[blockIdx.x];
-  const LfGeom L = lf_geom(a, r.lg);
-  uint64_t run = a.row_off[blockIdx.x];
-  for (uint32_t x0 = 0; x0 < r.width; x0 += blockDim.x) {
-    const uint32_t x = x0 + threadIdx.x;
-    uint32_t code = 0, clen = 0, nb = 0, bits = 0, tot = 0;
-    if (x < r.width) tot = lf_sample_bits(a, r, L, (int)(r.x0 + x), code, clen, nb, bits);
-    sScan[threadIdx.x] = tot;
-    __syncthreads();
-    for (int d = 1; d < 256; d <<= 1) {
-      uint32_t v = threadIdx.x >= (uint32_t)d ? sScan[threadIdx.x - d] : 0;
-      __syncthreads();
-      sScan[threadIdx.x] += v;
-      __syncthreads();
-    }
-    if (x < r.width) {
-      BitSink s{a.scratch, run + sScan[threadIdx.x] - tot, 0, 0};
-      s.put(clen, code);
-      s.put(nb, bits);
-      s.finish();
-    }
-    run += sScan[255];
-    __syncthreads();
+// workgroup exclusive scan of one value per thread (256 threads)
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* sWave) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t incl = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t t = __shfl_up(incl, d);
+    if (lane >= d) incl += t;
   }
+  if (lane == 63) sWave[wv] = incl;
+  __syncthreads();
+  uint32_t before = 0;
+  for (int i = 0; i < wv; i++) before += sWave[i];
+  return before + incl - v;
+}
+
+__global__ __launch_bounds__(256) void lf_emit_kernel(LfArgs a) {
+  __shared__ LfChunkLds S;
+  __shared__ uint32_t sWave[4];
+  const LfChunk ch = load_chunk(a, S);
+  uint32_t val[kLfPer], len[kLfPer];
+  uint32_t tot = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kLfPer; j++) len[j] = 0;
+  for_my_samples(a, ch, S, [&](uint32_t j, uint32_t u, int leaf) {
+    uint32_t tok, nb, bits;
+    hybrid420(u, tok, nb, bits);
+    const uint32_t cl = a.codes[((size_t)ch.sid * 4 + leaf) * kAlpha + tok];
+    // prefix code (<= 15 bits) then raw bits (<= 16): at most 31 bits
+    val[j] = (cl & 0xFFFFu) | (bits << (cl >> 16));
+    len[j] = (cl >> 16) + nb;
+    tot += len[j];
+  });
+  const uint32_t off = block_excl_scan256(tot, sWave);
+  BitSink s{a.scratch, a.chunk_off[blockIdx.x] + off, 0, 0};
+#pragma unroll
+  for (uint32_t j = 0; j < kLfPer; j++) s.put(len[j], val[j]);
+  s.finish();
 }
 
 // ------------------------------- concat ------------------------------------
@@ -202,17 +246,17 @@ __global__ __launch_bounds__(256) void concat_kernel(const ConcatPiece* pieces,
 }
 
 // ------------------------------- launchers ---------------------------------
-void launch_lf_hist(const LfArgs& a, uint32_t nrows, hipStream_t s) {
-  hipLaunchKernelGGL(lf_hist_kernel, dim3(nrows), dim3(256), 0, s, a);
+void launch_lf_hist(const LfArgs& a, uint32_t nchunks, hipStream_t s) {
+  hipLaunchKernelGGL(lf_hist_kernel, dim3(nchunks), dim3(256), 0, s, a);
 }
-void launch_lf_rowbits(const LfArgs& a, uint32_t nrows, hipStream_t s) {
-  hipLaunchKernelGGL(lf_rowbits_kernel, dim3(nrows), dim3(256), 0, s, a);
+void launch_lf_bits(const LfArgs& a, uint32_t nchunks, hipStream_t s) {
+  hipLaunchKernelGGL(lf_bits_kernel, dim3(nchunks), dim3(256), 0, s, a);
 }
 void launch_lf_scan(const LfArgs& a, uint32_t nstreams, hipStream_t s) {
   hipLaunchKernelGGL(lf_scan_kernel, dim3(nstreams), dim3(256), 0, s, a);
 }
-void launch_lf_emit(const LfArgs& a, uint32_t nrows, hipStream_t s) {
-  hipLaunchKernelGGL(lf_emit_kernel, dim3(nrows), dim3(256), 0, s, a);
+void launch_lf_emit(const LfArgs& a, uint32_t nchunks, hipStream_t s) {
+  hipLaunchKernelGGL(lf_emit_kernel, dim3(nchunks), dim3(256), 0, s, a);
 }
 void launch_concat(const ConcatPiece* pieces, uint32_t npieces, uint64_t max_words,
                    const uint32_t* scratch, const uint32_t* chunks, uint32_t* out,

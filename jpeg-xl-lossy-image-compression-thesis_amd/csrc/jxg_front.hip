@@ -303,7 +303,8 @@ struct GroupCtx {
 // Quantized values of one candidate: [channel X, Y, B][4 words of 2 x int16]
 // (lane r: working-array column r, rows k = 0..7).
 struct QVals {
-  uint32_t x[4], y[4], b[4];
+  uint32_t w[12];  // [channel X, Y, B][4]
+  uint32_t nz;  // non-zero AC counts of the block: X | Y << 8 | B << 16
 };
 
 // One 8-lane group quantizes one block under strategy T (channels Y, X, B)
@@ -402,11 +403,12 @@ __device__ __forceinline__ float quantize_group(const GroupCtx& G, float scale, 
     }
     const int nzc = group_int_sum(nz);
     bits += G.r == 0 ? bitlen((uint32_t)nzc) : 0;
+    q.nz = ci == 0 ? (uint32_t)nzc << 8 : (q.nz | ((uint32_t)nzc << (c == 0 ? 0 : 16)));
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-      q.x[i] = c == 0 ? pk[i] : q.x[i];
-      q.y[i] = c == 1 ? pk[i] : q.y[i];
-      q.b[i] = c == 2 ? pk[i] : q.b[i];
+      q.w[i] = c == 0 ? pk[i] : q.w[i];
+      q.w[4 + i] = c == 1 ? pk[i] : q.w[4 + i];
+      q.w[8 + i] = c == 2 ? pk[i] : q.w[8 + i];
     }
   }
   bits = group_int_sum(bits);
@@ -417,11 +419,8 @@ __device__ __forceinline__ float quantize_group(const GroupCtx& G, float scale, 
 
 __device__ __forceinline__ void copy_q(QVals& d, const QVals& s, bool take) {
 #pragma unroll
-  for (int i = 0; i < 4; i++) {
-    d.x[i] = take ? s.x[i] : d.x[i];
-    d.y[i] = take ? s.y[i] : d.y[i];
-    d.b[i] = take ? s.b[i] : d.b[i];
-  }
+  for (int i = 0; i < 12; i++) d.w[i] = take ? s.w[i] : d.w[i];
+  d.nz = take ? s.nz : d.nz;
 }
 
 __device__ __forceinline__ void load_xyb_tile(const FrontArgs& a, const float* lut, float* sPix,
@@ -590,6 +589,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     a.acs[gb] = (uint8_t)bt;
     a.qf[gb] = (uint8_t)(raw - 1);
   }
+  if (r < 3) a.nz[r * nb + gb] = (uint8_t)(best.nz >> (8 * r));
   // ---- phase D: zigzag scatter through LDS, 16-byte stores ----
   const int bti = bt == kDCT8 ? 0 : (bt == kDCT4X4 ? 1 : (bt == kDCT4X8 ? 2 : 3));
   const uint2 zz2 = *reinterpret_cast<const uint2*>(sZz + bti * 64 + r * 8);
@@ -598,11 +598,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   int16_t* out = a.ac + gb * 192;
 #pragma unroll
   for (int c = 0; c < 3; c++) {
-    const uint32_t* qc = c == 0 ? best.x : (c == 1 ? best.y : best.b);
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       const int pos = (zw[k >> 2] >> ((k & 3) * 8)) & 0xFF;
-      stage[pos] = (int16_t)(qc[k >> 1] >> ((k & 1) * 16));
+      stage[pos] = (int16_t)(best.w[c * 4 + (k >> 1)] >> ((k & 1) * 16));
     }
     wave_lds_sync();
     *reinterpret_cast<uint4*>(out + c * 64 + 8 * r) =

@@ -5,7 +5,7 @@
 //   ac_hist + lf_hist (token statistics)     [jxg_entropy.hip]
 //   -> D2H histograms; host builds prefix codes, LfGlobal/HfGlobal and the
 //      LF-group stream preludes (a few KB of header bits)
-//   ac_emit + lf_rowbits/lf_scan/lf_emit (bit emission into scratch)
+//   ac_emit + lf_bits/lf_scan/lf_emit (bit emission into scratch)
 //   -> D2H section sizes; host writes headers + TOC and the piece list
 //   concat (bit-exact assembly) -> D2H codestream
 // The byte stream equals the CPU oracle's (oracle/encode.c) bit for bit.
@@ -241,22 +241,24 @@ struct Ctx {
   hipEvent_t ev[6] = {};
   bool constants_ready = false;
   // device
-  DevBuf<uint8_t> rgb, acs, qf, cluster_map_dummy;
+  DevBuf<uint8_t> rgb, acs, qf, nz;
   DevBuf<int32_t> dc;
   DevBuf<int16_t> ac;
   DevBuf<float> homog, xyb, r3;
   DevBuf<uint8_t> type;
-  DevBuf<uint32_t> hist_ac, bound, ntok, codes_ac, gbits, lfhist, sbound, lfcodes, rowbits,
-      stream_rows, stream_bits, scratch, chunks, out;
-  DevBuf<uint64_t> gbase, rowoff, stream_base;
+  DevBuf<uint32_t> hist_ac, bound, ntok, codes_ac, gbits, lfhist, sbound, lfcodes, chunkbits,
+      stream_chunks, stream_bits, scratch, chunks, out;
+  DevBuf<uint64_t> gbase, chunkoff, stream_base;
   DevBuf<LfRow> rows;
+  DevBuf<LfChunk> lfchunks;
   DevBuf<ConcatPiece> pieces;
   // host
   PinBuf<uint32_t> h_hist_ac, h_bound, h_ntok, h_lfhist, h_sbound, h_gbits, h_sbits;
   // LF row segments cached per frame size
   uint32_t rows_w = 0, rows_h = 0;
   std::vector<LfRow> rows_h_cache;
-  std::vector<uint32_t> srows_cache;
+  std::vector<LfChunk> chunks_h_cache;
+  std::vector<uint32_t> schunks_cache;
   std::vector<uint8_t> m_acs, m_qf;
   std::vector<int32_t> m_dc, m_ac;
   std::vector<int16_t> m_ac16;
@@ -281,27 +283,40 @@ static jxg_status init_constants(Ctx* c) {
 }
 
 // LF-group row segments: (lf group, stream, channel, y, x0) in stream order
-static void build_rows(const Frame& f, std::vector<LfRow>& rows, std::vector<uint32_t>& srows) {
+// LF-group row segments: (lf group, stream, channel, y, x0) in stream order,
+// grouped into chunks of one stream (<= kLfChunkSamples samples,
+// <= kLfChunkRows segments)
+static void build_rows(const Frame& f, std::vector<LfRow>& rows, std::vector<LfChunk>& chunks,
+                       std::vector<uint32_t>& schunks) {
   rows.clear();
-  srows.clear();
+  chunks.clear();
+  schunks.clear();
   auto add = [&](uint32_t lg, uint16_t stream, uint16_t ch, uint32_t y, uint32_t width) {
-    for (uint32_t x0 = 0; x0 < width; x0 += kLfSeg)
-      rows.push_back({lg, stream, ch, y, x0, std::min(kLfSeg, width - x0), lg * 2 + stream});
+    for (uint32_t x0 = 0; x0 < width; x0 += kLfSeg) {
+      const uint32_t wseg = std::min(kLfSeg, width - x0);
+      const uint32_t sid = lg * 2 + stream;
+      if (chunks.empty() || chunks.back().sid != sid || chunks.back().nrows == kLfChunkRows ||
+          chunks.back().nsamp + wseg > kLfChunkSamples)
+        chunks.push_back({(uint32_t)rows.size(), 0, sid, 0});
+      chunks.back().nrows++;
+      chunks.back().nsamp += wseg;
+      rows.push_back({lg, stream, ch, y, x0, wseg, sid});
+    }
   };
   for (uint32_t lg = 0; lg < f.nlf; lg++) {
     const uint32_t bx0 = (lg % f.lfxs) * 256, by0 = (lg / f.lfxs) * 256;
     const uint32_t bw = std::min(256u, f.bxs - bx0), bh = std::min(256u, f.bys - by0);
-    srows.push_back((uint32_t)rows.size());
+    schunks.push_back((uint32_t)chunks.size());
     for (uint16_t ch = 0; ch < 3; ch++)
       for (uint32_t y = 0; y < bh; y++) add(lg, 0, ch, y, bw);
-    srows.push_back((uint32_t)rows.size());
+    schunks.push_back((uint32_t)chunks.size());
     const uint32_t cw = (bw + 7) / 8, chh = (bh + 7) / 8;
     for (uint16_t ch = 0; ch < 2; ch++)
       for (uint32_t y = 0; y < chh; y++) add(lg, 1, ch, y, cw);
     for (uint32_t y = 0; y < 2; y++) add(lg, 1, 2, y, bw * bh);
     for (uint32_t y = 0; y < bh; y++) add(lg, 1, 3, y, bw);
   }
-  srows.push_back((uint32_t)rows.size());
+  schunks.push_back((uint32_t)chunks.size());
 }
 
 static float elapsed(hipEvent_t a, hipEvent_t b) {
@@ -321,6 +336,7 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   if (st) return st;
   JXG_HIP(c->acs.ensure(nb));
   JXG_HIP(c->qf.ensure(nb));
+  JXG_HIP(c->nz.ensure(nb * 3));
   JXG_HIP(c->dc.ensure(nb * 3));
   JXG_HIP(c->ac.ensure(nb * 192));
   if (homog) JXG_HIP(c->homog.ensure(nb * 3));
@@ -333,20 +349,23 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   const uint32_t nstreams = f.nlf * 2;
   const bool new_rows = c->rows_w != w || c->rows_h != h;
   if (new_rows) {
-    build_rows(f, c->rows_h_cache, c->srows_cache);
+    build_rows(f, c->rows_h_cache, c->chunks_h_cache, c->schunks_cache);
     c->rows_w = w;
     c->rows_h = h;
   }
   const std::vector<LfRow>& rows = c->rows_h_cache;
-  const std::vector<uint32_t>& srows = c->srows_cache;
+  const std::vector<LfChunk>& lchunks = c->chunks_h_cache;
+  const std::vector<uint32_t>& schunks = c->schunks_cache;
   const uint32_t nrows = (uint32_t)rows.size();
+  const uint32_t nchunks = (uint32_t)lchunks.size();
   JXG_HIP(c->rows.ensure(nrows));
+  JXG_HIP(c->lfchunks.ensure(nchunks));
   JXG_HIP(c->lfhist.ensure(nstreams * 4 * kAlpha));
   JXG_HIP(c->lfcodes.ensure(nstreams * 4 * kAlpha));
   JXG_HIP(c->sbound.ensure(nstreams));
-  JXG_HIP(c->rowbits.ensure(nrows));
-  JXG_HIP(c->rowoff.ensure(nrows));
-  JXG_HIP(c->stream_rows.ensure(nstreams + 1));
+  JXG_HIP(c->chunkbits.ensure(nchunks));
+  JXG_HIP(c->chunkoff.ensure(nchunks));
+  JXG_HIP(c->stream_chunks.ensure(nstreams + 1));
   JXG_HIP(c->stream_base.ensure(nstreams));
   JXG_HIP(c->stream_bits.ensure(nstreams));
   JXG_HIP(c->h_hist_ac.ensure(kMaxClusters * kAlpha));
@@ -358,7 +377,10 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   JXG_HIP(c->h_sbits.ensure(nstreams));
   if (new_rows) {
     JXG_HIP(hipMemcpyAsync(c->rows.p, rows.data(), nrows * sizeof(LfRow), hipMemcpyHostToDevice, s));
-    JXG_HIP(hipMemcpyAsync(c->stream_rows.p, srows.data(), srows.size() * 4, hipMemcpyHostToDevice, s));
+    JXG_HIP(hipMemcpyAsync(c->lfchunks.p, lchunks.data(), nchunks * sizeof(LfChunk),
+                           hipMemcpyHostToDevice, s));
+    JXG_HIP(hipMemcpyAsync(c->stream_chunks.p, schunks.data(), schunks.size() * 4,
+                           hipMemcpyHostToDevice, s));
   }
 
   // ---------------- stage 1: front end ----------------
@@ -388,6 +410,7 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   fa.qf = c->qf.p;
   fa.dc = c->dc.p;
   fa.ac = c->ac.p;
+  fa.nz = c->nz.p;
   fa.homog = homog ? c->homog.p : nullptr;
   launch_front(fa, f.tiles_x, f.tiles_y, s);
   JXG_HIP(hipGetLastError());
@@ -400,6 +423,7 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   AcArgs aa{};
   aa.acs = c->acs.p;
   aa.ac = c->ac.p;
+  aa.nz = c->nz.p;
   aa.bxs = f.bxs;
   aa.bys = f.bys;
   aa.gxs = f.gxs;
@@ -412,6 +436,7 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   launch_ac_hist(aa, f.ngroups, s);
   LfArgs la{};
   la.rows = c->rows.p;
+  la.chunks = c->lfchunks.p;
   la.dc = c->dc.p;
   la.acs = c->acs.p;
   la.qf = c->qf.p;
@@ -421,12 +446,12 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   la.hist = c->lfhist.p;
   la.sbound = c->sbound.p;
   la.codes = c->lfcodes.p;
-  la.row_bits = c->rowbits.p;
-  la.row_off = c->rowoff.p;
-  la.stream_rows = c->stream_rows.p;
+  la.chunk_bits = c->chunkbits.p;
+  la.chunk_off = c->chunkoff.p;
+  la.stream_chunks = c->stream_chunks.p;
   la.stream_base = c->stream_base.p;
   la.stream_bits = c->stream_bits.p;
-  launch_lf_hist(la, nrows, s);
+  launch_lf_hist(la, nchunks, s);
   JXG_HIP(hipGetLastError());
   JXG_HIP(hipMemcpyAsync(c->h_hist_ac.p, c->hist_ac.p, kMaxClusters * kAlpha * 4, hipMemcpyDeviceToHost, s));
   JXG_HIP(hipMemcpyAsync(c->h_bound.p, c->bound.p, f.ngroups * 4, hipMemcpyDeviceToHost, s));
@@ -533,9 +558,9 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   aa.scratch = c->scratch.p;
   la.scratch = c->scratch.p;
   launch_ac_emit(aa, f.ngroups, s);
-  launch_lf_rowbits(la, nrows, s);
+  launch_lf_bits(la, nchunks, s);
   launch_lf_scan(la, nstreams, s);
-  launch_lf_emit(la, nrows, s);
+  launch_lf_emit(la, nchunks, s);
   JXG_HIP(hipGetLastError());
   JXG_HIP(hipMemcpyAsync(c->h_gbits.p, c->gbits.p, f.ngroups * 4, hipMemcpyDeviceToHost, s));
   JXG_HIP(hipMemcpyAsync(c->h_sbits.p, c->stream_bits.p, nstreams * 4, hipMemcpyDeviceToHost, s));

@@ -23,6 +23,7 @@ struct FrontArgs {
   uint8_t* qf;    // [nb] raw-1
   int32_t* dc;    // [3][nb] X,Y,B
   int16_t* ac;    // [nb][3 X,Y,B][64 zigzag]
+  uint8_t* nz;    // [3][nb] non-zero AC count per block and channel
   float* homog;   // [nb][3] or null
 };
 
@@ -40,6 +41,7 @@ struct HomogArgs {
 struct AcArgs {
   const uint8_t* acs;
   const int16_t* ac;  // [nb][3][64 zigzag]
+  const uint8_t* nz;  // [3][nb] non-zero counts (front kernel)
   uint32_t bxs, bys, gxs;
   uint32_t* hist;        // [kMaxClusters][kAlpha]      (hist pass)
   uint32_t* bound;       // [ngroups] bit upper bound   (hist pass)
@@ -62,8 +64,16 @@ struct LfRow {
   uint32_t y, x0, width;  // samples [x0, x0 + width) of row y
   uint32_t sid;           // stream index = lg*2 + stream
 };
+// A chunk: consecutive segments of ONE stream, <= kLfChunkSamples samples
+// and <= kLfChunkRows segments; one workgroup (256 threads, <= 16 samples
+// each, contiguous in stream order) per chunk.
+constexpr uint32_t kLfChunkSamples = 4096, kLfChunkRows = 64, kLfPer = 16;
+struct LfChunk {
+  uint32_t row0, nrows, sid, nsamp;
+};
 struct LfArgs {
   const LfRow* rows;
+  const LfChunk* chunks;
   const int32_t* dc;  // [3][nb]
   const uint8_t* acs;
   const uint8_t* qf;
@@ -71,9 +81,9 @@ struct LfArgs {
   uint32_t* hist;         // [nstreams][4 leaves][kAlpha]  (hist)
   uint32_t* sbound;       // [nstreams] (hist)
   const uint32_t* codes;  // [nstreams][4][kAlpha] (emit)
-  uint32_t* row_bits;     // [nrows]
-  uint64_t* row_off;      // [nrows] absolute scratch bit offset (scan -> emit)
-  const uint32_t* stream_rows;  // [nstreams+1] first row of each stream
+  uint32_t* chunk_bits;   // [nchunks]
+  uint64_t* chunk_off;    // [nchunks] absolute scratch bit offset (scan -> emit)
+  const uint32_t* stream_chunks;  // [nstreams+1] first chunk of each stream
   const uint64_t* stream_base;  // [nstreams] scratch bit offset of each stream
   uint32_t* stream_bits;        // [nstreams] exact bits (scan)
   uint32_t* scratch;
@@ -92,10 +102,10 @@ void launch_front(const FrontArgs& a, uint32_t tiles_x, uint32_t tiles_y, hipStr
 void launch_homog(const HomogArgs& a, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s);
 void launch_ac_hist(const AcArgs& a, uint32_t ngroups, hipStream_t s);
 void launch_ac_emit(const AcArgs& a, uint32_t ngroups, hipStream_t s);
-void launch_lf_hist(const LfArgs& a, uint32_t nrows, hipStream_t s);
-void launch_lf_rowbits(const LfArgs& a, uint32_t nrows, hipStream_t s);
+void launch_lf_hist(const LfArgs& a, uint32_t nchunks, hipStream_t s);
+void launch_lf_bits(const LfArgs& a, uint32_t nchunks, hipStream_t s);
 void launch_lf_scan(const LfArgs& a, uint32_t nstreams, hipStream_t s);
-void launch_lf_emit(const LfArgs& a, uint32_t nrows, hipStream_t s);
+void launch_lf_emit(const LfArgs& a, uint32_t nchunks, hipStream_t s);
 void set_cluster_table(const uint8_t* tab, hipStream_t s);
 void launch_concat(const ConcatPiece* pieces, uint32_t npieces, uint64_t max_words,
                    const uint32_t* scratch, const uint32_t* chunks, uint32_t* out,
