@@ -1,16 +1,18 @@
 // jxg_ac.hip -- pass-group AC token statistics and bit emission on gfx950.
 //
-// One 1024-thread workgroup per 256x256-pixel pass group (32x32 blocks, 3072
-// (block, channel) tasks, 3 per thread).  A task's 64 int16 coefficients
+// One 1024-thread workgroup per 256x256-pixel pass group: thread = 8x8 block,
+// its (block, channel) tasks Y, X, B in stream order.  A task's 64 int16 coefficients
 // (128 B) are loaded with 8 x 16-byte loads into 32 VGPRs and the token walk
 // runs on registers (fully unrolled, wave-uniform early exit every 8
 // coefficients), so there are no dependent global loads in the walk.
 //   ac_hist : non-zero counts -> predicted-nz + zero-density contexts ->
 //             clustered histograms (LDS, one global atomic per non-empty bin),
 //             exact per-group token counts, per-group bit upper bound.
-//   ac_emit : same walk with the prefix codes: per-task bit lengths ->
-//             workgroup exclusive scan (stream order: blocks raster, channels
-//             Y, X, B) -> every task writes its bits with atomicOr.
+//   ac_emit : same walk with the prefix codes (LDS table): per-block bit
+//             lengths -> workgroup exclusive scan (stream order: blocks
+//             raster, channels Y, X, B) -> every block writes its bits into an
+//             LDS bit buffer (ds_or), copied out with plain 4-byte stores
+//             (global atomics only for groups larger than the buffer).
 // Token order / contexts are those of oracle/encode.c group_tokens, [ext]
 // libjxl dec_group DecodeACVarBlock.
 #include "jxg_device.h"
@@ -90,23 +92,18 @@ __device__ __forceinline__ int block_ctx_of(int c, int acs) {
   return kDefaultCtxMap[(c < 2 ? c ^ 1 : 2) * 13 + kStrategyOrder[acs]];
 }
 
-// task t (stream order) -> (block x, block y, channel)
-struct Task {
-  int bx, by, c;
-  size_t gb;
-};
-__device__ __forceinline__ Task task_of(const AcArgs& a, const GroupGeom& G, int t) {
-  Task k;
-  const int b = t / 3, ci = t - b * 3;
-  k.c = ci == 0 ? 1 : (ci == 1 ? 0 : 2);
-  k.bx = b % G.gw;
-  k.by = b / G.gw;
-  k.gb = (size_t)(G.by0 + k.by) * a.bxs + G.bx0 + k.bx;
-  return k;
-}
+// AC tokens are < 64: |q| <= 32767 -> packed value <= 65534 -> hybrid token
+// <= 63; the non-zero count token is <= 63.  Device tables use 64 columns.
+constexpr int kAcTok = 64;
+// LDS bit buffer of ac_emit (groups whose exact size exceeds it fall back to
+// global atomics)
+constexpr int kEmitLdsWords = 8192;  // 32 KiB = 262144 bits
+
+__device__ __forceinline__ int channel_of(int ci) { return ci == 0 ? 1 : (ci == 1 ? 0 : 2); }
 
 // non-zero counts of the group's blocks (written by the front kernel)
-__device__ void fill_nz(const AcArgs& a, const GroupGeom& G, uint8_t (*sNz)[1024]) {
+__device__ __forceinline__ void fill_nz(const AcArgs& a, const GroupGeom& G,
+                                        uint8_t (*sNz)[1024]) {
   const size_t nb = (size_t)a.bxs * a.bys;
   for (int i = threadIdx.x; i < 3 * 1024; i += blockDim.x) {
     const int c = i >> 10, by = (i >> 5) & 31, bx = i & 31;
@@ -115,44 +112,96 @@ __device__ void fill_nz(const AcArgs& a, const GroupGeom& G, uint8_t (*sNz)[1024
   }
 }
 
+// workgroup (1024 threads) exclusive scan; *total = sum of all values
+__device__ __forceinline__ uint32_t block_excl_scan1024(uint32_t v, uint32_t* sWave,
+                                                        uint32_t* total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t incl = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t t = __shfl_up(incl, d);
+    if (lane >= d) incl += t;
+  }
+  if (lane == 63) sWave[wv] = incl;
+  __syncthreads();
+  uint32_t before = 0, all = 0;
+#pragma unroll
+  for (int i = 0; i < kAcThreads / 64; i++) {
+    const uint32_t x = sWave[i];
+    before += i < wv ? x : 0u;
+    all += x;
+  }
+  *total = all;
+  return before + incl - v;
+}
+
+// One thread per block of the group (<= 32 x 32 = 1024 blocks); its three
+// (block, channel) tasks Y, X, B are consecutive in the group's stream order.
+struct BlockTask {
+  bool valid;
+  int bx, by;
+  size_t gb;
+  int acs;
+};
+__device__ __forceinline__ BlockTask block_task(const AcArgs& a, const GroupGeom& G) {
+  BlockTask t;
+  const int b = threadIdx.x;
+  t.valid = b < G.gw * G.gh;
+  t.bx = t.valid ? b % G.gw : 0;
+  t.by = t.valid ? b / G.gw : 0;
+  t.gb = (size_t)(G.by0 + t.by) * a.bxs + G.bx0 + t.bx;
+  t.acs = t.valid ? a.acs[t.gb] : 0;
+  return t;
+}
+
+template <class F>
+__device__ __forceinline__ void block_channel_tokens(const AcArgs& a, const BlockTask& t,
+                                                     uint8_t (*sNz)[1024], int c, F&& f) {
+  uint32_t w[32];
+  load_coefs(a.ac + (t.gb * 3 + c) * 64, w);
+  block_tokens(w, sNz[c][t.by * 32 + t.bx], predict_nz(sNz[c], t.bx, t.by),
+               block_ctx_of(c, t.acs), f);
+}
+
 __global__ __launch_bounds__(kAcThreads) void ac_hist_kernel(AcArgs a) {
-  __shared__ uint32_t sHist[kMaxClusters * kAlpha];
+  __shared__ uint32_t sHist[kMaxClusters * kAcTok];
   __shared__ uint8_t sNz[3][1024];
   __shared__ uint8_t sClu[kAcCtx];
   __shared__ uint32_t sBound, sNtok[3];
   const int g = blockIdx.x;
   const GroupGeom G = group_geom(a, g);
-  for (int i = threadIdx.x; i < kMaxClusters * kAlpha; i += blockDim.x) sHist[i] = 0;
+  for (int i = threadIdx.x; i < kMaxClusters * kAcTok; i += blockDim.x) sHist[i] = 0;
   for (int i = threadIdx.x; i < kAcCtx; i += blockDim.x) sClu[i] = c_cluster[i];
   if (threadIdx.x < 3) sNtok[threadIdx.x] = 0;
   if (threadIdx.x == 0) sBound = 0;
   fill_nz(a, G, sNz);
   __syncthreads();
-  const int ntask = G.gw * G.gh * 3;
+  const BlockTask t = block_task(a, G);
   uint32_t bound = 0, nt[3] = {0, 0, 0};
-  for (int t = threadIdx.x; t < ntask; t += blockDim.x) {
-    const Task k = task_of(a, G, t);
-    uint32_t w[32];
-    load_coefs(a.ac + (k.gb * 3 + k.c) * 64, w);
-    const int nz = sNz[k.c][k.by * 32 + k.bx];
-    uint32_t cnt = 0;
-    block_tokens(w, nz, predict_nz(sNz[k.c], k.bx, k.by), block_ctx_of(k.c, a.acs[k.gb]),
-                 [&](int ctx, uint32_t v) {
-                   uint32_t tok, nb, bits;
-                   hybrid420(v, tok, nb, bits);
-                   atomicAdd(&sHist[sClu[ctx] * kAlpha + tok], 1u);
-                   bound += 15u + nb;
-                   cnt++;
-                 });
-    nt[k.c] += cnt;
+  if (t.valid) {
+#pragma unroll 1
+    for (int ci = 0; ci < 3; ci++) {
+      const int c = channel_of(ci);
+      uint32_t cnt = 0;
+      block_channel_tokens(a, t, sNz, c, [&](int ctx, uint32_t v) {
+        uint32_t tok, nb, bits;
+        hybrid420(v, tok, nb, bits);
+        atomicAdd(&sHist[sClu[ctx] * kAcTok + tok], 1u);
+        bound += 15u + nb;
+        cnt++;
+      });
+      nt[0] += c == 0 ? cnt : 0u;
+      nt[1] += c == 1 ? cnt : 0u;
+      nt[2] += c == 2 ? cnt : 0u;
+    }
   }
   atomicAdd(&sBound, bound);
   atomicAdd(&sNtok[0], nt[0]);
   atomicAdd(&sNtok[1], nt[1]);
   atomicAdd(&sNtok[2], nt[2]);
   __syncthreads();
-  for (int i = threadIdx.x; i < kMaxClusters * kAlpha; i += blockDim.x)
-    if (sHist[i]) atomicAdd(&a.hist[i], sHist[i]);
+  for (int i = threadIdx.x; i < kMaxClusters * kAcTok; i += blockDim.x)
+    if (sHist[i]) atomicAdd(&a.hist[(i / kAcTok) * kAlpha + (i % kAcTok)], sHist[i]);
   if (threadIdx.x == 0) {
     a.bound[g] = sBound;
     a.ntok[g * 3 + 0] = sNtok[0];
@@ -161,69 +210,68 @@ __global__ __launch_bounds__(kAcThreads) void ac_hist_kernel(AcArgs a) {
   }
 }
 
+template <class Sink>
+__device__ __forceinline__ void emit_block(const AcArgs& a, const BlockTask& t,
+                                           uint8_t (*sNz)[1024], const uint8_t* sClu,
+                                           const uint32_t* sCode, Sink& s) {
+#pragma unroll 1
+  for (int ci = 0; ci < 3; ci++) {
+    block_channel_tokens(a, t, sNz, channel_of(ci), [&](int ctx, uint32_t v) {
+      uint32_t tok, nb, bits;
+      hybrid420(v, tok, nb, bits);
+      const uint32_t cl = sCode[sClu[ctx] * kAcTok + tok];
+      // code (<= 15 bits) and raw bits (<= 13) in one put
+      s.put((cl >> 16) + nb, (cl & 0xFFFFu) | (bits << (cl >> 16)));
+    });
+  }
+  s.finish();
+}
+
 __global__ __launch_bounds__(kAcThreads) void ac_emit_kernel(AcArgs a) {
+  __shared__ uint32_t sCode[kMaxClusters * kAcTok];
+  __shared__ uint32_t sBits[kEmitLdsWords];
   __shared__ uint8_t sNz[3][1024];
   __shared__ uint8_t sClu[kAcCtx];
-  __shared__ uint32_t sOff[3 * 1024];
-  __shared__ uint32_t sScan[kAcThreads];
+  __shared__ uint32_t sWave[kAcThreads / 64];
   const int g = blockIdx.x;
   const GroupGeom G = group_geom(a, g);
   for (int i = threadIdx.x; i < kAcCtx; i += blockDim.x) sClu[i] = c_cluster[i];
+  for (int i = threadIdx.x; i < kMaxClusters * kAcTok; i += blockDim.x)
+    sCode[i] = a.codes[(i / kAcTok) * kAlpha + (i % kAcTok)];
+  for (int i = threadIdx.x; i < kEmitLdsWords; i += blockDim.x) sBits[i] = 0;
   fill_nz(a, G, sNz);
   __syncthreads();
-  const int ntask = G.gw * G.gh * 3;
-  // pass 1: bits per task
-  for (int t = threadIdx.x; t < ntask; t += blockDim.x) {
-    const Task k = task_of(a, G, t);
-    uint32_t w[32];
-    load_coefs(a.ac + (k.gb * 3 + k.c) * 64, w);
-    uint32_t bits_t = 0;
-    block_tokens(w, sNz[k.c][k.by * 32 + k.bx], predict_nz(sNz[k.c], k.bx, k.by),
-                 block_ctx_of(k.c, a.acs[k.gb]), [&](int ctx, uint32_t v) {
-                   uint32_t tok, nb, bits;
-                   hybrid420(v, tok, nb, bits);
-                   bits_t += (a.codes[sClu[ctx] * kAlpha + tok] >> 16) + nb;
-                 });
-    sOff[t] = bits_t;
+  const BlockTask t = block_task(a, G);
+  // pass 1: exact bits of this block's three tasks
+  uint32_t tot = 0;
+  if (t.valid) {
+#pragma unroll 1
+    for (int ci = 0; ci < 3; ci++) {
+      block_channel_tokens(a, t, sNz, channel_of(ci), [&](int ctx, uint32_t v) {
+        uint32_t tok, nb, bits;
+        hybrid420(v, tok, nb, bits);
+        tot += (sCode[sClu[ctx] * kAcTok + tok] >> 16) + nb;
+      });
+    }
   }
-  __syncthreads();
-  // exclusive scan over tasks in stream order: thread i owns [i*per, (i+1)*per)
-  const int per = (ntask + kAcThreads - 1) / kAcThreads;
-  const int t0 = threadIdx.x * per;
-  uint32_t local = 0;
-  for (int t = t0; t < t0 + per && t < ntask; t++) local += sOff[t];
-  sScan[threadIdx.x] = local;
-  __syncthreads();
-  for (int d = 1; d < kAcThreads; d <<= 1) {
-    uint32_t v = threadIdx.x >= (unsigned)d ? sScan[threadIdx.x - d] : 0;
+  uint32_t total;
+  const uint32_t off = block_excl_scan1024(tot, sWave, &total);
+  // pass 2: emission (LDS bit buffer when the group fits, else global atomics)
+  const uint64_t base = a.base[g];  // word aligned
+  if (total <= (uint32_t)kEmitLdsWords * 32u) {
+    if (t.valid) {
+      BitSink s{sBits, off, 0, 0};
+      emit_block(a, t, sNz, sClu, sCode, s);
+    }
     __syncthreads();
-    sScan[threadIdx.x] += v;
-    __syncthreads();
+    const uint32_t nw = (total + 31) / 32;
+    uint32_t* dst = a.scratch + (base >> 5);
+    for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = sBits[i];
+  } else if (t.valid) {
+    BitSink s{a.scratch, base + off, 0, 0};
+    emit_block(a, t, sNz, sClu, sCode, s);
   }
-  uint32_t run = sScan[threadIdx.x] - local;
-  for (int t = t0; t < t0 + per && t < ntask; t++) {
-    const uint32_t v = sOff[t];
-    sOff[t] = run;
-    run += v;
-  }
-  __syncthreads();
-  const uint64_t base = a.base[g];
-  for (int t = threadIdx.x; t < ntask; t += blockDim.x) {
-    const Task k = task_of(a, G, t);
-    uint32_t w[32];
-    load_coefs(a.ac + (k.gb * 3 + k.c) * 64, w);
-    BitSink s{a.scratch, base + sOff[t], 0, 0};
-    block_tokens(w, sNz[k.c][k.by * 32 + k.bx], predict_nz(sNz[k.c], k.bx, k.by),
-                 block_ctx_of(k.c, a.acs[k.gb]), [&](int ctx, uint32_t v) {
-                   uint32_t tok, nb, bits;
-                   hybrid420(v, tok, nb, bits);
-                   const uint32_t cl = a.codes[sClu[ctx] * kAlpha + tok];
-                   // code (<= 15 bits) and raw bits (<= 15) in one put
-                   s.put((cl >> 16) + nb, (cl & 0xFFFFu) | (bits << (cl >> 16)));
-                 });
-    s.finish();
-  }
-  if (threadIdx.x == kAcThreads - 1) a.bits[g] = sScan[kAcThreads - 1];
+  if (threadIdx.x == 0) a.bits[g] = total;
 }
 
 void launch_ac_hist(const AcArgs& a, uint32_t ngroups, hipStream_t s) {

@@ -26,27 +26,31 @@ namespace {
 
 // Huffman code lengths.  Leaves ordered by (count, symbol); two-queue merge
 // that prefers the leaf queue on ties; if the deepest leaf exceeds maxlen the
-// counts become (c >> 1) | 1 and the construction repeats.
+// counts become (c >> 1) | 1 and the construction repeats.  Allocation-free
+// (n <= 256): the leaf order is a sort of unique (count, symbol) keys.
 void huffman_lengths(const uint32_t* counts_in, int n, int maxlen, uint8_t* len) {
-  std::vector<uint32_t> counts(counts_in, counts_in + n);
+  uint32_t counts[256];
+  uint64_t key[256];
+  uint64_t weight[512];
+  int16_t parent[512];
+  uint8_t depth[512];
+  for (int i = 0; i < n; i++) counts[i] = counts_in[i];
   for (;;) {
-    std::vector<int> leaves;
+    int k = 0;
     for (int i = 0; i < n; i++) {
       len[i] = 0;
-      if (counts[i]) leaves.push_back(i);
+      if (counts[i]) key[k++] = ((uint64_t)counts[i] << 16) | (uint64_t)i;
     }
-    const int k = (int)leaves.size();
     if (k == 0) return;
     if (k == 1) {
-      len[leaves[0]] = 1;
+      len[key[0] & 0xFFFF] = 1;
       return;
     }
-    std::stable_sort(leaves.begin(), leaves.end(), [&](int a, int b) {
-      return counts[a] != counts[b] ? counts[a] < counts[b] : a < b;
-    });
-    std::vector<uint64_t> weight(2 * k);
-    std::vector<int> parent(2 * k, -1);
-    for (int i = 0; i < k; i++) weight[i] = counts[leaves[i]];
+    std::sort(key, key + k);
+    for (int i = 0; i < k; i++) {
+      weight[i] = key[i] >> 16;
+      parent[i] = -1;
+    }
     int next_leaf = 0, next_node = k, end = k;
     while ((k - next_leaf) + (end - next_node) > 1) {
       int pick[2];
@@ -57,19 +61,20 @@ void huffman_lengths(const uint32_t* counts_in, int n, int maxlen, uint8_t* len)
           p = next_node++;
       }
       weight[end] = weight[pick[0]] + weight[pick[1]];
-      parent[pick[0]] = parent[pick[1]] = end;
+      parent[pick[0]] = parent[pick[1]] = (int16_t)end;
+      parent[end] = -1;
       end++;
     }
-    std::vector<int> depth(end, 0);
-    for (int i = end - 2; i >= 0; i--) depth[i] = depth[parent[i]] + 1;
+    depth[end - 1] = 0;
+    for (int i = end - 2; i >= 0; i--) depth[i] = (uint8_t)(depth[parent[i]] + 1);
     int deepest = 0;
     for (int i = 0; i < k; i++) {
-      len[leaves[i]] = (uint8_t)depth[i];
-      deepest = std::max(deepest, depth[i]);
+      len[key[i] & 0xFFFF] = depth[i];
+      deepest = std::max<int>(deepest, depth[i]);
     }
     if (deepest <= maxlen) return;
-    for (auto& c : counts)
-      if (c) c = (c >> 1) | 1u;
+    for (int i = 0; i < n; i++)
+      if (counts[i]) counts[i] = (counts[i] >> 1) | 1u;
   }
 }
 

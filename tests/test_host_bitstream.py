@@ -1,0 +1,35 @@
+"""CPU tests of the product's host-side bitstream code (jxg_bitstream.cpp):
+prefix-code construction + serialisation must equal the oracle's
+(oracle/entropy.c) bit for bit.  Built with g++ from the sources (host-only
+code, no GPU needed)."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "jpeg-xl-lossy-image-compression-thesis_amd", "csrc")
+
+
+@pytest.fixture(scope="module")
+def prefix_parity_bin(tmp_path_factory):
+    if shutil.which("g++") is None or shutil.which("gcc") is None:
+        pytest.skip("no host compiler")
+    d = tmp_path_factory.mktemp("pp")
+    flags = ["-O2", "-ffp-contract=off"]
+    subprocess.check_call(["g++", "-std=c++17", *flags, "-c", os.path.join(PKG, "jxg_bitstream.cpp"),
+                           "-o", str(d / "bs.o")])
+    subprocess.check_call(["gcc", "-std=c11", *flags, "-I", os.path.join(ROOT, "oracle"), "-c",
+                           os.path.join(ROOT, "oracle", "entropy.c"), "-o", str(d / "ent.o")])
+    exe = d / "pp"
+    subprocess.check_call(["g++", "-std=c++17", *flags,
+                           os.path.join(ROOT, "tests", "native", "prefix_parity.cpp"),
+                           str(d / "bs.o"), str(d / "ent.o"), "-o", str(exe)])
+    return str(exe)
+
+
+def test_prefix_codes_match_oracle(prefix_parity_bin):
+    r = subprocess.run([prefix_parity_bin, "4000"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert "0 mismatches" in r.stdout
