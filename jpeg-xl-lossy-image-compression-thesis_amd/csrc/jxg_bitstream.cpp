@@ -198,6 +198,8 @@ void write_uint_config(BitWriter& w, const UintCfg& c) {  // log_alpha_size 15
     w.put(ceil_log2(c.split_exp - c.msb + 1), c.lsb);
   }
 }
+}  // namespace
+
 void write_context_map(BitWriter& w, const std::vector<uint8_t>& map, int nhist) {
   const int n = (int)map.size();
   if (nhist == 1) {
@@ -220,12 +222,17 @@ void write_context_map(BitWriter& w, const std::vector<uint8_t>& map, int nhist)
   write_histograms(w, std::vector<uint8_t>{0}, 1, code, kCfgMap);
   for (uint8_t v : map) write_token(w, code[0], kCfgMap, v);
 }
-}  // namespace
 
 void write_histograms(BitWriter& w, const std::vector<uint8_t>& ctxmap, int nhist,
-                      const std::vector<PrefixCode>& codes, const UintCfg& cfg) {
+                      const std::vector<PrefixCode>& codes, const UintCfg& cfg,
+                      const BitWriter* ctxmap_bits) {
   w.put(1, 0);  // lz77.enabled
-  if (ctxmap.size() > 1) write_context_map(w, ctxmap, nhist);
+  if (ctxmap.size() > 1) {
+    if (ctxmap_bits)
+      w.append(*ctxmap_bits);
+    else
+      write_context_map(w, ctxmap, nhist);
+  }
   w.put(1, 1);  // use_prefix_code
   for (int h = 0; h < nhist; h++) write_uint_config(w, cfg);
   for (int h = 0; h < nhist; h++) write_varlen16(w, codes[h].alphabet - 1);

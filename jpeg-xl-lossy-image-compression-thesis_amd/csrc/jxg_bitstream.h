@@ -16,17 +16,13 @@ class BitWriter {
  public:
   void put(uint32_t nbits, uint64_t v) {
     if (nbits == 0) return;
-    v &= (nbits >= 64) ? ~0ull : ((1ull << nbits) - 1);
-    while (nbits) {
-      const size_t word = bits_ >> 6;
-      const uint32_t off = (uint32_t)(bits_ & 63);
-      if (word >= words_.size()) words_.push_back(0);
-      const uint32_t take = nbits < 64 - off ? nbits : 64 - off;
-      words_[word] |= (v & (take == 64 ? ~0ull : ((1ull << take) - 1))) << off;
-      v = take == 64 ? 0 : v >> take;
-      nbits -= take;
-      bits_ += take;
-    }
+    if (nbits < 64) v &= (1ull << nbits) - 1;
+    const size_t word = bits_ >> 6;
+    const uint32_t off = (uint32_t)(bits_ & 63);
+    if (word + 2 > words_.size()) words_.resize(word + 2 + words_.size() / 2, 0);
+    words_[word] |= v << off;
+    if (off && off + nbits > 64) words_[word + 1] |= v >> (64 - off);
+    bits_ += nbits;
   }
   void pad_to_byte() { bits_ = (bits_ + 7) & ~(size_t)7; }
   size_t bits() const { return bits_; }
@@ -79,7 +75,11 @@ void write_prefix_code(BitWriter& w, const PrefixCode& p);
 void write_token(BitWriter& w, const PrefixCode& p, const UintCfg& c, uint32_t v);
 // DecodeHistograms: lz77 off, context map (ctxmap[nctx] dense ids), prefix codes
 void write_histograms(BitWriter& w, const std::vector<uint8_t>& ctxmap, int nhist,
-                      const std::vector<PrefixCode>& codes, const UintCfg& cfg);
+                      const std::vector<PrefixCode>& codes, const UintCfg& cfg,
+                      const BitWriter* ctxmap_bits = nullptr);
+// entropy-coded context map (the part of write_histograms that depends only
+// on the map; callers may cache it)
+void write_context_map(BitWriter& w, const std::vector<uint8_t>& map, int nhist);
 
 // Modular MA trees used by the LF-group streams (local trees, no transforms)
 struct TreeNode {

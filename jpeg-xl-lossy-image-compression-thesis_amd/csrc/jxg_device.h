@@ -176,6 +176,29 @@ __device__ __forceinline__ int nz_bucket(int n) {
   return n < 8 ? n : 4 + n / 2;
 }
 
+// Lane exchange inside 8-lane groups with DPP (no LDS traffic, no address
+// VGPRs): xor 1 / 2 are quad permutes; xor 4 = quad_perm(3,2,1,0) followed by
+// row_half_mirror (i -> 7 - i), since (i ^ 3) ^ 7 = i ^ 4.  Every source lane
+// is in the caller's (fully active) group.
+template <int D>
+__device__ __forceinline__ uint32_t xor_lane_u(uint32_t v) {
+  static_assert(D == 1 || D == 2 || D == 4, "xor distance");
+  if (D == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+  if (D == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+  const int t = __builtin_amdgcn_mov_dpp((int)v, 0x1B, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp(t, 0x141, 0xF, 0xF, false);
+}
+template <int D>
+__device__ __forceinline__ float xor_lane(float v) {
+  return __uint_as_float(xor_lane_u<D>(__float_as_uint(v)));
+}
+// value of lane K of this lane's 8-lane group (ds_swizzle bitmask mode:
+// and 0x18, or K, within 32-lane halves)
+template <int K>
+__device__ __forceinline__ float group_lane(float v) {
+  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x18 | (K << 5)));
+}
+
 // bit sink writing into a zero-initialised word buffer with atomicOr
 struct BitSink {
   uint32_t* buf;

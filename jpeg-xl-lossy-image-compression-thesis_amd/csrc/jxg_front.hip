@@ -245,21 +245,24 @@ __device__ __forceinline__ void dct4_1d(float* v) {
 // by three XOR butterflies; pure data movement.  The lane-dependent choice is
 // made with bit masks: a select between two array elements would be folded
 // into a dynamically indexed (scratch) array access.
-__device__ __forceinline__ void transpose8(float* v, int r) {
+template <int D>
+__device__ __forceinline__ void transpose_stage(float* v, int r) {
+  const uint32_t m = (r & D) ? 0xFFFFFFFFu : 0u;
 #pragma unroll
-  for (int d = 4; d >= 1; d >>= 1) {
-    const uint32_t m = (r & d) ? 0xFFFFFFFFu : 0u;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      if (i & d) continue;
-      const int j = i | d;
-      const uint32_t a = __float_as_uint(v[i]), b = __float_as_uint(v[j]);
-      const uint32_t send = (a & m) | (b & ~m);
-      const uint32_t recv = (uint32_t)__shfl_xor((int)send, d);
-      v[i] = __uint_as_float((recv & m) | (a & ~m));
-      v[j] = __uint_as_float((b & m) | (recv & ~m));
-    }
+  for (int i = 0; i < 8; i++) {
+    if (i & D) continue;
+    const int j = i | D;
+    const uint32_t a = __float_as_uint(v[i]), b = __float_as_uint(v[j]);
+    const uint32_t send = (a & m) | (b & ~m);
+    const uint32_t recv = xor_lane_u<D>(send);
+    v[i] = __uint_as_float((recv & m) | (a & ~m));
+    v[j] = __uint_as_float((b & m) | (recv & ~m));
   }
+}
+__device__ __forceinline__ void transpose8(float* v, int r) {
+  transpose_stage<4>(v, r);
+  transpose_stage<2>(v, r);
+  transpose_stage<1>(v, r);
 }
 
 template <int T>
@@ -278,15 +281,15 @@ __device__ __forceinline__ void wave_lds_sync() {
 // ((0+1)+(2+3))+((4+5)+(6+7)) in every lane (float + is commutative), the
 // order of oracle/front.c tree8
 __device__ __forceinline__ float group_tree_sum(float v) {
-  v += __shfl_xor(v, 1);
-  v += __shfl_xor(v, 2);
-  v += __shfl_xor(v, 4);
+  v += xor_lane<1>(v);
+  v += xor_lane<2>(v);
+  v += xor_lane<4>(v);
   return v;
 }
 __device__ __forceinline__ int group_int_sum(int v) {
-  v += __shfl_xor(v, 1);
-  v += __shfl_xor(v, 2);
-  v += __shfl_xor(v, 4);
+  v += (int)xor_lane_u<1>((uint32_t)v);
+  v += (int)xor_lane_u<2>((uint32_t)v);
+  v += (int)xor_lane_u<4>((uint32_t)v);
   return v;
 }
 
@@ -307,108 +310,128 @@ struct QVals {
   uint32_t nz;  // non-zero AC counts of the block: X | Y << 8 | B << 16
 };
 
+// One channel C (0 X, 1 Y, 2 B) of one block under strategy T, lane r =
+// working-array column r: transform, quantize 8 coefficients, accumulate
+// e*e (fmaf), rate bits and the non-zero count; Y records its dequantized
+// values (yd) for the B residual.  Float op order == oracle jxo_quantize_block.
+template <int T, int C>
+__device__ __forceinline__ void quantize_channel(const GroupCtx& G, float scale, float inv_scale,
+                                                 float* yd, int& bits, float& part,
+                                                 uint32_t* pk, int& nzc) {
+  constexpr int ti = tindex<T>();
+  constexpr float kBias1 = 1.0f - 0.07005449891748593f;
+  const float* plane = G.pix + C * kPlane;
+  const int base = lds_at(G.lx0, G.ly0 + G.r);  // 8 contiguous dwords (same skew)
+  float v[8];
+#pragma unroll
+  for (int x = 0; x < 8; x++) v[x] = plane[base + x];
+  // row pass
+  if (T == kDCT8 || T == kDCT8X4) {
+    dct8_1d(v);
+  } else {
+    dct4_1d(v);
+    dct4_1d(v + 4);
+  }
+  transpose8(v, G.r);
+  // column pass
+  if (T == kDCT8 || T == kDCT4X8) {
+    dct8_1d(v);
+  } else {
+    dct4_1d(v);
+    dct4_1d(v + 4);
+  }
+  // lowest-frequency combine (enc_transforms [ext]); slots per oracle
+  if (T == kDCT4X4) {
+    const float A = group_lane<0>(v[0]), Cc = group_lane<0>(v[4]);
+    const float B = group_lane<4>(v[0]), D = group_lane<4>(v[4]);
+    if (G.r == 0) {
+      v[0] = (((A + B) + Cc) + D) * 0.25f;
+      v[4] = (((A - B) + Cc) - D) * 0.25f;
+    } else if (G.r == 4) {
+      v[0] = (((A + B) - Cc) - D) * 0.25f;
+      v[4] = (((A - B) - Cc) + D) * 0.25f;
+    }
+  } else if (T == kDCT8X4) {
+    if (G.r == 0) {
+      const float A = v[0], B = v[4];
+      v[0] = (A + B) * 0.5f;
+      v[4] = (A - B) * 0.5f;
+    }
+  } else if (T == kDCT4X8) {
+    const float A = group_lane<0>(v[0]), B = group_lane<4>(v[0]);
+    if (G.r == 0) v[0] = (A + B) * 0.5f;
+    if (G.r == 4) v[0] = (A - B) * 0.5f;
+  }
+  if (G.r == 0) v[0] = 0.0f;  // DC slot: quantizes to 0, contributes nothing
+  const float4* wp = reinterpret_cast<const float4*>(G.wperm + ((ti * 3 + C) * 8 + G.r) * 8);
+  const float4 w0 = wp[0], w1 = wp[1];
+  const float wk[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+  float iwk[8];
+  if (C == 1) {
+    const float4* ip = reinterpret_cast<const float4*>(G.iwperm + (ti * 8 + G.r) * 8);
+    const float4 i0 = ip[0], i1 = ip[1];
+    iwk[0] = i0.x; iwk[1] = i0.y; iwk[2] = i0.z; iwk[3] = i0.w;
+    iwk[4] = i1.x; iwk[5] = i1.y; iwk[6] = i1.z; iwk[7] = i1.w;
+  }
+  int nz = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) pk[i] = 0u;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const float ws = wk[k] * scale;
+    float rv = v[k];
+    if (C == 2) rv = rv - yd[k];
+    const float vq = rv * ws;
+    const float a = fabsf(vq);
+    const int qa = a < 0.58f ? 0 : (int)(fminf(a, 32767.0f) + 0.5f);
+    if (C == 1) {
+      float bq = G.btab[qa < 255 ? qa : 255];
+      if (__any(qa >= 256)) {
+        if (qa >= 256) bq = 0.145f / (float)qa;
+      }
+      float adj = qa == 0 ? 0.0f : (qa == 1 ? kBias1 : (float)qa - bq);
+      if (vq < 0.0f) adj = -adj;
+      yd[k] = adj * (iwk[k] * inv_scale);
+    }
+    const float e = a - (float)qa;
+    part = fmaf(e, e, part);
+    bits += qa ? 2 + 2 * bitlen((uint32_t)qa) : 0;
+    nz += qa != 0;
+    const int qs = vq < 0.0f ? -qa : qa;
+    pk[k >> 1] |= ((uint32_t)qs & 0xFFFFu) << ((k & 1) * 16);
+  }
+  nzc = group_int_sum(nz);
+  bits += G.r == 0 ? bitlen((uint32_t)nzc) : 0;
+}
+
 // One 8-lane group quantizes one block under strategy T (channels Y, X, B)
 // and returns the rate/distortion cost (same in all 8 lanes); the quantized
-// values stay in registers (q).  Float op order == oracle jxo_quantize_block.
+// values stay in registers (q).
 template <int T>
 __device__ __forceinline__ float quantize_group(const GroupCtx& G, float scale, float inv_scale,
                                                 QVals& q) {
-  constexpr int ti = tindex<T>();
-  constexpr float kBias1 = 1.0f - 0.07005449891748593f;
   float yd[8];
   int bits = 0;
   float part = 0.0f;
 #pragma unroll 1  // one channel live at a time (keeps 4 waves/SIMD)
   for (int ci = 0; ci < 3; ci++) {
-    const int c = ci == 0 ? 1 : (ci == 1 ? 0 : 2);
-    const float* plane = G.pix + c * kPlane;
-    const int base = lds_at(G.lx0, G.ly0 + G.r);  // 8 contiguous dwords (same skew)
-    float v[8];
+    uint32_t pk[4];
+    int nzc;
+    if (ci == 0) {
+      quantize_channel<T, 1>(G, scale, inv_scale, yd, bits, part, pk, nzc);
+      q.nz = (uint32_t)nzc << 8;
 #pragma unroll
-    for (int x = 0; x < 8; x++) v[x] = plane[base + x];
-    // row pass
-    if (T == kDCT8 || T == kDCT8X4) {
-      dct8_1d(v);
+      for (int i = 0; i < 4; i++) q.w[4 + i] = pk[i];
+    } else if (ci == 1) {
+      quantize_channel<T, 0>(G, scale, inv_scale, yd, bits, part, pk, nzc);
+      q.nz |= (uint32_t)nzc;
+#pragma unroll
+      for (int i = 0; i < 4; i++) q.w[i] = pk[i];
     } else {
-      dct4_1d(v);
-      dct4_1d(v + 4);
-    }
-    transpose8(v, G.r);
-    // column pass
-    if (T == kDCT8 || T == kDCT4X8) {
-      dct8_1d(v);
-    } else {
-      dct4_1d(v);
-      dct4_1d(v + 4);
-    }
-    // lowest-frequency combine (enc_transforms [ext]); slots per oracle
-    const int g0 = (threadIdx.x & 63) & ~7;
-    if (T == kDCT4X4) {
-      const float A = __shfl(v[0], g0), C = __shfl(v[4], g0);
-      const float B = __shfl(v[0], g0 + 4), D = __shfl(v[4], g0 + 4);
-      if (G.r == 0) {
-        v[0] = (((A + B) + C) + D) * 0.25f;
-        v[4] = (((A - B) + C) - D) * 0.25f;
-      } else if (G.r == 4) {
-        v[0] = (((A + B) - C) - D) * 0.25f;
-        v[4] = (((A - B) - C) + D) * 0.25f;
-      }
-    } else if (T == kDCT8X4) {
-      if (G.r == 0) {
-        const float A = v[0], B = v[4];
-        v[0] = (A + B) * 0.5f;
-        v[4] = (A - B) * 0.5f;
-      }
-    } else if (T == kDCT4X8) {
-      const float A = __shfl(v[0], g0), B = __shfl(v[0], g0 + 4);
-      if (G.r == 0) v[0] = (A + B) * 0.5f;
-      if (G.r == 4) v[0] = (A - B) * 0.5f;
-    }
-    if (G.r == 0) v[0] = 0.0f;  // DC slot: quantizes to 0, contributes nothing
-    const float4* wp = reinterpret_cast<const float4*>(G.wperm + ((ti * 3 + c) * 8 + G.r) * 8);
-    const float4 w0 = wp[0], w1 = wp[1];
-    const float wk[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-    float iwk[8];
-    if (c == 1) {
-      const float4* ip = reinterpret_cast<const float4*>(G.iwperm + (ti * 8 + G.r) * 8);
-      const float4 i0 = ip[0], i1 = ip[1];
-      iwk[0] = i0.x; iwk[1] = i0.y; iwk[2] = i0.z; iwk[3] = i0.w;
-      iwk[4] = i1.x; iwk[5] = i1.y; iwk[6] = i1.z; iwk[7] = i1.w;
-    }
-    int nz = 0;
-    uint32_t pk[4] = {0u, 0u, 0u, 0u};
+      quantize_channel<T, 2>(G, scale, inv_scale, yd, bits, part, pk, nzc);
+      q.nz |= (uint32_t)nzc << 16;
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const float ws = wk[k] * scale;
-      float rv = v[k];
-      if (c == 2) rv = rv - yd[k];
-      const float vq = rv * ws;
-      const float a = fabsf(vq);
-      const int qa = a < 0.58f ? 0 : (int)(fminf(a, 32767.0f) + 0.5f);
-      if (c == 1) {
-        float bq = G.btab[qa < 255 ? qa : 255];
-        if (__any(qa >= 256)) {
-          if (qa >= 256) bq = 0.145f / (float)qa;
-        }
-        float adj = qa == 0 ? 0.0f : (qa == 1 ? kBias1 : (float)qa - bq);
-        if (vq < 0.0f) adj = -adj;
-        yd[k] = adj * (iwk[k] * inv_scale);
-      }
-      const float e = a - (float)qa;
-      part = fmaf(e, e, part);
-      bits += qa ? 2 + 2 * bitlen((uint32_t)qa) : 0;
-      nz += qa != 0;
-      const int qs = vq < 0.0f ? -qa : qa;
-      pk[k >> 1] |= ((uint32_t)qs & 0xFFFFu) << ((k & 1) * 16);
-    }
-    const int nzc = group_int_sum(nz);
-    bits += G.r == 0 ? bitlen((uint32_t)nzc) : 0;
-    q.nz = ci == 0 ? (uint32_t)nzc << 8 : (q.nz | ((uint32_t)nzc << (c == 0 ? 0 : 16)));
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      q.w[i] = c == 0 ? pk[i] : q.w[i];
-      q.w[4 + i] = c == 1 ? pk[i] : q.w[4 + i];
-      q.w[8 + i] = c == 2 ? pk[i] : q.w[8 + i];
+      for (int i = 0; i < 4; i++) q.w[8 + i] = pk[i];
     }
   }
   bits = group_int_sum(bits);
@@ -423,23 +446,42 @@ __device__ __forceinline__ void copy_q(QVals& d, const QVals& s, bool take) {
   d.nz = take ? s.nz : d.nz;
 }
 
+// RGB8 -> XYB for the 66 x 66 tile (+1 px halo).  All byte loads of a
+// thread are issued before any use (one memory latency per tile instead of
+// one per pixel), then converted.
+constexpr int kTilePx = kRows * 66;
+constexpr int kLoadIters = (kTilePx + kThreads - 1) / kThreads;
 __device__ __forceinline__ void load_xyb_tile(const FrontArgs& a, const float* lut, float* sPix,
                                               int ox, int oy) {
-  const float cb = cbrt_det(kOpsinBias);
-  for (int i = threadIdx.x; i < kRows * 66; i += kThreads) {
+  uint32_t rgb[kLoadIters];  // r | g << 8 | b << 16; bit 24 = outside the padded frame
+#pragma unroll
+  for (int k = 0; k < kLoadIters; k++) {
+    // branch-free: every lane loads from a clamped (valid) address so the
+    // compiler can keep all loads in flight; validity is tracked in bit 24
+    const int i = min(threadIdx.x + k * kThreads, kTilePx - 1);
     const int ly = i / 66, lx = i - ly * 66;
     const int gx = ox + lx, gy = oy + ly;
-    float X = 0.0f, Y = 0.0f, B = 0.0f;
-    if (gx >= 0 && gy >= 0 && gx < (int)a.xp && gy < (int)a.yp) {
-      const int sx = gx < (int)a.w ? gx : (int)a.w - 1;
-      const int sy = gy < (int)a.h ? gy : (int)a.h - 1;
-      const uint8_t* p = a.rgb + (size_t)sy * a.stride + 3 * (size_t)sx;
-      pixel_xyb(lut, cb, p[0], p[1], p[2], X, Y, B);
+    const bool inside = gx >= 0 && gy >= 0 && gx < (int)a.xp && gy < (int)a.yp;
+    const int sx = min(max(gx, 0), (int)a.w - 1);
+    const int sy = min(max(gy, 0), (int)a.h - 1);
+    const uint8_t* p = a.rgb + (size_t)sy * a.stride + 3 * (size_t)sx;
+    rgb[k] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) |
+             (inside ? 0u : (1u << 24));
+  }
+  const float cb = cbrt_det(kOpsinBias);
+#pragma unroll
+  for (int k = 0; k < kLoadIters; k++) {
+    const int i = threadIdx.x + k * kThreads;
+    if (i < kTilePx) {
+      const int ly = i / 66, lx = i - ly * 66;
+      float X = 0.0f, Y = 0.0f, B = 0.0f;
+      const uint32_t v = rgb[k];
+      if (!(v >> 24)) pixel_xyb(lut, cb, v & 0xFF, (v >> 8) & 0xFF, (v >> 16) & 0xFF, X, Y, B);
+      const int o = lds_at(lx, ly);
+      sPix[o] = X;
+      sPix[kPlane + o] = Y;
+      sPix[2 * kPlane + o] = B;
     }
-    const int o = lds_at(lx, ly);
-    sPix[o] = X;
-    sPix[kPlane + o] = Y;
-    sPix[2 * kPlane + o] = B;
   }
 }
 

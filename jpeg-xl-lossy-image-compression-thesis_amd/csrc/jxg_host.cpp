@@ -259,6 +259,10 @@ struct Ctx {
   std::vector<LfRow> rows_h_cache;
   std::vector<LfChunk> chunks_h_cache;
   std::vector<uint32_t> schunks_cache;
+  // serialised AC context map of the previous frame (reused when equal)
+  std::vector<uint8_t> cm_last;
+  int cm_nhist = -1;
+  BitWriter cm_bits;
   std::vector<uint8_t> m_acs, m_qf;
   std::vector<int32_t> m_dc, m_ac;
   std::vector<int16_t> m_ac16;
@@ -532,7 +536,13 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   hfglobal.put(1, 1);  // DequantMatrices all_default
   hfglobal.put(ceil_log2(f.ngroups), 0);  // num_hf_presets - 1
   write_u32_sel(hfglobal, 2, 0, 0);        // used_orders = 0
-  write_histograms(hfglobal, ctxmap, nhist, codes, kCfg420);
+  if (nhist != c->cm_nhist || ctxmap != c->cm_last) {
+    c->cm_bits = BitWriter();
+    write_context_map(c->cm_bits, ctxmap, nhist);
+    c->cm_last = ctxmap;
+    c->cm_nhist = nhist;
+  }
+  write_histograms(hfglobal, ctxmap, nhist, codes, kCfg420, &c->cm_bits);
 
   // scratch layout: AC groups then LF streams (32-bit aligned regions)
   std::vector<uint64_t> gbase(f.ngroups), sbase(nstreams);
