@@ -17,7 +17,7 @@
 #include "jxo_internal.h"
 
 int jxo_front_block(const jxo_frame* f, const float px[3][64], const float* homog,
-                    int32_t q[3][64], int32_t dcq[3], int* qf_raw);
+                    int32_t q[3][64], int32_t dcq[3], int* qf_raw, float* ent_out);
 
 static const jxo_uintcfg kCfg = {4, 2, 0};
 static const jxo_uintcfg kCfgMap = {8, 0, 0};
@@ -230,8 +230,12 @@ static void lf_group_section(const jxo_frame* f, const jxo_result* r, int lg,
   }
   put_modular(w, kDcTree, 5, 3, ch, 3);
   for (int i = 0; i < 3; i++) free(ch[i].data);
-  /* AC metadata: count, then [ytox, ytob, acs+qf, epf] */
-  const uint32_t count = bw * bh; /* all varblocks are 8x8-class */
+  /* AC metadata: count, then [ytox, ytob, acs+qf, epf]; one entry per
+   * varblock, in raster order of the varblocks' top-left blocks */
+  uint32_t count = 0;
+  for (uint32_t y = 0; y < bh; y++)
+    for (uint32_t x = 0; x < bw; x++)
+      count += !(r->acs[(size_t)(by0 + y) * f->bxs + bx0 + x] & 0x80);
   jxo_bw_put(w, ceil_log2(bw * bh), count - 1);
   const int cw = (int)((bw + 7) / 8), chh = (int)((bh + 7) / 8);
   for (int i = 0; i < 2; i++) {
@@ -244,10 +248,12 @@ static void lf_group_section(const jxo_frame* f, const jxo_result* r, int lg,
   ch[2].data = (int32_t*)malloc(sizeof(int32_t) * count * 2);
   uint32_t k = 0;
   for (uint32_t y = 0; y < bh; y++)
-    for (uint32_t x = 0; x < bw; x++, k++) {
+    for (uint32_t x = 0; x < bw; x++) {
       size_t b = (size_t)(by0 + y) * f->bxs + bx0 + x;
+      if (r->acs[b] & 0x80) continue;
       ch[2].data[k] = r->acs[b];
       ch[2].data[count + k] = r->qf[b];
+      k++;
     }
   ch[3].w = (int)bw;
   ch[3].h = (int)bh;
@@ -267,15 +273,14 @@ static int nz_bucket(int n) {
   return n < 8 ? n : 4 + n / 2;
 }
 
-/* tokens of one pass group in bitstream order: blocks raster, channels Y,X,B */
+/* tokens of one pass group in bitstream order: varblocks in raster order of
+ * their top-left blocks, channels Y, X, B [ext dec_group DecodeACVarBlock].
+ * A varblock covering cb = 2^lcb blocks codes cb*64 - cb coefficients
+ * (natural order after the LLF); its non-zero count is predicted at its
+ * top-left block and (nz + cb - 1) >> lcb is stored for every covered block;
+ * the zero-density context scales nz_left and k down by cb. */
 static size_t group_tokens(const jxo_frame* f, const jxo_result* r, int g,
                            actok* out, uint32_t* ntok_c) {
-  static uint8_t order[64];
-  static int init = 0;
-  if (!init) {
-    jxo_natural_order8(order);
-    init = 1;
-  }
   const uint32_t gx = g % f->gxs, gy = g / f->gxs;
   const uint32_t bx0 = gx * 32, by0 = gy * 32;
   const uint32_t gw = (f->bxs - bx0) < 32 ? f->bxs - bx0 : 32;
@@ -285,13 +290,22 @@ static size_t group_tokens(const jxo_frame* f, const jxo_result* r, int g,
   for (uint32_t by = 0; by < gh; by++)
     for (uint32_t bx = 0; bx < gw; bx++) {
       const size_t b = (size_t)(by0 + by) * f->bxs + bx0 + bx;
-      const int ord = jxo_strategy_order[r->acs[b]];
+      const int type = r->acs[b];
+      if (type & 0x80) continue;
+      const int si = jxo_shape_of(type);
+      const int cyb = si < 0 ? 1 : jxo_shapes[si].cy, cxb = si < 0 ? 1 : jxo_shapes[si].cx;
+      const int cb = cyb * cxb;
+      int lcb = 0;
+      while ((1 << lcb) < cb) lcb++;
+      const int size = cb * 64;
+      const int ord = jxo_strategy_order[type];
       static const int corder[3] = {1, 0, 2};
       for (int ci = 0; ci < 3; ci++) {
         const int c = corder[ci];
-        const int32_t* q = r->ac + (b * 3 + c) * 64;
+#define QAT(k) r->ac[(((size_t)(by0 + by + ((k) >> 6) / cxb) * f->bxs + bx0 + bx + \
+                       ((k) >> 6) % cxb) * 3 + c) * 64 + ((k) & 63)]
         int nz = 0;
-        for (int k = 1; k < 64; k++) nz += q[order[k]] != 0;
+        for (int k = cb; k < size; k++) nz += QAT(k) != 0;
         int pred;
         if (bx == 0)
           pred = by == 0 ? 32 : nzs[c][(by - 1) * 32 + bx];
@@ -299,21 +313,25 @@ static size_t group_tokens(const jxo_frame* f, const jxo_result* r, int g,
           pred = nzs[c][by * 32 + bx - 1];
         else
           pred = (nzs[c][(by - 1) * 32 + bx] + nzs[c][by * 32 + bx - 1] + 1) / 2;
-        nzs[c][by * 32 + bx] = nz;
+        for (int iy = 0; iy < cyb; iy++)
+          for (int ix = 0; ix < cxb; ix++)
+            nzs[c][(by + iy) * 32 + bx + ix] = (nz + cb - 1) >> lcb;
         const int bctx = jxo_default_ctx_map[(c < 2 ? c ^ 1 : 2) * JXO_NUM_ORDERS + ord];
         size_t n0 = n;
         out[n].ctx = (uint16_t)(nz_bucket(pred) * JXO_BLOCK_CTX + bctx);
         out[n++].v = (uint32_t)nz;
         const int zoff = JXO_BLOCK_CTX * JXO_NZ_BUCKETS + JXO_ZD_CTX * bctx;
-        int prev = nz > 4 ? 0 : 1;
+        int prev = nz > size / 16 ? 0 : 1;
         int left = nz;
-        for (int k = 1; k < 64 && left > 0; k++) {
-          const int32_t v = q[order[k]];
-          out[n].ctx = (uint16_t)(zoff + (jxo_nnz_ctx[left] + jxo_freq_ctx[k]) * 2 + prev);
+        for (int k = cb; k < size && left > 0; k++) {
+          const int32_t v = QAT(k);
+          out[n].ctx = (uint16_t)(zoff + (jxo_nnz_ctx[(left + cb - 1) >> lcb] +
+                                          jxo_freq_ctx[k >> lcb]) * 2 + prev);
           out[n++].v = pack_signed(v);
           prev = v != 0;
           left -= prev;
         }
+#undef QAT
         if (ntok_c) ntok_c[c] += (uint32_t)(n - n0);
       }
     }
@@ -401,6 +419,10 @@ int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h, size_t row_strid
     jxo_xyb img = {{xyb, xyb + plane, xyb + 2 * plane}, f.xp, f.yp, f.xp};
     jxo_homog_map(&img, p->distance, JXO_H1_FLOAT_ABS, out->homog, NULL);
   }
+  uint8_t order[64];
+  jxo_natural_order8(order);
+  float* ent = (float*)malloc(sizeof(float) * nb);
+  int* raws = (int*)malloc(sizeof(int) * nb);
   for (uint32_t by = 0; by < f.bys; by++)
     for (uint32_t bx = 0; bx < f.bxs; bx++) {
       float px[3][64];
@@ -412,14 +434,57 @@ int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h, size_t row_strid
       int32_t q[3][64], dcq[3];
       int raw;
       int t = jxo_front_block(&f, px, out->homog ? out->homog + 3 * b : NULL, q,
-                              dcq, &raw);
+                              dcq, &raw, &ent[b]);
       out->acs[b] = (uint8_t)t;
       out->qf[b] = (uint8_t)(raw - 1);
+      raws[b] = raw;
       for (int c = 0; c < 3; c++) {
         out->dc[c * nb + b] = dcq[c];
-        memcpy(out->ac + (b * 3 + c) * 64, q[c], sizeof(int32_t) * 64);
+        /* coefficients are kept in natural (zigzag) order */
+        for (int k = 0; k < 64; k++) out->ac[(b * 3 + c) * 64 + k] = q[c][order[k]];
       }
     }
+  /* ---- merge stage: 16x8 ... 64x64 varblocks (effort >= 5) ---- */
+  if (p->effort >= 5) {
+    const int max_s = p->effort >= 6 ? 8 : 4;
+    const uint32_t tx_n = (f.bxs + 7) / 8, ty_n = (f.bys + 7) / 8;
+    for (uint32_t ty = 0; ty < ty_n; ty++)
+      for (uint32_t tx = 0; tx < tx_n; tx++)
+        jxo_merge_tile(&f, xyb, out->homog, (int)tx, (int)ty, max_s, ent, raws, out->acs);
+    static int32_t vq[3 * 4096];
+    float llf[3 * 64];
+    for (uint32_t by = 0; by < f.bys; by++)
+      for (uint32_t bx = 0; bx < f.bxs; bx++) {
+        const size_t b = (size_t)by * f.bxs + bx;
+        const int si = jxo_shape_of(out->acs[b]);
+        if (si < 0) continue; /* 8x8 class or covered */
+        const jxo_shape* sh = &jxo_shapes[si];
+        int rmax = 0;
+        for (int iy = 0; iy < sh->cy; iy++)
+          for (int ix = 0; ix < sh->cx; ix++) {
+            const int v = raws[(by + iy) * f.bxs + bx + ix];
+            rmax = v > rmax ? v : rmax;
+          }
+        jxo_varblock(&f, sh, xyb, (int)bx * 8, (int)by * 8, rmax, vq, llf, NULL);
+        const int RC = 64 * sh->cy * sh->cx;
+        for (int iy = 0; iy < sh->cy; iy++)
+          for (int ix = 0; ix < sh->cx; ix++) {
+            const size_t bi = (size_t)(by + iy) * f.bxs + bx + ix;
+            const int slice = iy * sh->cx + ix;
+            float dcv[3];
+            int32_t dcq[3];
+            for (int c = 0; c < 3; c++) {
+              memcpy(out->ac + (bi * 3 + c) * 64, vq + c * RC + slice * 64, sizeof(int32_t) * 64);
+              dcv[c] = jxo_llf_dc(sh, llf + c * 64, iy, ix);
+            }
+            jxo_quant_dc(&f, dcv, dcq);
+            for (int c = 0; c < 3; c++) out->dc[c * nb + bi] = dcq[c];
+            out->qf[bi] = (uint8_t)(rmax - 1);
+          }
+      }
+  }
+  free(ent);
+  free(raws);
   free(xyb);
 
   /* ---- AC tokens and clustered histograms ---- */

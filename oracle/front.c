@@ -337,10 +337,23 @@ float jxo_quantize_block(const jxo_frame* f, int t, const float px[3][64],
   return ((float)bits + 8.0f * dist) * tmul[t];
 }
 
+/* DC quantization: Y first, B residual against dequantized Y (base
+ * correlation b = 1.0, x = 0.0) [ext] */
+void jxo_quant_dc(const jxo_frame* f, const float dc[3], int32_t dcq[3]) {
+  int qy = dc[1] * f->dc_mul[1] >= 0.0f ? (int)(dc[1] * f->dc_mul[1] + 0.5f)
+                                        : -(int)(-(dc[1] * f->dc_mul[1]) + 0.5f);
+  float ydq = (float)qy * f->dc_step[1];
+  float xv = dc[0] * f->dc_mul[0];
+  float bv = (dc[2] - ydq) * f->dc_mul[2];
+  dcq[1] = qy;
+  dcq[0] = xv >= 0.0f ? (int)(xv + 0.5f) : -(int)(-xv + 0.5f);
+  dcq[2] = bv >= 0.0f ? (int)(bv + 0.5f) : -(int)(-bv + 0.5f);
+}
+
 /* block-level front end: pixels px[c][64] (X,Y,B), returns chosen strategy,
  * writes qf raw (1..256), quantized AC and DC. */
 int jxo_front_block(const jxo_frame* f, const float px[3][64], const float* homog,
-                    int32_t q[3][64], int32_t dcq[3], int* qf_raw) {
+                    int32_t q[3][64], int32_t dcq[3], int* qf_raw, float* ent_out) {
   /* block DC = mean: row partial sums (left to right), then the 8 row sums
    * tree-summed -- the 8-lane order of the GPU path (lane = row) */
   float dc[3];
@@ -354,14 +367,7 @@ int jxo_front_block(const jxo_frame* f, const float px[3][64], const float* homo
   }
   /* DC quantization: Y first, B residual against dequantized Y (base
    * correlation b = 1.0, x = 0.0) */
-  int qy = dc[1] * f->dc_mul[1] >= 0.0f ? (int)(dc[1] * f->dc_mul[1] + 0.5f)
-                                        : -(int)(-(dc[1] * f->dc_mul[1]) + 0.5f);
-  float ydq = (float)qy * f->dc_step[1];
-  float xv = dc[0] * f->dc_mul[0];
-  float bv = (dc[2] - ydq) * f->dc_mul[2];
-  dcq[1] = qy;
-  dcq[0] = xv >= 0.0f ? (int)(xv + 0.5f) : -(int)(-xv + 0.5f);
-  dcq[2] = bv >= 0.0f ? (int)(bv + 0.5f) : -(int)(-bv + 0.5f);
+  jxo_quant_dc(f, dc, dcq);
 
   /* adaptive quantization: mean absolute gradient of Y inside the block;
    * per row y: horizontal diffs of row y plus vertical diffs to row y+1,
@@ -392,8 +398,8 @@ int jxo_front_block(const jxo_frame* f, const float px[3][64], const float* homo
   static const int cand[4] = {JXO_DCT8, JXO_DCT4X4, JXO_DCT4X8, JXO_DCT8X4};
   const int ncand = f->effort >= 5 ? 4 : 1;
   int best_t = JXO_DCT8;
+  float best = FLT_MAX;
   if (ncand > 1) {
-    float best = FLT_MAX;
     for (int i = 0; i < ncand; i++) {
       float e = jxo_quantize_block(f, cand[i], px, scale, NULL);
       if (f->proposals & 2) e = jxo_hook_f(e, homog[0], homog[1], homog[2]);
@@ -403,6 +409,9 @@ int jxo_front_block(const jxo_frame* f, const float px[3][64], const float* homo
       }
     }
   }
+  /* the estimate the merge stage sums is stored before the P override
+   * (homogeneity-partitioning.diff:271 context) */
+  if (ent_out) *ent_out = best;
   if ((f->proposals & 1) && best_t == JXO_DCT8) {
     /* HomogeneityPartition thresholds, combined.diff:219-234 */
     float T = 1.60f;

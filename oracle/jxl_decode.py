@@ -709,6 +709,105 @@ def _idct_mat(n):
 
 _I8, _I4 = _idct_mat(8), _idct_mat(4)
 
+# merged varblocks [ext AcStrategy]: raw id -> (blocks down, blocks across, kind)
+SHAPES = {6: (2, 1, 0), 7: (1, 2, 0), 4: (2, 2, 1), 10: (4, 2, 2), 11: (2, 4, 2), 5: (4, 4, 3),
+          19: (8, 4, 4), 20: (4, 8, 4), 18: (8, 8, 5)}
+# default weight bands per kind [ext quant_weights.cc]; stored dims rows x cols
+KIND_DIM = [(8, 16), (16, 16), (16, 32), (32, 32), (32, 64), (64, 64)]
+KIND_BANDS = [
+    [[7240.7734393502, -0.7, -0.7, -0.2, -0.2, -0.2, -0.5],
+     [1448.15468787004, -0.5, -0.5, -0.5, -0.2, -0.2, -0.2],
+     [506.854140754517, -1.4, -0.2, -0.5, -0.5, -1.5, -3.6]],
+    [[8996.8725711814115328, -1.3000777393353804, -0.49424529824571225, -0.439093774457103443,
+      -0.6350101832695744, -0.90177264050827612, -1.6162099239887414],
+     [3191.48366296844234752, -0.67424582104194355, -0.80745813428471001, -0.44925837484843441,
+      -0.35865440981033403, -0.31322389111877305, -0.37615025315725483],
+     [1157.50408145487200256, -2.0531423165804414, -1.4, -0.50687130033378396,
+      -0.42708730624733904, -1.4856834539296244, -4.9209142884401604]],
+    [[13844.97076442300573, -0.97113799999999995, -0.658, -0.42026, -0.22712, -0.2206, -0.226, -0.6],
+     [4798.964084220744293, -0.61125308982767057, -0.83770786552491361, -0.79014862079498627,
+      -0.2692727459704829, -0.38272769465388551, -0.22924222653091453, -0.20719098826199578],
+     [1807.236946760964614, -1.2, -1.2, -0.7, -0.7, -0.7, -0.4, -0.5]],
+    [[15718.40830982518931456, -1.025, -0.98, -0.9012, -0.4, -0.48819395464, -0.421064, -0.27],
+     [7305.7636810695983104, -0.8041958212306401, -0.7633036457487539, -0.55660379990111464,
+      -0.49785304658857626, -0.43699592683512467, -0.40180866526242109, -0.27321683125358037],
+     [3803.53173721215041536, -3.060733579805728, -2.0413270132490346, -2.0235650159727417,
+      -0.5495389509954993, -0.4, -0.4, -0.3]],
+    [[0.65 * 23629.073922049845, -1.025, -0.78, -0.65012, -0.19041574084286472, -0.20819395464,
+      -0.421064, -0.32733845535848671],
+     [0.65 * 8611.3238710010046, -0.3041958212306401, -0.3633036457487539, -0.35660379990111464,
+      -0.3443074455424403, -0.33699592683512467, -0.30180866526242109, -0.27321683125358037],
+     [0.65 * 4492.2486445538634, -1.2, -1.2, -0.8, -0.7, -0.7, -0.4, -0.5]],
+    [[0.9 * 26629.073922049845, -1.025, -0.78, -0.65012, -0.19041574084286472, -0.20819395464,
+      -0.421064, -0.32733845535848671],
+     [0.9 * 9311.3238710010046, -0.3041958212306401, -0.3633036457487539, -0.35660379990111464,
+      -0.3443074455424403, -0.33699592683512467, -0.30180866526242109, -0.27321683125358037],
+     [0.9 * 4992.2486445538634, -1.2, -1.2, -0.8, -0.7, -0.7, -0.4, -0.5]],
+]
+
+
+def natural_order(rows, cols):
+    """[position] -> stored raster index of a rows x cols (rows <= cols)
+    coefficient block: LLF raster first, then the y-scaled zigzag."""
+    cs, cl, xf = rows // 8, cols // 8, cols // rows
+    order = [y * cols + x for y in range(cs) for x in range(cl)]
+    for i in range(cols):
+        for j in range(i + 1):
+            x, y = j, i - j
+            if i % 2:
+                x, y = y, x
+            if y % xf:
+                continue
+            y //= xf
+            if x < cl and y < cs:
+                continue
+            order.append(y * cols + x)
+    for ip in range(cols - 1, 0, -1):
+        i = ip - 1
+        for j in range(i + 1):
+            x, y = cols - 1 - (i - j), cols - 1 - j
+            if i % 2:
+                x, y = y, x
+            if y % xf:
+                continue
+            y //= xf
+            order.append(y * cols + x)
+    assert len(order) == rows * cols and len(set(order)) == rows * cols
+    return order
+
+
+_KIND_CACHE = {}
+
+
+def kind_tables(kind):
+    """(inverse weights (3, rows*cols) stored raster, natural order)"""
+    if kind not in _KIND_CACHE:
+        r, c = KIND_DIM[kind]
+        w = _weights(r, c, KIND_BANDS[kind], len(KIND_BANDS[kind][0]))
+        _KIND_CACHE[kind] = (1.0 / w, natural_order(r, c))
+    return _KIND_CACHE[kind]
+
+
+def _llf_scale(M):
+    return np.array([math.cos(math.pi * k / (16 * M)) * math.cos(math.pi * k / (8 * M)) *
+                     math.cos(math.pi * k / (4 * M)) for k in range(M)])
+
+
+def _dct_mat(n):
+    """normalized forward DCT: out = m @ x, out[0] = mean"""
+    return np.linalg.inv(_idct_mat(n))
+
+
+def reconstruct_varblock(t, coefs, dcs):
+    """coefs: (R, C) dequantized coefficients in pixel orientation (LLF slots
+    ignored); dcs: (cy, cx) dequantized DC of the covered blocks -> pixels"""
+    cy, cx, _ = SHAPES[t]
+    co = coefs.copy()
+    llf = _dct_mat(cy) @ dcs @ _dct_mat(cx).T
+    llf = llf / np.outer(_llf_scale(cy), _llf_scale(cx))
+    co[:cy, :cx] = llf
+    return _idct_mat(8 * cy) @ co @ _idct_mat(8 * cx).T
+
 
 def inverse_transform(t, co):
     """co: 64 coefficients (layout of strategy t) -> 8x8 pixels."""
@@ -899,11 +998,17 @@ def decode(data: bytes, want_pixels: bool = True) -> Decoded:
                 if k >= count:
                     raise JxlError("too few varblocks")
                 t = meta[2][0][k]
-                if t not in (0, 3, 12, 13):
+                if t not in (0, 3, 12, 13) and t not in SHAPES:
                     raise JxlError("AC strategy %d not produced" % t)
-                d.acs[by0 + y, bx0 + x] = t
-                d.qf[by0 + y, bx0 + x] = 1 + min(max(meta[2][1][k], 0), 255)
-                covered[y, x] = True
+                cy, cx = SHAPES[t][:2] if t in SHAPES else (1, 1)
+                if y + cy > bh or x + cx > bw or covered[y:y + cy, x:x + cx].any():
+                    raise JxlError("varblock out of bounds / overlapping")
+                qv = 1 + min(max(meta[2][1][k], 0), 255)
+                for iy in range(cy):
+                    for ix in range(cx):
+                        d.acs[by0 + y + iy, bx0 + x + ix] = t | (0x80 if (iy or ix) else 0)
+                        d.qf[by0 + y + iy, bx0 + x + ix] = qv
+                covered[y:y + cy, x:x + cx] = True
                 k += 1
         if k != count:
             raise JxlError("varblock count mismatch")
@@ -917,7 +1022,6 @@ def decode(data: bytes, want_pixels: bool = True) -> Decoded:
         raise JxlError("custom coefficient orders not produced")
     nctx_ac = 15 * (37 + 458)
     hf = EntropyStream(s, npresets * nctx_ac)
-    order = natural_order8()
     d.ac = np.zeros((bys, bxs, 3, 64), dtype=np.int64)
     d.ac_tokens = np.zeros((ng, 3), dtype=np.int64)
     for g in range(ng):
@@ -932,6 +1036,12 @@ def decode(data: bytes, want_pixels: bool = True) -> Decoded:
         for by in range(gh):
             for bx in range(gw):
                 t = int(d.acs[by0 + by, bx0 + bx])
+                if t & 0x80:
+                    continue
+                cy, cx = SHAPES[t][:2] if t in SHAPES else (1, 1)
+                cb = cy * cx
+                lcb = cb.bit_length() - 1
+                size = 64 * cb
                 ordi = STRATEGY_ORDER[t]
                 for c in (1, 0, 2):
                     if bx == 0:
@@ -945,18 +1055,19 @@ def decode(data: bytes, want_pixels: bool = True) -> Decoded:
                     bucket = pp if pp < 8 else 4 + pp // 2
                     nz = hf.read(s, off + bucket * 15 + bctx)
                     ntok = 1
-                    if nz + 1 > 64:
+                    if nz > size - cb:
                         raise JxlError("nzeros too large")
-                    nzs[c, by, bx] = nz
+                    nzs[c, by:by + cy, bx:bx + cx] = (nz + cb - 1) >> lcb
                     zoff = off + 15 * 37 + 458 * bctx
-                    prev = 0 if nz > 4 else 1
-                    k = 1
+                    prev = 0 if nz > size // 16 else 1
+                    k = cb
                     left = nz
-                    while k < 64 and left > 0:
-                        u = hf.read(s, zoff + (NNZ_CTX[left] + FREQ_CTX[k]) * 2 + prev)
+                    while k < size and left > 0:
+                        u = hf.read(s, zoff + (NNZ_CTX[(left + cb - 1) >> lcb] + FREQ_CTX[k >> lcb]) * 2 + prev)
                         ntok += 1
                         v = unpack_signed(u)
-                        d.ac[by0 + by, bx0 + bx, c, order[k]] = v
+                        sl = k >> 6
+                        d.ac[by0 + by + sl // cx, bx0 + bx + sl % cx, c, k & 63] = v
                         prev = 1 if u else 0
                         left -= prev
                         k += 1
@@ -983,18 +1094,43 @@ def reconstruct(d: Decoded) -> np.ndarray:
     # AdjustQuantBias
     adj = np.where(np.abs(ac) == 1, np.sign(ac) * np.array(QUANT_BIAS[:3])[None, None, :, None],
                    np.where(ac == 0, 0.0, ac - QUANT_BIAS[3] / np.where(ac == 0, 1, ac)))
+    order8 = np.array(natural_order8())
+    dcq = np.stack([d.dc[0] * dc_step[0], d.dc[1] * dc_step[1],
+                    d.dc[2] * dc_step[2] + d.dc[1] * dc_step[1]])  # X, Y, B (ytob 1.0)
+    chm = (x_mul, 1.0, b_mul)
     for by in range(d.bys):
         for bx in range(d.bxs):
             t = int(d.acs[by, bx])
+            if t & 0x80:
+                continue
             qf = d.qf[by, bx]
+            if t in SHAPES:
+                ccy, ccx, kind = SHAPES[t]
+                R, C = 8 * ccy, 8 * ccx
+                iw, nat = kind_tables(kind)
+                nat = np.array(nat)
+                cols_s = KIND_DIM[kind][1]
+                sy, sx = nat // cols_s, nat % cols_s
+                ky, kx = (sy, sx) if ccx >= ccy else (sx, sy)
+                vals = np.zeros((3, R * C))
+                for i in range(ccy * ccx):
+                    vals[:, i * 64:(i + 1) * 64] = adj[by + i // ccx, bx + i % ccx]
+                co = np.zeros((3, R, C))
+                for c in range(3):
+                    co[c, ky, kx] = vals[c] * iw[c][nat] * (inv_gs / qf) * chm[c]
+                co[2] += co[1]  # ytob base 1.0
+                for c, arr in ((0, X), (1, Y), (2, B)):
+                    arr[by * 8:by * 8 + R, bx * 8:bx * 8 + C] = reconstruct_varblock(
+                        t, co[c], dcq[c, by:by + ccy, bx:bx + ccx])
+                continue
             mul = deq[t] * (inv_gs / qf)
-            cy = adj[by, bx, 1] * mul[1]
-            cx = adj[by, bx, 0] * mul[0] * x_mul
-            cb = adj[by, bx, 2] * mul[2] * b_mul + cy  # ytob base 1.0
-            dcy = d.dc[1, by, bx] * dc_step[1]
-            dcx = d.dc[0, by, bx] * dc_step[0]
-            dcb = d.dc[2, by, bx] * dc_step[2] + dcy
-            for arr, co, dcv in ((X, cx, dcx), (Y, cy, dcy), (B, cb, dcb)):
+            raster = np.zeros((3, 64))
+            raster[:, order8] = adj[by, bx]
+            cy = raster[1] * mul[1]
+            cx = raster[0] * mul[0] * x_mul
+            cb = raster[2] * mul[2] * b_mul + cy  # ytob base 1.0
+            for arr, co, dcv in ((X, cx, dcq[0, by, bx]), (Y, cy, dcq[1, by, bx]),
+                                 (B, cb, dcq[2, by, bx])):
                 co = co.copy()
                 co[0] = dcv
                 arr[by * 8:by * 8 + 8, bx * 8:bx * 8 + 8] = inverse_transform(t, co)

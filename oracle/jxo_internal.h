@@ -44,6 +44,7 @@ enum { JXO_QK_DCT8 = 0, JXO_QK_DCT4 = 1, JXO_QK_DCT4X8 = 2 };
 void jxo_frame_init(jxo_frame* f, uint32_t w, uint32_t h, const jxo_params* p);
 void jxo_quant_weights(int kind, float out[3][64]);
 void jxo_natural_order8(uint8_t order[64]);
+void jxo_quant_dc(const jxo_frame* f, const float dc[3], int32_t dcq[3]);
 
 /* AC context model constants [ext libjxl ac_context.h] */
 #define JXO_NUM_ORDERS 13
@@ -55,6 +56,34 @@ extern const uint8_t jxo_strategy_order[27];
 extern const uint8_t jxo_default_ctx_map[39];
 extern const uint8_t jxo_freq_ctx[64];
 extern const uint16_t jxo_nnz_ctx[64];
+
+/* merged varblocks (merge.c) [ext AcStrategy / quant_weights / coeff_order] */
+enum { JXO_VK_16X8 = 0, JXO_VK_16, JXO_VK_32X16, JXO_VK_32, JXO_VK_64X32, JXO_VK_64,
+       JXO_NVKINDS };
+typedef struct {
+  uint8_t type, cy, cx, kind; /* raw id, blocks down, blocks across, weight kind */
+  float tmul;                 /* cost multiplier of the search */
+} jxo_shape;
+#define JXO_NSHAPES 9
+extern const jxo_shape jxo_shapes[JXO_NSHAPES];
+typedef struct {
+  int rows, cols; /* stored orientation: rows = 8 min(cy,cx), cols = 8 max(cy,cx) */
+  float* w[3];    /* weights per channel X, Y, B, stored raster */
+  uint16_t* nat;  /* stored raster index -> natural order position */
+} jxo_vkind;
+const jxo_vkind* jxo_vkinds(void);
+int jxo_shape_of(int type); /* shape index of a merged raw id, -1 otherwise */
+float jxo_varblock(const jxo_frame* f, const jxo_shape* s, const float* xyb, int px0, int py0,
+                   int raw, int32_t* q /* [3][R*C] natural order */, float* llf /* [3][8][8] */,
+                   int* nz /* [3] */);
+float jxo_llf_dc(const jxo_shape* s, const float* llf_c, int by, int bx);
+void jxo_merge_tile(const jxo_frame* f, const float* xyb, const float* homog, int tx, int ty,
+                    int max_s, float* ent, const int* raw, uint8_t* acs);
+/* covered 8x8 blocks of a raw strategy id (1 for the 8x8 class) */
+static inline int jxo_covered(int type) {
+  const int s = jxo_shape_of(type);
+  return s < 0 ? 1 : jxo_shapes[s].cy * jxo_shapes[s].cx;
+}
 
 #define JXO_MAX_CLUSTERS 132
 #define JXO_ALPHA 128

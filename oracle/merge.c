@@ -1,0 +1,419 @@
+/*
+ * merge.c -- ORACLE (test infrastructure).  Variable-size varblocks: the
+ * second stage of the AC-strategy search, which merges 8x8-class decisions
+ * into 16x8 ... 64x64 DCTs, and the transform / quantization / LLF-derived DC
+ * of a merged varblock.
+ *
+ * [ext] libjxl enc_ac_strategy.cc (FindBestFirstLevelDivisionForSquare /
+ * TryMergeAcs), enc_transforms-inl.h (TransformFromPixels, DCFromLowest-
+ * Frequencies), quant_weights.cc (default DCT16..DCT64 weight bands),
+ * coeff_order.cc (natural coefficient order); none of it is in
+ * /root/reference, restated per DESIGN.md §3.4 -- parity unpinned vs libjxl.
+ *
+ * The thesis hooks reach this stage the way they reach libjxl's merge step:
+ *  - hook F (/root/reference/proposals/combined.diff:247-253) multiplies every
+ *    entropy estimate, here the estimate of every merge candidate, by
+ *    0.8 * avg(r_h, r_v, r_d) of the candidate's top-left 8x8 block;
+ *  - a candidate is accepted unless `entropy_candidate >= entropy_current`
+ *    (the comparison of TryMergeAcs, combined.diff:294 context), so a NaN
+ *    estimate is accepted;
+ *  - hook P (combined.diff:270-274) only overrides the 8x8 decision; the
+ *    per-block estimate the merge step sums is the pre-override one.
+ *
+ * Float contract (mirrored by jxg_merge.hip): 1-D DCTs are Lee's recursive
+ * even/odd split with float constants c_N[i] = (float)(1/(2 cos(pi(2i+1)/2N)))
+ * and output scales s_N[k] = (float)(k ? sqrt2/N : 1/N); rows first, then
+ * columns; the quantization walks pixel-orientation columns (one GPU lane per
+ * column) over channels Y, X, B and rows ky ascending, fmaf(e, e, part); the
+ * column partials are tree-summed pairwise (tree_sum).
+ */
+#include <float.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "jxo_internal.h"
+
+/* raw id, cy (blocks down), cx (blocks across), weight kind, cost multiplier */
+const jxo_shape jxo_shapes[JXO_NSHAPES] = {
+    {6, 2, 1, JXO_VK_16X8, 1.0f},   /* DCT16X8: 16 rows x 8 cols  */
+    {7, 1, 2, JXO_VK_16X8, 1.0f},   /* DCT8X16                    */
+    {4, 2, 2, JXO_VK_16, 1.0f},     /* DCT16X16                   */
+    {10, 4, 2, JXO_VK_32X16, 1.02f}, /* DCT32X16                  */
+    {11, 2, 4, JXO_VK_32X16, 1.02f}, /* DCT16X32                  */
+    {5, 4, 4, JXO_VK_32, 1.03f},    /* DCT32X32                   */
+    {19, 8, 4, JXO_VK_64X32, 1.05f}, /* DCT64X32                  */
+    {20, 4, 8, JXO_VK_64X32, 1.05f}, /* DCT32X64                  */
+    {18, 8, 8, JXO_VK_64, 1.05f},   /* DCT64X64                   */
+};
+
+int jxo_shape_of(int type) {
+  for (int i = 0; i < JXO_NSHAPES; i++)
+    if (jxo_shapes[i].type == type) return i;
+  return -1;
+}
+
+/* ---------------- tables (built once, double -> float) ---------------- */
+static float g_lee_c[7][32]; /* [log2 N][i], N = 2..64 */
+static float g_lee_s[7][64]; /* [log2 N][k], N = 1..64 */
+static float g_llf_p[4][8];  /* [log2 M][k]  M = 1..8 blocks */
+static float g_llf_ib[4][8][8]; /* [log2 M][n][k] inverse basis */
+static jxo_vkind g_kinds[JXO_NVKINDS];
+static int g_init = 0;
+
+/* default weight bands [ext quant_weights.cc] */
+static const double kBands[JXO_NVKINDS][3][8] = {
+    /* DCT16X8 */
+    {{7240.7734393502, -0.7, -0.7, -0.2, -0.2, -0.2, -0.5},
+     {1448.15468787004, -0.5, -0.5, -0.5, -0.2, -0.2, -0.2},
+     {506.854140754517, -1.4, -0.2, -0.5, -0.5, -1.5, -3.6}},
+    /* DCT16X16 */
+    {{8996.8725711814115328, -1.3000777393353804, -0.49424529824571225, -0.439093774457103443,
+      -0.6350101832695744, -0.90177264050827612, -1.6162099239887414},
+     {3191.48366296844234752, -0.67424582104194355, -0.80745813428471001,
+      -0.44925837484843441, -0.35865440981033403, -0.31322389111877305, -0.37615025315725483},
+     {1157.50408145487200256, -2.0531423165804414, -1.4, -0.50687130033378396,
+      -0.42708730624733904, -1.4856834539296244, -4.9209142884401604}},
+    /* DCT32X16 */
+    {{13844.97076442300573, -0.97113799999999995, -0.658, -0.42026, -0.22712, -0.2206, -0.226,
+      -0.6},
+     {4798.964084220744293, -0.61125308982767057, -0.83770786552491361, -0.79014862079498627,
+      -0.2692727459704829, -0.38272769465388551, -0.22924222653091453, -0.20719098826199578},
+     {1807.236946760964614, -1.2, -1.2, -0.7, -0.7, -0.7, -0.4, -0.5}},
+    /* DCT32X32 */
+    {{15718.40830982518931456, -1.025, -0.98, -0.9012, -0.4, -0.48819395464, -0.421064, -0.27},
+     {7305.7636810695983104, -0.8041958212306401, -0.7633036457487539, -0.55660379990111464,
+      -0.49785304658857626, -0.43699592683512467, -0.40180866526242109, -0.27321683125358037},
+     {3803.53173721215041536, -3.060733579805728, -2.0413270132490346, -2.0235650159727417,
+      -0.5495389509954993, -0.4, -0.4, -0.3}},
+    /* DCT64X32 */
+    {{0.65 * 23629.073922049845, -1.025, -0.78, -0.65012, -0.19041574084286472, -0.20819395464,
+      -0.421064, -0.32733845535848671},
+     {0.65 * 8611.3238710010046, -0.3041958212306401, -0.3633036457487539, -0.35660379990111464,
+      -0.3443074455424403, -0.33699592683512467, -0.30180866526242109, -0.27321683125358037},
+     {0.65 * 4492.2486445538634, -1.2, -1.2, -0.8, -0.7, -0.7, -0.4, -0.5}},
+    /* DCT64X64 */
+    {{0.9 * 26629.073922049845, -1.025, -0.78, -0.65012, -0.19041574084286472, -0.20819395464,
+      -0.421064, -0.32733845535848671},
+     {0.9 * 9311.3238710010046, -0.3041958212306401, -0.3633036457487539, -0.35660379990111464,
+      -0.3443074455424403, -0.33699592683512467, -0.30180866526242109, -0.27321683125358037},
+     {0.9 * 4992.2486445538634, -1.2, -1.2, -0.8, -0.7, -0.7, -0.4, -0.5}},
+};
+static const int kNumBands[JXO_NVKINDS] = {7, 7, 8, 8, 8, 8};
+static const int kKindDim[JXO_NVKINDS][2] = {{8, 16}, {16, 16}, {16, 32},
+                                             {32, 32}, {32, 64}, {64, 64}};
+
+/* GetQuantWeights [ext]: bands -> weights over a rows x cols table */
+static void kind_weights(int kind, float* out3[3]) {
+  const int rows = kKindDim[kind][0], cols = kKindDim[kind][1], nb = kNumBands[kind];
+  for (int c = 0; c < 3; c++) {
+    double bands[8];
+    bands[0] = kBands[kind][c][0];
+    for (int i = 1; i < nb; i++) {
+      const double v = kBands[kind][c][i];
+      bands[i] = bands[i - 1] * (v > 0 ? 1.0 + v : 1.0 / (1.0 - v));
+    }
+    const double scale = (nb - 1) / (1.4142135623730951 + 1e-6);
+    const double rc = scale / (cols - 1), rr = scale / (rows - 1);
+    for (int y = 0; y < rows; y++)
+      for (int x = 0; x < cols; x++) {
+        const double dx = x * rc, dy = y * rr;
+        const double pos = sqrt(dx * dx + dy * dy);
+        int idx = (int)pos;
+        if (idx > nb - 2) idx = nb - 2;
+        const double frac = pos - idx;
+        const double a = bands[idx], b = bands[idx + 1];
+        out3[c][y * cols + x] = (float)(a * pow(b / a, frac));
+      }
+  }
+}
+
+/* natural coefficient order of a stored rows x cols block (rows <= cols):
+ * the LLF (y < rows/8, x < cols/8) in raster order, then the zigzag over the
+ * cols x cols square with y scaled down by cols/rows [ext coeff_order.cc] */
+static void kind_order(int kind, uint16_t* nat /* [stored idx] -> position */) {
+  const int rows = kKindDim[kind][0], cols = kKindDim[kind][1];
+  const int cs = rows / 8, cl = cols / 8, xf = cols / rows;
+  int cur = 0;
+  for (int y = 0; y < cs; y++)
+    for (int x = 0; x < cl; x++) nat[y * cols + x] = (uint16_t)cur++;
+  for (int i = 0; i < cols; i++)
+    for (int j = 0; j <= i; j++) {
+      int x = j, y = i - j;
+      if (i & 1) {
+        const int t = x;
+        x = y;
+        y = t;
+      }
+      if (y % xf) continue;
+      y /= xf;
+      if (x < cl && y < cs) continue;
+      nat[y * cols + x] = (uint16_t)cur++;
+    }
+  for (int ip = cols - 1; ip > 0; ip--) {
+    const int i = ip - 1;
+    for (int j = 0; j <= i; j++) {
+      int x = cols - 1 - (i - j), y = cols - 1 - j;
+      if (i & 1) {
+        const int t = x;
+        x = y;
+        y = t;
+      }
+      if (y % xf) continue;
+      y /= xf;
+      nat[y * cols + x] = (uint16_t)cur++;
+    }
+  }
+}
+
+static void init_tables(void) {
+  if (g_init) return;
+  const double pi = 3.14159265358979323846;
+  for (int l = 0; l < 7; l++) {
+    const int N = 1 << l;
+    for (int i = 0; i < N / 2; i++) g_lee_c[l][i] = (float)(1.0 / (2.0 * cos(pi * (2 * i + 1) / (2.0 * N))));
+    for (int k = 0; k < N; k++) g_lee_s[l][k] = (float)(k ? sqrt(2.0) / N : 1.0 / N);
+  }
+  for (int l = 0; l < 4; l++) {
+    const int M = 1 << l;
+    for (int k = 0; k < M; k++)
+      g_llf_p[l][k] = (float)(cos(pi * k / (16.0 * M)) * cos(pi * k / (8.0 * M)) *
+                              cos(pi * k / (4.0 * M)));
+    for (int n = 0; n < M; n++)
+      for (int k = 0; k < M; k++)
+        g_llf_ib[l][n][k] = (float)(k ? sqrt(2.0) * cos(pi * (2 * n + 1) * k / (2.0 * M)) : 1.0);
+  }
+  for (int k = 0; k < JXO_NVKINDS; k++) {
+    jxo_vkind* K = &g_kinds[k];
+    K->rows = kKindDim[k][0];
+    K->cols = kKindDim[k][1];
+    const int n = K->rows * K->cols;
+    for (int c = 0; c < 3; c++) K->w[c] = (float*)malloc(sizeof(float) * n);
+    K->nat = (uint16_t*)malloc(sizeof(uint16_t) * n);
+    kind_weights(k, K->w);
+    kind_order(k, K->nat);
+  }
+  g_init = 1;
+}
+
+const jxo_vkind* jxo_vkinds(void) {
+  init_tables();
+  return g_kinds;
+}
+const float* jxo_lee_consts(void) { /* [7][32] then [7][64] (for the product's tables test) */
+  init_tables();
+  return &g_lee_c[0][0];
+}
+
+static int ilog2(int n) {
+  int l = 0;
+  while ((1 << l) < n) l++;
+  return l;
+}
+
+/* unnormalized DCT-II in place (Lee): X_k = sum_n x_n cos(pi(2n+1)k/2N) */
+static void lee(float* x, int N) {
+  if (N == 1) return;
+  const int h = N / 2, l = ilog2(N);
+  float a[32], b[32];
+  for (int i = 0; i < h; i++) {
+    a[i] = x[i] + x[N - 1 - i];
+    b[i] = (x[i] - x[N - 1 - i]) * g_lee_c[l][i];
+  }
+  lee(a, h);
+  lee(b, h);
+  for (int k = 0; k < h; k++) x[2 * k] = a[k];
+  for (int k = 0; k < h - 1; k++) x[2 * k + 1] = b[k] + b[k + 1];
+  x[N - 1] = b[h - 1];
+}
+/* normalized 1-D DCT (out[0] = mean) */
+static void dct_n(float* x, int N) {
+  const int l = ilog2(N);
+  lee(x, N);
+  for (int k = 0; k < N; k++) x[k] = x[k] * g_lee_s[l][k];
+}
+
+/* pairwise tree over n (power of two) values, the XOR-butterfly order */
+static float tree_sum(const float* v, int n) {
+  if (n == 1) return v[0];
+  return tree_sum(v, n / 2) + tree_sum(v + n / 2, n / 2);
+}
+
+static inline int bitlen(uint32_t v) {
+  int n = 0;
+  while (v) {
+    n++;
+    v >>= 1;
+  }
+  return n;
+}
+static inline int quant1(float v) { /* == front.c quant1 */
+  float a = fabsf(v);
+  if (a < 0.58f) return 0;
+  int q = a < 32767.0f ? (int)(a + 0.5f) : 32767;
+  if (q > 32767) q = 32767;
+  return v < 0.0f ? -q : q;
+}
+static const float kBias1 = 1.0f - 0.07005449891748593f;
+static inline float adjust_bias_y(int q) {
+  if (q == 0) return 0.0f;
+  if (q == 1) return kBias1;
+  if (q == -1) return -kBias1;
+  return (float)q - 0.145f / (float)q;
+}
+
+/* stored-table index of pixel-orientation frequency (ky, kx) */
+static inline int stored_index(const jxo_shape* s, int ky, int kx) {
+  const int C = 8 * s->cx, R = 8 * s->cy;
+  return s->cx >= s->cy ? ky * C + kx : kx * R + ky;
+}
+
+float jxo_varblock(const jxo_frame* f, const jxo_shape* s, const float* xyb, int px0, int py0,
+                   int raw, int32_t* q, float* llf, int* nzo) {
+  init_tables();
+  const int R = 8 * s->cy, C = 8 * s->cx;
+  const jxo_vkind* K = &g_kinds[s->kind];
+  const size_t plane = (size_t)f->xp * f->yp;
+  static float F[3][64 * 64];
+  float tmp[64];
+  for (int c = 0; c < 3; c++) {
+    const float* P = xyb + c * plane;
+    for (int y = 0; y < R; y++) {
+      for (int x = 0; x < C; x++) tmp[x] = P[(size_t)(py0 + y) * f->xp + px0 + x];
+      dct_n(tmp, C);
+      for (int x = 0; x < C; x++) F[c][y * C + x] = tmp[x];
+    }
+    for (int x = 0; x < C; x++) {
+      for (int y = 0; y < R; y++) tmp[y] = F[c][y * C + x];
+      dct_n(tmp, R);
+      for (int y = 0; y < R; y++) F[c][y * C + x] = tmp[y];
+    }
+  }
+  const float scale = (float)f->G * (float)raw / 65536.0f;
+  const float inv_scale = 1.0f / scale;
+  float part[64];
+  int bits = 0, nz[3] = {0, 0, 0};
+  static const int corder[3] = {1, 0, 2};
+  for (int x = 0; x < C; x++) {
+    float yd[64];
+    part[x] = 0.0f;
+    for (int ci = 0; ci < 3; ci++) {
+      const int c = corder[ci];
+      for (int ky = 0; ky < R; ky++) {
+        const int si = stored_index(s, ky, x);
+        if (ky < s->cy && x < s->cx) { /* LLF: carried by the DC image */
+          if (q) q[c * R * C + K->nat[si]] = 0;
+          continue;
+        }
+        const float w = K->w[c][si];
+        const float ws = w * scale;
+        float rv = F[c][ky * C + x];
+        if (c == 2) rv = rv - yd[ky];
+        const float v = rv * ws;
+        const int qq = quant1(v);
+        if (c == 1) yd[ky] = adjust_bias_y(qq) * ((1.0f / w) * inv_scale);
+        const uint32_t aq = (uint32_t)(qq < 0 ? -qq : qq);
+        const float e = fabsf(v) - (float)aq;
+        part[x] = fmaf(e, e, part[x]);
+        if (aq) {
+          bits += 2 + 2 * bitlen(aq);
+          nz[c]++;
+        }
+        if (q) q[c * R * C + K->nat[si]] = qq;
+      }
+    }
+  }
+  for (int c = 0; c < 3; c++) bits += bitlen((uint32_t)nz[c]);
+  if (nzo)
+    for (int c = 0; c < 3; c++) nzo[c] = nz[c];
+  if (llf)
+    for (int c = 0; c < 3; c++)
+      for (int ky = 0; ky < s->cy; ky++)
+        for (int kx = 0; kx < s->cx; kx++) llf[(c * 8 + ky) * 8 + kx] = F[c][ky * C + kx];
+  const float dist = tree_sum(part, C);
+  return ((float)bits + 8.0f * dist) * s->tmul;
+}
+
+/* DC of covered block (by, bx) from the LLF [ext DCFromLowestFrequencies]:
+ * t = (F * P_cy[ky]) * P_cx[kx]; u[ky] = sum_kx fmaf(t, IB_cx[bx][kx]);
+ * dc = sum_ky fmaf(u[ky], IB_cy[by][ky]) */
+float jxo_llf_dc(const jxo_shape* s, const float* llf_c /* [8][8] */, int by, int bx) {
+  init_tables();
+  const int ly = ilog2(s->cy), lx = ilog2(s->cx);
+  float acc = 0.0f;
+  for (int ky = 0; ky < s->cy; ky++) {
+    float u = 0.0f;
+    for (int kx = 0; kx < s->cx; kx++) {
+      const float t = (llf_c[ky * 8 + kx] * g_llf_p[ly][ky]) * g_llf_p[lx][kx];
+      u = fmaf(t, g_llf_ib[lx][bx][kx], u);
+    }
+    acc = fmaf(u, g_llf_ib[ly][by][ky], acc);
+  }
+  return acc;
+}
+
+/* merge search over one 64x64 tile; ent/raw/acs are whole-frame per-block
+ * arrays (acs holds raw ids, bit 7 set on covered non-first blocks) */
+void jxo_merge_tile(const jxo_frame* f, const float* xyb, const float* homog, int tx, int ty,
+                    int max_s, float* ent, const int* raw, uint8_t* acs) {
+  for (int s = 2; s <= max_s; s *= 2) {
+    const int full = s == 2 ? 2 : (s == 4 ? 5 : 8);      /* shape index */
+    const int tall = s == 2 ? 0 : (s == 4 ? 3 : 6);
+    const int wide = tall + 1;
+    for (int ry = 0; ry < 8 / s; ry++)
+      for (int rx = 0; rx < 8 / s; rx++) {
+        const int bx0 = tx * 8 + rx * s, by0 = ty * 8 + ry * s;
+        if (bx0 + s > (int)f->bxs || by0 + s > (int)f->bys) continue;
+        float cur = 0.0f;
+        for (int iy = 0; iy < s; iy++)
+          for (int ix = 0; ix < s; ix++) cur += ent[(size_t)(by0 + iy) * f->bxs + bx0 + ix];
+        /* candidate estimates (hook F at each varblock's top-left block) */
+        float e[5];
+        const int vs[5] = {full, tall, tall, wide, wide};
+        const int vx[5] = {0, 0, s / 2, 0, 0}, vy[5] = {0, 0, 0, 0, s / 2};
+        for (int i = 0; i < 5; i++) {
+          const jxo_shape* sh = &jxo_shapes[vs[i]];
+          const int bx = bx0 + vx[i], by = by0 + vy[i];
+          int r = 0;
+          for (int iy = 0; iy < sh->cy; iy++)
+            for (int ix = 0; ix < sh->cx; ix++) {
+              const int v = raw[(size_t)(by + iy) * f->bxs + bx + ix];
+              r = v > r ? v : r;
+            }
+          e[i] = jxo_varblock(f, sh, xyb, bx * 8, by * 8, r, NULL, NULL, NULL);
+          if (f->proposals & 2) {
+            const float* h = homog + 3 * ((size_t)by * f->bxs + bx);
+            e[i] = jxo_hook_f(e[i], h[0], h[1], h[2]);
+          }
+        }
+        const float et = e[1] + e[2], ew = e[3] + e[4];
+        float best = cur;
+        int choice = 0;
+        if (!(e[0] >= best)) {
+          best = e[0];
+          choice = 1;
+        }
+        if (!(et >= best)) {
+          best = et;
+          choice = 2;
+        }
+        if (!(ew >= best)) {
+          best = ew;
+          choice = 3;
+        }
+        if (!choice) continue;
+        const int first = choice == 1 ? 0 : (choice == 2 ? 1 : 3);
+        const int nv = choice == 1 ? 1 : 2;
+        for (int i = first; i < first + nv; i++) {
+          const jxo_shape* sh = &jxo_shapes[vs[i]];
+          const int bx = bx0 + vx[i], by = by0 + vy[i];
+          for (int iy = 0; iy < sh->cy; iy++)
+            for (int ix = 0; ix < sh->cx; ix++) {
+              const size_t b = (size_t)(by + iy) * f->bxs + bx + ix;
+              acs[b] = (uint8_t)(sh->type | ((iy | ix) ? 0x80 : 0));
+              ent[b] = (iy | ix) ? 0.0f : e[i];
+            }
+        }
+      }
+  }
+}
