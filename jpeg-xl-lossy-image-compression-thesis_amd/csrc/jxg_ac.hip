@@ -93,7 +93,7 @@ __device__ __forceinline__ int block_ctx_of(int c, int acs) {
 }
 
 // AC tokens are < 64: |q| <= 32767 -> packed value <= 65534 -> hybrid token
-// <= 63; the non-zero count token is <= 63.  Device tables use 64 columns.
+// <= 63; the non-zero count (<= 4032) token is <= 47.  Device tables use 64 columns.
 constexpr int kAcTok = 64;
 // LDS bit buffer of ac_emit (groups whose exact size exceeds it fall back to
 // global atomics)
@@ -101,14 +101,40 @@ constexpr int kEmitLdsWords = 8192;  // 32 KiB = 262144 bits
 
 __device__ __forceinline__ int channel_of(int ci) { return ci == 0 ? 1 : (ci == 1 ? 0 : 2); }
 
-// non-zero counts of the group's blocks (written by the front kernel)
+// covered blocks (log2) of a raw strategy id: 0 for the 8x8 class
+__device__ __forceinline__ int log2_covered(int type) {
+  switch (type) {
+    case 6: case 7: return 1;                 // 16x8, 8x16
+    case 4: case 10: case 11: return type == 4 ? 2 : 3;  // 16x16; 32x16, 16x32
+    case 5: case 19: case 20: return type == 5 ? 4 : 5;  // 32x32; 64x32, 32x64
+    case 18: return 6;                        // 64x64
+    default: return 0;
+  }
+}
+__device__ __forceinline__ int covered_x(int type) {  // blocks across
+  switch (type) {
+    case 7: case 4: return 2;
+    case 10: return 2;
+    case 11: case 5: case 19: return 4;
+    case 20: case 18: return 8;
+    default: return 1;
+  }
+}
+
+// predicted-nz image of the group: per block, the varblock's non-zero count
+// scaled down by its covered blocks (the merge kernel already stores the
+// scaled value at covered non-first blocks)
 __device__ __forceinline__ void fill_nz(const AcArgs& a, const GroupGeom& G,
                                         uint8_t (*sNz)[1024]) {
   const size_t nb = (size_t)a.bxs * a.bys;
   for (int i = threadIdx.x; i < 3 * 1024; i += blockDim.x) {
     const int c = i >> 10, by = (i >> 5) & 31, bx = i & 31;
-    if (bx < G.gw && by < G.gh)
-      sNz[c][by * 32 + bx] = a.nz[c * nb + (size_t)(G.by0 + by) * a.bxs + G.bx0 + bx];
+    if (bx < G.gw && by < G.gh) {
+      const size_t gb = (size_t)(G.by0 + by) * a.bxs + G.bx0 + bx;
+      const int t = a.acs[gb];
+      const int l = (t & 0x80) ? 0 : log2_covered(t);
+      sNz[c][by * 32 + bx] = (uint8_t)((a.nz[c * nb + gb] + (1 << l) - 1) >> l);
+    }
   }
 }
 
@@ -135,13 +161,16 @@ __device__ __forceinline__ uint32_t block_excl_scan1024(uint32_t v, uint32_t* sW
   return before + incl - v;
 }
 
-// One thread per block of the group (<= 32 x 32 = 1024 blocks); its three
-// (block, channel) tasks Y, X, B are consecutive in the group's stream order.
+// One thread per block of the group (<= 32 x 32 = 1024 blocks); the thread
+// of a varblock's first block codes the whole varblock, its three
+// (varblock, channel) tasks Y, X, B consecutive in the group's stream order;
+// threads of covered blocks code nothing.
 struct BlockTask {
   bool valid;
   int bx, by;
   size_t gb;
   int acs;
+  int lcb, cx;  // log2 covered blocks, blocks across
 };
 __device__ __forceinline__ BlockTask block_task(const AcArgs& a, const GroupGeom& G) {
   BlockTask t;
@@ -151,16 +180,55 @@ __device__ __forceinline__ BlockTask block_task(const AcArgs& a, const GroupGeom
   t.by = t.valid ? b / G.gw : 0;
   t.gb = (size_t)(G.by0 + t.by) * a.bxs + G.bx0 + t.bx;
   t.acs = t.valid ? a.acs[t.gb] : 0;
+  if (t.acs & 0x80) t.valid = false;
+  t.lcb = log2_covered(t.acs);
+  t.cx = covered_x(t.acs);
   return t;
+}
+
+// Tokens of one merged varblock and channel: the non-zero count, then the
+// coefficients k = cb .. (natural order, LLF skipped) while non-zeros are
+// left; slices of 64 coefficients live in the covered blocks in raster order.
+template <class F>
+__device__ __forceinline__ void varblock_tokens(const AcArgs& a, const BlockTask& t, int nz,
+                                                int pred, int bctx, int c, F&& f) {
+  f(nz_bucket(pred) * kBlockCtx + bctx, (uint32_t)nz);
+  const int cb = 1 << t.lcb, size = cb * 64;
+  const int zoff = kBlockCtx * kNzBuckets + kZdCtx * bctx;
+  int prev = nz > size / 16 ? 0 : 1;
+  int left = nz;
+#pragma unroll 1
+  for (int sl = 0; sl < cb && left > 0; sl++) {
+    const size_t gbs = t.gb + (size_t)(sl / t.cx) * a.bxs + sl % t.cx;
+    uint32_t w[32];
+    load_coefs(a.ac + (gbs * 3 + c) * 64, w);
+#pragma unroll
+    for (int kk = 0; kk < 64; kk++) {
+      const int k = sl * 64 + kk;
+      if (left > 0 && k >= cb) {
+        const int32_t v = coef(w, kk);
+        f(zoff + (kNnzCtx[(left + cb - 1) >> t.lcb] + kFreqCtx[k >> t.lcb]) * 2 + prev,
+          pack_signed(v));
+        prev = v != 0;
+        left -= prev;
+      }
+    }
+  }
 }
 
 template <class F>
 __device__ __forceinline__ void block_channel_tokens(const AcArgs& a, const BlockTask& t,
                                                      uint8_t (*sNz)[1024], int c, F&& f) {
-  uint32_t w[32];
-  load_coefs(a.ac + (t.gb * 3 + c) * 64, w);
-  block_tokens(w, sNz[c][t.by * 32 + t.bx], predict_nz(sNz[c], t.bx, t.by),
-               block_ctx_of(c, t.acs), f);
+  const int pred = predict_nz(sNz[c], t.bx, t.by);
+  const int bctx = block_ctx_of(c, t.acs);
+  const int nz = a.nz[c * (size_t)a.bxs * a.bys + t.gb];
+  if (t.lcb == 0) {
+    uint32_t w[32];
+    load_coefs(a.ac + (t.gb * 3 + c) * 64, w);
+    block_tokens(w, nz, pred, bctx, f);
+  } else {
+    varblock_tokens(a, t, nz, pred, bctx, c, f);
+  }
 }
 
 __global__ __launch_bounds__(kAcThreads) void ac_hist_kernel(AcArgs a) {

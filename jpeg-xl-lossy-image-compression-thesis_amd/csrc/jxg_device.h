@@ -51,6 +51,27 @@ __device__ __forceinline__ void pixel_xyb(const float* lut, float cb, uint32_t r
   B = m2;
 }
 
+// thesis hook F (combined.diff:247-253): ret * 0.8 * avg_r in double, stored
+// to float
+__device__ __forceinline__ float hook_f(float ret, float rh, float rv, float rd) {
+  const float avg_r = (rh + rv + rd) / 3.0f;
+  return (float)((double)ret * 0.8 * (double)avg_r);
+}
+
+// DC quantization of one block == oracle jxo_quant_dc: Y first, B residual
+// against the dequantized Y (base correlation b = 1.0, x = 0.0) [ext]
+__device__ __forceinline__ void quant_dc3(const float* dc, const float* dc_mul,
+                                          const float* dc_step, int32_t* q) {
+  const float vy = dc[1] * dc_mul[1];
+  const int qy = vy >= 0.0f ? (int)(vy + 0.5f) : -(int)(-vy + 0.5f);
+  const float ydq = (float)qy * dc_step[1];
+  const float xv = dc[0] * dc_mul[0];
+  const float bv = (dc[2] - ydq) * dc_mul[2];
+  q[1] = qy;
+  q[0] = xv >= 0.0f ? (int)(xv + 0.5f) : -(int)(-xv + 0.5f);
+  q[2] = bv >= 0.0f ? (int)(bv + 0.5f) : -(int)(-bv + 0.5f);
+}
+
 // [ext] AC context model tables (libjxl ac_context.h)
 __device__ __constant__ static const uint8_t kStrategyOrder[27] = {
     0, 1, 1, 1, 2, 3, 4, 4, 5, 5, 6, 6, 1, 1, 1, 1, 1, 1, 7, 8, 8, 9, 10, 10, 11, 12, 12};

@@ -34,8 +34,8 @@ __device__ __forceinline__ int32_t lf_value(const LfArgs& a, const LfRow& r, con
     return a.dc[c * nb + (size_t)(L.by0 + y) * a.bxs + L.bx0 + x];
   }
   if (r.chan != 2) return 0;
-  const uint32_t bx = (uint32_t)x % L.bw, by = (uint32_t)x / L.bw;
-  const size_t b = (size_t)(L.by0 + by) * a.bxs + L.bx0 + bx;
+  // varblock x of the LF group (raster order of first blocks)
+  const size_t b = a.vb[(size_t)r.lg * 65536 + (uint32_t)x];
   return y == 0 ? (int32_t)a.acs[b] : (int32_t)a.qf[b];
 }
 
@@ -106,10 +106,15 @@ __device__ __forceinline__ void for_my_samples(const LfArgs& a, const LfChunk& c
       while (S.start[seg + 1] <= pos) seg++;
       const LfRow& r = S.row[seg];
       const LfGeom L = lf_geom(a, r.lg);
-      uint32_t u;
-      int leaf;
-      lf_residual(a, r, L, (int)(r.x0 + pos - S.start[seg]), u, leaf);
-      f(j, u, leaf);
+      const uint32_t x = r.x0 + pos - S.start[seg];
+      // the strategy/quant-field channel is laid out for bw*bh entries; only
+      // the first count (= varblocks) exist
+      if (!(r.stream == 1 && r.chan == 2) || x < a.vcount[r.lg]) {
+        uint32_t u;
+        int leaf;
+        lf_residual(a, r, L, (int)x, u, leaf);
+        f(j, u, leaf);
+      }
     }
     pos++;
   }

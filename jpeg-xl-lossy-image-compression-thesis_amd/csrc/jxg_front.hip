@@ -204,10 +204,6 @@ __device__ __forceinline__ uint8_t partition_of(float rh, float rv, float rd, fl
   return kDCT8;
 }
 
-__device__ __forceinline__ float hook_f(float ret, float rh, float rv, float rd) {
-  const float avg_r = (rh + rv + rd) / 3.0f;
-  return (float)((double)ret * 0.8 * (double)avg_r);
-}
 
 // ---------------------------------------------------------------------------
 // 1-D DCT-II (out[0] = mean), fixed even/odd butterfly; op sequence and hex
@@ -630,8 +626,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   if (r == 0) {
     a.acs[gb] = (uint8_t)bt;
     a.qf[gb] = (uint8_t)(raw - 1);
+    // estimate summed by the merge stage: the search's best, stored before
+    // the hook-P override (homogeneity-partitioning.diff:271 context)
+    if (a.ent) a.ent[gb] = beste;
   }
-  if (r < 3) a.nz[r * nb + gb] = (uint8_t)(best.nz >> (8 * r));
+  if (r < 3) a.nz[r * nb + gb] = (uint16_t)((best.nz >> (8 * r)) & 0xFFu);
   // ---- phase D: zigzag scatter through LDS, 16-byte stores ----
   const int bti = bt == kDCT8 ? 0 : (bt == kDCT4X4 ? 1 : (bt == kDCT4X8 ? 2 : 3));
   const uint2 zz2 = *reinterpret_cast<const uint2*>(sZz + bti * 64 + r * 8);

@@ -235,13 +235,137 @@ static void srgb_lut(float lut[256]) {
   }
 }
 
+// ---- merge-stage tables [ext quant_weights.cc / coeff_order.cc]; same
+// double-precision formulas as oracle/merge.c ----
+static const double kKindBands[kNumKinds][3][8] = {
+    {{7240.7734393502, -0.7, -0.7, -0.2, -0.2, -0.2, -0.5},
+     {1448.15468787004, -0.5, -0.5, -0.5, -0.2, -0.2, -0.2},
+     {506.854140754517, -1.4, -0.2, -0.5, -0.5, -1.5, -3.6}},
+    {{8996.8725711814115328, -1.3000777393353804, -0.49424529824571225, -0.439093774457103443,
+      -0.6350101832695744, -0.90177264050827612, -1.6162099239887414},
+     {3191.48366296844234752, -0.67424582104194355, -0.80745813428471001,
+      -0.44925837484843441, -0.35865440981033403, -0.31322389111877305, -0.37615025315725483},
+     {1157.50408145487200256, -2.0531423165804414, -1.4, -0.50687130033378396,
+      -0.42708730624733904, -1.4856834539296244, -4.9209142884401604}},
+    {{13844.97076442300573, -0.97113799999999995, -0.658, -0.42026, -0.22712, -0.2206, -0.226,
+      -0.6},
+     {4798.964084220744293, -0.61125308982767057, -0.83770786552491361, -0.79014862079498627,
+      -0.2692727459704829, -0.38272769465388551, -0.22924222653091453, -0.20719098826199578},
+     {1807.236946760964614, -1.2, -1.2, -0.7, -0.7, -0.7, -0.4, -0.5}},
+    {{15718.40830982518931456, -1.025, -0.98, -0.9012, -0.4, -0.48819395464, -0.421064, -0.27},
+     {7305.7636810695983104, -0.8041958212306401, -0.7633036457487539, -0.55660379990111464,
+      -0.49785304658857626, -0.43699592683512467, -0.40180866526242109, -0.27321683125358037},
+     {3803.53173721215041536, -3.060733579805728, -2.0413270132490346, -2.0235650159727417,
+      -0.5495389509954993, -0.4, -0.4, -0.3}},
+    {{0.65 * 23629.073922049845, -1.025, -0.78, -0.65012, -0.19041574084286472, -0.20819395464,
+      -0.421064, -0.32733845535848671},
+     {0.65 * 8611.3238710010046, -0.3041958212306401, -0.3633036457487539, -0.35660379990111464,
+      -0.3443074455424403, -0.33699592683512467, -0.30180866526242109, -0.27321683125358037},
+     {0.65 * 4492.2486445538634, -1.2, -1.2, -0.8, -0.7, -0.7, -0.4, -0.5}},
+    {{0.9 * 26629.073922049845, -1.025, -0.78, -0.65012, -0.19041574084286472, -0.20819395464,
+      -0.421064, -0.32733845535848671},
+     {0.9 * 9311.3238710010046, -0.3041958212306401, -0.3633036457487539, -0.35660379990111464,
+      -0.3443074455424403, -0.33699592683512467, -0.30180866526242109, -0.27321683125358037},
+     {0.9 * 4992.2486445538634, -1.2, -1.2, -0.8, -0.7, -0.7, -0.4, -0.5}},
+};
+static const int kKindNumBands[kNumKinds] = {7, 7, 8, 8, 8, 8};
+static const int kKindDims[kNumKinds][2] = {{8, 16}, {16, 16}, {16, 32},
+                                           {32, 32}, {32, 64}, {64, 64}};
+
+struct MergeTables {
+  std::vector<float> wk, iwy;
+  std::vector<uint16_t> nat;
+  float lee_c[7][32], lee_s[7][64], llf_p[4][8], llf_ib[4][8][8];
+};
+static MergeTables build_merge_tables() {
+  MergeTables T;
+  const int tot = kKindOff[kNumKinds];
+  T.wk.assign((size_t)3 * tot, 0.0f);
+  T.iwy.assign(tot, 0.0f);
+  T.nat.assign(tot, 0);
+  for (int k = 0; k < kNumKinds; k++) {
+    const int rows = kKindDims[k][0], cols = kKindDims[k][1], nb = kKindNumBands[k];
+    for (int c = 0; c < 3; c++) {
+      double bands[8];
+      bands[0] = kKindBands[k][c][0];
+      for (int i = 1; i < nb; i++) {
+        const double v = kKindBands[k][c][i];
+        bands[i] = bands[i - 1] * (v > 0 ? 1.0 + v : 1.0 / (1.0 - v));
+      }
+      const double scale = (nb - 1) / (1.4142135623730951 + 1e-6);
+      const double rc = scale / (cols - 1), rr = scale / (rows - 1);
+      for (int y = 0; y < rows; y++)
+        for (int x = 0; x < cols; x++) {
+          const double dx = x * rc, dy = y * rr;
+          const double pos = std::sqrt(dx * dx + dy * dy);
+          int idx = (int)pos;
+          if (idx > nb - 2) idx = nb - 2;
+          const double frac = pos - idx;
+          const double a = bands[idx], b = bands[idx + 1];
+          T.wk[(size_t)c * tot + kKindOff[k] + y * cols + x] = (float)(a * std::pow(b / a, frac));
+        }
+    }
+    for (int i = 0; i < rows * cols; i++) T.iwy[kKindOff[k] + i] = 1.0f / T.wk[(size_t)tot + kKindOff[k] + i];
+    // natural order: LLF raster, then the y-scaled zigzag over cols x cols
+    uint16_t* nat = &T.nat[kKindOff[k]];
+    const int cs = rows / 8, cl = cols / 8, xf = cols / rows;
+    int cur = 0;
+    for (int y = 0; y < cs; y++)
+      for (int x = 0; x < cl; x++) nat[y * cols + x] = (uint16_t)cur++;
+    auto visit = [&](int x, int y, bool skip_llf) {
+      if (y % xf) return;
+      y /= xf;
+      if (skip_llf && x < cl && y < cs) return;
+      nat[y * cols + x] = (uint16_t)cur++;
+    };
+    for (int i = 0; i < cols; i++)
+      for (int j = 0; j <= i; j++) {
+        const bool odd = i & 1;
+        visit(odd ? i - j : j, odd ? j : i - j, true);
+      }
+    for (int ip = cols - 1; ip > 0; ip--) {
+      const int i = ip - 1;
+      for (int j = 0; j <= i; j++) {
+        const int x = cols - 1 - (i - j), y = cols - 1 - j;
+        const bool odd = i & 1;
+        visit(odd ? y : x, odd ? x : y, false);
+      }
+    }
+  }
+  const double pi = 3.14159265358979323846;
+  std::memset(T.lee_c, 0, sizeof(T.lee_c));
+  std::memset(T.lee_s, 0, sizeof(T.lee_s));
+  for (int l = 0; l < 7; l++) {
+    const int N = 1 << l;
+    for (int i = 0; i < N / 2; i++)
+      T.lee_c[l][i] = (float)(1.0 / (2.0 * std::cos(pi * (2 * i + 1) / (2.0 * N))));
+    for (int k = 0; k < N; k++) T.lee_s[l][k] = (float)(k ? std::sqrt(2.0) / N : 1.0 / N);
+  }
+  std::memset(T.llf_p, 0, sizeof(T.llf_p));
+  std::memset(T.llf_ib, 0, sizeof(T.llf_ib));
+  for (int l = 0; l < 4; l++) {
+    const int M = 1 << l;
+    for (int k = 0; k < M; k++)
+      T.llf_p[l][k] = (float)(std::cos(pi * k / (16.0 * M)) * std::cos(pi * k / (8.0 * M)) *
+                              std::cos(pi * k / (4.0 * M)));
+    for (int n = 0; n < M; n++)
+      for (int k = 0; k < M; k++)
+        T.llf_ib[l][n][k] =
+            (float)(k ? std::sqrt(2.0) * std::cos(pi * (2 * n + 1) * k / (2.0 * M)) : 1.0);
+  }
+  return T;
+}
+
 struct Ctx {
   jxg_params params{};
   hipStream_t stream = nullptr;
   hipEvent_t ev[6] = {};
   bool constants_ready = false;
   // device
-  DevBuf<uint8_t> rgb, acs, qf, nz;
+  DevBuf<uint8_t> rgb, acs, qf;
+  DevBuf<uint16_t> nz, mnat;
+  DevBuf<float> ent, mwk, miwy;
+  DevBuf<uint32_t> vb, vcount;
   DevBuf<int32_t> dc;
   DevBuf<int16_t> ac;
   DevBuf<float> homog, xyb, r3;
@@ -253,7 +377,7 @@ struct Ctx {
   DevBuf<LfChunk> lfchunks;
   DevBuf<ConcatPiece> pieces;
   // host
-  PinBuf<uint32_t> h_hist_ac, h_bound, h_ntok, h_lfhist, h_sbound, h_gbits, h_sbits;
+  PinBuf<uint32_t> h_hist_ac, h_bound, h_ntok, h_lfhist, h_sbound, h_gbits, h_sbits, h_vcount;
   // LF row segments cached per frame size
   uint32_t rows_w = 0, rows_h = 0;
   std::vector<LfRow> rows_h_cache;
@@ -265,7 +389,6 @@ struct Ctx {
   BitWriter cm_bits;
   std::vector<uint8_t> m_acs, m_qf;
   std::vector<int32_t> m_dc, m_ac;
-  std::vector<int16_t> m_ac16;
   std::vector<uint32_t> m_ntok;
   std::vector<float> m_homog;
   jxg_stats stats{};
@@ -281,6 +404,16 @@ static jxg_status init_constants(Ctx* c) {
   uint8_t tab[kAcCtx];
   for (int i = 0; i < kAcCtx; i++) tab[i] = (uint8_t)ac_cluster(i);
   set_cluster_table(tab, c->stream);
+  static const MergeTables mt = build_merge_tables();
+  set_merge_constants(lut, &mt.lee_c[0][0], &mt.lee_s[0][0], &mt.llf_p[0][0], &mt.llf_ib[0][0][0],
+                      c->stream);
+  JXG_HIP(c->mwk.ensure(mt.wk.size()));
+  JXG_HIP(c->miwy.ensure(mt.iwy.size()));
+  JXG_HIP(c->mnat.ensure(mt.nat.size()));
+  JXG_HIP(hipMemcpyAsync(c->mwk.p, mt.wk.data(), mt.wk.size() * 4, hipMemcpyHostToDevice, c->stream));
+  JXG_HIP(hipMemcpyAsync(c->miwy.p, mt.iwy.data(), mt.iwy.size() * 4, hipMemcpyHostToDevice, c->stream));
+  JXG_HIP(hipMemcpyAsync(c->mnat.p, mt.nat.data(), mt.nat.size() * 2, hipMemcpyHostToDevice, c->stream));
+  JXG_HIP(hipStreamSynchronize(c->stream));
   JXG_HIP(hipGetLastError());
   c->constants_ready = true;
   return JXG_OK;
@@ -344,6 +477,11 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   JXG_HIP(c->dc.ensure(nb * 3));
   JXG_HIP(c->ac.ensure(nb * 192));
   if (homog) JXG_HIP(c->homog.ensure(nb * 3));
+  const int max_s = P.effort >= 6 ? 8 : (P.effort >= 5 ? 4 : 0);  // merge levels
+  if (max_s) JXG_HIP(c->ent.ensure(nb));
+  JXG_HIP(c->vb.ensure((size_t)f.nlf * 65536));
+  JXG_HIP(c->vcount.ensure(f.nlf));
+  JXG_HIP(c->h_vcount.ensure(f.nlf));
   JXG_HIP(c->hist_ac.ensure(kMaxClusters * kAlpha));
   JXG_HIP(c->codes_ac.ensure(kMaxClusters * kAlpha));
   JXG_HIP(c->bound.ensure(f.ngroups));
@@ -416,7 +554,41 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   fa.ac = c->ac.p;
   fa.nz = c->nz.p;
   fa.homog = homog ? c->homog.p : nullptr;
+  fa.ent = max_s ? c->ent.p : nullptr;
   launch_front(fa, f.tiles_x, f.tiles_y, s);
+  JXG_HIP(hipGetLastError());
+  if (max_s) {
+    MergeArgs ma{};
+    ma.rgb = d_rgb;
+    ma.w = w;
+    ma.h = h;
+    ma.stride = stride;
+    ma.bxs = f.bxs;
+    ma.bys = f.bys;
+    ma.xp = f.xp;
+    ma.yp = f.yp;
+    ma.proposals = P.proposals;
+    ma.max_s = max_s;
+    ma.G = f.G;
+    for (int i = 0; i < 3; i++) {
+      ma.dc_mul[i] = f.dc_mul[i];
+      ma.dc_step[i] = f.dc_step[i];
+    }
+    ma.ent = c->ent.p;
+    ma.homog = homog ? c->homog.p : nullptr;
+    ma.acs = c->acs.p;
+    ma.qf = c->qf.p;
+    ma.dc = c->dc.p;
+    ma.ac = c->ac.p;
+    ma.nz = c->nz.p;
+    ma.wk = c->mwk.p;
+    ma.iwy = c->miwy.p;
+    ma.nat = c->mnat.p;
+    launch_merge(ma, f.tiles_x, f.tiles_y, s);
+    JXG_HIP(hipGetLastError());
+  }
+  VbArgs va{c->acs.p, f.bxs, f.bys, f.lfxs, c->vb.p, c->vcount.p};
+  launch_vb_list(va, f.nlf, s);
   JXG_HIP(hipGetLastError());
   JXG_HIP(hipEventRecord(c->ev[1], s));
 
@@ -444,6 +616,8 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   la.dc = c->dc.p;
   la.acs = c->acs.p;
   la.qf = c->qf.p;
+  la.vb = c->vb.p;
+  la.vcount = c->vcount.p;
   la.bxs = f.bxs;
   la.bys = f.bys;
   la.lfxs = f.lfxs;
@@ -462,6 +636,7 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   JXG_HIP(hipMemcpyAsync(c->h_ntok.p, c->ntok.p, f.ngroups * 12, hipMemcpyDeviceToHost, s));
   JXG_HIP(hipMemcpyAsync(c->h_lfhist.p, c->lfhist.p, (size_t)nstreams * 4 * kAlpha * 4, hipMemcpyDeviceToHost, s));
   JXG_HIP(hipMemcpyAsync(c->h_sbound.p, c->sbound.p, nstreams * 4, hipMemcpyDeviceToHost, s));
+  JXG_HIP(hipMemcpyAsync(c->h_vcount.p, c->vcount.p, f.nlf * 4, hipMemcpyDeviceToHost, s));
   JXG_HIP(hipEventRecord(c->ev[2], s));
   JXG_HIP(hipStreamSynchronize(s));
 
@@ -507,7 +682,7 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
         preA[lg].put(2, 0);  // extra_precision
         write_modular_prelude(preA[lg], kDcTree, 5, 3, lc);
       } else {
-        preB[lg].put(ceil_log2(bw * bh), bw * bh - 1);  // varblock count - 1
+        preB[lg].put(ceil_log2(bw * bh), c->h_vcount.p[lg] - 1);  // varblock count - 1
         write_modular_prelude(preB[lg], kMetaTree, 7, 4, lc);
       }
     }
@@ -650,15 +825,17 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
     return JXG_ERR_HIP;
   }
   JXG_HIP(hipEventRecord(c->ev[4], s));
+  std::vector<int16_t> m_ac16_tmp;
   if (P.flags & JXG_FLAG_KEEP_MAPS) {
     c->m_acs.resize(nb);
     c->m_qf.resize(nb);
     c->m_dc.resize(nb * 3);
-    c->m_ac16.resize(nb * 192);
+    c->m_ac.resize(nb * 192);
     JXG_HIP(hipMemcpyAsync(c->m_acs.data(), c->acs.p, nb, hipMemcpyDeviceToHost, s));
     JXG_HIP(hipMemcpyAsync(c->m_qf.data(), c->qf.p, nb, hipMemcpyDeviceToHost, s));
     JXG_HIP(hipMemcpyAsync(c->m_dc.data(), c->dc.p, nb * 12, hipMemcpyDeviceToHost, s));
-    JXG_HIP(hipMemcpyAsync(c->m_ac16.data(), c->ac.p, nb * 192 * 2, hipMemcpyDeviceToHost, s));
+    m_ac16_tmp.resize(nb * 192);
+    JXG_HIP(hipMemcpyAsync(m_ac16_tmp.data(), c->ac.p, nb * 192 * 2, hipMemcpyDeviceToHost, s));
     if (homog) {
       c->m_homog.resize(nb * 3);
       JXG_HIP(hipMemcpyAsync(c->m_homog.data(), c->homog.p, nb * 12, hipMemcpyDeviceToHost, s));
@@ -686,11 +863,8 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   c->m_ntok.assign(c->h_ntok.p, c->h_ntok.p + f.ngroups * 3);
   S.ac_tokens = c->m_ntok.data();
   if (P.flags & JXG_FLAG_KEEP_MAPS) {
-    // AC back to natural (raster) order for the caller
-    static const Order64 ord = make_order64();
-    c->m_ac.assign(nb * 192, 0);
-    for (size_t b = 0; b < nb * 3; b++)
-      for (int j = 0; j < 64; j++) c->m_ac[b * 64 + ord.v[j]] = c->m_ac16[b * 64 + j];
+    // coefficients in natural-order slices, widened to int32 for the caller
+    for (size_t i = 0; i < nb * 192; i++) c->m_ac[i] = m_ac16_tmp[i];
     S.ac_strategy = c->m_acs.data();
     S.quant_field = c->m_qf.data();
     S.dc = c->m_dc.data();

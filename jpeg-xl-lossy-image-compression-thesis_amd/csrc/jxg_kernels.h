@@ -23,8 +23,41 @@ struct FrontArgs {
   uint8_t* qf;    // [nb] raw-1
   int32_t* dc;    // [3][nb] X,Y,B
   int16_t* ac;    // [nb][3 X,Y,B][64 zigzag]
-  uint8_t* nz;    // [3][nb] non-zero AC count per block and channel
+  uint16_t* nz;   // [3][nb] non-zero AC count per block and channel
   float* homog;   // [nb][3] or null
+  float* ent;     // [nb] best 8x8 estimate (merge stage input) or null
+};
+
+// merge stage (jxg_merge.hip): tables of the merged varblock kinds
+constexpr int kNumKinds = 6;
+constexpr int kKindOff[kNumKinds + 1] = {0, 128, 384, 896, 1920, 3968, 8064};
+struct MergeArgs {
+  const uint8_t* rgb;
+  uint32_t w, h;
+  size_t stride;
+  uint32_t bxs, bys, xp, yp;
+  uint32_t proposals;
+  int max_s;      // largest merged square in blocks (2, 4 or 8); 0 = no merges
+  uint32_t G;
+  float dc_mul[3], dc_step[3];
+  const float* ent;     // [nb] per-block estimate (front kernel)
+  const float* homog;   // [nb][3] (hook F) or null
+  uint8_t* acs;         // in/out: raw id, bit 7 on covered non-first blocks
+  uint8_t* qf;          // in/out: raw - 1
+  int32_t* dc;          // out (merged varblocks)
+  int16_t* ac;          // out (merged varblocks), natural order slices
+  uint16_t* nz;         // out (merged varblocks): full count at the first block,
+                        //   (nz + cb - 1) >> log2 cb at covered blocks
+  const float* wk;      // [3][kKindOff[6]] weights per kind, stored raster
+  const float* iwy;     // [kKindOff[6]] 1 / Y weight
+  const uint16_t* nat;  // [kKindOff[6]] stored raster -> natural position
+};
+// per-LF-group varblock lists (AC metadata channel)
+struct VbArgs {
+  const uint8_t* acs;
+  uint32_t bxs, bys, lfxs;
+  uint32_t* vb;     // [nlf][65536] block index (frame raster) of each varblock
+  uint32_t* count;  // [nlf]
 };
 
 struct HomogArgs {
@@ -41,7 +74,7 @@ struct HomogArgs {
 struct AcArgs {
   const uint8_t* acs;
   const int16_t* ac;  // [nb][3][64 zigzag]
-  const uint8_t* nz;  // [3][nb] non-zero counts (front kernel)
+  const uint16_t* nz;  // [3][nb] non-zero counts (front / merge kernels)
   uint32_t bxs, bys, gxs;
   uint32_t* hist;        // [kMaxClusters][kAlpha]      (hist pass)
   uint32_t* bound;       // [ngroups] bit upper bound   (hist pass)
@@ -77,6 +110,8 @@ struct LfArgs {
   const int32_t* dc;  // [3][nb]
   const uint8_t* acs;
   const uint8_t* qf;
+  const uint32_t* vb;     // [nlf][65536] varblock -> block index
+  const uint32_t* vcount; // [nlf] varblocks per LF group
   uint32_t bxs, bys, lfxs;
   uint32_t* hist;         // [nstreams][4 leaves][kAlpha]  (hist)
   uint32_t* sbound;       // [nstreams] (hist)
@@ -107,6 +142,11 @@ void launch_lf_bits(const LfArgs& a, uint32_t nchunks, hipStream_t s);
 void launch_lf_scan(const LfArgs& a, uint32_t nstreams, hipStream_t s);
 void launch_lf_emit(const LfArgs& a, uint32_t nchunks, hipStream_t s);
 void set_cluster_table(const uint8_t* tab, hipStream_t s);
+void set_merge_constants(const float lut[256], const float* lee_c /*[7][32]*/,
+                         const float* lee_s /*[7][64]*/, const float* llf_p /*[4][8]*/,
+                         const float* llf_ib /*[4][8][8]*/, hipStream_t s);
+void launch_merge(const MergeArgs& a, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s);
+void launch_vb_list(const VbArgs& a, uint32_t nlf, hipStream_t s);
 void launch_concat(const ConcatPiece* pieces, uint32_t npieces, uint64_t max_words,
                    const uint32_t* scratch, const uint32_t* chunks, uint32_t* out,
                    hipStream_t s);

@@ -85,3 +85,51 @@ def test_4k_matches_oracle(jxg_mod, oracle):
         got = enc.encode(img)
     ref = oracle.encode(img, 1.0, 7, 0)
     assert got == ref.bytes
+
+
+def smooth_rgb8(w, h, seed):
+    """Smooth content (so the merge stage picks 16x8 ... 64x64 varblocks) with a
+    few noisy and flat 64x64 tiles (so 8x8-class blocks stay beside them)."""
+    rng = np.random.default_rng(seed)
+    y, x = np.mgrid[0:h, 0:w].astype(np.float64)
+    fx, fy = rng.uniform(5, 40, 3), rng.uniform(5, 40, 3)
+    img = np.stack([128 + 90 * np.sin(x / fx[c] + y / fy[c] + c) for c in range(3)], -1)
+    for ty in range(0, h, 64):
+        for tx in range(0, w, 64):
+            k = rng.integers(0, 6)
+            if k == 0:
+                img[ty:ty + 64, tx:tx + 64] += rng.normal(0, 25, img[ty:ty + 64, tx:tx + 64].shape)
+            elif k == 1:
+                img[ty:ty + 64, tx:tx + 64] = rng.uniform(0, 255, 3)
+    return np.clip(img, 0, 255).astype(np.uint8)
+
+
+# (width, height, distance, effort, proposals): merge levels 16/32 (e5) and 64
+# (e>=6), hooks on merge candidates, partial tiles at the right/bottom edges
+MERGE_CASES = [
+    (256, 256, 1.0, 7, 0),
+    (264, 200, 1.0, 5, 3),
+    (520, 136, 2.0, 6, 2),
+    (136, 520, 0.5, 7, 1),
+    (333, 333, 3.0, 7, 3),
+    (1000, 700, 1.0, 7, 0),
+]
+
+
+@pytest.mark.parametrize("w,h,d,e,p", MERGE_CASES)
+def test_merged_varblocks_match_oracle(jxg_mod, oracle, decoder, w, h, d, e, p):
+    img = smooth_rgb8(w, h, w * 31 + h)
+    with jxg_mod.Encoder(distance=d, effort=e, proposals=p, flags=jxg_mod.FLAG_KEEP_MAPS) as enc:
+        got = enc.encode(img)
+        st = enc.stats()
+    ref = oracle.encode(img, d, e, p)
+    assert (ref.acs & 0x80).any(), "case does not exercise merged varblocks"
+    assert np.array_equal(st["acs"], ref.acs)
+    assert np.array_equal(st["qf"], ref.qf)
+    assert np.array_equal(st["dc"], ref.dc)
+    assert np.array_equal(st["ac"], ref.ac)
+    assert np.array_equal(st["ac_tokens"], ref.ac_tokens)
+    assert got == ref.bytes
+    if w * h <= 300 * 300:
+        dec = decoder.decode(got)
+        assert np.array_equal(dec.acs, ref.acs)
