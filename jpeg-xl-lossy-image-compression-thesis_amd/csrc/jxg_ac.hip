@@ -1,18 +1,24 @@
 // jxg_ac.hip -- pass-group AC token statistics and bit emission on gfx950.
 //
-// One 1024-thread workgroup per 256x256-pixel pass group: thread = 8x8 block,
-// its (block, channel) tasks Y, X, B in stream order.  A task's 64 int16 coefficients
-// (128 B) are loaded with 8 x 16-byte loads into 32 VGPRs and the token walk
-// runs on registers (fully unrolled, wave-uniform early exit every 8
-// coefficients), so there are no dependent global loads in the walk.
+// One 1024-thread workgroup per 256x256-pixel pass group: thread = 8x8 block
+// = one 64-coefficient slice of a varblock (an 8x8-class block is a varblock
+// of one slice; a merged varblock covering cb blocks keeps slice i of its
+// natural-order coefficients in covered block i, raster order).  A task
+// (slice, channel) loads its 64 int16 coefficients (128 B) with 8 x 16-byte
+// loads into 32 VGPRs and walks them on registers (fully unrolled,
+// wave-uniform early exit every 8 coefficients).  A slice's walk state at its
+// first coefficient -- non-zeros left and the previous-coefficient flag --
+// follows from the per-slice non-zero counts of the earlier slices (LDS), so
+// every slice of a 64x64 varblock is walked in parallel.
 //   ac_hist : non-zero counts -> predicted-nz + zero-density contexts ->
 //             clustered histograms (LDS, one global atomic per non-empty bin),
 //             exact per-group token counts, per-group bit upper bound.
-//   ac_emit : same walk with the prefix codes (LDS table): per-block bit
-//             lengths -> workgroup exclusive scan (stream order: blocks
-//             raster, channels Y, X, B) -> every block writes its bits into an
-//             LDS bit buffer (ds_or), copied out with plain 4-byte stores
-//             (global atomics only for groups larger than the buffer).
+//   ac_emit : same walk with the prefix codes (LDS table): per-task bit
+//             lengths -> workgroup exclusive scan over varblocks (stream
+//             order: varblocks by first block raster, channels Y, X, B,
+//             slices) -> every task writes its bits into an LDS bit buffer
+//             (ds_or), copied out with plain 4-byte stores (global atomics
+//             only for groups larger than the buffer).
 // Token order / contexts are those of oracle/encode.c group_tokens, [ext]
 // libjxl dec_group DecodeACVarBlock.
 #include "jxg_device.h"
@@ -53,7 +59,19 @@ __device__ __forceinline__ int32_t coef(const uint32_t* w, int k) {
   return (int32_t)(int16_t)(w[k >> 1] >> ((k & 1) * 16));
 }
 
-// Tokens of one (block, channel): f(ctx, value) in bitstream order.
+// kFreqCtx / kNnzCtx as arithmetic (the varblock walk indexes them at run
+// time; table loads would be hoisted out of the unrolled walk)
+__device__ __forceinline__ int freq_ctx(int k) {
+  return k < 16 ? max(k - 1, 0) : (k < 32 ? 15 + ((k - 16) >> 1) : 23 + ((k - 32) >> 2));
+}
+__device__ __forceinline__ int nnz_ctx(int n) {
+  return n < 2 ? 0 : n < 3 ? 31 : n < 5 ? 62 : n < 9 ? 93 : n < 13 ? 123 : n < 21 ? 152
+       : n < 33 ? 180 : 206;
+}
+
+// Walk of one 8x8-class block and channel (libjxl DecodeACVarBlock with one
+// covered block): f(ctx, value) in bitstream order; contexts fold to
+// compile-time table entries.
 template <class F>
 __device__ __forceinline__ void block_tokens(const uint32_t* w, int nz, int pred, int bctx,
                                              F&& f) {
@@ -82,6 +100,36 @@ __device__ __forceinline__ void block_tokens(const uint32_t* w, int nz, int pred
   }
 }
 
+// Walk of one slice (64 coefficients at q) of a merged varblock: sl = slice
+// index, lcb = log2 covered blocks, left / prev = walk state at the slice's
+// first coefficient; slice 0 also emits the non-zero count token.  Chunks of
+// 8 coefficients are loaded one 16-byte load at a time inside a run-time
+// loop (no register-resident slice: keeps the 8x8 walk's registers).
+template <class F>
+__device__ __forceinline__ void varblock_slice_tokens(const int16_t* q, int sl, int lcb, int nz,
+                                                      int left, int prev, int pred, int bctx,
+                                                      F&& f) {
+  if (sl == 0) f(nz_bucket(pred) * kBlockCtx + bctx, (uint32_t)nz);
+  const int zoff = kBlockCtx * kNzBuckets + kZdCtx * bctx;
+  const int cb = 1 << lcb;
+#pragma unroll 1
+  for (int ch = 0; ch < 8 && left > 0; ch++) {
+    const uint4 t = reinterpret_cast<const uint4*>(q)[ch];
+    const uint32_t w[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+    for (int kk = 0; kk < 8; kk++) {
+      const int k = sl * 64 + ch * 8 + kk;
+      if (left > 0 && k >= cb) {
+        const int32_t v = coef(w, kk);
+        f(zoff + (nnz_ctx((left + cb - 1) >> lcb) + freq_ctx(k >> lcb)) * 2 + prev,
+          pack_signed(v));
+        prev = v != 0;
+        left -= prev;
+      }
+    }
+  }
+}
+
 __device__ __forceinline__ int predict_nz(const uint8_t* nzc, int bx, int by) {
   if (bx == 0) return by == 0 ? 32 : nzc[(by - 1) * 32 + bx];
   if (by == 0) return nzc[by * 32 + bx - 1];
@@ -101,40 +149,110 @@ constexpr int kEmitLdsWords = 8192;  // 32 KiB = 262144 bits
 
 __device__ __forceinline__ int channel_of(int ci) { return ci == 0 ? 1 : (ci == 1 ? 0 : 2); }
 
-// covered blocks (log2) of a raw strategy id: 0 for the 8x8 class
-__device__ __forceinline__ int log2_covered(int type) {
+// covered blocks of a raw strategy id: log2 and blocks across / down
+__device__ __forceinline__ void varblock_dims(int type, int& lcb, int& cx, int& cy) {
   switch (type) {
-    case 6: case 7: return 1;                 // 16x8, 8x16
-    case 4: case 10: case 11: return type == 4 ? 2 : 3;  // 16x16; 32x16, 16x32
-    case 5: case 19: case 20: return type == 5 ? 4 : 5;  // 32x32; 64x32, 32x64
-    case 18: return 6;                        // 64x64
-    default: return 0;
-  }
-}
-__device__ __forceinline__ int covered_x(int type) {  // blocks across
-  switch (type) {
-    case 7: case 4: return 2;
-    case 10: return 2;
-    case 11: case 5: case 19: return 4;
-    case 20: case 18: return 8;
-    default: return 1;
+    case 6: lcb = 1, cx = 1, cy = 2; break;   // 16x8
+    case 7: lcb = 1, cx = 2, cy = 1; break;   // 8x16
+    case 4: lcb = 2, cx = 2, cy = 2; break;   // 16x16
+    case 10: lcb = 3, cx = 2, cy = 4; break;  // 32x16
+    case 11: lcb = 3, cx = 4, cy = 2; break;  // 16x32
+    case 5: lcb = 4, cx = 4, cy = 4; break;   // 32x32
+    case 19: lcb = 5, cx = 4, cy = 8; break;  // 64x32
+    case 20: lcb = 5, cx = 8, cy = 4; break;  // 32x64
+    case 18: lcb = 6, cx = 8, cy = 8; break;  // 64x64
+    default: lcb = 0, cx = 1, cy = 1; break;  // 8x8 class
   }
 }
 
-// predicted-nz image of the group: per block, the varblock's non-zero count
-// scaled down by its covered blocks (the merge kernel already stores the
-// scaled value at covered non-first blocks)
-__device__ __forceinline__ void fill_nz(const AcArgs& a, const GroupGeom& G,
-                                        uint8_t (*sNz)[1024]) {
+// One thread per block of the group: slice `sl` of the varblock whose first
+// block is (obx, oby) (group-local; varblocks are aligned to their size).
+struct SliceTask {
+  bool valid;
+  int bx, by, obx, oby, sl, lcb, cx, type;
+  size_t gb, ogb;
+};
+__device__ __forceinline__ SliceTask slice_task(const AcArgs& a, const GroupGeom& G) {
+  SliceTask t;
+  const int b = threadIdx.x;
+  t.valid = b < G.gw * G.gh;
+  t.bx = t.valid ? b % G.gw : 0;
+  t.by = t.valid ? b / G.gw : 0;
+  t.gb = (size_t)(G.by0 + t.by) * a.bxs + G.bx0 + t.bx;
+  t.type = t.valid ? (a.acs[t.gb] & 0x7F) : 0;
+  int cy;
+  varblock_dims(t.type, t.lcb, t.cx, cy);
+  t.obx = t.bx & ~(t.cx - 1);
+  t.oby = t.by & ~(cy - 1);
+  t.sl = (t.by - t.oby) * t.cx + (t.bx - t.obx);
+  t.ogb = (size_t)(G.by0 + t.oby) * a.bxs + G.bx0 + t.obx;
+  return t;
+}
+__device__ __forceinline__ int block_of_slice(const SliceTask& t, int j) {
+  return (t.oby + j / t.cx) * 32 + t.obx + j % t.cx;
+}
+
+struct AcLds {
+  uint8_t nz[3][1024];   // predicted-nz image (scaled per covered block)
+  uint8_t snz[3][1024];  // non-zeros of each slice (positions >= cb)
+  uint8_t last[3][1024]; // last coefficient of the slice != 0
+};
+
+// predicted-nz image and per-slice non-zero counts of the group
+__device__ __forceinline__ void fill_slices(const AcArgs& a, const GroupGeom& G,
+                                            const SliceTask& t, AcLds& L) {
   const size_t nb = (size_t)a.bxs * a.bys;
   for (int i = threadIdx.x; i < 3 * 1024; i += blockDim.x) {
     const int c = i >> 10, by = (i >> 5) & 31, bx = i & 31;
     if (bx < G.gw && by < G.gh) {
       const size_t gb = (size_t)(G.by0 + by) * a.bxs + G.bx0 + bx;
-      const int t = a.acs[gb];
-      const int l = (t & 0x80) ? 0 : log2_covered(t);
-      sNz[c][by * 32 + bx] = (uint8_t)((a.nz[c * nb + gb] + (1 << l) - 1) >> l);
+      const int acs = a.acs[gb];
+      int l, cx, cy;
+      varblock_dims(acs, l, cx, cy);  // covered blocks (flag set) hold scaled counts
+      L.nz[c][by * 32 + bx] = (uint8_t)((a.nz[c * nb + gb] + (1 << l) - 1) >> l);
     }
+  }
+  if (t.valid && t.lcb > 0) {
+    const int cb = 1 << t.lcb;
+#pragma unroll 1
+    for (int c = 0; c < 3; c++) {
+      uint32_t w[32];
+      load_coefs(a.ac + (t.gb * 3 + c) * 64, w);
+      int n = 0;
+#pragma unroll
+      for (int kk = 0; kk < 64; kk++) n += (t.sl * 64 + kk >= cb) && coef(w, kk) != 0;
+      L.snz[c][t.by * 32 + t.bx] = (uint8_t)n;
+      L.last[c][t.by * 32 + t.bx] = coef(w, 63) != 0;
+    }
+  }
+}
+
+// walk state of task (t, c) at its first coefficient; nz = varblock count
+__device__ __forceinline__ void slice_state(const AcArgs& a, const SliceTask& t, const AcLds& L,
+                                            int c, int& nz, int& left, int& prev) {
+  nz = a.nz[c * (size_t)a.bxs * a.bys + t.ogb];
+  const int cb = 1 << t.lcb;
+  left = nz;
+  prev = nz > cb * 4 ? 0 : 1;  // nz > size / 16
+  if (t.sl > 0) {
+    for (int j = 0; j < t.sl; j++) left -= L.snz[c][block_of_slice(t, j)];
+    if (t.sl * 64 - 1 >= cb) prev = L.last[c][block_of_slice(t, t.sl - 1)];
+  }
+}
+
+template <class F>
+__device__ __forceinline__ void task_tokens(const AcArgs& a, const SliceTask& t, const AcLds& L,
+                                            int c, F&& f) {
+  int nz, left, prev;
+  slice_state(a, t, L, c, nz, left, prev);
+  const int pred = t.sl == 0 ? predict_nz(L.nz[c], t.bx, t.by) : 0;
+  const int16_t* q = a.ac + (t.gb * 3 + c) * 64;
+  if (t.lcb == 0) {
+    uint32_t w[32];
+    load_coefs(q, w);
+    block_tokens(w, nz, pred, block_ctx_of(c, t.type), f);
+  } else {
+    varblock_slice_tokens(q, t.sl, t.lcb, nz, left, prev, pred, block_ctx_of(c, t.type), f);
   }
 }
 
@@ -161,79 +279,9 @@ __device__ __forceinline__ uint32_t block_excl_scan1024(uint32_t v, uint32_t* sW
   return before + incl - v;
 }
 
-// One thread per block of the group (<= 32 x 32 = 1024 blocks); the thread
-// of a varblock's first block codes the whole varblock, its three
-// (varblock, channel) tasks Y, X, B consecutive in the group's stream order;
-// threads of covered blocks code nothing.
-struct BlockTask {
-  bool valid;
-  int bx, by;
-  size_t gb;
-  int acs;
-  int lcb, cx;  // log2 covered blocks, blocks across
-};
-__device__ __forceinline__ BlockTask block_task(const AcArgs& a, const GroupGeom& G) {
-  BlockTask t;
-  const int b = threadIdx.x;
-  t.valid = b < G.gw * G.gh;
-  t.bx = t.valid ? b % G.gw : 0;
-  t.by = t.valid ? b / G.gw : 0;
-  t.gb = (size_t)(G.by0 + t.by) * a.bxs + G.bx0 + t.bx;
-  t.acs = t.valid ? a.acs[t.gb] : 0;
-  if (t.acs & 0x80) t.valid = false;
-  t.lcb = log2_covered(t.acs);
-  t.cx = covered_x(t.acs);
-  return t;
-}
-
-// Tokens of one merged varblock and channel: the non-zero count, then the
-// coefficients k = cb .. (natural order, LLF skipped) while non-zeros are
-// left; slices of 64 coefficients live in the covered blocks in raster order.
-template <class F>
-__device__ __forceinline__ void varblock_tokens(const AcArgs& a, const BlockTask& t, int nz,
-                                                int pred, int bctx, int c, F&& f) {
-  f(nz_bucket(pred) * kBlockCtx + bctx, (uint32_t)nz);
-  const int cb = 1 << t.lcb, size = cb * 64;
-  const int zoff = kBlockCtx * kNzBuckets + kZdCtx * bctx;
-  int prev = nz > size / 16 ? 0 : 1;
-  int left = nz;
-#pragma unroll 1
-  for (int sl = 0; sl < cb && left > 0; sl++) {
-    const size_t gbs = t.gb + (size_t)(sl / t.cx) * a.bxs + sl % t.cx;
-    uint32_t w[32];
-    load_coefs(a.ac + (gbs * 3 + c) * 64, w);
-#pragma unroll
-    for (int kk = 0; kk < 64; kk++) {
-      const int k = sl * 64 + kk;
-      if (left > 0 && k >= cb) {
-        const int32_t v = coef(w, kk);
-        f(zoff + (kNnzCtx[(left + cb - 1) >> t.lcb] + kFreqCtx[k >> t.lcb]) * 2 + prev,
-          pack_signed(v));
-        prev = v != 0;
-        left -= prev;
-      }
-    }
-  }
-}
-
-template <class F>
-__device__ __forceinline__ void block_channel_tokens(const AcArgs& a, const BlockTask& t,
-                                                     uint8_t (*sNz)[1024], int c, F&& f) {
-  const int pred = predict_nz(sNz[c], t.bx, t.by);
-  const int bctx = block_ctx_of(c, t.acs);
-  const int nz = a.nz[c * (size_t)a.bxs * a.bys + t.gb];
-  if (t.lcb == 0) {
-    uint32_t w[32];
-    load_coefs(a.ac + (t.gb * 3 + c) * 64, w);
-    block_tokens(w, nz, pred, bctx, f);
-  } else {
-    varblock_tokens(a, t, nz, pred, bctx, c, f);
-  }
-}
-
 __global__ __launch_bounds__(kAcThreads) void ac_hist_kernel(AcArgs a) {
   __shared__ uint32_t sHist[kMaxClusters * kAcTok];
-  __shared__ uint8_t sNz[3][1024];
+  __shared__ AcLds L;
   __shared__ uint8_t sClu[kAcCtx];
   __shared__ uint32_t sBound, sNtok[3];
   const int g = blockIdx.x;
@@ -242,16 +290,16 @@ __global__ __launch_bounds__(kAcThreads) void ac_hist_kernel(AcArgs a) {
   for (int i = threadIdx.x; i < kAcCtx; i += blockDim.x) sClu[i] = c_cluster[i];
   if (threadIdx.x < 3) sNtok[threadIdx.x] = 0;
   if (threadIdx.x == 0) sBound = 0;
-  fill_nz(a, G, sNz);
+  const SliceTask t = slice_task(a, G);
+  fill_slices(a, G, t, L);
   __syncthreads();
-  const BlockTask t = block_task(a, G);
   uint32_t bound = 0, nt[3] = {0, 0, 0};
   if (t.valid) {
 #pragma unroll 1
     for (int ci = 0; ci < 3; ci++) {
       const int c = channel_of(ci);
       uint32_t cnt = 0;
-      block_channel_tokens(a, t, sNz, c, [&](int ctx, uint32_t v) {
+      task_tokens(a, t, L, c, [&](int ctx, uint32_t v) {
         uint32_t tok, nb, bits;
         hybrid420(v, tok, nb, bits);
         atomicAdd(&sHist[sClu[ctx] * kAcTok + tok], 1u);
@@ -278,27 +326,12 @@ __global__ __launch_bounds__(kAcThreads) void ac_hist_kernel(AcArgs a) {
   }
 }
 
-template <class Sink>
-__device__ __forceinline__ void emit_block(const AcArgs& a, const BlockTask& t,
-                                           uint8_t (*sNz)[1024], const uint8_t* sClu,
-                                           const uint32_t* sCode, Sink& s) {
-#pragma unroll 1
-  for (int ci = 0; ci < 3; ci++) {
-    block_channel_tokens(a, t, sNz, channel_of(ci), [&](int ctx, uint32_t v) {
-      uint32_t tok, nb, bits;
-      hybrid420(v, tok, nb, bits);
-      const uint32_t cl = sCode[sClu[ctx] * kAcTok + tok];
-      // code (<= 15 bits) and raw bits (<= 13) in one put
-      s.put((cl >> 16) + nb, (cl & 0xFFFFu) | (bits << (cl >> 16)));
-    });
-  }
-  s.finish();
-}
-
 __global__ __launch_bounds__(kAcThreads) void ac_emit_kernel(AcArgs a) {
   __shared__ uint32_t sCode[kMaxClusters * kAcTok];
   __shared__ uint32_t sBits[kEmitLdsWords];
-  __shared__ uint8_t sNz[3][1024];
+  __shared__ AcLds L;
+  __shared__ uint32_t sTask[3][1024];  // exact bits per (channel, slice task)
+  __shared__ uint32_t sBase[1024];     // bit offset of each varblock (first block)
   __shared__ uint8_t sClu[kAcCtx];
   __shared__ uint32_t sWave[kAcThreads / 64];
   const int g = blockIdx.x;
@@ -307,37 +340,69 @@ __global__ __launch_bounds__(kAcThreads) void ac_emit_kernel(AcArgs a) {
   for (int i = threadIdx.x; i < kMaxClusters * kAcTok; i += blockDim.x)
     sCode[i] = a.codes[(i / kAcTok) * kAlpha + (i % kAcTok)];
   for (int i = threadIdx.x; i < kEmitLdsWords; i += blockDim.x) sBits[i] = 0;
-  fill_nz(a, G, sNz);
+  const SliceTask t = slice_task(a, G);
+  fill_slices(a, G, t, L);
   __syncthreads();
-  const BlockTask t = block_task(a, G);
-  // pass 1: exact bits of this block's three tasks
-  uint32_t tot = 0;
+  const int me = t.by * 32 + t.bx;
+  // pass 1: exact bits of this thread's three tasks
   if (t.valid) {
 #pragma unroll 1
     for (int ci = 0; ci < 3; ci++) {
-      block_channel_tokens(a, t, sNz, channel_of(ci), [&](int ctx, uint32_t v) {
+      uint32_t tot = 0;
+      task_tokens(a, t, L, channel_of(ci), [&](int ctx, uint32_t v) {
         uint32_t tok, nb, bits;
         hybrid420(v, tok, nb, bits);
         tot += (sCode[sClu[ctx] * kAcTok + tok] >> 16) + nb;
       });
+      sTask[ci][me] = tot;
     }
   }
+  __syncthreads();
+  // varblock totals at first blocks, scanned in thread (= first-block raster) order
+  uint32_t vtot = 0;
+  const int cb = 1 << t.lcb;
+  if (t.valid && t.sl == 0) {
+    for (int ci = 0; ci < 3; ci++)
+      for (int j = 0; j < cb; j++) vtot += sTask[ci][block_of_slice(t, j)];
+  }
   uint32_t total;
-  const uint32_t off = block_excl_scan1024(tot, sWave, &total);
+  const uint32_t off = block_excl_scan1024(vtot, sWave, &total);
+  if (t.valid && t.sl == 0) sBase[me] = off;
+  __syncthreads();
   // pass 2: emission (LDS bit buffer when the group fits, else global atomics)
   const uint64_t base = a.base[g];  // word aligned
-  if (total <= (uint32_t)kEmitLdsWords * 32u) {
-    if (t.valid) {
-      BitSink s{sBits, off, 0, 0};
-      emit_block(a, t, sNz, sClu, sCode, s);
+  const bool lds = total <= (uint32_t)kEmitLdsWords * 32u;
+  if (t.valid) {
+    uint32_t pos = sBase[t.oby * 32 + t.obx];
+#pragma unroll 1
+    for (int ci = 0; ci < 3; ci++) {
+      uint32_t before = 0, chan_total = 0;
+      for (int j = 0; j < cb; j++) {
+        const uint32_t b = sTask[ci][block_of_slice(t, j)];
+        before += j < t.sl ? b : 0u;
+        chan_total += b;
+      }
+      const uint32_t start = pos + before;
+      if (sTask[ci][me]) {
+        BitSink s = lds ? BitSink{sBits, start, 0, 0} : BitSink{a.scratch, base + start, 0, 0};
+        const uint32_t* code = sCode;
+        task_tokens(a, t, L, channel_of(ci), [&](int ctx, uint32_t v) {
+          uint32_t tok, nb, bits;
+          hybrid420(v, tok, nb, bits);
+          const uint32_t cl = code[sClu[ctx] * kAcTok + tok];
+          // code (<= 15 bits) and raw bits (<= 13) in one put
+          s.put((cl >> 16) + nb, (cl & 0xFFFFu) | (bits << (cl >> 16)));
+        });
+        s.finish();
+      }
+      pos += chan_total;
     }
+  }
+  if (lds) {
     __syncthreads();
     const uint32_t nw = (total + 31) / 32;
     uint32_t* dst = a.scratch + (base >> 5);
     for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = sBits[i];
-  } else if (t.valid) {
-    BitSink s{a.scratch, base + off, 0, 0};
-    emit_block(a, t, sNz, sClu, sCode, s);
   }
   if (threadIdx.x == 0) a.bits[g] = total;
 }

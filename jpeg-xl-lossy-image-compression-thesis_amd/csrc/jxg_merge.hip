@@ -118,30 +118,35 @@ struct MCtx {
   int tx, ty, nbx, nby;
 };
 
-// Evaluate (WRITE = false: cost per varblock into S.cost[slot]) or emit
-// (WRITE = true) every varblock of shape SI on its grid in the tile.
+// run-time description of one shape pass
+struct Pass {
+  int si, type, cy, cx, koff, s;
+  float tmul;
+  bool write;
+  int slot;
+  __device__ __forceinline__ int R() const { return 8 * cy; }
+  __device__ __forceinline__ int C() const { return 8 * cx; }
+  __device__ __forceinline__ int GX() const { return 8 / cx; }
+  __device__ __forceinline__ int NV() const { return (8 / cx) * (8 / cy); }
+};
+
 // Eval validity: the level-s region containing the varblock lies inside the
-// frame's blocks.  Write validity: the tile's final map holds SI there.
-template <int SI, bool WRITE>
-__device__ void run_shape(const MergeArgs& a, const MCtx& m, int s, int slot) {
-  constexpr ShapeDesc D = kShapes[SI];
-  constexpr int CY = D.cy, CX = D.cx, R = 8 * CY, C = 8 * CX;
-  constexpr int GX = 8 / CX, GY = 8 / CY, NV = GX * GY;
-  constexpr int CB = CY * CX, LCB = ilog2c<CB>();
-  constexpr int KOFF = kKindOff[D.kind];
-  constexpr int KTOT = kKindOff[kNumKinds];
+// frame's blocks.  Write validity: the tile's final map holds the shape there.
+__device__ __forceinline__ bool vb_valid(const Pass& P, const MCtx& m, int bx0, int by0) {
+  if (P.write) return m.S->acs[by0 * 8 + bx0] == (uint8_t)P.type;
+  const int rx = bx0 / P.s, ry = by0 / P.s;
+  return (rx + 1) * P.s <= m.nbx && (ry + 1) * P.s <= m.nby;
+}
+
+// row pass: C-point DCT of every pixel row (3 channels) of every varblock
+template <int C>
+__device__ void row_pass(const Pass& P, const MCtx& m) {
   MergeLds& S = *m.S;
-  const int tid = threadIdx.x;
-  auto valid = [&](int bx0, int by0) -> bool {
-    if (WRITE) return S.acs[by0 * 8 + bx0] == (uint8_t)D.type;
-    const int rx = bx0 / s, ry = by0 / s;
-    return (rx + 1) * s <= m.nbx && (ry + 1) * s <= m.nby;
-  };
-  // ---- row pass: C-point DCT of every pixel row of every varblock ----
-  for (int i = tid; i < NV * 3 * R; i += kMThreads) {
+  const int R = P.R(), GX = P.GX(), n = P.NV() * 3 * R;
+  for (int i = threadIdx.x; i < n; i += kMThreads) {
     const int v = i / (3 * R), rem = i - v * (3 * R), c = rem / R, y = rem - c * R;
     const int vx = v % GX, vy = v / GX;
-    if (!valid(vx * CX, vy * CY)) continue;
+    if (!vb_valid(P, m, vx * P.cx, vy * P.cy)) continue;
     const int off = c * kMPlane + (vy * R + y) * kMS + vx * C;
     float x[C];
 #pragma unroll
@@ -150,43 +155,59 @@ __device__ void run_shape(const MergeArgs& a, const MCtx& m, int s, int slot) {
 #pragma unroll
     for (int k = 0; k < C; k++) S.co[off + k] = x[k];
   }
-  __syncthreads();
-  // ---- column pass: R-point DCT + quantization, lane = pixel column ----
-  for (int i = tid; i < NV * C; i += kMThreads) {  // NV * C is a multiple of 64
+}
+
+// column pass: R-point DCT of Y, X, B per pixel column (lane), quantization
+// with the CfL residual (the Y dequantized values go back into the lane's own
+// Y column of the coefficient plane), rate bits and e*e partials; C-lane
+// XOR-butterfly reductions.  Eval: cost per varblock; write: coefficients,
+// LLF, non-zero counts, origins.
+template <int R>
+__device__ void col_pass(const MergeArgs& a, const Pass& P, const MCtx& m) {
+  constexpr int KTOT = kKindOff[kNumKinds];
+  MergeLds& S = *m.S;
+  const int C = P.C(), GX = P.GX(), CY = P.cy, CX = P.cx, CB = CY * CX;
+  const int n = P.NV() * C;  // multiple of 64
+  for (int i = threadIdx.x; i < n; i += kMThreads) {
     const int v = i / C, x = i - v * C;
     const int vx = v % GX, vy = v / GX;
     const int bx0 = vx * CX, by0 = vy * CY;
-    if (!valid(bx0, by0)) continue;  // uniform over the varblock's C lanes
+    if (!vb_valid(P, m, bx0, by0)) continue;  // uniform over the varblock's C lanes
     int raw = 0;
-#pragma unroll
     for (int iy = 0; iy < CY; iy++)
-#pragma unroll
       for (int ix = 0; ix < CX; ix++) raw = max(raw, S.raw[(by0 + iy) * 8 + bx0 + ix]);
     const float scale = (float)a.G * (float)raw / 65536.0f;
     const float inv_scale = 1.0f / scale;
-    float yd[R];
     float part = 0.0f;
     int bits = 0, nz0 = 0, nz1 = 0, nz2 = 0;
+    const bool wide = CX >= CY;
 #pragma unroll 1
     for (int ci = 0; ci < 3; ci++) {
       const int c = ci == 0 ? 1 : (ci == 1 ? 0 : 2);
-      float col[R];
-      const int off = c * kMPlane + (vy * R) * kMS + vx * C + x;
+      float* cplane = S.co + c * kMPlane + (vy * R) * kMS + vx * C + x;
+      float* yplane = S.co + kMPlane + (vy * R) * kMS + vx * C + x;
+      {
+        // the column DCT in registers, written back to the lane's own column
+        float col[R];
 #pragma unroll
-      for (int ky = 0; ky < R; ky++) col[ky] = S.co[off + ky * kMS];
-      dct_n<R>(col);
-      const float* wrow = a.wk + (size_t)c * KTOT + KOFF;
+        for (int ky = 0; ky < R; ky++) col[ky] = cplane[ky * kMS];
+        dct_n<R>(col);
+#pragma unroll
+        for (int ky = 0; ky < R; ky++) cplane[ky * kMS] = col[ky];
+      }
+      const float* wrow = a.wk + (size_t)c * KTOT + P.koff;
       int nzc = 0;
-#pragma unroll
+#pragma unroll 4
       for (int ky = 0; ky < R; ky++) {
-        const int si = CX >= CY ? ky * C + x : x * R + ky;
+        const float coef_v = cplane[ky * kMS];
+        const int si = wide ? ky * C + x : x * R + ky;
         const bool is_llf = ky < CY && x < CX;
         int qq = 0;
         if (!is_llf) {
           const float w = wrow[si];
           const float ws = w * scale;
-          float rv = col[ky];
-          if (c == 2) rv = rv - yd[ky];
+          float rv = coef_v;
+          if (c == 2) rv = rv - yplane[ky * kMS];
           const float vq = rv * ws;
           const float av = fabsf(vq);
           const int qa = av < 0.58f ? 0 : (int)(fminf(av, 32767.0f) + 0.5f);
@@ -195,17 +216,17 @@ __device__ void run_shape(const MergeArgs& a, const MCtx& m, int s, int slot) {
             constexpr float kBias1 = 1.0f - 0.07005449891748593f;
             float adj = qa == 0 ? 0.0f : (qa == 1 ? kBias1 : (float)qa - 0.145f / (float)qa);
             if (vq < 0.0f) adj = -adj;
-            yd[ky] = adj * (a.iwy[KOFF + si] * inv_scale);
+            yplane[ky * kMS] = adj * (a.iwy[P.koff + si] * inv_scale);
           }
           const float e = av - (float)qa;
           part = fmaf(e, e, part);
           bits += qa ? 2 + 2 * bitlen_u((uint32_t)qa) : 0;
           nzc += qa != 0;
-        } else if (WRITE) {
-          S.llf[c][(by0 + ky) * 8 + bx0 + x] = col[ky];
+        } else if (P.write) {
+          S.llf[c][(by0 + ky) * 8 + bx0 + x] = coef_v;
         }
-        if (WRITE) {
-          const int p = a.nat[KOFF + si];
+        if (P.write) {
+          const int p = a.nat[P.koff + si];
           const int sl = p >> 6;
           const int lbx = bx0 + sl % CX, lby = by0 + sl / CX;
           const size_t gb = (size_t)(m.ty * 8 + lby) * a.bxs + m.tx * 8 + lbx;
@@ -217,7 +238,6 @@ __device__ void run_shape(const MergeArgs& a, const MCtx& m, int s, int slot) {
       nz2 += c == 2 ? nzc : 0;
     }
     // C-lane reductions (aligned groups inside one wave)
-#pragma unroll
     for (int msk = 1; msk < C; msk <<= 1) {
       part += __shfl_xor(part, msk, 64);
       bits += __shfl_xor(bits, msk, 64);
@@ -225,46 +245,59 @@ __device__ void run_shape(const MergeArgs& a, const MCtx& m, int s, int slot) {
       nz1 += __shfl_xor(nz1, msk, 64);
       nz2 += __shfl_xor(nz2, msk, 64);
     }
-    if (!WRITE) {
+    if (!P.write) {
       if (x == 0) {
         const int tb = bitlen_u((uint32_t)nz0) + bitlen_u((uint32_t)nz1) + bitlen_u((uint32_t)nz2);
-        float e = ((float)(bits + tb) + 8.0f * part) * D.tmul;
+        float e = ((float)(bits + tb) + 8.0f * part) * P.tmul;
         if (a.proposals & 2u) {
           const float* h = S.r3[by0 * 8 + bx0];
           e = hook_f(e, h[0], h[1], h[2]);
         }
-        S.cost[slot][v] = e;
+        S.cost[P.slot][v] = e;
       }
     } else if (x < CB) {
       // per covered block: non-zero counts, varblock origin, quant field
       const int lbx = bx0 + x % CX, lby = by0 + x / CX;
+      const int lcb = CB == 2 ? 1 : CB == 4 ? 2 : CB == 8 ? 3 : CB == 16 ? 4 : CB == 32 ? 5 : 6;
       const size_t nb = (size_t)a.bxs * a.bys;
       const size_t gb = (size_t)(m.ty * 8 + lby) * a.bxs + m.tx * 8 + lbx;
-      const int nzs[3] = {nz0, nz1, nz2};
-#pragma unroll
-      for (int c = 0; c < 3; c++)
-        a.nz[c * nb + gb] = (uint16_t)(x == 0 ? nzs[c] : (nzs[c] + CB - 1) >> LCB);
+      a.nz[gb] = (uint16_t)(x == 0 ? nz0 : (nz0 + CB - 1) >> lcb);
+      a.nz[nb + gb] = (uint16_t)(x == 0 ? nz1 : (nz1 + CB - 1) >> lcb);
+      a.nz[2 * nb + gb] = (uint16_t)(x == 0 ? nz2 : (nz2 + CB - 1) >> lcb);
       S.orig[lby * 8 + lbx] = (uint8_t)(by0 * 8 + bx0);
       S.rmax[lby * 8 + lbx] = raw;
     }
   }
-  __syncthreads();
 }
 
-template <bool WRITE>
-__device__ __forceinline__ void run_shape_rt(int si, const MergeArgs& a, const MCtx& m, int s,
-                                             int slot) {
-  switch (si) {
-    case 0: run_shape<0, WRITE>(a, m, s, slot); break;
-    case 1: run_shape<1, WRITE>(a, m, s, slot); break;
-    case 2: run_shape<2, WRITE>(a, m, s, slot); break;
-    case 3: run_shape<3, WRITE>(a, m, s, slot); break;
-    case 4: run_shape<4, WRITE>(a, m, s, slot); break;
-    case 5: run_shape<5, WRITE>(a, m, s, slot); break;
-    case 6: run_shape<6, WRITE>(a, m, s, slot); break;
-    case 7: run_shape<7, WRITE>(a, m, s, slot); break;
-    default: run_shape<8, WRITE>(a, m, s, slot); break;
+// one shape: row pass, barrier, column pass, barrier
+__device__ void run_shape(const MergeArgs& a, const MCtx& m, int si, int s, bool write,
+                          int slot) {
+  const ShapeDesc& D = kShapes[si];
+  Pass P;
+  P.si = si;
+  P.type = D.type;
+  P.cy = D.cy;
+  P.cx = D.cx;
+  P.koff = kKindOff[D.kind];
+  P.s = s;
+  P.tmul = D.tmul;
+  P.write = write;
+  P.slot = slot;
+  switch (P.cx) {
+    case 1: row_pass<8>(P, m); break;
+    case 2: row_pass<16>(P, m); break;
+    case 4: row_pass<32>(P, m); break;
+    default: row_pass<64>(P, m); break;
   }
+  __syncthreads();
+  switch (P.cy) {
+    case 1: col_pass<8>(a, P, m); break;
+    case 2: col_pass<16>(a, P, m); break;
+    case 4: col_pass<32>(a, P, m); break;
+    default: col_pass<64>(a, P, m); break;
+  }
+  __syncthreads();
 }
 
 __global__ __launch_bounds__(kMThreads) void merge_kernel(MergeArgs a) {
@@ -316,9 +349,9 @@ __global__ __launch_bounds__(kMThreads) void merge_kernel(MergeArgs a) {
     if (s > nbx || s > nby) break;  // no region of this size (or larger) fits
     const int full = s == 2 ? 2 : (s == 4 ? 5 : 8);
     const int tall = s == 2 ? 0 : (s == 4 ? 3 : 6);
-    run_shape_rt<false>(full, a, m, s, 0);
-    run_shape_rt<false>(tall, a, m, s, 1);
-    run_shape_rt<false>(tall + 1, a, m, s, 2);
+    run_shape(a, m, full, s, false, 0);
+    run_shape(a, m, tall, s, false, 1);
+    run_shape(a, m, tall + 1, s, false, 2);
     bool any = false;
     if (tid < nr * nr) {
       const int rx = tid % nr, ry = tid / nr;
@@ -378,7 +411,7 @@ __global__ __launch_bounds__(kMThreads) void merge_kernel(MergeArgs a) {
   for (int si = 0; si < 9; si++) {
     bool has = false;
     if (tid < 64) has = S.acs[tid] == (uint8_t)kShapes[si].type;
-    if (__syncthreads_or(has)) run_shape_rt<true>(si, a, m, 0, 0);
+    if (__syncthreads_or(has)) run_shape(a, m, si, 0, true, 0);
   }
   // ---- per covered block: LLF-derived DC, quant field, strategy ----
   if (tid < 64) {

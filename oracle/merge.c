@@ -417,3 +417,18 @@ void jxo_merge_tile(const jxo_frame* f, const float* xyb, const float* homog, in
       }
   }
 }
+
+/* ---- test exports (tests/test_oracle_varblocks.py) ---- */
+int jxo_export_kind(int kind, float* w3, uint16_t* nat) {
+  init_tables();
+  if (kind < 0 || kind >= JXO_NVKINDS) return 0;
+  const jxo_vkind* K = &g_kinds[kind];
+  const int n = K->rows * K->cols;
+  for (int c = 0; c < 3; c++) memcpy(w3 + c * n, K->w[c], sizeof(float) * n);
+  memcpy(nat, K->nat, sizeof(uint16_t) * n);
+  return n;
+}
+void jxo_export_dct(float* x, int N) {
+  init_tables();
+  dct_n(x, N);
+}

@@ -65,6 +65,9 @@ def lib():
                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
         _lib.jxo_cbrtf.argtypes = [ctypes.c_float]
         _lib.jxo_cbrtf.restype = ctypes.c_float
+        _lib.jxo_export_kind.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        _lib.jxo_export_kind.restype = ctypes.c_int
+        _lib.jxo_export_dct.argtypes = [ctypes.c_void_p, ctypes.c_int]
     return _lib
 
 
@@ -135,3 +138,23 @@ def srgb8_to_xyb(rgb: np.ndarray) -> np.ndarray:
     out = np.zeros((3, yp, xp), dtype=np.float32)
     lib().jxo_srgb8_to_xyb(rgb.ctypes.data, w, h, w * 3, xp, yp, out.ctypes.data)
     return out
+
+
+KIND_DIMS = [(8, 16), (16, 16), (16, 32), (32, 32), (32, 64), (64, 64)]
+
+
+def kind_tables(kind: int):
+    """(weights (3, rows*cols) float32, natural position of each stored index)"""
+    r, c = KIND_DIMS[kind]
+    w = np.zeros(3 * r * c, dtype=np.float32)
+    nat = np.zeros(r * c, dtype=np.uint16)
+    n = lib().jxo_export_kind(kind, w.ctypes.data, nat.ctypes.data)
+    assert n == r * c
+    return w.reshape(3, r * c), nat
+
+
+def dct(x: np.ndarray) -> np.ndarray:
+    """the oracle's normalized 1-D DCT (Lee) of a float32 vector"""
+    v = np.ascontiguousarray(x, dtype=np.float32).copy()
+    lib().jxo_export_dct(v.ctypes.data, len(v))
+    return v

@@ -133,3 +133,17 @@ def test_merged_varblocks_match_oracle(jxg_mod, oracle, decoder, w, h, d, e, p):
     if w * h <= 300 * 300:
         dec = decoder.decode(got)
         assert np.array_equal(dec.acs, ref.acs)
+
+
+def test_hook_f_nan_merges_match_oracle(jxg_mod, oracle):
+    """all-black tiles: hook F makes every estimate NaN; the merge comparison
+    accepts NaN (combined.diff:294 context) -> DCT32X64 pairs, GPU == oracle"""
+    img = np.zeros((136, 200, 3), dtype=np.uint8)
+    img[:, 128:] = smooth_rgb8(72, 136, 5)
+    with jxg_mod.Encoder(distance=1.0, effort=7, proposals=2, flags=jxg_mod.FLAG_KEEP_MAPS) as enc:
+        got = enc.encode(img)
+        st = enc.stats()
+    ref = oracle.encode(img, 1.0, 7, 2)
+    assert ((ref.acs[:8, :8] & 0x7F) == 20).all()
+    assert np.array_equal(st["acs"], ref.acs)
+    assert got == ref.bytes

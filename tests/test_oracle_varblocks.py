@@ -1,0 +1,111 @@
+"""CPU oracle: merged varblocks (16x8 ... 64x64).
+
+The tables and transforms of oracle/merge.c against independent restatements
+(numpy float64 DCT, the test decoder's Python natural order / weights), and
+encode -> decode round trips that exercise every merged shape, the thesis hook
+F on merge candidates (NaN estimates are accepted, combined.diff:294 context)
+and partial tiles.  [ext] libjxl stages: parity unpinned against libjxl.
+"""
+import math
+
+import numpy as np
+import pytest
+
+
+def smooth_rgb8(w, h, seed):
+    rng = np.random.default_rng(seed)
+    y, x = np.mgrid[0:h, 0:w].astype(np.float64)
+    fx, fy = rng.uniform(5, 40, 3), rng.uniform(5, 40, 3)
+    img = np.stack([128 + 90 * np.sin(x / fx[c] + y / fy[c] + c) for c in range(3)], -1)
+    for ty in range(0, h, 64):
+        for tx in range(0, w, 64):
+            k = rng.integers(0, 6)
+            if k == 0:
+                img[ty:ty + 64, tx:tx + 64] += rng.normal(0, 25, img[ty:ty + 64, tx:tx + 64].shape)
+            elif k == 1:
+                img[ty:ty + 64, tx:tx + 64] = rng.uniform(0, 255, 3)
+    return np.clip(img, 0, 255).astype(np.uint8)
+
+
+@pytest.mark.parametrize("n", [1, 2, 4, 8, 16, 32, 64])
+def test_lee_dct_matches_float64(oracle, n):
+    rng = np.random.default_rng(n)
+    x = rng.uniform(-1, 1, n).astype(np.float32)
+    k = np.arange(n)[:, None]
+    m = np.cos(math.pi * (2 * np.arange(n)[None, :] + 1) * k / (2 * n))
+    ref = (m @ x.astype(np.float64)) * np.where(k[:, 0] == 0, 1.0 / n, math.sqrt(2) / n)
+    got = oracle.dct(x)
+    assert np.allclose(got, ref, atol=2e-6 * max(1, n / 8)), (got, ref)
+
+
+@pytest.mark.parametrize("kind", range(6))
+def test_kind_tables_match_decoder(oracle, decoder, kind):
+    w, nat = oracle.kind_tables(kind)
+    iw, order = decoder.kind_tables(kind)
+    rows, cols = decoder.KIND_DIM[kind]
+    # natural order: a permutation, LLF (rows/8 x cols/8) first in raster order
+    assert sorted(nat.tolist()) == list(range(rows * cols))
+    inv = np.empty(rows * cols, dtype=np.int64)
+    inv[nat] = np.arange(rows * cols)
+    assert inv.tolist() == order
+    cs, cl = rows // 8, cols // 8
+    assert [inv[p] for p in range(cs * cl)] == [y * cols + x for y in range(cs) for x in range(cl)]
+    # weights: float32 of the decoder's double computation
+    assert np.array_equal(w, (1.0 / iw).astype(np.float32))
+
+
+CASES = [(256, 256, 1.0, 7, 0), (200, 264, 2.0, 5, 3), (520, 136, 0.5, 6, 2),
+         (333, 333, 3.0, 7, 1), (136, 520, 1.0, 7, 3)]
+
+
+@pytest.mark.parametrize("w,h,d,e,p", CASES)
+def test_varblock_roundtrip(oracle, decoder, w, h, d, e, p):
+    import jxg
+
+    img = smooth_rgb8(w, h, w * 31 + h)
+    r = oracle.encode(img, d, e, p)
+    assert (r.acs & 0x80).any()
+    dec = decoder.decode(r.bytes)
+    assert np.array_equal(dec.acs, r.acs)
+    assert np.array_equal(dec.qf - 1, r.qf)
+    assert np.array_equal(dec.dc, r.dc)
+    assert np.array_equal(dec.ac, r.ac)
+    assert np.array_equal(dec.ac_tokens, r.ac_tokens)
+
+
+@pytest.mark.parametrize("e", [5, 6, 7])
+def test_merges_pay_on_smooth_content(oracle, decoder, e):
+    """Pure smooth content: the merge stage must shrink the codestream without
+    losing PSNR against the 8x8-only search (effort 4)."""
+    import jxg
+
+    y, x = np.mgrid[0:256, 0:320].astype(np.float64)
+    img = np.stack([128 + 60 * np.sin(x / 19.0 + c) * np.cos(y / 23.0) for c in range(3)],
+                   -1).astype(np.uint8)
+    r, r4 = oracle.encode(img, 1.0, e, 0), oracle.encode(img, 1.0, 4, 0)
+    psnr = jxg.calculate_psnr(jxg.calculate_mse(img, decoder.decode(r.bytes).rgb))
+    psnr4 = jxg.calculate_psnr(jxg.calculate_mse(img, decoder.decode(r4.bytes).rgb))
+    assert len(r.bytes) < len(r4.bytes)
+    assert psnr > psnr4 - 0.25, (psnr, psnr4)
+
+
+def test_every_shape_is_reachable(oracle):
+    seen = set()
+    for w, h, d, e, p in CASES:
+        r = oracle.encode(smooth_rgb8(w, h, w * 31 + h), d, e, p)
+        seen |= set((r.acs[~(r.acs & 0x80).astype(bool)] & 0x7F).tolist())
+    assert {4, 5, 6, 7, 10, 11, 18, 19, 20} <= seen, sorted(seen)
+
+
+def test_hook_f_nan_estimates_merge(oracle):
+    """An all-black tile has 0/0 similarity ratios (NaN), so with hook F every
+    estimate is NaN: the 8x8 search keeps DCT8 (NaN never beats FLT_MAX) but
+    the merge comparison `candidate >= current` is false for NaN, so every
+    level accepts its last candidate -> two DCT32X64 varblocks at effort 7."""
+    img = np.zeros((64, 64, 3), dtype=np.uint8)
+    r0 = oracle.encode(img, 1.0, 7, 0)
+    rf = oracle.encode(img, 1.0, 7, 2)
+    assert (r0.acs == 0).all()
+    assert np.isnan(rf.homog).all()
+    assert rf.acs[0, 0] == 20 and rf.acs[4, 0] == 20
+    assert ((rf.acs & 0x7F) == 20).all()
