@@ -504,6 +504,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   __syncthreads();
   load_xyb_tile(a, sLut, sPix, ox, oy);
   __syncthreads();
+  if (a.xyb_out) {
+    // tile-major XYB copy for the merge stage: [tile][X, Y, B][64][64]
+    float* dst = a.xyb_out + (size_t)(ty * a.tiles_x + tx) * (3 * 4096);
+    for (int i = tid; i < 3 * 4096; i += kThreads) {
+      const int c = i >> 12, ly = (i >> 6) & 63, lx = i & 63;
+      dst[i] = sPix[c * kPlane + lds_at(lx + 1, ly + 1)];
+    }
+  }
   const int nbx = min(8, (int)a.bxs - tx * 8), nby = min(8, (int)a.bys - ty * 8);
   const int wave = tid >> 6, lane = tid & 63;
   const size_t nb = (size_t)a.bxs * a.bys;

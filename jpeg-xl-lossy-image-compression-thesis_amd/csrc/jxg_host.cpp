@@ -332,6 +332,30 @@ static MergeTables build_merge_tables() {
       }
     }
   }
+  // per-shape pixel-orientation copies ([ky * C + kx]; tall shapes read the
+  // stored table transposed) -- lanes of a column pass read consecutive kx
+  {
+    static const int kShapeDims[kNumShapes][3] = {{2, 1, 0}, {1, 2, 0}, {2, 2, 1}, {4, 2, 2}, {2, 4, 2},
+                                                 {4, 4, 3}, {8, 4, 4}, {4, 8, 4}, {8, 8, 5}};
+    const int stot = kShapeOff[kNumShapes];
+    std::vector<float> swk((size_t)3 * stot), siwy(stot);
+    std::vector<uint16_t> snat(stot);
+    for (int sh = 0; sh < kNumShapes; sh++) {
+      const int cy = kShapeDims[sh][0], cx = kShapeDims[sh][1], k = kShapeDims[sh][2];
+      const int R = 8 * cy, C = 8 * cx;
+      for (int ky = 0; ky < R; ky++)
+        for (int kx = 0; kx < C; kx++) {
+          const int si = cx >= cy ? ky * C + kx : kx * R + ky;
+          const int pi = kShapeOff[sh] + ky * C + kx;
+          for (int c = 0; c < 3; c++) swk[(size_t)c * stot + pi] = T.wk[(size_t)c * tot + kKindOff[k] + si];
+          siwy[pi] = T.iwy[kKindOff[k] + si];
+          snat[pi] = T.nat[kKindOff[k] + si];
+        }
+    }
+    T.wk.swap(swk);
+    T.iwy.swap(siwy);
+    T.nat.swap(snat);
+  }
   const double pi = 3.14159265358979323846;
   std::memset(T.lee_c, 0, sizeof(T.lee_c));
   std::memset(T.lee_s, 0, sizeof(T.lee_s));
@@ -364,7 +388,7 @@ struct Ctx {
   // device
   DevBuf<uint8_t> rgb, acs, qf;
   DevBuf<uint16_t> nz, mnat;
-  DevBuf<float> ent, mwk, miwy;
+  DevBuf<float> ent, mwk, miwy, xyb_tiles, mcost;
   DevBuf<uint32_t> vb, vcount;
   DevBuf<int32_t> dc;
   DevBuf<int16_t> ac;
@@ -405,8 +429,7 @@ static jxg_status init_constants(Ctx* c) {
   for (int i = 0; i < kAcCtx; i++) tab[i] = (uint8_t)ac_cluster(i);
   set_cluster_table(tab, c->stream);
   static const MergeTables mt = build_merge_tables();
-  set_merge_constants(lut, &mt.lee_c[0][0], &mt.lee_s[0][0], &mt.llf_p[0][0], &mt.llf_ib[0][0][0],
-                      c->stream);
+  set_merge_constants(&mt.llf_p[0][0], &mt.llf_ib[0][0][0], c->stream);
   JXG_HIP(c->mwk.ensure(mt.wk.size()));
   JXG_HIP(c->miwy.ensure(mt.iwy.size()));
   JXG_HIP(c->mnat.ensure(mt.nat.size()));
@@ -478,7 +501,12 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   JXG_HIP(c->ac.ensure(nb * 192));
   if (homog) JXG_HIP(c->homog.ensure(nb * 3));
   const int max_s = P.effort >= 6 ? 8 : (P.effort >= 5 ? 4 : 0);  // merge levels
-  if (max_s) JXG_HIP(c->ent.ensure(nb));
+  const uint32_t ntiles = f.tiles_x * f.tiles_y;
+  if (max_s) {
+    JXG_HIP(c->ent.ensure(nb));
+    JXG_HIP(c->xyb_tiles.ensure((size_t)ntiles * 3 * 4096));
+    JXG_HIP(c->mcost.ensure((size_t)ntiles * kNumShapes * 32));
+  }
   JXG_HIP(c->vb.ensure((size_t)f.nlf * 65536));
   JXG_HIP(c->vcount.ensure(f.nlf));
   JXG_HIP(c->h_vcount.ensure(f.nlf));
@@ -555,18 +583,16 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   fa.nz = c->nz.p;
   fa.homog = homog ? c->homog.p : nullptr;
   fa.ent = max_s ? c->ent.p : nullptr;
+  fa.xyb_out = max_s ? c->xyb_tiles.p : nullptr;
   launch_front(fa, f.tiles_x, f.tiles_y, s);
   JXG_HIP(hipGetLastError());
   if (max_s) {
     MergeArgs ma{};
-    ma.rgb = d_rgb;
-    ma.w = w;
-    ma.h = h;
-    ma.stride = stride;
+    ma.xyb = c->xyb_tiles.p;
     ma.bxs = f.bxs;
     ma.bys = f.bys;
-    ma.xp = f.xp;
-    ma.yp = f.yp;
+    ma.tiles_x = f.tiles_x;
+    ma.ntiles = ntiles;
     ma.proposals = P.proposals;
     ma.max_s = max_s;
     ma.G = f.G;
@@ -581,10 +607,11 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
     ma.dc = c->dc.p;
     ma.ac = c->ac.p;
     ma.nz = c->nz.p;
+    ma.cost = c->mcost.p;
     ma.wk = c->mwk.p;
     ma.iwy = c->miwy.p;
     ma.nat = c->mnat.p;
-    launch_merge(ma, f.tiles_x, f.tiles_y, s);
+    launch_merge(ma, s);
     JXG_HIP(hipGetLastError());
   }
   VbArgs va{c->acs.p, f.bxs, f.bys, f.lfxs, c->vb.p, c->vcount.p};

@@ -26,21 +26,23 @@ struct FrontArgs {
   uint16_t* nz;   // [3][nb] non-zero AC count per block and channel
   float* homog;   // [nb][3] or null
   float* ent;     // [nb] best 8x8 estimate (merge stage input) or null
+  float* xyb_out; // [tiles][3][64][64] XYB tiles (merge stage input) or null
 };
 
-// merge stage (jxg_merge.hip): tables of the merged varblock kinds
+// merge stage (jxg_merge.hip): weight kinds (stored orientation) and the
+// nine merged shapes' pixel-orientation tables ([ky * C + kx])
 constexpr int kNumKinds = 6;
 constexpr int kKindOff[kNumKinds + 1] = {0, 128, 384, 896, 1920, 3968, 8064};
+constexpr int kNumShapes = 9;
+constexpr int kShapeOff[kNumShapes + 1] = {0, 128, 256, 512, 1024, 1536, 2560, 4608, 6656, 10752};
 struct MergeArgs {
-  const uint8_t* rgb;
-  uint32_t w, h;
-  size_t stride;
-  uint32_t bxs, bys, xp, yp;
+  const float* xyb;     // [tiles][3][64][64] XYB tiles (front kernel)
+  uint32_t bxs, bys, tiles_x, ntiles;
   uint32_t proposals;
-  int max_s;      // largest merged square in blocks (2, 4 or 8); 0 = no merges
+  int max_s;      // largest merged square in blocks (2, 4 or 8)
   uint32_t G;
   float dc_mul[3], dc_step[3];
-  const float* ent;     // [nb] per-block estimate (front kernel)
+  float* ent;           // [nb] per-block estimate (front kernel; resolve rewrites)
   const float* homog;   // [nb][3] (hook F) or null
   uint8_t* acs;         // in/out: raw id, bit 7 on covered non-first blocks
   uint8_t* qf;          // in/out: raw - 1
@@ -48,9 +50,10 @@ struct MergeArgs {
   int16_t* ac;          // out (merged varblocks), natural order slices
   uint16_t* nz;         // out (merged varblocks): full count at the first block,
                         //   (nz + cb - 1) >> log2 cb at covered blocks
-  const float* wk;      // [3][kKindOff[6]] weights per kind, stored raster
-  const float* iwy;     // [kKindOff[6]] 1 / Y weight
-  const uint16_t* nat;  // [kKindOff[6]] stored raster -> natural position
+  float* cost;          // [tiles][9 shapes][32 varblocks] candidate estimates
+  const float* wk;      // [3][kShapeOff[9]] weights per shape, pixel orientation
+  const float* iwy;     // [kShapeOff[9]] 1 / Y weight
+  const uint16_t* nat;  // [kShapeOff[9]] natural-order position
 };
 // per-LF-group varblock lists (AC metadata channel)
 struct VbArgs {
@@ -142,10 +145,9 @@ void launch_lf_bits(const LfArgs& a, uint32_t nchunks, hipStream_t s);
 void launch_lf_scan(const LfArgs& a, uint32_t nstreams, hipStream_t s);
 void launch_lf_emit(const LfArgs& a, uint32_t nchunks, hipStream_t s);
 void set_cluster_table(const uint8_t* tab, hipStream_t s);
-void set_merge_constants(const float lut[256], const float* lee_c /*[7][32]*/,
-                         const float* lee_s /*[7][64]*/, const float* llf_p /*[4][8]*/,
-                         const float* llf_ib /*[4][8][8]*/, hipStream_t s);
-void launch_merge(const MergeArgs& a, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s);
+void set_merge_constants(const float* llf_p /*[4][8]*/, const float* llf_ib /*[4][8][8]*/,
+                         hipStream_t s);
+void launch_merge(const MergeArgs& a, hipStream_t s);
 void launch_vb_list(const VbArgs& a, uint32_t nlf, hipStream_t s);
 void launch_concat(const ConcatPiece* pieces, uint32_t npieces, uint64_t max_words,
                    const uint32_t* scratch, const uint32_t* chunks, uint32_t* out,

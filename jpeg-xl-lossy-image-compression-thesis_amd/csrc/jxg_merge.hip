@@ -2,38 +2,46 @@
 // 8x8-class decisions -> 16x8 ... 64x64 varblocks, and the transform,
 // quantization and LLF-derived DC of every merged varblock.
 //
-// One 512-thread workgroup per 64x64 tile (the unit libjxl's ProcessRectACS
-// works on, combined.diff:346 context).  The tile's XYB planes are rebuilt in
-// LDS from RGB8 (same pixel_xyb as the front kernel: 3 B/px re-read instead of
-// keeping 12 B/px of XYB in HBM).  Per merge level s (16, 32, 64 px squares)
-// the three candidate shapes (full, two tall halves, two wide halves) are
-// evaluated for every region of the tile at once:
-//   row pass    : lane = (varblock, channel, pixel row): C-point DCT in
-//                 registers, written to an LDS coefficient plane (row stride 65:
-//                 lanes on consecutive rows hit consecutive banks);
-//   column pass : lane = (varblock, pixel column): R-point DCT of Y, X, B in
-//                 registers, quantization with the CfL residual, rate bits and
-//                 e*e partials; a C-lane XOR-butterfly tree gives the cost.
-// One lane per region then resolves keep / full / tall / wide with the
-// TryMergeAcs comparison (NaN accepted, combined.diff:294 context) and hook F
-// (combined.diff:247-253) on every estimate.  Finally each chosen varblock is
-// re-run in write mode (coefficients scattered to natural-order slices, LLF
-// kept in LDS) and the DC of every covered block is derived from the LLF.
+// Three launches over the 64x64 tiles (the unit of libjxl's ProcessRectACS,
+// combined.diff:346 context):
+//   merge_eval    one 256-thread workgroup per (tile, candidate shape): the
+//                 shape's varblocks tile the 64x64 area, so every workgroup
+//                 does the same amount of work whatever the shape -- no idle
+//                 lanes at barriers.  The tile's XYB planes (written once by
+//                 the front kernel) are copied into an LDS coefficient image
+//                 (48 KB, 3 workgroups per CU) and transformed in place:
+//                   rows    lane = (channel, varblock, row), C-point DCT in
+//                           registers (64-point: two lanes, Lee's even / odd
+//                           halves, wave-uniform);
+//                   columns lane = (channel, varblock, column), same;
+//                   quant   lane = (channel, 16-row chunk, varblock, column):
+//                           Y first (its dequantized values replace its
+//                           coefficients for the B residual), then X and B;
+//                   reduce  lane = (varblock, column): chunk partials,
+//                           (Y + X) + B, C-lane XOR tree -> estimate (+hook F).
+//                 The nine shape workgroups of a tile get workgroup ids
+//                 congruent mod 8, so they land on one XCD and share its L2.
+//   merge_resolve one wave per tile: per level (16, 32, 64 px) and region,
+//                 keep / full / two tall / two wide halves with the
+//                 TryMergeAcs comparison (`candidate >= current` keeps: NaN
+//                 estimates are accepted, combined.diff:294 context).
+//   merge_write   one workgroup per (tile, shape) that holds chosen varblocks:
+//                 the same transform + quantization, coefficients scattered to
+//                 natural-order slices of the covered blocks, non-zero counts,
+//                 quant field, and the DC of each covered block from the LLF.
 // Float op order == oracle/merge.c (jxo_varblock, jxo_llf_dc, jxo_merge_tile).
 #include <float.h>
 
 #include "jxg_device.h"
 #include "jxg_kernels.h"
+#include "jxg_lee_tables.h"
 
 namespace jxg {
 
-__constant__ float c_mlut[256];
-__constant__ float c_lee_c[7 * 32];  // [log2 N][i] = 1 / (2 cos(pi (2i+1) / 2N))
-__constant__ float c_lee_s[7 * 64];  // [log2 N][k] = k ? sqrt2 / N : 1 / N
 __constant__ float c_llf_p[4 * 8];   // [log2 M][k]
 __constant__ float c_llf_ib[4 * 64]; // [log2 M][n][k]
 
-constexpr int kMThreads = 512;
+constexpr int kMThreads = 256;
 constexpr int kMS = 65;  // LDS row stride (floats)
 constexpr int kMPlane = 64 * kMS;
 
@@ -43,7 +51,7 @@ constexpr int ilog2c() {
 }
 
 // unnormalized DCT-II in registers, Lee's recursive even/odd split
-// (== oracle/merge.c lee)
+// (== oracle/merge.c lee); constants are instruction immediates
 template <int N>
 __device__ __forceinline__ void lee(float* x) {
   if constexpr (N > 1) {
@@ -52,7 +60,7 @@ __device__ __forceinline__ void lee(float* x) {
 #pragma unroll
     for (int i = 0; i < h; i++) {
       a[i] = x[i] + x[N - 1 - i];
-      b[i] = (x[i] - x[N - 1 - i]) * c_lee_c[l * 32 + i];
+      b[i] = (x[i] - x[N - 1 - i]) * kLeeC[l][i];
     }
     lee<h>(a);
     lee<h>(b);
@@ -63,307 +71,407 @@ __device__ __forceinline__ void lee(float* x) {
     x[N - 1] = b[h - 1];
   }
 }
+// normalized N-point DCT (N <= 32) of src[k * st] into x (registers)
 template <int N>
-__device__ __forceinline__ void dct_n(float* x) {
+__device__ __forceinline__ void dct_from(const float* src, int st, float* x) {
+#pragma unroll
+  for (int k = 0; k < N; k++) x[k] = src[k * st];
   lee<N>(x);
   constexpr int l = ilog2c<N>();
 #pragma unroll
-  for (int k = 0; k < N; k++) x[k] = x[k] * c_lee_s[l * 64 + k];
+  for (int k = 0; k < N; k++) x[k] = x[k] * kLeeS[l][k];
 }
-
-// merged shapes (== oracle jxo_shapes): raw id, blocks down, blocks across,
-// weight kind, cost multiplier
-struct ShapeDesc {
-  int type, cy, cx, kind;
-  float tmul;
-};
-constexpr ShapeDesc kShapes[9] = {
-    {6, 2, 1, 0, 1.0f},   {7, 1, 2, 0, 1.0f},   {4, 2, 2, 1, 1.0f},
-    {10, 4, 2, 2, 1.02f}, {11, 2, 4, 2, 1.02f}, {5, 4, 4, 3, 1.03f},
-    {19, 8, 4, 4, 1.05f}, {20, 4, 8, 4, 1.05f}, {18, 8, 8, 5, 1.05f}};
-
-__device__ __forceinline__ int shape_index(int type) {
-  switch (type) {
-    case 6: return 0;
-    case 7: return 1;
-    case 4: return 2;
-    case 10: return 3;
-    case 11: return 4;
-    case 5: return 5;
-    case 19: return 6;
-    case 20: return 7;
-    case 18: return 8;
-    default: return -1;
+// half h of the normalized 64-point DCT (Lee's first split: h = 0 the even
+// outputs 2k from the sums, h = 1 the odd outputs 2k+1 from the scaled
+// differences) -- the same float ops as lee<64>, spread over two lanes
+__device__ __forceinline__ void dct64_half(const float* src, int st, int h, float* y) {
+  float t[32];
+  if (h == 0) {
+#pragma unroll
+    for (int i = 0; i < 32; i++) t[i] = src[i * st] + src[(63 - i) * st];
+    lee<32>(t);
+#pragma unroll
+    for (int k = 0; k < 32; k++) y[k] = t[k] * kLeeS[6][2 * k];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 32; i++) t[i] = (src[i * st] - src[(63 - i) * st]) * kLeeC[6][i];
+    lee<32>(t);
+#pragma unroll
+    for (int k = 0; k < 31; k++) y[k] = (t[k] + t[k + 1]) * kLeeS[6][2 * k + 1];
+    y[31] = t[31] * kLeeS[6][63];
   }
 }
+
+// merged shapes (== oracle jxo_shapes): raw id, blocks down / across (log2),
+// cost multiplier
+struct ShapeDesc {
+  int type, lcy, lcx;
+  float tmul;
+};
+constexpr ShapeDesc kShapes[kNumShapes] = {
+    {6, 1, 0, 1.0f},   {7, 0, 1, 1.0f},   {4, 1, 1, 1.0f},
+    {10, 2, 1, 1.02f}, {11, 1, 2, 1.02f}, {5, 2, 2, 1.03f},
+    {19, 3, 2, 1.05f}, {20, 2, 3, 1.05f}, {18, 3, 3, 1.05f}};
 
 __device__ __forceinline__ int bitlen_u(uint32_t v) { return 32 - __clz(v); }
 
+// 53.9 KB: three workgroups per CU
 struct MergeLds {
-  float pix[3 * kMPlane];
-  float co[3 * kMPlane];
-  float cost[3][32];   // [candidate shape of the level][varblock grid index]
-  float llf[3][64];    // LLF of merged varblocks at their covered blocks
-  float ent[64];
-  float r3[64][3];
-  int raw[64];         // front-kernel quant field (raw, 1..256)
-  int rmax[64];        // merged: max raw over the varblock (at covered blocks)
-  uint8_t acs[64];
-  uint8_t orig[64];    // merged: local index of the varblock's first block
-  float lut[256];
+  float co[3 * kMPlane];  // coefficient image of the tile's varblocks; column
+                          // 64 of row b of plane c (padding) holds the LLF of
+                          // covered block b in write mode
+  float qsum[3][4][32];   // [Y, X, B][chunk][varblock]: column-tree chunk sums
+  float btab[256];        // 0.145f / q (AdjustQuantBias), q < 256
+  float vr3[32][3];       // hook F: similarity indices of each top-left block
+  int vbits[32];          // per varblock: rate bits
+  int vnz[32][3];         //               non-zeros per channel
+  int vraw[32];           //               max quant field
+  int valid[32];
+  uint8_t braw[64];       // front-kernel quant field (raw) of the tile's blocks
+  int any;
 };
+__device__ __forceinline__ float& llf_at(MergeLds& S, int c, int b) {
+  return S.co[c * kMPlane + b * kMS + 64];
+}
 
-struct MCtx {
-  MergeLds* S;
-  int tx, ty, nbx, nby;
-};
-
-// run-time description of one shape pass
+// one (tile, shape) workgroup: all index math is shifts and masks
 struct Pass {
-  int si, type, cy, cx, koff, s;
+  int type, lcy, lcx, soff, ls, tx, ty, tile;
   float tmul;
-  bool write;
-  int slot;
-  __device__ __forceinline__ int R() const { return 8 * cy; }
-  __device__ __forceinline__ int C() const { return 8 * cx; }
-  __device__ __forceinline__ int GX() const { return 8 / cx; }
-  __device__ __forceinline__ int NV() const { return (8 / cx) * (8 / cy); }
+  __device__ __forceinline__ int cy() const { return 1 << lcy; }
+  __device__ __forceinline__ int cx() const { return 1 << lcx; }
+  __device__ __forceinline__ int R() const { return 8 << lcy; }
+  __device__ __forceinline__ int C() const { return 8 << lcx; }
+  __device__ __forceinline__ int lR() const { return 3 + lcy; }
+  __device__ __forceinline__ int lC() const { return 3 + lcx; }
+  __device__ __forceinline__ int lGX() const { return 3 - lcx; }
+  __device__ __forceinline__ int lNV() const { return 6 - lcx - lcy; }
+  __device__ __forceinline__ int NV() const { return 1 << lNV(); }
+  __device__ __forceinline__ int bx0(int v) const { return (v & ((1 << lGX()) - 1)) << lcx; }
+  __device__ __forceinline__ int by0(int v) const { return (v >> lGX()) << lcy; }
+  __device__ __forceinline__ int off(int v, int c) const {
+    return c * kMPlane + by0(v) * 8 * kMS + bx0(v) * 8;
+  }
 };
 
-// Eval validity: the level-s region containing the varblock lies inside the
-// frame's blocks.  Write validity: the tile's final map holds the shape there.
-__device__ __forceinline__ bool vb_valid(const Pass& P, const MCtx& m, int bx0, int by0) {
-  if (P.write) return m.S->acs[by0 * 8 + bx0] == (uint8_t)P.type;
-  const int rx = bx0 / P.s, ry = by0 / P.s;
-  return (rx + 1) * P.s <= m.nbx && (ry + 1) * P.s <= m.nby;
+// workgroup id -> (tile, shape): the nine shapes of a tile share b % 8 (XCD)
+__device__ __forceinline__ bool decode_wg(const MergeArgs& a, int& tile, int& si) {
+  const int b = blockIdx.x, x = b & 7, q = b >> 3;
+  si = q % kNumShapes;
+  tile = (q / kNumShapes) * 8 + x;
+  return tile < (int)a.ntiles;
 }
 
-// row pass: C-point DCT of every pixel row (3 channels) of every varblock
-template <int C>
-__device__ void row_pass(const Pass& P, const MCtx& m) {
-  MergeLds& S = *m.S;
-  const int R = P.R(), GX = P.GX(), n = P.NV() * 3 * R;
-  for (int i = threadIdx.x; i < n; i += kMThreads) {
-    const int v = i / (3 * R), rem = i - v * (3 * R), c = rem / R, y = rem - c * R;
-    const int vx = v % GX, vy = v / GX;
-    if (!vb_valid(P, m, vx * P.cx, vy * P.cy)) continue;
-    const int off = c * kMPlane + (vy * R + y) * kMS + vx * C;
-    float x[C];
-#pragma unroll
-    for (int k = 0; k < C; k++) x[k] = S.pix[off + k];
-    dct_n<C>(x);
-#pragma unroll
-    for (int k = 0; k < C; k++) S.co[off + k] = x[k];
-  }
-}
-
-// column pass: R-point DCT of Y, X, B per pixel column (lane), quantization
-// with the CfL residual (the Y dequantized values go back into the lane's own
-// Y column of the coefficient plane), rate bits and e*e partials; C-lane
-// XOR-butterfly reductions.  Eval: cost per varblock; write: coefficients,
-// LLF, non-zero counts, origins.
-template <int R>
-__device__ void col_pass(const MergeArgs& a, const Pass& P, const MCtx& m) {
-  constexpr int KTOT = kKindOff[kNumKinds];
-  MergeLds& S = *m.S;
-  const int C = P.C(), GX = P.GX(), CY = P.cy, CX = P.cx, CB = CY * CX;
-  const int n = P.NV() * C;  // multiple of 64
-  for (int i = threadIdx.x; i < n; i += kMThreads) {
-    const int v = i / C, x = i - v * C;
-    const int vx = v % GX, vy = v / GX;
-    const int bx0 = vx * CX, by0 = vy * CY;
-    if (!vb_valid(P, m, bx0, by0)) continue;  // uniform over the varblock's C lanes
-    int raw = 0;
-    for (int iy = 0; iy < CY; iy++)
-      for (int ix = 0; ix < CX; ix++) raw = max(raw, S.raw[(by0 + iy) * 8 + bx0 + ix]);
-    const float scale = (float)a.G * (float)raw / 65536.0f;
-    const float inv_scale = 1.0f / scale;
-    float part = 0.0f;
-    int bits = 0, nz0 = 0, nz1 = 0, nz2 = 0;
-    const bool wide = CX >= CY;
-#pragma unroll 1
-    for (int ci = 0; ci < 3; ci++) {
-      const int c = ci == 0 ? 1 : (ci == 1 ? 0 : 2);
-      float* cplane = S.co + c * kMPlane + (vy * R) * kMS + vx * C + x;
-      float* yplane = S.co + kMPlane + (vy * R) * kMS + vx * C + x;
-      {
-        // the column DCT in registers, written back to the lane's own column
-        float col[R];
-#pragma unroll
-        for (int ky = 0; ky < R; ky++) col[ky] = cplane[ky * kMS];
-        dct_n<R>(col);
-#pragma unroll
-        for (int ky = 0; ky < R; ky++) cplane[ky * kMS] = col[ky];
-      }
-      const float* wrow = a.wk + (size_t)c * KTOT + P.koff;
-      int nzc = 0;
-#pragma unroll 4
-      for (int ky = 0; ky < R; ky++) {
-        const float coef_v = cplane[ky * kMS];
-        const int si = wide ? ky * C + x : x * R + ky;
-        const bool is_llf = ky < CY && x < CX;
-        int qq = 0;
-        if (!is_llf) {
-          const float w = wrow[si];
-          const float ws = w * scale;
-          float rv = coef_v;
-          if (c == 2) rv = rv - yplane[ky * kMS];
-          const float vq = rv * ws;
-          const float av = fabsf(vq);
-          const int qa = av < 0.58f ? 0 : (int)(fminf(av, 32767.0f) + 0.5f);
-          qq = vq < 0.0f ? -qa : qa;
-          if (c == 1) {
-            constexpr float kBias1 = 1.0f - 0.07005449891748593f;
-            float adj = qa == 0 ? 0.0f : (qa == 1 ? kBias1 : (float)qa - 0.145f / (float)qa);
-            if (vq < 0.0f) adj = -adj;
-            yplane[ky * kMS] = adj * (a.iwy[P.koff + si] * inv_scale);
-          }
-          const float e = av - (float)qa;
-          part = fmaf(e, e, part);
-          bits += qa ? 2 + 2 * bitlen_u((uint32_t)qa) : 0;
-          nzc += qa != 0;
-        } else if (P.write) {
-          S.llf[c][(by0 + ky) * 8 + bx0 + x] = coef_v;
-        }
-        if (P.write) {
-          const int p = a.nat[P.koff + si];
-          const int sl = p >> 6;
-          const int lbx = bx0 + sl % CX, lby = by0 + sl / CX;
-          const size_t gb = (size_t)(m.ty * 8 + lby) * a.bxs + m.tx * 8 + lbx;
-          a.ac[(gb * 3 + c) * 64 + (p & 63)] = (int16_t)qq;
-        }
-      }
-      nz0 += c == 0 ? nzc : 0;
-      nz1 += c == 1 ? nzc : 0;
-      nz2 += c == 2 ? nzc : 0;
-    }
-    // C-lane reductions (aligned groups inside one wave)
-    for (int msk = 1; msk < C; msk <<= 1) {
-      part += __shfl_xor(part, msk, 64);
-      bits += __shfl_xor(bits, msk, 64);
-      nz0 += __shfl_xor(nz0, msk, 64);
-      nz1 += __shfl_xor(nz1, msk, 64);
-      nz2 += __shfl_xor(nz2, msk, 64);
-    }
-    if (!P.write) {
-      if (x == 0) {
-        const int tb = bitlen_u((uint32_t)nz0) + bitlen_u((uint32_t)nz1) + bitlen_u((uint32_t)nz2);
-        float e = ((float)(bits + tb) + 8.0f * part) * P.tmul;
-        if (a.proposals & 2u) {
-          const float* h = S.r3[by0 * 8 + bx0];
-          e = hook_f(e, h[0], h[1], h[2]);
-        }
-        S.cost[P.slot][v] = e;
-      }
-    } else if (x < CB) {
-      // per covered block: non-zero counts, varblock origin, quant field
-      const int lbx = bx0 + x % CX, lby = by0 + x / CX;
-      const int lcb = CB == 2 ? 1 : CB == 4 ? 2 : CB == 8 ? 3 : CB == 16 ? 4 : CB == 32 ? 5 : 6;
-      const size_t nb = (size_t)a.bxs * a.bys;
-      const size_t gb = (size_t)(m.ty * 8 + lby) * a.bxs + m.tx * 8 + lbx;
-      a.nz[gb] = (uint16_t)(x == 0 ? nz0 : (nz0 + CB - 1) >> lcb);
-      a.nz[nb + gb] = (uint16_t)(x == 0 ? nz1 : (nz1 + CB - 1) >> lcb);
-      a.nz[2 * nb + gb] = (uint16_t)(x == 0 ? nz2 : (nz2 + CB - 1) >> lcb);
-      S.orig[lby * 8 + lbx] = (uint8_t)(by0 * 8 + bx0);
-      S.rmax[lby * 8 + lbx] = raw;
-    }
-  }
-}
-
-// one shape: row pass, barrier, column pass, barrier
-__device__ void run_shape(const MergeArgs& a, const MCtx& m, int si, int s, bool write,
-                          int slot) {
-  const ShapeDesc& D = kShapes[si];
+__device__ __forceinline__ Pass make_pass(const MergeArgs& a, int tile, int si) {
   Pass P;
-  P.si = si;
+  const ShapeDesc& D = kShapes[si];
   P.type = D.type;
-  P.cy = D.cy;
-  P.cx = D.cx;
-  P.koff = kKindOff[D.kind];
-  P.s = s;
+  P.lcy = D.lcy;
+  P.lcx = D.lcx;
   P.tmul = D.tmul;
-  P.write = write;
-  P.slot = slot;
-  switch (P.cx) {
-    case 1: row_pass<8>(P, m); break;
-    case 2: row_pass<16>(P, m); break;
-    case 4: row_pass<32>(P, m); break;
-    default: row_pass<64>(P, m); break;
-  }
-  __syncthreads();
-  switch (P.cy) {
-    case 1: col_pass<8>(a, P, m); break;
-    case 2: col_pass<16>(a, P, m); break;
-    case 4: col_pass<32>(a, P, m); break;
-    default: col_pass<64>(a, P, m); break;
-  }
-  __syncthreads();
+  P.soff = kShapeOff[si];
+  P.ls = max(D.lcy, D.lcx);  // level: the s x s region (log2 blocks) of the shape
+  P.tile = tile;
+  P.tx = tile % (int)a.tiles_x;
+  P.ty = tile / (int)a.tiles_x;
+  return P;
 }
 
-__global__ __launch_bounds__(kMThreads) void merge_kernel(MergeArgs a) {
-  __shared__ __attribute__((aligned(16))) MergeLds S;
-  const int tid = threadIdx.x;
-  const int tx = blockIdx.x, ty = blockIdx.y;
-  const int nbx = min(8, (int)a.bxs - tx * 8), nby = min(8, (int)a.bys - ty * 8);
-  if (nbx < 2 || nby < 2) return;  // no 16x16 region fits: nothing to merge
-  const size_t nb = (size_t)a.bxs * a.bys;
-  if (tid < 256) S.lut[tid] = c_mlut[tid];
-  if (tid < 64) {
-    const int lbx = tid & 7, lby = tid >> 3;
-    const bool in = lbx < nbx && lby < nby;
-    const size_t gb = (size_t)(ty * 8 + lby) * a.bxs + tx * 8 + lbx;
-    S.ent[tid] = in ? a.ent[gb] : 0.0f;
-    S.raw[tid] = in ? (int)a.qf[gb] + 1 : 1;
-    S.acs[tid] = in ? a.acs[gb] : 0;
-    if (a.homog) {
-      S.r3[tid][0] = in ? a.homog[gb * 3 + 0] : 0.0f;
-      S.r3[tid][1] = in ? a.homog[gb * 3 + 1] : 0.0f;
-      S.r3[tid][2] = in ? a.homog[gb * 3 + 2] : 0.0f;
-    }
+// XYB tile -> LDS (only the valid varblocks' rows are used later)
+__device__ __forceinline__ void load_tile(const MergeArgs& a, const Pass& P, MergeLds& S) {
+  const float4* src = reinterpret_cast<const float4*>(a.xyb + (size_t)P.tile * (3 * 4096));
+  for (int i = threadIdx.x; i < 3 * 1024; i += kMThreads) {
+    const int c = i >> 10, ly = (i >> 4) & 63, lx = (i & 15) * 4;
+    const float4 v = src[i];
+    float* d = S.co + c * kMPlane + ly * kMS + lx;
+    d[0] = v.x;
+    d[1] = v.y;
+    d[2] = v.z;
+    d[3] = v.w;
   }
-  __syncthreads();
-  // XYB tile (same conversion and edge handling as the front kernel)
-  {
-    const float cb = cbrt_det(kOpsinBias);
-    const int ox = tx * 64, oy = ty * 64;
-    for (int i = tid; i < 64 * 64; i += kMThreads) {
-      const int ly = i >> 6, lx = i & 63;
-      const int gx = ox + lx, gy = oy + ly;
-      float X = 0.0f, Y = 0.0f, B = 0.0f;
-      if (gx < (int)a.xp && gy < (int)a.yp) {
-        const int sx = min(gx, (int)a.w - 1), sy = min(gy, (int)a.h - 1);
-        const uint8_t* p = a.rgb + (size_t)sy * a.stride + 3 * (size_t)sx;
-        pixel_xyb(S.lut, cb, p[0], p[1], p[2], X, Y, B);
+}
+
+// rows: C-point DCT of every row of every valid varblock, in place.  For
+// C = 64 two lanes share a row; both read before either writes (barrier), and
+// the trip count is uniform so every thread reaches it.
+template <int C>
+__device__ void row_pass(const Pass& P, MergeLds& S) {
+  const int R = P.R(), nrows = 3 * P.NV() * R, lvr = P.lNV() + P.lR();
+  if constexpr (C == 64) {
+    const int n = 2 * nrows;  // nrows: multiple of 64
+    for (int i0 = 0; i0 < n; i0 += kMThreads) {
+      const int i = i0 + threadIdx.x;
+      const int h = (i >> 6) & 1, r = ((i >> 7) << 6) | (i & 63);
+      const int c = min(r >> lvr, 2), v = (r >> P.lR()) & (P.NV() - 1), y = r & (R - 1);
+      const bool act = i < n && S.valid[v];
+      const int off = P.off(v, c) + y * kMS;
+      float o[32];
+      if (act) dct64_half(S.co + off, 1, h, o);
+      __syncthreads();
+      if (act) {
+#pragma unroll
+        for (int k = 0; k < 32; k++) S.co[off + 2 * k + h] = o[k];
       }
-      const int o = ly * kMS + lx;
-      S.pix[o] = X;
-      S.pix[kMPlane + o] = Y;
-      S.pix[2 * kMPlane + o] = B;
+    }
+  } else {
+    for (int r = threadIdx.x; r < nrows; r += kMThreads) {
+      const int c = r >> lvr, v = (r >> P.lR()) & (P.NV() - 1), y = r & (R - 1);
+      if (!S.valid[v]) continue;
+      const int off = P.off(v, c) + y * kMS;
+      float o[C];
+      dct_from<C>(S.co + off, 1, o);
+#pragma unroll
+      for (int k = 0; k < C; k++) S.co[off + k] = o[k];
     }
   }
+}
+
+// columns: R-point DCT of every column, in place (64-point: two lanes)
+template <int R>
+__device__ void col_pass(const Pass& P, MergeLds& S) {
+  const int C = P.C(), ncols = 3 * P.NV() * C, lvc = P.lNV() + P.lC();
+  if constexpr (R == 64) {
+    const int n = 2 * ncols;
+    for (int i0 = 0; i0 < n; i0 += kMThreads) {
+      const int i = i0 + threadIdx.x;
+      const int h = (i >> 6) & 1, r = ((i >> 7) << 6) | (i & 63);
+      const int c = min(r >> lvc, 2), v = (r >> P.lC()) & (P.NV() - 1), x = r & (C - 1);
+      const bool act = i < n && S.valid[v];
+      const int off = P.off(v, c) + x;
+      float o[32];
+      if (act) dct64_half(S.co + off, kMS, h, o);
+      __syncthreads();
+      if (act) {
+#pragma unroll
+        for (int k = 0; k < 32; k++) S.co[off + (2 * k + h) * kMS] = o[k];
+      }
+    }
+  } else {
+    for (int r = threadIdx.x; r < ncols; r += kMThreads) {
+      const int c = r >> lvc, v = (r >> P.lC()) & (P.NV() - 1), x = r & (C - 1);
+      if (!S.valid[v]) continue;
+      const int off = P.off(v, c) + x;
+      float o[R];
+      dct_from<R>(S.co + off, kMS, o);
+#pragma unroll
+      for (int k = 0; k < R; k++) S.co[off + k * kMS] = o[k];
+    }
+  }
+}
+
+// quantization, phase 0 = Y, phase 1 = X and B; lane = (channel, chunk of
+// RPC rows, varblock, column).  Chunk partial: fmaf(e, e) over its rows
+// ascending.  WRITE: coefficients to their natural-order slices, LLF to LDS.
+template <int RPC, bool WRITE>
+__device__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S, int phase) {
+  constexpr int STOT = kShapeOff[kNumShapes];
+  constexpr int lper = RPC == 8 ? 9 : 8;  // items per channel: 512 (R = 8) or 256
+  const int C = P.C(), NV = P.NV();
+  const int n = phase == 0 ? 1 << lper : 2 << lper;
+  for (int i = threadIdx.x; i < n; i += kMThreads) {
+    const int cidx = phase == 0 ? 0 : 1 + (i >> lper);  // 0 Y, 1 X, 2 B
+    const int c = cidx == 0 ? 1 : (cidx == 1 ? 0 : 2);
+    const int j = i & ((1 << lper) - 1);
+    const int ch = j >> (P.lNV() + P.lC()), v = (j >> P.lC()) & (NV - 1), x = j & (C - 1);
+    if (!S.valid[v]) continue;
+    const int bx0 = P.bx0(v), by0 = P.by0(v);
+    const float scale = (float)a.G * (float)S.vraw[v] / 65536.0f;
+    const float inv_scale = 1.0f / scale;
+    float* cplane = S.co + P.off(v, c) + x;
+    const float* yd = S.co + P.off(v, 1) + x;
+    const float* wrow = a.wk + (size_t)c * STOT + P.soff + x;
+    float cp = 0.0f;
+    int bits = 0, nzc = 0;
+#pragma unroll
+    for (int kk = 0; kk < RPC; kk++) {
+      const int ky = ch * RPC + kk;
+      const bool is_llf = ky < P.cy() && x < P.cx();
+      const float coef_v = cplane[ky * kMS];
+      int qq = 0;
+      if (!is_llf) {
+        const float w = wrow[ky * C];
+        const float ws = w * scale;
+        float rv = coef_v;
+        if (c == 2) rv = rv - yd[ky * kMS];
+        const float vq = rv * ws;
+        const float av = fabsf(vq);
+        const int qa = av < 0.58f ? 0 : (int)(fminf(av, 32767.0f) + 0.5f);
+        qq = vq < 0.0f ? -qa : qa;
+        if (c == 1) {
+          constexpr float kBias1 = 1.0f - 0.07005449891748593f;
+          const float bq = qa < 256 ? S.btab[qa] : 0.145f / (float)qa;
+          float adj = qa == 0 ? 0.0f : (qa == 1 ? kBias1 : (float)qa - bq);
+          if (vq < 0.0f) adj = -adj;
+          cplane[ky * kMS] = adj * (a.iwy[P.soff + ky * C + x] * inv_scale);
+        }
+        const float e = av - (float)qa;
+        cp = fmaf(e, e, cp);
+        bits += qa ? 2 + 2 * bitlen_u((uint32_t)qa) : 0;
+        nzc += qa != 0;
+      } else if (WRITE) {
+        llf_at(S, c, (by0 + ky) * 8 + bx0 + x) = coef_v;
+      }
+      if (WRITE) {
+        const int p = a.nat[P.soff + ky * C + x];
+        const int sl = p >> 6;
+        const int lbx = bx0 + (sl & (P.cx() - 1)), lby = by0 + (sl >> P.lcx);
+        const size_t gb = (size_t)(P.ty * 8 + lby) * a.bxs + P.tx * 8 + lbx;
+        a.ac[(gb * 3 + c) * 64 + (p & 63)] = (int16_t)qq;
+      }
+    }
+    // the chunk's column partials, tree-summed over the varblock's C lanes
+    // (an aligned group inside one wave)
+    for (int msk = 1; msk < C; msk <<= 1) cp += __shfl_xor(cp, msk, 64);
+    if (x == 0) S.qsum[cidx][ch][v] = cp;
+    if (bits) atomicAdd(&S.vbits[v], bits);
+    if (nzc) atomicAdd(&S.vnz[v][c], nzc);
+  }
+}
+
+// transform + quantize every valid varblock of the pass; leaves per-varblock
+// bits / non-zeros and the chunk sums in LDS
+template <bool WRITE>
+__device__ void transform_quant(const MergeArgs& a, const Pass& P, MergeLds& S) {
+  switch (P.lcx) {
+    case 0: row_pass<8>(P, S); break;
+    case 1: row_pass<16>(P, S); break;
+    case 2: row_pass<32>(P, S); break;
+    default: row_pass<64>(P, S); break;
+  }
   __syncthreads();
-  const MCtx m{&S, tx, ty, nbx, nby};
-  bool merged = false;
-  for (int s = 2; s <= a.max_s; s *= 2) {
+  switch (P.lcy) {
+    case 0: col_pass<8>(P, S); break;
+    case 1: col_pass<16>(P, S); break;
+    case 2: col_pass<32>(P, S); break;
+    default: col_pass<64>(P, S); break;
+  }
+  __syncthreads();
+  for (int phase = 0; phase < 2; phase++) {
+    if (P.lcy == 0) quant_pass<8, WRITE>(a, P, S, phase);
+    else quant_pass<16, WRITE>(a, P, S, phase);
+    __syncthreads();
+  }
+}
+
+// distortion of varblock v: chunk sums in order per channel, (Y + X) + B
+__device__ __forceinline__ float varblock_dist(const Pass& P, const MergeLds& S, int v) {
+  const int nch = P.lcy == 0 ? 1 : P.R() >> 4;
+  float pc[3];
+#pragma unroll
+  for (int ci = 0; ci < 3; ci++) {
+    float t = S.qsum[ci][0][v];
+    for (int ch = 1; ch < nch; ch++) t = t + S.qsum[ci][ch][v];
+    pc[ci] = t;
+  }
+  return (pc[0] + pc[1]) + pc[2];
+}
+
+// per-varblock setup, before the tile-load barrier: validity (eval: the
+// level region lies inside the frame's blocks; write: the resolved map holds
+// the shape there), hook-F indices, sums reset; the blocks' quant field goes
+// to LDS (the varblock maxima are taken after the barrier: vraw_pass)
+template <bool WRITE>
+__device__ __forceinline__ void setup_varblocks(const MergeArgs& a, const Pass& P, MergeLds& S,
+                                                int nbx, int nby) {
+  const int t = threadIdx.x;
+  if (t < 64) {
+    const int lbx = t & 7, lby = t >> 3;
+    S.braw[t] = lbx < nbx && lby < nby
+                    ? a.qf[(size_t)(P.ty * 8 + lby) * a.bxs + P.tx * 8 + lbx] : 0;
+  }
+  if (t < 32) {
+    const int v = t;
+    bool ok = false;
+    if (v < P.NV()) {
+      const int bx0 = P.bx0(v), by0 = P.by0(v);
+      const size_t gb0 = (size_t)(P.ty * 8 + by0) * a.bxs + P.tx * 8 + bx0;
+      if (WRITE) {
+        ok = bx0 < nbx && by0 < nby && a.acs[gb0] == (uint8_t)P.type;
+      } else {
+        ok = (((bx0 >> P.ls) + 1) << P.ls) <= nbx && (((by0 >> P.ls) + 1) << P.ls) <= nby;
+        if (ok && (a.proposals & 2u)) {
+          S.vr3[v][0] = a.homog[gb0 * 3 + 0];
+          S.vr3[v][1] = a.homog[gb0 * 3 + 1];
+          S.vr3[v][2] = a.homog[gb0 * 3 + 2];
+        }
+      }
+    }
+    S.valid[v] = ok;
+    S.vbits[v] = 0;
+    S.vnz[v][0] = S.vnz[v][1] = S.vnz[v][2] = 0;
+  }
+  for (int i = t; i < 256; i += kMThreads) S.btab[i] = i < 2 ? 0.0f : 0.145f / (float)i;
+}
+// varblock quant field = max raw over its covered blocks (after a barrier)
+__device__ __forceinline__ void vraw_pass(const Pass& P, MergeLds& S) {
+  const int v = threadIdx.x;
+  if (v < P.NV() && S.valid[v]) {
+    const int bx0 = P.bx0(v), by0 = P.by0(v);
+    int raw = 0;
+    for (int iy = 0; iy < P.cy(); iy++)
+      for (int ix = 0; ix < P.cx(); ix++) raw = max(raw, (int)S.braw[(by0 + iy) * 8 + bx0 + ix] + 1);
+    S.vraw[v] = raw;
+  }
+}
+
+__device__ __forceinline__ int max_level(const MergeArgs& a) {
+  return a.max_s >= 8 ? 3 : (a.max_s >= 4 ? 2 : 1);
+}
+
+__global__ __launch_bounds__(kMThreads) void merge_eval_kernel(MergeArgs a) {
+  __shared__ __attribute__((aligned(16))) MergeLds S;
+  int tile, si;
+  if (!decode_wg(a, tile, si)) return;
+  const Pass P = make_pass(a, tile, si);
+  if (P.ls > max_level(a)) return;  // level not searched at this effort
+  const int nbx = min(8, (int)a.bxs - P.tx * 8), nby = min(8, (int)a.bys - P.ty * 8);
+  if ((1 << P.ls) > nbx || (1 << P.ls) > nby) return;  // no region of this level fits
+  setup_varblocks<false>(a, P, S, nbx, nby);
+  load_tile(a, P, S);
+  __syncthreads();
+  vraw_pass(P, S);
+  transform_quant<false>(a, P, S);
+  const int v = threadIdx.x;
+  if (v < P.NV() && S.valid[v]) {
+    const float dist = varblock_dist(P, S, v);
+    const int tb = bitlen_u((uint32_t)S.vnz[v][0]) + bitlen_u((uint32_t)S.vnz[v][1]) +
+                   bitlen_u((uint32_t)S.vnz[v][2]);
+    float e = ((float)(S.vbits[v] + tb) + 8.0f * dist) * P.tmul;
+    if (a.proposals & 2u) e = hook_f(e, S.vr3[v][0], S.vr3[v][1], S.vr3[v][2]);
+    a.cost[((size_t)tile * kNumShapes + si) * 32 + v] = e;
+  }
+}
+
+// one wave per tile: levels in order, one lane per region
+__global__ __launch_bounds__(64) void merge_resolve_kernel(MergeArgs a) {
+  __shared__ float sEnt[64];
+  __shared__ uint8_t sAcs[64];
+  const int tile = blockIdx.x;
+  const int tx = tile % (int)a.tiles_x, ty = tile / (int)a.tiles_x;
+  const int nbx = min(8, (int)a.bxs - tx * 8), nby = min(8, (int)a.bys - ty * 8);
+  const int t = threadIdx.x, lbx = t & 7, lby = t >> 3;
+  const bool in = lbx < nbx && lby < nby;
+  const size_t gb = (size_t)(ty * 8 + lby) * a.bxs + tx * 8 + lbx;
+  sEnt[t] = in ? a.ent[gb] : 0.0f;
+  sAcs[t] = in ? a.acs[gb] : 0;
+  __syncthreads();
+  const float* cost = a.cost + (size_t)tile * kNumShapes * 32;
+  for (int s = 2; s <= a.max_s && s <= nbx && s <= nby; s *= 2) {
     const int nr = 8 / s;
-    if (s > nbx || s > nby) break;  // no region of this size (or larger) fits
     const int full = s == 2 ? 2 : (s == 4 ? 5 : 8);
     const int tall = s == 2 ? 0 : (s == 4 ? 3 : 6);
-    run_shape(a, m, full, s, false, 0);
-    run_shape(a, m, tall, s, false, 1);
-    run_shape(a, m, tall + 1, s, false, 2);
-    bool any = false;
-    if (tid < nr * nr) {
-      const int rx = tid % nr, ry = tid / nr;
+    if (t < nr * nr) {
+      const int rx = t % nr, ry = t / nr;
       if ((rx + 1) * s <= nbx && (ry + 1) * s <= nby) {
         float cur = 0.0f;
         for (int iy = 0; iy < s; iy++)
-          for (int ix = 0; ix < s; ix++) cur += S.ent[(ry * s + iy) * 8 + rx * s + ix];
-        const float e0 = S.cost[0][ry * nr + rx];
-        const int vl = ry * (16 / s) + 2 * rx;
-        const float et = S.cost[1][vl] + S.cost[1][vl + 1];
-        const int vt = (2 * ry) * nr + rx;
-        const float ew = S.cost[2][vt] + S.cost[2][vt + nr];
+          for (int ix = 0; ix < s; ix++) cur += sEnt[(ry * s + iy) * 8 + rx * s + ix];
+        // varblock grid indices: full (8/s per row), tall (16/s), wide (8/s)
+        const int vf = ry * nr + rx, vl = ry * (16 / s) + 2 * rx, vt = (2 * ry) * nr + rx;
+        const float e0 = cost[full * 32 + vf];
+        const float el = cost[tall * 32 + vl], er = cost[tall * 32 + vl + 1];
+        const float etop = cost[(tall + 1) * 32 + vt], ebot = cost[(tall + 1) * 32 + vt + nr];
+        const float et = el + er, ew = etop + ebot;
         float best = cur;
         int choice = 0;
         if (!(e0 >= best)) {
@@ -378,78 +486,83 @@ __global__ __launch_bounds__(kMThreads) void merge_kernel(MergeArgs a) {
           best = ew;
           choice = 3;
         }
-        if (choice) {
-          any = true;
-          // varblocks of the choice: (shape, block origin, estimate)
-          const int nv = choice == 1 ? 1 : 2;
-          for (int j = 0; j < nv; j++) {
-            int si, bx, by;
-            float e;
-            if (choice == 1) {
-              si = full, bx = rx * s, by = ry * s, e = e0;
-            } else if (choice == 2) {
-              si = tall, bx = rx * s + j * (s / 2), by = ry * s, e = S.cost[1][vl + j];
-            } else {
-              si = tall + 1, bx = rx * s, by = ry * s + j * (s / 2), e = S.cost[2][vt + j * nr];
-            }
-            const int cy = kShapes[si].cy, cx = kShapes[si].cx, type = kShapes[si].type;
-            for (int iy = 0; iy < cy; iy++)
-              for (int ix = 0; ix < cx; ix++) {
-                const int b = (by + iy) * 8 + bx + ix;
-                S.acs[b] = (uint8_t)(type | ((iy | ix) ? 0x80 : 0));
-                S.ent[b] = (iy | ix) ? 0.0f : e;
-              }
+        for (int j = 0; choice && j < (choice == 1 ? 1 : 2); j++) {
+          int sh, bx, by;
+          float e;
+          if (choice == 1) {
+            sh = full, bx = rx * s, by = ry * s, e = e0;
+          } else if (choice == 2) {
+            sh = tall, bx = rx * s + j * (s / 2), by = ry * s, e = j ? er : el;
+          } else {
+            sh = tall + 1, bx = rx * s, by = ry * s + j * (s / 2), e = j ? ebot : etop;
           }
+          const int cy = 1 << kShapes[sh].lcy, cx = 1 << kShapes[sh].lcx;
+          for (int iy = 0; iy < cy; iy++)
+            for (int ix = 0; ix < cx; ix++) {
+              const int b = (by + iy) * 8 + bx + ix;
+              sAcs[b] = (uint8_t)(kShapes[sh].type | ((iy | ix) ? 0x80 : 0));
+              sEnt[b] = (iy | ix) ? 0.0f : e;
+            }
         }
       }
     }
-    merged |= __syncthreads_or(any) != 0;
+    __syncthreads();
   }
-  if (!merged) return;  // the front kernel's output stands
-  // ---- emit the chosen varblocks ----
-#pragma unroll 1
-  for (int si = 0; si < 9; si++) {
-    bool has = false;
-    if (tid < 64) has = S.acs[tid] == (uint8_t)kShapes[si].type;
-    if (__syncthreads_or(has)) run_shape(a, m, si, 0, true, 0);
-  }
-  // ---- per covered block: LLF-derived DC, quant field, strategy ----
-  if (tid < 64) {
-    const int lbx = tid & 7, lby = tid >> 3;
-    if (lbx < nbx && lby < nby) {
-      const size_t gb = (size_t)(ty * 8 + lby) * a.bxs + tx * 8 + lbx;
-      const int t = S.acs[tid];
-      a.acs[gb] = (uint8_t)t;
-      const int si = shape_index(t & 0x7F);
-      if (si >= 0) {
-        const int o = S.orig[tid];
-        const int oy = o >> 3, ox = o & 7;
-        const int cy = kShapes[si].cy, cx = kShapes[si].cx;
-        const int ly = cy == 1 ? 0 : (cy == 2 ? 1 : (cy == 4 ? 2 : 3));
-        const int lx = cx == 1 ? 0 : (cx == 2 ? 1 : (cx == 4 ? 2 : 3));
-        const int iy = lby - oy, ix = lbx - ox;
-        float dc[3];
-        for (int c = 0; c < 3; c++) {
-          float acc = 0.0f;
-          for (int ky = 0; ky < cy; ky++) {
-            float u = 0.0f;
-            for (int kx = 0; kx < cx; kx++) {
-              const float tt = (S.llf[c][(oy + ky) * 8 + ox + kx] * c_llf_p[ly * 8 + ky]) *
-                               c_llf_p[lx * 8 + kx];
-              u = fmaf(tt, c_llf_ib[lx * 64 + ix * 8 + kx], u);
-            }
-            acc = fmaf(u, c_llf_ib[ly * 64 + iy * 8 + ky], acc);
-          }
-          dc[c] = acc;
-        }
-        int32_t q[3];
-        quant_dc3(dc, a.dc_mul, a.dc_step, q);
-        a.dc[gb] = q[0];
-        a.dc[nb + gb] = q[1];
-        a.dc[2 * nb + gb] = q[2];
-        a.qf[gb] = (uint8_t)(S.rmax[tid] - 1);
-      }
+  if (in) a.acs[gb] = sAcs[t];
+}
+
+__global__ __launch_bounds__(kMThreads) void merge_write_kernel(MergeArgs a) {
+  __shared__ __attribute__((aligned(16))) MergeLds S;
+  int tile, si;
+  if (!decode_wg(a, tile, si)) return;
+  const Pass P = make_pass(a, tile, si);
+  if (P.ls > max_level(a)) return;
+  const int nbx = min(8, (int)a.bxs - P.tx * 8), nby = min(8, (int)a.bys - P.ty * 8);
+  if ((1 << P.ls) > nbx || (1 << P.ls) > nby) return;
+  if (threadIdx.x == 0) S.any = 0;
+  __syncthreads();
+  setup_varblocks<true>(a, P, S, nbx, nby);
+  if (threadIdx.x < 32 && S.valid[threadIdx.x]) S.any = 1;
+  __syncthreads();
+  if (!S.any) return;  // uniform: no varblock of this shape was chosen here
+  vraw_pass(P, S);
+  load_tile(a, P, S);
+  __syncthreads();
+  transform_quant<true>(a, P, S);
+  // per covered block: non-zero counts, quant field, LLF-derived DC
+  const int cb = P.cy() * P.cx(), lcb = P.lcy + P.lcx;
+  const size_t nb = (size_t)a.bxs * a.bys;
+  const int ly = P.lcy, lx = P.lcx;
+  for (int i = threadIdx.x; i < P.NV() * cb; i += kMThreads) {
+    const int v = i >> lcb, k = i & (cb - 1);
+    if (!S.valid[v]) continue;
+    const int iy = k >> P.lcx, ix = k & (P.cx() - 1);
+    const int bx0 = P.bx0(v), by0 = P.by0(v);
+    const size_t gb = (size_t)(P.ty * 8 + by0 + iy) * a.bxs + P.tx * 8 + bx0 + ix;
+    for (int c = 0; c < 3; c++) {
+      const int n = S.vnz[v][c];
+      a.nz[c * nb + gb] = (uint16_t)(k == 0 ? n : (n + cb - 1) >> lcb);
     }
+    float dc[3];
+    for (int c = 0; c < 3; c++) {
+      float acc = 0.0f;
+      for (int ky = 0; ky < P.cy(); ky++) {
+        float u = 0.0f;
+        for (int kx = 0; kx < P.cx(); kx++) {
+          const float tt = (llf_at(S, c, (by0 + ky) * 8 + bx0 + kx) * c_llf_p[ly * 8 + ky]) *
+                           c_llf_p[lx * 8 + kx];
+          u = fmaf(tt, c_llf_ib[lx * 64 + ix * 8 + kx], u);
+        }
+        acc = fmaf(u, c_llf_ib[ly * 64 + iy * 8 + ky], acc);
+      }
+      dc[c] = acc;
+    }
+    int32_t q[3];
+    quant_dc3(dc, a.dc_mul, a.dc_step, q);
+    a.dc[gb] = q[0];
+    a.dc[nb + gb] = q[1];
+    a.dc[2 * nb + gb] = q[2];
+    a.qf[gb] = (uint8_t)(S.vraw[v] - 1);
   }
 }
 
@@ -492,22 +605,18 @@ __global__ __launch_bounds__(1024) void vb_list_kernel(VbArgs a) {
   if (threadIdx.x == 0) a.count[lg] = sBase;
 }
 
-void set_merge_constants(const float lut[256], const float* lee_c, const float* lee_s,
-                         const float* llf_p, const float* llf_ib, hipStream_t s) {
-  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_mlut), lut, sizeof(float) * 256, 0,
-                               hipMemcpyHostToDevice, s);
-  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_lee_c), lee_c, sizeof(float) * 7 * 32, 0,
-                               hipMemcpyHostToDevice, s);
-  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_lee_s), lee_s, sizeof(float) * 7 * 64, 0,
-                               hipMemcpyHostToDevice, s);
+void set_merge_constants(const float* llf_p, const float* llf_ib, hipStream_t s) {
   (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_llf_p), llf_p, sizeof(float) * 4 * 8, 0,
                                hipMemcpyHostToDevice, s);
   (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_llf_ib), llf_ib, sizeof(float) * 4 * 64, 0,
                                hipMemcpyHostToDevice, s);
   (void)hipStreamSynchronize(s);
 }
-void launch_merge(const MergeArgs& a, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s) {
-  hipLaunchKernelGGL(merge_kernel, dim3(tiles_x, tiles_y), dim3(kMThreads), 0, s, a);
+void launch_merge(const MergeArgs& a, hipStream_t s) {
+  const uint32_t nwg = ((a.ntiles + 7) / 8) * 8 * kNumShapes;
+  hipLaunchKernelGGL(merge_eval_kernel, dim3(nwg), dim3(kMThreads), 0, s, a);
+  hipLaunchKernelGGL(merge_resolve_kernel, dim3(a.ntiles), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(merge_write_kernel, dim3(nwg), dim3(kMThreads), 0, s, a);
 }
 void launch_vb_list(const VbArgs& a, uint32_t nlf, hipStream_t s) {
   hipLaunchKernelGGL(vb_list_kernel, dim3(nlf), dim3(1024), 0, s, a);

@@ -23,9 +23,10 @@
  * Float contract (mirrored by jxg_merge.hip): 1-D DCTs are Lee's recursive
  * even/odd split with float constants c_N[i] = (float)(1/(2 cos(pi(2i+1)/2N)))
  * and output scales s_N[k] = (float)(k ? sqrt2/N : 1/N); rows first, then
- * columns; the quantization walks pixel-orientation columns (one GPU lane per
- * column) over channels Y, X, B and rows ky ascending, fmaf(e, e, part); the
- * column partials are tree-summed pairwise (tree_sum).
+ * columns; the quantization runs one GPU lane per (channel, 16-row chunk,
+ * column) with fmaf(e, e, part) over the chunk's rows ascending; a chunk's
+ * column partials are tree-summed pairwise (tree_sum), a channel adds its
+ * chunks in order, and dist = (Y + X) + B.
  */
 #include <float.h>
 #include <math.h>
@@ -291,38 +292,49 @@ float jxo_varblock(const jxo_frame* f, const jxo_shape* s, const float* xyb, int
   }
   const float scale = (float)f->G * (float)raw / 65536.0f;
   const float inv_scale = 1.0f / scale;
-  float part[64];
+  /* distortion: per channel, the rows are cut into chunks of 16 (one chunk
+   * when R = 8); per (chunk, column) fmaf(e, e) over the chunk's rows in
+   * ascending order from 0; a chunk's C column partials are tree-summed; a
+   * channel sums its chunks in order; dist = (Y + X) + B */
   int bits = 0, nz[3] = {0, 0, 0};
   static const int corder[3] = {1, 0, 2};
-  for (int x = 0; x < C; x++) {
-    float yd[64];
-    part[x] = 0.0f;
-    for (int ci = 0; ci < 3; ci++) {
-      const int c = corder[ci];
-      for (int ky = 0; ky < R; ky++) {
-        const int si = stored_index(s, ky, x);
-        if (ky < s->cy && x < s->cx) { /* LLF: carried by the DC image */
-          if (q) q[c * R * C + K->nat[si]] = 0;
-          continue;
+  const int rows_per_chunk = R < 16 ? R : 16;
+  float yd[64 * 64], pc[3] = {0.0f, 0.0f, 0.0f};
+  for (int ci = 0; ci < 3; ci++) {
+    const int c = corder[ci];
+    for (int ch = 0; ch * rows_per_chunk < R; ch++) {
+      float part[64];
+      for (int x = 0; x < C; x++) {
+        float cp = 0.0f;
+        for (int ky = ch * rows_per_chunk; ky < (ch + 1) * rows_per_chunk; ky++) {
+          const int si = stored_index(s, ky, x);
+          if (ky < s->cy && x < s->cx) { /* LLF: carried by the DC image */
+            if (q) q[c * R * C + K->nat[si]] = 0;
+            continue;
+          }
+          const float w = K->w[c][si];
+          const float ws = w * scale;
+          float rv = F[c][ky * C + x];
+          if (c == 2) rv = rv - yd[ky * C + x];
+          const float v = rv * ws;
+          const int qq = quant1(v);
+          if (c == 1) yd[ky * C + x] = adjust_bias_y(qq) * ((1.0f / w) * inv_scale);
+          const uint32_t aq = (uint32_t)(qq < 0 ? -qq : qq);
+          const float e = fabsf(v) - (float)aq;
+          cp = fmaf(e, e, cp);
+          if (aq) {
+            bits += 2 + 2 * bitlen(aq);
+            nz[c]++;
+          }
+          if (q) q[c * R * C + K->nat[si]] = qq;
         }
-        const float w = K->w[c][si];
-        const float ws = w * scale;
-        float rv = F[c][ky * C + x];
-        if (c == 2) rv = rv - yd[ky];
-        const float v = rv * ws;
-        const int qq = quant1(v);
-        if (c == 1) yd[ky] = adjust_bias_y(qq) * ((1.0f / w) * inv_scale);
-        const uint32_t aq = (uint32_t)(qq < 0 ? -qq : qq);
-        const float e = fabsf(v) - (float)aq;
-        part[x] = fmaf(e, e, part[x]);
-        if (aq) {
-          bits += 2 + 2 * bitlen(aq);
-          nz[c]++;
-        }
-        if (q) q[c * R * C + K->nat[si]] = qq;
+        part[x] = cp;
       }
+      const float chunk = tree_sum(part, C);
+      pc[c] = ch == 0 ? chunk : pc[c] + chunk;
     }
   }
+  const float dist = (pc[1] + pc[0]) + pc[2];
   for (int c = 0; c < 3; c++) bits += bitlen((uint32_t)nz[c]);
   if (nzo)
     for (int c = 0; c < 3; c++) nzo[c] = nz[c];
@@ -330,7 +342,6 @@ float jxo_varblock(const jxo_frame* f, const jxo_shape* s, const float* xyb, int
     for (int c = 0; c < 3; c++)
       for (int ky = 0; ky < s->cy; ky++)
         for (int kx = 0; kx < s->cx; kx++) llf[(c * 8 + ky) * 8 + kx] = F[c][ky * C + kx];
-  const float dist = tree_sum(part, C);
   return ((float)bits + 8.0f * dist) * s->tmul;
 }
 
