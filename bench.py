@@ -2,18 +2,29 @@
 """Benchmark: MPix/s of VarDCT encode at d1.0 on synthetic 8K RGB (BASELINE.json
 metric), device-resident RGB8 in HBM -> complete .jxl bytes in host memory.
 
-  python bench.py --gpus N --steps K --warmup W
+  python bench.py --gpus N --steps K --warmup W [--mode shard|replica]
 
-One step = one full encode of one 7680x4320 frame per rank (front end, token
-statistics, prefix codes, bit emission, assembly, D2H of the codestream).
-Multi-GPU (launched by torch.distributed.run): every rank encodes its own frame
-(frame-level data parallelism, no data-path collective), so scaling is weak;
-the barrier + max-over-ranks timing follows the driver contract.
+One step = one full encode (front end + merge stage, token statistics, prefix
+codes, bit emission, assembly, D2H of the codestream).
+
+N = 1: one 7680x4320 frame per step (BASELINE config 2's frame on one GPU).
+N > 1 (launched by torch.distributed.run, backend nccl = RCCL):
+  shard   (default) -- group sharding: ONE frame of 7680 x
+          (4320 N) pixels per step -- every rank owns 1/N of its 256x256 pass
+          groups, i.e. one 8K frame's worth of work (weak scaling) -- with
+          the real exchange: all-reduce of the AC histogram, all-gather of the
+          per-block DC/strategy records, gather of the section payloads and
+          assembly on rank 0.  The codestream is byte-identical to a
+          single-GPU encode of the same frame (tests/test_gpu_shard.py).
+  replica -- every rank encodes its own 8K frame (frame-level data
+          parallelism, no data-path collective).
+Timing: barrier + synchronize on both sides of the K steps, max over ranks.
 
 The JSON line also carries:
-  roofline     -- the fused front kernel (XYB + ACS + DCT + quant): algorithmic
-                  bytes per launch / its HIP-event duration vs 8.0 TB/s, plus
-                  PMC-measured HBM traffic from profiles/ when present;
+  roofline     -- the fused front kernel (XYB + homogeneity + AQ + 8x8 ACS +
+                  DCT + quant): algorithmic bytes per launch / its HIP-event
+                  duration (its own events, on the encoder's stream) vs 8.0
+                  TB/s, plus PMC-measured HBM traffic from profiles/ when present;
   cpu_baseline -- the CPU oracle (scalar C port, 1 core) on the same frame.
 """
 import argparse
@@ -34,12 +45,18 @@ from jxg.synth import CONFIGS, SEED_BASE, synth_rgb8  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
-def front_bytes_per_launch(w, h):
-    """Algorithmic HBM bytes of one front launch: RGB8 read (3 B/px), int16
-    coefficients written (3 ch x 2 B = 6 B/px), per 8x8 block 3 x int32 DC +
-    strategy + quant field (14 B / 64 px)."""
+def front_bytes_per_launch(w, h, effort):
+    """Algorithmic HBM bytes of one front-kernel launch: RGB8 read (3 B/px),
+    int16 coefficients written (3 ch x 2 B = 6 B/px), per 8x8 block 3 x int32
+    DC + strategy + quant field + 2 B x 3 non-zero counts (20 B / 64 px); with
+    the merge stage (effort >= 5) also the XYB tile copy (12 B/px) and the
+    per-block estimate (4 B / 64 px)."""
     bxs, bys = (w + 7) // 8, (h + 7) // 8
-    return 3 * w * h + 6 * (bxs * 8) * (bys * 8) + 14 * bxs * bys
+    px = (bxs * 8) * (bys * 8)
+    b = 3 * w * h + 6 * px + 20 * bxs * bys
+    if effort >= 5:
+        b += 12 * px + 4 * bxs * bys
+    return b
 
 
 def load_pmc_traffic(workload):
@@ -76,55 +93,83 @@ def main():
     ap.add_argument("--distance", type=float, default=1.0)
     ap.add_argument("--effort", type=int, default=7)
     ap.add_argument("--proposals", type=int, default=0)
+    ap.add_argument("--mode", choices=("shard", "replica"), default="shard")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local)
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("nccl", device_id=dev)
     name, w, h, _ = CONFIGS[args.config]
-    img = synth_rgb8(w, h, SEED_BASE + args.config + rank)
-    d_img = torch.from_numpy(img).to("cuda:%d" % local)
+    shard = world > 1 and args.mode == "shard"
+    img = synth_rgb8(w, h, SEED_BASE + args.config + (0 if shard else rank))
+    d_img = torch.from_numpy(img).to(dev)
+    fh = h
+    if shard:
+        # one frame of N stacked 8K frames: every rank owns 1/N of its groups
+        fh = h * world
+        d_img = d_img.repeat(world, 1, 1).contiguous()
     torch.cuda.synchronize()
 
     enc = jxg.Encoder(distance=args.distance, effort=args.effort, proposals=args.proposals,
                       device=local)
+    bufs = {}
+
+    def step():
+        if shard:
+            from jxg.dist import encode_sharded
+            return encode_sharded(enc, d_img, w, fh, rank, world, bufs=bufs)
+        return enc.encode_device(d_img.data_ptr(), w, fh, copy=False)
+
     for _ in range(args.warmup):
-        out = enc.encode_device(d_img.data_ptr(), w, h, copy=False)
-    # front-kernel duration over the timed region (HIP events on the encoder's
-    # own stream, bracketing exactly the front launch)
+        out = step()
     front_ms = []
+    host_ms = []
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     nbytes = 0
-    host_ms = []
     for _ in range(args.steps):
-        # the codestream ends in (pinned) host memory; copy=False keeps it there
-        out = enc.encode_device(d_img.data_ptr(), w, h, copy=False)
+        # the codestream ends in (pinned) host memory on rank 0
+        out = step()
         st = enc.stats()
-        front_ms.append(st["ms_front"])
+        front_ms.append(st["ms_front_kernel"])
         host_ms.append((st["ms_host_call"], st["ms_host_codes"], st["ms_host_layout"]))
-        nbytes = len(out)
+        nbytes = len(out) if out is not None else 0
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([dt], device="cuda:%d" % local, dtype=torch.float64)
+        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     enc.close()
     if rank == 0:
         ms_step = dt * 1e3 / args.steps
-        value = w * h * world * args.steps / dt / 1e6
-        fb = front_bytes_per_launch(w, h)
+        frame_px = w * fh
+        value = frame_px * (1 if shard else world) * args.steps / dt / 1e6
+        # roofline of the front kernel over this rank's launch (its tiles)
+        fw, fhh = (w, fh // world) if shard else (w, fh)
+        fb = front_bytes_per_launch(fw, fhh, args.effort)
         fms = sum(front_ms) / len(front_ms)
-        achieved = fb / (fms * 1e-3) / 1e9
+        achieved = fb / (fms * 1e-3) / 1e9 if fms > 0 else 0.0
+        if shard:
+            workload = ("%s x%d: %dx%d RGB8 (synth_rgb8 8K frame stacked %d times), VarDCT d%g "
+                        "e%d, proposals=%d, prefix-coded, 256x256 groups sharded over %d ranks"
+                        % (name, world, w, fh, world, args.distance, args.effort,
+                           args.proposals, world))
+            par = "group-shard%d" % world
+        else:
+            workload = ("%s %dx%d RGB8 (synth_rgb8), VarDCT d%g e%d, proposals=%d, prefix-coded, "
+                        "one frame per rank" % (name, w, h, args.distance, args.effort,
+                                                args.proposals))
+            par = "frame-dp%d" % world
         res = {
             "metric": "MPix/s VarDCT encode @ d1.0, 8K RGB",
             "value": round(value, 2),
@@ -138,20 +183,19 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
-            "config": {"workload": "%s %dx%d RGB8 (synth_rgb8), VarDCT d%g e%d, proposals=%d, "
-                                   "prefix-coded, one frame per rank" % (
-                                       name, w, h, args.distance, args.effort, args.proposals),
-                       "global_batch": world, "parallelism": "frame-dp%d" % world},
+            "config": {"workload": workload, "global_batch": 1 if shard else world,
+                       "parallelism": par},
             "bytes_per_frame": nbytes,
-            "bpp": round(nbytes * 8.0 / (w * h), 4),
-            "stages_ms": {k: round(st[k], 4) for k in ("ms_front", "ms_histogram", "ms_emit",
+            "bpp": round(nbytes * 8.0 / frame_px, 4),
+            "stages_ms": {k: round(st[k], 4) for k in ("ms_front_kernel", "ms_front",
+                                                       "ms_histogram", "ms_emit",
                                                        "ms_assemble", "ms_total")},
             "host_ms": {k: round(sum(x[i] for x in host_ms) / len(host_ms), 4)
                         for i, k in enumerate(("call", "codes", "layout"))},
             "roofline": {"kernel": "front_kernel", "bound": "hbm",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": load_pmc_traffic(name),
+                         "traffic": load_pmc_traffic(name) if world == 1 else None,
                          "algorithmic_bytes": fb, "avg_ms": round(fms, 4)},
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -71,6 +71,9 @@ typedef struct {
   float ms_front, ms_histogram, ms_emit, ms_assemble, ms_total;
   /* host wall clock of the whole call and of the host-side code/header work */
   float ms_host_call, ms_host_codes, ms_host_layout;
+  /* device time of the fused front kernel alone (XYB + ACS + DCT + quant);
+   * ms_front also covers the merge stage */
+  float ms_front_kernel;
 } jxg_stats;
 
 const char* jxg_status_str(jxg_status s);
@@ -89,6 +92,34 @@ jxg_status jxg_encode_batch_rgb8(void* ctx, const uint8_t* const* rgbs, uint32_t
                                  jxg_buffer* outs);
 jxg_status jxg_get_stats(void* ctx, jxg_stats* stats);
 void jxg_buffer_free(jxg_buffer* buf);
+
+/* ---- multi-GPU group sharding (one context per rank) ----
+ * A frame is split into `world` balanced contiguous raster ranges of 256x256
+ * pass groups (rank r: groups [n*r/world, n*(r+1)/world)); LF group lg is
+ * encoded by rank lg % world.  Per rank:
+ *   1. jxg_shard_sizes: words of the AC histogram and bytes of one exchange
+ *      slot (the exchange buffer is world slots);
+ *   2. jxg_shard_begin: front end + merge stage + AC token statistics of the
+ *      rank's groups; writes the rank's AC histogram to d_hist (u32, device)
+ *      and its per-block records to slot `rank` of d_xbuf (device);
+ *   -- caller: all-reduce(sum) d_hist, all-gather d_xbuf (RCCL over xGMI);
+ *   3. jxg_shard_end: LF-group streams of its LF groups, prefix codes from the
+ *      global histogram, emission; returns a host payload with the rank's
+ *      sections (rank 0's also carries LfGlobal and HfGlobal);
+ *   -- caller: gather the payloads on rank 0;
+ *   4. jxg_shard_assemble (host only, no device): payloads of all ranks ->
+ *      codestream, byte-identical to jxg_encode_rgb8 of the whole frame.
+ * The frame needs at least max(2, world) pass groups.  Payloads and the
+ * codestream are released with jxg_buffer_free. */
+jxg_status jxg_shard_sizes(uint32_t xsize, uint32_t ysize, uint32_t world, size_t* hist_words,
+                           size_t* slot_bytes);
+jxg_status jxg_shard_begin(void* ctx, const void* d_rgb, uint32_t xsize, uint32_t ysize,
+                           size_t row_stride, uint32_t rank, uint32_t world, uint32_t* d_hist,
+                           void* d_xbuf);
+jxg_status jxg_shard_end(void* ctx, const uint32_t* d_hist, const void* d_xbuf,
+                         jxg_buffer* payload);
+jxg_status jxg_shard_assemble(const uint8_t* const* payloads, const size_t* sizes, uint32_t n,
+                              jxg_buffer* out);
 
 /* thesis selector alone over a host XYB frame [3][ysize][xsize] (xsize, ysize
  * multiples of 8): r3 = (r_h, r_v, r_d) per block, type = raw strategy

@@ -284,7 +284,7 @@ __global__ __launch_bounds__(kAcThreads) void ac_hist_kernel(AcArgs a) {
   __shared__ AcLds L;
   __shared__ uint8_t sClu[kAcCtx];
   __shared__ uint32_t sBound, sNtok[3];
-  const int g = blockIdx.x;
+  const int g = blockIdx.x + (int)a.g0;
   const GroupGeom G = group_geom(a, g);
   for (int i = threadIdx.x; i < kMaxClusters * kAcTok; i += blockDim.x) sHist[i] = 0;
   for (int i = threadIdx.x; i < kAcCtx; i += blockDim.x) sClu[i] = c_cluster[i];
@@ -334,7 +334,7 @@ __global__ __launch_bounds__(kAcThreads) void ac_emit_kernel(AcArgs a) {
   __shared__ uint32_t sBase[1024];     // bit offset of each varblock (first block)
   __shared__ uint8_t sClu[kAcCtx];
   __shared__ uint32_t sWave[kAcThreads / 64];
-  const int g = blockIdx.x;
+  const int g = blockIdx.x + (int)a.g0;
   const GroupGeom G = group_geom(a, g);
   for (int i = threadIdx.x; i < kAcCtx; i += blockDim.x) sClu[i] = c_cluster[i];
   for (int i = threadIdx.x; i < kMaxClusters * kAcTok; i += blockDim.x)
@@ -407,11 +407,12 @@ __global__ __launch_bounds__(kAcThreads) void ac_emit_kernel(AcArgs a) {
   if (threadIdx.x == 0) a.bits[g] = total;
 }
 
+// groups [a.g0, a.g0 + ngroups)
 void launch_ac_hist(const AcArgs& a, uint32_t ngroups, hipStream_t s) {
-  hipLaunchKernelGGL(ac_hist_kernel, dim3(ngroups), dim3(kAcThreads), 0, s, a);
+  if (ngroups) hipLaunchKernelGGL(ac_hist_kernel, dim3(ngroups), dim3(kAcThreads), 0, s, a);
 }
 void launch_ac_emit(const AcArgs& a, uint32_t ngroups, hipStream_t s) {
-  hipLaunchKernelGGL(ac_emit_kernel, dim3(ngroups), dim3(kAcThreads), 0, s, a);
+  if (ngroups) hipLaunchKernelGGL(ac_emit_kernel, dim3(ngroups), dim3(kAcThreads), 0, s, a);
 }
 void set_cluster_table(const uint8_t* tab, hipStream_t s) {
   (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_cluster), tab, kAcCtx, 0, hipMemcpyHostToDevice, s);

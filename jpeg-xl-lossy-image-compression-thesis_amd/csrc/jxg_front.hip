@@ -492,7 +492,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   __shared__ float sH[8][64];
   __shared__ float sR[64][3];
   const int tid = threadIdx.x;
-  const int tx = blockIdx.x, ty = blockIdx.y;
+  // a shard launches its own tiles through a list (1-D grid)
+  const int tile_id = a.tile_list ? (int)a.tile_list[blockIdx.x] : -1;
+  const int tx = tile_id >= 0 ? tile_id % (int)a.tiles_x : (int)blockIdx.x;
+  const int ty = tile_id >= 0 ? tile_id / (int)a.tiles_x : (int)blockIdx.y;
   const int ox = tx * kTile - 1, oy = ty * kTile - 1;
   if (tid < 256) {
     sLut[tid] = c_lut[tid];
@@ -731,6 +734,9 @@ void set_front_constants(const float lut[256], const float wts[3][3][64], hipStr
 }
 void launch_front(const FrontArgs& a, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s) {
   hipLaunchKernelGGL(front_kernel, dim3(tiles_x, tiles_y), dim3(kThreads), 0, s, a);
+}
+void launch_front_list(const FrontArgs& a, uint32_t ntiles, hipStream_t s) {
+  if (ntiles) hipLaunchKernelGGL(front_kernel, dim3(ntiles), dim3(kThreads), 0, s, a);
 }
 void launch_homog(const HomogArgs& a, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s) {
   hipLaunchKernelGGL(homog_kernel, dim3(tiles_x, tiles_y), dim3(kThreads), 0, s, a);

@@ -15,6 +15,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -81,7 +82,8 @@ struct PinBuf {
 // process-wide pool by jxg_buffer_free.
 struct OutHeader {
   uint64_t magic;
-  size_t cap;  // usable bytes after the header
+  size_t cap;     // usable bytes after the header
+  uint64_t heap;  // 1: plain heap block (host-only paths), 0: pinned
 };
 constexpr uint64_t kOutMagic = 0x6a78674f75744275ull;  // "jxgOutBu"
 constexpr size_t kOutHdr = 64;
@@ -110,6 +112,18 @@ static uint8_t* out_alloc(size_t bytes) {
   OutHeader* hd = static_cast<OutHeader*>(p);
   hd->magic = kOutMagic;
   hd->cap = cap;
+  hd->heap = 0;
+  return static_cast<uint8_t*>(p) + kOutHdr;
+}
+
+// host-only outputs (jxg_shard_assemble runs without a device)
+static uint8_t* out_alloc_heap(size_t bytes) {
+  void* p = std::malloc(bytes + kOutHdr);
+  if (!p) return nullptr;
+  OutHeader* hd = static_cast<OutHeader*>(p);
+  hd->magic = kOutMagic;
+  hd->cap = bytes;
+  hd->heap = 1;
   return static_cast<uint8_t*>(p) + kOutHdr;
 }
 
@@ -117,6 +131,11 @@ static void out_release(uint8_t* data) {
   if (!data) return;
   uint8_t* b = data - kOutHdr;
   if (reinterpret_cast<OutHeader*>(b)->magic != kOutMagic) return;  // not ours
+  if (reinterpret_cast<OutHeader*>(b)->heap) {
+    reinterpret_cast<OutHeader*>(b)->magic = 0;
+    std::free(b);
+    return;
+  }
   std::lock_guard<std::mutex> lk(g_pool_mu);
   if (g_pool.size() < 8) {
     g_pool.push_back(b);
@@ -397,13 +416,14 @@ struct Ctx {
   DevBuf<uint32_t> hist_ac, bound, ntok, codes_ac, gbits, lfhist, sbound, lfcodes, chunkbits,
       stream_chunks, stream_bits, scratch, chunks, out;
   DevBuf<uint64_t> gbase, chunkoff, stream_base;
+  DevBuf<uint32_t> tile_list;
   DevBuf<LfRow> rows;
   DevBuf<LfChunk> lfchunks;
   DevBuf<ConcatPiece> pieces;
   // host
   PinBuf<uint32_t> h_hist_ac, h_bound, h_ntok, h_lfhist, h_sbound, h_gbits, h_sbits, h_vcount;
-  // LF row segments cached per frame size
-  uint32_t rows_w = 0, rows_h = 0;
+  // LF row segments cached per frame size and shard
+  uint32_t rows_w = 0, rows_h = 0, rows_rank = 0, rows_world = 1;
   std::vector<LfRow> rows_h_cache;
   std::vector<LfChunk> chunks_h_cache;
   std::vector<uint32_t> schunks_cache;
@@ -416,6 +436,7 @@ struct Ctx {
   std::vector<uint32_t> m_ntok;
   std::vector<float> m_homog;
   jxg_stats stats{};
+  std::unique_ptr<struct Job> job;  // sharded encode in flight (begin -> end)
 };
 
 static jxg_status init_constants(Ctx* c) {
@@ -442,12 +463,44 @@ static jxg_status init_constants(Ctx* c) {
   return JXG_OK;
 }
 
-// LF-group row segments: (lf group, stream, channel, y, x0) in stream order
+// ---------------------------------------------------------------------------
+// Work plan: which tiles, pass groups and LF groups this context encodes.
+// world == 1: everything.  Sharded: rank r owns the balanced
+// contiguous raster range of pass groups [ngroups*r/world, ngroups*(r+1)/world)
+// (and the 64x64 tiles inside them) and the LF groups lg with lg % world == r.
+// ---------------------------------------------------------------------------
+struct Plan {
+  uint32_t rank = 0, world = 1, g0 = 0, g1 = 0;
+  std::vector<uint32_t> tiles;  // shard: owned tile ids (ty * tiles_x + tx)
+  bool owns_lf(uint32_t lg) const { return world == 1 || lg % world == rank; }
+};
+static uint32_t shard_g0(uint32_t ngroups, uint32_t r, uint32_t world) {
+  return (uint32_t)(((uint64_t)ngroups * r) / world);
+}
+static Plan make_plan(const Frame& f, uint32_t rank, uint32_t world) {
+  Plan P;
+  P.rank = rank;
+  P.world = world;
+  P.g0 = shard_g0(f.ngroups, rank, world);
+  P.g1 = shard_g0(f.ngroups, rank + 1, world);
+  if (world > 1)
+    for (uint32_t g = P.g0; g < P.g1; g++) {
+      const uint32_t gx = g % f.gxs, gy = g / f.gxs;
+      for (uint32_t ty = gy * 4; ty < std::min(gy * 4 + 4, f.tiles_y); ty++)
+        for (uint32_t tx = gx * 4; tx < std::min(gx * 4 + 4, f.tiles_x); tx++)
+          P.tiles.push_back(ty * f.tiles_x + tx);
+    }
+  return P;
+}
+// exchange record of one pass group (jxg_shard.hip): acs, qf, 3 x int32 DC
+constexpr size_t kGroupRecordBytes = 1024 * 2 + 1024 * 4 * 3;
+
 // LF-group row segments: (lf group, stream, channel, y, x0) in stream order,
 // grouped into chunks of one stream (<= kLfChunkSamples samples,
-// <= kLfChunkRows segments)
-static void build_rows(const Frame& f, std::vector<LfRow>& rows, std::vector<LfChunk>& chunks,
-                       std::vector<uint32_t>& schunks) {
+// <= kLfChunkRows segments); only the plan's LF groups get rows (the stream
+// table keeps an empty range for the others)
+static void build_rows(const Frame& f, const Plan& P, std::vector<LfRow>& rows,
+                       std::vector<LfChunk>& chunks, std::vector<uint32_t>& schunks) {
   rows.clear();
   chunks.clear();
   schunks.clear();
@@ -466,15 +519,19 @@ static void build_rows(const Frame& f, std::vector<LfRow>& rows, std::vector<LfC
   for (uint32_t lg = 0; lg < f.nlf; lg++) {
     const uint32_t bx0 = (lg % f.lfxs) * 256, by0 = (lg / f.lfxs) * 256;
     const uint32_t bw = std::min(256u, f.bxs - bx0), bh = std::min(256u, f.bys - by0);
+    const bool own = P.owns_lf(lg);
     schunks.push_back((uint32_t)chunks.size());
-    for (uint16_t ch = 0; ch < 3; ch++)
-      for (uint32_t y = 0; y < bh; y++) add(lg, 0, ch, y, bw);
+    if (own)
+      for (uint16_t ch = 0; ch < 3; ch++)
+        for (uint32_t y = 0; y < bh; y++) add(lg, 0, ch, y, bw);
     schunks.push_back((uint32_t)chunks.size());
-    const uint32_t cw = (bw + 7) / 8, chh = (bh + 7) / 8;
-    for (uint16_t ch = 0; ch < 2; ch++)
-      for (uint32_t y = 0; y < chh; y++) add(lg, 1, ch, y, cw);
-    for (uint32_t y = 0; y < 2; y++) add(lg, 1, 2, y, bw * bh);
-    for (uint32_t y = 0; y < bh; y++) add(lg, 1, 3, y, bw);
+    if (own) {
+      const uint32_t cw = (bw + 7) / 8, chh = (bh + 7) / 8;
+      for (uint16_t ch = 0; ch < 2; ch++)
+        for (uint32_t y = 0; y < chh; y++) add(lg, 1, ch, y, cw);
+      for (uint32_t y = 0; y < 2; y++) add(lg, 1, 2, y, bw * bh);
+      for (uint32_t y = 0; y < bh; y++) add(lg, 1, 3, y, bw);
+    }
   }
   schunks.push_back((uint32_t)chunks.size());
 }
@@ -485,13 +542,32 @@ static float elapsed(hipEvent_t a, hipEvent_t b) {
   return ms;
 }
 
-static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32_t h,
-                                size_t stride, jxg_buffer* out, Clock::time_point t_call) {
+// state carried between the stages of one encode
+struct Job {
+  Frame f;
+  Plan plan;
+  uint32_t w = 0, h = 0;
+  size_t stride = 0;
+  const uint8_t* d_rgb = nullptr;
+  int max_s = 0;
+  bool homog = false;
+  uint32_t nrows = 0, nchunks = 0, nstreams = 0;
+  AcArgs aa{};
+  LfArgs la{};
+  // host stage results
+  std::vector<BitWriter> preA, preB;
+  BitWriter lfglobal, hfglobal;
+  std::vector<uint64_t> gbase, sbase;
+  float ms_codes = 0.0f;
+};
+
+// ---- stage A: buffers for the frame / plan ----
+static jxg_status stage_alloc(Ctx* c, Job& J) {
   hipStream_t s = c->stream;
   const jxg_params& P = c->params;
-  const Frame f = make_frame(w, h, P.distance);
+  const Frame& f = J.f;
   const size_t nb = (size_t)f.bxs * f.bys;
-  const bool homog = (P.proposals & 3u) != 0;
+  J.homog = (P.proposals & 3u) != 0;
   jxg_status st = init_constants(c);
   if (st) return st;
   JXG_HIP(c->acs.ensure(nb));
@@ -499,13 +575,18 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   JXG_HIP(c->nz.ensure(nb * 3));
   JXG_HIP(c->dc.ensure(nb * 3));
   JXG_HIP(c->ac.ensure(nb * 192));
-  if (homog) JXG_HIP(c->homog.ensure(nb * 3));
-  const int max_s = P.effort >= 6 ? 8 : (P.effort >= 5 ? 4 : 0);  // merge levels
+  if (J.homog) JXG_HIP(c->homog.ensure(nb * 3));
+  J.max_s = P.effort >= 6 ? 8 : (P.effort >= 5 ? 4 : 0);  // merge levels
   const uint32_t ntiles = f.tiles_x * f.tiles_y;
-  if (max_s) {
+  if (J.max_s) {
     JXG_HIP(c->ent.ensure(nb));
     JXG_HIP(c->xyb_tiles.ensure((size_t)ntiles * 3 * 4096));
     JXG_HIP(c->mcost.ensure((size_t)ntiles * kNumShapes * 32));
+  }
+  if (!J.plan.tiles.empty()) {
+    JXG_HIP(c->tile_list.ensure(J.plan.tiles.size()));
+    JXG_HIP(hipMemcpyAsync(c->tile_list.p, J.plan.tiles.data(), J.plan.tiles.size() * 4,
+                           hipMemcpyHostToDevice, s));
   }
   JXG_HIP(c->vb.ensure((size_t)f.nlf * 65536));
   JXG_HIP(c->vcount.ensure(f.nlf));
@@ -516,25 +597,26 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   JXG_HIP(c->ntok.ensure(f.ngroups * 3));
   JXG_HIP(c->gbits.ensure(f.ngroups));
   JXG_HIP(c->gbase.ensure(f.ngroups));
-  const uint32_t nstreams = f.nlf * 2;
-  const bool new_rows = c->rows_w != w || c->rows_h != h;
+  J.nstreams = f.nlf * 2;
+  const bool new_rows = c->rows_w != J.w || c->rows_h != J.h || c->rows_rank != J.plan.rank ||
+                        c->rows_world != J.plan.world;
   if (new_rows) {
-    build_rows(f, c->rows_h_cache, c->chunks_h_cache, c->schunks_cache);
-    c->rows_w = w;
-    c->rows_h = h;
+    build_rows(f, J.plan, c->rows_h_cache, c->chunks_h_cache, c->schunks_cache);
+    c->rows_w = J.w;
+    c->rows_h = J.h;
+    c->rows_rank = J.plan.rank;
+    c->rows_world = J.plan.world;
   }
-  const std::vector<LfRow>& rows = c->rows_h_cache;
-  const std::vector<LfChunk>& lchunks = c->chunks_h_cache;
-  const std::vector<uint32_t>& schunks = c->schunks_cache;
-  const uint32_t nrows = (uint32_t)rows.size();
-  const uint32_t nchunks = (uint32_t)lchunks.size();
-  JXG_HIP(c->rows.ensure(nrows));
-  JXG_HIP(c->lfchunks.ensure(nchunks));
+  J.nrows = (uint32_t)c->rows_h_cache.size();
+  J.nchunks = (uint32_t)c->chunks_h_cache.size();
+  const uint32_t nstreams = J.nstreams;
+  JXG_HIP(c->rows.ensure(J.nrows));
+  JXG_HIP(c->lfchunks.ensure(J.nchunks));
   JXG_HIP(c->lfhist.ensure(nstreams * 4 * kAlpha));
   JXG_HIP(c->lfcodes.ensure(nstreams * 4 * kAlpha));
   JXG_HIP(c->sbound.ensure(nstreams));
-  JXG_HIP(c->chunkbits.ensure(nchunks));
-  JXG_HIP(c->chunkoff.ensure(nchunks));
+  JXG_HIP(c->chunkbits.ensure(J.nchunks));
+  JXG_HIP(c->chunkoff.ensure(J.nchunks));
   JXG_HIP(c->stream_chunks.ensure(nstreams + 1));
   JXG_HIP(c->stream_base.ensure(nstreams));
   JXG_HIP(c->stream_bits.ensure(nstreams));
@@ -546,20 +628,64 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   JXG_HIP(c->h_gbits.ensure(f.ngroups));
   JXG_HIP(c->h_sbits.ensure(nstreams));
   if (new_rows) {
-    JXG_HIP(hipMemcpyAsync(c->rows.p, rows.data(), nrows * sizeof(LfRow), hipMemcpyHostToDevice, s));
-    JXG_HIP(hipMemcpyAsync(c->lfchunks.p, lchunks.data(), nchunks * sizeof(LfChunk),
-                           hipMemcpyHostToDevice, s));
-    JXG_HIP(hipMemcpyAsync(c->stream_chunks.p, schunks.data(), schunks.size() * 4,
-                           hipMemcpyHostToDevice, s));
+    if (J.nrows)
+      JXG_HIP(hipMemcpyAsync(c->rows.p, c->rows_h_cache.data(), J.nrows * sizeof(LfRow),
+                             hipMemcpyHostToDevice, s));
+    if (J.nchunks)
+      JXG_HIP(hipMemcpyAsync(c->lfchunks.p, c->chunks_h_cache.data(), J.nchunks * sizeof(LfChunk),
+                             hipMemcpyHostToDevice, s));
+    JXG_HIP(hipMemcpyAsync(c->stream_chunks.p, c->schunks_cache.data(),
+                           c->schunks_cache.size() * 4, hipMemcpyHostToDevice, s));
   }
+  // kernel argument blocks
+  AcArgs& aa = J.aa;
+  aa = AcArgs{};
+  aa.acs = c->acs.p;
+  aa.ac = c->ac.p;
+  aa.nz = c->nz.p;
+  aa.bxs = f.bxs;
+  aa.bys = f.bys;
+  aa.gxs = f.gxs;
+  aa.g0 = J.plan.g0;
+  aa.hist = c->hist_ac.p;
+  aa.bound = c->bound.p;
+  aa.ntok = c->ntok.p;
+  aa.codes = c->codes_ac.p;
+  aa.base = c->gbase.p;
+  aa.bits = c->gbits.p;
+  LfArgs& la = J.la;
+  la = LfArgs{};
+  la.rows = c->rows.p;
+  la.chunks = c->lfchunks.p;
+  la.dc = c->dc.p;
+  la.acs = c->acs.p;
+  la.qf = c->qf.p;
+  la.vb = c->vb.p;
+  la.vcount = c->vcount.p;
+  la.bxs = f.bxs;
+  la.bys = f.bys;
+  la.lfxs = f.lfxs;
+  la.hist = c->lfhist.p;
+  la.sbound = c->sbound.p;
+  la.codes = c->lfcodes.p;
+  la.chunk_bits = c->chunkbits.p;
+  la.chunk_off = c->chunkoff.p;
+  la.stream_chunks = c->stream_chunks.p;
+  la.stream_base = c->stream_base.p;
+  la.stream_bits = c->stream_bits.p;
+  return JXG_OK;
+}
 
-  // ---------------- stage 1: front end ----------------
-  JXG_HIP(hipEventRecord(c->ev[0], s));
+// ---- stage B: front end + merge stage over the plan's tiles ----
+static jxg_status stage_front(Ctx* c, Job& J) {
+  hipStream_t s = c->stream;
+  const jxg_params& P = c->params;
+  const Frame& f = J.f;
   FrontArgs fa{};
-  fa.rgb = d_rgb;
-  fa.w = w;
-  fa.h = h;
-  fa.stride = stride;
+  fa.rgb = J.d_rgb;
+  fa.w = J.w;
+  fa.h = J.h;
+  fa.stride = J.stride;
   fa.bxs = f.bxs;
   fa.bys = f.bys;
   fa.xp = f.xp;
@@ -581,27 +707,34 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   fa.dc = c->dc.p;
   fa.ac = c->ac.p;
   fa.nz = c->nz.p;
-  fa.homog = homog ? c->homog.p : nullptr;
-  fa.ent = max_s ? c->ent.p : nullptr;
-  fa.xyb_out = max_s ? c->xyb_tiles.p : nullptr;
-  launch_front(fa, f.tiles_x, f.tiles_y, s);
+  fa.homog = J.homog ? c->homog.p : nullptr;
+  fa.ent = J.max_s ? c->ent.p : nullptr;
+  fa.xyb_out = J.max_s ? c->xyb_tiles.p : nullptr;
+  const bool listed = !J.plan.tiles.empty();
+  fa.tile_list = listed ? c->tile_list.p : nullptr;
+  if (listed)
+    launch_front_list(fa, (uint32_t)J.plan.tiles.size(), s);
+  else if (J.plan.world == 1)
+    launch_front(fa, f.tiles_x, f.tiles_y, s);
   JXG_HIP(hipGetLastError());
-  if (max_s) {
+  JXG_HIP(hipEventRecord(c->ev[5], s));  // end of the front kernel alone
+  if (J.max_s) {
     MergeArgs ma{};
     ma.xyb = c->xyb_tiles.p;
     ma.bxs = f.bxs;
     ma.bys = f.bys;
     ma.tiles_x = f.tiles_x;
-    ma.ntiles = ntiles;
+    ma.ntiles = listed ? (uint32_t)J.plan.tiles.size() : (J.plan.world == 1 ? f.tiles_x * f.tiles_y : 0);
+    ma.tile_list = listed ? c->tile_list.p : nullptr;
     ma.proposals = P.proposals;
-    ma.max_s = max_s;
+    ma.max_s = J.max_s;
     ma.G = f.G;
     for (int i = 0; i < 3; i++) {
       ma.dc_mul[i] = f.dc_mul[i];
       ma.dc_step[i] = f.dc_step[i];
     }
     ma.ent = c->ent.p;
-    ma.homog = homog ? c->homog.p : nullptr;
+    ma.homog = J.homog ? c->homog.p : nullptr;
     ma.acs = c->acs.p;
     ma.qf = c->qf.p;
     ma.dc = c->dc.p;
@@ -614,51 +747,36 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
     launch_merge(ma, s);
     JXG_HIP(hipGetLastError());
   }
-  VbArgs va{c->acs.p, f.bxs, f.bys, f.lfxs, c->vb.p, c->vcount.p};
-  launch_vb_list(va, f.nlf, s);
-  JXG_HIP(hipGetLastError());
-  JXG_HIP(hipEventRecord(c->ev[1], s));
+  return JXG_OK;
+}
 
-  // ---------------- stage 2: statistics ----------------
-  JXG_HIP(hipMemsetAsync(c->hist_ac.p, 0, kMaxClusters * kAlpha * 4, s));
-  JXG_HIP(hipMemsetAsync(c->lfhist.p, 0, (size_t)nstreams * 4 * kAlpha * 4, s));
-  JXG_HIP(hipMemsetAsync(c->sbound.p, 0, nstreams * 4, s));
-  AcArgs aa{};
-  aa.acs = c->acs.p;
-  aa.ac = c->ac.p;
-  aa.nz = c->nz.p;
-  aa.bxs = f.bxs;
-  aa.bys = f.bys;
-  aa.gxs = f.gxs;
-  aa.hist = c->hist_ac.p;
-  aa.bound = c->bound.p;
-  aa.ntok = c->ntok.p;
-  aa.codes = c->codes_ac.p;
-  aa.base = c->gbase.p;
-  aa.bits = c->gbits.p;
-  launch_ac_hist(aa, f.ngroups, s);
-  LfArgs la{};
-  la.rows = c->rows.p;
-  la.chunks = c->lfchunks.p;
-  la.dc = c->dc.p;
-  la.acs = c->acs.p;
-  la.qf = c->qf.p;
-  la.vb = c->vb.p;
-  la.vcount = c->vcount.p;
-  la.bxs = f.bxs;
-  la.bys = f.bys;
-  la.lfxs = f.lfxs;
-  la.hist = c->lfhist.p;
-  la.sbound = c->sbound.p;
-  la.codes = c->lfcodes.p;
-  la.chunk_bits = c->chunkbits.p;
-  la.chunk_off = c->chunkoff.p;
-  la.stream_chunks = c->stream_chunks.p;
-  la.stream_base = c->stream_base.p;
-  la.stream_bits = c->stream_bits.p;
-  launch_lf_hist(la, nchunks, s);
+// ---- stage C: AC token statistics of the plan's pass groups ----
+static jxg_status stage_ac_stats(Ctx* c, Job& J) {
+  JXG_HIP(hipMemsetAsync(c->hist_ac.p, 0, kMaxClusters * kAlpha * 4, c->stream));
+  launch_ac_hist(J.aa, J.plan.g1 - J.plan.g0, c->stream);
   JXG_HIP(hipGetLastError());
-  JXG_HIP(hipMemcpyAsync(c->h_hist_ac.p, c->hist_ac.p, kMaxClusters * kAlpha * 4, hipMemcpyDeviceToHost, s));
+  return JXG_OK;
+}
+
+// ---- stage D: LF-group statistics (varblock lists, modular histograms) ----
+static jxg_status stage_lf_stats(Ctx* c, Job& J) {
+  hipStream_t s = c->stream;
+  const Frame& f = J.f;
+  VbArgs va{c->acs.p, f.bxs, f.bys, f.lfxs, J.plan.rank, J.plan.world, c->vb.p, c->vcount.p};
+  launch_vb_list(va, f.nlf, s);
+  JXG_HIP(hipMemsetAsync(c->lfhist.p, 0, (size_t)J.nstreams * 4 * kAlpha * 4, s));
+  JXG_HIP(hipMemsetAsync(c->sbound.p, 0, J.nstreams * 4, s));
+  if (J.nchunks) launch_lf_hist(J.la, J.nchunks, s);
+  JXG_HIP(hipGetLastError());
+  return JXG_OK;
+}
+
+// ---- stage E: statistics to the host (AC histogram from `hist`) ----
+static jxg_status stage_download(Ctx* c, Job& J, const uint32_t* hist) {
+  hipStream_t s = c->stream;
+  const Frame& f = J.f;
+  const uint32_t nstreams = J.nstreams;
+  JXG_HIP(hipMemcpyAsync(c->h_hist_ac.p, hist, kMaxClusters * kAlpha * 4, hipMemcpyDeviceToHost, s));
   JXG_HIP(hipMemcpyAsync(c->h_bound.p, c->bound.p, f.ngroups * 4, hipMemcpyDeviceToHost, s));
   JXG_HIP(hipMemcpyAsync(c->h_ntok.p, c->ntok.p, f.ngroups * 12, hipMemcpyDeviceToHost, s));
   JXG_HIP(hipMemcpyAsync(c->h_lfhist.p, c->lfhist.p, (size_t)nstreams * 4 * kAlpha * 4, hipMemcpyDeviceToHost, s));
@@ -666,8 +784,15 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   JXG_HIP(hipMemcpyAsync(c->h_vcount.p, c->vcount.p, f.nlf * 4, hipMemcpyDeviceToHost, s));
   JXG_HIP(hipEventRecord(c->ev[2], s));
   JXG_HIP(hipStreamSynchronize(s));
+  return JXG_OK;
+}
 
-  // ---------------- host: codes and header sections ----------------
+// ---- stage F (host): prefix codes, LF preludes, LfGlobal / HfGlobal,
+// scratch layout for the plan's groups and streams ----
+static jxg_status stage_codes(Ctx* c, Job& J) {
+  hipStream_t s = c->stream;
+  const Frame& f = J.f;
+  const uint32_t nstreams = J.nstreams;
   const Clock::time_point t_codes = Clock::now();
   int dense[kMaxClusters];
   std::fill(dense, dense + kMaxClusters, -1);
@@ -691,10 +816,12 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
     codes[dense[cl]] = build_prefix_code(c->h_hist_ac.p + cl * kAlpha, kAlpha);
     for (int k = 0; k < kAlpha; k++) packed[cl * kAlpha + k] = codes[dense[cl]].packed(k);
   }
-  // LF-group stream codes and preludes
+  // LF-group stream codes and preludes (the plan's LF groups)
   std::vector<uint32_t> lfpacked((size_t)nstreams * 4 * kAlpha, 0);
-  std::vector<BitWriter> preA(f.nlf), preB(f.nlf);
+  J.preA.assign(f.nlf, BitWriter());
+  J.preB.assign(f.nlf, BitWriter());
   for (uint32_t lg = 0; lg < f.nlf; lg++) {
+    if (!J.plan.owns_lf(lg)) continue;
     const uint32_t bx0 = (lg % f.lfxs) * 256, by0 = (lg / f.lfxs) * 256;
     const uint32_t bw = std::min(256u, f.bxs - bx0), bh = std::min(256u, f.bys - by0);
     for (int sidx = 0; sidx < 2; sidx++) {
@@ -706,86 +833,106 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
         for (int k = 0; k < kAlpha; k++) lfpacked[((size_t)sid * 4 + l) * kAlpha + k] = lc[l].packed(k);
       }
       if (sidx == 0) {
-        preA[lg].put(2, 0);  // extra_precision
-        write_modular_prelude(preA[lg], kDcTree, 5, 3, lc);
+        J.preA[lg].put(2, 0);  // extra_precision
+        write_modular_prelude(J.preA[lg], kDcTree, 5, 3, lc);
       } else {
-        preB[lg].put(ceil_log2(bw * bh), c->h_vcount.p[lg] - 1);  // varblock count - 1
-        write_modular_prelude(preB[lg], kMetaTree, 7, 4, lc);
+        J.preB[lg].put(ceil_log2(bw * bh), c->h_vcount.p[lg] - 1);  // varblock count - 1
+        write_modular_prelude(J.preB[lg], kMetaTree, 7, 4, lc);
       }
     }
   }
-  BitWriter lfglobal, hfglobal;
-  lfglobal.put(1, 1);  // LfChannelDequantization.all_default
-  if (f.G <= 2048)
-    write_u32_sel(lfglobal, 0, 11, f.G - 1);
-  else if (f.G <= 4096)
-    write_u32_sel(lfglobal, 1, 11, f.G - 2049);
-  else if (f.G <= 8192)
-    write_u32_sel(lfglobal, 2, 12, f.G - 4097);
-  else
-    write_u32_sel(lfglobal, 3, 16, f.G - 8193);
-  if (f.qdc == 16)
-    lfglobal.put(2, 0);
-  else if (f.qdc <= 32)
-    write_u32_sel(lfglobal, 1, 5, f.qdc - 1);
-  else if (f.qdc <= 256)
-    write_u32_sel(lfglobal, 2, 8, f.qdc - 1);
-  else
-    write_u32_sel(lfglobal, 3, 16, f.qdc - 1);
-  lfglobal.put(1, 1);  // BlockCtxMap default
-  lfglobal.put(1, 1);  // colour correlation default
-  lfglobal.put(1, 0);  // GlobalModular: no tree, no channels
-  hfglobal.put(1, 1);  // DequantMatrices all_default
-  hfglobal.put(ceil_log2(f.ngroups), 0);  // num_hf_presets - 1
-  write_u32_sel(hfglobal, 2, 0, 0);        // used_orders = 0
-  if (nhist != c->cm_nhist || ctxmap != c->cm_last) {
-    c->cm_bits = BitWriter();
-    write_context_map(c->cm_bits, ctxmap, nhist);
-    c->cm_last = ctxmap;
-    c->cm_nhist = nhist;
+  J.lfglobal = BitWriter();
+  J.hfglobal = BitWriter();
+  if (J.plan.rank == 0) {
+    BitWriter& lfglobal = J.lfglobal;
+    BitWriter& hfglobal = J.hfglobal;
+    lfglobal.put(1, 1);  // LfChannelDequantization.all_default
+    if (f.G <= 2048)
+      write_u32_sel(lfglobal, 0, 11, f.G - 1);
+    else if (f.G <= 4096)
+      write_u32_sel(lfglobal, 1, 11, f.G - 2049);
+    else if (f.G <= 8192)
+      write_u32_sel(lfglobal, 2, 12, f.G - 4097);
+    else
+      write_u32_sel(lfglobal, 3, 16, f.G - 8193);
+    if (f.qdc == 16)
+      lfglobal.put(2, 0);
+    else if (f.qdc <= 32)
+      write_u32_sel(lfglobal, 1, 5, f.qdc - 1);
+    else if (f.qdc <= 256)
+      write_u32_sel(lfglobal, 2, 8, f.qdc - 1);
+    else
+      write_u32_sel(lfglobal, 3, 16, f.qdc - 1);
+    lfglobal.put(1, 1);  // BlockCtxMap default
+    lfglobal.put(1, 1);  // colour correlation default
+    lfglobal.put(1, 0);  // GlobalModular: no tree, no channels
+    hfglobal.put(1, 1);  // DequantMatrices all_default
+    hfglobal.put(ceil_log2(f.ngroups), 0);  // num_hf_presets - 1
+    write_u32_sel(hfglobal, 2, 0, 0);        // used_orders = 0
+    if (nhist != c->cm_nhist || ctxmap != c->cm_last) {
+      c->cm_bits = BitWriter();
+      write_context_map(c->cm_bits, ctxmap, nhist);
+      c->cm_last = ctxmap;
+      c->cm_nhist = nhist;
+    }
+    write_histograms(hfglobal, ctxmap, nhist, codes, kCfg420, &c->cm_bits);
   }
-  write_histograms(hfglobal, ctxmap, nhist, codes, kCfg420, &c->cm_bits);
-
-  // scratch layout: AC groups then LF streams (32-bit aligned regions)
-  std::vector<uint64_t> gbase(f.ngroups), sbase(nstreams);
+  // scratch layout: the plan's AC groups then LF streams (32-bit aligned)
+  J.gbase.assign(f.ngroups, 0);
+  J.sbase.assign(nstreams, 0);
   uint64_t cursor = 0;
-  for (uint32_t g = 0; g < f.ngroups; g++) {
-    gbase[g] = cursor;
+  for (uint32_t g = J.plan.g0; g < J.plan.g1; g++) {
+    J.gbase[g] = cursor;
     cursor += ((uint64_t)c->h_bound.p[g] + 63) & ~31ull;
   }
   for (uint32_t i = 0; i < nstreams; i++) {
-    sbase[i] = cursor;
-    cursor += ((uint64_t)c->h_sbound.p[i] + 63) & ~31ull;
+    J.sbase[i] = cursor;
+    if (J.plan.owns_lf(i / 2)) cursor += ((uint64_t)c->h_sbound.p[i] + 63) & ~31ull;
   }
   const uint64_t scratch_words = cursor / 32 + 2;
-  const float ms_codes = ms_since(t_codes);
+  J.ms_codes = ms_since(t_codes);
   JXG_HIP(c->scratch.ensure(scratch_words));
   JXG_HIP(hipMemcpyAsync(c->codes_ac.p, packed.data(), packed.size() * 4, hipMemcpyHostToDevice, s));
   JXG_HIP(hipMemcpyAsync(c->lfcodes.p, lfpacked.data(), lfpacked.size() * 4, hipMemcpyHostToDevice, s));
-  JXG_HIP(hipMemcpyAsync(c->gbase.p, gbase.data(), gbase.size() * 8, hipMemcpyHostToDevice, s));
-  JXG_HIP(hipMemcpyAsync(c->stream_base.p, sbase.data(), sbase.size() * 8, hipMemcpyHostToDevice, s));
+  JXG_HIP(hipMemcpyAsync(c->gbase.p, J.gbase.data(), J.gbase.size() * 8, hipMemcpyHostToDevice, s));
+  JXG_HIP(hipMemcpyAsync(c->stream_base.p, J.sbase.data(), J.sbase.size() * 8, hipMemcpyHostToDevice, s));
   JXG_HIP(hipMemsetAsync(c->scratch.p, 0, scratch_words * 4, s));
+  return JXG_OK;
+}
 
-  // ---------------- stage 3: emission ----------------
-  aa.scratch = c->scratch.p;
-  la.scratch = c->scratch.p;
-  launch_ac_emit(aa, f.ngroups, s);
-  launch_lf_bits(la, nchunks, s);
-  launch_lf_scan(la, nstreams, s);
-  launch_lf_emit(la, nchunks, s);
+// ---- stage G: bit emission ----
+static jxg_status stage_emit(Ctx* c, Job& J) {
+  hipStream_t s = c->stream;
+  const Frame& f = J.f;
+  J.aa.scratch = c->scratch.p;
+  J.la.scratch = c->scratch.p;
+  launch_ac_emit(J.aa, J.plan.g1 - J.plan.g0, s);
+  if (J.nchunks) launch_lf_bits(J.la, J.nchunks, s);
+  launch_lf_scan(J.la, J.nstreams, s);
+  if (J.nchunks) launch_lf_emit(J.la, J.nchunks, s);
   JXG_HIP(hipGetLastError());
   JXG_HIP(hipMemcpyAsync(c->h_gbits.p, c->gbits.p, f.ngroups * 4, hipMemcpyDeviceToHost, s));
-  JXG_HIP(hipMemcpyAsync(c->h_sbits.p, c->stream_bits.p, nstreams * 4, hipMemcpyDeviceToHost, s));
+  JXG_HIP(hipMemcpyAsync(c->h_sbits.p, c->stream_bits.p, J.nstreams * 4, hipMemcpyDeviceToHost, s));
   JXG_HIP(hipEventRecord(c->ev[3], s));
   JXG_HIP(hipStreamSynchronize(s));
+  return JXG_OK;
+}
 
-  // ---------------- host: layout, TOC, pieces ----------------
-  const Clock::time_point t_layout = Clock::now();
-  struct Piece {
-    int arena;  // 0 scratch, 1 host chunk
-    uint64_t src, nbits;
-  };
+// ---- stage H: concatenation.  Sections are bit-exact piece lists (host
+// chunks + device scratch ranges).  full: headers + TOC + all sections into
+// one codestream; shard: the plan's sections, each byte-aligned, back to back
+// (`section_ids` receives their TOC indices) ----
+struct Piece {
+  int arena;  // 0 scratch, 1 host chunk
+  uint64_t src, nbits;
+};
+static jxg_status stage_concat(Ctx* c, Job& J, bool full, std::vector<uint32_t>* section_ids,
+                               std::vector<uint32_t>* section_bytes, uint8_t** host_out,
+                               size_t* out_bytes) {
+  hipStream_t s = c->stream;
+  const Frame& f = J.f;
   std::vector<std::vector<Piece>> sections;
+  std::vector<uint32_t> ids;
   std::vector<uint32_t> chunk_words;
   auto add_chunk = [&](const BitWriter& bw) -> Piece {
     Piece p{1, (uint64_t)chunk_words.size() * 32, bw.bits()};
@@ -793,14 +940,26 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
     chunk_words.insert(chunk_words.end(), wv.begin(), wv.end());
     return p;
   };
-  sections.push_back({add_chunk(lfglobal)});
-  for (uint32_t lg = 0; lg < f.nlf; lg++) {
-    sections.push_back({add_chunk(preA[lg]), Piece{0, sbase[lg * 2], c->h_sbits.p[lg * 2]},
-                        add_chunk(preB[lg]), Piece{0, sbase[lg * 2 + 1], c->h_sbits.p[lg * 2 + 1]}});
+  if (J.plan.rank == 0) {
+    sections.push_back({add_chunk(J.lfglobal)});
+    ids.push_back(0);
   }
-  sections.push_back({add_chunk(hfglobal)});
-  for (uint32_t g = 0; g < f.ngroups; g++) sections.push_back({Piece{0, gbase[g], c->h_gbits.p[g]}});
-  const bool single = f.ngroups == 1;
+  for (uint32_t lg = 0; lg < f.nlf; lg++) {
+    if (!J.plan.owns_lf(lg)) continue;
+    sections.push_back({add_chunk(J.preA[lg]), Piece{0, J.sbase[lg * 2], c->h_sbits.p[lg * 2]},
+                        add_chunk(J.preB[lg]),
+                        Piece{0, J.sbase[lg * 2 + 1], c->h_sbits.p[lg * 2 + 1]}});
+    ids.push_back(1 + lg);
+  }
+  if (J.plan.rank == 0) {
+    sections.push_back({add_chunk(J.hfglobal)});
+    ids.push_back(1 + f.nlf);
+  }
+  for (uint32_t g = J.plan.g0; g < J.plan.g1; g++) {
+    sections.push_back({Piece{0, J.gbase[g], c->h_gbits.p[g]}});
+    ids.push_back(2 + f.nlf + g);
+  }
+  const bool single = full && f.ngroups == 1;
   std::vector<uint32_t> sizes;
   if (single) {
     uint64_t total = 0;
@@ -814,10 +973,6 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
       sizes.push_back((uint32_t)((t + 7) / 8));
     }
   }
-  BitWriter head;
-  write_headers(head, w, h);
-  write_toc(head, sizes);
-  const Piece head_piece = add_chunk(head);
   std::vector<ConcatPiece> cps;
   uint64_t dst = 0, max_words = 0;
   auto emit_piece = [&](const Piece& p) {
@@ -827,31 +982,71 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
     }
     dst += p.nbits;
   };
-  emit_piece(head_piece);
+  if (full) {
+    BitWriter head;
+    write_headers(head, J.w, J.h);
+    write_toc(head, sizes);
+    emit_piece(add_chunk(head));
+  }
   for (auto& sec : sections) {
     for (auto& p : sec) emit_piece(p);
     if (!single) dst = (dst + 7) & ~7ull;
   }
   dst = (dst + 7) & ~7ull;
-  const size_t out_bytes = (size_t)(dst / 8);
-  const size_t out_words = (out_bytes + 3) / 4 + 1;
+  const size_t nbytes = (size_t)(dst / 8);
+  const size_t out_words = (nbytes + 3) / 4 + 1;
   chunk_words.push_back(0);  // read-ahead guard
   JXG_HIP(c->chunks.ensure(chunk_words.size()));
-  JXG_HIP(c->pieces.ensure(cps.size()));
+  JXG_HIP(c->pieces.ensure(std::max<size_t>(cps.size(), 1)));
   JXG_HIP(c->out.ensure(out_words));
-  uint8_t* host_out = out_alloc(out_words * 4);
-  if (!host_out) return JXG_ERR_OOM;
-  const float ms_layout = ms_since(t_layout);
+  uint8_t* ho = out_alloc(out_words * 4);
+  if (!ho) return JXG_ERR_OOM;
   JXG_HIP(hipMemcpyAsync(c->chunks.p, chunk_words.data(), chunk_words.size() * 4, hipMemcpyHostToDevice, s));
-  JXG_HIP(hipMemcpyAsync(c->pieces.p, cps.data(), cps.size() * sizeof(ConcatPiece), hipMemcpyHostToDevice, s));
+  if (!cps.empty())
+    JXG_HIP(hipMemcpyAsync(c->pieces.p, cps.data(), cps.size() * sizeof(ConcatPiece), hipMemcpyHostToDevice, s));
   JXG_HIP(hipMemsetAsync(c->out.p, 0, out_words * 4, s));
   launch_concat(c->pieces.p, (uint32_t)cps.size(), max_words, c->scratch.p, c->chunks.p, c->out.p, s);
   JXG_HIP(hipGetLastError());
-  if (hipMemcpyAsync(host_out, c->out.p, out_words * 4, hipMemcpyDeviceToHost, s) != hipSuccess) {
-    out_release(host_out);
+  if (hipMemcpyAsync(ho, c->out.p, out_words * 4, hipMemcpyDeviceToHost, s) != hipSuccess) {
+    out_release(ho);
     return JXG_ERR_HIP;
   }
   JXG_HIP(hipEventRecord(c->ev[4], s));
+  *host_out = ho;
+  *out_bytes = nbytes;
+  if (section_ids) *section_ids = ids;
+  if (section_bytes) *section_bytes = sizes;
+  return JXG_OK;
+}
+
+static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32_t h,
+                                size_t stride, jxg_buffer* out, Clock::time_point t_call) {
+  hipStream_t s = c->stream;
+  const jxg_params& P = c->params;
+  Job J;
+  J.f = make_frame(w, h, P.distance);
+  J.plan = make_plan(J.f, 0, 1);
+  J.w = w;
+  J.h = h;
+  J.stride = stride;
+  J.d_rgb = d_rgb;
+  const Frame& f = J.f;
+  const size_t nb = (size_t)f.bxs * f.bys;
+  jxg_status st = stage_alloc(c, J);
+  if (st) return st;
+  JXG_HIP(hipEventRecord(c->ev[0], s));
+  if ((st = stage_front(c, J))) return st;
+  JXG_HIP(hipEventRecord(c->ev[1], s));
+  if ((st = stage_ac_stats(c, J))) return st;
+  if ((st = stage_lf_stats(c, J))) return st;
+  if ((st = stage_download(c, J, c->hist_ac.p))) return st;
+  if ((st = stage_codes(c, J))) return st;
+  if ((st = stage_emit(c, J))) return st;
+  const Clock::time_point t_layout = Clock::now();
+  uint8_t* host_out = nullptr;
+  size_t out_bytes = 0;
+  if ((st = stage_concat(c, J, true, nullptr, nullptr, &host_out, &out_bytes))) return st;
+  const float ms_layout = ms_since(t_layout);
   std::vector<int16_t> m_ac16_tmp;
   if (P.flags & JXG_FLAG_KEEP_MAPS) {
     c->m_acs.resize(nb);
@@ -863,7 +1058,7 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
     JXG_HIP(hipMemcpyAsync(c->m_dc.data(), c->dc.p, nb * 12, hipMemcpyDeviceToHost, s));
     m_ac16_tmp.resize(nb * 192);
     JXG_HIP(hipMemcpyAsync(m_ac16_tmp.data(), c->ac.p, nb * 192 * 2, hipMemcpyDeviceToHost, s));
-    if (homog) {
+    if (J.homog) {
       c->m_homog.resize(nb * 3);
       JXG_HIP(hipMemcpyAsync(c->m_homog.data(), c->homog.p, nb * 12, hipMemcpyDeviceToHost, s));
     }
@@ -896,16 +1091,173 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
     S.quant_field = c->m_qf.data();
     S.dc = c->m_dc.data();
     S.ac = c->m_ac.data();
-    S.homogeneity = homog ? c->m_homog.data() : nullptr;
+    S.homogeneity = J.homog ? c->m_homog.data() : nullptr;
   }
   S.ms_front = elapsed(c->ev[0], c->ev[1]);
+  S.ms_front_kernel = elapsed(c->ev[0], c->ev[5]);
   S.ms_histogram = elapsed(c->ev[1], c->ev[2]);
   S.ms_emit = elapsed(c->ev[2], c->ev[3]);
   S.ms_assemble = elapsed(c->ev[3], c->ev[4]);
   S.ms_total = elapsed(c->ev[0], c->ev[4]);
-  S.ms_host_codes = ms_codes;
+  S.ms_host_codes = J.ms_codes;
   S.ms_host_layout = ms_layout;
   S.ms_host_call = ms_since(t_call);
+  return JXG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// sharded encode (jxg_shard_* in include/jxg.h)
+// payload: "JXGS" | version 1 | rank | world | xsize | ysize | nsections |
+//          nsections x (TOC index, bytes) | section bytes back to back
+// ---------------------------------------------------------------------------
+constexpr uint32_t kPayloadMagic = 0x5347584Au;  // "JXGS"
+
+static jxg_status shard_begin(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32_t h,
+                              size_t stride, uint32_t rank, uint32_t world, uint32_t* d_hist,
+                              uint8_t* d_xbuf) {
+  hipStream_t s = c->stream;
+  c->job = std::make_unique<Job>();
+  Job& J = *c->job;
+  J.f = make_frame(w, h, c->params.distance);
+  if (world < 1 || rank >= world || J.f.ngroups < world || J.f.ngroups < 2)
+    return JXG_ERR_INVALID_ARG;
+  J.plan = make_plan(J.f, rank, world);
+  J.w = w;
+  J.h = h;
+  J.stride = stride;
+  J.d_rgb = d_rgb;
+  jxg_status st = stage_alloc(c, J);
+  if (st) return st;
+  JXG_HIP(hipEventRecord(c->ev[0], s));
+  if ((st = stage_front(c, J))) return st;
+  if ((st = stage_ac_stats(c, J))) return st;
+  JXG_HIP(hipMemcpyAsync(d_hist, c->hist_ac.p, kMaxClusters * kAlpha * 4, hipMemcpyDeviceToDevice, s));
+  const uint32_t maxg = (J.f.ngroups + world - 1) / world;
+  PackArgs pa{c->acs.p, c->qf.p, c->dc.p, J.f.bxs, J.f.bys, J.f.gxs, d_xbuf,
+              (size_t)maxg * kGroupRecordBytes, rank, world, J.f.ngroups};
+  launch_pack(pa, s);
+  JXG_HIP(hipGetLastError());
+  JXG_HIP(hipEventRecord(c->ev[1], s));
+  JXG_HIP(hipStreamSynchronize(s));
+  return JXG_OK;
+}
+
+static jxg_status shard_end(Ctx* c, const uint32_t* d_hist, const uint8_t* d_xbuf,
+                            jxg_buffer* payload) {
+  if (!c->job) return JXG_ERR_INVALID_ARG;
+  Job& J = *c->job;
+  hipStream_t s = c->stream;
+  const uint32_t world = J.plan.world;
+  const uint32_t maxg = (J.f.ngroups + world - 1) / world;
+  PackArgs pa{c->acs.p, c->qf.p, c->dc.p, J.f.bxs, J.f.bys, J.f.gxs,
+              const_cast<uint8_t*>(d_xbuf), (size_t)maxg * kGroupRecordBytes,
+              J.plan.rank, world, J.f.ngroups};
+  launch_unpack(pa, s);
+  JXG_HIP(hipGetLastError());
+  jxg_status st;
+  if ((st = stage_lf_stats(c, J))) return st;
+  if ((st = stage_download(c, J, d_hist))) return st;
+  if ((st = stage_codes(c, J))) return st;
+  if ((st = stage_emit(c, J))) return st;
+  std::vector<uint32_t> ids, sizes;
+  uint8_t* body = nullptr;
+  size_t nbytes = 0;
+  if ((st = stage_concat(c, J, false, &ids, &sizes, &body, &nbytes))) return st;
+  if (hipStreamSynchronize(s) != hipSuccess) {
+    out_release(body);
+    return JXG_ERR_HIP;
+  }
+  const size_t head = 4 * (7 + 2 * ids.size());
+  uint8_t* pl = out_alloc(head + nbytes);
+  if (!pl) {
+    out_release(body);
+    return JXG_ERR_OOM;
+  }
+  uint32_t* hw = reinterpret_cast<uint32_t*>(pl);
+  hw[0] = kPayloadMagic;
+  hw[1] = 1;
+  hw[2] = J.plan.rank;
+  hw[3] = world;
+  hw[4] = J.w;
+  hw[5] = J.h;
+  hw[6] = (uint32_t)ids.size();
+  for (size_t i = 0; i < ids.size(); i++) {
+    hw[7 + 2 * i] = ids[i];
+    hw[8 + 2 * i] = sizes[i];
+  }
+  std::memcpy(pl + head, body, nbytes);
+  out_release(body);
+  payload->data = pl;
+  payload->size = head + nbytes;
+  c->stats = jxg_stats{};
+  c->stats.xsize = J.w;
+  c->stats.ysize = J.h;
+  c->stats.num_groups = J.f.ngroups;
+  c->stats.num_lf_groups = J.f.nlf;
+  c->stats.bytes = payload->size;
+  c->stats.ms_front = elapsed(c->ev[0], c->ev[1]);
+  c->stats.ms_front_kernel = elapsed(c->ev[0], c->ev[5]);
+  c->stats.ms_total = elapsed(c->ev[0], c->ev[4]);
+  c->job.reset();
+  return JXG_OK;
+}
+
+// host only: payloads of every rank -> codestream (headers, TOC, sections)
+static jxg_status shard_assemble(const uint8_t* const* payloads, const size_t* sizes, uint32_t n,
+                                 jxg_buffer* out) {
+  if (!payloads || !sizes || !out || n == 0) return JXG_ERR_INVALID_ARG;
+  uint32_t w = 0, h = 0;
+  std::vector<const uint8_t*> sec_data;
+  std::vector<uint32_t> sec_size;
+  for (uint32_t i = 0; i < n; i++) {
+    if (!payloads[i] || sizes[i] < 28) return JXG_ERR_INVALID_ARG;
+    uint32_t hw[7];
+    std::memcpy(hw, payloads[i], 28);
+    if (hw[0] != kPayloadMagic || hw[1] != 1 || hw[3] != n) return JXG_ERR_INVALID_ARG;
+    if (i == 0) {
+      w = hw[4];
+      h = hw[5];
+    } else if (hw[4] != w || hw[5] != h) {
+      return JXG_ERR_INVALID_ARG;
+    }
+    const size_t head = 4 * (7 + 2 * (size_t)hw[6]);
+    if (sizes[i] < head) return JXG_ERR_INVALID_ARG;
+    size_t off = head;
+    for (uint32_t k = 0; k < hw[6]; k++) {
+      uint32_t e[2];
+      std::memcpy(e, payloads[i] + 28 + 8 * k, 8);
+      if (off + e[1] > sizes[i]) return JXG_ERR_INVALID_ARG;
+      if (e[0] >= sec_data.size()) {
+        sec_data.resize(e[0] + 1, nullptr);
+        sec_size.resize(e[0] + 1, 0);
+      }
+      if (sec_data[e[0]]) return JXG_ERR_INVALID_ARG;  // section twice
+      sec_data[e[0]] = payloads[i] + off;
+      sec_size[e[0]] = e[1];
+      off += e[1];
+    }
+  }
+  const Frame f = make_frame(w, h, 1.0f);
+  if (sec_data.size() != 2 + f.nlf + f.ngroups) return JXG_ERR_INVALID_ARG;
+  size_t total = 0;
+  for (size_t i = 0; i < sec_data.size(); i++) {
+    if (!sec_data[i]) return JXG_ERR_INVALID_ARG;  // section missing
+    total += sec_size[i];
+  }
+  BitWriter head;
+  write_headers(head, w, h);
+  write_toc(head, sec_size);
+  const std::vector<uint8_t> hb = head.bytes();
+  uint8_t* o = out_alloc_heap(hb.size() + total);
+  if (!o) return JXG_ERR_OOM;
+  std::memcpy(o, hb.data(), hb.size());
+  size_t pos = hb.size();
+  for (size_t i = 0; i < sec_data.size(); i++) {
+    std::memcpy(o + pos, sec_data[i], sec_size[i]);
+    pos += sec_size[i];
+  }
+  out->data = o;
+  out->size = pos;
   return JXG_OK;
 }
 
@@ -1018,6 +1370,45 @@ void jxg_buffer_free(jxg_buffer* buf) {
   out_release(buf->data);
   buf->data = nullptr;
   buf->size = 0;
+}
+
+jxg_status jxg_shard_sizes(uint32_t xsize, uint32_t ysize, uint32_t world, size_t* hist_words,
+                           size_t* slot_bytes) {
+  if (!hist_words || !slot_bytes || xsize == 0 || ysize == 0 || world == 0)
+    return JXG_ERR_INVALID_ARG;
+  const Frame f = make_frame(xsize, ysize, 1.0f);
+  *hist_words = (size_t)kMaxClusters * kAlpha;
+  *slot_bytes = (size_t)((f.ngroups + world - 1) / world) * kGroupRecordBytes;
+  return JXG_OK;
+}
+
+jxg_status jxg_shard_begin(void* ctx, const void* d_rgb, uint32_t w, uint32_t h, size_t stride,
+                           uint32_t rank, uint32_t world, uint32_t* d_hist, void* d_xbuf) {
+  if (!ctx || !d_rgb || !d_hist || !d_xbuf || w == 0 || h == 0 || w > (1u << 18) ||
+      h > (1u << 18) || stride < (size_t)w * 3)
+    return JXG_ERR_INVALID_ARG;
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
+  return shard_begin(c, static_cast<const uint8_t*>(d_rgb), w, h, stride, rank, world, d_hist,
+                     static_cast<uint8_t*>(d_xbuf));
+}
+
+jxg_status jxg_shard_end(void* ctx, const uint32_t* d_hist, const void* d_xbuf,
+                         jxg_buffer* payload) {
+  if (!ctx || !d_hist || !d_xbuf || !payload) return JXG_ERR_INVALID_ARG;
+  Ctx* c = static_cast<Ctx*>(ctx);
+  payload->data = nullptr;
+  payload->size = 0;
+  if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
+  return shard_end(c, d_hist, static_cast<const uint8_t*>(d_xbuf), payload);
+}
+
+jxg_status jxg_shard_assemble(const uint8_t* const* payloads, const size_t* sizes, uint32_t n,
+                              jxg_buffer* out) {
+  if (!out) return JXG_ERR_INVALID_ARG;
+  out->data = nullptr;
+  out->size = 0;
+  return shard_assemble(payloads, sizes, n, out);
 }
 
 jxg_status jxg_homogeneity_map(void* ctx, const float* xyb, uint32_t xsize, uint32_t ysize,

@@ -27,6 +27,7 @@ struct FrontArgs {
   float* homog;   // [nb][3] or null
   float* ent;     // [nb] best 8x8 estimate (merge stage input) or null
   float* xyb_out; // [tiles][3][64][64] XYB tiles (merge stage input) or null
+  const uint32_t* tile_list;  // shard: tile ids (ty * tiles_x + tx), 1-D grid; or null
 };
 
 // merge stage (jxg_merge.hip): weight kinds (stored orientation) and the
@@ -37,7 +38,8 @@ constexpr int kNumShapes = 9;
 constexpr int kShapeOff[kNumShapes + 1] = {0, 128, 256, 512, 1024, 1536, 2560, 4608, 6656, 10752};
 struct MergeArgs {
   const float* xyb;     // [tiles][3][64][64] XYB tiles (front kernel)
-  uint32_t bxs, bys, tiles_x, ntiles;
+  uint32_t bxs, bys, tiles_x, ntiles;  // ntiles: entries of tile_list (or all tiles)
+  const uint32_t* tile_list;           // shard: tile ids, or null
   uint32_t proposals;
   int max_s;      // largest merged square in blocks (2, 4 or 8)
   uint32_t G;
@@ -59,6 +61,7 @@ struct MergeArgs {
 struct VbArgs {
   const uint8_t* acs;
   uint32_t bxs, bys, lfxs;
+  uint32_t rank, world;  // LF group lg belongs to shard lg % world
   uint32_t* vb;     // [nlf][65536] block index (frame raster) of each varblock
   uint32_t* count;  // [nlf]
 };
@@ -79,6 +82,7 @@ struct AcArgs {
   const int16_t* ac;  // [nb][3][64 zigzag]
   const uint16_t* nz;  // [3][nb] non-zero counts (front / merge kernels)
   uint32_t bxs, bys, gxs;
+  uint32_t g0;           // first pass group of the launch (shard)
   uint32_t* hist;        // [kMaxClusters][kAlpha]      (hist pass)
   uint32_t* bound;       // [ngroups] bit upper bound   (hist pass)
   uint32_t* ntok;        // [ngroups][3] token counts   (hist pass)
@@ -137,6 +141,19 @@ struct ConcatPiece {
 
 void set_front_constants(const float lut[256], const float wts[3][3][64], hipStream_t s);
 void launch_front(const FrontArgs& a, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s);
+void launch_front_list(const FrontArgs& a, uint32_t ntiles, hipStream_t s);
+// shard exchange: per-group block records (acs, qf, dc) <-> frame arrays
+struct PackArgs {
+  uint8_t* acs;
+  uint8_t* qf;
+  int32_t* dc;
+  uint32_t bxs, bys, gxs;
+  uint8_t* xbuf;           // [world][slot_bytes]
+  size_t slot_bytes;
+  uint32_t rank, world, ngroups;
+};
+void launch_pack(const PackArgs& a, hipStream_t s);    // own groups -> own slot
+void launch_unpack(const PackArgs& a, hipStream_t s);  // other slots -> frame arrays
 void launch_homog(const HomogArgs& a, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s);
 void launch_ac_hist(const AcArgs& a, uint32_t ngroups, hipStream_t s);
 void launch_ac_emit(const AcArgs& a, uint32_t ngroups, hipStream_t s);

@@ -155,11 +155,14 @@ struct Pass {
 };
 
 // workgroup id -> (tile, shape): the nine shapes of a tile share b % 8 (XCD)
+// (a shard's tiles come through a list: tile = list[index])
 __device__ __forceinline__ bool decode_wg(const MergeArgs& a, int& tile, int& si) {
   const int b = blockIdx.x, x = b & 7, q = b >> 3;
   si = q % kNumShapes;
   tile = (q / kNumShapes) * 8 + x;
-  return tile < (int)a.ntiles;
+  if (tile >= (int)a.ntiles) return false;
+  if (a.tile_list) tile = (int)a.tile_list[tile];
+  return true;
 }
 
 __device__ __forceinline__ Pass make_pass(const MergeArgs& a, int tile, int si) {
@@ -446,7 +449,7 @@ __global__ __launch_bounds__(kMThreads) void merge_eval_kernel(MergeArgs a) {
 __global__ __launch_bounds__(64) void merge_resolve_kernel(MergeArgs a) {
   __shared__ float sEnt[64];
   __shared__ uint8_t sAcs[64];
-  const int tile = blockIdx.x;
+  const int tile = a.tile_list ? (int)a.tile_list[blockIdx.x] : (int)blockIdx.x;
   const int tx = tile % (int)a.tiles_x, ty = tile / (int)a.tiles_x;
   const int nbx = min(8, (int)a.bxs - tx * 8), nby = min(8, (int)a.bys - ty * 8);
   const int t = threadIdx.x, lbx = t & 7, lby = t >> 3;
@@ -574,6 +577,7 @@ __global__ __launch_bounds__(1024) void vb_list_kernel(VbArgs a) {
   __shared__ uint32_t sWave[16];
   __shared__ uint32_t sBase;
   const uint32_t lg = blockIdx.x;
+  if (a.world > 1 && lg % a.world != a.rank) return;  // LF group of another shard
   const uint32_t bx0 = (lg % a.lfxs) * 256, by0 = (lg / a.lfxs) * 256;
   const uint32_t bw = min(256u, a.bxs - bx0), bh = min(256u, a.bys - by0);
   const uint32_t n = bw * bh;
@@ -613,6 +617,7 @@ void set_merge_constants(const float* llf_p, const float* llf_ib, hipStream_t s)
   (void)hipStreamSynchronize(s);
 }
 void launch_merge(const MergeArgs& a, hipStream_t s) {
+  if (!a.ntiles) return;
   const uint32_t nwg = ((a.ntiles + 7) / 8) * 8 * kNumShapes;
   hipLaunchKernelGGL(merge_eval_kernel, dim3(nwg), dim3(kMThreads), 0, s, a);
   hipLaunchKernelGGL(merge_resolve_kernel, dim3(a.ntiles), dim3(64), 0, s, a);

@@ -63,13 +63,15 @@ class _Stats(ctypes.Structure):
                 ("ms_front", ctypes.c_float), ("ms_histogram", ctypes.c_float),
                 ("ms_emit", ctypes.c_float), ("ms_assemble", ctypes.c_float),
                 ("ms_total", ctypes.c_float), ("ms_host_call", ctypes.c_float),
-                ("ms_host_codes", ctypes.c_float), ("ms_host_layout", ctypes.c_float)]
+                ("ms_host_codes", ctypes.c_float), ("ms_host_layout", ctypes.c_float),
+                ("ms_front_kernel", ctypes.c_float)]
 
 
 # every symbol declared in include/jxg.h
 EXPORTS = ("jxg_status_str", "jxg_create", "jxg_destroy", "jxg_encode_rgb8",
            "jxg_encode_rgb8_device", "jxg_encode_batch_rgb8", "jxg_get_stats",
-           "jxg_buffer_free", "jxg_homogeneity_map")
+           "jxg_buffer_free", "jxg_homogeneity_map", "jxg_shard_sizes", "jxg_shard_begin",
+           "jxg_shard_end", "jxg_shard_assemble")
 
 _lib = None
 
@@ -97,6 +99,14 @@ def load():
     lib.jxg_buffer_free.restype = None
     lib.jxg_homogeneity_map.argtypes = [vp, vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_float,
                                         ctypes.c_uint32, vp, vp]
+    sz = ctypes.c_size_t
+    lib.jxg_shard_sizes.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                    ctypes.POINTER(sz), ctypes.POINTER(sz)]
+    lib.jxg_shard_begin.argtypes = [vp, vp, ctypes.c_uint32, ctypes.c_uint32, sz, ctypes.c_uint32,
+                                    ctypes.c_uint32, vp, vp]
+    lib.jxg_shard_end.argtypes = [vp, vp, vp, ctypes.POINTER(_Buffer)]
+    lib.jxg_shard_assemble.argtypes = [ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)),
+                                       ctypes.POINTER(sz), ctypes.c_uint32, ctypes.POINTER(_Buffer)]
     _lib = lib
     return lib
 
@@ -197,7 +207,7 @@ class Encoder:
                                           "quant_dc", "bytes", "ms_front", "ms_histogram",
                                           "ms_emit", "ms_assemble", "ms_total",
                                           "ms_host_call", "ms_host_codes",
-                                          "ms_host_layout")}
+                                          "ms_host_layout", "ms_front_kernel")}
         if s.ac_tokens:
             out["ac_tokens"] = np.ctypeslib.as_array(s.ac_tokens, (s.num_groups * 3,)).reshape(-1, 3).copy()
         if s.ac_strategy:
@@ -210,6 +220,22 @@ class Encoder:
                 out["homog"] = np.ctypeslib.as_array(s.homogeneity, (nb * 3,)).reshape(shp + (3,)).copy()
         return out
 
+    # ---- sharded encode (one context per rank; see jxg.dist) ----
+    def shard_begin(self, ptr: int, width: int, height: int, rank: int, world: int,
+                    d_hist: int, d_xbuf: int, row_stride: int | None = None):
+        """Front end + merge + AC statistics of this rank's pass groups;
+        d_hist / d_xbuf are device pointers (sizes: :func:`shard_sizes`)."""
+        _check(load().jxg_shard_begin(self._ctx, ctypes.c_void_p(ptr), width, height,
+                                      row_stride or width * 3, rank, world,
+                                      ctypes.c_void_p(d_hist), ctypes.c_void_p(d_xbuf)))
+
+    def shard_end(self, d_hist: int, d_xbuf: int) -> bytes:
+        """After all-reduce(d_hist) and all-gather(d_xbuf): this rank's payload."""
+        buf = _Buffer()
+        _check(load().jxg_shard_end(self._ctx, ctypes.c_void_p(d_hist), ctypes.c_void_p(d_xbuf),
+                                    ctypes.byref(buf)))
+        return self._take(buf)
+
     def homogeneity_map(self, xyb: np.ndarray, distance: float, flags: int = 0):
         """Thesis selector over a (3, H, W) float32 XYB frame (H, W multiples of 8)."""
         xyb = np.ascontiguousarray(xyb, dtype=np.float32)
@@ -219,6 +245,58 @@ class Encoder:
         _check(load().jxg_homogeneity_map(self._ctx, xyb.ctypes.data, xs, ys, distance, flags,
                                           r3.ctypes.data, t.ctypes.data))
         return r3, t
+
+
+# ---------------------------------------------------------------------------
+# sharding helpers (host side; no device needed)
+# ---------------------------------------------------------------------------
+def shard_sizes(width: int, height: int, world: int):
+    """(AC histogram words, exchange slot bytes) of a sharded encode."""
+    hw, sb = ctypes.c_size_t(), ctypes.c_size_t()
+    _check(load().jxg_shard_sizes(width, height, world, ctypes.byref(hw), ctypes.byref(sb)))
+    return hw.value, sb.value
+
+
+def shard_assemble(payloads) -> bytes:
+    """Payloads of ranks 0..world-1 -> codestream (host only)."""
+    n = len(payloads)
+    keep = [np.frombuffer(bytes(p), dtype=np.uint8) for p in payloads]
+    ptrs = (ctypes.POINTER(ctypes.c_uint8) * n)(
+        *[k.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)) for k in keep])
+    sizes = (ctypes.c_size_t * n)(*[k.size for k in keep])
+    buf = _Buffer()
+    _check(load().jxg_shard_assemble(ptrs, sizes, n, ctypes.byref(buf)))
+    return Encoder._take(buf)
+
+
+def group_count(width: int, height: int) -> int:
+    return ((width + 255) // 256) * ((height + 255) // 256)
+
+
+def lf_group_count(width: int, height: int) -> int:
+    return ((width + 2047) // 2048) * ((height + 2047) // 2048)
+
+
+def shard_sections(width: int, height: int, rank: int, world: int):
+    """TOC indices of the sections rank `rank` of `world` produces (the
+    ownership of jxg_host.cpp make_plan): LfGlobal / HfGlobal on rank 0, LF
+    groups lg % world == rank, pass groups [n*rank/world, n*(rank+1)/world)."""
+    ng, nlf = group_count(width, height), lf_group_count(width, height)
+    ids = [0] if rank == 0 else []
+    ids += [1 + lg for lg in range(nlf) if lg % world == rank]
+    if rank == 0:
+        ids.append(1 + nlf)
+    g0, g1 = ng * rank // world, ng * (rank + 1) // world
+    ids += [2 + nlf + g for g in range(g0, g1)]
+    return ids
+
+
+def make_payload(rank: int, world: int, width: int, height: int, sections) -> bytes:
+    """The shard payload format of jxg_host.cpp (``JXGS`` v1) for a list of
+    (TOC index, bytes) -- used by tests to feed jxg_shard_assemble."""
+    head = np.array([0x5347584A, 1, rank, world, width, height, len(sections)] +
+                    [v for i, b in sections for v in (i, len(b))], dtype="<u4").tobytes()
+    return head + b"".join(b for _, b in sections)
 
 
 # ---------------------------------------------------------------------------

@@ -958,6 +958,7 @@ def decode(data: bytes, want_pixels: bool = True) -> Decoded:
     d = Decoded()
     d.xsize, d.ysize, d.bxs, d.bys = xs, ys, bxs, bys
     d.section_sizes = sizes
+    d.section_offsets = offs
     # LfGlobal
     s = sec(0)
     if not s.bool():

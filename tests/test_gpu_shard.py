@@ -1,0 +1,99 @@
+"""GPU group sharding on one device: `world` contexts play the
+ranks, the collectives are done with torch ops (sum of the histograms, slot
+concatenation), and the assembled codestream must equal the single-context
+encode byte for byte (one AC histogram -> one HF preset, so sharding does not
+change a bit).  The multi-process RCCL version of the same exchange is
+jxg.dist.encode_sharded (bench.py --gpus N)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def sharded_encode(jxg_mod, img, world, d=1.0, e=7, p=0):
+    import torch
+
+    h, w, _ = img.shape
+    t = torch.from_numpy(np.ascontiguousarray(img)).cuda()
+    hist_words, slot = jxg_mod.shard_sizes(w, h, world)
+    encs = [jxg_mod.Encoder(distance=d, effort=e, proposals=p) for _ in range(world)]
+    hists = [torch.zeros(hist_words, dtype=torch.int32, device="cuda") for _ in range(world)]
+    xbufs = [torch.zeros(world * slot, dtype=torch.uint8, device="cuda") for _ in range(world)]
+    for r in range(world):
+        encs[r].shard_begin(t.data_ptr(), w, h, r, world, hists[r].data_ptr(), xbufs[r].data_ptr())
+    hist = torch.stack(hists).sum(0).to(torch.int32).contiguous()
+    xbuf = torch.cat([xbufs[r][r * slot:(r + 1) * slot] for r in range(world)]).contiguous()
+    torch.cuda.synchronize()
+    payloads = [encs[r].shard_end(hist.data_ptr(), xbuf.data_ptr()) for r in range(world)]
+    for enc in encs:
+        enc.close()
+    return jxg_mod.shard_assemble(payloads)
+
+
+CASES = [(520, 300, 2, 1.0, 7, 0), (777, 333, 3, 2.0, 5, 3), (1000, 700, 4, 1.0, 7, 2),
+         (2100, 600, 8, 0.5, 4, 0), (1920, 1080, 5, 1.0, 7, 1)]
+
+
+@pytest.mark.parametrize("w,h,world,d,e,p", CASES)
+def test_sharded_equals_single(jxg_mod, w, h, world, d, e, p):
+    from jxg.synth import synth_rgb8
+
+    img = synth_rgb8(w, h, w * 3 + h)
+    with jxg_mod.Encoder(distance=d, effort=e, proposals=p) as enc:
+        ref = enc.encode(img)
+    assert sharded_encode(jxg_mod, img, world, d, e, p) == ref
+
+
+def test_sharded_8k_equals_single(jxg_mod):
+    from jxg.synth import config_image
+
+    img = config_image(2)
+    with jxg_mod.Encoder(distance=1.0, effort=7) as enc:
+        ref = enc.encode(img)
+    assert sharded_encode(jxg_mod, img, 8) == ref
+
+
+def _gloo_rank(rank, world, port, w, h, result):
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import jxg
+        from jxg.dist import encode_sharded
+        from jxg.synth import synth_rgb8
+
+        img = synth_rgb8(w, h, 5)
+        t = torch.from_numpy(img).cuda()
+        with jxg.Encoder(distance=1.0, effort=7) as enc:
+            out = encode_sharded(enc, t, w, h, rank, world)
+            if rank == 0:
+                ref = enc.encode(img)
+                result.put(out == ref)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_multiprocess_encode_sharded(jxg_mod):
+    """jxg.dist.encode_sharded in 2 processes (gloo, both ranks on cuda:0):
+    the multi-process orchestration bench.py --gpus N runs over RCCL."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gloo_rank, args=(r, 2, port, 1100, 700, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+        assert p.exitcode == 0
+    assert q.get(timeout=10) is True

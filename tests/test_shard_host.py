@@ -1,0 +1,96 @@
+"""Group sharding, host side (no GPU): the payload format, the section
+ownership of jxg_host.cpp make_plan and the host-only jxg_shard_assemble,
+pinned against the CPU oracle's codestream -- split into per-rank payloads
+by the TOC, exchanged over torch.distributed (gloo, world size 2) and
+re-assembled byte for byte.  The GPU side of the same path (jxg_shard_begin /
+jxg_shard_end) is covered by tests/test_gpu_shard.py."""
+import os
+
+import numpy as np
+import pytest
+
+
+def oracle_sections(oracle, decoder, img, d=1.0, e=7, p=0):
+    ref = oracle.encode(img, d, e, p)
+    dec = decoder.decode(ref.bytes, want_pixels=False)
+    secs = [ref.bytes[o:o + s] for o, s in zip(dec.section_offsets, dec.section_sizes)]
+    return ref.bytes, secs
+
+
+def payloads_for(jxg, w, h, world, secs):
+    out = []
+    for r in range(world):
+        ids = jxg.shard_sections(w, h, r, world)
+        out.append(jxg.make_payload(r, world, w, h, [(i, secs[i]) for i in ids]))
+    return out
+
+
+CASES = [(520, 300, 2), (777, 333, 3), (1000, 700, 4), (2100, 600, 8)]
+
+
+@pytest.mark.parametrize("w,h,world", CASES)
+def test_assemble_matches_oracle(jxg_mod, oracle, decoder, w, h, world):
+    from jxg.synth import synth_rgb8
+
+    full, secs = oracle_sections(oracle, decoder, synth_rgb8(w, h, w + h))
+    assert len(secs) == 2 + jxg_mod.lf_group_count(w, h) + jxg_mod.group_count(w, h)
+    # every section owned by exactly one rank
+    owned = sorted(i for r in range(world) for i in jxg_mod.shard_sections(w, h, r, world))
+    assert owned == list(range(len(secs)))
+    assert jxg_mod.shard_assemble(payloads_for(jxg_mod, w, h, world, secs)) == full
+
+
+def test_assemble_rejects_bad_payloads(jxg_mod, oracle, decoder):
+    from jxg.synth import synth_rgb8
+
+    w, h, world = 600, 300, 2
+    _, secs = oracle_sections(oracle, decoder, synth_rgb8(w, h, 3))
+    pl = payloads_for(jxg_mod, w, h, world, secs)
+    with pytest.raises(jxg_mod.JxgError):
+        jxg_mod.shard_assemble(pl[:1])            # a rank missing
+    with pytest.raises(jxg_mod.JxgError):
+        jxg_mod.shard_assemble([pl[0], pl[0]])    # sections twice
+    with pytest.raises(jxg_mod.JxgError):
+        jxg_mod.shard_assemble([pl[0][:20], pl[1]])  # truncated
+
+
+def _gloo_worker(rank, world, port, w, h, secs, full, result):
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import jxg
+        from jxg.dist import gather_payloads
+
+        ids = jxg.shard_sections(w, h, rank, world)
+        payload = jxg.make_payload(rank, world, w, h, [(i, secs[i]) for i in ids])
+        got = gather_payloads(payload, rank, world, "cpu")
+        if rank == 0:
+            result.put(jxg.shard_assemble(got) == full)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_gather_and_assemble(jxg_mod, oracle, decoder):
+    import socket
+
+    import torch.multiprocessing as mp
+    from jxg.synth import synth_rgb8
+
+    w, h, world = 1000, 520, 2
+    full, secs = oracle_sections(oracle, decoder, synth_rgb8(w, h, 11))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gloo_worker, args=(r, world, port, w, h, secs, full, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    assert q.get(timeout=10) is True
