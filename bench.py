@@ -100,10 +100,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # JXG_DIST_BACKEND=gloo rehearses the multi-rank path with host-staged
+    # collectives (several ranks may then share one device)
+    backend = os.environ.get("JXG_DIST_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     dev = torch.device("cuda", local)
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     name, w, h, _ = CONFIGS[args.config]
     shard = world > 1 and args.mode == "shard"
     img = synth_rgb8(w, h, SEED_BASE + args.config + (0 if shard else rank))
@@ -122,7 +130,7 @@ def main():
     def step():
         if shard:
             from jxg.dist import encode_sharded
-            return encode_sharded(enc, d_img, w, fh, rank, world, bufs=bufs)
+            return encode_sharded(enc, d_img, w, fh, rank, world, bufs=bufs, copy=False)
         return enc.encode_device(d_img.data_ptr(), w, fh, copy=False)
 
     for _ in range(args.warmup):

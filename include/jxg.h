@@ -104,20 +104,26 @@ void jxg_buffer_free(jxg_buffer* buf);
  *      and its per-block records to slot `rank` of d_xbuf (device);
  *   -- caller: all-reduce(sum) d_hist, all-gather d_xbuf (RCCL over xGMI);
  *   3. jxg_shard_end: LF-group streams of its LF groups, prefix codes from the
- *      global histogram, emission; returns a host payload with the rank's
- *      sections (rank 0's also carries LfGlobal and HfGlobal);
- *   -- caller: gather the payloads on rank 0;
- *   4. jxg_shard_assemble (host only, no device): payloads of all ranks ->
- *      codestream, byte-identical to jxg_encode_rgb8 of the whole frame.
- * The frame needs at least max(2, world) pass groups.  Payloads and the
- * codestream are released with jxg_buffer_free. */
+ *      global histogram, emission of the rank's sections into a payload kept
+ *      in device memory (rank 0's also carries LfGlobal and HfGlobal);
+ *      jxg_shard_payload copies it (payload_bytes) to device or host memory;
+ *   -- caller: gather the payloads on rank 0 (RCCL, device to device);
+ *   4. jxg_shard_assemble_device (rank 0): payloads in device memory (word
+ *      aligned offsets) -> codestream in host memory; or jxg_shard_assemble:
+ *      the same from host payloads, host only (no device).  Both are
+ *      byte-identical to jxg_encode_rgb8 of the whole frame.
+ * The frame needs at least max(2, world) pass groups.  Codestreams are
+ * released with jxg_buffer_free. */
 jxg_status jxg_shard_sizes(uint32_t xsize, uint32_t ysize, uint32_t world, size_t* hist_words,
                            size_t* slot_bytes);
 jxg_status jxg_shard_begin(void* ctx, const void* d_rgb, uint32_t xsize, uint32_t ysize,
                            size_t row_stride, uint32_t rank, uint32_t world, uint32_t* d_hist,
                            void* d_xbuf);
 jxg_status jxg_shard_end(void* ctx, const uint32_t* d_hist, const void* d_xbuf,
-                         jxg_buffer* payload);
+                         size_t* payload_bytes);
+jxg_status jxg_shard_payload(void* ctx, void* dst, int dst_on_device);
+jxg_status jxg_shard_assemble_device(void* ctx, const void* d_payloads, const size_t* offsets,
+                                     const size_t* sizes, uint32_t n, jxg_buffer* out);
 jxg_status jxg_shard_assemble(const uint8_t* const* payloads, const size_t* sizes, uint32_t n,
                               jxg_buffer* out);
 

@@ -437,6 +437,8 @@ struct Ctx {
   std::vector<float> m_homog;
   jxg_stats stats{};
   std::unique_ptr<struct Job> job;  // sharded encode in flight (begin -> end)
+  std::vector<uint32_t> payload_head;  // last jxg_shard_end: payload head words
+  size_t payload_body = 0;             //   and body bytes (in `out`)
 };
 
 static jxg_status init_constants(Ctx* c) {
@@ -999,20 +1001,23 @@ static jxg_status stage_concat(Ctx* c, Job& J, bool full, std::vector<uint32_t>*
   JXG_HIP(c->chunks.ensure(chunk_words.size()));
   JXG_HIP(c->pieces.ensure(std::max<size_t>(cps.size(), 1)));
   JXG_HIP(c->out.ensure(out_words));
-  uint8_t* ho = out_alloc(out_words * 4);
-  if (!ho) return JXG_ERR_OOM;
+  uint8_t* ho = nullptr;
+  if (host_out) {  // else the bytes stay in c->out (device)
+    ho = out_alloc(out_words * 4);
+    if (!ho) return JXG_ERR_OOM;
+  }
   JXG_HIP(hipMemcpyAsync(c->chunks.p, chunk_words.data(), chunk_words.size() * 4, hipMemcpyHostToDevice, s));
   if (!cps.empty())
     JXG_HIP(hipMemcpyAsync(c->pieces.p, cps.data(), cps.size() * sizeof(ConcatPiece), hipMemcpyHostToDevice, s));
   JXG_HIP(hipMemsetAsync(c->out.p, 0, out_words * 4, s));
   launch_concat(c->pieces.p, (uint32_t)cps.size(), max_words, c->scratch.p, c->chunks.p, c->out.p, s);
   JXG_HIP(hipGetLastError());
-  if (hipMemcpyAsync(ho, c->out.p, out_words * 4, hipMemcpyDeviceToHost, s) != hipSuccess) {
+  if (ho && hipMemcpyAsync(ho, c->out.p, out_words * 4, hipMemcpyDeviceToHost, s) != hipSuccess) {
     out_release(ho);
     return JXG_ERR_HIP;
   }
   JXG_HIP(hipEventRecord(c->ev[4], s));
-  *host_out = ho;
+  if (host_out) *host_out = ho;
   *out_bytes = nbytes;
   if (section_ids) *section_ids = ids;
   if (section_bytes) *section_bytes = sizes;
@@ -1143,7 +1148,7 @@ static jxg_status shard_begin(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32_t
 }
 
 static jxg_status shard_end(Ctx* c, const uint32_t* d_hist, const uint8_t* d_xbuf,
-                            jxg_buffer* payload) {
+                            size_t* payload_bytes) {
   if (!c->job) return JXG_ERR_INVALID_ARG;
   Job& J = *c->job;
   hipStream_t s = c->stream;
@@ -1160,20 +1165,11 @@ static jxg_status shard_end(Ctx* c, const uint32_t* d_hist, const uint8_t* d_xbu
   if ((st = stage_codes(c, J))) return st;
   if ((st = stage_emit(c, J))) return st;
   std::vector<uint32_t> ids, sizes;
-  uint8_t* body = nullptr;
   size_t nbytes = 0;
-  if ((st = stage_concat(c, J, false, &ids, &sizes, &body, &nbytes))) return st;
-  if (hipStreamSynchronize(s) != hipSuccess) {
-    out_release(body);
-    return JXG_ERR_HIP;
-  }
-  const size_t head = 4 * (7 + 2 * ids.size());
-  uint8_t* pl = out_alloc(head + nbytes);
-  if (!pl) {
-    out_release(body);
-    return JXG_ERR_OOM;
-  }
-  uint32_t* hw = reinterpret_cast<uint32_t*>(pl);
+  if ((st = stage_concat(c, J, false, &ids, &sizes, nullptr, &nbytes))) return st;
+  // payload head (host); the body stays in c->out until jxg_shard_payload
+  std::vector<uint32_t>& hw = c->payload_head;
+  hw.assign(7 + 2 * ids.size(), 0);
   hw[0] = kPayloadMagic;
   hw[1] = 1;
   hw[2] = J.plan.rank;
@@ -1185,16 +1181,15 @@ static jxg_status shard_end(Ctx* c, const uint32_t* d_hist, const uint8_t* d_xbu
     hw[7 + 2 * i] = ids[i];
     hw[8 + 2 * i] = sizes[i];
   }
-  std::memcpy(pl + head, body, nbytes);
-  out_release(body);
-  payload->data = pl;
-  payload->size = head + nbytes;
+  c->payload_body = nbytes;
+  *payload_bytes = hw.size() * 4 + nbytes;
+  JXG_HIP(hipStreamSynchronize(s));
   c->stats = jxg_stats{};
   c->stats.xsize = J.w;
   c->stats.ysize = J.h;
   c->stats.num_groups = J.f.ngroups;
   c->stats.num_lf_groups = J.f.nlf;
-  c->stats.bytes = payload->size;
+  c->stats.bytes = *payload_bytes;
   c->stats.ms_front = elapsed(c->ev[0], c->ev[1]);
   c->stats.ms_front_kernel = elapsed(c->ev[0], c->ev[5]);
   c->stats.ms_total = elapsed(c->ev[0], c->ev[4]);
@@ -1202,47 +1197,168 @@ static jxg_status shard_end(Ctx* c, const uint32_t* d_hist, const uint8_t* d_xbu
   return JXG_OK;
 }
 
-// host only: payloads of every rank -> codestream (headers, TOC, sections)
+// copy the payload of the last jxg_shard_end to dst (device or host memory)
+static jxg_status shard_payload(Ctx* c, void* dst, bool on_device) {
+  hipStream_t s = c->stream;
+  const size_t head = c->payload_head.size() * 4;
+  if (!head) return JXG_ERR_INVALID_ARG;
+  uint8_t* d = static_cast<uint8_t*>(dst);
+  if (on_device) {
+    JXG_HIP(hipMemcpyAsync(d, c->payload_head.data(), head, hipMemcpyHostToDevice, s));
+    JXG_HIP(hipMemcpyAsync(d + head, c->out.p, c->payload_body, hipMemcpyDeviceToDevice, s));
+  } else {
+    std::memcpy(d, c->payload_head.data(), head);
+    JXG_HIP(hipMemcpyAsync(d + head, c->out.p, c->payload_body, hipMemcpyDeviceToHost, s));
+  }
+  JXG_HIP(hipStreamSynchronize(s));
+  return JXG_OK;
+}
+
+// Parse payload heads (host copies) into the section table of the frame:
+// for each TOC index, (payload, byte offset inside it, size)
+struct SectionRef {
+  uint32_t payload;
+  uint64_t off;
+  uint32_t size;
+};
+static jxg_status parse_payload_heads(const std::vector<std::vector<uint32_t>>& heads,
+                                      const std::vector<size_t>& psizes, uint32_t* w,
+                                      uint32_t* h, std::vector<SectionRef>& secs) {
+  const uint32_t n = (uint32_t)heads.size();
+  secs.clear();
+  std::vector<bool> seen;
+  for (uint32_t i = 0; i < n; i++) {
+    const std::vector<uint32_t>& hw = heads[i];
+    if (hw.size() < 7 || hw[0] != kPayloadMagic || hw[1] != 1 || hw[3] != n)
+      return JXG_ERR_INVALID_ARG;
+    if (i == 0) {
+      *w = hw[4];
+      *h = hw[5];
+    } else if (hw[4] != *w || hw[5] != *h) {
+      return JXG_ERR_INVALID_ARG;
+    }
+    if (hw.size() < 7 + 2 * (size_t)hw[6]) return JXG_ERR_INVALID_ARG;
+    uint64_t off = 4 * (7 + 2 * (uint64_t)hw[6]);
+    for (uint32_t k = 0; k < hw[6]; k++) {
+      const uint32_t id = hw[7 + 2 * k], sz = hw[8 + 2 * k];
+      if (off + sz > psizes[i]) return JXG_ERR_INVALID_ARG;
+      if (id >= secs.size()) {
+        secs.resize(id + 1, SectionRef{0, 0, 0});
+        seen.resize(id + 1, false);
+      }
+      if (seen[id]) return JXG_ERR_INVALID_ARG;  // section twice
+      seen[id] = true;
+      secs[id] = SectionRef{i, off, sz};
+      off += sz;
+    }
+  }
+  if (*w == 0 || *h == 0) return JXG_ERR_INVALID_ARG;
+  const Frame f = make_frame(*w, *h, 1.0f);
+  if (secs.size() != 2 + f.nlf + f.ngroups) return JXG_ERR_INVALID_ARG;
+  for (size_t i = 0; i < secs.size(); i++)
+    if (!seen[i]) return JXG_ERR_INVALID_ARG;  // section missing
+  return JXG_OK;
+}
+
+static std::vector<uint32_t> read_head(const uint8_t* p, size_t size) {
+  if (size < 28) return {};
+  uint32_t h7[7];
+  std::memcpy(h7, p, 28);
+  const size_t words = 7 + 2 * (size_t)h7[6];
+  if (size < words * 4) return {};
+  std::vector<uint32_t> hw(words);
+  std::memcpy(hw.data(), p, words * 4);
+  return hw;
+}
+
+// device-resident payloads (payload i at d_base + offsets[i]) -> codestream in
+// host memory: headers + TOC on the host, every section moved by the concat
+// kernel, one D2H of the result
+static jxg_status shard_assemble_device(Ctx* c, const uint8_t* d_base, const size_t* offsets,
+                                        const size_t* psizes, uint32_t n, jxg_buffer* out) {
+  hipStream_t s = c->stream;
+  // payload heads to the host (a few KB each)
+  std::vector<std::vector<uint32_t>> heads(n);
+  std::vector<size_t> ps(psizes, psizes + n);
+  for (uint32_t i = 0; i < n; i++) {
+    uint32_t h7[7];
+    if (psizes[i] < 28) return JXG_ERR_INVALID_ARG;
+    JXG_HIP(hipMemcpy(h7, d_base + offsets[i], 28, hipMemcpyDeviceToHost));
+    const size_t words = 7 + 2 * (size_t)h7[6];
+    if (psizes[i] < words * 4) return JXG_ERR_INVALID_ARG;
+    heads[i].resize(words);
+    JXG_HIP(hipMemcpy(heads[i].data(), d_base + offsets[i], words * 4, hipMemcpyDeviceToHost));
+  }
+  uint32_t w = 0, h = 0;
+  std::vector<SectionRef> secs;
+  jxg_status st = parse_payload_heads(heads, ps, &w, &h, secs);
+  if (st) return st;
+  std::vector<uint32_t> sizes(secs.size());
+  for (size_t i = 0; i < secs.size(); i++) sizes[i] = secs[i].size;
+  BitWriter head;
+  write_headers(head, w, h);
+  write_toc(head, sizes);
+  std::vector<uint32_t> chunk_words = head.words32();
+  chunk_words.push_back(0);
+  std::vector<ConcatPiece> cps;
+  uint64_t dst = 0, max_words = 0;
+  cps.push_back({0, 0, head.bits(), 1, 0});
+  max_words = (head.bits() + 31) / 32;
+  dst = (head.bits() + 7) & ~7ull;
+  // payloads are read as one 32-bit-word arena starting at d_base
+  for (const SectionRef& r : secs) {
+    const uint64_t src_bit = (offsets[r.payload] + r.off) * 8;
+    if (r.size) {
+      cps.push_back({src_bit, dst, (uint64_t)r.size * 8, 0, 0});
+      max_words = std::max<uint64_t>(max_words, ((uint64_t)r.size * 8 + 31) / 32);
+    }
+    dst += (uint64_t)r.size * 8;
+  }
+  const size_t nbytes = (size_t)(dst / 8);
+  const size_t out_words = (nbytes + 3) / 4 + 1;
+  JXG_HIP(c->chunks.ensure(chunk_words.size()));
+  JXG_HIP(c->pieces.ensure(cps.size()));
+  JXG_HIP(c->out.ensure(out_words));
+  uint8_t* ho = out_alloc(out_words * 4);
+  if (!ho) return JXG_ERR_OOM;
+  JXG_HIP(hipMemcpyAsync(c->chunks.p, chunk_words.data(), chunk_words.size() * 4, hipMemcpyHostToDevice, s));
+  JXG_HIP(hipMemcpyAsync(c->pieces.p, cps.data(), cps.size() * sizeof(ConcatPiece), hipMemcpyHostToDevice, s));
+  JXG_HIP(hipMemsetAsync(c->out.p, 0, out_words * 4, s));
+  // arena 0 = the payload base (word aligned: offsets are multiples of 4)
+  launch_concat(c->pieces.p, (uint32_t)cps.size(), max_words,
+                reinterpret_cast<const uint32_t*>(d_base), c->chunks.p, c->out.p, s);
+  JXG_HIP(hipGetLastError());
+  if (hipMemcpyAsync(ho, c->out.p, out_words * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess) {
+    out_release(ho);
+    return JXG_ERR_HIP;
+  }
+  out->data = ho;
+  out->size = nbytes;
+  return JXG_OK;
+}
+
+// host only: payloads of every rank -> codestream (same layout as
+// shard_assemble_device; no device needed)
 static jxg_status shard_assemble(const uint8_t* const* payloads, const size_t* sizes, uint32_t n,
                                  jxg_buffer* out) {
   if (!payloads || !sizes || !out || n == 0) return JXG_ERR_INVALID_ARG;
-  uint32_t w = 0, h = 0;
-  std::vector<const uint8_t*> sec_data;
-  std::vector<uint32_t> sec_size;
+  std::vector<std::vector<uint32_t>> heads(n);
+  std::vector<size_t> ps(sizes, sizes + n);
   for (uint32_t i = 0; i < n; i++) {
-    if (!payloads[i] || sizes[i] < 28) return JXG_ERR_INVALID_ARG;
-    uint32_t hw[7];
-    std::memcpy(hw, payloads[i], 28);
-    if (hw[0] != kPayloadMagic || hw[1] != 1 || hw[3] != n) return JXG_ERR_INVALID_ARG;
-    if (i == 0) {
-      w = hw[4];
-      h = hw[5];
-    } else if (hw[4] != w || hw[5] != h) {
-      return JXG_ERR_INVALID_ARG;
-    }
-    const size_t head = 4 * (7 + 2 * (size_t)hw[6]);
-    if (sizes[i] < head) return JXG_ERR_INVALID_ARG;
-    size_t off = head;
-    for (uint32_t k = 0; k < hw[6]; k++) {
-      uint32_t e[2];
-      std::memcpy(e, payloads[i] + 28 + 8 * k, 8);
-      if (off + e[1] > sizes[i]) return JXG_ERR_INVALID_ARG;
-      if (e[0] >= sec_data.size()) {
-        sec_data.resize(e[0] + 1, nullptr);
-        sec_size.resize(e[0] + 1, 0);
-      }
-      if (sec_data[e[0]]) return JXG_ERR_INVALID_ARG;  // section twice
-      sec_data[e[0]] = payloads[i] + off;
-      sec_size[e[0]] = e[1];
-      off += e[1];
-    }
+    if (!payloads[i]) return JXG_ERR_INVALID_ARG;
+    heads[i] = read_head(payloads[i], sizes[i]);
+    if (heads[i].empty()) return JXG_ERR_INVALID_ARG;
   }
-  const Frame f = make_frame(w, h, 1.0f);
-  if (sec_data.size() != 2 + f.nlf + f.ngroups) return JXG_ERR_INVALID_ARG;
+  uint32_t w = 0, h = 0;
+  std::vector<SectionRef> secs;
+  jxg_status st = parse_payload_heads(heads, ps, &w, &h, secs);
+  if (st) return st;
+  std::vector<uint32_t> sec_size(secs.size());
   size_t total = 0;
-  for (size_t i = 0; i < sec_data.size(); i++) {
-    if (!sec_data[i]) return JXG_ERR_INVALID_ARG;  // section missing
-    total += sec_size[i];
+  for (size_t i = 0; i < secs.size(); i++) {
+    sec_size[i] = secs[i].size;
+    total += secs[i].size;
   }
   BitWriter head;
   write_headers(head, w, h);
@@ -1252,9 +1368,9 @@ static jxg_status shard_assemble(const uint8_t* const* payloads, const size_t* s
   if (!o) return JXG_ERR_OOM;
   std::memcpy(o, hb.data(), hb.size());
   size_t pos = hb.size();
-  for (size_t i = 0; i < sec_data.size(); i++) {
-    std::memcpy(o + pos, sec_data[i], sec_size[i]);
-    pos += sec_size[i];
+  for (const SectionRef& r : secs) {
+    std::memcpy(o + pos, payloads[r.payload] + r.off, r.size);
+    pos += r.size;
   }
   out->data = o;
   out->size = pos;
@@ -1394,13 +1510,31 @@ jxg_status jxg_shard_begin(void* ctx, const void* d_rgb, uint32_t w, uint32_t h,
 }
 
 jxg_status jxg_shard_end(void* ctx, const uint32_t* d_hist, const void* d_xbuf,
-                         jxg_buffer* payload) {
-  if (!ctx || !d_hist || !d_xbuf || !payload) return JXG_ERR_INVALID_ARG;
+                         size_t* payload_bytes) {
+  if (!ctx || !d_hist || !d_xbuf || !payload_bytes) return JXG_ERR_INVALID_ARG;
   Ctx* c = static_cast<Ctx*>(ctx);
-  payload->data = nullptr;
-  payload->size = 0;
+  *payload_bytes = 0;
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
-  return shard_end(c, d_hist, static_cast<const uint8_t*>(d_xbuf), payload);
+  return shard_end(c, d_hist, static_cast<const uint8_t*>(d_xbuf), payload_bytes);
+}
+
+jxg_status jxg_shard_payload(void* ctx, void* dst, int dst_on_device) {
+  if (!ctx || !dst) return JXG_ERR_INVALID_ARG;
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
+  return shard_payload(c, dst, dst_on_device != 0);
+}
+
+jxg_status jxg_shard_assemble_device(void* ctx, const void* d_payloads, const size_t* offsets,
+                                     const size_t* sizes, uint32_t n, jxg_buffer* out) {
+  if (!ctx || !d_payloads || !offsets || !sizes || !out || n == 0) return JXG_ERR_INVALID_ARG;
+  for (uint32_t i = 0; i < n; i++)
+    if (offsets[i] % 4) return JXG_ERR_INVALID_ARG;
+  Ctx* c = static_cast<Ctx*>(ctx);
+  out->data = nullptr;
+  out->size = 0;
+  if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
+  return shard_assemble_device(c, static_cast<const uint8_t*>(d_payloads), offsets, sizes, n, out);
 }
 
 jxg_status jxg_shard_assemble(const uint8_t* const* payloads, const size_t* sizes, uint32_t n,

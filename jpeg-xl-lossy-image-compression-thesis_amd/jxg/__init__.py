@@ -71,7 +71,8 @@ class _Stats(ctypes.Structure):
 EXPORTS = ("jxg_status_str", "jxg_create", "jxg_destroy", "jxg_encode_rgb8",
            "jxg_encode_rgb8_device", "jxg_encode_batch_rgb8", "jxg_get_stats",
            "jxg_buffer_free", "jxg_homogeneity_map", "jxg_shard_sizes", "jxg_shard_begin",
-           "jxg_shard_end", "jxg_shard_assemble")
+           "jxg_shard_end", "jxg_shard_payload", "jxg_shard_assemble_device",
+           "jxg_shard_assemble")
 
 _lib = None
 
@@ -104,7 +105,10 @@ def load():
                                     ctypes.POINTER(sz), ctypes.POINTER(sz)]
     lib.jxg_shard_begin.argtypes = [vp, vp, ctypes.c_uint32, ctypes.c_uint32, sz, ctypes.c_uint32,
                                     ctypes.c_uint32, vp, vp]
-    lib.jxg_shard_end.argtypes = [vp, vp, vp, ctypes.POINTER(_Buffer)]
+    lib.jxg_shard_end.argtypes = [vp, vp, vp, ctypes.POINTER(sz)]
+    lib.jxg_shard_payload.argtypes = [vp, vp, ctypes.c_int]
+    lib.jxg_shard_assemble_device.argtypes = [vp, vp, ctypes.POINTER(sz), ctypes.POINTER(sz),
+                                              ctypes.c_uint32, ctypes.POINTER(_Buffer)]
     lib.jxg_shard_assemble.argtypes = [ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)),
                                        ctypes.POINTER(sz), ctypes.c_uint32, ctypes.POINTER(_Buffer)]
     _lib = lib
@@ -229,12 +233,33 @@ class Encoder:
                                       row_stride or width * 3, rank, world,
                                       ctypes.c_void_p(d_hist), ctypes.c_void_p(d_xbuf)))
 
-    def shard_end(self, d_hist: int, d_xbuf: int) -> bytes:
-        """After all-reduce(d_hist) and all-gather(d_xbuf): this rank's payload."""
-        buf = _Buffer()
+    def shard_end(self, d_hist: int, d_xbuf: int) -> int:
+        """After all-reduce(d_hist) and all-gather(d_xbuf): emit this rank's
+        sections; returns the payload size (kept on the device, see
+        :meth:`shard_payload`)."""
+        n = ctypes.c_size_t()
         _check(load().jxg_shard_end(self._ctx, ctypes.c_void_p(d_hist), ctypes.c_void_p(d_xbuf),
-                                    ctypes.byref(buf)))
-        return self._take(buf)
+                                    ctypes.byref(n)))
+        return n.value
+
+    def shard_payload(self, dst: int, on_device: bool = True):
+        """Copy the last payload to `dst` (device or host pointer)."""
+        _check(load().jxg_shard_payload(self._ctx, ctypes.c_void_p(dst), 1 if on_device else 0))
+
+    def shard_payload_bytes(self, size: int) -> bytes:
+        buf = (ctypes.c_uint8 * size)()
+        self.shard_payload(ctypes.addressof(buf), on_device=False)
+        return bytes(buf)
+
+    def shard_assemble_device(self, d_base: int, offsets, sizes, copy: bool = True):
+        """Payloads gathered in device memory (d_base + offsets[i]) -> codestream."""
+        n = len(sizes)
+        offs = (ctypes.c_size_t * n)(*offsets)
+        szs = (ctypes.c_size_t * n)(*sizes)
+        buf = _Buffer()
+        _check(load().jxg_shard_assemble_device(self._ctx, ctypes.c_void_p(d_base), offs, szs, n,
+                                                ctypes.byref(buf)))
+        return self._take(buf) if copy else Codestream(buf)
 
     def homogeneity_map(self, xyb: np.ndarray, distance: float, flags: int = 0):
         """Thesis selector over a (3, H, W) float32 XYB frame (H, W multiples of 8)."""

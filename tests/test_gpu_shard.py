@@ -24,10 +24,23 @@ def sharded_encode(jxg_mod, img, world, d=1.0, e=7, p=0):
     hist = torch.stack(hists).sum(0).to(torch.int32).contiguous()
     xbuf = torch.cat([xbufs[r][r * slot:(r + 1) * slot] for r in range(world)]).contiguous()
     torch.cuda.synchronize()
-    payloads = [encs[r].shard_end(hist.data_ptr(), xbuf.data_ptr()) for r in range(world)]
+    payloads = []
+    for r in range(world):
+        size = encs[r].shard_end(hist.data_ptr(), xbuf.data_ptr())
+        payloads.append(encs[r].shard_payload_bytes(size))
+    # device assembly on "rank 0" from one buffer (word-aligned offsets)
+    cap = (max(len(p) for p in payloads) + 15) // 16 * 16
+    blob = np.zeros(world * cap + 64, dtype=np.uint8)
+    for r, p in enumerate(payloads):
+        blob[r * cap:r * cap + len(p)] = np.frombuffer(p, dtype=np.uint8)
+    d_blob = torch.from_numpy(blob).cuda()
+    dev_out = encs[0].shard_assemble_device(d_blob.data_ptr(), [r * cap for r in range(world)],
+                                            [len(p) for p in payloads])
     for enc in encs:
         enc.close()
-    return jxg_mod.shard_assemble(payloads)
+    host_out = jxg_mod.shard_assemble(payloads)
+    assert dev_out == host_out
+    return dev_out
 
 
 CASES = [(520, 300, 2, 1.0, 7, 0), (777, 333, 3, 2.0, 5, 3), (1000, 700, 4, 1.0, 7, 2),
