@@ -94,6 +94,8 @@ def main():
     ap.add_argument("--effort", type=int, default=7)
     ap.add_argument("--proposals", type=int, default=0)
     ap.add_argument("--mode", choices=("shard", "replica"), default="shard")
+    ap.add_argument("--coder", choices=("prefix", "ans"), default="prefix",
+                    help="AC entropy coder (libjxl codes with ANS at e7)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -124,7 +126,7 @@ def main():
     torch.cuda.synchronize()
 
     enc = jxg.Encoder(distance=args.distance, effort=args.effort, proposals=args.proposals,
-                      device=local)
+                      device=local, flags=jxg.FLAG_ANS if args.coder == "ans" else 0)
     bufs = {}
 
     def step():
@@ -169,14 +171,14 @@ def main():
         achieved = fb / (fms * 1e-3) / 1e9 if fms > 0 else 0.0
         if shard:
             workload = ("%s x%d: %dx%d RGB8 (synth_rgb8 8K frame stacked %d times), VarDCT d%g "
-                        "e%d, proposals=%d, prefix-coded, 256x256 groups sharded over %d ranks"
+                        "e%d, proposals=%d, %s-coded, 256x256 groups sharded over %d ranks"
                         % (name, world, w, fh, world, args.distance, args.effort,
-                           args.proposals, world))
+                           args.proposals, args.coder, world))
             par = "group-shard%d" % world
         else:
-            workload = ("%s %dx%d RGB8 (synth_rgb8), VarDCT d%g e%d, proposals=%d, prefix-coded, "
+            workload = ("%s %dx%d RGB8 (synth_rgb8), VarDCT d%g e%d, proposals=%d, %s-coded, "
                         "one frame per rank" % (name, w, h, args.distance, args.effort,
-                                                args.proposals))
+                                                args.proposals, args.coder))
             par = "frame-dp%d" % world
         res = {
             "metric": "MPix/s VarDCT encode @ d1.0, 8K RGB",

@@ -408,6 +408,141 @@ __global__ __launch_bounds__(kAcThreads) void ac_emit_kernel(AcArgs a) {
 }
 
 // groups [a.g0, a.g0 + ngroups)
+// ---------------------------------------------------------------------------
+// ANS: token records in stream order (same task scan as ac_emit), then one
+// lane per group runs the rANS encoder backwards over its records (the
+// stream's only sequential dependency), then the group's workgroup places
+// the emitted bits in parallel.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kAcThreads) void ac_tokens_kernel(AcArgs a) {
+  __shared__ AcLds L;
+  __shared__ uint32_t sTask[3][1024];  // tokens per (channel, slice task)
+  __shared__ uint32_t sBase[1024];     // first token of each varblock (first block)
+  __shared__ uint8_t sClu[kAcCtx];
+  __shared__ uint32_t sWave[kAcThreads / 64];
+  const int g = blockIdx.x + (int)a.g0;
+  const GroupGeom G = group_geom(a, g);
+  for (int i = threadIdx.x; i < kAcCtx; i += blockDim.x) sClu[i] = c_cluster[i];
+  const SliceTask t = slice_task(a, G);
+  fill_slices(a, G, t, L);
+  __syncthreads();
+  const int me = t.by * 32 + t.bx;
+  if (t.valid) {
+#pragma unroll 1
+    for (int ci = 0; ci < 3; ci++) {
+      uint32_t cnt = 0;
+      task_tokens(a, t, L, channel_of(ci), [&](int, uint32_t) { cnt++; });
+      sTask[ci][me] = cnt;
+    }
+  }
+  __syncthreads();
+  uint32_t vtot = 0;
+  const int cb = 1 << t.lcb;
+  if (t.valid && t.sl == 0) {
+    for (int ci = 0; ci < 3; ci++)
+      for (int j = 0; j < cb; j++) vtot += sTask[ci][block_of_slice(t, j)];
+  }
+  uint32_t total;
+  const uint32_t off = block_excl_scan1024(vtot, sWave, &total);
+  if (t.valid && t.sl == 0) sBase[me] = off;
+  __syncthreads();
+  if (t.valid) {
+    uint32_t pos = sBase[t.oby * 32 + t.obx];
+    uint32_t* rec = a.tokens + a.tbase[g];
+#pragma unroll 1
+    for (int ci = 0; ci < 3; ci++) {
+      uint32_t before = 0, chan_total = 0;
+      for (int j = 0; j < cb; j++) {
+        const uint32_t b = sTask[ci][block_of_slice(t, j)];
+        before += j < t.sl ? b : 0u;
+        chan_total += b;
+      }
+      uint32_t idx = pos + before;
+      task_tokens(a, t, L, channel_of(ci), [&](int ctx, uint32_t v) {
+        uint32_t tok, nb, bits;
+        hybrid420(v, tok, nb, bits);
+        rec[idx++] = (uint32_t)sClu[ctx] | (tok << 8) | (nb << 14) | (bits << 18);
+      });
+      pos += chan_total;
+    }
+  }
+}
+
+// rANS backwards over each group's records, one lane per group; the next
+// record is fetched one step ahead (only the inverse-table lookup depends on
+// the running state)
+__global__ __launch_bounds__(64) void ans_encode_kernel(AnsArgs a) {
+  const uint32_t g = a.g0 + blockIdx.x * 64 + threadIdx.x;
+  if (g >= a.g1) return;
+  const uint32_t n = a.ntok[g * 3] + a.ntok[g * 3 + 1] + a.ntok[g * 3 + 2];
+  const uint64_t b = a.tbase[g];
+  uint32_t x = 0x130000u;
+  uint32_t r = n ? a.tokens[b + n - 1] : 0u;
+  for (uint32_t k = n; k-- > 0;) {
+    const uint32_t rn = k ? a.tokens[b + k - 1] : 0u;  // prefetch
+    const uint32_t cl = r & 0xFF, tok = (r >> 8) & 63, nb = (r >> 14) & 15, raw = r >> 18;
+    const uint32_t f = a.freq[cl * 128 + tok];
+    const uint32_t c0 = a.cum[cl * 128 + tok];
+    uint32_t v = raw, l = nb;
+    if ((x >> 20) >= f) {
+      v = (x & 0xFFFFu) | (raw << 16);
+      l += 16;
+      x >>= 16;
+    }
+    const uint32_t q = x / f, rem = x - q * f;
+    x = (q << 12) + a.inv[(size_t)cl * 4096 + c0 + rem];
+    a.val[b + k] = v;
+    a.len[b + k] = (uint8_t)l;
+    r = rn;
+  }
+  a.state[g] = x;
+}
+
+// bit placement: the 32-bit state, then every record's bits, in order;
+// 1024 threads per group, contiguous record ranges, one scan
+__global__ __launch_bounds__(kAcThreads) void ans_emit_kernel(AnsArgs a) {
+  __shared__ uint32_t sBits[kEmitLdsWords];
+  __shared__ uint32_t sWave[kAcThreads / 64];
+  const uint32_t g = a.g0 + blockIdx.x;
+  const uint32_t n = a.ntok[g * 3] + a.ntok[g * 3 + 1] + a.ntok[g * 3 + 2];
+  const uint64_t b = a.tbase[g];
+  for (int i = threadIdx.x; i < kEmitLdsWords; i += blockDim.x) sBits[i] = 0;
+  const uint32_t per = (n + kAcThreads - 1) / kAcThreads;
+  const uint32_t k0 = min(n, threadIdx.x * per), k1 = min(n, k0 + per);
+  uint32_t tot = 0;
+  for (uint32_t k = k0; k < k1; k++) tot += a.len[b + k];
+  uint32_t total;
+  const uint32_t off = 32 + block_excl_scan1024(tot, sWave, &total);
+  total += 32;
+  const uint64_t base = a.base[g];
+  const bool lds = total <= (uint32_t)kEmitLdsWords * 32u;
+  BitSink s = lds ? BitSink{sBits, off, 0, 0} : BitSink{a.scratch, base + off, 0, 0};
+  for (uint32_t k = k0; k < k1; k++) s.put(a.len[b + k], a.val[b + k]);
+  s.finish();
+  if (threadIdx.x == 0) {
+    BitSink h = lds ? BitSink{sBits, 0, 0, 0} : BitSink{a.scratch, base, 0, 0};
+    h.put(32, a.state[g]);
+    h.finish();
+  }
+  if (lds) {
+    __syncthreads();
+    const uint32_t nw = (total + 31) / 32;
+    uint32_t* dst = a.scratch + (base >> 5);
+    for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = sBits[i];
+  }
+  if (threadIdx.x == 0) a.bits[g] = total;
+}
+
+void launch_ac_tokens(const AcArgs& a, uint32_t ngroups, hipStream_t s) {
+  if (ngroups) hipLaunchKernelGGL(ac_tokens_kernel, dim3(ngroups), dim3(kAcThreads), 0, s, a);
+}
+void launch_ans(const AnsArgs& a, hipStream_t s) {
+  const uint32_t n = a.g1 - a.g0;
+  if (!n) return;
+  hipLaunchKernelGGL(ans_encode_kernel, dim3((n + 63) / 64), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(ans_emit_kernel, dim3(n), dim3(kAcThreads), 0, s, a);
+}
+
 void launch_ac_hist(const AcArgs& a, uint32_t ngroups, hipStream_t s) {
   if (ngroups) hipLaunchKernelGGL(ac_hist_kernel, dim3(ngroups), dim3(kAcThreads), 0, s, a);
 }

@@ -239,6 +239,197 @@ void write_histograms(BitWriter& w, const std::vector<uint8_t>& ctxmap, int nhis
   for (int h = 0; h < nhist; h++) write_prefix_code(w, codes[h]);
 }
 
+// ---------------------------------------------------------------------------
+// ANS tables [ext spec Annex C]: same algorithm as oracle/ans.c
+// ---------------------------------------------------------------------------
+static int logcount(uint32_t f) {
+  int n = 0;
+  while (f) {
+    n++;
+    f >>= 1;
+  }
+  return n;
+}
+
+AnsTable build_ans_table(const uint32_t* counts) {
+  constexpr int kAlpha = 128, kTab = 4096, kEntry = kTab / kAlpha;
+  AnsTable t;
+  uint64_t total = 0;
+  int last = 0;
+  for (int s = 0; s < kAlpha; s++) {
+    total += counts[s];
+    if (counts[s]) {
+      t.nused++;
+      last = s;
+    }
+  }
+  if (t.nused <= 1) {
+    t.freq[t.nused ? last : 0] = kTab;
+    t.omit = t.nused ? last : 0;
+  } else {
+    for (int s = 0; s < kAlpha; s++) {
+      if (!counts[s]) continue;
+      const uint64_t f = counts[s] * (uint64_t)kTab / total;
+      t.freq[s] = (uint16_t)(f < 1 ? 1 : f);
+    }
+    int omit = -1, best = -1;
+    for (int s = 0; s < kAlpha; s++)
+      if (t.freq[s] && logcount(t.freq[s]) > best) {
+        best = logcount(t.freq[s]);
+        omit = s;
+      }
+    t.omit = omit;
+    t.omit_code = best;
+    int rem = kTab;
+    for (int s = 0; s < kAlpha; s++)
+      if (s != omit) rem -= t.freq[s];
+    while (rem < 1) {
+      int m = -1;
+      for (int s = 0; s < kAlpha; s++)
+        if (s != omit && t.freq[s] > 1 && (m < 0 || t.freq[s] > t.freq[m])) m = s;
+      t.freq[m]--;
+      rem++;
+    }
+    t.freq[omit] = (uint16_t)rem;
+  }
+  // alias table of the decoder, then its inverse
+  int cutoff[kAlpha], right[kAlpha], offset[kAlpha], cut[kAlpha];
+  int nz = 0, only = 0;
+  for (int i = 0; i < kAlpha; i++)
+    if (t.freq[i]) {
+      nz++;
+      only = i;
+    }
+  if (nz == 1) {
+    for (int i = 0; i < kAlpha; i++) {
+      right[i] = only;
+      offset[i] = i * kEntry;
+      cutoff[i] = 0;
+    }
+  } else {
+    int under[kAlpha], over[kAlpha], nu = 0, no = 0;
+    for (int i = 0; i < kAlpha; i++) {
+      cut[i] = t.freq[i];
+      right[i] = 0;
+      offset[i] = 0;
+      if (cut[i] > kEntry)
+        over[no++] = i;
+      else if (cut[i] < kEntry)
+        under[nu++] = i;
+    }
+    while (no) {
+      const int o = over[no - 1];
+      const int u = under[--nu];
+      const int by = kEntry - cut[u];
+      cut[o] -= by;
+      right[u] = o;
+      offset[u] = cut[o];
+      if (cut[o] < kEntry) {
+        no--;
+        under[nu++] = o;
+      } else if (cut[o] == kEntry) {
+        no--;
+      }
+    }
+    for (int i = 0; i < kAlpha; i++) {
+      if (cut[i] == kEntry) {
+        right[i] = i;
+        offset[i] = 0;
+        cutoff[i] = 0;
+      } else {
+        offset[i] -= cut[i];
+        cutoff[i] = cut[i];
+      }
+    }
+  }
+  int c = 0;
+  for (int s = 0; s < kAlpha; s++) {
+    t.cum[s] = (uint16_t)c;
+    c += t.freq[s];
+  }
+  t.inv.assign(kTab, 0);
+  for (int res = 0; res < kTab; res++) {
+    const int i = res / kEntry, pos = res % kEntry;
+    int sym, off;
+    if (pos >= cutoff[i]) {
+      sym = right[i];
+      off = offset[i] + pos;
+    } else {
+      sym = i;
+      off = pos;
+    }
+    t.inv[t.cum[sym] + off] = (uint16_t)res;
+  }
+  return t;
+}
+
+static void write_varlen8(BitWriter& w, uint32_t v) {
+  if (v == 0) {
+    w.put(1, 0);
+    return;
+  }
+  uint32_t n = 0;
+  while ((v >> (n + 1)) != 0) n++;
+  w.put(1, 1);
+  w.put(3, n);
+  w.put(n, v - (1u << n));
+}
+
+void write_ans_histogram(BitWriter& w, const AnsTable& t) {
+  static const uint8_t kLcBits[14] = {5, 4, 4, 4, 4, 4, 3, 3, 3, 3, 3, 6, 7, 7};
+  static const uint8_t kLcCode[14] = {17, 11, 15, 3, 9, 7, 4, 2, 5, 6, 0, 33, 1, 65};
+  if (t.nused <= 2) {
+    int syms[2], n = 0;
+    for (int s = 0; s < 128 && n < 2; s++)
+      if (t.freq[s]) syms[n++] = s;
+    if (n == 0) syms[n++] = 0;
+    w.put(1, 1);
+    w.put(1, (uint32_t)(n - 1));
+    for (int i = 0; i < n; i++) write_varlen8(w, (uint32_t)syms[i]);
+    if (n == 2) w.put(12, t.freq[syms[0]]);
+    return;
+  }
+  w.put(1, 0);
+  w.put(1, 0);
+  w.put(3, 7);  // shift 12
+  w.put(3, 5);
+  int length = 0;
+  for (int s = 0; s < 128; s++)
+    if (t.freq[s]) length = s + 1;
+  write_varlen8(w, (uint32_t)(length - 3));
+  for (int s = 0; s < length; s++) {
+    const int code = s == t.omit ? t.omit_code : logcount(t.freq[s]);
+    w.put(kLcBits[code], kLcCode[code]);
+  }
+  for (int s = 0; s < length; s++) {
+    if (s == t.omit || t.freq[s] == 0) continue;
+    const int L = logcount(t.freq[s]) - 1;
+    if (L > 0) w.put((uint32_t)L, t.freq[s] & ((1u << L) - 1));
+  }
+}
+
+void write_ans_histograms(BitWriter& w, const std::vector<uint8_t>& ctxmap, int nhist,
+                          const std::vector<AnsTable>& tables, const UintCfg& cfg,
+                          const BitWriter* ctxmap_bits) {
+  w.put(1, 0);  // lz77.enabled
+  if (ctxmap.size() > 1) {
+    if (ctxmap_bits)
+      w.append(*ctxmap_bits);
+    else
+      write_context_map(w, ctxmap, nhist);
+  }
+  w.put(1, 0);      // use_prefix_code = 0
+  w.put(2, 7 - 5);  // log_alpha 7
+  for (int h = 0; h < nhist; h++) {  // uint config at log_alpha 7
+    w.put(3, cfg.split_exp);
+    if (cfg.split_exp != 7) {
+      w.put(ceil_log2(cfg.split_exp + 1), cfg.msb);
+      w.put(ceil_log2(cfg.split_exp - cfg.msb + 1), cfg.lsb);
+    }
+  }
+  for (int h = 0; h < nhist; h++) write_ans_histogram(w, tables[h]);
+}
+
 // DC: split on channel -> leaves (Y), (B), (X); clamped gradient predictor
 const TreeNode kDcTree[5] = {{0, 0, 1, 2, 0, -1},
                              {0, 1, 3, 4, 0, -1},

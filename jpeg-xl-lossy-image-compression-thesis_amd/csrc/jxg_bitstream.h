@@ -81,6 +81,23 @@ void write_histograms(BitWriter& w, const std::vector<uint8_t>& ctxmap, int nhis
 // on the map; callers may cache it)
 void write_context_map(BitWriter& w, const std::vector<uint8_t>& map, int nhist);
 
+// ANS (12-bit rANS, alias mapping, alphabet 128) for the AC stream: the
+// restated encoder choices of oracle/ans.c (normalization, omitted symbol,
+// full-precision histograms) -- the device kernels encode with these tables
+struct AnsTable {
+  std::array<uint16_t, 128> freq{};
+  std::array<uint16_t, 128> cum{};
+  std::vector<uint16_t> inv;  // [cum[s] + off] -> alias-table position (4096)
+  int nused = 0, omit = 0, omit_code = 0;
+};
+AnsTable build_ans_table(const uint32_t* counts /* [128] */);
+void write_ans_histogram(BitWriter& w, const AnsTable& t);
+// DecodeHistograms for ANS: lz77 off, context map, use_prefix_code = 0,
+// log_alpha 7, uint configs, histograms
+void write_ans_histograms(BitWriter& w, const std::vector<uint8_t>& ctxmap, int nhist,
+                          const std::vector<AnsTable>& tables, const UintCfg& cfg,
+                          const BitWriter* ctxmap_bits = nullptr);
+
 // Modular MA trees used by the LF-group streams (local trees, no transforms)
 struct TreeNode {
   int prop, splitval, lchild, rchild, predictor, leaf;  // prop < 0: leaf

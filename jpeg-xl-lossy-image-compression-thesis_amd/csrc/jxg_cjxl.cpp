@@ -120,7 +120,7 @@ int main(int argc, char** argv) {
   if (argc < 3) {
     std::fprintf(stderr,
                  "usage: %s INPUT OUTPUT [--distance=D] [--effort=E] "
-                 "[--proposals=none|P|F|PF] [--device=N]\n",
+                 "[--proposals=none|P|F|PF] [--coder=prefix|ans] [--device=N]\n",
                  argv[0]);
     return 1;
   }
@@ -134,6 +134,13 @@ int main(int argc, char** argv) {
     else if (!std::strncmp(a, "--proposals=", 12)) {
       const char* v = a + 12;
       p.proposals = (std::strchr(v, 'P') ? JXG_PROPOSAL_P : 0u) | (std::strchr(v, 'F') ? JXG_PROPOSAL_F : 0u);
+    } else if (!std::strncmp(a, "--coder=", 8)) {
+      if (!std::strcmp(a + 8, "ans"))
+        p.flags |= JXG_FLAG_ANS;
+      else if (std::strcmp(a + 8, "prefix")) {
+        std::fprintf(stderr, "unknown coder: %s\n", a + 8);
+        return 1;
+      }
     } else if (!std::strncmp(a, "--device=", 9))
       p.device = std::atoi(a + 9);
     else {

@@ -417,6 +417,10 @@ struct Ctx {
       stream_chunks, stream_bits, scratch, chunks, out;
   DevBuf<uint64_t> gbase, chunkoff, stream_base;
   DevBuf<uint32_t> tile_list;
+  DevBuf<uint32_t> tokens, tval, ans_state;  // ANS coder
+  DevBuf<uint8_t> tlen;
+  DevBuf<uint64_t> tbase;
+  DevBuf<uint16_t> ans_freq, ans_cum, ans_inv;
   DevBuf<LfRow> rows;
   DevBuf<LfChunk> lfchunks;
   DevBuf<ConcatPiece> pieces;
@@ -553,13 +557,14 @@ struct Job {
   const uint8_t* d_rgb = nullptr;
   int max_s = 0;
   bool homog = false;
+  bool ans = false;  // ANS instead of prefix codes for the AC stream
   uint32_t nrows = 0, nchunks = 0, nstreams = 0;
   AcArgs aa{};
   LfArgs la{};
   // host stage results
   std::vector<BitWriter> preA, preB;
   BitWriter lfglobal, hfglobal;
-  std::vector<uint64_t> gbase, sbase;
+  std::vector<uint64_t> gbase, sbase, tbase;
   float ms_codes = 0.0f;
 };
 
@@ -570,6 +575,7 @@ static jxg_status stage_alloc(Ctx* c, Job& J) {
   const Frame& f = J.f;
   const size_t nb = (size_t)f.bxs * f.bys;
   J.homog = (P.proposals & 3u) != 0;
+  J.ans = (P.flags & JXG_FLAG_ANS) != 0;
   jxg_status st = init_constants(c);
   if (st) return st;
   JXG_HIP(c->acs.ensure(nb));
@@ -812,9 +818,24 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
     ctxmap[ctx] = (uint8_t)(dense[cl] < 0 ? 0 : dense[cl]);
   }
   std::vector<PrefixCode> codes(std::max(nhist, 1));
+  std::vector<AnsTable> ans_tables(J.ans ? std::max(nhist, 1) : 0);
   std::vector<uint32_t> packed(kMaxClusters * kAlpha, 0);
+  std::vector<uint16_t> afreq, acum, ainv;
+  if (J.ans) {
+    afreq.assign(kMaxClusters * 128, 0);
+    acum.assign(kMaxClusters * 128, 0);
+    ainv.assign((size_t)kMaxClusters * 4096, 0);
+  }
   for (int cl = 0; cl < kMaxClusters; cl++) {
     if (dense[cl] < 0) continue;
+    if (J.ans) {
+      AnsTable& t = ans_tables[dense[cl]];
+      t = build_ans_table(c->h_hist_ac.p + cl * kAlpha);
+      std::copy(t.freq.begin(), t.freq.end(), afreq.begin() + cl * 128);
+      std::copy(t.cum.begin(), t.cum.end(), acum.begin() + cl * 128);
+      std::copy(t.inv.begin(), t.inv.end(), ainv.begin() + (size_t)cl * 4096);
+      continue;
+    }
     codes[dense[cl]] = build_prefix_code(c->h_hist_ac.p + cl * kAlpha, kAlpha);
     for (int k = 0; k < kAlpha; k++) packed[cl * kAlpha + k] = codes[dense[cl]].packed(k);
   }
@@ -877,15 +898,25 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
       c->cm_last = ctxmap;
       c->cm_nhist = nhist;
     }
-    write_histograms(hfglobal, ctxmap, nhist, codes, kCfg420, &c->cm_bits);
+    if (J.ans)
+      write_ans_histograms(hfglobal, ctxmap, nhist, ans_tables, kCfg420, &c->cm_bits);
+    else
+      write_histograms(hfglobal, ctxmap, nhist, codes, kCfg420, &c->cm_bits);
   }
   // scratch layout: the plan's AC groups then LF streams (32-bit aligned)
   J.gbase.assign(f.ngroups, 0);
   J.sbase.assign(nstreams, 0);
   uint64_t cursor = 0;
+  J.tbase.assign(f.ngroups, 0);
+  uint64_t ntokens = 0;
   for (uint32_t g = J.plan.g0; g < J.plan.g1; g++) {
     J.gbase[g] = cursor;
-    cursor += ((uint64_t)c->h_bound.p[g] + 63) & ~31ull;
+    const uint64_t nt = (uint64_t)c->h_ntok.p[g * 3] + c->h_ntok.p[g * 3 + 1] + c->h_ntok.p[g * 3 + 2];
+    // ANS: <= 16 + raw bits per token (prefix: <= 15 + raw) and the 32-bit state
+    const uint64_t bound = (uint64_t)c->h_bound.p[g] + (J.ans ? nt + 32 : 0);
+    cursor += (bound + 63) & ~31ull;
+    J.tbase[g] = ntokens;
+    ntokens += nt;
   }
   for (uint32_t i = 0; i < nstreams; i++) {
     J.sbase[i] = cursor;
@@ -894,6 +925,22 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
   const uint64_t scratch_words = cursor / 32 + 2;
   J.ms_codes = ms_since(t_codes);
   JXG_HIP(c->scratch.ensure(scratch_words));
+  if (J.ans) {
+    JXG_HIP(c->tokens.ensure(ntokens));
+    JXG_HIP(c->tval.ensure(ntokens));
+    JXG_HIP(c->tlen.ensure(ntokens));
+    JXG_HIP(c->tbase.ensure(f.ngroups));
+    JXG_HIP(c->ans_state.ensure(f.ngroups));
+    JXG_HIP(c->ans_freq.ensure(afreq.size()));
+    JXG_HIP(c->ans_cum.ensure(acum.size()));
+    JXG_HIP(c->ans_inv.ensure(ainv.size()));
+    JXG_HIP(hipMemcpyAsync(c->tbase.p, J.tbase.data(), J.tbase.size() * 8, hipMemcpyHostToDevice, s));
+    JXG_HIP(hipMemcpyAsync(c->ans_freq.p, afreq.data(), afreq.size() * 2, hipMemcpyHostToDevice, s));
+    JXG_HIP(hipMemcpyAsync(c->ans_cum.p, acum.data(), acum.size() * 2, hipMemcpyHostToDevice, s));
+    JXG_HIP(hipMemcpyAsync(c->ans_inv.p, ainv.data(), ainv.size() * 2, hipMemcpyHostToDevice, s));
+    // the host tables must outlive the async copies
+    JXG_HIP(hipStreamSynchronize(s));
+  }
   JXG_HIP(hipMemcpyAsync(c->codes_ac.p, packed.data(), packed.size() * 4, hipMemcpyHostToDevice, s));
   JXG_HIP(hipMemcpyAsync(c->lfcodes.p, lfpacked.data(), lfpacked.size() * 4, hipMemcpyHostToDevice, s));
   JXG_HIP(hipMemcpyAsync(c->gbase.p, J.gbase.data(), J.gbase.size() * 8, hipMemcpyHostToDevice, s));
@@ -908,7 +955,29 @@ static jxg_status stage_emit(Ctx* c, Job& J) {
   const Frame& f = J.f;
   J.aa.scratch = c->scratch.p;
   J.la.scratch = c->scratch.p;
-  launch_ac_emit(J.aa, J.plan.g1 - J.plan.g0, s);
+  if (J.ans) {
+    J.aa.tokens = c->tokens.p;
+    J.aa.tbase = c->tbase.p;
+    launch_ac_tokens(J.aa, J.plan.g1 - J.plan.g0, s);
+    AnsArgs na{};
+    na.tokens = c->tokens.p;
+    na.val = c->tval.p;
+    na.len = c->tlen.p;
+    na.tbase = c->tbase.p;
+    na.ntok = c->ntok.p;
+    na.freq = c->ans_freq.p;
+    na.cum = c->ans_cum.p;
+    na.inv = c->ans_inv.p;
+    na.state = c->ans_state.p;
+    na.base = c->gbase.p;
+    na.scratch = c->scratch.p;
+    na.bits = c->gbits.p;
+    na.g0 = J.plan.g0;
+    na.g1 = J.plan.g1;
+    launch_ans(na, s);
+  } else {
+    launch_ac_emit(J.aa, J.plan.g1 - J.plan.g0, s);
+  }
   if (J.nchunks) launch_lf_bits(J.la, J.nchunks, s);
   launch_lf_scan(J.la, J.nstreams, s);
   if (J.nchunks) launch_lf_emit(J.la, J.nchunks, s);

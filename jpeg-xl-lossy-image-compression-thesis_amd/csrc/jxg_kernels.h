@@ -90,7 +90,28 @@ struct AcArgs {
   const uint64_t* base;  // [ngroups] scratch bit offset (emit pass)
   uint32_t* scratch;     // bit buffer (emit pass, zeroed)
   uint32_t* bits;        // [ngroups] exact bits (emit pass)
+  uint32_t* tokens;      // ANS: token records (cluster | tok << 8 | nbits << 14 | bits << 18)
+  const uint64_t* tbase; // ANS: [ngroups] first token of each group
 };
+
+// ANS coding of the pass groups' token records (jxg_ac.hip)
+struct AnsArgs {
+  const uint32_t* tokens;  // token records of ac_tokens_kernel
+  uint32_t* val;           // [tokens] emitted bits: 16-bit chunk (if any) then raw bits
+  uint8_t* len;            // [tokens] number of emitted bits
+  const uint64_t* tbase;   // [ngroups]
+  const uint32_t* ntok;    // [ngroups][3]
+  const uint16_t* freq;    // [132][128] normalized frequencies (sum 4096)
+  const uint16_t* cum;     // [132][128]
+  const uint16_t* inv;     // [132][4096] alias-table position of (symbol, offset)
+  uint32_t* state;         // [ngroups] final encoder state (= stream's first 32 bits)
+  const uint64_t* base;    // [ngroups] scratch bit offset
+  uint32_t* scratch;
+  uint32_t* bits;          // [ngroups] exact bits
+  uint32_t g0, g1;         // groups [g0, g1)
+};
+void launch_ac_tokens(const AcArgs& a, uint32_t ngroups, hipStream_t s);
+void launch_ans(const AnsArgs& a, hipStream_t s);
 
 // LF-group modular streams: rows of (lf group, stream, channel, y)
 // One segment of <= kLfSeg samples of a channel row (long rows -- the

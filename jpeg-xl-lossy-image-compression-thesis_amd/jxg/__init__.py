@@ -32,6 +32,7 @@ PROPOSAL_P = 1
 PROPOSAL_F = 2
 FLAG_H1_INT_ABS = 1
 FLAG_KEEP_MAPS = 2
+FLAG_ANS = 4
 
 
 class JxgError(RuntimeError):

@@ -397,7 +397,7 @@ int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h, size_t row_strid
   memset(out, 0, sizeof(*out));
   if (!rgb || w == 0 || h == 0 || w > (1u << 18) || h > (1u << 18)) return -1;
   if (!(p->distance > 0.0f) || p->distance > 25.0f) return -2;
-  if (p->coder != 0) return -3; /* ANS writer: not in the oracle yet */
+  if (p->coder != 0 && p->coder != 1) return -3;
   jxo_frame f;
   jxo_frame_init(&f, w, h, p);
   const size_t plane = (size_t)f.xp * f.yp, nb = (size_t)f.bxs * f.bys;
@@ -514,8 +514,14 @@ int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h, size_t row_strid
     ctxmap[ctx] = (uint8_t)(dense[cl] < 0 ? 0 : dense[cl]);
   }
   jxo_prefix* codes = (jxo_prefix*)malloc(sizeof(jxo_prefix) * (nhist ? nhist : 1));
+  jxo_ans* ans = p->coder == 1 ? (jxo_ans*)malloc(sizeof(jxo_ans) * (nhist ? nhist : 1)) : NULL;
   for (int cl = 0; cl < JXO_MAX_CLUSTERS; cl++)
-    if (dense[cl] >= 0) jxo_build_prefix(hist[cl], JXO_ALPHA, &codes[dense[cl]]);
+    if (dense[cl] >= 0) {
+      if (ans)
+        jxo_ans_normalize(hist[cl], &ans[dense[cl]]);
+      else
+        jxo_build_prefix(hist[cl], JXO_ALPHA, &codes[dense[cl]]);
+    }
 
   /* ---- sections ---- */
   const int nsec = (f.ngroups == 1) ? 1 : (int)(2 + f.nlf + f.ngroups);
@@ -544,13 +550,51 @@ int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h, size_t row_strid
     jxo_bw_put(s, 1, 1); /* DequantMatrices all_default */
     jxo_bw_put(s, ceil_log2(f.ngroups), 0); /* num_hf_presets - 1 */
     put_u32_sel(s, 2, 0, 0);                /* used_orders = 0 */
-    put_histograms(s, JXO_AC_CTX, ctxmap, nhist, codes, &kCfg);
+    if (!ans) {
+      put_histograms(s, JXO_AC_CTX, ctxmap, nhist, codes, &kCfg);
+    } else {
+      /* ANS: lz77 off, context map, use_prefix_code = 0, log_alpha 7 */
+      jxo_bw_put(s, 1, 0);
+      put_context_map(s, JXO_AC_CTX, ctxmap, nhist);
+      jxo_bw_put(s, 1, 0);
+      jxo_bw_put(s, 2, 7 - 5);
+      for (int h = 0; h < nhist; h++) { /* uint config at log_alpha 7 */
+        jxo_bw_put(s, 3, kCfg.split_exp);
+        if (kCfg.split_exp != 7) {
+          jxo_bw_put(s, ceil_log2(kCfg.split_exp + 1), kCfg.msb);
+          jxo_bw_put(s, ceil_log2(kCfg.split_exp - kCfg.msb + 1), kCfg.lsb);
+        }
+      }
+      for (int h = 0; h < nhist; h++) jxo_ans_write_hist(s, &ans[h]);
+    }
   }
   for (uint32_t g = 0; g < f.ngroups; g++) {
     jxo_bw* s = &sec[2 + f.nlf + g];
-    for (size_t i = 0; i < gn[g]; i++)
-      put_token(s, &codes[ctxmap[gt[g][i].ctx]], &kCfg, gt[g][i].v);
+    if (!ans) {
+      for (size_t i = 0; i < gn[g]; i++)
+        put_token(s, &codes[ctxmap[gt[g][i].ctx]], &kCfg, gt[g][i].v);
+    } else {
+      const size_t n = gn[g];
+      uint8_t* th = (uint8_t*)malloc(n + 1);
+      uint8_t* ts = (uint8_t*)malloc(n + 1);
+      uint8_t* tn = (uint8_t*)malloc(n + 1);
+      uint32_t* tb = (uint32_t*)malloc(sizeof(uint32_t) * (n + 1));
+      for (size_t i = 0; i < n; i++) {
+        uint32_t tok, nb, bits;
+        jxo_hybrid(gt[g][i].v, &kCfg, &tok, &nb, &bits);
+        th[i] = ctxmap[gt[g][i].ctx];
+        ts[i] = (uint8_t)tok;
+        tn[i] = (uint8_t)nb;
+        tb[i] = bits;
+      }
+      jxo_ans_write_stream(s, ans, n, th, ts, tn, tb);
+      free(th);
+      free(ts);
+      free(tn);
+      free(tb);
+    }
   }
+  free(ans);
 
   /* ---- assemble ---- */
   jxo_bw o;

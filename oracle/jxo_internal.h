@@ -121,4 +121,16 @@ typedef struct {
 void jxo_build_prefix(const uint32_t* counts, int n, jxo_prefix* p);
 void jxo_write_prefix(jxo_bw* w, const jxo_prefix* p);
 
+/* ANS (ans.c): normalized 12-bit frequencies, alias inverse */
+typedef struct {
+  uint16_t freq[128];
+  uint16_t cum[128];
+  uint16_t inv[4096]; /* [cum[s] + off] -> alias table position */
+  int nused, omit, omit_code;
+} jxo_ans;
+void jxo_ans_normalize(const uint32_t* counts /* [128] */, jxo_ans* a);
+void jxo_ans_write_hist(jxo_bw* w, const jxo_ans* a);
+void jxo_ans_write_stream(jxo_bw* w, const jxo_ans* hists, size_t n, const uint8_t* hist,
+                          const uint8_t* sym, const uint8_t* nbits, const uint32_t* bits);
+
 #endif

@@ -147,3 +147,22 @@ def test_hook_f_nan_merges_match_oracle(jxg_mod, oracle):
     assert ((ref.acs[:8, :8] & 0x7F) == 20).all()
     assert np.array_equal(st["acs"], ref.acs)
     assert got == ref.bytes
+
+
+# ANS coding of the AC stream (JXG_FLAG_ANS) against the oracle's coder=1
+ANS_CASES = [(64, 64, 1.0, 7, 0), (300, 200, 1.0, 7, 3), (520, 300, 2.0, 5, 0),
+             (1000, 700, 0.5, 7, 2), (9, 7, 3.0, 7, 3), (1920, 1080, 1.0, 7, 0)]
+
+
+@pytest.mark.parametrize("w,h,d,e,p", ANS_CASES)
+def test_ans_matches_oracle(jxg_mod, oracle, decoder, w, h, d, e, p):
+    from jxg.synth import synth_rgb8
+
+    img = synth_rgb8(w, h, w * 5 + h)
+    with jxg_mod.Encoder(distance=d, effort=e, proposals=p, flags=jxg_mod.FLAG_ANS) as enc:
+        got = enc.encode(img)
+    ref = oracle.encode(img, d, e, p, 1)
+    assert got == ref.bytes
+    if w * h <= 520 * 300:
+        dec = decoder.decode(got)
+        assert np.array_equal(dec.ac, ref.ac)

@@ -110,3 +110,30 @@ def test_multiprocess_encode_sharded(jxg_mod):
         p.join(300)
         assert p.exitcode == 0
     assert q.get(timeout=10) is True
+
+
+def test_sharded_ans_equals_single(jxg_mod):
+    from jxg.synth import synth_rgb8
+
+    img = synth_rgb8(1500, 900, 17)
+    with jxg_mod.Encoder(distance=1.0, effort=7, flags=jxg_mod.FLAG_ANS) as enc:
+        ref = enc.encode(img)
+    import torch
+
+    h, w, _ = img.shape
+    world = 3
+    t = torch.from_numpy(img).cuda()
+    hist_words, slot = jxg_mod.shard_sizes(w, h, world)
+    encs = [jxg_mod.Encoder(distance=1.0, effort=7, flags=jxg_mod.FLAG_ANS) for _ in range(world)]
+    hists = [torch.zeros(hist_words, dtype=torch.int32, device="cuda") for _ in range(world)]
+    xbufs = [torch.zeros(world * slot, dtype=torch.uint8, device="cuda") for _ in range(world)]
+    for r in range(world):
+        encs[r].shard_begin(t.data_ptr(), w, h, r, world, hists[r].data_ptr(), xbufs[r].data_ptr())
+    hist = torch.stack(hists).sum(0).to(torch.int32).contiguous()
+    xbuf = torch.cat([xbufs[r][r * slot:(r + 1) * slot] for r in range(world)]).contiguous()
+    torch.cuda.synchronize()
+    payloads = [encs[r].shard_payload_bytes(encs[r].shard_end(hist.data_ptr(), xbuf.data_ptr()))
+                for r in range(world)]
+    for e in encs:
+        e.close()
+    assert jxg_mod.shard_assemble(payloads) == ref
