@@ -468,34 +468,94 @@ __global__ __launch_bounds__(kAcThreads) void ac_tokens_kernel(AcArgs a) {
   }
 }
 
-// rANS backwards over each group's records, one lane per group; the next
-// record is fetched one step ahead (only the inverse-table lookup depends on
-// the running state)
-__global__ __launch_bounds__(64) void ans_encode_kernel(AnsArgs a) {
-  const uint32_t g = a.g0 + blockIdx.x * 64 + threadIdx.x;
+// rANS backwards over each group's records, one wave per group, 4 groups per
+// workgroup sharing the LDS tables (all alias inverses, 128 KB).  The state
+// recurrence is a uniform chain kept in VALU registers (a microbenchmark on
+// MI355X: dependent VALU op ~4.5 cycles, uniform LDS read ~70, while every
+// VALU <-> SALU crossing -- readlane, ballot -- costs ~30): per step compare,
+// select, magic-number division, one LDS lookup.  The lanes serve it: per 64
+// records they decode record, bound, division constants and table base in
+// parallel (the next 64 records are fetched meanwhile), and each lane keeps the
+// chunk of "its" record for one coalesced store of the record's emitted bits.
+constexpr int kAnsWaves = 4;
+__global__ __launch_bounds__(kAnsWaves * 64) void ans_encode_kernel(AnsArgs a) {
+  __shared__ uint32_t sSym[kAnsHists * 128];
+  __shared__ uint32_t sDiv[kAnsHists * 128];
+  __shared__ uint32_t sInv[kAnsHists * 4096 / 2];  // u16 pairs
+  __shared__ uint8_t sMap[136];
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(a.tab);
+  for (uint32_t i = threadIdx.x; i < a.nhist * 128; i += blockDim.x) {
+    sSym[i] = src[i];
+    sDiv[i] = src[kAnsDivOff / 4 + i];
+  }
+  for (uint32_t i = threadIdx.x; i < a.nhist * 2048; i += blockDim.x)
+    sInv[i] = src[kAnsInvOff / 4 + i];
+  for (uint32_t i = threadIdx.x; i < 136; i += blockDim.x) sMap[i] = a.tab[kAnsMapOff + i];
+  __syncthreads();
+  const uint16_t* inv = reinterpret_cast<const uint16_t*>(sInv);
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t g =
+      __builtin_amdgcn_readfirstlane(a.g0 + blockIdx.x * kAnsWaves + (threadIdx.x >> 6));
   if (g >= a.g1) return;
-  const uint32_t n = a.ntok[g * 3] + a.ntok[g * 3 + 1] + a.ntok[g * 3 + 2];
+  const int n = (int)(a.ntok[g * 3] + a.ntok[g * 3 + 1] + a.ntok[g * 3 + 2]);
   const uint64_t b = a.tbase[g];
   uint32_t x = 0x130000u;
-  uint32_t r = n ? a.tokens[b + n - 1] : 0u;
-  for (uint32_t k = n; k-- > 0;) {
-    const uint32_t rn = k ? a.tokens[b + k - 1] : 0u;  // prefetch
-    const uint32_t cl = r & 0xFF, tok = (r >> 8) & 63, nb = (r >> 14) & 15, raw = r >> 18;
-    const uint32_t f = a.freq[cl * 128 + tok];
-    const uint32_t c0 = a.cum[cl * 128 + tok];
-    uint32_t v = raw, l = nb;
-    if ((x >> 20) >= f) {
-      v = (x & 0xFFFFu) | (raw << 16);
-      l += 16;
-      x >>= 16;
+  uint32_t rec = (int)lane < min(64, n) ? a.tokens[b + n - 1 - lane] : 0u;
+  for (int hi = n; hi > 0; hi -= 64) {
+    const int cnt = min(64, hi);
+    // lane L: record hi - 1 - L -> renormalization bound, division constants,
+    // f, inverse-table base
+    uint32_t T = 0xFFFFFFFFu, M = 0, s1 = 0, s2 = 0, nf2 = (uint32_t)-8192, base = 0;
+    if ((int)lane < cnt) {
+      const uint32_t h = sMap[rec & 0xFF], sym = h * 128 + ((rec >> 8) & 63);
+      const uint32_t e = sSym[sym];
+      const uint32_t f = (e & 0xFFF) + 1;
+      nf2 = (uint32_t)(-(int)(2 * f));
+      base = 2 * (h * 4096 + (e >> 12));  // byte offset of the symbol's inverse row
+      M = sDiv[sym];
+      const uint32_t lg = f > 1 ? 32 - __clz(f - 1) : 0;
+      s1 = f > 1 ? 1 : 0;
+      s2 = lg > 0 ? lg - 1 : 0;
+      T = f < 4096 ? (f << 20) - 1 : 0xFFFFFFFFu;  // emit a chunk when x > T
     }
-    const uint32_t q = x / f, rem = x - q * f;
-    x = (q << 12) + a.inv[(size_t)cl * 4096 + c0 + rem];
-    a.val[b + k] = v;
-    a.len[b + k] = (uint8_t)l;
-    r = rn;
+    const int hn = hi - 64;
+    const uint32_t nrec = (int)lane < min(64, hn) ? a.tokens[b + hn - 1 - lane] : 0u;
+    uint32_t och = 0;  // lane L: the state before record L's chunk (0: none)
+    auto step = [&](int i) {
+      const uint32_t Ti = __builtin_amdgcn_readlane(T, i);
+      const uint32_t Mi = __builtin_amdgcn_readlane(M, i);
+      const uint32_t s1i = __builtin_amdgcn_readlane(s1, i);
+      const uint32_t s2i = __builtin_amdgcn_readlane(s2, i);
+      const uint32_t nf2i = __builtin_amdgcn_readlane(nf2, i);
+      const uint32_t bi = __builtin_amdgcn_readlane(base, i);
+      const bool emit = x > Ti;  // (x >> 20) >= f
+      och = lane == (uint32_t)i ? (emit ? x : 0u) : och;
+      x = emit ? x >> 16 : x;
+      // q = floor(x / f); f = 1: magic 0, s1 = s2 = 0 -> q = x
+      const uint32_t x2 = 2 * x + bi;  // (mod 2^32; the difference below is small)
+      const uint32_t t = __umulhi(x, Mi);
+      const uint32_t q = (t + ((x - t) >> s1i)) >> s2i;
+      // byte address 2 (base + x - q f): one 24-bit multiply-add (q < 2^20)
+      uint32_t addr;
+      asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(addr) : "v"(q), "s"(nf2i), "v"(x2));
+      x = (q << 12) + *reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(inv) + addr);
+      asm volatile("" : "+v"(x));  // keep the chain in VALU registers
+    };
+    if (cnt == 64) {
+#pragma unroll
+      for (int i = 0; i < 64; i++) step(i);
+    } else {
+      for (int i = 0; i < cnt; i++) step(i);
+    }
+    if ((int)lane < cnt) {
+      // emitted bits of the record: [16-bit chunk] then its raw bits
+      const uint32_t raw = rec >> 18, nb = (rec >> 14) & 15;
+      a.val[b + hi - 1 - lane] = och ? (och & 0xFFFFu) | raw << 16 : raw;
+      a.len[b + hi - 1 - lane] = (uint8_t)(och ? nb + 16 : nb);
+    }
+    rec = nrec;
   }
-  a.state[g] = x;
+  if (lane == 0) a.state[g] = __builtin_amdgcn_readfirstlane(x);
 }
 
 // bit placement: the 32-bit state, then every record's bits, in order;
@@ -539,7 +599,8 @@ void launch_ac_tokens(const AcArgs& a, uint32_t ngroups, hipStream_t s) {
 void launch_ans(const AnsArgs& a, hipStream_t s) {
   const uint32_t n = a.g1 - a.g0;
   if (!n) return;
-  hipLaunchKernelGGL(ans_encode_kernel, dim3((n + 63) / 64), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(ans_encode_kernel, dim3((n + kAnsWaves - 1) / kAnsWaves), dim3(kAnsWaves * 64),
+                     0, s, a);
   hipLaunchKernelGGL(ans_emit_kernel, dim3(n), dim3(kAcThreads), 0, s, a);
 }
 

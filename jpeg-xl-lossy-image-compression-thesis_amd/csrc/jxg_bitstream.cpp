@@ -251,6 +251,98 @@ static int logcount(uint32_t f) {
   return n;
 }
 
+// ---------------------------------------------------------------------------
+// Histogram clustering for ANS [ext libjxl enc_cluster.cc
+// FastClusterHistograms, restated in oracle/ans.c jxo_ans_cluster]: at most
+// kAnsMaxHists farthest-point centres, every histogram joins its nearest one.
+// Integer Q16 bit costs, so the choice is reproducible bit for bit.
+// ---------------------------------------------------------------------------
+namespace {
+constexpr uint16_t kLog2Frac[256] = {
+    0, 369, 736, 1102, 1466, 1829, 2190, 2551, 2909, 3267, 3623, 3978, 4331, 4683, 5034, 5384, 5732,
+    6079, 6425, 6769, 7112, 7454, 7795, 8134, 8473, 8810, 9146, 9480, 9814, 10146, 10477, 10807, 11136,
+    11464, 11791, 12116, 12440, 12764, 13086, 13407, 13727, 14046, 14363, 14680, 14996, 15310, 15624,
+    15937, 16248, 16559, 16868, 17177, 17484, 17791, 18096, 18401, 18704, 19007, 19308, 19609, 19909,
+    20207, 20505, 20802, 21098, 21393, 21687, 21980, 22272, 22564, 22854, 23144, 23433, 23720, 24007,
+    24293, 24579, 24863, 25146, 25429, 25711, 25992, 26272, 26551, 26830, 27108, 27384, 27660, 27936,
+    28210, 28484, 28757, 29029, 29300, 29571, 29840, 30109, 30378, 30645, 30912, 31178, 31443, 31707,
+    31971, 32234, 32496, 32758, 33019, 33279, 33538, 33797, 34055, 34312, 34569, 34825, 35080, 35334,
+    35588, 35841, 36094, 36346, 36597, 36847, 37097, 37346, 37595, 37842, 38090, 38336, 38582, 38827,
+    39072, 39316, 39559, 39802, 40044, 40286, 40527, 40767, 41006, 41246, 41484, 41722, 41959, 42196,
+    42432, 42667, 42902, 43137, 43370, 43603, 43836, 44068, 44300, 44530, 44761, 44990, 45220, 45448,
+    45676, 45904, 46131, 46357, 46583, 46809, 47034, 47258, 47482, 47705, 47928, 48150, 48372, 48593,
+    48813, 49034, 49253, 49472, 49691, 49909, 50127, 50344, 50560, 50776, 50992, 51207, 51422, 51636,
+    51850, 52063, 52276, 52488, 52700, 52911, 53122, 53332, 53542, 53751, 53960, 54169, 54377, 54584,
+    54791, 54998, 55204, 55410, 55615, 55820, 56025, 56229, 56432, 56635, 56838, 57040, 57242, 57443,
+    57644, 57845, 58045, 58245, 58444, 58643, 58841, 59039, 59237, 59434, 59631, 59827, 60023, 60219,
+    60414, 60609, 60803, 60997, 61190, 61384, 61576, 61769, 61961, 62152, 62343, 62534, 62725, 62915,
+    63104, 63294, 63483, 63671, 63859, 64047, 64234, 64421, 64608, 64794, 64980, 65166, 65351};
+
+inline int64_t log2_q16(uint32_t v) {
+  const int e = 31 - __builtin_clz(v);
+  const uint32_t m = e >= 8 ? (v >> (e - 8)) & 255u : (v << (8 - e)) & 255u;
+  return ((int64_t)e << 16) + kLog2Frac[m];
+}
+
+int64_t hist_cost(const uint32_t* h, uint64_t t) {
+  if (!t) return 0;
+  const int64_t lt = log2_q16((uint32_t)std::min<uint64_t>(t, 0xFFFFFFFFull));
+  int64_t c = 0;
+  for (int s = 0; s < 128; s++)
+    if (h[s]) c += (int64_t)h[s] * (lt - log2_q16(h[s]));
+  return c;
+}
+
+int64_t merge_cost(const uint32_t* a, uint64_t ta, int64_t ca, const uint32_t* b, uint64_t tb,
+                   int64_t cb) {
+  uint32_t m[128];
+  for (int s = 0; s < 128; s++) m[s] = a[s] + b[s];
+  return hist_cost(m, ta + tb) - ca - cb;
+}
+}  // namespace
+
+int cluster_ans_histograms(const uint32_t* hist, int nh, int* assign) {
+  std::vector<int64_t> cost(nh), dist(nh, 0);
+  std::vector<uint64_t> tot(nh, 0);
+  std::vector<uint8_t> centre(nh, 0);
+  int first = -1;
+  for (int i = 0; i < nh; i++) {
+    for (int s = 0; s < 128; s++) tot[i] += hist[i * 128 + s];
+    cost[i] = hist_cost(hist + i * 128, tot[i]);
+    assign[i] = -1;
+    if (tot[i] && (first < 0 || tot[i] > tot[first])) first = i;
+  }
+  if (first < 0) return 0;
+  int ncl = 1;
+  for (int i = 0; i < nh; i++) {
+    if (!tot[i]) continue;
+    assign[i] = 0;
+    if (i == first)
+      centre[i] = 1;
+    else
+      dist[i] = merge_cost(hist + i * 128, tot[i], cost[i], hist + first * 128, tot[first], cost[first]);
+  }
+  while (ncl < kAnsMaxHists) {
+    int pick = -1;
+    for (int i = 0; i < nh; i++)
+      if (tot[i] && !centre[i] && (pick < 0 || dist[i] > dist[pick])) pick = i;
+    if (pick < 0 || dist[pick] < kAnsMinDist) break;
+    const int c = ncl++;
+    assign[pick] = c;
+    centre[pick] = 1;
+    for (int i = 0; i < nh; i++) {
+      if (!tot[i] || centre[i]) continue;
+      const int64_t d =
+          merge_cost(hist + i * 128, tot[i], cost[i], hist + pick * 128, tot[pick], cost[pick]);
+      if (d < dist[i]) {
+        dist[i] = d;
+        assign[i] = c;
+      }
+    }
+  }
+  return ncl;
+}
+
 AnsTable build_ans_table(const uint32_t* counts) {
   constexpr int kAlpha = 128, kTab = 4096, kEntry = kTab / kAlpha;
   AnsTable t;

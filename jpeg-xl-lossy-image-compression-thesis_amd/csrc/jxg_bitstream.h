@@ -91,6 +91,12 @@ struct AnsTable {
   int nused = 0, omit = 0, omit_code = 0;
 };
 AnsTable build_ans_table(const uint32_t* counts /* [128] */);
+// ANS histogram clustering (oracle/ans.c jxo_ans_cluster): hist[nh][128] ->
+// assign[nh] (centre id, -1 for an empty histogram); returns the centre count
+// (<= kAnsMaxHists: their alias inverses fill 128 KB of LDS in the encoder)
+constexpr int kAnsMaxHists = 16;
+constexpr int64_t kAnsMinDist = 64ll << 16;  // Q16 bits
+int cluster_ans_histograms(const uint32_t* hist, int nh, int* assign);
 void write_ans_histogram(BitWriter& w, const AnsTable& t);
 // DecodeHistograms for ANS: lz77 off, context map, use_prefix_code = 0,
 // log_alpha 7, uint configs, histograms

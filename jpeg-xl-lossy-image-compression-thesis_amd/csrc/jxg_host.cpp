@@ -57,6 +57,8 @@ struct DevBuf {
   }
 };
 
+static_assert(kAnsHists == (uint32_t)kAnsMaxHists, "ANS table blob sized for kAnsMaxHists");
+
 template <class T>
 struct PinBuf {
   T* p = nullptr;
@@ -420,7 +422,8 @@ struct Ctx {
   DevBuf<uint32_t> tokens, tval, ans_state;  // ANS coder
   DevBuf<uint8_t> tlen;
   DevBuf<uint64_t> tbase;
-  DevBuf<uint16_t> ans_freq, ans_cum, ans_inv;
+  DevBuf<uint8_t> ans_tab;
+  PinBuf<uint8_t> h_ans_tab;
   DevBuf<LfRow> rows;
   DevBuf<LfChunk> lfchunks;
   DevBuf<ConcatPiece> pieces;
@@ -558,6 +561,7 @@ struct Job {
   int max_s = 0;
   bool homog = false;
   bool ans = false;  // ANS instead of prefix codes for the AC stream
+  uint32_t nhist_ans = 0;
   uint32_t nrows = 0, nchunks = 0, nstreams = 0;
   AcArgs aa{};
   LfArgs la{};
@@ -802,42 +806,72 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
   const Frame& f = J.f;
   const uint32_t nstreams = J.nstreams;
   const Clock::time_point t_codes = Clock::now();
+  // prefix codes: one histogram per (used) static cluster; ANS: the static
+  // clusters are clustered again into <= kAnsMaxHists groups (the alias
+  // inverses must fit the encoder's LDS).  Dense ids in order of first
+  // appearance over contexts (oracle/encode.c).
+  int group[kMaxClusters];
+  if (J.ans) {
+    cluster_ans_histograms(c->h_hist_ac.p, kMaxClusters, group);
+  } else {
+    int ng = 0;
+    for (int cl = 0; cl < kMaxClusters; cl++) {
+      uint64_t tot = 0;
+      for (int k = 0; k < kAlpha; k++) tot += c->h_hist_ac.p[cl * kAlpha + k];
+      group[cl] = tot ? ng++ : -1;
+    }
+  }
   int dense[kMaxClusters];
   std::fill(dense, dense + kMaxClusters, -1);
-  bool used[kMaxClusters];
-  for (int cl = 0; cl < kMaxClusters; cl++) {
-    uint64_t tot = 0;
-    for (int k = 0; k < kAlpha; k++) tot += c->h_hist_ac.p[cl * kAlpha + k];
-    used[cl] = tot != 0;
-  }
   int nhist = 0;
   std::vector<uint8_t> ctxmap(kAcCtx);
   for (int ctx = 0; ctx < kAcCtx; ctx++) {
-    const int cl = ac_cluster(ctx);
-    if (used[cl] && dense[cl] < 0) dense[cl] = nhist++;
-    ctxmap[ctx] = (uint8_t)(dense[cl] < 0 ? 0 : dense[cl]);
+    const int gr = group[ac_cluster(ctx)];
+    if (gr >= 0 && dense[gr] < 0) dense[gr] = nhist++;
+    ctxmap[ctx] = (uint8_t)(gr < 0 ? 0 : dense[gr]);
   }
   std::vector<PrefixCode> codes(std::max(nhist, 1));
   std::vector<AnsTable> ans_tables(J.ans ? std::max(nhist, 1) : 0);
   std::vector<uint32_t> packed(kMaxClusters * kAlpha, 0);
-  std::vector<uint16_t> afreq, acum, ainv;
   if (J.ans) {
-    afreq.assign(kMaxClusters * 128, 0);
-    acum.assign(kMaxClusters * 128, 0);
-    ainv.assign((size_t)kMaxClusters * 4096, 0);
-  }
-  for (int cl = 0; cl < kMaxClusters; cl++) {
-    if (dense[cl] < 0) continue;
-    if (J.ans) {
-      AnsTable& t = ans_tables[dense[cl]];
-      t = build_ans_table(c->h_hist_ac.p + cl * kAlpha);
-      std::copy(t.freq.begin(), t.freq.end(), afreq.begin() + cl * 128);
-      std::copy(t.cum.begin(), t.cum.end(), acum.begin() + cl * 128);
-      std::copy(t.inv.begin(), t.inv.end(), ainv.begin() + (size_t)cl * 4096);
-      continue;
+    std::vector<uint32_t> dh((size_t)std::max(nhist, 1) * kAlpha, 0);
+    for (int cl = 0; cl < kMaxClusters; cl++)
+      if (group[cl] >= 0)
+        for (int k = 0; k < kAlpha; k++) dh[dense[group[cl]] * kAlpha + k] += c->h_hist_ac.p[cl * kAlpha + k];
+    // device table blob (AnsArgs::tab): freq | cum << 16, alias inverses,
+    // static cluster -> dense histogram
+    JXG_HIP(c->h_ans_tab.ensure(kAnsTabBytes));
+    uint8_t* blob = c->h_ans_tab.p;
+    std::memset(blob, 0, kAnsTabBytes);
+    uint32_t* sym = reinterpret_cast<uint32_t*>(blob);
+    uint32_t* dv = reinterpret_cast<uint32_t*>(blob + kAnsDivOff);
+    uint16_t* inv = reinterpret_cast<uint16_t*>(blob + kAnsInvOff);
+    for (int h = 0; h < nhist; h++) {
+      AnsTable& t = ans_tables[h];
+      t = build_ans_table(dh.data() + h * kAlpha);
+      std::copy(t.inv.begin(), t.inv.end(), inv + (size_t)h * 4096);
+      for (int k = 0; k < 128; k++) {
+        const uint32_t f = t.freq[k];
+        if (!f) continue;
+        sym[h * 128 + k] = (f - 1) | (uint32_t)t.cum[k] << 12;
+        // round-up magic with the "add" fix-up: exact for every 32-bit x;
+        // f = 1 uses magic 0 and s1 = 0 (see ans_encode_kernel)
+        uint32_t lg = 0;
+        while ((1u << lg) < f) lg++;
+        dv[h * 128 + k] =
+            f == 1 ? 0u : (uint32_t)((((uint64_t)1 << 32) * ((1ull << lg) - f)) / f + 1);
+      }
     }
-    codes[dense[cl]] = build_prefix_code(c->h_hist_ac.p + cl * kAlpha, kAlpha);
-    for (int k = 0; k < kAlpha; k++) packed[cl * kAlpha + k] = codes[dense[cl]].packed(k);
+    for (int cl = 0; cl < kMaxClusters; cl++)
+      blob[kAnsMapOff + cl] = (uint8_t)(group[cl] >= 0 ? dense[group[cl]] : 0);
+    J.nhist_ans = (uint32_t)nhist;
+  } else {
+    for (int cl = 0; cl < kMaxClusters; cl++) {
+      if (group[cl] < 0) continue;
+      const int h = dense[group[cl]];
+      codes[h] = build_prefix_code(c->h_hist_ac.p + cl * kAlpha, kAlpha);
+      for (int k = 0; k < kAlpha; k++) packed[cl * kAlpha + k] = codes[h].packed(k);
+    }
   }
   // LF-group stream codes and preludes (the plan's LF groups)
   std::vector<uint32_t> lfpacked((size_t)nstreams * 4 * kAlpha, 0);
@@ -931,15 +965,11 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
     JXG_HIP(c->tlen.ensure(ntokens));
     JXG_HIP(c->tbase.ensure(f.ngroups));
     JXG_HIP(c->ans_state.ensure(f.ngroups));
-    JXG_HIP(c->ans_freq.ensure(afreq.size()));
-    JXG_HIP(c->ans_cum.ensure(acum.size()));
-    JXG_HIP(c->ans_inv.ensure(ainv.size()));
+    JXG_HIP(c->ans_tab.ensure(kAnsTabBytes));
     JXG_HIP(hipMemcpyAsync(c->tbase.p, J.tbase.data(), J.tbase.size() * 8, hipMemcpyHostToDevice, s));
-    JXG_HIP(hipMemcpyAsync(c->ans_freq.p, afreq.data(), afreq.size() * 2, hipMemcpyHostToDevice, s));
-    JXG_HIP(hipMemcpyAsync(c->ans_cum.p, acum.data(), acum.size() * 2, hipMemcpyHostToDevice, s));
-    JXG_HIP(hipMemcpyAsync(c->ans_inv.p, ainv.data(), ainv.size() * 2, hipMemcpyHostToDevice, s));
-    // the host tables must outlive the async copies
-    JXG_HIP(hipStreamSynchronize(s));
+    // pinned source: stays valid until the next frame's stage_codes, which
+    // runs after this frame's emission has completed
+    JXG_HIP(hipMemcpyAsync(c->ans_tab.p, c->h_ans_tab.p, kAnsTabBytes, hipMemcpyHostToDevice, s));
   }
   JXG_HIP(hipMemcpyAsync(c->codes_ac.p, packed.data(), packed.size() * 4, hipMemcpyHostToDevice, s));
   JXG_HIP(hipMemcpyAsync(c->lfcodes.p, lfpacked.data(), lfpacked.size() * 4, hipMemcpyHostToDevice, s));
@@ -965,9 +995,8 @@ static jxg_status stage_emit(Ctx* c, Job& J) {
     na.len = c->tlen.p;
     na.tbase = c->tbase.p;
     na.ntok = c->ntok.p;
-    na.freq = c->ans_freq.p;
-    na.cum = c->ans_cum.p;
-    na.inv = c->ans_inv.p;
+    na.tab = c->ans_tab.p;
+    na.nhist = J.nhist_ans;
     na.state = c->ans_state.p;
     na.base = c->gbase.p;
     na.scratch = c->scratch.p;

@@ -95,15 +95,24 @@ struct AcArgs {
 };
 
 // ANS coding of the pass groups' token records (jxg_ac.hip)
+constexpr uint32_t kAnsHists = 16;  // == kAnsMaxHists (jxg_bitstream.h)
+constexpr uint32_t kAnsDivOff = kAnsHists * 128 * 4;
+constexpr uint32_t kAnsInvOff = kAnsDivOff + kAnsHists * 128 * 4;
+constexpr uint32_t kAnsMapOff = kAnsInvOff + kAnsHists * 4096 * 2;
+constexpr uint32_t kAnsTabBytes = kAnsMapOff + 136;
 struct AnsArgs {
   const uint32_t* tokens;  // token records of ac_tokens_kernel
   uint32_t* val;           // [tokens] emitted bits: 16-bit chunk (if any) then raw bits
   uint8_t* len;            // [tokens] number of emitted bits
   const uint64_t* tbase;   // [ngroups]
   const uint32_t* ntok;    // [ngroups][3]
-  const uint16_t* freq;    // [132][128] normalized frequencies (sum 4096)
-  const uint16_t* cum;     // [132][128]
-  const uint16_t* inv;     // [132][4096] alias-table position of (symbol, offset)
+  const uint8_t* tab;      // table blob (kAnsDivOff / kAnsInvOff / kAnsMapOff):
+                           //  u32 [16][128] symbol: f - 1 | cum << 12
+                           //  u32 [16][128] division magic of f (floor(x / f) =
+                           //      (t + ((x - t) >> s1)) >> s2, t = mulhi(x, magic))
+                           //  u16 [16][4096] alias inverse: slot of position cum + offset
+                           //  u8 [132] static cluster -> histogram
+  uint32_t nhist;          // histograms in use (<= kAnsMaxHists)
   uint32_t* state;         // [ngroups] final encoder state (= stream's first 32 bits)
   const uint64_t* base;    // [ngroups] scratch bit offset
   uint32_t* scratch;

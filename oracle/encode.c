@@ -501,27 +501,42 @@ int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h, size_t row_strid
       hist[jxo_ac_cluster(gt[g][i].ctx)][tok]++;
     }
   }
-  /* dense cluster ids in order of first appearance over contexts */
+  /* prefix codes: one histogram per static cluster.  ANS: the static
+   * clusters are clustered again into <= JXO_ANS_MAX_HISTS centres
+   * (jxo_ans_cluster).  Dense ids in order of first appearance over contexts. */
+  int group[JXO_MAX_CLUSTERS]; /* static cluster -> histogram group (-1: empty) */
+  int ngrp = 0;
+  if (p->coder == 1) {
+    ngrp = jxo_ans_cluster((const uint32_t(*)[JXO_ALPHA])hist, JXO_MAX_CLUSTERS, group);
+  } else {
+    for (int cl = 0; cl < JXO_MAX_CLUSTERS; cl++) {
+      uint64_t tot = 0;
+      for (int s = 0; s < JXO_ALPHA; s++) tot += hist[cl][s];
+      group[cl] = tot ? ngrp++ : -1;
+    }
+  }
   int dense[JXO_MAX_CLUSTERS];
   for (int i = 0; i < JXO_MAX_CLUSTERS; i++) dense[i] = -1;
   int nhist = 0;
   uint8_t* ctxmap = (uint8_t*)malloc(JXO_AC_CTX);
   for (int ctx = 0; ctx < JXO_AC_CTX; ctx++) {
-    int cl = jxo_ac_cluster(ctx);
-    uint64_t tot = 0;
-    for (int s = 0; s < JXO_ALPHA; s++) tot += hist[cl][s];
-    if (tot && dense[cl] < 0) dense[cl] = nhist++;
-    ctxmap[ctx] = (uint8_t)(dense[cl] < 0 ? 0 : dense[cl]);
+    const int gr = group[jxo_ac_cluster(ctx)];
+    if (gr >= 0 && dense[gr] < 0) dense[gr] = nhist++;
+    ctxmap[ctx] = (uint8_t)(gr < 0 ? 0 : dense[gr]);
   }
+  static uint32_t dhist[JXO_MAX_CLUSTERS][JXO_ALPHA];
+  memset(dhist, 0, sizeof(dhist));
+  for (int cl = 0; cl < JXO_MAX_CLUSTERS; cl++)
+    if (group[cl] >= 0 && dense[group[cl]] >= 0)
+      for (int s = 0; s < JXO_ALPHA; s++) dhist[dense[group[cl]]][s] += hist[cl][s];
   jxo_prefix* codes = (jxo_prefix*)malloc(sizeof(jxo_prefix) * (nhist ? nhist : 1));
   jxo_ans* ans = p->coder == 1 ? (jxo_ans*)malloc(sizeof(jxo_ans) * (nhist ? nhist : 1)) : NULL;
-  for (int cl = 0; cl < JXO_MAX_CLUSTERS; cl++)
-    if (dense[cl] >= 0) {
-      if (ans)
-        jxo_ans_normalize(hist[cl], &ans[dense[cl]]);
-      else
-        jxo_build_prefix(hist[cl], JXO_ALPHA, &codes[dense[cl]]);
-    }
+  for (int h = 0; h < nhist; h++) {
+    if (ans)
+      jxo_ans_normalize(dhist[h], &ans[h]);
+    else
+      jxo_build_prefix(dhist[h], JXO_ALPHA, &codes[h]);
+  }
 
   /* ---- sections ---- */
   const int nsec = (f.ngroups == 1) ? 1 : (int)(2 + f.nlf + f.ngroups);

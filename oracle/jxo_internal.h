@@ -130,6 +130,14 @@ typedef struct {
 } jxo_ans;
 void jxo_ans_normalize(const uint32_t* counts /* [128] */, jxo_ans* a);
 void jxo_ans_write_hist(jxo_bw* w, const jxo_ans* a);
+/* at most 16 clustered histograms (their alias inverses fill 128 KB of LDS on
+ * the GPU); a new centre needs >= 64 bits of merge cost (Q16) */
+#ifndef JXO_ANS_MAX_HISTS
+#define JXO_ANS_MAX_HISTS 16
+#endif
+#define JXO_ANS_MIN_DIST (64ll << 16)
+/* hist[nh][128] -> assign[nh] (centre id, -1 for empty); returns #centres */
+int jxo_ans_cluster(const uint32_t (*hist)[JXO_ALPHA], int nh, int* assign);
 void jxo_ans_write_stream(jxo_bw* w, const jxo_ans* hists, size_t n, const uint8_t* hist,
                           const uint8_t* sym, const uint8_t* nbits, const uint32_t* bits);
 
