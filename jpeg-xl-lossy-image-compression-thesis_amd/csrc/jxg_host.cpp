@@ -353,8 +353,9 @@ static MergeTables build_merge_tables() {
       }
     }
   }
-  // per-shape pixel-orientation copies ([ky * C + kx]; tall shapes read the
-  // stored table transposed) -- lanes of a column pass read consecutive kx
+  // per-shape pixel-orientation copies, column-major ([kx * R + ky]; tall
+  // shapes read the stored table transposed) -- a quantization lane owns a
+  // column chunk of consecutive ky: 16-byte loads
   {
     static const int kShapeDims[kNumShapes][3] = {{2, 1, 0}, {1, 2, 0}, {2, 2, 1}, {4, 2, 2}, {2, 4, 2},
                                                  {4, 4, 3}, {8, 4, 4}, {4, 8, 4}, {8, 8, 5}};
@@ -367,7 +368,7 @@ static MergeTables build_merge_tables() {
       for (int ky = 0; ky < R; ky++)
         for (int kx = 0; kx < C; kx++) {
           const int si = cx >= cy ? ky * C + kx : kx * R + ky;
-          const int pi = kShapeOff[sh] + ky * C + kx;
+          const int pi = kShapeOff[sh] + kx * R + ky;
           for (int c = 0; c < 3; c++) swk[(size_t)c * stot + pi] = T.wk[(size_t)c * tot + kKindOff[k] + si];
           siwy[pi] = T.iwy[kKindOff[k] + si];
           snat[pi] = T.nat[kKindOff[k] + si];
@@ -410,7 +411,7 @@ struct Ctx {
   DevBuf<uint8_t> rgb, acs, qf;
   DevBuf<uint16_t> nz, mnat;
   DevBuf<float> ent, mwk, miwy, xyb_tiles, mcost;
-  DevBuf<uint32_t> vb, vcount;
+  DevBuf<uint32_t> vb, vcount, mwork;
   DevBuf<int32_t> dc;
   DevBuf<int16_t> ac;
   DevBuf<float> homog, xyb, r3;
@@ -594,6 +595,7 @@ static jxg_status stage_alloc(Ctx* c, Job& J) {
     JXG_HIP(c->ent.ensure(nb));
     JXG_HIP(c->xyb_tiles.ensure((size_t)ntiles * 3 * 4096));
     JXG_HIP(c->mcost.ensure((size_t)ntiles * kNumShapes * 32));
+    JXG_HIP(c->mwork.ensure(1 + (size_t)ntiles * kNumShapes));
   }
   if (!J.plan.tiles.empty()) {
     JXG_HIP(c->tile_list.ensure(J.plan.tiles.size()));
@@ -756,6 +758,8 @@ static jxg_status stage_front(Ctx* c, Job& J) {
     ma.wk = c->mwk.p;
     ma.iwy = c->miwy.p;
     ma.nat = c->mnat.p;
+    ma.work = c->mwork.p;
+    ma.nwrite = 256 * 3 * 4;  // CUs x resident workgroups x 4
     launch_merge(ma, s);
     JXG_HIP(hipGetLastError());
   }

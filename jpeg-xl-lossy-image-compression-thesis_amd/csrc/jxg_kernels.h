@@ -31,7 +31,7 @@ struct FrontArgs {
 };
 
 // merge stage (jxg_merge.hip): weight kinds (stored orientation) and the
-// nine merged shapes' pixel-orientation tables ([ky * C + kx])
+// nine merged shapes' pixel-orientation tables, column-major ([kx * R + ky])
 constexpr int kNumKinds = 6;
 constexpr int kKindOff[kNumKinds + 1] = {0, 128, 384, 896, 1920, 3968, 8064};
 constexpr int kNumShapes = 9;
@@ -56,6 +56,9 @@ struct MergeArgs {
   const float* wk;      // [3][kShapeOff[9]] weights per shape, pixel orientation
   const float* iwy;     // [kShapeOff[9]] 1 / Y weight
   const uint16_t* nat;  // [kShapeOff[9]] natural-order position
+  uint32_t* work;       // [1 + tiles * 9]: count, then (tile << 4 | shape) of every
+                        //   (tile, shape) holding a chosen varblock (resolve -> write)
+  uint32_t nwrite;      // merge_write workgroups (persistent loop over work)
 };
 // per-LF-group varblock lists (AC metadata channel)
 struct VbArgs {

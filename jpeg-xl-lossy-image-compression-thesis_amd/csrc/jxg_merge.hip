@@ -180,51 +180,62 @@ __device__ __forceinline__ Pass make_pass(const MergeArgs& a, int tile, int si) 
   return P;
 }
 
-// XYB tile -> LDS (only the valid varblocks' rows are used later)
-__device__ __forceinline__ void load_tile(const MergeArgs& a, const Pass& P, MergeLds& S) {
-  const float4* src = reinterpret_cast<const float4*>(a.xyb + (size_t)P.tile * (3 * 4096));
-  for (int i = threadIdx.x; i < 3 * 1024; i += kMThreads) {
-    const int c = i >> 10, ly = (i >> 4) & 63, lx = (i & 15) * 4;
-    const float4 v = src[i];
-    float* d = S.co + c * kMPlane + ly * kMS + lx;
-    d[0] = v.x;
-    d[1] = v.y;
-    d[2] = v.z;
-    d[3] = v.w;
+// rows: C-point DCT of every row of every valid varblock, read straight
+// from the tile-major XYB copy (16-byte loads; a thread issues all its rows'
+// loads before the first transform) into the LDS coefficient image.  For
+// C = 64 two lanes share a row (Lee halves), each reading the whole row.
+template <int C>
+__device__ __forceinline__ void load_row(const float* src, float* d) {
+#pragma unroll
+  for (int q = 0; q < C / 4; q++) {
+    const float4 u = reinterpret_cast<const float4*>(src)[q];
+    d[4 * q] = u.x;
+    d[4 * q + 1] = u.y;
+    d[4 * q + 2] = u.z;
+    d[4 * q + 3] = u.w;
   }
 }
-
-// rows: C-point DCT of every row of every valid varblock, in place.  For
-// C = 64 two lanes share a row; both read before either writes (barrier), and
-// the trip count is uniform so every thread reaches it.
 template <int C>
-__device__ void row_pass(const Pass& P, MergeLds& S) {
-  const int R = P.R(), nrows = 3 * P.NV() * R, lvr = P.lNV() + P.lR();
+__device__ void row_pass(const MergeArgs& a, const Pass& P, MergeLds& S) {
+  const float* tsrc = a.xyb + (size_t)P.tile * (3 * 4096);
+  const int R = P.R(), lvr = P.lNV() + P.lR();
   if constexpr (C == 64) {
-    const int n = 2 * nrows;  // nrows: multiple of 64
-    for (int i0 = 0; i0 < n; i0 += kMThreads) {
-      const int i = i0 + threadIdx.x;
+    const int n = 2 * 3 * P.NV() * R;  // <= 384
+    for (int i = threadIdx.x; i < n; i += kMThreads) {
       const int h = (i >> 6) & 1, r = ((i >> 7) << 6) | (i & 63);
-      const int c = min(r >> lvr, 2), v = (r >> P.lR()) & (P.NV() - 1), y = r & (R - 1);
-      const bool act = i < n && S.valid[v];
-      const int off = P.off(v, c) + y * kMS;
-      float o[32];
-      if (act) dct64_half(S.co + off, 1, h, o);
-      __syncthreads();
-      if (act) {
-#pragma unroll
-        for (int k = 0; k < 32; k++) S.co[off + 2 * k + h] = o[k];
-      }
-    }
-  } else {
-    for (int r = threadIdx.x; r < nrows; r += kMThreads) {
       const int c = r >> lvr, v = (r >> P.lR()) & (P.NV() - 1), y = r & (R - 1);
       if (!S.valid[v]) continue;
+      float row[64], o[32];
+      load_row<64>(tsrc + c * 4096 + (P.by0(v) * 8 + y) * 64, row);
+      dct64_half(row, 1, h, o);
       const int off = P.off(v, c) + y * kMS;
-      float o[C];
-      dct_from<C>(S.co + off, 1, o);
 #pragma unroll
-      for (int k = 0; k < C; k++) S.co[off + k] = o[k];
+      for (int k = 0; k < 32; k++) S.co[off + 2 * k + h] = o[k];
+    }
+  } else {
+    constexpr int PER = (3 * 4096 / C + kMThreads - 1) / kMThreads;  // 6, 3, 2
+    const int nrows = 3 * P.NV() * R;
+    float buf[PER][C];
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      const int r = threadIdx.x + k * kMThreads;
+      if (r < nrows) {
+        const int c = r >> lvr, v = (r >> P.lR()) & (P.NV() - 1), y = r & (R - 1);
+        load_row<C>(tsrc + c * 4096 + (P.by0(v) * 8 + y) * 64 + P.bx0(v) * 8, buf[k]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      const int r = threadIdx.x + k * kMThreads;
+      if (r >= nrows) continue;
+      const int c = r >> lvr, v = (r >> P.lR()) & (P.NV() - 1), y = r & (R - 1);
+      if (!S.valid[v]) continue;
+      float* x = buf[k];
+      lee<C>(x);
+      constexpr int l = ilog2c<C>();
+      const int off = P.off(v, c) + y * kMS;
+#pragma unroll
+      for (int q = 0; q < C; q++) S.co[off + q] = x[q] * kLeeS[l][q];
     }
   }
 }
@@ -264,7 +275,22 @@ __device__ void col_pass(const Pass& P, MergeLds& S) {
 
 // quantization, phase 0 = Y, phase 1 = X and B; lane = (channel, chunk of
 // RPC rows, varblock, column).  Chunk partial: fmaf(e, e) over its rows
-// ascending.  WRITE: coefficients to their natural-order slices, LLF to LDS.
+// ascending.  The lane's weights, inverse Y weights and natural positions
+// are RPC consecutive entries of the column-major tables (16-byte loads).
+// Rate bits and non-zeros are summed over the varblock's C lanes in-wave and
+// added to LDS by one lane.  WRITE: coefficients to their natural-order
+// slices, LLF to LDS.
+template <int N>
+__device__ __forceinline__ void load_f(const float* p, float* d) {
+#pragma unroll
+  for (int i = 0; i < N / 4; i++) {
+    const float4 v = reinterpret_cast<const float4*>(p)[i];
+    d[4 * i] = v.x;
+    d[4 * i + 1] = v.y;
+    d[4 * i + 2] = v.z;
+    d[4 * i + 3] = v.w;
+  }
+}
 template <int RPC, bool WRITE>
 __device__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S, int phase) {
   constexpr int STOT = kShapeOff[kNumShapes];
@@ -276,13 +302,26 @@ __device__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S, int p
     const int c = cidx == 0 ? 1 : (cidx == 1 ? 0 : 2);
     const int j = i & ((1 << lper) - 1);
     const int ch = j >> (P.lNV() + P.lC()), v = (j >> P.lC()) & (NV - 1), x = j & (C - 1);
-    if (!S.valid[v]) continue;
+    if (!S.valid[v]) continue;  // the varblock's C lanes leave together
     const int bx0 = P.bx0(v), by0 = P.by0(v);
     const float scale = (float)a.G * (float)S.vraw[v] / 65536.0f;
     const float inv_scale = 1.0f / scale;
     float* cplane = S.co + P.off(v, c) + x;
     const float* yd = S.co + P.off(v, 1) + x;
-    const float* wrow = a.wk + (size_t)c * STOT + P.soff + x;
+    const int tcol = P.soff + x * P.R() + ch * RPC;  // column chunk in the tables
+    float w[RPC], iw[RPC];
+    load_f<RPC>(a.wk + (size_t)c * STOT + tcol, w);
+    if (c == 1) load_f<RPC>(a.iwy + tcol, iw);
+    uint16_t nat[RPC];
+    if (WRITE) {
+#pragma unroll
+      for (int q = 0; q < RPC / 8; q++) {
+        const uint4 u = reinterpret_cast<const uint4*>(a.nat + tcol)[q];
+        const uint32_t uw[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int e = 0; e < 8; e++) nat[8 * q + e] = (uint16_t)(uw[e >> 1] >> ((e & 1) * 16));
+      }
+    }
     float cp = 0.0f;
     int bits = 0, nzc = 0;
 #pragma unroll
@@ -292,8 +331,7 @@ __device__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S, int p
       const float coef_v = cplane[ky * kMS];
       int qq = 0;
       if (!is_llf) {
-        const float w = wrow[ky * C];
-        const float ws = w * scale;
+        const float ws = w[kk] * scale;
         float rv = coef_v;
         if (c == 2) rv = rv - yd[ky * kMS];
         const float vq = rv * ws;
@@ -305,7 +343,7 @@ __device__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S, int p
           const float bq = qa < 256 ? S.btab[qa] : 0.145f / (float)qa;
           float adj = qa == 0 ? 0.0f : (qa == 1 ? kBias1 : (float)qa - bq);
           if (vq < 0.0f) adj = -adj;
-          cplane[ky * kMS] = adj * (a.iwy[P.soff + ky * C + x] * inv_scale);
+          cplane[ky * kMS] = adj * (iw[kk] * inv_scale);
         }
         const float e = av - (float)qa;
         cp = fmaf(e, e, cp);
@@ -315,7 +353,7 @@ __device__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S, int p
         llf_at(S, c, (by0 + ky) * 8 + bx0 + x) = coef_v;
       }
       if (WRITE) {
-        const int p = a.nat[P.soff + ky * C + x];
+        const int p = nat[kk];
         const int sl = p >> 6;
         const int lbx = bx0 + (sl & (P.cx() - 1)), lby = by0 + (sl >> P.lcx);
         const size_t gb = (size_t)(P.ty * 8 + lby) * a.bxs + P.tx * 8 + lbx;
@@ -323,11 +361,17 @@ __device__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S, int p
       }
     }
     // the chunk's column partials, tree-summed over the varblock's C lanes
-    // (an aligned group inside one wave)
-    for (int msk = 1; msk < C; msk <<= 1) cp += __shfl_xor(cp, msk, 64);
-    if (x == 0) S.qsum[cidx][ch][v] = cp;
-    if (bits) atomicAdd(&S.vbits[v], bits);
-    if (nzc) atomicAdd(&S.vnz[v][c], nzc);
+    // (an aligned group inside one wave); bits | non-zeros << 20 likewise
+    int packed = bits | nzc << 20;
+    for (int msk = 1; msk < C; msk <<= 1) {
+      cp += __shfl_xor(cp, msk, 64);
+      packed += __shfl_xor(packed, msk, 64);
+    }
+    if (x == 0) {
+      S.qsum[cidx][ch][v] = cp;
+      if (packed & 0xFFFFF) atomicAdd(&S.vbits[v], packed & 0xFFFFF);
+      if (packed >> 20) atomicAdd(&S.vnz[v][c], packed >> 20);
+    }
   }
 }
 
@@ -336,10 +380,10 @@ __device__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S, int p
 template <bool WRITE>
 __device__ void transform_quant(const MergeArgs& a, const Pass& P, MergeLds& S) {
   switch (P.lcx) {
-    case 0: row_pass<8>(P, S); break;
-    case 1: row_pass<16>(P, S); break;
-    case 2: row_pass<32>(P, S); break;
-    default: row_pass<64>(P, S); break;
+    case 0: row_pass<8>(a, P, S); break;
+    case 1: row_pass<16>(a, P, S); break;
+    case 2: row_pass<32>(a, P, S); break;
+    default: row_pass<64>(a, P, S); break;
   }
   __syncthreads();
   switch (P.lcy) {
@@ -430,7 +474,6 @@ __global__ __launch_bounds__(kMThreads) void merge_eval_kernel(MergeArgs a) {
   const int nbx = min(8, (int)a.bxs - P.tx * 8), nby = min(8, (int)a.bys - P.ty * 8);
   if ((1 << P.ls) > nbx || (1 << P.ls) > nby) return;  // no region of this level fits
   setup_varblocks<false>(a, P, S, nbx, nby);
-  load_tile(a, P, S);
   __syncthreads();
   vraw_pass(P, S);
   transform_quant<false>(a, P, S);
@@ -445,92 +488,118 @@ __global__ __launch_bounds__(kMThreads) void merge_eval_kernel(MergeArgs a) {
   }
 }
 
-// one wave per tile: levels in order, one lane per region
-__global__ __launch_bounds__(64) void merge_resolve_kernel(MergeArgs a) {
-  __shared__ float sEnt[64];
-  __shared__ uint8_t sAcs[64];
-  const int tile = a.tile_list ? (int)a.tile_list[blockIdx.x] : (int)blockIdx.x;
-  const int tx = tile % (int)a.tiles_x, ty = tile / (int)a.tiles_x;
-  const int nbx = min(8, (int)a.bxs - tx * 8), nby = min(8, (int)a.bys - ty * 8);
-  const int t = threadIdx.x, lbx = t & 7, lby = t >> 3;
-  const bool in = lbx < nbx && lby < nby;
-  const size_t gb = (size_t)(ty * 8 + lby) * a.bxs + tx * 8 + lbx;
-  sEnt[t] = in ? a.ent[gb] : 0.0f;
-  sAcs[t] = in ? a.acs[gb] : 0;
-  __syncthreads();
-  const float* cost = a.cost + (size_t)tile * kNumShapes * 32;
-  for (int s = 2; s <= a.max_s && s <= nbx && s <= nby; s *= 2) {
-    const int nr = 8 / s;
-    const int full = s == 2 ? 2 : (s == 4 ? 5 : 8);
-    const int tall = s == 2 ? 0 : (s == 4 ? 3 : 6);
-    if (t < nr * nr) {
-      const int rx = t % nr, ry = t / nr;
-      if ((rx + 1) * s <= nbx && (ry + 1) * s <= nby) {
-        float cur = 0.0f;
-        for (int iy = 0; iy < s; iy++)
-          for (int ix = 0; ix < s; ix++) cur += sEnt[(ry * s + iy) * 8 + rx * s + ix];
-        // varblock grid indices: full (8/s per row), tall (16/s), wide (8/s)
-        const int vf = ry * nr + rx, vl = ry * (16 / s) + 2 * rx, vt = (2 * ry) * nr + rx;
-        const float e0 = cost[full * 32 + vf];
-        const float el = cost[tall * 32 + vl], er = cost[tall * 32 + vl + 1];
-        const float etop = cost[(tall + 1) * 32 + vt], ebot = cost[(tall + 1) * 32 + vt + nr];
-        const float et = el + er, ew = etop + ebot;
-        float best = cur;
-        int choice = 0;
-        if (!(e0 >= best)) {
-          best = e0;
-          choice = 1;
-        }
-        if (!(et >= best)) {
-          best = et;
-          choice = 2;
-        }
-        if (!(ew >= best)) {
-          best = ew;
-          choice = 3;
-        }
-        for (int j = 0; choice && j < (choice == 1 ? 1 : 2); j++) {
-          int sh, bx, by;
-          float e;
-          if (choice == 1) {
-            sh = full, bx = rx * s, by = ry * s, e = e0;
-          } else if (choice == 2) {
-            sh = tall, bx = rx * s + j * (s / 2), by = ry * s, e = j ? er : el;
-          } else {
-            sh = tall + 1, bx = rx * s, by = ry * s + j * (s / 2), e = j ? ebot : etop;
+// one wave per tile (16 tiles per workgroup): levels in order, one lane per
+// region; then the tile's chosen shapes go to the merge_write work list (one
+// global atomic per workgroup)
+constexpr int kResolveWaves = 16;
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+__global__ __launch_bounds__(64 * kResolveWaves) void merge_resolve_kernel(MergeArgs a) {
+  __shared__ float sEntW[kResolveWaves][64];
+  __shared__ uint8_t sAcsW[kResolveWaves][64];
+  __shared__ uint32_t sCnt[kResolveWaves];
+  __shared__ uint32_t sBase;
+  const int wv = threadIdx.x >> 6, t = threadIdx.x & 63;
+  float* sEnt = sEntW[wv];
+  uint8_t* sAcs = sAcsW[wv];
+  const int idx = blockIdx.x * kResolveWaves + wv;
+  uint32_t has = 0;
+  int tile = 0;
+  if (idx < (int)a.ntiles) {
+    tile = a.tile_list ? (int)a.tile_list[idx] : idx;
+    const int tx = tile % (int)a.tiles_x, ty = tile / (int)a.tiles_x;
+    const int nbx = min(8, (int)a.bxs - tx * 8), nby = min(8, (int)a.bys - ty * 8);
+    const int lbx = t & 7, lby = t >> 3;
+    const bool in = lbx < nbx && lby < nby;
+    const size_t gb = (size_t)(ty * 8 + lby) * a.bxs + tx * 8 + lbx;
+    sEnt[t] = in ? a.ent[gb] : 0.0f;
+    sAcs[t] = in ? a.acs[gb] : 0;
+    wave_sync_lds();
+    const float* cost = a.cost + (size_t)tile * kNumShapes * 32;
+    for (int s = 2; s <= a.max_s && s <= nbx && s <= nby; s *= 2) {
+      const int nr = 8 / s;
+      const int full = s == 2 ? 2 : (s == 4 ? 5 : 8);
+      const int tall = s == 2 ? 0 : (s == 4 ? 3 : 6);
+      if (t < nr * nr) {
+        const int rx = t % nr, ry = t / nr;
+        if ((rx + 1) * s <= nbx && (ry + 1) * s <= nby) {
+          float cur = 0.0f;
+          for (int iy = 0; iy < s; iy++)
+            for (int ix = 0; ix < s; ix++) cur += sEnt[(ry * s + iy) * 8 + rx * s + ix];
+          // varblock grid indices: full (8/s per row), tall (16/s), wide (8/s)
+          const int vf = ry * nr + rx, vl = ry * (16 / s) + 2 * rx, vt = (2 * ry) * nr + rx;
+          const float e0 = cost[full * 32 + vf];
+          const float el = cost[tall * 32 + vl], er = cost[tall * 32 + vl + 1];
+          const float etop = cost[(tall + 1) * 32 + vt], ebot = cost[(tall + 1) * 32 + vt + nr];
+          const float et = el + er, ew = etop + ebot;
+          float best = cur;
+          int choice = 0;
+          if (!(e0 >= best)) {
+            best = e0;
+            choice = 1;
           }
-          const int cy = 1 << kShapes[sh].lcy, cx = 1 << kShapes[sh].lcx;
-          for (int iy = 0; iy < cy; iy++)
-            for (int ix = 0; ix < cx; ix++) {
-              const int b = (by + iy) * 8 + bx + ix;
-              sAcs[b] = (uint8_t)(kShapes[sh].type | ((iy | ix) ? 0x80 : 0));
-              sEnt[b] = (iy | ix) ? 0.0f : e;
+          if (!(et >= best)) {
+            best = et;
+            choice = 2;
+          }
+          if (!(ew >= best)) {
+            best = ew;
+            choice = 3;
+          }
+          for (int j = 0; choice && j < (choice == 1 ? 1 : 2); j++) {
+            int sh, bx, by;
+            float e;
+            if (choice == 1) {
+              sh = full, bx = rx * s, by = ry * s, e = e0;
+            } else if (choice == 2) {
+              sh = tall, bx = rx * s + j * (s / 2), by = ry * s, e = j ? er : el;
+            } else {
+              sh = tall + 1, bx = rx * s, by = ry * s + j * (s / 2), e = j ? ebot : etop;
             }
+            const int cy = 1 << kShapes[sh].lcy, cx = 1 << kShapes[sh].lcx;
+            for (int iy = 0; iy < cy; iy++)
+              for (int ix = 0; ix < cx; ix++) {
+                const int b = (by + iy) * 8 + bx + ix;
+                sAcs[b] = (uint8_t)(kShapes[sh].type | ((iy | ix) ? 0x80 : 0));
+                sEnt[b] = (iy | ix) ? 0.0f : e;
+              }
+          }
         }
       }
+      wave_sync_lds();
     }
-    __syncthreads();
+    if (in) a.acs[gb] = sAcs[t];
+    // the shapes chosen somewhere in this tile
+    if (in && !(sAcs[t] & 0x80)) {
+#pragma unroll
+      for (int si = 0; si < kNumShapes; si++) has |= sAcs[t] == kShapes[si].type ? 1u << si : 0u;
+    }
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) has |= __shfl_xor(has, m, 64);
   }
-  if (in) a.acs[gb] = sAcs[t];
+  if (t == 0) sCnt[wv] = (uint32_t)__popc(has);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t tot = 0;
+    for (int w = 0; w < kResolveWaves; w++) tot += sCnt[w];
+    sBase = tot ? atomicAdd(a.work, tot) : 0u;
+  }
+  __syncthreads();
+  uint32_t base = sBase;
+  for (int w = 0; w < wv; w++) base += sCnt[w];
+  if (t < kNumShapes && ((has >> t) & 1u))
+    a.work[1 + base + __popc(has & ((1u << t) - 1u))] = (uint32_t)tile << 4 | (uint32_t)t;
 }
 
-__global__ __launch_bounds__(kMThreads) void merge_write_kernel(MergeArgs a) {
-  __shared__ __attribute__((aligned(16))) MergeLds S;
-  int tile, si;
-  if (!decode_wg(a, tile, si)) return;
+// one (tile, shape) entry of the work list; returns after its last LDS use
+__device__ __forceinline__ void write_entry(const MergeArgs& a, int tile, int si, MergeLds& S) {
   const Pass P = make_pass(a, tile, si);
-  if (P.ls > max_level(a)) return;
   const int nbx = min(8, (int)a.bxs - P.tx * 8), nby = min(8, (int)a.bys - P.ty * 8);
-  if ((1 << P.ls) > nbx || (1 << P.ls) > nby) return;
-  if (threadIdx.x == 0) S.any = 0;
-  __syncthreads();
   setup_varblocks<true>(a, P, S, nbx, nby);
-  if (threadIdx.x < 32 && S.valid[threadIdx.x]) S.any = 1;
   __syncthreads();
-  if (!S.any) return;  // uniform: no varblock of this shape was chosen here
   vraw_pass(P, S);
-  load_tile(a, P, S);
-  __syncthreads();
   transform_quant<true>(a, P, S);
   // per covered block: non-zero counts, quant field, LLF-derived DC
   const int cb = P.cy() * P.cx(), lcb = P.lcy + P.lcx;
@@ -566,6 +635,18 @@ __global__ __launch_bounds__(kMThreads) void merge_write_kernel(MergeArgs a) {
     a.dc[nb + gb] = q[1];
     a.dc[2 * nb + gb] = q[2];
     a.qf[gb] = (uint8_t)(S.vraw[v] - 1);
+  }
+}
+
+// persistent workgroups over the (tile, shape) entries the resolve kernel
+// listed: only (tile, shape) pairs holding a chosen varblock cost anything
+__global__ __launch_bounds__(kMThreads) void merge_write_kernel(MergeArgs a) {
+  __shared__ __attribute__((aligned(16))) MergeLds S;
+  const uint32_t n = __builtin_amdgcn_readfirstlane(*(volatile uint32_t*)a.work);
+  for (uint32_t w = blockIdx.x; w < n; w += gridDim.x) {
+    const uint32_t e = a.work[1 + w];
+    write_entry(a, (int)(e >> 4), (int)(e & 15u), S);
+    __syncthreads();  // LDS reuse by the next entry
   }
 }
 
@@ -620,8 +701,11 @@ void launch_merge(const MergeArgs& a, hipStream_t s) {
   if (!a.ntiles) return;
   const uint32_t nwg = ((a.ntiles + 7) / 8) * 8 * kNumShapes;
   hipLaunchKernelGGL(merge_eval_kernel, dim3(nwg), dim3(kMThreads), 0, s, a);
-  hipLaunchKernelGGL(merge_resolve_kernel, dim3(a.ntiles), dim3(64), 0, s, a);
-  hipLaunchKernelGGL(merge_write_kernel, dim3(nwg), dim3(kMThreads), 0, s, a);
+  (void)hipMemsetAsync(a.work, 0, sizeof(uint32_t), s);
+  hipLaunchKernelGGL(merge_resolve_kernel, dim3((a.ntiles + kResolveWaves - 1) / kResolveWaves),
+                     dim3(64 * kResolveWaves), 0, s, a);
+  const uint32_t nw = min(a.nwrite, a.ntiles * (uint32_t)kNumShapes);
+  hipLaunchKernelGGL(merge_write_kernel, dim3(nw), dim3(kMThreads), 0, s, a);
 }
 void launch_vb_list(const VbArgs& a, uint32_t nlf, hipStream_t s) {
   hipLaunchKernelGGL(vb_list_kernel, dim3(nlf), dim3(1024), 0, s, a);

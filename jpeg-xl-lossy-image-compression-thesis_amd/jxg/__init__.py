@@ -25,7 +25,7 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libjxg.so")
+LIB_PATH = os.environ.get("JXG_LIB_PATH") or os.path.join(HERE, "libjxg.so")  # override: experiments only
 CLI_PATH = os.path.join(HERE, "jxg_cjxl")
 
 PROPOSAL_P = 1
