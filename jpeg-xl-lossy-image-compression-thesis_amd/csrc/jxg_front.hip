@@ -306,30 +306,48 @@ struct QVals {
   uint32_t nz;  // non-zero AC counts of the block: X | Y << 8 | B << 16
 };
 
-// One channel C (0 X, 1 Y, 2 B) of one block under strategy T, lane r =
-// working-array column r: transform, quantize 8 coefficients, accumulate
-// e*e (fmaf), rate bits and the non-zero count; Y records its dequantized
-// values (yd) for the B residual.  Float op order == oracle jxo_quantize_block.
-template <int T, int C>
-__device__ __forceinline__ void quantize_channel(const GroupCtx& G, float scale, float inv_scale,
-                                                 float* yd, int& bits, float& part,
-                                                 uint32_t* pk, int& nzc) {
-  constexpr int ti = tindex<T>();
-  constexpr float kBias1 = 1.0f - 0.07005449891748593f;
+// Row pass of one channel (lane r = pixel row r of the block): 8-point or
+// two 4-point DCTs, then the 8x8 transpose, so lane r holds working-array
+// column r.  Shared by the two candidates with the same row transform
+// (DCT8 / DCT8X4: 8-point rows; DCT4X4 / DCT4X8: 4-point rows).
+template <bool ROW8, int C>
+__device__ __forceinline__ void row_pass_t(const GroupCtx& G, float* v) {
   const float* plane = G.pix + C * kPlane;
   const int base = lds_at(G.lx0, G.ly0 + G.r);  // 8 contiguous dwords (same skew)
-  float v[8];
 #pragma unroll
   for (int x = 0; x < 8; x++) v[x] = plane[base + x];
-  // row pass
-  if (T == kDCT8 || T == kDCT8X4) {
+  if (ROW8) {
     dct8_1d(v);
   } else {
     dct4_1d(v);
     dct4_1d(v + 4);
   }
   transpose8(v, G.r);
-  // column pass
+}
+
+// Candidate state accumulated over the channels Y, X, B (lane r = working
+// column r): Y dequantized values for the B residual, rate bits, e*e
+// partial, packed quantized values.
+struct CandAcc {
+  float yd[8];
+  int bits;
+  float part;
+  QVals q;
+};
+
+// Column pass of one channel C (0 X, 1 Y, 2 B) of one block under strategy T
+// from the row-transformed, transposed values vt: transform, quantize the 8
+// coefficients, accumulate e*e (fmaf), rate bits and the non-zero count; Y
+// records its dequantized values for the B residual.  Float op order ==
+// oracle jxo_quantize_block.
+template <int T, int C>
+__device__ __forceinline__ void quantize_cols(const GroupCtx& G, const float* vt, float scale,
+                                              float inv_scale, CandAcc& A) {
+  constexpr int ti = tindex<T>();
+  constexpr float kBias1 = 1.0f - 0.07005449891748593f;
+  float v[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) v[k] = vt[k];
   if (T == kDCT8 || T == kDCT4X8) {
     dct8_1d(v);
   } else {
@@ -338,25 +356,25 @@ __device__ __forceinline__ void quantize_channel(const GroupCtx& G, float scale,
   }
   // lowest-frequency combine (enc_transforms [ext]); slots per oracle
   if (T == kDCT4X4) {
-    const float A = group_lane<0>(v[0]), Cc = group_lane<0>(v[4]);
-    const float B = group_lane<4>(v[0]), D = group_lane<4>(v[4]);
+    const float A0 = group_lane<0>(v[0]), Cc = group_lane<0>(v[4]);
+    const float B0 = group_lane<4>(v[0]), D = group_lane<4>(v[4]);
     if (G.r == 0) {
-      v[0] = (((A + B) + Cc) + D) * 0.25f;
-      v[4] = (((A - B) + Cc) - D) * 0.25f;
+      v[0] = (((A0 + B0) + Cc) + D) * 0.25f;
+      v[4] = (((A0 - B0) + Cc) - D) * 0.25f;
     } else if (G.r == 4) {
-      v[0] = (((A + B) - Cc) - D) * 0.25f;
-      v[4] = (((A - B) - Cc) + D) * 0.25f;
+      v[0] = (((A0 + B0) - Cc) - D) * 0.25f;
+      v[4] = (((A0 - B0) - Cc) + D) * 0.25f;
     }
   } else if (T == kDCT8X4) {
     if (G.r == 0) {
-      const float A = v[0], B = v[4];
-      v[0] = (A + B) * 0.5f;
-      v[4] = (A - B) * 0.5f;
+      const float A0 = v[0], B0 = v[4];
+      v[0] = (A0 + B0) * 0.5f;
+      v[4] = (A0 - B0) * 0.5f;
     }
   } else if (T == kDCT4X8) {
-    const float A = group_lane<0>(v[0]), B = group_lane<4>(v[0]);
-    if (G.r == 0) v[0] = (A + B) * 0.5f;
-    if (G.r == 4) v[0] = (A - B) * 0.5f;
+    const float A0 = group_lane<0>(v[0]), B0 = group_lane<4>(v[0]);
+    if (G.r == 0) v[0] = (A0 + B0) * 0.5f;
+    if (G.r == 4) v[0] = (A0 - B0) * 0.5f;
   }
   if (G.r == 0) v[0] = 0.0f;  // DC slot: quantizes to 0, contributes nothing
   const float4* wp = reinterpret_cast<const float4*>(G.wperm + ((ti * 3 + C) * 8 + G.r) * 8);
@@ -369,14 +387,13 @@ __device__ __forceinline__ void quantize_channel(const GroupCtx& G, float scale,
     iwk[0] = i0.x; iwk[1] = i0.y; iwk[2] = i0.z; iwk[3] = i0.w;
     iwk[4] = i1.x; iwk[5] = i1.y; iwk[6] = i1.z; iwk[7] = i1.w;
   }
-  int nz = 0;
-#pragma unroll
-  for (int i = 0; i < 4; i++) pk[i] = 0u;
+  int nz = 0, clzs = 0;
+  int qs[8];
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     const float ws = wk[k] * scale;
     float rv = v[k];
-    if (C == 2) rv = rv - yd[k];
+    if (C == 2) rv = rv - A.yd[k];
     const float vq = rv * ws;
     const float a = fabsf(vq);
     const int qa = a < 0.58f ? 0 : (int)(fminf(a, 32767.0f) + 0.5f);
@@ -387,59 +404,79 @@ __device__ __forceinline__ void quantize_channel(const GroupCtx& G, float scale,
       }
       float adj = qa == 0 ? 0.0f : (qa == 1 ? kBias1 : (float)qa - bq);
       if (vq < 0.0f) adj = -adj;
-      yd[k] = adj * (iwk[k] * inv_scale);
+      A.yd[k] = adj * (iwk[k] * inv_scale);
     }
     const float e = a - (float)qa;
-    part = fmaf(e, e, part);
-    bits += qa ? 2 + 2 * bitlen((uint32_t)qa) : 0;
+    A.part = fmaf(e, e, A.part);
+    // 2 + 2 bitlen(qa) per non-zero: bitlen(qa) = 31 - clz(2 qa + 1)
+    clzs += (int)__clz((uint32_t)(2 * qa + 1));
     nz += qa != 0;
-    const int qs = vq < 0.0f ? -qa : qa;
-    pk[k >> 1] |= ((uint32_t)qs & 0xFFFFu) << ((k & 1) * 16);
+    qs[k] = vq < 0.0f ? -qa : qa;
   }
-  nzc = group_int_sum(nz);
-  bits += G.r == 0 ? bitlen((uint32_t)nzc) : 0;
+  // sum over k of [qa != 0] (2 + 2 bitlen) = 2 nz + 2 (8 * 31 - clzs)
+  A.bits += 2 * nz + 2 * (8 * 31 - clzs);
+  uint32_t pk[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+    pk[i] = ((uint32_t)qs[2 * i] & 0xFFFFu) | ((uint32_t)qs[2 * i + 1] << 16);
+  const int nzc = group_int_sum(nz);
+  A.bits += G.r == 0 ? bitlen((uint32_t)nzc) : 0;
+  constexpr int slot = C == 1 ? 4 : (C == 0 ? 0 : 8);
+#pragma unroll
+  for (int i = 0; i < 4; i++) A.q.w[slot + i] = pk[i];
+  const uint32_t sh = C == 1 ? 8 : (C == 0 ? 0 : 16);
+  A.q.nz = (C == 1 ? 0u : A.q.nz) | ((uint32_t)nzc << sh);
 }
 
-// One 8-lane group quantizes one block under strategy T (channels Y, X, B)
-// and returns the rate/distortion cost (same in all 8 lanes); the quantized
-// values stay in registers (q).
-template <int T>
-__device__ __forceinline__ float quantize_group(const GroupCtx& G, float scale, float inv_scale,
-                                                QVals& q) {
-  float yd[8];
-  int bits = 0;
-  float part = 0.0f;
-#pragma unroll 1  // one channel live at a time (keeps 4 waves/SIMD)
+// The two candidates sharing a row transform, channels Y, X, B; need0/need1
+// are group-uniform.  Returns the rate/distortion costs (same in all 8 lanes
+// of the group) in e0/e1; quantized values stay in registers.
+template <bool ROW8>
+__device__ __forceinline__ void eval_pair(const GroupCtx& G, float scale, float inv_scale,
+                                          bool need0, bool need1, CandAcc& A0, CandAcc& A1,
+                                          float& e0, float& e1) {
+  constexpr int T0 = ROW8 ? kDCT8 : kDCT4X4;
+  constexpr int T1 = ROW8 ? kDCT8X4 : kDCT4X8;
+  A0.bits = A1.bits = 0;
+  A0.part = A1.part = 0.0f;
+#pragma unroll 1  // one channel live at a time
   for (int ci = 0; ci < 3; ci++) {
-    uint32_t pk[4];
-    int nzc;
+    float vt[8];
     if (ci == 0) {
-      quantize_channel<T, 1>(G, scale, inv_scale, yd, bits, part, pk, nzc);
-      q.nz = (uint32_t)nzc << 8;
-#pragma unroll
-      for (int i = 0; i < 4; i++) q.w[4 + i] = pk[i];
+      row_pass_t<ROW8, 1>(G, vt);
+      if (need0) quantize_cols<T0, 1>(G, vt, scale, inv_scale, A0);
+      if (need1) quantize_cols<T1, 1>(G, vt, scale, inv_scale, A1);
     } else if (ci == 1) {
-      quantize_channel<T, 0>(G, scale, inv_scale, yd, bits, part, pk, nzc);
-      q.nz |= (uint32_t)nzc;
-#pragma unroll
-      for (int i = 0; i < 4; i++) q.w[i] = pk[i];
+      row_pass_t<ROW8, 0>(G, vt);
+      if (need0) quantize_cols<T0, 0>(G, vt, scale, inv_scale, A0);
+      if (need1) quantize_cols<T1, 0>(G, vt, scale, inv_scale, A1);
     } else {
-      quantize_channel<T, 2>(G, scale, inv_scale, yd, bits, part, pk, nzc);
-      q.nz |= (uint32_t)nzc << 16;
-#pragma unroll
-      for (int i = 0; i < 4; i++) q.w[8 + i] = pk[i];
+      row_pass_t<ROW8, 2>(G, vt);
+      if (need0) quantize_cols<T0, 2>(G, vt, scale, inv_scale, A0);
+      if (need1) quantize_cols<T1, 2>(G, vt, scale, inv_scale, A1);
     }
   }
-  bits = group_int_sum(bits);
-  const float dist = group_tree_sum(part);
-  const float tmul = T == kDCT8 ? 1.0f : (T == kDCT4X4 ? 1.05f : 1.02f);
-  return ((float)bits + 8.0f * dist) * tmul;
+  constexpr float tm0 = T0 == kDCT8 ? 1.0f : 1.05f;
+  constexpr float tm1 = 1.02f;
+  e0 = ((float)group_int_sum(A0.bits) + 8.0f * group_tree_sum(A0.part)) * tm0;
+  e1 = ((float)group_int_sum(A1.bits) + 8.0f * group_tree_sum(A1.part)) * tm1;
 }
 
 __device__ __forceinline__ void copy_q(QVals& d, const QVals& s, bool take) {
 #pragma unroll
   for (int i = 0; i < 12; i++) d.w[i] = take ? s.w[i] : d.w[i];
   d.nz = take ? s.nz : d.nz;
+}
+
+// FindBest8x8Transform's scan (`e < best`, candidates in the order DCT8,
+// DCT4X4, DCT4X8, DCT8X4, best starting at FLT_MAX) as a tournament: a
+// candidate beats another when its estimate is below FLT_MAX and smaller, or
+// equal with a lower scan index; NaN never wins.
+__device__ __forceinline__ bool beats(float ea, int ia, float eb, int ib) {
+  const bool va = ea < FLT_MAX, vb = eb < FLT_MAX;
+  if (va && vb) return ea < eb || (ea == eb && ia < ib);
+  if (va != vb) return va;
+  return ia < ib;
 }
 
 // RGB8 -> XYB for the 66 x 66 tile (+1 px halo).  All byte loads of a
@@ -603,32 +640,53 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     rd = sR[b][2];
   }
   if (a.proposals & 1u) pt = partition_of(rh, rv, rd, a.distance);
-  QVals best, ptq, cur;
-  int bt = kDCT8;
+  // scan indices: DCT8 0, DCT4X4 1, DCT4X8 2, DCT8X4 3
+  QVals best, ptq;
+  int bt = kDCT8, bi = 0;
   float beste = FLT_MAX;
-#pragma unroll 1
-  for (int i = 0; i < 4; i++) {
-    const int T = i == 0 ? kDCT8 : (i == 1 ? kDCT4X4 : (i == 2 ? kDCT4X8 : kDCT8X4));
-    const bool scored = i < ncand;
-    const bool is_pt = pt != kDCT8 && T == pt;
-    if (!scored && !is_pt) continue;  // group-uniform
-    float e;
-    switch (i) {
-      case 0: e = quantize_group<kDCT8>(G, scale, inv_scale, cur); break;
-      case 1: e = quantize_group<kDCT4X4>(G, scale, inv_scale, cur); break;
-      case 2: e = quantize_group<kDCT4X8>(G, scale, inv_scale, cur); break;
-      default: e = quantize_group<kDCT8X4>(G, scale, inv_scale, cur); break;
+  {
+    CandAcc A0, A1;
+    float e0, e1;
+    eval_pair<true>(G, scale, inv_scale, true, ncand > 1 || pt == kDCT8X4, A0, A1, e0, e1);
+    if (hookF) {
+      e0 = hook_f(e0, rh, rv, rd);
+      e1 = hook_f(e1, rh, rv, rd);
     }
-    if (hookF) e = hook_f(e, rh, rv, rd);
-    const bool improve = scored && ncand > 1 && e < beste;
-    if (improve) {
-      beste = e;
-      bt = T;
+    copy_q(best, A0.q, true);
+    if (ncand > 1) {
+      beste = e0 < FLT_MAX ? e0 : FLT_MAX;
+      if (beats(e1, 3, e0, 0)) {
+        copy_q(best, A1.q, true);
+        bt = kDCT8X4;
+        bi = 3;
+        beste = e1;
+      }
     }
-    // DCT8 is copied first: it stays the default when no estimate beats
-    // FLT_MAX (NaN costs) or when only DCT8 is searched
-    copy_q(best, cur, i == 0 || improve);
-    copy_q(ptq, cur, is_pt);
+    copy_q(ptq, A1.q, pt == kDCT8X4);
+  }
+  const bool need44 = ncand > 1 || pt == kDCT4X4, need48 = ncand > 1 || pt == kDCT4X8;
+  if (need44 || need48) {
+    CandAcc A0, A1;
+    float e0, e1;
+    eval_pair<false>(G, scale, inv_scale, need44, need48, A0, A1, e0, e1);
+    if (ncand > 1) {
+      if (hookF) {
+        e0 = hook_f(e0, rh, rv, rd);
+        e1 = hook_f(e1, rh, rv, rd);
+      }
+      // winner of the pair, then against the first pair's
+      const bool w1 = beats(e1, 2, e0, 1);
+      const float ew = w1 ? e1 : e0;
+      const int iw = w1 ? 2 : 1;
+      if (beats(ew, iw, beste, bi)) {
+        copy_q(best, w1 ? A1.q : A0.q, true);
+        bt = w1 ? kDCT4X8 : kDCT4X4;
+        bi = iw;
+        beste = ew;
+      }
+    }
+    copy_q(ptq, A0.q, pt == kDCT4X4);
+    copy_q(ptq, A1.q, pt == kDCT4X8);
   }
   if (bt == kDCT8 && pt != kDCT8) {
     bt = pt;
