@@ -479,37 +479,68 @@ __device__ __forceinline__ bool beats(float ea, int ia, float eb, int ib) {
   return ia < ib;
 }
 
-// RGB8 -> XYB for the 66 x 66 tile (+1 px halo).  All byte loads of a
-// thread are issued before any use (one memory latency per tile instead of
-// one per pixel), then converted.
-constexpr int kTilePx = kRows * 66;
-constexpr int kLoadIters = (kTilePx + kThreads - 1) / kThreads;
+// RGB8 -> XYB for the 66 x 66 tile (+1 px halo).  The tile's rows are read
+// as 4-pixel chunks (12 bytes = 3 aligned dwords; the chunk grid is aligned
+// to the frame's 4-pixel columns, 18 chunks per tile row); chunks that cross
+// the frame's left/right edge (or an unaligned buffer) fall back to clamped
+// byte loads.  All loads of a thread are issued before any conversion.
+// Samples outside the block-padded frame read 0 (H2); padding inside it
+// replicates the last column / row.
+constexpr int kChunksX = 18;
+constexpr int kChunks = kRows * kChunksX;
+constexpr int kChunkIters = (kChunks + kThreads - 1) / kThreads;
 __device__ __forceinline__ void load_xyb_tile(const FrontArgs& a, const float* lut, float* sPix,
                                               int ox, int oy) {
-  uint32_t rgb[kLoadIters];  // r | g << 8 | b << 16; bit 24 = outside the padded frame
+  const bool al = ((a.stride | (size_t)a.rgb) & 3) == 0;
+  uint32_t d[kChunkIters][3];
 #pragma unroll
-  for (int k = 0; k < kLoadIters; k++) {
-    // branch-free: every lane loads from a clamped (valid) address so the
-    // compiler can keep all loads in flight; validity is tracked in bit 24
-    const int i = min(threadIdx.x + k * kThreads, kTilePx - 1);
-    const int ly = i / 66, lx = i - ly * 66;
-    const int gx = ox + lx, gy = oy + ly;
-    const bool inside = gx >= 0 && gy >= 0 && gx < (int)a.xp && gy < (int)a.yp;
-    const int sx = min(max(gx, 0), (int)a.w - 1);
+  for (int k = 0; k < kChunkIters; k++) {
+    const int i = min(threadIdx.x + k * kThreads, kChunks - 1);
+    const int ly = i / kChunksX, cx = i - ly * kChunksX;
+    const int gy = oy + ly, gx0 = ox - 3 + 4 * cx;
     const int sy = min(max(gy, 0), (int)a.h - 1);
-    const uint8_t* p = a.rgb + (size_t)sy * a.stride + 3 * (size_t)sx;
-    rgb[k] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) |
-             (inside ? 0u : (1u << 24));
+    const uint8_t* row = a.rgb + (size_t)sy * a.stride;
+    if (al && gx0 >= 0 && gx0 + 4 <= (int)a.w) {
+      const uint32_t* p = reinterpret_cast<const uint32_t*>(row + 3 * (size_t)gx0);
+      d[k][0] = p[0];
+      d[k][1] = p[1];
+      d[k][2] = p[2];
+    } else {
+      uint32_t by[12];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int sx = min(max(gx0 + j, 0), (int)a.w - 1);
+        const uint8_t* q = row + 3 * (size_t)sx;
+        by[3 * j] = q[0];
+        by[3 * j + 1] = q[1];
+        by[3 * j + 2] = q[2];
+      }
+#pragma unroll
+      for (int w = 0; w < 3; w++)
+        d[k][w] = by[4 * w] | by[4 * w + 1] << 8 | by[4 * w + 2] << 16 | by[4 * w + 3] << 24;
+    }
   }
   const float cb = cbrt_det(kOpsinBias);
 #pragma unroll
-  for (int k = 0; k < kLoadIters; k++) {
+  for (int k = 0; k < kChunkIters; k++) {
     const int i = threadIdx.x + k * kThreads;
-    if (i < kTilePx) {
-      const int ly = i / 66, lx = i - ly * 66;
+    if (i >= kChunks) continue;
+    const int ly = i / kChunksX, cx = i - ly * kChunksX;
+    const int gy = oy + ly, gx0 = ox - 3 + 4 * cx;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int lx = 4 * cx - 3 + j;
+      if (lx < 0 || lx >= 66) continue;
+      const int gx = gx0 + j;
+      const bool inside = gx >= 0 && gy >= 0 && gx < (int)a.xp && gy < (int)a.yp;
       float X = 0.0f, Y = 0.0f, B = 0.0f;
-      const uint32_t v = rgb[k];
-      if (!(v >> 24)) pixel_xyb(lut, cb, v & 0xFF, (v >> 8) & 0xFF, (v >> 16) & 0xFF, X, Y, B);
+      if (inside) {
+        const int b0 = 3 * j;
+        const uint32_t r8 = (d[k][b0 >> 2] >> ((b0 & 3) * 8)) & 0xFF;
+        const uint32_t g8 = (d[k][(b0 + 1) >> 2] >> (((b0 + 1) & 3) * 8)) & 0xFF;
+        const uint32_t b8 = (d[k][(b0 + 2) >> 2] >> (((b0 + 2) & 3) * 8)) & 0xFF;
+        pixel_xyb(lut, cb, r8, g8, b8, X, Y, B);
+      }
       const int o = lds_at(lx, ly);
       sPix[o] = X;
       sPix[kPlane + o] = Y;
@@ -547,9 +578,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   if (a.xyb_out) {
     // tile-major XYB copy for the merge stage: [tile][X, Y, B][64][64]
     float* dst = a.xyb_out + (size_t)(ty * a.tiles_x + tx) * (3 * 4096);
-    for (int i = tid; i < 3 * 4096; i += kThreads) {
-      const int c = i >> 12, ly = (i >> 6) & 63, lx = i & 63;
-      dst[i] = sPix[c * kPlane + lds_at(lx + 1, ly + 1)];
+    // 16-byte stores; the 4 pixels lx+1..lx+4 (lx % 4 == 0) are contiguous
+    // in LDS (they share a skew)
+    for (int i = tid; i < 3 * 1024; i += kThreads) {
+      const int c = i >> 10, ly = (i >> 4) & 63, lx = (i & 15) * 4;
+      const float* q = sPix + c * kPlane + lds_at(lx + 1, ly + 1);
+      reinterpret_cast<float4*>(dst)[i] = make_float4(q[0], q[1], q[2], q[3]);
     }
   }
   const int nbx = min(8, (int)a.bxs - tx * 8), nby = min(8, (int)a.bys - ty * 8);
