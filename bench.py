@@ -19,6 +19,13 @@ N > 1 (launched by torch.distributed.run, backend nccl = RCCL):
   replica -- every rank encodes its own 8K frame (frame-level data
           parallelism, no data-path collective).
 Timing: barrier + synchronize on both sides of the K steps, max over ranks.
+--streams S (non-shard modes) runs S concurrent encoders per GPU (one host
+thread, context and HIP stream each; the K frames split between them).
+
+The line's value is the prefix-coded encode (default --coder prefix, S = 1);
+'ans_coder' reports the same workload with the ANS coder (libjxl's e7 entropy
+coder) timed with --alt-ans-streams concurrent encoders, because each pass
+group's rANS state chain is serial and latency-bound.
 
 The JSON line also carries:
   roofline     -- the fused front kernel (XYB + homogeneity + AQ + 8x8 ACS +
@@ -96,6 +103,12 @@ def main():
     ap.add_argument("--mode", choices=("shard", "replica"), default="shard")
     ap.add_argument("--coder", choices=("prefix", "ans"), default="prefix",
                     help="AC entropy coder (libjxl codes with ANS at e7)")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="concurrent encoders per GPU (replica / N=1 mode): one host thread, "
+                         "context and HIP stream each; a step is still one frame")
+    ap.add_argument("--alt-ans-streams", type=int, default=3,
+                    help="also time the ANS coder with this many concurrent encoders "
+                         "(reported under 'ans_coder'; 0 = off)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -125,41 +138,82 @@ def main():
         d_img = d_img.repeat(world, 1, 1).contiguous()
     torch.cuda.synchronize()
 
-    enc = jxg.Encoder(distance=args.distance, effort=args.effort, proposals=args.proposals,
-                      device=local, flags=jxg.FLAG_ANS if args.coder == "ans" else 0)
-    bufs = {}
+    def run(coder, nstreams):
+        """Warm up, then time args.steps frames over `nstreams` concurrent
+        encoders (one host thread, context and HIP stream each)."""
+        flags = jxg.FLAG_ANS if coder == "ans" else 0
+        encs = [jxg.Encoder(distance=args.distance, effort=args.effort,
+                            proposals=args.proposals, device=local, flags=flags)
+                for _ in range(nstreams)]
+        bufs = {}
 
-    def step():
-        if shard:
-            from jxg.dist import encode_sharded
-            return encode_sharded(enc, d_img, w, fh, rank, world, bufs=bufs, copy=False)
-        return enc.encode_device(d_img.data_ptr(), w, fh, copy=False)
+        def step(e):
+            if shard:
+                from jxg.dist import encode_sharded
+                return encode_sharded(e, d_img, w, fh, rank, world, bufs=bufs, copy=False)
+            return e.encode_device(d_img.data_ptr(), w, fh, copy=False)
 
-    for _ in range(args.warmup):
-        out = step()
-    front_ms = []
-    host_ms = []
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    nbytes = 0
-    for _ in range(args.steps):
-        # the codestream ends in (pinned) host memory on rank 0
-        out = step()
-        st = enc.stats()
-        front_ms.append(st["ms_front_kernel"])
-        host_ms.append((st["ms_host_call"], st["ms_host_codes"], st["ms_host_layout"]))
-        nbytes = len(out) if out is not None else 0
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
-    enc.close()
+        for e in encs:  # contexts warmed one after another
+            for _ in range(args.warmup):
+                step(e)
+        rec = {"front_ms": [], "host_ms": [], "sizes": []}
+
+        def worker(e, n):
+            # the codestream ends in (pinned) host memory; ctypes calls release
+            # the GIL, so the encoders' host work and HIP streams overlap
+            for _ in range(n):
+                out = step(e)
+                st = e.stats()
+                rec["front_ms"].append(st["ms_front_kernel"])
+                rec["host_ms"].append((st["ms_host_call"], st["ms_host_codes"],
+                                       st["ms_host_layout"]))
+                rec["sizes"].append(len(out) if out is not None else 0)
+
+        share = [args.steps // nstreams + (1 if i < args.steps % nstreams else 0)
+                 for i in range(nstreams)]
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        if nstreams == 1:
+            worker(encs[0], args.steps)
+        else:
+            import threading
+            ths = [threading.Thread(target=worker, args=(e, n)) for e, n in zip(encs, share)]
+            for t in ths:
+                t.start()
+            for t in ths:
+                t.join()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            dt = float(tt.item())
+        rec["dt"] = dt
+        rec["st"] = encs[0].stats()
+        for e in encs:
+            e.close()
+        return rec
+
+    nstreams = 1 if shard else max(1, args.streams)
+    R = run(args.coder, nstreams)
+    dt, front_ms, host_ms, st = R["dt"], R["front_ms"], R["host_ms"], R["st"]
+    nbytes = R["sizes"][-1] if R["sizes"] else 0
+    alt = None
+    if not shard and args.alt_ans_streams > 0 and args.coder != "ans":
+        # the same workload with the ANS coder (libjxl's e7 entropy coder):
+        # its per-group rANS chain is latency-bound, so concurrent encoders
+        # overlap it with the other frames' kernels
+        A = run("ans", args.alt_ans_streams)
+        alt = {"coder": "ans", "streams_per_gpu": args.alt_ans_streams,
+               "value": round(w * fh * world * args.steps / A["dt"] / 1e6, 2),
+               "ms_per_step": round(A["dt"] * 1e3 / args.steps, 3),
+               "ms_latency": round(sum(x[0] for x in A["host_ms"]) / len(A["host_ms"]), 3),
+               "bytes_per_frame": A["sizes"][-1],
+               "bpp": round(A["sizes"][-1] * 8.0 / (w * fh), 4)}
     if rank == 0:
         ms_step = dt * 1e3 / args.steps
         frame_px = w * fh
@@ -177,8 +231,9 @@ def main():
             par = "group-shard%d" % world
         else:
             workload = ("%s %dx%d RGB8 (synth_rgb8), VarDCT d%g e%d, proposals=%d, %s-coded, "
-                        "one frame per rank" % (name, w, h, args.distance, args.effort,
-                                                args.proposals, args.coder))
+                        "one frame per step, %d concurrent encoder stream(s) per rank"
+                        % (name, w, h, args.distance, args.effort, args.proposals, args.coder,
+                           nstreams))
             par = "frame-dp%d" % world
         res = {
             "metric": "MPix/s VarDCT encode @ d1.0, 8K RGB",
@@ -195,6 +250,8 @@ def main():
             "data": "synthetic",
             "config": {"workload": workload, "global_batch": 1 if shard else world,
                        "parallelism": par},
+            "streams_per_gpu": nstreams,
+            "ms_latency": round(sum(x[0] for x in host_ms) / len(host_ms), 3),
             "bytes_per_frame": nbytes,
             "bpp": round(nbytes * 8.0 / frame_px, 4),
             "stages_ms": {k: round(st[k], 4) for k in ("ms_front_kernel", "ms_front",
@@ -208,6 +265,8 @@ def main():
                          "traffic": load_pmc_traffic(name) if world == 1 else None,
                          "algorithmic_bytes": fb, "avg_ms": round(fms, 4)},
         }
+        if alt is not None:
+            res["ans_coder"] = alt
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(img, args.distance, args.effort)
         print(json.dumps(res), flush=True)

@@ -549,6 +549,9 @@ __device__ __forceinline__ void load_xyb_tile(const FrontArgs& a, const float* l
   }
 }
 
+// HOOKP: hook P compiled in (proposals bit 0); without it the kernel keeps
+// no hook-P candidate aside (fewer live registers)
+template <bool HOOKP>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void front_kernel(FrontArgs a) {
   __shared__ __attribute__((aligned(16))) float sPix[3 * kPlane];
   __shared__ __attribute__((aligned(16))) int16_t sStage[8][8][64];
@@ -587,7 +590,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     }
   }
   const int nbx = min(8, (int)a.bxs - tx * 8), nby = min(8, (int)a.bys - ty * 8);
-  const int wave = tid >> 6, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const size_t nb = (size_t)a.bxs * a.bys;
   const Tile tile{sPix, sPix + kPlane, sPix + 2 * kPlane, ox, oy};
   // ---- phase A: thesis homogeneity; wave w = region w, lane = block ----
@@ -620,7 +623,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   const int lbx = g, lby = wave;
   if (lbx >= nbx || lby >= nby) return;  // whole groups leave; no barrier follows
   const int b = lby * 8 + lbx;
-  const size_t gb = (size_t)(ty * 8 + lby) * a.bxs + tx * 8 + lbx;
+  // block index (recomputed where used: keeps a 64-bit value out of the
+  // candidate search's live registers)
+  auto gblock = [&]() { return (size_t)(ty * 8 + lby) * a.bxs + tx * 8 + lbx; };
+  size_t gb = gblock();
   const GroupCtx G{sPix, lby * 8 + 1, lbx * 8 + 1, r, sWperm, sIwperm, sBtab};
   // block DC (row partials, tree over rows) and AQ activity
   float dc[3];
@@ -659,6 +665,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     a.dc[gb] = xv >= 0.0f ? (int)(xv + 0.5f) : -(int)(-xv + 0.5f);
     a.dc[2 * nb + gb] = bv >= 0.0f ? (int)(bv + 0.5f) : -(int)(-bv + 0.5f);
   }
+  if (r == 0) a.qf[gb] = (uint8_t)(raw - 1);
   const float scale = (float)a.G * (float)raw / 65536.0f;
   const float inv_scale = 1.0f / scale;
   // ---- phase C: strategy search (FindBest8x8Transform [ext] + hooks) ----
@@ -673,7 +680,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     rv = sR[b][1];
     rd = sR[b][2];
   }
-  if (a.proposals & 1u) pt = partition_of(rh, rv, rd, a.distance);
+  if (HOOKP && (a.proposals & 1u)) pt = partition_of(rh, rv, rd, a.distance);
   // scan indices: DCT8 0, DCT4X4 1, DCT4X8 2, DCT8X4 3
   QVals best, ptq;
   int bt = kDCT8, bi = 0;
@@ -696,7 +703,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         beste = e1;
       }
     }
-    copy_q(ptq, A1.q, pt == kDCT8X4);
+    if (HOOKP) copy_q(ptq, A1.q, pt == kDCT8X4);
   }
   const bool need44 = ncand > 1 || pt == kDCT4X4, need48 = ncand > 1 || pt == kDCT4X8;
   if (need44 || need48) {
@@ -719,16 +726,18 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         beste = ew;
       }
     }
-    copy_q(ptq, A0.q, pt == kDCT4X4);
-    copy_q(ptq, A1.q, pt == kDCT4X8);
+    if (HOOKP) {
+      copy_q(ptq, A0.q, pt == kDCT4X4);
+      copy_q(ptq, A1.q, pt == kDCT4X8);
+    }
   }
-  if (bt == kDCT8 && pt != kDCT8) {
+  if (HOOKP && bt == kDCT8 && pt != kDCT8) {
     bt = pt;
     copy_q(best, ptq, true);
   }
+  gb = gblock();
   if (r == 0) {
     a.acs[gb] = (uint8_t)bt;
-    a.qf[gb] = (uint8_t)(raw - 1);
     // estimate summed by the merge stage: the search's best, stored before
     // the hook-P override (homogeneity-partitioning.diff:271 context)
     if (a.ent) a.ent[gb] = beste;
@@ -825,10 +834,17 @@ void set_front_constants(const float lut[256], const float wts[3][3][64], hipStr
   (void)hipStreamSynchronize(s);  // the static host tables must outlive the copies
 }
 void launch_front(const FrontArgs& a, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s) {
-  hipLaunchKernelGGL(front_kernel, dim3(tiles_x, tiles_y), dim3(kThreads), 0, s, a);
+  if (a.proposals & 1u)
+    hipLaunchKernelGGL(front_kernel<true>, dim3(tiles_x, tiles_y), dim3(kThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL(front_kernel<false>, dim3(tiles_x, tiles_y), dim3(kThreads), 0, s, a);
 }
 void launch_front_list(const FrontArgs& a, uint32_t ntiles, hipStream_t s) {
-  if (ntiles) hipLaunchKernelGGL(front_kernel, dim3(ntiles), dim3(kThreads), 0, s, a);
+  if (!ntiles) return;
+  if (a.proposals & 1u)
+    hipLaunchKernelGGL(front_kernel<true>, dim3(ntiles), dim3(kThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL(front_kernel<false>, dim3(ntiles), dim3(kThreads), 0, s, a);
 }
 void launch_homog(const HomogArgs& a, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s) {
   hipLaunchKernelGGL(homog_kernel, dim3(tiles_x, tiles_y), dim3(kThreads), 0, s, a);

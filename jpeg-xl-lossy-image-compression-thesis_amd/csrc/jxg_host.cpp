@@ -449,8 +449,10 @@ struct Ctx {
   size_t payload_body = 0;             //   and body bytes (in `out`)
 };
 
+static std::mutex g_const_mu;  // device __constant__ tables are shared by all contexts
 static jxg_status init_constants(Ctx* c) {
   if (c->constants_ready) return JXG_OK;
+  std::lock_guard<std::mutex> lock(g_const_mu);
   float lut[256];
   srgb_lut(lut);
   static float wts[3][3][64];
