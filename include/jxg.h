@@ -134,6 +134,30 @@ jxg_status jxg_shard_assemble(const uint8_t* const* payloads, const size_t* size
 jxg_status jxg_homogeneity_map(void* ctx, const float* xyb, uint32_t xsize, uint32_t ysize,
                                float distance, uint32_t flags, float* r3, uint8_t* type);
 
+/* ---- decode-side quality: the harness's metrics on the GPU ----
+ * Replaces ImageReader::calculate_mse / calculate_psnr
+ * (benchmark-jpegxl/src/image_reader.rs:555-606, via metrics.rs:28-53) and
+ * calculate_ssim (metrics.rs:55-84, ImageMagick `compare -metric SSIM`).
+ * orig / comp: RGB8 interleaved rows (comp = the decoded image).  mse is
+ * bit-identical to the reference's sequential f64 sum; ssim is the mean
+ * Gaussian-window (11x11, sigma 1.5, K1 0.01, K2 0.03) SSIM over all window
+ * positions inside the image and the three channels -- ImageMagick's exact
+ * variant is not in the reference (parity unpinned). */
+typedef struct {
+  uint64_t sse;     /* sum of squared sample differences (exact) */
+  uint64_t samples; /* 3 * xsize * ysize */
+  double mse;       /* sse / samples */
+  double psnr;      /* 10 log10(255^2 / mse); +inf when mse == 0 */
+  double ssim;      /* NaN when not requested or the image is under 11x11 */
+} jxg_quality;
+
+jxg_status jxg_compare_rgb8(void* ctx, const uint8_t* orig, size_t orig_stride,
+                            const uint8_t* comp, size_t comp_stride, uint32_t xsize,
+                            uint32_t ysize, int want_ssim, jxg_quality* out);
+jxg_status jxg_compare_rgb8_device(void* ctx, const void* d_orig, size_t orig_stride,
+                                   const void* d_comp, size_t comp_stride, uint32_t xsize,
+                                   uint32_t ysize, int want_ssim, jxg_quality* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -427,6 +427,10 @@ struct Ctx {
   PinBuf<uint8_t> h_ans_tab;
   DevBuf<LfRow> rows;
   DevBuf<LfChunk> lfchunks;
+  DevBuf<uint8_t> q_orig, q_comp;  // decode-side quality (jxg_compare_rgb8)
+  DevBuf<uint64_t> q_sse;
+  DevBuf<double> q_part, q_ssim;
+  bool gauss_ready = false;
   DevBuf<ConcatPiece> pieces;
   // host
   PinBuf<uint32_t> h_hist_ac, h_bound, h_ntok, h_lfhist, h_sbound, h_gbits, h_sbits, h_vcount;
@@ -1669,6 +1673,86 @@ jxg_status jxg_homogeneity_map(void* ctx, const float* xyb, uint32_t xsize, uint
   JXG_HIP(hipMemcpyAsync(type, c->type.p, nb, hipMemcpyDeviceToHost, s));
   JXG_HIP(hipStreamSynchronize(s));
   return JXG_OK;
+}
+
+// ---- decode-side quality (benchmark-jpegxl image_reader.rs:555-606) ----
+// Gaussian window of the SSIM: exp(-(k-5)^2 / 4.5), normalized by the sum taken
+// in k order (== oracle/metrics.py gaussian_window, libm exp on both sides)
+static void gauss_window(double g[11]) {
+  double sum = 0.0;
+  for (int k = 0; k < 11; k++) {
+    const double d = (double)(k - 5);
+    g[k] = std::exp(-(d * d) / (2.0 * 1.5 * 1.5));
+    sum += g[k];
+  }
+  for (int k = 0; k < 11; k++) g[k] /= sum;
+}
+
+static jxg_status compare_device(Ctx* c, const uint8_t* d_orig, size_t so, const uint8_t* d_comp,
+                                 size_t sc, uint32_t w, uint32_t h, int want_ssim,
+                                 jxg_quality* out) {
+  hipStream_t s = c->stream;
+  if (!c->gauss_ready) {
+    std::lock_guard<std::mutex> lock(g_const_mu);
+    double g[11];
+    gauss_window(g);
+    set_gauss_table(g, s);
+    JXG_HIP(hipGetLastError());
+    c->gauss_ready = true;
+  }
+  const uint32_t np = ssim_partials(w, h);
+  const bool ssim = want_ssim && np > 0;
+  JXG_HIP(c->q_sse.ensure(1));
+  JXG_HIP(c->q_ssim.ensure(1));
+  if (ssim) JXG_HIP(c->q_part.ensure(np));
+  JXG_HIP(hipMemsetAsync(c->q_sse.p, 0, sizeof(uint64_t), s));
+  MetricArgs a{d_orig, d_comp, so, sc, w, h, c->q_sse.p, ssim ? c->q_part.p : nullptr,
+               ssim ? c->q_ssim.p : nullptr};
+  launch_metrics(a, s);
+  JXG_HIP(hipGetLastError());
+  uint64_t sse = 0;
+  double ssum = 0.0;
+  JXG_HIP(hipMemcpyAsync(&sse, c->q_sse.p, sizeof(sse), hipMemcpyDeviceToHost, s));
+  if (ssim) JXG_HIP(hipMemcpyAsync(&ssum, c->q_ssim.p, sizeof(ssum), hipMemcpyDeviceToHost, s));
+  JXG_HIP(hipStreamSynchronize(s));
+  out->sse = sse;
+  out->samples = (uint64_t)w * h * 3;
+  out->mse = (double)sse / (double)out->samples;
+  out->psnr = 10.0 * std::log10((255.0 * 255.0) / out->mse);  // mse 0 -> +inf (as f64 in Rust)
+  out->ssim = ssim ? ssum / (3.0 * (double)(w - 10) * (double)(h - 10)) : NAN;
+  return JXG_OK;
+}
+
+jxg_status jxg_compare_rgb8_device(void* ctx, const void* d_orig, size_t orig_stride,
+                                   const void* d_comp, size_t comp_stride, uint32_t xsize,
+                                   uint32_t ysize, int want_ssim, jxg_quality* out) {
+  if (!ctx || !d_orig || !d_comp || !out || xsize == 0 || ysize == 0 ||
+      orig_stride < (size_t)xsize * 3 || comp_stride < (size_t)xsize * 3)
+    return JXG_ERR_INVALID_ARG;
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
+  return compare_device(c, static_cast<const uint8_t*>(d_orig), orig_stride,
+                        static_cast<const uint8_t*>(d_comp), comp_stride, xsize, ysize, want_ssim,
+                        out);
+}
+
+jxg_status jxg_compare_rgb8(void* ctx, const uint8_t* orig, size_t orig_stride,
+                            const uint8_t* comp, size_t comp_stride, uint32_t xsize,
+                            uint32_t ysize, int want_ssim, jxg_quality* out) {
+  if (!ctx || !orig || !comp || !out || xsize == 0 || ysize == 0 ||
+      orig_stride < (size_t)xsize * 3 || comp_stride < (size_t)xsize * 3)
+    return JXG_ERR_INVALID_ARG;
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
+  const size_t row = (size_t)xsize * 3, n = row * ysize;
+  JXG_HIP(c->q_orig.ensure(n));
+  JXG_HIP(c->q_comp.ensure(n));
+  hipStream_t s = c->stream;
+  JXG_HIP(hipMemcpy2DAsync(c->q_orig.p, row, orig, orig_stride, row, ysize,
+                           hipMemcpyHostToDevice, s));
+  JXG_HIP(hipMemcpy2DAsync(c->q_comp.p, row, comp, comp_stride, row, ysize,
+                           hipMemcpyHostToDevice, s));
+  return compare_device(c, c->q_orig.p, row, c->q_comp.p, row, xsize, ysize, want_ssim, out);
 }
 
 }  // extern "C"

@@ -199,6 +199,19 @@ void set_merge_constants(const float* llf_p /*[4][8]*/, const float* llf_ib /*[4
                          hipStream_t s);
 void launch_merge(const MergeArgs& a, hipStream_t s);
 void launch_vb_list(const VbArgs& a, uint32_t nlf, hipStream_t s);
+// decode-side quality (jxg_metrics.hip): orig / comp RGB8 interleaved rows
+struct MetricArgs {
+  const uint8_t* orig;
+  const uint8_t* comp;
+  size_t so, sc;  // row strides (bytes)
+  uint32_t w, h;
+  uint64_t* sse;      // out: sum of squared sample differences (pre-zeroed)
+  double* partials;   // [ssim_partials(w, h)] per-workgroup SSIM sums
+  double* ssim;       // out: sum of window SSIMs over all channels, or null (skip SSIM)
+};
+uint32_t ssim_partials(uint32_t w, uint32_t h);
+void set_gauss_table(const double* g, hipStream_t s);
+void launch_metrics(const MetricArgs& a, hipStream_t s);
 void launch_concat(const ConcatPiece* pieces, uint32_t npieces, uint64_t max_words,
                    const uint32_t* scratch, const uint32_t* chunks, uint32_t* out,
                    hipStream_t s);

@@ -1,0 +1,173 @@
+// jxg_metrics.hip -- decode-side image quality on gfx950: the harness's
+// MSE / PSNR (benchmark-jpegxl/src/image_reader.rs:555-606, metrics.rs:28-53)
+// and SSIM (metrics.rs:55-84 shells out to ImageMagick `compare -metric SSIM`;
+// restated here as the Gaussian-window SSIM of Wang et al., parity unpinned).
+//
+//   sse_kernel    sum over samples of (orig - comp)^2 as exact 64-bit
+//                 integers.  The reference accumulates the same squares in
+//                 f64 one sample at a time; every partial sum stays below
+//                 2^53 (<= 65025 per sample), so the f64 sum is exact and
+//                 equals this integer sum bit for bit, in any order.
+//                 HBM-bound: 6 B read per pixel.
+//   ssim_kernel   one 256-thread workgroup per (32 x 32 output tile, channel):
+//                 the 42 x 42 input window of both images -> LDS, horizontal
+//                 11-tap Gaussian sums of a, b, a^2, b^2, ab (f64, taps in
+//                 ascending order) -> LDS, vertical sums (same order), the SSIM
+//                 of every valid window centre, per-workgroup partial (fixed
+//                 tree) -> partials[]; ssim_reduce_kernel sums the partials in
+//                 a fixed order, so the result is deterministic.
+// Op order == oracle/metrics.py (no FMA contraction: -ffp-contract=off).
+#include "jxg_kernels.h"
+
+namespace jxg {
+
+__constant__ double c_gauss[11];  // normalized exp(-(k-5)^2 / (2 * 1.5^2))
+
+constexpr int kSsimT = 32;             // output tile edge
+constexpr int kSsimIn = kSsimT + 10;   // input window edge (5 px halo)
+
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// grid-stride over rows; thread = 4-byte word of a row (byte tail: lane loop)
+__global__ __launch_bounds__(256) void sse_kernel(MetricArgs a) {
+  __shared__ uint64_t sW[4];
+  const size_t rowb = (size_t)a.w * 3;
+  uint64_t acc = 0;
+  for (uint32_t y = blockIdx.x; y < a.h; y += gridDim.x) {
+    const uint8_t* p = a.orig + (size_t)y * a.so;
+    const uint8_t* q = a.comp + (size_t)y * a.sc;
+    uint32_t racc = 0;  // <= ceil(rowb / 256) * 4 * 65025 < 2^32 for rows < 4 M samples
+    const bool al = ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(q)) & 3) == 0;
+    const size_t nw = al ? rowb / 4 : 0;
+    for (size_t i = threadIdx.x; i < nw; i += blockDim.x) {
+      const uint32_t u = reinterpret_cast<const uint32_t*>(p)[i];
+      const uint32_t v = reinterpret_cast<const uint32_t*>(q)[i];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int d = (int)((u >> (8 * k)) & 0xFF) - (int)((v >> (8 * k)) & 0xFF);
+        racc += (uint32_t)(d * d);
+      }
+    }
+    for (size_t i = nw * 4 + threadIdx.x; i < rowb; i += blockDim.x) {
+      const int d = (int)p[i] - (int)q[i];
+      racc += (uint32_t)(d * d);
+    }
+    acc += racc;
+  }
+  acc = wave_sum_u64(acc);
+  if ((threadIdx.x & 63) == 0) sW[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(reinterpret_cast<unsigned long long*>(a.sse),
+                                  (unsigned long long)(sW[0] + sW[1] + sW[2] + sW[3]));
+}
+
+__global__ __launch_bounds__(256) void ssim_kernel(MetricArgs a) {
+  __shared__ float sA[kSsimIn][kSsimIn + 1], sB[kSsimIn][kSsimIn + 1];
+  __shared__ double sH[5][kSsimIn][kSsimT];
+  __shared__ double sRed[4];
+  const int c = blockIdx.z;
+  const int x0 = blockIdx.x * kSsimT, y0 = blockIdx.y * kSsimT;  // first window centre - 5
+  const int t = threadIdx.x;
+  for (int i = t; i < kSsimIn * kSsimIn; i += 256) {
+    const int ly = i / kSsimIn, lx = i - ly * kSsimIn;
+    const int gx = x0 + lx, gy = y0 + ly;
+    float va = 0.0f, vb = 0.0f;
+    if (gx < (int)a.w && gy < (int)a.h) {
+      va = (float)a.orig[(size_t)gy * a.so + 3 * (size_t)gx + c];
+      vb = (float)a.comp[(size_t)gy * a.sc + 3 * (size_t)gx + c];
+    }
+    sA[ly][lx] = va;
+    sB[ly][lx] = vb;
+  }
+  __syncthreads();
+  // horizontal: window centre column x0 + 5 + j, all 42 input rows
+  for (int i = t; i < kSsimIn * kSsimT; i += 256) {
+    const int ly = i / kSsimT, j = i - ly * kSsimT;
+    double ha = 0.0, hb = 0.0, haa = 0.0, hbb = 0.0, hab = 0.0;
+#pragma unroll
+    for (int k = 0; k < 11; k++) {
+      const double g = c_gauss[k];
+      const double va = (double)sA[ly][j + k], vb = (double)sB[ly][j + k];
+      ha = ha + g * va;
+      hb = hb + g * vb;
+      haa = haa + g * (va * va);
+      hbb = hbb + g * (vb * vb);
+      hab = hab + g * (va * vb);
+    }
+    sH[0][ly][j] = ha;
+    sH[1][ly][j] = hb;
+    sH[2][ly][j] = haa;
+    sH[3][ly][j] = hbb;
+    sH[4][ly][j] = hab;
+  }
+  __syncthreads();
+  // vertical + SSIM: thread = (column j, 4 rows)
+  const int j = t & 31, r0 = (t >> 5) * 4;
+  const double C1 = (0.01 * 255.0) * (0.01 * 255.0), C2 = (0.03 * 255.0) * (0.03 * 255.0);
+  double part = 0.0;
+  for (int r = r0; r < r0 + 4; r++) {
+    const int cx = x0 + 5 + j, cy = y0 + 5 + r;  // window centre
+    if (cx + 5 >= (int)a.w || cy + 5 >= (int)a.h) continue;
+    double m[5];
+#pragma unroll
+    for (int q = 0; q < 5; q++) {
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < 11; k++) s = s + c_gauss[k] * sH[q][r + k][j];
+      m[q] = s;
+    }
+    const double mab = m[0] * m[1], maa = m[0] * m[0], mbb = m[1] * m[1];
+    const double vaa = m[2] - maa, vbb = m[3] - mbb, cab = m[4] - mab;
+    const double num = (2.0 * mab + C1) * (2.0 * cab + C2);
+    const double den = (maa + mbb + C1) * (vaa + vbb + C2);
+    part = part + num / den;
+  }
+  for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+  if ((t & 63) == 0) sRed[t >> 6] = part;
+  __syncthreads();
+  if (t == 0) {
+    const uint32_t wg = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    a.partials[wg] = (sRed[0] + sRed[1]) + (sRed[2] + sRed[3]);
+  }
+}
+
+// one workgroup: thread-strided partial sums in index order, then a fixed tree
+__global__ __launch_bounds__(256) void ssim_reduce_kernel(const double* partials, uint32_t n,
+                                                          double* out) {
+  __shared__ double s[256];
+  double v = 0.0;
+  for (uint32_t i = threadIdx.x; i < n; i += 256) v = v + partials[i];
+  s[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) s[threadIdx.x] = s[threadIdx.x] + s[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out = s[0];
+}
+
+uint32_t ssim_partials(uint32_t w, uint32_t h) {
+  if (w < 11 || h < 11) return 0;
+  const uint32_t tx = (w - 10 + kSsimT - 1) / kSsimT, ty = (h - 10 + kSsimT - 1) / kSsimT;
+  return tx * ty * 3;
+}
+
+void set_gauss_table(const double* g, hipStream_t s) {
+  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_gauss), g, 11 * sizeof(double), 0,
+                               hipMemcpyHostToDevice, s);
+}
+
+void launch_metrics(const MetricArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(sse_kernel, dim3(a.h < 2048 ? a.h : 2048), dim3(256), 0, s, a);
+  if (a.ssim && a.w >= 11 && a.h >= 11) {
+    const uint32_t tx = (a.w - 10 + kSsimT - 1) / kSsimT, ty = (a.h - 10 + kSsimT - 1) / kSsimT;
+    hipLaunchKernelGGL(ssim_kernel, dim3(tx, ty, 3), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(ssim_reduce_kernel, dim3(1), dim3(256), 0, s, a.partials, tx * ty * 3,
+                       a.ssim);
+  }
+}
+
+}  // namespace jxg

@@ -68,12 +68,17 @@ class _Stats(ctypes.Structure):
                 ("ms_front_kernel", ctypes.c_float)]
 
 
+class _Quality(ctypes.Structure):
+    _fields_ = [("sse", ctypes.c_uint64), ("samples", ctypes.c_uint64), ("mse", ctypes.c_double),
+                ("psnr", ctypes.c_double), ("ssim", ctypes.c_double)]
+
+
 # every symbol declared in include/jxg.h
 EXPORTS = ("jxg_status_str", "jxg_create", "jxg_destroy", "jxg_encode_rgb8",
            "jxg_encode_rgb8_device", "jxg_encode_batch_rgb8", "jxg_get_stats",
            "jxg_buffer_free", "jxg_homogeneity_map", "jxg_shard_sizes", "jxg_shard_begin",
            "jxg_shard_end", "jxg_shard_payload", "jxg_shard_assemble_device",
-           "jxg_shard_assemble")
+           "jxg_shard_assemble", "jxg_compare_rgb8", "jxg_compare_rgb8_device")
 
 _lib = None
 
@@ -112,6 +117,10 @@ def load():
                                               ctypes.c_uint32, ctypes.POINTER(_Buffer)]
     lib.jxg_shard_assemble.argtypes = [ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)),
                                        ctypes.POINTER(sz), ctypes.c_uint32, ctypes.POINTER(_Buffer)]
+    cmp_args = [vp, vp, sz, vp, sz, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+                ctypes.POINTER(_Quality)]
+    lib.jxg_compare_rgb8.argtypes = cmp_args
+    lib.jxg_compare_rgb8_device.argtypes = cmp_args
     _lib = lib
     return lib
 
@@ -272,6 +281,32 @@ class Encoder:
                                           r3.ctypes.data, t.ctypes.data))
         return r3, t
 
+    def compare(self, orig: np.ndarray, comp: np.ndarray, ssim: bool = True) -> dict:
+        """Decode-side quality on the GPU (jxg_compare_rgb8): orig / comp are
+        (H, W, 3) uint8 (comp = the decoded image).  Returns sse, samples, mse,
+        psnr (image_reader.rs:555-606) and ssim (metrics.rs:55-84 counterpart)."""
+        o = np.asarray(orig)
+        c = np.asarray(comp)
+        if o.shape != c.shape or o.ndim != 3 or o.shape[2] != 3:
+            raise ValueError("orig / comp must both be (H, W, 3) uint8")
+        o = np.ascontiguousarray(o, dtype=np.uint8)
+        c = np.ascontiguousarray(c, dtype=np.uint8)
+        h, w = o.shape[:2]
+        q = _Quality()
+        _check(load().jxg_compare_rgb8(self._ctx, o.ctypes.data, w * 3, c.ctypes.data, w * 3, w, h,
+                                       1 if ssim else 0, ctypes.byref(q)))
+        return {"sse": q.sse, "samples": q.samples, "mse": q.mse, "psnr": q.psnr, "ssim": q.ssim}
+
+    def compare_device(self, d_orig: int, d_comp: int, width: int, height: int,
+                       orig_stride: int | None = None, comp_stride: int | None = None,
+                       ssim: bool = True) -> dict:
+        """Same on device-resident RGB8 (e.g. torch tensors' data_ptr())."""
+        q = _Quality()
+        _check(load().jxg_compare_rgb8_device(
+            self._ctx, ctypes.c_void_p(d_orig), orig_stride or width * 3, ctypes.c_void_p(d_comp),
+            comp_stride or width * 3, width, height, 1 if ssim else 0, ctypes.byref(q)))
+        return {"sse": q.sse, "samples": q.samples, "mse": q.mse, "psnr": q.psnr, "ssim": q.ssim}
+
 
 # ---------------------------------------------------------------------------
 # sharding helpers (host side; no device needed)
@@ -328,11 +363,57 @@ def make_payload(rank: int, world: int, width: int, height: int, sections) -> by
 # ---------------------------------------------------------------------------
 # harness mirror (benchmark-jpegxl)
 # ---------------------------------------------------------------------------
+def _rust_plain(digits_repr: str) -> str:
+    """Shortest round-trip digits (Python repr) -> Rust's exponent-free form."""
+    s = digits_repr
+    neg = s.startswith("-")
+    if neg:
+        s = s[1:]
+    if "e" in s or "E" in s:
+        mant, exp = s.lower().split("e")
+        e = int(exp)
+        if "." in mant:
+            ip, fp = mant.split(".")
+        else:
+            ip, fp = mant, ""
+        point = len(ip) + e  # position of the decimal point within ip + fp
+        allds = ip + fp
+        if point <= 0:
+            s = "0." + "0" * (-point) + allds.lstrip("0")
+        elif point >= len(allds):
+            s = allds + "0" * (point - len(allds))
+        else:
+            s = allds[:point] + "." + allds[point:]
+    if s.endswith(".0"):
+        s = s[:-2]
+    return ("-" if neg else "") + s
+
+
 def rust_f64(v: float) -> str:
-    """Rust ``format!("{}", f64)``: 1.0 -> "1", 0.5 -> "0.5"."""
-    if float(v).is_integer():
-        return str(int(v))
-    return repr(float(v))
+    """Rust ``format!("{}", f64)`` / ``f64::to_string``: shortest round-trip
+    digits, never an exponent (1.0 -> "1", 1e-7 -> "0.0000001", 1e20 ->
+    "100000000000000000000"), "NaN", "inf", "-inf"."""
+    v = float(v)
+    if math.isnan(v):
+        return "NaN"
+    if math.isinf(v):
+        return "inf" if v > 0 else "-inf"
+    if v == 0.0:
+        return "-0" if math.copysign(1.0, v) < 0 else "0"
+    return _rust_plain(repr(v))
+
+
+def rust_f32(v: float) -> str:
+    """Rust ``f32::to_string`` (the CSV's Distance column, csv_writer.rs:27):
+    the shortest digits that round-trip through f32."""
+    f = np.float32(v)
+    if np.isnan(f):
+        return "NaN"
+    if np.isinf(f):
+        return "inf" if f > 0 else "-inf"
+    if f == 0:
+        return "-0" if np.signbit(f) else "0"
+    return _rust_plain(np.format_float_positional(f, unique=True, trim="-"))
 
 
 def comp_image_name(stem: str, distance: float, effort: int) -> str:
