@@ -1534,6 +1534,9 @@ void jxg_destroy(void* ctx) {
   Ctx* c = static_cast<Ctx*>(ctx);
   (void)hipSetDevice(c->params.device);
   (void)hipStreamSynchronize(c->stream);
+#ifdef JXG_MERGE_PROFILE
+  dump_merge_profile();
+#endif
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);

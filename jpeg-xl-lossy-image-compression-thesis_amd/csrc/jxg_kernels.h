@@ -198,6 +198,7 @@ void set_cluster_table(const uint8_t* tab, hipStream_t s);
 void set_merge_constants(const float* llf_p /*[4][8]*/, const float* llf_ib /*[4][8][8]*/,
                          hipStream_t s);
 void launch_merge(const MergeArgs& a, hipStream_t s);
+void dump_merge_profile();  // JXG_MERGE_PROFILE experiment builds; no-op otherwise
 void launch_vb_list(const VbArgs& a, uint32_t nlf, hipStream_t s);
 // decode-side quality (jxg_metrics.hip): orig / comp RGB8 interleaved rows
 struct MetricArgs {

@@ -32,6 +32,8 @@
 // Float op order == oracle/merge.c (jxo_varblock, jxo_llf_dc, jxo_merge_tile).
 #include <float.h>
 
+#include <cstdio>
+
 #include "jxg_device.h"
 #include "jxg_kernels.h"
 #include "jxg_lee_tables.h"
@@ -42,6 +44,9 @@ __constant__ float c_llf_p[4 * 8];   // [log2 M][k]
 __constant__ float c_llf_ib[4 * 64]; // [log2 M][n][k]
 
 constexpr int kMThreads = 256;
+#ifndef JXG_MERGE_WPE
+#define JXG_MERGE_WPE 3  // waves per SIMD the eval/write kernels are register-capped for
+#endif
 constexpr int kMS = 65;  // LDS row stride (floats)
 constexpr int kMPlane = 64 * kMS;
 
@@ -50,13 +55,19 @@ constexpr int ilog2c() {
   return N <= 1 ? 0 : 1 + ilog2c<N / 2>();
 }
 
+// Two independent transforms per lane: f2 holds the same element of two rows
+// (or columns), so every butterfly is one packed op (v_pk_add_f32 /
+// v_pk_mul_f32) with no operand shuffles; each half sees exactly the float ops
+// of the scalar transform (no contraction), so results are bit-identical.
+typedef float f2 __attribute__((ext_vector_type(2)));
+
 // unnormalized DCT-II in registers, Lee's recursive even/odd split
-// (== oracle/merge.c lee); constants are instruction immediates
-template <int N>
-__device__ __forceinline__ void lee(float* x) {
+// (== oracle/merge.c lee); T = float or f2
+template <int N, class T>
+__device__ __forceinline__ void lee(T* x) {
   if constexpr (N > 1) {
     constexpr int h = N / 2, l = ilog2c<N>();
-    float a[h], b[h];
+    T a[h], b[h];
 #pragma unroll
     for (int i = 0; i < h; i++) {
       a[i] = x[i] + x[N - 1 - i];
@@ -83,24 +94,44 @@ __device__ __forceinline__ void dct_from(const float* src, int st, float* x) {
 }
 // half h of the normalized 64-point DCT (Lee's first split: h = 0 the even
 // outputs 2k from the sums, h = 1 the odd outputs 2k+1 from the scaled
-// differences) -- the same float ops as lee<64>, spread over two lanes
-__device__ __forceinline__ void dct64_half(const float* src, int st, int h, float* y) {
-  float t[32];
+// differences) -- the same float ops as lee<64>, spread over two lanes.
+// dct64_first: t[i] from x[i] and its mirror x[63 - i]; dct64_rest: the
+// 32-point transform of t and the output scaling, out(k, value) for output
+// 2k + h.  T = f2: two independent rows / columns with the same h.
+template <class T>
+__device__ __forceinline__ T dct64_first(T xi, T xm, int i, int h) {
+  return h == 0 ? xi + xm : (xi - xm) * kLeeC[6][i];
+}
+template <class T, class Out>
+__device__ __forceinline__ void dct64_rest(T* t, int h, Out out) {
+  lee<32>(t);
   if (h == 0) {
 #pragma unroll
-    for (int i = 0; i < 32; i++) t[i] = src[i * st] + src[(63 - i) * st];
-    lee<32>(t);
-#pragma unroll
-    for (int k = 0; k < 32; k++) y[k] = t[k] * kLeeS[6][2 * k];
+    for (int k = 0; k < 32; k++) out(k, t[k] * kLeeS[6][2 * k]);
   } else {
 #pragma unroll
-    for (int i = 0; i < 32; i++) t[i] = (src[i * st] - src[(63 - i) * st]) * kLeeC[6][i];
-    lee<32>(t);
-#pragma unroll
-    for (int k = 0; k < 31; k++) y[k] = (t[k] + t[k + 1]) * kLeeS[6][2 * k + 1];
-    y[31] = t[31] * kLeeS[6][63];
+    for (int k = 0; k < 31; k++) out(k, (t[k] + t[k + 1]) * kLeeS[6][2 * k + 1]);
+    out(31, t[31] * kLeeS[6][63]);
   }
 }
+
+// JXG_MERGE_PROFILE (experiment builds only): per (shape, phase) cycle sums
+// of thread 0 of every eval workgroup, printed by dump_merge_profile()
+#ifdef JXG_MERGE_PROFILE
+__device__ unsigned long long g_mprof[16][8];
+#define MPROF_MARK(k)                                                 \
+  do {                                                                \
+    if (!WRITE && threadIdx.x == 0) {                                 \
+      const unsigned long long now_ = __builtin_readcyclecounter();   \
+      if ((k) > 0) atomicAdd(&g_mprof[P.si][(k)], now_ - mprof_t0);   \
+      mprof_t0 = now_;                                                \
+    }                                                                 \
+  } while (0)
+#else
+#define MPROF_MARK(k) \
+  do {                \
+  } while (0)
+#endif
 
 // merged shapes (== oracle jxo_shapes): raw id, blocks down / across (log2),
 // cost multiplier
@@ -115,7 +146,9 @@ constexpr ShapeDesc kShapes[kNumShapes] = {
 
 __device__ __forceinline__ int bitlen_u(uint32_t v) { return 32 - __clz(v); }
 
-// 53.9 KB: three workgroups per CU
+// 53.7 KB: three workgroups per CU (gfx950 allocates LDS in 1280-byte
+// granules: 42 granules = 53760 B is the most that fits three; measured --
+// 256 more bytes dropped the eval kernel to two workgroups per CU)
 struct MergeLds {
   float co[3 * kMPlane];  // coefficient image of the tile's varblocks; column
                           // 64 of row b of plane c (padding) holds the LLF of
@@ -136,7 +169,7 @@ __device__ __forceinline__ float& llf_at(MergeLds& S, int c, int b) {
 
 // one (tile, shape) workgroup: all index math is shifts and masks
 struct Pass {
-  int type, lcy, lcx, soff, ls, tx, ty, tile;
+  int si, type, lcy, lcx, soff, ls, tx, ty, tile;
   float tmul;
   __device__ __forceinline__ int cy() const { return 1 << lcy; }
   __device__ __forceinline__ int cx() const { return 1 << lcx; }
@@ -167,6 +200,7 @@ __device__ __forceinline__ bool decode_wg(const MergeArgs& a, int& tile, int& si
 
 __device__ __forceinline__ Pass make_pass(const MergeArgs& a, int tile, int si) {
   Pass P;
+  P.si = si;
   const ShapeDesc& D = kShapes[si];
   P.type = D.type;
   P.lcy = D.lcy;
@@ -200,19 +234,37 @@ __device__ void row_pass(const MergeArgs& a, const Pass& P, MergeLds& S) {
   const float* tsrc = a.xyb + (size_t)P.tile * (3 * 4096);
   const int R = P.R(), lvr = P.lNV() + P.lR();
   if constexpr (C == 64) {
-    const int n = 2 * 3 * P.NV() * R;  // <= 384
+    // item = (row pair, half h): rows r and r + 1 of one varblock and channel
+    // (R >= 32: pairs never straddle a varblock); h is wave-uniform: waves
+    // alternate h over 64-pair chunks
+    const int npairs = 3 * P.NV() * R / 2;  // 96
+    const int n = ((npairs + 63) >> 6) << 7;
     for (int i = threadIdx.x; i < n; i += kMThreads) {
-      const int h = (i >> 6) & 1, r = ((i >> 7) << 6) | (i & 63);
+      const int h = (i >> 6) & 1, pp = ((i >> 7) << 6) | (i & 63), r = pp * 2;
+      if (pp >= npairs) continue;
       const int c = r >> lvr, v = (r >> P.lR()) & (P.NV() - 1), y = r & (R - 1);
       if (!S.valid[v]) continue;
-      float row[64], o[32];
-      load_row<64>(tsrc + c * 4096 + (P.by0(v) * 8 + y) * 64, row);
-      dct64_half(row, 1, h, o);
-      const int off = P.off(v, c) + y * kMS;
+      const float4* s0 = reinterpret_cast<const float4*>(tsrc + c * 4096 + (P.by0(v) * 8 + y) * 64);
+      const float4* s1 = s0 + 16;  // row y + 1
+      f2 t[32];
+      // 16-byte loads of x[4q..4q+3] and of its mirror x[60-4q..63-4q]
 #pragma unroll
-      for (int k = 0; k < 32; k++) S.co[off + 2 * k + h] = o[k];
+      for (int q = 0; q < 8; q++) {
+        const float4 a0 = s0[q], b0 = s0[15 - q], a1 = s1[q], b1 = s1[15 - q];
+        const float fa0[4] = {a0.x, a0.y, a0.z, a0.w}, fb0[4] = {b0.x, b0.y, b0.z, b0.w};
+        const float fa1[4] = {a1.x, a1.y, a1.z, a1.w}, fb1[4] = {b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          t[4 * q + j] = dct64_first(f2{fa0[j], fa1[j]}, f2{fb0[3 - j], fb1[3 - j]}, 4 * q + j, h);
+      }
+      const int off = P.off(v, c) + y * kMS;
+      dct64_rest(t, h, [&](int k, f2 o) {
+        S.co[off + 2 * k + h] = o.x;
+        S.co[off + kMS + 2 * k + h] = o.y;
+      });
     }
   } else {
+    // thread: row pairs (r, r + 256) -- two rows per transform (f2 lanes)
     constexpr int PER = (3 * 4096 / C + kMThreads - 1) / kMThreads;  // 6, 3, 2
     const int nrows = 3 * P.NV() * R;
     float buf[PER][C];
@@ -222,53 +274,105 @@ __device__ void row_pass(const MergeArgs& a, const Pass& P, MergeLds& S) {
       if (r < nrows) {
         const int c = r >> lvr, v = (r >> P.lR()) & (P.NV() - 1), y = r & (R - 1);
         load_row<C>(tsrc + c * 4096 + (P.by0(v) * 8 + y) * 64 + P.bx0(v) * 8, buf[k]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < C; q++) buf[k][q] = 0.0f;
       }
     }
+    constexpr int l = ilog2c<C>();
 #pragma unroll
-    for (int k = 0; k < PER; k++) {
-      const int r = threadIdx.x + k * kMThreads;
-      if (r >= nrows) continue;
-      const int c = r >> lvr, v = (r >> P.lR()) & (P.NV() - 1), y = r & (R - 1);
-      if (!S.valid[v]) continue;
-      float* x = buf[k];
-      lee<C>(x);
-      constexpr int l = ilog2c<C>();
-      const int off = P.off(v, c) + y * kMS;
+    for (int k = 0; k < PER; k += 2) {
+      const int r0 = threadIdx.x + k * kMThreads, r1 = r0 + kMThreads;
+      if (r0 >= nrows) continue;
+      const int c0 = r0 >> lvr, v0 = (r0 >> P.lR()) & (P.NV() - 1), y0 = r0 & (R - 1);
+      const int c1 = r1 >> lvr, v1 = (r1 >> P.lR()) & (P.NV() - 1), y1 = r1 & (R - 1);
+      const bool ok0 = S.valid[v0], ok1 = k + 1 < PER && r1 < nrows && S.valid[v1];
+      if (!ok0 && !ok1) continue;
+      if (k + 1 < PER) {
+        f2 x[C];
 #pragma unroll
-      for (int q = 0; q < C; q++) S.co[off + q] = x[q] * kLeeS[l][q];
+        for (int q = 0; q < C; q++) x[q] = f2{buf[k][q], buf[k + 1][q]};
+        lee<C>(x);
+        const int off0 = P.off(v0, c0) + y0 * kMS, off1 = P.off(v1, c1) + y1 * kMS;
+#pragma unroll
+        for (int q = 0; q < C; q++) {
+          const f2 o = x[q] * kLeeS[l][q];
+          if (ok0) S.co[off0 + q] = o.x;
+          if (ok1) S.co[off1 + q] = o.y;
+        }
+      } else {
+        float* x = buf[k];
+        lee<C>(x);
+        const int off0 = P.off(v0, c0) + y0 * kMS;
+#pragma unroll
+        for (int q = 0; q < C; q++) S.co[off0 + q] = x[q] * kLeeS[l][q];
+      }
     }
   }
 }
 
-// columns: R-point DCT of every column, in place (64-point: two lanes)
+// columns: R-point DCT of every column, in place.  A lane transforms the
+// columns X and X + 32 (X < 32) of one band of R rows and one channel (f2
+// lanes; any two columns of a band have the same length, whatever varblocks
+// they belong to): the two LDS reads of a pair are one ds_read2 and the 32
+// lanes of a band read 64 consecutive columns.  64-point: item = (pair, h).
 template <int R>
 __device__ void col_pass(const Pass& P, MergeLds& S) {
-  const int C = P.C(), ncols = 3 * P.NV() * C, lvc = P.lNV() + P.lC();
+  constexpr int lR = ilog2c<R>(), nb = 64 / R, lnb = 6 - lR;
+  constexpr int npairs = 3 * nb * 32;  // (channel, band, X)
+  const int lGX = P.lGX(), lC = P.lC();
+  auto col_of = [&](int pidx, int& off, bool& okA, bool& okB) {
+    const int X = pidx & 31, band = (pidx >> 5) & (nb - 1), c = pidx >> (5 + lnb);
+    off = c * kMPlane + band * R * kMS + X;
+    okA = S.valid[(band << lGX) | (X >> lC)];
+    okB = S.valid[(band << lGX) | ((X + 32) >> lC)];
+  };
   if constexpr (R == 64) {
-    const int n = 2 * ncols;
+    // 96 pairs x 2 halves; h wave-uniform (waves alternate h over 64 pairs)
+    constexpr int n = ((npairs + 63) >> 6) << 7;
     for (int i0 = 0; i0 < n; i0 += kMThreads) {
       const int i = i0 + threadIdx.x;
-      const int h = (i >> 6) & 1, r = ((i >> 7) << 6) | (i & 63);
-      const int c = min(r >> lvc, 2), v = (r >> P.lC()) & (P.NV() - 1), x = r & (C - 1);
-      const bool act = i < n && S.valid[v];
-      const int off = P.off(v, c) + x;
-      float o[32];
-      if (act) dct64_half(S.co + off, kMS, h, o);
+      const int h = (i >> 6) & 1, p = ((i >> 7) << 6) | (i & 63);
+      int off = 0;
+      bool okA = false, okB = false;
+      if (p < npairs) col_of(p, off, okA, okB);
+      const bool act = okA || okB;
+      f2 o[32];
+      if (act) {
+        const float* q0 = S.co + off;
+        f2 t[32];
+#pragma unroll
+        for (int j = 0; j < 32; j++)
+          t[j] = dct64_first(f2{q0[j * kMS], q0[j * kMS + 32]},
+                             f2{q0[(63 - j) * kMS], q0[(63 - j) * kMS + 32]}, j, h);
+        dct64_rest(t, h, [&](int k, f2 u) { o[k] = u; });
+      }
       __syncthreads();
       if (act) {
 #pragma unroll
-        for (int k = 0; k < 32; k++) S.co[off + (2 * k + h) * kMS] = o[k];
+        for (int k = 0; k < 32; k++) {
+          if (okA) S.co[off + (2 * k + h) * kMS] = o[k].x;
+          if (okB) S.co[off + 32 + (2 * k + h) * kMS] = o[k].y;
+        }
       }
     }
   } else {
-    for (int r = threadIdx.x; r < ncols; r += kMThreads) {
-      const int c = r >> lvc, v = (r >> P.lC()) & (P.NV() - 1), x = r & (C - 1);
-      if (!S.valid[v]) continue;
-      const int off = P.off(v, c) + x;
-      float o[R];
-      dct_from<R>(S.co + off, kMS, o);
+    for (int p = threadIdx.x; p < npairs; p += kMThreads) {
+      int off;
+      bool okA, okB;
+      col_of(p, off, okA, okB);
+      if (!okA && !okB) continue;
+      float* col = S.co + off;
+      f2 o[R];
 #pragma unroll
-      for (int k = 0; k < R; k++) S.co[off + k * kMS] = o[k];
+      for (int k = 0; k < R; k++) o[k] = f2{col[k * kMS], col[k * kMS + 32]};
+      lee<R>(o);
+#pragma unroll
+      for (int k = 0; k < R; k++) {
+        const f2 u = o[k] * kLeeS[lR][k];
+        if (okA) col[k * kMS] = u.x;
+        if (okB) col[k * kMS + 32] = u.y;
+      }
     }
   }
 }
@@ -291,27 +395,29 @@ __device__ __forceinline__ void load_f(const float* p, float* d) {
     d[4 * i + 3] = v.w;
   }
 }
-template <int RPC, bool WRITE>
-__device__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S, int phase) {
+template <int RPC, bool WRITE, int CH>
+__device__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S) {
   constexpr int STOT = kShapeOff[kNumShapes];
   constexpr int lper = RPC == 8 ? 9 : 8;  // items per channel: 512 (R = 8) or 256
+  constexpr int cidx = CH == 1 ? 0 : (CH == 0 ? 1 : 2);  // 0 Y, 1 X, 2 B
+  constexpr float kBias1 = 1.0f - 0.07005449891748593f;
   const int C = P.C(), NV = P.NV();
-  const int n = phase == 0 ? 1 << lper : 2 << lper;
-  for (int i = threadIdx.x; i < n; i += kMThreads) {
-    const int cidx = phase == 0 ? 0 : 1 + (i >> lper);  // 0 Y, 1 X, 2 B
-    const int c = cidx == 0 ? 1 : (cidx == 1 ? 0 : 2);
-    const int j = i & ((1 << lper) - 1);
+  for (int j = threadIdx.x; j < (1 << lper); j += kMThreads) {
     const int ch = j >> (P.lNV() + P.lC()), v = (j >> P.lC()) & (NV - 1), x = j & (C - 1);
     if (!S.valid[v]) continue;  // the varblock's C lanes leave together
     const int bx0 = P.bx0(v), by0 = P.by0(v);
     const float scale = (float)a.G * (float)S.vraw[v] / 65536.0f;
-    const float inv_scale = 1.0f / scale;
-    float* cplane = S.co + P.off(v, c) + x;
+    float* cplane = S.co + P.off(v, CH) + x;
     const float* yd = S.co + P.off(v, 1) + x;
     const int tcol = P.soff + x * P.R() + ch * RPC;  // column chunk in the tables
     float w[RPC], iw[RPC];
-    load_f<RPC>(a.wk + (size_t)c * STOT + tcol, w);
-    if (c == 1) load_f<RPC>(a.iwy + tcol, iw);
+    load_f<RPC>(a.wk + (size_t)CH * STOT + tcol, w);
+    if (CH == 1) {
+      load_f<RPC>(a.iwy + tcol, iw);
+      const float inv_scale = 1.0f / scale;
+#pragma unroll
+      for (int kk = 0; kk < RPC; kk++) iw[kk] = iw[kk] * inv_scale;
+    }
     uint16_t nat[RPC];
     if (WRITE) {
 #pragma unroll
@@ -322,44 +428,46 @@ __device__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S, int p
         for (int e = 0; e < 8; e++) nat[8 * q + e] = (uint16_t)(uw[e >> 1] >> ((e & 1) * 16));
       }
     }
+    // the LLF (first cy rows x cx columns) only occurs in chunk 0
+    const bool llf_col = ch == 0 && x < P.cx();
     float cp = 0.0f;
-    int bits = 0, nzc = 0;
+    int clzs = 0, nzc = 0;
 #pragma unroll
     for (int kk = 0; kk < RPC; kk++) {
       const int ky = ch * RPC + kk;
-      const bool is_llf = ky < P.cy() && x < P.cx();
+      const bool is_llf = llf_col && kk < P.cy();
       const float coef_v = cplane[ky * kMS];
-      int qq = 0;
-      if (!is_llf) {
-        const float ws = w[kk] * scale;
-        float rv = coef_v;
-        if (c == 2) rv = rv - yd[ky * kMS];
-        const float vq = rv * ws;
-        const float av = fabsf(vq);
-        const int qa = av < 0.58f ? 0 : (int)(fminf(av, 32767.0f) + 0.5f);
-        qq = vq < 0.0f ? -qa : qa;
-        if (c == 1) {
-          constexpr float kBias1 = 1.0f - 0.07005449891748593f;
-          const float bq = qa < 256 ? S.btab[qa] : 0.145f / (float)qa;
-          float adj = qa == 0 ? 0.0f : (qa == 1 ? kBias1 : (float)qa - bq);
-          if (vq < 0.0f) adj = -adj;
-          cplane[ky * kMS] = adj * (iw[kk] * inv_scale);
+      if (WRITE && is_llf) llf_at(S, CH, (by0 + ky) * 8 + bx0 + x) = coef_v;
+      float rv = coef_v;
+      if (CH == 2) rv = rv - yd[ky * kMS];
+      rv = is_llf ? 0.0f : rv;  // LLF: quantizes to 0, contributes nothing
+      const float vq = rv * (w[kk] * scale);
+      const float av = fabsf(vq);
+      const int qa = av < 0.58f ? 0 : (int)(fminf(av, 32767.0f) + 0.5f);
+      if (CH == 1) {
+        float bq = S.btab[min(qa, 255)];
+        if (__builtin_expect(__any(qa >= 256), 0)) {
+          if (qa >= 256) bq = 0.145f / (float)qa;
         }
-        const float e = av - (float)qa;
-        cp = fmaf(e, e, cp);
-        bits += qa ? 2 + 2 * bitlen_u((uint32_t)qa) : 0;
-        nzc += qa != 0;
-      } else if (WRITE) {
-        llf_at(S, c, (by0 + ky) * 8 + bx0 + x) = coef_v;
+        float adj = qa == 0 ? 0.0f : (qa == 1 ? kBias1 : (float)qa - bq);
+        if (vq < 0.0f) adj = -adj;
+        if (!is_llf) cplane[ky * kMS] = adj * iw[kk];
       }
+      const float e = av - (float)qa;
+      cp = fmaf(e, e, cp);
+      // 2 + 2 bitlen(qa) per non-zero: bitlen(qa) = 31 - clz(2 qa + 1)
+      clzs += (int)__clz((uint32_t)(2 * qa + 1));
+      nzc += qa != 0;
       if (WRITE) {
+        const int qq = vq < 0.0f ? -qa : qa;
         const int p = nat[kk];
         const int sl = p >> 6;
         const int lbx = bx0 + (sl & (P.cx() - 1)), lby = by0 + (sl >> P.lcx);
         const size_t gb = (size_t)(P.ty * 8 + lby) * a.bxs + P.tx * 8 + lbx;
-        a.ac[(gb * 3 + c) * 64 + (p & 63)] = (int16_t)qq;
+        a.ac[(gb * 3 + CH) * 64 + (p & 63)] = (int16_t)qq;
       }
     }
+    const int bits = 2 * nzc + 2 * (RPC * 31 - clzs);
     // the chunk's column partials, tree-summed over the varblock's C lanes
     // (an aligned group inside one wave); bits | non-zeros << 20 likewise
     int packed = bits | nzc << 20;
@@ -370,7 +478,7 @@ __device__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S, int p
     if (x == 0) {
       S.qsum[cidx][ch][v] = cp;
       if (packed & 0xFFFFF) atomicAdd(&S.vbits[v], packed & 0xFFFFF);
-      if (packed >> 20) atomicAdd(&S.vnz[v][c], packed >> 20);
+      if (packed >> 20) atomicAdd(&S.vnz[v][CH], packed >> 20);
     }
   }
 }
@@ -379,6 +487,10 @@ __device__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S, int p
 // bits / non-zeros and the chunk sums in LDS
 template <bool WRITE>
 __device__ void transform_quant(const MergeArgs& a, const Pass& P, MergeLds& S) {
+#ifdef JXG_MERGE_PROFILE
+  unsigned long long mprof_t0 = 0;
+#endif
+  MPROF_MARK(0);
   switch (P.lcx) {
     case 0: row_pass<8>(a, P, S); break;
     case 1: row_pass<16>(a, P, S); break;
@@ -386,6 +498,7 @@ __device__ void transform_quant(const MergeArgs& a, const Pass& P, MergeLds& S) 
     default: row_pass<64>(a, P, S); break;
   }
   __syncthreads();
+  MPROF_MARK(1);
   switch (P.lcy) {
     case 0: col_pass<8>(P, S); break;
     case 1: col_pass<16>(P, S); break;
@@ -393,11 +506,21 @@ __device__ void transform_quant(const MergeArgs& a, const Pass& P, MergeLds& S) 
     default: col_pass<64>(P, S); break;
   }
   __syncthreads();
-  for (int phase = 0; phase < 2; phase++) {
-    if (P.lcy == 0) quant_pass<8, WRITE>(a, P, S, phase);
-    else quant_pass<16, WRITE>(a, P, S, phase);
-    __syncthreads();
+  MPROF_MARK(2);
+  // Y first: its dequantized values replace its coefficients (B residual)
+  if (P.lcy == 0) quant_pass<8, WRITE, 1>(a, P, S);
+  else quant_pass<16, WRITE, 1>(a, P, S);
+  __syncthreads();
+  MPROF_MARK(3);
+  if (P.lcy == 0) {
+    quant_pass<8, WRITE, 0>(a, P, S);
+    quant_pass<8, WRITE, 2>(a, P, S);
+  } else {
+    quant_pass<16, WRITE, 0>(a, P, S);
+    quant_pass<16, WRITE, 2>(a, P, S);
   }
+  __syncthreads();
+  MPROF_MARK(4);
 }
 
 // distortion of varblock v: chunk sums in order per channel, (Y + X) + B
@@ -450,7 +573,7 @@ __device__ __forceinline__ void setup_varblocks(const MergeArgs& a, const Pass& 
   for (int i = t; i < 256; i += kMThreads) S.btab[i] = i < 2 ? 0.0f : 0.145f / (float)i;
 }
 // varblock quant field = max raw over its covered blocks (after a barrier)
-__device__ __forceinline__ void vraw_pass(const Pass& P, MergeLds& S) {
+__device__ __forceinline__ void vraw_pass(const MergeArgs& a, const Pass& P, MergeLds& S) {
   const int v = threadIdx.x;
   if (v < P.NV() && S.valid[v]) {
     const int bx0 = P.bx0(v), by0 = P.by0(v);
@@ -465,7 +588,8 @@ __device__ __forceinline__ int max_level(const MergeArgs& a) {
   return a.max_s >= 8 ? 3 : (a.max_s >= 4 ? 2 : 1);
 }
 
-__global__ __launch_bounds__(kMThreads) void merge_eval_kernel(MergeArgs a) {
+__global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(JXG_MERGE_WPE)))
+void merge_eval_kernel(MergeArgs a) {
   __shared__ __attribute__((aligned(16))) MergeLds S;
   int tile, si;
   if (!decode_wg(a, tile, si)) return;
@@ -475,7 +599,7 @@ __global__ __launch_bounds__(kMThreads) void merge_eval_kernel(MergeArgs a) {
   if ((1 << P.ls) > nbx || (1 << P.ls) > nby) return;  // no region of this level fits
   setup_varblocks<false>(a, P, S, nbx, nby);
   __syncthreads();
-  vraw_pass(P, S);
+  vraw_pass(a, P, S);
   transform_quant<false>(a, P, S);
   const int v = threadIdx.x;
   if (v < P.NV() && S.valid[v]) {
@@ -599,7 +723,7 @@ __device__ __forceinline__ void write_entry(const MergeArgs& a, int tile, int si
   const int nbx = min(8, (int)a.bxs - P.tx * 8), nby = min(8, (int)a.bys - P.ty * 8);
   setup_varblocks<true>(a, P, S, nbx, nby);
   __syncthreads();
-  vraw_pass(P, S);
+  vraw_pass(a, P, S);
   transform_quant<true>(a, P, S);
   // per covered block: non-zero counts, quant field, LLF-derived DC
   const int cb = P.cy() * P.cx(), lcb = P.lcy + P.lcx;
@@ -640,7 +764,8 @@ __device__ __forceinline__ void write_entry(const MergeArgs& a, int tile, int si
 
 // persistent workgroups over the (tile, shape) entries the resolve kernel
 // listed: only (tile, shape) pairs holding a chosen varblock cost anything
-__global__ __launch_bounds__(kMThreads) void merge_write_kernel(MergeArgs a) {
+__global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(JXG_MERGE_WPE)))
+void merge_write_kernel(MergeArgs a) {
   __shared__ __attribute__((aligned(16))) MergeLds S;
   const uint32_t n = __builtin_amdgcn_readfirstlane(*(volatile uint32_t*)a.work);
   for (uint32_t w = blockIdx.x; w < n; w += gridDim.x) {
@@ -689,6 +814,20 @@ __global__ __launch_bounds__(1024) void vb_list_kernel(VbArgs a) {
   }
   if (threadIdx.x == 0) a.count[lg] = sBase;
 }
+
+#ifdef JXG_MERGE_PROFILE
+void dump_merge_profile() {
+  unsigned long long h[16][8];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_mprof), sizeof(h)) != hipSuccess) return;
+  std::fprintf(stderr, "merge_eval cycles (thread 0 sums, Mcycles): shape rows cols quantY quantXB\n");
+  for (int si = 0; si < kNumShapes; si++)
+    std::fprintf(stderr, "  %dx%d %8.1f %8.1f %8.1f %8.1f\n", 8 << kShapes[si].lcy,
+                 8 << kShapes[si].lcx, h[si][1] / 1e6, h[si][2] / 1e6, h[si][3] / 1e6,
+                 h[si][4] / 1e6);
+}
+#else
+void dump_merge_profile() {}
+#endif
 
 void set_merge_constants(const float* llf_p, const float* llf_ib, hipStream_t s) {
   (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_llf_p), llf_p, sizeof(float) * 4 * 8, 0,

@@ -1,0 +1,15 @@
+#!/bin/bash
+# Same-box A/B of experiment builds: bash tools/ab.sh TAG name1 name2 ...
+# (tools/exp/libjxg_NAME.so; "prod" = the product libjxg.so), two rounds each.
+set -e
+export TMPDIR=/tmp
+TAG=$1; shift
+R=$PWD
+mkdir -p gpurun_out/$TAG
+for round in 1 2; do
+  for n in "$@"; do
+    if [ "$n" = prod ]; then L=$R/jpeg-xl-lossy-image-compression-thesis_amd/jxg/libjxg.so; else L=$R/tools/exp/libjxg_$n.so; fi
+    cd /tmp && JXG_LIB_PATH=$L timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/$TAG/${n}_$round -o run --output-format csv -- python3 $R/tools/mprof_run.py 8 > $R/gpurun_out/$TAG/${n}_$round.log 2>&1
+    cd $R
+  done
+done
