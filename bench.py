@@ -13,8 +13,11 @@ N > 1 (launched by torch.distributed.run, backend nccl = RCCL):
           (4320 N) pixels per step -- every rank owns 1/N of its 256x256 pass
           groups, i.e. one 8K frame's worth of work (weak scaling) -- with
           the real exchange: all-reduce of the AC histogram, all-gather of the
-          per-block DC/strategy records, gather of the section payloads and
-          assembly on rank 0.  The codestream is byte-identical to a
+          per-block DC/strategy records, then (--assembly host, default)
+          all-gather of the payload heads and every rank's D2H of its own
+          sections into one /dev/shm codestream buffer of the node (rank 0
+          writes headers + TOC), or (--assembly device) gather of the section
+          payloads and assembly on rank 0.  The codestream is byte-identical to a
           single-GPU encode of the same frame (tests/test_gpu_shard.py).
   replica -- every rank encodes its own 8K frame (frame-level data
           parallelism, no data-path collective).
@@ -101,6 +104,10 @@ def main():
     ap.add_argument("--effort", type=int, default=7)
     ap.add_argument("--proposals", type=int, default=0)
     ap.add_argument("--mode", choices=("shard", "replica"), default="shard")
+    ap.add_argument("--assembly", choices=("host", "device"), default="host",
+                    help="shard mode: host = every rank DMAs its sections into one /dev/shm "
+                         "buffer (rank 0 adds headers + TOC); device = payload gather to rank 0, "
+                         "device assembly, one D2H")
     ap.add_argument("--coder", choices=("prefix", "ans"), default="prefix",
                     help="AC entropy coder (libjxl codes with ANS at e7)")
     ap.add_argument("--streams", type=int, default=1,
@@ -146,11 +153,16 @@ def main():
                             proposals=args.proposals, device=local, flags=flags)
                 for _ in range(nstreams)]
         bufs = {}
+        host = None
+        if shard and args.assembly == "host":
+            from jxg.dist import SharedHostBuffer
+            host = SharedHostBuffer(rank, world)
 
         def step(e):
             if shard:
                 from jxg.dist import encode_sharded
-                return encode_sharded(e, d_img, w, fh, rank, world, bufs=bufs, copy=False)
+                return encode_sharded(e, d_img, w, fh, rank, world, bufs=bufs, copy=False,
+                                      host=host)
             return e.encode_device(d_img.data_ptr(), w, fh, copy=False)
 
         for e in encs:  # contexts warmed one after another
@@ -196,6 +208,9 @@ def main():
         rec["st"] = encs[0].stats()
         for e in encs:
             e.close()
+        if host is not None:
+            dist.barrier()
+            host.close()
         return rec
 
     nstreams = 1 if shard else max(1, args.streams)
@@ -225,9 +240,10 @@ def main():
         achieved = fb / (fms * 1e-3) / 1e9 if fms > 0 else 0.0
         if shard:
             workload = ("%s x%d: %dx%d RGB8 (synth_rgb8 8K frame stacked %d times), VarDCT d%g "
-                        "e%d, proposals=%d, %s-coded, 256x256 groups sharded over %d ranks"
+                        "e%d, proposals=%d, %s-coded, 256x256 groups sharded over %d ranks, "
+                        "%s assembly"
                         % (name, world, w, fh, world, args.distance, args.effort,
-                           args.proposals, args.coder, world))
+                           args.proposals, args.coder, world, args.assembly))
             par = "group-shard%d" % world
         else:
             workload = ("%s %dx%d RGB8 (synth_rgb8), VarDCT d%g e%d, proposals=%d, %s-coded, "

@@ -128,6 +128,23 @@ jxg_status jxg_shard_assemble_device(void* ctx, const void* d_payloads, const si
 jxg_status jxg_shard_assemble(const uint8_t* const* payloads, const size_t* sizes, uint32_t n,
                               jxg_buffer* out);
 
+/* Distributed host assembly (instead of the payload gather + rank-0
+ * assembly): after jxg_shard_end every rank exports its payload head
+ * (jxg_shard_head: a few hundred u32; dst NULL -> *nwords = size), the heads
+ * are all-gathered (any collective), and every rank calls
+ * jxg_shard_write_host with all heads in rank order: it writes its own
+ * sections D2H into `dst` -- one host buffer shared by all ranks (e.g. a
+ * /dev/shm mapping, registered with jxg_host_register for DMA) -- at their
+ * codestream offsets; rank 0 also writes headers + TOC.  *total = codestream
+ * bytes (also returned with JXG_ERR_INVALID_ARG when dst_size is too small).
+ * Once every rank has returned (a barrier), dst[0, total) holds the
+ * codestream, byte-identical to jxg_shard_assemble_device. */
+jxg_status jxg_shard_head(void* ctx, uint32_t* dst, size_t* nwords);
+jxg_status jxg_shard_write_host(void* ctx, const uint32_t* const* heads, const size_t* head_words,
+                                uint32_t n, void* dst, size_t dst_size, size_t* total);
+jxg_status jxg_host_register(void* ptr, size_t size);
+jxg_status jxg_host_unregister(void* ptr);
+
 /* thesis selector alone over a host XYB frame [3][ysize][xsize] (xsize, ysize
  * multiples of 8): r3 = (r_h, r_v, r_d) per block, type = raw strategy
  * (combined.diff:183-235) */

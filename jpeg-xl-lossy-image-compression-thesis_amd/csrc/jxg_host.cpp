@@ -1446,6 +1446,70 @@ static jxg_status shard_assemble_device(Ctx* c, const uint8_t* d_base, const siz
   return JXG_OK;
 }
 
+// Distributed host assembly: with every rank's payload head (host), each rank
+// writes its own sections straight from its device body into one host buffer
+// shared by all ranks (one D2H per contiguous run: its pass groups are one
+// run, its LF groups one each); rank 0 also writes headers + TOC.  Same bytes
+// as shard_assemble_device, without the payload gather and the serial D2H of
+// the whole codestream on rank 0.
+static jxg_status shard_write_host(Ctx* c, const uint32_t* const* heads_in, const size_t* words,
+                                   uint32_t n, uint8_t* dst, size_t dst_size, size_t* total) {
+  if (c->payload_head.size() < 7) return JXG_ERR_INVALID_ARG;
+  std::vector<std::vector<uint32_t>> heads(n);
+  std::vector<size_t> ps(n);
+  for (uint32_t i = 0; i < n; i++) {
+    if (!heads_in[i] || words[i] < 7) return JXG_ERR_INVALID_ARG;
+    heads[i].assign(heads_in[i], heads_in[i] + words[i]);
+    if (words[i] < 7 + 2 * (size_t)heads[i][6]) return JXG_ERR_INVALID_ARG;
+    size_t body = 0;
+    for (uint32_t k = 0; k < heads[i][6]; k++) body += heads[i][8 + 2 * k];
+    ps[i] = words[i] * 4 + body;
+  }
+  const uint32_t me = c->payload_head[2];
+  if (me >= n || heads[me] != c->payload_head) return JXG_ERR_INVALID_ARG;
+  uint32_t w = 0, h = 0;
+  std::vector<SectionRef> secs;
+  jxg_status st = parse_payload_heads(heads, ps, &w, &h, secs);
+  if (st) return st;
+  std::vector<uint32_t> sec_size(secs.size());
+  for (size_t i = 0; i < secs.size(); i++) sec_size[i] = secs[i].size;
+  BitWriter head;
+  write_headers(head, w, h);
+  write_toc(head, sec_size);
+  const std::vector<uint8_t> hb = head.bytes();
+  std::vector<uint64_t> out_off(secs.size());
+  uint64_t pos = hb.size();
+  for (size_t i = 0; i < secs.size(); i++) {
+    out_off[i] = pos;
+    pos += sec_size[i];
+  }
+  *total = (size_t)pos;
+  if (!dst || pos > dst_size) return JXG_ERR_INVALID_ARG;  // *total tells the size needed
+  hipStream_t s = c->stream;
+  const std::vector<uint32_t>& hw = c->payload_head;
+  uint64_t body = 0, run_src = 0, run_dst = 0, run_len = 0;
+  for (uint32_t k = 0; k < hw[6]; k++) {
+    const uint32_t id = hw[7 + 2 * k], sz = hw[8 + 2 * k];
+    if (run_len && run_src + run_len == body && run_dst + run_len == out_off[id]) {
+      run_len += sz;
+    } else {
+      if (run_len)
+        JXG_HIP(hipMemcpyAsync(dst + run_dst, reinterpret_cast<const uint8_t*>(c->out.p) + run_src,
+                               run_len, hipMemcpyDeviceToHost, s));
+      run_src = body;
+      run_dst = out_off[id];
+      run_len = sz;
+    }
+    body += sz;
+  }
+  if (run_len)
+    JXG_HIP(hipMemcpyAsync(dst + run_dst, reinterpret_cast<const uint8_t*>(c->out.p) + run_src,
+                           run_len, hipMemcpyDeviceToHost, s));
+  if (me == 0) std::memcpy(dst, hb.data(), hb.size());
+  JXG_HIP(hipStreamSynchronize(s));
+  return JXG_OK;
+}
+
 // host only: payloads of every rank -> codestream (same layout as
 // shard_assemble_device; no device needed)
 static jxg_status shard_assemble(const uint8_t* const* payloads, const size_t* sizes, uint32_t n,
@@ -1646,6 +1710,38 @@ jxg_status jxg_shard_assemble_device(void* ctx, const void* d_payloads, const si
   out->size = 0;
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
   return shard_assemble_device(c, static_cast<const uint8_t*>(d_payloads), offsets, sizes, n, out);
+}
+
+jxg_status jxg_shard_head(void* ctx, uint32_t* dst, size_t* nwords) {
+  if (!ctx || !nwords) return JXG_ERR_INVALID_ARG;
+  Ctx* c = static_cast<Ctx*>(ctx);
+  const size_t n = c->payload_head.size();
+  if (n == 0) return JXG_ERR_INVALID_ARG;
+  if (dst) {
+    if (*nwords < n) return JXG_ERR_INVALID_ARG;
+    std::memcpy(dst, c->payload_head.data(), n * 4);
+  }
+  *nwords = n;
+  return JXG_OK;
+}
+
+jxg_status jxg_shard_write_host(void* ctx, const uint32_t* const* heads, const size_t* head_words,
+                                uint32_t n, void* dst, size_t dst_size, size_t* total) {
+  if (!ctx || !heads || !head_words || !total || n == 0) return JXG_ERR_INVALID_ARG;
+  *total = 0;
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
+  return shard_write_host(c, heads, head_words, n, static_cast<uint8_t*>(dst), dst_size, total);
+}
+
+jxg_status jxg_host_register(void* ptr, size_t size) {
+  if (!ptr || size == 0) return JXG_ERR_INVALID_ARG;
+  return hipHostRegister(ptr, size, hipHostRegisterDefault) == hipSuccess ? JXG_OK : JXG_ERR_HIP;
+}
+
+jxg_status jxg_host_unregister(void* ptr) {
+  if (!ptr) return JXG_ERR_INVALID_ARG;
+  return hipHostUnregister(ptr) == hipSuccess ? JXG_OK : JXG_ERR_HIP;
 }
 
 jxg_status jxg_shard_assemble(const uint8_t* const* payloads, const size_t* sizes, uint32_t n,

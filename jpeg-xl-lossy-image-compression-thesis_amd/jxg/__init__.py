@@ -78,7 +78,8 @@ EXPORTS = ("jxg_status_str", "jxg_create", "jxg_destroy", "jxg_encode_rgb8",
            "jxg_encode_rgb8_device", "jxg_encode_batch_rgb8", "jxg_get_stats",
            "jxg_buffer_free", "jxg_homogeneity_map", "jxg_shard_sizes", "jxg_shard_begin",
            "jxg_shard_end", "jxg_shard_payload", "jxg_shard_assemble_device",
-           "jxg_shard_assemble", "jxg_compare_rgb8", "jxg_compare_rgb8_device")
+           "jxg_shard_assemble", "jxg_compare_rgb8", "jxg_compare_rgb8_device",
+           "jxg_shard_head", "jxg_shard_write_host", "jxg_host_register", "jxg_host_unregister")
 
 _lib = None
 
@@ -117,6 +118,11 @@ def load():
                                               ctypes.c_uint32, ctypes.POINTER(_Buffer)]
     lib.jxg_shard_assemble.argtypes = [ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)),
                                        ctypes.POINTER(sz), ctypes.c_uint32, ctypes.POINTER(_Buffer)]
+    lib.jxg_shard_head.argtypes = [vp, vp, ctypes.POINTER(sz)]
+    lib.jxg_shard_write_host.argtypes = [vp, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(sz),
+                                         ctypes.c_uint32, vp, sz, ctypes.POINTER(sz)]
+    lib.jxg_host_register.argtypes = [vp, sz]
+    lib.jxg_host_unregister.argtypes = [vp]
     cmp_args = [vp, vp, sz, vp, sz, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
                 ctypes.POINTER(_Quality)]
     lib.jxg_compare_rgb8.argtypes = cmp_args
@@ -270,6 +276,30 @@ class Encoder:
         _check(load().jxg_shard_assemble_device(self._ctx, ctypes.c_void_p(d_base), offs, szs, n,
                                                 ctypes.byref(buf)))
         return self._take(buf) if copy else Codestream(buf)
+
+    def shard_head(self) -> np.ndarray:
+        """This rank's payload head (u32 words) after shard_end."""
+        n = ctypes.c_size_t(0)
+        _check(load().jxg_shard_head(self._ctx, None, ctypes.byref(n)))
+        out = np.zeros(n.value, dtype=np.uint32)
+        _check(load().jxg_shard_head(self._ctx, out.ctypes.data, ctypes.byref(n)))
+        return out
+
+    def shard_write_host(self, heads, dst_ptr: int, dst_size: int):
+        """Write this rank's sections (and, on rank 0, headers + TOC) into the
+        shared host buffer at dst_ptr; returns (ok, total codestream bytes) --
+        ok False when dst_size < total (nothing written)."""
+        heads = [np.ascontiguousarray(h, dtype=np.uint32) for h in heads]
+        n = len(heads)
+        ptrs = (ctypes.c_void_p * n)(*[h.ctypes.data for h in heads])
+        words = (ctypes.c_size_t * n)(*[h.size for h in heads])
+        total = ctypes.c_size_t(0)
+        st = load().jxg_shard_write_host(self._ctx, ptrs, words, n, ctypes.c_void_p(dst_ptr),
+                                         dst_size, ctypes.byref(total))
+        if st == -1 and total.value > dst_size:
+            return False, total.value
+        _check(st)
+        return True, total.value
 
     def homogeneity_map(self, xyb: np.ndarray, distance: float, flags: int = 0):
         """Thesis selector over a (3, H, W) float32 XYB frame (H, W multiples of 8)."""

@@ -7,16 +7,101 @@ collectives are
      ranks derive the same prefix codes,
   2. all_gather of the per-block records (strategy, quant field, quantized DC;
      14 B per 8x8 block) that the LF-group streams of other ranks read,
-  3. a gather of the per-rank section payloads on rank 0, which writes the
-     headers and TOC (jxg_shard_assemble, host only).
+  3. assembly, either
+     host   (``host=SharedHostBuffer``): an all-gather of the payload heads
+            (section ids and sizes, ~2 KB per rank), then every rank DMAs its
+            own sections into one /dev/shm buffer shared by the node's ranks
+            at their codestream offsets (rank 0 adds headers + TOC) -- the
+            node's PCIe links work in parallel and nothing crosses xGMI; or
+     device (default): a gather of the per-rank section payloads on rank 0
+            (device to device), which writes headers + TOC and moves every
+            section with the concat kernel, then one D2H of the codestream.
 The result is byte-identical to a single-GPU encode of the same frame.
 """
 from __future__ import annotations
 
+import ctypes
+import mmap
+import os
+
+import numpy as np
 import torch
 import torch.distributed as dist
 
-from . import Encoder, shard_assemble, shard_sizes
+from . import Encoder, load, shard_assemble, shard_sizes
+
+
+class SharedHostBuffer:
+    """One host buffer mapped by every rank of a node (/dev/shm file, MAP_SHARED),
+    page-locked in each process (jxg_host_register) so the ranks' D2H copies
+    are DMA.  Grown collectively: every rank sees the same required size (it
+    follows from the all-gathered heads), so all re-map together."""
+
+    def __init__(self, rank: int, world: int, group=None):
+        self.rank, self.world, self.group = rank, world, group
+        tag = [os.getpid()] if rank == 0 else [None]
+        dist.broadcast_object_list(tag, src=0, group=group)
+        self.tag = tag[0]
+        self.gen = 0
+        self.cap = 0
+        self.mm = None
+        self.addr = 0
+        self.path = None
+
+    def _release(self):
+        if self.mm is not None:
+            load().jxg_host_unregister(ctypes.c_void_p(self.addr))
+            try:
+                self.mm.close()
+            except BufferError:  # a caller still holds a zero-copy view: GC unmaps later
+                pass
+            self.mm = None
+            if self.rank == 0 and self.path and os.path.exists(self.path):
+                os.unlink(self.path)
+
+    def ensure(self, need: int):
+        if need <= self.cap:
+            return
+        cap = max(need + (1 << 20), 2 * self.cap)
+        cap = (cap + (1 << 21) - 1) & ~((1 << 21) - 1)
+        dist.barrier(group=self.group)  # nobody still reads the old mapping
+        self._release()
+        self.gen += 1
+        self.path = "/dev/shm/jxg_cs_%d_%d" % (self.tag, self.gen)
+        if self.rank == 0:
+            fd = os.open(self.path, os.O_CREAT | os.O_RDWR | os.O_TRUNC, 0o600)
+            os.ftruncate(fd, cap)
+            os.close(fd)
+        dist.barrier(group=self.group)
+        fd = os.open(self.path, os.O_RDWR)
+        self.mm = mmap.mmap(fd, cap, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+        os.close(fd)
+        self.addr = ctypes.addressof(ctypes.c_char.from_buffer(self.mm))
+        if load().jxg_host_register(ctypes.c_void_p(self.addr), cap) != 0:
+            raise RuntimeError("jxg_host_register failed")
+        self.cap = cap
+
+    def view(self, n: int) -> np.ndarray:
+        return np.frombuffer(self.mm, dtype=np.uint8, count=n)
+
+    def close(self):
+        self._release()
+        self.cap = 0
+
+
+def _all_gather_heads(head: np.ndarray, rank: int, world: int, group=None):
+    """Variable-length u32 heads of all ranks (rank order), on every rank."""
+    dev = "cpu" if dist.get_backend(group) == "gloo" else torch.device("cuda", torch.cuda.current_device())
+    n = torch.tensor([head.size], dtype=torch.int64, device=dev)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n, group=group)
+    ns = [int(x.item()) for x in ns]
+    cap = max(ns)
+    mine = torch.zeros(cap, dtype=torch.int32, device=dev)
+    mine[:head.size] = torch.from_numpy(head.view(np.int32).copy()).to(dev)
+    parts = [torch.empty(cap, dtype=torch.int32, device=dev) for _ in range(world)]
+    dist.all_gather(parts, mine, group=group)
+    return [p[:k].cpu().numpy().view(np.uint32) for p, k in zip(parts, ns)]
 
 
 def gather_payloads(payload: bytes, rank: int, world: int, device, group=None):
@@ -39,11 +124,13 @@ def gather_payloads(payload: bytes, rank: int, world: int, device, group=None):
 
 
 def encode_sharded(enc: Encoder, d_rgb: torch.Tensor, width: int, height: int, rank: int,
-                   world: int, group=None, bufs=None, copy: bool = True):
+                   world: int, group=None, bufs=None, copy: bool = True,
+                   host: SharedHostBuffer | None = None):
     """Encode one frame (device-resident (H, W, 3) uint8 on every rank) with
-    group sharding; returns the codestream on rank 0 (bytes, or a
-    :class:`jxg.Codestream` view of pinned memory with copy=False), None
-    elsewhere.  `bufs` caches the exchange tensors across calls."""
+    group sharding; returns the codestream on rank 0 (bytes, or a zero-copy
+    view with copy=False: a :class:`jxg.Codestream` of pinned memory, or with
+    ``host`` a numpy view of the shared buffer), None elsewhere.  `bufs`
+    caches the exchange tensors across calls."""
     dev = d_rgb.device
     hist_words, slot = shard_sizes(width, height, world)
     if bufs is None:
@@ -73,6 +160,17 @@ def encode_sharded(enc: Encoder, d_rgb: torch.Tensor, width: int, height: int, r
         dist.all_gather_into_tensor(xbuf, mine.clone(), group=group)
     torch.cuda.synchronize(dev)  # the library's stream reads what the collectives wrote
     size = enc.shard_end(hist.data_ptr(), xbuf.data_ptr())
+    if host is not None:
+        heads = _all_gather_heads(enc.shard_head(), rank, world, group)
+        ok, total = enc.shard_write_host(heads, host.addr, host.cap)
+        if not ok:  # same `total` on every rank: all grow together
+            host.ensure(total)
+            ok, total = enc.shard_write_host(heads, host.addr, host.cap)
+        dist.barrier(group=group)  # every rank's sections are in place
+        if rank != 0:
+            return None
+        v = host.view(total)
+        return bytes(v) if copy else v
     if gloo:
         payloads = gather_payloads(enc.shard_payload_bytes(size), rank, world, "cpu", group)
         return shard_assemble(payloads) if rank == 0 else None

@@ -28,6 +28,17 @@ def sharded_encode(jxg_mod, img, world, d=1.0, e=7, p=0):
     for r in range(world):
         size = encs[r].shard_end(hist.data_ptr(), xbuf.data_ptr())
         payloads.append(encs[r].shard_payload_bytes(size))
+    # distributed host assembly: every "rank" writes its sections into one
+    # host buffer (first call with a too-small buffer reports the size)
+    heads = [e.shard_head() for e in encs]
+    ok, total = encs[0].shard_write_host(heads, 0, 0)
+    assert not ok and total > 0
+    hbuf = np.full(total + 7, 0xAB, dtype=np.uint8)
+    for r in range(world):
+        ok, t2 = encs[r].shard_write_host(heads, hbuf.ctypes.data, hbuf.size)
+        assert ok and t2 == total
+    host_written = hbuf[:total].tobytes()
+    assert (hbuf[total:] == 0xAB).all()
     # device assembly on "rank 0" from one buffer (word-aligned offsets)
     cap = (max(len(p) for p in payloads) + 15) // 16 * 16
     blob = np.zeros(world * cap + 64, dtype=np.uint8)
@@ -40,6 +51,7 @@ def sharded_encode(jxg_mod, img, world, d=1.0, e=7, p=0):
         enc.close()
     host_out = jxg_mod.shard_assemble(payloads)
     assert dev_out == host_out
+    assert host_written == host_out
     return dev_out
 
 
@@ -66,7 +78,7 @@ def test_sharded_8k_equals_single(jxg_mod):
     assert sharded_encode(jxg_mod, img, 8) == ref
 
 
-def _gloo_rank(rank, world, port, w, h, result):
+def _gloo_rank(rank, world, port, w, h, result, shm=False):
     import os
 
     import torch
@@ -77,23 +89,30 @@ def _gloo_rank(rank, world, port, w, h, result):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import jxg
-        from jxg.dist import encode_sharded
+        from jxg.dist import SharedHostBuffer, encode_sharded
         from jxg.synth import synth_rgb8
 
         img = synth_rgb8(w, h, 5)
         t = torch.from_numpy(img).cuda()
+        host = SharedHostBuffer(rank, world) if shm else None
         with jxg.Encoder(distance=1.0, effort=7) as enc:
-            out = encode_sharded(enc, t, w, h, rank, world)
+            out = encode_sharded(enc, t, w, h, rank, world, host=host)
+            out2 = encode_sharded(enc, t, w, h, rank, world, host=host)  # buffer reuse
             if rank == 0:
                 ref = enc.encode(img)
-                result.put(out == ref)
+                result.put(out == ref and out2 == ref)
+        if host is not None:
+            dist.barrier()
+            host.close()
     finally:
         dist.destroy_process_group()
 
 
-def test_multiprocess_encode_sharded(jxg_mod):
+@pytest.mark.parametrize("shm", [False, True])
+def test_multiprocess_encode_sharded(jxg_mod, shm):
     """jxg.dist.encode_sharded in 2 processes (gloo, both ranks on cuda:0):
-    the multi-process orchestration bench.py --gpus N runs over RCCL."""
+    the multi-process orchestration bench.py --gpus N runs over RCCL; shm:
+    the distributed host assembly into a /dev/shm buffer."""
     import socket
 
     import torch.multiprocessing as mp
@@ -103,7 +122,8 @@ def test_multiprocess_encode_sharded(jxg_mod):
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_gloo_rank, args=(r, 2, port, 1100, 700, q)) for r in range(2)]
+    procs = [ctx.Process(target=_gloo_rank, args=(r, 2, port, 1100, 700, q, shm))
+             for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
