@@ -12,13 +12,17 @@
 // every slice of a 64x64 varblock is walked in parallel.
 //   ac_hist : non-zero counts -> predicted-nz + zero-density contexts ->
 //             clustered histograms (LDS, one global atomic per non-empty bin),
-//             exact per-group token counts, per-group bit upper bound.
-//   ac_emit : same walk with the prefix codes (LDS table): per-task bit
-//             lengths -> workgroup exclusive scan over varblocks (stream
-//             order: varblocks by first block raster, channels Y, X, B,
-//             slices) -> every task writes its bits into an LDS bit buffer
-//             (ds_or), copied out with plain 4-byte stores (global atomics
-//             only for groups larger than the buffer).
+//             exact per-group token counts, per-group bit upper bound; then a
+//             workgroup scan over varblocks (stream order: varblocks by first
+//             block raster, channels Y, X, B, slices) and a second walk that
+//             writes every token as a 32-bit record (cluster | token << 8 |
+//             raw-bit count << 14 | raw bits << 18) at its stream position.
+//   ac_emit : prefix codes from the records alone (no coefficient walk):
+//             a contiguous record range per wave, coalesced reads, wave scans
+//             of the code lengths -> LDS bit buffer (ds_or), copied out with
+//             plain 4-byte stores (global atomics only for groups larger than
+//             the buffer).
+//   ans_*   : the rANS coder over the same records.
 // Token order / contexts are those of oracle/encode.c group_tokens, [ext]
 // libjxl dec_group DecodeACVarBlock.
 #include "jxg_device.h"
@@ -196,7 +200,31 @@ struct AcLds {
   uint8_t nz[3][1024];   // predicted-nz image (scaled per covered block)
   uint8_t snz[3][1024];  // non-zeros of each slice (positions >= cb)
   uint8_t last[3][1024]; // last coefficient of the slice != 0
+  int8_t lastk[3][1024]; // highest slice-local index >= cb - 64 sl holding a non-zero, or -1
 };
+
+// tokens of task (t, c) without walking it: the walk runs from the slice's
+// first position >= cb up to the varblock's last non-zero K (1 + K for an
+// 8x8-class block), plus the non-zero count token on slice 0
+__device__ __forceinline__ uint32_t task_token_count(const AcArgs& a, const SliceTask& t,
+                                                     const AcLds& L, int c) {
+  if (t.lcb == 0) {
+    uint32_t w[32];
+    load_coefs(a.ac + (t.gb * 3 + c) * 64, w);
+    int last = 0;
+#pragma unroll
+    for (int kk = 1; kk < 64; kk++) last = coef(w, kk) != 0 ? kk : last;
+    return 1u + (uint32_t)last;
+  }
+  const int cb = 1 << t.lcb;
+  int K = -1;
+  for (int j = 0; j < cb; j++) {
+    const int lk = L.lastk[c][block_of_slice(t, j)];
+    K = lk >= 0 ? j * 64 + lk : K;
+  }
+  const int lo = max(t.sl * 64, cb), hi = min(t.sl * 64 + 63, K);
+  return (t.sl == 0 ? 1u : 0u) + (hi >= lo ? (uint32_t)(hi - lo + 1) : 0u);
+}
 
 // predicted-nz image and per-slice non-zero counts of the group
 __device__ __forceinline__ void fill_slices(const AcArgs& a, const GroupGeom& G,
@@ -218,11 +246,16 @@ __device__ __forceinline__ void fill_slices(const AcArgs& a, const GroupGeom& G,
     for (int c = 0; c < 3; c++) {
       uint32_t w[32];
       load_coefs(a.ac + (t.gb * 3 + c) * 64, w);
-      int n = 0;
+      int n = 0, lk = -1;
 #pragma unroll
-      for (int kk = 0; kk < 64; kk++) n += (t.sl * 64 + kk >= cb) && coef(w, kk) != 0;
+      for (int kk = 0; kk < 64; kk++) {
+        const bool on = (t.sl * 64 + kk >= cb) && coef(w, kk) != 0;
+        n += on;
+        lk = on ? kk : lk;
+      }
       L.snz[c][t.by * 32 + t.bx] = (uint8_t)n;
       L.last[c][t.by * 32 + t.bx] = coef(w, 63) != 0;
+      L.lastk[c][t.by * 32 + t.bx] = (int8_t)lk;
     }
   }
 }
@@ -283,6 +316,9 @@ __global__ __launch_bounds__(kAcThreads) void ac_hist_kernel(AcArgs a) {
   __shared__ uint32_t sHist[kMaxClusters * kAcTok];
   __shared__ AcLds L;
   __shared__ uint8_t sClu[kAcCtx];
+  __shared__ uint32_t sTask[3][1024];  // tokens per (channel, slice task)
+  __shared__ uint32_t sBase[1024];     // first token of each varblock (first block)
+  __shared__ uint32_t sWave[kAcThreads / 64];
   __shared__ uint32_t sBound, sNtok[3];
   const int g = blockIdx.x + (int)a.g0;
   const GroupGeom G = group_geom(a, g);
@@ -293,22 +329,53 @@ __global__ __launch_bounds__(kAcThreads) void ac_hist_kernel(AcArgs a) {
   const SliceTask t = slice_task(a, G);
   fill_slices(a, G, t, L);
   __syncthreads();
+  const int me = t.by * 32 + t.bx;
+  // token counts per task without a walk -> stream positions (varblocks by
+  // first block raster, channels Y, X, B, slices): one scan over varblocks
+  if (t.valid) {
+#pragma unroll 1
+    for (int ci = 0; ci < 3; ci++) sTask[ci][me] = task_token_count(a, t, L, channel_of(ci));
+  }
+  __syncthreads();
+  uint32_t vtot = 0;
+  const int cb = 1 << t.lcb;
+  if (t.valid && t.sl == 0) {
+    for (int ci = 0; ci < 3; ci++)
+      for (int j = 0; j < cb; j++) vtot += sTask[ci][block_of_slice(t, j)];
+  }
+  uint32_t total;
+  const uint32_t off = block_excl_scan1024(vtot, sWave, &total);
+  if (t.valid && t.sl == 0) sBase[me] = off;
+  __syncthreads();
+  // one walk: clustered histogram, bit bound, and every token's 32-bit record
+  // at its stream position
   uint32_t bound = 0, nt[3] = {0, 0, 0};
   if (t.valid) {
+    uint32_t pos = sBase[t.oby * 32 + t.obx];
+    uint32_t* rec = a.tokens + (uint64_t)(g - (int)a.g0) * kGroupTokStride;
 #pragma unroll 1
     for (int ci = 0; ci < 3; ci++) {
       const int c = channel_of(ci);
-      uint32_t cnt = 0;
+      uint32_t before = 0, chan_total = 0;
+      for (int j = 0; j < cb; j++) {
+        const uint32_t b = sTask[ci][block_of_slice(t, j)];
+        before += j < t.sl ? b : 0u;
+        chan_total += b;
+      }
+      uint32_t idx = pos + before;
       task_tokens(a, t, L, c, [&](int ctx, uint32_t v) {
         uint32_t tok, nb, bits;
         hybrid420(v, tok, nb, bits);
-        atomicAdd(&sHist[sClu[ctx] * kAcTok + tok], 1u);
+        const uint32_t clu = sClu[ctx];
+        atomicAdd(&sHist[clu * kAcTok + tok], 1u);
         bound += 15u + nb;
-        cnt++;
+        rec[idx++] = clu | (tok << 8) | (nb << 14) | (bits << 18);
       });
+      const uint32_t cnt = sTask[ci][me];
       nt[0] += c == 0 ? cnt : 0u;
       nt[1] += c == 1 ? cnt : 0u;
       nt[2] += c == 2 ? cnt : 0u;
+      pos += chan_total;
     }
   }
   atomicAdd(&sBound, bound);
@@ -326,77 +393,75 @@ __global__ __launch_bounds__(kAcThreads) void ac_hist_kernel(AcArgs a) {
   }
 }
 
+// prefix-code emission from the group's token records (no coefficient walk):
+// wave w owns a contiguous record range; lanes read consecutive records
+// (coalesced), the wave's bit total -> workgroup offsets; then per 64
+// records a wave inclusive scan of the lengths gives every record its bit
+// position, and each lane ORs its <= 28 bits into the LDS bit buffer (global
+// atomics for groups larger than the buffer)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t t = __shfl_up(v, d);
+    if (lane >= d) v += t;
+  }
+  return v;
+}
 __global__ __launch_bounds__(kAcThreads) void ac_emit_kernel(AcArgs a) {
   __shared__ uint32_t sCode[kMaxClusters * kAcTok];
   __shared__ uint32_t sBits[kEmitLdsWords];
-  __shared__ AcLds L;
-  __shared__ uint32_t sTask[3][1024];  // exact bits per (channel, slice task)
-  __shared__ uint32_t sBase[1024];     // bit offset of each varblock (first block)
-  __shared__ uint8_t sClu[kAcCtx];
   __shared__ uint32_t sWave[kAcThreads / 64];
   const int g = blockIdx.x + (int)a.g0;
-  const GroupGeom G = group_geom(a, g);
-  for (int i = threadIdx.x; i < kAcCtx; i += blockDim.x) sClu[i] = c_cluster[i];
   for (int i = threadIdx.x; i < kMaxClusters * kAcTok; i += blockDim.x)
     sCode[i] = a.codes[(i / kAcTok) * kAlpha + (i % kAcTok)];
   for (int i = threadIdx.x; i < kEmitLdsWords; i += blockDim.x) sBits[i] = 0;
-  const SliceTask t = slice_task(a, G);
-  fill_slices(a, G, t, L);
+  const uint32_t n = a.ntok[g * 3] + a.ntok[g * 3 + 1] + a.ntok[g * 3 + 2];
+  const uint32_t* rec = a.tokens + (uint64_t)(g - (int)a.g0) * kGroupTokStride;
+  constexpr int kWaves = kAcThreads / 64;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t chunk = ((n + kWaves * 64 - 1) / (kWaves * 64)) * 64;
+  const uint32_t lo = min(n, wv * chunk), hi = min(n, lo + chunk);
   __syncthreads();
-  const int me = t.by * 32 + t.bx;
-  // pass 1: exact bits of this thread's three tasks
-  if (t.valid) {
-#pragma unroll 1
-    for (int ci = 0; ci < 3; ci++) {
-      uint32_t tot = 0;
-      task_tokens(a, t, L, channel_of(ci), [&](int ctx, uint32_t v) {
-        uint32_t tok, nb, bits;
-        hybrid420(v, tok, nb, bits);
-        tot += (sCode[sClu[ctx] * kAcTok + tok] >> 16) + nb;
-      });
-      sTask[ci][me] = tot;
-    }
+  auto code_of = [&](uint32_t r) { return sCode[(r & 0xFF) * kAcTok + ((r >> 8) & 63)]; };
+  uint32_t tot = 0;
+  for (uint32_t k = lo + lane; k < hi; k += 64) {
+    const uint32_t r = rec[k];
+    tot += (code_of(r) >> 16) + ((r >> 14) & 15);
   }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) tot += __shfl_xor(tot, d, 64);
+  if (lane == 0) sWave[wv] = tot;
   __syncthreads();
-  // varblock totals at first blocks, scanned in thread (= first-block raster) order
-  uint32_t vtot = 0;
-  const int cb = 1 << t.lcb;
-  if (t.valid && t.sl == 0) {
-    for (int ci = 0; ci < 3; ci++)
-      for (int j = 0; j < cb; j++) vtot += sTask[ci][block_of_slice(t, j)];
+  uint32_t run = 0, total = 0;
+#pragma unroll
+  for (int i = 0; i < kWaves; i++) {
+    const uint32_t x = sWave[i];
+    run += i < wv ? x : 0u;
+    total += x;
   }
-  uint32_t total;
-  const uint32_t off = block_excl_scan1024(vtot, sWave, &total);
-  if (t.valid && t.sl == 0) sBase[me] = off;
-  __syncthreads();
-  // pass 2: emission (LDS bit buffer when the group fits, else global atomics)
   const uint64_t base = a.base[g];  // word aligned
   const bool lds = total <= (uint32_t)kEmitLdsWords * 32u;
-  if (t.valid) {
-    uint32_t pos = sBase[t.oby * 32 + t.obx];
-#pragma unroll 1
-    for (int ci = 0; ci < 3; ci++) {
-      uint32_t before = 0, chan_total = 0;
-      for (int j = 0; j < cb; j++) {
-        const uint32_t b = sTask[ci][block_of_slice(t, j)];
-        before += j < t.sl ? b : 0u;
-        chan_total += b;
-      }
-      const uint32_t start = pos + before;
-      if (sTask[ci][me]) {
-        BitSink s = lds ? BitSink{sBits, start, 0, 0} : BitSink{a.scratch, base + start, 0, 0};
-        const uint32_t* code = sCode;
-        task_tokens(a, t, L, channel_of(ci), [&](int ctx, uint32_t v) {
-          uint32_t tok, nb, bits;
-          hybrid420(v, tok, nb, bits);
-          const uint32_t cl = code[sClu[ctx] * kAcTok + tok];
-          // code (<= 15 bits) and raw bits (<= 13) in one put
-          s.put((cl >> 16) + nb, (cl & 0xFFFFu) | (bits << (cl >> 16)));
-        });
-        s.finish();
-      }
-      pos += chan_total;
+  uint32_t* buf = lds ? sBits : a.scratch;
+  const uint64_t bias = lds ? 0 : base;
+  for (uint32_t k0 = lo; k0 < hi; k0 += 64) {
+    const uint32_t k = k0 + lane;
+    uint32_t len = 0, val = 0;
+    if (k < hi) {
+      const uint32_t r = rec[k], cl = code_of(r);
+      len = (cl >> 16) + ((r >> 14) & 15);
+      // code (<= 15 bits) and raw bits (<= 13): one <= 28-bit value
+      val = (cl & 0xFFFFu) | ((r >> 18) << (cl >> 16));
     }
+    const uint32_t incl = wave_incl_scan(len);
+    if (len) {
+      const uint64_t pos = bias + run + incl - len;
+      const uint64_t w = pos >> 5;
+      const uint32_t sh = (uint32_t)(pos & 31);
+      atomicOr(&buf[w], val << sh);
+      if (sh + len > 32) atomicOr(&buf[w + 1], val >> (32 - sh));
+    }
+    run += __shfl(incl, 63, 64);
   }
   if (lds) {
     __syncthreads();
@@ -409,65 +474,11 @@ __global__ __launch_bounds__(kAcThreads) void ac_emit_kernel(AcArgs a) {
 
 // groups [a.g0, a.g0 + ngroups)
 // ---------------------------------------------------------------------------
-// ANS: token records in stream order (same task scan as ac_emit), then one
-// lane per group runs the rANS encoder backwards over its records (the
-// stream's only sequential dependency), then the group's workgroup places
-// the emitted bits in parallel.
+// ANS: the token records ac_hist wrote in stream order; one lane per group
+// runs the rANS encoder backwards over its records (the stream's only
+// sequential dependency), then the group's workgroup places the emitted bits
+// in parallel.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kAcThreads) void ac_tokens_kernel(AcArgs a) {
-  __shared__ AcLds L;
-  __shared__ uint32_t sTask[3][1024];  // tokens per (channel, slice task)
-  __shared__ uint32_t sBase[1024];     // first token of each varblock (first block)
-  __shared__ uint8_t sClu[kAcCtx];
-  __shared__ uint32_t sWave[kAcThreads / 64];
-  const int g = blockIdx.x + (int)a.g0;
-  const GroupGeom G = group_geom(a, g);
-  for (int i = threadIdx.x; i < kAcCtx; i += blockDim.x) sClu[i] = c_cluster[i];
-  const SliceTask t = slice_task(a, G);
-  fill_slices(a, G, t, L);
-  __syncthreads();
-  const int me = t.by * 32 + t.bx;
-  if (t.valid) {
-#pragma unroll 1
-    for (int ci = 0; ci < 3; ci++) {
-      uint32_t cnt = 0;
-      task_tokens(a, t, L, channel_of(ci), [&](int, uint32_t) { cnt++; });
-      sTask[ci][me] = cnt;
-    }
-  }
-  __syncthreads();
-  uint32_t vtot = 0;
-  const int cb = 1 << t.lcb;
-  if (t.valid && t.sl == 0) {
-    for (int ci = 0; ci < 3; ci++)
-      for (int j = 0; j < cb; j++) vtot += sTask[ci][block_of_slice(t, j)];
-  }
-  uint32_t total;
-  const uint32_t off = block_excl_scan1024(vtot, sWave, &total);
-  if (t.valid && t.sl == 0) sBase[me] = off;
-  __syncthreads();
-  if (t.valid) {
-    uint32_t pos = sBase[t.oby * 32 + t.obx];
-    uint32_t* rec = a.tokens + a.tbase[g];
-#pragma unroll 1
-    for (int ci = 0; ci < 3; ci++) {
-      uint32_t before = 0, chan_total = 0;
-      for (int j = 0; j < cb; j++) {
-        const uint32_t b = sTask[ci][block_of_slice(t, j)];
-        before += j < t.sl ? b : 0u;
-        chan_total += b;
-      }
-      uint32_t idx = pos + before;
-      task_tokens(a, t, L, channel_of(ci), [&](int ctx, uint32_t v) {
-        uint32_t tok, nb, bits;
-        hybrid420(v, tok, nb, bits);
-        rec[idx++] = (uint32_t)sClu[ctx] | (tok << 8) | (nb << 14) | (bits << 18);
-      });
-      pos += chan_total;
-    }
-  }
-}
-
 // rANS backwards over each group's records, one wave per group, 4 groups per
 // workgroup sharing the LDS tables (all alias inverses, 128 KB).  The state
 // recurrence is a uniform chain kept in VALU registers (a microbenchmark on
@@ -498,7 +509,7 @@ __global__ __launch_bounds__(kAnsWaves * 64) void ans_encode_kernel(AnsArgs a) {
       __builtin_amdgcn_readfirstlane(a.g0 + blockIdx.x * kAnsWaves + (threadIdx.x >> 6));
   if (g >= a.g1) return;
   const int n = (int)(a.ntok[g * 3] + a.ntok[g * 3 + 1] + a.ntok[g * 3 + 2]);
-  const uint64_t b = a.tbase[g];
+  const uint64_t b = (uint64_t)(g - a.g0) * kGroupTokStride;
   uint32_t x = 0x130000u;
   uint32_t rec = (int)lane < min(64, n) ? a.tokens[b + n - 1 - lane] : 0u;
   for (int hi = n; hi > 0; hi -= 64) {
@@ -558,31 +569,55 @@ __global__ __launch_bounds__(kAnsWaves * 64) void ans_encode_kernel(AnsArgs a) {
   if (lane == 0) a.state[g] = __builtin_amdgcn_readfirstlane(x);
 }
 
-// bit placement: the 32-bit state, then every record's bits, in order;
-// 1024 threads per group, contiguous record ranges, one scan
+// bit placement: the 32-bit state, then every record's bits, in order; a
+// contiguous record range per wave, coalesced reads, wave scans of the
+// lengths (as ac_emit)
 __global__ __launch_bounds__(kAcThreads) void ans_emit_kernel(AnsArgs a) {
   __shared__ uint32_t sBits[kEmitLdsWords];
   __shared__ uint32_t sWave[kAcThreads / 64];
   const uint32_t g = a.g0 + blockIdx.x;
   const uint32_t n = a.ntok[g * 3] + a.ntok[g * 3 + 1] + a.ntok[g * 3 + 2];
-  const uint64_t b = a.tbase[g];
+  const uint64_t b = (uint64_t)(g - a.g0) * kGroupTokStride;
   for (int i = threadIdx.x; i < kEmitLdsWords; i += blockDim.x) sBits[i] = 0;
-  const uint32_t per = (n + kAcThreads - 1) / kAcThreads;
-  const uint32_t k0 = min(n, threadIdx.x * per), k1 = min(n, k0 + per);
+  constexpr int kWaves = kAcThreads / 64;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t chunk = ((n + kWaves * 64 - 1) / (kWaves * 64)) * 64;
+  const uint32_t lo = min(n, wv * chunk), hi = min(n, lo + chunk);
   uint32_t tot = 0;
-  for (uint32_t k = k0; k < k1; k++) tot += a.len[b + k];
-  uint32_t total;
-  const uint32_t off = 32 + block_excl_scan1024(tot, sWave, &total);
-  total += 32;
+  for (uint32_t k = lo + lane; k < hi; k += 64) tot += a.len[b + k];
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) tot += __shfl_xor(tot, d, 64);
+  if (lane == 0) sWave[wv] = tot;
+  __syncthreads();
+  uint32_t run = 32, total = 32;  // the state comes first
+#pragma unroll
+  for (int i = 0; i < kWaves; i++) {
+    const uint32_t x = sWave[i];
+    run += i < wv ? x : 0u;
+    total += x;
+  }
   const uint64_t base = a.base[g];
   const bool lds = total <= (uint32_t)kEmitLdsWords * 32u;
-  BitSink s = lds ? BitSink{sBits, off, 0, 0} : BitSink{a.scratch, base + off, 0, 0};
-  for (uint32_t k = k0; k < k1; k++) s.put(a.len[b + k], a.val[b + k]);
-  s.finish();
+  uint32_t* buf = lds ? sBits : a.scratch;
+  const uint64_t bias = lds ? 0 : base;
   if (threadIdx.x == 0) {
-    BitSink h = lds ? BitSink{sBits, 0, 0, 0} : BitSink{a.scratch, base, 0, 0};
-    h.put(32, a.state[g]);
-    h.finish();
+    // base is word aligned: the state is word 0
+    if (lds) sBits[0] = a.state[g];
+    else a.scratch[base >> 5] = a.state[g];
+  }
+  for (uint32_t k0 = lo; k0 < hi; k0 += 64) {
+    const uint32_t k = k0 + lane;
+    const uint32_t len = k < hi ? a.len[b + k] : 0u;
+    const uint32_t val = k < hi ? a.val[b + k] : 0u;
+    const uint32_t incl = wave_incl_scan(len);
+    if (len) {
+      const uint64_t pos = bias + run + incl - len;
+      const uint64_t w = pos >> 5;
+      const uint32_t sh = (uint32_t)(pos & 31);
+      atomicOr(&buf[w], val << sh);
+      if (sh + len > 32) atomicOr(&buf[w + 1], val >> (32 - sh));
+    }
+    run += __shfl(incl, 63, 64);
   }
   if (lds) {
     __syncthreads();
@@ -593,9 +628,6 @@ __global__ __launch_bounds__(kAcThreads) void ans_emit_kernel(AnsArgs a) {
   if (threadIdx.x == 0) a.bits[g] = total;
 }
 
-void launch_ac_tokens(const AcArgs& a, uint32_t ngroups, hipStream_t s) {
-  if (ngroups) hipLaunchKernelGGL(ac_tokens_kernel, dim3(ngroups), dim3(kAcThreads), 0, s, a);
-}
 void launch_ans(const AnsArgs& a, hipStream_t s) {
   const uint32_t n = a.g1 - a.g0;
   if (!n) return;

@@ -422,7 +422,6 @@ struct Ctx {
   DevBuf<uint32_t> tile_list;
   DevBuf<uint32_t> tokens, tval, ans_state;  // ANS coder
   DevBuf<uint8_t> tlen;
-  DevBuf<uint64_t> tbase;
   DevBuf<uint8_t> ans_tab;
   PinBuf<uint8_t> h_ans_tab;
   DevBuf<LfRow> rows;
@@ -575,7 +574,7 @@ struct Job {
   // host stage results
   std::vector<BitWriter> preA, preB;
   BitWriter lfglobal, hfglobal;
-  std::vector<uint64_t> gbase, sbase, tbase;
+  std::vector<uint64_t> gbase, sbase;
   float ms_codes = 0.0f;
 };
 
@@ -673,6 +672,8 @@ static jxg_status stage_alloc(Ctx* c, Job& J) {
   aa.codes = c->codes_ac.p;
   aa.base = c->gbase.p;
   aa.bits = c->gbits.p;
+  JXG_HIP(c->tokens.ensure((uint64_t)(J.plan.g1 - J.plan.g0) * kGroupTokStride));
+  aa.tokens = c->tokens.p;
   LfArgs& la = J.la;
   la = LfArgs{};
   la.rows = c->rows.p;
@@ -951,16 +952,12 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
   J.gbase.assign(f.ngroups, 0);
   J.sbase.assign(nstreams, 0);
   uint64_t cursor = 0;
-  J.tbase.assign(f.ngroups, 0);
-  uint64_t ntokens = 0;
   for (uint32_t g = J.plan.g0; g < J.plan.g1; g++) {
     J.gbase[g] = cursor;
     const uint64_t nt = (uint64_t)c->h_ntok.p[g * 3] + c->h_ntok.p[g * 3 + 1] + c->h_ntok.p[g * 3 + 2];
     // ANS: <= 16 + raw bits per token (prefix: <= 15 + raw) and the 32-bit state
     const uint64_t bound = (uint64_t)c->h_bound.p[g] + (J.ans ? nt + 32 : 0);
     cursor += (bound + 63) & ~31ull;
-    J.tbase[g] = ntokens;
-    ntokens += nt;
   }
   for (uint32_t i = 0; i < nstreams; i++) {
     J.sbase[i] = cursor;
@@ -970,13 +967,11 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
   J.ms_codes = ms_since(t_codes);
   JXG_HIP(c->scratch.ensure(scratch_words));
   if (J.ans) {
-    JXG_HIP(c->tokens.ensure(ntokens));
-    JXG_HIP(c->tval.ensure(ntokens));
-    JXG_HIP(c->tlen.ensure(ntokens));
-    JXG_HIP(c->tbase.ensure(f.ngroups));
+    const uint64_t nrec = (uint64_t)(J.plan.g1 - J.plan.g0) * kGroupTokStride;
+    JXG_HIP(c->tval.ensure(nrec));
+    JXG_HIP(c->tlen.ensure(nrec));
     JXG_HIP(c->ans_state.ensure(f.ngroups));
     JXG_HIP(c->ans_tab.ensure(kAnsTabBytes));
-    JXG_HIP(hipMemcpyAsync(c->tbase.p, J.tbase.data(), J.tbase.size() * 8, hipMemcpyHostToDevice, s));
     // pinned source: stays valid until the next frame's stage_codes, which
     // runs after this frame's emission has completed
     JXG_HIP(hipMemcpyAsync(c->ans_tab.p, c->h_ans_tab.p, kAnsTabBytes, hipMemcpyHostToDevice, s));
@@ -996,14 +991,10 @@ static jxg_status stage_emit(Ctx* c, Job& J) {
   J.aa.scratch = c->scratch.p;
   J.la.scratch = c->scratch.p;
   if (J.ans) {
-    J.aa.tokens = c->tokens.p;
-    J.aa.tbase = c->tbase.p;
-    launch_ac_tokens(J.aa, J.plan.g1 - J.plan.g0, s);
     AnsArgs na{};
     na.tokens = c->tokens.p;
     na.val = c->tval.p;
     na.len = c->tlen.p;
-    na.tbase = c->tbase.p;
     na.ntok = c->ntok.p;
     na.tab = c->ans_tab.p;
     na.nhist = J.nhist_ans;

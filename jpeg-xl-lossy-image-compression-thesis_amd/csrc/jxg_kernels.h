@@ -93,9 +93,11 @@ struct AcArgs {
   const uint64_t* base;  // [ngroups] scratch bit offset (emit pass)
   uint32_t* scratch;     // bit buffer (emit pass, zeroed)
   uint32_t* bits;        // [ngroups] exact bits (emit pass)
-  uint32_t* tokens;      // ANS: token records (cluster | tok << 8 | nbits << 14 | bits << 18)
-  const uint64_t* tbase; // ANS: [ngroups] first token of each group
+  uint32_t* tokens;      // token records (cluster | tok << 8 | nbits << 14 | bits << 18),
+                         //   group g at (g - g0) * kGroupTokStride (hist pass writes them)
 };
+// records per pass group: 1024 blocks x 3 channels x <= 64 tokens per slice
+constexpr uint64_t kGroupTokStride = 1024ull * 3 * 64;
 
 // ANS coding of the pass groups' token records (jxg_ac.hip)
 constexpr uint32_t kAnsHists = 16;  // == kAnsMaxHists (jxg_bitstream.h)
@@ -104,10 +106,9 @@ constexpr uint32_t kAnsInvOff = kAnsDivOff + kAnsHists * 128 * 4;
 constexpr uint32_t kAnsMapOff = kAnsInvOff + kAnsHists * 4096 * 2;
 constexpr uint32_t kAnsTabBytes = kAnsMapOff + 136;
 struct AnsArgs {
-  const uint32_t* tokens;  // token records of ac_tokens_kernel
-  uint32_t* val;           // [tokens] emitted bits: 16-bit chunk (if any) then raw bits
-  uint8_t* len;            // [tokens] number of emitted bits
-  const uint64_t* tbase;   // [ngroups]
+  const uint32_t* tokens;  // token records of ac_hist_kernel (kGroupTokStride per group)
+  uint32_t* val;           // [records] emitted bits: 16-bit chunk (if any) then raw bits
+  uint8_t* len;            // [records] number of emitted bits
   const uint32_t* ntok;    // [ngroups][3]
   const uint8_t* tab;      // table blob (kAnsDivOff / kAnsInvOff / kAnsMapOff):
                            //  u32 [16][128] symbol: f - 1 | cum << 12
@@ -122,7 +123,6 @@ struct AnsArgs {
   uint32_t* bits;          // [ngroups] exact bits
   uint32_t g0, g1;         // groups [g0, g1)
 };
-void launch_ac_tokens(const AcArgs& a, uint32_t ngroups, hipStream_t s);
 void launch_ans(const AnsArgs& a, hipStream_t s);
 
 // LF-group modular streams: rows of (lf group, stream, channel, y)
