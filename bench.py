@@ -97,7 +97,7 @@ def cpu_baseline(img, distance, effort):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=2, help="BASELINE config index (2 = 8K)")
     ap.add_argument("--distance", type=float, default=1.0)
