@@ -431,7 +431,8 @@ __device__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S) {
     // the LLF (first cy rows x cx columns) only occurs in chunk 0
     const bool llf_col = ch == 0 && x < P.cx();
     float cp = 0.0f;
-    int clzs = 0, nzc = 0;
+    uint32_t ebits = 0;
+    int nzc = 0;
 #pragma unroll
     for (int kk = 0; kk < RPC; kk++) {
       const int ky = ch * RPC + kk;
@@ -443,22 +444,28 @@ __device__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S) {
       rv = is_llf ? 0.0f : rv;  // LLF: quantizes to 0, contributes nothing
       const float vq = rv * (w[kk] * scale);
       const float av = fabsf(vq);
-      const int qa = av < 0.58f ? 0 : (int)(fminf(av, 32767.0f) + 0.5f);
+      // qa = (int)(min(av, 32767) + 0.5) as an integer-valued float (the
+      // truncation of a positive value is its floor): no conversions needed
+      // for the error and the rate
+      const float qf = av < 0.58f ? 0.0f : floorf(fminf(av, 32767.0f) + 0.5f);
       if (CH == 1) {
+        const int qa = (int)qf;
         float bq = S.btab[min(qa, 255)];
         if (__builtin_expect(__any(qa >= 256), 0)) {
-          if (qa >= 256) bq = 0.145f / (float)qa;
+          if (qa >= 256) bq = 0.145f / qf;
         }
-        float adj = qa == 0 ? 0.0f : (qa == 1 ? kBias1 : (float)qa - bq);
+        float adj = qa == 0 ? 0.0f : (qa == 1 ? kBias1 : qf - bq);
         if (vq < 0.0f) adj = -adj;
         if (!is_llf) cplane[ky * kMS] = adj * iw[kk];
       }
-      const float e = av - (float)qa;
+      const float e = av - qf;
       cp = fmaf(e, e, cp);
-      // 2 + 2 bitlen(qa) per non-zero: bitlen(qa) = 31 - clz(2 qa + 1)
-      clzs += (int)__clz((uint32_t)(2 * qa + 1));
-      nzc += qa != 0;
+      // 2 + 2 bitlen(qa) per non-zero = 2 E - 250, E = biased exponent of qf
+      // (qf = 0 has E = 0 and is not counted in nzc)
+      ebits += __float_as_uint(qf) >> 23;
+      nzc += qf != 0.0f;
       if (WRITE) {
+        const int qa = (int)qf;
         const int qq = vq < 0.0f ? -qa : qa;
         const int p = nat[kk];
         const int sl = p >> 6;
@@ -467,7 +474,7 @@ __device__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S) {
         a.ac[(gb * 3 + CH) * 64 + (p & 63)] = (int16_t)qq;
       }
     }
-    const int bits = 2 * nzc + 2 * (RPC * 31 - clzs);
+    const int bits = 2 * (int)ebits - 250 * nzc;
     // the chunk's column partials, tree-summed over the varblock's C lanes
     // (an aligned group inside one wave); bits | non-zeros << 20 likewise
     int packed = bits | nzc << 20;
