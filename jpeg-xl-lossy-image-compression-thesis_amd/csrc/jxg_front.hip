@@ -64,48 +64,49 @@ __device__ __forceinline__ float lap(const Tile& t, int px, int py) {
   return sum;
 }
 
-// The Laplacian is recomputed for the column walk instead of being kept in a
-// per-lane array (identical values; keeps the function register-light).
-template <int XS, int YS>
-__device__ __forceinline__ float homogeneity(const Tile& t, int x, int y, int bx, int by, float dist,
-                             int ysize, int h1_int) {
+// edge threshold of CalculateHomogeneity (combined.diff:163-168)
+__device__ __forceinline__ float edge_threshold(float dist) {
   float thr = 0.25f;
   if ((double)dist > 10.0)
     thr = 0.40f;
   else if ((double)dist <= 2.0)
     thr = 0.15f;
+  return thr;
+}
+
+// The tile's (Laplacian > threshold) map, one 64-bit word per interior row
+// (bit k = column k): wave w evaluates rows w, w + 8, ... with lane = column
+// and one ballot per row.  Every region of every block then counts its zero
+// crossings from these words instead of re-walking the Laplacian.
+__device__ __forceinline__ void lap_bits(const Tile& t, float thr, uint64_t* bits) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int y = wave; y < 64; y += (int)(blockDim.x >> 6)) {
+    const float v = lap(t, t.ox + 1 + lane, t.oy + 1 + y);
+    const uint64_t b = __ballot(v > thr);
+    if (lane == 0) bits[y] = b;
+  }
+}
+
+// CalculateNumZeroCrossings (combined.diff:17-55) on the bit map: a crossing
+// is an entry into L > t, i.e. a set bit whose predecessor along the row
+// (column) inside the region is clear -- the walk's in_edge flag is exactly
+// the previous entry's comparison (no NaN: L is a sum of finite samples).
+template <int XS, int YS>
+__device__ __forceinline__ float homogeneity(const Tile& t, const uint64_t* lbits, int x, int y,
+                                             int bx, int by, float dist, int ysize, int h1_int) {
+  (void)dist;
   const int x0 = x + bx, y0 = y + by;
-  uint32_t nh = 0;
-#pragma unroll 1
-  for (int i = 0; i < YS; i++) {
-    bool in_edge = false;
+  const int lx0 = x0 - (t.ox + 1), ly0 = y0 - (t.oy + 1);
+  uint32_t nh = 0, nv = 0;
+  uint32_t prev = 0;
 #pragma unroll
-    for (int j = 0; j < XS; j++) {
-      const float v = lap(t, x0 + j, y0 + i);
-      if (!in_edge && v > thr) {
-        nh++;
-        in_edge = true;
-      } else if (in_edge && v <= thr) {
-        in_edge = false;
-      }
-    }
+  for (int i = 0; i < YS; i++) {
+    const uint32_t r = (uint32_t)(lbits[ly0 + i] >> lx0) & ((1u << XS) - 1u);
+    nh += __popc(r & ~(r << 1));
+    nv += __popc(r & ~prev);
+    prev = r;
   }
   const float avg_h = (float)nh / (float)YS;
-  uint32_t nv = 0;
-#pragma unroll 1
-  for (int i = 0; i < XS; i++) {
-    bool in_edge = false;
-#pragma unroll
-    for (int j = 0; j < YS; j++) {
-      const float v = lap(t, x0 + i, y0 + j);
-      if (!in_edge && v > thr) {
-        nv++;
-        in_edge = true;
-      } else if (in_edge && v <= thr) {
-        in_edge = false;
-      }
-    }
-  }
   const float avg_v = (float)nv / (float)XS;
   const uint32_t nc = (uint32_t)(avg_h + avg_v);
   float sml = 0.0f;
@@ -167,17 +168,17 @@ __device__ __forceinline__ float homogeneity(const Tile& t, int x, int y, int bx
 // region r of CalculateHomogeneitySimilarityIndices (combined.diff:189-204):
 // 0 h1(8,4,0,0) 1 h2(8,4,0,4) 2 v1(4,8,0,0) 3 v2(4,8,4,0)
 // 4 (4,4,0,0) 5 (4,4,4,4) 6 (4,4,0,4) 7 (4,4,4,0)
-__device__ __forceinline__ float homog_region(const Tile& t, int r, int x, int y, float dist, int ysize,
-                              int h1) {
+__device__ __forceinline__ float homog_region(const Tile& t, const uint64_t* lb, int r, int x, int y,
+                                              float dist, int ysize, int h1) {
   switch (r) {
-    case 0: return homogeneity<8, 4>(t, x, y, 0, 0, dist, ysize, h1);
-    case 1: return homogeneity<8, 4>(t, x, y, 0, 4, dist, ysize, h1);
-    case 2: return homogeneity<4, 8>(t, x, y, 0, 0, dist, ysize, h1);
-    case 3: return homogeneity<4, 8>(t, x, y, 4, 0, dist, ysize, h1);
-    case 4: return homogeneity<4, 4>(t, x, y, 0, 0, dist, ysize, h1);
-    case 5: return homogeneity<4, 4>(t, x, y, 4, 4, dist, ysize, h1);
-    case 6: return homogeneity<4, 4>(t, x, y, 0, 4, dist, ysize, h1);
-    default: return homogeneity<4, 4>(t, x, y, 4, 0, dist, ysize, h1);
+    case 0: return homogeneity<8, 4>(t, lb, x, y, 0, 0, dist, ysize, h1);
+    case 1: return homogeneity<8, 4>(t, lb, x, y, 0, 4, dist, ysize, h1);
+    case 2: return homogeneity<4, 8>(t, lb, x, y, 0, 0, dist, ysize, h1);
+    case 3: return homogeneity<4, 8>(t, lb, x, y, 4, 0, dist, ysize, h1);
+    case 4: return homogeneity<4, 4>(t, lb, x, y, 0, 0, dist, ysize, h1);
+    case 5: return homogeneity<4, 4>(t, lb, x, y, 4, 4, dist, ysize, h1);
+    case 6: return homogeneity<4, 4>(t, lb, x, y, 0, 4, dist, ysize, h1);
+    default: return homogeneity<4, 4>(t, lb, x, y, 4, 0, dist, ysize, h1);
   }
 }
 
@@ -562,6 +563,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   __shared__ float sBtab[256];
   __shared__ float sH[8][64];
   __shared__ float sR[64][3];
+  __shared__ uint64_t sLapBits[64];
   const int tid = threadIdx.x;
   // a shard launches its own tiles through a list (1-D grid)
   const int tile_id = a.tile_list ? (int)a.tile_list[blockIdx.x] : -1;
@@ -596,9 +598,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   // ---- phase A: thesis homogeneity; wave w = region w, lane = block ----
   if (a.proposals & 3u) {
     const int lbx = lane & 7, lby = lane >> 3;
+    lap_bits(tile, edge_threshold(a.distance), sLapBits);
+    __syncthreads();
     if (lbx < nbx && lby < nby)
-      sH[wave][lane] = homog_region(tile, wave, tx * kTile + lbx * 8, ty * kTile + lby * 8,
-                                    a.distance, (int)a.yp, a.h1_int);
+      sH[wave][lane] = homog_region(tile, sLapBits, wave, tx * kTile + lbx * 8,
+                                    ty * kTile + lby * 8, a.distance, (int)a.yp, a.h1_int);
     __syncthreads();
     if (tid < 64 && lbx < nbx && lby < nby) {
       float h[8];
@@ -768,6 +772,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 __global__ __launch_bounds__(kThreads) void homog_kernel(HomogArgs a) {
   __shared__ float sPix[3 * kPlane];
   __shared__ float sH[8][64];
+  __shared__ uint64_t sLapBits[64];
   const int tid = threadIdx.x;
   const int tx = blockIdx.x, ty = blockIdx.y;
   const int ox = tx * kTile - 1, oy = ty * kTile - 1;
@@ -787,8 +792,10 @@ __global__ __launch_bounds__(kThreads) void homog_kernel(HomogArgs a) {
   const int lbx = lane & 7, lby = lane >> 3;
   const bool valid = tx * 8 + lbx < bxs && ty * 8 + lby < bys;
   const Tile tile{sPix, sPix + kPlane, sPix + 2 * kPlane, ox, oy};
+  lap_bits(tile, edge_threshold(a.distance), sLapBits);
+  __syncthreads();
   if (valid)
-    sH[wave][lane] = homog_region(tile, wave, tx * kTile + lbx * 8, ty * kTile + lby * 8,
+    sH[wave][lane] = homog_region(tile, sLapBits, wave, tx * kTile + lbx * 8, ty * kTile + lby * 8,
                                   a.distance, (int)a.ysize, a.h1_int);
   __syncthreads();
   if (tid < 64 && valid) {
