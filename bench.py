@@ -80,6 +80,15 @@ def load_pmc_traffic(workload):
         return None
 
 
+def load_merge_pmc(workload):
+    p = os.path.join(ROOT, "profiles", "merge_pmc_%s.json" % workload)
+    try:
+        with open(p) as f:
+            return json.load(f).get("valu_issue_frac")
+    except Exception:
+        return None
+
+
 def cpu_baseline(img, distance, effort):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_ffi  # the checker, timed here only as the reported baseline
@@ -280,6 +289,12 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": load_pmc_traffic(name) if world == 1 else None,
                          "algorithmic_bytes": fb, "avg_ms": round(fms, 4)},
+            # the dominant kernels (merge stage) are VALU-issue-bound, not
+            # HBM-bound: their live time and the PMC-measured VALU issue rate
+            "merge_stage": {"kernels": "merge_eval + merge_resolve + merge_write",
+                            "bound": "valu",
+                            "avg_ms": round(st["ms_front"] - st["ms_front_kernel"], 4),
+                            "valu_issue_frac_pmc": load_merge_pmc(name) if world == 1 else None},
         }
         if alt is not None:
             res["ans_coder"] = alt
