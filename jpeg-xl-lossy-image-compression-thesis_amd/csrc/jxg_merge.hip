@@ -746,17 +746,34 @@ __device__ __forceinline__ void write_entry(const MergeArgs& a, int tile, int si
       const int n = S.vnz[v][c];
       a.nz[c * nb + gb] = (uint16_t)(k == 0 ? n : (n + cb - 1) >> lcb);
     }
+    // the LLF -> DC tables of this block in registers (static indices, loop
+    // bounds cx, cy <= 8 as predicates): no dependent constant loads
+    float px[8], py[8], ibx[8], iby[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      px[k] = c_llf_p[lx * 8 + k];
+      py[k] = c_llf_p[ly * 8 + k];
+      ibx[k] = c_llf_ib[lx * 64 + ix * 8 + k];
+      iby[k] = c_llf_ib[ly * 64 + iy * 8 + k];
+    }
+    const int cx = P.cx(), cy = P.cy();
     float dc[3];
+#pragma unroll 1
     for (int c = 0; c < 3; c++) {
       float acc = 0.0f;
-      for (int ky = 0; ky < P.cy(); ky++) {
-        float u = 0.0f;
-        for (int kx = 0; kx < P.cx(); kx++) {
-          const float tt = (llf_at(S, c, (by0 + ky) * 8 + bx0 + kx) * c_llf_p[ly * 8 + ky]) *
-                           c_llf_p[lx * 8 + kx];
-          u = fmaf(tt, c_llf_ib[lx * 64 + ix * 8 + kx], u);
+#pragma unroll
+      for (int ky = 0; ky < 8; ky++) {
+        if (ky < cy) {
+          float u = 0.0f;
+#pragma unroll
+          for (int kx = 0; kx < 8; kx++) {
+            if (kx < cx) {
+              const float tt = (llf_at(S, c, (by0 + ky) * 8 + bx0 + kx) * py[ky]) * px[kx];
+              u = fmaf(tt, ibx[kx], u);
+            }
+          }
+          acc = fmaf(u, iby[ky], acc);
         }
-        acc = fmaf(u, c_llf_ib[ly * 64 + iy * 8 + ky], acc);
       }
       dc[c] = acc;
     }
