@@ -369,7 +369,11 @@ static MergeTables build_merge_tables() {
         for (int kx = 0; kx < C; kx++) {
           const int si = cx >= cy ? ky * C + kx : kx * R + ky;
           const int pi = kShapeOff[sh] + kx * R + ky;
-          for (int c = 0; c < 3; c++) swk[(size_t)c * stot + pi] = T.wk[(size_t)c * tot + kKindOff[k] + si];
+          // LLF positions (the first cy x cx): weight 0, so they quantize to 0
+          // and add nothing without a per-coefficient test in the kernels
+          const bool llf = ky < cy && kx < cx;
+          for (int c = 0; c < 3; c++)
+            swk[(size_t)c * stot + pi] = llf ? 0.0f : T.wk[(size_t)c * tot + kKindOff[k] + si];
           siwy[pi] = T.iwy[kKindOff[k] + si];
           snat[pi] = T.nat[kKindOff[k] + si];
         }

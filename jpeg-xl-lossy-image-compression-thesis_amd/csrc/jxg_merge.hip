@@ -441,7 +441,8 @@ __device__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S) {
       if (WRITE && is_llf) llf_at(S, CH, (by0 + ky) * 8 + bx0 + x) = coef_v;
       float rv = coef_v;
       if (CH == 2) rv = rv - yd[ky * kMS];
-      rv = is_llf ? 0.0f : rv;  // LLF: quantizes to 0, contributes nothing
+      // LLF positions carry weight 0 (host tables): vq = +-0 quantizes to 0
+      // and contributes nothing
       const float vq = rv * (w[kk] * scale);
       const float av = fabsf(vq);
       // qa = (int)(min(av, 32767) + 0.5) as an integer-valued float (the
@@ -456,7 +457,7 @@ __device__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S) {
         }
         float adj = qa == 0 ? 0.0f : (qa == 1 ? kBias1 : qf - bq);
         if (vq < 0.0f) adj = -adj;
-        if (!is_llf) cplane[ky * kMS] = adj * iw[kk];
+        cplane[ky * kMS] = adj * iw[kk];  // LLF: 0 (its value lives in llf_at)
       }
       const float e = av - qf;
       cp = fmaf(e, e, cp);
