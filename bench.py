@@ -125,6 +125,9 @@ def main():
     ap.add_argument("--alt-ans-streams", type=int, default=3,
                     help="also time the ANS coder with this many concurrent encoders "
                          "(reported under 'ans_coder'; 0 = off)")
+    ap.add_argument("--alt-thesis", type=int, default=1,
+                    help="also time the workload with the thesis proposals P+F "
+                         "(reported under 'thesis_proposals'; 0 = off)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -154,12 +157,13 @@ def main():
         d_img = d_img.repeat(world, 1, 1).contiguous()
     torch.cuda.synchronize()
 
-    def run(coder, nstreams):
+    def run(coder, nstreams, proposals=None):
         """Warm up, then time args.steps frames over `nstreams` concurrent
         encoders (one host thread, context and HIP stream each)."""
         flags = jxg.FLAG_ANS if coder == "ans" else 0
+        props = args.proposals if proposals is None else proposals
         encs = [jxg.Encoder(distance=args.distance, effort=args.effort,
-                            proposals=args.proposals, device=local, flags=flags)
+                            proposals=props, device=local, flags=flags)
                 for _ in range(nstreams)]
         bufs = {}
         host = None
@@ -238,6 +242,18 @@ def main():
                "ms_latency": round(sum(x[0] for x in A["host_ms"]) / len(A["host_ms"]), 3),
                "bytes_per_frame": A["sizes"][-1],
                "bpp": round(A["sizes"][-1] * 8.0 / (w * fh), 4)}
+    thesis = None
+    if not shard and args.alt_thesis and args.proposals != 3:
+        # the thesis proposals P + F (combined.diff) on the same workload:
+        # the homogeneity selector in the front kernel, hook F on every
+        # 8x8 and merge candidate
+        T = run(args.coder, 1, proposals=3)
+        thesis = {"proposals": "P+F (combined.diff)",
+                  "value": round(w * fh * world * args.steps / T["dt"] / 1e6, 2),
+                  "ms_per_step": round(T["dt"] * 1e3 / args.steps, 3),
+                  "ms_front_kernel": round(sum(T["front_ms"]) / len(T["front_ms"]), 4),
+                  "bytes_per_frame": T["sizes"][-1],
+                  "bpp": round(T["sizes"][-1] * 8.0 / (w * fh), 4)}
     if rank == 0:
         ms_step = dt * 1e3 / args.steps
         frame_px = w * fh
@@ -298,6 +314,8 @@ def main():
         }
         if alt is not None:
             res["ans_coder"] = alt
+        if thesis is not None:
+            res["thesis_proposals"] = thesis
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(img, args.distance, args.effort)
         print(json.dumps(res), flush=True)
