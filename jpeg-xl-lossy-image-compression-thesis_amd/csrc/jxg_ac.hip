@@ -3,19 +3,20 @@
 // One 1024-thread workgroup per 256x256-pixel pass group: thread = 8x8 block
 // = one 64-coefficient slice of a varblock (an 8x8-class block is a varblock
 // of one slice; a merged varblock covering cb blocks keeps slice i of its
-// natural-order coefficients in covered block i, raster order).  A task
-// (slice, channel) loads its 64 int16 coefficients (128 B) with 8 x 16-byte
-// loads into 32 VGPRs and walks them on registers (fully unrolled,
-// wave-uniform early exit every 8 coefficients).  A slice's walk state at its
-// first coefficient -- non-zeros left and the previous-coefficient flag --
-// follows from the per-slice non-zero counts of the earlier slices (LDS), so
-// every slice of a 64x64 varblock is walked in parallel.
+// natural-order coefficients in covered block i, raster order).  A slice's
+// walk state at its first coefficient -- non-zeros left and the
+// previous-coefficient flag -- follows from the per-slice non-zero counts of
+// the earlier slices (LDS), so every slice of a 64x64 varblock is independent.
+// The token walk is wave-parallel: a wave takes the tasks (slice, channel) of
+// its 64 threads one at a time, lane = coefficient; ballot + popcount give
+// each coefficient its non-zeros-left context, so a task costs one pass
+// whatever its token count and its records are stored contiguously.
 //   ac_hist : non-zero counts -> predicted-nz + zero-density contexts ->
 //             clustered histograms (LDS, one global atomic per non-empty bin),
 //             exact per-group token counts, per-group bit upper bound; then a
 //             workgroup scan over varblocks (stream order: varblocks by first
-//             block raster, channels Y, X, B, slices) and a second walk that
-//             writes every token as a 32-bit record (cluster | token << 8 |
+//             block raster, channels Y, X, B, slices) and the wave-parallel
+//             walk that writes every token as a 32-bit record (cluster | token << 8 |
 //             raw-bit count << 14 | raw bits << 18) at its stream position.
 //   ac_emit : prefix codes from the records alone (no coefficient walk):
 //             a contiguous record range per wave, coalesced reads, wave scans
@@ -63,75 +64,14 @@ __device__ __forceinline__ int32_t coef(const uint32_t* w, int k) {
   return (int32_t)(int16_t)(w[k >> 1] >> ((k & 1) * 16));
 }
 
-// kFreqCtx / kNnzCtx as arithmetic (the varblock walk indexes them at run
-// time; table loads would be hoisted out of the unrolled walk)
+// kFreqCtx / kNnzCtx as arithmetic (lane-varying indices; no constant-table
+// gathers in the walk)
 __device__ __forceinline__ int freq_ctx(int k) {
   return k < 16 ? max(k - 1, 0) : (k < 32 ? 15 + ((k - 16) >> 1) : 23 + ((k - 32) >> 2));
 }
 __device__ __forceinline__ int nnz_ctx(int n) {
   return n < 2 ? 0 : n < 3 ? 31 : n < 5 ? 62 : n < 9 ? 93 : n < 13 ? 123 : n < 21 ? 152
        : n < 33 ? 180 : 206;
-}
-
-// Walk of one 8x8-class block and channel (libjxl DecodeACVarBlock with one
-// covered block): f(ctx, value) in bitstream order; contexts fold to
-// compile-time table entries.
-template <class F>
-__device__ __forceinline__ void block_tokens(const uint32_t* w, int nz, int pred, int bctx,
-                                             F&& f) {
-  f(nz_bucket(pred) * kBlockCtx + bctx, (uint32_t)nz);
-  const int zoff = kBlockCtx * kNzBuckets + kZdCtx * bctx;
-  int prev = nz > 4 ? 0 : 1;
-  int left = nz;
-  // 8 chunks of 8 coefficients; a chunk is skipped (wave-uniform branch) once
-  // no lane of the wave has non-zeros left.  No loop exit, so every k stays a
-  // compile-time register index.
-#pragma unroll
-  for (int ch = 0; ch < 8; ch++) {
-    if (__any(left > 0)) {
-#pragma unroll
-      for (int kk = 0; kk < 8; kk++) {
-        const int k = ch * 8 + kk;
-        if (k == 0) continue;
-        if (left > 0) {
-          const int32_t v = coef(w, k);
-          f(zoff + (kNnzCtx[left] + kFreqCtx[k]) * 2 + prev, pack_signed(v));
-          prev = v != 0;
-          left -= prev;
-        }
-      }
-    }
-  }
-}
-
-// Walk of one slice (64 coefficients at q) of a merged varblock: sl = slice
-// index, lcb = log2 covered blocks, left / prev = walk state at the slice's
-// first coefficient; slice 0 also emits the non-zero count token.  Chunks of
-// 8 coefficients are loaded one 16-byte load at a time inside a run-time
-// loop (no register-resident slice: keeps the 8x8 walk's registers).
-template <class F>
-__device__ __forceinline__ void varblock_slice_tokens(const int16_t* q, int sl, int lcb, int nz,
-                                                      int left, int prev, int pred, int bctx,
-                                                      F&& f) {
-  if (sl == 0) f(nz_bucket(pred) * kBlockCtx + bctx, (uint32_t)nz);
-  const int zoff = kBlockCtx * kNzBuckets + kZdCtx * bctx;
-  const int cb = 1 << lcb;
-#pragma unroll 1
-  for (int ch = 0; ch < 8 && left > 0; ch++) {
-    const uint4 t = reinterpret_cast<const uint4*>(q)[ch];
-    const uint32_t w[4] = {t.x, t.y, t.z, t.w};
-#pragma unroll
-    for (int kk = 0; kk < 8; kk++) {
-      const int k = sl * 64 + ch * 8 + kk;
-      if (left > 0 && k >= cb) {
-        const int32_t v = coef(w, kk);
-        f(zoff + (nnz_ctx((left + cb - 1) >> lcb) + freq_ctx(k >> lcb)) * 2 + prev,
-          pack_signed(v));
-        prev = v != 0;
-        left -= prev;
-      }
-    }
-  }
 }
 
 __device__ __forceinline__ int predict_nz(const uint8_t* nzc, int bx, int by) {
@@ -273,22 +213,6 @@ __device__ __forceinline__ void slice_state(const AcArgs& a, const SliceTask& t,
   }
 }
 
-template <class F>
-__device__ __forceinline__ void task_tokens(const AcArgs& a, const SliceTask& t, const AcLds& L,
-                                            int c, F&& f) {
-  int nz, left, prev;
-  slice_state(a, t, L, c, nz, left, prev);
-  const int pred = t.sl == 0 ? predict_nz(L.nz[c], t.bx, t.by) : 0;
-  const int16_t* q = a.ac + (t.gb * 3 + c) * 64;
-  if (t.lcb == 0) {
-    uint32_t w[32];
-    load_coefs(q, w);
-    block_tokens(w, nz, pred, block_ctx_of(c, t.type), f);
-  } else {
-    varblock_slice_tokens(q, t.sl, t.lcb, nz, left, prev, pred, block_ctx_of(c, t.type), f);
-  }
-}
-
 // workgroup (1024 threads) exclusive scan; *total = sum of all values
 __device__ __forceinline__ uint32_t block_excl_scan1024(uint32_t v, uint32_t* sWave,
                                                         uint32_t* total) {
@@ -348,34 +272,97 @@ __global__ __launch_bounds__(kAcThreads) void ac_hist_kernel(AcArgs a) {
   if (t.valid && t.sl == 0) sBase[me] = off;
   __syncthreads();
   // one walk: clustered histogram, bit bound, and every token's 32-bit record
-  // at its stream position
+  // at its stream position.  Wave-parallel: each thread derives the walk state
+  // of its own task (slice, channel); the wave then takes its 64 tasks one at
+  // a time with lane = coefficient, so a task costs one pass whatever its token
+  // count (no walk divergence) and its records are stored contiguously.
+  // Per coefficient k >= lo: left_k = left - (non-zeros in [lo, k)) (ballot +
+  // popcount), prev_k = the walk's start flag at lo, else (coef k-1 != 0);
+  // token iff left_k > 0 -- the serial walk of block_tokens /
+  // varblock_slice_tokens, restated.
   uint32_t bound = 0, nt[3] = {0, 0, 0};
-  if (t.valid) {
-    uint32_t pos = sBase[t.oby * 32 + t.obx];
-    uint32_t* rec = a.tokens + (uint64_t)(g - (int)a.g0) * kGroupTokStride;
+  uint32_t* rec = a.tokens + (uint64_t)(g - (int)a.g0) * kGroupTokStride;
+  uint32_t pos = t.valid ? sBase[t.oby * 32 + t.obx] : 0u;
+  const int lane = threadIdx.x & 63;
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
 #pragma unroll 1
-    for (int ci = 0; ci < 3; ci++) {
-      const int c = channel_of(ci);
+  for (int ci = 0; ci < 3; ci++) {
+    const int c = channel_of(ci);
+    uint32_t idx = 0, cnt = 0, info = 0, tok0 = 0;
+    if (t.valid) {
       uint32_t before = 0, chan_total = 0;
       for (int j = 0; j < cb; j++) {
         const uint32_t b = sTask[ci][block_of_slice(t, j)];
         before += j < t.sl ? b : 0u;
         chan_total += b;
       }
-      uint32_t idx = pos + before;
-      task_tokens(a, t, L, c, [&](int ctx, uint32_t v) {
+      idx = pos + before;
+      cnt = sTask[ci][me];
+      pos += chan_total;
+      int nz, left, prev;
+      slice_state(a, t, L, c, nz, left, prev);
+      const int bctx = block_ctx_of(c, t.type);
+      // info: left (12 bits) | prev << 12 | lcb << 13 | sl << 16 | bctx << 22
+      info = (uint32_t)left | ((uint32_t)prev << 12) | ((uint32_t)t.lcb << 13) |
+             ((uint32_t)t.sl << 16) | ((uint32_t)bctx << 22);
+      if (t.sl == 0) {  // the non-zero count token, written by the task's own thread
+        const int pred = predict_nz(L.nz[c], t.bx, t.by);
         uint32_t tok, nb, bits;
-        hybrid420(v, tok, nb, bits);
-        const uint32_t clu = sClu[ctx];
+        hybrid420((uint32_t)nz, tok, nb, bits);
+        const uint32_t clu = sClu[nz_bucket(pred) * kBlockCtx + bctx];
         atomicAdd(&sHist[clu * kAcTok + tok], 1u);
         bound += 15u + nb;
-        rec[idx++] = clu | (tok << 8) | (nb << 14) | (bits << 18);
-      });
-      const uint32_t cnt = sTask[ci][me];
+        tok0 = clu | (tok << 8) | (nb << 14) | (bits << 18);
+        rec[idx] = tok0;
+      }
       nt[0] += c == 0 ? cnt : 0u;
       nt[1] += c == 1 ? cnt : 0u;
       nt[2] += c == 2 ? cnt : 0u;
-      pos += chan_total;
+    }
+    // tasks with coefficient tokens, taken 8 at a time: their 8 coefficient
+    // loads are issued together (one memory latency per 8 tasks)
+    const bool need = t.valid && cnt > (t.sl == 0 ? 1u : 0u);
+    const uint32_t qoff = (uint32_t)((t.gb * 3 + c) * 64);
+    uint64_t M = __ballot(need);
+    while (M) {
+      int js[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        js[u] = M ? (int)__builtin_ctzll(M) : -1;
+        M = M ? M & (M - 1) : 0ull;
+      }
+      int32_t v8[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++)
+        v8[u] = js[u] >= 0 ? a.ac[(uint32_t)__builtin_amdgcn_readlane((int)qoff, js[u]) + lane] : 0;
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        if (js[u] < 0) break;
+        const int j = js[u];
+        const uint32_t ij = (uint32_t)__builtin_amdgcn_readlane((int)info, j);
+        const uint32_t idxj = (uint32_t)__builtin_amdgcn_readlane((int)idx, j);
+        const int slj = (ij >> 16) & 63, lcbj = (ij >> 13) & 7;
+        const int leftj = ij & 4095, prevj = (ij >> 12) & 1, bctxj = ij >> 22;
+        const int cbj = 1 << lcbj;
+        const int k = slj * 64 + lane;
+        const int lo = max(slj * 64, cbj);
+        const int32_t v = v8[u];
+        const bool on = k >= cbj;
+        const uint64_t m = __ballot(on && v != 0);
+        const int left_k = leftj - __popcll(m & below);
+        if (on && left_k > 0) {
+          const int prev_k = k == lo ? prevj : (int)((m >> (lane - 1)) & 1);
+          const int ctx = kBlockCtx * kNzBuckets + kZdCtx * bctxj +
+                          (nnz_ctx((left_k + cbj - 1) >> lcbj) + freq_ctx(k >> lcbj)) * 2 + prev_k;
+          uint32_t tok, nb, bits;
+          hybrid420(pack_signed(v), tok, nb, bits);
+          const uint32_t clu = sClu[ctx];
+          atomicAdd(&sHist[clu * kAcTok + tok], 1u);
+          bound += 15u + nb;
+          rec[idxj + (slj == 0 ? 1u : 0u) + (uint32_t)(k - lo)] =
+              clu | (tok << 8) | (nb << 14) | (bits << 18);
+        }
+      }
     }
   }
   atomicAdd(&sBound, bound);
