@@ -236,7 +236,9 @@ __device__ __forceinline__ uint32_t block_excl_scan1024(uint32_t v, uint32_t* sW
   return before + incl - v;
 }
 
-__global__ __launch_bounds__(kAcThreads) void ac_hist_kernel(AcArgs a) {
+// 8 waves per SIMD (<= 64 VGPRs): two 1024-thread workgroups per CU, so all
+// pass groups of an 8K frame are resident at once
+__global__ __launch_bounds__(kAcThreads) __attribute__((amdgpu_waves_per_eu(8))) void ac_hist_kernel(AcArgs a) {
   __shared__ uint32_t sHist[kMaxClusters * kAcTok];
   __shared__ AcLds L;
   __shared__ uint8_t sClu[kAcCtx];
@@ -244,9 +246,15 @@ __global__ __launch_bounds__(kAcThreads) void ac_hist_kernel(AcArgs a) {
   __shared__ uint32_t sBase[1024];     // first token of each varblock (first block)
   __shared__ uint32_t sWave[kAcThreads / 64];
   __shared__ uint32_t sBound, sNtok[3];
+  __shared__ uint16_t sNnzCtx[64];
+  __shared__ uint8_t sFreqCtx[64];
   const int g = blockIdx.x + (int)a.g0;
   const GroupGeom G = group_geom(a, g);
   for (int i = threadIdx.x; i < kMaxClusters * kAcTok; i += blockDim.x) sHist[i] = 0;
+  if (threadIdx.x < 64) {
+    sNnzCtx[threadIdx.x] = (uint16_t)nnz_ctx(threadIdx.x);
+    sFreqCtx[threadIdx.x] = (uint8_t)freq_ctx(threadIdx.x);
+  }
   for (int i = threadIdx.x; i < kAcCtx; i += blockDim.x) sClu[i] = c_cluster[i];
   if (threadIdx.x < 3) sNtok[threadIdx.x] = 0;
   if (threadIdx.x == 0) sBound = 0;
@@ -319,24 +327,28 @@ __global__ __launch_bounds__(kAcThreads) void ac_hist_kernel(AcArgs a) {
       nt[1] += c == 1 ? cnt : 0u;
       nt[2] += c == 2 ? cnt : 0u;
     }
-    // tasks with coefficient tokens, taken 8 at a time: their 8 coefficient
-    // loads are issued together (one memory latency per 8 tasks)
+    // tasks with coefficient tokens, taken kBatch at a time: their coefficient
+    // loads are issued together (one memory latency per batch)
     const bool need = t.valid && cnt > (t.sl == 0 ? 1u : 0u);
     const uint32_t qoff = (uint32_t)((t.gb * 3 + c) * 64);
     uint64_t M = __ballot(need);
+#ifndef JXG_AC_BATCH
+#define JXG_AC_BATCH 8
+#endif
+    constexpr int kBatch = JXG_AC_BATCH;
     while (M) {
-      int js[8];
+      int js[kBatch];
 #pragma unroll
-      for (int u = 0; u < 8; u++) {
+      for (int u = 0; u < kBatch; u++) {
         js[u] = M ? (int)__builtin_ctzll(M) : -1;
         M = M ? M & (M - 1) : 0ull;
       }
-      int32_t v8[8];
+      int32_t v8[kBatch];
 #pragma unroll
-      for (int u = 0; u < 8; u++)
+      for (int u = 0; u < kBatch; u++)
         v8[u] = js[u] >= 0 ? a.ac[(uint32_t)__builtin_amdgcn_readlane((int)qoff, js[u]) + lane] : 0;
 #pragma unroll
-      for (int u = 0; u < 8; u++) {
+      for (int u = 0; u < kBatch; u++) {
         if (js[u] < 0) break;
         const int j = js[u];
         const uint32_t ij = (uint32_t)__builtin_amdgcn_readlane((int)info, j);
@@ -353,7 +365,7 @@ __global__ __launch_bounds__(kAcThreads) void ac_hist_kernel(AcArgs a) {
         if (on && left_k > 0) {
           const int prev_k = k == lo ? prevj : (int)((m >> (lane - 1)) & 1);
           const int ctx = kBlockCtx * kNzBuckets + kZdCtx * bctxj +
-                          (nnz_ctx((left_k + cbj - 1) >> lcbj) + freq_ctx(k >> lcbj)) * 2 + prev_k;
+                          (sNnzCtx[(left_k + cbj - 1) >> lcbj] + sFreqCtx[k >> lcbj]) * 2 + prev_k;
           uint32_t tok, nb, bits;
           hybrid420(pack_signed(v), tok, nb, bits);
           const uint32_t clu = sClu[ctx];
