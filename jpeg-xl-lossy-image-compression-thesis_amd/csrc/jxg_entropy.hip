@@ -234,11 +234,12 @@ __device__ __forceinline__ uint32_t read_bits32(const uint32_t* src, uint64_t bi
 
 __global__ __launch_bounds__(256) void concat_kernel(const ConcatPiece* pieces,
                                                      const uint32_t* scratch,
-                                                     const uint32_t* chunks, uint32_t* out) {
+                                                     const uint32_t* chunks,
+                                                     const uint32_t* scratch2, uint32_t* out) {
   const ConcatPiece p = pieces[blockIdx.y];
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i * 32 >= p.nbits) return;
-  const uint32_t* src = p.arena ? chunks : scratch;
+  const uint32_t* src = p.arena == 1 ? chunks : (p.arena == 2 ? scratch2 : scratch);
   const uint64_t nb = p.nbits - i * 32 < 32 ? p.nbits - i * 32 : 32;
   uint32_t v = read_bits32(src, p.src_bit + i * 32);
   if (nb < 32) v &= (1u << nb) - 1u;
@@ -264,12 +265,12 @@ void launch_lf_emit(const LfArgs& a, uint32_t nchunks, hipStream_t s) {
   hipLaunchKernelGGL(lf_emit_kernel, dim3(nchunks), dim3(256), 0, s, a);
 }
 void launch_concat(const ConcatPiece* pieces, uint32_t npieces, uint64_t max_words,
-                   const uint32_t* scratch, const uint32_t* chunks, uint32_t* out,
-                   hipStream_t s) {
+                   const uint32_t* scratch, const uint32_t* chunks, const uint32_t* scratch2,
+                   uint32_t* out, hipStream_t s) {
   if (npieces == 0 || max_words == 0) return;
   const uint32_t gx = (uint32_t)((max_words + 255) / 256);
   hipLaunchKernelGGL(concat_kernel, dim3(gx, npieces), dim3(256), 0, s, pieces, scratch,
-                     chunks, out);
+                     chunks, scratch2, out);
 }
 
 

@@ -409,7 +409,7 @@ static MergeTables build_merge_tables() {
 struct Ctx {
   jxg_params params{};
   hipStream_t stream = nullptr;
-  hipEvent_t ev[6] = {};
+  hipEvent_t ev[7] = {};  // ev[6]: AC statistics downloaded (stage_download_ac)
   bool constants_ready = false;
   // device
   DevBuf<uint8_t> rgb, acs, qf;
@@ -421,7 +421,7 @@ struct Ctx {
   DevBuf<float> homog, xyb, r3;
   DevBuf<uint8_t> type;
   DevBuf<uint32_t> hist_ac, bound, ntok, codes_ac, gbits, lfhist, sbound, lfcodes, chunkbits,
-      stream_chunks, stream_bits, scratch, chunks, out;
+      stream_chunks, stream_bits, scratch, scratch_lf, chunks, out;
   DevBuf<uint64_t> gbase, chunkoff, stream_base;
   DevBuf<uint32_t> tile_list;
   DevBuf<uint32_t> tokens, tval, ans_state;  // ANS coder
@@ -436,7 +436,9 @@ struct Ctx {
   bool gauss_ready = false;
   DevBuf<ConcatPiece> pieces;
   // host
-  PinBuf<uint32_t> h_hist_ac, h_bound, h_ntok, h_lfhist, h_sbound, h_gbits, h_sbits, h_vcount;
+  PinBuf<uint32_t> h_hist_ac, h_bound, h_ntok, h_lfhist, h_sbound, h_gbits, h_sbits, h_vcount,
+      h_codes_ac, h_lfcodes;
+  PinBuf<uint64_t> h_gbase, h_sbase;
   // LF row segments cached per frame size and shard
   uint32_t rows_w = 0, rows_h = 0, rows_rank = 0, rows_world = 1;
   std::vector<LfRow> rows_h_cache;
@@ -799,18 +801,26 @@ static jxg_status stage_lf_stats(Ctx* c, Job& J) {
 }
 
 // ---- stage E: statistics to the host (AC histogram from `hist`) ----
-static jxg_status stage_download(Ctx* c, Job& J, const uint32_t* hist) {
+// AC statistics (histogram, bit bounds, token counts) are downloaded as soon as
+// ac_hist is done, so the host builds the AC prefix codes while the LF
+// statistics kernels still run; the LF statistics follow in stage_download_lf.
+static jxg_status stage_download_ac(Ctx* c, Job& J, const uint32_t* hist) {
   hipStream_t s = c->stream;
   const Frame& f = J.f;
-  const uint32_t nstreams = J.nstreams;
   JXG_HIP(hipMemcpyAsync(c->h_hist_ac.p, hist, kMaxClusters * kAlpha * 4, hipMemcpyDeviceToHost, s));
   JXG_HIP(hipMemcpyAsync(c->h_bound.p, c->bound.p, f.ngroups * 4, hipMemcpyDeviceToHost, s));
   JXG_HIP(hipMemcpyAsync(c->h_ntok.p, c->ntok.p, f.ngroups * 12, hipMemcpyDeviceToHost, s));
+  JXG_HIP(hipEventRecord(c->ev[6], s));
+  return JXG_OK;
+}
+static jxg_status stage_download_lf(Ctx* c, Job& J) {
+  hipStream_t s = c->stream;
+  const Frame& f = J.f;
+  const uint32_t nstreams = J.nstreams;
   JXG_HIP(hipMemcpyAsync(c->h_lfhist.p, c->lfhist.p, (size_t)nstreams * 4 * kAlpha * 4, hipMemcpyDeviceToHost, s));
   JXG_HIP(hipMemcpyAsync(c->h_sbound.p, c->sbound.p, nstreams * 4, hipMemcpyDeviceToHost, s));
   JXG_HIP(hipMemcpyAsync(c->h_vcount.p, c->vcount.p, f.nlf * 4, hipMemcpyDeviceToHost, s));
   JXG_HIP(hipEventRecord(c->ev[2], s));
-  JXG_HIP(hipStreamSynchronize(s));
   return JXG_OK;
 }
 
@@ -820,6 +830,7 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
   hipStream_t s = c->stream;
   const Frame& f = J.f;
   const uint32_t nstreams = J.nstreams;
+  JXG_HIP(hipEventSynchronize(c->ev[6]));  // AC statistics on the host; LF kernels may still run
   const Clock::time_point t_codes = Clock::now();
   // prefix codes: one histogram per (used) static cluster; ANS: the static
   // clusters are clustered again into <= kAnsMaxHists groups (the alias
@@ -888,31 +899,7 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
       for (int k = 0; k < kAlpha; k++) packed[cl * kAlpha + k] = codes[h].packed(k);
     }
   }
-  // LF-group stream codes and preludes (the plan's LF groups)
-  std::vector<uint32_t> lfpacked((size_t)nstreams * 4 * kAlpha, 0);
-  J.preA.assign(f.nlf, BitWriter());
-  J.preB.assign(f.nlf, BitWriter());
-  for (uint32_t lg = 0; lg < f.nlf; lg++) {
-    if (!J.plan.owns_lf(lg)) continue;
-    const uint32_t bx0 = (lg % f.lfxs) * 256, by0 = (lg / f.lfxs) * 256;
-    const uint32_t bw = std::min(256u, f.bxs - bx0), bh = std::min(256u, f.bys - by0);
-    for (int sidx = 0; sidx < 2; sidx++) {
-      const uint32_t sid = lg * 2 + sidx;
-      const int nleaves = sidx == 0 ? 3 : 4;
-      std::vector<PrefixCode> lc(nleaves);
-      for (int l = 0; l < nleaves; l++) {
-        lc[l] = build_prefix_code(c->h_lfhist.p + ((size_t)sid * 4 + l) * kAlpha, kAlpha);
-        for (int k = 0; k < kAlpha; k++) lfpacked[((size_t)sid * 4 + l) * kAlpha + k] = lc[l].packed(k);
-      }
-      if (sidx == 0) {
-        J.preA[lg].put(2, 0);  // extra_precision
-        write_modular_prelude(J.preA[lg], kDcTree, 5, 3, lc);
-      } else {
-        J.preB[lg].put(ceil_log2(bw * bh), c->h_vcount.p[lg] - 1);  // varblock count - 1
-        write_modular_prelude(J.preB[lg], kMetaTree, 7, 4, lc);
-      }
-    }
-  }
+  // LfGlobal / HfGlobal (rank 0): need the AC codes only
   J.lfglobal = BitWriter();
   J.hfglobal = BitWriter();
   if (J.plan.rank == 0) {
@@ -952,9 +939,10 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
     else
       write_histograms(hfglobal, ctxmap, nhist, codes, kCfg420, &c->cm_bits);
   }
-  // scratch layout: the plan's AC groups then LF streams (32-bit aligned)
+  // AC layout: the plan's groups in the scratch arena (32-bit aligned); the AC
+  // emission is launched at once and runs while the host builds the LF-group
+  // codes below
   J.gbase.assign(f.ngroups, 0);
-  J.sbase.assign(nstreams, 0);
   uint64_t cursor = 0;
   for (uint32_t g = J.plan.g0; g < J.plan.g1; g++) {
     J.gbase[g] = cursor;
@@ -963,37 +951,27 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
     const uint64_t bound = (uint64_t)c->h_bound.p[g] + (J.ans ? nt + 32 : 0);
     cursor += (bound + 63) & ~31ull;
   }
-  for (uint32_t i = 0; i < nstreams; i++) {
-    J.sbase[i] = cursor;
-    if (J.plan.owns_lf(i / 2)) cursor += ((uint64_t)c->h_sbound.p[i] + 63) & ~31ull;
-  }
-  const uint64_t scratch_words = cursor / 32 + 2;
-  J.ms_codes = ms_since(t_codes);
-  JXG_HIP(c->scratch.ensure(scratch_words));
+  const uint64_t ac_words = cursor / 32 + 2;
+  JXG_HIP(c->scratch.ensure(ac_words));
+  // pinned upload sources: valid until the next frame's stage_codes, which
+  // runs after this frame's emission has completed
+  JXG_HIP(c->h_codes_ac.ensure(packed.size()));
+  std::copy(packed.begin(), packed.end(), c->h_codes_ac.p);
+  JXG_HIP(c->h_gbase.ensure(J.gbase.size()));
+  std::copy(J.gbase.begin(), J.gbase.end(), c->h_gbase.p);
   if (J.ans) {
     const uint64_t nrec = (uint64_t)(J.plan.g1 - J.plan.g0) * kGroupTokStride;
     JXG_HIP(c->tval.ensure(nrec));
     JXG_HIP(c->tlen.ensure(nrec));
     JXG_HIP(c->ans_state.ensure(f.ngroups));
     JXG_HIP(c->ans_tab.ensure(kAnsTabBytes));
-    // pinned source: stays valid until the next frame's stage_codes, which
-    // runs after this frame's emission has completed
     JXG_HIP(hipMemcpyAsync(c->ans_tab.p, c->h_ans_tab.p, kAnsTabBytes, hipMemcpyHostToDevice, s));
   }
-  JXG_HIP(hipMemcpyAsync(c->codes_ac.p, packed.data(), packed.size() * 4, hipMemcpyHostToDevice, s));
-  JXG_HIP(hipMemcpyAsync(c->lfcodes.p, lfpacked.data(), lfpacked.size() * 4, hipMemcpyHostToDevice, s));
-  JXG_HIP(hipMemcpyAsync(c->gbase.p, J.gbase.data(), J.gbase.size() * 8, hipMemcpyHostToDevice, s));
-  JXG_HIP(hipMemcpyAsync(c->stream_base.p, J.sbase.data(), J.sbase.size() * 8, hipMemcpyHostToDevice, s));
-  JXG_HIP(hipMemsetAsync(c->scratch.p, 0, scratch_words * 4, s));
-  return JXG_OK;
-}
-
-// ---- stage G: bit emission ----
-static jxg_status stage_emit(Ctx* c, Job& J) {
-  hipStream_t s = c->stream;
-  const Frame& f = J.f;
+  JXG_HIP(hipMemcpyAsync(c->codes_ac.p, c->h_codes_ac.p, packed.size() * 4, hipMemcpyHostToDevice, s));
+  JXG_HIP(hipMemcpyAsync(c->gbase.p, c->h_gbase.p, J.gbase.size() * 8, hipMemcpyHostToDevice, s));
+  JXG_HIP(hipMemsetAsync(c->scratch.p, 0, ac_words * 4, s));
+  const float ms_ac_codes = ms_since(t_codes);
   J.aa.scratch = c->scratch.p;
-  J.la.scratch = c->scratch.p;
   if (J.ans) {
     AnsArgs na{};
     na.tokens = c->tokens.p;
@@ -1012,11 +990,66 @@ static jxg_status stage_emit(Ctx* c, Job& J) {
   } else {
     launch_ac_emit(J.aa, J.plan.g1 - J.plan.g0, s);
   }
+  JXG_HIP(hipGetLastError());
+  JXG_HIP(hipMemcpyAsync(c->h_gbits.p, c->gbits.p, f.ngroups * 4, hipMemcpyDeviceToHost, s));
+
+  // LF-group stream codes and preludes (the plan's LF groups)
+  JXG_HIP(hipEventSynchronize(c->ev[2]));  // LF statistics (stage_download_lf)
+  const Clock::time_point t_lf = Clock::now();
+  const size_t nlfcodes = (size_t)nstreams * 4 * kAlpha;
+  JXG_HIP(c->h_lfcodes.ensure(nlfcodes));
+  uint32_t* lfpacked = c->h_lfcodes.p;
+  std::fill(lfpacked, lfpacked + nlfcodes, 0u);
+  J.preA.assign(f.nlf, BitWriter());
+  J.preB.assign(f.nlf, BitWriter());
+  for (uint32_t lg = 0; lg < f.nlf; lg++) {
+    if (!J.plan.owns_lf(lg)) continue;
+    const uint32_t bx0 = (lg % f.lfxs) * 256, by0 = (lg / f.lfxs) * 256;
+    const uint32_t bw = std::min(256u, f.bxs - bx0), bh = std::min(256u, f.bys - by0);
+    for (int sidx = 0; sidx < 2; sidx++) {
+      const uint32_t sid = lg * 2 + sidx;
+      const int nleaves = sidx == 0 ? 3 : 4;
+      std::vector<PrefixCode> lc(nleaves);
+      for (int l = 0; l < nleaves; l++) {
+        lc[l] = build_prefix_code(c->h_lfhist.p + ((size_t)sid * 4 + l) * kAlpha, kAlpha);
+        for (int k = 0; k < kAlpha; k++) lfpacked[((size_t)sid * 4 + l) * kAlpha + k] = lc[l].packed(k);
+      }
+      if (sidx == 0) {
+        J.preA[lg].put(2, 0);  // extra_precision
+        write_modular_prelude(J.preA[lg], kDcTree, 5, 3, lc);
+      } else {
+        J.preB[lg].put(ceil_log2(bw * bh), c->h_vcount.p[lg] - 1);  // varblock count - 1
+        write_modular_prelude(J.preB[lg], kMetaTree, 7, 4, lc);
+      }
+    }
+  }
+  // LF layout: the plan's LF streams in their own arena (32-bit aligned)
+  J.sbase.assign(nstreams, 0);
+  cursor = 0;
+  for (uint32_t i = 0; i < nstreams; i++) {
+    J.sbase[i] = cursor;
+    if (J.plan.owns_lf(i / 2)) cursor += ((uint64_t)c->h_sbound.p[i] + 63) & ~31ull;
+  }
+  const uint64_t lf_words = cursor / 32 + 2;
+  JXG_HIP(c->scratch_lf.ensure(lf_words));
+  JXG_HIP(c->h_sbase.ensure(J.sbase.size()));
+  std::copy(J.sbase.begin(), J.sbase.end(), c->h_sbase.p);
+  JXG_HIP(hipMemcpyAsync(c->lfcodes.p, lfpacked, nlfcodes * 4, hipMemcpyHostToDevice, s));
+  JXG_HIP(hipMemcpyAsync(c->stream_base.p, c->h_sbase.p, J.sbase.size() * 8, hipMemcpyHostToDevice, s));
+  JXG_HIP(hipMemsetAsync(c->scratch_lf.p, 0, lf_words * 4, s));
+  J.ms_codes = ms_ac_codes + ms_since(t_lf);
+  return JXG_OK;
+}
+
+// ---- stage G: LF-stream bit emission (the AC emission was launched by
+// stage_codes), bit counts to the host ----
+static jxg_status stage_emit(Ctx* c, Job& J) {
+  hipStream_t s = c->stream;
+  J.la.scratch = c->scratch_lf.p;
   if (J.nchunks) launch_lf_bits(J.la, J.nchunks, s);
   launch_lf_scan(J.la, J.nstreams, s);
   if (J.nchunks) launch_lf_emit(J.la, J.nchunks, s);
   JXG_HIP(hipGetLastError());
-  JXG_HIP(hipMemcpyAsync(c->h_gbits.p, c->gbits.p, f.ngroups * 4, hipMemcpyDeviceToHost, s));
   JXG_HIP(hipMemcpyAsync(c->h_sbits.p, c->stream_bits.p, J.nstreams * 4, hipMemcpyDeviceToHost, s));
   JXG_HIP(hipEventRecord(c->ev[3], s));
   JXG_HIP(hipStreamSynchronize(s));
@@ -1028,7 +1061,7 @@ static jxg_status stage_emit(Ctx* c, Job& J) {
 // one codestream; shard: the plan's sections, each byte-aligned, back to back
 // (`section_ids` receives their TOC indices) ----
 struct Piece {
-  int arena;  // 0 scratch, 1 host chunk
+  int arena;  // 0 AC scratch, 1 host chunk, 2 LF scratch
   uint64_t src, nbits;
 };
 static jxg_status stage_concat(Ctx* c, Job& J, bool full, std::vector<uint32_t>* section_ids,
@@ -1051,9 +1084,9 @@ static jxg_status stage_concat(Ctx* c, Job& J, bool full, std::vector<uint32_t>*
   }
   for (uint32_t lg = 0; lg < f.nlf; lg++) {
     if (!J.plan.owns_lf(lg)) continue;
-    sections.push_back({add_chunk(J.preA[lg]), Piece{0, J.sbase[lg * 2], c->h_sbits.p[lg * 2]},
+    sections.push_back({add_chunk(J.preA[lg]), Piece{2, J.sbase[lg * 2], c->h_sbits.p[lg * 2]},
                         add_chunk(J.preB[lg]),
-                        Piece{0, J.sbase[lg * 2 + 1], c->h_sbits.p[lg * 2 + 1]}});
+                        Piece{2, J.sbase[lg * 2 + 1], c->h_sbits.p[lg * 2 + 1]}});
     ids.push_back(1 + lg);
   }
   if (J.plan.rank == 0) {
@@ -1113,7 +1146,8 @@ static jxg_status stage_concat(Ctx* c, Job& J, bool full, std::vector<uint32_t>*
   if (!cps.empty())
     JXG_HIP(hipMemcpyAsync(c->pieces.p, cps.data(), cps.size() * sizeof(ConcatPiece), hipMemcpyHostToDevice, s));
   JXG_HIP(hipMemsetAsync(c->out.p, 0, out_words * 4, s));
-  launch_concat(c->pieces.p, (uint32_t)cps.size(), max_words, c->scratch.p, c->chunks.p, c->out.p, s);
+  launch_concat(c->pieces.p, (uint32_t)cps.size(), max_words, c->scratch.p, c->chunks.p,
+                c->scratch_lf.p, c->out.p, s);
   JXG_HIP(hipGetLastError());
   if (ho && hipMemcpyAsync(ho, c->out.p, out_words * 4, hipMemcpyDeviceToHost, s) != hipSuccess) {
     out_release(ho);
@@ -1146,8 +1180,9 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   if ((st = stage_front(c, J))) return st;
   JXG_HIP(hipEventRecord(c->ev[1], s));
   if ((st = stage_ac_stats(c, J))) return st;
+  if ((st = stage_download_ac(c, J, c->hist_ac.p))) return st;
   if ((st = stage_lf_stats(c, J))) return st;
-  if ((st = stage_download(c, J, c->hist_ac.p))) return st;
+  if ((st = stage_download_lf(c, J))) return st;
   if ((st = stage_codes(c, J))) return st;
   if ((st = stage_emit(c, J))) return st;
   const Clock::time_point t_layout = Clock::now();
@@ -1263,8 +1298,9 @@ static jxg_status shard_end(Ctx* c, const uint32_t* d_hist, const uint8_t* d_xbu
   launch_unpack(pa, s);
   JXG_HIP(hipGetLastError());
   jxg_status st;
+  if ((st = stage_download_ac(c, J, d_hist))) return st;
   if ((st = stage_lf_stats(c, J))) return st;
-  if ((st = stage_download(c, J, d_hist))) return st;
+  if ((st = stage_download_lf(c, J))) return st;
   if ((st = stage_codes(c, J))) return st;
   if ((st = stage_emit(c, J))) return st;
   std::vector<uint32_t> ids, sizes;
@@ -1429,7 +1465,7 @@ static jxg_status shard_assemble_device(Ctx* c, const uint8_t* d_base, const siz
   JXG_HIP(hipMemsetAsync(c->out.p, 0, out_words * 4, s));
   // arena 0 = the payload base (word aligned: offsets are multiples of 4)
   launch_concat(c->pieces.p, (uint32_t)cps.size(), max_words,
-                reinterpret_cast<const uint32_t*>(d_base), c->chunks.p, c->out.p, s);
+                reinterpret_cast<const uint32_t*>(d_base), c->chunks.p, nullptr, c->out.p, s);
   JXG_HIP(hipGetLastError());
   if (hipMemcpyAsync(ho, c->out.p, out_words * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess) {

@@ -168,7 +168,7 @@ struct ConcatPiece {
   uint64_t src_bit;  // bit offset into the source arena
   uint64_t dst_bit;  // bit offset into the output
   uint64_t nbits;
-  uint32_t arena;    // 0 = device scratch, 1 = host-chunk upload
+  uint32_t arena;    // 0 = device scratch, 1 = host-chunk upload, 2 = second scratch
   uint32_t pad;
 };
 
@@ -214,7 +214,7 @@ uint32_t ssim_partials(uint32_t w, uint32_t h);
 void set_gauss_table(const double* g, hipStream_t s);
 void launch_metrics(const MetricArgs& a, hipStream_t s);
 void launch_concat(const ConcatPiece* pieces, uint32_t npieces, uint64_t max_words,
-                   const uint32_t* scratch, const uint32_t* chunks, uint32_t* out,
-                   hipStream_t s);
+                   const uint32_t* scratch, const uint32_t* chunks, const uint32_t* scratch2,
+                   uint32_t* out, hipStream_t s);
 
 }  // namespace jxg
