@@ -129,8 +129,28 @@ static uint8_t* out_alloc_heap(size_t bytes) {
   return static_cast<uint8_t*>(p) + kOutHdr;
 }
 
+// A codestream assembled at an offset inside its block (stage_concat_split:
+// the AC block is copied first, the prefix lands right before it) carries a
+// back reference to the block's data start in the kOutHdr bytes before it.
+constexpr uint64_t kOutBackMagic = 0x6a7867426b526566ull;  // "jxgBkRef"
+struct OutBackRef {
+  uint64_t magic;
+  uint8_t* data0;
+};
+static void out_set_backref(uint8_t* data, uint8_t* data0) {
+  if (data == data0) return;
+  OutBackRef* r = reinterpret_cast<OutBackRef*>(data - kOutHdr);
+  r->magic = kOutBackMagic;
+  r->data0 = data0;
+}
+
 static void out_release(uint8_t* data) {
   if (!data) return;
+  if (reinterpret_cast<OutBackRef*>(data - kOutHdr)->magic == kOutBackMagic) {
+    OutBackRef* r = reinterpret_cast<OutBackRef*>(data - kOutHdr);
+    r->magic = 0;
+    data = r->data0;
+  }
   uint8_t* b = data - kOutHdr;
   if (reinterpret_cast<OutHeader*>(b)->magic != kOutMagic) return;  // not ours
   if (reinterpret_cast<OutHeader*>(b)->heap) {
@@ -409,7 +429,10 @@ static MergeTables build_merge_tables() {
 struct Ctx {
   jxg_params params{};
   hipStream_t stream = nullptr;
-  hipEvent_t ev[7] = {};  // ev[6]: AC statistics downloaded (stage_download_ac)
+  hipStream_t stream2 = nullptr;  // AC-block concat + D2H (stage_concat_split)
+  // ev[6]: AC statistics downloaded (stage_download_ac); ev[7]: AC emission
+  // done and its bit counts on the host; ev[8]: AC block in host memory
+  hipEvent_t ev[9] = {};
   bool constants_ready = false;
   // device
   DevBuf<uint8_t> rgb, acs, qf;
@@ -421,7 +444,7 @@ struct Ctx {
   DevBuf<float> homog, xyb, r3;
   DevBuf<uint8_t> type;
   DevBuf<uint32_t> hist_ac, bound, ntok, codes_ac, gbits, lfhist, sbound, lfcodes, chunkbits,
-      stream_chunks, stream_bits, scratch, scratch_lf, chunks, out;
+      stream_chunks, stream_bits, scratch, scratch_lf, chunks, out, out_ac;
   DevBuf<uint64_t> gbase, chunkoff, stream_base;
   DevBuf<uint32_t> tile_list;
   DevBuf<uint32_t> tokens, tval, ans_state;  // ANS coder
@@ -434,7 +457,8 @@ struct Ctx {
   DevBuf<uint64_t> q_sse;
   DevBuf<double> q_part, q_ssim;
   bool gauss_ready = false;
-  DevBuf<ConcatPiece> pieces;
+  DevBuf<ConcatPiece> pieces, pieces_ac;
+  PinBuf<ConcatPiece> h_pieces_ac;
   // host
   PinBuf<uint32_t> h_hist_ac, h_bound, h_ntok, h_lfhist, h_sbound, h_gbits, h_sbits, h_vcount,
       h_codes_ac, h_lfcodes;
@@ -582,6 +606,7 @@ struct Job {
   BitWriter lfglobal, hfglobal;
   std::vector<uint64_t> gbase, sbase;
   float ms_codes = 0.0f;
+  float ms_layout = 0.0f;  // stage_concat_split host layout
 };
 
 // ---- stage A: buffers for the frame / plan ----
@@ -992,6 +1017,7 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
   }
   JXG_HIP(hipGetLastError());
   JXG_HIP(hipMemcpyAsync(c->h_gbits.p, c->gbits.p, f.ngroups * 4, hipMemcpyDeviceToHost, s));
+  JXG_HIP(hipEventRecord(c->ev[7], s));
 
   // LF-group stream codes and preludes (the plan's LF groups)
   JXG_HIP(hipEventSynchronize(c->ev[2]));  // LF statistics (stage_download_lf)
@@ -1043,7 +1069,7 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
 
 // ---- stage G: LF-stream bit emission (the AC emission was launched by
 // stage_codes), bit counts to the host ----
-static jxg_status stage_emit(Ctx* c, Job& J) {
+static jxg_status stage_emit(Ctx* c, Job& J, bool sync = true) {
   hipStream_t s = c->stream;
   J.la.scratch = c->scratch_lf.p;
   if (J.nchunks) launch_lf_bits(J.la, J.nchunks, s);
@@ -1052,7 +1078,7 @@ static jxg_status stage_emit(Ctx* c, Job& J) {
   JXG_HIP(hipGetLastError());
   JXG_HIP(hipMemcpyAsync(c->h_sbits.p, c->stream_bits.p, J.nstreams * 4, hipMemcpyDeviceToHost, s));
   JXG_HIP(hipEventRecord(c->ev[3], s));
-  JXG_HIP(hipStreamSynchronize(s));
+  if (sync) JXG_HIP(hipStreamSynchronize(s));
   return JXG_OK;
 }
 
@@ -1161,6 +1187,136 @@ static jxg_status stage_concat(Ctx* c, Job& J, bool full, std::vector<uint32_t>*
   return JXG_OK;
 }
 
+// Full codestream of a multi-group frame with the AC block moved early: the
+// pass-group sections (the bulk of the bytes) are concatenated on stream2 as
+// soon as the AC emission is done and copied to the END region of the host
+// block while the LF streams are still being emitted; the prefix (headers,
+// TOC, LfGlobal, LF groups, HfGlobal) follows on the main stream and lands
+// right before it.  Same bytes as stage_concat(full).
+static jxg_status stage_concat_split(Ctx* c, Job& J, uint8_t** host_out, size_t* out_bytes) {
+  hipStream_t s = c->stream, s2 = c->stream2;
+  const Frame& f = J.f;
+  JXG_HIP(hipEventSynchronize(c->ev[7]));  // AC emission done, its bit counts on the host
+  const uint32_t g0 = J.plan.g0, ng = J.plan.g1 - J.plan.g0;
+  JXG_HIP(c->h_pieces_ac.ensure(std::max<uint32_t>(ng, 1)));
+  std::vector<uint32_t> ac_sizes(ng);
+  uint64_t dst = 0, max_words = 0;
+  uint32_t np = 0;
+  for (uint32_t i = 0; i < ng; i++) {
+    const uint64_t nb = c->h_gbits.p[g0 + i];
+    ac_sizes[i] = (uint32_t)((nb + 7) / 8);
+    if (nb) {
+      c->h_pieces_ac.p[np++] = {J.gbase[g0 + i], dst, nb, 0u, 0u};
+      max_words = std::max<uint64_t>(max_words, (nb + 31) / 32);
+    }
+    dst += (uint64_t)ac_sizes[i] * 8;
+  }
+  const size_t ac_bytes = (size_t)(dst / 8);
+  // prefix upper bound: chunks + LF stream bounds + headers / TOC + slack for
+  // the back reference
+  uint64_t pbits = J.lfglobal.bits() + J.hfglobal.bits() + 16;
+  for (uint32_t lg = 0; lg < f.nlf; lg++)
+    if (J.plan.owns_lf(lg))
+      pbits += J.preA[lg].bits() + J.preB[lg].bits() + c->h_sbound.p[lg * 2] +
+               c->h_sbound.p[lg * 2 + 1] + 8;
+  const size_t nsec = 2 + (size_t)f.nlf + f.ngroups;
+  size_t pmax = (size_t)(pbits / 8) + 256 + 4 * nsec + 16 + kOutHdr;
+  pmax = (pmax + 63) & ~(size_t)63;
+  uint8_t* ho = out_alloc(pmax + ac_bytes + 8);
+  if (!ho) return JXG_ERR_OOM;
+  auto fail = [&](jxg_status e) {
+    (void)hipStreamSynchronize(s2);
+    (void)hipStreamSynchronize(s);
+    out_release(ho);
+    return e;
+  };
+  const size_t ac_words = ac_bytes / 4 + 2;
+  if (c->out_ac.ensure(ac_words) != hipSuccess ||
+      c->pieces_ac.ensure(std::max<uint32_t>(np, 1)) != hipSuccess)
+    return fail(JXG_ERR_HIP);
+  if (hipStreamWaitEvent(s2, c->ev[7], 0) != hipSuccess ||
+      (np && hipMemcpyAsync(c->pieces_ac.p, c->h_pieces_ac.p, np * sizeof(ConcatPiece),
+                            hipMemcpyHostToDevice, s2) != hipSuccess) ||
+      hipMemsetAsync(c->out_ac.p, 0, ac_words * 4, s2) != hipSuccess)
+    return fail(JXG_ERR_HIP);
+  launch_concat(c->pieces_ac.p, np, max_words, c->scratch.p, c->chunks.p, nullptr, c->out_ac.p, s2);
+  if (hipGetLastError() != hipSuccess ||
+      (ac_bytes && hipMemcpyAsync(ho + pmax, c->out_ac.p, ac_bytes, hipMemcpyDeviceToHost, s2) !=
+                       hipSuccess) ||
+      hipEventRecord(c->ev[8], s2) != hipSuccess)
+    return fail(JXG_ERR_HIP);
+
+  // prefix, after the LF emission (stage_emit without its sync)
+  if (hipStreamSynchronize(s) != hipSuccess) return fail(JXG_ERR_HIP);
+  const Clock::time_point t_layout = Clock::now();
+  std::vector<std::vector<Piece>> sections;
+  std::vector<uint32_t> chunk_words;
+  auto add_chunk = [&](const BitWriter& bw) -> Piece {
+    Piece p{1, (uint64_t)chunk_words.size() * 32, bw.bits()};
+    auto wv = bw.words32();
+    chunk_words.insert(chunk_words.end(), wv.begin(), wv.end());
+    return p;
+  };
+  sections.push_back({add_chunk(J.lfglobal)});
+  for (uint32_t lg = 0; lg < f.nlf; lg++)
+    sections.push_back({add_chunk(J.preA[lg]), Piece{2, J.sbase[lg * 2], c->h_sbits.p[lg * 2]},
+                        add_chunk(J.preB[lg]),
+                        Piece{2, J.sbase[lg * 2 + 1], c->h_sbits.p[lg * 2 + 1]}});
+  sections.push_back({add_chunk(J.hfglobal)});
+  std::vector<uint32_t> sizes;
+  for (auto& sec : sections) {
+    uint64_t t = 0;
+    for (auto& p : sec) t += p.nbits;
+    sizes.push_back((uint32_t)((t + 7) / 8));
+  }
+  sizes.insert(sizes.end(), ac_sizes.begin(), ac_sizes.end());
+  std::vector<ConcatPiece> cps;
+  dst = 0;
+  max_words = 0;
+  auto emit_piece = [&](const Piece& p) {
+    if (p.nbits) {
+      cps.push_back({p.src, dst, p.nbits, (uint32_t)p.arena, 0});
+      max_words = std::max<uint64_t>(max_words, (p.nbits + 31) / 32);
+    }
+    dst += p.nbits;
+  };
+  BitWriter head;
+  write_headers(head, J.w, J.h);
+  write_toc(head, sizes);
+  emit_piece(add_chunk(head));
+  for (auto& sec : sections) {
+    for (auto& p : sec) emit_piece(p);
+    dst = (dst + 7) & ~7ull;
+  }
+  const size_t pbytes = (size_t)(dst / 8);
+  if (pbytes + kOutHdr > pmax) return fail(JXG_ERR_INTERNAL);  // bound violated
+  const size_t out_words = (pbytes + 3) / 4 + 1;
+  chunk_words.push_back(0);  // read-ahead guard
+  if (c->chunks.ensure(chunk_words.size()) != hipSuccess ||
+      c->pieces.ensure(std::max<size_t>(cps.size(), 1)) != hipSuccess ||
+      c->out.ensure(out_words) != hipSuccess)
+    return fail(JXG_ERR_HIP);
+  uint8_t* data = ho + pmax - pbytes;
+  if (hipMemcpyAsync(c->chunks.p, chunk_words.data(), chunk_words.size() * 4,
+                     hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(c->pieces.p, cps.data(), cps.size() * sizeof(ConcatPiece),
+                     hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemsetAsync(c->out.p, 0, out_words * 4, s) != hipSuccess)
+    return fail(JXG_ERR_HIP);
+  launch_concat(c->pieces.p, (uint32_t)cps.size(), max_words, c->scratch.p, c->chunks.p,
+                c->scratch_lf.p, c->out.p, s);
+  if (hipGetLastError() != hipSuccess ||
+      hipMemcpyAsync(data, c->out.p, pbytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamWaitEvent(s, c->ev[8], 0) != hipSuccess ||
+      hipEventRecord(c->ev[4], s) != hipSuccess)
+    return fail(JXG_ERR_HIP);
+  J.ms_layout = ms_since(t_layout);
+  out_set_backref(data, ho);
+  *host_out = data;
+  *out_bytes = pbytes + ac_bytes;
+  return JXG_OK;
+}
+
 static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32_t h,
                                 size_t stride, jxg_buffer* out, Clock::time_point t_call) {
   hipStream_t s = c->stream;
@@ -1184,12 +1340,17 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   if ((st = stage_lf_stats(c, J))) return st;
   if ((st = stage_download_lf(c, J))) return st;
   if ((st = stage_codes(c, J))) return st;
-  if ((st = stage_emit(c, J))) return st;
+  const bool split = f.ngroups > 1;  // single-group frames: one section (stage_concat)
+  if ((st = stage_emit(c, J, !split))) return st;
   const Clock::time_point t_layout = Clock::now();
   uint8_t* host_out = nullptr;
   size_t out_bytes = 0;
-  if ((st = stage_concat(c, J, true, nullptr, nullptr, &host_out, &out_bytes))) return st;
-  const float ms_layout = ms_since(t_layout);
+  if (split) {
+    if ((st = stage_concat_split(c, J, &host_out, &out_bytes))) return st;
+  } else {
+    if ((st = stage_concat(c, J, true, nullptr, nullptr, &host_out, &out_bytes))) return st;
+  }
+  const float ms_layout = split ? J.ms_layout : ms_since(t_layout);
   std::vector<int16_t> m_ac16_tmp;
   if (P.flags & JXG_FLAG_KEEP_MAPS) {
     c->m_acs.resize(nb);
@@ -1611,7 +1772,8 @@ jxg_status jxg_create(const jxg_params* params, void** out) {
   Ctx* c = new (std::nothrow) Ctx();
   if (!c) return JXG_ERR_OOM;
   c->params = *params;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return JXG_ERR_HIP;
   }
@@ -1635,6 +1797,7 @@ void jxg_destroy(void* ctx) {
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->stream2) (void)hipStreamDestroy(c->stream2);
   delete c;
 }
 
