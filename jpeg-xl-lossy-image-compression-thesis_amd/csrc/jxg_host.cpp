@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -483,6 +484,11 @@ struct Ctx {
 };
 
 static std::mutex g_const_mu;  // device __constant__ tables are shared by all contexts
+// Live contexts of the process.  A HIP process has 4 hardware queues
+// (GPU_MAX_HW_QUEUES); with several contexts their second streams would
+// share queues with other contexts' main streams, so the split assembly
+// (stage_concat_split, second stream) is used by a lone context only.
+static std::atomic<int> g_live_ctx{0};
 static jxg_status init_constants(Ctx* c) {
   if (c->constants_ready) return JXG_OK;
   std::lock_guard<std::mutex> lock(g_const_mu);
@@ -997,27 +1003,14 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
   JXG_HIP(hipMemsetAsync(c->scratch.p, 0, ac_words * 4, s));
   const float ms_ac_codes = ms_since(t_codes);
   J.aa.scratch = c->scratch.p;
-  if (J.ans) {
-    AnsArgs na{};
-    na.tokens = c->tokens.p;
-    na.val = c->tval.p;
-    na.len = c->tlen.p;
-    na.ntok = c->ntok.p;
-    na.tab = c->ans_tab.p;
-    na.nhist = J.nhist_ans;
-    na.state = c->ans_state.p;
-    na.base = c->gbase.p;
-    na.scratch = c->scratch.p;
-    na.bits = c->gbits.p;
-    na.g0 = J.plan.g0;
-    na.g1 = J.plan.g1;
-    launch_ans(na, s);
-  } else {
+  if (!J.ans) {
     launch_ac_emit(J.aa, J.plan.g1 - J.plan.g0, s);
+    JXG_HIP(hipGetLastError());
+    JXG_HIP(hipMemcpyAsync(c->h_gbits.p, c->gbits.p, f.ngroups * 4, hipMemcpyDeviceToHost, s));
+    JXG_HIP(hipEventRecord(c->ev[7], s));
   }
-  JXG_HIP(hipGetLastError());
-  JXG_HIP(hipMemcpyAsync(c->h_gbits.p, c->gbits.p, f.ngroups * 4, hipMemcpyDeviceToHost, s));
-  JXG_HIP(hipEventRecord(c->ev[7], s));
+  // (the rANS coder -- a long latency-bound chain that hides the LF-code
+  // construction anyway -- is launched by stage_emit)
 
   // LF-group stream codes and preludes (the plan's LF groups)
   JXG_HIP(hipEventSynchronize(c->ev[2]));  // LF statistics (stage_download_lf)
@@ -1067,10 +1060,30 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
   return JXG_OK;
 }
 
-// ---- stage G: LF-stream bit emission (the AC emission was launched by
-// stage_codes), bit counts to the host ----
+// ---- stage G: rANS coder (the prefix-code AC emission was launched by
+// stage_codes), LF-stream bit emission, bit counts to the host ----
 static jxg_status stage_emit(Ctx* c, Job& J, bool sync = true) {
   hipStream_t s = c->stream;
+  const Frame& f = J.f;
+  if (J.ans) {
+    AnsArgs na{};
+    na.tokens = c->tokens.p;
+    na.val = c->tval.p;
+    na.len = c->tlen.p;
+    na.ntok = c->ntok.p;
+    na.tab = c->ans_tab.p;
+    na.nhist = J.nhist_ans;
+    na.state = c->ans_state.p;
+    na.base = c->gbase.p;
+    na.scratch = c->scratch.p;
+    na.bits = c->gbits.p;
+    na.g0 = J.plan.g0;
+    na.g1 = J.plan.g1;
+    launch_ans(na, s);
+    JXG_HIP(hipGetLastError());
+    JXG_HIP(hipMemcpyAsync(c->h_gbits.p, c->gbits.p, f.ngroups * 4, hipMemcpyDeviceToHost, s));
+    JXG_HIP(hipEventRecord(c->ev[7], s));
+  }
   J.la.scratch = c->scratch_lf.p;
   if (J.nchunks) launch_lf_bits(J.la, J.nchunks, s);
   launch_lf_scan(J.la, J.nstreams, s);
@@ -1194,6 +1207,8 @@ static jxg_status stage_concat(Ctx* c, Job& J, bool full, std::vector<uint32_t>*
 // TOC, LfGlobal, LF groups, HfGlobal) follows on the main stream and lands
 // right before it.  Same bytes as stage_concat(full).
 static jxg_status stage_concat_split(Ctx* c, Job& J, uint8_t** host_out, size_t* out_bytes) {
+  if (!c->stream2 && hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess)
+    return JXG_ERR_HIP;  // created on first use: only lone contexts take this path
   hipStream_t s = c->stream, s2 = c->stream2;
   const Frame& f = J.f;
   JXG_HIP(hipEventSynchronize(c->ev[7]));  // AC emission done, its bit counts on the host
@@ -1340,7 +1355,9 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   if ((st = stage_lf_stats(c, J))) return st;
   if ((st = stage_download_lf(c, J))) return st;
   if ((st = stage_codes(c, J))) return st;
-  const bool split = f.ngroups > 1;  // single-group frames: one section (stage_concat)
+  // split assembly for a single context of a multi-group frame (single-group
+  // frames are one section; several contexts keep the one-stream assembly)
+  const bool split = f.ngroups > 1 && g_live_ctx.load() <= 1;
   if ((st = stage_emit(c, J, !split))) return st;
   const Clock::time_point t_layout = Clock::now();
   uint8_t* host_out = nullptr;
@@ -1772,8 +1789,7 @@ jxg_status jxg_create(const jxg_params* params, void** out) {
   Ctx* c = new (std::nothrow) Ctx();
   if (!c) return JXG_ERR_OOM;
   c->params = *params;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return JXG_ERR_HIP;
   }
@@ -1782,6 +1798,7 @@ jxg_status jxg_create(const jxg_params* params, void** out) {
       delete c;
       return JXG_ERR_HIP;
     }
+  g_live_ctx++;
   *out = c;
   return JXG_OK;
 }
@@ -1791,6 +1808,8 @@ void jxg_destroy(void* ctx) {
   Ctx* c = static_cast<Ctx*>(ctx);
   (void)hipSetDevice(c->params.device);
   (void)hipStreamSynchronize(c->stream);
+  if (c->stream2) (void)hipStreamSynchronize(c->stream2);
+  g_live_ctx--;
 #ifdef JXG_MERGE_PROFILE
   dump_merge_profile();
 #endif

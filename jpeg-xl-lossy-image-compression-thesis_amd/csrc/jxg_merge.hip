@@ -804,40 +804,59 @@ void merge_write_kernel(MergeArgs a) {
 // varblock lists of the LF groups (AC metadata channel of size count x 2):
 // block indices of the varblocks' first blocks in LF-group raster order
 // ---------------------------------------------------------------------------
+// Varblock list of one LF group: the frame-raster block index of every
+// varblock's first block, in raster order inside the LF group.  Thread t
+// holds the first-block flags of blocks t, t + 1024, ... (all 64 loads in
+// flight at once); per-(chunk, wave) counts -> one workgroup scan -> stores.
 __global__ __launch_bounds__(1024) void vb_list_kernel(VbArgs a) {
+  __shared__ uint32_t sCnt[64 * 16];
   __shared__ uint32_t sWave[16];
-  __shared__ uint32_t sBase;
   const uint32_t lg = blockIdx.x;
   if (a.world > 1 && lg % a.world != a.rank) return;  // LF group of another shard
   const uint32_t bx0 = (lg % a.lfxs) * 256, by0 = (lg / a.lfxs) * 256;
   const uint32_t bw = min(256u, a.bxs - bx0), bh = min(256u, a.bys - by0);
   const uint32_t n = bw * bh;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (threadIdx.x == 0) sBase = 0;
-  __syncthreads();
-  for (uint32_t c0 = 0; c0 < n; c0 += 1024) {
-    const uint32_t i = c0 + threadIdx.x;
-    size_t b = 0;
-    uint32_t f = 0;
-    if (i < n) {
-      b = (size_t)(by0 + i / bw) * a.bxs + bx0 + i % bw;
-      f = (a.acs[b] & 0x80) ? 0u : 1u;
-    }
-    const uint64_t bal = __ballot(f);
-    const uint32_t below = (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
-    if (lane == 0) sWave[wv] = (uint32_t)__popcll(bal);
-    __syncthreads();
-    uint32_t before = sBase, tot = 0;
-    for (int w = 0; w < 16; w++) {
-      before += w < wv ? sWave[w] : 0u;
-      tot += sWave[w];
-    }
-    if (f) a.vb[(size_t)lg * 65536 + before + below] = (uint32_t)b;
-    __syncthreads();
-    if (threadIdx.x == 0) sBase += tot;
-    __syncthreads();
+  const uint64_t lt = (1ull << lane) - 1ull;
+  auto block_of = [&](uint32_t i) {
+    return (size_t)(by0 + i / bw) * a.bxs + bx0 + i % bw;
+  };
+  uint64_t fl = 0;  // bit k: block k * 1024 + threadIdx.x starts a varblock
+#pragma unroll 16
+  for (int k = 0; k < 64; k++) {
+    const uint32_t i = (uint32_t)k * 1024 + threadIdx.x;
+    if (i < n && !(a.acs[block_of(i)] & 0x80)) fl |= 1ull << k;
   }
-  if (threadIdx.x == 0) a.count[lg] = sBase;
+  for (int k = 0; k < 64; k++) {
+    const uint64_t bal = __ballot((fl >> k) & 1);
+    if (lane == 0) sCnt[k * 16 + wv] = (uint32_t)__popcll(bal);
+  }
+  __syncthreads();
+  // exclusive scan of the 1024 (chunk, wave) counts in (chunk, wave) order
+  const uint32_t v = sCnt[threadIdx.x];
+  uint32_t incl = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t t = __shfl_up(incl, d);
+    if (lane >= d) incl += t;
+  }
+  if (lane == 63) sWave[wv] = incl;
+  __syncthreads();
+  uint32_t before = 0, total = 0;
+  for (int w = 0; w < 16; w++) {
+    before += w < wv ? sWave[w] : 0u;
+    total += sWave[w];
+  }
+  sCnt[threadIdx.x] = before + incl - v;
+  __syncthreads();
+  for (int k = 0; k < 64; k++) {
+    const bool f = (fl >> k) & 1;
+    const uint64_t bal = __ballot(f);
+    if (f)
+      a.vb[(size_t)lg * 65536 + sCnt[k * 16 + wv] + (uint32_t)__popcll(bal & lt)] =
+          (uint32_t)block_of((uint32_t)k * 1024 + threadIdx.x);
+  }
+  if (threadIdx.x == 0) a.count[lg] = total;
 }
 
 #ifdef JXG_MERGE_PROFILE
