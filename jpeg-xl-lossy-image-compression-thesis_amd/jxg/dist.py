@@ -8,7 +8,7 @@ collectives are
   2. all_gather of the per-block records (strategy, quant field, quantized DC;
      14 B per 8x8 block) that the LF-group streams of other ranks read,
   3. assembly, either
-     host   (``host=SharedHostBuffer``): an all-gather of the payload heads
+     host   (``host=SharedHostBuffer``): one all-gather of the payload heads
             (section ids and sizes, ~2 KB per rank), then every rank DMAs its
             own sections into one /dev/shm buffer shared by the node's ranks
             at their codestream offsets (rank 0 adds headers + TOC) -- the
@@ -89,19 +89,29 @@ class SharedHostBuffer:
         self.cap = 0
 
 
-def _all_gather_heads(head: np.ndarray, rank: int, world: int, group=None):
-    """Variable-length u32 heads of all ranks (rank order), on every rank."""
+def _head_cap(width: int, height: int) -> int:
+    """Upper bound of a payload head in u32 words: 7 + 2 x sections, a rank
+    holding at most LfGlobal, HfGlobal, every LF group and every pass group."""
+    nlf = -(-width // 2048) * -(-height // 2048)
+    ngroups = -(-width // 256) * -(-height // 256)
+    return 7 + 2 * (2 + nlf + ngroups)
+
+
+def _all_gather_heads(head: np.ndarray, rank: int, world: int, width: int, height: int,
+                      group=None):
+    """Variable-length u32 payload heads of all ranks (rank order), on every
+    rank, with ONE all-gather of fixed-capacity slots (no size exchange): a
+    head's own length is 7 + 2 x its section count (word 6)."""
     dev = "cpu" if dist.get_backend(group) == "gloo" else torch.device("cuda", torch.cuda.current_device())
-    n = torch.tensor([head.size], dtype=torch.int64, device=dev)
-    ns = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(ns, n, group=group)
-    ns = [int(x.item()) for x in ns]
-    cap = max(ns)
+    cap = _head_cap(width, height)
+    if head.size > cap or head.size < 7:
+        raise RuntimeError("payload head of %d words outside [7, %d]" % (head.size, cap))
     mine = torch.zeros(cap, dtype=torch.int32, device=dev)
     mine[:head.size] = torch.from_numpy(head.view(np.int32).copy()).to(dev)
     parts = [torch.empty(cap, dtype=torch.int32, device=dev) for _ in range(world)]
     dist.all_gather(parts, mine, group=group)
-    return [p[:k].cpu().numpy().view(np.uint32) for p, k in zip(parts, ns)]
+    allh = torch.stack(parts).cpu().numpy().view(np.uint32)  # one copy to the host
+    return [allh[r, :7 + 2 * int(allh[r, 6])].copy() for r in range(world)]
 
 
 def gather_payloads(payload: bytes, rank: int, world: int, device, group=None):
@@ -161,7 +171,7 @@ def encode_sharded(enc: Encoder, d_rgb: torch.Tensor, width: int, height: int, r
     torch.cuda.synchronize(dev)  # the library's stream reads what the collectives wrote
     size = enc.shard_end(hist.data_ptr(), xbuf.data_ptr())
     if host is not None:
-        heads = _all_gather_heads(enc.shard_head(), rank, world, group)
+        heads = _all_gather_heads(enc.shard_head(), rank, world, width, height, group)
         ok, total = enc.shard_write_host(heads, host.addr, host.cap)
         if not ok:  # same `total` on every rank: all grow together
             host.ensure(total)

@@ -61,14 +61,22 @@ def _gloo_worker(rank, world, port, w, h, secs, full, result):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        import numpy as np
+
         import jxg
-        from jxg.dist import gather_payloads
+        from jxg.dist import _all_gather_heads, gather_payloads
 
         ids = jxg.shard_sections(w, h, rank, world)
         payload = jxg.make_payload(rank, world, w, h, [(i, secs[i]) for i in ids])
         got = gather_payloads(payload, rank, world, "cpu")
+        # payload heads (7 + 2 x sections words) in one fixed-capacity all-gather
+        head = np.frombuffer(payload[:4 * (7 + 2 * len(ids))], dtype=np.uint32)
+        heads = _all_gather_heads(head, rank, world, w, h)
+        heads_ok = (len(heads) == world and np.array_equal(heads[rank], head) and
+                    all(int(hd[2]) == r and hd.size == 7 + 2 * int(hd[6])
+                        for r, hd in enumerate(heads)))
         if rank == 0:
-            result.put(jxg.shard_assemble(got) == full)
+            result.put((jxg.shard_assemble(got) == full, heads_ok))
     finally:
         dist.destroy_process_group()
 
@@ -93,4 +101,4 @@ def test_gloo_world2_gather_and_assemble(jxg_mod, oracle, decoder):
     for p in procs:
         p.join(120)
         assert p.exitcode == 0
-    assert q.get(timeout=10) is True
+    assert q.get(timeout=10) == (True, True)
