@@ -1304,7 +1304,11 @@ static jxg_status stage_concat_split(Ctx* c, Job& J, uint8_t** host_out, size_t*
     dst = (dst + 7) & ~7ull;
   }
   const size_t pbytes = (size_t)(dst / 8);
-  if (pbytes + kOutHdr > pmax) return fail(JXG_ERR_INTERNAL);  // bound violated
+  if (pbytes + kOutHdr > pmax) {  // prefix bound violated: one-stream assembly instead
+    if (hipStreamSynchronize(s2) != hipSuccess) return fail(JXG_ERR_HIP);
+    out_release(ho);
+    return stage_concat(c, J, true, nullptr, nullptr, host_out, out_bytes);
+  }
   const size_t out_words = (pbytes + 3) / 4 + 1;
   chunk_words.push_back(0);  // read-ahead guard
   if (c->chunks.ensure(chunk_words.size()) != hipSuccess ||
