@@ -193,10 +193,9 @@ def main():
             # the GIL, so the encoders' host work and HIP streams overlap
             for k in ks:
                 out = step(e, k)
-                st = e.stats()
-                rec["front_ms"].append(st["ms_front_kernel"])
-                rec["host_ms"].append((st["ms_host_call"], st["ms_host_codes"],
-                                       st["ms_host_layout"]))
+                t = e.timings()
+                rec["front_ms"].append(t[0])
+                rec["host_ms"].append(t[1:])
                 rec["sizes"].append(len(out) if out is not None else 0)
 
         total = args.steps * frames

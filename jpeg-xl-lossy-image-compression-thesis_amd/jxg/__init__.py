@@ -218,6 +218,13 @@ class Encoder:
                                              row_stride or width * 3, ctypes.byref(buf)))
         return self._take(buf) if copy else Codestream(buf)
 
+    def timings(self) -> tuple:
+        """(ms_front_kernel, ms_host_call, ms_host_codes, ms_host_layout) of the
+        last encode -- the per-frame subset of :meth:`stats` without its copies."""
+        s = _Stats()
+        _check(load().jxg_get_stats(self._ctx, ctypes.byref(s)))
+        return s.ms_front_kernel, s.ms_host_call, s.ms_host_codes, s.ms_host_layout
+
     def stats(self) -> dict:
         s = _Stats()
         _check(load().jxg_get_stats(self._ctx, ctypes.byref(s)))
