@@ -3,39 +3,40 @@
 metric), device-resident RGB8 in HBM -> complete .jxl bytes in host memory.
 
   python bench.py --gpus N --steps K --warmup W [--mode shard|replica]
+                  [--scaling strong|weak] [--coder prefix|ans] [--config C]
 
-One step = one full encode (front end + merge stage, token statistics, prefix
+One step = one full encode (front end + merge stage, token statistics, entropy
 codes, bit emission, assembly, D2H of the codestream).
 
 N = 1: one 7680x4320 frame per step (BASELINE config 2's frame on one GPU).
 N > 1 (launched by torch.distributed.run, backend nccl = RCCL):
-  shard   (default) -- group sharding: ONE frame of 7680 x
-          (4320 N) pixels per step -- every rank owns 1/N of its 256x256 pass
-          groups, i.e. one 8K frame's worth of work (weak scaling) -- with
-          the real exchange: all-reduce of the AC histogram, all-gather of the
-          per-block DC/strategy records, then (--assembly host, default)
-          all-gather of the payload heads and every rank's D2H of its own
-          sections into one /dev/shm codestream buffer of the node (rank 0
-          writes headers + TOC), or (--assembly device) gather of the section
-          payloads and assembly on rank 0.  The codestream is byte-identical to a
-          single-GPU encode of the same frame (tests/test_gpu_shard.py).
+  shard   (default) -- group sharding with the real exchange
+          (jxg/dist.py) and assembly (--assembly host: every rank DMAs its
+          sections into one /dev/shm codestream buffer of the node, rank 0
+          writes headers + TOC; --assembly device: payload gather to rank 0):
+            --scaling strong (default): ONE 7680x4320 frame per step split
+              over the N ranks -- BASELINE config 2 as written;
+            --scaling weak: one frame of N stacked 8K frames (every rank owns
+              one 8K frame's worth of groups).
+          The codestream is byte-identical to a single-GPU encode of the same
+          frame (tests/test_gpu_shard.py).
   replica -- every rank encodes its own 8K frame (frame-level data
           parallelism, no data-path collective).
 Timing: barrier + synchronize on both sides of the K steps, max over ranks.
 --streams S (non-shard modes) runs S concurrent encoders per GPU (one host
 thread, context and HIP stream each; the K frames split between them).
 
-The line's value is the prefix-coded encode (default --coder prefix, S = 1);
-'ans_coder' reports the same workload with the ANS coder (libjxl's e7 entropy
-coder) timed with --alt-ans-streams concurrent encoders, because each pass
-group's rANS state chain is serial and latency-bound.
-
 The JSON line also carries:
   roofline     -- the fused front kernel (XYB + homogeneity + AQ + 8x8 ACS +
-                  DCT + quant): algorithmic bytes per launch / its HIP-event
-                  duration (its own events, on the encoder's stream) vs 8.0
-                  TB/s, plus PMC-measured HBM traffic from profiles/ when present;
-  cpu_baseline -- the CPU oracle (scalar C port, 1 core) on the same frame.
+                  DCT + quant): SURVEY.md §8(d)'s algorithmic bytes (15.078
+                  B/px) per launch / its HIP-event duration (its own events, on
+                  the encoder's stream) vs 8.0 TB/s; the design's own bytes
+                  and the PMC-measured HBM traffic (profiles/) beside it;
+  ans_coder    -- the same workload with the other AC entropy coder;
+  quality      -- decoded PSNR / bpp of a 1920x1080 crop (untimed);
+  cpu_baseline -- the oracle/ C restatement with OpenMP on the host's cores
+                  (libjxl absent on the box) on the same frame, and whether
+                  its bytes equal the GPU's.
 """
 import argparse
 import json
@@ -46,6 +47,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "jpeg-xl-lossy-image-compression-thesis_amd"))
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402  (import before libjxg: one HIP runtime per process)
 import torch.distributed as dist  # noqa: E402
 
@@ -55,12 +57,23 @@ from jxg.synth import CONFIGS, SEED_BASE, synth_rgb8  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
-def front_bytes_per_launch(w, h, effort):
-    """Algorithmic HBM bytes of one front-kernel launch: RGB8 read (3 B/px),
-    int16 coefficients written (3 ch x 2 B = 6 B/px), per 8x8 block 3 x int32
-    DC + strategy + quant field + 2 B x 3 non-zero counts (20 B / 64 px); with
-    the merge stage (effort >= 5) also the XYB tile copy (12 B/px) and the
-    per-block estimate (4 B / 64 px)."""
+SURVEY_BYTES_PER_PX = 15.078  # RGB8 3 + quant field/ACS 5/64 + 3 x int32 12
+
+
+def front_bytes_survey(w, h):
+    """SURVEY.md §8(d)'s algorithmic bytes of the fused XYB + DCT + quant
+    kernel: read RGB8 (3 B/px), read the per-block quant field and ACS
+    (5/64 B/px), write 3 x int32 coefficients (12 B/px) = 15.078 B/px.  The
+    roofline fraction is priced on these bytes."""
+    return SURVEY_BYTES_PER_PX * w * h
+
+
+def front_bytes_design(w, h, effort):
+    """The bytes this design's front kernel moves per launch (reported beside
+    the §8(d) figure, not used for the fraction): RGB8 read (3 B/px), int16
+    coefficients (6 B/px), per 8x8 block 3 x int32 DC + strategy + quant field
+    + 3 x u16 non-zero counts (20 B); with the merge stage (effort >= 5) the
+    XYB tile copy for merge_eval (12 B/px) and the per-block estimate (4 B)."""
     bxs, bys = (w + 7) // 8, (h + 7) // 8
     px = (bxs * 8) * (bys * 8)
     b = 3 * w * h + 6 * px + 20 * bxs * bys
@@ -89,18 +102,54 @@ def load_merge_pmc(workload):
         return None
 
 
-def cpu_baseline(img, distance, effort):
+def cpu_threads():
+    """host threads for the CPU baseline: the process's CPU affinity, capped at
+    16 (the GPU box's CPU share per GPU; its nproc shows the whole host)"""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def cpu_baseline(img, distance, effort, proposals, coder, gpu_bytes):
+    """The oracle/ C restatement (libjxl/cjxl are absent on the box: probe in
+    profiles/r02a/probe.txt) timed on the host with OpenMP over
+    cpu_threads() threads, on the same frame and settings as the GPU line.
+    Its codestream is also compared with the GPU's (byte-exact parity)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_ffi  # the checker, timed here only as the reported baseline
 
     oracle_ffi.build()
+    n = oracle_ffi.set_threads(cpu_threads())
     t = time.perf_counter()
-    oracle_ffi.encode(img, distance, effort, 0)
+    r = oracle_ffi.encode(img, distance, effort, proposals, coder)
     dt = time.perf_counter() - t
     h, w, _ = img.shape
-    return {"value": round(w * h / 1e6 / dt, 3), "unit": "MPix/s", "cores": 1, "kind": "port",
-            "sample": "one full %dx%d frame, oracle/ C restatement (libjxl unavailable), %.1f s"
-                      % (w, h, dt)}
+    return {"value": round(w * h / 1e6 / dt, 3), "unit": "MPix/s", "cores": n, "kind": "port",
+            "sample": "one full %dx%d frame (the bench frame), oracle/ C restatement with OpenMP "
+                      "(libjxl/cjxl absent on the box), %.2f s" % (w, h, dt),
+            "bytes_equal_gpu": gpu_bytes is not None and r.bytes == gpu_bytes}
+
+
+def quality_probe(enc, img, distance, effort):
+    """Decoded quality at the bench settings (untimed): the top-left 1920x1080
+    crop of the bench frame, encoded on the GPU, decoded by oracle/jxl_decode.py
+    (no djxl on the box), PSNR by the reference formula (image_reader.rs:
+    569-606); the full 8K frame takes minutes in the Python decoder."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import jxl_decode
+
+    crop = np.ascontiguousarray(img[:1080, :1920])
+    data = enc.encode(crop)
+    dec = jxl_decode.decode(data).rgb
+    mse = jxg.calculate_mse(crop, dec)
+    pc = [round(jxg.calculate_psnr(jxg.calculate_mse(crop[..., c:c + 1], dec[..., c:c + 1])), 3)
+          for c in range(3)]
+    return {"frame": "top-left 1920x1080 crop of the bench frame, d%g e%d" % (distance, effort),
+            "psnr_db": round(jxg.calculate_psnr(mse), 3), "psnr_rgb_db": pc,
+            "bpp": round(len(data) * 8.0 / (1920 * 1080), 4),
+            "decoder": "oracle/jxl_decode.py (djxl absent)"}
 
 
 def main():
@@ -113,6 +162,10 @@ def main():
     ap.add_argument("--effort", type=int, default=7)
     ap.add_argument("--proposals", type=int, default=0)
     ap.add_argument("--mode", choices=("shard", "replica"), default="shard")
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
+                    help="shard mode: strong = ONE frame of the config split over the N ranks "
+                         "(BASELINE config 2 as written); weak = a frame of N stacked config "
+                         "frames (every rank owns one frame's worth of groups)")
     ap.add_argument("--assembly", choices=("host", "device"), default="host",
                     help="shard mode: host = every rank DMAs its sections into one /dev/shm "
                          "buffer (rank 0 adds headers + TOC); device = payload gather to rank 0, "
@@ -122,13 +175,15 @@ def main():
     ap.add_argument("--streams", type=int, default=1,
                     help="concurrent encoders per GPU (replica / N=1 mode): one host thread, "
                          "context and HIP stream each; a step is still one frame")
-    ap.add_argument("--alt-ans-streams", type=int, default=3,
+    ap.add_argument("--alt-ans-streams", type=int, default=1,
                     help="also time the ANS coder with this many concurrent encoders "
                          "(reported under 'ans_coder'; 0 = off)")
     ap.add_argument("--alt-thesis", type=int, default=1,
                     help="also time the workload with the thesis proposals P+F "
                          "(reported under 'thesis_proposals'; 0 = off)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-quality", action="store_true",
+                    help="skip the untimed decode-PSNR probe")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -148,6 +203,7 @@ def main():
             dist.init_process_group(backend)
     name, w, h, nframes = CONFIGS[args.config]
     shard = world > 1 and args.mode == "shard"
+    strong = shard and args.scaling == "strong"
     img = synth_rgb8(w, h, SEED_BASE + args.config + (0 if shard else rank))
     d_img = torch.from_numpy(img).to(dev)
     # batch configs (64 x 1080p): a step is the whole batch of distinct frames,
@@ -156,8 +212,8 @@ def main():
     d_imgs = [d_img] + [torch.from_numpy(synth_rgb8(w, h, SEED_BASE + args.config + f)).to(dev)
                         for f in range(1, frames)]
     fh = h
-    if shard:
-        # one frame of N stacked 8K frames: every rank owns 1/N of its groups
+    if shard and not strong:
+        # one frame of N stacked config frames: every rank owns 1/N of its groups
         fh = h * world
         d_img = d_img.repeat(world, 1, 1).contiguous()
     torch.cuda.synchronize()
@@ -186,7 +242,7 @@ def main():
         for e in encs:  # contexts warmed one after another
             for _ in range(args.warmup):
                 step(e)
-        rec = {"front_ms": [], "host_ms": [], "sizes": []}
+        rec = {"front_ms": [], "host_ms": [], "sizes": [], "last": None}
 
         def worker(e, ks):
             # the codestream ends in (pinned) host memory; ctypes calls release
@@ -197,6 +253,8 @@ def main():
                 rec["front_ms"].append(t[0])
                 rec["host_ms"].append(t[1:])
                 rec["sizes"].append(len(out) if out is not None else 0)
+                if k % frames == 0:
+                    rec["last"] = out
 
         total = args.steps * frames
         share = [list(range(i, total, nstreams)) for i in range(nstreams)]
@@ -223,8 +281,11 @@ def main():
             dt = float(tt.item())
         rec["dt"] = dt
         rec["st"] = encs[0].stats()
-        for e in encs:
+        last = rec["last"]
+        rec["last"] = last.tobytes() if hasattr(last, "tobytes") else last
+        for e in encs[1:]:
             e.close()
+        rec["enc"] = encs[0]
         if host is not None:
             dist.barrier()
             host.close()
@@ -234,14 +295,14 @@ def main():
     R = run(args.coder, nstreams)
     dt, front_ms, host_ms, st = R["dt"], R["front_ms"], R["host_ms"], R["st"]
     nbytes = R["sizes"][-1] if R["sizes"] else 0
+    px_step = w * fh * (1 if shard else world) * frames
     alt = None
     if not shard and args.alt_ans_streams > 0 and args.coder != "ans":
-        # the same workload with the ANS coder (libjxl's e7 entropy coder):
-        # its per-group rANS chain is latency-bound, so concurrent encoders
-        # overlap it with the other frames' kernels
+        # the same workload with the ANS coder (libjxl's e7 entropy coder)
         A = run("ans", args.alt_ans_streams)
+        A["enc"].close()
         alt = {"coder": "ans", "streams_per_gpu": args.alt_ans_streams,
-               "value": round(w * fh * world * frames * args.steps / A["dt"] / 1e6, 2),
+               "value": round(px_step * args.steps / A["dt"] / 1e6, 2),
                "ms_per_step": round(A["dt"] * 1e3 / args.steps, 3),
                "ms_latency": round(sum(x[0] for x in A["host_ms"]) / len(A["host_ms"]), 3),
                "bytes_per_frame": A["sizes"][-1],
@@ -252,8 +313,9 @@ def main():
         # the homogeneity selector in the front kernel, hook F on every
         # 8x8 and merge candidate
         T = run(args.coder, 1, proposals=3)
+        T["enc"].close()
         thesis = {"proposals": "P+F (combined.diff)",
-                  "value": round(w * fh * world * frames * args.steps / T["dt"] / 1e6, 2),
+                  "value": round(px_step * args.steps / T["dt"] / 1e6, 2),
                   "ms_per_step": round(T["dt"] * 1e3 / args.steps, 3),
                   "ms_front_kernel": round(sum(T["front_ms"]) / len(T["front_ms"]), 4),
                   "bytes_per_frame": T["sizes"][-1],
@@ -261,27 +323,31 @@ def main():
     if rank == 0:
         ms_step = dt * 1e3 / args.steps
         frame_px = w * fh
-        value = frame_px * (1 if shard else world) * frames * args.steps / dt / 1e6
+        value = px_step * args.steps / dt / 1e6
         # roofline of the front kernel over this rank's launch (its tiles)
         fw, fhh = (w, fh // world) if shard else (w, fh)
-        fb = front_bytes_per_launch(fw, fhh, args.effort)
+        fb = front_bytes_survey(fw, fhh)
         fms = sum(front_ms) / len(front_ms)
         achieved = fb / (fms * 1e-3) / 1e9 if fms > 0 else 0.0
+        coder_desc = "%s-coded" % args.coder
         if shard:
-            workload = ("%s x%d: %dx%d RGB8 (synth_rgb8 8K frame stacked %d times), VarDCT d%g "
-                        "e%d, proposals=%d, %s-coded, 256x256 groups sharded over %d ranks, "
-                        "%s assembly"
-                        % (name, world, w, fh, world, args.distance, args.effort,
-                           args.proposals, args.coder, world, args.assembly))
+            workload = ("%s: %dx%d RGB8 (synth_rgb8%s), VarDCT d%g e%d, proposals=%d, %s, "
+                        "256x256 groups sharded over %d ranks (%s scaling), %s assembly"
+                        % (name, w, fh, "" if strong else ", config frame stacked %d times" % world,
+                           args.distance, args.effort, args.proposals, coder_desc, world,
+                           args.scaling, args.assembly))
             par = "group-shard%d" % world
         else:
-            workload = ("%s %dx%d RGB8 (synth_rgb8), VarDCT d%g e%d, proposals=%d, %s-coded, "
+            workload = ("%s %dx%d RGB8 (synth_rgb8), VarDCT d%g e%d, proposals=%d, %s, "
                         "%d distinct frame(s) per step, %d concurrent encoder stream(s) per rank"
-                        % (name, w, h, args.distance, args.effort, args.proposals, args.coder,
+                        % (name, w, h, args.distance, args.effort, args.proposals, coder_desc,
                            frames, nstreams))
             par = "frame-dp%d" % world
+        label = {"8k": "8K", "4k": "4K", "16k": "16384x16384", "cpu512": "512x512",
+                 "1080p_x64": "64 x 1080p"}.get(name, name)
         res = {
-            "metric": "MPix/s VarDCT encode @ d1.0, 8K RGB",
+            "metric": "MPix/s VarDCT encode @ d%s, %s RGB" % (
+                "1.0" if args.distance == 1.0 else "%g" % args.distance, label),
             "value": round(value, 2),
             "unit": "MPix/s",
             "n_gpus": world,
@@ -289,7 +355,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
@@ -308,7 +374,10 @@ def main():
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": load_pmc_traffic(name) if world == 1 else None,
-                         "algorithmic_bytes": fb, "avg_ms": round(fms, 4)},
+                         "algorithmic_bytes": int(fb),
+                         "bytes_per_px": SURVEY_BYTES_PER_PX,
+                         "design_bytes": front_bytes_design(fw, fhh, args.effort),
+                         "avg_ms": round(fms, 4)},
             # the dominant kernels (merge stage) are VALU-issue-bound, not
             # HBM-bound: their live time and the PMC-measured VALU issue rate
             "merge_stage": {"kernels": "merge_eval + merge_resolve + merge_write",
@@ -320,9 +389,14 @@ def main():
             res["ans_coder"] = alt
         if thesis is not None:
             res["thesis_proposals"] = thesis
+        if world == 1 and not args.no_quality:
+            res["quality"] = quality_probe(R["enc"], img, args.distance, args.effort)
         if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(img, args.distance, args.effort)
+            res["cpu_baseline"] = cpu_baseline(img, args.distance, args.effort, args.proposals,
+                                               1 if args.coder == "ans" else 0,
+                                               R["last"])
         print(json.dumps(res), flush=True)
+    R["enc"].close()
     if world > 1:
         dist.destroy_process_group()
 

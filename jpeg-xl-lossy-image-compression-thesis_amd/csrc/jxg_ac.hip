@@ -87,9 +87,11 @@ __device__ __forceinline__ int block_ctx_of(int c, int acs) {
 // AC tokens are < 64: |q| <= 32767 -> packed value <= 65534 -> hybrid token
 // <= 63; the non-zero count (<= 4032) token is <= 47.  Device tables use 64 columns.
 constexpr int kAcTok = 64;
-// LDS bit buffer of ac_emit (groups whose exact size exceeds it fall back to
-// global atomics)
-constexpr int kEmitLdsWords = 8192;  // 32 KiB = 262144 bits
+// LDS bit buffer of ac_emit / ans_emit (groups whose exact size exceeds it
+// fall back to global atomics): 96 KiB = 786432 bits = 12 bpp over a full
+// 256x256 group, so only near-incompressible groups take the slow path
+// (ac_emit: 96 KiB + 33 KiB of code tables, one 1024-thread workgroup per CU)
+constexpr int kEmitLdsWords = 24576;
 
 __device__ __forceinline__ int channel_of(int ci) { return ci == 0 ? 1 : (ci == 1 ? 0 : 2); }
 
@@ -409,12 +411,13 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
 }
 __global__ __launch_bounds__(kAcThreads) void ac_emit_kernel(AcArgs a) {
   __shared__ uint32_t sCode[kMaxClusters * kAcTok];
-  __shared__ uint32_t sBits[kEmitLdsWords];
+  __shared__ __attribute__((aligned(16))) uint32_t sBits[kEmitLdsWords];
   __shared__ uint32_t sWave[kAcThreads / 64];
   const int g = blockIdx.x + (int)a.g0;
   for (int i = threadIdx.x; i < kMaxClusters * kAcTok; i += blockDim.x)
     sCode[i] = a.codes[(i / kAcTok) * kAlpha + (i % kAcTok)];
-  for (int i = threadIdx.x; i < kEmitLdsWords; i += blockDim.x) sBits[i] = 0;
+  for (int i = threadIdx.x; i < kEmitLdsWords / 4; i += blockDim.x)
+    reinterpret_cast<uint4*>(sBits)[i] = make_uint4(0, 0, 0, 0);
   const uint32_t n = a.ntok[g * 3] + a.ntok[g * 3 + 1] + a.ntok[g * 3 + 2];
   const uint32_t* rec = a.tokens + (uint64_t)(g - (int)a.g0) * kGroupTokStride;
   constexpr int kWaves = kAcThreads / 64;
@@ -572,12 +575,13 @@ __global__ __launch_bounds__(kAnsWaves * 64) void ans_encode_kernel(AnsArgs a) {
 // contiguous record range per wave, coalesced reads, wave scans of the
 // lengths (as ac_emit)
 __global__ __launch_bounds__(kAcThreads) void ans_emit_kernel(AnsArgs a) {
-  __shared__ uint32_t sBits[kEmitLdsWords];
+  __shared__ __attribute__((aligned(16))) uint32_t sBits[kEmitLdsWords];
   __shared__ uint32_t sWave[kAcThreads / 64];
   const uint32_t g = a.g0 + blockIdx.x;
   const uint32_t n = a.ntok[g * 3] + a.ntok[g * 3 + 1] + a.ntok[g * 3 + 2];
   const uint64_t b = (uint64_t)(g - a.g0) * kGroupTokStride;
-  for (int i = threadIdx.x; i < kEmitLdsWords; i += blockDim.x) sBits[i] = 0;
+  for (int i = threadIdx.x; i < kEmitLdsWords / 4; i += blockDim.x)
+    reinterpret_cast<uint4*>(sBits)[i] = make_uint4(0, 0, 0, 0);
   constexpr int kWaves = kAcThreads / 64;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t chunk = ((n + kWaves * 64 - 1) / (kWaves * 64)) * 64;
@@ -641,8 +645,8 @@ void launch_ac_hist(const AcArgs& a, uint32_t ngroups, hipStream_t s) {
 void launch_ac_emit(const AcArgs& a, uint32_t ngroups, hipStream_t s) {
   if (ngroups) hipLaunchKernelGGL(ac_emit_kernel, dim3(ngroups), dim3(kAcThreads), 0, s, a);
 }
-void set_cluster_table(const uint8_t* tab, hipStream_t s) {
-  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_cluster), tab, kAcCtx, 0, hipMemcpyHostToDevice, s);
+hipError_t set_cluster_table(const uint8_t* tab, hipStream_t s) {
+  return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_cluster), tab, kAcCtx, 0, hipMemcpyHostToDevice, s);
 }
 
 }  // namespace jxg

@@ -26,6 +26,7 @@ __constant__ float c_lut[256];
 // per-lane quantization tables, built on the host from the weights
 __constant__ float c_wperm[4 * 3 * 64];  // [T][c][lane r][row k] = w[qkind(T)][c][co_index(T,k,r)]
 __constant__ float c_iwperm[4 * 64];     // [T][r][k] = 1.0f / (Y weight) at the same slot
+__constant__ float c_sdperm[4 * 3 * 64]; // [T][c][r][k] distortion weight at the same slot
 __constant__ float c_btab[256];          // [q] = 0.145f / q (AdjustQuantBias, |q| >= 2)
 __constant__ uint8_t c_zz[4 * 64];       // [T][r][k] = zigzag index of co_index(T,k,r)
 
@@ -298,6 +299,7 @@ struct GroupCtx {
   const float* wperm;  // LDS [4 T][3 c][8 r][8 k] weights per lane
   const float* iwperm; // LDS [4 T][8 r][8 k] Y inverse weights per lane
   const float* btab;   // LDS [256] 0.145f / q
+  const float* sdperm; // LDS [4 T][3 c][8 r][8 k] distortion weights per lane
 };
 
 // Quantized values of one candidate: [channel X, Y, B][4 words of 2 x int16]
@@ -381,6 +383,7 @@ __device__ __forceinline__ void quantize_cols(const GroupCtx& G, const float* vt
   const float4* wp = reinterpret_cast<const float4*>(G.wperm + ((ti * 3 + C) * 8 + G.r) * 8);
   const float4 w0 = wp[0], w1 = wp[1];
   const float wk[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+  const float* sdk = G.sdperm + ((ti * 3 + C) * 8 + G.r) * 8;  // read at use
   float iwk[8];
   if (C == 1) {
     const float4* ip = reinterpret_cast<const float4*>(G.iwperm + (ti * 8 + G.r) * 8);
@@ -407,7 +410,9 @@ __device__ __forceinline__ void quantize_cols(const GroupCtx& G, const float* vt
       if (vq < 0.0f) adj = -adj;
       A.yd[k] = adj * (iwk[k] * inv_scale);
     }
-    const float e = a - (float)qa;
+    // quantization error in steps, times the distortion weight: the
+    // coefficient's pixel-domain error (oracle jxo_dist_weight)
+    const float e = (a - (float)qa) * sdk[k];
     A.part = fmaf(e, e, A.part);
     // 2 + 2 bitlen(qa) per non-zero: bitlen(qa) = 31 - clz(2 qa + 1)
     clzs += (int)__clz((uint32_t)(2 * qa + 1));
@@ -558,6 +563,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   __shared__ __attribute__((aligned(16))) int16_t sStage[8][8][64];
   __shared__ __attribute__((aligned(16))) float sWperm[4 * 3 * 64];
   __shared__ __attribute__((aligned(16))) float sIwperm[4 * 64];
+  __shared__ __attribute__((aligned(16))) float sSdperm[4 * 3 * 64];
   __shared__ __attribute__((aligned(16))) uint8_t sZz[4 * 64];
   __shared__ float sLut[256];
   __shared__ float sBtab[256];
@@ -576,7 +582,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     sIwperm[tid] = c_iwperm[tid];
     sZz[tid] = c_zz[tid];
   }
-  for (int i = tid; i < 768; i += kThreads) sWperm[i] = c_wperm[i];
+  for (int i = tid; i < 768; i += kThreads) {
+    sWperm[i] = c_wperm[i];
+    sSdperm[i] = c_sdperm[i];
+  }
   __syncthreads();
   load_xyb_tile(a, sLut, sPix, ox, oy);
   __syncthreads();
@@ -631,7 +640,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   // candidate search's live registers)
   auto gblock = [&]() { return (size_t)(ty * 8 + lby) * a.bxs + tx * 8 + lbx; };
   size_t gb = gblock();
-  const GroupCtx G{sPix, lby * 8 + 1, lbx * 8 + 1, r, sWperm, sIwperm, sBtab};
+  const GroupCtx G{sPix, lby * 8 + 1, lbx * 8 + 1, r, sWperm, sIwperm, sBtab, sSdperm};
   // block DC (row partials, tree over rows) and AQ activity
   float dc[3];
 #pragma unroll
@@ -684,7 +693,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     rv = sR[b][1];
     rd = sR[b][2];
   }
-  if (HOOKP && (a.proposals & 1u)) pt = partition_of(rh, rv, rd, a.distance);
+  // hook P lives in FindBest8x8Transform, which libjxl does not run below
+  // effort 5 (all-DCT8 speed tiers [ext]): no override there either
+  if (HOOKP && (a.proposals & 1u) && ncand > 1) pt = partition_of(rh, rv, rd, a.distance);
   // scan indices: DCT8 0, DCT4X4 1, DCT4X8 2, DCT8X4 3
   QVals best, ptq;
   int bt = kDCT8, bi = 0;
@@ -812,8 +823,8 @@ __global__ __launch_bounds__(kThreads) void homog_kernel(HomogArgs a) {
   }
 }
 
-void set_front_constants(const float lut[256], const float wts[3][3][64], hipStream_t s) {
-  static float wperm[4 * 3 * 64], iwperm[4 * 64], btab[256];
+hipError_t set_front_constants(const float lut[256], const float wts[3][3][64], hipStream_t s) {
+  static float wperm[4 * 3 * 64], iwperm[4 * 64], btab[256], sdperm[4 * 3 * 64];
   static uint8_t zz[4 * 64];
   const int types[4] = {kDCT8, kDCT4X4, kDCT4X8, kDCT8X4};
   for (int ti = 0; ti < 4; ti++) {
@@ -822,23 +833,42 @@ void set_front_constants(const float lut[256], const float wts[3][3][64], hipStr
     for (int r = 0; r < 8; r++)
       for (int k = 0; k < 8; k++) {
         const int co = co_index_rt(T, k, r);
-        for (int c = 0; c < 3; c++) wperm[((ti * 3 + c) * 8 + r) * 8 + k] = wts[qk][c][co];
+        // area a coefficient's basis spans: the lowest-frequency combine slots
+        // the whole block, other DCT4X4 coefficients a 4x4 sub-block, other
+        // DCT4X8 / DCT8X4 ones a 4x8 half (oracle jxo_frame_init)
+        const int row = co >> 3, col = co & 7;
+        int area = 64;
+        if (ti == 1 && !(row < 2 && col < 2)) area = 16;
+        if (ti >= 2 && !(row < 2 && col == 0)) area = 32;
+        for (int c = 0; c < 3; c++) {
+          wperm[((ti * 3 + c) * 8 + r) * 8 + k] = wts[qk][c][co];
+          sdperm[((ti * 3 + c) * 8 + r) * 8 + k] = dist_weight(c, area, wts[qk][c][co]);
+        }
         iwperm[(ti * 8 + r) * 8 + k] = 1.0f / wts[qk][1][co];
         zz[(ti * 8 + r) * 8 + k] = (uint8_t)c_inv_order_h(co);
       }
   }
   btab[0] = btab[1] = 0.0f;
   for (int q = 2; q < 256; q++) btab[q] = 0.145f / (float)q;
-  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_lut), lut, sizeof(float) * 256, 0,
+  hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_lut), lut, sizeof(float) * 256, 0,
+                                        hipMemcpyHostToDevice, s);
+  if (e == hipSuccess)
+    e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_wperm), wperm, sizeof(wperm), 0,
                                hipMemcpyHostToDevice, s);
-  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_wperm), wperm, sizeof(wperm), 0,
+  if (e == hipSuccess)
+    e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_iwperm), iwperm, sizeof(iwperm), 0,
                                hipMemcpyHostToDevice, s);
-  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_iwperm), iwperm, sizeof(iwperm), 0,
+  if (e == hipSuccess)
+    e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_sdperm), sdperm, sizeof(sdperm), 0,
                                hipMemcpyHostToDevice, s);
-  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_btab), btab, sizeof(btab), 0,
+  if (e == hipSuccess)
+    e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_btab), btab, sizeof(btab), 0,
                                hipMemcpyHostToDevice, s);
-  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_zz), zz, sizeof(zz), 0, hipMemcpyHostToDevice, s);
-  (void)hipStreamSynchronize(s);  // the static host tables must outlive the copies
+  if (e == hipSuccess)
+    e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_zz), zz, sizeof(zz), 0, hipMemcpyHostToDevice, s);
+  // the static host tables must outlive the copies
+  const hipError_t e2 = hipStreamSynchronize(s);
+  return e != hipSuccess ? e : e2;
 }
 void launch_front(const FrontArgs& a, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s) {
   if (a.proposals & 1u)

@@ -315,7 +315,7 @@ static const int kKindDims[kNumKinds][2] = {{8, 16}, {16, 16}, {16, 32},
                                            {32, 32}, {32, 64}, {64, 64}};
 
 struct MergeTables {
-  std::vector<float> wk, iwy;
+  std::vector<float> wk, sdk, iwy;
   std::vector<uint16_t> nat;
   float lee_c[7][32], lee_s[7][64], llf_p[4][8], llf_ib[4][8][8];
 };
@@ -381,7 +381,7 @@ static MergeTables build_merge_tables() {
     static const int kShapeDims[kNumShapes][3] = {{2, 1, 0}, {1, 2, 0}, {2, 2, 1}, {4, 2, 2}, {2, 4, 2},
                                                  {4, 4, 3}, {8, 4, 4}, {4, 8, 4}, {8, 8, 5}};
     const int stot = kShapeOff[kNumShapes];
-    std::vector<float> swk((size_t)3 * stot), siwy(stot);
+    std::vector<float> swk((size_t)3 * stot), ssdk((size_t)3 * stot), siwy(stot);
     std::vector<uint16_t> snat(stot);
     for (int sh = 0; sh < kNumShapes; sh++) {
       const int cy = kShapeDims[sh][0], cx = kShapeDims[sh][1], k = kShapeDims[sh][2];
@@ -393,13 +393,17 @@ static MergeTables build_merge_tables() {
           // LLF positions (the first cy x cx): weight 0, so they quantize to 0
           // and add nothing without a per-coefficient test in the kernels
           const bool llf = ky < cy && kx < cx;
-          for (int c = 0; c < 3; c++)
-            swk[(size_t)c * stot + pi] = llf ? 0.0f : T.wk[(size_t)c * tot + kKindOff[k] + si];
+          for (int c = 0; c < 3; c++) {
+            const float wv = T.wk[(size_t)c * tot + kKindOff[k] + si];
+            swk[(size_t)c * stot + pi] = llf ? 0.0f : wv;
+            ssdk[(size_t)c * stot + pi] = llf ? 0.0f : dist_weight(c, R * C, wv);
+          }
           siwy[pi] = T.iwy[kKindOff[k] + si];
           snat[pi] = T.nat[kKindOff[k] + si];
         }
     }
     T.wk.swap(swk);
+    T.sdk.swap(ssdk);
     T.iwy.swap(siwy);
     T.nat.swap(snat);
   }
@@ -438,7 +442,7 @@ struct Ctx {
   // device
   DevBuf<uint8_t> rgb, acs, qf;
   DevBuf<uint16_t> nz, mnat;
-  DevBuf<float> ent, mwk, miwy, xyb_tiles, mcost;
+  DevBuf<float> ent, mwk, msdk, miwy, xyb_tiles, mcost;
   DevBuf<uint32_t> vb, vcount, mwork;
   DevBuf<int32_t> dc;
   DevBuf<int16_t> ac;
@@ -496,16 +500,18 @@ static jxg_status init_constants(Ctx* c) {
   srgb_lut(lut);
   static float wts[3][3][64];
   quant_weights(wts);
-  set_front_constants(lut, wts, c->stream);
+  JXG_HIP(set_front_constants(lut, wts, c->stream));
   uint8_t tab[kAcCtx];
   for (int i = 0; i < kAcCtx; i++) tab[i] = (uint8_t)ac_cluster(i);
-  set_cluster_table(tab, c->stream);
+  JXG_HIP(set_cluster_table(tab, c->stream));
   static const MergeTables mt = build_merge_tables();
-  set_merge_constants(&mt.llf_p[0][0], &mt.llf_ib[0][0][0], c->stream);
+  JXG_HIP(set_merge_constants(&mt.llf_p[0][0], &mt.llf_ib[0][0][0], c->stream));
   JXG_HIP(c->mwk.ensure(mt.wk.size()));
+  JXG_HIP(c->msdk.ensure(mt.sdk.size()));
   JXG_HIP(c->miwy.ensure(mt.iwy.size()));
   JXG_HIP(c->mnat.ensure(mt.nat.size()));
   JXG_HIP(hipMemcpyAsync(c->mwk.p, mt.wk.data(), mt.wk.size() * 4, hipMemcpyHostToDevice, c->stream));
+  JXG_HIP(hipMemcpyAsync(c->msdk.p, mt.sdk.data(), mt.sdk.size() * 4, hipMemcpyHostToDevice, c->stream));
   JXG_HIP(hipMemcpyAsync(c->miwy.p, mt.iwy.data(), mt.iwy.size() * 4, hipMemcpyHostToDevice, c->stream));
   JXG_HIP(hipMemcpyAsync(c->mnat.p, mt.nat.data(), mt.nat.size() * 2, hipMemcpyHostToDevice, c->stream));
   JXG_HIP(hipStreamSynchronize(c->stream));
@@ -800,11 +806,12 @@ static jxg_status stage_front(Ctx* c, Job& J) {
     ma.nz = c->nz.p;
     ma.cost = c->mcost.p;
     ma.wk = c->mwk.p;
+    ma.sdk = c->msdk.p;
     ma.iwy = c->miwy.p;
     ma.nat = c->mnat.p;
     ma.work = c->mwork.p;
     ma.nwrite = 256 * 3 * 4;  // CUs x resident workgroups x 4
-    launch_merge(ma, s);
+    JXG_HIP(launch_merge(ma, s));
     JXG_HIP(hipGetLastError());
   }
   return JXG_OK;
@@ -1307,7 +1314,9 @@ static jxg_status stage_concat_split(Ctx* c, Job& J, uint8_t** host_out, size_t*
   if (pbytes + kOutHdr > pmax) {  // prefix bound violated: one-stream assembly instead
     if (hipStreamSynchronize(s2) != hipSuccess) return fail(JXG_ERR_HIP);
     out_release(ho);
-    return stage_concat(c, J, true, nullptr, nullptr, host_out, out_bytes);
+    const jxg_status st = stage_concat(c, J, true, nullptr, nullptr, host_out, out_bytes);
+    J.ms_layout = ms_since(t_layout);
+    return st;
   }
   const size_t out_words = (pbytes + 3) / 4 + 1;
   chunk_words.push_back(0);  // read-ahead guard
@@ -1470,6 +1479,7 @@ static jxg_status shard_begin(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32_t
 static jxg_status shard_end(Ctx* c, const uint32_t* d_hist, const uint8_t* d_xbuf,
                             size_t* payload_bytes) {
   if (!c->job) return JXG_ERR_INVALID_ARG;
+  const Clock::time_point t_call = Clock::now();
   Job& J = *c->job;
   hipStream_t s = c->stream;
   const uint32_t world = J.plan.world;
@@ -1514,6 +1524,7 @@ static jxg_status shard_end(Ctx* c, const uint32_t* d_hist, const uint8_t* d_xbu
   c->stats.ms_front = elapsed(c->ev[0], c->ev[1]);
   c->stats.ms_front_kernel = elapsed(c->ev[0], c->ev[5]);
   c->stats.ms_total = elapsed(c->ev[0], c->ev[4]);
+  c->stats.ms_host_call = ms_since(t_call);
   c->job.reset();
   return JXG_OK;
 }
@@ -2012,7 +2023,7 @@ static jxg_status compare_device(Ctx* c, const uint8_t* d_orig, size_t so, const
     std::lock_guard<std::mutex> lock(g_const_mu);
     double g[11];
     gauss_window(g);
-    set_gauss_table(g, s);
+    JXG_HIP(set_gauss_table(g, s));
     JXG_HIP(hipGetLastError());
     c->gauss_ready = true;
   }

@@ -1,6 +1,7 @@
 // jxg_kernels.h -- kernel argument blocks and device-symbol setup shared by
 // the HIP translation units and the host orchestrator (jxg_host.cpp).
 #pragma once
+#include <cmath>
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
@@ -55,6 +56,7 @@ struct MergeArgs {
   float* cost;          // [tiles][9 shapes][32 varblocks] candidate estimates
   const float* wk;      // [3][kShapeOff[9]] weights per shape, pixel orientation
   const float* iwy;     // [kShapeOff[9]] 1 / Y weight
+  const float* sdk;     // [3][kShapeOff[9]] distortion weights (dist_weight), same layout
   const uint16_t* nat;  // [kShapeOff[9]] natural-order position
   uint32_t* work;       // [1 + tiles * 9]: count, then (tile << 4 | shape) of every
                         //   (tile, shape) holding a chosen varblock (resolve -> write)
@@ -172,7 +174,14 @@ struct ConcatPiece {
   uint32_t pad;
 };
 
-void set_front_constants(const float lut[256], const float wts[3][3][64], hipStream_t s);
+// distortion weight of a coefficient in the strategy search's estimates
+// (== oracle/front.c jxo_dist_weight): sqrt(area / 64) * w0[c] / w, in
+// double, rounded once; w0 = the DCT8 band-0 weights of X, Y, B
+inline float dist_weight(int c, int area, float w) {
+  static const float kW0[3] = {3150.0f, 560.0f, 512.0f};
+  return (float)(std::sqrt((double)area / 64.0) * ((double)kW0[c] / (double)w));
+}
+hipError_t set_front_constants(const float lut[256], const float wts[3][3][64], hipStream_t s);
 void launch_front(const FrontArgs& a, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s);
 void launch_front_list(const FrontArgs& a, uint32_t ntiles, hipStream_t s);
 // shard exchange: per-group block records (acs, qf, dc) <-> frame arrays
@@ -194,10 +203,10 @@ void launch_lf_hist(const LfArgs& a, uint32_t nchunks, hipStream_t s);
 void launch_lf_bits(const LfArgs& a, uint32_t nchunks, hipStream_t s);
 void launch_lf_scan(const LfArgs& a, uint32_t nstreams, hipStream_t s);
 void launch_lf_emit(const LfArgs& a, uint32_t nchunks, hipStream_t s);
-void set_cluster_table(const uint8_t* tab, hipStream_t s);
-void set_merge_constants(const float* llf_p /*[4][8]*/, const float* llf_ib /*[4][8][8]*/,
+hipError_t set_cluster_table(const uint8_t* tab, hipStream_t s);
+hipError_t set_merge_constants(const float* llf_p /*[4][8]*/, const float* llf_ib /*[4][8][8]*/,
                          hipStream_t s);
-void launch_merge(const MergeArgs& a, hipStream_t s);
+hipError_t launch_merge(const MergeArgs& a, hipStream_t s);
 void dump_merge_profile();  // JXG_MERGE_PROFILE experiment builds; no-op otherwise
 void launch_vb_list(const VbArgs& a, uint32_t nlf, hipStream_t s);
 // decode-side quality (jxg_metrics.hip): orig / comp RGB8 interleaved rows
@@ -211,7 +220,7 @@ struct MetricArgs {
   double* ssim;       // out: sum of window SSIMs over all channels, or null (skip SSIM)
 };
 uint32_t ssim_partials(uint32_t w, uint32_t h);
-void set_gauss_table(const double* g, hipStream_t s);
+hipError_t set_gauss_table(const double* g, hipStream_t s);
 void launch_metrics(const MetricArgs& a, hipStream_t s);
 void launch_concat(const ConcatPiece* pieces, uint32_t npieces, uint64_t max_words,
                    const uint32_t* scratch, const uint32_t* chunks, const uint32_t* scratch2,

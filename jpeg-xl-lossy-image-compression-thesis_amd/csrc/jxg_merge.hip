@@ -410,8 +410,9 @@ __device__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S) {
     float* cplane = S.co + P.off(v, CH) + x;
     const float* yd = S.co + P.off(v, 1) + x;
     const int tcol = P.soff + x * P.R() + ch * RPC;  // column chunk in the tables
-    float w[RPC], iw[RPC];
+    float w[RPC], iw[RPC], sd[RPC];
     load_f<RPC>(a.wk + (size_t)CH * STOT + tcol, w);
+    if (!WRITE) load_f<RPC>(a.sdk + (size_t)CH * STOT + tcol, sd);
     if (CH == 1) {
       load_f<RPC>(a.iwy + tcol, iw);
       const float inv_scale = 1.0f / scale;
@@ -459,8 +460,12 @@ __device__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S) {
         if (vq < 0.0f) adj = -adj;
         cplane[ky * kMS] = adj * iw[kk];  // LLF: 0 (its value lives in llf_at)
       }
-      const float e = av - qf;
-      cp = fmaf(e, e, cp);
+      // error in steps times the distortion weight (oracle jxo_dist_weight);
+      // the write pass needs no estimate
+      if (!WRITE) {
+        const float e = (av - qf) * sd[kk];
+        cp = fmaf(e, e, cp);
+      }
       // 2 + 2 bitlen(qa) per non-zero = 2 E - 250, E = biased exponent of qf
       // (qf = 0 has E = 0 and is not counted in nzc)
       ebits += __float_as_uint(qf) >> 23;
@@ -873,22 +878,26 @@ void dump_merge_profile() {
 void dump_merge_profile() {}
 #endif
 
-void set_merge_constants(const float* llf_p, const float* llf_ib, hipStream_t s) {
-  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_llf_p), llf_p, sizeof(float) * 4 * 8, 0,
+hipError_t set_merge_constants(const float* llf_p, const float* llf_ib, hipStream_t s) {
+  hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_llf_p), llf_p, sizeof(float) * 4 * 8, 0,
+                                        hipMemcpyHostToDevice, s);
+  if (e == hipSuccess)
+    e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_llf_ib), llf_ib, sizeof(float) * 4 * 64, 0,
                                hipMemcpyHostToDevice, s);
-  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_llf_ib), llf_ib, sizeof(float) * 4 * 64, 0,
-                               hipMemcpyHostToDevice, s);
-  (void)hipStreamSynchronize(s);
+  const hipError_t e2 = hipStreamSynchronize(s);
+  return e != hipSuccess ? e : e2;
 }
-void launch_merge(const MergeArgs& a, hipStream_t s) {
-  if (!a.ntiles) return;
+hipError_t launch_merge(const MergeArgs& a, hipStream_t s) {
+  if (!a.ntiles) return hipSuccess;
   const uint32_t nwg = ((a.ntiles + 7) / 8) * 8 * kNumShapes;
   hipLaunchKernelGGL(merge_eval_kernel, dim3(nwg), dim3(kMThreads), 0, s, a);
-  (void)hipMemsetAsync(a.work, 0, sizeof(uint32_t), s);
+  const hipError_t e = hipMemsetAsync(a.work, 0, sizeof(uint32_t), s);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(merge_resolve_kernel, dim3((a.ntiles + kResolveWaves - 1) / kResolveWaves),
                      dim3(64 * kResolveWaves), 0, s, a);
   const uint32_t nw = min(a.nwrite, a.ntiles * (uint32_t)kNumShapes);
   hipLaunchKernelGGL(merge_write_kernel, dim3(nw), dim3(kMThreads), 0, s, a);
+  return hipGetLastError();
 }
 void launch_vb_list(const VbArgs& a, uint32_t nlf, hipStream_t s) {
   hipLaunchKernelGGL(vb_list_kernel, dim3(nlf), dim3(1024), 0, s, a);

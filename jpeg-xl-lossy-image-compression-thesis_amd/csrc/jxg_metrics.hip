@@ -155,9 +155,9 @@ uint32_t ssim_partials(uint32_t w, uint32_t h) {
   return tx * ty * 3;
 }
 
-void set_gauss_table(const double* g, hipStream_t s) {
-  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_gauss), g, 11 * sizeof(double), 0,
-                               hipMemcpyHostToDevice, s);
+hipError_t set_gauss_table(const double* g, hipStream_t s) {
+  return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_gauss), g, 11 * sizeof(double), 0,
+                                hipMemcpyHostToDevice, s);
 }
 
 void launch_metrics(const MetricArgs& a, hipStream_t s) {

@@ -62,6 +62,30 @@ def _synth(w: int, h: int, seed: int) -> np.ndarray:
     return out
 
 
+def natural_rgb8(w: int, h: int, seed: int) -> np.ndarray:
+    """A photographic stand-in for rate-distortion checks: smooth colour
+    fields, a dozen soft-blended discs (edges) and band-limited texture (a
+    Gaussian low-pass of white noise, not aligned to any block grid).
+    Deterministic for a given numpy (PCG64 + FFT).  Returns (h, w, 3) uint8."""
+    rng = np.random.default_rng(seed)
+    y, x = np.mgrid[0:h, 0:w].astype(np.float64)
+    img = np.zeros((h, w, 3))
+    for c in range(3):
+        img[..., c] = 128 + 60 * np.sin(x / (17 + 7 * c)) * np.cos(y / (23 + 5 * c))
+    for _ in range(12):
+        cx, cy, r = rng.uniform(0, w), rng.uniform(0, h), rng.uniform(8, w / 4)
+        col = rng.uniform(0, 255, 3)
+        m = (x - cx) ** 2 + (y - cy) ** 2 < r * r
+        img[m] = 0.6 * img[m] + 0.4 * col
+    wn = rng.normal(0, 1, (h, w, 3))
+    fy = np.fft.fftfreq(h)[:, None]
+    fx = np.fft.fftfreq(w)[None, :]
+    lp = np.exp(-(fx ** 2 + fy ** 2) / (2 * 0.06 ** 2))[..., None]
+    tex = np.real(np.fft.ifft2(np.fft.fft2(wn, axes=(0, 1)) * lp, axes=(0, 1)))
+    tex *= 8.0 / tex.std()
+    return np.clip(img + tex, 0, 255).astype(np.uint8)
+
+
 # SURVEY.md §8(d) workload shapes: (name, width, height, frames)
 CONFIGS = {
     0: ("cpu512", 512, 512, 1),

@@ -180,7 +180,7 @@ static void put_modular(jxo_bw* w, const tnode* t, int nnodes, int nleaves,
   uint32_t counts[8][JXO_ALPHA];
   memset(counts, 0, sizeof(counts));
   for (int pass = 0; pass < 2; pass++) {
-    static jxo_prefix codes[8];
+    static _Thread_local jxo_prefix codes[8];
     if (pass == 1) {
       for (int l = 0; l < nleaves; l++) jxo_build_prefix(counts[l], JXO_ALPHA, &codes[l]);
       uint8_t map[8];
@@ -423,6 +423,11 @@ int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h, size_t row_strid
   jxo_natural_order8(order);
   float* ent = (float*)malloc(sizeof(float) * nb);
   int* raws = (int*)malloc(sizeof(int) * nb);
+  (void)jxo_vkinds(); /* build the merge tables before any parallel region */
+  /* Parallel loops (OpenMP, test/baseline speed only): every iteration
+   * writes disjoint outputs, and every reduction is an integer sum, so the
+   * bytes do not depend on the thread count. */
+#pragma omp parallel for schedule(dynamic)
   for (uint32_t by = 0; by < f.bys; by++)
     for (uint32_t bx = 0; bx < f.bxs; bx++) {
       float px[3][64];
@@ -448,13 +453,15 @@ int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h, size_t row_strid
   if (p->effort >= 5) {
     const int max_s = p->effort >= 6 ? 8 : 4;
     const uint32_t tx_n = (f.bxs + 7) / 8, ty_n = (f.bys + 7) / 8;
+#pragma omp parallel for schedule(dynamic) collapse(2)
     for (uint32_t ty = 0; ty < ty_n; ty++)
       for (uint32_t tx = 0; tx < tx_n; tx++)
         jxo_merge_tile(&f, xyb, out->homog, (int)tx, (int)ty, max_s, ent, raws, out->acs);
-    static int32_t vq[3 * 4096];
-    float llf[3 * 64];
+#pragma omp parallel for schedule(dynamic)
     for (uint32_t by = 0; by < f.bys; by++)
       for (uint32_t bx = 0; bx < f.bxs; bx++) {
+        static _Thread_local int32_t vq[3 * 4096];
+        float llf[3 * 64];
         const size_t b = (size_t)by * f.bxs + bx;
         const int si = jxo_shape_of(out->acs[b]);
         if (si < 0) continue; /* 8x8 class or covered */
@@ -492,14 +499,23 @@ int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h, size_t row_strid
   size_t* gn = (size_t*)malloc(sizeof(size_t) * f.ngroups);
   static uint32_t hist[JXO_MAX_CLUSTERS][JXO_ALPHA];
   memset(hist, 0, sizeof(hist));
-  for (uint32_t g = 0; g < f.ngroups; g++) {
-    gt[g] = (actok*)malloc(sizeof(actok) * 32 * 32 * 3 * 64);
-    gn[g] = group_tokens(&f, out, (int)g, gt[g], out->ac_tokens + g * 3);
-    for (size_t i = 0; i < gn[g]; i++) {
-      uint32_t tok, nbt, bits;
-      jxo_hybrid(gt[g][i].v, &kCfg, &tok, &nbt, &bits);
-      hist[jxo_ac_cluster(gt[g][i].ctx)][tok]++;
+#pragma omp parallel
+  {
+    static _Thread_local uint32_t lh[JXO_MAX_CLUSTERS][JXO_ALPHA];
+    memset(lh, 0, sizeof(lh));
+#pragma omp for schedule(dynamic)
+    for (uint32_t g = 0; g < f.ngroups; g++) {
+      gt[g] = (actok*)malloc(sizeof(actok) * 32 * 32 * 3 * 64);
+      gn[g] = group_tokens(&f, out, (int)g, gt[g], out->ac_tokens + g * 3);
+      for (size_t i = 0; i < gn[g]; i++) {
+        uint32_t tok, nbt, bits;
+        jxo_hybrid(gt[g][i].v, &kCfg, &tok, &nbt, &bits);
+        lh[jxo_ac_cluster(gt[g][i].ctx)][tok]++;
+      }
     }
+#pragma omp critical
+    for (int cl = 0; cl < JXO_MAX_CLUSTERS; cl++)
+      for (int s = 0; s < JXO_ALPHA; s++) hist[cl][s] += lh[cl][s];
   }
   /* prefix codes: one histogram per static cluster.  ANS: the static
    * clusters are clustered again into <= JXO_ANS_MAX_HISTS centres
@@ -559,6 +575,7 @@ int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h, size_t row_strid
     jxo_bw_put(s, 1, 1); /* ColorCorrelation DC all_default */
     jxo_bw_put(s, 1, 0); /* GlobalModular: no global tree; 0 channels */
   }
+#pragma omp parallel for schedule(dynamic)
   for (uint32_t lg = 0; lg < f.nlf; lg++) lf_group_section(&f, out, (int)lg, &sec[1 + lg]);
   {
     jxo_bw* s = &sec[1 + f.nlf];
@@ -583,6 +600,7 @@ int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h, size_t row_strid
       for (int h = 0; h < nhist; h++) jxo_ans_write_hist(s, &ans[h]);
     }
   }
+#pragma omp parallel for schedule(dynamic)
   for (uint32_t g = 0; g < f.ngroups; g++) {
     jxo_bw* s = &sec[2 + f.nlf + g];
     if (!ans) {
@@ -646,6 +664,21 @@ int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h, size_t row_strid
   free(ctxmap);
   free(codes);
   return 0;
+}
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+/* threads of the parallel loops (bench.py's cpu_baseline states the count);
+ * returns the count in effect */
+int jxo_set_threads(int n) {
+#ifdef _OPENMP
+  if (n > 0) omp_set_num_threads(n);
+  return omp_get_max_threads();
+#else
+  (void)n;
+  return 1;
+#endif
 }
 
 void jxo_result_free(jxo_result* r) {

@@ -72,6 +72,25 @@ void jxo_quant_weights(int kind, float out[3][64]) {
   }
 }
 
+/* Distortion weight of one quantized coefficient in the rate-distortion
+ * estimates of the strategy search (8x8 class here, merged varblocks in
+ * merge.c).  e = |v| - |q| is the quantization error in quantizer steps;
+ * the step of a coefficient with weight w is 1/(w scale) in coefficient
+ * units, and with this DCT normalization (out[0] = mean) a coefficient error
+ * spreads sqrt(area) times its size over the `area` pixels its basis covers
+ * (Parseval).  e * jxo_dist_weight(c, area, w) / scale is therefore the
+ * pixel-domain (XYB) error of channel c, normalized by the channel's DCT8
+ * band-0 weight jxo_w0[c] so that the three channels stay comparable
+ * (the per-channel multiplier of libjxl's EstimateEntropy loss [ext]) and so
+ * that a DCT8 band-0 coefficient keeps weight 1.  Without it the estimate
+ * measured error in step units, which stay below 0.58 however coarse the
+ * step, so coarse (large) transforms looked cheap.  Computed in double,
+ * rounded once. */
+const float jxo_w0[3] = {3150.0f, 560.0f, 512.0f};
+float jxo_dist_weight(int c, int area, float w) {
+  return (float)(sqrt((double)area / 64.0) * ((double)jxo_w0[c] / (double)w));
+}
+
 /* [ext] natural coefficient order of an 8x8 varblock (zigzag) */
 void jxo_natural_order8(uint8_t order[64]) {
   int cur = 1;
@@ -142,6 +161,21 @@ void jxo_frame_init(jxo_frame* f, uint32_t w, uint32_t h, const jxo_params* p) {
     f->dc_step[c] = (float)(65536.0 / (double)G / (double)qdc * m_lf[c]);
   }
   for (int k = 0; k < 3; k++) jxo_quant_weights(k, f->wts[k]);
+  /* distortion weights per 8x8-class strategy (scan index DCT8, DCT4X4,
+   * DCT4X8, DCT8X4) and coefficient-layout position: the lowest-frequency
+   * combine slots span the whole block (area 64); other DCT4X4 coefficients
+   * span a 4x4 sub-block (16), DCT4X8 / DCT8X4 ones a 4x8 half (32) */
+  for (int ti = 0; ti < 4; ti++) {
+    const int qk = ti == 0 ? JXO_QK_DCT8 : (ti == 1 ? JXO_QK_DCT4 : JXO_QK_DCT4X8);
+    for (int c = 0; c < 3; c++)
+      for (int co = 0; co < 64; co++) {
+        const int row = co >> 3, col = co & 7;
+        int area = 64;
+        if (ti == 1 && !(row < 2 && col < 2)) area = 16;
+        if (ti >= 2 && !(row < 2 && col == 0)) area = 32;
+        f->sdw[ti][c][co] = jxo_dist_weight(c, area, f->wts[qk][c][co]);
+      }
+  }
 }
 
 /* ---------- transforms ----------
@@ -302,6 +336,8 @@ float jxo_quantize_block(const jxo_frame* f, int t, const float px[3][64],
   for (int c = 0; c < 3; c++) jxo_transform(t, px[c], co[c]);
   const int qk = qkind(t);
   const float inv_scale = 1.0f / scale;
+  const int ti = t == JXO_DCT8 ? 0 : (t == JXO_DCT4X4 ? 1 : (t == JXO_DCT4X8 ? 2 : 3));
+  const float(*sd)[64] = f->sdw[ti];
   float yd[64];
   float part[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   int bits = 0;
@@ -320,7 +356,7 @@ float jxo_quantize_block(const jxo_frame* f, int t, const float px[3][64],
         const int qq = quant1(v);
         if (c == 1) yd[ci_] = adjust_bias(1, qq) * ((1.0f / f->wts[qk][c][ci_]) * inv_scale);
         const uint32_t aq = (uint32_t)(qq < 0 ? -qq : qq);
-        const float e = fabsf(v) - (float)aq;
+        const float e = (fabsf(v) - (float)aq) * sd[c][ci_];
         part[r] = fmaf(e, e, part[r]);
         if (aq) {
           bits += 2 + 2 * bitlen(aq);
@@ -412,7 +448,11 @@ int jxo_front_block(const jxo_frame* f, const float px[3][64], const float* homo
   /* the estimate the merge stage sums is stored before the P override
    * (homogeneity-partitioning.diff:271 context) */
   if (ent_out) *ent_out = best;
-  if ((f->proposals & 1) && best_t == JXO_DCT8) {
+  /* hook P sits inside FindBest8x8Transform (combined.diff:266-276), which
+   * libjxl's AC-strategy heuristics do not run at the all-DCT8 speed tiers
+   * (effort < 5 here, the same condition as the candidate search above) [ext]:
+   * no override there */
+  if ((f->proposals & 1) && ncand > 1 && best_t == JXO_DCT8) {
     /* HomogeneityPartition thresholds, combined.diff:219-234 */
     float T = 1.60f;
     if ((double)f->distance > 10.0)

@@ -215,6 +215,7 @@ float jxo_hook_f(float ret, float r_h, float r_v, float r_d) {
 void jxo_homog_map(const jxo_xyb* img, float distance, int h1_mode, float* r3,
                    uint8_t* type) {
   size_t bxs = img->xsize / 8, bys = img->ysize / 8;
+#pragma omp parallel for schedule(dynamic)
   for (size_t by = 0; by < bys; by++) {
     for (size_t bx = 0; bx < bxs; bx++) {
       size_t b = by * bxs + bx;

@@ -82,6 +82,8 @@ typedef struct {
 int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h,
                     size_t row_stride, const jxo_params* p, jxo_result* out);
 void jxo_result_free(jxo_result* r);
+/* OpenMP threads of the encode's parallel loops (n <= 0: query only) */
+int jxo_set_threads(int n);
 
 /* stage-level entry points (used by tests) */
 void jxo_srgb8_to_xyb(const uint8_t* rgb, uint32_t w, uint32_t h,

@@ -37,12 +37,16 @@ typedef struct {
   uint32_t G, qdc;
   float dc_mul[3], dc_step[3];
   float wts[3][3][64]; /* [quant kind][channel X,Y,B][coef] */
+  float sdw[4][3][64];  /* [8x8-class strategy index][channel][coef] distortion weights */
 } jxo_frame;
 
 enum { JXO_QK_DCT8 = 0, JXO_QK_DCT4 = 1, JXO_QK_DCT4X8 = 2 };
 
 void jxo_frame_init(jxo_frame* f, uint32_t w, uint32_t h, const jxo_params* p);
 void jxo_quant_weights(int kind, float out[3][64]);
+/* distortion weight of a coefficient (see front.c jxo_dist_weight) */
+float jxo_dist_weight(int c, int area, float w);
+extern const float jxo_w0[3];
 void jxo_natural_order8(uint8_t order[64]);
 void jxo_quant_dc(const jxo_frame* f, const float dc[3], int32_t dcq[3]);
 
@@ -69,6 +73,7 @@ extern const jxo_shape jxo_shapes[JXO_NSHAPES];
 typedef struct {
   int rows, cols; /* stored orientation: rows = 8 min(cy,cx), cols = 8 max(cy,cx) */
   float* w[3];    /* weights per channel X, Y, B, stored raster */
+  float* sd[3];   /* distortion weights jxo_dist_weight(c, rows*cols, w) */
   uint16_t* nat;  /* stored raster index -> natural order position */
 } jxo_vkind;
 const jxo_vkind* jxo_vkinds(void);

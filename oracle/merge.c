@@ -190,9 +190,12 @@ static void init_tables(void) {
     K->cols = kKindDim[k][1];
     const int n = K->rows * K->cols;
     for (int c = 0; c < 3; c++) K->w[c] = (float*)malloc(sizeof(float) * n);
+    for (int c = 0; c < 3; c++) K->sd[c] = (float*)malloc(sizeof(float) * n);
     K->nat = (uint16_t*)malloc(sizeof(uint16_t) * n);
     kind_weights(k, K->w);
     kind_order(k, K->nat);
+    for (int c = 0; c < 3; c++)
+      for (int i = 0; i < n; i++) K->sd[c][i] = jxo_dist_weight(c, n, K->w[c][i]);
   }
   g_init = 1;
 }
@@ -275,7 +278,7 @@ float jxo_varblock(const jxo_frame* f, const jxo_shape* s, const float* xyb, int
   const int R = 8 * s->cy, C = 8 * s->cx;
   const jxo_vkind* K = &g_kinds[s->kind];
   const size_t plane = (size_t)f->xp * f->yp;
-  static float F[3][64 * 64];
+  static _Thread_local float F[3][64 * 64];
   float tmp[64];
   for (int c = 0; c < 3; c++) {
     const float* P = xyb + c * plane;
@@ -299,7 +302,8 @@ float jxo_varblock(const jxo_frame* f, const jxo_shape* s, const float* xyb, int
   int bits = 0, nz[3] = {0, 0, 0};
   static const int corder[3] = {1, 0, 2};
   const int rows_per_chunk = R < 16 ? R : 16;
-  float yd[64 * 64], pc[3] = {0.0f, 0.0f, 0.0f};
+  static _Thread_local float yd[64 * 64];
+  float pc[3] = {0.0f, 0.0f, 0.0f};
   for (int ci = 0; ci < 3; ci++) {
     const int c = corder[ci];
     for (int ch = 0; ch * rows_per_chunk < R; ch++) {
@@ -320,7 +324,7 @@ float jxo_varblock(const jxo_frame* f, const jxo_shape* s, const float* xyb, int
           const int qq = quant1(v);
           if (c == 1) yd[ky * C + x] = adjust_bias_y(qq) * ((1.0f / w) * inv_scale);
           const uint32_t aq = (uint32_t)(qq < 0 ? -qq : qq);
-          const float e = fabsf(v) - (float)aq;
+          const float e = (fabsf(v) - (float)aq) * K->sd[c][si];
           cp = fmaf(e, e, cp);
           if (aq) {
             bits += 2 + 2 * bitlen(aq);

@@ -68,7 +68,14 @@ def lib():
         _lib.jxo_export_kind.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         _lib.jxo_export_kind.restype = ctypes.c_int
         _lib.jxo_export_dct.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        _lib.jxo_set_threads.argtypes = [ctypes.c_int]
+        _lib.jxo_set_threads.restype = ctypes.c_int
     return _lib
+
+
+def set_threads(n: int) -> int:
+    """OpenMP threads of the oracle encode (n <= 0: query); returns the count."""
+    return lib().jxo_set_threads(n)
 
 
 class OracleResult:

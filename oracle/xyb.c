@@ -61,6 +61,7 @@ void jxo_srgb8_to_xyb(const uint8_t* rgb, uint32_t w, uint32_t h,
   jxo_srgb_lut(lut);
   const float cb = jxo_cbrtf(JXO_BIAS);
   const size_t plane = (size_t)xp * yp;
+#pragma omp parallel for schedule(static)
   for (uint32_t y = 0; y < yp; y++) {
     const uint8_t* row = rgb + (size_t)(y < h ? y : h - 1) * row_stride;
     for (uint32_t x = 0; x < xp; x++) {

@@ -81,16 +81,20 @@ def test_full_8k_frame_sse(enc, jxg_mod):
 
 
 def test_encode_decode_psnr(enc, jxg_mod, decoder):
-    """End to end: GPU encode -> oracle decoder -> GPU PSNR == host PSNR."""
-    from jxg.synth import synth_rgb8
+    """End to end: GPU encode -> oracle decoder -> GPU PSNR == host PSNR, with
+    quality floors at d1 e7 (tests/test_oracle_rd.py has the RD checks)."""
+    from jxg.synth import natural_rgb8, synth_rgb8
     img = synth_rgb8(200, 136, 0x4A584C00)
     dec = decoder.decode(enc.encode(img)).rgb
     q = enc.compare(img, dec)
     assert q["mse"] == jxg_mod.calculate_mse(img, dec) or q["mse"] == metrics.mse(img, dec)
     assert q["psnr"] == metrics.psnr(metrics.mse(img, dec))
-    # the synthetic frame's full-range noise tiles are quantized to near their
-    # mean at d1 (DESIGN.md §3.4), so the whole-frame PSNR is modest
-    assert 10.0 < q["psnr"] < 60.0
+    # the synthetic mix holds full-range RGB noise tiles (their chroma is
+    # quantized coarsely at d1), so the floor is modest
+    assert q["psnr"] >= 24.0, q["psnr"]
+    nat = natural_rgb8(256, 256, 3)
+    qn = enc.compare(nat, decoder.decode(enc.encode(nat)).rgb)
+    assert qn["psnr"] >= 38.0, qn["psnr"]
 
 
 def test_harness_compare_to_orig(enc, decoder, tmp_path):
