@@ -52,7 +52,7 @@ import torch  # noqa: E402  (import before libjxg: one HIP runtime per process)
 import torch.distributed as dist  # noqa: E402
 
 import jxg  # noqa: E402
-from jxg.synth import CONFIGS, SEED_BASE, synth_rgb8  # noqa: E402
+from jxg.synth import CONFIGS, SEED_BASE, synth_rgb8_device  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
@@ -204,13 +204,18 @@ def main():
     name, w, h, nframes = CONFIGS[args.config]
     shard = world > 1 and args.mode == "shard"
     strong = shard and args.scaling == "strong"
-    img = synth_rgb8(w, h, SEED_BASE + args.config + (0 if shard else rank))
-    d_img = torch.from_numpy(img).to(dev)
+    # inputs generated on the device (jxg_synth_rgb8_device: the bytes of
+    # jxg.synth.synth_rgb8, without minutes of numpy at 8K / 16K)
+    d_img = synth_rgb8_device(w, h, SEED_BASE + args.config + (0 if shard else rank), local)
+    img = d_img.cpu().numpy() if world == 1 else None  # quality probe / CPU baseline
     # batch configs (64 x 1080p): a step is the whole batch of distinct frames,
-    # device-resident, split over the concurrent encoders
+    # device-resident
     frames = 1 if shard else nframes
-    d_imgs = [d_img] + [torch.from_numpy(synth_rgb8(w, h, SEED_BASE + args.config + f)).to(dev)
+    d_imgs = [d_img] + [synth_rgb8_device(w, h, SEED_BASE + args.config + f, local)
                         for f in range(1, frames)]
+    # batch configs: one step = the whole batch through the batched entry point
+    batch = frames > 1 and args.streams == 1
+    ptrs = [t.data_ptr() for t in d_imgs]
     fh = h
     if shard and not strong:
         # one frame of N stacked config frames: every rank owns 1/N of its groups
@@ -237,6 +242,10 @@ def main():
                 from jxg.dist import encode_sharded
                 return encode_sharded(e, d_img, w, fh, rank, world, bufs=bufs, copy=False,
                                       host=host)
+            if batch:
+                # the whole batch through the library's batched entry point
+                # (jxg_encode_batch_rgb8_device: three lanes, own streams)
+                return e.encode_batch_device(ptrs, w, fh, copy=False)[0]
             return e.encode_device(d_imgs[k % frames].data_ptr(), w, fh, copy=False)
 
         for e in encs:  # contexts warmed one after another
@@ -253,10 +262,10 @@ def main():
                 rec["front_ms"].append(t[0])
                 rec["host_ms"].append(t[1:])
                 rec["sizes"].append(len(out) if out is not None else 0)
-                if k % frames == 0:
+                if batch or k % frames == 0:
                     rec["last"] = out
 
-        total = args.steps * frames
+        total = args.steps * (1 if batch else frames)
         share = [list(range(i, total, nstreams)) for i in range(nstreams)]
         if world > 1:
             dist.barrier()
@@ -339,9 +348,10 @@ def main():
             par = "group-shard%d" % world
         else:
             workload = ("%s %dx%d RGB8 (synth_rgb8), VarDCT d%g e%d, proposals=%d, %s, "
-                        "%d distinct frame(s) per step, %d concurrent encoder stream(s) per rank"
+                        "%d distinct frame(s) per step, %s"
                         % (name, w, h, args.distance, args.effort, args.proposals, coder_desc,
-                           frames, nstreams))
+                           frames, "jxg_encode_batch_rgb8_device (3 lanes)" if batch else
+                           "%d concurrent encoder stream(s) per rank" % nstreams))
             par = "frame-dp%d" % world
         label = {"8k": "8K", "4k": "4K", "16k": "16384x16384", "cpu512": "512x512",
                  "1080p_x64": "64 x 1080p"}.get(name, name)

@@ -87,10 +87,22 @@ jxg_status jxg_encode_rgb8(void* ctx, const uint8_t* rgb, uint32_t xsize, uint32
 /* device-resident RGB8 (same layout, device pointer) -> codestream */
 jxg_status jxg_encode_rgb8_device(void* ctx, const void* d_rgb, uint32_t xsize,
                                   uint32_t ysize, size_t row_stride, jxg_buffer* out);
-/* n frames of equal size (benchmark config 3: 64 x 1080p) */
+/* n frames of equal size (benchmark config 3: 64 x 1080p; the reference's
+ * caller encodes every image at 10 distances x 5 efforts, benchmark.rs:
+ * 637-642).  The frames are spread over three lanes -- this context plus two
+ * it creates on first use (same parameters; released by jxg_destroy) -- one
+ * host thread, HIP stream and pinned staging buffer each, so the frames'
+ * H2D copies, kernels and host-side code construction overlap.  outs[i] is
+ * frame i's codestream (byte-identical to jxg_encode_rgb8 of that frame); on
+ * error every output is released.  jxg_get_stats then describes the last
+ * frame this context encoded. */
 jxg_status jxg_encode_batch_rgb8(void* ctx, const uint8_t* const* rgbs, uint32_t n,
                                  uint32_t xsize, uint32_t ysize, size_t row_stride,
                                  jxg_buffer* outs);
+/* the same with device-resident frames */
+jxg_status jxg_encode_batch_rgb8_device(void* ctx, const void* const* d_rgbs, uint32_t n,
+                                        uint32_t xsize, uint32_t ysize, size_t row_stride,
+                                        jxg_buffer* outs);
 jxg_status jxg_get_stats(void* ctx, jxg_stats* stats);
 void jxg_buffer_free(jxg_buffer* buf);
 
@@ -174,6 +186,15 @@ jxg_status jxg_compare_rgb8(void* ctx, const uint8_t* orig, size_t orig_stride,
 jxg_status jxg_compare_rgb8_device(void* ctx, const void* d_orig, size_t orig_stride,
                                    const void* d_comp, size_t comp_stride, uint32_t xsize,
                                    uint32_t ysize, int want_ssim, jxg_quality* out);
+
+/* ---- benchmark input ----
+ * The deterministic synthetic RGB8 frame of SURVEY.md §8(d) (64x64 tiles of
+ * flat / gradient / stripe / checker / edge / noise content, splitmix64
+ * hashes, seed 0x4A584C00 + config index), written into device memory
+ * d_out (row_stride bytes per row) on the context's stream; returns when it
+ * is complete.  Same bytes as jxg/synth.py synth_rgb8. */
+jxg_status jxg_synth_rgb8_device(void* ctx, void* d_out, uint32_t xsize, uint32_t ysize,
+                                 size_t row_stride, uint64_t seed);
 
 #ifdef __cplusplus
 }

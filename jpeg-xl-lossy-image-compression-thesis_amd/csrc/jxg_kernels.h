@@ -222,6 +222,9 @@ struct MetricArgs {
 uint32_t ssim_partials(uint32_t w, uint32_t h);
 hipError_t set_gauss_table(const double* g, hipStream_t s);
 void launch_metrics(const MetricArgs& a, hipStream_t s);
+// synthetic benchmark input (jxg_synth.hip): RGB8 rows of `stride` bytes
+hipError_t launch_synth(uint8_t* out, uint32_t w, uint32_t h, size_t stride, uint64_t seed,
+                        hipStream_t s);
 void launch_concat(const ConcatPiece* pieces, uint32_t npieces, uint64_t max_words,
                    const uint32_t* scratch, const uint32_t* chunks, const uint32_t* scratch2,
                    uint32_t* out, hipStream_t s);

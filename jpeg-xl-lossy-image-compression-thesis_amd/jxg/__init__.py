@@ -79,7 +79,8 @@ EXPORTS = ("jxg_status_str", "jxg_create", "jxg_destroy", "jxg_encode_rgb8",
            "jxg_buffer_free", "jxg_homogeneity_map", "jxg_shard_sizes", "jxg_shard_begin",
            "jxg_shard_end", "jxg_shard_payload", "jxg_shard_assemble_device",
            "jxg_shard_assemble", "jxg_compare_rgb8", "jxg_compare_rgb8_device",
-           "jxg_shard_head", "jxg_shard_write_host", "jxg_host_register", "jxg_host_unregister")
+           "jxg_shard_head", "jxg_shard_write_host", "jxg_host_register", "jxg_host_unregister",
+           "jxg_encode_batch_rgb8_device", "jxg_synth_rgb8_device")
 
 _lib = None
 
@@ -102,6 +103,10 @@ def load():
                                     ctypes.POINTER(_Buffer)]
     lib.jxg_encode_rgb8_device.argtypes = [vp, vp, ctypes.c_uint32, ctypes.c_uint32,
                                            ctypes.c_size_t, ctypes.POINTER(_Buffer)]
+    lib.jxg_encode_batch_rgb8.argtypes = [vp, ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32,
+                                          ctypes.c_uint32, ctypes.c_uint32, ctypes.c_size_t,
+                                          ctypes.POINTER(_Buffer)]
+    lib.jxg_encode_batch_rgb8_device.argtypes = lib.jxg_encode_batch_rgb8.argtypes
     lib.jxg_get_stats.argtypes = [vp, ctypes.POINTER(_Stats)]
     lib.jxg_buffer_free.argtypes = [ctypes.POINTER(_Buffer)]
     lib.jxg_buffer_free.restype = None
@@ -127,6 +132,8 @@ def load():
                 ctypes.POINTER(_Quality)]
     lib.jxg_compare_rgb8.argtypes = cmp_args
     lib.jxg_compare_rgb8_device.argtypes = cmp_args
+    lib.jxg_synth_rgb8_device.argtypes = [vp, vp, ctypes.c_uint32, ctypes.c_uint32, sz,
+                                          ctypes.c_uint64]
     _lib = lib
     return lib
 
@@ -206,6 +213,35 @@ class Encoder:
         buf = _Buffer()
         _check(load().jxg_encode_rgb8(self._ctx, rgb.ctypes.data, w, h, w * 3, ctypes.byref(buf)))
         return self._take(buf)
+
+    def encode_batch(self, frames) -> list:
+        """Host frames of equal size, each (H, W, 3) uint8 -> list of codestream
+        bytes (jxg_encode_batch_rgb8, BASELINE config 3)."""
+        frames = [np.ascontiguousarray(f, dtype=np.uint8) for f in frames]
+        if not frames:
+            return []
+        h, w, c = frames[0].shape
+        if c != 3 or any(f.shape != frames[0].shape for f in frames):
+            raise ValueError("expected equal-size (H, W, 3) uint8 frames")
+        n = len(frames)
+        ptrs = (ctypes.c_void_p * n)(*[f.ctypes.data for f in frames])
+        outs = (_Buffer * n)()
+        _check(load().jxg_encode_batch_rgb8(self._ctx, ptrs, n, w, h, w * 3, outs))
+        return [self._take(outs[i]) for i in range(n)]
+
+    def encode_batch_device(self, ptrs, width: int, height: int, row_stride: int | None = None,
+                            copy: bool = True) -> list:
+        """Device-resident frames of equal size (pointers) -> list of
+        codestreams (jxg_encode_batch_rgb8_device); copy=False returns
+        :class:`Codestream` views of the library's pinned buffers."""
+        n = len(ptrs)
+        if n == 0:
+            return []
+        arr = (ctypes.c_void_p * n)(*ptrs)
+        outs = (_Buffer * n)()
+        _check(load().jxg_encode_batch_rgb8_device(self._ctx, arr, n, width, height,
+                                                   row_stride or width * 3, outs))
+        return [self._take(outs[i]) if copy else Codestream(outs[i]) for i in range(n)]
 
     def encode_device(self, ptr: int, width: int, height: int, row_stride: int | None = None,
                       copy: bool = True):
@@ -317,6 +353,14 @@ class Encoder:
         _check(load().jxg_homogeneity_map(self._ctx, xyb.ctypes.data, xs, ys, distance, flags,
                                           r3.ctypes.data, t.ctypes.data))
         return r3, t
+
+    def synth_device(self, ptr: int, width: int, height: int, seed: int,
+                     row_stride: int | None = None):
+        """Fill device memory with the benchmark's synthetic RGB8 frame
+        (jxg.synth.synth_rgb8 bytes) on this context's stream."""
+        _check(load().jxg_synth_rgb8_device(self._ctx, ctypes.c_void_p(ptr), width, height,
+                                            row_stride or width * 3,
+                                            seed & 0xFFFFFFFFFFFFFFFF))
 
     def compare(self, orig: np.ndarray, comp: np.ndarray, ssim: bool = True) -> dict:
         """Decode-side quality on the GPU (jxg_compare_rgb8): orig / comp are

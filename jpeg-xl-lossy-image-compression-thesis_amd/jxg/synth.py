@@ -62,6 +62,25 @@ def _synth(w: int, h: int, seed: int) -> np.ndarray:
     return out
 
 
+def synth_rgb8_device(w: int, h: int, seed: int, device=0, enc=None):
+    """The same frame as :func:`synth_rgb8`, generated on the GPU
+    (jxg_synth_rgb8_device) into a new uint8 CUDA tensor (h, w, 3)."""
+    import torch
+
+    from . import Encoder
+
+    t = torch.empty((h, w, 3), dtype=torch.uint8, device=torch.device("cuda", device))
+    own = enc is None
+    e = Encoder(device=device) if own else enc
+    try:
+        torch.cuda.synchronize(t.device)
+        e.synth_device(t.data_ptr(), w, h, seed)
+    finally:
+        if own:
+            e.close()
+    return t
+
+
 def natural_rgb8(w: int, h: int, seed: int) -> np.ndarray:
     """A photographic stand-in for rate-distortion checks: smooth colour
     fields, a dozen soft-blended discs (edges) and band-limited texture (a

@@ -82,6 +82,8 @@ typedef struct {
 int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h,
                     size_t row_stride, const jxo_params* p, jxo_result* out);
 void jxo_result_free(jxo_result* r);
+/* synthetic RGB8 frame (jxg/synth.py synth_rgb8), out: h*w*3 bytes */
+void jxo_synth_rgb8(uint32_t w, uint32_t h, uint64_t seed, uint8_t* out);
 /* OpenMP threads of the encode's parallel loops (n <= 0: query only) */
 int jxo_set_threads(int n);
 

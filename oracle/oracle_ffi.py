@@ -68,9 +68,18 @@ def lib():
         _lib.jxo_export_kind.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         _lib.jxo_export_kind.restype = ctypes.c_int
         _lib.jxo_export_dct.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        _lib.jxo_synth_rgb8.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,
+                                        ctypes.c_void_p]
         _lib.jxo_set_threads.argtypes = [ctypes.c_int]
         _lib.jxo_set_threads.restype = ctypes.c_int
     return _lib
+
+
+def synth_rgb8(w: int, h: int, seed: int) -> np.ndarray:
+    """C restatement of jxg.synth.synth_rgb8 (same bytes, OpenMP)."""
+    out = np.empty((h, w, 3), dtype=np.uint8)
+    lib().jxo_synth_rgb8(w, h, seed & 0xFFFFFFFFFFFFFFFF, out.ctypes.data)
+    return out
 
 
 def set_threads(n: int) -> int:
