@@ -235,7 +235,9 @@ def main():
         host = None
         if shard and args.assembly == "host":
             from jxg.dist import SharedHostBuffer
-            host = SharedHostBuffer(rank, world)
+            if SharedHostBuffer.single_node():
+                host = SharedHostBuffer(rank, world)
+            # else: ranks on several nodes -> device assembly (payload gather)
 
         def step(e, k=0):
             if shard:

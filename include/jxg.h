@@ -108,27 +108,36 @@ void jxg_buffer_free(jxg_buffer* buf);
 
 /* ---- multi-GPU group sharding (one context per rank) ----
  * A frame is split into `world` balanced contiguous raster ranges of 256x256
- * pass groups (rank r: groups [n*r/world, n*(r+1)/world)); LF group lg is
- * encoded by rank lg % world.  Per rank:
- *   1. jxg_shard_sizes: words of the AC histogram and bytes of one exchange
- *      slot (the exchange buffer is world slots);
+ * pass groups (rank r: groups [n*r/world, n*(r+1)/world)); every LF group
+ * (2048x2048) has one owner rank, the one holding most of its pass groups
+ * (near ties spread over ranks), which encodes its LF-group stream.  Per rank:
+ *   1. jxg_shard_sizes: words of the AC histogram and the byte capacity of
+ *      the record send / receive buffers (the largest of any rank);
+ *      jxg_shard_exchange: this rank's send and receive bytes per peer;
  *   2. jxg_shard_begin: front end + merge stage + AC token statistics of the
  *      rank's groups; writes the rank's AC histogram to d_hist (u32, device)
- *      and its per-block records to slot `rank` of d_xbuf (device);
- *   -- caller: all-reduce(sum) d_hist, all-gather d_xbuf (RCCL over xGMI);
- *   3. jxg_shard_end: LF-group streams of its LF groups, prefix codes from the
- *      global histogram, emission of the rank's sections into a payload kept
- *      in device memory (rank 0's also carries LfGlobal and HfGlobal);
- *      jxg_shard_payload copies it (payload_bytes) to device or host memory;
+ *      and, into d_xbuf (device), the per-block records (strategy, quant
+ *      field, quantized DC; 14 KB per pass group) of its groups whose LF group
+ *      another rank owns, ordered by destination rank;
+ *   -- caller: all-reduce(sum) d_hist; all_to_all of the records with the
+ *      jxg_shard_exchange splits (RCCL over xGMI) into a receive buffer;
+ *   3. jxg_shard_end(d_hist, receive buffer): LF-group streams of its LF
+ *      groups, prefix codes from the global histogram, emission of the
+ *      rank's sections into a payload kept in device memory (rank 0's also
+ *      carries LfGlobal and HfGlobal); jxg_shard_payload copies it
+ *      (payload_bytes) to device or host memory;
  *   -- caller: gather the payloads on rank 0 (RCCL, device to device);
  *   4. jxg_shard_assemble_device (rank 0): payloads in device memory (word
  *      aligned offsets) -> codestream in host memory; or jxg_shard_assemble:
  *      the same from host payloads, host only (no device).  Both are
  *      byte-identical to jxg_encode_rgb8 of the whole frame.
- * The frame needs at least max(2, world) pass groups.  Codestreams are
- * released with jxg_buffer_free. */
+ * At 16384^2 over 8 ranks every LF group lies inside one rank's range: no
+ * records move.  The frame needs at least max(2, world) pass groups.
+ * Codestreams are released with jxg_buffer_free. */
 jxg_status jxg_shard_sizes(uint32_t xsize, uint32_t ysize, uint32_t world, size_t* hist_words,
                            size_t* slot_bytes);
+jxg_status jxg_shard_exchange(uint32_t xsize, uint32_t ysize, uint32_t world, uint32_t rank,
+                              size_t* send_bytes /* [world] */, size_t* recv_bytes /* [world] */);
 jxg_status jxg_shard_begin(void* ctx, const void* d_rgb, uint32_t xsize, uint32_t ysize,
                            size_t row_stride, uint32_t rank, uint32_t world, uint32_t* d_hist,
                            void* d_xbuf);

@@ -453,7 +453,8 @@ struct Ctx {
   DevBuf<uint8_t> rgb, acs, qf;
   DevBuf<uint16_t> nz, mnat;
   DevBuf<float> ent, mwk, msdk, miwy, xyb_tiles, mcost;
-  DevBuf<uint32_t> vb, vcount, mwork;
+  DevBuf<uint32_t> vb, vcount, mwork, xlist;
+  DevBuf<uint8_t> lf_mine;  // shard: [nlf] owned LF groups (vb_list)
   DevBuf<int32_t> dc;
   DevBuf<int16_t> ac;
   DevBuf<float> homog, xyb, r3;
@@ -536,29 +537,101 @@ static jxg_status init_constants(Ctx* c) {
 // Work plan: which tiles, pass groups and LF groups this context encodes.
 // world == 1: everything.  Sharded: rank r owns the balanced
 // contiguous raster range of pass groups [ngroups*r/world, ngroups*(r+1)/world)
-// (and the 64x64 tiles inside them) and the LF groups lg with lg % world == r.
+// (and the 64x64 tiles inside them) and the LF groups shard_map assigns it.
 // ---------------------------------------------------------------------------
-struct Plan {
-  uint32_t rank = 0, world = 1, g0 = 0, g1 = 0;
-  std::vector<uint32_t> tiles;  // shard: owned tile ids (ty * tiles_x + tx)
-  bool owns_lf(uint32_t lg) const { return world == 1 || lg % world == rank; }
-};
 static uint32_t shard_g0(uint32_t ngroups, uint32_t r, uint32_t world) {
   return (uint32_t)(((uint64_t)ngroups * r) / world);
 }
+static uint32_t shard_of(uint32_t ngroups, uint32_t g, uint32_t world) {
+  uint32_t r = (uint32_t)(((uint64_t)g * world) / ngroups);  // then correct the rounding
+  while (r + 1 < world && shard_g0(ngroups, r + 1, world) <= g) r++;
+  while (r > 0 && shard_g0(ngroups, r, world) > g) r--;
+  return r;
+}
+static uint32_t lf_of_group(const Frame& f, uint32_t g) {
+  return ((g / f.gxs) / 8) * f.lfxs + (g % f.gxs) / 8;
+}
+// LF-group owners: the rank holding the most of the LF group's pass groups,
+// less 16 per LF group already assigned to it (so near ties -- an LF group
+// split over ranks' row ranges -- spread over ranks instead of piling onto
+// one); ties go to the lower rank.  An LF group inside one rank's range
+// (16384^2 over 8 ranks: every one) stays with it: nothing to exchange.
+static std::vector<uint32_t> lf_owners(const Frame& f, uint32_t world) {
+  std::vector<uint32_t> own(f.nlf, 0), nassigned(world, 0), cnt(world);
+  if (world == 1) return own;
+  for (uint32_t lg = 0; lg < f.nlf; lg++) {
+    std::fill(cnt.begin(), cnt.end(), 0u);
+    const uint32_t lx = lg % f.lfxs, ly = lg / f.lfxs;
+    for (uint32_t gy = ly * 8; gy < std::min(ly * 8 + 8, f.gys); gy++)
+      for (uint32_t gx = lx * 8; gx < std::min(lx * 8 + 8, f.gxs); gx++)
+        cnt[shard_of(f.ngroups, gy * f.gxs + gx, world)]++;
+    int best = -1;
+    long bs = 0;
+    for (uint32_t r = 0; r < world; r++) {
+      if (!cnt[r]) continue;
+      const long sc = (long)cnt[r] - 16 * (long)nassigned[r];
+      if (best < 0 || sc > bs) {
+        best = (int)r;
+        bs = sc;
+      }
+    }
+    own[lg] = (uint32_t)best;
+    nassigned[best]++;
+  }
+  return own;
+}
+// Record exchange of rank `rank`: send = its groups whose LF group another
+// rank owns, ordered by (destination rank, group); recv = other ranks' groups
+// inside its own LF groups, ordered by (source rank, group).  Counts per peer.
+struct Exchange {
+  std::vector<uint32_t> send, recv, nsend, nrecv;
+};
+static Exchange make_exchange(const Frame& f, const std::vector<uint32_t>& owner,
+                              uint32_t rank, uint32_t world) {
+  Exchange X;
+  X.nsend.assign(world, 0);
+  X.nrecv.assign(world, 0);
+  for (uint32_t p = 0; p < world; p++) {
+    if (p == rank) continue;
+    for (uint32_t g = shard_g0(f.ngroups, rank, world); g < shard_g0(f.ngroups, rank + 1, world); g++)
+      if (owner[lf_of_group(f, g)] == p) {
+        X.send.push_back(g);
+        X.nsend[p]++;
+      }
+    for (uint32_t g = shard_g0(f.ngroups, p, world); g < shard_g0(f.ngroups, p + 1, world); g++)
+      if (owner[lf_of_group(f, g)] == rank) {
+        X.recv.push_back(g);
+        X.nrecv[p]++;
+      }
+  }
+  return X;
+}
+
+struct Plan {
+  uint32_t rank = 0, world = 1, g0 = 0, g1 = 0;
+  std::vector<uint32_t> tiles;  // shard: owned tile ids (ty * tiles_x + tx)
+  std::vector<uint8_t> lf_mine; // shard: [nlf] 1 = owned LF group
+  Exchange x;                   // shard: record exchange
+  bool owns_lf(uint32_t lg) const { return world == 1 || lf_mine[lg]; }
+};
 static Plan make_plan(const Frame& f, uint32_t rank, uint32_t world) {
   Plan P;
   P.rank = rank;
   P.world = world;
   P.g0 = shard_g0(f.ngroups, rank, world);
   P.g1 = shard_g0(f.ngroups, rank + 1, world);
-  if (world > 1)
+  if (world > 1) {
     for (uint32_t g = P.g0; g < P.g1; g++) {
       const uint32_t gx = g % f.gxs, gy = g / f.gxs;
       for (uint32_t ty = gy * 4; ty < std::min(gy * 4 + 4, f.tiles_y); ty++)
         for (uint32_t tx = gx * 4; tx < std::min(gx * 4 + 4, f.tiles_x); tx++)
           P.tiles.push_back(ty * f.tiles_x + tx);
     }
+    const std::vector<uint32_t> owner = lf_owners(f, world);
+    P.lf_mine.resize(f.nlf);
+    for (uint32_t lg = 0; lg < f.nlf; lg++) P.lf_mine[lg] = owner[lg] == rank;
+    P.x = make_exchange(f, owner, rank, world);
+  }
   return P;
 }
 // exchange record of one pass group (jxg_shard.hip): acs, qf, 3 x int32 DC
@@ -660,6 +733,11 @@ static jxg_status stage_alloc(Ctx* c, Job& J) {
   if (!J.plan.tiles.empty()) {
     JXG_HIP(c->tile_list.ensure(J.plan.tiles.size()));
     JXG_HIP(hipMemcpyAsync(c->tile_list.p, J.plan.tiles.data(), J.plan.tiles.size() * 4,
+                           hipMemcpyHostToDevice, s));
+  }
+  if (!J.plan.lf_mine.empty()) {
+    JXG_HIP(c->lf_mine.ensure(J.plan.lf_mine.size()));
+    JXG_HIP(hipMemcpyAsync(c->lf_mine.p, J.plan.lf_mine.data(), J.plan.lf_mine.size(),
                            hipMemcpyHostToDevice, s));
   }
   JXG_HIP(c->vb.ensure((size_t)f.nlf * 65536));
@@ -841,7 +919,8 @@ static jxg_status stage_ac_stats(Ctx* c, Job& J) {
 static jxg_status stage_lf_stats(Ctx* c, Job& J) {
   hipStream_t s = c->stream;
   const Frame& f = J.f;
-  VbArgs va{c->acs.p, f.bxs, f.bys, f.lfxs, J.plan.rank, J.plan.world, c->vb.p, c->vcount.p};
+  VbArgs va{c->acs.p, f.bxs, f.bys, f.lfxs, J.plan.world > 1 ? c->lf_mine.p : nullptr, c->vb.p,
+            c->vcount.p};
   launch_vb_list(va, f.nlf, s);
   JXG_HIP(hipMemsetAsync(c->lfhist.p, 0, (size_t)J.nstreams * 4 * kAlpha * 4, s));
   JXG_HIP(hipMemsetAsync(c->sbound.p, 0, J.nstreams * 4, s));
@@ -1478,9 +1557,16 @@ static jxg_status shard_begin(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32_t
   if ((st = stage_front(c, J))) return st;
   if ((st = stage_ac_stats(c, J))) return st;
   JXG_HIP(hipMemcpyAsync(d_hist, c->hist_ac.p, kMaxClusters * kAlpha * 4, hipMemcpyDeviceToDevice, s));
-  const uint32_t maxg = (J.f.ngroups + world - 1) / world;
-  PackArgs pa{c->acs.p, c->qf.p, c->dc.p, J.f.bxs, J.f.bys, J.f.gxs, d_xbuf,
-              (size_t)maxg * kGroupRecordBytes, rank, world, J.f.ngroups};
+  // the send list (then the receive list) of the record exchange
+  const Exchange& X = J.plan.x;
+  JXG_HIP(c->xlist.ensure(X.send.size() + X.recv.size() + 1));
+  if (!X.send.empty())
+    JXG_HIP(hipMemcpyAsync(c->xlist.p, X.send.data(), X.send.size() * 4, hipMemcpyHostToDevice, s));
+  if (!X.recv.empty())
+    JXG_HIP(hipMemcpyAsync(c->xlist.p + X.send.size(), X.recv.data(), X.recv.size() * 4,
+                           hipMemcpyHostToDevice, s));
+  PackArgs pa{c->acs.p, c->qf.p, c->dc.p, J.f.bxs, J.f.bys, J.f.gxs, d_xbuf, c->xlist.p,
+              (uint32_t)X.send.size()};
   launch_pack(pa, s);
   JXG_HIP(hipGetLastError());
   JXG_HIP(hipEventRecord(c->ev[1], s));
@@ -1495,10 +1581,10 @@ static jxg_status shard_end(Ctx* c, const uint32_t* d_hist, const uint8_t* d_xbu
   Job& J = *c->job;
   hipStream_t s = c->stream;
   const uint32_t world = J.plan.world;
-  const uint32_t maxg = (J.f.ngroups + world - 1) / world;
+  const Exchange& X = J.plan.x;
   PackArgs pa{c->acs.p, c->qf.p, c->dc.p, J.f.bxs, J.f.bys, J.f.gxs,
-              const_cast<uint8_t*>(d_xbuf), (size_t)maxg * kGroupRecordBytes,
-              J.plan.rank, world, J.f.ngroups};
+              const_cast<uint8_t*>(d_xbuf), c->xlist.p + X.send.size(),
+              (uint32_t)X.recv.size()};
   launch_unpack(pa, s);
   JXG_HIP(hipGetLastError());
   jxg_status st;
@@ -1988,7 +2074,27 @@ jxg_status jxg_shard_sizes(uint32_t xsize, uint32_t ysize, uint32_t world, size_
     return JXG_ERR_INVALID_ARG;
   const Frame f = make_frame(xsize, ysize, 1.0f);
   *hist_words = (size_t)kMaxClusters * kAlpha;
-  *slot_bytes = (size_t)((f.ngroups + world - 1) / world) * kGroupRecordBytes;
+  // the largest send or receive buffer of any rank
+  const std::vector<uint32_t> owner = lf_owners(f, world);
+  size_t most = 1;
+  for (uint32_t r = 0; r < world && world > 1; r++) {
+    const Exchange X = make_exchange(f, owner, r, world);
+    most = std::max(most, std::max(X.send.size(), X.recv.size()));
+  }
+  *slot_bytes = most * kGroupRecordBytes;
+  return JXG_OK;
+}
+
+jxg_status jxg_shard_exchange(uint32_t xsize, uint32_t ysize, uint32_t world, uint32_t rank,
+                              size_t* send_bytes, size_t* recv_bytes) {
+  if (!send_bytes || !recv_bytes || xsize == 0 || ysize == 0 || world == 0 || rank >= world)
+    return JXG_ERR_INVALID_ARG;
+  const Frame f = make_frame(xsize, ysize, 1.0f);
+  const Exchange X = make_exchange(f, lf_owners(f, world), rank, world);
+  for (uint32_t p = 0; p < world; p++) {
+    send_bytes[p] = (size_t)X.nsend[p] * kGroupRecordBytes;
+    recv_bytes[p] = (size_t)X.nrecv[p] * kGroupRecordBytes;
+  }
   return JXG_OK;
 }
 

@@ -66,7 +66,7 @@ struct MergeArgs {
 struct VbArgs {
   const uint8_t* acs;
   uint32_t bxs, bys, lfxs;
-  uint32_t rank, world;  // LF group lg belongs to shard lg % world
+  const uint8_t* lf_mine;  // [nlf] 1 = this shard owns the LF group (null: all)
   uint32_t* vb;     // [nlf][65536] block index (frame raster) of each varblock
   uint32_t* count;  // [nlf]
 };
@@ -190,12 +190,12 @@ struct PackArgs {
   uint8_t* qf;
   int32_t* dc;
   uint32_t bxs, bys, gxs;
-  uint8_t* xbuf;           // [world][slot_bytes]
-  size_t slot_bytes;
-  uint32_t rank, world, ngroups;
+  uint8_t* xbuf;          // n group records back to back
+  const uint32_t* list;   // [n] group of each record
+  uint32_t n;
 };
-void launch_pack(const PackArgs& a, hipStream_t s);    // own groups -> own slot
-void launch_unpack(const PackArgs& a, hipStream_t s);  // other slots -> frame arrays
+void launch_pack(const PackArgs& a, hipStream_t s);    // frame arrays -> records
+void launch_unpack(const PackArgs& a, hipStream_t s);  // records -> frame arrays
 void launch_homog(const HomogArgs& a, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s);
 void launch_ac_hist(const AcArgs& a, uint32_t ngroups, hipStream_t s);
 void launch_ac_emit(const AcArgs& a, uint32_t ngroups, hipStream_t s);

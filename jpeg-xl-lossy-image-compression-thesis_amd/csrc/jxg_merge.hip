@@ -817,7 +817,7 @@ __global__ __launch_bounds__(1024) void vb_list_kernel(VbArgs a) {
   __shared__ uint32_t sCnt[64 * 16];
   __shared__ uint32_t sWave[16];
   const uint32_t lg = blockIdx.x;
-  if (a.world > 1 && lg % a.world != a.rank) return;  // LF group of another shard
+  if (a.lf_mine && !a.lf_mine[lg]) return;  // LF group of another shard
   const uint32_t bx0 = (lg % a.lfxs) * 256, by0 = (lg / a.lfxs) * 256;
   const uint32_t bw = min(256u, a.bxs - bx0), bh = min(256u, a.bys - by0);
   const uint32_t n = bw * bh;

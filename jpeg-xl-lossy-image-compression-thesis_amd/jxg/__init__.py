@@ -80,7 +80,7 @@ EXPORTS = ("jxg_status_str", "jxg_create", "jxg_destroy", "jxg_encode_rgb8",
            "jxg_shard_end", "jxg_shard_payload", "jxg_shard_assemble_device",
            "jxg_shard_assemble", "jxg_compare_rgb8", "jxg_compare_rgb8_device",
            "jxg_shard_head", "jxg_shard_write_host", "jxg_host_register", "jxg_host_unregister",
-           "jxg_encode_batch_rgb8_device", "jxg_synth_rgb8_device")
+           "jxg_encode_batch_rgb8_device", "jxg_synth_rgb8_device", "jxg_shard_exchange")
 
 _lib = None
 
@@ -115,6 +115,8 @@ def load():
     sz = ctypes.c_size_t
     lib.jxg_shard_sizes.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                     ctypes.POINTER(sz), ctypes.POINTER(sz)]
+    lib.jxg_shard_exchange.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                       ctypes.c_uint32, ctypes.POINTER(sz), ctypes.POINTER(sz)]
     lib.jxg_shard_begin.argtypes = [vp, vp, ctypes.c_uint32, ctypes.c_uint32, sz, ctypes.c_uint32,
                                     ctypes.c_uint32, vp, vp]
     lib.jxg_shard_end.argtypes = [vp, vp, vp, ctypes.POINTER(sz)]
@@ -393,10 +395,20 @@ class Encoder:
 # sharding helpers (host side; no device needed)
 # ---------------------------------------------------------------------------
 def shard_sizes(width: int, height: int, world: int):
-    """(AC histogram words, exchange slot bytes) of a sharded encode."""
+    """(AC histogram words, record buffer bytes) of a sharded encode: the
+    capacity of the send and of the receive buffer (largest of any rank)."""
     hw, sb = ctypes.c_size_t(), ctypes.c_size_t()
     _check(load().jxg_shard_sizes(width, height, world, ctypes.byref(hw), ctypes.byref(sb)))
     return hw.value, sb.value
+
+
+def shard_exchange(width: int, height: int, world: int, rank: int):
+    """(send bytes per peer, receive bytes per peer) of this rank's record
+    exchange (an all_to_all with these splits)."""
+    snd = (ctypes.c_size_t * world)()
+    rcv = (ctypes.c_size_t * world)()
+    _check(load().jxg_shard_exchange(width, height, world, rank, snd, rcv))
+    return [int(x) for x in snd], [int(x) for x in rcv]
 
 
 def shard_assemble(payloads) -> bytes:
@@ -419,13 +431,49 @@ def lf_group_count(width: int, height: int) -> int:
     return ((width + 2047) // 2048) * ((height + 2047) // 2048)
 
 
+def _shard_of(ng: int, g: int, world: int) -> int:
+    r = g * world // ng
+    while r + 1 < world and ng * (r + 1) // world <= g:
+        r += 1
+    while r > 0 and ng * r // world > g:
+        r -= 1
+    return r
+
+
+def lf_owners(width: int, height: int, world: int) -> list:
+    """Owner rank of every LF group in a sharded encode (== jxg_host.cpp
+    lf_owners): the rank holding the most of the LF group's pass groups, less
+    16 per LF group already assigned to it; ties to the lower rank."""
+    gxs, gys = -(-width // 256), -(-height // 256)
+    lfxs, lfys = -(-width // 2048), -(-height // 2048)
+    ng = gxs * gys
+    own, nas = [], [0] * world
+    for lg in range(lfxs * lfys):
+        if world == 1:
+            own.append(0)
+            continue
+        lx, ly = lg % lfxs, lg // lfxs
+        cnt = [0] * world
+        for gy in range(ly * 8, min(ly * 8 + 8, gys)):
+            for gx in range(lx * 8, min(lx * 8 + 8, gxs)):
+                cnt[_shard_of(ng, gy * gxs + gx, world)] += 1
+        best, bs = -1, 0
+        for r in range(world):
+            if cnt[r] and (best < 0 or cnt[r] - 16 * nas[r] > bs):
+                best, bs = r, cnt[r] - 16 * nas[r]
+        own.append(best)
+        nas[best] += 1
+    return own
+
+
 def shard_sections(width: int, height: int, rank: int, world: int):
     """TOC indices of the sections rank `rank` of `world` produces (the
-    ownership of jxg_host.cpp make_plan): LfGlobal / HfGlobal on rank 0, LF
-    groups lg % world == rank, pass groups [n*rank/world, n*(rank+1)/world)."""
+    ownership of jxg_host.cpp make_plan): LfGlobal / HfGlobal on rank 0, the
+    LF groups it owns (lf_owners), pass groups [n*rank/world, n*(rank+1)/world)."""
     ng, nlf = group_count(width, height), lf_group_count(width, height)
     ids = [0] if rank == 0 else []
-    ids += [1 + lg for lg in range(nlf) if lg % world == rank]
+    owners = lf_owners(width, height, world)
+    ids += [1 + lg for lg in range(nlf) if owners[lg] == rank]
     if rank == 0:
         ids.append(1 + nlf)
     g0, g1 = ng * rank // world, ng * (rank + 1) // world

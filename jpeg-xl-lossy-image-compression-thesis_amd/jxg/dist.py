@@ -1,12 +1,16 @@
 """Multi-GPU group-sharded encode over torch.distributed.
 
 One process per GPU (backend "nccl" = RCCL over xGMI).  Each rank encodes a
-balanced contiguous raster range of the frame's 256x256 pass groups; the only
-collectives are
+balanced contiguous raster range of the frame's 256x256 pass groups and the
+LF groups it owns (the rank holding most of an LF group's pass groups); the
+only collectives are
   1. all_reduce(sum) of the AC token histogram (132 x 128 u32, 68 KB) so all
      ranks derive the same prefix codes,
-  2. all_gather of the per-block records (strategy, quant field, quantized DC;
-     14 B per 8x8 block) that the LF-group streams of other ranks read,
+  2. all_to_all of per-block records (strategy, quant field, quantized DC;
+     14 B per 8x8 block): a rank sends the records of its pass groups whose LF
+     group another rank owns to that rank only (jxg_shard_exchange splits;
+     8K over 8 ranks: ~0.7 MB per rank instead of an all-gather of 7.3 MB;
+     16384^2 over 8 ranks: nothing),
   3. assembly, either
      host   (``host=SharedHostBuffer``): one all-gather of the payload heads
             (section ids and sizes, ~2 KB per rank), then every rank DMAs its
@@ -28,7 +32,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from . import Encoder, load, shard_assemble, shard_sizes
+from . import Encoder, load, shard_assemble, shard_exchange, shard_sizes
 
 
 class SharedHostBuffer:
@@ -39,6 +43,10 @@ class SharedHostBuffer:
 
     def __init__(self, rank: int, world: int, group=None):
         self.rank, self.world, self.group = rank, world, group
+        # every rank must map the same /dev/shm file: refuse (on every rank,
+        # before any shared-memory use) unless all ranks run on one node
+        if not self.single_node(group):
+            raise RuntimeError("SharedHostBuffer needs all ranks on one node; use device assembly")
         tag = [os.getpid()] if rank == 0 else [None]
         dist.broadcast_object_list(tag, src=0, group=group)
         self.tag = tag[0]
@@ -47,6 +55,16 @@ class SharedHostBuffer:
         self.mm = None
         self.addr = 0
         self.path = None
+
+    @staticmethod
+    def single_node(group=None) -> bool:
+        """True when every rank of `group` runs on this host (a collective)."""
+        import socket
+
+        names = [None] * dist.get_world_size(group)
+        dist.all_gather_object(names, (socket.gethostname(), os.path.exists("/dev/shm")),
+                               group=group)
+        return len(set(names)) == 1 and names[0][1]
 
     def _release(self):
         if self.mm is not None:
@@ -82,6 +100,8 @@ class SharedHostBuffer:
         self.cap = cap
 
     def view(self, n: int) -> np.ndarray:
+        """zero-copy view of the codestream; valid until the next frame's
+        write into the buffer (or close)"""
         return np.frombuffer(self.mm, dtype=np.uint8, count=n)
 
     def close(self):
@@ -142,19 +162,26 @@ def encode_sharded(enc: Encoder, d_rgb: torch.Tensor, width: int, height: int, r
     ``host`` a numpy view of the shared buffer), None elsewhere.  `bufs`
     caches the exchange tensors across calls."""
     dev = d_rgb.device
-    hist_words, slot = shard_sizes(width, height, world)
     if bufs is None:
         bufs = {}
-    key = (width, height, world)
+    key = (width, height, world, rank)
     if bufs.get("key") != key:
+        hist_words, cap = shard_sizes(width, height, world)
+        snd, rcv = shard_exchange(width, height, world, rank)
         bufs.clear()
         bufs["key"] = key
         bufs["hist"] = torch.zeros(hist_words, dtype=torch.int32, device=dev)
-        bufs["xbuf"] = torch.zeros(world * slot, dtype=torch.uint8, device=dev)
-    hist, xbuf = bufs["hist"], bufs["xbuf"]
+        bufs["send"] = torch.zeros(cap, dtype=torch.uint8, device=dev)
+        bufs["recv"] = torch.zeros(cap, dtype=torch.uint8, device=dev)
+        bufs["splits"] = (snd, rcv)
+        # a collective is skipped only when NO rank exchanges (every rank
+        # derives the same answer from the geometry)
+        bufs["any"] = any(sum(shard_exchange(width, height, world, r)[0]) for r in range(world))
+    hist, send, recv = bufs["hist"], bufs["send"], bufs["recv"]
+    snd, rcv = bufs["splits"]
     enc.shard_begin(d_rgb.data_ptr(), width, height, rank, world, hist.data_ptr(),
-                    xbuf.data_ptr())
-    mine = xbuf[rank * slot:(rank + 1) * slot]
+                    send.data_ptr())
+    ns, nr = sum(snd), sum(rcv)
     gloo = dist.get_backend(group) == "gloo"
     if gloo:
         # host staging (gloo: CPU rehearsal of the exchange, e.g. several ranks
@@ -162,14 +189,18 @@ def encode_sharded(enc: Encoder, d_rgb: torch.Tensor, width: int, height: int, r
         h = hist.cpu()
         dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
         hist.copy_(h)
-        parts = [torch.empty(slot, dtype=torch.uint8) for _ in range(world)]
-        dist.all_gather(parts, mine.cpu(), group=group)
-        xbuf.copy_(torch.cat(parts))
+        if bufs["any"]:
+            r_cpu = torch.empty(nr, dtype=torch.uint8)
+            dist.all_to_all_single(r_cpu, send[:ns].cpu(), output_split_sizes=rcv,
+                                   input_split_sizes=snd, group=group)
+            recv[:nr].copy_(r_cpu)
     else:
         dist.all_reduce(hist, op=dist.ReduceOp.SUM, group=group)
-        dist.all_gather_into_tensor(xbuf, mine.clone(), group=group)
+        if bufs["any"]:
+            dist.all_to_all_single(recv[:nr], send[:ns], output_split_sizes=rcv,
+                                   input_split_sizes=snd, group=group)
     torch.cuda.synchronize(dev)  # the library's stream reads what the collectives wrote
-    size = enc.shard_end(hist.data_ptr(), xbuf.data_ptr())
+    size = enc.shard_end(hist.data_ptr(), recv.data_ptr())
     if host is not None:
         heads = _all_gather_heads(enc.shard_head(), rank, world, width, height, group)
         ok, total = enc.shard_write_host(heads, host.addr, host.cap)

@@ -1,6 +1,7 @@
 """GPU group sharding on one device: `world` contexts play the
-ranks, the collectives are done with torch ops (sum of the histograms, slot
-concatenation), and the assembled codestream must equal the single-context
+ranks, the collectives are done with torch ops (sum of the histograms; the
+all_to_all of the per-block records by the jxg_shard_exchange splits), and the
+assembled codestream must equal the single-context
 encode byte for byte (one AC histogram -> one HF preset, so sharding does not
 change a bit).  The multi-process RCCL version of the same exchange is
 jxg.dist.encode_sharded (bench.py --gpus N)."""
@@ -10,23 +11,41 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def sharded_encode(jxg_mod, img, world, d=1.0, e=7, p=0):
+def sharded_encode(jxg_mod, img, world, d=1.0, e=7, p=0, flags=0, t=None):
     import torch
 
-    h, w, _ = img.shape
-    t = torch.from_numpy(np.ascontiguousarray(img)).cuda()
-    hist_words, slot = jxg_mod.shard_sizes(w, h, world)
-    encs = [jxg_mod.Encoder(distance=d, effort=e, proposals=p) for _ in range(world)]
+    if t is None:
+        h, w, _ = img.shape
+        t = torch.from_numpy(np.ascontiguousarray(img)).cuda()
+    else:
+        h, w, _ = t.shape
+    hist_words, cap = jxg_mod.shard_sizes(w, h, world)
+    plan = [jxg_mod.shard_exchange(w, h, world, r) for r in range(world)]
+    encs = [jxg_mod.Encoder(distance=d, effort=e, proposals=p, flags=flags) for _ in range(world)]
     hists = [torch.zeros(hist_words, dtype=torch.int32, device="cuda") for _ in range(world)]
-    xbufs = [torch.zeros(world * slot, dtype=torch.uint8, device="cuda") for _ in range(world)]
+    sends = [torch.zeros(cap, dtype=torch.uint8, device="cuda") for _ in range(world)]
     for r in range(world):
-        encs[r].shard_begin(t.data_ptr(), w, h, r, world, hists[r].data_ptr(), xbufs[r].data_ptr())
+        encs[r].shard_begin(t.data_ptr(), w, h, r, world, hists[r].data_ptr(), sends[r].data_ptr())
     hist = torch.stack(hists).sum(0).to(torch.int32).contiguous()
-    xbuf = torch.cat([xbufs[r][r * slot:(r + 1) * slot] for r in range(world)]).contiguous()
+
+    def segment(src, dst):  # src's records for dst (send order: by destination)
+        snd = plan[src][0]
+        o = sum(snd[:dst])
+        return sends[src][o:o + snd[dst]]
+
+    recvs = []
+    for r in range(world):
+        parts = [segment(q, r) for q in range(world) if q != r]
+        rb = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+        if parts:
+            cat = torch.cat(parts)
+            assert cat.numel() == sum(plan[r][1])
+            rb[:cat.numel()] = cat
+        recvs.append(rb)
     torch.cuda.synchronize()
     payloads = []
     for r in range(world):
-        size = encs[r].shard_end(hist.data_ptr(), xbuf.data_ptr())
+        size = encs[r].shard_end(hist.data_ptr(), recvs[r].data_ptr())
         payloads.append(encs[r].shard_payload_bytes(size))
     # distributed host assembly: every "rank" writes its sections into one
     # host buffer (first call with a too-small buffer reports the size)
@@ -138,22 +157,16 @@ def test_sharded_ans_equals_single(jxg_mod):
     img = synth_rgb8(1500, 900, 17)
     with jxg_mod.Encoder(distance=1.0, effort=7, flags=jxg_mod.FLAG_ANS) as enc:
         ref = enc.encode(img)
-    import torch
+    assert sharded_encode(jxg_mod, img, 3, flags=jxg_mod.FLAG_ANS) == ref
 
-    h, w, _ = img.shape
-    world = 3
-    t = torch.from_numpy(img).cuda()
-    hist_words, slot = jxg_mod.shard_sizes(w, h, world)
-    encs = [jxg_mod.Encoder(distance=1.0, effort=7, flags=jxg_mod.FLAG_ANS) for _ in range(world)]
-    hists = [torch.zeros(hist_words, dtype=torch.int32, device="cuda") for _ in range(world)]
-    xbufs = [torch.zeros(world * slot, dtype=torch.uint8, device="cuda") for _ in range(world)]
-    for r in range(world):
-        encs[r].shard_begin(t.data_ptr(), w, h, r, world, hists[r].data_ptr(), xbufs[r].data_ptr())
-    hist = torch.stack(hists).sum(0).to(torch.int32).contiguous()
-    xbuf = torch.cat([xbufs[r][r * slot:(r + 1) * slot] for r in range(world)]).contiguous()
-    torch.cuda.synchronize()
-    payloads = [encs[r].shard_payload_bytes(encs[r].shard_end(hist.data_ptr(), xbuf.data_ptr()))
-                for r in range(world)]
-    for e in encs:
-        e.close()
-    assert jxg_mod.shard_assemble(payloads) == ref
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_sharded_8k_strong(jxg_mod, world):
+    """BASELINE config 2 as written: one 8K frame split over `world` ranks
+    (strong scaling), records exchanged only to the LF-group owners"""
+    from jxg.synth import synth_rgb8_device
+
+    t = synth_rgb8_device(7680, 4320, 0x4A584C02)
+    with jxg_mod.Encoder(distance=1.0, effort=7) as enc:
+        ref = enc.encode_device(t.data_ptr(), 7680, 4320)
+    assert sharded_encode(jxg_mod, None, world, t=t) == ref

@@ -102,3 +102,34 @@ def test_gloo_world2_gather_and_assemble(jxg_mod, oracle, decoder):
         p.join(120)
         assert p.exitcode == 0
     assert q.get(timeout=10) == (True, True)
+
+
+@pytest.mark.parametrize("w,h,world", [(7680, 4320, 2), (7680, 4320, 8), (16384, 16384, 8),
+                                       (3840, 2160, 4), (2100, 600, 8), (4100, 5000, 3)])
+def test_record_exchange_plan(jxg_mod, w, h, world):
+    """jxg_shard_exchange (C++) against the Python mirror of the LF ownership:
+    a rank sends each of its pass groups' records to the owner of the group's
+    LF group (if another rank), receives the other ranks' groups inside its
+    own LF groups; sends and receives pair up across ranks."""
+    rec = 1024 * 2 + 1024 * 4 * 3
+    owners = jxg_mod.lf_owners(w, h, world)
+    gxs, gys = -(-w // 256), -(-h // 256)
+    lfxs = -(-w // 2048)
+    ng = gxs * gys
+    plan = [jxg_mod.shard_exchange(w, h, world, r) for r in range(world)]
+    for r in range(world):
+        snd, rcv = plan[r]
+        for p in range(world):
+            want = sum(1 for g in range(ng * r // world, ng * (r + 1) // world)
+                       if p != r and owners[(g // gxs) // 8 * lfxs + (g % gxs) // 8] == p)
+            assert snd[p] == want * rec
+            assert rcv[p] == plan[p][0][r]  # what p sends to r
+    # every LF group has an owner that holds part of it; owners spread out
+    assert all(0 <= o < world for o in owners)
+    _, cap = jxg_mod.shard_sizes(w, h, world)
+    assert all(max(sum(s), sum(rv)) <= cap for s, rv in plan)
+    if (w, h, world) == (16384, 16384, 8):
+        assert all(sum(s) == 0 for s, _ in plan)  # LF groups aligned with the ranks
+    if (w, h, world) == (7680, 4320, 8):
+        total = sum(sum(s) for s, _ in plan)
+        assert total < 7680 * 4320 // 64 * 14  # well under an all-gather's worth
