@@ -6,7 +6,13 @@ metric), device-resident RGB8 in HBM -> complete .jxl bytes in host memory.
                   [--scaling strong|weak] [--coder prefix|ans] [--config C]
 
 One step = one full encode (front end + merge stage, token statistics, entropy
-codes, bit emission, assembly, D2H of the codestream).
+codes, bit emission, assembly, D2H of the codestream).  The AC stream is
+ANS-coded by default (libjxl's e7 entropy coder; --coder prefix for prefix
+codes).  Single-GPU and replica steps go through the library's streaming entry
+points (jxg_submit_rgb8_device / jxg_receive: a one-thread software pipeline
+inside the library in which the rANS chains of earlier frames run under the
+transform kernels of later ones); the timed region ends when the last
+codestream of the K steps is in host memory.
 
 N = 1: one 7680x4320 frame per step (BASELINE config 2's frame on one GPU).
 N > 1 (launched by torch.distributed.run, backend nccl = RCCL):
@@ -24,7 +30,8 @@ N > 1 (launched by torch.distributed.run, backend nccl = RCCL):
           parallelism, no data-path collective).
 Timing: barrier + synchronize on both sides of the K steps, max over ranks.
 --streams S (non-shard modes) runs S concurrent encoders per GPU (one host
-thread, context and HIP stream each; the K frames split between them).
+thread, context and HIP stream each; the K frames split between them) through
+the one-at-a-time entry point instead (--no-pipeline: S = 1 of those).
 
 The JSON line also carries:
   roofline     -- the fused front kernel (XYB + homogeneity + AQ + 8x8 ACS +
@@ -32,7 +39,7 @@ The JSON line also carries:
                   B/px) per launch / its HIP-event duration (its own events, on
                   the encoder's stream) vs 8.0 TB/s; the design's own bytes
                   and the PMC-measured HBM traffic (profiles/) beside it;
-  ans_coder    -- the same workload with the other AC entropy coder;
+  alt_coder    -- the same workload with the other AC entropy coder;
   quality      -- decoded PSNR / bpp of a 1920x1080 crop (untimed);
   cpu_baseline -- the oracle/ C restatement with OpenMP on the host's cores
                   (libjxl absent on the box) on the same frame, and whether
@@ -43,6 +50,13 @@ import json
 import os
 import sys
 import time
+
+# The library's streaming pipeline runs four encoder lanes, one HIP stream
+# each; HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues per process
+# (default 4, one of them taken by torch's stream), and two lanes sharing a
+# queue serialise their kernels (the box exports 4).  Must be set before HIP
+# initialises.
+os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "jpeg-xl-lossy-image-compression-thesis_amd"))
@@ -170,14 +184,16 @@ def main():
                     help="shard mode: host = every rank DMAs its sections into one /dev/shm "
                          "buffer (rank 0 adds headers + TOC); device = payload gather to rank 0, "
                          "device assembly, one D2H")
-    ap.add_argument("--coder", choices=("prefix", "ans"), default="prefix",
+    ap.add_argument("--coder", choices=("prefix", "ans"), default="ans",
                     help="AC entropy coder (libjxl codes with ANS at e7)")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="one-at-a-time jxg_encode_rgb8_device calls instead of the streaming "
+                         "entry points")
     ap.add_argument("--streams", type=int, default=1,
                     help="concurrent encoders per GPU (replica / N=1 mode): one host thread, "
                          "context and HIP stream each; a step is still one frame")
-    ap.add_argument("--alt-ans-streams", type=int, default=1,
-                    help="also time the ANS coder with this many concurrent encoders "
-                         "(reported under 'ans_coder'; 0 = off)")
+    ap.add_argument("--alt-coder", type=int, default=1,
+                    help="also time the other AC coder (reported under 'alt_coder'; 0 = off)")
     ap.add_argument("--alt-thesis", type=int, default=1,
                     help="also time the workload with the thesis proposals P+F "
                          "(reported under 'thesis_proposals'; 0 = off)")
@@ -213,8 +229,7 @@ def main():
     frames = 1 if shard else nframes
     d_imgs = [d_img] + [synth_rgb8_device(w, h, SEED_BASE + args.config + f, local)
                         for f in range(1, frames)]
-    # batch configs: one step = the whole batch through the batched entry point
-    batch = frames > 1 and args.streams == 1
+    pipeline = not shard and args.streams == 1 and not args.no_pipeline
     ptrs = [t.data_ptr() for t in d_imgs]
     fh = h
     if shard and not strong:
@@ -244,30 +259,48 @@ def main():
                 from jxg.dist import encode_sharded
                 return encode_sharded(e, d_img, w, fh, rank, world, bufs=bufs, copy=False,
                                       host=host)
-            if batch:
-                # the whole batch through the library's batched entry point
-                # (jxg_encode_batch_rgb8_device: three lanes, own streams)
-                return e.encode_batch_device(ptrs, w, fh, copy=False)[0]
             return e.encode_device(d_imgs[k % frames].data_ptr(), w, fh, copy=False)
 
-        for e in encs:  # contexts warmed one after another
-            for _ in range(args.warmup):
-                step(e)
         rec = {"front_ms": [], "host_ms": [], "sizes": [], "last": None}
+
+        def took(e, k, out):
+            t = e.timings()
+            rec["front_ms"].append(t[0])
+            rec["host_ms"].append(t[1:])
+            rec["sizes"].append(len(out) if out is not None else 0)
+            if k % frames == 0:
+                rec["last"] = out
 
         def worker(e, ks):
             # the codestream ends in (pinned) host memory; ctypes calls release
             # the GIL, so the encoders' host work and HIP streams overlap
+            if pipeline:
+                # streaming entry points: submit every frame, receive each
+                # codestream as soon as it is done (more than the library's
+                # pipeline depth pending => the oldest is complete)
+                got = 0
+                for k in ks:
+                    e.submit_device(d_imgs[k % frames].data_ptr(), w, fh)
+                    while e.pending() > 4:
+                        took(e, got, e.receive(copy=False))
+                        got += 1
+                while e.pending():
+                    took(e, got, e.receive(copy=False))
+                    got += 1
+                return
             for k in ks:
-                out = step(e, k)
-                t = e.timings()
-                rec["front_ms"].append(t[0])
-                rec["host_ms"].append(t[1:])
-                rec["sizes"].append(len(out) if out is not None else 0)
-                if batch or k % frames == 0:
-                    rec["last"] = out
+                took(e, k, step(e, k))
 
-        total = args.steps * (1 if batch else frames)
+        for e in encs:  # contexts warmed one after another
+            if pipeline:
+                worker(e, range(max(args.warmup, 1) * frames))
+            else:
+                for _ in range(args.warmup):
+                    step(e)
+        for key in ("front_ms", "host_ms", "sizes"):
+            rec[key] = []
+
+        total = args.steps * frames
         share = [list(range(i, total, nstreams)) for i in range(nstreams)]
         if world > 1:
             dist.barrier()
@@ -308,11 +341,12 @@ def main():
     nbytes = R["sizes"][-1] if R["sizes"] else 0
     px_step = w * fh * (1 if shard else world) * frames
     alt = None
-    if not shard and args.alt_ans_streams > 0 and args.coder != "ans":
-        # the same workload with the ANS coder (libjxl's e7 entropy coder)
-        A = run("ans", args.alt_ans_streams)
+    other = "prefix" if args.coder == "ans" else "ans"
+    if not shard and args.alt_coder > 0:
+        # the same workload with the other AC entropy coder
+        A = run(other, nstreams)
         A["enc"].close()
-        alt = {"coder": "ans", "streams_per_gpu": args.alt_ans_streams,
+        alt = {"coder": other, "streams_per_gpu": nstreams, "pipeline": pipeline,
                "value": round(px_step * args.steps / A["dt"] / 1e6, 2),
                "ms_per_step": round(A["dt"] * 1e3 / args.steps, 3),
                "ms_latency": round(sum(x[0] for x in A["host_ms"]) / len(A["host_ms"]), 3),
@@ -323,7 +357,7 @@ def main():
         # the thesis proposals P + F (combined.diff) on the same workload:
         # the homogeneity selector in the front kernel, hook F on every
         # 8x8 and merge candidate
-        T = run(args.coder, 1, proposals=3)
+        T = run(args.coder, nstreams, proposals=3)
         T["enc"].close()
         thesis = {"proposals": "P+F (combined.diff)",
                   "value": round(px_step * args.steps / T["dt"] / 1e6, 2),
@@ -352,7 +386,8 @@ def main():
             workload = ("%s %dx%d RGB8 (synth_rgb8), VarDCT d%g e%d, proposals=%d, %s, "
                         "%d distinct frame(s) per step, %s"
                         % (name, w, h, args.distance, args.effort, args.proposals, coder_desc,
-                           frames, "jxg_encode_batch_rgb8_device (3 lanes)" if batch else
+                           frames, "streaming entry points (jxg_submit_rgb8_device / "
+                           "jxg_receive, one host thread)" if pipeline else
                            "%d concurrent encoder stream(s) per rank" % nstreams))
             par = "frame-dp%d" % world
         label = {"8k": "8K", "4k": "4K", "16k": "16384x16384", "cpu512": "512x512",
@@ -374,6 +409,7 @@ def main():
             "config": {"workload": workload, "global_batch": 1 if shard else world * frames,
                        "parallelism": par},
             "streams_per_gpu": nstreams,
+            "pipeline": pipeline,
             "ms_latency": round(sum(x[0] for x in host_ms) / len(host_ms), 3),
             "bytes_per_frame": nbytes,
             "bpp": round(nbytes * 8.0 / frame_px, 4),
@@ -398,7 +434,7 @@ def main():
                             "valu_issue_frac_pmc": load_merge_pmc(name) if world == 1 else None},
         }
         if alt is not None:
-            res["ans_coder"] = alt
+            res["alt_coder"] = alt
         if thesis is not None:
             res["thesis_proposals"] = thesis
         if world == 1 and not args.no_quality:

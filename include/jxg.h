@@ -103,6 +103,26 @@ jxg_status jxg_encode_batch_rgb8(void* ctx, const uint8_t* const* rgbs, uint32_t
 jxg_status jxg_encode_batch_rgb8_device(void* ctx, const void* const* d_rgbs, uint32_t n,
                                         uint32_t xsize, uint32_t ysize, size_t row_stride,
                                         jxg_buffer* outs);
+/* Streaming encode, one host thread: frames are submitted in order and their
+ * codestreams received in the same order (byte-identical to jxg_encode_rgb8
+ * of each frame).  Internally a software pipeline over this context and three
+ * lanes it creates on first use (same parameters; released by jxg_destroy):
+ * a submit finishes the frame submitted four calls earlier if it is still in
+ * flight, launches the new frame's front end / merge stage / statistics, and
+ * builds the previous frame's codes and launches its emission -- so the rANS
+ * chains (JXG_FLAG_ANS) of two frames run under the transform kernels of the
+ * next.  jxg_receive blocks until the oldest frame is complete
+ * (JXG_ERR_INVALID_ARG if none is pending); jxg_pending counts frames
+ * submitted and not yet received.  A device frame must stay unchanged until
+ * its codestream is received; a host frame is copied into pinned staging
+ * before jxg_submit_rgb8 returns.  jxg_get_stats after jxg_receive describes
+ * the received frame.  On an error every frame in flight is dropped. */
+jxg_status jxg_submit_rgb8(void* ctx, const uint8_t* rgb, uint32_t xsize, uint32_t ysize,
+                           size_t row_stride);
+jxg_status jxg_submit_rgb8_device(void* ctx, const void* d_rgb, uint32_t xsize, uint32_t ysize,
+                                  size_t row_stride);
+jxg_status jxg_receive(void* ctx, jxg_buffer* out);
+jxg_status jxg_pending(void* ctx, uint32_t* n);
 jxg_status jxg_get_stats(void* ctx, jxg_stats* stats);
 void jxg_buffer_free(jxg_buffer* buf);
 

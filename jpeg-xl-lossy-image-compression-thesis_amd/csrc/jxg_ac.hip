@@ -92,6 +92,9 @@ constexpr int kAcTok = 64;
 // 256x256 group, so only near-incompressible groups take the slow path
 // (ac_emit: 96 KiB + 33 KiB of code tables, one 1024-thread workgroup per CU)
 constexpr int kEmitLdsWords = 24576;
+// ans_emit's buffer: 80 KiB (10 bpp over a full group), so the kernel shares a
+// CU with a resident rANS chain workgroup (68 KB) of the next frame
+constexpr int kAnsEmitLdsWords = 20480;
 
 __device__ __forceinline__ int channel_of(int ci) { return ci == 0 ? 1 : (ci == 1 ? 0 : 2); }
 
@@ -481,106 +484,152 @@ __global__ __launch_bounds__(kAcThreads) void ac_emit_kernel(AcArgs a) {
 // sequential dependency), then the group's workgroup places the emitted bits
 // in parallel.
 // ---------------------------------------------------------------------------
-// rANS backwards over each group's records, one wave per group, 4 groups per
-// workgroup sharing the LDS tables (all alias inverses, 128 KB).  The state
-// recurrence is a uniform chain kept in VALU registers (a microbenchmark on
-// MI355X: dependent VALU op ~4.5 cycles, uniform LDS read ~70, while every
-// VALU <-> SALU crossing -- readlane, ballot -- costs ~30): per step compare,
-// select, magic-number division, one LDS lookup.  The lanes serve it: per 64
-// records they decode record, bound, division constants and table base in
-// parallel (the next 64 records are fetched meanwhile), and each lane keeps the
-// chunk of "its" record for one coalesced store of the record's emitted bits.
-constexpr int kAnsWaves = 4;
+// rANS backwards over each group's records, one wave per group, kAnsWaves
+// groups per workgroup sharing the LDS tables (all alias inverses, 64 KB).
+//
+// The state recurrence is the stream's only sequential dependency, so its
+// per-step latency sets the kernel time (a pass group holds up to ~100K
+// tokens).  The chain runs "on the diagonal": lane L holds record L's
+// constants in registers (no readlane per step) and step L is computed in
+// lane L from lane L-1's result, which a DPP wave rotation (wave_ror:1, VALU
+// to VALU) hands over; the other lanes run the same rANS steps on other
+// (valid) states, so every lane's table address stays in range.  The state
+// x = k << 12 | v is kept as (k = quotient of the previous step, v = its
+// inverse-table entry), which moves everything but the lookup off the
+// critical path:
+//   * emission: x >= f << 20  <=>  k >= f << 8, and then x >> 16 = k >> 4 --
+//     both known before v arrives;
+//   * quotient: floor(xs / f) = trunc((xs + 0.5) * rcp(f)) in f64 (exact: the
+//     error of the two roundings is < 2^-19 while (xs + .5) / f stays >= .5 / f
+//     from an integer), and (t + 0.5) * rcp is formed before v arrives, so
+//     after the LDS read: cvt, fma, cvt, one 24-bit multiply-add, the next read;
+//   * lane s saves its own pre-step state with a constant-mask select.
+// Per 64 records the lanes decode record, f, rcp and table base in parallel
+// (the next 64 records are fetched meanwhile) and store the emitted bits of
+// their record with one coalesced store.
+// One chain wave per SIMD (4 per workgroup; 68 KB of LDS, so the workgroup
+// shares its CU with a transform kernel of the next frame): a second chain
+// wave on the SIMD delays every step by its own issue (8 per workgroup: 6.7 vs
+// 6.0 ms at 8K, profiles/r02g); the chain waves run at the highest wave
+// priority so co-resident transform waves only fill their idle issue slots.
+#ifndef JXG_ANS_WAVES  // (experiment builds override it: tools/build_variant.sh)
+#define JXG_ANS_WAVES 4
+#endif
+constexpr int kAnsWaves = JXG_ANS_WAVES;
+__device__ __forceinline__ uint32_t wave_ror1(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x13C, 0xF, 0xF, false);
+}
 __global__ __launch_bounds__(kAnsWaves * 64) void ans_encode_kernel(AnsArgs a) {
   __shared__ uint32_t sSym[kAnsHists * 128];
-  __shared__ uint32_t sDiv[kAnsHists * 128];
   __shared__ uint32_t sInv[kAnsHists * 4096 / 2];  // u16 pairs
   __shared__ uint8_t sMap[136];
   const uint32_t* src = reinterpret_cast<const uint32_t*>(a.tab);
-  for (uint32_t i = threadIdx.x; i < a.nhist * 128; i += blockDim.x) {
-    sSym[i] = src[i];
-    sDiv[i] = src[kAnsDivOff / 4 + i];
-  }
+  for (uint32_t i = threadIdx.x; i < a.nhist * 128; i += blockDim.x) sSym[i] = src[i];
   for (uint32_t i = threadIdx.x; i < a.nhist * 2048; i += blockDim.x)
     sInv[i] = src[kAnsInvOff / 4 + i];
   for (uint32_t i = threadIdx.x; i < 136; i += blockDim.x) sMap[i] = a.tab[kAnsMapOff + i];
   __syncthreads();
-  const uint16_t* inv = reinterpret_cast<const uint16_t*>(sInv);
+  const uint8_t* inv = reinterpret_cast<const uint8_t*>(sInv);
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t g =
       __builtin_amdgcn_readfirstlane(a.g0 + blockIdx.x * kAnsWaves + (threadIdx.x >> 6));
   if (g >= a.g1) return;
+  __builtin_amdgcn_s_setprio(3);
   const int n = (int)(a.ntok[g * 3] + a.ntok[g * 3 + 1] + a.ntok[g * 3 + 2]);
   const uint64_t b = (uint64_t)(g - a.g0) * kGroupTokStride;
-  uint32_t x = 0x130000u;
+  // every lane starts from the initial state x = 0x130000
+  uint32_t k = 0x130u, v = 0;
   uint32_t rec = (int)lane < min(64, n) ? a.tokens[b + n - 1 - lane] : 0u;
   for (int hi = n; hi > 0; hi -= 64) {
     const int cnt = min(64, hi);
-    // lane L: record hi - 1 - L -> renormalization bound, division constants,
-    // f, inverse-table base
-    uint32_t T = 0xFFFFFFFFu, M = 0, s1 = 0, s2 = 0, nf2 = (uint32_t)-8192, base = 0;
+    // lane L: record hi - 1 - L.  Lanes past cnt get f = 4096 (a valid
+    // never-emitting step on histogram 0).
+    uint32_t f = 4096, base2 = 0;
     if ((int)lane < cnt) {
-      const uint32_t h = sMap[rec & 0xFF], sym = h * 128 + ((rec >> 8) & 63);
-      const uint32_t e = sSym[sym];
-      const uint32_t f = (e & 0xFFF) + 1;
-      nf2 = (uint32_t)(-(int)(2 * f));
-      base = 2 * (h * 4096 + (e >> 12));  // byte offset of the symbol's inverse row
-      M = sDiv[sym];
-      const uint32_t lg = f > 1 ? 32 - __clz(f - 1) : 0;
-      s1 = f > 1 ? 1 : 0;
-      s2 = lg > 0 ? lg - 1 : 0;
-      T = f < 4096 ? (f << 20) - 1 : 0xFFFFFFFFu;  // emit a chunk when x > T
+      const uint32_t h = sMap[rec & 0xFF], e = sSym[h * 128 + ((rec >> 8) & 63)];
+      f = (e & 0xFFF) + 1;
+      base2 = 2 * (h * 4096 + (e >> 12));  // byte offset of the symbol's inverse row
     }
+    const uint32_t Fq = f << 8;  // emit iff k >= Fq
+    const uint32_t nf2 = (uint32_t)(-(int)(2 * f));
+    const double rcp = 1.0 / (double)f, hr = 0.5 * rcp;
     const int hn = hi - 64;
     const uint32_t nrec = (int)lane < min(64, hn) ? a.tokens[b + hn - 1 - lane] : 0u;
-    uint32_t och = 0;  // lane L: the state before record L's chunk (0: none)
-    auto step = [&](int i) {
-      const uint32_t Ti = __builtin_amdgcn_readlane(T, i);
-      const uint32_t Mi = __builtin_amdgcn_readlane(M, i);
-      const uint32_t s1i = __builtin_amdgcn_readlane(s1, i);
-      const uint32_t s2i = __builtin_amdgcn_readlane(s2, i);
-      const uint32_t nf2i = __builtin_amdgcn_readlane(nf2, i);
-      const uint32_t bi = __builtin_amdgcn_readlane(base, i);
-      const bool emit = x > Ti;  // (x >> 20) >= f
-      och = lane == (uint32_t)i ? (emit ? x : 0u) : och;
-      x = emit ? x >> 16 : x;
-      // q = floor(x / f); f = 1: magic 0, s1 = s2 = 0 -> q = x
-      const uint32_t x2 = 2 * x + bi;  // (mod 2^32; the difference below is small)
-      const uint32_t t = __umulhi(x, Mi);
-      const uint32_t q = (t + ((x - t) >> s1i)) >> s2i;
-      // byte address 2 (base + x - q f): one 24-bit multiply-add (q < 2^20)
-      uint32_t addr;
-      asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(addr) : "v"(q), "s"(nf2i), "v"(x2));
-      x = (q << 12) + *reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(inv) + addr);
-      asm volatile("" : "+v"(x));  // keep the chain in VALU registers
+    uint32_t X = 0;     // lane L: the state before record L's step
+    uint32_t xin = 0;   // the state handed to the previous step
+    auto step = [&](int s) {
+      // in the shadow of the previous step's LDS read: everything that needs
+      // only k (emission, the v-free part of the quotient and address, and
+      // the factors that drop v on an emitting step); then save the
+      // previous step's input state in its lane
+      const uint32_t kin = wave_ror1(k);
+      const bool emit = kin >= Fq;
+      const uint32_t t = (kin << 12) >> (emit ? 16 : 0);  // xs without v
+      const double P = __builtin_fma((double)t, rcp, hr);
+      const double rs = emit ? 0.0 : rcp;
+      const uint32_t two = emit ? 0u : 2u;
+      const uint32_t C = 2 * t + base2;
+      if (s > 0)
+        asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(X) : "v"(X), "v"(xin), "s"(1ull << (s - 1)));
+      __builtin_amdgcn_sched_barrier(0);
+      // critical path: v -> quotient -> address -> next read
+      const uint32_t vin = wave_ror1(v);
+      const uint32_t kk = (uint32_t)__builtin_fma((double)vin, rs, P);
+      uint32_t x2, addr;
+      asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(x2) : "v"(vin), "v"(two), "v"(C));
+      asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(addr) : "v"(kk), "v"(nf2), "v"(x2));
+      v = *reinterpret_cast<const uint16_t*>(inv + addr);
+      k = kk;
+      xin = (kin << 12) + vin;
+      __builtin_amdgcn_sched_barrier(0);
     };
     if (cnt == 64) {
 #pragma unroll
-      for (int i = 0; i < 64; i++) step(i);
+      for (int s = 0; s < 64; s++) step(s);
+      asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(X) : "v"(X), "v"(xin), "s"(1ull << 63));
     } else {
-      for (int i = 0; i < cnt; i++) step(i);
+      for (int s = 0; s < cnt; s++) {
+        const uint32_t kin = wave_ror1(k);
+        const bool emit = kin >= Fq;
+        const uint32_t t = (kin << 12) >> (emit ? 16 : 0);
+        const double P = __builtin_fma((double)t, rcp, hr);
+        const uint32_t C = 2 * t + base2;
+        const uint32_t vin = wave_ror1(v);
+        X = (int)lane == s ? (kin << 12) + vin : X;
+        const uint32_t vv = emit ? 0u : vin;
+        const uint32_t kk = (uint32_t)__builtin_fma((double)vv, rcp, P);
+        const uint32_t addr = (uint32_t)((int)(2 * vv + C) - (int)(2 * f) * (int)kk);
+        v = *reinterpret_cast<const uint16_t*>(inv + addr);
+        k = kk;
+      }
     }
     if ((int)lane < cnt) {
       // emitted bits of the record: [16-bit chunk] then its raw bits
+      const bool em = (X >> 20) >= f;
       const uint32_t raw = rec >> 18, nb = (rec >> 14) & 15;
-      a.val[b + hi - 1 - lane] = och ? (och & 0xFFFFu) | raw << 16 : raw;
-      a.len[b + hi - 1 - lane] = (uint8_t)(och ? nb + 16 : nb);
+      a.val[b + hi - 1 - lane] = em ? (X & 0xFFFFu) | raw << 16 : raw;
+      a.len[b + hi - 1 - lane] = (uint8_t)(em ? nb + 16 : nb);
     }
     rec = nrec;
+    if (hi <= 64) {  // the final state: lane cnt - 1's result
+      const uint32_t kf = __builtin_amdgcn_readlane(k, cnt - 1);
+      const uint32_t vf = __builtin_amdgcn_readlane(v, cnt - 1);
+      if (lane == 0) a.state[g] = (kf << 12) + vf;
+    }
   }
-  if (lane == 0) a.state[g] = __builtin_amdgcn_readfirstlane(x);
+  if (n == 0 && lane == 0) a.state[g] = 0x130000u;
 }
 
 // bit placement: the 32-bit state, then every record's bits, in order; a
 // contiguous record range per wave, coalesced reads, wave scans of the
 // lengths (as ac_emit)
 __global__ __launch_bounds__(kAcThreads) void ans_emit_kernel(AnsArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t sBits[kEmitLdsWords];
+  __shared__ __attribute__((aligned(16))) uint32_t sBits[kAnsEmitLdsWords];
   __shared__ uint32_t sWave[kAcThreads / 64];
   const uint32_t g = a.g0 + blockIdx.x;
   const uint32_t n = a.ntok[g * 3] + a.ntok[g * 3 + 1] + a.ntok[g * 3 + 2];
   const uint64_t b = (uint64_t)(g - a.g0) * kGroupTokStride;
-  for (int i = threadIdx.x; i < kEmitLdsWords / 4; i += blockDim.x)
+  for (int i = threadIdx.x; i < kAnsEmitLdsWords / 4; i += blockDim.x)
     reinterpret_cast<uint4*>(sBits)[i] = make_uint4(0, 0, 0, 0);
   constexpr int kWaves = kAcThreads / 64;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -600,7 +649,7 @@ __global__ __launch_bounds__(kAcThreads) void ans_emit_kernel(AnsArgs a) {
     total += x;
   }
   const uint64_t base = a.base[g];
-  const bool lds = total <= (uint32_t)kEmitLdsWords * 32u;
+  const bool lds = total <= (uint32_t)kAnsEmitLdsWords * 32u;
   uint32_t* buf = lds ? sBits : a.scratch;
   const uint64_t bias = lds ? 0 : base;
   if (threadIdx.x == 0) {

@@ -93,8 +93,10 @@ struct AnsTable {
 AnsTable build_ans_table(const uint32_t* counts /* [128] */);
 // ANS histogram clustering (oracle/ans.c jxo_ans_cluster): hist[nh][128] ->
 // assign[nh] (centre id, -1 for an empty histogram); returns the centre count
-// (<= kAnsMaxHists: their alias inverses fill 128 KB of LDS in the encoder)
-constexpr int kAnsMaxHists = 16;
+// (<= kAnsMaxHists: their alias inverses fill 64 KB of LDS in the encoder, so
+// the rANS chain kernel co-resides with the transform kernels of the next
+// frame; oracle/jxo_internal.h JXO_ANS_MAX_HISTS)
+constexpr int kAnsMaxHists = 8;
 constexpr int64_t kAnsMinDist = 64ll << 16;  // Q16 bits
 int cluster_ans_histograms(const uint32_t* hist, int nh, int* assign);
 void write_ans_histogram(BitWriter& w, const AnsTable& t);

@@ -494,6 +494,7 @@ struct Ctx {
   std::vector<float> m_homog;
   jxg_stats stats{};
   std::unique_ptr<struct Job> job;  // sharded encode in flight (begin -> end)
+  std::unique_ptr<struct Pipe> pipe;  // streaming encode (jxg_submit_* / jxg_receive)
   std::vector<uint32_t> payload_head;  // last jxg_shard_end: payload head words
   size_t payload_body = 0;             //   and body bytes (in `out`)
 };
@@ -999,7 +1000,6 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
     uint8_t* blob = c->h_ans_tab.p;
     std::memset(blob, 0, kAnsTabBytes);
     uint32_t* sym = reinterpret_cast<uint32_t*>(blob);
-    uint32_t* dv = reinterpret_cast<uint32_t*>(blob + kAnsDivOff);
     uint16_t* inv = reinterpret_cast<uint16_t*>(blob + kAnsInvOff);
     for (int h = 0; h < nhist; h++) {
       AnsTable& t = ans_tables[h];
@@ -1009,12 +1009,6 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
         const uint32_t f = t.freq[k];
         if (!f) continue;
         sym[h * 128 + k] = (f - 1) | (uint32_t)t.cum[k] << 12;
-        // round-up magic with the "add" fix-up: exact for every 32-bit x;
-        // f = 1 uses magic 0 and s1 = 0 (see ans_encode_kernel)
-        uint32_t lg = 0;
-        while ((1u << lg) < f) lg++;
-        dv[h * 128 + k] =
-            f == 1 ? 0u : (uint32_t)((((uint64_t)1 << 32) * ((1ull << lg) - f)) / f + 1);
       }
     }
     for (int cl = 0; cl < kMaxClusters; cl++)
@@ -1436,19 +1430,19 @@ static jxg_status stage_concat_split(Ctx* c, Job& J, uint8_t** host_out, size_t*
   return JXG_OK;
 }
 
-static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32_t h,
-                                size_t stride, jxg_buffer* out, Clock::time_point t_call) {
+// ---- one frame, in three phases (encode_device runs them back to back; the
+// streaming pipeline interleaves the phases of consecutive frames) ----
+// phase 1: buffers, front end + merge stage + AC / LF statistics and their
+// downloads, all launched asynchronously on the context's stream
+static jxg_status enc_launch(Ctx* c, Job& J, const uint8_t* d_rgb, uint32_t w, uint32_t h,
+                             size_t stride) {
   hipStream_t s = c->stream;
-  const jxg_params& P = c->params;
-  Job J;
-  J.f = make_frame(w, h, P.distance);
+  J.f = make_frame(w, h, c->params.distance);
   J.plan = make_plan(J.f, 0, 1);
   J.w = w;
   J.h = h;
   J.stride = stride;
   J.d_rgb = d_rgb;
-  const Frame& f = J.f;
-  const size_t nb = (size_t)f.bxs * f.bys;
   jxg_status st = stage_alloc(c, J);
   if (st) return st;
   JXG_HIP(hipEventRecord(c->ev[0], s));
@@ -1457,18 +1451,34 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   if ((st = stage_ac_stats(c, J))) return st;
   if ((st = stage_download_ac(c, J, c->hist_ac.p))) return st;
   if ((st = stage_lf_stats(c, J))) return st;
-  if ((st = stage_download_lf(c, J))) return st;
-  if ((st = stage_codes(c, J))) return st;
-  // split assembly for a single context of a multi-group frame (single-group
-  // frames are one section; several contexts keep the one-stream assembly)
-  const bool split = f.ngroups > 1 && g_live_ctx.load() <= 1;
-  if ((st = stage_emit(c, J, !split))) return st;
+  return stage_download_lf(c, J);
+}
+
+// phase 2: (host, after the statistics arrive) codes and headers; AC / LF
+// emission launched
+static jxg_status enc_codes(Ctx* c, Job& J, bool sync) {
+  const jxg_status st = stage_codes(c, J);
+  if (st) return st;
+  return stage_emit(c, J, sync);
+}
+
+// phase 3: assembly, the codestream in host memory, stats
+static jxg_status enc_finish(Ctx* c, Job& J, bool split, jxg_buffer* out,
+                             Clock::time_point t_call) {
+  hipStream_t s = c->stream;
+  const jxg_params& P = c->params;
+  const Frame& f = J.f;
+  const size_t nb = (size_t)f.bxs * f.bys;
   const Clock::time_point t_layout = Clock::now();
   uint8_t* host_out = nullptr;
   size_t out_bytes = 0;
+  jxg_status st;
   if (split) {
     if ((st = stage_concat_split(c, J, &host_out, &out_bytes))) return st;
   } else {
+    // the emission's bit counts on the host (stage_emit may have returned
+    // without waiting)
+    JXG_HIP(hipStreamSynchronize(s));
     if ((st = stage_concat(c, J, true, nullptr, nullptr, &host_out, &out_bytes))) return st;
   }
   const float ms_layout = split ? J.ms_layout : ms_since(t_layout);
@@ -1498,8 +1508,8 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   // stats
   jxg_stats& S = c->stats;
   S = jxg_stats{};
-  S.xsize = w;
-  S.ysize = h;
+  S.xsize = J.w;
+  S.ysize = J.h;
   S.xsize_blocks = f.bxs;
   S.ysize_blocks = f.bys;
   S.num_groups = f.ngroups;
@@ -1527,6 +1537,143 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
   S.ms_host_codes = J.ms_codes;
   S.ms_host_layout = ms_layout;
   S.ms_host_call = ms_since(t_call);
+  return JXG_OK;
+}
+
+static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32_t h,
+                                size_t stride, jxg_buffer* out, Clock::time_point t_call) {
+  Job J;
+  jxg_status st = enc_launch(c, J, d_rgb, w, h, stride);
+  if (st) return st;
+  // split assembly for a single context of a multi-group frame (single-group
+  // frames are one section; several contexts keep the one-stream assembly)
+  const bool split = J.f.ngroups > 1 && g_live_ctx.load() <= 1;
+  if ((st = enc_codes(c, J, !split))) return st;
+  return enc_finish(c, J, split, out, t_call);
+}
+
+// ---------------------------------------------------------------------------
+// streaming encode (jxg_submit_rgb8[_device] / jxg_receive): a software
+// pipeline over kPipeLanes contexts (the caller's plus lanes it owns), driven
+// by the caller's one host thread.  Frame j runs on lane j % kPipeLanes:
+//   submit(j): finish frame j - kPipeLanes (its lane is needed again: wait for
+//              its emission, assemble, codestream to the host) -> launch frame
+//              j's front end, merge stage and statistics -> build frame j-1's
+//              codes and launch its emission.
+// So the rANS chains of frames j-1 and j-2 (latency-bound waves that use little
+// of their SIMDs; 68 KB of LDS per CU) run while frame j's transform kernels
+// fill the rest of the chip, and every chain has two submit periods to finish.
+// Four lanes = four streams = the process's hardware queues.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kPipeLanes = 4;
+struct PipeFrame {
+  Ctx* lane = nullptr;
+  Job J;
+  int phase = 1;  // 1: statistics launched; 2: emission launched
+  Clock::time_point t0;
+};
+struct PipeDone {
+  jxg_buffer buf;
+  jxg_stats stats;
+};
+struct Pipe {
+  std::vector<std::unique_ptr<PipeFrame>> inflight;  // submission order
+  std::vector<PipeDone> done;                        // submission order
+  uint64_t submitted = 0;
+};
+
+static jxg_status ensure_lanes(Ctx* c, uint32_t extra) {
+  while (c->lanes.size() < extra) {
+    void* lc = nullptr;
+    const jxg_status st = jxg_create(&c->params, &lc);
+    if (st) return st;
+    c->lanes.emplace_back(static_cast<Ctx*>(lc));
+  }
+  return JXG_OK;
+}
+
+// drop every frame in flight (after an error): wait for the lanes' streams
+static void pipe_abort(Ctx* c) {
+  Pipe& p = *c->pipe;
+  for (auto& fr : p.inflight) (void)hipStreamSynchronize(fr->lane->stream);
+  p.inflight.clear();
+}
+
+// oldest frame in flight -> done
+static jxg_status pipe_complete_oldest(Ctx* c) {
+  Pipe& p = *c->pipe;
+  PipeFrame& fr = *p.inflight.front();
+  jxg_status st = JXG_OK;
+  if (fr.phase == 1) st = enc_codes(fr.lane, fr.J, false);
+  PipeDone d{{nullptr, 0}, {}};
+  if (!st) st = enc_finish(fr.lane, fr.J, false, &d.buf, fr.t0);
+  if (st) {
+    pipe_abort(c);
+    return st;
+  }
+  d.stats = fr.lane->stats;
+  p.done.push_back(d);
+  p.inflight.erase(p.inflight.begin());
+  return JXG_OK;
+}
+
+static jxg_status pipe_submit(Ctx* c, const uint8_t* src, bool on_device, uint32_t w,
+                              uint32_t h, size_t stride) {
+  if (!c->pipe) c->pipe.reset(new (std::nothrow) Pipe());
+  if (!c->pipe) return JXG_ERR_OOM;
+  Pipe& p = *c->pipe;
+  jxg_status st = ensure_lanes(c, kPipeLanes - 1);
+  if (st) return st;
+  const Clock::time_point t0 = Clock::now();
+  if (p.inflight.size() >= kPipeLanes && (st = pipe_complete_oldest(c))) return st;
+  const uint32_t li = (uint32_t)(p.submitted % kPipeLanes);
+  Ctx* L = li == 0 ? c : c->lanes[li - 1].get();
+  std::unique_ptr<PipeFrame> fr(new (std::nothrow) PipeFrame());
+  if (!fr) return JXG_ERR_OOM;
+  fr->lane = L;
+  fr->t0 = t0;
+  if (!on_device) {
+    // the lane's previous frame has completed, so its staging is free
+    const size_t bytes = stride * (h - 1) + (size_t)w * 3;
+    if (L->h_stage.ensure(bytes) != hipSuccess || L->rgb.ensure(bytes) != hipSuccess)
+      return JXG_ERR_OOM;
+    std::memcpy(L->h_stage.p, src, bytes);
+    if (hipMemcpyAsync(L->rgb.p, L->h_stage.p, bytes, hipMemcpyHostToDevice, L->stream) !=
+        hipSuccess)
+      return JXG_ERR_HIP;
+    src = L->rgb.p;
+  }
+  if ((st = enc_launch(L, fr->J, src, w, h, stride))) {
+    (void)hipStreamSynchronize(L->stream);
+    return st;
+  }
+  p.inflight.push_back(std::move(fr));
+  p.submitted++;
+  // the previous frame: codes, emission launched
+  if (p.inflight.size() >= 2) {
+    PipeFrame& prev = *p.inflight[p.inflight.size() - 2];
+    if (prev.phase == 1) {
+      if ((st = enc_codes(prev.lane, prev.J, false))) {
+        pipe_abort(c);
+        return st;
+      }
+      prev.phase = 2;
+    }
+  }
+  return JXG_OK;
+}
+
+static jxg_status pipe_receive(Ctx* c, jxg_buffer* out) {
+  if (!c->pipe) return JXG_ERR_INVALID_ARG;
+  Pipe& p = *c->pipe;
+  if (p.done.empty()) {
+    if (p.inflight.empty()) return JXG_ERR_INVALID_ARG;
+    const jxg_status st = pipe_complete_oldest(c);
+    if (st) return st;
+  }
+  *out = p.done.front().buf;
+  c->stats = p.done.front().stats;
+  p.done.erase(p.done.begin());
   return JXG_OK;
 }
 
@@ -1919,7 +2066,12 @@ jxg_status jxg_create(const jxg_params* params, void** out) {
 void jxg_destroy(void* ctx) {
   if (!ctx) return;
   Ctx* c = static_cast<Ctx*>(ctx);
-  c->lanes.clear();  // batch lanes (jxg_destroy each)
+  if (c->pipe) {  // frames still in the pipeline (their lanes are released below)
+    pipe_abort(c);
+    for (auto& d : c->pipe->done) jxg_buffer_free(&d.buf);
+    c->pipe.reset();
+  }
+  c->lanes.clear();  // batch / pipeline lanes (jxg_destroy each)
   (void)hipSetDevice(c->params.device);
   (void)hipStreamSynchronize(c->stream);
   if (c->stream2) (void)hipStreamSynchronize(c->stream2);
@@ -2053,6 +2205,41 @@ jxg_status jxg_encode_batch_rgb8_device(void* ctx, const void* const* d_rgbs, ui
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
   return batch_encode(c, reinterpret_cast<const uint8_t* const*>(d_rgbs), true, n, w, h, stride,
                       outs);
+}
+
+jxg_status jxg_submit_rgb8_device(void* ctx, const void* d_rgb, uint32_t w, uint32_t h,
+                                  size_t stride) {
+  if (!ctx || !d_rgb || w == 0 || h == 0 || w > (1u << 18) || h > (1u << 18) ||
+      stride < (size_t)w * 3)
+    return JXG_ERR_INVALID_ARG;
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
+  return pipe_submit(c, static_cast<const uint8_t*>(d_rgb), true, w, h, stride);
+}
+
+jxg_status jxg_submit_rgb8(void* ctx, const uint8_t* rgb, uint32_t w, uint32_t h, size_t stride) {
+  if (!ctx || !rgb || w == 0 || h == 0 || w > (1u << 18) || h > (1u << 18) ||
+      stride < (size_t)w * 3)
+    return JXG_ERR_INVALID_ARG;
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
+  return pipe_submit(c, rgb, false, w, h, stride);
+}
+
+jxg_status jxg_receive(void* ctx, jxg_buffer* out) {
+  if (!ctx || !out) return JXG_ERR_INVALID_ARG;
+  out->data = nullptr;
+  out->size = 0;
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
+  return pipe_receive(c, out);
+}
+
+jxg_status jxg_pending(void* ctx, uint32_t* n) {
+  if (!ctx || !n) return JXG_ERR_INVALID_ARG;
+  Ctx* c = static_cast<Ctx*>(ctx);
+  *n = c->pipe ? (uint32_t)(c->pipe->inflight.size() + c->pipe->done.size()) : 0u;
+  return JXG_OK;
 }
 
 jxg_status jxg_get_stats(void* ctx, jxg_stats* stats) {

@@ -102,9 +102,8 @@ struct AcArgs {
 constexpr uint64_t kGroupTokStride = 1024ull * 3 * 64;
 
 // ANS coding of the pass groups' token records (jxg_ac.hip)
-constexpr uint32_t kAnsHists = 16;  // == kAnsMaxHists (jxg_bitstream.h)
-constexpr uint32_t kAnsDivOff = kAnsHists * 128 * 4;
-constexpr uint32_t kAnsInvOff = kAnsDivOff + kAnsHists * 128 * 4;
+constexpr uint32_t kAnsHists = 8;   // == kAnsMaxHists (jxg_bitstream.h)
+constexpr uint32_t kAnsInvOff = kAnsHists * 128 * 4;
 constexpr uint32_t kAnsMapOff = kAnsInvOff + kAnsHists * 4096 * 2;
 constexpr uint32_t kAnsTabBytes = kAnsMapOff + 136;
 struct AnsArgs {
@@ -112,11 +111,9 @@ struct AnsArgs {
   uint32_t* val;           // [records] emitted bits: 16-bit chunk (if any) then raw bits
   uint8_t* len;            // [records] number of emitted bits
   const uint32_t* ntok;    // [ngroups][3]
-  const uint8_t* tab;      // table blob (kAnsDivOff / kAnsInvOff / kAnsMapOff):
-                           //  u32 [16][128] symbol: f - 1 | cum << 12
-                           //  u32 [16][128] division magic of f (floor(x / f) =
-                           //      (t + ((x - t) >> s1)) >> s2, t = mulhi(x, magic))
-                           //  u16 [16][4096] alias inverse: slot of position cum + offset
+  const uint8_t* tab;      // table blob (kAnsInvOff / kAnsMapOff):
+                           //  u32 [8][128] symbol: f - 1 | cum << 12
+                           //  u16 [8][4096] alias inverse: slot of position cum + offset
                            //  u8 [132] static cluster -> histogram
   uint32_t nhist;          // histograms in use (<= kAnsMaxHists)
   uint32_t* state;         // [ngroups] final encoder state (= stream's first 32 bits)

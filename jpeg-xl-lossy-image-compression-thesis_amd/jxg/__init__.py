@@ -80,7 +80,8 @@ EXPORTS = ("jxg_status_str", "jxg_create", "jxg_destroy", "jxg_encode_rgb8",
            "jxg_shard_end", "jxg_shard_payload", "jxg_shard_assemble_device",
            "jxg_shard_assemble", "jxg_compare_rgb8", "jxg_compare_rgb8_device",
            "jxg_shard_head", "jxg_shard_write_host", "jxg_host_register", "jxg_host_unregister",
-           "jxg_encode_batch_rgb8_device", "jxg_synth_rgb8_device", "jxg_shard_exchange")
+           "jxg_encode_batch_rgb8_device", "jxg_synth_rgb8_device", "jxg_shard_exchange",
+           "jxg_submit_rgb8", "jxg_submit_rgb8_device", "jxg_receive", "jxg_pending")
 
 _lib = None
 
@@ -107,6 +108,10 @@ def load():
                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_size_t,
                                           ctypes.POINTER(_Buffer)]
     lib.jxg_encode_batch_rgb8_device.argtypes = lib.jxg_encode_batch_rgb8.argtypes
+    lib.jxg_submit_rgb8.argtypes = [vp, vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_size_t]
+    lib.jxg_submit_rgb8_device.argtypes = lib.jxg_submit_rgb8.argtypes
+    lib.jxg_receive.argtypes = [vp, ctypes.POINTER(_Buffer)]
+    lib.jxg_pending.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32)]
     lib.jxg_get_stats.argtypes = [vp, ctypes.POINTER(_Stats)]
     lib.jxg_buffer_free.argtypes = [ctypes.POINTER(_Buffer)]
     lib.jxg_buffer_free.restype = None
@@ -255,6 +260,33 @@ class Encoder:
         _check(load().jxg_encode_rgb8_device(self._ctx, ctypes.c_void_p(ptr), width, height,
                                              row_stride or width * 3, ctypes.byref(buf)))
         return self._take(buf) if copy else Codestream(buf)
+
+    # streaming encode (jxg_submit_rgb8[_device] / jxg_receive): a software
+    # pipeline inside the library, driven by this thread
+    def submit(self, rgb: np.ndarray):
+        """Queue a host (H, W, 3) uint8 frame (copied before returning)."""
+        rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
+        h, w, c = rgb.shape
+        if c != 3:
+            raise ValueError("expected (H, W, 3) uint8")
+        _check(load().jxg_submit_rgb8(self._ctx, rgb.ctypes.data, w, h, w * 3))
+
+    def submit_device(self, ptr: int, width: int, height: int, row_stride: int | None = None):
+        """Queue a device-resident RGB8 frame; it must stay unchanged until its
+        codestream has been received."""
+        _check(load().jxg_submit_rgb8_device(self._ctx, ctypes.c_void_p(ptr), width, height,
+                                             row_stride or width * 3))
+
+    def receive(self, copy: bool = True):
+        """Codestream of the oldest submitted frame (blocks until complete)."""
+        buf = _Buffer()
+        _check(load().jxg_receive(self._ctx, ctypes.byref(buf)))
+        return self._take(buf) if copy else Codestream(buf)
+
+    def pending(self) -> int:
+        n = ctypes.c_uint32()
+        _check(load().jxg_pending(self._ctx, ctypes.byref(n)))
+        return n.value
 
     def timings(self) -> tuple:
         """(ms_front_kernel, ms_host_call, ms_host_codes, ms_host_layout) of the

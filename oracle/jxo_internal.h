@@ -135,10 +135,13 @@ typedef struct {
 } jxo_ans;
 void jxo_ans_normalize(const uint32_t* counts /* [128] */, jxo_ans* a);
 void jxo_ans_write_hist(jxo_bw* w, const jxo_ans* a);
-/* at most 16 clustered histograms (their alias inverses fill 128 KB of LDS on
- * the GPU); a new centre needs >= 64 bits of merge cost (Q16) */
+/* at most 8 clustered histograms: their alias inverses (64 KB) share a CU's
+ * LDS with the GPU's other kernels, so the rANS chains of one frame overlap the
+ * transform stages of the next (16 would be 128 KB for +1.2% smaller output on
+ * the synthetic 8K frame, +0.2% on natural content); a new centre needs >= 64
+ * bits of merge cost (Q16) */
 #ifndef JXO_ANS_MAX_HISTS
-#define JXO_ANS_MAX_HISTS 16
+#define JXO_ANS_MAX_HISTS 8
 #endif
 #define JXO_ANS_MIN_DIST (64ll << 16)
 /* hist[nh][128] -> assign[nh] (centre id, -1 for empty); returns #centres */

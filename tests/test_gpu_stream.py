@@ -1,0 +1,70 @@
+"""Streaming encode (jxg_submit_rgb8[_device] / jxg_receive): the library's
+one-thread software pipeline over four lanes returns, in submission order,
+exactly the codestreams of one-at-a-time jxg_encode_rgb8 calls -- for frames of
+mixed sizes and content, both AC coders, receives interleaved with submits, and
+a full-size 8K ANS sequence against the oracle's committed fingerprint."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = {g["name"]: g for g in json.load(open(os.path.join(HERE, "golden", "config_golden.json")))}
+
+pytestmark = pytest.mark.gpu
+
+
+def _frames():
+    from jxg.synth import natural_rgb8, synth_rgb8
+
+    sizes = [(640, 480), (333, 250), (640, 480), (1024, 520), (64, 64), (777, 301), (640, 480),
+             (9, 7), (1280, 720)]
+    out = []
+    for i, (w, h) in enumerate(sizes):
+        out.append(natural_rgb8(w, h, 50 + i) if i % 2 and min(w, h) >= 200 else
+                   synth_rgb8(w, h, 90 + i))
+    return out
+
+
+@pytest.mark.parametrize("flags_name", ["prefix", "ans"])
+def test_stream_equals_single(jxg_mod, flags_name):
+    flags = jxg_mod.FLAG_ANS if flags_name == "ans" else 0
+    frames = _frames()
+    with jxg_mod.Encoder(distance=1.0, effort=7, flags=flags) as enc:
+        want = [enc.encode(f) for f in frames]
+    with jxg_mod.Encoder(distance=1.0, effort=7, flags=flags) as enc:
+        got = []
+        for i, f in enumerate(frames):
+            enc.submit(f)
+            if i == 2:  # a receive in the middle of the stream
+                got.append(enc.receive())
+        assert enc.pending() == len(frames) - 1
+        while enc.pending():
+            got.append(enc.receive())
+        with pytest.raises(jxg_mod.JxgError):
+            enc.receive()
+        # the context still encodes one-at-a-time afterwards
+        assert enc.encode(frames[0]) == want[0]
+    assert [len(g) for g in got] == [len(w) for w in want]
+    assert got == want
+
+
+def test_stream_device_8k_ans_matches_oracle(jxg_mod):
+    import torch
+
+    from jxg.synth import synth_rgb8_device
+
+    g = GOLD["8k_d1_ans"]
+    t = synth_rgb8_device(g["width"], g["height"], g["seed"])
+    torch.cuda.synchronize()
+    with jxg_mod.Encoder(distance=1.0, effort=7, flags=jxg_mod.FLAG_ANS) as enc:
+        for _ in range(6):
+            enc.submit_device(t.data_ptr(), g["width"], g["height"])
+        outs = [enc.receive() for _ in range(6)]
+        st = enc.stats()
+    del t
+    for data in outs:
+        assert hashlib.sha256(data).hexdigest() == g["sha256"]
+    assert st["bytes"] == g["bytes"]
