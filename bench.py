@@ -175,7 +175,13 @@ def main():
     ap.add_argument("--distance", type=float, default=1.0)
     ap.add_argument("--effort", type=int, default=7)
     ap.add_argument("--proposals", type=int, default=0)
-    ap.add_argument("--mode", choices=("shard", "replica"), default="shard")
+    ap.add_argument("--mode", choices=("shard", "replica"), default="replica",
+                    help="N > 1: replica = every rank streams its own frames through the "
+                         "pipelined entry points (frame-level data parallelism, no data-path "
+                         "collective); shard = one frame's pass groups split over the ranks")
+    ap.add_argument("--alt-shard", type=int, default=1,
+                    help="replica mode, N > 1: also time the sharded strong-scaling encode of "
+                         "one frame over the N ranks (reported under 'sharded')")
     ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
                     help="shard mode: strong = ONE frame of the config split over the N ranks "
                          "(BASELINE config 2 as written); weak = a frame of N stacked config "
@@ -218,7 +224,8 @@ def main():
         else:
             dist.init_process_group(backend)
     name, w, h, nframes = CONFIGS[args.config]
-    shard = world > 1 and args.mode == "shard"
+    shard0 = world > 1 and args.mode == "shard"
+    shard = shard0
     strong = shard and args.scaling == "strong"
     # inputs generated on the device (jxg_synth_rgb8_device: the bytes of
     # jxg.synth.synth_rgb8, without minutes of numpy at 8K / 16K)
@@ -238,9 +245,16 @@ def main():
         d_img = d_img.repeat(world, 1, 1).contiguous()
     torch.cuda.synchronize()
 
-    def run(coder, nstreams, proposals=None):
+    def run(coder, nstreams, proposals=None, as_shard=None, pipe=None):
         """Warm up, then time args.steps frames over `nstreams` concurrent
         encoders (one host thread, context and HIP stream each)."""
+        nonlocal shard, pipeline, frames, d_img
+        pipe_saved = pipeline
+        if pipe is not None:
+            pipeline = pipe
+        if as_shard is not None:  # the sharded strong-scaling line of a replica run
+            shard, pipeline, frames = as_shard, False, 1
+            d_img = synth_rgb8_device(w, h, SEED_BASE + args.config, local)
         flags = jxg.FLAG_ANS if coder == "ans" else 0
         props = args.proposals if proposals is None else proposals
         encs = [jxg.Encoder(distance=args.distance, effort=args.effort,
@@ -333,6 +347,7 @@ def main():
         if host is not None:
             dist.barrier()
             host.close()
+        pipeline = pipe_saved
         return rec
 
     nstreams = 1 if shard else max(1, args.streams)
@@ -352,6 +367,24 @@ def main():
                "ms_latency": round(sum(x[0] for x in A["host_ms"]) / len(A["host_ms"]), 3),
                "bytes_per_frame": A["sizes"][-1],
                "bpp": round(A["sizes"][-1] * 8.0 / (w * fh), 4)}
+    sharded = None
+    if world > 1 and not shard and args.alt_shard:
+        # the same frame's groups split over the N ranks (strong scaling,
+        # one frame per step, SURVEY §8e exchange + host assembly)
+        S = run(args.coder, 1, as_shard=True)
+        if rank == 0:
+            sharded = {"mode": "shard", "scaling": "strong", "coder": args.coder,
+                       "value": round(w * h * args.steps / S["dt"] / 1e6, 2),
+                       "ms_per_step": round(S["dt"] * 1e3 / args.steps, 3),
+                       "bytes_per_frame": S["sizes"][-1]}
+        S["enc"].close()
+        shard, pipeline, frames = False, not args.no_pipeline and args.streams == 1, nframes
+    iso = None
+    if pipeline:
+        # the kernels alone on the GPU (one-at-a-time encodes, same coder): the
+        # front kernel's roofline, the rANS chain kernel's duration
+        iso = run(args.coder, 1, pipe=False)
+        iso["enc"].close()
     thesis = None
     if not shard and args.alt_thesis and args.proposals != 3:
         # the thesis proposals P + F (combined.diff) on the same workload:
@@ -372,7 +405,8 @@ def main():
         # roofline of the front kernel over this rank's launch (its tiles)
         fw, fhh = (w, fh // world) if shard else (w, fh)
         fb = front_bytes_survey(fw, fhh)
-        fms = sum(front_ms) / len(front_ms)
+        fms_pipe = sum(front_ms) / len(front_ms)
+        fms = sum(iso["front_ms"]) / len(iso["front_ms"]) if iso else fms_pipe
         achieved = fb / (fms * 1e-3) / 1e9 if fms > 0 else 0.0
         coder_desc = "%s-coded" % args.coder
         if shard:
@@ -425,18 +459,36 @@ def main():
                          "algorithmic_bytes": int(fb),
                          "bytes_per_px": SURVEY_BYTES_PER_PX,
                          "design_bytes": front_bytes_design(fw, fhh, args.effort),
-                         "avg_ms": round(fms, 4)},
+                         "avg_ms": round(fms, 4),
+                         "measured": ("one-at-a-time encodes (the kernel alone on the GPU); "
+                                      "under the pipeline, sharing the GPU with rANS chains: "
+                                      "%.4f ms" % fms_pipe) if iso else "timed region"},
             # the dominant kernels (merge stage) are VALU-issue-bound, not
             # HBM-bound: their live time and the PMC-measured VALU issue rate
             "merge_stage": {"kernels": "merge_eval + merge_resolve + merge_write",
                             "bound": "valu",
-                            "avg_ms": round(st["ms_front"] - st["ms_front_kernel"], 4),
+                            "avg_ms": round((iso["st"] if iso else st)["ms_front"] -
+                                            (iso["st"] if iso else st)["ms_front_kernel"], 4),
                             "valu_issue_frac_pmc": load_merge_pmc(name) if world == 1 else None},
         }
+        if iso is not None and args.coder == "ans":
+            # the rANS chain: one serial state recurrence per pass group (the
+            # format's), so its kernel time is set by the group with the most
+            # tokens x the per-step latency (latency-bound, not HBM / MFMA)
+            tok = np.asarray(iso["st"]["ac_tokens"]).reshape(-1, 3).sum(axis=1)
+            ms_emit = iso["st"]["ms_emit"]
+            res["ans_chain"] = {"kernel": "ans_encode_kernel (+ LF emission in the same span)",
+                                "bound": "latency (dependent LDS lookups)",
+                                "ms_emit_isolated": round(ms_emit, 4),
+                                "tokens_max_group": int(tok.max()),
+                                "tokens_mean_group": round(float(tok.mean()), 1),
+                                "ns_per_token_max_group": round(ms_emit * 1e6 / max(1, tok.max()), 2)}
         if alt is not None:
             res["alt_coder"] = alt
         if thesis is not None:
             res["thesis_proposals"] = thesis
+        if sharded is not None:
+            res["sharded"] = sharded
         if world == 1 and not args.no_quality:
             res["quality"] = quality_probe(R["enc"], img, args.distance, args.effort)
         if world == 1 and not args.no_cpu_baseline:
