@@ -33,6 +33,9 @@ __device__ __forceinline__ int32_t lf_value(const LfArgs& a, const LfRow& r, con
     const int c = r.chan == 0 ? 1 : (r.chan == 1 ? 0 : 2);
     return a.dc[c * nb + (size_t)(L.by0 + y) * a.bxs + L.bx0 + x];
   }
+  if (r.chan < 2)  // colour tile (x, y) of the LF group
+    return a.cmap[(size_t)r.chan * a.ntiles_all + (size_t)(L.by0 / 8 + y) * a.tiles_x +
+                  L.bx0 / 8 + x];
   if (r.chan != 2) return 0;
   // varblock x of the LF group (raster order of first blocks)
   const size_t b = a.vb[(size_t)r.lg * 65536 + (uint32_t)x];

@@ -300,6 +300,7 @@ struct GroupCtx {
   const float* iwperm; // LDS [4 T][8 r][8 k] Y inverse weights per lane
   const float* btab;   // LDS [256] 0.145f / q
   const float* sdperm; // LDS [4 T][3 c][8 r][8 k] distortion weights per lane
+  float kx, kb;        // chroma from luma of the tile: X - kx Yd, B - kb Yd
 };
 
 // Quantized values of one candidate: [channel X, Y, B][4 words of 2 x int16]
@@ -397,7 +398,8 @@ __device__ __forceinline__ void quantize_cols(const GroupCtx& G, const float* vt
   for (int k = 0; k < 8; k++) {
     const float ws = wk[k] * scale;
     float rv = v[k];
-    if (C == 2) rv = rv - A.yd[k];
+    if (C == 0) rv = rv - G.kx * A.yd[k];
+    if (C == 2) rv = rv - G.kb * A.yd[k];
     const float vq = rv * ws;
     const float a = fabsf(vq);
     const int qa = a < 0.58f ? 0 : (int)(fminf(a, 32767.0f) + 0.5f);
@@ -555,6 +557,14 @@ __device__ __forceinline__ void load_xyb_tile(const FrontArgs& a, const float* l
   }
 }
 
+// chroma-from-luma factor as an int8 multiple of 1/84 (oracle cfl_quant)
+__device__ __forceinline__ int cfl_quant(float k) {
+  float v = k * 84.0f;
+  v = fminf(fmaxf(v, -128.0f), 127.0f);
+  const int q = v >= 0.0f ? (int)(v + 0.5f) : -(int)(-v + 0.5f);
+  return q > 127 ? 127 : (q < -128 ? -128 : q);
+}
+
 // HOOKP: hook P compiled in (proposals bit 0); without it the kernel keeps
 // no hook-P candidate aside (fewer live registers)
 template <bool HOOKP>
@@ -634,13 +644,76 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   // ---- phase B: wave w = block row, 8-lane group g = block column ----
   const int g = lane >> 3, r = lane & 7;
   const int lbx = g, lby = wave;
-  if (lbx >= nbx || lby >= nby) return;  // whole groups leave; no barrier follows
   const int b = lby * 8 + lbx;
+  // chroma from luma (oracle jxo_cfl_tile): weighted least squares of X on Y
+  // and of B - Y on Y over the tile's DCT8 AC coefficients; lane r of a block
+  // accumulates its coefficient column, the block's 8 lanes tree-sum, the
+  // tile sums its blocks in raster order (phase-A scratch sH reused)
+  float kx = 0.0f, kb = 1.0f;
+  if (a.effort >= 5) {
+    float* cs = &sH[0][0];  // [4 sums][64 blocks]
+    {
+      const GroupCtx G0{sPix, lby * 8 + 1, lbx * 8 + 1, r, sWperm, sIwperm, sBtab, sSdperm,
+                        0.0f, 1.0f};
+      float vy[8], vx[8], vb[8];
+      row_pass_t<true, 1>(G0, vy);
+      dct8_1d(vy);
+      row_pass_t<true, 0>(G0, vx);
+      dct8_1d(vx);
+      row_pass_t<true, 2>(G0, vb);
+      dct8_1d(vb);
+      const float* wx = sWperm + (0 * 8 + r) * 8;  // DCT8 weights, X: [r][k]
+      const float* wbp = sWperm + (2 * 8 + r) * 8; // DCT8 weights, B
+      float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        if (k == 0 && r == 0) continue;  // DC
+        const float w2x = wx[k] * wx[k], w2b = wbp[k] * wbp[k];
+        a0 = fmaf(w2x * vx[k], vy[k], a0);
+        a1 = fmaf(w2x * vy[k], vy[k], a1);
+        a2 = fmaf(w2b * (vb[k] - vy[k]), vy[k], a2);
+        a3 = fmaf(w2b * vy[k], vy[k], a3);
+      }
+      a0 = group_tree_sum(a0);
+      a1 = group_tree_sum(a1);
+      a2 = group_tree_sum(a2);
+      a3 = group_tree_sum(a3);
+      if (r == 0) {
+        cs[b] = a0;
+        cs[64 + b] = a1;
+        cs[128 + b] = a2;
+        cs[192 + b] = a3;
+      }
+    }
+    __syncthreads();
+    if (tid < 4) {
+      float T = 0.0f;
+      for (int bb = 0; bb < 64; bb++)
+        if ((bb & 7) < nbx && (bb >> 3) < nby) T = T + cs[tid * 64 + bb];
+      cs[256 + tid] = T;
+    }
+    __syncthreads();
+    const float T0 = cs[256], T1 = cs[257], T2 = cs[258], T3 = cs[259];
+    const int ytox = cfl_quant(T1 > 0.0f ? T0 / T1 : 0.0f);
+    const int ytob = cfl_quant(T3 > 0.0f ? T2 / T3 : 0.0f);
+    kx = (float)ytox * (1.0f / 84.0f);
+    kb = 1.0f + (float)ytob * (1.0f / 84.0f);
+    if (tid == 0 && a.cmap) {
+      const size_t t = (size_t)ty * a.tiles_x + tx;
+      a.cmap[t] = (int8_t)ytox;
+      a.cmap[a.ntiles_all + t] = (int8_t)ytob;
+    }
+  } else if (tid == 0 && a.cmap) {
+    const size_t t = (size_t)ty * a.tiles_x + tx;
+    a.cmap[t] = 0;
+    a.cmap[a.ntiles_all + t] = 0;
+  }
+  if (lbx >= nbx || lby >= nby) return;  // whole groups leave; no barrier follows
   // block index (recomputed where used: keeps a 64-bit value out of the
   // candidate search's live registers)
   auto gblock = [&]() { return (size_t)(ty * 8 + lby) * a.bxs + tx * 8 + lbx; };
   size_t gb = gblock();
-  const GroupCtx G{sPix, lby * 8 + 1, lbx * 8 + 1, r, sWperm, sIwperm, sBtab, sSdperm};
+  const GroupCtx G{sPix, lby * 8 + 1, lbx * 8 + 1, r, sWperm, sIwperm, sBtab, sSdperm, kx, kb};
   // block DC (row partials, tree over rows) and AQ activity
   float dc[3];
 #pragma unroll

@@ -451,6 +451,7 @@ struct Ctx {
   bool constants_ready = false;
   // device
   DevBuf<uint8_t> rgb, acs, qf;
+  DevBuf<int8_t> cmap;  // [2][tiles] chroma from luma (front kernel)
   DevBuf<uint16_t> nz, mnat;
   DevBuf<float> ent, mwk, msdk, miwy, xyb_tiles, mcost;
   DevBuf<uint32_t> vb, vcount, mwork, xlist;
@@ -636,7 +637,7 @@ static Plan make_plan(const Frame& f, uint32_t rank, uint32_t world) {
   return P;
 }
 // exchange record of one pass group (jxg_shard.hip): acs, qf, 3 x int32 DC
-constexpr size_t kGroupRecordBytes = 1024 * 2 + 1024 * 4 * 3;
+constexpr size_t kGroupRecordBytes = 1024 * 2 + 1024 * 4 * 3 + 32;  // jxg_shard.hip
 
 // LF-group row segments: (lf group, stream, channel, y, x0) in stream order,
 // grouped into chunks of one stream (<= kLfChunkSamples samples,
@@ -725,6 +726,7 @@ static jxg_status stage_alloc(Ctx* c, Job& J) {
   if (J.homog) JXG_HIP(c->homog.ensure(nb * 3));
   J.max_s = P.effort >= 6 ? 8 : (P.effort >= 5 ? 4 : 0);  // merge levels
   const uint32_t ntiles = f.tiles_x * f.tiles_y;
+  JXG_HIP(c->cmap.ensure((size_t)ntiles * 2));
   if (J.max_s) {
     JXG_HIP(c->ent.ensure(nb));
     JXG_HIP(c->xyb_tiles.ensure((size_t)ntiles * 3 * 4096));
@@ -820,6 +822,9 @@ static jxg_status stage_alloc(Ctx* c, Job& J) {
   la.bxs = f.bxs;
   la.bys = f.bys;
   la.lfxs = f.lfxs;
+  la.cmap = c->cmap.p;
+  la.tiles_x = f.tiles_x;
+  la.ntiles_all = f.tiles_x * f.tiles_y;
   la.hist = c->lfhist.p;
   la.sbound = c->sbound.p;
   la.codes = c->lfcodes.p;
@@ -867,6 +872,8 @@ static jxg_status stage_front(Ctx* c, Job& J) {
   fa.xyb_out = J.max_s ? c->xyb_tiles.p : nullptr;
   const bool listed = !J.plan.tiles.empty();
   fa.tile_list = listed ? c->tile_list.p : nullptr;
+  fa.cmap = c->cmap.p;
+  fa.ntiles_all = f.tiles_x * f.tiles_y;
   if (listed)
     launch_front_list(fa, (uint32_t)J.plan.tiles.size(), s);
   else if (J.plan.world == 1)
@@ -889,6 +896,8 @@ static jxg_status stage_front(Ctx* c, Job& J) {
       ma.dc_step[i] = f.dc_step[i];
     }
     ma.ent = c->ent.p;
+    ma.cmap = c->cmap.p;
+    ma.ntiles_all = f.tiles_x * f.tiles_y;
     ma.homog = J.homog ? c->homog.p : nullptr;
     ma.acs = c->acs.p;
     ma.qf = c->qf.p;
@@ -1712,8 +1721,8 @@ static jxg_status shard_begin(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32_t
   if (!X.recv.empty())
     JXG_HIP(hipMemcpyAsync(c->xlist.p + X.send.size(), X.recv.data(), X.recv.size() * 4,
                            hipMemcpyHostToDevice, s));
-  PackArgs pa{c->acs.p, c->qf.p, c->dc.p, J.f.bxs, J.f.bys, J.f.gxs, d_xbuf, c->xlist.p,
-              (uint32_t)X.send.size()};
+  PackArgs pa{c->acs.p, c->qf.p, c->dc.p, J.f.bxs, J.f.bys, J.f.gxs, c->cmap.p, J.f.tiles_x,
+              J.f.tiles_y, d_xbuf, c->xlist.p, (uint32_t)X.send.size()};
   launch_pack(pa, s);
   JXG_HIP(hipGetLastError());
   JXG_HIP(hipEventRecord(c->ev[1], s));
@@ -1729,8 +1738,8 @@ static jxg_status shard_end(Ctx* c, const uint32_t* d_hist, const uint8_t* d_xbu
   hipStream_t s = c->stream;
   const uint32_t world = J.plan.world;
   const Exchange& X = J.plan.x;
-  PackArgs pa{c->acs.p, c->qf.p, c->dc.p, J.f.bxs, J.f.bys, J.f.gxs,
-              const_cast<uint8_t*>(d_xbuf), c->xlist.p + X.send.size(),
+  PackArgs pa{c->acs.p, c->qf.p, c->dc.p, J.f.bxs, J.f.bys, J.f.gxs, c->cmap.p, J.f.tiles_x,
+              J.f.tiles_y, const_cast<uint8_t*>(d_xbuf), c->xlist.p + X.send.size(),
               (uint32_t)X.recv.size()};
   launch_unpack(pa, s);
   JXG_HIP(hipGetLastError());

@@ -29,6 +29,8 @@ struct FrontArgs {
   float* ent;     // [nb] best 8x8 estimate (merge stage input) or null
   float* xyb_out; // [tiles][3][64][64] XYB tiles (merge stage input) or null
   const uint32_t* tile_list;  // shard: tile ids (ty * tiles_x + tx), 1-D grid; or null
+  int8_t* cmap;   // [2][tiles] chroma from luma ytox, ytob per 64x64 tile (out)
+  uint32_t ntiles_all;  // tiles_x * tiles_y (cmap plane stride)
 };
 
 // merge stage (jxg_merge.hip): weight kinds (stored orientation) and the
@@ -61,6 +63,8 @@ struct MergeArgs {
   uint32_t* work;       // [1 + tiles * 9]: count, then (tile << 4 | shape) of every
                         //   (tile, shape) holding a chosen varblock (resolve -> write)
   uint32_t nwrite;      // merge_write workgroups (persistent loop over work)
+  const int8_t* cmap;   // [2][tiles_all] chroma from luma (front kernel)
+  uint32_t ntiles_all;
 };
 // per-LF-group varblock lists (AC metadata channel)
 struct VbArgs {
@@ -152,6 +156,8 @@ struct LfArgs {
   const uint32_t* vb;     // [nlf][65536] varblock -> block index
   const uint32_t* vcount; // [nlf] varblocks per LF group
   uint32_t bxs, bys, lfxs;
+  const int8_t* cmap;     // [2][tiles_y][tiles_x] ytox, ytob (AC metadata channels 0, 1)
+  uint32_t tiles_x, ntiles_all;
   uint32_t* hist;         // [nstreams][4 leaves][kAlpha]  (hist)
   uint32_t* sbound;       // [nstreams] (hist)
   const uint32_t* codes;  // [nstreams][4][kAlpha] (emit)
@@ -187,6 +193,8 @@ struct PackArgs {
   uint8_t* qf;
   int32_t* dc;
   uint32_t bxs, bys, gxs;
+  int8_t* cmap;           // [2][ntiles_all] chroma from luma of the group's 4 x 4 tiles
+  uint32_t tiles_x, tiles_y;
   uint8_t* xbuf;          // n group records back to back
   const uint32_t* list;   // [n] group of each record
   uint32_t n;

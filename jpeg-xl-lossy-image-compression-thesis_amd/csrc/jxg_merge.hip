@@ -402,6 +402,12 @@ __device__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S) {
   constexpr int cidx = CH == 1 ? 0 : (CH == 0 ? 1 : 2);  // 0 Y, 1 X, 2 B
   constexpr float kBias1 = 1.0f - 0.07005449891748593f;
   const int C = P.C(), NV = P.NV();
+  // chroma from luma of the tile (front kernel): X - kx Yd, B - kb Yd
+  float kc = 0.0f;
+  if (CH != 1) {
+    const float f = (float)a.cmap[(CH == 0 ? 0u : a.ntiles_all) + (uint32_t)P.tile];
+    kc = CH == 0 ? f * (1.0f / 84.0f) : 1.0f + f * (1.0f / 84.0f);
+  }
   for (int j = threadIdx.x; j < (1 << lper); j += kMThreads) {
     const int ch = j >> (P.lNV() + P.lC()), v = (j >> P.lC()) & (NV - 1), x = j & (C - 1);
     if (!S.valid[v]) continue;  // the varblock's C lanes leave together
@@ -441,7 +447,7 @@ __device__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S) {
       const float coef_v = cplane[ky * kMS];
       if (WRITE && is_llf) llf_at(S, CH, (by0 + ky) * 8 + bx0 + x) = coef_v;
       float rv = coef_v;
-      if (CH == 2) rv = rv - yd[ky * kMS];
+      if (CH != 1) rv = rv - kc * yd[ky * kMS];
       // LLF positions carry weight 0 (host tables): vq = +-0 quantizes to 0
       // and contributes nothing
       const float vq = rv * (w[kk] * scale);

@@ -5,19 +5,34 @@
 // field, quantized DC) of all their blocks, so a rank sends the records of
 // each of its groups whose LF group another rank owns -- to that rank only
 // (one all_to_all over RCCL / xGMI) -- instead of all-gathering every record.
-// Group record: [acs 1024 B][qf 1024 B][dc X 4 KB][dc Y 4 KB][dc B 4 KB].
+// Group record: [acs 1024 B][qf 1024 B][dc X 4 KB][dc Y 4 KB][dc B 4 KB]
+// [ytox 16 B][ytob 16 B] (the chroma-from-luma factors of its 4 x 4 colour tiles).
 // pack: send-buffer slot i <- group list[i]; unpack: group list[i] <- slot i.
 #include "jxg_device.h"
 #include "jxg_kernels.h"
 
 namespace jxg {
 
-constexpr size_t kGroupRecord = 1024 * 2 + 1024 * 4 * 3;
+constexpr size_t kGroupRecord = 1024 * 2 + 1024 * 4 * 3 + 32;
 
 __device__ __forceinline__ void group_record(const PackArgs& a, uint32_t g, uint8_t* rec,
                                              bool pack) {
   const int gx = (int)(g % a.gxs), gy = (int)(g / a.gxs);
   const int b = threadIdx.x, bx = gx * 32 + (b & 31), by = gy * 32 + (b >> 5);
+  if (b < 16) {
+    const int tx = gx * 4 + (b & 3), ty = gy * 4 + (b >> 2);
+    if (tx < (int)a.tiles_x && ty < (int)a.tiles_y) {
+      const size_t t = (size_t)ty * a.tiles_x + tx, nt = (size_t)a.tiles_x * a.tiles_y;
+      int8_t* cr = reinterpret_cast<int8_t*>(rec + 2048 + 12288);
+      if (pack) {
+        cr[b] = a.cmap[t];
+        cr[16 + b] = a.cmap[nt + t];
+      } else {
+        a.cmap[t] = cr[b];
+        a.cmap[nt + t] = cr[16 + b];
+      }
+    }
+  }
   if (bx >= (int)a.bxs || by >= (int)a.bys) return;
   const size_t nb = (size_t)a.bxs * a.bys, gb = (size_t)by * a.bxs + bx;
   int32_t* dcr = reinterpret_cast<int32_t*>(rec + 2048);

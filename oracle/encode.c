@@ -17,7 +17,8 @@
 #include "jxo_internal.h"
 
 int jxo_front_block(const jxo_frame* f, const float px[3][64], const float* homog,
-                    int32_t q[3][64], int32_t dcq[3], int* qf_raw, float* ent_out);
+                    int32_t q[3][64], int32_t dcq[3], int* qf_raw, float* ent_out,
+                    const float cfl[2]);
 
 static const jxo_uintcfg kCfg = {4, 2, 0};
 static const jxo_uintcfg kCfgMap = {8, 0, 0};
@@ -238,10 +239,15 @@ static void lf_group_section(const jxo_frame* f, const jxo_result* r, int lg,
       count += !(r->acs[(size_t)(by0 + y) * f->bxs + bx0 + x] & 0x80);
   jxo_bw_put(w, ceil_log2(bw * bh), count - 1);
   const int cw = (int)((bw + 7) / 8), chh = (int)((bh + 7) / 8);
-  for (int i = 0; i < 2; i++) {
+  const size_t ntiles = (size_t)r->tiles_x * r->tiles_y;
+  for (int i = 0; i < 2; i++) { /* the LF group's colour tiles: ytox, ytob */
     ch[i].w = cw;
     ch[i].h = chh;
     ch[i].data = (int32_t*)calloc((size_t)cw * chh, sizeof(int32_t));
+    for (int ty = 0; ty < chh; ty++)
+      for (int tx = 0; tx < cw; tx++)
+        ch[i].data[ty * cw + tx] =
+            r->cmap[i * ntiles + (size_t)(by0 / 8 + ty) * r->tiles_x + bx0 / 8 + tx];
   }
   ch[2].w = (int)count;
   ch[2].h = 2;
@@ -421,6 +427,17 @@ int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h, size_t row_strid
   }
   uint8_t order[64];
   jxo_natural_order8(order);
+  /* chroma from luma: one (ytox, ytob) pair per 64x64 tile, before the
+   * AC-strategy search (front.c jxo_cfl_tile) */
+  const uint32_t tiles_x = (f.bxs + 7) / 8, tiles_y = (f.bys + 7) / 8;
+  const size_t ntiles = (size_t)tiles_x * tiles_y;
+  out->tiles_x = tiles_x;
+  out->tiles_y = tiles_y;
+  out->cmap = (int8_t*)malloc(2 * ntiles);
+#pragma omp parallel for schedule(dynamic)
+  for (size_t t = 0; t < ntiles; t++)
+    jxo_cfl_tile(&f, xyb, (int)(t % tiles_x), (int)(t / tiles_x), &out->cmap[t],
+                 &out->cmap[ntiles + t]);
   float* ent = (float*)malloc(sizeof(float) * nb);
   int* raws = (int*)malloc(sizeof(int) * nb);
   (void)jxo_vkinds(); /* build the merge tables before any parallel region */
@@ -438,8 +455,11 @@ int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h, size_t row_strid
       const size_t b = (size_t)by * f.bxs + bx;
       int32_t q[3][64], dcq[3];
       int raw;
+      const size_t ti = (size_t)(by / 8) * tiles_x + bx / 8;
+      float cfl[2];
+      jxo_cfl_factors(out->cmap[ti], out->cmap[ntiles + ti], cfl);
       int t = jxo_front_block(&f, px, out->homog ? out->homog + 3 * b : NULL, q,
-                              dcq, &raw, &ent[b]);
+                              dcq, &raw, &ent[b], cfl);
       out->acs[b] = (uint8_t)t;
       out->qf[b] = (uint8_t)(raw - 1);
       raws[b] = raw;
@@ -455,8 +475,12 @@ int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h, size_t row_strid
     const uint32_t tx_n = (f.bxs + 7) / 8, ty_n = (f.bys + 7) / 8;
 #pragma omp parallel for schedule(dynamic) collapse(2)
     for (uint32_t ty = 0; ty < ty_n; ty++)
-      for (uint32_t tx = 0; tx < tx_n; tx++)
-        jxo_merge_tile(&f, xyb, out->homog, (int)tx, (int)ty, max_s, ent, raws, out->acs);
+      for (uint32_t tx = 0; tx < tx_n; tx++) {
+        const size_t ti = (size_t)ty * tiles_x + tx;
+        float cfl[2];
+        jxo_cfl_factors(out->cmap[ti], out->cmap[ntiles + ti], cfl);
+        jxo_merge_tile(&f, xyb, out->homog, (int)tx, (int)ty, max_s, ent, raws, out->acs, cfl);
+      }
 #pragma omp parallel for schedule(dynamic)
     for (uint32_t by = 0; by < f.bys; by++)
       for (uint32_t bx = 0; bx < f.bxs; bx++) {
@@ -472,7 +496,10 @@ int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h, size_t row_strid
             const int v = raws[(by + iy) * f.bxs + bx + ix];
             rmax = v > rmax ? v : rmax;
           }
-        jxo_varblock(&f, sh, xyb, (int)bx * 8, (int)by * 8, rmax, vq, llf, NULL);
+        const size_t ti = (size_t)(by / 8) * tiles_x + bx / 8;
+        float cfl[2];
+        jxo_cfl_factors(out->cmap[ti], out->cmap[ntiles + ti], cfl);
+        jxo_varblock(&f, sh, xyb, (int)bx * 8, (int)by * 8, rmax, vq, llf, NULL, cfl);
         const int RC = 64 * sh->cy * sh->cx;
         for (int iy = 0; iy < sh->cy; iy++)
           for (int ix = 0; ix < sh->cx; ix++) {
@@ -688,6 +715,7 @@ void jxo_result_free(jxo_result* r) {
   free(r->ac);
   free(r->ac_tokens);
   free(r->homog);
+  free(r->cmap);
   free(r->bytes);
   memset(r, 0, sizeof(*r));
 }

@@ -331,7 +331,7 @@ static int co_index(int t, int p) {
  * used for the B residual multiplies by the inverse weight (1/w) and the
  * inverse scale (1/scale), like libjxl's dequantization [ext]. */
 float jxo_quantize_block(const jxo_frame* f, int t, const float px[3][64],
-                         float scale, int32_t q[3][64]) {
+                         float scale, int32_t q[3][64], const float cfl[2]) {
   float co[3][64];
   for (int c = 0; c < 3; c++) jxo_transform(t, px[c], co[c]);
   const int qk = qkind(t);
@@ -351,7 +351,9 @@ float jxo_quantize_block(const jxo_frame* f, int t, const float px[3][64],
         if (ci_ == 0) continue;
         const float ws = f->wts[qk][c][ci_] * scale;
         float rv = co[c][ci_];
-        if (c == 2) rv = rv - yd[ci_];
+        /* chroma from luma: X - kx Yd, B - kb Yd (the tile's factors) */
+        if (c == 0) rv = rv - cfl[0] * yd[ci_];
+        if (c == 2) rv = rv - cfl[1] * yd[ci_];
         const float v = rv * ws;
         const int qq = quant1(v);
         if (c == 1) yd[ci_] = adjust_bias(1, qq) * ((1.0f / f->wts[qk][c][ci_]) * inv_scale);
@@ -389,7 +391,8 @@ void jxo_quant_dc(const jxo_frame* f, const float dc[3], int32_t dcq[3]) {
 /* block-level front end: pixels px[c][64] (X,Y,B), returns chosen strategy,
  * writes qf raw (1..256), quantized AC and DC. */
 int jxo_front_block(const jxo_frame* f, const float px[3][64], const float* homog,
-                    int32_t q[3][64], int32_t dcq[3], int* qf_raw, float* ent_out) {
+                    int32_t q[3][64], int32_t dcq[3], int* qf_raw, float* ent_out,
+                    const float cfl[2]) {
   /* block DC = mean: row partial sums (left to right), then the 8 row sums
    * tree-summed -- the 8-lane order of the GPU path (lane = row) */
   float dc[3];
@@ -437,7 +440,7 @@ int jxo_front_block(const jxo_frame* f, const float px[3][64], const float* homo
   float best = FLT_MAX;
   if (ncand > 1) {
     for (int i = 0; i < ncand; i++) {
-      float e = jxo_quantize_block(f, cand[i], px, scale, NULL);
+      float e = jxo_quantize_block(f, cand[i], px, scale, NULL, cfl);
       if (f->proposals & 2) e = jxo_hook_f(e, homog[0], homog[1], homog[2]);
       if (e < best) {
         best = e;
@@ -467,6 +470,74 @@ int jxo_front_block(const jxo_frame* f, const float px[3][64], const float* homo
     else if (rv > rh && rv > T)
       best_t = JXO_DCT4X8;
   }
-  jxo_quantize_block(f, best_t, px, scale, q);
+  jxo_quantize_block(f, best_t, px, scale, q, cfl);
   return best_t;
+}
+
+/* ---------- chroma from luma: per-64x64-tile factors ----------
+ * [ext] libjxl enc_chroma_from_luma (per colour tile, before the AC-strategy
+ * search; EstimateEntropy then scores every candidate on the CfL residual --
+ * the cmap_factors argument of combined.diff:240), restated as a weighted
+ * least-squares fit in quantization steps over the DCT8 AC coefficients of
+ * the tile's blocks:
+ *   X ~ kx Y : kx = sum(wx^2 x y) / sum(wx^2 y^2)
+ *   B ~ (1 + kb) Y : kb = sum(wb^2 (b - y) y) / sum(wb^2 y^2)
+ * (w = the DCT8 quant weight of the coefficient), stored as int8 multiples of
+ * 1/84 (the default colour_factor): ytox = clamp(round(84 kx)).  The decoder
+ * (and the quantizer) use kx = ytox / 84, kb = 1 + ytob / 84.
+ * Summation order = the GPU's: per block, lane r (= coefficient column r)
+ * accumulates rows k = 0..7 with fmaf, the 8 lane partials are tree-summed
+ * (tree8), and the tile sums the blocks inside the frame in raster order.
+ * Effort < 5 (no AC-strategy search either): no fit, factors 0. */
+static int8_t cfl_quant(float k) {
+  float v = k * 84.0f;
+  v = fminf(fmaxf(v, -128.0f), 127.0f);
+  const int q = v >= 0.0f ? (int)(v + 0.5f) : -(int)(-v + 0.5f);
+  return (int8_t)(q > 127 ? 127 : (q < -128 ? -128 : q));
+}
+void jxo_cfl_tile(const jxo_frame* f, const float* xyb, int tx, int ty, int8_t* ytox,
+                  int8_t* ytob) {
+  *ytox = 0;
+  *ytob = 0;
+  if (f->effort < 5) return;
+  const size_t plane = (size_t)f->xp * f->yp;
+  float T[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  for (int lby = 0; lby < 8; lby++)
+    for (int lbx = 0; lbx < 8; lbx++) {
+      const int bx = tx * 8 + lbx, by = ty * 8 + lby;
+      if (bx >= (int)f->bxs || by >= (int)f->bys) continue;
+      float px[64], co[3][64];
+      for (int c = 0; c < 3; c++) {
+        for (int y = 0; y < 8; y++)
+          for (int x = 0; x < 8; x++)
+            px[y * 8 + x] = xyb[c * plane + (size_t)(by * 8 + y) * f->xp + bx * 8 + x];
+        jxo_transform(JXO_DCT8, px, co[c]);
+      }
+      float acc[4][8];
+      for (int r = 0; r < 8; r++) {
+        float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+        for (int k = 0; k < 8; k++) {
+          const int p = k * 8 + r;
+          if (p == 0) continue;
+          const float wx = f->wts[JXO_QK_DCT8][0][p], wb = f->wts[JXO_QK_DCT8][2][p];
+          const float w2x = wx * wx, w2b = wb * wb;
+          const float y = co[1][p], x = co[0][p], b = co[2][p];
+          a0 = fmaf(w2x * x, y, a0);
+          a1 = fmaf(w2x * y, y, a1);
+          a2 = fmaf(w2b * (b - y), y, a2);
+          a3 = fmaf(w2b * y, y, a3);
+        }
+        acc[0][r] = a0;
+        acc[1][r] = a1;
+        acc[2][r] = a2;
+        acc[3][r] = a3;
+      }
+      for (int i = 0; i < 4; i++) T[i] = T[i] + tree8(acc[i]);
+    }
+  *ytox = cfl_quant(T[1] > 0.0f ? T[0] / T[1] : 0.0f);
+  *ytob = cfl_quant(T[3] > 0.0f ? T[2] / T[3] : 0.0f);
+}
+void jxo_cfl_factors(int8_t ytox, int8_t ytob, float cfl[2]) {
+  cfl[0] = (float)ytox * (1.0f / 84.0f);
+  cfl[1] = 1.0f + (float)ytob * (1.0f / 84.0f);
 }

@@ -975,6 +975,8 @@ def decode(data: bytes, want_pixels: bool = True) -> Decoded:
     d.dc = np.zeros((3, bys, bxs), dtype=np.int64)
     d.acs = np.zeros((bys, bxs), dtype=np.int32)
     d.qf = np.zeros((bys, bxs), dtype=np.int32)
+    # chroma from luma: int8 (ytox, ytob) per 64x64 colour tile
+    d.cmap = np.zeros((2, (bys + 7) // 8, (bxs + 7) // 8), dtype=np.int32)
     for lg in range(nlf):
         s = sec(1 + lg)
         lgx, lgy = lg % lfxs, lg // lfxs
@@ -988,8 +990,11 @@ def decode(data: bytes, want_pixels: bool = True) -> Decoded:
         count = s.read(ceil_log2(bw * bh)) + 1
         cw, chh = (bw + 7) // 8, (bh + 7) // 8
         meta = read_modular(s, [(cw, chh), (cw, chh), (count, 2), (bw, bh)])
-        if any(v for row in meta[0] for v in row) or any(v for row in meta[1] for v in row):
-            raise JxlError("non-zero CfL map not produced")
+        for i in range(2):
+            m = np.array(meta[i], dtype=np.int32)
+            if m.min() < -128 or m.max() > 127:
+                raise JxlError("CfL factor out of int8 range")
+            d.cmap[i, by0 // 8:by0 // 8 + chh, bx0 // 8:bx0 // 8 + cw] = m
         k = 0
         covered = np.zeros((bh, bw), dtype=bool)
         for y in range(bh):
@@ -1099,12 +1104,17 @@ def reconstruct(d: Decoded) -> np.ndarray:
     dcq = np.stack([d.dc[0] * dc_step[0], d.dc[1] * dc_step[1],
                     d.dc[2] * dc_step[2] + d.dc[1] * dc_step[1]])  # X, Y, B (ytob 1.0)
     chm = (x_mul, 1.0, b_mul)
+    cmap = getattr(d, "cmap", np.zeros((2, (d.bys + 7) // 8, (d.bxs + 7) // 8), dtype=np.int32))
     for by in range(d.bys):
         for bx in range(d.bxs):
             t = int(d.acs[by, bx])
             if t & 0x80:
                 continue
             qf = d.qf[by, bx]
+            # colour correlation of the block's tile [ext ColorCorrelationMap:
+            # base_correlation_x 0, base_correlation_b 1, colour_factor 84]
+            cfx = float(np.float32(cmap[0, by // 8, bx // 8]) * np.float32(1.0 / 84.0))
+            cfb = 1.0 + float(np.float32(cmap[1, by // 8, bx // 8]) * np.float32(1.0 / 84.0))
             if t in SHAPES:
                 ccy, ccx, kind = SHAPES[t]
                 R, C = 8 * ccy, 8 * ccx
@@ -1119,7 +1129,8 @@ def reconstruct(d: Decoded) -> np.ndarray:
                 co = np.zeros((3, R, C))
                 for c in range(3):
                     co[c, ky, kx] = vals[c] * iw[c][nat] * (inv_gs / qf) * chm[c]
-                co[2] += co[1]  # ytob base 1.0
+                co[0] += cfx * co[1]
+                co[2] += cfb * co[1]
                 for c, arr in ((0, X), (1, Y), (2, B)):
                     arr[by * 8:by * 8 + R, bx * 8:bx * 8 + C] = reconstruct_varblock(
                         t, co[c], dcq[c, by:by + ccy, bx:bx + ccx])
@@ -1128,8 +1139,8 @@ def reconstruct(d: Decoded) -> np.ndarray:
             raster = np.zeros((3, 64))
             raster[:, order8] = adj[by, bx]
             cy = raster[1] * mul[1]
-            cx = raster[0] * mul[0] * x_mul
-            cb = raster[2] * mul[2] * b_mul + cy  # ytob base 1.0
+            cx = raster[0] * mul[0] * x_mul + cfx * cy
+            cb = raster[2] * mul[2] * b_mul + cfb * cy
             for arr, co, dcv in ((X, cx, dcq[0, by, bx]), (Y, cy, dcq[1, by, bx]),
                                  (B, cb, dcq[2, by, bx])):
                 co = co.copy()

@@ -74,6 +74,8 @@ typedef struct {
   int32_t* ac;             /* [bys*bxs][3][64] quantized coeffs (X,Y,B) */
   uint32_t* ac_tokens;     /* [ngroups][3] number of AC tokens per channel */
   float* homog;            /* [bys*bxs][3] r_h r_v r_d (only if P|F) */
+  int8_t* cmap;            /* [2][tiles_y*tiles_x] chroma from luma: ytox, ytob per 64x64 tile */
+  uint32_t tiles_x, tiles_y;
   uint32_t global_scale, quant_dc;
   uint8_t* bytes;          /* encoded codestream */
   size_t nbytes;

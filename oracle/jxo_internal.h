@@ -80,10 +80,15 @@ const jxo_vkind* jxo_vkinds(void);
 int jxo_shape_of(int type); /* shape index of a merged raw id, -1 otherwise */
 float jxo_varblock(const jxo_frame* f, const jxo_shape* s, const float* xyb, int px0, int py0,
                    int raw, int32_t* q /* [3][R*C] natural order */, float* llf /* [3][8][8] */,
-                   int* nz /* [3] */);
+                   int* nz /* [3] */, const float cfl[2] /* chroma-from-luma kx, kb */);
 float jxo_llf_dc(const jxo_shape* s, const float* llf_c, int by, int bx);
 void jxo_merge_tile(const jxo_frame* f, const float* xyb, const float* homog, int tx, int ty,
-                    int max_s, float* ent, const int* raw, uint8_t* acs);
+                    int max_s, float* ent, const int* raw, uint8_t* acs, const float cfl[2]);
+/* chroma from luma (front.c): the tile's int8 factors, and kx, kb from them */
+void jxo_cfl_tile(const jxo_frame* f, const float* xyb, int tx, int ty, int8_t* ytox,
+                  int8_t* ytob);
+void jxo_cfl_factors(int8_t ytox, int8_t ytob, float cfl[2]);
+void jxo_transform(int t, const float* px, float* co);
 /* covered 8x8 blocks of a raw strategy id (1 for the 8x8 class) */
 static inline int jxo_covered(int type) {
   const int s = jxo_shape_of(type);

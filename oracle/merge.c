@@ -273,7 +273,7 @@ static inline int stored_index(const jxo_shape* s, int ky, int kx) {
 }
 
 float jxo_varblock(const jxo_frame* f, const jxo_shape* s, const float* xyb, int px0, int py0,
-                   int raw, int32_t* q, float* llf, int* nzo) {
+                   int raw, int32_t* q, float* llf, int* nzo, const float cfl[2]) {
   init_tables();
   const int R = 8 * s->cy, C = 8 * s->cx;
   const jxo_vkind* K = &g_kinds[s->kind];
@@ -319,7 +319,8 @@ float jxo_varblock(const jxo_frame* f, const jxo_shape* s, const float* xyb, int
           const float w = K->w[c][si];
           const float ws = w * scale;
           float rv = F[c][ky * C + x];
-          if (c == 2) rv = rv - yd[ky * C + x];
+          if (c == 0) rv = rv - cfl[0] * yd[ky * C + x];
+          if (c == 2) rv = rv - cfl[1] * yd[ky * C + x];
           const float v = rv * ws;
           const int qq = quant1(v);
           if (c == 1) yd[ky * C + x] = adjust_bias_y(qq) * ((1.0f / w) * inv_scale);
@@ -370,7 +371,7 @@ float jxo_llf_dc(const jxo_shape* s, const float* llf_c /* [8][8] */, int by, in
 /* merge search over one 64x64 tile; ent/raw/acs are whole-frame per-block
  * arrays (acs holds raw ids, bit 7 set on covered non-first blocks) */
 void jxo_merge_tile(const jxo_frame* f, const float* xyb, const float* homog, int tx, int ty,
-                    int max_s, float* ent, const int* raw, uint8_t* acs) {
+                    int max_s, float* ent, const int* raw, uint8_t* acs, const float cfl[2]) {
   for (int s = 2; s <= max_s; s *= 2) {
     const int full = s == 2 ? 2 : (s == 4 ? 5 : 8);      /* shape index */
     const int tall = s == 2 ? 0 : (s == 4 ? 3 : 6);
@@ -395,7 +396,7 @@ void jxo_merge_tile(const jxo_frame* f, const float* xyb, const float* homog, in
               const int v = raw[(size_t)(by + iy) * f->bxs + bx + ix];
               r = v > r ? v : r;
             }
-          e[i] = jxo_varblock(f, sh, xyb, bx * 8, by * 8, r, NULL, NULL, NULL);
+          e[i] = jxo_varblock(f, sh, xyb, bx * 8, by * 8, r, NULL, NULL, NULL, cfl);
           if (f->proposals & 2) {
             const float* h = homog + 3 * ((size_t)by * f->bxs + bx);
             e[i] = jxo_hook_f(e[i], h[0], h[1], h[2]);

@@ -33,6 +33,8 @@ class _Result(ctypes.Structure):
                 ("acs", ctypes.POINTER(ctypes.c_uint8)), ("qf", ctypes.POINTER(ctypes.c_uint8)),
                 ("dc", ctypes.POINTER(ctypes.c_int32)), ("ac", ctypes.POINTER(ctypes.c_int32)),
                 ("ac_tokens", ctypes.POINTER(ctypes.c_uint32)), ("homog", ctypes.POINTER(ctypes.c_float)),
+                ("cmap", ctypes.POINTER(ctypes.c_int8)), ("tiles_x", ctypes.c_uint32),
+                ("tiles_y", ctypes.c_uint32),
                 ("global_scale", ctypes.c_uint32), ("quant_dc", ctypes.c_uint32),
                 ("bytes", ctypes.POINTER(ctypes.c_uint8)), ("nbytes", ctypes.c_size_t)]
 
@@ -111,6 +113,8 @@ def encode(rgb: np.ndarray, distance=1.0, effort=7, proposals=0, coder=0) -> Ora
         o.ac_tokens = np.ctypeslib.as_array(r.ac_tokens, (ng * 3,)).copy().reshape(ng, 3)
         o.homog = (np.ctypeslib.as_array(r.homog, (nb * 3,)).copy().reshape(r.bys, r.bxs, 3)
                    if r.homog else None)
+        nt = r.tiles_x * r.tiles_y
+        o.cmap = np.ctypeslib.as_array(r.cmap, (2 * nt,)).copy().reshape(2, r.tiles_y, r.tiles_x)
         o.global_scale, o.quant_dc = r.global_scale, r.quant_dc
         o.bytes = bytes(np.ctypeslib.as_array(r.bytes, (r.nbytes,)))
         return o

@@ -94,6 +94,13 @@ def test_every_shape_is_reachable(oracle):
     for w, h, d, e, p in CASES:
         r = oracle.encode(smooth_rgb8(w, h, w * 31 + h), d, e, p)
         seen |= set((r.acs[~(r.acs & 0x80).astype(bool)] & 0x7F).tolist())
+    # a vertical edge in the middle of every tile over a vertical gradient:
+    # two 64x32 (tall) halves per tile
+    y, x = np.mgrid[0:128, 0:128].astype(np.float64)
+    img = np.stack([100 + 40 * np.sin(y / 37.0 + c) + np.where((x % 64) < 32, 0, 70 + 20 * c)
+                    for c in range(3)], -1)
+    r = oracle.encode(np.clip(img, 0, 255).astype(np.uint8), 1.0, 7, 0)
+    seen |= set((r.acs[~(r.acs & 0x80).astype(bool)] & 0x7F).tolist())
     assert {4, 5, 6, 7, 10, 11, 18, 19, 20} <= seen, sorted(seen)
 
 

@@ -111,7 +111,7 @@ def test_record_exchange_plan(jxg_mod, w, h, world):
     a rank sends each of its pass groups' records to the owner of the group's
     LF group (if another rank), receives the other ranks' groups inside its
     own LF groups; sends and receives pair up across ranks."""
-    rec = 1024 * 2 + 1024 * 4 * 3
+    rec = 1024 * 2 + 1024 * 4 * 3 + 32  # acs, qf, DC, and the 16 colour tiles ytox / ytob
     owners = jxg_mod.lf_owners(w, h, world)
     gxs, gys = -(-w // 256), -(-h // 256)
     lfxs = -(-w // 2048)
