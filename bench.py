@@ -295,7 +295,7 @@ def main():
                 got = 0
                 for k in ks:
                     e.submit_device(d_imgs[k % frames].data_ptr(), w, fh)
-                    while e.pending() > 4:
+                    while e.pending() > 8:
                         took(e, got, e.receive(copy=False))
                         got += 1
                 while e.pending():

@@ -96,7 +96,10 @@ AnsTable build_ans_table(const uint32_t* counts /* [128] */);
 // (<= kAnsMaxHists: their alias inverses fill 64 KB of LDS in the encoder, so
 // the rANS chain kernel co-resides with the transform kernels of the next
 // frame; oracle/jxo_internal.h JXO_ANS_MAX_HISTS)
-constexpr int kAnsMaxHists = 8;
+#ifndef JXG_ANS_HISTS  // (experiment builds override it: tools/build_variant.sh)
+#define JXG_ANS_HISTS 8
+#endif
+constexpr int kAnsMaxHists = JXG_ANS_HISTS;
 constexpr int64_t kAnsMinDist = 64ll << 16;  // Q16 bits
 int cluster_ans_histograms(const uint32_t* hist, int nh, int* assign);
 void write_ans_histogram(BitWriter& w, const AnsTable& t);

@@ -17,6 +17,8 @@
 // (nearly) bank-conflict free.  Float op order == oracle/front.c.
 #include <float.h>
 
+#include <type_traits>
+
 #include "jxg_device.h"
 #include "jxg_kernels.h"
 
@@ -436,38 +438,30 @@ __device__ __forceinline__ void quantize_cols(const GroupCtx& G, const float* vt
   A.q.nz = (C == 1 ? 0u : A.q.nz) | ((uint32_t)nzc << sh);
 }
 
-// The two candidates sharing a row transform, channels Y, X, B; need0/need1
-// are group-uniform.  Returns the rate/distortion costs (same in all 8 lanes
-// of the group) in e0/e1; quantized values stay in registers.
-template <bool ROW8>
-__device__ __forceinline__ void eval_pair(const GroupCtx& G, float scale, float inv_scale,
-                                          bool need0, bool need1, CandAcc& A0, CandAcc& A1,
-                                          float& e0, float& e1) {
-  constexpr int T0 = ROW8 ? kDCT8 : kDCT4X4;
-  constexpr int T1 = ROW8 ? kDCT8X4 : kDCT4X8;
-  A0.bits = A1.bits = 0;
-  A0.part = A1.part = 0.0f;
+// One candidate, channels Y, X, B (its own row passes): only one candidate's
+// state is live at a time, which keeps the kernel inside 128 VGPRs.
+template <int T>
+__device__ __forceinline__ float eval_one(const GroupCtx& G, float scale, float inv_scale,
+                                          CandAcc& A) {
+  constexpr bool ROW8 = T == kDCT8 || T == kDCT8X4;
+  A.bits = 0;
+  A.part = 0.0f;
 #pragma unroll 1  // one channel live at a time
   for (int ci = 0; ci < 3; ci++) {
     float vt[8];
     if (ci == 0) {
       row_pass_t<ROW8, 1>(G, vt);
-      if (need0) quantize_cols<T0, 1>(G, vt, scale, inv_scale, A0);
-      if (need1) quantize_cols<T1, 1>(G, vt, scale, inv_scale, A1);
+      quantize_cols<T, 1>(G, vt, scale, inv_scale, A);
     } else if (ci == 1) {
       row_pass_t<ROW8, 0>(G, vt);
-      if (need0) quantize_cols<T0, 0>(G, vt, scale, inv_scale, A0);
-      if (need1) quantize_cols<T1, 0>(G, vt, scale, inv_scale, A1);
+      quantize_cols<T, 0>(G, vt, scale, inv_scale, A);
     } else {
       row_pass_t<ROW8, 2>(G, vt);
-      if (need0) quantize_cols<T0, 2>(G, vt, scale, inv_scale, A0);
-      if (need1) quantize_cols<T1, 2>(G, vt, scale, inv_scale, A1);
+      quantize_cols<T, 2>(G, vt, scale, inv_scale, A);
     }
   }
-  constexpr float tm0 = T0 == kDCT8 ? 1.0f : 1.05f;
-  constexpr float tm1 = 1.02f;
-  e0 = ((float)group_int_sum(A0.bits) + 8.0f * group_tree_sum(A0.part)) * tm0;
-  e1 = ((float)group_int_sum(A1.bits) + 8.0f * group_tree_sum(A1.part)) * tm1;
+  constexpr float tm = T == kDCT8 ? 1.0f : (T == kDCT4X4 ? 1.05f : 1.02f);
+  return ((float)group_int_sum(A.bits) + 8.0f * group_tree_sum(A.part)) * tm;
 }
 
 __device__ __forceinline__ void copy_q(QVals& d, const QVals& s, bool take) {
@@ -567,8 +561,11 @@ __device__ __forceinline__ int cfl_quant(float k) {
 
 // HOOKP: hook P compiled in (proposals bit 0); without it the kernel keeps
 // no hook-P candidate aside (fewer live registers)
+#ifndef JXG_FRONT_WPE  // (experiment builds override it: tools/build_variant.sh)
+#define JXG_FRONT_WPE 4
+#endif
 template <bool HOOKP>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void front_kernel(FrontArgs a) {
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FRONT_WPE))) void front_kernel(FrontArgs a) {
   __shared__ __attribute__((aligned(16))) float sPix[3 * kPlane];
   __shared__ __attribute__((aligned(16))) int16_t sStage[8][8][64];
   __shared__ __attribute__((aligned(16))) float sWperm[4 * 3 * 64];
@@ -773,52 +770,34 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   QVals best, ptq;
   int bt = kDCT8, bi = 0;
   float beste = FLT_MAX;
+  // candidates one at a time; `beats` is a strict total order on (estimate,
+  // scan index), so this finds the scan's winner
   {
-    CandAcc A0, A1;
-    float e0, e1;
-    eval_pair<true>(G, scale, inv_scale, true, ncand > 1 || pt == kDCT8X4, A0, A1, e0, e1);
-    if (hookF) {
-      e0 = hook_f(e0, rh, rv, rd);
-      e1 = hook_f(e1, rh, rv, rd);
-    }
-    copy_q(best, A0.q, true);
-    if (ncand > 1) {
-      beste = e0 < FLT_MAX ? e0 : FLT_MAX;
-      if (beats(e1, 3, e0, 0)) {
-        copy_q(best, A1.q, true);
-        bt = kDCT8X4;
-        bi = 3;
-        beste = e1;
-      }
-    }
-    if (HOOKP) copy_q(ptq, A1.q, pt == kDCT8X4);
+    CandAcc A;
+    float e = eval_one<kDCT8>(G, scale, inv_scale, A);
+    if (hookF) e = hook_f(e, rh, rv, rd);
+    copy_q(best, A.q, true);
+    if (ncand > 1) beste = e < FLT_MAX ? e : FLT_MAX;
   }
-  const bool need44 = ncand > 1 || pt == kDCT4X4, need48 = ncand > 1 || pt == kDCT4X8;
-  if (need44 || need48) {
-    CandAcc A0, A1;
-    float e0, e1;
-    eval_pair<false>(G, scale, inv_scale, need44, need48, A0, A1, e0, e1);
+  auto cand = [&](auto tag, int idx) {
+    constexpr int T = decltype(tag)::value;
+    if (!(ncand > 1 || pt == T)) return;
+    CandAcc A;
+    float e = eval_one<T>(G, scale, inv_scale, A);
     if (ncand > 1) {
-      if (hookF) {
-        e0 = hook_f(e0, rh, rv, rd);
-        e1 = hook_f(e1, rh, rv, rd);
-      }
-      // winner of the pair, then against the first pair's
-      const bool w1 = beats(e1, 2, e0, 1);
-      const float ew = w1 ? e1 : e0;
-      const int iw = w1 ? 2 : 1;
-      if (beats(ew, iw, beste, bi)) {
-        copy_q(best, w1 ? A1.q : A0.q, true);
-        bt = w1 ? kDCT4X8 : kDCT4X4;
-        bi = iw;
-        beste = ew;
+      if (hookF) e = hook_f(e, rh, rv, rd);
+      if (beats(e, idx, beste, bi)) {
+        copy_q(best, A.q, true);
+        bt = T;
+        bi = idx;
+        beste = e;
       }
     }
-    if (HOOKP) {
-      copy_q(ptq, A0.q, pt == kDCT4X4);
-      copy_q(ptq, A1.q, pt == kDCT4X8);
-    }
-  }
+    if (HOOKP) copy_q(ptq, A.q, pt == T);
+  };
+  cand(std::integral_constant<int, kDCT8X4>(), 3);
+  cand(std::integral_constant<int, kDCT4X4>(), 1);
+  cand(std::integral_constant<int, kDCT4X8>(), 2);
   if (HOOKP && bt == kDCT8 && pt != kDCT8) {
     bt = pt;
     copy_q(best, ptq, true);

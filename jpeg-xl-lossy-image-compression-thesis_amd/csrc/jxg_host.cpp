@@ -1574,7 +1574,12 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
 // fill the rest of the chip, and every chain has two submit periods to finish.
 // Four lanes = four streams = the process's hardware queues.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kPipeLanes = 4;
+#ifndef JXG_PIPE_LANES  // (experiment builds override them: tools/build_variant.sh)
+#define JXG_PIPE_LANES 4
+#define JXG_PIPE_LAG 1
+#endif
+constexpr uint32_t kPipeLanes = JXG_PIPE_LANES;
+constexpr uint32_t kPipeLag = JXG_PIPE_LAG;  // submit(j) builds the codes of frame j - lag
 struct PipeFrame {
   Ctx* lane = nullptr;
   Job J;
@@ -1658,9 +1663,9 @@ static jxg_status pipe_submit(Ctx* c, const uint8_t* src, bool on_device, uint32
   }
   p.inflight.push_back(std::move(fr));
   p.submitted++;
-  // the previous frame: codes, emission launched
-  if (p.inflight.size() >= 2) {
-    PipeFrame& prev = *p.inflight[p.inflight.size() - 2];
+  // frame j - lag: codes, emission launched
+  if (p.inflight.size() >= 1 + kPipeLag) {
+    PipeFrame& prev = *p.inflight[p.inflight.size() - 1 - kPipeLag];
     if (prev.phase == 1) {
       if ((st = enc_codes(prev.lane, prev.J, false))) {
         pipe_abort(c);

@@ -106,7 +106,10 @@ struct AcArgs {
 constexpr uint64_t kGroupTokStride = 1024ull * 3 * 64;
 
 // ANS coding of the pass groups' token records (jxg_ac.hip)
-constexpr uint32_t kAnsHists = 8;   // == kAnsMaxHists (jxg_bitstream.h)
+#ifndef JXG_ANS_HISTS  // (jxg_bitstream.h kAnsMaxHists; experiment builds override it)
+#define JXG_ANS_HISTS 8
+#endif
+constexpr uint32_t kAnsHists = JXG_ANS_HISTS;  // == kAnsMaxHists (jxg_bitstream.h)
 constexpr uint32_t kAnsInvOff = kAnsHists * 128 * 4;
 constexpr uint32_t kAnsMapOff = kAnsInvOff + kAnsHists * 4096 * 2;
 constexpr uint32_t kAnsTabBytes = kAnsMapOff + 136;
