@@ -51,12 +51,12 @@ import os
 import sys
 import time
 
-# The library's streaming pipeline runs four encoder lanes, one HIP stream
-# each; HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues per process
-# (default 4, one of them taken by torch's stream), and two lanes sharing a
-# queue serialise their kernels (the box exports 4).  Must be set before HIP
-# initialises.
-os.environ["GPU_MAX_HW_QUEUES"] = "8"
+# The library's streaming pipeline runs up to 12 encoder lanes (4 at 8K, more
+# for small frames), one HIP stream each; HIP maps streams onto
+# GPU_MAX_HW_QUEUES hardware queues per process (the box exports 4, one of them
+# taken by torch's stream), and two lanes sharing a queue serialise their
+# kernels.  Must be set before HIP initialises.
+os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "jpeg-xl-lossy-image-compression-thesis_amd"))
@@ -236,7 +236,7 @@ def main():
     frames = 1 if shard else nframes
     d_imgs = [d_img] + [synth_rgb8_device(w, h, SEED_BASE + args.config + f, local)
                         for f in range(1, frames)]
-    pipeline = not shard and args.streams == 1 and not args.no_pipeline
+    pipeline = not shard and not args.no_pipeline
     ptrs = [t.data_ptr() for t in d_imgs]
     fh = h
     if shard and not strong:
@@ -295,7 +295,7 @@ def main():
                 got = 0
                 for k in ks:
                     e.submit_device(d_imgs[k % frames].data_ptr(), w, fh)
-                    while e.pending() > 8:
+                    while e.pending() > 16:
                         took(e, got, e.receive(copy=False))
                         got += 1
                 while e.pending():
@@ -378,7 +378,7 @@ def main():
                        "ms_per_step": round(S["dt"] * 1e3 / args.steps, 3),
                        "bytes_per_frame": S["sizes"][-1]}
         S["enc"].close()
-        shard, pipeline, frames = False, not args.no_pipeline and args.streams == 1, nframes
+        shard, pipeline, frames = False, not args.no_pipeline, nframes
     iso = None
     if pipeline:
         # the kernels alone on the GPU (one-at-a-time encodes, same coder): the

@@ -284,20 +284,22 @@ inline int64_t log2_q16(uint32_t v) {
   return ((int64_t)e << 16) + kLog2Frac[m];
 }
 
-int64_t hist_cost(const uint32_t* h, uint64_t t) {
+// bins [0, n) hold every non-zero count (n = 1 + last non-zero bin)
+int64_t hist_cost(const uint32_t* h, uint64_t t, int n = 128) {
   if (!t) return 0;
   const int64_t lt = log2_q16((uint32_t)std::min<uint64_t>(t, 0xFFFFFFFFull));
   int64_t c = 0;
-  for (int s = 0; s < 128; s++)
+  for (int s = 0; s < n; s++)
     if (h[s]) c += (int64_t)h[s] * (lt - log2_q16(h[s]));
   return c;
 }
 
-int64_t merge_cost(const uint32_t* a, uint64_t ta, int64_t ca, const uint32_t* b, uint64_t tb,
-                   int64_t cb) {
+int64_t merge_cost(const uint32_t* a, uint64_t ta, int64_t ca, int na, const uint32_t* b,
+                   uint64_t tb, int64_t cb, int nb) {
   uint32_t m[128];
-  for (int s = 0; s < 128; s++) m[s] = a[s] + b[s];
-  return hist_cost(m, ta + tb) - ca - cb;
+  const int n = std::max(na, nb);
+  for (int s = 0; s < n; s++) m[s] = a[s] + b[s];
+  return hist_cost(m, ta + tb, n) - ca - cb;
 }
 }  // namespace
 
@@ -305,10 +307,14 @@ int cluster_ans_histograms(const uint32_t* hist, int nh, int* assign) {
   std::vector<int64_t> cost(nh), dist(nh, 0);
   std::vector<uint64_t> tot(nh, 0);
   std::vector<uint8_t> centre(nh, 0);
+  std::vector<int> len(nh, 0);  // 1 + last non-zero bin (AC tokens stay below 64)
   int first = -1;
   for (int i = 0; i < nh; i++) {
-    for (int s = 0; s < 128; s++) tot[i] += hist[i * 128 + s];
-    cost[i] = hist_cost(hist + i * 128, tot[i]);
+    for (int s = 0; s < 128; s++) {
+      tot[i] += hist[i * 128 + s];
+      if (hist[i * 128 + s]) len[i] = s + 1;
+    }
+    cost[i] = hist_cost(hist + i * 128, tot[i], len[i]);
     assign[i] = -1;
     if (tot[i] && (first < 0 || tot[i] > tot[first])) first = i;
   }
@@ -320,7 +326,8 @@ int cluster_ans_histograms(const uint32_t* hist, int nh, int* assign) {
     if (i == first)
       centre[i] = 1;
     else
-      dist[i] = merge_cost(hist + i * 128, tot[i], cost[i], hist + first * 128, tot[first], cost[first]);
+      dist[i] = merge_cost(hist + i * 128, tot[i], cost[i], len[i], hist + first * 128, tot[first],
+                           cost[first], len[first]);
   }
   while (ncl < kAnsMaxHists) {
     int pick = -1;
@@ -332,8 +339,8 @@ int cluster_ans_histograms(const uint32_t* hist, int nh, int* assign) {
     centre[pick] = 1;
     for (int i = 0; i < nh; i++) {
       if (!tot[i] || centre[i]) continue;
-      const int64_t d =
-          merge_cost(hist + i * 128, tot[i], cost[i], hist + pick * 128, tot[pick], cost[pick]);
+      const int64_t d = merge_cost(hist + i * 128, tot[i], cost[i], len[i], hist + pick * 128,
+                                   tot[pick], cost[pick], len[pick]);
       if (d < dist[i]) {
         dist[i] = d;
         assign[i] = c;

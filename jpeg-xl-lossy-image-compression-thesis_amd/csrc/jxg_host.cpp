@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <future>
 #include <memory>
 #include <mutex>
 #include <new>
@@ -703,6 +704,12 @@ struct Job {
   // host stage results
   std::vector<BitWriter> preA, preB;
   BitWriter lfglobal, hfglobal;
+  // sharded ANS encode with one HF preset per rank: no histogram
+  // all-reduce; the rank's clustered histograms travel in its payload head and
+  // HfGlobal is written at assembly (build_hf_presets)
+  bool presets = false;
+  std::vector<uint8_t> pre_ctxmap;   // [kAcCtx] context -> the rank's dense histogram
+  std::vector<uint32_t> pre_counts;  // [nhist][kAlpha] clustered counts
   std::vector<uint64_t> gbase, sbase;
   float ms_codes = 0.0f;
   float ms_layout = 0.0f;  // stage_concat_split host layout
@@ -1023,6 +1030,10 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
     for (int cl = 0; cl < kMaxClusters; cl++)
       blob[kAnsMapOff + cl] = (uint8_t)(group[cl] >= 0 ? dense[group[cl]] : 0);
     J.nhist_ans = (uint32_t)nhist;
+    if (J.presets) {
+      J.pre_ctxmap = ctxmap;
+      J.pre_counts.assign(dh.begin(), dh.begin() + (size_t)nhist * kAlpha);
+    }
   } else {
     for (int cl = 0; cl < kMaxClusters; cl++) {
       if (group[cl] < 0) continue;
@@ -1057,19 +1068,21 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
     lfglobal.put(1, 1);  // BlockCtxMap default
     lfglobal.put(1, 1);  // colour correlation default
     lfglobal.put(1, 0);  // GlobalModular: no tree, no channels
-    hfglobal.put(1, 1);  // DequantMatrices all_default
-    hfglobal.put(ceil_log2(f.ngroups), 0);  // num_hf_presets - 1
-    write_u32_sel(hfglobal, 2, 0, 0);        // used_orders = 0
-    if (nhist != c->cm_nhist || ctxmap != c->cm_last) {
-      c->cm_bits = BitWriter();
-      write_context_map(c->cm_bits, ctxmap, nhist);
-      c->cm_last = ctxmap;
-      c->cm_nhist = nhist;
+    if (!J.presets) {  // (per-rank presets: HfGlobal at assembly, build_hf_presets)
+      hfglobal.put(1, 1);  // DequantMatrices all_default
+      hfglobal.put(ceil_log2(f.ngroups), 0);  // num_hf_presets - 1
+      write_u32_sel(hfglobal, 2, 0, 0);        // used_orders = 0
+      if (nhist != c->cm_nhist || ctxmap != c->cm_last) {
+        c->cm_bits = BitWriter();
+        write_context_map(c->cm_bits, ctxmap, nhist);
+        c->cm_last = ctxmap;
+        c->cm_nhist = nhist;
+      }
+      if (J.ans)
+        write_ans_histograms(hfglobal, ctxmap, nhist, ans_tables, kCfg420, &c->cm_bits);
+      else
+        write_histograms(hfglobal, ctxmap, nhist, codes, kCfg420, &c->cm_bits);
     }
-    if (J.ans)
-      write_ans_histograms(hfglobal, ctxmap, nhist, ans_tables, kCfg420, &c->cm_bits);
-    else
-      write_histograms(hfglobal, ctxmap, nhist, codes, kCfg420, &c->cm_bits);
   }
   // AC layout: the plan's groups in the scratch arena (32-bit aligned); the AC
   // emission is launched at once and runs while the host builds the LF-group
@@ -1229,12 +1242,18 @@ static jxg_status stage_concat(Ctx* c, Job& J, bool full, std::vector<uint32_t>*
                         Piece{2, J.sbase[lg * 2 + 1], c->h_sbits.p[lg * 2 + 1]}});
     ids.push_back(1 + lg);
   }
-  if (J.plan.rank == 0) {
+  if (J.plan.rank == 0 && !J.presets) {
     sections.push_back({add_chunk(J.hfglobal)});
     ids.push_back(1 + f.nlf);
   }
+  // per-rank presets: every pass group starts with its preset index
+  BitWriter sel;
+  if (J.presets) sel.put(ceil_log2(J.plan.world), J.plan.rank);
   for (uint32_t g = J.plan.g0; g < J.plan.g1; g++) {
-    sections.push_back({Piece{0, J.gbase[g], c->h_gbits.p[g]}});
+    if (J.presets)
+      sections.push_back({add_chunk(sel), Piece{0, J.gbase[g], c->h_gbits.p[g]}});
+    else
+      sections.push_back({Piece{0, J.gbase[g], c->h_gbits.p[g]}});
     ids.push_back(2 + f.nlf + g);
   }
   const bool single = full && f.ngroups == 1;
@@ -1563,23 +1582,31 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
 
 // ---------------------------------------------------------------------------
 // streaming encode (jxg_submit_rgb8[_device] / jxg_receive): a software
-// pipeline over kPipeLanes contexts (the caller's plus lanes it owns), driven
-// by the caller's one host thread.  Frame j runs on lane j % kPipeLanes:
-//   submit(j): finish frame j - kPipeLanes (its lane is needed again: wait for
-//              its emission, assemble, codestream to the host) -> launch frame
-//              j's front end, merge stage and statistics -> build frame j-1's
-//              codes and launch its emission.
-// So the rANS chains of frames j-1 and j-2 (latency-bound waves that use little
-// of their SIMDs; 68 KB of LDS per CU) run while frame j's transform kernels
-// fill the rest of the chip, and every chain has two submit periods to finish.
-// Four lanes = four streams = the process's hardware queues.
+// pipeline over D lanes (the caller's context plus lanes it owns, one stream
+// each), driven by the caller's one host thread.  submit(j):
+//   finish the oldest frame if D are in flight (wait for its emission,
+//   assemble, codestream to the host) -> launch frame j's front end, merge
+//   stage and statistics on a free lane -> build frame j-1's codes and launch
+//   its emission.
+// So the rANS chains of the D - 2 frames before j (latency-bound waves that use
+// little of their SIMDs; 68 KB of LDS per CU) run while frame j's transform
+// kernels fill the rest of the chip.  A frame's chain lasts as long as its
+// longest pass group's, whatever the frame size, so the depth follows the
+// frame: D = 4 from ~500 pass groups up (8K: more frames in flight only add
+// contention), up to kPipeMaxLanes for small frames (a 1080p
+// frame has 40 groups: 40 chain waves on a 1024-SIMD chip).  Every lane needs
+// its own hardware queue (GPU_MAX_HW_QUEUES > D, bench.py sets 16).
 // ---------------------------------------------------------------------------
-#ifndef JXG_PIPE_LANES  // (experiment builds override them: tools/build_variant.sh)
-#define JXG_PIPE_LANES 4
+#ifndef JXG_PIPE_LAG  // (experiment builds override them: tools/build_variant.sh)
 #define JXG_PIPE_LAG 1
+#define JXG_PIPE_MAX_LANES 12
 #endif
-constexpr uint32_t kPipeLanes = JXG_PIPE_LANES;
+constexpr uint32_t kPipeMaxLanes = JXG_PIPE_MAX_LANES;
 constexpr uint32_t kPipeLag = JXG_PIPE_LAG;  // submit(j) builds the codes of frame j - lag
+static uint32_t pipe_depth(uint32_t ngroups) {
+  const uint32_t d = (2048 + ngroups - 1) / std::max(1u, ngroups);
+  return std::min(kPipeMaxLanes, std::max(4u, d));
+}
 struct PipeFrame {
   Ctx* lane = nullptr;
   Job J;
@@ -1613,7 +1640,7 @@ static void pipe_abort(Ctx* c) {
   p.inflight.clear();
 }
 
-// oldest frame in flight -> done
+// oldest frame in flight -> done (on an error the caller aborts the pipe)
 static jxg_status pipe_complete_oldest(Ctx* c) {
   Pipe& p = *c->pipe;
   PipeFrame& fr = *p.inflight.front();
@@ -1621,10 +1648,7 @@ static jxg_status pipe_complete_oldest(Ctx* c) {
   if (fr.phase == 1) st = enc_codes(fr.lane, fr.J, false);
   PipeDone d{{nullptr, 0}, {}};
   if (!st) st = enc_finish(fr.lane, fr.J, false, &d.buf, fr.t0);
-  if (st) {
-    pipe_abort(c);
-    return st;
-  }
+  if (st) return st;
   d.stats = fr.lane->stats;
   p.done.push_back(d);
   p.inflight.erase(p.inflight.begin());
@@ -1636,43 +1660,72 @@ static jxg_status pipe_submit(Ctx* c, const uint8_t* src, bool on_device, uint32
   if (!c->pipe) c->pipe.reset(new (std::nothrow) Pipe());
   if (!c->pipe) return JXG_ERR_OOM;
   Pipe& p = *c->pipe;
-  jxg_status st = ensure_lanes(c, kPipeLanes - 1);
+  const uint32_t depth = pipe_depth(make_frame(w, h, c->params.distance).ngroups);
+  jxg_status st = ensure_lanes(c, depth - 1);
   if (st) return st;
   const Clock::time_point t0 = Clock::now();
-  if (p.inflight.size() >= kPipeLanes && (st = pipe_complete_oldest(c))) return st;
-  const uint32_t li = (uint32_t)(p.submitted % kPipeLanes);
-  Ctx* L = li == 0 ? c : c->lanes[li - 1].get();
+  // frame j - lag's codes (host work: clustering, ANS / prefix tables,
+  // headers, LF-group codes; ~0.4-1 ms whatever the frame size) on a helper
+  // thread, while this thread finishes the oldest frame and launches frame j
+  // on other lanes
+  PipeFrame* prev = p.inflight.size() >= kPipeLag ? p.inflight[p.inflight.size() - kPipeLag].get()
+                                                  : nullptr;
+  if (prev && prev->phase != 1) prev = nullptr;
+  std::future<jxg_status> codes;
+  if (prev) {
+    const int dev = c->params.device;
+    codes = std::async(std::launch::async, [prev, dev]() {
+      if (hipSetDevice(dev) != hipSuccess) return JXG_ERR_HIP;
+      return enc_codes(prev->lane, prev->J, false);
+    });
+  }
+  auto join_codes = [&]() -> jxg_status {
+    if (!prev) return JXG_OK;
+    const jxg_status s2 = codes.get();
+    prev->phase = 2;
+    prev = nullptr;
+    return s2;
+  };
+  auto fail = [&](jxg_status e) {
+    (void)join_codes();
+    pipe_abort(c);
+    return e;
+  };
+  while (p.inflight.size() >= depth)
+    if ((st = pipe_complete_oldest(c))) return fail(st);
+  // a lane no frame in flight uses (the lowest index)
+  Ctx* L = nullptr;
+  for (uint32_t li = 0; li < depth && !L; li++) {
+    Ctx* cand = li == 0 ? c : c->lanes[li - 1].get();
+    bool used = false;
+    for (auto& q : p.inflight) used = used || q->lane == cand;
+    if (!used) L = cand;
+  }
+  if (!L) return fail(JXG_ERR_INTERNAL);
   std::unique_ptr<PipeFrame> fr(new (std::nothrow) PipeFrame());
-  if (!fr) return JXG_ERR_OOM;
+  if (!fr) return fail(JXG_ERR_OOM);
   fr->lane = L;
   fr->t0 = t0;
   if (!on_device) {
     // the lane's previous frame has completed, so its staging is free
     const size_t bytes = stride * (h - 1) + (size_t)w * 3;
     if (L->h_stage.ensure(bytes) != hipSuccess || L->rgb.ensure(bytes) != hipSuccess)
-      return JXG_ERR_OOM;
+      return fail(JXG_ERR_OOM);
     std::memcpy(L->h_stage.p, src, bytes);
     if (hipMemcpyAsync(L->rgb.p, L->h_stage.p, bytes, hipMemcpyHostToDevice, L->stream) !=
         hipSuccess)
-      return JXG_ERR_HIP;
+      return fail(JXG_ERR_HIP);
     src = L->rgb.p;
   }
   if ((st = enc_launch(L, fr->J, src, w, h, stride))) {
     (void)hipStreamSynchronize(L->stream);
-    return st;
+    return fail(st);
   }
   p.inflight.push_back(std::move(fr));
   p.submitted++;
-  // frame j - lag: codes, emission launched
-  if (p.inflight.size() >= 1 + kPipeLag) {
-    PipeFrame& prev = *p.inflight[p.inflight.size() - 1 - kPipeLag];
-    if (prev.phase == 1) {
-      if ((st = enc_codes(prev.lane, prev.J, false))) {
-        pipe_abort(c);
-        return st;
-      }
-      prev.phase = 2;
-    }
+  if ((st = join_codes())) {  // frame j - lag: codes built, emission launched
+    pipe_abort(c);
+    return st;
   }
   return JXG_OK;
 }
@@ -1683,7 +1736,10 @@ static jxg_status pipe_receive(Ctx* c, jxg_buffer* out) {
   if (p.done.empty()) {
     if (p.inflight.empty()) return JXG_ERR_INVALID_ARG;
     const jxg_status st = pipe_complete_oldest(c);
-    if (st) return st;
+    if (st) {
+      pipe_abort(c);
+      return st;
+    }
   }
   *out = p.done.front().buf;
   c->stats = p.done.front().stats;
@@ -1714,6 +1770,10 @@ static jxg_status shard_begin(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32_t
   J.d_rgb = d_rgb;
   jxg_status st = stage_alloc(c, J);
   if (st) return st;
+  // ANS: one HF preset per rank (its own histograms; the caller need not
+  // all-reduce d_hist).  Prefix codes keep one preset from the summed
+  // histogram (N x 132 clusters would not fit one context map).
+  J.presets = J.ans && world > 1;
   JXG_HIP(hipEventRecord(c->ev[0], s));
   if ((st = stage_front(c, J))) return st;
   if ((st = stage_ac_stats(c, J))) return st;
@@ -1761,7 +1821,7 @@ static jxg_status shard_end(Ctx* c, const uint32_t* d_hist, const uint8_t* d_xbu
   std::vector<uint32_t>& hw = c->payload_head;
   hw.assign(7 + 2 * ids.size(), 0);
   hw[0] = kPayloadMagic;
-  hw[1] = 1;
+  hw[1] = J.presets ? 2 : 1;
   hw[2] = J.plan.rank;
   hw[3] = world;
   hw[4] = J.w;
@@ -1770,6 +1830,17 @@ static jxg_status shard_end(Ctx* c, const uint32_t* d_hist, const uint8_t* d_xbu
   for (size_t i = 0; i < ids.size(); i++) {
     hw[7 + 2 * i] = ids[i];
     hw[8 + 2 * i] = sizes[i];
+  }
+  if (J.presets) {
+    // version 2: the rank's HF preset -- [B][nhist][context map, bytes packed
+    // in words][clustered counts nhist x kAlpha], B = words after B
+    const uint32_t nh = J.nhist_ans, cw = (kAcCtx + 3) / 4;
+    hw.push_back(1 + cw + nh * kAlpha);
+    hw.push_back(nh);
+    const size_t o = hw.size();
+    hw.resize(o + cw, 0);
+    std::memcpy(hw.data() + o, J.pre_ctxmap.data(), kAcCtx);
+    hw.insert(hw.end(), J.pre_counts.begin(), J.pre_counts.end());
   }
   c->payload_body = nbytes;
   *payload_bytes = hw.size() * 4 + nbytes;
@@ -1812,15 +1883,66 @@ struct SectionRef {
   uint64_t off;
   uint32_t size;
 };
+// words of a payload head from its first words (avail of them; 0: malformed
+// or more words needed to tell -- version 2 needs 7 + 2 nsections + 1)
+static size_t head_words(const uint32_t* hw, size_t avail) {
+  if (avail < 7 || hw[0] != kPayloadMagic) return 0;
+  const size_t base = 7 + 2 * (size_t)hw[6];
+  if (hw[1] == 1) return base;
+  if (hw[1] != 2 || avail < base + 1) return 0;
+  return base + 1 + hw[base];
+}
+
+// HfGlobal of a frame sharded with one HF preset per rank (payload heads of
+// version 2): num_hf_presets = ranks, one context map over every preset's
+// contexts (rank r's clusters after those of ranks < r), every rank's ANS
+// histograms rebuilt from its clustered counts [ext HfGlobal / HfPass]
+static jxg_status build_hf_presets(const std::vector<std::vector<uint32_t>>& heads,
+                                   const Frame& f, BitWriter& hf) {
+  const uint32_t n = (uint32_t)heads.size();
+  const size_t cw = (kAcCtx + 3) / 4;
+  std::vector<uint8_t> ctxmap((size_t)n * kAcCtx);
+  std::vector<AnsTable> tables;
+  uint32_t off = 0;
+  for (uint32_t r = 0; r < n; r++) {
+    const std::vector<uint32_t>& hw = heads[r];
+    const size_t base = 7 + 2 * (size_t)hw[6];
+    if (hw[1] != 2 || hw.size() < base + 2) return JXG_ERR_INVALID_ARG;
+    const uint32_t B = hw[base], nh = hw[base + 1];
+    if (nh < 1 || nh > (uint32_t)kAnsMaxHists || B != 1 + cw + nh * kAlpha ||
+        hw.size() != base + 1 + B)
+      return JXG_ERR_INVALID_ARG;
+    const uint8_t* cm = reinterpret_cast<const uint8_t*>(hw.data() + base + 2);
+    for (int k = 0; k < kAcCtx; k++) {
+      if (cm[k] >= nh) return JXG_ERR_INVALID_ARG;
+      ctxmap[(size_t)r * kAcCtx + k] = (uint8_t)(off + cm[k]);
+    }
+    const uint32_t* cnt = hw.data() + base + 2 + cw;
+    for (uint32_t h = 0; h < nh; h++) tables.push_back(build_ans_table(cnt + (size_t)h * kAlpha));
+    off += nh;
+  }
+  if (off > 255 || n - 1 >= (1u << ceil_log2(f.ngroups))) return JXG_ERR_INVALID_ARG;
+  hf.put(1, 1);                            // DequantMatrices all_default
+  hf.put(ceil_log2(f.ngroups), n - 1);     // num_hf_presets - 1
+  write_u32_sel(hf, 2, 0, 0);              // used_orders = 0
+  write_ans_histograms(hf, ctxmap, (int)off, tables, kCfg420, nullptr);
+  return JXG_OK;
+}
+
+// hf: with version-2 heads, the generated HfGlobal (section 1 + nlf, whose
+// SectionRef then names payload n = "generated")
 static jxg_status parse_payload_heads(const std::vector<std::vector<uint32_t>>& heads,
                                       const std::vector<size_t>& psizes, uint32_t* w,
-                                      uint32_t* h, std::vector<SectionRef>& secs) {
+                                      uint32_t* h, std::vector<SectionRef>& secs,
+                                      std::vector<uint8_t>& hf) {
   const uint32_t n = (uint32_t)heads.size();
   secs.clear();
+  hf.clear();
   std::vector<bool> seen;
   for (uint32_t i = 0; i < n; i++) {
     const std::vector<uint32_t>& hw = heads[i];
-    if (hw.size() < 7 || hw[0] != kPayloadMagic || hw[1] != 1 || hw[3] != n)
+    if (hw.size() < 7 || hw[0] != kPayloadMagic || (hw[1] != 1 && hw[1] != 2) ||
+        hw[1] != heads[0][1] || hw[3] != n)
       return JXG_ERR_INVALID_ARG;
     if (i == 0) {
       *w = hw[4];
@@ -1828,8 +1950,9 @@ static jxg_status parse_payload_heads(const std::vector<std::vector<uint32_t>>& 
     } else if (hw[4] != *w || hw[5] != *h) {
       return JXG_ERR_INVALID_ARG;
     }
-    if (hw.size() < 7 + 2 * (size_t)hw[6]) return JXG_ERR_INVALID_ARG;
-    uint64_t off = 4 * (7 + 2 * (uint64_t)hw[6]);
+    const size_t hwords = head_words(hw.data(), hw.size());
+    if (!hwords || hw.size() != hwords) return JXG_ERR_INVALID_ARG;
+    uint64_t off = 4 * (uint64_t)hwords;  // the body follows the whole head
     for (uint32_t k = 0; k < hw[6]; k++) {
       const uint32_t id = hw[7 + 2 * k], sz = hw[8 + 2 * k];
       if (off + sz > psizes[i]) return JXG_ERR_INVALID_ARG;
@@ -1846,6 +1969,16 @@ static jxg_status parse_payload_heads(const std::vector<std::vector<uint32_t>>& 
   if (*w == 0 || *h == 0) return JXG_ERR_INVALID_ARG;
   const Frame f = make_frame(*w, *h, 1.0f);
   if (secs.size() != 2 + f.nlf + f.ngroups) return JXG_ERR_INVALID_ARG;
+  if (heads[0][1] == 2) {  // per-rank presets: HfGlobal from the heads
+    const uint32_t id = 1 + f.nlf;
+    if (seen[id]) return JXG_ERR_INVALID_ARG;
+    BitWriter bw;
+    const jxg_status st = build_hf_presets(heads, f, bw);
+    if (st) return st;
+    hf = bw.bytes();
+    secs[id] = SectionRef{n, 0, (uint32_t)hf.size()};
+    seen[id] = true;
+  }
   for (size_t i = 0; i < secs.size(); i++)
     if (!seen[i]) return JXG_ERR_INVALID_ARG;  // section missing
   return JXG_OK;
@@ -1853,11 +1986,16 @@ static jxg_status parse_payload_heads(const std::vector<std::vector<uint32_t>>& 
 
 static std::vector<uint32_t> read_head(const uint8_t* p, size_t size) {
   if (size < 28) return {};
-  uint32_t h7[7];
-  std::memcpy(h7, p, 28);
-  const size_t words = 7 + 2 * (size_t)h7[6];
-  if (size < words * 4) return {};
-  std::vector<uint32_t> hw(words);
+  std::vector<uint32_t> hw(7);
+  std::memcpy(hw.data(), p, 28);
+  const size_t base = 7 + 2 * (size_t)hw[6];
+  if (hw[1] == 2 && size >= (base + 1) * 4) {  // version 2: the preset block's length
+    hw.resize(base + 1);
+    std::memcpy(hw.data(), p, (base + 1) * 4);
+  }
+  const size_t words = head_words(hw.data(), hw.size());
+  if (!words || size < words * 4) return {};
+  hw.resize(words);
   std::memcpy(hw.data(), p, words * 4);
   return hw;
 }
@@ -1872,17 +2010,25 @@ static jxg_status shard_assemble_device(Ctx* c, const uint8_t* d_base, const siz
   std::vector<std::vector<uint32_t>> heads(n);
   std::vector<size_t> ps(psizes, psizes + n);
   for (uint32_t i = 0; i < n; i++) {
-    uint32_t h7[7];
+    std::vector<uint32_t>& hw = heads[i];
     if (psizes[i] < 28) return JXG_ERR_INVALID_ARG;
-    JXG_HIP(hipMemcpy(h7, d_base + offsets[i], 28, hipMemcpyDeviceToHost));
-    const size_t words = 7 + 2 * (size_t)h7[6];
-    if (psizes[i] < words * 4) return JXG_ERR_INVALID_ARG;
-    heads[i].resize(words);
-    JXG_HIP(hipMemcpy(heads[i].data(), d_base + offsets[i], words * 4, hipMemcpyDeviceToHost));
+    hw.resize(7);
+    JXG_HIP(hipMemcpy(hw.data(), d_base + offsets[i], 28, hipMemcpyDeviceToHost));
+    const size_t base = 7 + 2 * (size_t)hw[6];
+    if (hw[1] == 2) {  // version 2: read up to the preset block's length
+      if (psizes[i] < (base + 1) * 4) return JXG_ERR_INVALID_ARG;
+      hw.resize(base + 1);
+      JXG_HIP(hipMemcpy(hw.data(), d_base + offsets[i], (base + 1) * 4, hipMemcpyDeviceToHost));
+    }
+    const size_t words = head_words(hw.data(), hw.size());
+    if (!words || psizes[i] < words * 4) return JXG_ERR_INVALID_ARG;
+    hw.resize(words);
+    JXG_HIP(hipMemcpy(hw.data(), d_base + offsets[i], words * 4, hipMemcpyDeviceToHost));
   }
   uint32_t w = 0, h = 0;
   std::vector<SectionRef> secs;
-  jxg_status st = parse_payload_heads(heads, ps, &w, &h, secs);
+  std::vector<uint8_t> hf;
+  jxg_status st = parse_payload_heads(heads, ps, &w, &h, secs, hf);
   if (st) return st;
   std::vector<uint32_t> sizes(secs.size());
   for (size_t i = 0; i < secs.size(); i++) sizes[i] = secs[i].size;
@@ -1890,6 +2036,13 @@ static jxg_status shard_assemble_device(Ctx* c, const uint8_t* d_base, const siz
   write_headers(head, w, h);
   write_toc(head, sizes);
   std::vector<uint32_t> chunk_words = head.words32();
+  // a generated HfGlobal (per-rank presets) follows the headers in the chunk arena
+  const uint64_t hf_src = (uint64_t)chunk_words.size() * 32;
+  for (size_t i = 0; i < hf.size(); i += 4) {
+    uint32_t wv = 0;
+    for (size_t b = 0; b < 4 && i + b < hf.size(); b++) wv |= (uint32_t)hf[i + b] << (8 * b);
+    chunk_words.push_back(wv);
+  }
   chunk_words.push_back(0);
   std::vector<ConcatPiece> cps;
   uint64_t dst = 0, max_words = 0;
@@ -1898,9 +2051,11 @@ static jxg_status shard_assemble_device(Ctx* c, const uint8_t* d_base, const siz
   dst = (head.bits() + 7) & ~7ull;
   // payloads are read as one 32-bit-word arena starting at d_base
   for (const SectionRef& r : secs) {
-    const uint64_t src_bit = (offsets[r.payload] + r.off) * 8;
     if (r.size) {
-      cps.push_back({src_bit, dst, (uint64_t)r.size * 8, 0, 0});
+      if (r.payload == n)
+        cps.push_back({hf_src, dst, (uint64_t)r.size * 8, 1, 0});
+      else
+        cps.push_back({(offsets[r.payload] + r.off) * 8, dst, (uint64_t)r.size * 8, 0, 0});
       max_words = std::max<uint64_t>(max_words, ((uint64_t)r.size * 8 + 31) / 32);
     }
     dst += (uint64_t)r.size * 8;
@@ -1943,7 +2098,7 @@ static jxg_status shard_write_host(Ctx* c, const uint32_t* const* heads_in, cons
   for (uint32_t i = 0; i < n; i++) {
     if (!heads_in[i] || words[i] < 7) return JXG_ERR_INVALID_ARG;
     heads[i].assign(heads_in[i], heads_in[i] + words[i]);
-    if (words[i] < 7 + 2 * (size_t)heads[i][6]) return JXG_ERR_INVALID_ARG;
+    if (head_words(heads[i].data(), words[i]) != words[i]) return JXG_ERR_INVALID_ARG;
     size_t body = 0;
     for (uint32_t k = 0; k < heads[i][6]; k++) body += heads[i][8 + 2 * k];
     ps[i] = words[i] * 4 + body;
@@ -1952,7 +2107,8 @@ static jxg_status shard_write_host(Ctx* c, const uint32_t* const* heads_in, cons
   if (me >= n || heads[me] != c->payload_head) return JXG_ERR_INVALID_ARG;
   uint32_t w = 0, h = 0;
   std::vector<SectionRef> secs;
-  jxg_status st = parse_payload_heads(heads, ps, &w, &h, secs);
+  std::vector<uint8_t> hf;
+  jxg_status st = parse_payload_heads(heads, ps, &w, &h, secs, hf);
   if (st) return st;
   std::vector<uint32_t> sec_size(secs.size());
   for (size_t i = 0; i < secs.size(); i++) sec_size[i] = secs[i].size;
@@ -1988,7 +2144,11 @@ static jxg_status shard_write_host(Ctx* c, const uint32_t* const* heads_in, cons
   if (run_len)
     JXG_HIP(hipMemcpyAsync(dst + run_dst, reinterpret_cast<const uint8_t*>(c->out.p) + run_src,
                            run_len, hipMemcpyDeviceToHost, s));
-  if (me == 0) std::memcpy(dst, hb.data(), hb.size());
+  if (me == 0) {
+    std::memcpy(dst, hb.data(), hb.size());
+    for (size_t i = 0; i < secs.size(); i++)  // a generated HfGlobal (per-rank presets)
+      if (secs[i].payload == n && secs[i].size) std::memcpy(dst + out_off[i], hf.data(), hf.size());
+  }
   JXG_HIP(hipStreamSynchronize(s));
   return JXG_OK;
 }
@@ -2007,7 +2167,8 @@ static jxg_status shard_assemble(const uint8_t* const* payloads, const size_t* s
   }
   uint32_t w = 0, h = 0;
   std::vector<SectionRef> secs;
-  jxg_status st = parse_payload_heads(heads, ps, &w, &h, secs);
+  std::vector<uint8_t> hf;
+  jxg_status st = parse_payload_heads(heads, ps, &w, &h, secs, hf);
   if (st) return st;
   std::vector<uint32_t> sec_size(secs.size());
   size_t total = 0;
@@ -2024,7 +2185,7 @@ static jxg_status shard_assemble(const uint8_t* const* payloads, const size_t* s
   std::memcpy(o, hb.data(), hb.size());
   size_t pos = hb.size();
   for (const SectionRef& r : secs) {
-    std::memcpy(o + pos, payloads[r.payload] + r.off, r.size);
+    std::memcpy(o + pos, r.payload == n ? hf.data() : payloads[r.payload] + r.off, r.size);
     pos += r.size;
   }
   out->data = o;

@@ -4,8 +4,11 @@ One process per GPU (backend "nccl" = RCCL over xGMI).  Each rank encodes a
 balanced contiguous raster range of the frame's 256x256 pass groups and the
 LF groups it owns (the rank holding most of an LF group's pass groups); the
 only collectives are
-  1. all_reduce(sum) of the AC token histogram (132 x 128 u32, 68 KB) so all
-     ranks derive the same prefix codes,
+  1. prefix codes only: all_reduce(sum) of the AC token histogram (132 x 128
+     u32, 68 KB) so all ranks derive the same codes (one HF preset).  With ANS
+     every rank codes its groups with its own histograms (one HF preset per
+     rank; its clustered counts ride in its payload head and
+     HfGlobal is written at assembly), so there is no histogram collective,
   2. all_to_all of per-block records (strategy, quant field, quantized DC;
      14 B per 8x8 block): a rank sends the records of its pass groups whose LF
      group another rank owns to that rank only (jxg_shard_exchange splits;
@@ -13,14 +16,17 @@ only collectives are
      16384^2 over 8 ranks: nothing),
   3. assembly, either
      host   (``host=SharedHostBuffer``): one all-gather of the payload heads
-            (section ids and sizes, ~2 KB per rank), then every rank DMAs its
+            (section ids and sizes, ~2 KB per rank; + ~13 KB of preset with
+            ANS), then every rank DMAs its
             own sections into one /dev/shm buffer shared by the node's ranks
             at their codestream offsets (rank 0 adds headers + TOC) -- the
             node's PCIe links work in parallel and nothing crosses xGMI; or
      device (default): a gather of the per-rank section payloads on rank 0
             (device to device), which writes headers + TOC and moves every
             section with the concat kernel, then one D2H of the codestream.
-The result is byte-identical to a single-GPU encode of the same frame.
+With prefix codes the result is byte-identical to a single-GPU encode of the
+same frame; with ANS it decodes to the same image (same coefficients, strategy,
+quant field, DC and CfL maps) with per-rank histograms.
 """
 from __future__ import annotations
 
@@ -32,7 +38,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from . import Encoder, load, shard_assemble, shard_exchange, shard_sizes
+from . import FLAG_ANS, Encoder, load, shard_assemble, shard_exchange, shard_sizes
 
 
 class SharedHostBuffer:
@@ -109,12 +115,27 @@ class SharedHostBuffer:
         self.cap = 0
 
 
+AC_CONTEXTS = 7425   # AC contexts of one HF preset (15 block contexts x 495)
+ANS_MAX_HISTS = 8    # histograms per preset (csrc/jxg_bitstream.h kAnsMaxHists)
+ALPHA = 128
+
+
 def _head_cap(width: int, height: int) -> int:
     """Upper bound of a payload head in u32 words: 7 + 2 x sections, a rank
-    holding at most LfGlobal, HfGlobal, every LF group and every pass group."""
+    holding at most LfGlobal, HfGlobal, every LF group and every pass group;
+    plus, for version-2 heads (ANS, one HF preset per rank), the preset block
+    [B][nhist][context map packed in words][counts nhist x 128]."""
     nlf = -(-width // 2048) * -(-height // 2048)
     ngroups = -(-width // 256) * -(-height // 256)
-    return 7 + 2 * (2 + nlf + ngroups)
+    preset = 2 + -(-AC_CONTEXTS // 4) + ANS_MAX_HISTS * ALPHA
+    return 7 + 2 * (2 + nlf + ngroups) + preset
+
+
+def _head_len(h) -> int:
+    """Words of a payload head (version 1: 7 + 2 x sections; version 2: + the
+    preset block, whose first word counts the words after it)."""
+    base = 7 + 2 * int(h[6])
+    return base if int(h[1]) == 1 else base + 1 + int(h[base])
 
 
 def _all_gather_heads(head: np.ndarray, rank: int, world: int, width: int, height: int,
@@ -124,14 +145,14 @@ def _all_gather_heads(head: np.ndarray, rank: int, world: int, width: int, heigh
     head's own length is 7 + 2 x its section count (word 6)."""
     dev = "cpu" if dist.get_backend(group) == "gloo" else torch.device("cuda", torch.cuda.current_device())
     cap = _head_cap(width, height)
-    if head.size > cap or head.size < 7:
+    if head.size > cap or head.size < 7 or head.size != _head_len(head):
         raise RuntimeError("payload head of %d words outside [7, %d]" % (head.size, cap))
     mine = torch.zeros(cap, dtype=torch.int32, device=dev)
     mine[:head.size] = torch.from_numpy(head.view(np.int32).copy()).to(dev)
     parts = [torch.empty(cap, dtype=torch.int32, device=dev) for _ in range(world)]
     dist.all_gather(parts, mine, group=group)
     allh = torch.stack(parts).cpu().numpy().view(np.uint32)  # one copy to the host
-    return [allh[r, :7 + 2 * int(allh[r, 6])].copy() for r in range(world)]
+    return [allh[r, :_head_len(allh[r])].copy() for r in range(world)]
 
 
 def gather_payloads(payload: bytes, rank: int, world: int, device, group=None):
@@ -183,19 +204,26 @@ def encode_sharded(enc: Encoder, d_rgb: torch.Tensor, width: int, height: int, r
                     send.data_ptr())
     ns, nr = sum(snd), sum(rcv)
     gloo = dist.get_backend(group) == "gloo"
+    # ANS: one HF preset per rank -- every rank codes its groups
+    # with its own histograms, no all-reduce; HfGlobal is built at assembly
+    # from the presets in the payload heads.  Prefix codes: one preset from
+    # the summed histogram.
+    presets = bool(enc.params.flags & FLAG_ANS)
     if gloo:
         # host staging (gloo: CPU rehearsal of the exchange, e.g. several ranks
         # on one device); the nccl (RCCL) path below keeps everything in HBM
-        h = hist.cpu()
-        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
-        hist.copy_(h)
+        if not presets:
+            h = hist.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+            hist.copy_(h)
         if bufs["any"]:
             r_cpu = torch.empty(nr, dtype=torch.uint8)
             dist.all_to_all_single(r_cpu, send[:ns].cpu(), output_split_sizes=rcv,
                                    input_split_sizes=snd, group=group)
             recv[:nr].copy_(r_cpu)
     else:
-        dist.all_reduce(hist, op=dist.ReduceOp.SUM, group=group)
+        if not presets:
+            dist.all_reduce(hist, op=dist.ReduceOp.SUM, group=group)
         if bufs["any"]:
             dist.all_to_all_single(recv[:nr], send[:ns], output_split_sizes=rcv,
                                    input_split_sizes=snd, group=group)

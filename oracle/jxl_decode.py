@@ -1028,6 +1028,8 @@ def decode(data: bytes, want_pixels: bool = True) -> Decoded:
         raise JxlError("custom coefficient orders not produced")
     nctx_ac = 15 * (37 + 458)
     hf = EntropyStream(s, npresets * nctx_ac)
+    d.npresets = npresets
+    d.group_presets = np.zeros(ng, dtype=np.int64)
     d.ac = np.zeros((bys, bxs, 3, 64), dtype=np.int64)
     d.ac_tokens = np.zeros((ng, 3), dtype=np.int64)
     for g in range(ng):
@@ -1036,6 +1038,9 @@ def decode(data: bytes, want_pixels: bool = True) -> Decoded:
         bx0, by0 = gx * 32, gy * 32
         gw, gh = min(32, bxs - bx0), min(32, bys - by0)
         preset = s.read(ceil_log2(npresets))
+        if preset >= npresets:
+            raise JxlError("HF preset index out of range")
+        d.group_presets[g] = preset
         off = preset * nctx_ac
         hf.begin(s)
         nzs = np.zeros((3, gh, gw), dtype=np.int64)

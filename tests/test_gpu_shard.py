@@ -26,6 +26,9 @@ def sharded_encode(jxg_mod, img, world, d=1.0, e=7, p=0, flags=0, t=None):
     sends = [torch.zeros(cap, dtype=torch.uint8, device="cuda") for _ in range(world)]
     for r in range(world):
         encs[r].shard_begin(t.data_ptr(), w, h, r, world, hists[r].data_ptr(), sends[r].data_ptr())
+    # prefix codes: one HF preset from the summed histogram; ANS: one preset
+    # per rank (its own histogram, no all-reduce)
+    presets = bool(flags & jxg_mod.FLAG_ANS) and world > 1
     hist = torch.stack(hists).sum(0).to(torch.int32).contiguous()
 
     def segment(src, dst):  # src's records for dst (send order: by destination)
@@ -45,7 +48,8 @@ def sharded_encode(jxg_mod, img, world, d=1.0, e=7, p=0, flags=0, t=None):
     torch.cuda.synchronize()
     payloads = []
     for r in range(world):
-        size = encs[r].shard_end(hist.data_ptr(), recvs[r].data_ptr())
+        size = encs[r].shard_end((hists[r] if presets else hist).data_ptr(),
+                                 recvs[r].data_ptr())
         payloads.append(encs[r].shard_payload_bytes(size))
     # distributed host assembly: every "rank" writes its sections into one
     # host buffer (first call with a too-small buffer reports the size)
@@ -97,7 +101,7 @@ def test_sharded_8k_equals_single(jxg_mod):
     assert sharded_encode(jxg_mod, img, 8) == ref
 
 
-def _gloo_rank(rank, world, port, w, h, result, shm=False):
+def _gloo_rank(rank, world, port, w, h, result, shm=False, flags=0):
     import os
 
     import torch
@@ -114,12 +118,12 @@ def _gloo_rank(rank, world, port, w, h, result, shm=False):
         img = synth_rgb8(w, h, 5)
         t = torch.from_numpy(img).cuda()
         host = SharedHostBuffer(rank, world) if shm else None
-        with jxg.Encoder(distance=1.0, effort=7) as enc:
+        with jxg.Encoder(distance=1.0, effort=7, flags=flags) as enc:
             out = encode_sharded(enc, t, w, h, rank, world, host=host)
             out2 = encode_sharded(enc, t, w, h, rank, world, host=host)  # buffer reuse
             if rank == 0:
                 ref = enc.encode(img)
-                result.put(out == ref and out2 == ref)
+                result.put((bytes(out), bytes(out2), ref))
         if host is not None:
             dist.barrier()
             host.close()
@@ -127,11 +131,13 @@ def _gloo_rank(rank, world, port, w, h, result, shm=False):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("shm", [False, True])
-def test_multiprocess_encode_sharded(jxg_mod, shm):
+@pytest.mark.parametrize("shm,ans", [(False, False), (True, False), (True, True), (False, True)])
+def test_multiprocess_encode_sharded(jxg_mod, decoder, shm, ans):
     """jxg.dist.encode_sharded in 2 processes (gloo, both ranks on cuda:0):
     the multi-process orchestration bench.py --gpus N runs over RCCL; shm:
-    the distributed host assembly into a /dev/shm buffer."""
+    the distributed host assembly into a /dev/shm buffer.  Prefix codes: the
+    single-GPU bytes; ANS (one HF preset per rank, no histogram all-reduce):
+    the single-GPU image."""
     import socket
 
     import torch.multiprocessing as mp
@@ -141,23 +147,50 @@ def test_multiprocess_encode_sharded(jxg_mod, shm):
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_gloo_rank, args=(r, 2, port, 1100, 700, q, shm))
+    flags = jxg_mod.FLAG_ANS if ans else 0
+    procs = [ctx.Process(target=_gloo_rank, args=(r, 2, port, 1100, 700, q, shm, flags))
              for r in range(2)]
     for p in procs:
         p.start()
+    # read before joining: a child holding queued data does not exit until it
+    # has been consumed
+    got = q.get(timeout=280)
     for p in procs:
         p.join(300)
         assert p.exitcode == 0
-    assert q.get(timeout=10) is True
+    out, out2, ref = got
+    assert out == out2
+    if not ans:
+        assert out == ref
+    else:
+        dr, dg = decoder.decode(ref), decoder.decode(out)
+        assert dg.npresets == 2
+        _same_image(dr, dg)
 
 
-def test_sharded_ans_equals_single(jxg_mod):
+def _same_image(a, b):
+    for k in ("acs", "qf", "dc", "ac", "cmap"):
+        assert np.array_equal(getattr(a, k), getattr(b, k)), k
+    assert np.array_equal(a.rgb, b.rgb)
+
+
+@pytest.mark.parametrize("world", [2, 3, 5])
+def test_sharded_ans_per_rank_presets(jxg_mod, decoder, world):
+    """ANS sharding with one HF preset per rank (no histogram
+    all-reduce): the codestream carries `world` presets, every pass group
+    selects its rank's, and it decodes to exactly the single-GPU image."""
     from jxg.synth import synth_rgb8
 
     img = synth_rgb8(1500, 900, 17)
     with jxg_mod.Encoder(distance=1.0, effort=7, flags=jxg_mod.FLAG_ANS) as enc:
         ref = enc.encode(img)
-    assert sharded_encode(jxg_mod, img, 3, flags=jxg_mod.FLAG_ANS) == ref
+    got = sharded_encode(jxg_mod, img, world, flags=jxg_mod.FLAG_ANS)
+    dr, dg = decoder.decode(ref), decoder.decode(got)
+    assert dr.npresets == 1 and dg.npresets == world
+    ng = len(dg.group_presets)
+    assert list(dg.group_presets) == [min(r for r in range(world) if g < ng * (r + 1) // world)
+                                      for g in range(ng)]
+    _same_image(dr, dg)
 
 
 @pytest.mark.parametrize("world", [2, 8])
