@@ -507,13 +507,15 @@ __global__ __launch_bounds__(kAcThreads) void ac_emit_kernel(AcArgs a) {
 // Per 64 records the lanes decode record, f, rcp and table base in parallel
 // (the next 64 records are fetched meanwhile) and store the emitted bits of
 // their record with one coalesced store.
-// One chain wave per SIMD (4 per workgroup; 68 KB of LDS, so the workgroup
-// shares its CU with a transform kernel of the next frame): a second chain
-// wave on the SIMD delays every step by its own issue (8 per workgroup: 6.7 vs
-// 6.0 ms at 8K, profiles/r02g); the chain waves run at the highest wave
-// priority so co-resident transform waves only fill their idle issue slots.
+// Two chain waves per SIMD (8 per workgroup, 68 KB of LDS): the second wave
+// delays every step by its own issue (one frame's chains 6.7 vs 6.0 ms at 8K
+// with 4 per workgroup, profiles/r02g), but the chains of a frame occupy 64
+// CUs instead of 128, so the transform kernels of the frames behind keep full
+// occupancy on the rest (pipelined 8K +3.5 %).  The chain waves
+// run at the highest wave priority so co-resident transform waves only fill
+// their idle issue slots.
 #ifndef JXG_ANS_WAVES  // (experiment builds override it: tools/build_variant.sh)
-#define JXG_ANS_WAVES 4
+#define JXG_ANS_WAVES 8
 #endif
 constexpr int kAnsWaves = JXG_ANS_WAVES;
 __device__ __forceinline__ uint32_t wave_ror1(uint32_t x) {

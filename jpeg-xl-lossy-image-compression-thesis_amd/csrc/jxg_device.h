@@ -14,6 +14,8 @@ namespace jxg {
 // raw AcStrategy ids returned by the thesis selector
 // (proposals/combined.diff:227-233)
 enum : int { kDCT8 = 0, kDCT4X4 = 3, kDCT4X8 = 12, kDCT8X4 = 13 };
+// the two Haar-type 8x8 candidates of the strategy search [ext AcStrategy]
+enum : int { kIDENTITY = 1, kDCT2X2 = 2 };
 
 // opsin absorbance [ext libjxl opsin_params.h]
 constexpr float kM00 = 0.30f, kM01 = 0.622f, kM02 = 0.078f;
@@ -187,6 +189,13 @@ __host__ __device__ constexpr int c_inv_order_h(int k) {
 // (0, 0) maps to the DC slot
 __host__ __device__ __forceinline__ int co_index_rt(int T, int prow, int pcol) {
   if (T == kDCT8) return prow * 8 + pcol;
+  // IDENTITY / DCT2X2: lane pcol's value prow (front kernel haar_lane)
+  if (T == kIDENTITY) return ((pcol >> 2) + 2 * (pcol & 3)) * 8 + (prow >> 2) + 2 * (prow & 3);
+  if (T == kDCT2X2) {
+    const int q = pcol >> 1;
+    const int row = (pcol & 1) ? 4 + q : (prow >= 4 ? q : ((q & 1) ? 2 + (q >> 1) : (q >> 1)));
+    return row * 8 + prow;
+  }
   if (T == kDCT4X4) return ((prow >> 2) + 2 * (prow & 3)) * 8 + (pcol >> 2) + 2 * (pcol & 3);
   if (T == kDCT8X4) return ((prow >> 2) + 2 * (prow & 3)) * 8 + pcol;
   return ((pcol >> 2) + 2 * (pcol & 3)) * 8 + prow;  // kDCT4X8

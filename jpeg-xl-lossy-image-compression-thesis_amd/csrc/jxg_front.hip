@@ -26,11 +26,13 @@ namespace jxg {
 
 __constant__ float c_lut[256];
 // per-lane quantization tables, built on the host from the weights
-__constant__ float c_wperm[4 * 3 * 64];  // [T][c][lane r][row k] = w[qkind(T)][c][co_index(T,k,r)]
-__constant__ float c_iwperm[4 * 64];     // [T][r][k] = 1.0f / (Y weight) at the same slot
-__constant__ float c_sdperm[4 * 3 * 64]; // [T][c][r][k] distortion weight at the same slot
-__constant__ float c_btab[256];          // [q] = 0.145f / q (AdjustQuantBias, |q| >= 2)
-__constant__ uint8_t c_zz[4 * 64];       // [T][r][k] = zigzag index of co_index(T,k,r)
+// (T: table index tindex -- DCT8, DCT4X4, DCT4X8, DCT8X4, DCT2X2, IDENTITY)
+constexpr int kNT = 6;
+__constant__ float c_wperm[kNT * 3 * 64];  // [T][c][lane r][row k] = w[qkind(T)][c][co_index(T,k,r)]
+__constant__ float c_iwperm[kNT * 64];     // [T][r][k] = 1.0f / (Y weight) at the same slot
+__constant__ float c_sdperm[kNT * 3 * 64]; // [T][c][r][k] distortion weight at the same slot
+__constant__ float c_btab[256];            // [q] = 0.145f / q (AdjustQuantBias, |q| >= 2)
+__constant__ uint8_t c_zz[kNT * 64];       // [T][r][k] = zigzag index of co_index(T,k,r)
 
 constexpr int kTile = 64;
 constexpr int kRows = 66;           // 64 + halo above/below
@@ -267,7 +269,14 @@ __device__ __forceinline__ void transpose8(float* v, int r) {
 
 template <int T>
 constexpr int tindex() {
-  return T == kDCT8 ? 0 : (T == kDCT4X4 ? 1 : (T == kDCT4X8 ? 2 : 3));
+  return T == kDCT8 ? 0
+                    : (T == kDCT4X4 ? 1
+                                    : (T == kDCT4X8 ? 2 : (T == kDCT8X4 ? 3 : (T == kDCT2X2 ? 4 : 5))));
+}
+__device__ __forceinline__ int tindex_rt(int t) {
+  return t == kDCT8 ? 0
+                    : (t == kDCT4X4 ? 1
+                                    : (t == kDCT4X8 ? 2 : (t == kDCT8X4 ? 3 : (t == kDCT2X2 ? 4 : 5))));
 }
 
 __device__ __forceinline__ int bitlen(uint32_t v) { return 32 - __clz(v); }  // __clz(0) = 32
@@ -298,10 +307,10 @@ struct GroupCtx {
   int ly0;             // tile-local row of the block's pixel row 0 (= lby*8 + 1)
   int lx0;             // tile-local column of pixel column 0 (= lbx*8 + 1)
   int r;
-  const float* wperm;  // LDS [4 T][3 c][8 r][8 k] weights per lane
-  const float* iwperm; // LDS [4 T][8 r][8 k] Y inverse weights per lane
+  const float* wperm;  // LDS [kNT T][3 c][8 r][8 k] weights per lane
+  const float* iwperm; // LDS [kNT T][8 r][8 k] Y inverse weights per lane
   const float* btab;   // LDS [256] 0.145f / q
-  const float* sdperm; // LDS [4 T][3 c][8 r][8 k] distortion weights per lane
+  const float* sdperm; // LDS [kNT T][3 c][8 r][8 k] distortion weights per lane
   float kx, kb;        // chroma from luma of the tile: X - kx Yd, B - kb Yd
 };
 
@@ -341,26 +350,17 @@ struct CandAcc {
   QVals q;
 };
 
-// Column pass of one channel C (0 X, 1 Y, 2 B) of one block under strategy T
-// from the row-transformed, transposed values vt: transform, quantize the 8
-// coefficients, accumulate e*e (fmaf), rate bits and the non-zero count; Y
-// records its dequantized values for the B residual.  Float op order ==
-// oracle jxo_quantize_block.
-template <int T, int C>
-__device__ __forceinline__ void quantize_cols(const GroupCtx& G, const float* vt, float scale,
-                                              float inv_scale, CandAcc& A) {
-  constexpr int ti = tindex<T>();
-  constexpr float kBias1 = 1.0f - 0.07005449891748593f;
-  float v[8];
-#pragma unroll
-  for (int k = 0; k < 8; k++) v[k] = vt[k];
+// Column transform of strategy T (lane r: working-array column r) from the
+// row-transformed, transposed values, with the lowest-frequency combine
+// (enc_transforms [ext]; slots per oracle)
+template <int T>
+__device__ __forceinline__ void col_transform(const GroupCtx& G, float* v) {
   if (T == kDCT8 || T == kDCT4X8) {
     dct8_1d(v);
   } else {
     dct4_1d(v);
     dct4_1d(v + 4);
   }
-  // lowest-frequency combine (enc_transforms [ext]); slots per oracle
   if (T == kDCT4X4) {
     const float A0 = group_lane<0>(v[0]), Cc = group_lane<0>(v[4]);
     const float B0 = group_lane<4>(v[0]), D = group_lane<4>(v[4]);
@@ -382,6 +382,101 @@ __device__ __forceinline__ void quantize_cols(const GroupCtx& G, const float* vt
     if (G.r == 0) v[0] = (A0 + B0) * 0.5f;
     if (G.r == 4) v[0] = (A0 - B0) * 0.5f;
   }
+}
+
+// The Haar-type candidates of channel C straight from the pixels (lane r =
+// pixel row r), leaving lane r's 8 values in the slot order of co_index_rt
+// (oracle jxo_transform, same float ops):
+//   DCT2X2    three levels of 2x2 Haar steps; a level's cells pair lanes
+//             r ^ 1 (level 1: all rows), r ^ 2 (level 2: the even lanes'
+//             first four values), r ^ 4 (level 3: lanes 0 and 4, first two);
+//             the top lane of a pair keeps (a_top +- a_bottom) / 4, the bottom
+//             lane (b_top +- b_bottom) / 4;
+//   IDENTITY  lane r = row iy = r & 3 of sub-block row r >> 2: residuals
+//             against the sub-block's pixel (1, 1) (from lane 4y + 1), the
+//             (0, 0) residual moved into the (1, 1) slot (from lane 4y), the
+//             sub-block means (row sums, quad tree) in the (0, 0) slots and
+//             combined over lanes 0 / 4 like DCT4X4's.
+template <int T, int C>
+__device__ __forceinline__ void haar_lane(const GroupCtx& G, float* v) {
+  const float* plane = G.pix + C * kPlane;
+  const int base = lds_at(G.lx0, G.ly0 + G.r);
+  float p[8];
+#pragma unroll
+  for (int x = 0; x < 8; x++) p[x] = plane[base + x];
+  if constexpr (T == kDCT2X2) {
+    const bool top1 = (G.r & 1) == 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const float a = p[2 * j] + p[2 * j + 1], b = p[2 * j] - p[2 * j + 1];
+      const float ap = xor_lane<1>(a), bp = xor_lane<1>(b);
+      v[j] = top1 ? (a + ap) * 0.25f : (bp + b) * 0.25f;
+      v[4 + j] = top1 ? (a - ap) * 0.25f : (bp - b) * 0.25f;
+    }
+    const bool top2 = (G.r & 2) == 0, even = (G.r & 1) == 0;
+    float n2[4];
+#pragma unroll
+    for (int x = 0; x < 2; x++) {
+      const float a = v[2 * x] + v[2 * x + 1], b = v[2 * x] - v[2 * x + 1];
+      const float ap = xor_lane<2>(a), bp = xor_lane<2>(b);
+      n2[x] = top2 ? (a + ap) * 0.25f : (bp + b) * 0.25f;
+      n2[2 + x] = top2 ? (a - ap) * 0.25f : (bp - b) * 0.25f;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) v[k] = even ? n2[k] : v[k];
+    const bool top3 = (G.r & 4) == 0, l3 = (G.r & 3) == 0;
+    const float a = v[0] + v[1], b = v[0] - v[1];
+    const float ap = xor_lane<4>(a), bp = xor_lane<4>(b);
+    const float n30 = top3 ? (a + ap) * 0.25f : (bp + b) * 0.25f;
+    const float n31 = top3 ? (a - ap) * 0.25f : (bp - b) * 0.25f;
+    v[0] = l3 ? n30 : v[0];
+    v[1] = l3 ? n31 : v[1];
+  } else {  // kIDENTITY
+    const float rs0 = ((p[0] + p[1]) + p[2]) + p[3], rs1 = ((p[4] + p[5]) + p[6]) + p[7];
+    float s0 = rs0 + xor_lane<1>(rs0), s1 = rs1 + xor_lane<1>(rs1);
+    s0 = s0 + xor_lane<2>(s0);
+    s1 = s1 + xor_lane<2>(s1);
+    const float dc0 = s0 * (1.0f / 16.0f), dc1 = s1 * (1.0f / 16.0f);
+    const bool hi = (G.r & 4) != 0;
+    const float p11a = group_lane<1>(p[1]), p11b = group_lane<5>(p[1]);
+    const float p15a = group_lane<1>(p[5]), p15b = group_lane<5>(p[5]);
+    const float q0 = hi ? p11b : p11a, q1 = hi ? p15b : p15a;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      v[k] = p[k] - q0;
+      v[4 + k] = p[4 + k] - q1;
+    }
+    const float t0 = xor_lane<1>(v[0]), t1 = xor_lane<1>(v[4]);
+    const int iy = G.r & 3;
+    if (iy == 1) {
+      v[1] = t0;
+      v[5] = t1;
+    }
+    const float o0 = xor_lane<4>(dc0), o1 = xor_lane<4>(dc1);
+    const float A = hi ? o0 : dc0, B = hi ? o1 : dc1, Cc = hi ? dc0 : o0, D = hi ? dc1 : o1;
+    if (iy == 0) {
+      v[0] = dc0;
+      v[4] = dc1;
+    }
+    if (G.r == 0) {
+      v[0] = (((A + B) + Cc) + D) * 0.25f;
+      v[4] = (((A + B) - Cc) - D) * 0.25f;
+    } else if (G.r == 4) {
+      v[0] = (((A - B) + Cc) - D) * 0.25f;
+      v[4] = (((A - B) - Cc) + D) * 0.25f;
+    }
+  }
+}
+
+// Quantization of lane r's 8 values of channel C (0 X, 1 Y, 2 B) under
+// strategy T: accumulate e*e (fmaf), rate bits and the non-zero count; Y
+// records its dequantized values for the X / B residuals.  Float op order ==
+// oracle jxo_quantize_block.
+template <int T, int C>
+__device__ __forceinline__ void quant_lane(const GroupCtx& G, float* v, float scale,
+                                           float inv_scale, CandAcc& A) {
+  constexpr int ti = tindex<T>();
+  constexpr float kBias1 = 1.0f - 0.07005449891748593f;
   if (G.r == 0) v[0] = 0.0f;  // DC slot: quantizes to 0, contributes nothing
   const float4* wp = reinterpret_cast<const float4*>(G.wperm + ((ti * 3 + C) * 8 + G.r) * 8);
   const float4 w0 = wp[0], w1 = wp[1];
@@ -438,29 +533,39 @@ __device__ __forceinline__ void quantize_cols(const GroupCtx& G, const float* vt
   A.q.nz = (C == 1 ? 0u : A.q.nz) | ((uint32_t)nzc << sh);
 }
 
+// one channel of one candidate: transform (row pass + transpose + column
+// transform, or the Haar steps) and quantization
+template <int T, int C>
+__device__ __forceinline__ void eval_chan(const GroupCtx& G, float scale, float inv_scale,
+                                          CandAcc& A) {
+  float v[8];
+  if constexpr (T == kDCT2X2 || T == kIDENTITY) {
+    haar_lane<T, C>(G, v);
+  } else {
+    row_pass_t<T == kDCT8 || T == kDCT8X4, C>(G, v);
+    col_transform<T>(G, v);
+  }
+  quant_lane<T, C>(G, v, scale, inv_scale, A);
+}
+
 // One candidate, channels Y, X, B (its own row passes): only one candidate's
 // state is live at a time, which keeps the kernel inside 128 VGPRs.
 template <int T>
 __device__ __forceinline__ float eval_one(const GroupCtx& G, float scale, float inv_scale,
                                           CandAcc& A) {
-  constexpr bool ROW8 = T == kDCT8 || T == kDCT8X4;
   A.bits = 0;
   A.part = 0.0f;
 #pragma unroll 1  // one channel live at a time
   for (int ci = 0; ci < 3; ci++) {
-    float vt[8];
-    if (ci == 0) {
-      row_pass_t<ROW8, 1>(G, vt);
-      quantize_cols<T, 1>(G, vt, scale, inv_scale, A);
-    } else if (ci == 1) {
-      row_pass_t<ROW8, 0>(G, vt);
-      quantize_cols<T, 0>(G, vt, scale, inv_scale, A);
-    } else {
-      row_pass_t<ROW8, 2>(G, vt);
-      quantize_cols<T, 2>(G, vt, scale, inv_scale, A);
-    }
+    if (ci == 0) eval_chan<T, 1>(G, scale, inv_scale, A);
+    else if (ci == 1) eval_chan<T, 0>(G, scale, inv_scale, A);
+    else eval_chan<T, 2>(G, scale, inv_scale, A);
   }
-  constexpr float tm = T == kDCT8 ? 1.0f : (T == kDCT4X4 ? 1.05f : 1.02f);
+  // estimate multipliers (== oracle jxo_quantize_block tmul, JXO_TMUL_*)
+  constexpr float tm = T == kDCT8 ? 1.0f
+                                  : (T == kDCT4X4 ? 1.05f
+                                                  : (T == kDCT2X2 ? 1.05f
+                                                                  : (T == kIDENTITY ? 1.08f : 1.02f)));
   return ((float)group_int_sum(A.bits) + 8.0f * group_tree_sum(A.part)) * tm;
 }
 
@@ -471,7 +576,8 @@ __device__ __forceinline__ void copy_q(QVals& d, const QVals& s, bool take) {
 }
 
 // FindBest8x8Transform's scan (`e < best`, candidates in the order DCT8,
-// DCT4X4, DCT4X8, DCT8X4, best starting at FLT_MAX) as a tournament: a
+// DCT4X4, DCT2X2, DCT4X8, DCT8X4, IDENTITY, best starting at FLT_MAX) as a
+// tournament: a
 // candidate beats another when its estimate is below FLT_MAX and smaller, or
 // equal with a lower scan index; NaN never wins.
 __device__ __forceinline__ bool beats(float ea, int ia, float eb, int ib) {
@@ -567,14 +673,19 @@ __device__ __forceinline__ int cfl_quant(float k) {
 template <bool HOOKP>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FRONT_WPE))) void front_kernel(FrontArgs a) {
   __shared__ __attribute__((aligned(16))) float sPix[3 * kPlane];
-  __shared__ __attribute__((aligned(16))) int16_t sStage[8][8][64];
-  __shared__ __attribute__((aligned(16))) float sWperm[4 * 3 * 64];
-  __shared__ __attribute__((aligned(16))) float sIwperm[4 * 64];
-  __shared__ __attribute__((aligned(16))) float sSdperm[4 * 3 * 64];
-  __shared__ __attribute__((aligned(16))) uint8_t sZz[4 * 64];
-  __shared__ float sLut[256];
+  // phase D's zigzag staging [wave][group][64] reuses the bytes of the sRGB
+  // LUT (XYB load only) and of the phase-A / CfL scratch sH (a barrier
+  // separates their last reads from the first staging store): 81 KB in all,
+  // two workgroups per CU
+  __shared__ __attribute__((aligned(16))) float sUnion[2048];
+  int16_t(*sStage)[8][64] = reinterpret_cast<int16_t(*)[8][64]>(sUnion);
+  float* sLut = sUnion;
+  float(*sH)[64] = reinterpret_cast<float(*)[64]>(sUnion + 256);
+  __shared__ __attribute__((aligned(16))) float sWperm[kNT * 3 * 64];
+  __shared__ __attribute__((aligned(16))) float sIwperm[kNT * 64];
+  __shared__ __attribute__((aligned(16))) float sSdperm[kNT * 3 * 64];
+  __shared__ __attribute__((aligned(16))) uint8_t sZz[kNT * 64];
   __shared__ float sBtab[256];
-  __shared__ float sH[8][64];
   __shared__ float sR[64][3];
   __shared__ uint64_t sLapBits[64];
   const int tid = threadIdx.x;
@@ -586,10 +697,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
   if (tid < 256) {
     sLut[tid] = c_lut[tid];
     sBtab[tid] = c_btab[tid];
-    sIwperm[tid] = c_iwperm[tid];
-    sZz[tid] = c_zz[tid];
   }
-  for (int i = tid; i < 768; i += kThreads) {
+  for (int i = tid; i < kNT * 64; i += kThreads) {
+    sIwperm[i] = c_iwperm[i];
+    sZz[i] = c_zz[i];
+  }
+  for (int i = tid; i < kNT * 3 * 64; i += kThreads) {
     sWperm[i] = c_wperm[i];
     sSdperm[i] = c_sdperm[i];
   }
@@ -691,6 +804,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
     }
     __syncthreads();
     const float T0 = cs[256], T1 = cs[257], T2 = cs[258], T3 = cs[259];
+    __syncthreads();  // cs (sH) is phase D's staging from here on
     const int ytox = cfl_quant(T1 > 0.0f ? T0 / T1 : 0.0f);
     const int ytob = cfl_quant(T3 > 0.0f ? T2 / T3 : 0.0f);
     kx = (float)ytox * (1.0f / 84.0f);
@@ -752,7 +866,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
   const float scale = (float)a.G * (float)raw / 65536.0f;
   const float inv_scale = 1.0f / scale;
   // ---- phase C: strategy search (FindBest8x8Transform [ext] + hooks) ----
-  const int ncand = a.effort >= 5 ? 4 : 1;
+  const int ncand = a.effort >= 5 ? 6 : 1;
   const bool hookF = (a.proposals & 2u) != 0 && ncand > 1;
   // hook P target (combined.diff:270-274) is known before the search: it only
   // depends on the homogeneity indices; its coefficients are kept aside
@@ -766,7 +880,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
   // hook P lives in FindBest8x8Transform, which libjxl does not run below
   // effort 5 (all-DCT8 speed tiers [ext]): no override there either
   if (HOOKP && (a.proposals & 1u) && ncand > 1) pt = partition_of(rh, rv, rd, a.distance);
-  // scan indices: DCT8 0, DCT4X4 1, DCT4X8 2, DCT8X4 3
+  // scan indices: DCT8 0, DCT4X4 1, DCT2X2 2, DCT4X8 3, DCT8X4 4, IDENTITY 5
   QVals best, ptq;
   int bt = kDCT8, bi = 0;
   float beste = FLT_MAX;
@@ -795,9 +909,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
     }
     if (HOOKP) copy_q(ptq, A.q, pt == T);
   };
-  cand(std::integral_constant<int, kDCT8X4>(), 3);
+  cand(std::integral_constant<int, kDCT8X4>(), 4);
   cand(std::integral_constant<int, kDCT4X4>(), 1);
-  cand(std::integral_constant<int, kDCT4X8>(), 2);
+  cand(std::integral_constant<int, kDCT4X8>(), 3);
+  if (ncand > 1) {
+    cand(std::integral_constant<int, kDCT2X2>(), 2);
+    cand(std::integral_constant<int, kIDENTITY>(), 5);
+  }
   if (HOOKP && bt == kDCT8 && pt != kDCT8) {
     bt = pt;
     copy_q(best, ptq, true);
@@ -811,7 +929,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
   }
   if (r < 3) a.nz[r * nb + gb] = (uint16_t)((best.nz >> (8 * r)) & 0xFFu);
   // ---- phase D: zigzag scatter through LDS, 16-byte stores ----
-  const int bti = bt == kDCT8 ? 0 : (bt == kDCT4X4 ? 1 : (bt == kDCT4X8 ? 2 : 3));
+  const int bti = tindex_rt(bt);
   const uint2 zz2 = *reinterpret_cast<const uint2*>(sZz + bti * 64 + r * 8);
   const uint32_t zw[2] = {zz2.x, zz2.y};
   int16_t* stage = &sStage[wave][g][0];
@@ -875,23 +993,29 @@ __global__ __launch_bounds__(kThreads) void homog_kernel(HomogArgs a) {
   }
 }
 
-hipError_t set_front_constants(const float lut[256], const float wts[3][3][64], hipStream_t s) {
-  static float wperm[4 * 3 * 64], iwperm[4 * 64], btab[256], sdperm[4 * 3 * 64];
-  static uint8_t zz[4 * 64];
-  const int types[4] = {kDCT8, kDCT4X4, kDCT4X8, kDCT8X4};
-  for (int ti = 0; ti < 4; ti++) {
+hipError_t set_front_constants(const float lut[256], const float wts[5][3][64], hipStream_t s) {
+  static float wperm[kNT * 3 * 64], iwperm[kNT * 64], btab[256], sdperm[kNT * 3 * 64];
+  static uint8_t zz[kNT * 64];
+  const int types[kNT] = {kDCT8, kDCT4X4, kDCT4X8, kDCT8X4, kDCT2X2, kIDENTITY};
+  // quant kinds (host quant_weights): DCT8 0, DCT4 1, DCT4X8 2, IDENTITY 3, DCT2X2 4
+  const int qks[kNT] = {0, 1, 2, 2, 4, 3};
+  for (int ti = 0; ti < kNT; ti++) {
     const int T = types[ti];
-    const int qk = T == kDCT8 ? 0 : (T == kDCT4X4 ? 1 : 2);
+    const int qk = qks[ti];
     for (int r = 0; r < 8; r++)
       for (int k = 0; k < 8; k++) {
         const int co = co_index_rt(T, k, r);
         // area a coefficient's basis spans: the lowest-frequency combine slots
         // the whole block, other DCT4X4 coefficients a 4x4 sub-block, other
-        // DCT4X8 / DCT8X4 ones a 4x8 half (oracle jxo_frame_init)
+        // DCT4X8 / DCT8X4 ones a 4x8 half, DCT2X2 level-2 / level-1 ones a 4x4
+        // quarter / 2x2 cell, IDENTITY residuals one pixel (oracle
+        // jxo_frame_init)
         const int row = co >> 3, col = co & 7;
         int area = 64;
         if (ti == 1 && !(row < 2 && col < 2)) area = 16;
-        if (ti >= 2 && !(row < 2 && col == 0)) area = 32;
+        if ((ti == 2 || ti == 3) && !(row < 2 && col == 0)) area = 32;
+        if (ti == 4 && !(row < 2 && col < 2)) area = row < 4 && col < 4 ? 16 : 4;
+        if (ti == 5 && !(row < 2 && col < 2)) area = 1;
         for (int c = 0; c < 3; c++) {
           wperm[((ti * 3 + c) * 8 + r) * 8 + k] = wts[qk][c][co];
           sdperm[((ti * 3 + c) * 8 + r) * 8 + k] = dist_weight(c, area, wts[qk][c][co]);

@@ -224,7 +224,8 @@ static Frame make_frame(uint32_t w, uint32_t h, float distance) {
 }
 
 // default dequantization weights (inverse steps) [ext libjxl quant_weights.cc]
-static void quant_weights(float out[3][3][64]) {
+// kinds: 0 DCT8, 1 DCT4X4, 2 DCT4X8 / DCT8X4, 3 IDENTITY, 4 DCT2X2
+static void quant_weights(float out[5][3][64]) {
   static const double dct8[3][6] = {{3150.0, 0.0, -0.4, -0.4, -0.4, -2.0},
                                     {560.0, 0.0, -0.3, -0.3, -0.3, -0.3},
                                     {512.0, -2.0, -1.0, 0.0, -1.0, -2.0}};
@@ -270,6 +271,28 @@ static void quant_weights(float out[3][3][64]) {
   for (int c = 0; c < 3; c++)
     for (int y = 0; y < 8; y++)
       for (int x = 0; x < 8; x++) out[2][c][y * 8 + x] = (float)w[c * 64 + (y / 2) * 8 + x];
+  // IDENTITY: weight [0] everywhere, [1] at slots 1 / 8, [2] at slot 9;
+  // DCT2X2: [0] slots 1 / 8, [1] slot 9, level-2 quadrants [2] / [3]
+  // (off-diagonal / diagonal), level-1 quadrants [4] / [5]
+  // [ext quant_weights.cc kQuantModeID / kQuantModeDCT2 defaults; == oracle]
+  static const float id_w[3][3] = {{280.0f, 3160.0f, 3160.0f}, {60.0f, 864.0f, 864.0f},
+                                   {18.0f, 200.0f, 200.0f}};
+  static const float dct2_w[3][6] = {{3840.0f, 2560.0f, 1280.0f, 640.0f, 480.0f, 300.0f},
+                                     {960.0f, 640.0f, 320.0f, 180.0f, 140.0f, 120.0f},
+                                     {640.0f, 320.0f, 128.0f, 64.0f, 32.0f, 16.0f}};
+  for (int c = 0; c < 3; c++) {
+    for (int i = 0; i < 64; i++) out[3][c][i] = id_w[c][0];
+    out[3][c][1] = out[3][c][8] = id_w[c][1];
+    out[3][c][9] = id_w[c][2];
+    for (int y = 0; y < 8; y++)
+      for (int x = 0; x < 8; x++) {
+        int k;
+        if (y < 2 && x < 2) k = (y && x) ? 1 : 0;
+        else if (y < 4 && x < 4) k = (y >= 2 && x >= 2) ? 3 : 2;
+        else k = (y >= 4 && x >= 4) ? 5 : 4;
+        out[4][c][y * 8 + x] = dct2_w[c][k];
+      }
+  }
 }
 
 static void srgb_lut(float lut[256]) {
@@ -514,7 +537,7 @@ static jxg_status init_constants(Ctx* c) {
   std::lock_guard<std::mutex> lock(g_const_mu);
   float lut[256];
   srgb_lut(lut);
-  static float wts[3][3][64];
+  static float wts[5][3][64];
   quant_weights(wts);
   JXG_HIP(set_front_constants(lut, wts, c->stream));
   uint8_t tab[kAcCtx];

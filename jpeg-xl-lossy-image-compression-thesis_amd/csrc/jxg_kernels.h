@@ -187,7 +187,7 @@ inline float dist_weight(int c, int area, float w) {
   static const float kW0[3] = {3150.0f, 560.0f, 512.0f};
   return (float)(std::sqrt((double)area / 64.0) * ((double)kW0[c] / (double)w));
 }
-hipError_t set_front_constants(const float lut[256], const float wts[3][3][64], hipStream_t s);
+hipError_t set_front_constants(const float lut[256], const float wts[5][3][64], hipStream_t s);
 void launch_front(const FrontArgs& a, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s);
 void launch_front_list(const FrontArgs& a, uint32_t ntiles, hipStream_t s);
 // shard exchange: per-group block records (acs, qf, dc) <-> frame arrays

@@ -54,6 +54,36 @@ void jxo_quant_weights(int kind, float out[3][64]) {
       {2198.050556016380522, -0.96269623020744692, -0.76194253026666783, -0.6551140670773547},
       {764.3655248643528689, -0.92630200888366945, -0.9675229603596517, -0.27845290869168118},
       {527.107573587542228, -1.4594385811273854, -1.450082094097871593, -1.5843722511996204}};
+  /* IDENTITY: every slot weight [0], the DC-combination slots 1 / 8 weight
+   * [1], slot 9 weight [2]; DCT2X2: slots 1 / 8 [0], 9 [1], the level-2
+   * quadrants [2] (off-diagonal) / [3] (diagonal), the level-1 quadrants [4] /
+   * [5] [ext quant_weights.cc kQuantModeID / kQuantModeDCT2 defaults] */
+  static const float id_w[3][3] = {{280.0f, 3160.0f, 3160.0f},
+                                    {60.0f, 864.0f, 864.0f},
+                                    {18.0f, 200.0f, 200.0f}};
+  static const float dct2_w[3][6] = {{3840.0f, 2560.0f, 1280.0f, 640.0f, 480.0f, 300.0f},
+                                     {960.0f, 640.0f, 320.0f, 180.0f, 140.0f, 120.0f},
+                                     {640.0f, 320.0f, 128.0f, 64.0f, 32.0f, 16.0f}};
+  if (kind == JXO_QK_ID) {
+    for (int c = 0; c < 3; c++) {
+      for (int i = 0; i < 64; i++) out[c][i] = id_w[c][0];
+      out[c][1] = out[c][8] = id_w[c][1];
+      out[c][9] = id_w[c][2];
+    }
+    return;
+  }
+  if (kind == JXO_QK_DCT2) {
+    for (int c = 0; c < 3; c++)
+      for (int y = 0; y < 8; y++)
+        for (int x = 0; x < 8; x++) {
+          int k;
+          if (y < 2 && x < 2) k = (y && x) ? 1 : 0;
+          else if (y < 4 && x < 4) k = (y >= 2 && x >= 2) ? 3 : 2;
+          else k = (y >= 4 && x >= 4) ? 5 : 4;
+          out[c][y * 8 + x] = dct2_w[c][k];
+        }
+    return;
+  }
   double w[3][64];
   if (kind == JXO_QK_DCT8) {
     get_quant_weights(8, 8, dct8, 6, w);
@@ -160,19 +190,25 @@ void jxo_frame_init(jxo_frame* f, uint32_t w, uint32_t h, const jxo_params* p) {
     f->dc_mul[c] = (float)((double)G * (double)qdc / 65536.0 / m_lf[c]);
     f->dc_step[c] = (float)(65536.0 / (double)G / (double)qdc * m_lf[c]);
   }
-  for (int k = 0; k < 3; k++) jxo_quant_weights(k, f->wts[k]);
-  /* distortion weights per 8x8-class strategy (scan index DCT8, DCT4X4,
-   * DCT4X8, DCT8X4) and coefficient-layout position: the lowest-frequency
-   * combine slots span the whole block (area 64); other DCT4X4 coefficients
-   * span a 4x4 sub-block (16), DCT4X8 / DCT8X4 ones a 4x8 half (32) */
-  for (int ti = 0; ti < 4; ti++) {
-    const int qk = ti == 0 ? JXO_QK_DCT8 : (ti == 1 ? JXO_QK_DCT4 : JXO_QK_DCT4X8);
+  for (int k = 0; k < 5; k++) jxo_quant_weights(k, f->wts[k]);
+  /* distortion weights per 8x8-class strategy (table index DCT8, DCT4X4,
+   * DCT4X8, DCT8X4, DCT2X2, IDENTITY -- jxo_tindex) and coefficient-layout
+   * position: the lowest-frequency combine slots span the whole block (area
+   * 64); other DCT4X4 coefficients span a 4x4 sub-block (16), DCT4X8 / DCT8X4
+   * ones a 4x8 half (32); DCT2X2 level-2 coefficients a 4x4 quarter (16),
+   * level-1 ones a 2x2 cell (4); IDENTITY residuals one pixel (1) */
+  for (int ti = 0; ti < 6; ti++) {
+    static const int qks[6] = {JXO_QK_DCT8, JXO_QK_DCT4, JXO_QK_DCT4X8, JXO_QK_DCT4X8,
+                               JXO_QK_DCT2, JXO_QK_ID};
+    const int qk = qks[ti];
     for (int c = 0; c < 3; c++)
       for (int co = 0; co < 64; co++) {
         const int row = co >> 3, col = co & 7;
         int area = 64;
         if (ti == 1 && !(row < 2 && col < 2)) area = 16;
-        if (ti >= 2 && !(row < 2 && col == 0)) area = 32;
+        if ((ti == 2 || ti == 3) && !(row < 2 && col == 0)) area = 32;
+        if (ti == 4 && !(row < 2 && col < 2)) area = row < 4 && col < 4 ? 16 : 4;
+        if (ti == 5 && !(row < 2 && col < 2)) area = 1;
         f->sdw[ti][c][co] = jxo_dist_weight(c, area, f->wts[qk][c][co]);
       }
   }
@@ -261,6 +297,52 @@ void jxo_transform(int t, const float* px /* 8x8, stride 8 */, float* co) {
     float A = co[0], B = co[8];
     co[0] = (A + B) * 0.5f;
     co[8] = (A - B) * 0.5f;
+  } else if (t == JXO_DCT2X2) {
+    /* three levels of 2x2 Haar steps, 0.25 per level [ext enc_transforms-inl.h
+     * DCT2TopBlock<8, 4, 2>]: per 2x2 cell the row sums / differences
+     * a = c00 + c01, b = c00 - c01, then r00 = (a_top + a_bottom) / 4 ->
+     * (y, x), r01 = (a_top - a_bottom) / 4 -> (y, n + x), r10 = (b_top +
+     * b_bottom) / 4 -> (n + y, x), r11 = (b_top - b_bottom) / 4 -> (n + y,
+     * n + x), n = S / 2 */
+    for (int i = 0; i < 64; i++) co[i] = px[i];
+    for (int S = 8; S >= 2; S >>= 1) {
+      const int n = S / 2;
+      for (int i = 0; i < 64; i++) o[i] = co[i];
+      for (int y = 0; y < n; y++)
+        for (int x = 0; x < n; x++) {
+          const float c00 = o[(2 * y) * 8 + 2 * x], c01 = o[(2 * y) * 8 + 2 * x + 1];
+          const float c10 = o[(2 * y + 1) * 8 + 2 * x], c11 = o[(2 * y + 1) * 8 + 2 * x + 1];
+          const float at = c00 + c01, bt = c00 - c01, ab = c10 + c11, bb = c10 - c11;
+          co[y * 8 + x] = (at + ab) * 0.25f;
+          co[y * 8 + n + x] = (at - ab) * 0.25f;
+          co[(n + y) * 8 + x] = (bt + bb) * 0.25f;
+          co[(n + y) * 8 + n + x] = (bt - bb) * 0.25f;
+        }
+    }
+  } else if (t == JXO_IDENTITY) {
+    /* per 4x4 sub-block (y, x): residuals against its pixel (1, 1) in the
+     * interleaved slots (y + 2 iy, x + 2 ix); the (0, 0) residual moves to
+     * the slot of (1, 1); slot (y, x) holds the sub-block mean (row sums left
+     * to right, rows ((0 + 1) + (2 + 3)), / 16); the four means are then
+     * combined like DCT4X4's [ext enc_transforms-inl.h IDENTITY] */
+    for (int y = 0; y < 2; y++)
+      for (int x = 0; x < 2; x++) {
+        const float* sb = px + (4 * y) * 8 + 4 * x;
+        float rs[4];
+        for (int iy = 0; iy < 4; iy++)
+          rs[iy] = ((sb[iy * 8] + sb[iy * 8 + 1]) + sb[iy * 8 + 2]) + sb[iy * 8 + 3];
+        const float dc = ((rs[0] + rs[1]) + (rs[2] + rs[3])) * (1.0f / 16.0f);
+        const float p11 = sb[8 + 1];
+        for (int iy = 0; iy < 4; iy++)
+          for (int ix = 0; ix < 4; ix++) co[(y + 2 * iy) * 8 + x + 2 * ix] = sb[iy * 8 + ix] - p11;
+        co[(y + 2) * 8 + x + 2] = sb[0] - p11;
+        co[y * 8 + x] = dc;
+      }
+    float A = co[0], B = co[1], C = co[8], D = co[9];
+    co[0] = (((A + B) + C) + D) * 0.25f;
+    co[1] = (((A + B) - C) - D) * 0.25f;
+    co[8] = (((A - B) + C) - D) * 0.25f;
+    co[9] = (((A - B) - C) + D) * 0.25f;
   } else { /* JXO_DCT4X8: two 8-row x 4-col halves side by side, stored transposed */
     for (int sx = 0; sx < 2; sx++) {
       dct2d(px + sx * 4, 8, 4, o);
@@ -306,7 +388,20 @@ static inline int bitlen(uint32_t v) {
 }
 
 static int qkind(int t) {
+  if (t == JXO_IDENTITY) return JXO_QK_ID;
+  if (t == JXO_DCT2X2) return JXO_QK_DCT2;
   return t == JXO_DCT8 ? JXO_QK_DCT8 : (t == JXO_DCT4X4 ? JXO_QK_DCT4 : JXO_QK_DCT4X8);
+}
+/* table index of an 8x8-class strategy (distortion weights; GPU tables) */
+static int jxo_tindex(int t) {
+  switch (t) {
+    case JXO_DCT8: return 0;
+    case JXO_DCT4X4: return 1;
+    case JXO_DCT4X8: return 2;
+    case JXO_DCT8X4: return 3;
+    case JXO_DCT2X2: return 4;
+    default: return 5; /* JXO_IDENTITY */
+  }
 }
 
 /* Quantize one block under strategy t.  Channel order Y, X, B (Y first: X/B
@@ -318,6 +413,17 @@ static int qkind(int t) {
 static int co_index(int t, int p) {
   const int prow = p >> 3, pcol = p & 7;
   if (t == JXO_DCT8) return p;
+  /* IDENTITY / DCT2X2: GPU lane pcol holds one layout row (IDENTITY: pixel row
+   * pcol's residuals, pixel column prow -> slot column (prow >> 2) + 2 (prow &
+   * 3)); DCT2X2: lane pcol's k-th value after the three Haar levels (odd
+   * lanes: level-1 bottom rows; even lanes: level-1 top row (k >= 4) and the
+   * level-2 / level-3 outputs (k < 4)) */
+  if (t == JXO_IDENTITY) return ((pcol >> 2) + 2 * (pcol & 3)) * 8 + (prow >> 2) + 2 * (prow & 3);
+  if (t == JXO_DCT2X2) {
+    const int q = pcol >> 1;
+    const int row = (pcol & 1) ? 4 + q : (prow >= 4 ? q : ((q & 1) ? 2 + (q >> 1) : (q >> 1)));
+    return row * 8 + prow;
+  }
   if (t == JXO_DCT4X4)
     return ((prow >> 2) + 2 * (prow & 3)) * 8 + (pcol >> 2) + 2 * (pcol & 3);
   if (t == JXO_DCT8X4) return ((prow >> 2) + 2 * (prow & 3)) * 8 + pcol;
@@ -336,8 +442,7 @@ float jxo_quantize_block(const jxo_frame* f, int t, const float px[3][64],
   for (int c = 0; c < 3; c++) jxo_transform(t, px[c], co[c]);
   const int qk = qkind(t);
   const float inv_scale = 1.0f / scale;
-  const int ti = t == JXO_DCT8 ? 0 : (t == JXO_DCT4X4 ? 1 : (t == JXO_DCT4X8 ? 2 : 3));
-  const float(*sd)[64] = f->sdw[ti];
+  const float(*sd)[64] = f->sdw[jxo_tindex(t)];
   float yd[64];
   float part[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   int bits = 0;
@@ -371,7 +476,8 @@ float jxo_quantize_block(const jxo_frame* f, int t, const float px[3][64],
     if (q) q[c][0] = 0;
   }
   const float dist = tree8(part);
-  static const float tmul[14] = {1.0f, 0, 0, 1.05f, 0, 0, 0, 0, 0, 0, 0, 0, 1.02f, 1.02f};
+  static const float tmul[14] = {1.0f, JXO_TMUL_ID, JXO_TMUL_DCT2, 1.05f, 0, 0, 0, 0, 0, 0, 0, 0,
+                                 1.02f, 1.02f};
   return ((float)bits + 8.0f * dist) * tmul[t];
 }
 
@@ -434,8 +540,11 @@ int jxo_front_block(const jxo_frame* f, const float px[3][64], const float* homo
 
   /* AC strategy search over the 8x8-class candidates [ext
    * FindBest8x8Transform], hook F on every estimate, hook P on a DCT8 win */
-  static const int cand[4] = {JXO_DCT8, JXO_DCT4X4, JXO_DCT4X8, JXO_DCT8X4};
-  const int ncand = f->effort >= 5 ? 4 : 1;
+  /* scan order of libjxl's kTransforms8x8 (DCT, DCT4X4, DCT2X2, DCT4X8,
+   * DCT8X4, IDENTITY; AFV0-3 not searched) */
+  static const int cand[6] = {JXO_DCT8, JXO_DCT4X4, JXO_DCT2X2, JXO_DCT4X8, JXO_DCT8X4,
+                              JXO_IDENTITY};
+  const int ncand = f->effort >= 5 ? 6 : 1;
   int best_t = JXO_DCT8;
   float best = FLT_MAX;
   if (ncand > 1) {

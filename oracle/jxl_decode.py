@@ -696,7 +696,26 @@ def default_dequant():
         for x in range(8):
             k4[:, y * 8 + x] = w4[:, (y // 2) * 4 + x // 2]
             k48[:, y * 8 + x] = w48[:, (y // 2) * 8 + x]
-    return {0: 1.0 / w8, 3: 1.0 / k4, 12: 1.0 / k48, 13: 1.0 / k48}
+    # IDENTITY / DCT2X2 [ext quant_weights.cc kQuantModeID / kQuantModeDCT2 defaults]
+    idw = [[280.0, 3160.0, 3160.0], [60.0, 864.0, 864.0], [18.0, 200.0, 200.0]]
+    d2w = [[3840.0, 2560.0, 1280.0, 640.0, 480.0, 300.0], [960.0, 640.0, 320.0, 180.0, 140.0, 120.0],
+           [640.0, 320.0, 128.0, 64.0, 32.0, 16.0]]
+    kid = np.zeros((3, 64))
+    kd2 = np.zeros((3, 64))
+    for c in range(3):
+        kid[c, :] = idw[c][0]
+        kid[c, 1] = kid[c, 8] = idw[c][1]
+        kid[c, 9] = idw[c][2]
+        for y in range(8):
+            for x in range(8):
+                if y < 2 and x < 2:
+                    k = 1 if (y and x) else 0
+                elif y < 4 and x < 4:
+                    k = 3 if (y >= 2 and x >= 2) else 2
+                else:
+                    k = 5 if (y >= 4 and x >= 4) else 4
+                kd2[c, y * 8 + x] = d2w[c][k]
+    return {0: 1.0 / w8, 1: 1.0 / kid, 2: 1.0 / kd2, 3: 1.0 / k4, 12: 1.0 / k48, 13: 1.0 / k48}
 
 
 def _idct_mat(n):
@@ -815,6 +834,33 @@ def inverse_transform(t, co):
     if t == 0:
         return _I8 @ c @ _I8.T
     out = np.zeros((8, 8))
+    if t == 2:  # DCT2X2: inverse 2x2 Haar steps, S = 2, 4, 8 [ext IDCT2TopBlock]
+        cur = c.copy()
+        for S in (2, 4, 8):
+            n = S // 2
+            nxt = cur.copy()
+            for y in range(n):
+                for x in range(n):
+                    c00, c01 = cur[y, x], cur[y, n + x]
+                    c10, c11 = cur[n + y, x], cur[n + y, n + x]
+                    nxt[2 * y, 2 * x] = c00 + c01 + c10 + c11
+                    nxt[2 * y, 2 * x + 1] = c00 + c01 - c10 - c11
+                    nxt[2 * y + 1, 2 * x] = c00 - c01 + c10 - c11
+                    nxt[2 * y + 1, 2 * x + 1] = c00 - c01 - c10 + c11
+            cur = nxt
+        return cur
+    if t == 1:  # IDENTITY [ext dec_transforms IDENTITY]
+        A, B, C, D = c[0, 0], c[0, 1], c[1, 0], c[1, 1]
+        dcs = [A + B + C + D, A + B - C - D, A - B + C - D, A - B - C + D]
+        for sy in range(2):
+            for sx in range(2):
+                res = np.array([[c[sy + 2 * iy, sx + 2 * ix] for ix in range(4)] for iy in range(4)])
+                p11 = dcs[sy * 2 + sx] - (res.sum() - res[0, 0]) / 16.0
+                blk = res + p11
+                blk[1, 1] = p11
+                blk[0, 0] = res[1, 1] + p11
+                out[4 * sy:4 * sy + 4, 4 * sx:4 * sx + 4] = blk
+        return out
     if t == 3:
         A, B, C, D = c[0, 0], c[0, 1], c[1, 0], c[1, 1]
         dcs = [A + B + C + D, A + B - C - D, A - B + C - D, A - B - C + D]
@@ -1004,7 +1050,7 @@ def decode(data: bytes, want_pixels: bool = True) -> Decoded:
                 if k >= count:
                     raise JxlError("too few varblocks")
                 t = meta[2][0][k]
-                if t not in (0, 3, 12, 13) and t not in SHAPES:
+                if t not in (0, 1, 2, 3, 12, 13) and t not in SHAPES:
                     raise JxlError("AC strategy %d not produced" % t)
                 cy, cx = SHAPES[t][:2] if t in SHAPES else (1, 1)
                 if y + cy > bh or x + cx > bw or covered[y:y + cy, x:x + cx].any():

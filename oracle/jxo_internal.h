@@ -36,11 +36,19 @@ typedef struct {
   float qf_base, inv_g;
   uint32_t G, qdc;
   float dc_mul[3], dc_step[3];
-  float wts[3][3][64]; /* [quant kind][channel X,Y,B][coef] */
-  float sdw[4][3][64];  /* [8x8-class strategy index][channel][coef] distortion weights */
+  float wts[5][3][64]; /* [quant kind][channel X,Y,B][coef] */
+  float sdw[6][3][64];  /* [8x8-class strategy index][channel][coef] distortion weights */
 } jxo_frame;
 
-enum { JXO_QK_DCT8 = 0, JXO_QK_DCT4 = 1, JXO_QK_DCT4X8 = 2 };
+/* estimate multipliers of the two Haar-type 8x8 candidates (the search's
+ * (bits + 8 dist) * tmul; DCT8 1.0, DCT4X4 1.05, DCT4X8 / DCT8X4 1.02) */
+#ifndef JXO_TMUL_DCT2
+#define JXO_TMUL_DCT2 1.05f
+#endif
+#ifndef JXO_TMUL_ID
+#define JXO_TMUL_ID 1.08f
+#endif
+enum { JXO_QK_DCT8 = 0, JXO_QK_DCT4 = 1, JXO_QK_DCT4X8 = 2, JXO_QK_ID = 3, JXO_QK_DCT2 = 4 };
 
 void jxo_frame_init(jxo_frame* f, uint32_t w, uint32_t h, const jxo_params* p);
 void jxo_quant_weights(int kind, float out[3][64]);
