@@ -399,9 +399,11 @@ static MergeTables build_merge_tables() {
       }
     }
   }
-  // per-shape pixel-orientation copies, column-major ([kx * R + ky]; tall
-  // shapes read the stored table transposed) -- a quantization lane owns a
-  // column chunk of consecutive ky: 16-byte loads
+  // per-shape pixel-orientation copies, row-major ([ky * C + kx]; tall shapes
+  // read the stored table transposed) -- the lanes of a quantization pass are
+  // consecutive columns kx, so each of a lane's per-row loads is one coalesced
+  // 256-byte wave access (per-lane 16-byte column chunks touched 64 cache
+  // lines per load and cost merge_eval ~13 % in address processing)
   {
     static const int kShapeDims[kNumShapes][3] = {{2, 1, 0}, {1, 2, 0}, {2, 2, 1}, {4, 2, 2}, {2, 4, 2},
                                                  {4, 4, 3}, {8, 4, 4}, {4, 8, 4}, {8, 8, 5}};
@@ -414,7 +416,7 @@ static MergeTables build_merge_tables() {
       for (int ky = 0; ky < R; ky++)
         for (int kx = 0; kx < C; kx++) {
           const int si = cx >= cy ? ky * C + kx : kx * R + ky;
-          const int pi = kShapeOff[sh] + kx * R + ky;
+          const int pi = kShapeOff[sh] + ky * C + kx;
           // LLF positions (the first cy x cx): weight 0, so they quantize to 0
           // and add nothing without a per-coefficient test in the kernels
           const bool llf = ky < cy && kx < cx;
@@ -1609,33 +1611,65 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
 // each), driven by the caller's one host thread.  submit(j):
 //   finish the oldest frame if D are in flight (wait for its emission,
 //   assemble, codestream to the host) -> launch frame j's front end, merge
-//   stage and statistics on a free lane -> build frame j-1's codes and launch
-//   its emission.
+//   stage and statistics on a free lane; frame j-1's codes (host work:
+//   clustering, ANS / prefix tables, headers, LF-group codes) start on a
+//   helper thread, and the codes of frame j-lag are joined (its emission is
+//   launched by then).
 // So the rANS chains of the D - 2 frames before j (latency-bound waves that use
 // little of their SIMDs; 68 KB of LDS per CU) run while frame j's transform
 // kernels fill the rest of the chip.  A frame's chain lasts as long as its
 // longest pass group's, whatever the frame size, so the depth follows the
 // frame: D = 4 from ~500 pass groups up (8K: more frames in flight only add
 // contention), up to kPipeMaxLanes for small frames (a 1080p
-// frame has 40 groups: 40 chain waves on a 1024-SIMD chip).  Every lane needs
-// its own hardware queue (GPU_MAX_HW_QUEUES > D, bench.py sets 16).
+// frame has 40 groups: 40 chain waves on a 1024-SIMD chip).  The lag follows
+// it too: 1 for large frames (the codes of j-1 are joined in submit(j): the
+// GPU is the bound), 3 for small ones, whose host work per frame (0.5 ms of
+// ANS codes, 0.6 ms of launches and assembly) is the bound: three helpers run
+// at once and each has two submit periods (64 x 1080p ANS: lag 1 2.2, lag 2
+// 2.5, lag 3 2.7 GPix/s).  Every lane needs its own
+// hardware queue (GPU_MAX_HW_QUEUES > D, bench.py sets 16).
 // ---------------------------------------------------------------------------
-#ifndef JXG_PIPE_LAG  // (experiment builds override them: tools/build_variant.sh)
-#define JXG_PIPE_LAG 1
+#ifndef JXG_PIPE_MAX_LANES  // (experiment builds override them: tools/build_variant.sh)
 #define JXG_PIPE_MAX_LANES 12
 #endif
+#ifndef JXG_PIPE_LAG_SMALL
+#define JXG_PIPE_LAG_SMALL 3
+#endif
 constexpr uint32_t kPipeMaxLanes = JXG_PIPE_MAX_LANES;
-constexpr uint32_t kPipeLag = JXG_PIPE_LAG;  // submit(j) builds the codes of frame j - lag
 static uint32_t pipe_depth(uint32_t ngroups) {
   const uint32_t d = (2048 + ngroups - 1) / std::max(1u, ngroups);
   return std::min(kPipeMaxLanes, std::max(4u, d));
 }
+static uint32_t pipe_lag(uint32_t ngroups) { return ngroups >= 256 ? 1u : (uint32_t)JXG_PIPE_LAG_SMALL; }
+// JXG_PIPE_PROFILE (experiment builds only): host time per pipeline step,
+// printed by jxg_destroy of the owning context
+#ifdef JXG_PIPE_PROFILE
+struct PipeProf {
+  double complete = 0, finish_wait = 0, launch = 0, join = 0, codes = 0, submit = 0;
+  uint64_t n = 0;
+};
+static PipeProf g_pprof;
+#define PPROF_ADD(field, t0) (g_pprof.field += ms_since(t0))
+#else
+#define PPROF_ADD(field, t0) ((void)0)
+#endif
 struct PipeFrame {
   Ctx* lane = nullptr;
   Job J;
   int phase = 1;  // 1: statistics launched; 2: emission launched
   Clock::time_point t0;
+  std::future<jxg_status> codes;  // valid while a helper builds the codes
 };
+// the helper's codes of a frame -> phase 2 (on an error the caller aborts)
+static jxg_status pipe_join_codes(PipeFrame& fr) {
+  if (!fr.codes.valid()) return JXG_OK;
+  const jxg_status st = fr.codes.get();
+  fr.phase = 2;
+#ifdef JXG_PIPE_PROFILE
+  g_pprof.codes += fr.J.ms_codes;
+#endif
+  return st;
+}
 struct PipeDone {
   jxg_buffer buf;
   jxg_stats stats;
@@ -1656,9 +1690,11 @@ static jxg_status ensure_lanes(Ctx* c, uint32_t extra) {
   return JXG_OK;
 }
 
-// drop every frame in flight (after an error): wait for the lanes' streams
+// drop every frame in flight (after an error): wait for the helpers and the
+// lanes' streams
 static void pipe_abort(Ctx* c) {
   Pipe& p = *c->pipe;
+  for (auto& fr : p.inflight) (void)pipe_join_codes(*fr);
   for (auto& fr : p.inflight) (void)hipStreamSynchronize(fr->lane->stream);
   p.inflight.clear();
 }
@@ -1667,9 +1703,16 @@ static void pipe_abort(Ctx* c) {
 static jxg_status pipe_complete_oldest(Ctx* c) {
   Pipe& p = *c->pipe;
   PipeFrame& fr = *p.inflight.front();
-  jxg_status st = JXG_OK;
-  if (fr.phase == 1) st = enc_codes(fr.lane, fr.J, false);
+  jxg_status st = pipe_join_codes(fr);
+  if (!st && fr.phase == 1) st = enc_codes(fr.lane, fr.J, false);
   PipeDone d{{nullptr, 0}, {}};
+#ifdef JXG_PIPE_PROFILE
+  if (!st) {
+    const Clock::time_point tw = Clock::now();
+    (void)hipStreamSynchronize(fr.lane->stream);
+    PPROF_ADD(finish_wait, tw);
+  }
+#endif
   if (!st) st = enc_finish(fr.lane, fr.J, false, &d.buf, fr.t0);
   if (st) return st;
   d.stats = fr.lane->stats;
@@ -1683,39 +1726,33 @@ static jxg_status pipe_submit(Ctx* c, const uint8_t* src, bool on_device, uint32
   if (!c->pipe) c->pipe.reset(new (std::nothrow) Pipe());
   if (!c->pipe) return JXG_ERR_OOM;
   Pipe& p = *c->pipe;
-  const uint32_t depth = pipe_depth(make_frame(w, h, c->params.distance).ngroups);
+  const uint32_t ngroups = make_frame(w, h, c->params.distance).ngroups;
+  const uint32_t depth = pipe_depth(ngroups), lag = pipe_lag(ngroups);
   jxg_status st = ensure_lanes(c, depth - 1);
   if (st) return st;
   const Clock::time_point t0 = Clock::now();
-  // frame j - lag's codes (host work: clustering, ANS / prefix tables,
-  // headers, LF-group codes; ~0.4-1 ms whatever the frame size) on a helper
-  // thread, while this thread finishes the oldest frame and launches frame j
-  // on other lanes
-  PipeFrame* prev = p.inflight.size() >= kPipeLag ? p.inflight[p.inflight.size() - kPipeLag].get()
-                                                  : nullptr;
-  if (prev && prev->phase != 1) prev = nullptr;
-  std::future<jxg_status> codes;
-  if (prev) {
-    const int dev = c->params.device;
-    codes = std::async(std::launch::async, [prev, dev]() {
-      if (hipSetDevice(dev) != hipSuccess) return JXG_ERR_HIP;
-      return enc_codes(prev->lane, prev->J, false);
-    });
+  // the newest frame's codes on a helper thread, while this thread finishes
+  // the oldest frame and launches frame j on another lane
+  if (!p.inflight.empty()) {
+    PipeFrame* prev = p.inflight.back().get();
+    if (prev->phase == 1 && !prev->codes.valid()) {
+      const int dev = c->params.device;
+      prev->codes = std::async(std::launch::async, [prev, dev]() {
+        if (hipSetDevice(dev) != hipSuccess) return JXG_ERR_HIP;
+        return enc_codes(prev->lane, prev->J, false);
+      });
+    }
   }
-  auto join_codes = [&]() -> jxg_status {
-    if (!prev) return JXG_OK;
-    const jxg_status s2 = codes.get();
-    prev->phase = 2;
-    prev = nullptr;
-    return s2;
-  };
   auto fail = [&](jxg_status e) {
-    (void)join_codes();
     pipe_abort(c);
     return e;
   };
+#ifdef JXG_PIPE_PROFILE
+  const Clock::time_point tc = Clock::now();
+#endif
   while (p.inflight.size() >= depth)
     if ((st = pipe_complete_oldest(c))) return fail(st);
+  PPROF_ADD(complete, tc);
   // a lane no frame in flight uses (the lowest index)
   Ctx* L = nullptr;
   for (uint32_t li = 0; li < depth && !L; li++) {
@@ -1740,16 +1777,27 @@ static jxg_status pipe_submit(Ctx* c, const uint8_t* src, bool on_device, uint32
       return fail(JXG_ERR_HIP);
     src = L->rgb.p;
   }
+#ifdef JXG_PIPE_PROFILE
+  const Clock::time_point tl = Clock::now();
+#endif
   if ((st = enc_launch(L, fr->J, src, w, h, stride))) {
     (void)hipStreamSynchronize(L->stream);
     return fail(st);
   }
+  PPROF_ADD(launch, tl);
   p.inflight.push_back(std::move(fr));
   p.submitted++;
-  if ((st = join_codes())) {  // frame j - lag: codes built, emission launched
-    pipe_abort(c);
-    return st;
-  }
+  // frame j - lag: codes built, emission launched
+#ifdef JXG_PIPE_PROFILE
+  const Clock::time_point tj = Clock::now();
+#endif
+  if (p.inflight.size() > lag && (st = pipe_join_codes(*p.inflight[p.inflight.size() - 1 - lag])))
+    return fail(st);
+#ifdef JXG_PIPE_PROFILE
+  PPROF_ADD(join, tj);
+  PPROF_ADD(submit, t0);
+  g_pprof.n++;
+#endif
   return JXG_OK;
 }
 
@@ -2276,6 +2324,17 @@ void jxg_destroy(void* ctx) {
   g_live_ctx--;
 #ifdef JXG_MERGE_PROFILE
   dump_merge_profile();
+#endif
+#ifdef JXG_PIPE_PROFILE
+  if (g_pprof.n && !c->lanes.size()) {
+    const double n = (double)g_pprof.n;
+    std::fprintf(stderr,
+                 "pipe profile (ms per submit, %llu submits): submit %.3f = complete %.3f "
+                 "(of which GPU wait %.3f) + launch %.3f + join %.3f; codes (helper) %.3f\n",
+                 (unsigned long long)g_pprof.n, g_pprof.submit / n, g_pprof.complete / n,
+                 g_pprof.finish_wait / n, g_pprof.launch / n, g_pprof.join / n, g_pprof.codes / n);
+    g_pprof = PipeProf{};
+  }
 #endif
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);

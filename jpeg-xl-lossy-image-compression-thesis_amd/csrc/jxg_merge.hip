@@ -33,6 +33,7 @@
 #include <float.h>
 
 #include <cstdio>
+#include <type_traits>
 
 #include "jxg_device.h"
 #include "jxg_kernels.h"
@@ -264,15 +265,26 @@ __device__ void row_pass(const MergeArgs& a, const Pass& P, MergeLds& S) {
       });
     }
   } else {
-    // thread: row pairs (r, r + 256) -- two rows per transform (f2 lanes)
+    // thread: row pairs (r, r + 256) -- two rows per transform (f2 lanes).
+    // Row r of a channel: the varblock column is the fastest index, so the
+    // lanes of a wave read whole 256-byte tile rows (coalesced) instead of
+    // one C-float chunk per cache line
     constexpr int PER = (3 * 4096 / C + kMThreads - 1) / kMThreads;  // 6, 3, 2
     const int nrows = 3 * P.NV() * R;
+    const int lgx = P.lGX();
+    auto row_of = [&](int rr, int& c, int& v, int& y) {
+      c = rr >> lvr;
+      const int i = rr & ((1 << lvr) - 1);
+      y = (i >> lgx) & (R - 1);
+      v = ((i >> (lgx + P.lR())) << lgx) | (i & ((1 << lgx) - 1));
+    };
     float buf[PER][C];
 #pragma unroll
     for (int k = 0; k < PER; k++) {
       const int r = threadIdx.x + k * kMThreads;
       if (r < nrows) {
-        const int c = r >> lvr, v = (r >> P.lR()) & (P.NV() - 1), y = r & (R - 1);
+        int c, v, y;
+        row_of(r, c, v, y);
         load_row<C>(tsrc + c * 4096 + (P.by0(v) * 8 + y) * 64 + P.bx0(v) * 8, buf[k]);
       } else {
 #pragma unroll
@@ -284,8 +296,9 @@ __device__ void row_pass(const MergeArgs& a, const Pass& P, MergeLds& S) {
     for (int k = 0; k < PER; k += 2) {
       const int r0 = threadIdx.x + k * kMThreads, r1 = r0 + kMThreads;
       if (r0 >= nrows) continue;
-      const int c0 = r0 >> lvr, v0 = (r0 >> P.lR()) & (P.NV() - 1), y0 = r0 & (R - 1);
-      const int c1 = r1 >> lvr, v1 = (r1 >> P.lR()) & (P.NV() - 1), y1 = r1 & (R - 1);
+      int c0, v0, y0, c1, v1, y1;
+      row_of(r0, c0, v0, y0);
+      row_of(r1, c1, v1, y1);
       const bool ok0 = S.valid[v0], ok1 = k + 1 < PER && r1 < nrows && S.valid[v1];
       if (!ok0 && !ok1) continue;
       if (k + 1 < PER) {
@@ -395,10 +408,35 @@ __device__ __forceinline__ void load_f(const float* p, float* d) {
     d[4 * i + 3] = v.w;
   }
 }
+// A thread's quantization tables for one channel: its NIT items' weights,
+// distortion weights and (Y) inverse weights.  They are loaded before the
+// barrier that precedes the channel's pass (load_qtab), so their L2 latency
+// overlaps the barrier wait (-1 % measured; a build without any table loads
+// ran 13 % faster, so the loads' issue, not their latency, is what costs).
+template <int RPC>
+struct QTab {
+  static constexpr int NIT = RPC == 8 ? 2 : 1;  // items per thread: 512 or 256 / 256
+  float w[NIT][RPC], sd[NIT][RPC], iw[NIT][RPC];
+};
 template <int RPC, bool WRITE, int CH>
-__device__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S) {
+__device__ __forceinline__ void load_qtab(const MergeArgs& a, const Pass& P, QTab<RPC>& T) {
   constexpr int STOT = kShapeOff[kNumShapes];
-  constexpr int lper = RPC == 8 ? 9 : 8;  // items per channel: 512 (R = 8) or 256
+#pragma unroll
+  for (int it = 0; it < QTab<RPC>::NIT; it++) {
+    const int j = threadIdx.x + it * kMThreads;
+    const int ch = j >> (P.lNV() + P.lC()), x = j & (P.C() - 1);
+    const int t0 = P.soff + ch * RPC * P.C() + x;  // row ch * RPC, column x (row-major)
+#pragma unroll
+    for (int kk = 0; kk < RPC; kk++) {
+      const int ti = t0 + kk * P.C();
+      T.w[it][kk] = a.wk[(size_t)CH * STOT + ti];
+      if (!WRITE) T.sd[it][kk] = a.sdk[(size_t)CH * STOT + ti];
+      if (CH == 1) T.iw[it][kk] = a.iwy[ti];
+    }
+  }
+}
+template <int RPC, bool WRITE, int CH>
+__device__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S, const QTab<RPC>& T) {
   constexpr int cidx = CH == 1 ? 0 : (CH == 0 ? 1 : 2);  // 0 Y, 1 X, 2 B
   constexpr float kBias1 = 1.0f - 0.07005449891748593f;
   const int C = P.C(), NV = P.NV();
@@ -408,32 +446,27 @@ __device__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S) {
     const float f = (float)a.cmap[(CH == 0 ? 0u : a.ntiles_all) + (uint32_t)P.tile];
     kc = CH == 0 ? f * (1.0f / 84.0f) : 1.0f + f * (1.0f / 84.0f);
   }
-  for (int j = threadIdx.x; j < (1 << lper); j += kMThreads) {
+#pragma unroll
+  for (int it = 0; it < QTab<RPC>::NIT; it++) {
+    const int j = threadIdx.x + it * kMThreads;
     const int ch = j >> (P.lNV() + P.lC()), v = (j >> P.lC()) & (NV - 1), x = j & (C - 1);
     if (!S.valid[v]) continue;  // the varblock's C lanes leave together
     const int bx0 = P.bx0(v), by0 = P.by0(v);
     const float scale = (float)a.G * (float)S.vraw[v] / 65536.0f;
     float* cplane = S.co + P.off(v, CH) + x;
     const float* yd = S.co + P.off(v, 1) + x;
-    const int tcol = P.soff + x * P.R() + ch * RPC;  // column chunk in the tables
-    float w[RPC], iw[RPC], sd[RPC];
-    load_f<RPC>(a.wk + (size_t)CH * STOT + tcol, w);
-    if (!WRITE) load_f<RPC>(a.sdk + (size_t)CH * STOT + tcol, sd);
+    const float* w = T.w[it];
+    const float* sd = T.sd[it];
+    float iw[RPC];
     if (CH == 1) {
-      load_f<RPC>(a.iwy + tcol, iw);
       const float inv_scale = 1.0f / scale;
 #pragma unroll
-      for (int kk = 0; kk < RPC; kk++) iw[kk] = iw[kk] * inv_scale;
+      for (int kk = 0; kk < RPC; kk++) iw[kk] = T.iw[it][kk] * inv_scale;
     }
     uint16_t nat[RPC];
     if (WRITE) {
 #pragma unroll
-      for (int q = 0; q < RPC / 8; q++) {
-        const uint4 u = reinterpret_cast<const uint4*>(a.nat + tcol)[q];
-        const uint32_t uw[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-        for (int e = 0; e < 8; e++) nat[8 * q + e] = (uint16_t)(uw[e >> 1] >> ((e & 1) * 16));
-      }
+      for (int kk = 0; kk < RPC; kk++) nat[kk] = a.nat[P.soff + (ch * RPC + kk) * C + x];
     }
     // the LLF (first cy rows x cx columns) only occurs in chunk 0
     const bool llf_col = ch == 0 && x < P.cx();
@@ -524,20 +557,27 @@ __device__ void transform_quant(const MergeArgs& a, const Pass& P, MergeLds& S) 
     case 2: col_pass<32>(P, S); break;
     default: col_pass<64>(P, S); break;
   }
-  __syncthreads();
-  MPROF_MARK(2);
-  // Y first: its dequantized values replace its coefficients (B residual)
-  if (P.lcy == 0) quant_pass<8, WRITE, 1>(a, P, S);
-  else quant_pass<16, WRITE, 1>(a, P, S);
-  __syncthreads();
-  MPROF_MARK(3);
-  if (P.lcy == 0) {
-    quant_pass<8, WRITE, 0>(a, P, S);
-    quant_pass<8, WRITE, 2>(a, P, S);
-  } else {
-    quant_pass<16, WRITE, 0>(a, P, S);
-    quant_pass<16, WRITE, 2>(a, P, S);
-  }
+  // Y first: its dequantized values replace its coefficients (X / B
+  // residuals); every pass's tables are in flight across the barrier before it
+  auto quant3 = [&](auto rpc_tag) {
+    constexpr int RPC = decltype(rpc_tag)::value;
+    {
+      QTab<RPC> ty;
+      load_qtab<RPC, WRITE, 1>(a, P, ty);
+      __syncthreads();
+      MPROF_MARK(2);
+      quant_pass<RPC, WRITE, 1>(a, P, S, ty);
+    }
+    QTab<RPC> tx, tb;
+    load_qtab<RPC, WRITE, 0>(a, P, tx);
+    load_qtab<RPC, WRITE, 2>(a, P, tb);
+    __syncthreads();
+    MPROF_MARK(3);
+    quant_pass<RPC, WRITE, 0>(a, P, S, tx);
+    quant_pass<RPC, WRITE, 2>(a, P, S, tb);
+  };
+  if (P.lcy == 0) quant3(std::integral_constant<int, 8>());
+  else quant3(std::integral_constant<int, 16>());
   __syncthreads();
   MPROF_MARK(4);
 }

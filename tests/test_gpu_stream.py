@@ -68,3 +68,24 @@ def test_stream_device_8k_ans_matches_oracle(jxg_mod):
     for data in outs:
         assert hashlib.sha256(data).hexdigest() == g["sha256"]
     assert st["bytes"] == g["bytes"]
+
+
+def test_stream_many_small_frames_ans(jxg_mod):
+    """Small frames run the deepest pipeline (12 lanes, codes joined three
+    submits later, three helpers at once): 30 frames, receives only once more
+    than 14 are pending, so lanes are recycled by submit itself."""
+    from jxg.synth import natural_rgb8, synth_rgb8
+
+    frames = [(natural_rgb8 if i % 3 == 0 else synth_rgb8)(320 + 16 * (i % 5), 240 + 8 * (i % 4), 300 + i)
+              for i in range(30)]
+    with jxg_mod.Encoder(distance=1.0, effort=7, flags=jxg_mod.FLAG_ANS) as enc:
+        want = [enc.encode(f) for f in frames]
+    with jxg_mod.Encoder(distance=1.0, effort=7, flags=jxg_mod.FLAG_ANS) as enc:
+        got = []
+        for f in frames:
+            enc.submit(f)
+            while enc.pending() > 14:
+                got.append(enc.receive())
+        while enc.pending():
+            got.append(enc.receive())
+    assert got == want
