@@ -473,50 +473,63 @@ __device__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S, const
     float cp = 0.0f;
     uint32_t ebits = 0;
     int nzc = 0;
+    // rows in pairs: the float multiplies / adds of the two rows are one
+    // packed op each (f2, no contraction: each half is the scalar op order);
+    // the distortion chain stays in row order
 #pragma unroll
-    for (int kk = 0; kk < RPC; kk++) {
+    for (int kk = 0; kk < RPC; kk += 2) {
       const int ky = ch * RPC + kk;
-      const bool is_llf = llf_col && kk < P.cy();
-      const float coef_v = cplane[ky * kMS];
-      if (WRITE && is_llf) llf_at(S, CH, (by0 + ky) * 8 + bx0 + x) = coef_v;
-      float rv = coef_v;
-      if (CH != 1) rv = rv - kc * yd[ky * kMS];
+      const f2 coef = f2{cplane[ky * kMS], cplane[(ky + 1) * kMS]};
+      if (WRITE && llf_col) {
+        if (kk < P.cy()) llf_at(S, CH, (by0 + ky) * 8 + bx0 + x) = coef.x;
+        if (kk + 1 < P.cy()) llf_at(S, CH, (by0 + ky + 1) * 8 + bx0 + x) = coef.y;
+      }
+      f2 rv = coef;
+      if (CH != 1) rv = rv - f2{kc, kc} * f2{yd[ky * kMS], yd[(ky + 1) * kMS]};
       // LLF positions carry weight 0 (host tables): vq = +-0 quantizes to 0
       // and contributes nothing
-      const float vq = rv * (w[kk] * scale);
-      const float av = fabsf(vq);
-      // qa = (int)(min(av, 32767) + 0.5) as an integer-valued float (the
-      // truncation of a positive value is its floor): no conversions needed
-      // for the error and the rate
-      const float qf = av < 0.58f ? 0.0f : floorf(fminf(av, 32767.0f) + 0.5f);
-      if (CH == 1) {
-        const int qa = (int)qf;
-        float bq = S.btab[min(qa, 255)];
-        if (__builtin_expect(__any(qa >= 256), 0)) {
-          if (qa >= 256) bq = 0.145f / qf;
+      const f2 vq = rv * (f2{w[kk], w[kk + 1]} * f2{scale, scale});
+      float avs[2], qfs[2];
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const float vqh = h ? vq.y : vq.x;
+        const float av = fabsf(vqh);
+        // qa = (int)(min(av, 32767) + 0.5) as an integer-valued float (the
+        // truncation of a positive value is its floor): no conversions
+        // needed for the error and the rate
+        const float qf = av < 0.58f ? 0.0f : floorf(fminf(av, 32767.0f) + 0.5f);
+        avs[h] = av;
+        qfs[h] = qf;
+        if (CH == 1) {
+          const int qa = (int)qf;
+          float bq = S.btab[min(qa, 255)];
+          if (__builtin_expect(__any(qa >= 256), 0)) {
+            if (qa >= 256) bq = 0.145f / qf;
+          }
+          float adj = qa == 0 ? 0.0f : (qa == 1 ? kBias1 : qf - bq);
+          if (vqh < 0.0f) adj = -adj;
+          cplane[(ky + h) * kMS] = adj * iw[kk + h];  // LLF: 0 (its value lives in llf_at)
         }
-        float adj = qa == 0 ? 0.0f : (qa == 1 ? kBias1 : qf - bq);
-        if (vq < 0.0f) adj = -adj;
-        cplane[ky * kMS] = adj * iw[kk];  // LLF: 0 (its value lives in llf_at)
+        // 2 + 2 bitlen(qa) per non-zero = 2 E - 250, E = biased exponent of
+        // qf (qf = 0 has E = 0 and is not counted in nzc)
+        ebits += __float_as_uint(qf) >> 23;
+        nzc += qf != 0.0f;
+        if (WRITE) {
+          const int qa = (int)qf;
+          const int qq = vqh < 0.0f ? -qa : qa;
+          const int p = nat[kk + h];
+          const int sl = p >> 6;
+          const int lbx = bx0 + (sl & (P.cx() - 1)), lby = by0 + (sl >> P.lcx);
+          const size_t gb = (size_t)(P.ty * 8 + lby) * a.bxs + P.tx * 8 + lbx;
+          a.ac[(gb * 3 + CH) * 64 + (p & 63)] = (int16_t)qq;
+        }
       }
       // error in steps times the distortion weight (oracle jxo_dist_weight);
       // the write pass needs no estimate
       if (!WRITE) {
-        const float e = (av - qf) * sd[kk];
-        cp = fmaf(e, e, cp);
-      }
-      // 2 + 2 bitlen(qa) per non-zero = 2 E - 250, E = biased exponent of qf
-      // (qf = 0 has E = 0 and is not counted in nzc)
-      ebits += __float_as_uint(qf) >> 23;
-      nzc += qf != 0.0f;
-      if (WRITE) {
-        const int qa = (int)qf;
-        const int qq = vq < 0.0f ? -qa : qa;
-        const int p = nat[kk];
-        const int sl = p >> 6;
-        const int lbx = bx0 + (sl & (P.cx() - 1)), lby = by0 + (sl >> P.lcx);
-        const size_t gb = (size_t)(P.ty * 8 + lby) * a.bxs + P.tx * 8 + lbx;
-        a.ac[(gb * 3 + CH) * 64 + (p & 63)] = (int16_t)qq;
+        const f2 e = (f2{avs[0], avs[1]} - f2{qfs[0], qfs[1]}) * f2{sd[kk], sd[kk + 1]};
+        cp = fmaf(e.x, e.x, cp);
+        cp = fmaf(e.y, e.y, cp);
       }
     }
     const int bits = 2 * (int)ebits - 250 * nzc;
