@@ -63,3 +63,35 @@ def test_psnr_monotone_in_distance(oracle, decoder, images):
 def test_per_channel_psnr_floor(oracle, decoder, images, name, floor):
     _, _, pc = _rd(oracle, decoder, images[name], 1.0, 7)
     assert min(pc) >= floor, pc
+
+
+def _text_like():
+    rng = np.random.default_rng(1)
+    img = np.full((256, 256, 3), 255, np.uint8)
+    for _ in range(40):
+        y, x = rng.integers(0, 240, 2)
+        img[y:y + 3, x:x + rng.integers(4, 16)] = 0
+    return img
+
+
+def test_haar_candidates_chosen_and_decoded(oracle, decoder):
+    """DCT2X2 (raw 2) and IDENTITY (raw 1) enter the 8x8 search (libjxl's
+    kTransforms8x8 scan, oracle/front.c): on sharp-edged, text-like content
+    they are chosen, the test decoder inverts them (IDCT2TopBlock / the
+    identity residual layout) and the image comes back nearly exact."""
+    img = _text_like()
+    o = oracle.encode(img, 1.0, 7, 0)
+    types = set(int(t) & 0x7F for t in np.unique(o.acs))
+    assert {1, 2} <= types, types
+    dec = decoder.decode(o.bytes)
+    assert np.array_equal(dec.acs & 0x7F, o.acs & 0x7F)
+    assert _psnr(img, dec.rgb) > 55.0
+
+
+def test_haar_candidates_pay_on_text(oracle, decoder):
+    """The same content with the search restricted to DCT8 (effort 4) costs
+    more bits at a lower PSNR."""
+    img = _text_like()
+    b7, p7, _ = _rd(oracle, decoder, img, 1.0, 7)
+    b4, p4, _ = _rd(oracle, decoder, img, 1.0, 4)
+    assert b7 < b4 and p7 > p4, (b7, p7, b4, p4)
