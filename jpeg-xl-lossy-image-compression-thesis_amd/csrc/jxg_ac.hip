@@ -533,9 +533,12 @@ __global__ __launch_bounds__(kAnsWaves * 64) void ans_encode_kernel(AnsArgs a) {
   __syncthreads();
   const uint8_t* inv = reinterpret_cast<const uint8_t*>(sInv);
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t g =
-      __builtin_amdgcn_readfirstlane(a.g0 + blockIdx.x * kAnsWaves + (threadIdx.x >> 6));
-  if (g >= a.g1) return;
+  // the chain's group: groups sorted longest first (host), kAnsWaves per
+  // workgroup, so a workgroup's waves finish at about the same time and the
+  // workgroups of short groups free their CUs early
+  const uint32_t gi = __builtin_amdgcn_readfirstlane(blockIdx.x * kAnsWaves + (threadIdx.x >> 6));
+  if (gi >= a.g1 - a.g0) return;
+  const uint32_t g = __builtin_amdgcn_readfirstlane(a.order[gi]);
   __builtin_amdgcn_s_setprio(3);
   const int n = (int)(a.ntok[g * 3] + a.ntok[g * 3 + 1] + a.ntok[g * 3 + 2]);
   const uint64_t b = (uint64_t)(g - a.g0) * kGroupTokStride;

@@ -490,7 +490,7 @@ struct Ctx {
       stream_chunks, stream_bits, scratch, scratch_lf, chunks, out, out_ac;
   DevBuf<uint64_t> gbase, chunkoff, stream_base;
   DevBuf<uint32_t> tile_list;
-  DevBuf<uint32_t> tokens, tval, ans_state;  // ANS coder
+  DevBuf<uint32_t> tokens, tval, ans_state, ans_order;  // ANS coder
   DevBuf<uint8_t> tlen;
   DevBuf<uint8_t> ans_tab;
   PinBuf<uint8_t> h_ans_tab;
@@ -506,6 +506,7 @@ struct Ctx {
   PinBuf<uint32_t> h_hist_ac, h_bound, h_ntok, h_lfhist, h_sbound, h_gbits, h_sbits, h_vcount,
       h_codes_ac, h_lfcodes;
   PinBuf<uint64_t> h_gbase, h_sbase;
+  PinBuf<uint32_t> h_ans_order;
   // LF row segments cached per frame size and shard
   uint32_t rows_w = 0, rows_h = 0, rows_rank = 0, rows_world = 1;
   std::vector<LfRow> rows_h_cache;
@@ -1136,6 +1137,20 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
     JXG_HIP(c->ans_state.ensure(f.ngroups));
     JXG_HIP(c->ans_tab.ensure(kAnsTabBytes));
     JXG_HIP(hipMemcpyAsync(c->ans_tab.p, c->h_ans_tab.p, kAnsTabBytes, hipMemcpyHostToDevice, s));
+    // chain order: the plan's groups by token count, longest first, so a
+    // chain workgroup holds groups of similar length and the workgroups of
+    // short groups give their CUs (and 68 KB of LDS each) back early -- the
+    // kernel still lasts as long as the longest group
+    const uint32_t ng = J.plan.g1 - J.plan.g0;
+    JXG_HIP(c->h_ans_order.ensure(ng));
+    JXG_HIP(c->ans_order.ensure(ng));
+    uint32_t* ord = c->h_ans_order.p;
+    for (uint32_t i = 0; i < ng; i++) ord[i] = J.plan.g0 + i;
+    const uint32_t* nt = c->h_ntok.p;
+    std::stable_sort(ord, ord + ng, [nt](uint32_t x, uint32_t y) {
+      return nt[x * 3] + nt[x * 3 + 1] + nt[x * 3 + 2] > nt[y * 3] + nt[y * 3 + 1] + nt[y * 3 + 2];
+    });
+    JXG_HIP(hipMemcpyAsync(c->ans_order.p, ord, ng * 4, hipMemcpyHostToDevice, s));
   }
   JXG_HIP(hipMemcpyAsync(c->codes_ac.p, c->h_codes_ac.p, packed.size() * 4, hipMemcpyHostToDevice, s));
   JXG_HIP(hipMemcpyAsync(c->gbase.p, c->h_gbase.p, J.gbase.size() * 8, hipMemcpyHostToDevice, s));
@@ -1218,6 +1233,7 @@ static jxg_status stage_emit(Ctx* c, Job& J, bool sync = true) {
     na.bits = c->gbits.p;
     na.g0 = J.plan.g0;
     na.g1 = J.plan.g1;
+    na.order = c->ans_order.p;
     launch_ans(na, s);
     JXG_HIP(hipGetLastError());
     JXG_HIP(hipMemcpyAsync(c->h_gbits.p, c->gbits.p, f.ngroups * 4, hipMemcpyDeviceToHost, s));

@@ -128,6 +128,7 @@ struct AnsArgs {
   uint32_t* scratch;
   uint32_t* bits;          // [ngroups] exact bits
   uint32_t g0, g1;         // groups [g0, g1)
+  const uint32_t* order;   // chain order of the g1 - g0 groups (longest first)
 };
 void launch_ans(const AnsArgs& a, hipStream_t s);
 
