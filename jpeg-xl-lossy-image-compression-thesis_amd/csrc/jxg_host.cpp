@@ -1635,9 +1635,9 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
 // little of their SIMDs; 68 KB of LDS per CU) run while frame j's transform
 // kernels fill the rest of the chip.  A frame's chain lasts as long as its
 // longest pass group's, whatever the frame size, so the depth follows the
-// frame: D = 4 from ~500 pass groups up (8K: more frames in flight only add
-// contention), up to kPipeMaxLanes for small frames (a 1080p
-// frame has 40 groups: 40 chain waves on a 1024-SIMD chip).  The lag follows
+// frame: ~3570 pass groups in flight (8K: 7 lanes, 4 % faster than 5 at 100
+// frames), at least 4, up to kPipeMaxLanes for small frames (a
+// 1080p frame has 40 groups: 40 chain waves on a 1024-SIMD chip).  The lag follows
 // it too: 1 for large frames (the codes of j-1 are joined in submit(j): the
 // GPU is the bound), 3 for small ones, whose host work per frame (0.5 ms of
 // ANS codes, 0.6 ms of launches and assembly) is the bound: three helpers run
@@ -1651,12 +1651,23 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
 #ifndef JXG_PIPE_LAG_SMALL
 #define JXG_PIPE_LAG_SMALL 3
 #endif
+#ifndef JXG_PIPE_LAG_LARGE
+#define JXG_PIPE_LAG_LARGE 1
+#endif
+#ifndef JXG_PIPE_MIN_LANES
+#define JXG_PIPE_MIN_LANES 4
+#endif
+#ifndef JXG_PIPE_CHAIN_GROUPS  // pass groups in flight the depth aims at
+#define JXG_PIPE_CHAIN_GROUPS 3570  // 8K (510 groups): 7 lanes
+#endif
 constexpr uint32_t kPipeMaxLanes = JXG_PIPE_MAX_LANES;
 static uint32_t pipe_depth(uint32_t ngroups) {
-  const uint32_t d = (2048 + ngroups - 1) / std::max(1u, ngroups);
-  return std::min(kPipeMaxLanes, std::max(4u, d));
+  const uint32_t d = (JXG_PIPE_CHAIN_GROUPS + ngroups - 1) / std::max(1u, ngroups);
+  return std::min(kPipeMaxLanes, std::max((uint32_t)JXG_PIPE_MIN_LANES, d));
 }
-static uint32_t pipe_lag(uint32_t ngroups) { return ngroups >= 256 ? 1u : (uint32_t)JXG_PIPE_LAG_SMALL; }
+static uint32_t pipe_lag(uint32_t ngroups) {
+  return ngroups >= 256 ? (uint32_t)JXG_PIPE_LAG_LARGE : (uint32_t)JXG_PIPE_LAG_SMALL;
+}
 // JXG_PIPE_PROFILE (experiment builds only): host time per pipeline step,
 // printed by jxg_destroy of the owning context
 #ifdef JXG_PIPE_PROFILE
