@@ -107,6 +107,16 @@ def load_pmc_traffic(workload):
         return None
 
 
+def load_front_valu(workload):
+    """PMC VALU-issue fraction of the front kernel (profiles/front_pmc_*.json)"""
+    p = os.path.join(ROOT, "profiles", "front_pmc_%s.json" % workload)
+    try:
+        with open(p) as f:
+            return json.load(f).get("valu_issue_frac")
+    except Exception:
+        return None
+
+
 def load_merge_pmc(workload):
     p = os.path.join(ROOT, "profiles", "merge_pmc_%s.json" % workload)
     try:
@@ -466,13 +476,17 @@ def main():
                          "bytes_per_px": SURVEY_BYTES_PER_PX,
                          "design_bytes": front_bytes_design(fw, fhh, args.effort),
                          "avg_ms": round(fms, 4),
+                         # the kernel is VALU-bound (the six-candidate 8x8 search):
+                         # its PMC VALU issue rate beside the HBM fraction
+                         "valu_issue_frac_pmc": load_front_valu(name) if world == 1 else None,
                          "measured": ("one-at-a-time encodes (the kernel alone on the GPU); "
                                       "under the pipeline, sharing the GPU with rANS chains: "
                                       "%.4f ms" % fms_pipe) if iso else "timed region"},
-            # the dominant kernels (merge stage) are VALU-issue-bound, not
-            # HBM-bound: their live time and the PMC-measured VALU issue rate
+            # the merge stage is latency-bound (VALU issue 35 %, waves waiting
+            # on memory / LDS 41 % of their lifetime): its live time and the
+            # PMC-measured VALU issue rate
             "merge_stage": {"kernels": "merge_eval + merge_resolve + merge_write",
-                            "bound": "valu",
+                            "bound": "latency",
                             "avg_ms": round((iso["st"] if iso else st)["ms_front"] -
                                             (iso["st"] if iso else st)["ms_front_kernel"], 4),
                             "valu_issue_frac_pmc": load_merge_pmc(name) if world == 1 else None},
