@@ -92,9 +92,14 @@ constexpr int kAcTok = 64;
 // 256x256 group, so only near-incompressible groups take the slow path
 // (ac_emit: 96 KiB + 33 KiB of code tables, one 1024-thread workgroup per CU)
 constexpr int kEmitLdsWords = 24576;
-// ans_emit's buffer: 80 KiB (10 bpp over a full group), so the kernel shares a
-// CU with a resident rANS chain workgroup (68 KB) of the next frame
-constexpr int kAnsEmitLdsWords = 20480;
+// ans_emit's buffer: 48 KiB (6 bpp over a full group; larger sections take the
+// global-atomics path), so the kernel shares a CU with a resident rANS chain
+// workgroup (68 KB) and a transform workgroup of later frames (80 -> 48 KiB:
+// +2 % pipelined 8K at 100 frames, 8 / 16 / 32 / 48 KiB within 1 %)
+#ifndef JXG_ANS_EMIT_WORDS  // (experiment builds override it: tools/build_variant.sh)
+#define JXG_ANS_EMIT_WORDS 12288
+#endif
+constexpr int kAnsEmitLdsWords = JXG_ANS_EMIT_WORDS;
 
 __device__ __forceinline__ int channel_of(int ci) { return ci == 0 ? 1 : (ci == 1 ? 0 : 2); }
 
@@ -634,8 +639,6 @@ __global__ __launch_bounds__(kAcThreads) void ans_emit_kernel(AnsArgs a) {
   const uint32_t g = a.g0 + blockIdx.x;
   const uint32_t n = a.ntok[g * 3] + a.ntok[g * 3 + 1] + a.ntok[g * 3 + 2];
   const uint64_t b = (uint64_t)(g - a.g0) * kGroupTokStride;
-  for (int i = threadIdx.x; i < kAnsEmitLdsWords / 4; i += blockDim.x)
-    reinterpret_cast<uint4*>(sBits)[i] = make_uint4(0, 0, 0, 0);
   constexpr int kWaves = kAcThreads / 64;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t chunk = ((n + kWaves * 64 - 1) / (kWaves * 64)) * 64;
@@ -655,6 +658,12 @@ __global__ __launch_bounds__(kAcThreads) void ans_emit_kernel(AnsArgs a) {
   }
   const uint64_t base = a.base[g];
   const bool lds = total <= (uint32_t)kAnsEmitLdsWords * 32u;
+  if (lds) {  // clear only the section's words
+    const uint32_t nq = (total + 127) / 128;
+    for (uint32_t i = threadIdx.x; i < nq; i += blockDim.x)
+      reinterpret_cast<uint4*>(sBits)[i] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+  }
   uint32_t* buf = lds ? sBits : a.scratch;
   const uint64_t bias = lds ? 0 : base;
   if (threadIdx.x == 0) {
