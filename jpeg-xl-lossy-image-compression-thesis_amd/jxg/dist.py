@@ -198,6 +198,11 @@ def encode_sharded(enc: Encoder, d_rgb: torch.Tensor, width: int, height: int, r
         # a collective is skipped only when NO rank exchanges (every rank
         # derives the same answer from the geometry)
         bufs["any"] = any(sum(shard_exchange(width, height, world, r)[0]) for r in range(world))
+        # the zero fills run on torch's stream; the library writes these
+        # buffers on its own stream -- without this wait a late fill could
+        # clear the histogram shard_begin just wrote (seen: a rank's HF preset
+        # with no histogram when the GPU was busy with earlier work)
+        torch.cuda.synchronize(dev)
     hist, send, recv = bufs["hist"], bufs["send"], bufs["recv"]
     snd, rcv = bufs["splits"]
     enc.shard_begin(d_rgb.data_ptr(), width, height, rank, world, hist.data_ptr(),

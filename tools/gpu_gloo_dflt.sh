@@ -1,0 +1,6 @@
+#!/bin/bash
+# 2-rank gloo rehearsal of the default multi-GPU bench (replica lines, then the sharded line)
+set -e
+export TMPDIR=/tmp
+O=gpurun_out/$1; mkdir -p $O
+JXG_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu-baseline --no-quality > $O/bench_gloo2.log 2>&1
