@@ -105,13 +105,18 @@ jxg_status jxg_encode_batch_rgb8_device(void* ctx, const void* const* d_rgbs, ui
                                         jxg_buffer* outs);
 /* Streaming encode, one host thread: frames are submitted in order and their
  * codestreams received in the same order (byte-identical to jxg_encode_rgb8
- * of each frame).  Internally a software pipeline over this context and three
- * lanes it creates on first use (same parameters; released by jxg_destroy):
- * a submit finishes the frame submitted four calls earlier if it is still in
- * flight, launches the new frame's front end / merge stage / statistics, and
- * builds the previous frame's codes and launches its emission -- so the rANS
- * chains (JXG_FLAG_ANS) of two frames run under the transform kernels of the
- * next.  jxg_receive blocks until the oldest frame is complete
+ * of each frame).  Internally a software pipeline over this context and up to
+ * 11 lanes it creates on first use (same parameters; released by
+ * jxg_destroy); the depth D follows the frame size (7 lanes at 8K, 12 at 4K
+ * and below): a submit finishes the frame submitted D calls earlier if it is
+ * still in flight, launches the new frame's front end / merge stage /
+ * statistics on a free lane, starts the previous frame's codes on a helper
+ * thread and joins the codes of the frame `lag` submits back (1 at 8K, 3 for
+ * small frames), whose helper launched its emission -- so the rANS chains
+ * (JXG_FLAG_ANS) of earlier frames run under the transform kernels of the
+ * next.  Each lane uses its own HIP stream: the process needs that many
+ * hardware queues (GPU_MAX_HW_QUEUES=16 set before the HIP runtime starts).
+ * jxg_receive blocks until the oldest frame is complete
  * (JXG_ERR_INVALID_ARG if none is pending); jxg_pending counts frames
  * submitted and not yet received.  A device frame must stay unchanged until
  * its codestream is received; a host frame is copied into pinned staging
