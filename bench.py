@@ -51,12 +51,13 @@ import os
 import sys
 import time
 
-# The library's streaming pipeline runs up to 12 encoder lanes (4 at 8K, more
-# for small frames), one HIP stream each; HIP maps streams onto
+# The library's streaming pipeline runs up to 12 encoder lanes (7 at 8K, 12
+# for 4K and smaller), one HIP stream each; HIP maps streams onto
 # GPU_MAX_HW_QUEUES hardware queues per process (the box exports 4, one of them
 # taken by torch's stream), and two lanes sharing a queue serialise their
-# kernels.  Must be set before HIP initialises.
-os.environ["GPU_MAX_HW_QUEUES"] = "16"
+# kernels.  Must be set before HIP initialises (JXG_BENCH_HW_QUEUES overrides
+# it for experiments; at most 32).
+os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, int(os.environ.get("JXG_BENCH_HW_QUEUES", "16"))))
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "jpeg-xl-lossy-image-compression-thesis_amd"))
