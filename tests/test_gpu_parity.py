@@ -166,3 +166,23 @@ def test_ans_matches_oracle(jxg_mod, oracle, decoder, w, h, d, e, p):
     if w * h <= 520 * 300:
         dec = decoder.decode(got)
         assert np.array_equal(dec.ac, ref.ac)
+
+
+@pytest.mark.parametrize("d,p", [(1.0, 0), (1.0, 3), (0.3, 2), (4.0, 1)])
+def test_haar_candidates_match_oracle(jxg_mod, oracle, d, p):
+    """Sharp-edged, text-like content, where DCT2X2 and IDENTITY win many 8x8
+    searches (DPP Haar steps of the front kernel vs oracle jxo_transform), with
+    and without the thesis hooks."""
+    rng = np.random.default_rng(11)
+    img = np.full((264, 392, 3), 250, np.uint8)
+    for _ in range(120):
+        y, x = rng.integers(0, 250, 2)
+        img[y:y + rng.integers(2, 5), x:x + rng.integers(3, 24)] = rng.integers(0, 80, 3)
+    with jxg_mod.Encoder(distance=d, effort=7, proposals=p, flags=jxg_mod.FLAG_KEEP_MAPS) as enc:
+        got = enc.encode(img)
+        st = enc.stats()
+    ref = oracle.encode(img, d, 7, p)
+    assert {1, 2} & set(int(t) & 0x7F for t in np.unique(ref.acs))
+    assert np.array_equal(st["acs"], ref.acs)
+    assert np.array_equal(st["ac"], ref.ac)
+    assert got == ref.bytes
