@@ -89,13 +89,13 @@ jxg_status jxg_encode_rgb8_device(void* ctx, const void* d_rgb, uint32_t xsize,
                                   uint32_t ysize, size_t row_stride, jxg_buffer* out);
 /* n frames of equal size (benchmark config 3: 64 x 1080p; the reference's
  * caller encodes every image at 10 distances x 5 efforts, benchmark.rs:
- * 637-642).  The frames are spread over three lanes -- this context plus two
- * it creates on first use (same parameters; released by jxg_destroy) -- one
- * host thread, HIP stream and pinned staging buffer each, so the frames'
- * H2D copies, kernels and host-side code construction overlap.  outs[i] is
- * frame i's codestream (byte-identical to jxg_encode_rgb8 of that frame); on
- * error every output is released.  jxg_get_stats then describes the last
- * frame this context encoded. */
+ * 637-642), through the streaming pipeline below (jxg_submit_rgb8 of every
+ * frame, codestreams collected as they complete), so the frames' H2D copies,
+ * kernels, rANS chains and host-side code construction overlap over the
+ * pipeline's lanes.  outs[i] is frame i's codestream (byte-identical to
+ * jxg_encode_rgb8 of that frame); on error every output is released.  The
+ * context must have no streamed frames pending (JXG_ERR_INVALID_ARG
+ * otherwise).  jxg_get_stats then describes the last frame. */
 jxg_status jxg_encode_batch_rgb8(void* ctx, const uint8_t* const* rgbs, uint32_t n,
                                  uint32_t xsize, uint32_t ysize, size_t row_stride,
                                  jxg_buffer* outs);

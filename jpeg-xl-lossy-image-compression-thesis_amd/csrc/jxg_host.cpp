@@ -2400,69 +2400,33 @@ jxg_status jxg_encode_rgb8(void* ctx, const uint8_t* rgb, uint32_t w, uint32_t h
   return encode_device(c, c->rgb.p, w, h, stride, out, t0);
 }
 
-// Batched encode (BASELINE config 3: 64 x 1080p).  Frames are spread over
-// kBatchLanes contexts -- the caller's plus lanes it owns (same parameters),
-// one host thread, HIP stream and pinned staging buffer each -- pulling frame
-// indices from a shared counter.  A 1080p frame (40 pass groups) fills a
-// fraction of the chip, so the lanes' kernels, H2D copies (pinned, async) and
-// host-side code construction overlap.  Three lanes: the GPU has 4 hardware
-// queues per process (GPU_MAX_HW_QUEUES), and the bench measured 3 concurrent
-// encoders as the knee.  Outputs are in frame order; the bytes of every frame
-// equal jxg_encode_rgb8's.
-static constexpr uint32_t kBatchLanes = 3;
-
+// Batched encode (BASELINE config 3: 64 x 1080p) through the streaming
+// pipeline (pipe_submit / pipe_receive): every frame is
+// submitted in order and the codestreams already complete are collected after
+// each submit, so the frames' transform kernels, rANS chains, host-side code
+// construction (helper threads) and pinned H2D copies overlap over the
+// pipeline's lanes.  Outputs are in frame order; the bytes of every frame equal
+// jxg_encode_rgb8's.  The context must have no streamed frames pending.
 static jxg_status batch_encode(Ctx* c, const uint8_t* const* frames, bool on_device, uint32_t n,
                                uint32_t w, uint32_t h, size_t stride, jxg_buffer* outs) {
   for (uint32_t i = 0; i < n; i++) outs[i] = jxg_buffer{nullptr, 0};
-  const uint32_t nl = std::min(n, kBatchLanes);
-  while (c->lanes.size() + 1 < nl) {
-    void* lc = nullptr;
-    const jxg_status st = jxg_create(&c->params, &lc);
-    if (st) return st;
-    c->lanes.emplace_back(static_cast<Ctx*>(lc));
+  if (c->pipe && (!c->pipe->inflight.empty() || !c->pipe->done.empty()))
+    return JXG_ERR_INVALID_ARG;  // would interleave with the caller's stream
+  uint32_t got = 0;
+  jxg_status st = JXG_OK;
+  for (uint32_t i = 0; i < n && !st; i++) {
+    st = pipe_submit(c, frames[i], on_device, w, h, stride);
+    while (!st && !c->pipe->done.empty()) st = pipe_receive(c, &outs[got++]);
   }
-  std::atomic<uint32_t> next{0};
-  std::atomic<int> err{0};
-  const size_t bytes = stride * (h - 1) + (size_t)w * 3;
-  auto lane = [&](Ctx* L) {
-    if (hipSetDevice(L->params.device) != hipSuccess) {
-      err = JXG_ERR_HIP;
-      return;
+  while (!st && got < n) st = pipe_receive(c, &outs[got++]);
+  if (st) {  // the pipe is aborted by then; drop what it completed, and ours
+    if (c->pipe) {
+      for (auto& d : c->pipe->done) jxg_buffer_free(&d.buf);
+      c->pipe->done.clear();
     }
-    for (uint32_t i; !err && (i = next++) < n;) {
-      const Clock::time_point t0 = Clock::now();
-      const uint8_t* src = frames[i];
-      jxg_status st = JXG_OK;
-      if (!on_device) {
-        if (L->h_stage.ensure(bytes) != hipSuccess || L->rgb.ensure(bytes) != hipSuccess) {
-          err = JXG_ERR_OOM;
-          return;
-        }
-        // the previous frame's H2D has completed: encode_device synchronizes
-        std::memcpy(L->h_stage.p, src, bytes);
-        if (hipMemcpyAsync(L->rgb.p, L->h_stage.p, bytes, hipMemcpyHostToDevice, L->stream) !=
-            hipSuccess) {
-          err = JXG_ERR_HIP;
-          return;
-        }
-        src = L->rgb.p;
-      }
-      st = encode_device(L, src, w, h, stride, &outs[i], t0);
-      if (st) {
-        int z = 0;
-        err.compare_exchange_strong(z, (int)st);
-      }
-    }
-  };
-  std::vector<std::thread> th;
-  for (uint32_t l = 1; l < nl; l++) th.emplace_back(lane, c->lanes[l - 1].get());
-  lane(c);
-  for (auto& t : th) t.join();
-  if (err) {
     for (uint32_t i = 0; i < n; i++) jxg_buffer_free(&outs[i]);
-    return (jxg_status)err.load();
   }
-  return JXG_OK;
+  return st;
 }
 
 jxg_status jxg_encode_batch_rgb8(void* ctx, const uint8_t* const* rgbs, uint32_t n, uint32_t w,

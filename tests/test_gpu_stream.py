@@ -1,8 +1,9 @@
 """Streaming encode (jxg_submit_rgb8[_device] / jxg_receive): the library's
-one-thread software pipeline over four lanes returns, in submission order,
+one-thread software pipeline (4-12 lanes) returns, in submission order,
 exactly the codestreams of one-at-a-time jxg_encode_rgb8 calls -- for frames of
 mixed sizes and content, both AC coders, receives interleaved with submits, and
-a full-size 8K ANS sequence against the oracle's committed fingerprint."""
+a full-size 8K ANS sequence against the oracle's committed fingerprint; the
+batch entry point (jxg_encode_batch_rgb8, built on the same pipeline) too."""
 import hashlib
 import json
 import os
@@ -89,3 +90,22 @@ def test_stream_many_small_frames_ans(jxg_mod):
         while enc.pending():
             got.append(enc.receive())
     assert got == want
+
+
+def test_batch_ans_equals_single_and_refuses_pending(jxg_mod):
+    """jxg_encode_batch_rgb8 runs through the streaming pipeline: its outputs
+    equal one-at-a-time encodes (ANS, 20 frames, so completions interleave
+    with submits), and it refuses while streamed frames are pending."""
+    from jxg.synth import natural_rgb8, synth_rgb8
+
+    frames = [(natural_rgb8 if i % 2 else synth_rgb8)(480, 272, 700 + i) for i in range(20)]
+    with jxg_mod.Encoder(distance=1.0, effort=7, flags=jxg_mod.FLAG_ANS) as enc:
+        want = [enc.encode(f) for f in frames]
+    with jxg_mod.Encoder(distance=1.0, effort=7, flags=jxg_mod.FLAG_ANS) as enc:
+        assert enc.encode_batch(frames) == want
+        enc.submit(frames[0])
+        with pytest.raises(jxg_mod.JxgError):
+            enc.encode_batch(frames[:2])
+        assert enc.receive() == want[0]
+        assert enc.encode_batch(frames[:3]) == want[:3]
+        assert enc.pending() == 0
