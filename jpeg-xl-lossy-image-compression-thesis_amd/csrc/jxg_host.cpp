@@ -399,11 +399,13 @@ static MergeTables build_merge_tables() {
       }
     }
   }
-  // per-shape pixel-orientation copies, row-major ([ky * C + kx]; tall shapes
-  // read the stored table transposed) -- the lanes of a quantization pass are
-  // consecutive columns kx, so each of a lane's per-row loads is one coalesced
-  // 256-byte wave access (per-lane 16-byte column chunks touched 64 cache
-  // lines per load and cost merge_eval ~13 % in address processing)
+  // per-shape pixel-orientation copies in row quads ([ky / 4][kx][ky % 4]; tall
+  // shapes read the stored table transposed) -- the lanes of a quantization
+  // pass are consecutive columns kx, so one 16-byte load per lane brings a
+  // lane's four rows and the wave's access is 1 KB contiguous: the cache lines
+  // of four row-major loads in a quarter of the load instructions (per-lane
+  // 16-byte column chunks [kx][ky] touched 64 cache lines per load and cost
+  // merge_eval ~13 % in address processing)
   {
     static const int kShapeDims[kNumShapes][3] = {{2, 1, 0}, {1, 2, 0}, {2, 2, 1}, {4, 2, 2}, {2, 4, 2},
                                                  {4, 4, 3}, {8, 4, 4}, {4, 8, 4}, {8, 8, 5}};
@@ -416,7 +418,7 @@ static MergeTables build_merge_tables() {
       for (int ky = 0; ky < R; ky++)
         for (int kx = 0; kx < C; kx++) {
           const int si = cx >= cy ? ky * C + kx : kx * R + ky;
-          const int pi = kShapeOff[sh] + ky * C + kx;
+          const int pi = kShapeOff[sh] + ((ky >> 2) * C + kx) * 4 + (ky & 3);
           // LLF positions (the first cy x cx): weight 0, so they quantize to 0
           // and add nothing without a per-coefficient test in the kernels
           const bool llf = ky < cy && kx < cx;

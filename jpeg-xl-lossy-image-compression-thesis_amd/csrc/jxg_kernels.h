@@ -56,7 +56,7 @@ struct MergeArgs {
   uint16_t* nz;         // out (merged varblocks): full count at the first block,
                         //   (nz + cb - 1) >> log2 cb at covered blocks
   float* cost;          // [tiles][9 shapes][32 varblocks] candidate estimates
-  const float* wk;      // [3][kShapeOff[9]] weights per shape, pixel orientation
+  const float* wk;      // [3][kShapeOff[9]] weights per shape, pixel orientation, row quads ([ky/4][kx][ky%4])
   const float* iwy;     // [kShapeOff[9]] 1 / Y weight
   const float* sdk;     // [3][kShapeOff[9]] distortion weights (dist_weight), same layout
   const uint16_t* nat;  // [kShapeOff[9]] natural-order position

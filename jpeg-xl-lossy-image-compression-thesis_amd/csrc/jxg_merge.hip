@@ -418,6 +418,11 @@ struct QTab {
   static constexpr int NIT = RPC == 8 ? 2 : 1;  // items per thread: 512 or 256 / 256
   float w[NIT][RPC], sd[NIT][RPC], iw[NIT][RPC];
 };
+// Tables in row quads ([ky / 4][kx][ky % 4], host quant tables): one 16-byte
+// load per lane and four rows, the wave's 64 lanes 1 KB contiguous.
+__device__ __forceinline__ int qtab_index(const Pass& P, int ky, int x) {
+  return P.soff + ((ky >> 2) * P.C() + x) * 4;
+}
 template <int RPC, bool WRITE, int CH>
 __device__ __forceinline__ void load_qtab(const MergeArgs& a, const Pass& P, QTab<RPC>& T) {
   constexpr int STOT = kShapeOff[kNumShapes];
@@ -425,13 +430,12 @@ __device__ __forceinline__ void load_qtab(const MergeArgs& a, const Pass& P, QTa
   for (int it = 0; it < QTab<RPC>::NIT; it++) {
     const int j = threadIdx.x + it * kMThreads;
     const int ch = j >> (P.lNV() + P.lC()), x = j & (P.C() - 1);
-    const int t0 = P.soff + ch * RPC * P.C() + x;  // row ch * RPC, column x (row-major)
 #pragma unroll
-    for (int kk = 0; kk < RPC; kk++) {
-      const int ti = t0 + kk * P.C();
-      T.w[it][kk] = a.wk[(size_t)CH * STOT + ti];
-      if (!WRITE) T.sd[it][kk] = a.sdk[(size_t)CH * STOT + ti];
-      if (CH == 1) T.iw[it][kk] = a.iwy[ti];
+    for (int kk = 0; kk < RPC; kk += 4) {
+      const int ti = qtab_index(P, ch * RPC + kk, x);
+      load_f<4>(a.wk + (size_t)CH * STOT + ti, &T.w[it][kk]);
+      if (!WRITE) load_f<4>(a.sdk + (size_t)CH * STOT + ti, &T.sd[it][kk]);
+      if (CH == 1) load_f<4>(a.iwy + ti, &T.iw[it][kk]);
     }
   }
 }
@@ -466,7 +470,13 @@ __device__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S, const
     uint16_t nat[RPC];
     if (WRITE) {
 #pragma unroll
-      for (int kk = 0; kk < RPC; kk++) nat[kk] = a.nat[P.soff + (ch * RPC + kk) * C + x];
+      for (int kk = 0; kk < RPC; kk += 4) {
+        const uint2 u = *reinterpret_cast<const uint2*>(a.nat + qtab_index(P, ch * RPC + kk, x));
+        nat[kk] = (uint16_t)u.x;
+        nat[kk + 1] = (uint16_t)(u.x >> 16);
+        nat[kk + 2] = (uint16_t)u.y;
+        nat[kk + 3] = (uint16_t)(u.y >> 16);
+      }
     }
     // the LLF (first cy rows x cx columns) only occurs in chunk 0
     const bool llf_col = ch == 0 && x < P.cx();
