@@ -393,7 +393,7 @@ __device__ void col_pass(const Pass& P, MergeLds& S) {
 // quantization, phase 0 = Y, phase 1 = X and B; lane = (channel, chunk of
 // RPC rows, varblock, column).  Chunk partial: fmaf(e, e) over its rows
 // ascending.  The lane's weights, inverse Y weights and natural positions
-// are RPC consecutive entries of the column-major tables (16-byte loads).
+// come in 16-byte loads of four rows each (row-quad tables, load_qtab).
 // Rate bits and non-zeros are summed over the varblock's C lanes in-wave and
 // added to LDS by one lane.  WRITE: coefficients to their natural-order
 // slices, LLF to LDS.
