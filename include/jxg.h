@@ -41,6 +41,9 @@ typedef enum {
 #define JXG_FLAG_H1_INT_ABS 1u /* thesis SML with int abs(int) */
 #define JXG_FLAG_KEEP_MAPS 2u  /* keep per-block maps for jxg_get_stats */
 #define JXG_FLAG_ANS 4u        /* ANS (12-bit rANS) for the AC stream instead of prefix codes */
+#define JXG_FLAG_FORCE_ONE_STREAM 8u /* testing: the split assembly takes its one-stream
+                                      * fallback (as when its prefix bound is exceeded);
+                                      * same bytes */
 
 typedef struct {
   float distance;      /* cjxl --distance (butteraugli target), (0, 25] */

@@ -1467,7 +1467,9 @@ static jxg_status stage_concat_split(Ctx* c, Job& J, uint8_t** host_out, size_t*
     dst = (dst + 7) & ~7ull;
   }
   const size_t pbytes = (size_t)(dst / 8);
-  if (pbytes + kOutHdr > pmax) {  // prefix bound violated: one-stream assembly instead
+  // prefix bound violated (or forced, JXG_FLAG_FORCE_ONE_STREAM): one-stream
+  // assembly instead
+  if (pbytes + kOutHdr > pmax || (c->params.flags & JXG_FLAG_FORCE_ONE_STREAM)) {
     if (hipStreamSynchronize(s2) != hipSuccess) return fail(JXG_ERR_HIP);
     out_release(ho);
     const jxg_status st = stage_concat(c, J, true, nullptr, nullptr, host_out, out_bytes);

@@ -33,6 +33,7 @@ PROPOSAL_F = 2
 FLAG_H1_INT_ABS = 1
 FLAG_KEEP_MAPS = 2
 FLAG_ANS = 4
+FLAG_FORCE_ONE_STREAM = 8  # testing: the split assembly's one-stream fallback (same bytes)
 
 
 class JxgError(RuntimeError):

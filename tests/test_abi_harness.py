@@ -37,6 +37,16 @@ def test_nm_dynamic_symbols(jxg_mod):
         assert re.search(r"\bT %s$" % f, out, re.M), f
 
 
+def test_flag_constants_match_header(jxg_mod):
+    import re
+
+    src = open(os.path.join(ROOT, "include", "jxg.h")).read()
+    flags = dict(re.findall(r"#define JXG_(FLAG_\w+) (\d+)u", src))
+    assert len(flags) >= 4
+    for name, val in flags.items():
+        assert getattr(jxg_mod, name) == int(val), name
+
+
 def test_status_strings(jxg_mod):
     lib = jxg_mod.load()
     assert lib.jxg_status_str(0) == b"ok"

@@ -66,3 +66,22 @@ def test_batch_1080p_matches_oracle(jxg_mod, distance):
         outs = enc.encode_batch(frames)
     for data, g in zip(outs, gs):
         assert len(data) == g["bytes"] and hashlib.sha256(data).hexdigest() == g["sha256"], g["name"]
+
+
+@pytest.mark.parametrize("coder", ["prefix", "ans"])
+def test_one_stream_fallback_same_bytes(jxg_mod, coder):
+    """The split assembly's fallback (one-stream stage_concat, taken when the
+    prefix bound is exceeded; forced here by JXG_FLAG_FORCE_ONE_STREAM) gives
+    the split path's bytes, and both equal the oracle's fingerprint."""
+    name = "8k_d1_ans" if coder == "ans" else "4k_d1"
+    g = BY_NAME[name]
+    t = _device_frame(jxg_mod, g)
+    base = jxg_mod.FLAG_ANS if coder == "ans" else 0
+    outs = []
+    for extra in (0, jxg_mod.FLAG_FORCE_ONE_STREAM):
+        with jxg_mod.Encoder(distance=g["distance"], effort=g["effort"], proposals=g["proposals"],
+                             flags=base | extra) as enc:
+            outs.append(enc.encode_device(t.data_ptr(), g["width"], g["height"]))
+    del t
+    assert outs[0] == outs[1]
+    assert hashlib.sha256(outs[1]).hexdigest() == g["sha256"]
