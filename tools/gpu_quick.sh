@@ -11,5 +11,5 @@ if [ -n "$K" ]; then
 else
   timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/$TAG/tests.log 2>&1
 fi
-timeout -k 10 200 python bench.py --no-cpu-baseline --alt-ans-streams 0 > gpurun_out/$TAG/bench.log 2>&1
-cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/$TAG/prof -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --alt-ans-streams 0 > $R/gpurun_out/$TAG/bench_prof.log 2>&1
+timeout -k 10 200 python bench.py --no-cpu-baseline > gpurun_out/$TAG/bench.log 2>&1
+cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/$TAG/prof -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline > $R/gpurun_out/$TAG/bench_prof.log 2>&1
