@@ -188,12 +188,22 @@ struct Pass {
   }
 };
 
-// workgroup id -> (tile, shape): the nine shapes of a tile share b % 8 (XCD)
+// workgroup id -> (tile, shape): the nine shapes of a tile share b % 8 (XCD);
+// per XCD the tiles go in chunks of JXG_MERGE_CHUNK, shape-major inside a
+// chunk, so the workgroups resident on a CU at a time mostly run one shape's
+// code (the kernel is 53 KB of code; interleaved shapes, chunk 1, took 1.595
+// ms at 8K, chunk 64 1.545 ms: profiles/r02s4_merge_chunk) while a chunk's
+// tiles (64 x 48 KB) are still re-read from the XCD's L2 / the MALL.
 // (a shard's tiles come through a list: tile = list[index])
+#ifndef JXG_MERGE_CHUNK
+#define JXG_MERGE_CHUNK 64
+#endif
 __device__ __forceinline__ bool decode_wg(const MergeArgs& a, int& tile, int& si) {
+  constexpr int T = JXG_MERGE_CHUNK;
   const int b = blockIdx.x, x = b & 7, q = b >> 3;
-  si = q % kNumShapes;
-  tile = (q / kNumShapes) * 8 + x;
+  const int r = q % (kNumShapes * T);
+  si = r / T;
+  tile = ((q / (kNumShapes * T)) * T + r % T) * 8 + x;
   if (tile >= (int)a.ntiles) return false;
   if (a.tile_list) tile = (int)a.tile_list[tile];
   return true;
@@ -958,7 +968,8 @@ hipError_t set_merge_constants(const float* llf_p, const float* llf_ib, hipStrea
 }
 hipError_t launch_merge(const MergeArgs& a, hipStream_t s) {
   if (!a.ntiles) return hipSuccess;
-  const uint32_t nwg = ((a.ntiles + 7) / 8) * 8 * kNumShapes;
+  constexpr uint32_t T = JXG_MERGE_CHUNK;
+  const uint32_t nwg = (((a.ntiles + 7) / 8 + T - 1) / T) * T * 8 * kNumShapes;
   hipLaunchKernelGGL(merge_eval_kernel, dim3(nwg), dim3(kMThreads), 0, s, a);
   const hipError_t e = hipMemsetAsync(a.work, 0, sizeof(uint32_t), s);
   if (e != hipSuccess) return e;
