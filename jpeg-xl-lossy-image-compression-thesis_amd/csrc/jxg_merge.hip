@@ -48,6 +48,9 @@ constexpr int kMThreads = 256;
 #ifndef JXG_MERGE_WPE
 #define JXG_MERGE_WPE 3  // waves per SIMD the eval/write kernels are register-capped for
 #endif
+#ifndef JXG_MERGE_WRITE_WPE
+#define JXG_MERGE_WRITE_WPE JXG_MERGE_WPE
+#endif
 constexpr int kMS = 65;  // LDS row stride (floats)
 constexpr int kMPlane = 64 * kMS;
 
@@ -873,7 +876,7 @@ __device__ __forceinline__ void write_entry(const MergeArgs& a, int tile, int si
 
 // persistent workgroups over the (tile, shape) entries the resolve kernel
 // listed: only (tile, shape) pairs holding a chosen varblock cost anything
-__global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(JXG_MERGE_WPE)))
+__global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(JXG_MERGE_WRITE_WPE)))
 void merge_write_kernel(MergeArgs a) {
   __shared__ __attribute__((aligned(16))) MergeLds S;
   const uint32_t n = __builtin_amdgcn_readfirstlane(*(volatile uint32_t*)a.work);
