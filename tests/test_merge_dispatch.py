@@ -1,0 +1,57 @@
+"""merge_eval's workgroup -> (tile, shape) map covers every pair exactly once.
+
+Restates `decode_wg` and the grid size of `launch_merge`
+(jpeg-xl-lossy-image-compression-thesis_amd/csrc/jxg_merge.hip): per XCD
+(workgroup id mod 8) the tiles go in chunks of JXG_MERGE_CHUNK, shape-major
+inside a chunk.  The GPU parity tests check the outputs; this checks the index
+arithmetic for frame sizes and chunk settings they do not reach.
+"""
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "jpeg-xl-lossy-image-compression-thesis_amd", "csrc", "jxg_merge.hip")
+NUM_SHAPES = 9
+
+
+def default_chunk():
+    text = open(SRC).read()
+    m = re.search(r"#define JXG_MERGE_CHUNK (\d+)", text)
+    assert m, "JXG_MERGE_CHUNK default not found"
+    return int(m.group(1))
+
+
+def grid(ntiles, T):
+    return (((ntiles + 7) // 8 + T - 1) // T) * T * 8 * NUM_SHAPES
+
+
+def decode(b, ntiles, T):
+    x, q = b & 7, b >> 3
+    r = q % (NUM_SHAPES * T)
+    si = r // T
+    tile = ((q // (NUM_SHAPES * T)) * T + r % T) * 8 + x
+    return (tile, si) if tile < ntiles else None
+
+
+@pytest.mark.parametrize("T", [1, 4, 32, None, 128])
+@pytest.mark.parametrize("ntiles", [1, 7, 8, 9, 135, 510, 8160])
+def test_every_tile_shape_once(T, ntiles):
+    T = T or default_chunk()
+    seen = {}
+    for b in range(grid(ntiles, T)):
+        ts = decode(b, ntiles, T)
+        if ts is None:
+            continue
+        assert ts not in seen, (ts, b, seen.get(ts))
+        seen[ts] = b
+        assert ts[0] % 8 == b % 8  # the nine shapes of a tile share an XCD
+    assert len(seen) == ntiles * NUM_SHAPES
+
+
+def test_source_matches_restatement():
+    text = open(SRC).read()
+    assert "const int r = q % (kNumShapes * T);" in text
+    assert "tile = ((q / (kNumShapes * T)) * T + r % T) * 8 + x;" in text
+    assert "(((a.ntiles + 7) / 8 + T - 1) / T) * T * 8 * kNumShapes" in text
