@@ -14,20 +14,26 @@ inside the library in which the rANS chains of earlier frames run under the
 transform kernels of later ones); the timed region ends when the last
 codestream of the K steps is in host memory.
 
-N = 1: one 7680x4320 frame per step (BASELINE config 2's frame on one GPU).
+N = 1: one 7680x4320 frame per step (BASELINE config 2's frame on one GPU);
+the steps cycle through two distinct synthetic frames.
 N > 1 (launched by torch.distributed.run, backend nccl = RCCL):
-  shard   (default) -- group sharding with the real exchange
-          (jxg/dist.py) and assembly (--assembly host: every rank DMAs its
-          sections into one /dev/shm codestream buffer of the node, rank 0
-          writes headers + TOC; --assembly device: payload gather to rank 0):
-            --scaling strong (default): ONE 7680x4320 frame per step split
-              over the N ranks -- BASELINE config 2 as written;
-            --scaling weak: one frame of N stacked 8K frames (every rank owns
-              one 8K frame's worth of groups).
-          The codestream is byte-identical to a single-GPU encode of the same
-          frame (tests/test_gpu_shard.py).
-  replica -- every rank encodes its own 8K frame (frame-level data
-          parallelism, no data-path collective).
+  shard   (default) -- BASELINE config 2 as written, strong scaling: every
+          step is ONE 7680x4320 frame whose 256x256 pass groups are split over
+          the N ranks (whole LF groups per rank, jxg_shard_plan kind 1: no
+          per-block records move; one HF preset per rank: no histogram
+          collective), streamed through jxg.dist.ShardStream -- each rank keeps
+          up to jxg_pipeline_depth frames' shards in flight in the library's
+          lanes, swaps the frame's payload heads with the other ranks through
+          a node-shared /dev/shm region and DMAs its sections into the frame's
+          codestream there (rank 0 adds headers + TOC).  value = frames x
+          7680 x 4320 / time over all ranks.  --scaling weak: one frame of N
+          stacked 8K frames per step instead.
+  shard-sync -- the same split one frame at a time (jxg.dist.encode_sharded:
+          record exchange + histogram all-reduce when the plan / coder needs
+          them, --assembly host|device).
+  replica -- every rank streams its own 8K frames (frame-level data
+          parallelism, no data-path collective); also reported beside the
+          shard line as `replicas`.
 Timing: barrier + synchronize on both sides of the K steps, max over ranks.
 --streams S (non-shard modes) runs S concurrent encoders per GPU (one host
 thread, context and HIP stream each; the K frames split between them) through
@@ -129,13 +135,13 @@ def load_merge_pmc(workload):
 
 
 def cpu_threads():
-    """host threads for the CPU baseline: the process's CPU affinity, capped at
-    16 (the GPU box's CPU share per GPU; its nproc shows the whole host)"""
+    """host threads for the CPU baseline: every core this process may run on
+    (its CPU affinity; nproc is reported beside it)"""
     try:
         n = len(os.sched_getaffinity(0))
     except AttributeError:
         n = os.cpu_count() or 1
-    return max(1, min(16, n))
+    return max(1, n)
 
 
 def cpu_baseline(img, distance, effort, proposals, coder, gpu_bytes):
@@ -153,8 +159,10 @@ def cpu_baseline(img, distance, effort, proposals, coder, gpu_bytes):
     dt = time.perf_counter() - t
     h, w, _ = img.shape
     return {"value": round(w * h / 1e6 / dt, 3), "unit": "MPix/s", "cores": n, "kind": "port",
+            "nproc": os.cpu_count(), "affinity": cpu_threads(),
             "sample": "one full %dx%d frame (the bench frame), oracle/ C restatement with OpenMP "
-                      "(libjxl/cjxl absent on the box), %.2f s" % (w, h, dt),
+                      "on all %d cores of the process's affinity (nproc %s; libjxl/cjxl absent "
+                      "on the box), %.2f s" % (w, h, n, os.cpu_count(), dt),
             "bytes_equal_gpu": gpu_bytes is not None and r.bytes == gpu_bytes}
 
 
@@ -202,13 +210,16 @@ def main():
     ap.add_argument("--distance", type=float, default=1.0)
     ap.add_argument("--effort", type=int, default=7)
     ap.add_argument("--proposals", type=int, default=0)
-    ap.add_argument("--mode", choices=("shard", "replica"), default="replica",
-                    help="N > 1: replica = every rank streams its own frames through the "
-                         "pipelined entry points (frame-level data parallelism, no data-path "
-                         "collective); shard = one frame's pass groups split over the ranks")
-    ap.add_argument("--alt-shard", type=int, default=1,
-                    help="replica mode, N > 1: also time the sharded strong-scaling encode of "
-                         "one frame over the N ranks (reported under 'sharded')")
+    ap.add_argument("--mode", choices=("shard", "shard-sync", "replica"), default="shard",
+                    help="N > 1: shard = every frame's pass groups split over the ranks, "
+                         "streamed (ShardStream; BASELINE config 2 as written); shard-sync = the "
+                         "same one frame at a time (encode_sharded); replica = every rank "
+                         "streams its own frames (frame-level data parallelism)")
+    ap.add_argument("--alt-replica", type=int, default=1,
+                    help="shard mode, N > 1: also time frame replicas (reported under "
+                         "'replicas')")
+    ap.add_argument("--distinct", type=int, default=2,
+                    help="distinct synthetic frames the steps cycle through")
     ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
                     help="shard mode: strong = ONE frame of the config split over the N ranks "
                          "(BASELINE config 2 as written); weak = a frame of N stacked config "
@@ -251,57 +262,43 @@ def main():
         else:
             dist.init_process_group(backend)
     name, w, h, nframes = CONFIGS[args.config]
-    shard0 = world > 1 and args.mode == "shard"
-    shard = shard0
-    strong = shard and args.scaling == "strong"
+    sharded_mode = world > 1 and args.mode in ("shard", "shard-sync")
+    strong = sharded_mode and args.scaling == "strong"
+    fh = h if strong or not sharded_mode else h * world
     # inputs generated on the device (jxg_synth_rgb8_device: the bytes of
-    # jxg.synth.synth_rgb8, without minutes of numpy at 8K / 16K)
-    d_img = synth_rgb8_device(w, h, SEED_BASE + args.config + (0 if shard else rank), local)
-    img = d_img.cpu().numpy() if world == 1 else None  # quality probe / CPU baseline
-    # batch configs (64 x 1080p): a step is the whole batch of distinct frames,
-    # device-resident
-    frames = 1 if shard else nframes
-    d_imgs = [d_img] + [synth_rgb8_device(w, h, SEED_BASE + args.config + f, local)
-                        for f in range(1, frames)]
-    pipeline = not shard and not args.no_pipeline
-    ptrs = [t.data_ptr() for t in d_imgs]
-    fh = h
-    if shard and not strong:
-        # one frame of N stacked config frames: every rank owns 1/N of its groups
-        fh = h * world
-        d_img = d_img.repeat(world, 1, 1).contiguous()
+    # jxg.synth.synth_rgb8, without minutes of numpy at 8K / 16K).  Every rank
+    # of a sharded run holds the same frames; replicas get their own.  Batch
+    # configs (64 x 1080p): a step is the whole batch of distinct frames.
+    def make_frames(sharded):
+        per_step = 1 if sharded else nframes
+        n = per_step * max(1, args.distinct) if per_step == 1 else per_step
+        seed0 = SEED_BASE + args.config + (0 if sharded else 1000 * rank)
+        out = []
+        for f in range(n):
+            t = synth_rgb8_device(w, h, seed0 + (f if per_step > 1 else 100 * f), local)
+            if sharded and not strong:
+                # one frame of N stacked config frames: every rank owns 1/N of its groups
+                t = t.repeat(world, 1, 1).contiguous()
+            out.append(t)
+        return per_step, out
+
+    img = None
+    if world == 1:  # quality probe / CPU baseline: the first frame
+        img = synth_rgb8_device(w, h, SEED_BASE + args.config, local).cpu().numpy()
     torch.cuda.synchronize()
 
-    def run(coder, nstreams, proposals=None, as_shard=None, pipe=None):
-        """Warm up, then time args.steps frames over `nstreams` concurrent
-        encoders (one host thread, context and HIP stream each)."""
-        nonlocal shard, pipeline, frames, d_img
-        pipe_saved = pipeline
-        if pipe is not None:
-            pipeline = pipe
-        if as_shard is not None:  # the sharded strong-scaling line of a replica run
-            shard, pipeline, frames = as_shard, False, 1
-            d_img = synth_rgb8_device(w, h, SEED_BASE + args.config, local)
+    def run(mode, coder, nstreams=1, proposals=None, pipe=True):
+        """Warm up, then time args.steps steps of `mode` ("frames": each rank
+        encodes whole frames -- N = 1 / replicas; "shard": ShardStream;
+        "shard-sync": encode_sharded)."""
+        sharded = mode != "frames"
+        per_step, d_imgs = make_frames(sharded)
+        nd = len(d_imgs)
         flags = jxg.FLAG_ANS if coder == "ans" else 0
         props = args.proposals if proposals is None else proposals
         encs = [jxg.Encoder(distance=args.distance, effort=args.effort,
                             proposals=props, device=local, flags=flags)
                 for _ in range(nstreams)]
-        bufs = {}
-        host = None
-        if shard and args.assembly == "host":
-            from jxg.dist import SharedHostBuffer
-            if SharedHostBuffer.single_node():
-                host = SharedHostBuffer(rank, world)
-            # else: ranks on several nodes -> device assembly (payload gather)
-
-        def step(e, k=0):
-            if shard:
-                from jxg.dist import encode_sharded
-                return encode_sharded(e, d_img, w, fh, rank, world, bufs=bufs, copy=False,
-                                      host=host)
-            return e.encode_device(d_imgs[k % frames].data_ptr(), w, fh, copy=False)
-
         rec = {"front_ms": [], "host_ms": [], "sizes": [], "last": None}
 
         def took(e, k, out):
@@ -309,42 +306,66 @@ def main():
             rec["front_ms"].append(t[0])
             rec["host_ms"].append(t[1:])
             rec["sizes"].append(len(out) if out is not None else 0)
-            if k % frames == 0:
+            if k % nd == 0:
                 rec["last"] = out
 
+        ss = None
+        host = None
+        bufs = {}
+        if mode == "shard":
+            from jxg.dist import ShardStream
+            ss = ShardStream(encs[0], w, fh, rank, world)
+        elif mode == "shard-sync" and args.assembly == "host":
+            from jxg.dist import SharedHostBuffer
+            if SharedHostBuffer.single_node():
+                host = SharedHostBuffer(rank, world)
+            # else: ranks on several nodes -> device assembly (payload gather)
+
         def worker(e, ks):
-            # the codestream ends in (pinned) host memory; ctypes calls release
-            # the GIL, so the encoders' host work and HIP streams overlap
-            if pipeline:
+            # the codestream ends in (pinned / shared) host memory; ctypes
+            # calls release the GIL, so several encoders' host work overlaps
+            if ss is not None:
+                got = 0
+                for k in ks:
+                    ss.submit(d_imgs[k % nd].data_ptr())
+                    while ss.pending() > ss.depth:
+                        took(e, got, ss.receive())
+                        got += 1
+                while ss.pending():
+                    took(e, got, ss.receive())
+                    got += 1
+            elif mode == "shard-sync":
+                from jxg.dist import encode_sharded
+                for k in ks:
+                    took(e, k, encode_sharded(e, d_imgs[k % nd], w, fh, rank, world, bufs=bufs,
+                                              copy=False, host=host))
+            elif pipe:
                 # streaming entry points: submit every frame, receive each
                 # codestream as soon as it is done (more than the library's
                 # pipeline depth pending => the oldest is complete)
                 got = 0
                 for k in ks:
-                    e.submit_device(d_imgs[k % frames].data_ptr(), w, fh)
+                    e.submit_device(d_imgs[k % nd].data_ptr(), w, h)
                     while e.pending() > 16:
                         took(e, got, e.receive(copy=False))
                         got += 1
                 while e.pending():
                     took(e, got, e.receive(copy=False))
                     got += 1
-                return
-            for k in ks:
-                took(e, k, step(e, k))
+            else:
+                for k in ks:
+                    took(e, k, e.encode_device(d_imgs[k % nd].data_ptr(), w, h, copy=False))
 
         for e in encs:  # contexts warmed one after another
-            if pipeline:
-                # at least 16 frames: every lane of the library's pipeline (up
-                # to 12) allocates its buffers on its first frame, which must
-                # not land in the timed region
-                worker(e, range(max(max(args.warmup, 1) * frames, 16)))
-            else:
-                for _ in range(args.warmup):
-                    step(e)
+            # at least 16 frames when streaming: every lane of the library's
+            # pipeline (up to 12) allocates its buffers on its first frame,
+            # which must not land in the timed region
+            nw = max(args.warmup, 1) * per_step
+            worker(e, range(max(nw, 16) if (pipe or ss is not None) else args.warmup * per_step))
         for key in ("front_ms", "host_ms", "sizes"):
             rec[key] = []
 
-        total = args.steps * frames
+        total = args.steps * per_step
         share = [list(range(i, total, nstreams)) for i in range(nstreams)]
         if world > 1:
             dist.barrier()
@@ -364,93 +385,109 @@ def main():
             dist.barrier()
         dt = time.perf_counter() - t0
         if world > 1:
-            tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+            tt = torch.tensor([dt], dtype=torch.float64,
+                              device="cpu" if backend == "gloo" else dev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             dt = float(tt.item())
         rec["dt"] = dt
+        rec["per_step"] = per_step
         rec["st"] = encs[0].stats()
         last = rec["last"]
         rec["last"] = last.tobytes() if hasattr(last, "tobytes") else last
+        if ss is not None:
+            ss.close()
         for e in encs[1:]:
             e.close()
         rec["enc"] = encs[0]
         if host is not None:
             dist.barrier()
             host.close()
-        pipeline = pipe_saved
+        rec["depth"] = ss.depth if ss is not None else None
         return rec
 
-    nstreams = 1 if shard else max(1, args.streams)
-    R = run(args.coder, nstreams)
+    if world == 1 or args.mode == "replica":
+        mode = "frames"
+    else:
+        mode = args.mode
+    pipeline = mode == "frames" and not args.no_pipeline
+    nstreams = 1 if mode != "frames" else max(1, args.streams)
+    R = run(mode, args.coder, nstreams, pipe=pipeline)
     dt, front_ms, host_ms, st = R["dt"], R["front_ms"], R["host_ms"], R["st"]
+    per_step = R["per_step"]
     nbytes = R["sizes"][-1] if R["sizes"] else 0
-    px_step = w * fh * (1 if shard else world) * frames
+    # pixels of one step over the whole job
+    px_step = w * fh * per_step * (1 if mode != "frames" else world)
     alt = None
     other = "prefix" if args.coder == "ans" else "ans"
-    if not shard and args.alt_coder > 0:
+    if mode == "frames" and args.alt_coder > 0:
         # the same workload with the other AC entropy coder
-        A = run(other, nstreams)
+        A = run("frames", other, nstreams, pipe=pipeline)
         A["enc"].close()
         alt = {"coder": other, "streams_per_gpu": nstreams, "pipeline": pipeline,
                "value": round(px_step * args.steps / A["dt"] / 1e6, 2),
                "ms_per_step": round(A["dt"] * 1e3 / args.steps, 3),
                "ms_latency": round(sum(x[0] for x in A["host_ms"]) / len(A["host_ms"]), 3),
                "bytes_per_frame": A["sizes"][-1],
-               "bpp": round(A["sizes"][-1] * 8.0 / (w * fh), 4)}
-    sharded = None
-    if world > 1 and not shard and args.alt_shard:
-        # the same frame's groups split over the N ranks (strong scaling,
-        # one frame per step, SURVEY §8e exchange + host assembly)
-        S = run(args.coder, 1, as_shard=True)
+               "bpp": round(A["sizes"][-1] * 8.0 / (w * h), 4)}
+    replicas = None
+    if mode != "frames" and args.alt_replica:
+        # every rank streams its own frames (frame-level data parallelism)
+        P = run("frames", args.coder, 1, pipe=True)
         if rank == 0:
-            sharded = {"mode": "shard", "scaling": "strong", "coder": args.coder,
-                       "value": round(w * h * args.steps / S["dt"] / 1e6, 2),
-                       "ms_per_step": round(S["dt"] * 1e3 / args.steps, 3),
-                       "bytes_per_frame": S["sizes"][-1]}
-        S["enc"].close()
-        shard, pipeline, frames = False, not args.no_pipeline, nframes
+            replicas = {"mode": "replica", "scaling": "weak", "coder": args.coder,
+                        "value": round(w * h * world * args.steps / P["dt"] / 1e6, 2),
+                        "ms_per_step": round(P["dt"] * 1e3 / args.steps, 3),
+                        "bytes_per_frame": P["sizes"][-1]}
+        P["enc"].close()
     iso = None
-    if pipeline:
-        # the kernels alone on the GPU (one-at-a-time encodes, same coder): the
-        # front kernel's roofline, the rANS chain kernel's duration
-        iso = run(args.coder, 1, pipe=False)
+    if mode == "frames" and pipeline or mode == "shard":
+        # the kernels alone on the GPU (one-at-a-time encodes of this rank's
+        # frame, same coder): the front kernel's roofline, the rANS chain
+        # kernel's duration
+        iso = run("frames", args.coder, 1, pipe=False)
         iso["enc"].close()
     thesis = None
-    if not shard and args.alt_thesis and args.proposals != 3:
+    if mode == "frames" and args.alt_thesis and args.proposals != 3:
         # the thesis proposals P + F (combined.diff) on the same workload:
         # the homogeneity selector in the front kernel, hook F on every
         # 8x8 and merge candidate
-        T = run(args.coder, nstreams, proposals=3)
+        T = run("frames", args.coder, nstreams, proposals=3, pipe=pipeline)
         T["enc"].close()
         thesis = {"proposals": "P+F (combined.diff)",
                   "value": round(px_step * args.steps / T["dt"] / 1e6, 2),
                   "ms_per_step": round(T["dt"] * 1e3 / args.steps, 3),
                   "ms_front_kernel": round(sum(T["front_ms"]) / len(T["front_ms"]), 4),
                   "bytes_per_frame": T["sizes"][-1],
-                  "bpp": round(T["sizes"][-1] * 8.0 / (w * fh), 4)}
+                  "bpp": round(T["sizes"][-1] * 8.0 / (w * h), 4)}
     if rank == 0:
         ms_step = dt * 1e3 / args.steps
-        frame_px = w * fh
         value = px_step * args.steps / dt / 1e6
-        # roofline of the front kernel over this rank's launch (its tiles)
-        fw, fhh = (w, fh // world) if shard else (w, fh)
+        # roofline of the front kernel: the isolated one-at-a-time launch over
+        # a whole frame (the kernel alone on the GPU)
+        fw, fhh = w, h
         fb = front_bytes_survey(fw, fhh)
         fms_pipe = sum(front_ms) / len(front_ms)
         fms = sum(iso["front_ms"]) / len(iso["front_ms"]) if iso else fms_pipe
+        if not iso and mode != "frames":
+            fb = front_bytes_survey(w, fh) / world  # this rank's share of the frame
         achieved = fb / (fms * 1e-3) / 1e9 if fms > 0 else 0.0
         coder_desc = "%s-coded" % args.coder
-        if shard:
-            workload = ("%s: %dx%d RGB8 (synth_rgb8%s), VarDCT d%g e%d, proposals=%d, %s, "
-                        "256x256 groups sharded over %d ranks (%s scaling), %s assembly"
-                        % (name, w, fh, "" if strong else ", config frame stacked %d times" % world,
-                           args.distance, args.effort, args.proposals, coder_desc, world,
-                           args.scaling, args.assembly))
+        distinct = max(1, args.distinct) if per_step == 1 else per_step
+        if mode != "frames":
+            workload = ("%s: %dx%d RGB8 (synth_rgb8, %d distinct frames cycled), VarDCT d%g e%d, "
+                        "proposals=%d, %s, 256x256 groups sharded over %d ranks (%s scaling; "
+                        "partition kind %d), %s"
+                        % (name, w, fh, distinct, args.distance, args.effort, args.proposals,
+                           coder_desc, world, args.scaling, jxg.shard_plan(w, fh, world)[2],
+                           "streamed (jxg.dist.ShardStream, %d frames in flight per rank, heads "
+                           "and sections through /dev/shm)" % R["depth"] if mode == "shard" else
+                           "one frame at a time (encode_sharded), %s assembly" % args.assembly))
             par = "group-shard%d" % world
         else:
             workload = ("%s %dx%d RGB8 (synth_rgb8), VarDCT d%g e%d, proposals=%d, %s, "
-                        "%d distinct frame(s) per step, %s"
+                        "%d frame(s) per step, %d distinct frames cycled, %s"
                         % (name, w, h, args.distance, args.effort, args.proposals, coder_desc,
-                           frames, "streaming entry points (jxg_submit_rgb8_device / "
+                           per_step, distinct, "streaming entry points (jxg_submit_rgb8_device / "
                            "jxg_receive, one host thread)" if pipeline else
                            "%d concurrent encoder stream(s) per rank" % nstreams))
             par = "frame-dp%d" % world
@@ -466,17 +503,18 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 3),
             "higher_is_better": True,
-            "scaling": "strong" if strong else "weak",
+            "scaling": "strong" if strong or world == 1 else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
-            "config": {"workload": workload, "global_batch": 1 if shard else world * frames,
+            "config": {"workload": workload,
+                       "global_batch": per_step * (1 if mode != "frames" else world),
                        "parallelism": par},
             "streams_per_gpu": nstreams,
-            "pipeline": pipeline,
+            "pipeline": pipeline or mode == "shard",
             "ms_latency": round(sum(x[0] for x in host_ms) / len(host_ms), 3),
             "bytes_per_frame": nbytes,
-            "bpp": round(nbytes * 8.0 / frame_px, 4),
+            "bpp": round(nbytes * 8.0 / (w * fh), 4) if mode == "frames" or rank == 0 else None,
             "stages_ms": {k: round(st[k], 4) for k in ("ms_front_kernel", "ms_front",
                                                        "ms_histogram", "ms_emit",
                                                        "ms_assemble", "ms_total")},
@@ -485,17 +523,20 @@ def main():
             "roofline": {"kernel": "front_kernel", "bound": "hbm",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": load_pmc_traffic(name) if world == 1 else None,
+                         "traffic": load_pmc_traffic(name),
                          "algorithmic_bytes": int(fb),
                          "bytes_per_px": SURVEY_BYTES_PER_PX,
                          "design_bytes": front_bytes_design(fw, fhh, args.effort),
                          "avg_ms": round(fms, 4),
                          # the kernel is VALU-bound (the six-candidate 8x8 search):
                          # its PMC VALU issue rate beside the HBM fraction
-                         "valu_issue_frac_pmc": load_front_valu(name) if world == 1 else None,
-                         "measured": ("one-at-a-time encodes (the kernel alone on the GPU); "
-                                      "under the pipeline, sharing the GPU with rANS chains: "
-                                      "%.4f ms" % fms_pipe) if iso else "timed region"},
+                         "valu_issue_frac_pmc": load_front_valu(name),
+                         "measured": ("one-at-a-time encodes of a whole frame (the kernel alone "
+                                      "on the GPU, HIP events on its stream); in the timed run "
+                                      "(sharing the GPU with rANS chains%s): %.4f ms"
+                                      % ("" if mode == "frames" else
+                                         ", this rank's 1/%d of the frame" % world, fms_pipe))
+                         if iso else "timed region"},
             # the merge stage is latency-bound (VALU issue 35 %, waves waiting
             # on memory / LDS 41 % of their lifetime): its live time and the
             # PMC-measured VALU issue rate
@@ -503,7 +544,7 @@ def main():
                             "bound": "latency",
                             "avg_ms": round((iso["st"] if iso else st)["ms_front"] -
                                             (iso["st"] if iso else st)["ms_front_kernel"], 4),
-                            "valu_issue_frac_pmc": load_merge_pmc(name) if world == 1 else None},
+                            "valu_issue_frac_pmc": load_merge_pmc(name)},
         }
         if iso is not None and args.coder == "ans":
             # the rANS chain: one serial state recurrence per pass group (the
@@ -521,8 +562,8 @@ def main():
             res["alt_coder"] = alt
         if thesis is not None:
             res["thesis_proposals"] = thesis
-        if sharded is not None:
-            res["sharded"] = sharded
+        if replicas is not None:
+            res["replicas"] = replicas
         if world == 1 and not args.no_quality:
             res["quality"] = quality_probe(R["enc"], img, args.distance, args.effort)
         if world == 1 and not args.no_cpu_baseline:

@@ -13,6 +13,20 @@
  * Conventions: status 0 = OK, negative on error (never aborts); one context
  * per host thread; device memory is owned by the context; output buffers are
  * allocated by the library and released with jxg_buffer_free.
+ *
+ * Device inputs (jxg_encode_rgb8_device, jxg_submit_rgb8_device,
+ * jxg_shard_submit_device, jxg_shard_begin, jxg_compare_rgb8_device) are
+ * read on the library's own HIP streams.  Either the caller's writes to them
+ * are complete before the call (e.g. hipStreamSynchronize of the producing
+ * stream), or the caller names its producing stream with
+ * jxg_set_input_stream: every later device-input call then orders its reads
+ * after all work submitted to that stream so far (an event recorded on it,
+ * waited on by the library's stream -- no host synchronisation).
+ *
+ * A context with streamed frames pending (jxg_pending > 0) serves them as a
+ * pipeline lane: the one-at-a-time, batch, sharded-begin/end, homogeneity
+ * and compare entry points return JXG_ERR_INVALID_ARG until they are
+ * received.
  */
 #ifndef JXG_H_
 #define JXG_H_
@@ -83,6 +97,9 @@ typedef struct {
 const char* jxg_status_str(jxg_status s);
 jxg_status jxg_create(const jxg_params* params, void** ctx);
 void jxg_destroy(void* ctx);
+/* the caller's stream (hipStream_t) that produces device inputs; NULL: none
+ * (writes complete before each call) -- see the conventions above */
+jxg_status jxg_set_input_stream(void* ctx, void* stream);
 
 /* host RGB8 (interleaved, row_stride bytes per row) -> codestream */
 jxg_status jxg_encode_rgb8(void* ctx, const uint8_t* rgb, uint32_t xsize, uint32_t ysize,
@@ -111,7 +128,10 @@ jxg_status jxg_encode_batch_rgb8_device(void* ctx, const void* const* d_rgbs, ui
  * of each frame).  Internally a software pipeline over this context and up to
  * 11 lanes it creates on first use (same parameters; released by
  * jxg_destroy); the depth D follows the frame size (7 lanes at 8K, 12 at 4K
- * and below): a submit finishes the frame submitted D calls earlier if it is
+ * and below; jxg_pipeline_depth), never more than the process's hardware
+ * queues - 1 (GPU_MAX_HW_QUEUES, HIP's default 4: raise it, at most 32,
+ * before HIP initialises for the full depth -- two lanes on one queue
+ * serialise their kernels): a submit finishes the frame submitted D calls earlier if it is
  * still in flight, launches the new frame's front end / merge stage /
  * statistics on a free lane, starts the previous frame's codes on a helper
  * thread and joins the codes of the frame `lag` submits back (1 at 8K, 3 for
@@ -131,14 +151,24 @@ jxg_status jxg_submit_rgb8_device(void* ctx, const void* d_rgb, uint32_t xsize, 
                                   size_t row_stride);
 jxg_status jxg_receive(void* ctx, jxg_buffer* out);
 jxg_status jxg_pending(void* ctx, uint32_t* n);
+/* lanes of the streaming pipeline for frames of this size (world == 1) or for
+ * this rank's shard of them (jxg_shard_submit_device) */
+jxg_status jxg_pipeline_depth(void* ctx, uint32_t xsize, uint32_t ysize, uint32_t rank,
+                              uint32_t world, uint32_t* depth);
 jxg_status jxg_get_stats(void* ctx, jxg_stats* stats);
 void jxg_buffer_free(jxg_buffer* buf);
 
 /* ---- multi-GPU group sharding (one context per rank) ----
- * A frame is split into `world` balanced contiguous raster ranges of 256x256
- * pass groups (rank r: groups [n*r/world, n*(r+1)/world)); every LF group
- * (2048x2048) has one owner rank, the one holding most of its pass groups
- * (near ties spread over ranks), which encodes its LF-group stream.  Per rank:
+ * A frame's 256x256 pass groups are split over `world` ranks (jxg_shard_plan):
+ *   kind 0: balanced contiguous raster ranges (rank r: [n*r/world,
+ *           n*(r+1)/world)), every LF group (2048x2048) owned by the rank of
+ *           most of its pass groups, when that leaves no LF group split over
+ *           ranks (16384^2 over 8);
+ *   kind 1: else whole LF groups per rank (largest first to the least-loaded
+ *           rank) when the largest load is within 5 % of the mean (8K over
+ *           2 / 4 / 8): no per-block records move;
+ *   kind 2: else the ranges of kind 0 with the record exchange below.
+ * The owner of an LF group encodes its LF-group stream.  Per rank:
  *   1. jxg_shard_sizes: words of the AC histogram and the byte capacity of
  *      the record send / receive buffers (the largest of any rank);
  *      jxg_shard_exchange: this rank's send and receive bytes per peer;
@@ -147,23 +177,34 @@ void jxg_buffer_free(jxg_buffer* buf);
  *      and, into d_xbuf (device), the per-block records (strategy, quant
  *      field, quantized DC; 14 KB per pass group) of its groups whose LF group
  *      another rank owns, ordered by destination rank;
- *   -- caller: all-reduce(sum) d_hist; all_to_all of the records with the
- *      jxg_shard_exchange splits (RCCL over xGMI) into a receive buffer;
+ *   -- caller: prefix codes only, all-reduce(sum) d_hist (ANS: nothing, see
+ *      below); all_to_all of the records with the jxg_shard_exchange splits
+ *      (RCCL over xGMI) into a receive buffer (kinds 0 / 1: all splits 0);
  *   3. jxg_shard_end(d_hist, receive buffer): LF-group streams of its LF
- *      groups, prefix codes from the global histogram, emission of the
- *      rank's sections into a payload kept in device memory (rank 0's also
- *      carries LfGlobal and HfGlobal); jxg_shard_payload copies it
- *      (payload_bytes) to device or host memory;
+ *      groups, entropy codes, emission of the rank's sections into a payload
+ *      kept in device memory (rank 0's also carries LfGlobal, and HfGlobal
+ *      with prefix codes); jxg_shard_payload copies it (payload_bytes) to
+ *      device or host memory;
  *   -- caller: gather the payloads on rank 0 (RCCL, device to device);
  *   4. jxg_shard_assemble_device (rank 0): payloads in device memory (word
  *      aligned offsets) -> codestream in host memory; or jxg_shard_assemble:
- *      the same from host payloads, host only (no device).  Both are
- *      byte-identical to jxg_encode_rgb8 of the whole frame.
- * At 16384^2 over 8 ranks every LF group lies inside one rank's range: no
- * records move.  The frame needs at least max(2, world) pass groups.
+ *      the same from host payloads, host only (no device).
+ * Prefix codes (one HF preset from the summed histogram): payload heads of
+ * version 1, and the codestream is byte-identical to jxg_encode_rgb8 of the
+ * whole frame.  ANS (JXG_FLAG_ANS) with world > 1: every rank clusters its
+ * own histogram into its own HF preset, so d_hist needs NO all-reduce; the
+ * payload head is version 2 and carries the preset, HfGlobal is written at
+ * assembly with num_hf_presets = world, and every pass group selects its
+ * rank's preset -- the codestream decodes to exactly the single-GPU image
+ * (same coefficients, strategies, quant field, DC, CfL), but its bytes differ
+ * from jxg_encode_rgb8's.  The frame needs at least max(2, world) pass groups.
  * Codestreams are released with jxg_buffer_free. */
 jxg_status jxg_shard_sizes(uint32_t xsize, uint32_t ysize, uint32_t world, size_t* hist_words,
                            size_t* slot_bytes);
+/* the partition: owner rank of every pass group ([num_groups]) and LF group
+ * ([num_lf_groups]), and its kind (0 / 1 / 2 above); any pointer may be NULL */
+jxg_status jxg_shard_plan(uint32_t xsize, uint32_t ysize, uint32_t world, uint32_t* group_owner,
+                          uint32_t* lf_owner, int* kind);
 jxg_status jxg_shard_exchange(uint32_t xsize, uint32_t ysize, uint32_t world, uint32_t rank,
                               size_t* send_bytes /* [world] */, size_t* recv_bytes /* [world] */);
 jxg_status jxg_shard_begin(void* ctx, const void* d_rgb, uint32_t xsize, uint32_t ysize,
@@ -190,6 +231,28 @@ jxg_status jxg_shard_assemble(const uint8_t* const* payloads, const size_t* size
  * codestream, byte-identical to jxg_shard_assemble_device. */
 jxg_status jxg_shard_head(void* ctx, uint32_t* dst, size_t* nwords);
 jxg_status jxg_shard_write_host(void* ctx, const uint32_t* const* heads, const size_t* head_words,
+                                uint32_t n, void* dst, size_t dst_size, size_t* total);
+/* Streaming sharded encode (the multi-GPU pipeline; kinds 0 / 1 with ANS, or
+ * world == 1): every rank submits its shard of consecutive frames, in the
+ * same order, through the same lanes as jxg_submit_rgb8_device -- front end,
+ * merge stage, statistics, codes and rANS chains of several frames overlap,
+ * with no collective inside a frame.  For each frame, in submission order:
+ *   jxg_shard_next_head: waits until the oldest pending frame's sections are
+ *     emitted and exports its payload head (dst NULL -> *nwords = size; the
+ *     frame stays pending);
+ *   -- caller: all-gather the heads (any collective);
+ *   jxg_shard_write_next: as jxg_shard_write_host for that frame (its
+ *     sections D2H into the shared host buffer at their codestream offsets,
+ *     rank 0 adds headers + TOC), then releases its lane.
+ * A frame's codestream is complete once every rank's write has returned.  At
+ * most jxg_pipeline_depth frames may be pending (submit returns
+ * JXG_ERR_INVALID_ARG when full; JXG_ERR_UNSUPPORTED for a plan needing the
+ * record exchange or, with world > 1, for prefix codes).  The frame's device
+ * RGB8 must stay unchanged until its write. */
+jxg_status jxg_shard_submit_device(void* ctx, const void* d_rgb, uint32_t xsize, uint32_t ysize,
+                                   size_t row_stride, uint32_t rank, uint32_t world);
+jxg_status jxg_shard_next_head(void* ctx, uint32_t* dst, size_t* nwords);
+jxg_status jxg_shard_write_next(void* ctx, const uint32_t* const* heads, const size_t* head_words,
                                 uint32_t n, void* dst, size_t dst_size, size_t* total);
 jxg_status jxg_host_register(void* ptr, size_t size);
 jxg_status jxg_host_unregister(void* ptr);

@@ -38,6 +38,10 @@ constexpr int kAcThreads = 1024;
 struct GroupGeom {
   int bx0, by0, gw, gh;
 };
+// pass group of launch slot i: a shard's group list, or the range g0 + i
+__device__ __forceinline__ uint32_t slot_group(const uint32_t* glist, uint32_t g0, uint32_t i) {
+  return glist ? glist[i] : g0 + i;
+}
 __device__ __forceinline__ GroupGeom group_geom(const AcArgs& a, int g) {
   GroupGeom r;
   const int gx = g % (int)a.gxs, gy = g / (int)a.gxs;
@@ -258,7 +262,7 @@ __global__ __launch_bounds__(kAcThreads) __attribute__((amdgpu_waves_per_eu(8)))
   __shared__ uint32_t sBound, sNtok[3];
   __shared__ uint16_t sNnzCtx[64];
   __shared__ uint8_t sFreqCtx[64];
-  const int g = blockIdx.x + (int)a.g0;
+  const int g = (int)slot_group(a.glist, a.g0, blockIdx.x);
   const GroupGeom G = group_geom(a, g);
   for (int i = threadIdx.x; i < kMaxClusters * kAcTok; i += blockDim.x) sHist[i] = 0;
   if (threadIdx.x < 64) {
@@ -299,7 +303,7 @@ __global__ __launch_bounds__(kAcThreads) __attribute__((amdgpu_waves_per_eu(8)))
   // token iff left_k > 0 -- the serial walk of block_tokens /
   // varblock_slice_tokens, restated.
   uint32_t bound = 0, nt[3] = {0, 0, 0};
-  uint32_t* rec = a.tokens + (uint64_t)(g - (int)a.g0) * kGroupTokStride;
+  uint32_t* rec = a.tokens + (uint64_t)blockIdx.x * kGroupTokStride;
   uint32_t pos = t.valid ? sBase[t.oby * 32 + t.obx] : 0u;
   const int lane = threadIdx.x & 63;
   const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
@@ -421,13 +425,13 @@ __global__ __launch_bounds__(kAcThreads) void ac_emit_kernel(AcArgs a) {
   __shared__ uint32_t sCode[kMaxClusters * kAcTok];
   __shared__ __attribute__((aligned(16))) uint32_t sBits[kEmitLdsWords];
   __shared__ uint32_t sWave[kAcThreads / 64];
-  const int g = blockIdx.x + (int)a.g0;
+  const int g = (int)slot_group(a.glist, a.g0, blockIdx.x);
   for (int i = threadIdx.x; i < kMaxClusters * kAcTok; i += blockDim.x)
     sCode[i] = a.codes[(i / kAcTok) * kAlpha + (i % kAcTok)];
   for (int i = threadIdx.x; i < kEmitLdsWords / 4; i += blockDim.x)
     reinterpret_cast<uint4*>(sBits)[i] = make_uint4(0, 0, 0, 0);
   const uint32_t n = a.ntok[g * 3] + a.ntok[g * 3 + 1] + a.ntok[g * 3 + 2];
-  const uint32_t* rec = a.tokens + (uint64_t)(g - (int)a.g0) * kGroupTokStride;
+  const uint32_t* rec = a.tokens + (uint64_t)blockIdx.x * kGroupTokStride;
   constexpr int kWaves = kAcThreads / 64;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t chunk = ((n + kWaves * 64 - 1) / (kWaves * 64)) * 64;
@@ -482,7 +486,6 @@ __global__ __launch_bounds__(kAcThreads) void ac_emit_kernel(AcArgs a) {
   if (threadIdx.x == 0) a.bits[g] = total;
 }
 
-// groups [a.g0, a.g0 + ngroups)
 // ---------------------------------------------------------------------------
 // ANS: the token records ac_hist wrote in stream order; one lane per group
 // runs the rANS encoder backwards over its records (the stream's only
@@ -542,11 +545,12 @@ __global__ __launch_bounds__(kAnsWaves * 64) void ans_encode_kernel(AnsArgs a) {
   // workgroup, so a workgroup's waves finish at about the same time and the
   // workgroups of short groups free their CUs early
   const uint32_t gi = __builtin_amdgcn_readfirstlane(blockIdx.x * kAnsWaves + (threadIdx.x >> 6));
-  if (gi >= a.g1 - a.g0) return;
-  const uint32_t g = __builtin_amdgcn_readfirstlane(a.order[gi]);
+  if (gi >= a.n) return;
+  const uint32_t slot = __builtin_amdgcn_readfirstlane(a.order[gi]);
+  const uint32_t g = __builtin_amdgcn_readfirstlane(slot_group(a.glist, a.g0, slot));
   __builtin_amdgcn_s_setprio(3);
   const int n = (int)(a.ntok[g * 3] + a.ntok[g * 3 + 1] + a.ntok[g * 3 + 2]);
-  const uint64_t b = (uint64_t)(g - a.g0) * kGroupTokStride;
+  const uint64_t b = (uint64_t)slot * kGroupTokStride;
   // every lane starts from the initial state x = 0x130000
   uint32_t k = 0x130u, v = 0;
   uint32_t rec = (int)lane < min(64, n) ? a.tokens[b + n - 1 - lane] : 0u;
@@ -636,9 +640,9 @@ __global__ __launch_bounds__(kAnsWaves * 64) void ans_encode_kernel(AnsArgs a) {
 __global__ __launch_bounds__(kAcThreads) void ans_emit_kernel(AnsArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t sBits[kAnsEmitLdsWords];
   __shared__ uint32_t sWave[kAcThreads / 64];
-  const uint32_t g = a.g0 + blockIdx.x;
+  const uint32_t g = slot_group(a.glist, a.g0, blockIdx.x);
   const uint32_t n = a.ntok[g * 3] + a.ntok[g * 3 + 1] + a.ntok[g * 3 + 2];
-  const uint64_t b = (uint64_t)(g - a.g0) * kGroupTokStride;
+  const uint64_t b = (uint64_t)blockIdx.x * kGroupTokStride;
   constexpr int kWaves = kAcThreads / 64;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t chunk = ((n + kWaves * 64 - 1) / (kWaves * 64)) * 64;
@@ -695,7 +699,7 @@ __global__ __launch_bounds__(kAcThreads) void ans_emit_kernel(AnsArgs a) {
 }
 
 void launch_ans(const AnsArgs& a, hipStream_t s) {
-  const uint32_t n = a.g1 - a.g0;
+  const uint32_t n = a.n;
   if (!n) return;
   hipLaunchKernelGGL(ans_encode_kernel, dim3((n + kAnsWaves - 1) / kAnsWaves), dim3(kAnsWaves * 64),
                      0, s, a);

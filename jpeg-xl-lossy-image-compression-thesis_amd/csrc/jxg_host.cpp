@@ -491,7 +491,7 @@ struct Ctx {
   DevBuf<uint32_t> hist_ac, bound, ntok, codes_ac, gbits, lfhist, sbound, lfcodes, chunkbits,
       stream_chunks, stream_bits, scratch, scratch_lf, chunks, out, out_ac;
   DevBuf<uint64_t> gbase, chunkoff, stream_base;
-  DevBuf<uint32_t> tile_list;
+  DevBuf<uint32_t> tile_list, glist;  // shard: tile ids, pass groups (non-contiguous plans)
   DevBuf<uint32_t> tokens, tval, ans_state, ans_order;  // ANS coder
   DevBuf<uint8_t> tlen;
   DevBuf<uint8_t> ans_tab;
@@ -523,6 +523,11 @@ struct Ctx {
   std::vector<uint32_t> m_ntok;
   std::vector<float> m_homog;
   jxg_stats stats{};
+  // ordering of device inputs (jxg_set_input_stream): the caller's stream
+  // whose work so far every device-input entry point orders itself after
+  hipStream_t in_stream = nullptr;
+  hipEvent_t ev_in = nullptr;
+  bool owned_lane = false;  // a pipeline / batch lane of another context
   std::unique_ptr<struct Job> job;  // sharded encode in flight (begin -> end)
   std::unique_ptr<struct Pipe> pipe;  // streaming encode (jxg_submit_* / jxg_receive)
   std::vector<uint32_t> payload_head;  // last jxg_shard_end: payload head words
@@ -536,7 +541,7 @@ static std::mutex g_const_mu;  // device __constant__ tables are shared by all c
 // (GPU_MAX_HW_QUEUES); with several contexts their second streams would
 // share queues with other contexts' main streams, so the split assembly
 // (stage_concat_split, second stream) is used by a lone context only.
-static std::atomic<int> g_live_ctx{0};
+static std::atomic<int> g_live_ctx{0};  // caller-created contexts (owned lanes excluded)
 static jxg_status init_constants(Ctx* c) {
   if (c->constants_ready) return JXG_OK;
   std::lock_guard<std::mutex> lock(g_const_mu);
@@ -566,9 +571,18 @@ static jxg_status init_constants(Ctx* c) {
 
 // ---------------------------------------------------------------------------
 // Work plan: which tiles, pass groups and LF groups this context encodes.
-// world == 1: everything.  Sharded: rank r owns the balanced
-// contiguous raster range of pass groups [ngroups*r/world, ngroups*(r+1)/world)
-// (and the 64x64 tiles inside them) and the LF groups shard_map assigns it.
+// world == 1: everything.  Sharded, make_partition:
+//   1. balanced contiguous raster ranges of pass groups (rank r: [n*r/world,
+//      n*(r+1)/world)), each LF group owned by the rank holding most of its
+//      pass groups -- kept when that needs no record exchange (16384^2 over 8
+//      ranks: LF-group rows fall on range boundaries);
+//   2. otherwise whole LF groups per rank, when they balance: LF groups
+//      assigned largest first (pixel area) to the least-loaded rank, kept if
+//      the largest rank load is within 5 % of the mean (8K over 2 / 4 / 8
+//      ranks: 1.1 %) -- every rank then owns the LF groups of all its pass
+//      groups, so no per-block records move between ranks and a rank's frames
+//      need no collective until assembly (the streaming shard pipeline);
+//   3. else the ranges of 1 with the record exchange.
 // ---------------------------------------------------------------------------
 static uint32_t shard_g0(uint32_t ngroups, uint32_t r, uint32_t world) {
   return (uint32_t)(((uint64_t)ngroups * r) / world);
@@ -582,12 +596,11 @@ static uint32_t shard_of(uint32_t ngroups, uint32_t g, uint32_t world) {
 static uint32_t lf_of_group(const Frame& f, uint32_t g) {
   return ((g / f.gxs) / 8) * f.lfxs + (g % f.gxs) / 8;
 }
-// LF-group owners: the rank holding the most of the LF group's pass groups,
-// less 16 per LF group already assigned to it (so near ties -- an LF group
-// split over ranks' row ranges -- spread over ranks instead of piling onto
-// one); ties go to the lower rank.  An LF group inside one rank's range
-// (16384^2 over 8 ranks: every one) stays with it: nothing to exchange.
-static std::vector<uint32_t> lf_owners(const Frame& f, uint32_t world) {
+// LF-group owners under the contiguous ranges: the rank holding the most of
+// the LF group's pass groups, less 16 per LF group already assigned to it (so
+// near ties -- an LF group split over ranks' row ranges -- spread over ranks
+// instead of piling onto one); ties go to the lower rank.
+static std::vector<uint32_t> lf_owners_ranges(const Frame& f, uint32_t world) {
   std::vector<uint32_t> own(f.nlf, 0), nassigned(world, 0), cnt(world);
   if (world == 1) return own;
   for (uint32_t lg = 0; lg < f.nlf; lg++) {
@@ -611,58 +624,118 @@ static std::vector<uint32_t> lf_owners(const Frame& f, uint32_t world) {
   }
   return own;
 }
+struct Partition {
+  std::vector<uint32_t> group;  // [ngroups] owner rank of each pass group
+  std::vector<uint32_t> lf;     // [nlf] owner rank of each LF group
+  int kind = 0;                 // 0 ranges (no exchange), 1 whole LF groups, 2 ranges + exchange
+};
+static Partition make_partition(const Frame& f, uint32_t world) {
+  Partition P;
+  P.group.assign(f.ngroups, 0);
+  P.lf.assign(f.nlf, 0);
+  if (world <= 1) return P;
+  for (uint32_t g = 0; g < f.ngroups; g++) P.group[g] = shard_of(f.ngroups, g, world);
+  P.lf = lf_owners_ranges(f, world);
+  bool exchange = false;
+  for (uint32_t g = 0; g < f.ngroups && !exchange; g++)
+    exchange = P.lf[lf_of_group(f, g)] != P.group[g];
+  if (!exchange) return P;
+  if (f.nlf >= world) {
+    // whole LF groups, largest first (pixel area; ties: lower index) to the
+    // least-loaded rank (ties: lower rank)
+    std::vector<uint64_t> area(f.nlf);
+    uint64_t total = 0;
+    for (uint32_t lg = 0; lg < f.nlf; lg++) {
+      const uint64_t x0 = (uint64_t)(lg % f.lfxs) * 2048, y0 = (uint64_t)(lg / f.lfxs) * 2048;
+      area[lg] = std::min<uint64_t>(2048, f.w - x0) * std::min<uint64_t>(2048, f.h - y0);
+      total += area[lg];
+    }
+    std::vector<uint32_t> order(f.nlf);
+    for (uint32_t i = 0; i < f.nlf; i++) order[i] = i;
+    std::stable_sort(order.begin(), order.end(),
+                     [&](uint32_t a, uint32_t b) { return area[a] > area[b]; });
+    std::vector<uint64_t> load(world, 0);
+    std::vector<uint32_t> lfo(f.nlf, 0);
+    for (uint32_t lg : order) {
+      uint32_t r = 0;
+      for (uint32_t q = 1; q < world; q++)
+        if (load[q] < load[r]) r = q;
+      lfo[lg] = r;
+      load[r] += area[lg];
+    }
+    const uint64_t most = *std::max_element(load.begin(), load.end());
+    const uint64_t least = *std::min_element(load.begin(), load.end());
+    if (least > 0 && most * 100 * world <= total * 105) {
+      P.lf = lfo;
+      for (uint32_t g = 0; g < f.ngroups; g++) P.group[g] = lfo[lf_of_group(f, g)];
+      P.kind = 1;
+      return P;
+    }
+  }
+  P.kind = 2;
+  return P;
+}
 // Record exchange of rank `rank`: send = its groups whose LF group another
 // rank owns, ordered by (destination rank, group); recv = other ranks' groups
 // inside its own LF groups, ordered by (source rank, group).  Counts per peer.
 struct Exchange {
   std::vector<uint32_t> send, recv, nsend, nrecv;
 };
-static Exchange make_exchange(const Frame& f, const std::vector<uint32_t>& owner,
-                              uint32_t rank, uint32_t world) {
+static Exchange make_exchange(const Frame& f, const Partition& part, uint32_t rank,
+                              uint32_t world) {
   Exchange X;
   X.nsend.assign(world, 0);
   X.nrecv.assign(world, 0);
   for (uint32_t p = 0; p < world; p++) {
     if (p == rank) continue;
-    for (uint32_t g = shard_g0(f.ngroups, rank, world); g < shard_g0(f.ngroups, rank + 1, world); g++)
-      if (owner[lf_of_group(f, g)] == p) {
+    for (uint32_t g = 0; g < f.ngroups; g++) {
+      const uint32_t lo = part.lf[lf_of_group(f, g)];
+      if (part.group[g] == rank && lo == p) {
         X.send.push_back(g);
         X.nsend[p]++;
       }
-    for (uint32_t g = shard_g0(f.ngroups, p, world); g < shard_g0(f.ngroups, p + 1, world); g++)
-      if (owner[lf_of_group(f, g)] == rank) {
+      if (part.group[g] == p && lo == rank) {
         X.recv.push_back(g);
         X.nrecv[p]++;
       }
+    }
   }
   return X;
 }
 
 struct Plan {
-  uint32_t rank = 0, world = 1, g0 = 0, g1 = 0;
+  uint32_t rank = 0, world = 1;
+  std::vector<uint32_t> groups; // pass groups, ascending (launch slot i = groups[i])
+  bool contiguous = true;       // groups == [groups[0], groups[0] + size)
   std::vector<uint32_t> tiles;  // shard: owned tile ids (ty * tiles_x + tx)
   std::vector<uint8_t> lf_mine; // shard: [nlf] 1 = owned LF group
   Exchange x;                   // shard: record exchange
   bool owns_lf(uint32_t lg) const { return world == 1 || lf_mine[lg]; }
+  uint32_t g0() const { return groups.empty() ? 0 : groups[0]; }
+  uint32_t ng() const { return (uint32_t)groups.size(); }
 };
 static Plan make_plan(const Frame& f, uint32_t rank, uint32_t world) {
   Plan P;
   P.rank = rank;
   P.world = world;
-  P.g0 = shard_g0(f.ngroups, rank, world);
-  P.g1 = shard_g0(f.ngroups, rank + 1, world);
-  if (world > 1) {
-    for (uint32_t g = P.g0; g < P.g1; g++) {
-      const uint32_t gx = g % f.gxs, gy = g / f.gxs;
-      for (uint32_t ty = gy * 4; ty < std::min(gy * 4 + 4, f.tiles_y); ty++)
-        for (uint32_t tx = gx * 4; tx < std::min(gx * 4 + 4, f.tiles_x); tx++)
-          P.tiles.push_back(ty * f.tiles_x + tx);
-    }
-    const std::vector<uint32_t> owner = lf_owners(f, world);
-    P.lf_mine.resize(f.nlf);
-    for (uint32_t lg = 0; lg < f.nlf; lg++) P.lf_mine[lg] = owner[lg] == rank;
-    P.x = make_exchange(f, owner, rank, world);
+  if (world <= 1) {
+    P.groups.resize(f.ngroups);
+    for (uint32_t g = 0; g < f.ngroups; g++) P.groups[g] = g;
+    return P;
   }
+  const Partition part = make_partition(f, world);
+  for (uint32_t g = 0; g < f.ngroups; g++)
+    if (part.group[g] == rank) P.groups.push_back(g);
+  P.contiguous = P.groups.empty() || P.groups.back() - P.groups.front() + 1 == P.groups.size();
+  for (uint32_t g : P.groups) {
+    const uint32_t gx = g % f.gxs, gy = g / f.gxs;
+    for (uint32_t ty = gy * 4; ty < std::min(gy * 4 + 4, f.tiles_y); ty++)
+      for (uint32_t tx = gx * 4; tx < std::min(gx * 4 + 4, f.tiles_x); tx++)
+        P.tiles.push_back(ty * f.tiles_x + tx);
+  }
+  P.lf_mine.resize(f.nlf);
+  for (uint32_t lg = 0; lg < f.nlf; lg++) P.lf_mine[lg] = part.lf[lg] == rank;
+  P.x = make_exchange(f, part, rank, world);
   return P;
 }
 // exchange record of one pass group (jxg_shard.hip): acs, qf, 3 x int32 DC
@@ -836,14 +909,20 @@ static jxg_status stage_alloc(Ctx* c, Job& J) {
   aa.bxs = f.bxs;
   aa.bys = f.bys;
   aa.gxs = f.gxs;
-  aa.g0 = J.plan.g0;
+  aa.g0 = J.plan.g0();
+  if (!J.plan.contiguous) {
+    JXG_HIP(c->glist.ensure(J.plan.ng()));
+    JXG_HIP(hipMemcpyAsync(c->glist.p, J.plan.groups.data(), J.plan.ng() * 4,
+                           hipMemcpyHostToDevice, s));
+    aa.glist = c->glist.p;
+  }
   aa.hist = c->hist_ac.p;
   aa.bound = c->bound.p;
   aa.ntok = c->ntok.p;
   aa.codes = c->codes_ac.p;
   aa.base = c->gbase.p;
   aa.bits = c->gbits.p;
-  JXG_HIP(c->tokens.ensure((uint64_t)(J.plan.g1 - J.plan.g0) * kGroupTokStride));
+  JXG_HIP(c->tokens.ensure((uint64_t)std::max(1u, J.plan.ng()) * kGroupTokStride));
   aa.tokens = c->tokens.p;
   LfArgs& la = J.la;
   la = LfArgs{};
@@ -955,7 +1034,7 @@ static jxg_status stage_front(Ctx* c, Job& J) {
 // ---- stage C: AC token statistics of the plan's pass groups ----
 static jxg_status stage_ac_stats(Ctx* c, Job& J) {
   JXG_HIP(hipMemsetAsync(c->hist_ac.p, 0, kMaxClusters * kAlpha * 4, c->stream));
-  launch_ac_hist(J.aa, J.plan.g1 - J.plan.g0, c->stream);
+  launch_ac_hist(J.aa, J.plan.ng(), c->stream);
   JXG_HIP(hipGetLastError());
   return JXG_OK;
 }
@@ -1117,7 +1196,7 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
   // codes below
   J.gbase.assign(f.ngroups, 0);
   uint64_t cursor = 0;
-  for (uint32_t g = J.plan.g0; g < J.plan.g1; g++) {
+  for (uint32_t g : J.plan.groups) {
     J.gbase[g] = cursor;
     const uint64_t nt = (uint64_t)c->h_ntok.p[g * 3] + c->h_ntok.p[g * 3 + 1] + c->h_ntok.p[g * 3 + 2];
     // ANS: <= 16 + raw bits per token (prefix: <= 15 + raw) and the 32-bit state
@@ -1133,7 +1212,7 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
   JXG_HIP(c->h_gbase.ensure(J.gbase.size()));
   std::copy(J.gbase.begin(), J.gbase.end(), c->h_gbase.p);
   if (J.ans) {
-    const uint64_t nrec = (uint64_t)(J.plan.g1 - J.plan.g0) * kGroupTokStride;
+    const uint64_t nrec = (uint64_t)std::max(1u, J.plan.ng()) * kGroupTokStride;
     JXG_HIP(c->tval.ensure(nrec));
     JXG_HIP(c->tlen.ensure(nrec));
     JXG_HIP(c->ans_state.ensure(f.ngroups));
@@ -1143,14 +1222,16 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
     // chain workgroup holds groups of similar length and the workgroups of
     // short groups give their CUs (and 68 KB of LDS each) back early -- the
     // kernel still lasts as long as the longest group
-    const uint32_t ng = J.plan.g1 - J.plan.g0;
+    const uint32_t ng = J.plan.ng();
     JXG_HIP(c->h_ans_order.ensure(ng));
     JXG_HIP(c->ans_order.ensure(ng));
     uint32_t* ord = c->h_ans_order.p;
-    for (uint32_t i = 0; i < ng; i++) ord[i] = J.plan.g0 + i;
+    for (uint32_t i = 0; i < ng; i++) ord[i] = i;  // launch slots
     const uint32_t* nt = c->h_ntok.p;
-    std::stable_sort(ord, ord + ng, [nt](uint32_t x, uint32_t y) {
-      return nt[x * 3] + nt[x * 3 + 1] + nt[x * 3 + 2] > nt[y * 3] + nt[y * 3 + 1] + nt[y * 3 + 2];
+    const uint32_t* gl = J.plan.groups.data();
+    std::stable_sort(ord, ord + ng, [nt, gl](uint32_t x, uint32_t y) {
+      const uint32_t gx = gl[x], gy = gl[y];
+      return nt[gx * 3] + nt[gx * 3 + 1] + nt[gx * 3 + 2] > nt[gy * 3] + nt[gy * 3 + 1] + nt[gy * 3 + 2];
     });
     JXG_HIP(hipMemcpyAsync(c->ans_order.p, ord, ng * 4, hipMemcpyHostToDevice, s));
   }
@@ -1160,7 +1241,7 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
   const float ms_ac_codes = ms_since(t_codes);
   J.aa.scratch = c->scratch.p;
   if (!J.ans) {
-    launch_ac_emit(J.aa, J.plan.g1 - J.plan.g0, s);
+    launch_ac_emit(J.aa, J.plan.ng(), s);
     JXG_HIP(hipGetLastError());
     JXG_HIP(hipMemcpyAsync(c->h_gbits.p, c->gbits.p, f.ngroups * 4, hipMemcpyDeviceToHost, s));
     JXG_HIP(hipEventRecord(c->ev[7], s));
@@ -1233,8 +1314,9 @@ static jxg_status stage_emit(Ctx* c, Job& J, bool sync = true) {
     na.base = c->gbase.p;
     na.scratch = c->scratch.p;
     na.bits = c->gbits.p;
-    na.g0 = J.plan.g0;
-    na.g1 = J.plan.g1;
+    na.g0 = J.plan.g0();
+    na.n = J.plan.ng();
+    na.glist = J.aa.glist;
     na.order = c->ans_order.p;
     launch_ans(na, s);
     JXG_HIP(hipGetLastError());
@@ -1292,7 +1374,7 @@ static jxg_status stage_concat(Ctx* c, Job& J, bool full, std::vector<uint32_t>*
   // per-rank presets: every pass group starts with its preset index
   BitWriter sel;
   if (J.presets) sel.put(ceil_log2(J.plan.world), J.plan.rank);
-  for (uint32_t g = J.plan.g0; g < J.plan.g1; g++) {
+  for (uint32_t g : J.plan.groups) {
     if (J.presets)
       sections.push_back({add_chunk(sel), Piece{0, J.gbase[g], c->h_gbits.p[g]}});
     else
@@ -1375,7 +1457,7 @@ static jxg_status stage_concat_split(Ctx* c, Job& J, uint8_t** host_out, size_t*
   hipStream_t s = c->stream, s2 = c->stream2;
   const Frame& f = J.f;
   JXG_HIP(hipEventSynchronize(c->ev[7]));  // AC emission done, its bit counts on the host
-  const uint32_t g0 = J.plan.g0, ng = J.plan.g1 - J.plan.g0;
+  const uint32_t g0 = J.plan.g0(), ng = J.plan.ng();  // (one context: all groups)
   JXG_HIP(c->h_pieces_ac.ensure(std::max<uint32_t>(ng, 1)));
   std::vector<uint32_t> ac_sizes(ng);
   uint64_t dst = 0, max_words = 0;
@@ -1503,21 +1585,36 @@ static jxg_status stage_concat_split(Ctx* c, Job& J, uint8_t** host_out, size_t*
   return JXG_OK;
 }
 
+// Device inputs (jxg_set_input_stream): `lane`'s stream is ordered after the
+// work the caller has submitted to its input stream so far; without an input
+// stream the caller's writes must be complete before the call (include/jxg.h).
+static jxg_status order_input(Ctx* owner, Ctx* lane) {
+  if (!owner->in_stream) return JXG_OK;
+  if (!lane->ev_in && hipEventCreateWithFlags(&lane->ev_in, hipEventDisableTiming) != hipSuccess)
+    return JXG_ERR_HIP;
+  JXG_HIP(hipEventRecord(lane->ev_in, owner->in_stream));
+  JXG_HIP(hipStreamWaitEvent(lane->stream, lane->ev_in, 0));
+  return JXG_OK;
+}
+
 // ---- one frame, in three phases (encode_device runs them back to back; the
 // streaming pipeline interleaves the phases of consecutive frames) ----
 // phase 1: buffers, front end + merge stage + AC / LF statistics and their
 // downloads, all launched asynchronously on the context's stream
+// (rank, world): a shard of a frame whose plan needs no record exchange and,
+// with world > 1, ANS (one HF preset per rank): no collective before assembly
 static jxg_status enc_launch(Ctx* c, Job& J, const uint8_t* d_rgb, uint32_t w, uint32_t h,
-                             size_t stride) {
+                             size_t stride, uint32_t rank = 0, uint32_t world = 1) {
   hipStream_t s = c->stream;
   J.f = make_frame(w, h, c->params.distance);
-  J.plan = make_plan(J.f, 0, 1);
+  J.plan = make_plan(J.f, rank, world);
   J.w = w;
   J.h = h;
   J.stride = stride;
   J.d_rgb = d_rgb;
   jxg_status st = stage_alloc(c, J);
   if (st) return st;
+  J.presets = J.ans && world > 1;
   JXG_HIP(hipEventRecord(c->ev[0], s));
   if ((st = stage_front(c, J))) return st;
   JXG_HIP(hipEventRecord(c->ev[1], s));
@@ -1613,8 +1710,12 @@ static jxg_status enc_finish(Ctx* c, Job& J, bool split, jxg_buffer* out,
   return JXG_OK;
 }
 
+static bool pipe_busy(const Ctx* c);
 static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32_t h,
                                 size_t stride, jxg_buffer* out, Clock::time_point t_call) {
+  // streamed frames in flight use this context as a lane (and its helper
+  // threads its host state): one-at-a-time calls wait until they are received
+  if (pipe_busy(c)) return JXG_ERR_INVALID_ARG;
   Job J;
   jxg_status st = enc_launch(c, J, d_rgb, w, h, stride);
   if (st) return st;
@@ -1665,12 +1766,25 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
 #define JXG_PIPE_CHAIN_GROUPS 3570  // 8K (510 groups): 7 lanes
 #endif
 constexpr uint32_t kPipeMaxLanes = JXG_PIPE_MAX_LANES;
+// Hardware queues of this process (GPU_MAX_HW_QUEUES as HIP read it at start
+// up; HIP's default is 4).  Lanes beyond queues - 1 (one is left for the
+// caller's own stream) would share a queue with another lane and serialise
+// its kernels (5.5 vs 6.7 GPix/s at 8K), so the depth never
+// exceeds it: a caller that wants the full depth raises the variable (at most
+// 32) before HIP initialises, as bench.py and tests/conftest.py do.
+static uint32_t hw_queues() {
+  const char* e = std::getenv("GPU_MAX_HW_QUEUES");
+  const long q = e && *e ? std::strtol(e, nullptr, 10) : 4;
+  return (uint32_t)std::min<long>(32, std::max<long>(1, q));
+}
 static uint32_t pipe_depth(uint32_t ngroups) {
   const uint32_t d = (JXG_PIPE_CHAIN_GROUPS + ngroups - 1) / std::max(1u, ngroups);
-  return std::min(kPipeMaxLanes, std::max((uint32_t)JXG_PIPE_MIN_LANES, d));
+  const uint32_t want = std::min(kPipeMaxLanes, std::max((uint32_t)JXG_PIPE_MIN_LANES, d));
+  return std::max(2u, std::min(want, hw_queues() - 1));
 }
-static uint32_t pipe_lag(uint32_t ngroups) {
-  return ngroups >= 256 ? (uint32_t)JXG_PIPE_LAG_LARGE : (uint32_t)JXG_PIPE_LAG_SMALL;
+static uint32_t pipe_lag(uint32_t ngroups, uint32_t depth) {
+  const uint32_t lag = ngroups >= 256 ? (uint32_t)JXG_PIPE_LAG_LARGE : (uint32_t)JXG_PIPE_LAG_SMALL;
+  return std::max(1u, std::min(lag, depth - 1));
 }
 // JXG_PIPE_PROFILE (experiment builds only): host time per pipeline step,
 // printed by jxg_destroy of the owning context
@@ -1688,6 +1802,7 @@ struct PipeFrame {
   Ctx* lane = nullptr;
   Job J;
   int phase = 1;  // 1: statistics launched; 2: emission launched
+  bool shard = false;
   Clock::time_point t0;
   std::future<jxg_status> codes;  // valid while a helper builds the codes
 };
@@ -1708,15 +1823,27 @@ struct PipeDone {
 struct Pipe {
   std::vector<std::unique_ptr<PipeFrame>> inflight;  // submission order
   std::vector<PipeDone> done;                        // submission order
+  // shard frames whose sections are emitted and payload head built; each
+  // holds its lane (sections in lane->out) until jxg_shard_write_next
+  std::vector<std::unique_ptr<PipeFrame>> ready;
   uint64_t submitted = 0;
+  int mode = 0;  // 1 whole frames, 2 shards (while any frame is pending)
+  uint32_t depth = 0;
 };
+static bool pipe_busy(const Ctx* c) {
+  return c->pipe && (!c->pipe->inflight.empty() || !c->pipe->done.empty() ||
+                     !c->pipe->ready.empty());
+}
 
 static jxg_status ensure_lanes(Ctx* c, uint32_t extra) {
   while (c->lanes.size() < extra) {
     void* lc = nullptr;
     const jxg_status st = jxg_create(&c->params, &lc);
     if (st) return st;
-    c->lanes.emplace_back(static_cast<Ctx*>(lc));
+    Ctx* l = static_cast<Ctx*>(lc);
+    l->owned_lane = true;  // not a caller context (g_live_ctx counts those)
+    g_live_ctx--;
+    c->lanes.emplace_back(l);
   }
   return JXG_OK;
 }
@@ -1727,15 +1854,82 @@ static void pipe_abort(Ctx* c) {
   Pipe& p = *c->pipe;
   for (auto& fr : p.inflight) (void)pipe_join_codes(*fr);
   for (auto& fr : p.inflight) (void)hipStreamSynchronize(fr->lane->stream);
+  for (auto& fr : p.ready) (void)hipStreamSynchronize(fr->lane->stream);
   p.inflight.clear();
+  p.ready.clear();
 }
 
-// oldest frame in flight -> done (on an error the caller aborts the pipe)
+// A rank's sections of a frame (codes built, emission launched) -> payload
+// head (host, lane->payload_head) + body (device, lane->out); the stream is
+// synchronised.
+// payload: "JXGS" | version | rank | world | xsize | ysize | nsections |
+//          nsections x (TOC index, bytes) [| version 2: the rank's HF preset]
+//          | section bytes back to back
+constexpr uint32_t kPayloadMagic = 0x5347584Au;  // "JXGS"
+static jxg_status shard_finish(Ctx* c, Job& J, size_t* payload_bytes) {
+  hipStream_t s = c->stream;
+  JXG_HIP(hipStreamSynchronize(s));  // the emission's bit counts on the host
+  std::vector<uint32_t> ids, sizes;
+  size_t nbytes = 0;
+  jxg_status st;
+  if ((st = stage_concat(c, J, false, &ids, &sizes, nullptr, &nbytes))) return st;
+  std::vector<uint32_t>& hw = c->payload_head;
+  hw.assign(7 + 2 * ids.size(), 0);
+  hw[0] = kPayloadMagic;
+  hw[1] = J.presets ? 2 : 1;
+  hw[2] = J.plan.rank;
+  hw[3] = J.plan.world;
+  hw[4] = J.w;
+  hw[5] = J.h;
+  hw[6] = (uint32_t)ids.size();
+  for (size_t i = 0; i < ids.size(); i++) {
+    hw[7 + 2 * i] = ids[i];
+    hw[8 + 2 * i] = sizes[i];
+  }
+  if (J.presets) {
+    // version 2: the rank's HF preset -- [B][nhist][context map, bytes packed
+    // in words][clustered counts nhist x kAlpha], B = words after B
+    const uint32_t nh = J.nhist_ans, cw = (kAcCtx + 3) / 4;
+    hw.push_back(1 + cw + nh * kAlpha);
+    hw.push_back(nh);
+    const size_t o = hw.size();
+    hw.resize(o + cw, 0);
+    std::memcpy(hw.data() + o, J.pre_ctxmap.data(), kAcCtx);
+    hw.insert(hw.end(), J.pre_counts.begin(), J.pre_counts.end());
+  }
+  c->payload_body = nbytes;
+  *payload_bytes = hw.size() * 4 + nbytes;
+  JXG_HIP(hipStreamSynchronize(s));
+  return JXG_OK;
+}
+
+// oldest frame in flight -> done (a whole frame: assembled, codestream on
+// the host) or ready (a shard: sections emitted, payload head built); on an
+// error the caller aborts the pipe
 static jxg_status pipe_complete_oldest(Ctx* c) {
   Pipe& p = *c->pipe;
   PipeFrame& fr = *p.inflight.front();
   jxg_status st = pipe_join_codes(fr);
   if (!st && fr.phase == 1) st = enc_codes(fr.lane, fr.J, false);
+  if (fr.shard) {
+    size_t bytes = 0;
+    if (!st) st = shard_finish(fr.lane, fr.J, &bytes);
+    if (st) return st;
+    jxg_stats& S = fr.lane->stats;
+    S = jxg_stats{};
+    S.xsize = fr.J.w;
+    S.ysize = fr.J.h;
+    S.num_groups = fr.J.f.ngroups;
+    S.num_lf_groups = fr.J.f.nlf;
+    S.bytes = bytes;
+    S.ms_front_kernel = elapsed(fr.lane->ev[0], fr.lane->ev[5]);
+    S.ms_front = elapsed(fr.lane->ev[0], fr.lane->ev[1]);
+    S.ms_host_codes = fr.J.ms_codes;
+    S.ms_host_call = ms_since(fr.t0);
+    p.ready.push_back(std::move(p.inflight.front()));
+    p.inflight.erase(p.inflight.begin());
+    return JXG_OK;
+  }
   PipeDone d{{nullptr, 0}, {}};
 #ifdef JXG_PIPE_PROFILE
   if (!st) {
@@ -1752,26 +1946,55 @@ static jxg_status pipe_complete_oldest(Ctx* c) {
   return JXG_OK;
 }
 
+// submit one frame (world == 1) or this rank's shard of one frame
 static jxg_status pipe_submit(Ctx* c, const uint8_t* src, bool on_device, uint32_t w,
-                              uint32_t h, size_t stride) {
+                              uint32_t h, size_t stride, uint32_t rank = 0, uint32_t world = 1,
+                              bool shard = false) {
   if (!c->pipe) c->pipe.reset(new (std::nothrow) Pipe());
   if (!c->pipe) return JXG_ERR_OOM;
   Pipe& p = *c->pipe;
-  const uint32_t ngroups = make_frame(w, h, c->params.distance).ngroups;
-  const uint32_t depth = pipe_depth(ngroups), lag = pipe_lag(ngroups);
+  const int mode = shard ? 2 : 1;
+  if (pipe_busy(c) && p.mode != mode) return JXG_ERR_INVALID_ARG;  // one kind at a time
+  const Frame f0 = make_frame(w, h, c->params.distance);
+  uint32_t ngroups = f0.ngroups;
+  if (shard) {
+    if (world < 1 || rank >= world || f0.ngroups < world || (world > 1 && f0.ngroups < 2))
+      return JXG_ERR_INVALID_ARG;
+    // no collective inside the pipeline: no record exchange, and with more
+    // than one rank one HF preset per rank (ANS)
+    const Plan P = make_plan(f0, rank, world);
+    if (!P.x.send.empty() || !P.x.recv.empty() ||
+        (world > 1 && !(c->params.flags & JXG_FLAG_ANS)))
+      return JXG_ERR_UNSUPPORTED;
+    ngroups = P.ng();
+  }
+  const uint32_t depth = pipe_depth(ngroups), lag = pipe_lag(ngroups, depth);
   jxg_status st = ensure_lanes(c, depth - 1);
   if (st) return st;
   const Clock::time_point t0 = Clock::now();
+  // a shard frame holds its lane until its sections are written: the caller
+  // must take one first (jxg_shard_next_head / jxg_shard_write_next)
+  if (shard && p.ready.size() >= depth) return JXG_ERR_INVALID_ARG;
+  p.mode = mode;
+  p.depth = depth;
   // the newest frame's codes on a helper thread, while this thread finishes
   // the oldest frame and launches frame j on another lane
   if (!p.inflight.empty()) {
     PipeFrame* prev = p.inflight.back().get();
     if (prev->phase == 1 && !prev->codes.valid()) {
       const int dev = c->params.device;
-      prev->codes = std::async(std::launch::async, [prev, dev]() {
-        if (hipSetDevice(dev) != hipSuccess) return JXG_ERR_HIP;
-        return enc_codes(prev->lane, prev->J, false);
-      });
+      try {
+        prev->codes = std::async(std::launch::async, [prev, dev]() {
+          if (hipSetDevice(dev) != hipSuccess) return JXG_ERR_HIP;
+          return enc_codes(prev->lane, prev->J, false);
+        });
+      } catch (...) {  // no thread: build the codes on this one
+        if ((st = enc_codes(prev->lane, prev->J, false))) {
+          pipe_abort(c);
+          return st;
+        }
+        prev->phase = 2;
+      }
     }
   }
   auto fail = [&](jxg_status e) {
@@ -1781,22 +2004,24 @@ static jxg_status pipe_submit(Ctx* c, const uint8_t* src, bool on_device, uint32
 #ifdef JXG_PIPE_PROFILE
   const Clock::time_point tc = Clock::now();
 #endif
-  while (p.inflight.size() >= depth)
+  while (!p.inflight.empty() && p.inflight.size() + p.ready.size() >= depth)
     if ((st = pipe_complete_oldest(c))) return fail(st);
   PPROF_ADD(complete, tc);
-  // a lane no frame in flight uses (the lowest index)
+  // a lane no frame in flight (or ready) uses (the lowest index)
   Ctx* L = nullptr;
   for (uint32_t li = 0; li < depth && !L; li++) {
     Ctx* cand = li == 0 ? c : c->lanes[li - 1].get();
     bool used = false;
     for (auto& q : p.inflight) used = used || q->lane == cand;
+    for (auto& q : p.ready) used = used || q->lane == cand;
     if (!used) L = cand;
   }
-  if (!L) return fail(JXG_ERR_INTERNAL);
+  if (!L) return shard ? JXG_ERR_INVALID_ARG : fail(JXG_ERR_INTERNAL);
   std::unique_ptr<PipeFrame> fr(new (std::nothrow) PipeFrame());
   if (!fr) return fail(JXG_ERR_OOM);
   fr->lane = L;
   fr->t0 = t0;
+  fr->shard = shard;
   if (!on_device) {
     // the lane's previous frame has completed, so its staging is free
     const size_t bytes = stride * (h - 1) + (size_t)w * 3;
@@ -1807,11 +2032,13 @@ static jxg_status pipe_submit(Ctx* c, const uint8_t* src, bool on_device, uint32
         hipSuccess)
       return fail(JXG_ERR_HIP);
     src = L->rgb.p;
+  } else if ((st = order_input(c, L))) {
+    return fail(st);
   }
 #ifdef JXG_PIPE_PROFILE
   const Clock::time_point tl = Clock::now();
 #endif
-  if ((st = enc_launch(L, fr->J, src, w, h, stride))) {
+  if ((st = enc_launch(L, fr->J, src, w, h, stride, rank, world))) {
     (void)hipStreamSynchronize(L->stream);
     return fail(st);
   }
@@ -1833,7 +2060,7 @@ static jxg_status pipe_submit(Ctx* c, const uint8_t* src, bool on_device, uint32
 }
 
 static jxg_status pipe_receive(Ctx* c, jxg_buffer* out) {
-  if (!c->pipe) return JXG_ERR_INVALID_ARG;
+  if (!c->pipe || c->pipe->mode != 1) return JXG_ERR_INVALID_ARG;
   Pipe& p = *c->pipe;
   if (p.done.empty()) {
     if (p.inflight.empty()) return JXG_ERR_INVALID_ARG;
@@ -1849,13 +2076,26 @@ static jxg_status pipe_receive(Ctx* c, jxg_buffer* out) {
   return JXG_OK;
 }
 
-// ---------------------------------------------------------------------------
-// sharded encode (jxg_shard_* in include/jxg.h)
-// payload: "JXGS" | version 1 | rank | world | xsize | ysize | nsections |
-//          nsections x (TOC index, bytes) | section bytes back to back
-// ---------------------------------------------------------------------------
-constexpr uint32_t kPayloadMagic = 0x5347584Au;  // "JXGS"
+// streaming shards: the oldest pending shard frame, completed if needed
+static jxg_status pipe_shard_oldest(Ctx* c, PipeFrame** fr) {
+  if (!c->pipe || c->pipe->mode != 2) return JXG_ERR_INVALID_ARG;
+  Pipe& p = *c->pipe;
+  if (p.ready.empty()) {
+    if (p.inflight.empty()) return JXG_ERR_INVALID_ARG;
+    const jxg_status st = pipe_complete_oldest(c);
+    if (st) {
+      pipe_abort(c);
+      return st;
+    }
+  }
+  *fr = p.ready.front().get();
+  return JXG_OK;
+}
 
+// ---------------------------------------------------------------------------
+// sharded encode, one frame at a time (jxg_shard_begin / jxg_shard_end), with
+// the caller's collectives in between
+// ---------------------------------------------------------------------------
 static jxg_status shard_begin(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32_t h,
                               size_t stride, uint32_t rank, uint32_t world, uint32_t* d_hist,
                               uint8_t* d_xbuf) {
@@ -1876,6 +2116,7 @@ static jxg_status shard_begin(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32_t
   // all-reduce d_hist).  Prefix codes keep one preset from the summed
   // histogram (N x 132 clusters would not fit one context map).
   J.presets = J.ans && world > 1;
+  if ((st = order_input(c, c))) return st;
   JXG_HIP(hipEventRecord(c->ev[0], s));
   if ((st = stage_front(c, J))) return st;
   if ((st = stage_ac_stats(c, J))) return st;
@@ -1903,7 +2144,6 @@ static jxg_status shard_end(Ctx* c, const uint32_t* d_hist, const uint8_t* d_xbu
   const Clock::time_point t_call = Clock::now();
   Job& J = *c->job;
   hipStream_t s = c->stream;
-  const uint32_t world = J.plan.world;
   const Exchange& X = J.plan.x;
   PackArgs pa{c->acs.p, c->qf.p, c->dc.p, J.f.bxs, J.f.bys, J.f.gxs, c->cmap.p, J.f.tiles_x,
               J.f.tiles_y, const_cast<uint8_t*>(d_xbuf), c->xlist.p + X.send.size(),
@@ -1916,37 +2156,7 @@ static jxg_status shard_end(Ctx* c, const uint32_t* d_hist, const uint8_t* d_xbu
   if ((st = stage_download_lf(c, J))) return st;
   if ((st = stage_codes(c, J))) return st;
   if ((st = stage_emit(c, J))) return st;
-  std::vector<uint32_t> ids, sizes;
-  size_t nbytes = 0;
-  if ((st = stage_concat(c, J, false, &ids, &sizes, nullptr, &nbytes))) return st;
-  // payload head (host); the body stays in c->out until jxg_shard_payload
-  std::vector<uint32_t>& hw = c->payload_head;
-  hw.assign(7 + 2 * ids.size(), 0);
-  hw[0] = kPayloadMagic;
-  hw[1] = J.presets ? 2 : 1;
-  hw[2] = J.plan.rank;
-  hw[3] = world;
-  hw[4] = J.w;
-  hw[5] = J.h;
-  hw[6] = (uint32_t)ids.size();
-  for (size_t i = 0; i < ids.size(); i++) {
-    hw[7 + 2 * i] = ids[i];
-    hw[8 + 2 * i] = sizes[i];
-  }
-  if (J.presets) {
-    // version 2: the rank's HF preset -- [B][nhist][context map, bytes packed
-    // in words][clustered counts nhist x kAlpha], B = words after B
-    const uint32_t nh = J.nhist_ans, cw = (kAcCtx + 3) / 4;
-    hw.push_back(1 + cw + nh * kAlpha);
-    hw.push_back(nh);
-    const size_t o = hw.size();
-    hw.resize(o + cw, 0);
-    std::memcpy(hw.data() + o, J.pre_ctxmap.data(), kAcCtx);
-    hw.insert(hw.end(), J.pre_counts.begin(), J.pre_counts.end());
-  }
-  c->payload_body = nbytes;
-  *payload_bytes = hw.size() * 4 + nbytes;
-  JXG_HIP(hipStreamSynchronize(s));
+  if ((st = shard_finish(c, J, payload_bytes))) return st;
   c->stats = jxg_stats{};
   c->stats.xsize = J.w;
   c->stats.ysize = J.h;
@@ -2352,7 +2562,7 @@ void jxg_destroy(void* ctx) {
   (void)hipSetDevice(c->params.device);
   (void)hipStreamSynchronize(c->stream);
   if (c->stream2) (void)hipStreamSynchronize(c->stream2);
-  g_live_ctx--;
+  if (!c->owned_lane) g_live_ctx--;
 #ifdef JXG_MERGE_PROFILE
   dump_merge_profile();
 #endif
@@ -2369,6 +2579,7 @@ void jxg_destroy(void* ctx) {
 #endif
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
+  if (c->ev_in) (void)hipEventDestroy(c->ev_in);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
   delete c;
@@ -2384,6 +2595,9 @@ jxg_status jxg_encode_rgb8_device(void* ctx, const void* d_rgb, uint32_t w, uint
   out->data = nullptr;
   out->size = 0;
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
+  if (pipe_busy(c)) return JXG_ERR_INVALID_ARG;
+  const jxg_status st = order_input(c, c);
+  if (st) return st;
   return encode_device(c, static_cast<const uint8_t*>(d_rgb), w, h, stride, out, t0);
 }
 
@@ -2395,6 +2609,7 @@ jxg_status jxg_encode_rgb8(void* ctx, const uint8_t* rgb, uint32_t w, uint32_t h
   const Clock::time_point t0 = Clock::now();
   Ctx* c = static_cast<Ctx*>(ctx);
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
+  if (pipe_busy(c)) return JXG_ERR_INVALID_ARG;  // c->rgb may be an in-flight lane's input
   const size_t bytes = stride * (h - 1) + (size_t)w * 3;
   if (c->rgb.ensure(bytes) != hipSuccess) return JXG_ERR_OOM;
   if (hipMemcpyAsync(c->rgb.p, rgb, bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess)
@@ -2414,8 +2629,7 @@ jxg_status jxg_encode_rgb8(void* ctx, const uint8_t* rgb, uint32_t w, uint32_t h
 static jxg_status batch_encode(Ctx* c, const uint8_t* const* frames, bool on_device, uint32_t n,
                                uint32_t w, uint32_t h, size_t stride, jxg_buffer* outs) {
   for (uint32_t i = 0; i < n; i++) outs[i] = jxg_buffer{nullptr, 0};
-  if (c->pipe && (!c->pipe->inflight.empty() || !c->pipe->done.empty()))
-    return JXG_ERR_INVALID_ARG;  // would interleave with the caller's stream
+  if (pipe_busy(c)) return JXG_ERR_INVALID_ARG;  // would interleave with the caller's stream
   uint32_t got = 0;
   jxg_status st = JXG_OK;
   for (uint32_t i = 0; i < n && !st; i++) {
@@ -2490,7 +2704,9 @@ jxg_status jxg_receive(void* ctx, jxg_buffer* out) {
 jxg_status jxg_pending(void* ctx, uint32_t* n) {
   if (!ctx || !n) return JXG_ERR_INVALID_ARG;
   Ctx* c = static_cast<Ctx*>(ctx);
-  *n = c->pipe ? (uint32_t)(c->pipe->inflight.size() + c->pipe->done.size()) : 0u;
+  *n = c->pipe ? (uint32_t)(c->pipe->inflight.size() + c->pipe->done.size() +
+                            c->pipe->ready.size())
+               : 0u;
   return JXG_OK;
 }
 
@@ -2514,10 +2730,10 @@ jxg_status jxg_shard_sizes(uint32_t xsize, uint32_t ysize, uint32_t world, size_
   const Frame f = make_frame(xsize, ysize, 1.0f);
   *hist_words = (size_t)kMaxClusters * kAlpha;
   // the largest send or receive buffer of any rank
-  const std::vector<uint32_t> owner = lf_owners(f, world);
+  const Partition part = make_partition(f, world);
   size_t most = 1;
   for (uint32_t r = 0; r < world && world > 1; r++) {
-    const Exchange X = make_exchange(f, owner, r, world);
+    const Exchange X = make_exchange(f, part, r, world);
     most = std::max(most, std::max(X.send.size(), X.recv.size()));
   }
   *slot_bytes = most * kGroupRecordBytes;
@@ -2529,7 +2745,7 @@ jxg_status jxg_shard_exchange(uint32_t xsize, uint32_t ysize, uint32_t world, ui
   if (!send_bytes || !recv_bytes || xsize == 0 || ysize == 0 || world == 0 || rank >= world)
     return JXG_ERR_INVALID_ARG;
   const Frame f = make_frame(xsize, ysize, 1.0f);
-  const Exchange X = make_exchange(f, lf_owners(f, world), rank, world);
+  const Exchange X = make_exchange(f, make_partition(f, world), rank, world);
   for (uint32_t p = 0; p < world; p++) {
     send_bytes[p] = (size_t)X.nsend[p] * kGroupRecordBytes;
     recv_bytes[p] = (size_t)X.nrecv[p] * kGroupRecordBytes;
@@ -2544,6 +2760,7 @@ jxg_status jxg_shard_begin(void* ctx, const void* d_rgb, uint32_t w, uint32_t h,
     return JXG_ERR_INVALID_ARG;
   Ctx* c = static_cast<Ctx*>(ctx);
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
+  if (pipe_busy(c)) return JXG_ERR_INVALID_ARG;
   return shard_begin(c, static_cast<const uint8_t*>(d_rgb), w, h, stride, rank, world, d_hist,
                      static_cast<uint8_t*>(d_xbuf));
 }
@@ -2554,6 +2771,7 @@ jxg_status jxg_shard_end(void* ctx, const uint32_t* d_hist, const void* d_xbuf,
   Ctx* c = static_cast<Ctx*>(ctx);
   *payload_bytes = 0;
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
+  if (pipe_busy(c)) return JXG_ERR_INVALID_ARG;
   return shard_end(c, d_hist, static_cast<const uint8_t*>(d_xbuf), payload_bytes);
 }
 
@@ -2561,6 +2779,7 @@ jxg_status jxg_shard_payload(void* ctx, void* dst, int dst_on_device) {
   if (!ctx || !dst) return JXG_ERR_INVALID_ARG;
   Ctx* c = static_cast<Ctx*>(ctx);
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
+  if (pipe_busy(c)) return JXG_ERR_INVALID_ARG;
   return shard_payload(c, dst, dst_on_device != 0);
 }
 
@@ -2573,6 +2792,7 @@ jxg_status jxg_shard_assemble_device(void* ctx, const void* d_payloads, const si
   out->data = nullptr;
   out->size = 0;
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
+  if (pipe_busy(c)) return JXG_ERR_INVALID_ARG;
   return shard_assemble_device(c, static_cast<const uint8_t*>(d_payloads), offsets, sizes, n, out);
 }
 
@@ -2595,6 +2815,7 @@ jxg_status jxg_shard_write_host(void* ctx, const uint32_t* const* heads, const s
   *total = 0;
   Ctx* c = static_cast<Ctx*>(ctx);
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
+  if (pipe_busy(c)) return JXG_ERR_INVALID_ARG;
   return shard_write_host(c, heads, head_words, n, static_cast<uint8_t*>(dst), dst_size, total);
 }
 
@@ -2616,12 +2837,82 @@ jxg_status jxg_shard_assemble(const uint8_t* const* payloads, const size_t* size
   return shard_assemble(payloads, sizes, n, out);
 }
 
+jxg_status jxg_shard_plan(uint32_t xsize, uint32_t ysize, uint32_t world, uint32_t* group_owner,
+                          uint32_t* lf_owner, int* kind) {
+  if (xsize == 0 || ysize == 0 || world == 0 || xsize > (1u << 18) || ysize > (1u << 18))
+    return JXG_ERR_INVALID_ARG;
+  const Frame f = make_frame(xsize, ysize, 1.0f);
+  const Partition part = make_partition(f, world);
+  if (group_owner) std::copy(part.group.begin(), part.group.end(), group_owner);
+  if (lf_owner) std::copy(part.lf.begin(), part.lf.end(), lf_owner);
+  if (kind) *kind = part.kind;
+  return JXG_OK;
+}
+
+jxg_status jxg_set_input_stream(void* ctx, void* stream) {
+  if (!ctx) return JXG_ERR_INVALID_ARG;
+  static_cast<Ctx*>(ctx)->in_stream = static_cast<hipStream_t>(stream);
+  return JXG_OK;
+}
+
+jxg_status jxg_pipeline_depth(void* ctx, uint32_t xsize, uint32_t ysize, uint32_t rank,
+                              uint32_t world, uint32_t* depth) {
+  if (!ctx || !depth || xsize == 0 || ysize == 0 || world == 0 || rank >= world)
+    return JXG_ERR_INVALID_ARG;
+  const Frame f = make_frame(xsize, ysize, static_cast<Ctx*>(ctx)->params.distance);
+  *depth = pipe_depth(world > 1 ? make_plan(f, rank, world).ng() : f.ngroups);
+  return JXG_OK;
+}
+
+jxg_status jxg_shard_submit_device(void* ctx, const void* d_rgb, uint32_t w, uint32_t h,
+                                   size_t stride, uint32_t rank, uint32_t world) {
+  if (!ctx || !d_rgb || w == 0 || h == 0 || w > (1u << 18) || h > (1u << 18) ||
+      stride < (size_t)w * 3)
+    return JXG_ERR_INVALID_ARG;
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
+  return pipe_submit(c, static_cast<const uint8_t*>(d_rgb), true, w, h, stride, rank, world, true);
+}
+
+jxg_status jxg_shard_next_head(void* ctx, uint32_t* dst, size_t* nwords) {
+  if (!ctx || !nwords) return JXG_ERR_INVALID_ARG;
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
+  PipeFrame* fr = nullptr;
+  const jxg_status st = pipe_shard_oldest(c, &fr);
+  if (st) return st;
+  const std::vector<uint32_t>& hw = fr->lane->payload_head;
+  if (dst) {
+    if (*nwords < hw.size()) return JXG_ERR_INVALID_ARG;
+    std::memcpy(dst, hw.data(), hw.size() * 4);
+  }
+  *nwords = hw.size();
+  c->stats = fr->lane->stats;
+  return JXG_OK;
+}
+
+jxg_status jxg_shard_write_next(void* ctx, const uint32_t* const* heads, const size_t* head_words,
+                                uint32_t n, void* dst, size_t dst_size, size_t* total) {
+  if (!ctx || !heads || !head_words || !total || n == 0) return JXG_ERR_INVALID_ARG;
+  *total = 0;
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
+  PipeFrame* fr = nullptr;
+  jxg_status st = pipe_shard_oldest(c, &fr);
+  if (st) return st;
+  st = shard_write_host(fr->lane, heads, head_words, n, static_cast<uint8_t*>(dst), dst_size, total);
+  if (st) return st;  // (too small a buffer: the frame stays, *total tells the size)
+  c->pipe->ready.erase(c->pipe->ready.begin());  // its lane is free again
+  return JXG_OK;
+}
+
 jxg_status jxg_homogeneity_map(void* ctx, const float* xyb, uint32_t xsize, uint32_t ysize,
                                float distance, uint32_t flags, float* r3, uint8_t* type) {
   if (!ctx || !xyb || !r3 || !type || xsize == 0 || ysize == 0 || xsize % 8 || ysize % 8)
     return JXG_ERR_INVALID_ARG;
   Ctx* c = static_cast<Ctx*>(ctx);
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
+  if (pipe_busy(c)) return JXG_ERR_INVALID_ARG;
   const size_t plane = (size_t)xsize * ysize, nb = plane / 64;
   JXG_HIP(c->xyb.ensure(plane * 3));
   JXG_HIP(c->r3.ensure(nb * 3));
@@ -2694,6 +2985,9 @@ jxg_status jxg_compare_rgb8_device(void* ctx, const void* d_orig, size_t orig_st
     return JXG_ERR_INVALID_ARG;
   Ctx* c = static_cast<Ctx*>(ctx);
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
+  if (pipe_busy(c)) return JXG_ERR_INVALID_ARG;
+  const jxg_status st = order_input(c, c);
+  if (st) return st;
   return compare_device(c, static_cast<const uint8_t*>(d_orig), orig_stride,
                         static_cast<const uint8_t*>(d_comp), comp_stride, xsize, ysize, want_ssim,
                         out);
@@ -2707,6 +3001,7 @@ jxg_status jxg_compare_rgb8(void* ctx, const uint8_t* orig, size_t orig_stride,
     return JXG_ERR_INVALID_ARG;
   Ctx* c = static_cast<Ctx*>(ctx);
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
+  if (pipe_busy(c)) return JXG_ERR_INVALID_ARG;
   const size_t row = (size_t)xsize * 3, n = row * ysize;
   JXG_HIP(c->q_orig.ensure(n));
   JXG_HIP(c->q_comp.ensure(n));

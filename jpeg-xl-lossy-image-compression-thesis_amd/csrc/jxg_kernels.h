@@ -91,7 +91,9 @@ struct AcArgs {
   const int16_t* ac;  // [nb][3][64 zigzag]
   const uint16_t* nz;  // [3][nb] non-zero counts (front / merge kernels)
   uint32_t bxs, bys, gxs;
-  uint32_t g0;           // first pass group of the launch (shard)
+  uint32_t g0;           // first pass group of the launch (contiguous shard / whole frame)
+  const uint32_t* glist; // [slots] pass group of each slot (a shard's non-contiguous
+                         //   group set), or null: slot i = group g0 + i
   uint32_t* hist;        // [kMaxClusters][kAlpha]      (hist pass)
   uint32_t* bound;       // [ngroups] bit upper bound   (hist pass)
   uint32_t* ntok;        // [ngroups][3] token counts   (hist pass)
@@ -100,7 +102,8 @@ struct AcArgs {
   uint32_t* scratch;     // bit buffer (emit pass, zeroed)
   uint32_t* bits;        // [ngroups] exact bits (emit pass)
   uint32_t* tokens;      // token records (cluster | tok << 8 | nbits << 14 | bits << 18),
-                         //   group g at (g - g0) * kGroupTokStride (hist pass writes them)
+                         //   slot i (group glist[i] or g0 + i) at i * kGroupTokStride
+                         //   (hist pass writes them)
 };
 // records per pass group: 1024 blocks x 3 channels x <= 64 tokens per slice
 constexpr uint64_t kGroupTokStride = 1024ull * 3 * 64;
@@ -127,8 +130,9 @@ struct AnsArgs {
   const uint64_t* base;    // [ngroups] scratch bit offset
   uint32_t* scratch;
   uint32_t* bits;          // [ngroups] exact bits
-  uint32_t g0, g1;         // groups [g0, g1)
-  const uint32_t* order;   // chain order of the g1 - g0 groups (longest first)
+  uint32_t g0, n;          // slots [0, n): group glist[i], or g0 + i when glist is null
+  const uint32_t* glist;
+  const uint32_t* order;   // chain order of the n slots (longest group first)
 };
 void launch_ans(const AnsArgs& a, hipStream_t s);
 

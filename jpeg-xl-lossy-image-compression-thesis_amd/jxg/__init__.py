@@ -82,7 +82,9 @@ EXPORTS = ("jxg_status_str", "jxg_create", "jxg_destroy", "jxg_encode_rgb8",
            "jxg_shard_assemble", "jxg_compare_rgb8", "jxg_compare_rgb8_device",
            "jxg_shard_head", "jxg_shard_write_host", "jxg_host_register", "jxg_host_unregister",
            "jxg_encode_batch_rgb8_device", "jxg_synth_rgb8_device", "jxg_shard_exchange",
-           "jxg_submit_rgb8", "jxg_submit_rgb8_device", "jxg_receive", "jxg_pending")
+           "jxg_submit_rgb8", "jxg_submit_rgb8_device", "jxg_receive", "jxg_pending",
+           "jxg_set_input_stream", "jxg_pipeline_depth", "jxg_shard_plan",
+           "jxg_shard_submit_device", "jxg_shard_next_head", "jxg_shard_write_next")
 
 _lib = None
 
@@ -134,6 +136,15 @@ def load():
     lib.jxg_shard_head.argtypes = [vp, vp, ctypes.POINTER(sz)]
     lib.jxg_shard_write_host.argtypes = [vp, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(sz),
                                          ctypes.c_uint32, vp, sz, ctypes.POINTER(sz)]
+    lib.jxg_set_input_stream.argtypes = [vp, vp]
+    lib.jxg_pipeline_depth.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                       ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
+    lib.jxg_shard_plan.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, vp, vp,
+                                   ctypes.POINTER(ctypes.c_int)]
+    lib.jxg_shard_submit_device.argtypes = [vp, vp, ctypes.c_uint32, ctypes.c_uint32, sz,
+                                            ctypes.c_uint32, ctypes.c_uint32]
+    lib.jxg_shard_next_head.argtypes = [vp, vp, ctypes.POINTER(sz)]
+    lib.jxg_shard_write_next.argtypes = lib.jxg_shard_write_host.argtypes
     lib.jxg_host_register.argtypes = [vp, sz]
     lib.jxg_host_unregister.argtypes = [vp]
     cmp_args = [vp, vp, sz, vp, sz, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
@@ -289,6 +300,40 @@ class Encoder:
         _check(load().jxg_pending(self._ctx, ctypes.byref(n)))
         return n.value
 
+    def pipeline_depth(self, width: int, height: int, rank: int = 0, world: int = 1) -> int:
+        """Lanes of the streaming pipeline for these frames (or this rank's shard)."""
+        n = ctypes.c_uint32()
+        _check(load().jxg_pipeline_depth(self._ctx, width, height, rank, world, ctypes.byref(n)))
+        return n.value
+
+    def set_input_stream(self, stream) -> None:
+        """Order every later device-input call after the work submitted so far
+        to `stream` (a hipStream_t handle, e.g. ``torch.cuda.current_stream()
+        .cuda_stream``; None: the caller's writes are complete before each
+        call) -- include/jxg.h."""
+        _check(load().jxg_set_input_stream(self._ctx, ctypes.c_void_p(stream or None)))
+
+    # streaming sharded encode (jxg_shard_submit_device / jxg_shard_next_head /
+    # jxg_shard_write_next): see jxg.dist.ShardStream
+    def shard_submit_device(self, ptr: int, width: int, height: int, rank: int, world: int,
+                            row_stride: int | None = None):
+        _check(load().jxg_shard_submit_device(self._ctx, ctypes.c_void_p(ptr), width, height,
+                                              row_stride or width * 3, rank, world))
+
+    def shard_next_head(self) -> np.ndarray:
+        """Payload head of the oldest pending shard frame (waits for its sections)."""
+        n = ctypes.c_size_t(0)
+        _check(load().jxg_shard_next_head(self._ctx, None, ctypes.byref(n)))
+        out = np.zeros(n.value, dtype=np.uint32)
+        _check(load().jxg_shard_next_head(self._ctx, out.ctypes.data, ctypes.byref(n)))
+        return out
+
+    def shard_write_next(self, heads, dst_ptr: int, dst_size: int):
+        """jxg_shard_write_host for the oldest pending shard frame, which is then
+        released; returns (ok, total) -- ok False when dst_size < total (the
+        frame stays pending, nothing written)."""
+        return self._write(load().jxg_shard_write_next, heads, dst_ptr, dst_size)
+
     def timings(self) -> tuple:
         """(ms_front_kernel, ms_host_call, ms_host_codes, ms_host_layout) of the
         last encode -- the per-frame subset of :meth:`stats` without its copies."""
@@ -367,13 +412,15 @@ class Encoder:
         """Write this rank's sections (and, on rank 0, headers + TOC) into the
         shared host buffer at dst_ptr; returns (ok, total codestream bytes) --
         ok False when dst_size < total (nothing written)."""
+        return self._write(load().jxg_shard_write_host, heads, dst_ptr, dst_size)
+
+    def _write(self, fn, heads, dst_ptr: int, dst_size: int):
         heads = [np.ascontiguousarray(h, dtype=np.uint32) for h in heads]
         n = len(heads)
         ptrs = (ctypes.c_void_p * n)(*[h.ctypes.data for h in heads])
         words = (ctypes.c_size_t * n)(*[h.size for h in heads])
         total = ctypes.c_size_t(0)
-        st = load().jxg_shard_write_host(self._ctx, ptrs, words, n, ctypes.c_void_p(dst_ptr),
-                                         dst_size, ctypes.byref(total))
+        st = fn(self._ctx, ptrs, words, n, ctypes.c_void_p(dst_ptr), dst_size, ctypes.byref(total))
         if st == -1 and total.value > dst_size:
             return False, total.value
         _check(st)
@@ -464,53 +511,37 @@ def lf_group_count(width: int, height: int) -> int:
     return ((width + 2047) // 2048) * ((height + 2047) // 2048)
 
 
-def _shard_of(ng: int, g: int, world: int) -> int:
-    r = g * world // ng
-    while r + 1 < world and ng * (r + 1) // world <= g:
-        r += 1
-    while r > 0 and ng * r // world > g:
-        r -= 1
-    return r
+def shard_plan(width: int, height: int, world: int):
+    """The partition of a sharded encode (jxg_shard_plan; include/jxg.h):
+    (owner rank of every pass group, owner rank of every LF group, kind) --
+    kind 0 contiguous ranges, 1 whole LF groups per rank, 2 ranges with the
+    per-block record exchange."""
+    ng, nlf = group_count(width, height), lf_group_count(width, height)
+    go = np.zeros(ng, dtype=np.uint32)
+    lo = np.zeros(nlf, dtype=np.uint32)
+    kind = ctypes.c_int(0)
+    _check(load().jxg_shard_plan(width, height, world, go.ctypes.data, lo.ctypes.data,
+                                 ctypes.byref(kind)))
+    return go.tolist(), lo.tolist(), kind.value
 
 
 def lf_owners(width: int, height: int, world: int) -> list:
-    """Owner rank of every LF group in a sharded encode (== jxg_host.cpp
-    lf_owners): the rank holding the most of the LF group's pass groups, less
-    16 per LF group already assigned to it; ties to the lower rank."""
-    gxs, gys = -(-width // 256), -(-height // 256)
-    lfxs, lfys = -(-width // 2048), -(-height // 2048)
-    ng = gxs * gys
-    own, nas = [], [0] * world
-    for lg in range(lfxs * lfys):
-        if world == 1:
-            own.append(0)
-            continue
-        lx, ly = lg % lfxs, lg // lfxs
-        cnt = [0] * world
-        for gy in range(ly * 8, min(ly * 8 + 8, gys)):
-            for gx in range(lx * 8, min(lx * 8 + 8, gxs)):
-                cnt[_shard_of(ng, gy * gxs + gx, world)] += 1
-        best, bs = -1, 0
-        for r in range(world):
-            if cnt[r] and (best < 0 or cnt[r] - 16 * nas[r] > bs):
-                best, bs = r, cnt[r] - 16 * nas[r]
-        own.append(best)
-        nas[best] += 1
-    return own
+    """Owner rank of every LF group in a sharded encode (jxg_shard_plan)."""
+    return shard_plan(width, height, world)[1]
 
 
-def shard_sections(width: int, height: int, rank: int, world: int):
-    """TOC indices of the sections rank `rank` of `world` produces (the
-    ownership of jxg_host.cpp make_plan): LfGlobal / HfGlobal on rank 0, the
-    LF groups it owns (lf_owners), pass groups [n*rank/world, n*(rank+1)/world)."""
-    ng, nlf = group_count(width, height), lf_group_count(width, height)
+def shard_sections(width: int, height: int, rank: int, world: int, ans: bool = False):
+    """TOC indices of the sections rank `rank` of `world` produces: LfGlobal on
+    rank 0, the LF groups it owns, its pass groups (jxg_shard_plan), and on
+    rank 0 HfGlobal -- except with ANS over several ranks, where HfGlobal is
+    written at assembly from the ranks' HF presets (version-2 payload heads)."""
+    go, lo, _ = shard_plan(width, height, world)
+    nlf = len(lo)
     ids = [0] if rank == 0 else []
-    owners = lf_owners(width, height, world)
-    ids += [1 + lg for lg in range(nlf) if owners[lg] == rank]
-    if rank == 0:
+    ids += [1 + lg for lg in range(nlf) if lo[lg] == rank]
+    if rank == 0 and not (ans and world > 1):
         ids.append(1 + nlf)
-    g0, g1 = ng * rank // world, ng * (rank + 1) // world
-    ids += [2 + nlf + g for g in range(g0, g1)]
+    ids += [2 + nlf + g for g in range(len(go)) if go[g] == rank]
     return ids
 
 

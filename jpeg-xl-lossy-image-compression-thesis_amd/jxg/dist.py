@@ -22,17 +22,27 @@ only collectives are
             at their codestream offsets (rank 0 adds headers + TOC) -- the
             node's PCIe links work in parallel and nothing crosses xGMI; or
      device (default): a gather of the per-rank section payloads on rank 0
-            (device to device), which writes headers + TOC and moves every
-            section with the concat kernel, then one D2H of the codestream.
+            (device to device; staged through the host under gloo), which
+            writes headers + TOC and moves every section with the concat
+            kernel, then one D2H of the codestream.
 With prefix codes the result is byte-identical to a single-GPU encode of the
 same frame; with ANS it decodes to the same image (same coefficients, strategy,
 quant field, DC and CfL maps) with per-rank histograms.
+
+:class:`ShardStream` is the streaming form (the multi-GPU pipeline bench.py
+--gpus N times): consecutive frames, each split over the ranks by a partition
+that needs no record exchange (whole LF groups per rank, jxg_shard_plan kind
+0 / 1) and coded with one HF preset per rank (ANS), so a rank's frames flow
+through the library's lanes with no collective at all; per frame the ranks
+only swap their payload heads through a node-shared /dev/shm region and DMA
+their sections into it.
 """
 from __future__ import annotations
 
 import ctypes
 import mmap
 import os
+import time
 
 import numpy as np
 import torch
@@ -105,10 +115,10 @@ class SharedHostBuffer:
             raise RuntimeError("jxg_host_register failed")
         self.cap = cap
 
-    def view(self, n: int) -> np.ndarray:
+    def view(self, n: int, offset: int = 0) -> np.ndarray:
         """zero-copy view of the codestream; valid until the next frame's
         write into the buffer (or close)"""
-        return np.frombuffer(self.mm, dtype=np.uint8, count=n)
+        return np.frombuffer(self.mm, dtype=np.uint8, count=n, offset=offset)
 
     def close(self):
         self._release()
@@ -183,6 +193,9 @@ def encode_sharded(enc: Encoder, d_rgb: torch.Tensor, width: int, height: int, r
     ``host`` a numpy view of the shared buffer), None elsewhere.  `bufs`
     caches the exchange tensors across calls."""
     dev = d_rgb.device
+    # the frame was produced on torch's stream: the library orders its reads
+    # after it (include/jxg.h, device inputs)
+    enc.set_input_stream(torch.cuda.current_stream(dev).cuda_stream)
     if bufs is None:
         bufs = {}
     key = (width, height, world, rank)
@@ -245,29 +258,152 @@ def encode_sharded(enc: Encoder, d_rgb: torch.Tensor, width: int, height: int, r
             return None
         v = host.view(total)
         return bytes(v) if copy else v
-    if gloo:
-        payloads = gather_payloads(enc.shard_payload_bytes(size), rank, world, "cpu", group)
-        return shard_assemble(payloads) if rank == 0 else None
-    # payloads gathered device to device into one buffer on rank 0
-    n = torch.tensor([size], dtype=torch.int64, device=dev)
+    # device assembly: payloads gathered into one buffer on rank 0 (RCCL,
+    # device to device; the gloo rehearsal stages the same gather through the
+    # host), which assembles them with the concat kernel
+    n = torch.tensor([size], dtype=torch.int64, device="cpu" if gloo else dev)
     sizes = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(sizes, n, group=group)
     sizes = [int(x.item()) for x in sizes]
+    # payload buffers under their own keys: "send" / "recv" are the record
+    # exchange's (reused by the next frame's shard_begin / shard_end)
     cap = (max(sizes) + 15) // 16 * 16
-    if bufs.get("cap", 0) < cap:
-        bufs["cap"] = cap
-        bufs["send"] = torch.empty(cap, dtype=torch.uint8, device=dev)
-        bufs["recv"] = torch.empty(world * cap + 64, dtype=torch.uint8, device=dev) \
+    if bufs.get("pcap", 0) < cap:
+        bufs["pcap"] = cap
+        bufs["psend"] = torch.empty(cap, dtype=torch.uint8, device=dev)
+        bufs["precv"] = torch.empty(world * cap + 64, dtype=torch.uint8, device=dev) \
             if rank == 0 else None
-    cap_alloc = bufs["cap"]
-    send = bufs["send"][:cap]
-    enc.shard_payload(send.data_ptr(), on_device=True)
-    recv = bufs["recv"]
-    views = [recv[r * cap:(r + 1) * cap] for r in range(world)] if rank == 0 else None
-    dist.gather(send, views, dst=0, group=group)
-    del cap_alloc
+        torch.cuda.synchronize(dev)  # allocated on torch's stream, written on the library's
+    psend = bufs["psend"][:cap]
+    enc.shard_payload(psend.data_ptr(), on_device=True)  # returns with the copy complete
+    precv = bufs["precv"]
+    views = [precv[r * cap:(r + 1) * cap] for r in range(world)] if rank == 0 else None
+    if gloo:
+        parts = [torch.empty(cap, dtype=torch.uint8) for _ in range(world)] if rank == 0 else None
+        dist.gather(psend.cpu(), parts, dst=0, group=group)
+        if rank == 0:
+            for v, part in zip(views, parts):
+                v.copy_(part)
+    else:
+        dist.gather(psend, views, dst=0, group=group)
     if rank != 0:
         return None
     torch.cuda.synchronize(dev)
-    return enc.shard_assemble_device(recv.data_ptr(), [r * cap for r in range(world)], sizes,
+    return enc.shard_assemble_device(precv.data_ptr(), [r * cap for r in range(world)], sizes,
                                      copy=copy)
+
+
+class ShardStream:
+    """Streaming group-sharded encode (jxg_shard_submit_device /
+    jxg_shard_next_head / jxg_shard_write_next): every rank submits its shard
+    of the same frames in the same order; frames flow through the library's
+    pipeline lanes (front end, merge stage, statistics, codes and rANS chains
+    of up to jxg_pipeline_depth frames overlap) with no collective inside a
+    frame.  Per frame, in order, each rank
+      1. takes its payload head (the oldest frame's sections emitted),
+      2. publishes it in the node-shared /dev/shm region (slot k % S) and
+         reads the other ranks' heads there (a sequence word per rank and
+         slot: spin until every rank has published frame k),
+      3. DMAs its sections into frame k's codestream slot (rank 0 adds headers
+         + TOC) and marks frame k done.
+    Rank 0's :meth:`receive` returns a zero-copy view of frame k's codestream
+    once every rank has marked it done (valid for the next S - 1 receives);
+    other ranks get None.  All ranks must run on one node (the shared
+    mapping); the partition must need no record exchange and the coder must
+    be ANS when world > 1 (jxg_shard_submit_device refuses otherwise)."""
+
+    def __init__(self, enc: Encoder, width: int, height: int, rank: int, world: int,
+                 group=None, slots: int = 4, slot_bytes: int | None = None):
+        self.enc, self.w, self.h, self.rank, self.world = enc, width, height, rank, world
+        self.depth = enc.pipeline_depth(width, height, rank, world)
+        self.slots = slots
+        self.hcap = _head_cap(width, height)
+        # codestream slot: 12 bpp + 1 MiB (a d1 8K frame is ~2 bpp); a frame
+        # over it raises (pass slot_bytes)
+        self.slot_bytes = slot_bytes or ((width * height * 3 // 2 + (1 << 20) + 4095) & ~4095)
+        self.meta_words = 2 * slots * world          # int64: published[S][W], done[S][W]
+        self.heads_off = 8 * self.meta_words
+        self.data_off = (self.heads_off + 4 * slots * world * self.hcap + 4095) & ~4095
+        self.host = SharedHostBuffer(rank, world, group)
+        self.host.ensure(self.data_off + slots * self.slot_bytes)
+        self.meta = np.frombuffer(self.host.mm, dtype=np.int64, count=self.meta_words)
+        if rank == 0:
+            self.meta[:] = -1
+        dist.barrier(group=group)
+        self.published = self.meta[:slots * world].reshape(slots, world)
+        self.done = self.meta[slots * world:].reshape(slots, world)
+        self.heads = np.frombuffer(self.host.mm, dtype=np.uint32,
+                                   count=slots * world * self.hcap,
+                                   offset=self.heads_off).reshape(slots, world, self.hcap)
+        self.submitted = 0   # frames submitted
+        self.written = 0     # frames whose sections this rank has written
+        self.received = 0    # frames returned by receive()
+        self.totals = {}
+
+    @staticmethod
+    def _wait(cond, what):
+        t0 = time.perf_counter()
+        spins = 0
+        while not cond():
+            spins += 1
+            if spins > 64:
+                time.sleep(20e-6)
+            if time.perf_counter() - t0 > 120:
+                raise RuntimeError("ShardStream: timed out waiting for " + what)
+
+    def pending(self) -> int:
+        return self.submitted - self.received
+
+    def submit(self, ptr: int):
+        """Queue this rank's shard of the next frame (device RGB8, unchanged
+        until the frame is received).  When the library's lanes are all busy
+        the oldest frame is written out first (its codestream is then taken by
+        a later :meth:`receive`)."""
+        if self.submitted - self.written >= self.depth:
+            self._write_one()
+        self.enc.shard_submit_device(ptr, self.w, self.h, self.rank, self.world)
+        self.submitted += 1
+
+    def _write_one(self):
+        k = self.written
+        s, r = k % self.slots, self.rank
+        head = self.enc.shard_next_head()
+        if head.size > self.hcap:
+            raise RuntimeError("payload head of %d words over %d" % (head.size, self.hcap))
+        # slot s was last used by frame k - S: every rank must be done with it
+        self._wait(lambda: bool((self.done[s] >= k - self.slots).all()), "slot %d" % s)
+        self.heads[s, r, :head.size] = head
+        self.published[s, r] = k          # (x86: the head's stores are visible first)
+        self._wait(lambda: bool((self.published[s] >= k).all()), "heads of frame %d" % k)
+        heads = [self.heads[s, q, :_head_len(self.heads[s, q])].copy() for q in range(self.world)]
+        base = self.host.addr + self.data_off + s * self.slot_bytes
+        ok, total = self.enc.shard_write_next(heads, base, self.slot_bytes)
+        if not ok:
+            raise RuntimeError("codestream of %d bytes over the %d-byte slot" % (total,
+                                                                               self.slot_bytes))
+        self.totals[k] = total
+        self.done[s, r] = k
+        self.written += 1
+
+    def receive(self):
+        """The oldest frame not yet received: rank 0 gets a numpy view of its
+        codestream (valid for the next slots - 1 receives), other ranks None."""
+        k = self.received
+        if k >= self.submitted:
+            raise RuntimeError("ShardStream: nothing pending")
+        while self.written <= k:
+            self._write_one()
+        self.received += 1
+        total = self.totals.pop(k)
+        if self.rank != 0:
+            return None
+        s = k % self.slots
+        self._wait(lambda: bool((self.done[s] >= k).all()), "frame %d" % k)
+        return self.host.view(total, self.data_off + s * self.slot_bytes)
+
+    def close(self):
+        while self.received < self.submitted:
+            self.receive()
+        dist.barrier(group=self.host.group)
+        self.meta = self.published = self.done = self.heads = None
+        self.host.close()

@@ -917,7 +917,10 @@ class Decoded:
     pass
 
 
-def decode(data: bytes, want_pixels: bool = True) -> Decoded:
+def decode(data: bytes, want_pixels: bool = True, groups=None) -> Decoded:
+    """groups: decode only these pass groups (and the LF groups holding them;
+    every other block stays zero, no pixels) -- for spot checks of large
+    frames, whose full decode takes minutes in Python."""
     br = BitReader(data)
     if br.read(16) != 0x0AFF:
         raise JxlError("not a JPEG XL codestream")
@@ -1023,7 +1026,13 @@ def decode(data: bytes, want_pixels: bool = True) -> Decoded:
     d.qf = np.zeros((bys, bxs), dtype=np.int32)
     # chroma from luma: int8 (ytox, ytob) per 64x64 colour tile
     d.cmap = np.zeros((2, (bys + 7) // 8, (bxs + 7) // 8), dtype=np.int32)
+    gsel = None if groups is None else set(int(g) for g in groups)
+    if gsel is not None:
+        want_pixels = False
+        lfsel = set(((g // gxs) // 8) * lfxs + (g % gxs) // 8 for g in gsel)
     for lg in range(nlf):
+        if gsel is not None and lg not in lfsel:
+            continue
         s = sec(1 + lg)
         lgx, lgy = lg % lfxs, lg // lfxs
         bx0, by0 = lgx * 256, lgy * 256
@@ -1079,6 +1088,8 @@ def decode(data: bytes, want_pixels: bool = True) -> Decoded:
     d.ac = np.zeros((bys, bxs, 3, 64), dtype=np.int64)
     d.ac_tokens = np.zeros((ng, 3), dtype=np.int64)
     for g in range(ng):
+        if gsel is not None and g not in gsel:
+            continue
         s = sec(2 + nlf + g)
         gx, gy = g % gxs, g // gxs
         bx0, by0 = gx * 32, gy * 32

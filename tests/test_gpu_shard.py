@@ -187,9 +187,8 @@ def test_sharded_ans_per_rank_presets(jxg_mod, decoder, world):
     got = sharded_encode(jxg_mod, img, world, flags=jxg_mod.FLAG_ANS)
     dr, dg = decoder.decode(ref), decoder.decode(got)
     assert dr.npresets == 1 and dg.npresets == world
-    ng = len(dg.group_presets)
-    assert list(dg.group_presets) == [min(r for r in range(world) if g < ng * (r + 1) // world)
-                                      for g in range(ng)]
+    go, _, _ = jxg_mod.shard_plan(1500, 900, world)
+    assert list(dg.group_presets) == go  # every pass group selects its rank's preset
     _same_image(dr, dg)
 
 
@@ -203,3 +202,289 @@ def test_sharded_8k_strong(jxg_mod, world):
     with jxg_mod.Encoder(distance=1.0, effort=7) as enc:
         ref = enc.encode_device(t.data_ptr(), 7680, 4320)
     assert sharded_encode(jxg_mod, None, world, t=t) == ref
+
+
+# ---------------------------------------------------------------------------
+# streaming shards (jxg_shard_submit_device / next_head / write_next): the
+# multi-GPU pipeline, `world` contexts of one process playing the ranks
+# ---------------------------------------------------------------------------
+def streamed_shards(jxg_mod, ts, w, h, world, d=1.0, e=7, p=0, flags=None):
+    """Frames ts (device tensors) through `world` contexts' streaming shard
+    pipelines; heads swapped in-process, sections written into one host
+    buffer per frame.  Returns the codestreams in order."""
+    flags = jxg_mod.FLAG_ANS if flags is None else flags
+    encs = [jxg_mod.Encoder(distance=d, effort=e, proposals=p, flags=flags) for _ in range(world)]
+    depth = min(enc.pipeline_depth(w, h, r, world) for r, enc in enumerate(encs))
+    outs = []
+    buf = np.zeros(w * h * 2 + (1 << 20), dtype=np.uint8)
+
+    def take():
+        heads = [enc.shard_next_head() for enc in encs]
+        buf[:] = 0xCD
+        total = None
+        for enc in encs:
+            ok, t = enc.shard_write_next(heads, buf.ctypes.data, buf.size)
+            assert ok and (total is None or t == total)
+            total = t
+        outs.append(buf[:total].tobytes())
+
+    for t in ts:
+        for r, enc in enumerate(encs):
+            enc.shard_submit_device(t.data_ptr(), w, h, r, world)
+        if encs[0].pending() >= depth:
+            take()
+    while encs[0].pending():
+        take()
+    for enc in encs:
+        assert enc.pending() == 0
+        enc.close()
+    return outs
+
+
+@pytest.mark.parametrize("w,h,world,nframes", [(4096, 512, 2, 9), (8192, 512, 4, 5), (1100, 700, 1, 14)])
+def test_stream_shards_equal_one_at_a_time(jxg_mod, decoder, w, h, world, nframes):
+    """Streamed shards (several frames in flight per rank, more than the
+    pipeline depth for the 1-rank case) give the bytes of the one-frame-at-a-
+    time sharded encode of every frame; they decode to the single-GPU image
+    (ANS: one HF preset per rank)."""
+    from jxg.synth import synth_rgb8_device
+
+    ts = [synth_rgb8_device(w, h, 0x4A58 + 31 * k) for k in range(nframes)]
+    got = streamed_shards(jxg_mod, ts, w, h, world)
+    assert len(got) == nframes
+    for k in (0, nframes // 2, nframes - 1):
+        if world > 1:
+            assert got[k] == sharded_encode(jxg_mod, None, world, flags=jxg_mod.FLAG_ANS, t=ts[k])
+        else:  # world 1: the whole frame, == the single-GPU bytes
+            with jxg_mod.Encoder(distance=1.0, effort=7, flags=jxg_mod.FLAG_ANS) as enc:
+                assert got[k] == enc.encode_device(ts[k].data_ptr(), w, h)
+    with jxg_mod.Encoder(distance=1.0, effort=7, flags=jxg_mod.FLAG_ANS) as enc:
+        ref = enc.encode_device(ts[1].data_ptr(), w, h)
+    dr, dg = decoder.decode(ref), decoder.decode(got[1])
+    assert dg.npresets == world
+    _same_image(dr, dg)
+
+
+def test_stream_shards_refusals(jxg_mod):
+    """No collective inside the streaming pipeline: a plan that needs the
+    record exchange, or prefix codes over several ranks, is refused; a full
+    pipeline refuses another frame; one-at-a-time calls wait for the
+    pending frames."""
+    import torch
+
+    t = torch.zeros((2160, 3840, 3), dtype=torch.uint8, device="cuda")
+    with jxg_mod.Encoder(flags=jxg_mod.FLAG_ANS) as enc:
+        assert jxg_mod.shard_plan(3840, 2160, 8)[2] == 2
+        with pytest.raises(jxg_mod.JxgError, match="unsupported"):
+            enc.shard_submit_device(t.data_ptr(), 3840, 2160, 0, 8)
+    with jxg_mod.Encoder() as enc:  # prefix codes: the histogram all-reduce
+        with pytest.raises(jxg_mod.JxgError, match="unsupported"):
+            enc.shard_submit_device(t.data_ptr(), 4096, 512, 0, 2)
+    small = torch.zeros((512, 4096, 3), dtype=torch.uint8, device="cuda")
+    with jxg_mod.Encoder(flags=jxg_mod.FLAG_ANS) as enc:
+        depth = enc.pipeline_depth(4096, 512, 0, 2)
+        for _ in range(depth):
+            enc.shard_submit_device(small.data_ptr(), 4096, 512, 0, 2)
+        with pytest.raises(jxg_mod.JxgError, match="invalid"):  # every lane holds a frame
+            enc.shard_submit_device(small.data_ptr(), 4096, 512, 0, 2)
+        with pytest.raises(jxg_mod.JxgError, match="invalid"):  # lanes busy
+            enc.encode_device(small.data_ptr(), 4096, 512)
+        with pytest.raises(jxg_mod.JxgError, match="invalid"):  # shard frames, not whole ones
+            enc.receive()
+        assert enc.pending() == depth
+        enc.shard_next_head()
+        assert enc.pending() == depth
+
+
+def test_stream_pending_refuses_one_at_a_time(jxg_mod):
+    """ADVICE r2: a context with streamed frames in flight is a pipeline lane;
+    encode / encode_device / compare refuse until they are received."""
+    from jxg.synth import synth_rgb8
+
+    img = synth_rgb8(640, 480, 3)
+    with jxg_mod.Encoder(flags=jxg_mod.FLAG_ANS) as enc:
+        ref = enc.encode(img)
+        enc.submit(img)
+        enc.submit(img)
+        for call in (lambda: enc.encode(img), lambda: enc.compare(img, img),
+                     lambda: enc.encode_batch([img])):
+            with pytest.raises(jxg_mod.JxgError, match="invalid"):
+                call()
+        assert enc.receive() == ref and enc.receive() == ref
+        assert enc.encode(img) == ref  # drained: one-at-a-time again
+
+
+def test_input_stream_ordering(jxg_mod):
+    """jxg_set_input_stream: the library's reads of a device frame are ordered
+    after the caller's stream, without a host synchronisation -- the frame is
+    written by a long chain of torch kernels on a side stream right before
+    the submit."""
+    import torch
+
+    from jxg.synth import synth_rgb8
+
+    img = synth_rgb8(1024, 768, 9)
+    side = torch.cuda.Stream()
+    with jxg_mod.Encoder(flags=jxg_mod.FLAG_ANS) as enc:
+        ref = enc.encode(img)
+        enc.set_input_stream(side.cuda_stream)
+        src = torch.from_numpy(img).cuda()
+        torch.cuda.synchronize()
+        outs = []
+        for _ in range(3):
+            dst = torch.zeros_like(src)
+            side.wait_stream(torch.cuda.current_stream())  # dst's zero fill first
+            with torch.cuda.stream(side):
+                x = src.to(torch.float32)
+                for _ in range(200):  # keep the side stream busy
+                    x = x * 1.0
+                dst.copy_(x.to(torch.uint8))
+            enc.submit_device(dst.data_ptr(), 1024, 768)
+            outs.append(dst)
+        got = [enc.receive() for _ in range(3)]
+        assert all(g == ref for g in got)
+        dst2 = torch.zeros_like(src)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            x = src.to(torch.float32)
+            for _ in range(200):
+                x = x * 1.0
+            dst2.copy_(x.to(torch.uint8))
+        assert enc.encode_device(dst2.data_ptr(), 1024, 768) == ref
+
+
+def test_sharded_8k_ans_over_8(jxg_mod, decoder):
+    """BASELINE config 2 with the north-star coder: an 8K frame, ANS, over 8
+    contexts (whole LF groups per rank, one HF preset per rank).  LfGlobal and
+    every LF-group section equal the single-GPU encode's; the pass groups of
+    the bottom group row (ranks 6 and 7, with all 8 presets in HfGlobal)
+    decode to the single-GPU coefficients; each group selects its rank's
+    preset; the streamed shards give the same bytes."""
+    from jxg.synth import synth_rgb8_device
+
+    w, h, world = 7680, 4320, 8
+    t = synth_rgb8_device(w, h, 0x4A584C02)
+    with jxg_mod.Encoder(distance=1.0, effort=7, flags=jxg_mod.FLAG_ANS | jxg_mod.FLAG_KEEP_MAPS) as enc:
+        ref = enc.encode_device(t.data_ptr(), w, h)
+        st = enc.stats()
+    got = sharded_encode(jxg_mod, None, world, flags=jxg_mod.FLAG_ANS, t=t)
+    go, lo, kind = jxg_mod.shard_plan(w, h, world)
+    assert kind == 1
+    nlf = len(lo)
+    dr = decoder.decode(ref, groups=[])
+    gxs = -(-w // 256)
+    bottom = [16 * gxs + gx for gx in range(gxs)]
+    dg = decoder.decode(got, groups=bottom)
+    for i in range(1 + nlf):  # LfGlobal + LF groups: byte-identical sections
+        a = ref[dr.section_offsets[i]:dr.section_offsets[i] + dr.section_sizes[i]]
+        b = got[dg.section_offsets[i]:dg.section_offsets[i] + dg.section_sizes[i]]
+        assert a == b, i
+    assert dg.npresets == world
+    assert [int(dg.group_presets[g]) for g in bottom] == [go[g] for g in bottom]
+    rows = slice(16 * 32, dg.bys)
+    assert np.array_equal(dg.ac[rows], st["ac"][rows])
+    assert np.array_equal(dg.acs[rows], st["acs"][rows].astype(np.int32))
+    assert np.array_equal(dg.ac_tokens[bottom], st["ac_tokens"][bottom])
+    assert streamed_shards(jxg_mod, [t], w, h, world)[0] == got
+
+
+def test_sharded_16k_pf_over_8(jxg_mod):
+    """BASELINE config 4 as written: 16384^2, proposals P+F, over 8 contexts
+    (LF-group rows aligned with the ranks: no record moves); prefix codes ->
+    the codestream equals the oracle fingerprint of the whole frame."""
+    import hashlib
+
+    import json
+    import os
+
+    from jxg.synth import synth_rgb8_device
+
+    g = {e["name"]: e for e in json.load(open(os.path.join(os.path.dirname(__file__), "golden",
+                                                           "config_golden.json")))}["16k_d1_pf"]
+    t = synth_rgb8_device(16384, 16384, g["seed"])
+    assert jxg_mod.shard_plan(16384, 16384, 8)[2] == 0
+    assert all(sum(jxg_mod.shard_exchange(16384, 16384, 8, r)[0]) == 0 for r in range(8))
+    out = sharded_encode(jxg_mod, None, 8, p=3, t=t)
+    assert len(out) == g["bytes"]
+    assert hashlib.sha256(out).hexdigest() == g["sha256"]
+
+
+def _gloo_stream_rank(rank, world, port, result, nframes):
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import jxg
+        from jxg.dist import SharedHostBuffer, ShardStream, encode_sharded
+        from jxg.synth import synth_rgb8_device
+
+        w, h = 4096, 512
+        ts = [synth_rgb8_device(w, h, 0x77 + k) for k in range(nframes)]
+        res = {}
+        for ans in (False, True):
+            flags = jxg.FLAG_ANS if ans else 0
+            with jxg.Encoder(flags=flags) as enc:
+                bufs = {}  # persistent exchange / payload buffers across frames
+                dev = [encode_sharded(enc, t, w, h, rank, world, bufs=bufs) for t in ts]
+                host = SharedHostBuffer(rank, world)
+                hst = [encode_sharded(enc, t, w, h, rank, world, bufs=bufs, host=host) for t in ts]
+                dist.barrier()
+                host.close()
+                ref = [enc.encode_device(t.data_ptr(), w, h) for t in ts] if rank == 0 else None
+            res[ans] = (dev, hst, ref)
+        with jxg.Encoder(flags=jxg.FLAG_ANS) as enc:
+            ss = ShardStream(enc, w, h, rank, world)
+            got = []
+            for t in ts:
+                ss.submit(t.data_ptr())
+                while ss.pending() > ss.depth:
+                    got.append(ss.receive())
+            while ss.pending():
+                got.append(ss.receive())
+            got = [None if g is None else g.tobytes() for g in got]
+            ss.close()
+        if rank == 0:
+            result.put((res, got))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_multiprocess_streamed_frames(jxg_mod, decoder):
+    """Two processes (gloo, both ranks on cuda:0) stream 12 frames: the
+    one-frame-at-a-time sharded encode with persistent exchange / payload
+    buffers, device and host assembly, both coders; and jxg.dist.ShardStream
+    (the multi-GPU pipeline: no collective inside a frame, heads swapped in
+    /dev/shm).  Prefix codes: every frame == the single-GPU bytes; ANS: the
+    streamed bytes == the one-at-a-time sharded bytes, and the image == the
+    single-GPU image."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    nframes = 12
+    procs = [ctx.Process(target=_gloo_stream_rank, args=(r, 2, port, q, nframes))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    res, got = q.get(timeout=280)
+    for p in procs:
+        p.join(300)
+        assert p.exitcode == 0
+    dev, hst, ref = res[False]
+    assert [bytes(x) for x in dev] == ref and [bytes(x) for x in hst] == ref
+    dev, hst, ref = res[True]
+    assert [bytes(x) for x in dev] == [bytes(x) for x in hst]
+    assert got == [bytes(x) for x in dev]
+    dr, dg = decoder.decode(ref[3]), decoder.decode(got[3])
+    assert dg.npresets == 2
+    _same_image(dr, dg)

@@ -104,32 +104,151 @@ def test_gloo_world2_gather_and_assemble(jxg_mod, oracle, decoder):
     assert q.get(timeout=10) == (True, True)
 
 
-@pytest.mark.parametrize("w,h,world", [(7680, 4320, 2), (7680, 4320, 8), (16384, 16384, 8),
-                                       (3840, 2160, 4), (2100, 600, 8), (4100, 5000, 3)])
-def test_record_exchange_plan(jxg_mod, w, h, world):
-    """jxg_shard_exchange (C++) against the Python mirror of the LF ownership:
-    a rank sends each of its pass groups' records to the owner of the group's
-    LF group (if another rank), receives the other ranks' groups inside its
-    own LF groups; sends and receives pair up across ranks."""
-    rec = 1024 * 2 + 1024 * 4 * 3 + 32  # acs, qf, DC, and the 16 colour tiles ytox / ytob
-    owners = jxg_mod.lf_owners(w, h, world)
+def partition_py(w, h, world):
+    """Restatement of jxg_host.cpp make_partition (include/jxg.h): kind 0
+    contiguous raster ranges when no LF group is split over ranks; else kind 1
+    whole LF groups (largest pixel area first, ties by index, to the
+    least-loaded rank, ties to the lower rank) when the largest load is within
+    5 % of the mean; else kind 2 (ranges + the record exchange)."""
     gxs, gys = -(-w // 256), -(-h // 256)
+    lfxs, lfys = -(-w // 2048), -(-h // 2048)
+    ng, nlf = gxs * gys, lfxs * lfys
+    if world == 1:
+        return [0] * ng, [0] * nlf, 0
+
+    def shard_of(g):
+        r = g * world // ng
+        while r + 1 < world and ng * (r + 1) // world <= g:
+            r += 1
+        while r > 0 and ng * r // world > g:
+            r -= 1
+        return r
+
+    def lf_of(g):
+        return (g // gxs) // 8 * lfxs + (g % gxs) // 8
+
+    grp = [shard_of(g) for g in range(ng)]
+    own, nas = [], [0] * world
+    for lg in range(nlf):
+        lx, ly = lg % lfxs, lg // lfxs
+        cnt = [0] * world
+        for gy in range(ly * 8, min(ly * 8 + 8, gys)):
+            for gx in range(lx * 8, min(lx * 8 + 8, gxs)):
+                cnt[shard_of(gy * gxs + gx)] += 1
+        best, bs = -1, 0
+        for r in range(world):
+            if cnt[r] and (best < 0 or cnt[r] - 16 * nas[r] > bs):
+                best, bs = r, cnt[r] - 16 * nas[r]
+        own.append(best)
+        nas[best] += 1
+    if all(own[lf_of(g)] == grp[g] for g in range(ng)):
+        return grp, own, 0
+    if nlf >= world:
+        area = [min(2048, w - (lg % lfxs) * 2048) * min(2048, h - (lg // lfxs) * 2048)
+                for lg in range(nlf)]
+        load, lfo = [0] * world, [0] * nlf
+        for lg in sorted(range(nlf), key=lambda i: -area[i]):
+            r = min(range(world), key=lambda q: (load[q], q))
+            lfo[lg] = r
+            load[r] += area[lg]
+        if min(load) > 0 and max(load) * 100 * world <= sum(area) * 105:
+            return [lfo[lf_of(g)] for g in range(ng)], lfo, 1
+    return grp, own, 2
+
+
+SHAPES = [(7680, 4320, 2), (7680, 4320, 4), (7680, 4320, 8), (16384, 16384, 8),
+          (3840, 2160, 2), (3840, 2160, 4), (2100, 600, 8), (4100, 5000, 3), (4096, 512, 2),
+          (8192, 512, 4), (1920, 1080, 1)]
+
+
+@pytest.mark.parametrize("w,h,world", SHAPES)
+def test_partition_matches_restatement(jxg_mod, w, h, world):
+    assert jxg_mod.shard_plan(w, h, world) == partition_py(w, h, world)
+
+
+def test_partition_kinds(jxg_mod):
+    """BASELINE config 2 (8K) over 2 / 4 / 8 ranks: whole LF groups, balanced
+    to a few percent, no record exchange; config 4 (16384^2 over 8): aligned
+    ranges."""
+    for world in (2, 4, 8):
+        go, lo, kind = jxg_mod.shard_plan(7680, 4320, world)
+        assert kind == 1
+        cnt = [go.count(r) for r in range(world)]
+        assert max(cnt) <= 1.05 * 510 / world
+        assert all(sum(jxg_mod.shard_exchange(7680, 4320, world, r)[0]) == 0 for r in range(world))
+    go, lo, kind = jxg_mod.shard_plan(16384, 16384, 8)
+    assert kind == 0 and go == [g * 8 // 4096 for g in range(4096)]
+
+
+@pytest.mark.parametrize("w,h,world", SHAPES)
+def test_record_exchange_plan(jxg_mod, w, h, world):
+    """jxg_shard_exchange (C++) against the partition: a rank sends each of its
+    pass groups' records to the owner of the group's LF group (if another
+    rank), receives the other ranks' groups inside its own LF groups; sends
+    and receives pair up across ranks."""
+    rec = 1024 * 2 + 1024 * 4 * 3 + 32  # acs, qf, DC, and the 16 colour tiles ytox / ytob
+    go, owners, kind = jxg_mod.shard_plan(w, h, world)
+    gxs = -(-w // 256)
     lfxs = -(-w // 2048)
-    ng = gxs * gys
+    ng = len(go)
     plan = [jxg_mod.shard_exchange(w, h, world, r) for r in range(world)]
     for r in range(world):
         snd, rcv = plan[r]
         for p in range(world):
-            want = sum(1 for g in range(ng * r // world, ng * (r + 1) // world)
-                       if p != r and owners[(g // gxs) // 8 * lfxs + (g % gxs) // 8] == p)
+            want = sum(1 for g in range(ng)
+                       if go[g] == r and p != r and owners[(g // gxs) // 8 * lfxs + (g % gxs) // 8] == p)
             assert snd[p] == want * rec
             assert rcv[p] == plan[p][0][r]  # what p sends to r
-    # every LF group has an owner that holds part of it; owners spread out
     assert all(0 <= o < world for o in owners)
     _, cap = jxg_mod.shard_sizes(w, h, world)
     assert all(max(sum(s), sum(rv)) <= cap for s, rv in plan)
-    if (w, h, world) == (16384, 16384, 8):
-        assert all(sum(s) == 0 for s, _ in plan)  # LF groups aligned with the ranks
-    if (w, h, world) == (7680, 4320, 8):
-        total = sum(sum(s) for s, _ in plan)
-        assert total < 7680 * 4320 // 64 * 14  # well under an all-gather's worth
+    assert (kind == 2) == any(sum(s) for s, _ in plan)
+
+
+def _v2_payload(rank, world, w, h, sections, nh=1, cm=None, counts=None, fix_b=None):
+    """A version-2 payload (one HF preset per rank, jxg_host.cpp shard_finish):
+    head, [B][nhist][context map bytes in words][counts nhist x 128], body."""
+    cw = (7425 + 3) // 4
+    cm = np.zeros(7425, dtype=np.uint8) if cm is None else cm
+    counts = np.full((nh, 128), 0, dtype=np.uint32) if counts is None else counts
+    if counts.size:
+        counts[:, 0] = 1000
+        counts[:, 1] = 24
+    cmw = np.zeros(cw * 4, dtype=np.uint8)
+    cmw[:7425] = cm
+    B = 1 + cw + counts.size if fix_b is None else fix_b
+    head = np.array([0x5347584A, 2, rank, world, w, h, len(sections)] +
+                    [v for i, b in sections for v in (i, len(b))] + [B, nh], dtype="<u4")
+    body = head.tobytes() + cmw.tobytes() + counts.astype("<u4").tobytes()
+    return body + b"".join(b for _, b in sections)
+
+
+def test_assemble_v2_presets(jxg_mod):
+    """Host-only assembly of version-2 payload heads (ANS, one HF preset per
+    rank): HfGlobal is generated from the presets (num_hf_presets = ranks);
+    malformed preset blocks are refused."""
+    w, h, world = 4096, 512, 2
+    ids = [jxg_mod.shard_sections(w, h, r, world, ans=True) for r in range(world)]
+    nlf = jxg_mod.lf_group_count(w, h)
+    assert 1 + nlf not in ids[0] + ids[1]  # HfGlobal comes from the presets
+    secs = {i: bytes([(i * 7 + k) & 255 for k in range(5 + i % 3)]) for r in ids for i in r}
+    good = [_v2_payload(r, world, w, h, [(i, secs[i]) for i in ids[r]]) for r in range(world)]
+    out = jxg_mod.shard_assemble(good)
+    body = sum(len(b) for b in secs.values())
+    assert len(out) > body
+    for r in range(world):  # every section's bytes appear in the codestream
+        for i in ids[r]:
+            assert secs[i] in out
+    bad = []
+    bad.append([_v2_payload(0, world, w, h, [(i, secs[i]) for i in ids[0]], nh=0), good[1]])
+    bad.append([_v2_payload(0, world, w, h, [(i, secs[i]) for i in ids[0]], nh=9,
+                            counts=np.zeros((9, 128), dtype=np.uint32)), good[1]])
+    cm = np.zeros(7425, dtype=np.uint8)
+    cm[100] = 1  # context mapped past the preset's one histogram
+    bad.append([_v2_payload(0, world, w, h, [(i, secs[i]) for i in ids[0]], cm=cm), good[1]])
+    bad.append([_v2_payload(0, world, w, h, [(i, secs[i]) for i in ids[0]], fix_b=5), good[1]])
+    # a version-1 rank among version-2 ranks
+    bad.append([jxg_mod.make_payload(0, world, w, h, [(i, secs[i]) for i in ids[0]]), good[1]])
+    for pl in bad:
+        with pytest.raises(jxg_mod.JxgError):
+            jxg_mod.shard_assemble(pl)
