@@ -12,10 +12,12 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "liboracle.so")
+LIB = os.environ.get("JXO_LIB_PATH") or os.path.join(HERE, "liboracle.so")  # ASan runs
 
 
 def build(force: bool = False):
+    if os.environ.get("JXO_LIB_PATH"):
+        return  # a prebuilt variant (tools/asan_suite.sh)
     if force or not os.path.exists(LIB) or any(
             os.path.getmtime(os.path.join(HERE, f)) > os.path.getmtime(LIB)
             for f in os.listdir(HERE) if f.endswith((".c", ".h"))):

@@ -17,7 +17,8 @@ def prefix_parity_bin(tmp_path_factory):
     if shutil.which("g++") is None or shutil.which("gcc") is None:
         pytest.skip("no host compiler")
     d = tmp_path_factory.mktemp("pp")
-    flags = ["-O2", "-ffp-contract=off"]
+    # JXG_NATIVE_CFLAGS: extra flags, e.g. the sanitizers of tools/asan_suite.sh
+    flags = ["-O2", "-ffp-contract=off"] + os.environ.get("JXG_NATIVE_CFLAGS", "").split()
     subprocess.check_call(["g++", "-std=c++17", *flags, "-c", os.path.join(PKG, "jxg_bitstream.cpp"),
                            "-o", str(d / "bs.o")])
     subprocess.check_call(["gcc", "-std=c11", *flags, "-I", os.path.join(ROOT, "oracle"), "-c",
