@@ -471,7 +471,13 @@ __device__ __forceinline__ void haar_lane(const GroupCtx& G, float* v) {
 // Quantization of lane r's 8 values of channel C (0 X, 1 Y, 2 B) under
 // strategy T: accumulate e*e (fmaf), rate bits and the non-zero count; Y
 // records its dequantized values for the X / B residuals.  Float op order ==
-// oracle jxo_quantize_block.
+// oracle jxo_quantize_block.  Coefficients go in pairs (k, k + 1): every
+// float multiply / add / subtract of the pair is one packed op (f2: each half
+// is exactly the scalar op, no contraction); the e*e chain stays in k order.
+// qa is kept as an integer-valued float qf (the truncation of a positive value
+// is its floor): the error needs no conversion, and the rate 2 + 2 bitlen(qa)
+// of a non-zero is 2 E - 250, E = the biased exponent of qf.
+typedef float f2 __attribute__((ext_vector_type(2)));
 template <int T, int C>
 __device__ __forceinline__ void quant_lane(const GroupCtx& G, float* v, float scale,
                                            float inv_scale, CandAcc& A) {
@@ -480,46 +486,66 @@ __device__ __forceinline__ void quant_lane(const GroupCtx& G, float* v, float sc
   if (G.r == 0) v[0] = 0.0f;  // DC slot: quantizes to 0, contributes nothing
   const float4* wp = reinterpret_cast<const float4*>(G.wperm + ((ti * 3 + C) * 8 + G.r) * 8);
   const float4 w0 = wp[0], w1 = wp[1];
-  const float wk[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-  const float* sdk = G.sdperm + ((ti * 3 + C) * 8 + G.r) * 8;  // read at use
-  float iwk[8];
+  const f2 wk2[4] = {f2{w0.x, w0.y}, f2{w0.z, w0.w}, f2{w1.x, w1.y}, f2{w1.z, w1.w}};
+  const float2* sdp = reinterpret_cast<const float2*>(G.sdperm + ((ti * 3 + C) * 8 + G.r) * 8);
+  f2 iwk2[4];
   if (C == 1) {
     const float4* ip = reinterpret_cast<const float4*>(G.iwperm + (ti * 8 + G.r) * 8);
     const float4 i0 = ip[0], i1 = ip[1];
-    iwk[0] = i0.x; iwk[1] = i0.y; iwk[2] = i0.z; iwk[3] = i0.w;
-    iwk[4] = i1.x; iwk[5] = i1.y; iwk[6] = i1.z; iwk[7] = i1.w;
+    iwk2[0] = f2{i0.x, i0.y};
+    iwk2[1] = f2{i0.z, i0.w};
+    iwk2[2] = f2{i1.x, i1.y};
+    iwk2[3] = f2{i1.z, i1.w};
   }
-  int nz = 0, clzs = 0;
+  const f2 sc2 = f2{scale, scale}, isc2 = f2{inv_scale, inv_scale};
+  int nz = 0;
+  uint32_t ebits = 0;
   int qs[8];
 #pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const float ws = wk[k] * scale;
-    float rv = v[k];
-    if (C == 0) rv = rv - G.kx * A.yd[k];
-    if (C == 2) rv = rv - G.kb * A.yd[k];
-    const float vq = rv * ws;
-    const float a = fabsf(vq);
-    const int qa = a < 0.58f ? 0 : (int)(fminf(a, 32767.0f) + 0.5f);
+  for (int kp = 0; kp < 4; kp++) {
+    const int k = 2 * kp;
+    const f2 ws = wk2[kp] * sc2;
+    f2 rv = f2{v[k], v[k + 1]};
+    if (C == 0) rv = rv - f2{G.kx, G.kx} * f2{A.yd[k], A.yd[k + 1]};
+    if (C == 2) rv = rv - f2{G.kb, G.kb} * f2{A.yd[k], A.yd[k + 1]};
+    const f2 vq = rv * ws;
+    const f2 a = f2{fabsf(vq.x), fabsf(vq.y)};
+    f2 qf;
+    qf.x = a.x < 0.58f ? 0.0f : floorf(fminf(a.x, 32767.0f) + 0.5f);
+    qf.y = a.y < 0.58f ? 0.0f : floorf(fminf(a.y, 32767.0f) + 0.5f);
     if (C == 1) {
-      float bq = G.btab[qa < 255 ? qa : 255];
-      if (__any(qa >= 256)) {
-        if (qa >= 256) bq = 0.145f / (float)qa;
+      f2 adj;
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const float q = h ? qf.y : qf.x;
+        const int qa = (int)q;
+        float bq = G.btab[qa < 255 ? qa : 255];
+        if (__any(qa >= 256)) {
+          if (qa >= 256) bq = 0.145f / q;
+        }
+        float ad = qa == 0 ? 0.0f : (qa == 1 ? kBias1 : q - bq);
+        if ((h ? vq.y : vq.x) < 0.0f) ad = -ad;
+        if (h) adj.y = ad;
+        else adj.x = ad;
       }
-      float adj = qa == 0 ? 0.0f : (qa == 1 ? kBias1 : (float)qa - bq);
-      if (vq < 0.0f) adj = -adj;
-      A.yd[k] = adj * (iwk[k] * inv_scale);
+      const f2 yd = adj * (iwk2[kp] * isc2);
+      A.yd[k] = yd.x;
+      A.yd[k + 1] = yd.y;
     }
     // quantization error in steps, times the distortion weight: the
     // coefficient's pixel-domain error (oracle jxo_dist_weight)
-    const float e = (a - (float)qa) * sdk[k];
-    A.part = fmaf(e, e, A.part);
-    // 2 + 2 bitlen(qa) per non-zero: bitlen(qa) = 31 - clz(2 qa + 1)
-    clzs += (int)__clz((uint32_t)(2 * qa + 1));
-    nz += qa != 0;
-    qs[k] = vq < 0.0f ? -qa : qa;
+    const float2 sd = sdp[kp];
+    const f2 e = (a - qf) * f2{sd.x, sd.y};
+    A.part = fmaf(e.x, e.x, A.part);
+    A.part = fmaf(e.y, e.y, A.part);
+    ebits += (__float_as_uint(qf.x) >> 23) + (__float_as_uint(qf.y) >> 23);
+    nz += (qf.x != 0.0f) + (qf.y != 0.0f);
+    const int q0 = (int)qf.x, q1 = (int)qf.y;
+    qs[k] = vq.x < 0.0f ? -q0 : q0;
+    qs[k + 1] = vq.y < 0.0f ? -q1 : q1;
   }
-  // sum over k of [qa != 0] (2 + 2 bitlen) = 2 nz + 2 (8 * 31 - clzs)
-  A.bits += 2 * nz + 2 * (8 * 31 - clzs);
+  // sum over k of [qa != 0] (2 + 2 bitlen) = 2 E-sum - 250 nz
+  A.bits += 2 * (int)ebits - 250 * nz;
   uint32_t pk[4];
 #pragma unroll
   for (int i = 0; i < 4; i++)
@@ -534,12 +560,16 @@ __device__ __forceinline__ void quant_lane(const GroupCtx& G, float* v, float sc
 }
 
 // one channel of one candidate: transform (row pass + transpose + column
-// transform, or the Haar steps) and quantization
-template <int T, int C>
+// transform, or the Haar steps) and quantization.  PRE: the DCT8 coefficients
+// of the channel were already computed (the chroma-from-luma fit, phase B0)
+template <int T, int C, bool PRE = false>
 __device__ __forceinline__ void eval_chan(const GroupCtx& G, float scale, float inv_scale,
-                                          CandAcc& A) {
+                                          CandAcc& A, const float* pre = nullptr) {
   float v[8];
-  if constexpr (T == kDCT2X2 || T == kIDENTITY) {
+  if constexpr (PRE) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[k] = pre[k];
+  } else if constexpr (T == kDCT2X2 || T == kIDENTITY) {
     haar_lane<T, C>(G, v);
   } else {
     row_pass_t<T == kDCT8 || T == kDCT8X4, C>(G, v);
@@ -549,17 +579,24 @@ __device__ __forceinline__ void eval_chan(const GroupCtx& G, float scale, float 
 }
 
 // One candidate, channels Y, X, B (its own row passes): only one candidate's
-// state is live at a time, which keeps the kernel inside 128 VGPRs.
-template <int T>
+// state is live at a time, which keeps the kernel inside 128 VGPRs.  PRE
+// (DCT8 only): pre[c] holds the channel's DCT8 coefficients.
+template <int T, bool PRE = false>
 __device__ __forceinline__ float eval_one(const GroupCtx& G, float scale, float inv_scale,
-                                          CandAcc& A) {
+                                          CandAcc& A, const float (*pre)[8] = nullptr) {
   A.bits = 0;
   A.part = 0.0f;
+  if constexpr (PRE) {  // registers, no channel loop (pre[c] indexed statically)
+    eval_chan<T, 1, true>(G, scale, inv_scale, A, pre[1]);
+    eval_chan<T, 0, true>(G, scale, inv_scale, A, pre[0]);
+    eval_chan<T, 2, true>(G, scale, inv_scale, A, pre[2]);
+  } else {
 #pragma unroll 1  // one channel live at a time
-  for (int ci = 0; ci < 3; ci++) {
-    if (ci == 0) eval_chan<T, 1>(G, scale, inv_scale, A);
-    else if (ci == 1) eval_chan<T, 0>(G, scale, inv_scale, A);
-    else eval_chan<T, 2>(G, scale, inv_scale, A);
+    for (int ci = 0; ci < 3; ci++) {
+      if (ci == 0) eval_chan<T, 1>(G, scale, inv_scale, A);
+      else if (ci == 1) eval_chan<T, 0>(G, scale, inv_scale, A);
+      else eval_chan<T, 2>(G, scale, inv_scale, A);
+    }
   }
   // estimate multipliers (== oracle jxo_quantize_block tmul, JXO_TMUL_*)
   constexpr float tm = T == kDCT8 ? 1.0f
@@ -760,12 +797,17 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
   // accumulates its coefficient column, the block's 8 lanes tree-sum, the
   // tile sums its blocks in raster order (phase-A scratch sH reused)
   float kx = 0.0f, kb = 1.0f;
+  // the fit's DCT8 coefficients [X, Y, B] (lane r: column r) are the DCT8
+  // candidate's transform too: kept for phase C instead of recomputed
+  float cf[3][8];
   if (a.effort >= 5) {
     float* cs = &sH[0][0];  // [4 sums][64 blocks]
     {
       const GroupCtx G0{sPix, lby * 8 + 1, lbx * 8 + 1, r, sWperm, sIwperm, sBtab, sSdperm,
                         0.0f, 1.0f};
-      float vy[8], vx[8], vb[8];
+      float* vy = cf[1];
+      float* vx = cf[0];
+      float* vb = cf[2];
       row_pass_t<true, 1>(G0, vy);
       dct8_1d(vy);
       row_pass_t<true, 0>(G0, vx);
@@ -888,7 +930,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
   // scan index), so this finds the scan's winner
   {
     CandAcc A;
-    float e = eval_one<kDCT8>(G, scale, inv_scale, A);
+    float e = ncand > 1 ? eval_one<kDCT8, true>(G, scale, inv_scale, A, cf)
+                        : eval_one<kDCT8>(G, scale, inv_scale, A);
     if (hookF) e = hook_f(e, rh, rv, rd);
     copy_q(best, A.q, true);
     if (ncand > 1) beste = e < FLT_MAX ? e : FLT_MAX;

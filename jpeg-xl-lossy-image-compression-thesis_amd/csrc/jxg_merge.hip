@@ -46,10 +46,10 @@ __constant__ float c_llf_ib[4 * 64]; // [log2 M][n][k]
 
 constexpr int kMThreads = 256;
 #ifndef JXG_MERGE_WPE
-#define JXG_MERGE_WPE 3  // waves per SIMD the eval/write kernels are register-capped for
+#define JXG_MERGE_WPE 4  // waves per SIMD the eval kernel is register-capped for (4 WGs / CU)
 #endif
 #ifndef JXG_MERGE_WRITE_WPE
-#define JXG_MERGE_WRITE_WPE JXG_MERGE_WPE
+#define JXG_MERGE_WRITE_WPE 3  // write: 167 VGPRs, no spills
 #endif
 constexpr int kMS = 65;  // LDS row stride (floats)
 constexpr int kMPlane = 64 * kMS;
@@ -150,13 +150,14 @@ constexpr ShapeDesc kShapes[kNumShapes] = {
 
 __device__ __forceinline__ int bitlen_u(uint32_t v) { return 32 - __clz(v); }
 
-// 53.7 KB: three workgroups per CU (gfx950 allocates LDS in 1280-byte
-// granules: 42 granules = 53760 B is the most that fits three; measured --
-// 256 more bytes dropped the eval kernel to two workgroups per CU)
+// Two coefficient planes (37.9 KB: four workgroups per CU -- gfx950
+// allocates LDS in 1280-byte granules, 31 granules = 39680 B is the most that
+// fits four; three planes, 53.7 KB, allowed three): plane 0 holds Y (its
+// dequantized values after the Y quantization, for the X / B residuals),
+// plane 1 X, then B -- B is transformed into plane 1 once X is quantized.
 struct MergeLds {
-  float co[3 * kMPlane];  // coefficient image of the tile's varblocks; column
-                          // 64 of row b of plane c (padding) holds the LLF of
-                          // covered block b in write mode
+  float co[2 * kMPlane];  // coefficient image of the tile's varblocks
+  float llf[3][64];       // write mode: the LLF of covered block b, per channel
   float qsum[3][4][32];   // [Y, X, B][chunk][varblock]: column-tree chunk sums
   float btab[256];        // 0.145f / q (AdjustQuantBias), q < 256
   float vr3[32][3];       // hook F: similarity indices of each top-left block
@@ -167,9 +168,13 @@ struct MergeLds {
   uint8_t braw[64];       // front-kernel quant field (raw) of the tile's blocks
   int any;
 };
-__device__ __forceinline__ float& llf_at(MergeLds& S, int c, int b) {
-  return S.co[c * kMPlane + b * kMS + 64];
-}
+__device__ __forceinline__ float& llf_at(MergeLds& S, int c, int b) { return S.llf[c][b]; }
+// the two transform passes of a tile: pass 0 = Y (plane 0) and X (plane 1),
+// pass 1 = B (plane 1); local channel lc of a pass -> frame channel (X 0, Y 1,
+// B 2) and LDS plane
+__device__ __forceinline__ int pass_src(int pass, int lc) { return pass ? 2 : 1 - lc; }
+__device__ __forceinline__ int pass_plane(int pass, int lc) { return pass ? 1 : lc; }
+__device__ __forceinline__ constexpr int chan_plane(int ch) { return ch == 1 ? 0 : 1; }
 
 // one (tile, shape) workgroup: all index math is shifts and masks
 struct Pass {
@@ -186,8 +191,8 @@ struct Pass {
   __device__ __forceinline__ int NV() const { return 1 << lNV(); }
   __device__ __forceinline__ int bx0(int v) const { return (v & ((1 << lGX()) - 1)) << lcx; }
   __device__ __forceinline__ int by0(int v) const { return (v >> lGX()) << lcy; }
-  __device__ __forceinline__ int off(int v, int c) const {
-    return c * kMPlane + by0(v) * 8 * kMS + bx0(v) * 8;
+  __device__ __forceinline__ int off(int v, int plane) const {
+    return plane * kMPlane + by0(v) * 8 * kMS + bx0(v) * 8;
   }
 };
 
@@ -243,22 +248,23 @@ __device__ __forceinline__ void load_row(const float* src, float* d) {
     d[4 * q + 3] = u.w;
   }
 }
-template <int C>
-__device__ void row_pass(const MergeArgs& a, const Pass& P, MergeLds& S) {
+template <int C, int NCH>
+__device__ __forceinline__ void row_pass(const MergeArgs& a, const Pass& P, MergeLds& S, int pass) {
   const float* tsrc = a.xyb + (size_t)P.tile * (3 * 4096);
   const int R = P.R(), lvr = P.lNV() + P.lR();
   if constexpr (C == 64) {
     // item = (row pair, half h): rows r and r + 1 of one varblock and channel
     // (R >= 32: pairs never straddle a varblock); h is wave-uniform: waves
     // alternate h over 64-pair chunks
-    const int npairs = 3 * P.NV() * R / 2;  // 96
+    const int npairs = NCH * P.NV() * R / 2;  // 64 / 32
     const int n = ((npairs + 63) >> 6) << 7;
     for (int i = threadIdx.x; i < n; i += kMThreads) {
       const int h = (i >> 6) & 1, pp = ((i >> 7) << 6) | (i & 63), r = pp * 2;
       if (pp >= npairs) continue;
       const int c = r >> lvr, v = (r >> P.lR()) & (P.NV() - 1), y = r & (R - 1);
       if (!S.valid[v]) continue;
-      const float4* s0 = reinterpret_cast<const float4*>(tsrc + c * 4096 + (P.by0(v) * 8 + y) * 64);
+      const float4* s0 =
+          reinterpret_cast<const float4*>(tsrc + pass_src(pass, c) * 4096 + (P.by0(v) * 8 + y) * 64);
       const float4* s1 = s0 + 16;  // row y + 1
       f2 t[32];
       // 16-byte loads of x[4q..4q+3] and of its mirror x[60-4q..63-4q]
@@ -271,7 +277,7 @@ __device__ void row_pass(const MergeArgs& a, const Pass& P, MergeLds& S) {
         for (int j = 0; j < 4; j++)
           t[4 * q + j] = dct64_first(f2{fa0[j], fa1[j]}, f2{fb0[3 - j], fb1[3 - j]}, 4 * q + j, h);
       }
-      const int off = P.off(v, c) + y * kMS;
+      const int off = P.off(v, pass_plane(pass, c)) + y * kMS;
       dct64_rest(t, h, [&](int k, f2 o) {
         S.co[off + 2 * k + h] = o.x;
         S.co[off + kMS + 2 * k + h] = o.y;
@@ -282,8 +288,8 @@ __device__ void row_pass(const MergeArgs& a, const Pass& P, MergeLds& S) {
     // Row r of a channel: the varblock column is the fastest index, so the
     // lanes of a wave read whole 256-byte tile rows (coalesced) instead of
     // one C-float chunk per cache line
-    constexpr int PER = (3 * 4096 / C + kMThreads - 1) / kMThreads;  // 6, 3, 2
-    const int nrows = 3 * P.NV() * R;
+    constexpr int PER = (NCH * 4096 / C + kMThreads - 1) / kMThreads;  // 2 ch: 4, 2, 1
+    const int nrows = NCH * P.NV() * R;
     const int lgx = P.lGX();
     auto row_of = [&](int rr, int& c, int& v, int& y) {
       c = rr >> lvr;
@@ -298,7 +304,8 @@ __device__ void row_pass(const MergeArgs& a, const Pass& P, MergeLds& S) {
       if (r < nrows) {
         int c, v, y;
         row_of(r, c, v, y);
-        load_row<C>(tsrc + c * 4096 + (P.by0(v) * 8 + y) * 64 + P.bx0(v) * 8, buf[k]);
+        load_row<C>(tsrc + pass_src(pass, c) * 4096 + (P.by0(v) * 8 + y) * 64 + P.bx0(v) * 8,
+                    buf[k]);
       } else {
 #pragma unroll
         for (int q = 0; q < C; q++) buf[k][q] = 0.0f;
@@ -319,7 +326,8 @@ __device__ void row_pass(const MergeArgs& a, const Pass& P, MergeLds& S) {
 #pragma unroll
         for (int q = 0; q < C; q++) x[q] = f2{buf[k][q], buf[k + 1][q]};
         lee<C>(x);
-        const int off0 = P.off(v0, c0) + y0 * kMS, off1 = P.off(v1, c1) + y1 * kMS;
+        const int off0 = P.off(v0, pass_plane(pass, c0)) + y0 * kMS,
+                  off1 = P.off(v1, pass_plane(pass, c1)) + y1 * kMS;
 #pragma unroll
         for (int q = 0; q < C; q++) {
           const f2 o = x[q] * kLeeS[l][q];
@@ -329,7 +337,7 @@ __device__ void row_pass(const MergeArgs& a, const Pass& P, MergeLds& S) {
       } else {
         float* x = buf[k];
         lee<C>(x);
-        const int off0 = P.off(v0, c0) + y0 * kMS;
+        const int off0 = P.off(v0, pass_plane(pass, c0)) + y0 * kMS;
 #pragma unroll
         for (int q = 0; q < C; q++) S.co[off0 + q] = x[q] * kLeeS[l][q];
       }
@@ -342,14 +350,14 @@ __device__ void row_pass(const MergeArgs& a, const Pass& P, MergeLds& S) {
 // lanes; any two columns of a band have the same length, whatever varblocks
 // they belong to): the two LDS reads of a pair are one ds_read2 and the 32
 // lanes of a band read 64 consecutive columns.  64-point: item = (pair, h).
-template <int R>
-__device__ void col_pass(const Pass& P, MergeLds& S) {
+template <int R, int NCH>
+__device__ __forceinline__ void col_pass(const Pass& P, MergeLds& S, int pass) {
   constexpr int lR = ilog2c<R>(), nb = 64 / R, lnb = 6 - lR;
-  constexpr int npairs = 3 * nb * 32;  // (channel, band, X)
+  constexpr int npairs = NCH * nb * 32;  // (channel, band, X)
   const int lGX = P.lGX(), lC = P.lC();
   auto col_of = [&](int pidx, int& off, bool& okA, bool& okB) {
     const int X = pidx & 31, band = (pidx >> 5) & (nb - 1), c = pidx >> (5 + lnb);
-    off = c * kMPlane + band * R * kMS + X;
+    off = pass_plane(pass, c) * kMPlane + band * R * kMS + X;
     okA = S.valid[(band << lGX) | (X >> lC)];
     okB = S.valid[(band << lGX) | ((X + 32) >> lC)];
   };
@@ -453,7 +461,7 @@ __device__ __forceinline__ void load_qtab(const MergeArgs& a, const Pass& P, QTa
   }
 }
 template <int RPC, bool WRITE, int CH>
-__device__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S, const QTab<RPC>& T) {
+__device__ __forceinline__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S, const QTab<RPC>& T) {
   constexpr int cidx = CH == 1 ? 0 : (CH == 0 ? 1 : 2);  // 0 Y, 1 X, 2 B
   constexpr float kBias1 = 1.0f - 0.07005449891748593f;
   const int C = P.C(), NV = P.NV();
@@ -470,8 +478,8 @@ __device__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S, const
     if (!S.valid[v]) continue;  // the varblock's C lanes leave together
     const int bx0 = P.bx0(v), by0 = P.by0(v);
     const float scale = (float)a.G * (float)S.vraw[v] / 65536.0f;
-    float* cplane = S.co + P.off(v, CH) + x;
-    const float* yd = S.co + P.off(v, 1) + x;
+    float* cplane = S.co + P.off(v, chan_plane(CH)) + x;
+    const float* yd = S.co + P.off(v, 0) + x;
     const float* w = T.w[it];
     const float* sd = T.sd[it];
     float iw[RPC];
@@ -574,28 +582,34 @@ __device__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S, const
 // transform + quantize every valid varblock of the pass; leaves per-varblock
 // bits / non-zeros and the chunk sums in LDS
 template <bool WRITE>
-__device__ void transform_quant(const MergeArgs& a, const Pass& P, MergeLds& S) {
+__device__ __forceinline__ void transform_quant(const MergeArgs& a, const Pass& P, MergeLds& S) {
 #ifdef JXG_MERGE_PROFILE
   unsigned long long mprof_t0 = 0;
 #endif
   MPROF_MARK(0);
-  switch (P.lcx) {
-    case 0: row_pass<8>(a, P, S); break;
-    case 1: row_pass<16>(a, P, S); break;
-    case 2: row_pass<32>(a, P, S); break;
-    default: row_pass<64>(a, P, S); break;
-  }
-  __syncthreads();
+  auto transform = [&](auto nch_tag, int pass) {
+    constexpr int NCH = decltype(nch_tag)::value;
+    switch (P.lcx) {
+      case 0: row_pass<8, NCH>(a, P, S, pass); break;
+      case 1: row_pass<16, NCH>(a, P, S, pass); break;
+      case 2: row_pass<32, NCH>(a, P, S, pass); break;
+      default: row_pass<64, NCH>(a, P, S, pass); break;
+    }
+    __syncthreads();
+    switch (P.lcy) {
+      case 0: col_pass<8, NCH>(P, S, pass); break;
+      case 1: col_pass<16, NCH>(P, S, pass); break;
+      case 2: col_pass<32, NCH>(P, S, pass); break;
+      default: col_pass<64, NCH>(P, S, pass); break;
+    }
+  };
+  transform(std::integral_constant<int, 2>(), 0);  // Y -> plane 0, X -> plane 1
   MPROF_MARK(1);
-  switch (P.lcy) {
-    case 0: col_pass<8>(P, S); break;
-    case 1: col_pass<16>(P, S); break;
-    case 2: col_pass<32>(P, S); break;
-    default: col_pass<64>(P, S); break;
-  }
   // Y first: its dequantized values replace its coefficients (X / B
-  // residuals); every pass's tables are in flight across the barrier before it
-  auto quant3 = [&](auto rpc_tag) {
+  // residuals); then X; then B is transformed into X's plane.  Every pass's
+  // tables are in flight across the barrier before it.  A lane's X / B items
+  // read the Y values its own Y item wrote (same item map).
+  auto quant_yx = [&](auto rpc_tag) {
     constexpr int RPC = decltype(rpc_tag)::value;
     {
       QTab<RPC> ty;
@@ -604,16 +618,24 @@ __device__ void transform_quant(const MergeArgs& a, const Pass& P, MergeLds& S) 
       MPROF_MARK(2);
       quant_pass<RPC, WRITE, 1>(a, P, S, ty);
     }
-    QTab<RPC> tx, tb;
+    QTab<RPC> tx;
     load_qtab<RPC, WRITE, 0>(a, P, tx);
+    quant_pass<RPC, WRITE, 0>(a, P, S, tx);
+  };
+  auto quant_b = [&](auto rpc_tag) {
+    constexpr int RPC = decltype(rpc_tag)::value;
+    QTab<RPC> tb;
     load_qtab<RPC, WRITE, 2>(a, P, tb);
     __syncthreads();
-    MPROF_MARK(3);
-    quant_pass<RPC, WRITE, 0>(a, P, S, tx);
     quant_pass<RPC, WRITE, 2>(a, P, S, tb);
   };
-  if (P.lcy == 0) quant3(std::integral_constant<int, 8>());
-  else quant3(std::integral_constant<int, 16>());
+  if (P.lcy == 0) quant_yx(std::integral_constant<int, 8>());
+  else quant_yx(std::integral_constant<int, 16>());
+  __syncthreads();  // plane 1 (X) fully read
+  MPROF_MARK(3);
+  transform(std::integral_constant<int, 1>(), 1);  // B -> plane 1
+  if (P.lcy == 0) quant_b(std::integral_constant<int, 8>());
+  else quant_b(std::integral_constant<int, 16>());
   __syncthreads();
   MPROF_MARK(4);
 }

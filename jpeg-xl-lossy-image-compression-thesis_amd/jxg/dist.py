@@ -340,15 +340,20 @@ class ShardStream:
         self.received = 0    # frames returned by receive()
         self.totals = {}
 
-    @staticmethod
-    def _wait(cond, what):
+    def _wait(self, cond, what):
         t0 = time.perf_counter()
-        spins = 0
+        spins, told = 0, False
         while not cond():
             spins += 1
             if spins > 64:
                 time.sleep(20e-6)
-            if time.perf_counter() - t0 > 120:
+            dt = time.perf_counter() - t0
+            if dt > 10 and not told:  # a rank is far behind (or gone): say so once
+                import sys
+                print("ShardStream rank %d: waiting %.0f s for %s" % (self.rank, dt, what),
+                      file=sys.stderr, flush=True)
+                told = True
+            if dt > 120:
                 raise RuntimeError("ShardStream: timed out waiting for " + what)
 
     def pending(self) -> int:

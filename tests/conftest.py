@@ -7,7 +7,7 @@ import pytest
 # caps its depth at the process's hardware queues - 1 (GPU_MAX_HW_QUEUES,
 # HIP's default 4): the tests run it at the depth bench.py uses.  Set before
 # HIP initialises (the torch import below).
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 # torch's bundled HIP runtime has the same soname (libamdhip64.so.7) as the
 # system one libjxg.so links; importing torch first makes the process use a

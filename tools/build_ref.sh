@@ -1,0 +1,21 @@
+#!/bin/bash
+# A/B baseline builds: tools/build_ref.sh GITREF NAME [FILE...] -> tools/var/libjxg_NAME.so
+# (csrc/ and include/ as of GITREF, with the listed csrc files taken from the
+# working tree instead; same flags as the product Makefile)
+set -e
+REF=$1; NAME=$2; shift 2
+D=$(cd "$(dirname "$0")/.." && pwd)
+T=$(mktemp -d)
+git -C $D archive $REF jpeg-xl-lossy-image-compression-thesis_amd/csrc include | tar -x -C $T
+P=$T/jpeg-xl-lossy-image-compression-thesis_amd
+for f in "$@"; do cp $D/jpeg-xl-lossy-image-compression-thesis_amd/csrc/$f $P/csrc/$f; done
+HIPFLAGS="-O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=gfx950 -Wno-unused-function"
+pids=()
+for f in $P/csrc/*.hip $P/csrc/jxg_host.cpp $P/csrc/jxg_bitstream.cpp; do
+  b=$(basename $f); /opt/rocm/bin/hipcc $HIPFLAGS -c $f -o $T/${b%.*}.o & pids+=($!)
+done
+for p in ${pids[@]}; do wait $p; done
+mkdir -p $D/tools/var
+/opt/rocm/bin/hipcc $HIPFLAGS -shared -o $D/tools/var/libjxg_$NAME.so $T/*.o
+rm -rf $T
+echo built tools/var/libjxg_$NAME.so
