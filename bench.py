@@ -307,7 +307,8 @@ def main():
             rec["host_ms"].append(t[1:])
             rec["sizes"].append(len(out) if out is not None else 0)
             if k % nd == 0:
-                rec["last"] = out
+                # shared-memory views (ShardStream) are recycled: keep a copy
+                rec["last"] = out.tobytes() if isinstance(out, np.ndarray) else out
 
         ss = None
         host = None
@@ -325,6 +326,9 @@ def main():
             # the codestream ends in (pinned / shared) host memory; ctypes
             # calls release the GIL, so several encoders' host work overlaps
             if ss is not None:
+                # (a received view stays valid for the next slots - 1
+                # receives: took() keeps only its size, and the first frame's
+                # bytes are copied when it is the last one kept)
                 got = 0
                 for k in ks:
                     ss.submit(d_imgs[k % nd].data_ptr())

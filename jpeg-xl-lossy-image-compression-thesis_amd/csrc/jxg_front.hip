@@ -219,28 +219,43 @@ constexpr float kA = 0x1.63150cp-3f, kB = 0x1.2d062ep-3f, kC = 0x1.92469cp-4f,
                 kD = 0x1.1a855ep-5f, kE1 = 0x1.4e7aeap-3f, kE3 = 0x1.1517a8p-4f,
                 kF1 = 0x1.4e7aeap-2f, kF3 = 0x1.1517a8p-3f;
 
-__device__ __forceinline__ void dct8_1d(float* v) {
-  const float x0 = v[0], x1 = v[1], x2 = v[2], x3 = v[3], x4 = v[4], x5 = v[5], x6 = v[6],
-              x7 = v[7];
-  const float s0 = x0 + x7, s1 = x1 + x6, s2 = x2 + x5, s3 = x3 + x4;
-  const float d0 = x0 - x7, d1 = x1 - x6, d2 = x2 - x5, d3 = x3 - x4;
-  const float a0 = s0 + s3, a1 = s1 + s2, b0 = s0 - s3, b1 = s1 - s2;
-  v[0] = (a0 + a1) * 0.125f;
-  v[4] = (a0 - a1) * 0.125f;
-  v[2] = fmaf(b1, kE3, b0 * kE1);
-  v[6] = fmaf(b1, -kE1, b0 * kE3);
-  v[1] = fmaf(d3, kD, fmaf(d2, kC, fmaf(d1, kB, d0 * kA)));
-  v[3] = fmaf(d3, -kC, fmaf(d2, -kA, fmaf(d1, -kD, d0 * kB)));
-  v[5] = fmaf(d3, kB, fmaf(d2, kD, fmaf(d1, -kA, d0 * kC)));
-  v[7] = fmaf(d3, -kA, fmaf(d2, kB, fmaf(d1, -kC, d0 * kD)));
+// X and B go through the candidates together: f2 holds (X, B) of one
+// element, and every float op of the pair is one packed VALU op (v_pk_*: each
+// half is exactly the scalar op, no contraction) -- the per-channel float op
+// sequence is unchanged, so the results stay bit-identical.
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float vfma(float a, float b, float c) { return fmaf(a, b, c); }
+__device__ __forceinline__ f2 vfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+template <class V>
+__device__ __forceinline__ V splat(float c) {
+  if constexpr (std::is_same<V, float>::value) return c;
+  else return f2{c, c};
 }
-__device__ __forceinline__ void dct4_1d(float* v) {
-  const float x0 = v[0], x1 = v[1], x2 = v[2], x3 = v[3];
-  const float s0 = x0 + x3, s1 = x1 + x2, d0 = x0 - x3, d1 = x1 - x2;
-  v[0] = (s0 + s1) * 0.25f;
-  v[2] = (s0 - s1) * 0.25f;
-  v[1] = fmaf(d1, kF3, d0 * kF1);
-  v[3] = fmaf(d1, -kF1, d0 * kF3);
+
+template <class V>
+__device__ __forceinline__ void dct8_1d(V* v) {
+  const V x0 = v[0], x1 = v[1], x2 = v[2], x3 = v[3], x4 = v[4], x5 = v[5], x6 = v[6], x7 = v[7];
+  const V s0 = x0 + x7, s1 = x1 + x6, s2 = x2 + x5, s3 = x3 + x4;
+  const V d0 = x0 - x7, d1 = x1 - x6, d2 = x2 - x5, d3 = x3 - x4;
+  const V a0 = s0 + s3, a1 = s1 + s2, b0 = s0 - s3, b1 = s1 - s2;
+  const V cA = splat<V>(kA), cB = splat<V>(kB), cC = splat<V>(kC), cD = splat<V>(kD);
+  v[0] = (a0 + a1) * splat<V>(0.125f);
+  v[4] = (a0 - a1) * splat<V>(0.125f);
+  v[2] = vfma(b1, splat<V>(kE3), b0 * splat<V>(kE1));
+  v[6] = vfma(b1, splat<V>(-kE1), b0 * splat<V>(kE3));
+  v[1] = vfma(d3, cD, vfma(d2, cC, vfma(d1, cB, d0 * cA)));
+  v[3] = vfma(d3, -cC, vfma(d2, -cA, vfma(d1, -cD, d0 * cB)));
+  v[5] = vfma(d3, cB, vfma(d2, cD, vfma(d1, -cA, d0 * cC)));
+  v[7] = vfma(d3, -cA, vfma(d2, cB, vfma(d1, -cC, d0 * cD)));
+}
+template <class V>
+__device__ __forceinline__ void dct4_1d(V* v) {
+  const V x0 = v[0], x1 = v[1], x2 = v[2], x3 = v[3];
+  const V s0 = x0 + x3, s1 = x1 + x2, d0 = x0 - x3, d1 = x1 - x2;
+  v[0] = (s0 + s1) * splat<V>(0.25f);
+  v[2] = (s0 - s1) * splat<V>(0.25f);
+  v[1] = vfma(d1, splat<V>(kF3), d0 * splat<V>(kF1));
+  v[3] = vfma(d1, splat<V>(-kF1), d0 * splat<V>(kF3));
 }
 
 // 8x8 transpose across the 8 lanes of a group (lane r: row r -> column r)
@@ -265,6 +280,26 @@ __device__ __forceinline__ void transpose8(float* v, int r) {
   transpose_stage<4>(v, r);
   transpose_stage<2>(v, r);
   transpose_stage<1>(v, r);
+}
+__device__ __forceinline__ void transpose8(f2* v, int r) {  // each channel on its own
+  float a[8], b[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    a[i] = v[i].x;
+    b[i] = v[i].y;
+  }
+  transpose8(a, r);
+  transpose8(b, r);
+#pragma unroll
+  for (int i = 0; i < 8; i++) v[i] = f2{a[i], b[i]};
+}
+template <int D>
+__device__ __forceinline__ f2 xor_lane(f2 v) {
+  return f2{xor_lane<D>(v.x), xor_lane<D>(v.y)};
+}
+template <int K>
+__device__ __forceinline__ f2 group_lane(f2 v) {
+  return f2{group_lane<K>(v.x), group_lane<K>(v.y)};
 }
 
 template <int T>
@@ -325,12 +360,25 @@ struct QVals {
 // two 4-point DCTs, then the 8x8 transpose, so lane r holds working-array
 // column r.  Shared by the two candidates with the same row transform
 // (DCT8 / DCT8X4: 8-point rows; DCT4X4 / DCT4X8: 4-point rows).
-template <bool ROW8, int C>
-__device__ __forceinline__ void row_pass_t(const GroupCtx& G, float* v) {
-  const float* plane = G.pix + C * kPlane;
+// C = kXB: X and B together (f2)
+constexpr int kXB = 3;
+template <int C, class V>
+__device__ __forceinline__ void load_row8(const GroupCtx& G, V* v) {
   const int base = lds_at(G.lx0, G.ly0 + G.r);  // 8 contiguous dwords (same skew)
+  if constexpr (C == kXB) {
+    const float* px = G.pix + base;
+    const float* pb = G.pix + 2 * kPlane + base;
 #pragma unroll
-  for (int x = 0; x < 8; x++) v[x] = plane[base + x];
+    for (int x = 0; x < 8; x++) v[x] = f2{px[x], pb[x]};
+  } else {
+    const float* plane = G.pix + C * kPlane + base;
+#pragma unroll
+    for (int x = 0; x < 8; x++) v[x] = plane[x];
+  }
+}
+template <bool ROW8, int C, class V>
+__device__ __forceinline__ void row_pass_t(const GroupCtx& G, V* v) {
+  load_row8<C>(G, v);
   if (ROW8) {
     dct8_1d(v);
   } else {
@@ -353,34 +401,35 @@ struct CandAcc {
 // Column transform of strategy T (lane r: working-array column r) from the
 // row-transformed, transposed values, with the lowest-frequency combine
 // (enc_transforms [ext]; slots per oracle)
-template <int T>
-__device__ __forceinline__ void col_transform(const GroupCtx& G, float* v) {
+template <int T, class V>
+__device__ __forceinline__ void col_transform(const GroupCtx& G, V* v) {
   if (T == kDCT8 || T == kDCT4X8) {
     dct8_1d(v);
   } else {
     dct4_1d(v);
     dct4_1d(v + 4);
   }
+  const V q = splat<V>(0.25f), h = splat<V>(0.5f);
   if (T == kDCT4X4) {
-    const float A0 = group_lane<0>(v[0]), Cc = group_lane<0>(v[4]);
-    const float B0 = group_lane<4>(v[0]), D = group_lane<4>(v[4]);
+    const V A0 = group_lane<0>(v[0]), Cc = group_lane<0>(v[4]);
+    const V B0 = group_lane<4>(v[0]), D = group_lane<4>(v[4]);
     if (G.r == 0) {
-      v[0] = (((A0 + B0) + Cc) + D) * 0.25f;
-      v[4] = (((A0 - B0) + Cc) - D) * 0.25f;
+      v[0] = (((A0 + B0) + Cc) + D) * q;
+      v[4] = (((A0 - B0) + Cc) - D) * q;
     } else if (G.r == 4) {
-      v[0] = (((A0 + B0) - Cc) - D) * 0.25f;
-      v[4] = (((A0 - B0) - Cc) + D) * 0.25f;
+      v[0] = (((A0 + B0) - Cc) - D) * q;
+      v[4] = (((A0 - B0) - Cc) + D) * q;
     }
   } else if (T == kDCT8X4) {
     if (G.r == 0) {
-      const float A0 = v[0], B0 = v[4];
-      v[0] = (A0 + B0) * 0.5f;
-      v[4] = (A0 - B0) * 0.5f;
+      const V A0 = v[0], B0 = v[4];
+      v[0] = (A0 + B0) * h;
+      v[4] = (A0 - B0) * h;
     }
   } else if (T == kDCT4X8) {
-    const float A0 = group_lane<0>(v[0]), B0 = group_lane<4>(v[0]);
-    if (G.r == 0) v[0] = (A0 + B0) * 0.5f;
-    if (G.r == 4) v[0] = (A0 - B0) * 0.5f;
+    const V A0 = group_lane<0>(v[0]), B0 = group_lane<4>(v[0]);
+    if (G.r == 0) v[0] = (A0 + B0) * h;
+    if (G.r == 4) v[0] = (A0 - B0) * h;
   }
 }
 
@@ -397,63 +446,60 @@ __device__ __forceinline__ void col_transform(const GroupCtx& G, float* v) {
 //             (0, 0) residual moved into the (1, 1) slot (from lane 4y), the
 //             sub-block means (row sums, quad tree) in the (0, 0) slots and
 //             combined over lanes 0 / 4 like DCT4X4's.
-template <int T, int C>
-__device__ __forceinline__ void haar_lane(const GroupCtx& G, float* v) {
-  const float* plane = G.pix + C * kPlane;
-  const int base = lds_at(G.lx0, G.ly0 + G.r);
-  float p[8];
-#pragma unroll
-  for (int x = 0; x < 8; x++) p[x] = plane[base + x];
+template <int T, int C, class V>
+__device__ __forceinline__ void haar_lane(const GroupCtx& G, V* v) {
+  V p[8];
+  load_row8<C>(G, p);
   if constexpr (T == kDCT2X2) {
     const bool top1 = (G.r & 1) == 0;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      const float a = p[2 * j] + p[2 * j + 1], b = p[2 * j] - p[2 * j + 1];
-      const float ap = xor_lane<1>(a), bp = xor_lane<1>(b);
+      const V a = p[2 * j] + p[2 * j + 1], b = p[2 * j] - p[2 * j + 1];
+      const V ap = xor_lane<1>(a), bp = xor_lane<1>(b);
       v[j] = top1 ? (a + ap) * 0.25f : (bp + b) * 0.25f;
       v[4 + j] = top1 ? (a - ap) * 0.25f : (bp - b) * 0.25f;
     }
     const bool top2 = (G.r & 2) == 0, even = (G.r & 1) == 0;
-    float n2[4];
+    V n2[4];
 #pragma unroll
     for (int x = 0; x < 2; x++) {
-      const float a = v[2 * x] + v[2 * x + 1], b = v[2 * x] - v[2 * x + 1];
-      const float ap = xor_lane<2>(a), bp = xor_lane<2>(b);
+      const V a = v[2 * x] + v[2 * x + 1], b = v[2 * x] - v[2 * x + 1];
+      const V ap = xor_lane<2>(a), bp = xor_lane<2>(b);
       n2[x] = top2 ? (a + ap) * 0.25f : (bp + b) * 0.25f;
       n2[2 + x] = top2 ? (a - ap) * 0.25f : (bp - b) * 0.25f;
     }
 #pragma unroll
     for (int k = 0; k < 4; k++) v[k] = even ? n2[k] : v[k];
     const bool top3 = (G.r & 4) == 0, l3 = (G.r & 3) == 0;
-    const float a = v[0] + v[1], b = v[0] - v[1];
-    const float ap = xor_lane<4>(a), bp = xor_lane<4>(b);
-    const float n30 = top3 ? (a + ap) * 0.25f : (bp + b) * 0.25f;
-    const float n31 = top3 ? (a - ap) * 0.25f : (bp - b) * 0.25f;
+    const V a = v[0] + v[1], b = v[0] - v[1];
+    const V ap = xor_lane<4>(a), bp = xor_lane<4>(b);
+    const V n30 = top3 ? (a + ap) * 0.25f : (bp + b) * 0.25f;
+    const V n31 = top3 ? (a - ap) * 0.25f : (bp - b) * 0.25f;
     v[0] = l3 ? n30 : v[0];
     v[1] = l3 ? n31 : v[1];
   } else {  // kIDENTITY
-    const float rs0 = ((p[0] + p[1]) + p[2]) + p[3], rs1 = ((p[4] + p[5]) + p[6]) + p[7];
-    float s0 = rs0 + xor_lane<1>(rs0), s1 = rs1 + xor_lane<1>(rs1);
+    const V rs0 = ((p[0] + p[1]) + p[2]) + p[3], rs1 = ((p[4] + p[5]) + p[6]) + p[7];
+    V s0 = rs0 + xor_lane<1>(rs0), s1 = rs1 + xor_lane<1>(rs1);
     s0 = s0 + xor_lane<2>(s0);
     s1 = s1 + xor_lane<2>(s1);
-    const float dc0 = s0 * (1.0f / 16.0f), dc1 = s1 * (1.0f / 16.0f);
+    const V dc0 = s0 * (1.0f / 16.0f), dc1 = s1 * (1.0f / 16.0f);
     const bool hi = (G.r & 4) != 0;
-    const float p11a = group_lane<1>(p[1]), p11b = group_lane<5>(p[1]);
-    const float p15a = group_lane<1>(p[5]), p15b = group_lane<5>(p[5]);
-    const float q0 = hi ? p11b : p11a, q1 = hi ? p15b : p15a;
+    const V p11a = group_lane<1>(p[1]), p11b = group_lane<5>(p[1]);
+    const V p15a = group_lane<1>(p[5]), p15b = group_lane<5>(p[5]);
+    const V q0 = hi ? p11b : p11a, q1 = hi ? p15b : p15a;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       v[k] = p[k] - q0;
       v[4 + k] = p[4 + k] - q1;
     }
-    const float t0 = xor_lane<1>(v[0]), t1 = xor_lane<1>(v[4]);
+    const V t0 = xor_lane<1>(v[0]), t1 = xor_lane<1>(v[4]);
     const int iy = G.r & 3;
     if (iy == 1) {
       v[1] = t0;
       v[5] = t1;
     }
-    const float o0 = xor_lane<4>(dc0), o1 = xor_lane<4>(dc1);
-    const float A = hi ? o0 : dc0, B = hi ? o1 : dc1, Cc = hi ? dc0 : o0, D = hi ? dc1 : o1;
+    const V o0 = xor_lane<4>(dc0), o1 = xor_lane<4>(dc1);
+    const V A = hi ? o0 : dc0, B = hi ? o1 : dc1, Cc = hi ? dc0 : o0, D = hi ? dc1 : o1;
     if (iy == 0) {
       v[0] = dc0;
       v[4] = dc1;
@@ -477,7 +523,6 @@ __device__ __forceinline__ void haar_lane(const GroupCtx& G, float* v) {
 // qa is kept as an integer-valued float qf (the truncation of a positive value
 // is its floor): the error needs no conversion, and the rate 2 + 2 bitlen(qa)
 // of a non-zero is 2 E - 250, E = the biased exponent of qf.
-typedef float f2 __attribute__((ext_vector_type(2)));
 template <int T, int C>
 __device__ __forceinline__ void quant_lane(const GroupCtx& G, float* v, float scale,
                                            float inv_scale, CandAcc& A) {
@@ -559,45 +604,103 @@ __device__ __forceinline__ void quant_lane(const GroupCtx& G, float* v, float sc
   A.q.nz = (C == 1 ? 0u : A.q.nz) | ((uint32_t)nzc << sh);
 }
 
-// one channel of one candidate: transform (row pass + transpose + column
-// transform, or the Haar steps) and quantization.  PRE: the DCT8 coefficients
-// of the channel were already computed (the chroma-from-luma fit, phase B0)
-template <int T, int C, bool PRE = false>
+// Quantization of lane r's 8 values of X and B together (f2 = (X, B) per
+// coefficient k), each channel with its own weights, chroma-from-luma factor
+// and distortion weights: every float op of the pair is one packed op.  The
+// e*e chain keeps the scalar order (X's k = 0..7, then B's).
+template <int T>
+__device__ __forceinline__ void quant_xb(const GroupCtx& G, f2* v, float scale, CandAcc& A) {
+  constexpr int ti = tindex<T>();
+  if (G.r == 0) v[0] = f2{0.0f, 0.0f};  // DC slots quantize to 0
+  const float* wxp = G.wperm + ((ti * 3 + 0) * 8 + G.r) * 8;
+  const float* wbp = G.wperm + ((ti * 3 + 2) * 8 + G.r) * 8;
+  const float* sxp = G.sdperm + ((ti * 3 + 0) * 8 + G.r) * 8;
+  const float* sbp = G.sdperm + ((ti * 3 + 2) * 8 + G.r) * 8;
+  const float4 wx0 = reinterpret_cast<const float4*>(wxp)[0], wx1 = reinterpret_cast<const float4*>(wxp)[1];
+  const float4 wb0 = reinterpret_cast<const float4*>(wbp)[0], wb1 = reinterpret_cast<const float4*>(wbp)[1];
+  const f2 wk[8] = {f2{wx0.x, wb0.x}, f2{wx0.y, wb0.y}, f2{wx0.z, wb0.z}, f2{wx0.w, wb0.w},
+                    f2{wx1.x, wb1.x}, f2{wx1.y, wb1.y}, f2{wx1.z, wb1.z}, f2{wx1.w, wb1.w}};
+  const f2 sc2 = f2{scale, scale}, kxb = f2{G.kx, G.kb};
+  int nzx = 0, nzb = 0;
+  uint32_t ebits = 0;
+  float eb[8];
+  uint32_t pkx[4], pkb[4];
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const f2 ws = wk[k] * sc2;
+    const f2 rv = v[k] - kxb * f2{A.yd[k], A.yd[k]};
+    const f2 vq = rv * ws;
+    const f2 a = f2{fabsf(vq.x), fabsf(vq.y)};
+    f2 qf;
+    qf.x = a.x < 0.58f ? 0.0f : floorf(fminf(a.x, 32767.0f) + 0.5f);
+    qf.y = a.y < 0.58f ? 0.0f : floorf(fminf(a.y, 32767.0f) + 0.5f);
+    const f2 e = (a - qf) * f2{sxp[k], sbp[k]};
+    A.part = fmaf(e.x, e.x, A.part);  // X's chain
+    eb[k] = e.y;
+    ebits += (__float_as_uint(qf.x) >> 23) + (__float_as_uint(qf.y) >> 23);
+    nzx += qf.x != 0.0f;
+    nzb += qf.y != 0.0f;
+    const int q0 = (int)qf.x, q1 = (int)qf.y;
+    const uint32_t sx = (uint32_t)(vq.x < 0.0f ? -q0 : q0) & 0xFFFFu;
+    const uint32_t sb = (uint32_t)(vq.y < 0.0f ? -q1 : q1) & 0xFFFFu;
+    if (k & 1) {
+      pkx[k >> 1] |= sx << 16;
+      pkb[k >> 1] |= sb << 16;
+    } else {
+      pkx[k >> 1] = sx;
+      pkb[k >> 1] = sb;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; k++) A.part = fmaf(eb[k], eb[k], A.part);  // then B's
+  A.bits += 2 * (int)ebits - 250 * (nzx + nzb);
+  const int nzcx = group_int_sum(nzx), nzcb = group_int_sum(nzb);
+  A.bits += G.r == 0 ? bitlen((uint32_t)nzcx) + bitlen((uint32_t)nzcb) : 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    A.q.w[i] = pkx[i];
+    A.q.w[8 + i] = pkb[i];
+  }
+  A.q.nz |= (uint32_t)nzcx | ((uint32_t)nzcb << 16);
+}
+
+// one channel of one candidate (C = kXB: X and B together): transform (row
+// pass + transpose + column transform, or the Haar steps) and quantization.
+// PRE: the row pass and its transpose were already done and are shared by
+// the two candidates with the same row transform (DCT8 / DCT8X4: 8-point rows,
+// from the chroma-from-luma fit of phase B0; DCT4X4 / DCT4X8: 4-point rows):
+// only the column transform is left.
+template <int T, int C, bool PRE = false, class V>
 __device__ __forceinline__ void eval_chan(const GroupCtx& G, float scale, float inv_scale,
-                                          CandAcc& A, const float* pre = nullptr) {
-  float v[8];
+                                          CandAcc& A, const V* pre = nullptr) {
+  V v[8];
   if constexpr (PRE) {
+    static_assert(T != kDCT2X2 && T != kIDENTITY, "DCT candidates only");
 #pragma unroll
     for (int k = 0; k < 8; k++) v[k] = pre[k];
+    col_transform<T>(G, v);
   } else if constexpr (T == kDCT2X2 || T == kIDENTITY) {
     haar_lane<T, C>(G, v);
   } else {
     row_pass_t<T == kDCT8 || T == kDCT8X4, C>(G, v);
     col_transform<T>(G, v);
   }
-  quant_lane<T, C>(G, v, scale, inv_scale, A);
+  if constexpr (C == kXB) quant_xb<T>(G, v, scale, A);
+  else quant_lane<T, C>(G, v, scale, inv_scale, A);
 }
 
-// One candidate, channels Y, X, B (its own row passes): only one candidate's
-// state is live at a time, which keeps the kernel inside 128 VGPRs.  PRE
-// (DCT8 only): pre[c] holds the channel's DCT8 coefficients.
+// One candidate: Y, then X and B together (f2); only one candidate's state is
+// live at a time, which keeps the kernel inside 128 VGPRs.  PRE (DCT8,
+// DCT8X4): the fit's transposed 8-point row passes, y[k] and xb[k] = (X, B).
 template <int T, bool PRE = false>
 __device__ __forceinline__ float eval_one(const GroupCtx& G, float scale, float inv_scale,
-                                          CandAcc& A, const float (*pre)[8] = nullptr) {
+                                          CandAcc& A, const float* pre_y = nullptr,
+                                          const f2* pre_xb = nullptr) {
   A.bits = 0;
   A.part = 0.0f;
-  if constexpr (PRE) {  // registers, no channel loop (pre[c] indexed statically)
-    eval_chan<T, 1, true>(G, scale, inv_scale, A, pre[1]);
-    eval_chan<T, 0, true>(G, scale, inv_scale, A, pre[0]);
-    eval_chan<T, 2, true>(G, scale, inv_scale, A, pre[2]);
-  } else {
-#pragma unroll 1  // one channel live at a time
-    for (int ci = 0; ci < 3; ci++) {
-      if (ci == 0) eval_chan<T, 1>(G, scale, inv_scale, A);
-      else if (ci == 1) eval_chan<T, 0>(G, scale, inv_scale, A);
-      else eval_chan<T, 2>(G, scale, inv_scale, A);
-    }
-  }
+  A.q.nz = 0;
+  eval_chan<T, 1, PRE, float>(G, scale, inv_scale, A, pre_y);
+  eval_chan<T, kXB, PRE, f2>(G, scale, inv_scale, A, pre_xb);
   // estimate multipliers (== oracle jxo_quantize_block tmul, JXO_TMUL_*)
   constexpr float tm = T == kDCT8 ? 1.0f
                                   : (T == kDCT4X4 ? 1.05f
@@ -797,23 +900,32 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
   // accumulates its coefficient column, the block's 8 lanes tree-sum, the
   // tile sums its blocks in raster order (phase-A scratch sH reused)
   float kx = 0.0f, kb = 1.0f;
-  // the fit's DCT8 coefficients [X, Y, B] (lane r: column r) are the DCT8
-  // candidate's transform too: kept for phase C instead of recomputed
-  float cf[3][8];
+  // the fit's 8-point row passes (transposed: lane r = working column r) of
+  // Y and (X, B) are those of the DCT8 and DCT8X4 candidates too: kept for
+  // phase C, which only adds their column transforms
+  float rty[8];  // Y
+  f2 rtxb[8];    // (X, B)
   if (a.effort >= 5) {
     float* cs = &sH[0][0];  // [4 sums][64 blocks]
     {
       const GroupCtx G0{sPix, lby * 8 + 1, lbx * 8 + 1, r, sWperm, sIwperm, sBtab, sSdperm,
                         0.0f, 1.0f};
-      float* vy = cf[1];
-      float* vx = cf[0];
-      float* vb = cf[2];
-      row_pass_t<true, 1>(G0, vy);
+      row_pass_t<true, 1>(G0, rty);
+      row_pass_t<true, kXB>(G0, rtxb);
+      float vy[8], vx[8], vb[8];
+      f2 cxb[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        vy[k] = rty[k];
+        cxb[k] = rtxb[k];
+      }
       dct8_1d(vy);
-      row_pass_t<true, 0>(G0, vx);
-      dct8_1d(vx);
-      row_pass_t<true, 2>(G0, vb);
-      dct8_1d(vb);
+      dct8_1d(cxb);
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        vx[k] = cxb[k].x;
+        vb[k] = cxb[k].y;
+      }
       const float* wx = sWperm + (0 * 8 + r) * 8;  // DCT8 weights, X: [r][k]
       const float* wbp = sWperm + (2 * 8 + r) * 8; // DCT8 weights, B
       float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
@@ -923,14 +1035,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
   // effort 5 (all-DCT8 speed tiers [ext]): no override there either
   if (HOOKP && (a.proposals & 1u) && ncand > 1) pt = partition_of(rh, rv, rd, a.distance);
   // scan indices: DCT8 0, DCT4X4 1, DCT2X2 2, DCT4X8 3, DCT8X4 4, IDENTITY 5
-  QVals best, ptq;
+  QVals best;
   int bt = kDCT8, bi = 0;
   float beste = FLT_MAX;
   // candidates one at a time; `beats` is a strict total order on (estimate,
   // scan index), so this finds the scan's winner
   {
     CandAcc A;
-    float e = ncand > 1 ? eval_one<kDCT8, true>(G, scale, inv_scale, A, cf)
+    float e = ncand > 1 ? eval_one<kDCT8, true>(G, scale, inv_scale, A, rty, rtxb)
                         : eval_one<kDCT8>(G, scale, inv_scale, A);
     if (hookF) e = hook_f(e, rh, rv, rd);
     copy_q(best, A.q, true);
@@ -940,7 +1052,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
     constexpr int T = decltype(tag)::value;
     if (!(ncand > 1 || pt == T)) return;
     CandAcc A;
-    float e = eval_one<T>(G, scale, inv_scale, A);
+    float e;
+    if constexpr (T == kDCT8X4) {  // (ncand > 1 here: the fit ran)
+      e = eval_one<T, true>(G, scale, inv_scale, A, rty, rtxb);
+    } else {
+      e = eval_one<T>(G, scale, inv_scale, A);
+    }
     if (ncand > 1) {
       if (hookF) e = hook_f(e, rh, rv, rd);
       if (beats(e, idx, beste, bi)) {
@@ -950,9 +1067,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
         beste = e;
       }
     }
-    if (HOOKP) copy_q(ptq, A.q, pt == T);
   };
   cand(std::integral_constant<int, kDCT8X4>(), 4);
+  // (DCT4X4 / DCT4X8 could share their 4-point row passes the same way, but
+  // holding them through DCT4X4's evaluation spills: 115+ VGPRs at 128)
   cand(std::integral_constant<int, kDCT4X4>(), 1);
   cand(std::integral_constant<int, kDCT4X8>(), 3);
   if (ncand > 1) {
@@ -960,8 +1078,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
     cand(std::integral_constant<int, kIDENTITY>(), 5);
   }
   if (HOOKP && bt == kDCT8 && pt != kDCT8) {
+    // hook P's override: its candidate is evaluated again (keeping it aside
+    // through the search would hold 13 more VGPRs); same inputs, same values
+    CandAcc A;
+    if (pt == kDCT4X4) (void)eval_one<kDCT4X4>(G, scale, inv_scale, A);
+    else if (pt == kDCT8X4) (void)eval_one<kDCT8X4>(G, scale, inv_scale, A);
+    else (void)eval_one<kDCT4X8>(G, scale, inv_scale, A);
     bt = pt;
-    copy_q(best, ptq, true);
+    copy_q(best, A.q, true);
   }
   gb = gblock();
   if (r == 0) {

@@ -440,13 +440,17 @@ def _gloo_stream_rank(rank, world, port, result, nframes):
         with jxg.Encoder(flags=jxg.FLAG_ANS) as enc:
             ss = ShardStream(enc, w, h, rank, world)
             got = []
+
+            def take():  # a view is valid for the next slots - 1 receives: copy now
+                g = ss.receive()
+                got.append(None if g is None else g.tobytes())
+
             for t in ts:
                 ss.submit(t.data_ptr())
                 while ss.pending() > ss.depth:
-                    got.append(ss.receive())
+                    take()
             while ss.pending():
-                got.append(ss.receive())
-            got = [None if g is None else g.tobytes() for g in got]
+                take()
             ss.close()
         if rank == 0:
             result.put((res, got))
@@ -480,11 +484,16 @@ def test_multiprocess_streamed_frames(jxg_mod, decoder):
     for p in procs:
         p.join(300)
         assert p.exitcode == 0
+    import hashlib
+
+    def digests(xs):  # (a failing comparison of 12 MB byte lists takes pytest minutes to diff)
+        return [hashlib.sha256(bytes(x)).hexdigest()[:16] for x in xs]
+
     dev, hst, ref = res[False]
-    assert [bytes(x) for x in dev] == ref and [bytes(x) for x in hst] == ref
+    assert digests(dev) == digests(ref) and digests(hst) == digests(ref)
     dev, hst, ref = res[True]
-    assert [bytes(x) for x in dev] == [bytes(x) for x in hst]
-    assert got == [bytes(x) for x in dev]
+    assert digests(dev) == digests(hst)
+    assert digests(got) == digests(dev)
     dr, dg = decoder.decode(ref[3]), decoder.decode(got[3])
     assert dg.npresets == 2
     _same_image(dr, dg)
