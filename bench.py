@@ -23,11 +23,14 @@ N > 1 (launched by torch.distributed.run, backend nccl = RCCL):
           per-block records move; one HF preset per rank: no histogram
           collective), streamed through jxg.dist.ShardStream -- each rank keeps
           up to jxg_pipeline_depth frames' shards in flight in the library's
-          lanes, swaps the frame's payload heads with the other ranks through
-          a node-shared /dev/shm region and DMAs its sections into the frame's
+          lanes; a native completion thread per rank (jxg_shard_stream_*)
+          swaps the frame's payload heads with the other ranks through a
+          node-shared /dev/shm region and DMAs its sections into the frame's
           codestream there (rank 0 adds headers + TOC).  value = frames x
           7680 x 4320 / time over all ranks.  --scaling weak: one frame of N
           stacked 8K frames per step instead.
+  shard-py -- the same stream with the per-frame protocol in Python
+          (jxg.dist.HostShardStream over jxg_shard_next_head / write_next).
   shard-sync -- the same split one frame at a time (jxg.dist.encode_sharded:
           record exchange + histogram all-reduce when the plan / coder needs
           them, --assembly host|device).
@@ -210,7 +213,8 @@ def main():
     ap.add_argument("--distance", type=float, default=1.0)
     ap.add_argument("--effort", type=int, default=7)
     ap.add_argument("--proposals", type=int, default=0)
-    ap.add_argument("--mode", choices=("shard", "shard-sync", "replica"), default="shard",
+    ap.add_argument("--mode", choices=("shard", "shard-py", "shard-sync", "replica"),
+                    default="shard",
                     help="N > 1: shard = every frame's pass groups split over the ranks, "
                          "streamed (ShardStream; BASELINE config 2 as written); shard-sync = the "
                          "same one frame at a time (encode_sharded); replica = every rank "
@@ -262,7 +266,7 @@ def main():
         else:
             dist.init_process_group(backend)
     name, w, h, nframes = CONFIGS[args.config]
-    sharded_mode = world > 1 and args.mode in ("shard", "shard-sync")
+    sharded_mode = world > 1 and args.mode in ("shard", "shard-py", "shard-sync")
     strong = sharded_mode and args.scaling == "strong"
     fh = h if strong or not sharded_mode else h * world
     # inputs generated on the device (jxg_synth_rgb8_device: the bytes of
@@ -313,9 +317,9 @@ def main():
         ss = None
         host = None
         bufs = {}
-        if mode == "shard":
-            from jxg.dist import ShardStream
-            ss = ShardStream(encs[0], w, fh, rank, world)
+        if mode in ("shard", "shard-py"):
+            from jxg.dist import HostShardStream, ShardStream
+            ss = (ShardStream if mode == "shard" else HostShardStream)(encs[0], w, fh, rank, world)
         elif mode == "shard-sync" and args.assembly == "host":
             from jxg.dist import SharedHostBuffer
             if SharedHostBuffer.single_node():
@@ -326,13 +330,13 @@ def main():
             # the codestream ends in (pinned / shared) host memory; ctypes
             # calls release the GIL, so several encoders' host work overlaps
             if ss is not None:
-                # (a received view stays valid for the next slots - 1
-                # receives: took() keeps only its size, and the first frame's
-                # bytes are copied when it is the last one kept)
+                # (a received view stays valid until the next receive: took()
+                # keeps only its size, and copies the bytes of the frames it
+                # keeps); frames are taken as soon as they are complete
                 got = 0
                 for k in ks:
                     ss.submit(d_imgs[k % nd].data_ptr())
-                    while ss.pending() > ss.depth:
+                    while ss.pending() >= ss.max_pending or (ss.pending() and ss.ready()):
                         took(e, got, ss.receive())
                         got += 1
                 while ss.pending():
@@ -400,6 +404,7 @@ def main():
         rec["last"] = last.tobytes() if hasattr(last, "tobytes") else last
         if ss is not None:
             ss.close()
+            rec["ms_wait_ranks"] = getattr(ss, "ms_wait_ranks", None)
         for e in encs[1:]:
             e.close()
         rec["enc"] = encs[0]
@@ -444,7 +449,8 @@ def main():
                         "bytes_per_frame": P["sizes"][-1]}
         P["enc"].close()
     iso = None
-    if mode == "frames" and pipeline or mode == "shard":
+    streamed = mode in ("shard", "shard-py")
+    if mode == "frames" and pipeline or streamed:
         # the kernels alone on the GPU (one-at-a-time encodes of this rank's
         # frame, same coder): the front kernel's roofline, the rANS chain
         # kernel's duration
@@ -483,8 +489,10 @@ def main():
                         "partition kind %d), %s"
                         % (name, w, fh, distinct, args.distance, args.effort, args.proposals,
                            coder_desc, world, args.scaling, jxg.shard_plan(w, fh, world)[2],
-                           "streamed (jxg.dist.ShardStream, %d frames in flight per rank, heads "
-                           "and sections through /dev/shm)" % R["depth"] if mode == "shard" else
+                           "streamed (jxg.dist.%s, %d frames in flight per rank, heads "
+                           "and sections through /dev/shm)"
+                           % ("ShardStream" if mode == "shard" else "HostShardStream", R["depth"])
+                           if streamed else
                            "one frame at a time (encode_sharded), %s assembly" % args.assembly))
             par = "group-shard%d" % world
         else:
@@ -515,7 +523,7 @@ def main():
                        "global_batch": per_step * (1 if mode != "frames" else world),
                        "parallelism": par},
             "streams_per_gpu": nstreams,
-            "pipeline": pipeline or mode == "shard",
+            "pipeline": pipeline or streamed,
             "ms_latency": round(sum(x[0] for x in host_ms) / len(host_ms), 3),
             "bytes_per_frame": nbytes,
             "bpp": round(nbytes * 8.0 / (w * fh), 4) if mode == "frames" or rank == 0 else None,
@@ -568,6 +576,10 @@ def main():
             res["thesis_proposals"] = thesis
         if replicas is not None:
             res["replicas"] = replicas
+        if R.get("ms_wait_ranks") is not None:
+            # rank 0's completion thread: time spent waiting for the other
+            # ranks' heads over warmup + timed frames (their critical path)
+            res["ms_wait_ranks_rank0"] = round(R["ms_wait_ranks"], 2)
         if world == 1 and not args.no_quality:
             res["quality"] = quality_probe(R["enc"], img, args.distance, args.effort)
         if world == 1 and not args.no_cpu_baseline:

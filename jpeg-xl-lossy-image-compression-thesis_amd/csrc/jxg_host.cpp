@@ -15,9 +15,11 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <future>
 #include <memory>
 #include <mutex>
@@ -530,6 +532,7 @@ struct Ctx {
   bool owned_lane = false;  // a pipeline / batch lane of another context
   std::unique_ptr<struct Job> job;  // sharded encode in flight (begin -> end)
   std::unique_ptr<struct Pipe> pipe;  // streaming encode (jxg_submit_* / jxg_receive)
+  std::unique_ptr<struct SStream> ss; // streaming shards over a shared region (jxg_shard_stream_*)
   std::vector<uint32_t> payload_head;  // last jxg_shard_end: payload head words
   size_t payload_body = 0;             //   and body bytes (in `out`)
 };
@@ -1805,6 +1808,9 @@ struct PipeFrame {
   bool shard = false;
   Clock::time_point t0;
   std::future<jxg_status> codes;  // valid while a helper builds the codes
+  // jxg_shard_stream: the codes (a helper's, or the completion thread's own)
+  // waited on by the completion thread and by the submitting thread's lag join
+  std::shared_future<jxg_status> sf;
 };
 // the helper's codes of a frame -> phase 2 (on an error the caller aborts)
 static jxg_status pipe_join_codes(PipeFrame& fr) {
@@ -1831,8 +1837,8 @@ struct Pipe {
   uint32_t depth = 0;
 };
 static bool pipe_busy(const Ctx* c) {
-  return c->pipe && (!c->pipe->inflight.empty() || !c->pipe->done.empty() ||
-                     !c->pipe->ready.empty());
+  return c->ss || (c->pipe && (!c->pipe->inflight.empty() || !c->pipe->done.empty() ||
+                               !c->pipe->ready.empty()));
 }
 
 static jxg_status ensure_lanes(Ctx* c, uint32_t extra) {
@@ -1852,7 +1858,10 @@ static jxg_status ensure_lanes(Ctx* c, uint32_t extra) {
 // lanes' streams
 static void pipe_abort(Ctx* c) {
   Pipe& p = *c->pipe;
-  for (auto& fr : p.inflight) (void)pipe_join_codes(*fr);
+  for (auto& fr : p.inflight) {
+    (void)pipe_join_codes(*fr);
+    if (fr->sf.valid()) fr->sf.wait();
+  }
   for (auto& fr : p.inflight) (void)hipStreamSynchronize(fr->lane->stream);
   for (auto& fr : p.ready) (void)hipStreamSynchronize(fr->lane->stream);
   p.inflight.clear();
@@ -1906,6 +1915,21 @@ static jxg_status shard_finish(Ctx* c, Job& J, size_t* payload_bytes) {
 // oldest frame in flight -> done (a whole frame: assembled, codestream on
 // the host) or ready (a shard: sections emitted, payload head built); on an
 // error the caller aborts the pipe
+// a shard frame's stats (its lane's) once its sections are emitted
+static void shard_frame_stats(PipeFrame& fr, size_t bytes) {
+  jxg_stats& S = fr.lane->stats;
+  S = jxg_stats{};
+  S.xsize = fr.J.w;
+  S.ysize = fr.J.h;
+  S.num_groups = fr.J.f.ngroups;
+  S.num_lf_groups = fr.J.f.nlf;
+  S.bytes = bytes;
+  S.ms_front_kernel = elapsed(fr.lane->ev[0], fr.lane->ev[5]);
+  S.ms_front = elapsed(fr.lane->ev[0], fr.lane->ev[1]);
+  S.ms_host_codes = fr.J.ms_codes;
+  S.ms_host_call = ms_since(fr.t0);
+}
+
 static jxg_status pipe_complete_oldest(Ctx* c) {
   Pipe& p = *c->pipe;
   PipeFrame& fr = *p.inflight.front();
@@ -1915,17 +1939,7 @@ static jxg_status pipe_complete_oldest(Ctx* c) {
     size_t bytes = 0;
     if (!st) st = shard_finish(fr.lane, fr.J, &bytes);
     if (st) return st;
-    jxg_stats& S = fr.lane->stats;
-    S = jxg_stats{};
-    S.xsize = fr.J.w;
-    S.ysize = fr.J.h;
-    S.num_groups = fr.J.f.ngroups;
-    S.num_lf_groups = fr.J.f.nlf;
-    S.bytes = bytes;
-    S.ms_front_kernel = elapsed(fr.lane->ev[0], fr.lane->ev[5]);
-    S.ms_front = elapsed(fr.lane->ev[0], fr.lane->ev[1]);
-    S.ms_host_codes = fr.J.ms_codes;
-    S.ms_host_call = ms_since(fr.t0);
+    shard_frame_stats(fr, bytes);
     p.ready.push_back(std::move(p.inflight.front()));
     p.inflight.erase(p.inflight.begin());
     return JXG_OK;
@@ -1954,6 +1968,7 @@ static jxg_status pipe_submit(Ctx* c, const uint8_t* src, bool on_device, uint32
   if (!c->pipe) return JXG_ERR_OOM;
   Pipe& p = *c->pipe;
   const int mode = shard ? 2 : 1;
+  if (c->ss) return JXG_ERR_INVALID_ARG;  // a jxg_shard_stream owns the lanes
   if (pipe_busy(c) && p.mode != mode) return JXG_ERR_INVALID_ARG;  // one kind at a time
   const Frame f0 = make_frame(w, h, c->params.distance);
   uint32_t ngroups = f0.ngroups;
@@ -2060,7 +2075,7 @@ static jxg_status pipe_submit(Ctx* c, const uint8_t* src, bool on_device, uint32
 }
 
 static jxg_status pipe_receive(Ctx* c, jxg_buffer* out) {
-  if (!c->pipe || c->pipe->mode != 1) return JXG_ERR_INVALID_ARG;
+  if (c->ss || !c->pipe || c->pipe->mode != 1) return JXG_ERR_INVALID_ARG;
   Pipe& p = *c->pipe;
   if (p.done.empty()) {
     if (p.inflight.empty()) return JXG_ERR_INVALID_ARG;
@@ -2078,7 +2093,7 @@ static jxg_status pipe_receive(Ctx* c, jxg_buffer* out) {
 
 // streaming shards: the oldest pending shard frame, completed if needed
 static jxg_status pipe_shard_oldest(Ctx* c, PipeFrame** fr) {
-  if (!c->pipe || c->pipe->mode != 2) return JXG_ERR_INVALID_ARG;
+  if (c->ss || !c->pipe || c->pipe->mode != 2) return JXG_ERR_INVALID_ARG;
   Pipe& p = *c->pipe;
   if (p.ready.empty()) {
     if (p.inflight.empty()) return JXG_ERR_INVALID_ARG;
@@ -2505,6 +2520,349 @@ static jxg_status shard_assemble(const uint8_t* const* payloads, const size_t* s
   return JXG_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Streaming shards over a node-shared host region (jxg_shard_stream_*): the
+// multi-GPU pipeline with its per-frame host work off the caller's thread.
+// The caller's thread only submits (launches a frame's shard on a free lane,
+// starts the previous frame's codes on a helper thread); one completion thread
+// per context takes the frames in order: waits for the shard's sections
+// (codes joined, emission done, sections concatenated, payload head built),
+// publishes the head in the region, waits for every rank's head of that
+// frame, DMAs its sections into the frame's codestream slot (rank 0 adds
+// headers + TOC) and marks the frame done.  Ranks synchronise through the
+// region only (64-bit sequence words, lock-free atomics across processes).
+// Region: [header 4 KB][pub: slots x world int64][done: slots x world int64]
+//         [heads: slots x world x hcap u32][pad to 4 KB][data: slots x slot_bytes]
+// ---------------------------------------------------------------------------
+constexpr uint64_t kShmMagic = 0x6a78675348534d31ull;  // "jxgSHSM1"
+struct ShmHeader {
+  uint64_t magic, w, h, world, slots, slot_bytes, hcap, data_off, total;
+  int64_t consumed;  // frames rank 0's caller has received
+};
+static size_t shm_hcap(const Frame& f) {
+  return 7 + 2 * (2 + (size_t)f.nlf + f.ngroups) + 2 + (kAcCtx + 3) / 4 + (size_t)kAnsMaxHists * kAlpha;
+}
+struct ShmLayout {
+  size_t pub, done, heads, data, total;
+};
+static ShmLayout shm_layout(const Frame& f, uint32_t world, uint32_t slots, size_t slot_bytes) {
+  ShmLayout L;
+  L.pub = 4096;
+  L.done = L.pub + 8 * (size_t)slots * world;
+  L.heads = L.done + 8 * (size_t)slots * world;
+  L.data = (L.heads + 4 * (size_t)slots * world * shm_hcap(f) + 4095) & ~(size_t)4095;
+  L.total = L.data + (size_t)slots * slot_bytes;
+  return L;
+}
+static int64_t shm_load(const int64_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+static void shm_store(int64_t* p, int64_t v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
+
+struct SStream {
+  uint8_t* base = nullptr;
+  ShmHeader* hd = nullptr;
+  int64_t* pub = nullptr;   // [slots][world]: frame whose head rank r published in slot s
+  int64_t* done = nullptr;  // [slots][world]: frame whose sections rank r wrote in slot s
+  uint32_t* heads = nullptr;
+  uint32_t w = 0, h = 0, rank = 0, world = 1, slots = 0, depth = 0, lag = 1;
+  size_t stride = 0, slot_bytes = 0, hcap = 0, data_off = 0;
+  std::thread worker;
+  std::mutex mu;
+  std::condition_variable cv;
+  uint64_t submitted = 0, completed = 0, received = 0;
+  std::deque<size_t> totals;  // codestream bytes of completed, unreceived frames
+  jxg_status err = JXG_OK;
+  std::atomic<bool> stop{false};
+  float ms_wait_ranks = 0.0f;  // completion thread: time spent waiting for other ranks
+};
+
+// spin (then sleep) until pred(), at most 120 s
+template <class Pred>
+static bool shm_wait(Pred pred, SStream* S) {
+  const Clock::time_point t0 = Clock::now();
+  for (int spin = 0; !pred(); spin++) {
+    if (spin > 256) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    if (S && S->stop) return false;
+    if (ms_since(t0) > 120000.0f) return false;
+  }
+  return true;
+}
+
+static void sstream_fail(SStream& S, jxg_status st) {
+  std::lock_guard<std::mutex> lk(S.mu);
+  if (!S.err) S.err = st;
+  S.cv.notify_all();
+}
+
+// the completion thread: frames in submission order
+static void sstream_worker(Ctx* c) {
+  SStream& S = *c->ss;
+  Pipe& p = *c->pipe;
+  if (hipSetDevice(c->params.device) != hipSuccess) return sstream_fail(S, JXG_ERR_HIP);
+  for (uint64_t k = 0;; k++) {
+    PipeFrame* fr = nullptr;
+    std::shared_future<jxg_status> codes;
+    std::promise<jxg_status> own;
+    bool mine = false;
+    {
+      std::unique_lock<std::mutex> lk(S.mu);
+      S.cv.wait(lk, [&] { return S.stop || S.err || !p.inflight.empty(); });
+      if (S.err || p.inflight.empty()) return;  // stopped and drained (or failed)
+      fr = p.inflight.front().get();
+      mine = !fr->sf.valid();
+      if (mine) fr->sf = own.get_future().share();  // no helper will start for it now
+      codes = fr->sf;
+    }
+    if (mine) own.set_value(enc_codes(fr->lane, fr->J, false));
+    jxg_status st = codes.get();
+    fr->phase = 2;
+    size_t bytes = 0;
+    if (!st) st = shard_finish(fr->lane, fr->J, &bytes);
+    if (st) return sstream_fail(S, st);
+    shard_frame_stats(*fr, bytes);
+    const std::vector<uint32_t>& hw = fr->lane->payload_head;
+    if (hw.size() > S.hcap) return sstream_fail(S, JXG_ERR_INTERNAL);
+    const uint32_t s = (uint32_t)(k % S.slots), r = S.rank, W = S.world;
+    const Clock::time_point tw = Clock::now();
+    // slot s held frame k - slots: every rank wrote it and rank 0's caller has
+    // moved past its view (views stay valid until the next receive)
+    const int64_t prev = (int64_t)k - (int64_t)S.slots;
+    if (!shm_wait([&] {
+          for (uint32_t q = 0; q < W; q++)
+            if (shm_load(&S.done[s * W + q]) < prev) return false;
+          return shm_load(&S.hd->consumed) >= prev + 2;
+        }, &S))
+      return sstream_fail(S, JXG_ERR_INTERNAL);
+    std::memcpy(S.heads + ((size_t)s * W + r) * S.hcap, hw.data(), hw.size() * 4);
+    shm_store(&S.pub[s * W + r], (int64_t)k);
+    if (!shm_wait([&] {
+          for (uint32_t q = 0; q < W; q++)
+            if (shm_load(&S.pub[s * W + q]) < (int64_t)k) return false;
+          return true;
+        }, &S))
+      return sstream_fail(S, JXG_ERR_INTERNAL);
+    S.ms_wait_ranks += ms_since(tw);
+    std::vector<const uint32_t*> hp(W);
+    std::vector<size_t> hwords(W);
+    for (uint32_t q = 0; q < W; q++) {
+      hp[q] = S.heads + ((size_t)s * W + q) * S.hcap;
+      hwords[q] = head_words(hp[q], S.hcap);
+      if (!hwords[q]) return sstream_fail(S, JXG_ERR_INTERNAL);
+    }
+    size_t total = 0;
+    st = shard_write_host(fr->lane, hp.data(), hwords.data(), W, S.base + S.data_off +
+                          (size_t)s * S.slot_bytes, S.slot_bytes, &total);
+    if (st) return sstream_fail(S, st == JXG_ERR_INVALID_ARG && total > S.slot_bytes
+                                        ? JXG_ERR_OOM : st);
+    shm_store(&S.done[s * W + r], (int64_t)k);
+    {
+      std::lock_guard<std::mutex> lk(S.mu);
+      c->stats = fr->lane->stats;
+      p.inflight.erase(p.inflight.begin());  // its lane is free again
+      S.totals.push_back(total);
+      S.completed++;
+      S.cv.notify_all();
+    }
+  }
+}
+
+static jxg_status sstream_begin(Ctx* c, void* base, size_t size, uint32_t w, uint32_t h,
+                                size_t stride, uint32_t rank, uint32_t world, uint32_t slots,
+                                size_t slot_bytes, int init) {
+  if (c->ss || pipe_busy(c)) return JXG_ERR_INVALID_ARG;
+  if (!base || ((uintptr_t)base & 4095) || world < 1 || rank >= world || slots < 3)
+    return JXG_ERR_INVALID_ARG;
+  const Frame f = make_frame(w, h, c->params.distance);
+  if (f.ngroups < world || (world > 1 && f.ngroups < 2)) return JXG_ERR_INVALID_ARG;
+  const Plan P = make_plan(f, rank, world);
+  if (!P.x.send.empty() || !P.x.recv.empty() || (world > 1 && !(c->params.flags & JXG_FLAG_ANS)))
+    return JXG_ERR_UNSUPPORTED;
+  slot_bytes = (slot_bytes + 4095) & ~(size_t)4095;
+  const ShmLayout L = shm_layout(f, world, slots, slot_bytes);
+  if (size < L.total) return JXG_ERR_INVALID_ARG;
+  ShmHeader* hd = static_cast<ShmHeader*>(base);
+  uint8_t* b = static_cast<uint8_t*>(base);
+  if (init) {
+    std::memset(b, 0, L.data);
+    hd->w = w;
+    hd->h = h;
+    hd->world = world;
+    hd->slots = slots;
+    hd->slot_bytes = slot_bytes;
+    hd->hcap = shm_hcap(f);
+    hd->data_off = L.data;
+    hd->total = L.total;
+    int64_t* pub = reinterpret_cast<int64_t*>(b + L.pub);
+    int64_t* done = reinterpret_cast<int64_t*>(b + L.done);
+    for (size_t i = 0; i < (size_t)slots * world; i++) pub[i] = done[i] = -1;
+    shm_store(&hd->consumed, 0);
+    __atomic_store_n(&hd->magic, kShmMagic, __ATOMIC_RELEASE);
+  } else if (__atomic_load_n(&hd->magic, __ATOMIC_ACQUIRE) != kShmMagic || hd->w != w ||
+             hd->h != h || hd->world != world || hd->slots != slots ||
+             hd->slot_bytes != slot_bytes || hd->total != L.total) {
+    return JXG_ERR_INVALID_ARG;  // not initialised by rank 0 with the same geometry
+  }
+  if (!c->pipe) c->pipe.reset(new (std::nothrow) Pipe());
+  if (!c->pipe) return JXG_ERR_OOM;
+  std::unique_ptr<SStream> S(new (std::nothrow) SStream());
+  if (!S) return JXG_ERR_OOM;
+  S->base = b;
+  S->hd = hd;
+  S->pub = reinterpret_cast<int64_t*>(b + L.pub);
+  S->done = reinterpret_cast<int64_t*>(b + L.done);
+  S->heads = reinterpret_cast<uint32_t*>(b + L.heads);
+  S->w = w;
+  S->h = h;
+  S->stride = stride;
+  S->rank = rank;
+  S->world = world;
+  S->slots = slots;
+  S->slot_bytes = slot_bytes;
+  S->hcap = shm_hcap(f);
+  S->data_off = L.data;
+  S->depth = pipe_depth(P.ng());
+  S->lag = pipe_lag(P.ng(), S->depth);
+  jxg_status st = ensure_lanes(c, S->depth - 1);
+  if (st) return st;
+  c->pipe->mode = 2;
+  c->pipe->depth = S->depth;
+  c->ss = std::move(S);
+  try {
+    c->ss->worker = std::thread(sstream_worker, c);
+  } catch (...) {
+    c->ss.reset();
+    return JXG_ERR_INTERNAL;
+  }
+  return JXG_OK;
+}
+
+static jxg_status sstream_submit(Ctx* c, const uint8_t* d_rgb) {
+  SStream& S = *c->ss;
+  Pipe& p = *c->pipe;
+  Ctx* L = nullptr;
+  std::unique_ptr<PipeFrame> fr(new (std::nothrow) PipeFrame());
+  if (!fr) return JXG_ERR_OOM;
+  {
+    std::unique_lock<std::mutex> lk(S.mu);
+    // (a frame completes only after rank 0's caller receives the one S - 2
+    // frames before it: a caller that never receives times out here)
+    if (!S.cv.wait_for(lk, std::chrono::seconds(120),
+                       [&] { return S.err || p.inflight.size() < S.depth; }))
+      return JXG_ERR_INTERNAL;
+    if (S.err) return S.err;
+    // the newest frame's codes on a helper thread (unless the completion
+    // thread already took them on)
+    if (!p.inflight.empty()) {
+      PipeFrame* prev = p.inflight.back().get();
+      if (!prev->sf.valid()) {
+        const int dev = c->params.device;
+        try {
+          prev->sf = std::async(std::launch::async, [prev, dev]() {
+                       if (hipSetDevice(dev) != hipSuccess) return JXG_ERR_HIP;
+                       return enc_codes(prev->lane, prev->J, false);
+                     }).share();
+        } catch (...) {  // no thread: the completion thread builds them
+        }
+      }
+    }
+    for (uint32_t li = 0; li < S.depth && !L; li++) {
+      Ctx* cand = li == 0 ? c : c->lanes[li - 1].get();
+      bool used = false;
+      for (auto& q : p.inflight) used = used || q->lane == cand;
+      if (!used) L = cand;
+    }
+  }
+  if (!L) return JXG_ERR_INTERNAL;
+  fr->lane = L;
+  fr->t0 = Clock::now();
+  fr->shard = true;
+  jxg_status st = order_input(c, L);
+  if (!st) st = enc_launch(L, fr->J, d_rgb, S.w, S.h, S.stride, S.rank, S.world);
+  if (st) {
+    (void)hipStreamSynchronize(L->stream);
+    sstream_fail(S, st);
+    return st;
+  }
+  std::shared_future<jxg_status> lagged;
+  {
+    std::lock_guard<std::mutex> lk(S.mu);
+    p.inflight.push_back(std::move(fr));
+    S.submitted++;
+    S.cv.notify_all();
+    // frame j - lag: codes built, emission launched before this thread
+    // launches frame j + 1 (the pacing of pipe_submit: a chain is queued
+    // before the transform kernels of the frames behind it)
+    if (p.inflight.size() > S.lag) lagged = p.inflight[p.inflight.size() - 1 - S.lag]->sf;
+  }
+  if (lagged.valid() && (st = lagged.get())) {
+    sstream_fail(S, st);
+    return st;
+  }
+  return JXG_OK;
+}
+
+// rank 0: the frame is complete once every rank has written it
+static bool sstream_all_done(SStream& S, uint64_t k) {
+  const uint32_t s = (uint32_t)(k % S.slots);
+  for (uint32_t q = 0; q < S.world; q++)
+    if (shm_load(&S.done[s * S.world + q]) < (int64_t)k) return false;
+  return true;
+}
+
+// frames the caller can receive without waiting (rank 0: written by every rank)
+static uint32_t sstream_ready(Ctx* c) {
+  SStream& S = *c->ss;
+  std::lock_guard<std::mutex> lk(S.mu);
+  uint64_t k = S.received;
+  while (k < S.completed && (S.rank != 0 || sstream_all_done(S, k))) k++;
+  return (uint32_t)(k - S.received);
+}
+
+static jxg_status sstream_receive(Ctx* c, size_t* offset, size_t* bytes) {
+  SStream& S = *c->ss;
+  size_t total = 0;
+  const uint64_t k = S.received;
+  {
+    std::unique_lock<std::mutex> lk(S.mu);
+    if (k >= S.submitted) return JXG_ERR_INVALID_ARG;  // nothing pending
+    if (!S.cv.wait_for(lk, std::chrono::seconds(150), [&] { return S.err || S.completed > k; }))
+      return JXG_ERR_INTERNAL;
+    if (S.err) return S.err;
+    total = S.totals.front();
+  }
+  if (S.rank == 0) {
+    if (!shm_wait([&] { return sstream_all_done(S, k); }, nullptr)) return JXG_ERR_INTERNAL;
+    *offset = S.data_off + (size_t)(k % S.slots) * S.slot_bytes;
+    *bytes = total;
+    shm_store(&S.hd->consumed, (int64_t)k + 1);
+  } else {
+    *offset = 0;
+    *bytes = 0;
+  }
+  std::lock_guard<std::mutex> lk(S.mu);
+  S.totals.pop_front();
+  S.received++;
+  return JXG_OK;
+}
+
+// stop the completion thread (after the frames pending are received, or on
+// an error / destroy: abandon them)
+static void sstream_end(Ctx* c, float* ms_wait_ranks = nullptr) {
+  if (!c->ss) return;
+  SStream& S = *c->ss;
+  {
+    std::lock_guard<std::mutex> lk(S.mu);
+    S.stop = true;
+    S.cv.notify_all();
+  }
+  if (S.worker.joinable()) S.worker.join();
+  if (ms_wait_ranks) *ms_wait_ranks = S.ms_wait_ranks;
+  if (c->pipe) {
+    pipe_abort(c);
+    c->pipe->mode = 0;
+  }
+  c->ss.reset();
+}
+
 }  // namespace jxg
 
 using namespace jxg;
@@ -2553,6 +2911,7 @@ jxg_status jxg_create(const jxg_params* params, void** out) {
 void jxg_destroy(void* ctx) {
   if (!ctx) return;
   Ctx* c = static_cast<Ctx*>(ctx);
+  sstream_end(c);  // a streaming-shard completion thread first
   if (c->pipe) {  // frames still in the pipeline (their lanes are released below)
     pipe_abort(c);
     for (auto& d : c->pipe->done) jxg_buffer_free(&d.buf);
@@ -2704,6 +3063,11 @@ jxg_status jxg_receive(void* ctx, jxg_buffer* out) {
 jxg_status jxg_pending(void* ctx, uint32_t* n) {
   if (!ctx || !n) return JXG_ERR_INVALID_ARG;
   Ctx* c = static_cast<Ctx*>(ctx);
+  if (c->ss) {
+    std::lock_guard<std::mutex> lk(c->ss->mu);
+    *n = (uint32_t)(c->ss->submitted - c->ss->received);
+    return JXG_OK;
+  }
   *n = c->pipe ? (uint32_t)(c->pipe->inflight.size() + c->pipe->done.size() +
                             c->pipe->ready.size())
                : 0u;
@@ -2712,7 +3076,13 @@ jxg_status jxg_pending(void* ctx, uint32_t* n) {
 
 jxg_status jxg_get_stats(void* ctx, jxg_stats* stats) {
   if (!ctx || !stats) return JXG_ERR_INVALID_ARG;
-  *stats = static_cast<Ctx*>(ctx)->stats;
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (c->ss) {  // the completion thread updates them
+    std::lock_guard<std::mutex> lk(c->ss->mu);
+    *stats = c->stats;
+    return JXG_OK;
+  }
+  *stats = c->stats;
   return JXG_OK;
 }
 
@@ -2904,6 +3274,63 @@ jxg_status jxg_shard_write_next(void* ctx, const uint32_t* const* heads, const s
   if (st) return st;  // (too small a buffer: the frame stays, *total tells the size)
   c->pipe->ready.erase(c->pipe->ready.begin());  // its lane is free again
   return JXG_OK;
+}
+
+size_t jxg_shard_stream_region_size(void* ctx, uint32_t w, uint32_t h, uint32_t world,
+                                    uint32_t slots, size_t slot_bytes) {
+  if (!ctx || w == 0 || h == 0 || w > (1u << 18) || h > (1u << 18) || world == 0 || slots == 0)
+    return 0;
+  const Frame f = make_frame(w, h, static_cast<Ctx*>(ctx)->params.distance);
+  return shm_layout(f, world, slots, (slot_bytes + 4095) & ~(size_t)4095).total;
+}
+
+jxg_status jxg_shard_stream_begin(void* ctx, void* region, size_t region_size, uint32_t w,
+                                  uint32_t h, size_t stride, uint32_t rank, uint32_t world,
+                                  uint32_t slots, size_t slot_bytes, int init) {
+  if (!ctx || w == 0 || h == 0 || w > (1u << 18) || h > (1u << 18) || stride < (size_t)w * 3 ||
+      slot_bytes == 0)
+    return JXG_ERR_INVALID_ARG;
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
+  return sstream_begin(c, region, region_size, w, h, stride, rank, world, slots, slot_bytes, init);
+}
+
+jxg_status jxg_shard_stream_submit(void* ctx, const void* d_rgb) {
+  if (!ctx || !d_rgb) return JXG_ERR_INVALID_ARG;
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c->ss) return JXG_ERR_INVALID_ARG;
+  if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
+  return sstream_submit(c, static_cast<const uint8_t*>(d_rgb));
+}
+
+jxg_status jxg_shard_stream_ready(void* ctx, uint32_t* n) {
+  if (!ctx || !n) return JXG_ERR_INVALID_ARG;
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c->ss) return JXG_ERR_INVALID_ARG;
+  *n = sstream_ready(c);
+  std::lock_guard<std::mutex> lk(c->ss->mu);
+  return c->ss->err;
+}
+
+jxg_status jxg_shard_stream_receive(void* ctx, size_t* offset, size_t* bytes) {
+  if (!ctx || !offset || !bytes) return JXG_ERR_INVALID_ARG;
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c->ss) return JXG_ERR_INVALID_ARG;
+  return sstream_receive(c, offset, bytes);
+}
+
+jxg_status jxg_shard_stream_end(void* ctx, float* ms_wait_ranks) {
+  if (!ctx) return JXG_ERR_INVALID_ARG;
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c->ss) return JXG_ERR_INVALID_ARG;
+  jxg_status st;
+  {
+    std::lock_guard<std::mutex> lk(c->ss->mu);
+    st = c->ss->err;
+    if (!st && c->ss->received < c->ss->submitted) st = JXG_ERR_INVALID_ARG;  // frames dropped
+  }
+  sstream_end(c, ms_wait_ranks);
+  return st;
 }
 
 jxg_status jxg_homogeneity_map(void* ctx, const float* xyb, uint32_t xsize, uint32_t ysize,

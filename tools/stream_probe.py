@@ -1,0 +1,105 @@
+"""Throughput of the streamed-shard paths in ONE process (`world` contexts on
+one GPU play the ranks): native (jxg_shard_stream_*, completion threads) vs
+the Python protocol over jxg_shard_next_head / write_next.  For rocprofv3
+(no torch.distributed launcher in between).
+  python tools/stream_probe.py --mode native --world 2 --frames 40"""
+import argparse
+import ctypes
+import mmap
+import os
+import sys
+import time
+
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("JXG_BENCH_HW_QUEUES", "16")
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..",
+                                "jpeg-xl-lossy-image-compression-thesis_amd"))
+import jxg  # noqa: E402
+from jxg.synth import synth_rgb8_device  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--mode", choices=("native", "host"), default="native")
+ap.add_argument("--world", type=int, default=2)
+ap.add_argument("--frames", type=int, default=40)
+ap.add_argument("--warmup", type=int, default=16)
+ap.add_argument("--w", type=int, default=7680)
+ap.add_argument("--h", type=int, default=4320)
+ap.add_argument("--slots", type=int, default=6)
+a = ap.parse_args()
+w, h, W = a.w, a.h, a.world
+ts = [synth_rgb8_device(w, h, 0x4A584C02 + 100 * k) for k in range(2)]
+torch.cuda.synchronize()
+encs = [jxg.Encoder(flags=jxg.FLAG_ANS) for _ in range(W)]
+depth = min(e.pipeline_depth(w, h, r, W) for r, e in enumerate(encs))
+stamps = []
+sizes = []
+
+if a.mode == "native":
+    sb = w * h * 3 // 2 + (1 << 20)
+    size = encs[0].shard_stream_region_size(w, h, W, a.slots, sb)
+    region = mmap.mmap(-1, size)
+    addr = ctypes.addressof(ctypes.c_char.from_buffer(region))
+    assert jxg.load().jxg_host_register(ctypes.c_void_p(addr), size) == 0
+    for r, e in enumerate(encs):
+        e.shard_stream_begin(addr, size, w, h, r, W, a.slots, sb, r == 0)
+    maxp = depth + a.slots - 2
+    pend = 0
+
+    def take():
+        for r, e in enumerate(encs):
+            off, n = e.shard_stream_receive()
+            if r == 0:
+                sizes.append(n)
+        stamps.append(time.perf_counter())
+
+    def run(n):
+        global pend
+        for k in range(n):
+            for e in encs:
+                e.shard_stream_submit(ts[k % 2].data_ptr())
+            pend += 1
+            while pend >= maxp or (pend and encs[0].shard_stream_ready()):
+                take()
+                pend -= 1
+        while pend:
+            take()
+            pend -= 1
+else:
+    buf = np.zeros(w * h * 2 + (1 << 20), dtype=np.uint8)
+
+    def take():
+        heads = [e.shard_next_head() for e in encs]
+        for e in encs:
+            ok, t = e.shard_write_next(heads, buf.ctypes.data, buf.size)
+        sizes.append(t)
+        stamps.append(time.perf_counter())
+
+    def run(n):
+        for k in range(n):
+            for r, e in enumerate(encs):
+                e.shard_submit_device(ts[k % 2].data_ptr(), w, h, r, W)
+            if encs[0].pending() >= depth:
+                take()
+        while encs[0].pending():
+            take()
+
+run(a.warmup)
+torch.cuda.synchronize()
+stamps.clear()
+t0 = time.perf_counter()
+run(a.frames)
+torch.cuda.synchronize()
+dt = time.perf_counter() - t0
+gaps = np.diff(np.array([t0] + stamps)) * 1e3
+print("mode %s world %d depth %d: %.3f ms/frame, %.1f MPix/s, bytes %d; receive gaps ms "
+      "p50 %.3f p90 %.3f max %.3f" % (a.mode, W, depth, dt * 1e3 / a.frames,
+                                      w * h * a.frames / dt / 1e6, sizes[-1],
+                                      np.median(gaps), np.percentile(gaps, 90), gaps.max()),
+      flush=True)
+if a.mode == "native":
+    for e in encs:
+        e.shard_stream_end()
+for e in encs:
+    e.close()
