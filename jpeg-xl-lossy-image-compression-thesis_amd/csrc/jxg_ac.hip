@@ -503,18 +503,24 @@ __global__ __launch_bounds__(kAcThreads) void ac_emit_kernel(AcArgs a) {
 // to VALU) hands over; the other lanes run the same rANS steps on other
 // (valid) states, so every lane's table address stays in range.  The state
 // x = k << 12 | v is kept as (k = quotient of the previous step, v = its
-// inverse-table entry), which moves everything but the lookup off the
-// critical path:
-//   * emission: x >= f << 20  <=>  k >= f << 8, and then x >> 16 = k >> 4 --
-//     both known before v arrives;
-//   * quotient: floor(xs / f) = trunc((xs + 0.5) * rcp(f)) in f64 (exact: the
-//     error of the two roundings is < 2^-19 while (xs + .5) / f stays >= .5 / f
-//     from an integer), and (t + 0.5) * rcp is formed before v arrives, so
-//     after the LDS read: cvt, fma, cvt, one 24-bit multiply-add, the next read;
-//   * lane s saves its own pre-step state with a constant-mask select.
+// inverse-table entry).  One wave issues about one instruction per 4 cycles
+// whatever its dependency depth, so the step is cut to its fewest
+// instructions (15 issue slots; ns per token at 8K: 62.3 -> 56.5 -> 49.6 over
+// the three forms tried, profiles/r03p):
+//   * in the read's shadow: k from lane L-1 (DPP), emission k >= f << 8
+//     (x >= f << 20), which makes the shift sh = 16 (x >> 16 = k >> 4: v
+//     drops out) or 0; lane s-1 saves its pre-step state (constant-mask select);
+//   * after the read: x = k << 12 + v, xs = x >> sh, the quotient
+//     floor(xs / f) = trunc((xs + 0.5) * rcp(f)) in f64 (cvt, fma, cvt; exact:
+//     one rounding, < 2^-19, while (xs + .5) / f stays >= .5 / f from an
+//     integer), the table address base + 2 (xs - q f) (shift-add, 24-bit
+//     multiply-add), the next read.
 // Per 64 records the lanes decode record, f, rcp and table base in parallel
 // (the next 64 records are fetched meanwhile) and store the emitted bits of
 // their record with one coalesced store.
+// (A uniform variant -- every lane runs the same step, the quotient on the
+// scalar unit from readlane'd constants, two vector multiply-adds between the
+// reads -- is exact but took 17.5 vs 6.35 ms: ~60 instructions per step.)
 // Two chain waves per SIMD (8 per workgroup, 68 KB of LDS): the second wave
 // delays every step by its own issue (one frame's chains 6.7 vs 6.0 ms at 8K
 // with 4 per workgroup, profiles/r02g), but the chains of a frame occupy 64
@@ -572,29 +578,24 @@ __global__ __launch_bounds__(kAnsWaves * 64) void ans_encode_kernel(AnsArgs a) {
     uint32_t X = 0;     // lane L: the state before record L's step
     uint32_t xin = 0;   // the state handed to the previous step
     auto step = [&](int s) {
-      // in the shadow of the previous step's LDS read: everything that needs
-      // only k (emission, the v-free part of the quotient and address, and
-      // the factors that drop v on an emitting step); then save the
-      // previous step's input state in its lane
+      // shadow: emission (a shift of 16 drops v: (k << 12 | v) >> 16 = k >> 4),
+      // and the previous step's input state into its lane
       const uint32_t kin = wave_ror1(k);
-      const bool emit = kin >= Fq;
-      const uint32_t t = (kin << 12) >> (emit ? 16 : 0);  // xs without v
-      const double P = __builtin_fma((double)t, rcp, hr);
-      const double rs = emit ? 0.0 : rcp;
-      const uint32_t two = emit ? 0u : 2u;
-      const uint32_t C = 2 * t + base2;
+      const uint32_t sh = kin >= Fq ? 16u : 0u;
       if (s > 0)
         asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(X) : "v"(X), "v"(xin), "s"(1ull << (s - 1)));
       __builtin_amdgcn_sched_barrier(0);
-      // critical path: v -> quotient -> address -> next read
+      // critical path: v -> x -> xs -> quotient -> address -> next read
       const uint32_t vin = wave_ror1(v);
-      const uint32_t kk = (uint32_t)__builtin_fma((double)vin, rs, P);
-      uint32_t x2, addr;
-      asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(x2) : "v"(vin), "v"(two), "v"(C));
+      const uint32_t x = (kin << 12) + vin;
+      const uint32_t xs = x >> sh;
+      const uint32_t kk = (uint32_t)__builtin_fma((double)xs, rcp, hr);
+      const uint32_t x2 = (xs << 1) + base2;
+      uint32_t addr;
       asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(addr) : "v"(kk), "v"(nf2), "v"(x2));
       v = *reinterpret_cast<const uint16_t*>(inv + addr);
       k = kk;
-      xin = (kin << 12) + vin;
+      xin = x;
       __builtin_amdgcn_sched_barrier(0);
     };
     if (cnt == 64) {

@@ -64,6 +64,19 @@ struct DevBuf {
 
 static_assert(kAnsHists == (uint32_t)kAnsMaxHists, "ANS table blob sized for kAnsMaxHists");
 
+// A typed window into an arena (Ctx::stat / up and their host mirrors): the
+// arena is laid out per frame by stage_alloc, so ensure() only checks.
+template <class T>
+struct View {
+  T* p = nullptr;
+  size_t n = 0;
+  hipError_t ensure(size_t count) const { return count <= n ? hipSuccess : hipErrorInvalidValue; }
+  void set(void* base, size_t byte_off, size_t count) {
+    p = reinterpret_cast<T*>(static_cast<uint8_t*>(base) + byte_off);
+    n = count;
+  }
+};
+
 template <class T>
 struct PinBuf {
   T* p = nullptr;
@@ -484,20 +497,38 @@ struct Ctx {
   DevBuf<int8_t> cmap;  // [2][tiles] chroma from luma (front kernel)
   DevBuf<uint16_t> nz, mnat;
   DevBuf<float> ent, mwk, msdk, miwy, xyb_tiles, mcost;
-  DevBuf<uint32_t> vb, vcount, mwork, xlist;
+  DevBuf<uint32_t> vb, mwork, xlist;
   DevBuf<uint8_t> lf_mine;  // shard: [nlf] owned LF groups (vb_list)
   DevBuf<int32_t> dc;
   DevBuf<int16_t> ac;
   DevBuf<float> homog, xyb, r3;
   DevBuf<uint8_t> type;
-  DevBuf<uint32_t> hist_ac, bound, ntok, codes_ac, gbits, lfhist, sbound, lfcodes, chunkbits,
-      stream_chunks, stream_bits, scratch, scratch_lf, chunks, out, out_ac;
-  DevBuf<uint64_t> gbase, chunkoff, stream_base;
+  DevBuf<uint32_t> chunkbits, stream_chunks, scratch, scratch_lf, chunks, out, out_ac;
+  DevBuf<uint64_t> chunkoff;
+  // Per-frame statistics, zeroed by one memset and downloaded by two copies
+  // (AC part, LF part): [hist_ac | bound | ntok][lfhist | sbound | vcount]
+  DevBuf<uint8_t> stat;
+  PinBuf<uint8_t> h_stat;
+  View<uint32_t> hist_ac, bound, ntok, lfhist, sbound, vcount;
+  View<uint32_t> h_hist_ac, h_bound, h_ntok, h_lfhist, h_sbound, h_vcount;
+  size_t stat_lf = 0, stat_bytes = 0;  // byte offset of the LF part, total
+  // Per-frame code tables, uploaded by one copy (ANS) or two (prefix codes:
+  // the AC part ahead of the AC emission): [codes_ac | gbase | ans_order |
+  // ans_tab][lfcodes | stream_base]
+  DevBuf<uint8_t> up;
+  PinBuf<uint8_t> h_up;
+  View<uint32_t> codes_ac, ans_order, lfcodes, h_codes_ac, h_ans_order, h_lfcodes;
+  View<uint64_t> gbase, stream_base, h_gbase, h_sbase;
+  View<uint8_t> ans_tab, h_ans_tab;
+  size_t up_gbase = 0, up_ac = 0, up_lf = 0, up_bytes = 0;
+  // emitted bit counts, one download: [gbits | stream_bits]
+  DevBuf<uint32_t> bits;
+  PinBuf<uint32_t> h_bits;
+  View<uint32_t> gbits, stream_bits, h_gbits, h_sbits;
+  uint32_t* lf_scratch = nullptr;  // LF-stream bit arena (scratch_lf, or in scratch)
   DevBuf<uint32_t> tile_list, glist;  // shard: tile ids, pass groups (non-contiguous plans)
-  DevBuf<uint32_t> tokens, tval, ans_state, ans_order;  // ANS coder
+  DevBuf<uint32_t> tokens, tval, ans_state;  // ANS coder
   DevBuf<uint8_t> tlen;
-  DevBuf<uint8_t> ans_tab;
-  PinBuf<uint8_t> h_ans_tab;
   DevBuf<LfRow> rows;
   DevBuf<LfChunk> lfchunks;
   DevBuf<uint8_t> q_orig, q_comp;  // decode-side quality (jxg_compare_rgb8)
@@ -505,12 +536,11 @@ struct Ctx {
   DevBuf<double> q_part, q_ssim;
   bool gauss_ready = false;
   DevBuf<ConcatPiece> pieces, pieces_ac;
+  DevBuf<uint8_t> cat;  // stage_concat: [pieces | chunk words], one upload
+  PinBuf<uint8_t> h_cat;
   PinBuf<ConcatPiece> h_pieces_ac;
   // host
-  PinBuf<uint32_t> h_hist_ac, h_bound, h_ntok, h_lfhist, h_sbound, h_gbits, h_sbits, h_vcount,
-      h_codes_ac, h_lfcodes;
-  PinBuf<uint64_t> h_gbase, h_sbase;
-  PinBuf<uint32_t> h_ans_order;
+
   // LF row segments cached per frame size and shard
   uint32_t rows_w = 0, rows_h = 0, rows_rank = 0, rows_world = 1;
   std::vector<LfRow> rows_h_cache;
@@ -844,26 +874,97 @@ static jxg_status stage_alloc(Ctx* c, Job& J) {
     JXG_HIP(c->mcost.ensure((size_t)ntiles * kNumShapes * 32));
     JXG_HIP(c->mwork.ensure(1 + (size_t)ntiles * kNumShapes));
   }
+  // the plan's tile, LF-group and pass-group lists: uploaded when the plan
+  // changes (the same key as the LF row cache below)
+  const bool new_plan = c->rows_w != J.w || c->rows_h != J.h || c->rows_rank != J.plan.rank ||
+                        c->rows_world != J.plan.world;
   if (!J.plan.tiles.empty()) {
     JXG_HIP(c->tile_list.ensure(J.plan.tiles.size()));
-    JXG_HIP(hipMemcpyAsync(c->tile_list.p, J.plan.tiles.data(), J.plan.tiles.size() * 4,
-                           hipMemcpyHostToDevice, s));
+    if (new_plan)
+      JXG_HIP(hipMemcpyAsync(c->tile_list.p, J.plan.tiles.data(), J.plan.tiles.size() * 4,
+                             hipMemcpyHostToDevice, s));
   }
   if (!J.plan.lf_mine.empty()) {
     JXG_HIP(c->lf_mine.ensure(J.plan.lf_mine.size()));
-    JXG_HIP(hipMemcpyAsync(c->lf_mine.p, J.plan.lf_mine.data(), J.plan.lf_mine.size(),
-                           hipMemcpyHostToDevice, s));
+    if (new_plan)
+      JXG_HIP(hipMemcpyAsync(c->lf_mine.p, J.plan.lf_mine.data(), J.plan.lf_mine.size(),
+                             hipMemcpyHostToDevice, s));
   }
   JXG_HIP(c->vb.ensure((size_t)f.nlf * 65536));
-  JXG_HIP(c->vcount.ensure(f.nlf));
-  JXG_HIP(c->h_vcount.ensure(f.nlf));
-  JXG_HIP(c->hist_ac.ensure(kMaxClusters * kAlpha));
-  JXG_HIP(c->codes_ac.ensure(kMaxClusters * kAlpha));
-  JXG_HIP(c->bound.ensure(f.ngroups));
-  JXG_HIP(c->ntok.ensure(f.ngroups * 3));
-  JXG_HIP(c->gbits.ensure(f.ngroups));
-  JXG_HIP(c->gbase.ensure(f.ngroups));
   J.nstreams = f.nlf * 2;
+  {
+    // the statistics, code-table and bit-count arenas of this frame
+    const uint32_t ns = J.nstreams;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    size_t o = 0;
+    const size_t o_hist = o;
+    o = al(o + (size_t)kMaxClusters * kAlpha * 4);
+    const size_t o_bound = o;
+    o = al(o + (size_t)f.ngroups * 4);
+    const size_t o_ntok = o;
+    o = al(o + (size_t)f.ngroups * 12);
+    const size_t o_lfhist = o;
+    o = al(o + (size_t)ns * 4 * kAlpha * 4);
+    const size_t o_sbound = o;
+    o = al(o + (size_t)ns * 4);
+    const size_t o_vcount = o;
+    o = al(o + (size_t)f.nlf * 4);
+    JXG_HIP(c->stat.ensure(o));
+    JXG_HIP(c->h_stat.ensure(o));
+    c->stat_lf = o_lfhist;
+    c->stat_bytes = o;
+    c->hist_ac.set(c->stat.p, o_hist, (size_t)kMaxClusters * kAlpha);
+    c->bound.set(c->stat.p, o_bound, f.ngroups);
+    c->ntok.set(c->stat.p, o_ntok, (size_t)f.ngroups * 3);
+    c->lfhist.set(c->stat.p, o_lfhist, (size_t)ns * 4 * kAlpha);
+    c->sbound.set(c->stat.p, o_sbound, ns);
+    c->vcount.set(c->stat.p, o_vcount, f.nlf);
+    c->h_hist_ac.set(c->h_stat.p, o_hist, (size_t)kMaxClusters * kAlpha);
+    c->h_bound.set(c->h_stat.p, o_bound, f.ngroups);
+    c->h_ntok.set(c->h_stat.p, o_ntok, (size_t)f.ngroups * 3);
+    c->h_lfhist.set(c->h_stat.p, o_lfhist, (size_t)ns * 4 * kAlpha);
+    c->h_sbound.set(c->h_stat.p, o_sbound, ns);
+    c->h_vcount.set(c->h_stat.p, o_vcount, f.nlf);
+    const uint32_t ng = std::max(1u, J.plan.ng());
+    o = 0;
+    const size_t o_codes = o;
+    o = al(o + (size_t)kMaxClusters * kAlpha * 4);
+    const size_t o_gbase = o;
+    o = al(o + (size_t)f.ngroups * 8);
+    const size_t o_order = o;
+    o = al(o + (size_t)ng * 4);
+    const size_t o_tab = o;
+    o = al(o + kAnsTabBytes);
+    const size_t o_lfcodes = o;
+    o = al(o + (size_t)ns * 4 * kAlpha * 4);
+    const size_t o_sbase = o;
+    o = al(o + (size_t)ns * 8);
+    JXG_HIP(c->up.ensure(o));
+    JXG_HIP(c->h_up.ensure(o));
+    c->up_gbase = o_gbase;
+    c->up_ac = o_order;
+    c->up_lf = o_lfcodes;
+    c->up_bytes = o;
+    c->codes_ac.set(c->up.p, o_codes, (size_t)kMaxClusters * kAlpha);
+    c->gbase.set(c->up.p, o_gbase, f.ngroups);
+    c->ans_order.set(c->up.p, o_order, ng);
+    c->ans_tab.set(c->up.p, o_tab, kAnsTabBytes);
+    c->lfcodes.set(c->up.p, o_lfcodes, (size_t)ns * 4 * kAlpha);
+    c->stream_base.set(c->up.p, o_sbase, ns);
+    c->h_codes_ac.set(c->h_up.p, o_codes, (size_t)kMaxClusters * kAlpha);
+    c->h_gbase.set(c->h_up.p, o_gbase, f.ngroups);
+    c->h_ans_order.set(c->h_up.p, o_order, ng);
+    c->h_ans_tab.set(c->h_up.p, o_tab, kAnsTabBytes);
+    c->h_lfcodes.set(c->h_up.p, o_lfcodes, (size_t)ns * 4 * kAlpha);
+    c->h_sbase.set(c->h_up.p, o_sbase, ns);
+    const size_t nbits = (size_t)f.ngroups + ns;
+    JXG_HIP(c->bits.ensure(nbits));
+    JXG_HIP(c->h_bits.ensure(nbits));
+    c->gbits.set(c->bits.p, 0, f.ngroups);
+    c->stream_bits.set(c->bits.p, (size_t)f.ngroups * 4, ns);
+    c->h_gbits.set(c->h_bits.p, 0, f.ngroups);
+    c->h_sbits.set(c->h_bits.p, (size_t)f.ngroups * 4, ns);
+  }
   const bool new_rows = c->rows_w != J.w || c->rows_h != J.h || c->rows_rank != J.plan.rank ||
                         c->rows_world != J.plan.world;
   if (new_rows) {
@@ -878,21 +979,9 @@ static jxg_status stage_alloc(Ctx* c, Job& J) {
   const uint32_t nstreams = J.nstreams;
   JXG_HIP(c->rows.ensure(J.nrows));
   JXG_HIP(c->lfchunks.ensure(J.nchunks));
-  JXG_HIP(c->lfhist.ensure(nstreams * 4 * kAlpha));
-  JXG_HIP(c->lfcodes.ensure(nstreams * 4 * kAlpha));
-  JXG_HIP(c->sbound.ensure(nstreams));
   JXG_HIP(c->chunkbits.ensure(J.nchunks));
   JXG_HIP(c->chunkoff.ensure(J.nchunks));
   JXG_HIP(c->stream_chunks.ensure(nstreams + 1));
-  JXG_HIP(c->stream_base.ensure(nstreams));
-  JXG_HIP(c->stream_bits.ensure(nstreams));
-  JXG_HIP(c->h_hist_ac.ensure(kMaxClusters * kAlpha));
-  JXG_HIP(c->h_bound.ensure(f.ngroups));
-  JXG_HIP(c->h_ntok.ensure(f.ngroups * 3));
-  JXG_HIP(c->h_lfhist.ensure(nstreams * 4 * kAlpha));
-  JXG_HIP(c->h_sbound.ensure(nstreams));
-  JXG_HIP(c->h_gbits.ensure(f.ngroups));
-  JXG_HIP(c->h_sbits.ensure(nstreams));
   if (new_rows) {
     if (J.nrows)
       JXG_HIP(hipMemcpyAsync(c->rows.p, c->rows_h_cache.data(), J.nrows * sizeof(LfRow),
@@ -915,8 +1004,9 @@ static jxg_status stage_alloc(Ctx* c, Job& J) {
   aa.g0 = J.plan.g0();
   if (!J.plan.contiguous) {
     JXG_HIP(c->glist.ensure(J.plan.ng()));
-    JXG_HIP(hipMemcpyAsync(c->glist.p, J.plan.groups.data(), J.plan.ng() * 4,
-                           hipMemcpyHostToDevice, s));
+    if (new_plan)
+      JXG_HIP(hipMemcpyAsync(c->glist.p, J.plan.groups.data(), J.plan.ng() * 4,
+                             hipMemcpyHostToDevice, s));
     aa.glist = c->glist.p;
   }
   aa.hist = c->hist_ac.p;
@@ -1036,7 +1126,8 @@ static jxg_status stage_front(Ctx* c, Job& J) {
 
 // ---- stage C: AC token statistics of the plan's pass groups ----
 static jxg_status stage_ac_stats(Ctx* c, Job& J) {
-  JXG_HIP(hipMemsetAsync(c->hist_ac.p, 0, kMaxClusters * kAlpha * 4, c->stream));
+  // the whole statistics arena (AC and LF histograms, bounds) in one memset
+  JXG_HIP(hipMemsetAsync(c->stat.p, 0, c->stat_bytes, c->stream));
   launch_ac_hist(J.aa, J.plan.ng(), c->stream);
   JXG_HIP(hipGetLastError());
   return JXG_OK;
@@ -1048,9 +1139,7 @@ static jxg_status stage_lf_stats(Ctx* c, Job& J) {
   const Frame& f = J.f;
   VbArgs va{c->acs.p, f.bxs, f.bys, f.lfxs, J.plan.world > 1 ? c->lf_mine.p : nullptr, c->vb.p,
             c->vcount.p};
-  launch_vb_list(va, f.nlf, s);
-  JXG_HIP(hipMemsetAsync(c->lfhist.p, 0, (size_t)J.nstreams * 4 * kAlpha * 4, s));
-  JXG_HIP(hipMemsetAsync(c->sbound.p, 0, J.nstreams * 4, s));
+  launch_vb_list(va, f.nlf, s);  // (lfhist, sbound: zeroed by stage_ac_stats)
   if (J.nchunks) launch_lf_hist(J.la, J.nchunks, s);
   JXG_HIP(hipGetLastError());
   return JXG_OK;
@@ -1061,21 +1150,24 @@ static jxg_status stage_lf_stats(Ctx* c, Job& J) {
 // ac_hist is done, so the host builds the AC prefix codes while the LF
 // statistics kernels still run; the LF statistics follow in stage_download_lf.
 static jxg_status stage_download_ac(Ctx* c, Job& J, const uint32_t* hist) {
+  (void)J;
   hipStream_t s = c->stream;
-  const Frame& f = J.f;
-  JXG_HIP(hipMemcpyAsync(c->h_hist_ac.p, hist, kMaxClusters * kAlpha * 4, hipMemcpyDeviceToHost, s));
-  JXG_HIP(hipMemcpyAsync(c->h_bound.p, c->bound.p, f.ngroups * 4, hipMemcpyDeviceToHost, s));
-  JXG_HIP(hipMemcpyAsync(c->h_ntok.p, c->ntok.p, f.ngroups * 12, hipMemcpyDeviceToHost, s));
+  if (hist == c->hist_ac.p) {  // [hist_ac | bound | ntok]: one copy
+    JXG_HIP(hipMemcpyAsync(c->h_stat.p, c->stat.p, c->stat_lf, hipMemcpyDeviceToHost, s));
+  } else {  // a caller's (all-reduced) histogram
+    const size_t hb = (size_t)kMaxClusters * kAlpha * 4, ob = (uint8_t*)c->bound.p - c->stat.p;
+    JXG_HIP(hipMemcpyAsync(c->h_hist_ac.p, hist, hb, hipMemcpyDeviceToHost, s));
+    JXG_HIP(hipMemcpyAsync(c->h_stat.p + ob, c->stat.p + ob, c->stat_lf - ob, hipMemcpyDeviceToHost, s));
+  }
   JXG_HIP(hipEventRecord(c->ev[6], s));
   return JXG_OK;
 }
 static jxg_status stage_download_lf(Ctx* c, Job& J) {
+  (void)J;
   hipStream_t s = c->stream;
-  const Frame& f = J.f;
-  const uint32_t nstreams = J.nstreams;
-  JXG_HIP(hipMemcpyAsync(c->h_lfhist.p, c->lfhist.p, (size_t)nstreams * 4 * kAlpha * 4, hipMemcpyDeviceToHost, s));
-  JXG_HIP(hipMemcpyAsync(c->h_sbound.p, c->sbound.p, nstreams * 4, hipMemcpyDeviceToHost, s));
-  JXG_HIP(hipMemcpyAsync(c->h_vcount.p, c->vcount.p, f.nlf * 4, hipMemcpyDeviceToHost, s));
+  // [lfhist | sbound | vcount]: one copy
+  JXG_HIP(hipMemcpyAsync(c->h_stat.p + c->stat_lf, c->stat.p + c->stat_lf, c->stat_bytes - c->stat_lf,
+                         hipMemcpyDeviceToHost, s));
   JXG_HIP(hipEventRecord(c->ev[2], s));
   return JXG_OK;
 }
@@ -1206,8 +1298,8 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
     const uint64_t bound = (uint64_t)c->h_bound.p[g] + (J.ans ? nt + 32 : 0);
     cursor += (bound + 63) & ~31ull;
   }
-  const uint64_t ac_words = cursor / 32 + 2;
-  JXG_HIP(c->scratch.ensure(ac_words));
+  const uint64_t ac_words = (cursor / 32 + 2 + 63) & ~63ull;
+  if (!J.ans) JXG_HIP(c->scratch.ensure(ac_words));  // (ANS: with the LF arena below)
   // pinned upload sources: valid until the next frame's stage_codes, which
   // runs after this frame's emission has completed
   JXG_HIP(c->h_codes_ac.ensure(packed.size()));
@@ -1220,7 +1312,6 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
     JXG_HIP(c->tlen.ensure(nrec));
     JXG_HIP(c->ans_state.ensure(f.ngroups));
     JXG_HIP(c->ans_tab.ensure(kAnsTabBytes));
-    JXG_HIP(hipMemcpyAsync(c->ans_tab.p, c->h_ans_tab.p, kAnsTabBytes, hipMemcpyHostToDevice, s));
     // chain order: the plan's groups by token count, longest first, so a
     // chain workgroup holds groups of similar length and the workgroups of
     // short groups give their CUs (and 68 KB of LDS each) back early -- the
@@ -1236,14 +1327,14 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
       const uint32_t gx = gl[x], gy = gl[y];
       return nt[gx * 3] + nt[gx * 3 + 1] + nt[gx * 3 + 2] > nt[gy * 3] + nt[gy * 3 + 1] + nt[gy * 3 + 2];
     });
-    JXG_HIP(hipMemcpyAsync(c->ans_order.p, ord, ng * 4, hipMemcpyHostToDevice, s));
   }
-  JXG_HIP(hipMemcpyAsync(c->codes_ac.p, c->h_codes_ac.p, packed.size() * 4, hipMemcpyHostToDevice, s));
-  JXG_HIP(hipMemcpyAsync(c->gbase.p, c->h_gbase.p, J.gbase.size() * 8, hipMemcpyHostToDevice, s));
-  JXG_HIP(hipMemsetAsync(c->scratch.p, 0, ac_words * 4, s));
   const float ms_ac_codes = ms_since(t_codes);
-  J.aa.scratch = c->scratch.p;
   if (!J.ans) {
+    // prefix codes: the AC code tables now, so the AC emission runs while the
+    // host builds the LF-group codes (ANS: every table in one upload below)
+    JXG_HIP(hipMemcpyAsync(c->up.p, c->h_up.p, c->up_ac, hipMemcpyHostToDevice, s));
+    JXG_HIP(hipMemsetAsync(c->scratch.p, 0, ac_words * 4, s));
+    J.aa.scratch = c->scratch.p;
     launch_ac_emit(J.aa, J.plan.ng(), s);
     JXG_HIP(hipGetLastError());
     JXG_HIP(hipMemcpyAsync(c->h_gbits.p, c->gbits.p, f.ngroups * 4, hipMemcpyDeviceToHost, s));
@@ -1290,12 +1381,24 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
     if (J.plan.owns_lf(i / 2)) cursor += ((uint64_t)c->h_sbound.p[i] + 63) & ~31ull;
   }
   const uint64_t lf_words = cursor / 32 + 2;
-  JXG_HIP(c->scratch_lf.ensure(lf_words));
   JXG_HIP(c->h_sbase.ensure(J.sbase.size()));
   std::copy(J.sbase.begin(), J.sbase.end(), c->h_sbase.p);
-  JXG_HIP(hipMemcpyAsync(c->lfcodes.p, lfpacked, nlfcodes * 4, hipMemcpyHostToDevice, s));
-  JXG_HIP(hipMemcpyAsync(c->stream_base.p, c->h_sbase.p, J.sbase.size() * 8, hipMemcpyHostToDevice, s));
-  JXG_HIP(hipMemsetAsync(c->scratch_lf.p, 0, lf_words * 4, s));
+  if (J.ans) {
+    // one arena for the AC and LF bits (one memset) and every table in one
+    // upload
+    JXG_HIP(c->scratch.ensure(ac_words + lf_words));
+    c->lf_scratch = c->scratch.p + ac_words;
+    J.aa.scratch = c->scratch.p;
+    JXG_HIP(hipMemcpyAsync(c->up.p + c->up_gbase, c->h_up.p + c->up_gbase,
+                           c->up_bytes - c->up_gbase, hipMemcpyHostToDevice, s));
+    JXG_HIP(hipMemsetAsync(c->scratch.p, 0, (ac_words + lf_words) * 4, s));
+  } else {
+    JXG_HIP(c->scratch_lf.ensure(lf_words));
+    c->lf_scratch = c->scratch_lf.p;
+    JXG_HIP(hipMemcpyAsync(c->up.p + c->up_lf, c->h_up.p + c->up_lf, c->up_bytes - c->up_lf,
+                           hipMemcpyHostToDevice, s));
+    JXG_HIP(hipMemsetAsync(c->scratch_lf.p, 0, lf_words * 4, s));
+  }
   J.ms_codes = ms_ac_codes + ms_since(t_lf);
   return JXG_OK;
 }
@@ -1323,15 +1426,19 @@ static jxg_status stage_emit(Ctx* c, Job& J, bool sync = true) {
     na.order = c->ans_order.p;
     launch_ans(na, s);
     JXG_HIP(hipGetLastError());
-    JXG_HIP(hipMemcpyAsync(c->h_gbits.p, c->gbits.p, f.ngroups * 4, hipMemcpyDeviceToHost, s));
-    JXG_HIP(hipEventRecord(c->ev[7], s));
   }
-  J.la.scratch = c->scratch_lf.p;
+  J.la.scratch = c->lf_scratch;
   if (J.nchunks) launch_lf_bits(J.la, J.nchunks, s);
   launch_lf_scan(J.la, J.nstreams, s);
   if (J.nchunks) launch_lf_emit(J.la, J.nchunks, s);
   JXG_HIP(hipGetLastError());
-  JXG_HIP(hipMemcpyAsync(c->h_sbits.p, c->stream_bits.p, J.nstreams * 4, hipMemcpyDeviceToHost, s));
+  if (J.ans) {  // [gbits | stream_bits]: one copy
+    JXG_HIP(hipMemcpyAsync(c->h_bits.p, c->bits.p, ((size_t)f.ngroups + J.nstreams) * 4,
+                           hipMemcpyDeviceToHost, s));
+    JXG_HIP(hipEventRecord(c->ev[7], s));
+  } else {
+    JXG_HIP(hipMemcpyAsync(c->h_sbits.p, c->stream_bits.p, J.nstreams * 4, hipMemcpyDeviceToHost, s));
+  }
   JXG_HIP(hipEventRecord(c->ev[3], s));
   if (sync) JXG_HIP(hipStreamSynchronize(s));
   return JXG_OK;
@@ -1421,20 +1528,25 @@ static jxg_status stage_concat(Ctx* c, Job& J, bool full, std::vector<uint32_t>*
   const size_t nbytes = (size_t)(dst / 8);
   const size_t out_words = (nbytes + 3) / 4 + 1;
   chunk_words.push_back(0);  // read-ahead guard
-  JXG_HIP(c->chunks.ensure(chunk_words.size()));
-  JXG_HIP(c->pieces.ensure(std::max<size_t>(cps.size(), 1)));
+  // pieces and chunk words through one pinned staging buffer, one upload
+  // (the previous frame of this context has completed: the staging is free)
+  const size_t pb = (std::max<size_t>(cps.size(), 1) * sizeof(ConcatPiece) + 255) & ~(size_t)255;
+  const size_t wb = chunk_words.size() * 4;
+  JXG_HIP(c->cat.ensure(pb + wb));
+  JXG_HIP(c->h_cat.ensure(pb + wb));
   JXG_HIP(c->out.ensure(out_words));
   uint8_t* ho = nullptr;
   if (host_out) {  // else the bytes stay in c->out (device)
     ho = out_alloc(out_words * 4);
     if (!ho) return JXG_ERR_OOM;
   }
-  JXG_HIP(hipMemcpyAsync(c->chunks.p, chunk_words.data(), chunk_words.size() * 4, hipMemcpyHostToDevice, s));
-  if (!cps.empty())
-    JXG_HIP(hipMemcpyAsync(c->pieces.p, cps.data(), cps.size() * sizeof(ConcatPiece), hipMemcpyHostToDevice, s));
+  if (!cps.empty()) std::memcpy(c->h_cat.p, cps.data(), cps.size() * sizeof(ConcatPiece));
+  std::memcpy(c->h_cat.p + pb, chunk_words.data(), wb);
+  JXG_HIP(hipMemcpyAsync(c->cat.p, c->h_cat.p, pb + wb, hipMemcpyHostToDevice, s));
   JXG_HIP(hipMemsetAsync(c->out.p, 0, out_words * 4, s));
-  launch_concat(c->pieces.p, (uint32_t)cps.size(), max_words, c->scratch.p, c->chunks.p,
-                c->scratch_lf.p, c->out.p, s);
+  launch_concat(reinterpret_cast<const ConcatPiece*>(c->cat.p), (uint32_t)cps.size(), max_words,
+                c->scratch.p, reinterpret_cast<const uint32_t*>(c->cat.p + pb), c->lf_scratch,
+                c->out.p, s);
   JXG_HIP(hipGetLastError());
   if (ho && hipMemcpyAsync(ho, c->out.p, out_words * 4, hipMemcpyDeviceToHost, s) != hipSuccess) {
     out_release(ho);
@@ -1575,7 +1687,7 @@ static jxg_status stage_concat_split(Ctx* c, Job& J, uint8_t** host_out, size_t*
       hipMemsetAsync(c->out.p, 0, out_words * 4, s) != hipSuccess)
     return fail(JXG_ERR_HIP);
   launch_concat(c->pieces.p, (uint32_t)cps.size(), max_words, c->scratch.p, c->chunks.p,
-                c->scratch_lf.p, c->out.p, s);
+                c->lf_scratch, c->out.p, s);
   if (hipGetLastError() != hipSuccess ||
       hipMemcpyAsync(data, c->out.p, pbytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipStreamWaitEvent(s, c->ev[8], 0) != hipSuccess ||
@@ -2573,6 +2685,10 @@ struct SStream {
   jxg_status err = JXG_OK;
   std::atomic<bool> stop{false};
   float ms_wait_ranks = 0.0f;  // completion thread: time spent waiting for other ranks
+  // completion thread profile (JXG_SS_PROFILE=1: printed by end): ms in
+  // codes, finish (sections), slot wait, heads wait, write; frames
+  double prof[5] = {};
+  uint64_t prof_n = 0;
 };
 
 // spin (then sleep) until pred(), at most 120 s
@@ -2612,13 +2728,20 @@ static void sstream_worker(Ctx* c) {
       if (mine) fr->sf = own.get_future().share();  // no helper will start for it now
       codes = fr->sf;
     }
+    Clock::time_point tp = Clock::now();
+    auto lap = [&](int i) {
+      S.prof[i] += ms_since(tp);
+      tp = Clock::now();
+    };
     if (mine) own.set_value(enc_codes(fr->lane, fr->J, false));
     jxg_status st = codes.get();
     fr->phase = 2;
+    lap(0);
     size_t bytes = 0;
     if (!st) st = shard_finish(fr->lane, fr->J, &bytes);
     if (st) return sstream_fail(S, st);
     shard_frame_stats(*fr, bytes);
+    lap(1);
     const std::vector<uint32_t>& hw = fr->lane->payload_head;
     if (hw.size() > S.hcap) return sstream_fail(S, JXG_ERR_INTERNAL);
     const uint32_t s = (uint32_t)(k % S.slots), r = S.rank, W = S.world;
@@ -2632,6 +2755,7 @@ static void sstream_worker(Ctx* c) {
           return shm_load(&S.hd->consumed) >= prev + 2;
         }, &S))
       return sstream_fail(S, JXG_ERR_INTERNAL);
+    lap(2);
     std::memcpy(S.heads + ((size_t)s * W + r) * S.hcap, hw.data(), hw.size() * 4);
     shm_store(&S.pub[s * W + r], (int64_t)k);
     if (!shm_wait([&] {
@@ -2641,6 +2765,7 @@ static void sstream_worker(Ctx* c) {
         }, &S))
       return sstream_fail(S, JXG_ERR_INTERNAL);
     S.ms_wait_ranks += ms_since(tw);
+    lap(3);
     std::vector<const uint32_t*> hp(W);
     std::vector<size_t> hwords(W);
     for (uint32_t q = 0; q < W; q++) {
@@ -2654,6 +2779,8 @@ static void sstream_worker(Ctx* c) {
     if (st) return sstream_fail(S, st == JXG_ERR_INVALID_ARG && total > S.slot_bytes
                                         ? JXG_ERR_OOM : st);
     shm_store(&S.done[s * W + r], (int64_t)k);
+    lap(4);
+    S.prof_n++;
     {
       std::lock_guard<std::mutex> lk(S.mu);
       c->stats = fr->lane->stats;
@@ -2856,6 +2983,13 @@ static void sstream_end(Ctx* c, float* ms_wait_ranks = nullptr) {
   }
   if (S.worker.joinable()) S.worker.join();
   if (ms_wait_ranks) *ms_wait_ranks = S.ms_wait_ranks;
+  if (const char* e = std::getenv("JXG_SS_PROFILE"))
+    if (e[0] == '1' && S.prof_n)
+      std::fprintf(stderr,
+                   "shard stream rank %u: %llu frames, ms/frame codes %.3f finish %.3f slot %.3f "
+                   "heads %.3f write %.3f\n",
+                   S.rank, (unsigned long long)S.prof_n, S.prof[0] / S.prof_n, S.prof[1] / S.prof_n,
+                   S.prof[2] / S.prof_n, S.prof[3] / S.prof_n, S.prof[4] / S.prof_n);
   if (c->pipe) {
     pipe_abort(c);
     c->pipe->mode = 0;

@@ -35,6 +35,13 @@ encs = [jxg.Encoder(flags=jxg.FLAG_ANS) for _ in range(W)]
 depth = min(e.pipeline_depth(w, h, r, W) for r, e in enumerate(encs))
 stamps = []
 sizes = []
+tsub = [0.0]  # main thread: seconds inside submit calls
+
+
+def timed_submit(fn, *args):
+    t = time.perf_counter()
+    fn(*args)
+    tsub[0] += time.perf_counter() - t
 
 if a.mode == "native":
     sb = w * h * 3 // 2 + (1 << 20)
@@ -58,7 +65,7 @@ if a.mode == "native":
         global pend
         for k in range(n):
             for e in encs:
-                e.shard_stream_submit(ts[k % 2].data_ptr())
+                timed_submit(e.shard_stream_submit, ts[k % 2].data_ptr())
             pend += 1
             while pend >= maxp or (pend and encs[0].shard_stream_ready()):
                 take()
@@ -79,7 +86,7 @@ else:
     def run(n):
         for k in range(n):
             for r, e in enumerate(encs):
-                e.shard_submit_device(ts[k % 2].data_ptr(), w, h, r, W)
+                timed_submit(e.shard_submit_device, ts[k % 2].data_ptr(), w, h, r, W)
             if encs[0].pending() >= depth:
                 take()
         while encs[0].pending():
@@ -88,15 +95,16 @@ else:
 run(a.warmup)
 torch.cuda.synchronize()
 stamps.clear()
+tsub[0] = 0.0
 t0 = time.perf_counter()
 run(a.frames)
 torch.cuda.synchronize()
 dt = time.perf_counter() - t0
 gaps = np.diff(np.array([t0] + stamps)) * 1e3
-print("mode %s world %d depth %d: %.3f ms/frame, %.1f MPix/s, bytes %d; receive gaps ms "
-      "p50 %.3f p90 %.3f max %.3f" % (a.mode, W, depth, dt * 1e3 / a.frames,
-                                      w * h * a.frames / dt / 1e6, sizes[-1],
-                                      np.median(gaps), np.percentile(gaps, 90), gaps.max()),
+print("mode %s %dx%d world %d depth %d: %.3f ms/frame, %.1f MPix/s, bytes %d; in submit "
+      "%.3f ms/frame; receive gaps ms p50 %.3f p90 %.3f max %.3f"
+      % (a.mode, w, h, W, depth, dt * 1e3 / a.frames, w * h * a.frames / dt / 1e6, sizes[-1],
+         tsub[0] * 1e3 / a.frames, np.median(gaps), np.percentile(gaps, 90), gaps.max()),
       flush=True)
 if a.mode == "native":
     for e in encs:
