@@ -21,16 +21,18 @@ N > 1 (launched by torch.distributed.run, backend nccl = RCCL):
           step is ONE 7680x4320 frame whose 256x256 pass groups are split over
           the N ranks (whole LF groups per rank, jxg_shard_plan kind 1: no
           per-block records move; one HF preset per rank: no histogram
-          collective), streamed through jxg.dist.ShardStream -- each rank keeps
-          up to jxg_pipeline_depth frames' shards in flight in the library's
-          lanes; a native completion thread per rank (jxg_shard_stream_*)
-          swaps the frame's payload heads with the other ranks through a
-          node-shared /dev/shm region and DMAs its sections into the frame's
-          codestream there (rank 0 adds headers + TOC).  value = frames x
-          7680 x 4320 / time over all ranks.  --scaling weak: one frame of N
-          stacked 8K frames per step instead.
-  shard-py -- the same stream with the per-frame protocol in Python
-          (jxg.dist.HostShardStream over jxg_shard_next_head / write_next).
+          collective), streamed through jxg.dist.HostShardStream -- each rank
+          keeps up to jxg_pipeline_depth frames' shards in flight in the
+          library's lanes (jxg_shard_submit_device), swaps each frame's payload
+          heads with the other ranks through a node-shared /dev/shm region and
+          DMAs its sections into the frame's codestream there
+          (jxg_shard_next_head / jxg_shard_write_next; rank 0 adds headers +
+          TOC).  value = frames x 7680 x 4320 / time over all ranks.
+          --scaling weak: one frame of N stacked 8K frames per step instead.
+  shard-native -- the same stream with the per-frame completion in the
+          library (jxg.dist.ShardStream over jxg_shard_stream_*: a completion
+          thread per rank; same bytes, slower in the measurements so far:
+          DESIGN.md §5).
   shard-sync -- the same split one frame at a time (jxg.dist.encode_sharded:
           record exchange + histogram all-reduce when the plan / coder needs
           them, --assembly host|device).
@@ -213,11 +215,13 @@ def main():
     ap.add_argument("--distance", type=float, default=1.0)
     ap.add_argument("--effort", type=int, default=7)
     ap.add_argument("--proposals", type=int, default=0)
-    ap.add_argument("--mode", choices=("shard", "shard-py", "shard-sync", "replica"),
+    ap.add_argument("--mode", choices=("shard", "shard-native", "shard-sync", "replica"),
                     default="shard",
                     help="N > 1: shard = every frame's pass groups split over the ranks, "
-                         "streamed (ShardStream; BASELINE config 2 as written); shard-sync = the "
-                         "same one frame at a time (encode_sharded); replica = every rank "
+                         "streamed (HostShardStream; BASELINE config 2 as written); "
+                         "shard-native = the same with the library's completion thread "
+                         "(ShardStream); shard-sync = the same one frame at a time "
+                         "(encode_sharded); replica = every rank "
                          "streams its own frames (frame-level data parallelism)")
     ap.add_argument("--alt-replica", type=int, default=1,
                     help="shard mode, N > 1: also time frame replicas (reported under "
@@ -266,7 +270,7 @@ def main():
         else:
             dist.init_process_group(backend)
     name, w, h, nframes = CONFIGS[args.config]
-    sharded_mode = world > 1 and args.mode in ("shard", "shard-py", "shard-sync")
+    sharded_mode = world > 1 and args.mode in ("shard", "shard-native", "shard-sync")
     strong = sharded_mode and args.scaling == "strong"
     fh = h if strong or not sharded_mode else h * world
     # inputs generated on the device (jxg_synth_rgb8_device: the bytes of
@@ -293,8 +297,8 @@ def main():
 
     def run(mode, coder, nstreams=1, proposals=None, pipe=True):
         """Warm up, then time args.steps steps of `mode` ("frames": each rank
-        encodes whole frames -- N = 1 / replicas; "shard": ShardStream;
-        "shard-sync": encode_sharded)."""
+        encodes whole frames -- N = 1 / replicas; "shard": HostShardStream;
+        "shard-native": ShardStream; "shard-sync": encode_sharded)."""
         sharded = mode != "frames"
         per_step, d_imgs = make_frames(sharded)
         nd = len(d_imgs)
@@ -317,9 +321,9 @@ def main():
         ss = None
         host = None
         bufs = {}
-        if mode in ("shard", "shard-py"):
+        if mode in ("shard", "shard-native"):
             from jxg.dist import HostShardStream, ShardStream
-            ss = (ShardStream if mode == "shard" else HostShardStream)(encs[0], w, fh, rank, world)
+            ss = (HostShardStream if mode == "shard" else ShardStream)(encs[0], w, fh, rank, world)
         elif mode == "shard-sync" and args.assembly == "host":
             from jxg.dist import SharedHostBuffer
             if SharedHostBuffer.single_node():
@@ -449,7 +453,7 @@ def main():
                         "bytes_per_frame": P["sizes"][-1]}
         P["enc"].close()
     iso = None
-    streamed = mode in ("shard", "shard-py")
+    streamed = mode in ("shard", "shard-native")
     if mode == "frames" and pipeline or streamed:
         # the kernels alone on the GPU (one-at-a-time encodes of this rank's
         # frame, same coder): the front kernel's roofline, the rANS chain
@@ -491,7 +495,7 @@ def main():
                            coder_desc, world, args.scaling, jxg.shard_plan(w, fh, world)[2],
                            "streamed (jxg.dist.%s, %d frames in flight per rank, heads "
                            "and sections through /dev/shm)"
-                           % ("ShardStream" if mode == "shard" else "HostShardStream", R["depth"])
+                           % ("HostShardStream" if mode == "shard" else "ShardStream", R["depth"])
                            if streamed else
                            "one frame at a time (encode_sharded), %s assembly" % args.assembly))
             par = "group-shard%d" % world

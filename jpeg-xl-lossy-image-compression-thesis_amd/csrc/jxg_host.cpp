@@ -1987,7 +1987,10 @@ static void pipe_abort(Ctx* c) {
 //          nsections x (TOC index, bytes) [| version 2: the rank's HF preset]
 //          | section bytes back to back
 constexpr uint32_t kPayloadMagic = 0x5347584Au;  // "JXGS"
-static jxg_status shard_finish(Ctx* c, Job& J, size_t* payload_bytes) {
+// (sync false: the body may still be in flight on the context's stream; the
+// streaming paths enqueue its D2H behind it -- shard_write_host -- so the head
+// goes out one GPU round trip earlier)
+static jxg_status shard_finish(Ctx* c, Job& J, size_t* payload_bytes, bool sync = true) {
   hipStream_t s = c->stream;
   JXG_HIP(hipStreamSynchronize(s));  // the emission's bit counts on the host
   std::vector<uint32_t> ids, sizes;
@@ -2020,7 +2023,7 @@ static jxg_status shard_finish(Ctx* c, Job& J, size_t* payload_bytes) {
   }
   c->payload_body = nbytes;
   *payload_bytes = hw.size() * 4 + nbytes;
-  JXG_HIP(hipStreamSynchronize(s));
+  if (sync) JXG_HIP(hipStreamSynchronize(s));
   return JXG_OK;
 }
 
@@ -2049,7 +2052,7 @@ static jxg_status pipe_complete_oldest(Ctx* c) {
   if (!st && fr.phase == 1) st = enc_codes(fr.lane, fr.J, false);
   if (fr.shard) {
     size_t bytes = 0;
-    if (!st) st = shard_finish(fr.lane, fr.J, &bytes);
+    if (!st) st = shard_finish(fr.lane, fr.J, &bytes, false);
     if (st) return st;
     shard_frame_stats(fr, bytes);
     p.ready.push_back(std::move(p.inflight.front()));
@@ -2529,8 +2532,10 @@ static jxg_status shard_assemble_device(Ctx* c, const uint8_t* d_base, const siz
 // run, its LF groups one each); rank 0 also writes headers + TOC.  Same bytes
 // as shard_assemble_device, without the payload gather and the serial D2H of
 // the whole codestream on rank 0.
+// (sync false: the copies are left in flight on the context's stream)
 static jxg_status shard_write_host(Ctx* c, const uint32_t* const* heads_in, const size_t* words,
-                                   uint32_t n, uint8_t* dst, size_t dst_size, size_t* total) {
+                                   uint32_t n, uint8_t* dst, size_t dst_size, size_t* total,
+                                   bool sync = true) {
   if (c->payload_head.size() < 7) return JXG_ERR_INVALID_ARG;
   std::vector<std::vector<uint32_t>> heads(n);
   std::vector<size_t> ps(n);
@@ -2588,7 +2593,7 @@ static jxg_status shard_write_host(Ctx* c, const uint32_t* const* heads_in, cons
     for (size_t i = 0; i < secs.size(); i++)  // a generated HfGlobal (per-rank presets)
       if (secs[i].payload == n && secs[i].size) std::memcpy(dst + out_off[i], hf.data(), hf.size());
   }
-  JXG_HIP(hipStreamSynchronize(s));
+  if (sync) JXG_HIP(hipStreamSynchronize(s));
   return JXG_OK;
 }
 
@@ -2689,6 +2694,7 @@ struct SStream {
   // codes, finish (sections), slot wait, heads wait, write; frames
   double prof[5] = {};
   uint64_t prof_n = 0;
+  double sprof[3] = {};  // submitting thread: lane wait, launch, lag join
 };
 
 // spin (then sleep) until pred(), at most 120 s
@@ -2714,19 +2720,50 @@ static void sstream_worker(Ctx* c) {
   SStream& S = *c->ss;
   Pipe& p = *c->pipe;
   if (hipSetDevice(c->params.device) != hipSuccess) return sstream_fail(S, JXG_ERR_HIP);
-  for (uint64_t k = 0;; k++) {
+  const uint32_t r = S.rank, W = S.world;
+  // Frame k's sections are DMA'd without waiting; it is marked done (and its
+  // lane freed) after frame k + 1's D2H is queued, or at once when no frame
+  // follows yet: the completion of consecutive frames overlaps.
+  PipeFrame* pend = nullptr;
+  uint64_t pend_k = 0;
+  size_t pend_total = 0;
+  auto flush = [&]() -> bool {
+    if (!pend) return true;
+    if (hipStreamSynchronize(pend->lane->stream) != hipSuccess) {
+      sstream_fail(S, JXG_ERR_HIP);
+      return false;
+    }
+    shm_store(&S.done[(pend_k % S.slots) * W + r], (int64_t)pend_k);
+    std::lock_guard<std::mutex> lk(S.mu);
+    c->stats = pend->lane->stats;
+    p.inflight.erase(p.inflight.begin());  // its lane is free again
+    S.totals.push_back(pend_total);
+    S.completed++;
+    S.cv.notify_all();
+    pend = nullptr;
+    return true;
+  };
+  for (uint64_t k = 0;;) {
     PipeFrame* fr = nullptr;
     std::shared_future<jxg_status> codes;
     std::promise<jxg_status> own;
     bool mine = false;
     {
       std::unique_lock<std::mutex> lk(S.mu);
-      S.cv.wait(lk, [&] { return S.stop || S.err || !p.inflight.empty(); });
-      if (S.err || p.inflight.empty()) return;  // stopped and drained (or failed)
-      fr = p.inflight.front().get();
-      mine = !fr->sf.valid();
-      if (mine) fr->sf = own.get_future().share();  // no helper will start for it now
-      codes = fr->sf;
+      const size_t at = pend ? 1 : 0;  // the frame after the pending one
+      if (!pend) S.cv.wait(lk, [&] { return S.stop || S.err || !p.inflight.empty(); });
+      if (S.err) return;
+      if (p.inflight.size() > at) {
+        fr = p.inflight[at].get();
+        mine = !fr->sf.valid();
+        if (mine) fr->sf = own.get_future().share();  // no helper will start for it now
+        codes = fr->sf;
+      }
+    }
+    if (!fr) {  // nothing behind the pending frame (or stopped and drained)
+      if (!pend) return;
+      if (!flush()) return;
+      continue;
     }
     Clock::time_point tp = Clock::now();
     auto lap = [&](int i) {
@@ -2738,13 +2775,13 @@ static void sstream_worker(Ctx* c) {
     fr->phase = 2;
     lap(0);
     size_t bytes = 0;
-    if (!st) st = shard_finish(fr->lane, fr->J, &bytes);
+    if (!st) st = shard_finish(fr->lane, fr->J, &bytes, false);
     if (st) return sstream_fail(S, st);
     shard_frame_stats(*fr, bytes);
     lap(1);
     const std::vector<uint32_t>& hw = fr->lane->payload_head;
     if (hw.size() > S.hcap) return sstream_fail(S, JXG_ERR_INTERNAL);
-    const uint32_t s = (uint32_t)(k % S.slots), r = S.rank, W = S.world;
+    const uint32_t s = (uint32_t)(k % S.slots);
     const Clock::time_point tw = Clock::now();
     // slot s held frame k - slots: every rank wrote it and rank 0's caller has
     // moved past its view (views stay valid until the next receive)
@@ -2774,21 +2811,18 @@ static void sstream_worker(Ctx* c) {
       if (!hwords[q]) return sstream_fail(S, JXG_ERR_INTERNAL);
     }
     size_t total = 0;
-    st = shard_write_host(fr->lane, hp.data(), hwords.data(), W, S.base + S.data_off +
-                          (size_t)s * S.slot_bytes, S.slot_bytes, &total);
+    st = shard_write_host(fr->lane, hp.data(), hwords.data(), W,
+                          S.base + S.data_off + (size_t)s * S.slot_bytes, S.slot_bytes, &total,
+                          false);
     if (st) return sstream_fail(S, st == JXG_ERR_INVALID_ARG && total > S.slot_bytes
                                         ? JXG_ERR_OOM : st);
-    shm_store(&S.done[s * W + r], (int64_t)k);
+    pend = fr;
+    pend_k = k;
+    pend_total = total;
+    if (!flush()) return;  // (marked done once its copies have landed)
     lap(4);
     S.prof_n++;
-    {
-      std::lock_guard<std::mutex> lk(S.mu);
-      c->stats = fr->lane->stats;
-      p.inflight.erase(p.inflight.begin());  // its lane is free again
-      S.totals.push_back(total);
-      S.completed++;
-      S.cv.notify_all();
-    }
+    k++;
   }
 }
 
@@ -2848,6 +2882,10 @@ static jxg_status sstream_begin(Ctx* c, void* base, size_t size, uint32_t w, uin
   S->data_off = L.data;
   S->depth = pipe_depth(P.ng());
   S->lag = pipe_lag(P.ng(), S->depth);
+  if (const char* e = std::getenv("JXG_SS_DEPTH"))  // (tuning experiments)
+    S->depth = std::max(2u, std::min(S->depth, (uint32_t)std::strtoul(e, nullptr, 10)));
+  if (const char* e = std::getenv("JXG_SS_LAG"))
+    S->lag = std::max(1u, std::min(S->depth - 1, (uint32_t)std::strtoul(e, nullptr, 10)));
   jxg_status st = ensure_lanes(c, S->depth - 1);
   if (st) return st;
   c->pipe->mode = 2;
@@ -2868,6 +2906,7 @@ static jxg_status sstream_submit(Ctx* c, const uint8_t* d_rgb) {
   Ctx* L = nullptr;
   std::unique_ptr<PipeFrame> fr(new (std::nothrow) PipeFrame());
   if (!fr) return JXG_ERR_OOM;
+  const Clock::time_point t_in = Clock::now();
   {
     std::unique_lock<std::mutex> lk(S.mu);
     // (a frame completes only after rank 0's caller receives the one S - 2
@@ -2876,21 +2915,6 @@ static jxg_status sstream_submit(Ctx* c, const uint8_t* d_rgb) {
                        [&] { return S.err || p.inflight.size() < S.depth; }))
       return JXG_ERR_INTERNAL;
     if (S.err) return S.err;
-    // the newest frame's codes on a helper thread (unless the completion
-    // thread already took them on)
-    if (!p.inflight.empty()) {
-      PipeFrame* prev = p.inflight.back().get();
-      if (!prev->sf.valid()) {
-        const int dev = c->params.device;
-        try {
-          prev->sf = std::async(std::launch::async, [prev, dev]() {
-                       if (hipSetDevice(dev) != hipSuccess) return JXG_ERR_HIP;
-                       return enc_codes(prev->lane, prev->J, false);
-                     }).share();
-        } catch (...) {  // no thread: the completion thread builds them
-        }
-      }
-    }
     for (uint32_t li = 0; li < S.depth && !L; li++) {
       Ctx* cand = li == 0 ? c : c->lanes[li - 1].get();
       bool used = false;
@@ -2902,8 +2926,11 @@ static jxg_status sstream_submit(Ctx* c, const uint8_t* d_rgb) {
   fr->lane = L;
   fr->t0 = Clock::now();
   fr->shard = true;
+  S.sprof[0] += ms_since(t_in);
+  const Clock::time_point t_l = Clock::now();
   jxg_status st = order_input(c, L);
   if (!st) st = enc_launch(L, fr->J, d_rgb, S.w, S.h, S.stride, S.rank, S.world);
+  S.sprof[1] += ms_since(t_l);
   if (st) {
     (void)hipStreamSynchronize(L->stream);
     sstream_fail(S, st);
@@ -2912,6 +2939,18 @@ static jxg_status sstream_submit(Ctx* c, const uint8_t* d_rgb) {
   std::shared_future<jxg_status> lagged;
   {
     std::lock_guard<std::mutex> lk(S.mu);
+    // this frame's codes on a helper thread from now on: it waits for the
+    // statistics download and builds them as soon as they land (the
+    // completion thread builds them itself if no thread can be started)
+    PipeFrame* nf = fr.get();
+    const int dev = c->params.device;
+    try {
+      nf->sf = std::async(std::launch::async, [nf, dev]() {
+                 if (hipSetDevice(dev) != hipSuccess) return JXG_ERR_HIP;
+                 return enc_codes(nf->lane, nf->J, false);
+               }).share();
+    } catch (...) {
+    }
     p.inflight.push_back(std::move(fr));
     S.submitted++;
     S.cv.notify_all();
@@ -2920,10 +2959,12 @@ static jxg_status sstream_submit(Ctx* c, const uint8_t* d_rgb) {
     // before the transform kernels of the frames behind it)
     if (p.inflight.size() > S.lag) lagged = p.inflight[p.inflight.size() - 1 - S.lag]->sf;
   }
+  const Clock::time_point t_j = Clock::now();
   if (lagged.valid() && (st = lagged.get())) {
     sstream_fail(S, st);
     return st;
   }
+  S.sprof[2] += ms_since(t_j);
   return JXG_OK;
 }
 
@@ -2987,9 +3028,10 @@ static void sstream_end(Ctx* c, float* ms_wait_ranks = nullptr) {
     if (e[0] == '1' && S.prof_n)
       std::fprintf(stderr,
                    "shard stream rank %u: %llu frames, ms/frame codes %.3f finish %.3f slot %.3f "
-                   "heads %.3f write %.3f\n",
+                   "heads %.3f write %.3f; submit: lane wait %.3f launch %.3f lag join %.3f\n",
                    S.rank, (unsigned long long)S.prof_n, S.prof[0] / S.prof_n, S.prof[1] / S.prof_n,
-                   S.prof[2] / S.prof_n, S.prof[3] / S.prof_n, S.prof[4] / S.prof_n);
+                   S.prof[2] / S.prof_n, S.prof[3] / S.prof_n, S.prof[4] / S.prof_n,
+                   S.sprof[0] / S.prof_n, S.sprof[1] / S.prof_n, S.sprof[2] / S.prof_n);
   if (c->pipe) {
     pipe_abort(c);
     c->pipe->mode = 0;
