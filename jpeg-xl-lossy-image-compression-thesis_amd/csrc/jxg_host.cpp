@@ -560,6 +560,10 @@ struct Ctx {
   hipStream_t in_stream = nullptr;
   hipEvent_t ev_in = nullptr;
   bool owned_lane = false;  // a pipeline / batch lane of another context
+  // streaming pipeline (ANS): the rANS chains go to the pipeline's chain
+  // batcher instead of this context's stream (ev_up: codes uploaded)
+  struct ChainBatcher* batcher = nullptr;
+  hipEvent_t ev_up = nullptr;
   std::unique_ptr<struct Job> job;  // sharded encode in flight (begin -> end)
   std::unique_ptr<struct Pipe> pipe;  // streaming encode (jxg_submit_* / jxg_receive)
   std::unique_ptr<struct SStream> ss; // streaming shards over a shared region (jxg_shard_stream_*)
@@ -847,7 +851,183 @@ struct Job {
   std::vector<uint64_t> gbase, sbase;
   float ms_codes = 0.0f;
   float ms_layout = 0.0f;  // stage_concat_split host layout
+  // enc_finish_start -> enc_finish_end: the codestream (pinned pool block,
+  // D2H in flight), its size, the host layout time
+  uint8_t* host_out = nullptr;
+  size_t out_bytes = 0;
+  float ms_finish_layout = 0.0f;
+  // chain batcher: set once this frame's chains, bit placement and group bit
+  // counts are enqueued (then ev[7] of its context marks them done)
+  std::shared_future<jxg_status> chain;
 };
+
+// ---------------------------------------------------------------------------
+// Chain batches (streaming pipeline, ANS).  A frame's rANS chains last as
+// long as its longest pass group's (≈ 5 ms at 256×256 groups, whatever the
+// frame size), so with one chain launch per frame on the frame's own lane a
+// lane is held ≥ 5 ms per frame and small frames (1080p: 40 groups; a rank's
+// 1/8 of an 8K frame: 64) are bound by lanes / latency, not by the GPU.  The
+// pipeline's batcher thread instead launches the chains of every frame whose
+// codes are uploaded as ONE kernel (ans_encode_multi_kernel) on its own
+// stream, each time the previous batch has finished, then each frame's bit
+// placement and group bit counts; the lanes never wait on a chain.
+// ---------------------------------------------------------------------------
+struct ChainEntry {
+  Ctx* lane = nullptr;
+  AnsArgs na{};
+  uint32_t ngroups = 0;
+  std::promise<jxg_status> enq;
+};
+struct ChainBatcher {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev_batch = nullptr;
+  bool have_prev = false;
+  DevBuf<uint8_t> d_desc;  // [AnsArgs frames][u32 workgroup map]
+  PinBuf<uint8_t> h_desc;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::unique_ptr<ChainEntry>> pending;
+  bool stop = false;
+  std::thread th;
+  uint64_t batches = 0, frames = 0;  // (profile)
+};
+// Measured slower than per-lane chains at every size tried (1/8 of an 8K
+// frame, 64 x 1080p, 8K; with 12 to 28 lanes, profiles/r03_stream): off
+// unless JXG_CHAIN_BATCH=1.
+static bool chain_batch_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("JXG_CHAIN_BATCH");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+static jxg_status chain_launch(ChainBatcher& B, std::vector<std::unique_ptr<ChainEntry>>& batch) {
+  const size_t nf = batch.size();
+  std::vector<uint32_t> wg;
+  for (size_t i = 0; i < nf; i++)
+    for (uint32_t w = 0; w < ans_chain_wgs(batch[i]->na.n); w++) wg.push_back((uint32_t)i << 20 | w);
+  const size_t fb = (nf * sizeof(AnsArgs) + 255) & ~(size_t)255, total = fb + wg.size() * 4 + 4;
+  // (the previous batch has finished: its descriptors are free)
+  JXG_HIP(B.h_desc.ensure(total));
+  JXG_HIP(B.d_desc.ensure(total));
+  for (size_t i = 0; i < nf; i++)
+    std::memcpy(B.h_desc.p + i * sizeof(AnsArgs), &batch[i]->na, sizeof(AnsArgs));
+  if (!wg.empty()) std::memcpy(B.h_desc.p + fb, wg.data(), wg.size() * 4);
+  JXG_HIP(hipMemcpyAsync(B.d_desc.p, B.h_desc.p, total, hipMemcpyHostToDevice, B.stream));
+  for (auto& e : batch) JXG_HIP(hipStreamWaitEvent(B.stream, e->lane->ev_up, 0));
+  launch_ans_multi(reinterpret_cast<const AnsArgs*>(B.d_desc.p),
+                   reinterpret_cast<const uint32_t*>(B.d_desc.p + fb), (uint32_t)wg.size(), B.stream);
+  JXG_HIP(hipGetLastError());
+  for (auto& e : batch) {
+    launch_ans_emit(e->na, B.stream);
+    JXG_HIP(hipGetLastError());
+    Ctx* L = e->lane;
+    JXG_HIP(hipMemcpyAsync(L->h_gbits.p, L->gbits.p, (size_t)e->ngroups * 4, hipMemcpyDeviceToHost,
+                           B.stream));
+    JXG_HIP(hipEventRecord(L->ev[7], B.stream));
+  }
+  JXG_HIP(hipEventRecord(B.ev_batch, B.stream));
+  B.have_prev = true;
+  B.batches++;
+  B.frames += nf;
+  return JXG_OK;
+}
+static void chain_thread(ChainBatcher* B) {
+  (void)hipSetDevice(B->device);
+  for (;;) {
+    {
+      std::unique_lock<std::mutex> lk(B->mu);
+      B->cv.wait(lk, [&] { return B->stop || !B->pending.empty(); });
+      if (B->pending.empty()) return;  // stopped and drained
+    }
+    // let the running batch finish: the frames that arrive meanwhile join
+    // the next one
+    if (B->have_prev) (void)hipEventSynchronize(B->ev_batch);
+    std::vector<std::unique_ptr<ChainEntry>> batch;
+    {
+      std::lock_guard<std::mutex> lk(B->mu);
+      while (!B->pending.empty()) {
+        batch.push_back(std::move(B->pending.front()));
+        B->pending.pop_front();
+      }
+    }
+    const jxg_status st = chain_launch(*B, batch);
+    for (auto& e : batch) e->enq.set_value(st);
+  }
+}
+static std::unique_ptr<ChainBatcher> chain_batcher_create(int device) {
+  std::unique_ptr<ChainBatcher> B(new (std::nothrow) ChainBatcher());
+  if (!B) return nullptr;
+  B->device = device;
+  if (hipStreamCreateWithFlags(&B->stream, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  if (hipEventCreateWithFlags(&B->ev_batch, hipEventDisableTiming) != hipSuccess) {
+    (void)hipStreamDestroy(B->stream);
+    return nullptr;
+  }
+  try {
+    B->th = std::thread(chain_thread, B.get());
+  } catch (...) {
+    (void)hipEventDestroy(B->ev_batch);
+    (void)hipStreamDestroy(B->stream);
+    return nullptr;
+  }
+  return B;
+}
+// drain (every queued frame's chains are launched) and stop
+static void chain_batcher_destroy(std::unique_ptr<ChainBatcher>& B) {
+  if (!B) return;
+  {
+    std::lock_guard<std::mutex> lk(B->mu);
+    B->stop = true;
+    B->cv.notify_all();
+  }
+  if (B->th.joinable()) B->th.join();
+  (void)hipStreamSynchronize(B->stream);
+  (void)hipEventDestroy(B->ev_batch);
+  (void)hipStreamDestroy(B->stream);
+  if (const char* e = std::getenv("JXG_CHAIN_PROFILE"))
+    if (e[0] == '1' && B->batches)
+      std::fprintf(stderr, "chain batches: %llu, %.2f frames per batch\n",
+                   (unsigned long long)B->batches, (double)B->frames / (double)B->batches);
+  B.reset();
+}
+static std::shared_future<jxg_status> chain_submit(ChainBatcher* B, Ctx* lane, const AnsArgs& na,
+                                                   uint32_t ngroups) {
+  std::unique_ptr<ChainEntry> e(new ChainEntry());
+  e->lane = lane;
+  e->na = na;
+  e->ngroups = ngroups;
+  std::shared_future<jxg_status> f = e->enq.get_future().share();
+  std::lock_guard<std::mutex> lk(B->mu);
+  B->pending.push_back(std::move(e));
+  B->cv.notify_all();
+  return f;
+}
+// the emission of J on c is done and its bit counts are on the host
+static jxg_status wait_emission(Ctx* c, Job& J) {
+  if (J.chain.valid()) {
+    const jxg_status st = J.chain.get();
+    J.chain = std::shared_future<jxg_status>();
+    if (st) return st;
+    JXG_HIP(hipEventSynchronize(c->ev[7]));
+  }
+  JXG_HIP(hipStreamSynchronize(c->stream));
+  return JXG_OK;
+}
+// non-blocking: 1 done, 0 not yet, < 0 error
+static int emission_done(Ctx* c, Job& J) {
+  if (J.chain.valid()) {
+    if (J.chain.wait_for(std::chrono::seconds(0)) != std::future_status::ready) return 0;
+    if (J.chain.get()) return -1;
+    const hipError_t q = hipEventQuery(c->ev[7]);
+    if (q == hipErrorNotReady) return 0;
+    if (q != hipSuccess) return -1;
+  }
+  const hipError_t q = hipEventQuery(c->ev[3]);
+  if (q == hipErrorNotReady) return 0;
+  return q == hipSuccess ? 1 : -1;
+}
 
 // ---- stage A: buffers for the frame / plan ----
 static jxg_status stage_alloc(Ctx* c, Job& J) {
@@ -1424,15 +1604,21 @@ static jxg_status stage_emit(Ctx* c, Job& J, bool sync = true) {
     na.n = J.plan.ng();
     na.glist = J.aa.glist;
     na.order = c->ans_order.p;
-    launch_ans(na, s);
-    JXG_HIP(hipGetLastError());
+    if (c->batcher) {  // the pipeline's chain batcher (group bit counts: its D2H)
+      if (!c->ev_up) JXG_HIP(hipEventCreateWithFlags(&c->ev_up, hipEventDisableTiming));
+      JXG_HIP(hipEventRecord(c->ev_up, s));
+      J.chain = chain_submit(c->batcher, c, na, f.ngroups);
+    } else {
+      launch_ans(na, s);
+      JXG_HIP(hipGetLastError());
+    }
   }
   J.la.scratch = c->lf_scratch;
   if (J.nchunks) launch_lf_bits(J.la, J.nchunks, s);
   launch_lf_scan(J.la, J.nstreams, s);
   if (J.nchunks) launch_lf_emit(J.la, J.nchunks, s);
   JXG_HIP(hipGetLastError());
-  if (J.ans) {  // [gbits | stream_bits]: one copy
+  if (J.ans && !J.chain.valid()) {  // [gbits | stream_bits]: one copy
     JXG_HIP(hipMemcpyAsync(c->h_bits.p, c->bits.p, ((size_t)f.ngroups + J.nstreams) * 4,
                            hipMemcpyDeviceToHost, s));
     JXG_HIP(hipEventRecord(c->ev[7], s));
@@ -1440,7 +1626,10 @@ static jxg_status stage_emit(Ctx* c, Job& J, bool sync = true) {
     JXG_HIP(hipMemcpyAsync(c->h_sbits.p, c->stream_bits.p, J.nstreams * 4, hipMemcpyDeviceToHost, s));
   }
   JXG_HIP(hipEventRecord(c->ev[3], s));
-  if (sync) JXG_HIP(hipStreamSynchronize(s));
+  if (sync) {
+    jxg_status st = wait_emission(c, J);
+    if (st) return st;
+  }
   return JXG_OK;
 }
 
@@ -1571,6 +1760,11 @@ static jxg_status stage_concat_split(Ctx* c, Job& J, uint8_t** host_out, size_t*
     return JXG_ERR_HIP;  // created on first use: only lone contexts take this path
   hipStream_t s = c->stream, s2 = c->stream2;
   const Frame& f = J.f;
+  if (J.chain.valid()) {  // (a chain batch records ev[7] once it has enqueued this frame)
+    const jxg_status st = J.chain.get();
+    J.chain = std::shared_future<jxg_status>();
+    if (st) return st;
+  }
   JXG_HIP(hipEventSynchronize(c->ev[7]));  // AC emission done, its bit counts on the host
   const uint32_t g0 = J.plan.g0(), ng = J.plan.ng();  // (one context: all groups)
   JXG_HIP(c->h_pieces_ac.ensure(std::max<uint32_t>(ng, 1)));
@@ -1748,25 +1942,35 @@ static jxg_status enc_codes(Ctx* c, Job& J, bool sync) {
 }
 
 // phase 3: assembly, the codestream in host memory, stats
-static jxg_status enc_finish(Ctx* c, Job& J, bool split, jxg_buffer* out,
-                             Clock::time_point t_call) {
+// phase 3 in two halves: enc_finish_start (the emission's bit counts on the
+// host -> layout, concat and the codestream's D2H enqueued) and enc_finish_end
+// (wait for them, stats).  The streaming pipeline starts a frame's assembly
+// as soon as its emission is done and ends it when the frame is taken.
+static jxg_status enc_finish_start(Ctx* c, Job& J, bool split) {
+  const Clock::time_point t_layout = Clock::now();
+  J.host_out = nullptr;
+  J.out_bytes = 0;
+  jxg_status st;
+  if (split) {
+    if ((st = stage_concat_split(c, J, &J.host_out, &J.out_bytes))) return st;
+  } else {
+    // the emission's bit counts on the host (stage_emit may have returned
+    // without waiting)
+    if ((st = wait_emission(c, J))) return st;
+    if ((st = stage_concat(c, J, true, nullptr, nullptr, &J.host_out, &J.out_bytes))) return st;
+  }
+  J.ms_finish_layout = split ? J.ms_layout : ms_since(t_layout);
+  return JXG_OK;
+}
+static jxg_status enc_finish_end(Ctx* c, Job& J, jxg_buffer* out, Clock::time_point t_call) {
   hipStream_t s = c->stream;
   const jxg_params& P = c->params;
   const Frame& f = J.f;
   const size_t nb = (size_t)f.bxs * f.bys;
-  const Clock::time_point t_layout = Clock::now();
-  uint8_t* host_out = nullptr;
-  size_t out_bytes = 0;
-  jxg_status st;
-  if (split) {
-    if ((st = stage_concat_split(c, J, &host_out, &out_bytes))) return st;
-  } else {
-    // the emission's bit counts on the host (stage_emit may have returned
-    // without waiting)
-    JXG_HIP(hipStreamSynchronize(s));
-    if ((st = stage_concat(c, J, true, nullptr, nullptr, &host_out, &out_bytes))) return st;
-  }
-  const float ms_layout = split ? J.ms_layout : ms_since(t_layout);
+  uint8_t* host_out = J.host_out;
+  const size_t out_bytes = J.out_bytes;
+  J.host_out = nullptr;
+  const float ms_layout = J.ms_finish_layout;
   std::vector<int16_t> m_ac16_tmp;
   if (P.flags & JXG_FLAG_KEEP_MAPS) {
     c->m_acs.resize(nb);
@@ -1823,6 +2027,11 @@ static jxg_status enc_finish(Ctx* c, Job& J, bool split, jxg_buffer* out,
   S.ms_host_layout = ms_layout;
   S.ms_host_call = ms_since(t_call);
   return JXG_OK;
+}
+static jxg_status enc_finish(Ctx* c, Job& J, bool split, jxg_buffer* out,
+                             Clock::time_point t_call) {
+  const jxg_status st = enc_finish_start(c, J, split);
+  return st ? st : enc_finish_end(c, J, out, t_call);
 }
 
 static bool pipe_busy(const Ctx* c);
@@ -1894,7 +2103,12 @@ static uint32_t hw_queues() {
 }
 static uint32_t pipe_depth(uint32_t ngroups) {
   const uint32_t d = (JXG_PIPE_CHAIN_GROUPS + ngroups - 1) / std::max(1u, ngroups);
-  const uint32_t want = std::min(kPipeMaxLanes, std::max((uint32_t)JXG_PIPE_MIN_LANES, d));
+  uint32_t maxl = kPipeMaxLanes;
+  if (const char* e = std::getenv("JXG_PIPE_MAX_LANES"))  // (tuning experiments)
+    maxl = std::max(2u, std::min(64u, (uint32_t)std::strtoul(e, nullptr, 10)));
+  const uint32_t want = std::min(maxl, std::max((uint32_t)JXG_PIPE_MIN_LANES, d));
+  const char* qc = std::getenv("JXG_PIPE_QUEUE_CAP");  // 0: lanes may share queues
+  if (qc && qc[0] == '0') return std::max(2u, want);
   return std::max(2u, std::min(want, hw_queues() - 1));
 }
 static uint32_t pipe_lag(uint32_t ngroups, uint32_t depth) {
@@ -1916,7 +2130,7 @@ static PipeProf g_pprof;
 struct PipeFrame {
   Ctx* lane = nullptr;
   Job J;
-  int phase = 1;  // 1: statistics launched; 2: emission launched
+  int phase = 1;  // 1: statistics launched; 2: emission launched; 3: assembly enqueued
   bool shard = false;
   Clock::time_point t0;
   std::future<jxg_status> codes;  // valid while a helper builds the codes
@@ -1947,7 +2161,20 @@ struct Pipe {
   uint64_t submitted = 0;
   int mode = 0;  // 1 whole frames, 2 shards (while any frame is pending)
   uint32_t depth = 0;
+  std::unique_ptr<ChainBatcher> batcher;  // (ANS; created with the lanes)
 };
+// the pipeline's chain batcher on every lane (ANS, JXG_CHAIN_BATCH != 0)
+static jxg_status pipe_batcher(Ctx* c) {
+  Pipe& p = *c->pipe;
+  if (!(c->params.flags & JXG_FLAG_ANS) || !chain_batch_enabled()) return JXG_OK;
+  if (!p.batcher) {
+    p.batcher = chain_batcher_create(c->params.device);
+    if (!p.batcher) return JXG_ERR_INTERNAL;
+  }
+  c->batcher = p.batcher.get();
+  for (auto& l : c->lanes) l->batcher = p.batcher.get();
+  return JXG_OK;
+}
 static bool pipe_busy(const Ctx* c) {
   return c->ss || (c->pipe && (!c->pipe->inflight.empty() || !c->pipe->done.empty() ||
                                !c->pipe->ready.empty()));
@@ -1973,9 +2200,16 @@ static void pipe_abort(Ctx* c) {
   for (auto& fr : p.inflight) {
     (void)pipe_join_codes(*fr);
     if (fr->sf.valid()) fr->sf.wait();
+    if (fr->J.chain.valid()) fr->J.chain.wait();  // (the batcher launches every queued frame)
   }
+  if (p.batcher) (void)hipStreamSynchronize(p.batcher->stream);
   for (auto& fr : p.inflight) (void)hipStreamSynchronize(fr->lane->stream);
   for (auto& fr : p.ready) (void)hipStreamSynchronize(fr->lane->stream);
+  for (auto& fr : p.inflight)  // codestreams of frames whose assembly had started
+    if (fr->J.host_out) {
+      out_release(fr->J.host_out);
+      fr->J.host_out = nullptr;
+    }
   p.inflight.clear();
   p.ready.clear();
 }
@@ -1992,7 +2226,8 @@ constexpr uint32_t kPayloadMagic = 0x5347584Au;  // "JXGS"
 // goes out one GPU round trip earlier)
 static jxg_status shard_finish(Ctx* c, Job& J, size_t* payload_bytes, bool sync = true) {
   hipStream_t s = c->stream;
-  JXG_HIP(hipStreamSynchronize(s));  // the emission's bit counts on the host
+  jxg_status st0 = wait_emission(c, J);  // the emission's bit counts on the host
+  if (st0) return st0;
   std::vector<uint32_t> ids, sizes;
   size_t nbytes = 0;
   jxg_status st;
@@ -2045,6 +2280,41 @@ static void shard_frame_stats(PipeFrame& fr, size_t bytes) {
   S.ms_host_call = ms_since(fr.t0);
 }
 
+// Non-blocking progress of whole frames in flight, oldest first: codes
+// joined once their helper has finished, assembly (layout, concat, the
+// codestream's D2H) started once the emission is done -- so the blocking
+// completion of the oldest frame later finds its bytes on the way.
+static bool pipe_progress_enabled() {  // (measured slower: off unless JXG_PIPE_PROGRESS=1)
+  static const bool on = [] {
+    const char* e = std::getenv("JXG_PIPE_PROGRESS");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+static jxg_status pipe_progress(Ctx* c) {
+  Pipe& p = *c->pipe;
+  for (auto& up : p.inflight) {
+    PipeFrame& fr = *up;
+    if (fr.shard) break;
+    if (fr.phase == 1) {
+      if (!fr.codes.valid() ||
+          fr.codes.wait_for(std::chrono::seconds(0)) != std::future_status::ready)
+        break;
+      const jxg_status st = pipe_join_codes(fr);
+      if (st) return st;
+    }
+    if (fr.phase == 2) {
+      const int q = emission_done(fr.lane, fr.J);
+      if (q == 0) break;
+      if (q < 0) return JXG_ERR_HIP;
+      const jxg_status st = enc_finish_start(fr.lane, fr.J, false);
+      if (st) return st;
+      fr.phase = 3;
+    }
+  }
+  return JXG_OK;
+}
+
 static jxg_status pipe_complete_oldest(Ctx* c) {
   Pipe& p = *c->pipe;
   PipeFrame& fr = *p.inflight.front();
@@ -2067,7 +2337,8 @@ static jxg_status pipe_complete_oldest(Ctx* c) {
     PPROF_ADD(finish_wait, tw);
   }
 #endif
-  if (!st) st = enc_finish(fr.lane, fr.J, false, &d.buf, fr.t0);
+  if (!st && fr.phase < 3) st = enc_finish_start(fr.lane, fr.J, false);
+  if (!st) st = enc_finish_end(fr.lane, fr.J, &d.buf, fr.t0);
   if (st) return st;
   d.stats = fr.lane->stats;
   p.done.push_back(d);
@@ -2100,6 +2371,7 @@ static jxg_status pipe_submit(Ctx* c, const uint8_t* src, bool on_device, uint32
   }
   const uint32_t depth = pipe_depth(ngroups), lag = pipe_lag(ngroups, depth);
   jxg_status st = ensure_lanes(c, depth - 1);
+  if (!st) st = pipe_batcher(c);
   if (st) return st;
   const Clock::time_point t0 = Clock::now();
   // a shard frame holds its lane until its sections are written: the caller
@@ -2181,6 +2453,7 @@ static jxg_status pipe_submit(Ctx* c, const uint8_t* src, bool on_device, uint32
 #endif
   if (p.inflight.size() > lag && (st = pipe_join_codes(*p.inflight[p.inflight.size() - 1 - lag])))
     return fail(st);
+  if (mode == 1 && pipe_progress_enabled() && (st = pipe_progress(c))) return fail(st);
 #ifdef JXG_PIPE_PROFILE
   PPROF_ADD(join, tj);
   PPROF_ADD(submit, t0);
@@ -2887,6 +3160,7 @@ static jxg_status sstream_begin(Ctx* c, void* base, size_t size, uint32_t w, uin
   if (const char* e = std::getenv("JXG_SS_LAG"))
     S->lag = std::max(1u, std::min(S->depth - 1, (uint32_t)std::strtoul(e, nullptr, 10)));
   jxg_status st = ensure_lanes(c, S->depth - 1);
+  if (!st) st = pipe_batcher(c);
   if (st) return st;
   c->pipe->mode = 2;
   c->pipe->depth = S->depth;
@@ -3090,6 +3364,9 @@ void jxg_destroy(void* ctx) {
   sstream_end(c);  // a streaming-shard completion thread first
   if (c->pipe) {  // frames still in the pipeline (their lanes are released below)
     pipe_abort(c);
+    chain_batcher_destroy(c->pipe->batcher);
+    c->batcher = nullptr;
+    for (auto& l : c->lanes) l->batcher = nullptr;
     for (auto& d : c->pipe->done) jxg_buffer_free(&d.buf);
     c->pipe.reset();
   }
@@ -3115,6 +3392,7 @@ void jxg_destroy(void* ctx) {
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   if (c->ev_in) (void)hipEventDestroy(c->ev_in);
+  if (c->ev_up) (void)hipEventDestroy(c->ev_up);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
   delete c;

@@ -135,6 +135,12 @@ struct AnsArgs {
   const uint32_t* order;   // chain order of the n slots (longest group first)
 };
 void launch_ans(const AnsArgs& a, hipStream_t s);
+// chain batches (the streaming pipeline): workgroups per frame, the chains of
+// several frames in one launch (d_wg[b] = frame << 20 | workgroup in frame),
+// then each frame's bit placement
+uint32_t ans_chain_wgs(uint32_t ngroups);
+void launch_ans_multi(const AnsArgs* d_frames, const uint32_t* d_wg, uint32_t nwg, hipStream_t s);
+void launch_ans_emit(const AnsArgs& a, hipStream_t s);
 
 // LF-group modular streams: rows of (lf group, stream, channel, y)
 // One segment of <= kLfSeg samples of a channel row (long rows -- the
