@@ -58,6 +58,15 @@ typedef enum {
 #define JXG_FLAG_FORCE_ONE_STREAM 8u /* testing: the split assembly takes its one-stream
                                       * fallback (as when its prefix bound is exceeded);
                                       * same bytes */
+/* restoration filters (cjxl --gaborish / --epf), off by
+ * default: GABORISH applies the encoder's inverse Gaborish to the XYB image
+ * before every other stage and enables the decoder's 3x3 Gaborish; EPF enables
+ * the decoder's edge-preserving filter (iterations from the distance: 1 below
+ * d 1.5, 2 below d 4, else 3; constant sharpness 4 per block).  Both are
+ * signalled in the frame header (LoopFilter) [ext, parity with libjxl
+ * unpinned; DESIGN.md §3.8] */
+#define JXG_FLAG_GABORISH 16u
+#define JXG_FLAG_EPF 32u
 
 typedef struct {
   float distance;      /* cjxl --distance (butteraugli target), (0, 25] */

@@ -1,6 +1,8 @@
 // jxg_bitstream.cpp -- see jxg_bitstream.h.
 #include "jxg_bitstream.h"
 
+#include "../../include/jxg.h"
+
 #include <algorithm>
 #include <cstring>
 
@@ -540,6 +542,12 @@ const TreeNode kMetaTree[7] = {{0, 1, 1, 2, 0, -1},  {0, 2, 3, 4, 0, -1},
                                {-1, 0, 0, 0, 0, 0},  {-1, 0, 0, 0, 0, 1},
                                {2, 0, 5, 6, 0, -1},  {-1, 0, 0, 0, 1, 2},
                                {-1, 0, 0, 0, 0, 3}};
+// with EPF: every block's sharpness is kEpfSharpness, carried by the EPF
+// leaf's offset (the residuals the GPU emits stay 0; oracle encode.c)
+const TreeNode kMetaTreeEpf[7] = {{0, 1, 1, 2, 0, -1},  {0, 2, 3, 4, 0, -1},
+                                  {-1, 0, 0, 0, 0, 0},  {-1, 0, 0, 0, 0, 1, kEpfSharpness},
+                                  {2, 0, 5, 6, 0, -1},  {-1, 0, 0, 0, 1, 2},
+                                  {-1, 0, 0, 0, 0, 3}};
 
 void write_modular_prelude(BitWriter& w, const TreeNode* tree, int nnodes, int nleaves,
                            const std::vector<PrefixCode>& leaf_codes) {
@@ -553,7 +561,7 @@ void write_modular_prelude(BitWriter& w, const TreeNode* tree, int nnodes, int n
     if (t.prop < 0) {
       toks.push_back({1, 0});
       toks.push_back({2, (uint32_t)t.predictor});
-      toks.push_back({3, 0});
+      toks.push_back({3, t.offset >= 0 ? (uint32_t)t.offset * 2u : (uint32_t)(-t.offset) * 2u - 1u});
       toks.push_back({4, 0});
       toks.push_back({5, 0});
     } else {
@@ -590,7 +598,13 @@ void write_size(BitWriter& w, uint32_t v) {
 }
 }  // namespace
 
-void write_headers(BitWriter& w, uint32_t xs, uint32_t ys) {
+uint32_t lf_code(uint32_t flags, float distance) {
+  uint32_t c = (flags & JXG_FLAG_GABORISH) ? 1u : 0u;
+  if (flags & JXG_FLAG_EPF) c |= (distance < 1.5f ? 1u : (distance < 4.0f ? 2u : 3u)) << 1;
+  return c;
+}
+
+void write_headers(BitWriter& w, uint32_t xs, uint32_t ys, uint32_t lf) {
   w.put(8, 0xFF);
   w.put(8, 0x0A);
   if (xs % 8 == 0 && ys % 8 == 0 && xs <= 256 && ys <= 256) {
@@ -619,10 +633,22 @@ void write_headers(BitWriter& w, uint32_t xs, uint32_t ys) {
   w.put(2, 0);                      // blending: replace
   w.put(1, 1);                      // is_last
   w.put(2, 0);                      // name length 0
-  w.put(1, 0);                      // loop filter not all_default
-  w.put(1, 0);                      //   no gaborish
-  w.put(2, 0);                      //   epf_iters 0
-  w.put(2, 0);                      //   loop filter extensions
+  // LoopFilter [ext loop_filter.h]: all_default = Gaborish + one EPF iteration
+  const uint32_t gab = lf & 1u, epf = (lf >> 1) & 3u;
+  if (gab && epf == 1) {
+    w.put(1, 1);                    // loop filter all_default
+  } else {
+    w.put(1, 0);                    // loop filter not all_default
+    w.put(1, gab);                  //   gab
+    if (gab) w.put(1, 0);           //   gab_custom
+    w.put(2, epf);                  //   epf_iters
+    if (epf) {
+      w.put(1, 0);                  //   epf_sharp_custom
+      w.put(1, 0);                  //   epf_weight_custom
+      w.put(1, 0);                  //   epf_sigma_custom
+    }
+    w.put(2, 0);                    //   loop filter extensions
+  }
   w.put(2, 0);                      // frame extensions
 }
 

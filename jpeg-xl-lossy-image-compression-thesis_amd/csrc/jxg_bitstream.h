@@ -112,16 +112,22 @@ void write_ans_histograms(BitWriter& w, const std::vector<uint8_t>& ctxmap, int 
 // Modular MA trees used by the LF-group streams (local trees, no transforms)
 struct TreeNode {
   int prop, splitval, lchild, rchild, predictor, leaf;  // prop < 0: leaf
+  int offset;                                          // leaf: value offset
 };
 extern const TreeNode kDcTree[5];
 extern const TreeNode kMetaTree[7];
+extern const TreeNode kMetaTreeEpf[7];  // the EPF leaf's offset = kEpfSharpness
+constexpr int kEpfSharpness = 4;        // [ext] constant EPF sharpness per block
 // GroupHeader + tree + data histograms (leaf codes); the residual tokens are
 // emitted on the GPU
 void write_modular_prelude(BitWriter& w, const TreeNode* tree, int nnodes, int nleaves,
                            const std::vector<PrefixCode>& leaf_codes);
 
+// loop-filter code of the frame header: bit 0 Gaborish, bits 1-2 EPF
+// iterations (oracle/xyb.c jxo_lf_code)
+uint32_t lf_code(uint32_t flags, float distance);
 // SizeHeader + all-default ImageMetadata + byte padding + FrameHeader
-void write_headers(BitWriter& w, uint32_t xsize, uint32_t ysize);
+void write_headers(BitWriter& w, uint32_t xsize, uint32_t ysize, uint32_t lf = 0);
 void write_toc(BitWriter& w, const std::vector<uint32_t>& section_bytes);
 void write_u32_sel(BitWriter& w, uint32_t sel, uint32_t nbits, uint32_t v);
 

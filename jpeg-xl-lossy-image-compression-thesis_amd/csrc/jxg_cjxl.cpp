@@ -120,7 +120,8 @@ int main(int argc, char** argv) {
   if (argc < 3) {
     std::fprintf(stderr,
                  "usage: %s INPUT OUTPUT [--distance=D] [--effort=E] "
-                 "[--proposals=none|P|F|PF] [--coder=prefix|ans] [--device=N]\n",
+                 "[--proposals=none|P|F|PF] [--coder=prefix|ans] [--gaborish=0|1] "
+                 "[--epf=-1|0] [--device=N]\n",
                  argv[0]);
     return 1;
   }
@@ -139,6 +140,20 @@ int main(int argc, char** argv) {
         p.flags |= JXG_FLAG_ANS;
       else if (std::strcmp(a + 8, "prefix")) {
         std::fprintf(stderr, "unknown coder: %s\n", a + 8);
+        return 1;
+      }
+    } else if (!std::strncmp(a, "--gaborish=", 11)) {  // cjxl --gaborish
+      if (!std::strcmp(a + 11, "1"))
+        p.flags |= JXG_FLAG_GABORISH;
+      else if (std::strcmp(a + 11, "0")) {
+        std::fprintf(stderr, "unsupported --gaborish: %s\n", a + 11);
+        return 1;
+      }
+    } else if (!std::strncmp(a, "--epf=", 6)) {  // cjxl --epf: -1 = by distance
+      if (!std::strcmp(a + 6, "-1"))
+        p.flags |= JXG_FLAG_EPF;
+      else if (std::strcmp(a + 6, "0")) {
+        std::fprintf(stderr, "unsupported --epf (-1 or 0): %s\n", a + 6);
         return 1;
       }
     } else if (!std::strncmp(a, "--device=", 9))

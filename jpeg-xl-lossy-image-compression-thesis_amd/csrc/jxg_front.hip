@@ -797,6 +797,107 @@ __device__ __forceinline__ void load_xyb_tile(const FrontArgs& a, const float* l
   }
 }
 
+// ---------------------------------------------------------------------------
+// inverse Gaborish (JXG_FLAG_GABORISH; oracle/xyb.c jxo_gab_inverse): the
+// 3x3 symmetric least-squares inverse of the decoder's Gaborish kernel, on
+// the padded frame with edge replication, before every other stage.  The
+// 66 x 66 LDS tile (1 px halo) is filtered in place; its outer ring (tile-local
+// rows / columns -1 and 66: 268 pixels) is converted into a small LDS ring
+// first.  Samples are read at coordinates clamped to the padded frame; pixels
+// outside it stay 0 (H2).
+// ---------------------------------------------------------------------------
+constexpr float kGabK0 = 1.8012209f;
+constexpr float kGabK1 = -0.15485205f;
+constexpr float kGabK2 = -0.04545318f;
+constexpr int kRing = 2 * 68 + 2 * 66;
+__device__ __forceinline__ int ring_index(int lx, int ly) {  // (lx, ly) on the ring
+  if (ly == -1) return lx + 1;
+  if (ly == 66) return 69 + lx;
+  if (lx == -1) return 136 + ly;
+  return 202 + ly;
+}
+// RGB8 -> XYB of the ring pixels (the tile load's replication rule)
+__device__ __forceinline__ void gab_ring(const FrontArgs& a, const float* lut, float* ring, int ox,
+                                         int oy) {
+  const float cb = cbrt_det(kOpsinBias);
+  for (int i = threadIdx.x; i < kRing; i += kThreads) {
+    int lx, ly;
+    if (i < 68) {
+      lx = i - 1;
+      ly = -1;
+    } else if (i < 136) {
+      lx = i - 69;
+      ly = 66;
+    } else if (i < 202) {
+      lx = -1;
+      ly = i - 136;
+    } else {
+      lx = 66;
+      ly = i - 202;
+    }
+    const int sx = min(max(ox + lx, 0), (int)a.w - 1), sy = min(max(oy + ly, 0), (int)a.h - 1);
+    const uint8_t* q = a.rgb + (size_t)sy * a.stride + 3 * (size_t)sx;
+    float X, Y, B;
+    pixel_xyb(lut, cb, q[0], q[1], q[2], X, Y, B);
+    ring[i] = X;
+    ring[kRing + i] = Y;
+    ring[2 * kRing + i] = B;
+  }
+}
+// the unfiltered sample at tile-local (lx, ly) in [-1, 66]^2, clamped to the
+// padded frame
+__device__ __forceinline__ float gab_src(const float* P, const float* R, int lx, int ly, int ox,
+                                         int oy, int xp, int yp) {
+  lx = min(max(lx, -ox), xp - 1 - ox);
+  ly = min(max(ly, -oy), yp - 1 - oy);
+  if (lx >= 0 && lx < 66 && ly >= 0 && ly < 66) return P[lds_at(lx, ly)];
+  return R[ring_index(lx, ly)];
+}
+// In-place sweep: thread = (row half, channel, column), 396 threads; a 3 x 3
+// window in registers, one new row per step, one barrier per step before the
+// step's store (every thread has read the rows it still needs by then; the
+// first half reads row 33 up front, which the second half overwrites first).
+__device__ __forceinline__ void gab_sweep(const FrontArgs& a, float* sPix, const float* ring,
+                                          int ox, int oy) {
+  const int t = threadIdx.x;
+  const bool act = t < 396;
+  const int half = t >= 198 ? 1 : 0, c = (t - 198 * half) / 66, lx = t % 66;
+  const int y0 = 33 * half;
+  const int xp = (int)a.xp, yp = (int)a.yp;
+  float* P = sPix + c * kPlane;
+  const float* R = ring + c * kRing;
+  const bool colin = ox + lx >= 0 && ox + lx < xp;
+  float n[3], m[3], sn[3], ex[3];
+  if (act) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      n[k] = gab_src(P, R, lx + k - 1, y0 - 1, ox, oy, xp, yp);
+      m[k] = gab_src(P, R, lx + k - 1, y0, ox, oy, xp, yp);
+      ex[k] = half == 0 ? gab_src(P, R, lx + k - 1, 33, ox, oy, xp, yp) : 0.0f;
+    }
+  }
+#pragma unroll 1
+  for (int st = 0; st < 33; st++) {
+    const int ly = y0 + st;
+    float o = 0.0f;
+    if (act) {
+#pragma unroll
+      for (int k = 0; k < 3; k++)
+        sn[k] = (half == 0 && st == 32) ? ex[k] : gab_src(P, R, lx + k - 1, ly + 1, ox, oy, xp, yp);
+      const float s1 = (n[1] + sn[1]) + (m[0] + m[2]);
+      const float s2 = (n[0] + n[2]) + (sn[0] + sn[2]);
+      o = (m[1] * kGabK0 + s1 * kGabK1) + s2 * kGabK2;
+    }
+    __syncthreads();
+    if (act && colin && oy + ly >= 0 && oy + ly < yp) P[lds_at(lx, ly)] = o;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      n[k] = m[k];
+      m[k] = sn[k];
+    }
+  }
+}
+
 // chroma-from-luma factor as an int8 multiple of 1/84 (oracle cfl_quant)
 __device__ __forceinline__ int cfl_quant(float k) {
   float v = k * 84.0f;
@@ -848,6 +949,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
   }
   __syncthreads();
   load_xyb_tile(a, sLut, sPix, ox, oy);
+  if (a.gab) {  // (uniform) the ring beside the tile, then the in-place sweep
+    float* ring = sUnion + 256;  // 3 x 268 floats, before phase A's sH
+    gab_ring(a, sLut, ring, ox, oy);
+    __syncthreads();
+    gab_sweep(a, sPix, ring, ox, oy);
+  }
   __syncthreads();
   if (a.xyb_out) {
     // tile-major XYB copy for the merge stage: [tile][X, Y, B][64][64]

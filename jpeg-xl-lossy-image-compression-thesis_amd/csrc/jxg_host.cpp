@@ -835,6 +835,7 @@ struct Job {
   int max_s = 0;
   bool homog = false;
   bool ans = false;  // ANS instead of prefix codes for the AC stream
+  uint32_t lf = 0;   // frame header loop-filter code (lf_code: Gaborish / EPF)
   uint32_t nhist_ans = 0;
   uint32_t nrows = 0, nchunks = 0, nstreams = 0;
   AcArgs aa{};
@@ -1037,6 +1038,7 @@ static jxg_status stage_alloc(Ctx* c, Job& J) {
   const size_t nb = (size_t)f.bxs * f.bys;
   J.homog = (P.proposals & 3u) != 0;
   J.ans = (P.flags & JXG_FLAG_ANS) != 0;
+  J.lf = lf_code(P.flags, P.distance);
   jxg_status st = init_constants(c);
   if (st) return st;
   JXG_HIP(c->acs.ensure(nb));
@@ -1242,6 +1244,7 @@ static jxg_status stage_front(Ctx* c, Job& J) {
   fa.effort = P.effort;
   fa.proposals = P.proposals;
   fa.h1_int = (P.flags & JXG_FLAG_H1_INT_ABS) ? 1 : 0;
+  fa.gab = (P.flags & JXG_FLAG_GABORISH) ? 1 : 0;
   fa.qf_base = f.qf_base;
   fa.inv_g = f.inv_g;
   fa.G = f.G;
@@ -1549,7 +1552,7 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
         write_modular_prelude(J.preA[lg], kDcTree, 5, 3, lc);
       } else {
         J.preB[lg].put(ceil_log2(bw * bh), c->h_vcount.p[lg] - 1);  // varblock count - 1
-        write_modular_prelude(J.preB[lg], kMetaTree, 7, 4, lc);
+        write_modular_prelude(J.preB[lg], (J.lf >> 1) ? kMetaTreeEpf : kMetaTree, 7, 4, lc);
       }
     }
   }
@@ -1705,7 +1708,7 @@ static jxg_status stage_concat(Ctx* c, Job& J, bool full, std::vector<uint32_t>*
   };
   if (full) {
     BitWriter head;
-    write_headers(head, J.w, J.h);
+    write_headers(head, J.w, J.h, J.lf);
     write_toc(head, sizes);
     emit_piece(add_chunk(head));
   }
@@ -1850,7 +1853,7 @@ static jxg_status stage_concat_split(Ctx* c, Job& J, uint8_t** host_out, size_t*
     dst += p.nbits;
   };
   BitWriter head;
-  write_headers(head, J.w, J.h);
+  write_headers(head, J.w, J.h, J.lf);
   write_toc(head, sizes);
   emit_piece(add_chunk(head));
   for (auto& sec : sections) {
@@ -2236,7 +2239,7 @@ static jxg_status shard_finish(Ctx* c, Job& J, size_t* payload_bytes, bool sync 
   hw.assign(7 + 2 * ids.size(), 0);
   hw[0] = kPayloadMagic;
   hw[1] = J.presets ? 2 : 1;
-  hw[2] = J.plan.rank;
+  hw[2] = J.plan.rank | J.lf << 16;  // the rank, the frame's loop-filter code
   hw[3] = J.plan.world;
   hw[4] = J.w;
   hw[5] = J.h;
@@ -2649,7 +2652,7 @@ static jxg_status build_hf_presets(const std::vector<std::vector<uint32_t>>& hea
 static jxg_status parse_payload_heads(const std::vector<std::vector<uint32_t>>& heads,
                                       const std::vector<size_t>& psizes, uint32_t* w,
                                       uint32_t* h, std::vector<SectionRef>& secs,
-                                      std::vector<uint8_t>& hf) {
+                                      std::vector<uint8_t>& hf, uint32_t* lf) {
   const uint32_t n = (uint32_t)heads.size();
   secs.clear();
   hf.clear();
@@ -2662,7 +2665,8 @@ static jxg_status parse_payload_heads(const std::vector<std::vector<uint32_t>>& 
     if (i == 0) {
       *w = hw[4];
       *h = hw[5];
-    } else if (hw[4] != *w || hw[5] != *h) {
+      *lf = hw[2] >> 16;  // loop-filter code (shard_finish)
+    } else if (hw[4] != *w || hw[5] != *h || (hw[2] >> 16) != *lf) {
       return JXG_ERR_INVALID_ARG;
     }
     const size_t hwords = head_words(hw.data(), hw.size());
@@ -2681,7 +2685,7 @@ static jxg_status parse_payload_heads(const std::vector<std::vector<uint32_t>>& 
       off += sz;
     }
   }
-  if (*w == 0 || *h == 0) return JXG_ERR_INVALID_ARG;
+  if (*w == 0 || *h == 0 || *lf > 7) return JXG_ERR_INVALID_ARG;
   const Frame f = make_frame(*w, *h, 1.0f);
   if (secs.size() != 2 + f.nlf + f.ngroups) return JXG_ERR_INVALID_ARG;
   if (heads[0][1] == 2) {  // per-rank presets: HfGlobal from the heads
@@ -2743,12 +2747,13 @@ static jxg_status shard_assemble_device(Ctx* c, const uint8_t* d_base, const siz
   uint32_t w = 0, h = 0;
   std::vector<SectionRef> secs;
   std::vector<uint8_t> hf;
-  jxg_status st = parse_payload_heads(heads, ps, &w, &h, secs, hf);
+  uint32_t lf = 0;
+  jxg_status st = parse_payload_heads(heads, ps, &w, &h, secs, hf, &lf);
   if (st) return st;
   std::vector<uint32_t> sizes(secs.size());
   for (size_t i = 0; i < secs.size(); i++) sizes[i] = secs[i].size;
   BitWriter head;
-  write_headers(head, w, h);
+  write_headers(head, w, h, lf);
   write_toc(head, sizes);
   std::vector<uint32_t> chunk_words = head.words32();
   // a generated HfGlobal (per-rank presets) follows the headers in the chunk arena
@@ -2820,17 +2825,18 @@ static jxg_status shard_write_host(Ctx* c, const uint32_t* const* heads_in, cons
     for (uint32_t k = 0; k < heads[i][6]; k++) body += heads[i][8 + 2 * k];
     ps[i] = words[i] * 4 + body;
   }
-  const uint32_t me = c->payload_head[2];
+  const uint32_t me = c->payload_head[2] & 0xFFFFu;
   if (me >= n || heads[me] != c->payload_head) return JXG_ERR_INVALID_ARG;
   uint32_t w = 0, h = 0;
   std::vector<SectionRef> secs;
   std::vector<uint8_t> hf;
-  jxg_status st = parse_payload_heads(heads, ps, &w, &h, secs, hf);
+  uint32_t lf = 0;
+  jxg_status st = parse_payload_heads(heads, ps, &w, &h, secs, hf, &lf);
   if (st) return st;
   std::vector<uint32_t> sec_size(secs.size());
   for (size_t i = 0; i < secs.size(); i++) sec_size[i] = secs[i].size;
   BitWriter head;
-  write_headers(head, w, h);
+  write_headers(head, w, h, lf);
   write_toc(head, sec_size);
   const std::vector<uint8_t> hb = head.bytes();
   std::vector<uint64_t> out_off(secs.size());
@@ -2885,7 +2891,8 @@ static jxg_status shard_assemble(const uint8_t* const* payloads, const size_t* s
   uint32_t w = 0, h = 0;
   std::vector<SectionRef> secs;
   std::vector<uint8_t> hf;
-  jxg_status st = parse_payload_heads(heads, ps, &w, &h, secs, hf);
+  uint32_t lf = 0;
+  jxg_status st = parse_payload_heads(heads, ps, &w, &h, secs, hf, &lf);
   if (st) return st;
   std::vector<uint32_t> sec_size(secs.size());
   size_t total = 0;
@@ -2894,7 +2901,7 @@ static jxg_status shard_assemble(const uint8_t* const* payloads, const size_t* s
     total += secs[i].size;
   }
   BitWriter head;
-  write_headers(head, w, h);
+  write_headers(head, w, h, lf);
   write_toc(head, sec_size);
   const std::vector<uint8_t> hb = head.bytes();
   uint8_t* o = out_alloc_heap(hb.size() + total);

@@ -17,6 +17,7 @@ struct FrontArgs {
   int effort;
   uint32_t proposals;
   int h1_int;
+  int gab;        // inverse Gaborish on the XYB tile before every other stage
   float qf_base, inv_g;
   uint32_t G;
   float dc_mul[3], dc_step[3];

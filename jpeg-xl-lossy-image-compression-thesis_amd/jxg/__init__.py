@@ -34,6 +34,8 @@ FLAG_H1_INT_ABS = 1
 FLAG_KEEP_MAPS = 2
 FLAG_ANS = 4
 FLAG_FORCE_ONE_STREAM = 8  # testing: the split assembly's one-stream fallback (same bytes)
+FLAG_GABORISH = 16  # encoder inverse Gaborish + the decoder's Gaborish (cjxl --gaborish=1)
+FLAG_EPF = 32  # the decoder's edge-preserving filter, iterations by distance (cjxl --epf=-1)
 
 
 class JxgError(RuntimeError):

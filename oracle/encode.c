@@ -105,6 +105,7 @@ static void put_histograms(jxo_bw* w, int nctx, const uint8_t* ctxmap, int nhist
 /* --------------------- modular streams (LF group) --------------------- */
 typedef struct {
   int prop, splitval, lchild, rchild, predictor, leaf; /* prop<0 => leaf */
+  int offset;                                         /* leaf: value offset */
 } tnode;
 /* DC tree: split on channel -> 3 leaves (Y, B, X), clamped gradient */
 static const tnode kDcTree[5] = {{0, 0, 1, 2, 0, -1},  {0, 1, 3, 4, 0, -1},
@@ -124,7 +125,7 @@ static void put_tree(jxo_bw* w, const tnode* t, int n) {
     if (t[i].prop < 0) {
       tv[nt][0] = 1; tv[nt++][1] = 0;
       tv[nt][0] = 2; tv[nt++][1] = (uint32_t)t[i].predictor;
-      tv[nt][0] = 3; tv[nt++][1] = 0;
+      tv[nt][0] = 3; tv[nt++][1] = pack_signed(t[i].offset);
       tv[nt][0] = 4; tv[nt++][1] = 0;
       tv[nt][0] = 5; tv[nt++][1] = 0;
     } else {
@@ -194,7 +195,7 @@ static void put_modular(jxo_bw* w, const tnode* t, int nnodes, int nleaves,
         const int node = tree_leaf(t, c, y);
         const int leaf = t[node].leaf;
         for (int x = 0; x < ch[c].w; x++) {
-          int32_t r = ch[c].data[y * ch[c].w + x] -
+          int32_t r = ch[c].data[y * ch[c].w + x] - t[node].offset -
                       predict(t[node].predictor, ch[c].data, ch[c].w, x, y);
           uint32_t u = pack_signed(r);
           if (pass == 0) {
@@ -211,7 +212,7 @@ static void put_modular(jxo_bw* w, const tnode* t, int nnodes, int nleaves,
 }
 
 static void lf_group_section(const jxo_frame* f, const jxo_result* r, int lg,
-                             jxo_bw* w) {
+                             uint32_t filters, jxo_bw* w) {
   const uint32_t lgx = lg % f->lfxs, lgy = lg / f->lfxs;
   const uint32_t bx0 = lgx * 256, by0 = lgy * 256;
   const uint32_t bw = (f->bxs - bx0) < 256 ? f->bxs - bx0 : 256;
@@ -264,7 +265,15 @@ static void lf_group_section(const jxo_frame* f, const jxo_result* r, int lg,
   ch[3].w = (int)bw;
   ch[3].h = (int)bh;
   ch[3].data = (int32_t*)calloc((size_t)bw * bh, sizeof(int32_t));
-  put_modular(w, kMetaTree, 7, 4, ch, 4);
+  /* EPF sharpness per block: a constant [ext: libjxl's encoder default,
+   * unpinned], carried by the EPF leaf's offset (every residual 0) */
+  tnode meta[7];
+  memcpy(meta, kMetaTree, sizeof(meta));
+  if (filters & JXO_FILTER_EPF) {
+    meta[3].offset = JXO_EPF_SHARPNESS;
+    for (size_t i = 0; i < (size_t)bw * bh; i++) ch[3].data[i] = JXO_EPF_SHARPNESS;
+  }
+  put_modular(w, meta, 7, 4, ch, 4);
   for (int i = 0; i < 4; i++) free(ch[i].data);
 }
 
@@ -353,7 +362,7 @@ static void put_size(jxo_bw* w, uint32_t v) { /* U32(BitsOffset(9,1),13,18,30) *
   else put_u32_sel(w, 3, 30, m);
 }
 
-static void put_headers(jxo_bw* w, uint32_t xs, uint32_t ys) {
+static void put_headers(jxo_bw* w, uint32_t xs, uint32_t ys, uint32_t lf) {
   jxo_bw_put(w, 8, 0xFF);
   jxo_bw_put(w, 8, 0x0A);
   /* SizeHeader */
@@ -383,10 +392,22 @@ static void put_headers(jxo_bw* w, uint32_t xs, uint32_t ys) {
   jxo_bw_put(w, 2, 0);   /* blending mode replace */
   jxo_bw_put(w, 1, 1);   /* is_last */
   jxo_bw_put(w, 2, 0);   /* name length 0 */
-  jxo_bw_put(w, 1, 0);   /* loop_filter.all_default */
-  jxo_bw_put(w, 1, 0);   /*   gab */
-  jxo_bw_put(w, 2, 0);   /*   epf_iters */
-  jxo_bw_put(w, 2, 0);   /*   extensions */
+  /* LoopFilter [ext loop_filter.h]: all_default = gab on + one EPF iteration */
+  const uint32_t gab = lf & 1u, epf = (lf >> 1) & 3u;
+  if (gab && epf == 1) {
+    jxo_bw_put(w, 1, 1); /* loop_filter.all_default */
+  } else {
+    jxo_bw_put(w, 1, 0); /* loop_filter.all_default */
+    jxo_bw_put(w, 1, gab);
+    if (gab) jxo_bw_put(w, 1, 0); /* gab_custom */
+    jxo_bw_put(w, 2, epf); /* epf_iters */
+    if (epf) {
+      jxo_bw_put(w, 1, 0); /* epf_sharp_custom (VarDCT) */
+      jxo_bw_put(w, 1, 0); /* epf_weight_custom */
+      jxo_bw_put(w, 1, 0); /* epf_sigma_custom */
+    }
+    jxo_bw_put(w, 2, 0); /* extensions */
+  }
   jxo_bw_put(w, 2, 0);   /* extensions */
 }
 
@@ -404,11 +425,13 @@ int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h, size_t row_strid
   if (!rgb || w == 0 || h == 0 || w > (1u << 18) || h > (1u << 18)) return -1;
   if (!(p->distance > 0.0f) || p->distance > 25.0f) return -2;
   if (p->coder != 0 && p->coder != 1) return -3;
+  if (p->filters & ~(JXO_FILTER_GAB | JXO_FILTER_EPF)) return -4;
   jxo_frame f;
   jxo_frame_init(&f, w, h, p);
   const size_t plane = (size_t)f.xp * f.yp, nb = (size_t)f.bxs * f.bys;
   float* xyb = (float*)malloc(sizeof(float) * plane * 3);
   jxo_srgb8_to_xyb(rgb, w, h, row_stride, f.xp, f.yp, xyb);
+  if (p->filters & JXO_FILTER_GAB) jxo_gab_inverse(xyb, f.xp, f.yp);
   out->xsize = w;
   out->ysize = h;
   out->bxs = f.bxs;
@@ -603,7 +626,7 @@ int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h, size_t row_strid
     jxo_bw_put(s, 1, 0); /* GlobalModular: no global tree; 0 channels */
   }
 #pragma omp parallel for schedule(dynamic)
-  for (uint32_t lg = 0; lg < f.nlf; lg++) lf_group_section(&f, out, (int)lg, &sec[1 + lg]);
+  for (uint32_t lg = 0; lg < f.nlf; lg++) lf_group_section(&f, out, (int)lg, p->filters, &sec[1 + lg]);
   {
     jxo_bw* s = &sec[1 + f.nlf];
     jxo_bw_put(s, 1, 1); /* DequantMatrices all_default */
@@ -659,7 +682,7 @@ int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h, size_t row_strid
   /* ---- assemble ---- */
   jxo_bw o;
   jxo_bw_init(&o);
-  put_headers(&o, w, h);
+  put_headers(&o, w, h, jxo_lf_code(p->filters, p->distance));
   jxo_bw_put(&o, 1, 0); /* TOC not permuted */
   jxo_bw_pad(&o);
   if (nsec == 1) {

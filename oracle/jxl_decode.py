@@ -962,21 +962,25 @@ def decode(data: bytes, want_pixels: bool = True, groups=None) -> Decoded:
         raise JxlError("is_last")
     nlen = br.u32(("v", 0), ("b", 4, 0), ("b", 5, 16), ("b", 10, 48))
     br.skip(8 * nlen)
+    # LoopFilter [ext loop_filter.h]: all_default = Gaborish + one EPF iteration
     if br.bool():
         gab, epf = True, 1
     else:
         gab = br.bool()
-        if gab:
-            raise JxlError("gaborish not produced")
+        if gab and br.bool():
+            raise JxlError("custom Gaborish weights not produced")
         epf = br.read(2)
         if epf:
-            raise JxlError("EPF not produced")
+            if br.bool():
+                raise JxlError("custom EPF sharpness LUT not produced")
+            if br.bool():
+                raise JxlError("custom EPF channel scales not produced")
+            if br.bool():
+                raise JxlError("custom EPF sigmas not produced")
         if br.u64():
             raise JxlError("loop filter extensions")
     if br.u64():
         raise JxlError("frame extensions")
-    if gab or epf:
-        raise JxlError("default loop filters not produced")
     bxs, bys = (xs + 7) // 8, (ys + 7) // 8
     gxs, gys = (xs + 255) // 256, (ys + 255) // 256
     ng = gxs * gys
@@ -1006,6 +1010,8 @@ def decode(data: bytes, want_pixels: bool = True, groups=None) -> Decoded:
     shared = BitReader(data, base * 8, (base + sizes[0]) * 8) if nent == 1 else None
     d = Decoded()
     d.xsize, d.ysize, d.bxs, d.bys = xs, ys, bxs, bys
+    d.gab, d.epf_iters = bool(gab), int(epf)
+    d.sharpness = np.zeros((bys, bxs), dtype=np.int32)
     d.section_sizes = sizes
     d.section_offsets = offs
     # LfGlobal
@@ -1050,6 +1056,10 @@ def decode(data: bytes, want_pixels: bool = True, groups=None) -> Decoded:
             if m.min() < -128 or m.max() > 127:
                 raise JxlError("CfL factor out of int8 range")
             d.cmap[i, by0 // 8:by0 // 8 + chh, bx0 // 8:bx0 // 8 + cw] = m
+        sh = np.array(meta[3], dtype=np.int32).reshape(bh, bw)
+        if sh.min() < 0 or sh.max() > 7:
+            raise JxlError("EPF sharpness out of range")
+        d.sharpness[by0:by0 + bh, bx0:bx0 + bw] = sh
         k = 0
         covered = np.zeros((bh, bw), dtype=bool)
         for y in range(bh):
@@ -1208,8 +1218,98 @@ def reconstruct(d: Decoded) -> np.ndarray:
                 co = co.copy()
                 co[0] = dcv
                 arr[by * 8:by * 8 + 8, bx * 8:bx * 8 + 8] = inverse_transform(t, co)
+    if getattr(d, "gab", False):
+        X, Y, B = gaborish(X), gaborish(Y), gaborish(B)
+    if getattr(d, "epf_iters", 0):
+        X, Y, B = epf(X, Y, B, d)
     rgb = xyb_to_srgb8(X, Y, B)
     return rgb[:d.ysize, :d.xsize]
+
+
+# ----------------------------------------------------------------------------
+# restoration filters [ext: libjxl's decoder, restated from the format's
+# description; constants are the LoopFilter defaults; parity with libjxl/djxl
+# unpinned].  Both run on the block-padded XYB planes, mirrored at their edges
+# (the encoder's inverse Gaborish, oracle/xyb.c jxo_gab_inverse, replicates the
+# same edges).
+# ----------------------------------------------------------------------------
+GAB_W1, GAB_W2 = 0.115169525, 0.061248592
+EPF_CHANNEL_SCALE = (40.0, 5.0, 3.5)
+EPF_QUANT_MUL = 0.46
+EPF_SHARP_LUT = tuple(i / 7.0 for i in range(8))
+EPF_PASS0_SIGMA_SCALE = 0.9
+EPF_PASS2_SIGMA_SCALE = 6.5
+EPF_BORDER_SAD_MUL = 2.0 / 3.0
+EPF_INV_SIGMA_NUM = -1.1715728752538099
+EPF_MIN_SIGMA = -3.90625  # inverse sigma below this: the block is not filtered
+
+
+def gaborish(P: np.ndarray) -> np.ndarray:
+    """3x3 symmetric smoothing (1 centre, w1 edges, w2 corners), normalised."""
+    Q = np.pad(P, 1, mode="symmetric")
+    s1 = (Q[:-2, 1:-1] + Q[2:, 1:-1]) + (Q[1:-1, :-2] + Q[1:-1, 2:])
+    s2 = (Q[:-2, :-2] + Q[:-2, 2:]) + (Q[2:, :-2] + Q[2:, 2:])
+    return (P + GAB_W1 * s1 + GAB_W2 * s2) / (1.0 + 4.0 * GAB_W1 + 4.0 * GAB_W2)
+
+
+def epf_inv_sigma(d) -> np.ndarray:
+    """Per-block inverse sigma (negative; -inf-like when not filtered):
+    sigma = quant_mul * sharp_lut[s] / (scale * qf * kInvSigmaNum)."""
+    scale = d.global_scale / 65536.0
+    lut = np.array(EPF_SHARP_LUT)[d.sharpness]
+    sigma = EPF_QUANT_MUL / (scale * d.qf.astype(np.float64) * EPF_INV_SIGMA_NUM) * lut
+    sigma = np.minimum(-1e-4, sigma)
+    return 1.0 / sigma
+
+
+def _epf_step(planes, inv_px, neigh, plus_sad, pad=3):
+    Q = [np.pad(p, pad, mode="symmetric") for p in planes]
+    H, W = planes[0].shape
+
+    def sh(q, dy, dx):
+        return q[pad + dy:pad + dy + H, pad + dx:pad + dx + W]
+
+    sad_pat = ((0, 0), (-1, 0), (1, 0), (0, -1), (0, 1)) if plus_sad else ((0, 0),)
+    wsum = np.ones((H, W))
+    acc = [p.copy() for p in planes]
+    for dy, dx in neigh:
+        sad = np.zeros((H, W))
+        for c in range(3):
+            a = np.zeros((H, W))
+            for oy, ox in sad_pat:
+                a += np.abs(sh(Q[c], dy + oy, dx + ox) - sh(Q[c], oy, ox))
+            sad += EPF_CHANNEL_SCALE[c] * a
+        w = np.maximum(0.0, 1.0 + sad * inv_px)
+        wsum += w
+        for c in range(3):
+            acc[c] += w * sh(Q[c], dy, dx)
+    return [a / wsum for a in acc]
+
+
+def epf(X, Y, B, d):
+    """Edge-preserving filter, d.epf_iters passes (3: pass 0 over 12
+    neighbours; >= 1: pass 1 over 4; 2-3: pass 2 with one-pixel SADs); blocks
+    whose inverse sigma is below EPF_MIN_SIGMA keep their input."""
+    inv_b = epf_inv_sigma(d)
+    H, W = X.shape
+    inv = np.repeat(np.repeat(inv_b, 8, axis=0), 8, axis=1)[:H, :W]
+    skip = inv < EPF_MIN_SIGMA
+    yy, xx = np.arange(H) % 8, np.arange(W) % 8
+    border = ((yy == 0) | (yy == 7))[:, None] | ((xx == 0) | (xx == 7))[None, :]
+    sad_mul = np.where(border, EPF_BORDER_SAD_MUL, 1.0)
+    plus = ((-1, 0), (0, -1), (0, 1), (1, 0))
+    steps = []
+    if d.epf_iters >= 3:
+        steps.append((EPF_PASS0_SIGMA_SCALE, plus + ((-1, -1), (-1, 1), (1, -1), (1, 1),
+                                                     (-2, 0), (0, -2), (0, 2), (2, 0)), True))
+    steps.append((1.0, plus, True))
+    if d.epf_iters >= 2:
+        steps.append((EPF_PASS2_SIGMA_SCALE, plus, False))
+    planes = [X, Y, B]
+    for scale, neigh, plus_sad in steps:
+        out = _epf_step(planes, inv * sad_mul * scale, neigh, plus_sad)
+        planes = [np.where(skip, p, o) for p, o in zip(planes, out)]
+    return planes
 
 
 def mse_psnr(orig: np.ndarray, comp: np.ndarray):

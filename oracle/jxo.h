@@ -63,7 +63,21 @@ typedef struct {
   int effort;
   uint32_t proposals; /* bit0 = P (homogeneity-partitioning), bit1 = F */
   int coder;          /* 0 = prefix codes, 1 = ANS */
+  uint32_t filters;   /* JXO_FILTER_*: restoration filters the frame signals */
 } jxo_params;
+
+/* restoration filters [ext: libjxl LoopFilter, cjxl
+ * --gaborish / --epf]: GAB = the encoder's inverse Gaborish on XYB and the
+ * decoder's 3x3 Gaborish; EPF = the decoder's edge-preserving filter,
+ * jxo_epf_iters(distance) iterations, constant sharpness JXO_EPF_SHARPNESS */
+#define JXO_FILTER_GAB 1u
+#define JXO_FILTER_EPF 2u
+#define JXO_EPF_SHARPNESS 4
+int jxo_epf_iters(float distance);
+/* loop-filter code of the frame header: bit 0 gab, bits 1-2 epf_iters */
+uint32_t jxo_lf_code(uint32_t filters, float distance);
+/* in place on a [3][yp][xp] XYB frame (edge replication at its borders) */
+void jxo_gab_inverse(float* xyb, uint32_t xp, uint32_t yp);
 
 typedef struct {
   uint32_t xsize, ysize;   /* image */

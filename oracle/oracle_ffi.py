@@ -26,7 +26,11 @@ def build(force: bool = False):
 
 class _Params(ctypes.Structure):
     _fields_ = [("distance", ctypes.c_float), ("effort", ctypes.c_int),
-                ("proposals", ctypes.c_uint32), ("coder", ctypes.c_int)]
+                ("proposals", ctypes.c_uint32), ("coder", ctypes.c_int),
+                ("filters", ctypes.c_uint32)]
+
+FILTER_GAB = 1  # jxo.h JXO_FILTER_GAB
+FILTER_EPF = 2  # jxo.h JXO_FILTER_EPF
 
 
 class _Result(ctypes.Structure):
@@ -95,10 +99,11 @@ class OracleResult:
     pass
 
 
-def encode(rgb: np.ndarray, distance=1.0, effort=7, proposals=0, coder=0) -> OracleResult:
+def encode(rgb: np.ndarray, distance=1.0, effort=7, proposals=0, coder=0,
+           filters=0) -> OracleResult:
     rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
     h, w, _ = rgb.shape
-    p = _Params(distance, effort, proposals, coder)
+    p = _Params(distance, effort, proposals, coder, filters)
     r = _Result()
     st = lib().jxo_encode_rgb8(rgb.ctypes.data, w, h, w * 3, ctypes.byref(p), ctypes.byref(r))
     if st != 0:

@@ -7,6 +7,7 @@
  * deterministic in-house cube root).
  */
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "jxo_internal.h"
@@ -71,4 +72,58 @@ void jxo_srgb8_to_xyb(const uint8_t* rgb, uint32_t w, uint32_t h,
                     &xyb[2 * plane + o]);
     }
   }
+}
+
+/* ---------------- restoration filters ----------------
+ * [ext] libjxl enables Gaborish and the edge-preserving filter for VarDCT at
+ * cjxl's defaults (LoopFilter gab = true, epf_iters from the distance).  The
+ * decoder's Gaborish is the 3x3 symmetric kernel (1, w1 edge, w2 corner) /
+ * (1 + 4 w1 + 4 w2) with the default weights w1 = 0.115169525, w2 =
+ * 0.061248592 (decoder: oracle/jxl_decode.py gaborish).  The encoder applies an
+ * approximate inverse to its XYB image before every other stage; libjxl's own
+ * inverse is a tuned 5x5 [ext, not restated]: this one is the 3x3 symmetric
+ * least-squares inverse of the decoder kernel over the frequency square with
+ * unit DC gain (K0 + 4 K1 + 4 K2 = 1; residual 5.8 % rms), so the GPU tile
+ * needs a one-pixel ring only.  Parity with libjxl unpinned. */
+#ifndef JXO_GAB_K0
+#define JXO_GAB_K0 1.8012209f
+#define JXO_GAB_K1 -0.15485205f
+#define JXO_GAB_K2 -0.04545318f
+#endif
+
+int jxo_epf_iters(float distance) {
+  /* [ext] cjxl --epf=-1 picks the iterations from the distance; restated:
+   * 1 below d 1.5, 2 below d 4, else 3 (unpinned) */
+  return distance < 1.5f ? 1 : (distance < 4.0f ? 2 : 3);
+}
+
+uint32_t jxo_lf_code(uint32_t filters, float distance) {
+  uint32_t c = (filters & JXO_FILTER_GAB) ? 1u : 0u;
+  if (filters & JXO_FILTER_EPF) c |= (uint32_t)jxo_epf_iters(distance) << 1;
+  return c;
+}
+
+/* out = (C K0 + ((N + S) + (W + E)) K1) + ((NW + NE) + (SW + SE)) K2, float,
+ * no contraction (the GPU front kernel's gab_sweep has the same order);
+ * neighbours outside the padded frame replicate its edge */
+void jxo_gab_inverse(float* xyb, uint32_t xp, uint32_t yp) {
+  const size_t plane = (size_t)xp * yp;
+  float* src = (float*)malloc(sizeof(float) * plane);
+  for (int c = 0; c < 3; c++) {
+    float* p = xyb + c * plane;
+    memcpy(src, p, sizeof(float) * plane);
+#pragma omp parallel for schedule(static)
+    for (uint32_t y = 0; y < yp; y++) {
+      const float* rn = src + (size_t)(y > 0 ? y - 1 : 0) * xp;
+      const float* rc = src + (size_t)y * xp;
+      const float* rs = src + (size_t)(y + 1 < yp ? y + 1 : y) * xp;
+      for (uint32_t x = 0; x < xp; x++) {
+        const uint32_t xw = x > 0 ? x - 1 : 0, xe = x + 1 < xp ? x + 1 : x;
+        const float s1 = (rn[x] + rs[x]) + (rc[xw] + rc[xe]);
+        const float s2 = (rn[xw] + rn[xe]) + (rs[xw] + rs[xe]);
+        p[(size_t)y * xp + x] = (rc[x] * JXO_GAB_K0 + s1 * JXO_GAB_K1) + s2 * JXO_GAB_K2;
+      }
+    }
+  }
+  free(src);
 }
