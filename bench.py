@@ -356,9 +356,10 @@ def main():
                 # codestream as soon as it is done (more than the library's
                 # pipeline depth pending => the oldest is complete)
                 got = 0
+                hold = max(16, e.pipeline_depth(w, h))
                 for k in ks:
                     e.submit_device(d_imgs[k % nd].data_ptr(), w, h)
-                    while e.pending() > 16:
+                    while e.pending() > hold:
                         took(e, got, e.receive(copy=False))
                         got += 1
                 while e.pending():

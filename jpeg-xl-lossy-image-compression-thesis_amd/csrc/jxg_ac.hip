@@ -649,6 +649,12 @@ __global__ __launch_bounds__(kAnsWaves * 64) void ans_encode_multi_kernel(const 
   ans_chain(a, m & 0xFFFFFu);
 }
 
+__global__ __launch_bounds__(kAnsWaves * 64) void ans_encode_batch_kernel(AnsBatch b) {
+  uint32_t i = 0;
+  while (i + 1 < b.nf && blockIdx.x >= b.wg0[i + 1]) i++;
+  ans_chain(b.f[i], blockIdx.x - b.wg0[i]);
+}
+
 // bit placement: the 32-bit state, then every record's bits, in order; a
 // contiguous record range per wave, coalesced reads, wave scans of the
 // lengths (as ac_emit)
@@ -724,6 +730,10 @@ uint32_t ans_chain_wgs(uint32_t ngroups) { return (ngroups + kAnsWaves - 1) / kA
 void launch_ans_multi(const AnsArgs* d_frames, const uint32_t* d_wg, uint32_t nwg, hipStream_t s) {
   if (nwg)
     hipLaunchKernelGGL(ans_encode_multi_kernel, dim3(nwg), dim3(kAnsWaves * 64), 0, s, d_frames, d_wg);
+}
+void launch_ans_batch(const AnsBatch& b, hipStream_t s) {
+  if (b.nf && b.wg0[b.nf])
+    hipLaunchKernelGGL(ans_encode_batch_kernel, dim3(b.wg0[b.nf]), dim3(kAnsWaves * 64), 0, s, b);
 }
 void launch_ans_emit(const AnsArgs& a, hipStream_t s) {
   if (a.n) hipLaunchKernelGGL(ans_emit_kernel, dim3(a.n), dim3(kAcThreads), 0, s, a);

@@ -485,6 +485,10 @@ struct CtxDeleter {
 struct Ctx {
   jxg_params params{};
   std::vector<std::unique_ptr<Ctx, CtxDeleter>> lanes;
+  // lane batches (pipe_submit, small frames): D physical lanes x K slots, the
+  // slots of a lane share its leader's stream (blanes_k = K they were built for)
+  std::vector<std::unique_ptr<Ctx, CtxDeleter>> blanes;
+  uint32_t blanes_k = 0;
   PinBuf<uint8_t> h_stage;  // pinned staging of one host frame (batch lanes)
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;  // AC-block concat + D2H (stage_concat_split)
@@ -564,6 +568,15 @@ struct Ctx {
   // batcher instead of this context's stream (ev_up: codes uploaded)
   struct ChainBatcher* batcher = nullptr;
   hipEvent_t ev_up = nullptr;
+  // lane batches (pipe_submit, small frames): this slot's chain is launched
+  // with the other slots of its physical lane; `stream` may be the lane
+  // leader's (stream_borrowed: not destroyed here); completion (concat + D2H)
+  // runs on the pipeline's assembly stream
+  bool defer_chain = false;
+  bool stream_borrowed = false;
+  hipStream_t asm_stream = nullptr;
+  DevBuf<uint8_t> d_cdesc;  // leader: chain descriptors per slot [AnsArgs K][wg map]
+  PinBuf<uint8_t> h_cdesc;
   std::unique_ptr<struct Job> job;  // sharded encode in flight (begin -> end)
   std::unique_ptr<struct Pipe> pipe;  // streaming encode (jxg_submit_* / jxg_receive)
   std::unique_ptr<struct SStream> ss; // streaming shards over a shared region (jxg_shard_stream_*)
@@ -822,6 +835,9 @@ static void build_rows(const Frame& f, const Plan& P, std::vector<LfRow>& rows,
 static float elapsed(hipEvent_t a, hipEvent_t b) {
   float ms = 0.0f;
   (void)hipEventElapsedTime(&ms, a, b);
+#ifdef JXG_PIPE_LEAN
+  (void)hipGetLastError();  // (the unrecorded markers' error)
+#endif
   return ms;
 }
 
@@ -860,6 +876,11 @@ struct Job {
   // chain batcher: set once this frame's chains, bit placement and group bit
   // counts are enqueued (then ev[7] of its context marks them done)
   std::shared_future<jxg_status> chain;
+  // lane batches (small frames, pipe_submit): stage_emit leaves the rANS
+  // chain to the lane's batch launch (lane_batch_launch), which then places
+  // the bits and downloads the bit counts
+  AnsArgs na{};
+  bool chain_deferred = false, chain_launched = false;
 };
 
 // ---------------------------------------------------------------------------
@@ -1007,6 +1028,11 @@ static std::shared_future<jxg_status> chain_submit(ChainBatcher* B, Ctx* lane, c
 }
 // the emission of J on c is done and its bit counts are on the host
 static jxg_status wait_emission(Ctx* c, Job& J) {
+  if (J.chain_deferred) {  // a lane-batch slot: its stream carries other slots' work
+    if (!J.chain_launched) return JXG_ERR_INTERNAL;
+    JXG_HIP(hipEventSynchronize(c->ev[3]));
+    return JXG_OK;
+  }
   if (J.chain.valid()) {
     const jxg_status st = J.chain.get();
     J.chain = std::shared_future<jxg_status>();
@@ -1018,6 +1044,7 @@ static jxg_status wait_emission(Ctx* c, Job& J) {
 }
 // non-blocking: 1 done, 0 not yet, < 0 error
 static int emission_done(Ctx* c, Job& J) {
+  if (J.chain_deferred && !J.chain_launched) return 0;
   if (J.chain.valid()) {
     if (J.chain.wait_for(std::chrono::seconds(0)) != std::future_status::ready) return 0;
     if (J.chain.get()) return -1;
@@ -1269,7 +1296,9 @@ static jxg_status stage_front(Ctx* c, Job& J) {
   else if (J.plan.world == 1)
     launch_front(fa, f.tiles_x, f.tiles_y, s);
   JXG_HIP(hipGetLastError());
+#ifndef JXG_PIPE_LEAN  // (experiment: no timing markers)
   JXG_HIP(hipEventRecord(c->ev[5], s));  // end of the front kernel alone
+#endif
   if (J.max_s) {
     MergeArgs ma{};
     ma.xyb = c->xyb_tiles.p;
@@ -1607,7 +1636,11 @@ static jxg_status stage_emit(Ctx* c, Job& J, bool sync = true) {
     na.n = J.plan.ng();
     na.glist = J.aa.glist;
     na.order = c->ans_order.p;
-    if (c->batcher) {  // the pipeline's chain batcher (group bit counts: its D2H)
+    if (c->defer_chain) {  // the lane batch launches it (lane_batch_launch)
+      J.na = na;
+      J.chain_deferred = true;
+      J.chain_launched = false;
+    } else if (c->batcher) {  // the pipeline's chain batcher (group bit counts: its D2H)
       if (!c->ev_up) JXG_HIP(hipEventCreateWithFlags(&c->ev_up, hipEventDisableTiming));
       JXG_HIP(hipEventRecord(c->ev_up, s));
       J.chain = chain_submit(c->batcher, c, na, f.ngroups);
@@ -1621,6 +1654,7 @@ static jxg_status stage_emit(Ctx* c, Job& J, bool sync = true) {
   launch_lf_scan(J.la, J.nstreams, s);
   if (J.nchunks) launch_lf_emit(J.la, J.nchunks, s);
   JXG_HIP(hipGetLastError());
+  if (J.chain_deferred) return JXG_OK;  // bit counts and ev[3] after the batch's chains
   if (J.ans && !J.chain.valid()) {  // [gbits | stream_bits]: one copy
     JXG_HIP(hipMemcpyAsync(c->h_bits.p, c->bits.p, ((size_t)f.ngroups + J.nstreams) * 4,
                            hipMemcpyDeviceToHost, s));
@@ -1647,7 +1681,7 @@ struct Piece {
 static jxg_status stage_concat(Ctx* c, Job& J, bool full, std::vector<uint32_t>* section_ids,
                                std::vector<uint32_t>* section_bytes, uint8_t** host_out,
                                size_t* out_bytes) {
-  hipStream_t s = c->stream;
+  hipStream_t s = c->asm_stream ? c->asm_stream : c->stream;  // (lane batches: assembly stream)
   const Frame& f = J.f;
   std::vector<std::vector<Piece>> sections;
   std::vector<uint32_t> ids;
@@ -1744,7 +1778,9 @@ static jxg_status stage_concat(Ctx* c, Job& J, bool full, std::vector<uint32_t>*
     out_release(ho);
     return JXG_ERR_HIP;
   }
+#ifndef JXG_PIPE_LEAN
   JXG_HIP(hipEventRecord(c->ev[4], s));
+#endif
   if (host_out) *host_out = ho;
   *out_bytes = nbytes;
   if (section_ids) *section_ids = ids;
@@ -1927,9 +1963,13 @@ static jxg_status enc_launch(Ctx* c, Job& J, const uint8_t* d_rgb, uint32_t w, u
   jxg_status st = stage_alloc(c, J);
   if (st) return st;
   J.presets = J.ans && world > 1;
+#ifndef JXG_PIPE_LEAN
   JXG_HIP(hipEventRecord(c->ev[0], s));
+#endif
   if ((st = stage_front(c, J))) return st;
+#ifndef JXG_PIPE_LEAN
   JXG_HIP(hipEventRecord(c->ev[1], s));
+#endif
   if ((st = stage_ac_stats(c, J))) return st;
   if ((st = stage_download_ac(c, J, c->hist_ac.p))) return st;
   if ((st = stage_lf_stats(c, J))) return st;
@@ -1966,7 +2006,7 @@ static jxg_status enc_finish_start(Ctx* c, Job& J, bool split) {
   return JXG_OK;
 }
 static jxg_status enc_finish_end(Ctx* c, Job& J, jxg_buffer* out, Clock::time_point t_call) {
-  hipStream_t s = c->stream;
+  hipStream_t s = c->asm_stream ? c->asm_stream : c->stream;
   const jxg_params& P = c->params;
   const Frame& f = J.f;
   const size_t nb = (size_t)f.bxs * f.bys;
@@ -2038,6 +2078,31 @@ static jxg_status enc_finish(Ctx* c, Job& J, bool split, jxg_buffer* out,
 }
 
 static bool pipe_busy(const Ctx* c);
+static jxg_status lane_batch_launch(Ctx* c, uint32_t lead, bool force);
+// a lane of another context: its own stream, or (borrow) a lane-batch
+// leader's; not counted in g_live_ctx
+static jxg_status ctx_new_lane(const jxg_params& params, hipStream_t borrow, Ctx** out) {
+  *out = nullptr;
+  Ctx* c = new (std::nothrow) Ctx();
+  if (!c) return JXG_ERR_OOM;
+  c->params = params;
+  c->owned_lane = true;
+  if (borrow) {
+    c->stream = borrow;
+    c->stream_borrowed = true;
+  } else if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return JXG_ERR_HIP;
+  }
+  for (auto& e : c->ev)
+    if (hipEventCreate(&e) != hipSuccess) {
+      jxg_destroy(c);
+      return JXG_ERR_HIP;
+    }
+  *out = c;
+  return JXG_OK;
+}
+
 static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32_t h,
                                 size_t stride, jxg_buffer* out, Clock::time_point t_call) {
   // streamed frames in flight use this context as a lane (and its helper
@@ -2130,8 +2195,19 @@ static PipeProf g_pprof;
 #else
 #define PPROF_ADD(field, t0) ((void)0)
 #endif
+struct PipeDone {
+  jxg_buffer buf;
+  jxg_stats stats;
+};
+// the completion workers' state of a whole frame (under Pipe::cmu)
+struct PipeCompletion {
+  int state = 0;  // 0 not handed over, 1 queued / in progress, 2 completed
+  jxg_status st = JXG_OK;
+  PipeDone res{{nullptr, 0}, {}};
+};
 struct PipeFrame {
   Ctx* lane = nullptr;
+  uint32_t li = 0;  // lane index (lane batches: physical lane li / K, slot li % K)
   Job J;
   int phase = 1;  // 1: statistics launched; 2: emission launched; 3: assembly enqueued
   bool shard = false;
@@ -2140,6 +2216,7 @@ struct PipeFrame {
   // jxg_shard_stream: the codes (a helper's, or the completion thread's own)
   // waited on by the completion thread and by the submitting thread's lag join
   std::shared_future<jxg_status> sf;
+  PipeCompletion cw;  // whole frames with completion workers
 };
 // the helper's codes of a frame -> phase 2 (on an error the caller aborts)
 static jxg_status pipe_join_codes(PipeFrame& fr) {
@@ -2151,10 +2228,6 @@ static jxg_status pipe_join_codes(PipeFrame& fr) {
 #endif
   return st;
 }
-struct PipeDone {
-  jxg_buffer buf;
-  jxg_stats stats;
-};
 struct Pipe {
   std::vector<std::unique_ptr<PipeFrame>> inflight;  // submission order
   std::vector<PipeDone> done;                        // submission order
@@ -2165,6 +2238,17 @@ struct Pipe {
   int mode = 0;  // 1 whole frames, 2 shards (while any frame is pending)
   uint32_t depth = 0;
   std::unique_ptr<ChainBatcher> batcher;  // (ANS; created with the lanes)
+  uint32_t batch_k = 1;                   // lane batches: slots per physical lane (1: off)
+  hipStream_t asm_stream = nullptr;       // lane batches: completion (concat + D2H)
+  // completion workers (whole frames): frames whose emission is launched are
+  // handed over in submission order; a worker assembles one (layout, concat,
+  // codestream D2H, stats) while the submitting thread launches the next
+  std::vector<std::thread> workers;
+  std::mutex cmu;
+  std::condition_variable ccv, dcv;  // work queued / a frame completed
+  std::deque<PipeFrame*> cq;
+  bool cstop = false;
+  int device = 0;
 };
 // the pipeline's chain batcher on every lane (ANS, JXG_CHAIN_BATCH != 0)
 static jxg_status pipe_batcher(Ctx* c) {
@@ -2200,12 +2284,23 @@ static jxg_status ensure_lanes(Ctx* c, uint32_t extra) {
 // lanes' streams
 static void pipe_abort(Ctx* c) {
   Pipe& p = *c->pipe;
+  if (!p.workers.empty()) {  // frames handed to the workers finish first
+    std::unique_lock<std::mutex> lk(p.cmu);
+    p.dcv.wait(lk, [&] {
+      for (auto& q : p.inflight)
+        if (q->cw.state == 1) return false;
+      return true;
+    });
+    for (auto& q : p.inflight)
+      if (q->cw.state == 2 && q->cw.res.buf.data) jxg_buffer_free(&q->cw.res.buf);
+  }
   for (auto& fr : p.inflight) {
     (void)pipe_join_codes(*fr);
     if (fr->sf.valid()) fr->sf.wait();
     if (fr->J.chain.valid()) fr->J.chain.wait();  // (the batcher launches every queued frame)
   }
   if (p.batcher) (void)hipStreamSynchronize(p.batcher->stream);
+  if (p.asm_stream) (void)hipStreamSynchronize(p.asm_stream);
   for (auto& fr : p.inflight) (void)hipStreamSynchronize(fr->lane->stream);
   for (auto& fr : p.ready) (void)hipStreamSynchronize(fr->lane->stream);
   for (auto& fr : p.inflight)  // codestreams of frames whose assembly had started
@@ -2318,11 +2413,125 @@ static jxg_status pipe_progress(Ctx* c) {
   return JXG_OK;
 }
 
+// ---- completion workers (whole frames) ----
+// The host work of a frame's completion (its layout, the concat launch, the
+// codestream D2H and the wait for it: ≈ 0.45 ms at 1080p, profiles/r03s2_batch)
+// used to run on the submitting thread, which then bounded small frames at
+// ≈ 0.5 ms per frame, it seemed.  JXG_PIPE_WORKERS threads take it over (0:
+// the submitting thread completes).  Measured (profiles/r03s2_batch): no gain
+// at 1080p (1-3 workers ≈ 3.8-4.0 GPix/s, as without), 8K within noise, and
+// two processes on one GPU share the same ≈ 4 GPix/s: the small-frame stream
+// is bound on the GPU side.  Off by default.
+#ifndef JXG_PIPE_WORKERS
+#define JXG_PIPE_WORKERS 0
+#endif
+static uint32_t pipe_workers() {
+  uint32_t n = JXG_PIPE_WORKERS;
+  if (const char* e = std::getenv("JXG_PIPE_WORKERS")) n = (uint32_t)std::strtoul(e, nullptr, 10);
+  return std::min(n, 8u);
+}
+static void pipe_worker(Pipe* p) {
+  (void)hipSetDevice(p->device);
+  for (;;) {
+    PipeFrame* fr = nullptr;
+    {
+      std::unique_lock<std::mutex> lk(p->cmu);
+      p->ccv.wait(lk, [&] { return p->cstop || !p->cq.empty(); });
+      if (p->cq.empty()) return;  // stopped and drained
+      fr = p->cq.front();
+      p->cq.pop_front();
+    }
+    PipeDone d{{nullptr, 0}, {}};
+    jxg_status st = fr->phase < 3 ? enc_finish_start(fr->lane, fr->J, false) : JXG_OK;
+    if (!st) st = enc_finish_end(fr->lane, fr->J, &d.buf, fr->t0);
+    if (!st) d.stats = fr->lane->stats;
+    {
+      std::lock_guard<std::mutex> lk(p->cmu);
+      fr->cw.st = st;
+      fr->cw.res = d;
+      fr->cw.state = 2;
+    }
+    p->dcv.notify_all();
+  }
+}
+static void pipe_workers_start(Ctx* c) {
+  Pipe& p = *c->pipe;
+  if (!p.workers.empty()) return;
+  p.device = c->params.device;
+  const uint32_t n = pipe_workers();
+  for (uint32_t i = 0; i < n; i++) {
+    try {
+      p.workers.emplace_back(pipe_worker, &p);
+    } catch (...) {  // fewer (or no) workers: the submitting thread completes the rest
+      break;
+    }
+  }
+}
+static void pipe_workers_stop(Pipe& p) {
+  {
+    std::lock_guard<std::mutex> lk(p.cmu);
+    p.cstop = true;
+  }
+  p.ccv.notify_all();
+  for (auto& t : p.workers) t.join();
+  p.workers.clear();
+  p.cstop = false;
+}
+// hand over, in submission order, every whole frame whose codes are joined
+// and whose emission is done (a worker then never waits on the GPU for long);
+// oldest: the oldest frame once its emission is launched (the submitting
+// thread waits for it next)
+static void pipe_handoff(Ctx* c, bool oldest = false) {
+  Pipe& p = *c->pipe;
+  if (p.workers.empty()) return;
+  bool any = false;
+  {
+    std::lock_guard<std::mutex> lk(p.cmu);
+    bool first = true;
+    for (auto& q : p.inflight) {
+      PipeFrame& f = *q;
+      if (f.shard) break;
+      const bool forced = oldest && first;
+      first = false;
+      if (f.cw.state) continue;
+      if (f.phase < 2 || f.codes.valid() || (f.J.chain_deferred && !f.J.chain_launched)) break;
+      if (!forced && emission_done(f.lane, f.J) != 1) break;
+      f.cw.state = 1;
+      p.cq.push_back(&f);
+      any = true;
+    }
+  }
+  if (any) p.ccv.notify_all();
+}
+
 static jxg_status pipe_complete_oldest(Ctx* c) {
   Pipe& p = *c->pipe;
   PipeFrame& fr = *p.inflight.front();
+  // lane batches: a lane whose slots are not all filled (the stream's end,
+  // mixed sizes) launches the chains it has
+  if (p.batch_k > 1 && !fr.shard && !fr.J.chain_launched) {
+    const jxg_status sb = lane_batch_launch(c, fr.li / p.batch_k, true);
+    if (sb) return sb;
+  }
   jxg_status st = pipe_join_codes(fr);
-  if (!st && fr.phase == 1) st = enc_codes(fr.lane, fr.J, false);
+  if (!st && fr.phase == 1) {
+    st = enc_codes(fr.lane, fr.J, false);
+    fr.phase = 2;
+  }
+  if (!fr.shard && !p.workers.empty()) {  // the workers complete it
+    if (st) return st;
+    pipe_handoff(c, true);
+    {
+      std::unique_lock<std::mutex> lk(p.cmu);
+      p.dcv.wait(lk, [&] { return fr.cw.state == 2; });
+      st = fr.cw.st;
+    }
+    if (st) return st;
+    p.done.push_back(fr.cw.res);
+    fr.cw.res.buf = jxg_buffer{nullptr, 0};
+    p.inflight.erase(p.inflight.begin());
+    return JXG_OK;
+  }
   if (fr.shard) {
     size_t bytes = 0;
     if (!st) st = shard_finish(fr.lane, fr.J, &bytes, false);
@@ -2336,7 +2545,10 @@ static jxg_status pipe_complete_oldest(Ctx* c) {
 #ifdef JXG_PIPE_PROFILE
   if (!st) {
     const Clock::time_point tw = Clock::now();
-    (void)hipStreamSynchronize(fr.lane->stream);
+    if (fr.J.chain_deferred)  // lane batches: the frame's emission (its stream has other slots' work)
+      (void)hipEventSynchronize(fr.lane->ev[3]);
+    else
+      (void)hipStreamSynchronize(fr.lane->stream);
     PPROF_ADD(finish_wait, tw);
   }
 #endif
@@ -2346,6 +2558,137 @@ static jxg_status pipe_complete_oldest(Ctx* c) {
   d.stats = fr.lane->stats;
   p.done.push_back(d);
   p.inflight.erase(p.inflight.begin());
+  return JXG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Lane batches (whole frames, ANS, frames of at most 128 pass groups: 1080p
+// has 40).  A small frame's rANS chains still last as long as its longest
+// group's (≈ 3.5 ms at 1080p), and with one frame per lane the pipeline holds
+// at most as many frames as the process has hardware queues (lanes sharing a
+// queue serialise behind each other's chains), so 64 x 1080p was bound by
+// lanes x frame latency.  With batches a physical lane
+// (one stream, one hardware queue) holds K frames: their transform kernels,
+// statistics and codes go one after the other, and their chains go out as ONE
+// launch (ans_encode_batch_kernel, K x 40 chain waves) once the last slot's
+// codes are joined; each slot then places its bits.  Completion (concat +
+// codestream D2H) runs on one pipeline-wide assembly stream, so it never
+// waits behind the next batch's kernels on the lane's stream.  Bytes are the
+// one-at-a-time bytes (tests/test_gpu_stream.py).
+// ---------------------------------------------------------------------------
+// Measured (profiles/r03s2_batch): no gain -- 64 x 1080p streams at ≈ 4.0
+// GPix/s with 1, 2, 3, 4 or 8 slots (the per-frame latency grows with K), so
+// the stream is not bound by frames in flight: off unless JXG_PIPE_BATCH > 1.
+#ifndef JXG_PIPE_BATCH  // slots per lane (JXG_PIPE_BATCH env overrides; 1: off)
+#define JXG_PIPE_BATCH 1
+#endif
+#ifndef JXG_PIPE_BATCH_MAX_GROUPS
+#define JXG_PIPE_BATCH_MAX_GROUPS 128
+#endif
+static uint32_t batch_slots(uint32_t ngroups, const jxg_params& P) {
+  if (!(P.flags & JXG_FLAG_ANS) || ngroups > JXG_PIPE_BATCH_MAX_GROUPS) return 1;
+  uint32_t k = JXG_PIPE_BATCH;
+  if (const char* e = std::getenv("JXG_PIPE_BATCH")) k = (uint32_t)std::strtoul(e, nullptr, 10);
+  return std::max(1u, std::min<uint32_t>(k, (uint32_t)kAnsBatchMax));
+}
+// frames in flight with lane batches: physical lanes (one hardware queue each
+// beside the caller's stream and the assembly stream) x slots
+static uint32_t batch_depth(uint32_t lanes, uint32_t k) {
+  const uint32_t q = hw_queues();
+  return std::max(1u, std::min(lanes, q > 2 ? q - 2 : 1u)) * k;
+}
+static Ctx* pipe_lane(Ctx* c, uint32_t li) {
+  if (c->pipe->batch_k > 1) return c->blanes[li].get();
+  return li == 0 ? c : c->lanes[li - 1].get();
+}
+// n batch slots of k per physical lane (the caller's context is not one: its
+// stream stays idle), and the assembly stream
+static jxg_status ensure_blanes(Ctx* c, uint32_t n, uint32_t k) {
+  Pipe& p = *c->pipe;
+  if (c->blanes_k != k) {
+    while (!c->blanes.empty()) c->blanes.pop_back();
+    c->blanes_k = k;
+  }
+  if (!p.asm_stream) JXG_HIP(hipStreamCreateWithFlags(&p.asm_stream, hipStreamNonBlocking));
+  while (c->blanes.size() < n) {
+    const size_t li = c->blanes.size();
+    Ctx* l = nullptr;
+    const jxg_status st =
+        ctx_new_lane(c->params, li % k ? c->blanes[li - li % k]->stream : nullptr, &l);
+    if (st) return st;
+    l->defer_chain = true;
+    l->asm_stream = p.asm_stream;
+    c->blanes.emplace_back(l);
+  }
+  return JXG_OK;
+}
+// the deferred chains of physical lane `lead`: every frame in flight on its
+// slots whose chain is not out yet, in one launch on the lane's stream, then
+// each frame's bit placement, bit-count download and emission events.
+// force: now (codes built here where no helper has, helpers waited for);
+// else only once the lane's last slot is taken and every frame's codes are
+// in (no wait)
+static jxg_status lane_batch_launch(Ctx* c, uint32_t lead, bool force) {
+  Pipe& p = *c->pipe;
+  const uint32_t K = p.batch_k;
+  std::vector<PipeFrame*> fr;
+  bool closed = false;
+  for (auto& q : p.inflight)
+    if (!q->shard && q->li / K == lead && !q->J.chain_launched) {
+      fr.push_back(q.get());
+      closed = closed || q->li % K == K - 1;
+    }
+  if (fr.empty()) return JXG_OK;
+  if (fr.size() > (size_t)kAnsBatchMax) return JXG_ERR_INTERNAL;
+  if (!force) {
+    if (!closed) return JXG_OK;
+    for (PipeFrame* f : fr)
+      if (f->phase == 1 && (!f->codes.valid() || f->codes.wait_for(std::chrono::seconds(0)) !=
+                                                         std::future_status::ready))
+        return JXG_OK;
+  }
+  for (PipeFrame* f : fr) {
+    jxg_status st = pipe_join_codes(*f);
+    if (!st && f->phase == 1) {
+      st = enc_codes(f->lane, f->J, false);
+      f->phase = 2;
+    }
+    if (st) return st;
+    if (!f->J.chain_deferred) return JXG_ERR_INTERNAL;
+  }
+  hipStream_t s = fr[0]->lane->stream;
+  AnsBatch b{};
+  uint32_t nwg = 0;
+  for (size_t i = 0; i < fr.size(); i++) {
+    b.f[i] = fr[i]->J.na;
+    b.wg0[i] = nwg;
+    nwg += ans_chain_wgs(fr[i]->J.na.n);
+  }
+  b.wg0[fr.size()] = nwg;
+  b.nf = (uint32_t)fr.size();
+  launch_ans_batch(b, s);
+  JXG_HIP(hipGetLastError());
+  for (PipeFrame* f : fr) {
+    Ctx* L = f->lane;
+    Job& J = f->J;
+    launch_ans_emit(J.na, s);
+    JXG_HIP(hipGetLastError());
+    JXG_HIP(hipMemcpyAsync(L->h_bits.p, L->bits.p, ((size_t)J.f.ngroups + J.nstreams) * 4,
+                           hipMemcpyDeviceToHost, s));
+    JXG_HIP(hipEventRecord(L->ev[7], s));
+    JXG_HIP(hipEventRecord(L->ev[3], s));
+    J.chain_launched = true;
+  }
+  return JXG_OK;
+}
+// every physical lane (see lane_batch_launch for `force`)
+static jxg_status lane_batch_poll(Ctx* c, bool force) {
+  Pipe& p = *c->pipe;
+  const uint32_t nl = (uint32_t)(c->blanes.size() / std::max(1u, p.batch_k));
+  for (uint32_t l = 0; l < nl; l++) {
+    const jxg_status st = lane_batch_launch(c, l, force);
+    if (st) return st;
+  }
   return JXG_OK;
 }
 
@@ -2372,10 +2715,15 @@ static jxg_status pipe_submit(Ctx* c, const uint8_t* src, bool on_device, uint32
       return JXG_ERR_UNSUPPORTED;
     ngroups = P.ng();
   }
-  const uint32_t depth = pipe_depth(ngroups), lag = pipe_lag(ngroups, depth);
-  jxg_status st = ensure_lanes(c, depth - 1);
-  if (!st) st = pipe_batcher(c);
+  uint32_t depth = pipe_depth(ngroups);
+  const uint32_t lag = pipe_lag(ngroups, depth);
+  // lane batches or one frame per lane: chosen when the pipeline is empty
+  if (!pipe_busy(c)) p.batch_k = shard ? 1 : batch_slots(ngroups, c->params);
+  if (p.batch_k > 1) depth = batch_depth(depth, p.batch_k);
+  jxg_status st = p.batch_k > 1 ? ensure_blanes(c, depth, p.batch_k) : ensure_lanes(c, depth - 1);
+  if (!st && p.batch_k == 1) st = pipe_batcher(c);
   if (st) return st;
+  if (mode == 1) pipe_workers_start(c);
   const Clock::time_point t0 = Clock::now();
   // a shard frame holds its lane until its sections are written: the caller
   // must take one first (jxg_shard_next_head / jxg_shard_write_next)
@@ -2414,17 +2762,22 @@ static jxg_status pipe_submit(Ctx* c, const uint8_t* src, bool on_device, uint32
   PPROF_ADD(complete, tc);
   // a lane no frame in flight (or ready) uses (the lowest index)
   Ctx* L = nullptr;
+  uint32_t L_li = 0;
   for (uint32_t li = 0; li < depth && !L; li++) {
-    Ctx* cand = li == 0 ? c : c->lanes[li - 1].get();
+    Ctx* cand = pipe_lane(c, li);
     bool used = false;
     for (auto& q : p.inflight) used = used || q->lane == cand;
     for (auto& q : p.ready) used = used || q->lane == cand;
-    if (!used) L = cand;
+    if (!used) {
+      L = cand;
+      L_li = li;
+    }
   }
   if (!L) return shard ? JXG_ERR_INVALID_ARG : fail(JXG_ERR_INTERNAL);
   std::unique_ptr<PipeFrame> fr(new (std::nothrow) PipeFrame());
   if (!fr) return fail(JXG_ERR_OOM);
   fr->lane = L;
+  fr->li = L_li;
   fr->t0 = t0;
   fr->shard = shard;
   if (!on_device) {
@@ -2454,9 +2807,17 @@ static jxg_status pipe_submit(Ctx* c, const uint8_t* src, bool on_device, uint32
 #ifdef JXG_PIPE_PROFILE
   const Clock::time_point tj = Clock::now();
 #endif
-  if (p.inflight.size() > lag && (st = pipe_join_codes(*p.inflight[p.inflight.size() - 1 - lag])))
+  if (p.inflight.size() > lag) {
+    PipeFrame& fj = *p.inflight[p.inflight.size() - 1 - lag];
+    st = pipe_join_codes(fj);
+    if (st) return fail(st);
+  }
+  // lane batches: every lane whose slots are taken and whose codes are in
+  // sends its chains out (checked at every submit, no wait)
+  if (p.batch_k > 1 && (st = lane_batch_poll(c, false))) return fail(st);
+  if (mode == 1) pipe_handoff(c);
+  if (mode == 1 && p.workers.empty() && pipe_progress_enabled() && (st = pipe_progress(c)))
     return fail(st);
-  if (mode == 1 && pipe_progress_enabled() && (st = pipe_progress(c))) return fail(st);
 #ifdef JXG_PIPE_PROFILE
   PPROF_ADD(join, tj);
   PPROF_ADD(submit, t0);
@@ -2470,7 +2831,15 @@ static jxg_status pipe_receive(Ctx* c, jxg_buffer* out) {
   Pipe& p = *c->pipe;
   if (p.done.empty()) {
     if (p.inflight.empty()) return JXG_ERR_INVALID_ARG;
-    const jxg_status st = pipe_complete_oldest(c);
+    // lane batches: every lane whose slots are taken and whose codes are in
+    // sends its chains out before this thread waits on the oldest (whose
+    // lane, if partly filled, pipe_complete_oldest launches)
+    jxg_status st = p.batch_k > 1 ? lane_batch_poll(c, false) : JXG_OK;
+    if (st) {
+      pipe_abort(c);
+      return st;
+    }
+    st = pipe_complete_oldest(c);
     if (st) {
       pipe_abort(c);
       return st;
@@ -3338,6 +3707,7 @@ const char* jxg_status_str(jxg_status s) {
   }
 }
 
+
 jxg_status jxg_create(const jxg_params* params, void** out) {
   if (!params || !out) return JXG_ERR_INVALID_ARG;
   *out = nullptr;
@@ -3348,18 +3718,10 @@ jxg_status jxg_create(const jxg_params* params, void** out) {
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return JXG_ERR_NO_DEVICE;
   if (params->device < 0 || params->device >= ndev) return JXG_ERR_INVALID_ARG;
   if (hipSetDevice(params->device) != hipSuccess) return JXG_ERR_HIP;
-  Ctx* c = new (std::nothrow) Ctx();
-  if (!c) return JXG_ERR_OOM;
-  c->params = *params;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-    delete c;
-    return JXG_ERR_HIP;
-  }
-  for (auto& e : c->ev)
-    if (hipEventCreate(&e) != hipSuccess) {
-      delete c;
-      return JXG_ERR_HIP;
-    }
+  Ctx* c = nullptr;
+  const jxg_status st = ctx_new_lane(*params, nullptr, &c);
+  if (st) return st;
+  c->owned_lane = false;
   g_live_ctx++;
   *out = c;
   return JXG_OK;
@@ -3374,10 +3736,13 @@ void jxg_destroy(void* ctx) {
     chain_batcher_destroy(c->pipe->batcher);
     c->batcher = nullptr;
     for (auto& l : c->lanes) l->batcher = nullptr;
+    pipe_workers_stop(*c->pipe);
     for (auto& d : c->pipe->done) jxg_buffer_free(&d.buf);
+    if (c->pipe->asm_stream) (void)hipStreamDestroy(c->pipe->asm_stream);
     c->pipe.reset();
   }
   c->lanes.clear();  // batch / pipeline lanes (jxg_destroy each)
+  while (!c->blanes.empty()) c->blanes.pop_back();  // slots before the leader whose stream they use
   (void)hipSetDevice(c->params.device);
   (void)hipStreamSynchronize(c->stream);
   if (c->stream2) (void)hipStreamSynchronize(c->stream2);
@@ -3400,7 +3765,7 @@ void jxg_destroy(void* ctx) {
     if (e) (void)hipEventDestroy(e);
   if (c->ev_in) (void)hipEventDestroy(c->ev_in);
   if (c->ev_up) (void)hipEventDestroy(c->ev_up);
-  if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->stream && !c->stream_borrowed) (void)hipStreamDestroy(c->stream);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
   delete c;
 }
@@ -3690,8 +4055,11 @@ jxg_status jxg_pipeline_depth(void* ctx, uint32_t xsize, uint32_t ysize, uint32_
                               uint32_t world, uint32_t* depth) {
   if (!ctx || !depth || xsize == 0 || ysize == 0 || world == 0 || rank >= world)
     return JXG_ERR_INVALID_ARG;
-  const Frame f = make_frame(xsize, ysize, static_cast<Ctx*>(ctx)->params.distance);
+  const Ctx* c = static_cast<Ctx*>(ctx);
+  const Frame f = make_frame(xsize, ysize, c->params.distance);
   *depth = pipe_depth(world > 1 ? make_plan(f, rank, world).ng() : f.ngroups);
+  const uint32_t k = world > 1 ? 1 : batch_slots(f.ngroups, c->params);
+  if (k > 1) *depth = batch_depth(*depth, k);  // whole small frames: lane batches
   return JXG_OK;
 }
 

@@ -109,3 +109,46 @@ def test_batch_ans_equals_single_and_refuses_pending(jxg_mod):
         assert enc.receive() == want[0]
         assert enc.encode_batch(frames[:3]) == want[:3]
         assert enc.pending() == 0
+
+
+@pytest.mark.parametrize("k,workers", [("1", "0"), ("1", "2"), ("2", "0"), ("3", "0"), ("3", "2"),
+                                       ("8", "3")])
+def test_lane_batches_equal_single(jxg_mod, monkeypatch, k, workers):
+    """Lane batches (small ANS frames; JXG_PIPE_BATCH slots per physical lane,
+    one chain launch per lane, completion on the assembly stream) and
+    completion workers (JXG_PIPE_WORKERS threads assemble): 41 frames
+    (not a multiple of K or of the depth), host and device inputs, a 4K frame
+    (135 groups) in the middle of a batch-mode stream, receives interleaved,
+    the drain launching partly filled lanes -- every codestream equals the
+    one-at-a-time encode's."""
+    import torch
+
+    from jxg.synth import natural_rgb8, synth_rgb8
+
+    monkeypatch.setenv("JXG_PIPE_BATCH", k)
+    monkeypatch.setenv("JXG_PIPE_WORKERS", workers)
+    sizes = [(640, 480), (1920, 1080), (333, 250), (800, 600)]
+    frames = [(natural_rgb8 if i % 3 else synth_rgb8)(*sizes[i % 4], 900 + i) for i in range(41)]
+    frames[17] = synth_rgb8(3840, 2160, 77)
+    with jxg_mod.Encoder(distance=1.0, effort=7, flags=jxg_mod.FLAG_ANS) as enc:
+        want = [enc.encode(f) for f in frames]
+    dev = [torch.from_numpy(f).cuda() if i % 2 else None for i, f in enumerate(frames)]
+    torch.cuda.synchronize()
+    with jxg_mod.Encoder(distance=1.0, effort=7, flags=jxg_mod.FLAG_ANS) as enc:
+        got = []
+        for i, f in enumerate(frames):
+            if dev[i] is None:
+                enc.submit(f)
+            else:
+                h, w, _ = f.shape
+                enc.submit_device(dev[i].data_ptr(), w, h)
+            while enc.pending() > 30:
+                got.append(enc.receive())
+            if i == 5:
+                got.append(enc.receive())
+        while enc.pending():
+            got.append(enc.receive())
+        # one-at-a-time on the same context afterwards
+        assert enc.encode(frames[1]) == want[1]
+    assert [len(g) for g in got] == [len(w) for w in want]
+    assert got == want
