@@ -153,7 +153,14 @@ jxg_status jxg_encode_batch_rgb8_device(void* ctx, const void* const* d_rgbs, ui
  * submitted and not yet received.  A device frame must stay unchanged until
  * its codestream is received; a host frame is copied into pinned staging
  * before jxg_submit_rgb8 returns.  jxg_get_stats after jxg_receive describes
- * the received frame.  On an error every frame in flight is dropped. */
+ * the received frame.  On an error every frame in flight is dropped.
+ * Two optional modes, same bytes, off by default (measured without gain,
+ * DESIGN.md §3.7): JXG_PIPE_BATCH=K (environment, 2..8) -- lane batches for
+ * ANS frames of at most 128 pass groups: K frames per lane share its stream
+ * and their rANS chains go out as one launch, the depth becomes lanes x K
+ * (jxg_pipeline_depth reports it), completion runs on one extra assembly
+ * stream; JXG_PIPE_WORKERS=N -- N threads assemble completed frames (layout,
+ * concat, codestream D2H) instead of the submitting thread. */
 jxg_status jxg_submit_rgb8(void* ctx, const uint8_t* rgb, uint32_t xsize, uint32_t ysize,
                            size_t row_stride);
 jxg_status jxg_submit_rgb8_device(void* ctx, const void* d_rgb, uint32_t xsize, uint32_t ysize,
