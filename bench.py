@@ -133,18 +133,16 @@ def load_front_valu(workload):
 def load_front_valu_floor(workload, avg_ms):
     """The front kernel's VALU floor from its PMC counters: SQ_INSTS_VALU
     wave-instructions x 2 cycles each (wave64 on a 32-lane SIMD,
-    MI355X_MICROARCH.md 'v_fma_f32 (wave64) 2 cyc') / (1024 SIMDs x the clock the
-    chip held, GRBM_GUI_ACTIVE / 8 XCDs / kernel time)."""
+    MI355X_MICROARCH.md 'v_fma_f32 (wave64) 2 cyc') / (1024 SIMDs x 2.4 GHz, the
+    guide's max clock: the lowest floor), against the measured kernel time."""
     p = os.path.join(ROOT, "profiles", "front_pmc_%s.json" % workload)
     try:
         with open(p) as f:
-            d = json.load(f)
-        insts, grbm = d["SQ_INSTS_VALU"], d["GRBM_GUI_ACTIVE"]
-        ms_pmc = d.get("avg_ms_pmc") or avg_ms
-        clk = grbm / 8.0 / (ms_pmc * 1e-3)
+            insts = json.load(f)["SQ_INSTS_VALU"]
+        clk = 2.4e9
         floor = insts * 2.0 / (1024 * clk) * 1e3
         return {"valu_insts": int(insts), "cycles_per_inst": 2, "simds": 1024,
-                "clock_ghz": round(clk / 1e9, 3), "floor_ms": round(floor, 4),
+                "clock_ghz": 2.4, "floor_ms": round(floor, 4),
                 "frac": round(floor / avg_ms, 4) if avg_ms else None}
     except Exception:
         return None
