@@ -2315,7 +2315,7 @@ static void pipe_abort(Ctx* c) {
 // A rank's sections of a frame (codes built, emission launched) -> payload
 // head (host, lane->payload_head) + body (device, lane->out); the stream is
 // synchronised.
-// payload: "JXGS" | version | rank | world | xsize | ysize | nsections |
+// payload: "JXGS" | version | rank (| loop-filter code << 16) | world | xsize | ysize | nsections |
 //          nsections x (TOC index, bytes) [| version 2: the rank's HF preset]
 //          | section bytes back to back
 constexpr uint32_t kPayloadMagic = 0x5347584Au;  // "JXGS"
@@ -2523,6 +2523,7 @@ static jxg_status pipe_complete_oldest(Ctx* c) {
     pipe_handoff(c, true);
     {
       std::unique_lock<std::mutex> lk(p.cmu);
+      if (fr.cw.state == 0) return JXG_ERR_INTERNAL;  // (not handed over: never waited on)
       p.dcv.wait(lk, [&] { return fr.cw.state == 2; });
       st = fr.cw.st;
     }
