@@ -692,20 +692,48 @@ __device__ __forceinline__ void eval_chan(const GroupCtx& G, float scale, float 
 // One candidate: Y, then X and B together (f2); only one candidate's state is
 // live at a time, which keeps the kernel inside 128 VGPRs.  PRE (DCT8,
 // DCT8X4): the fit's transposed 8-point row passes, y[k] and xb[k] = (X, B).
+// Scan pruning (no effect on any result): the estimate's bits and e*e sum
+// only grow from channel to channel (every non-zero adds 2 + 2 bitlen > 0,
+// bitlen(nz) >= 0; fmaf(e, e, acc) >= acc and the tree sum of non-negative
+// lane sums is monotone in each of them), so the estimate after Y alone is a
+// lower bound of the final one, and so is hook F of it while hook F's factor
+// 0.8 avg_r is not negative (a NaN factor makes both NaN: no pruning).  When
+// that bound exceeds the best estimate so far for every block of the wave,
+// the candidate cannot win the scan (`beats` needs e < best, or e == best with
+// a lower index) and its X / B half is skipped: NaN is returned, which never
+// wins.  The hook-P override re-evaluates its candidate in full.
+struct Prune {
+  bool on;          // a best estimate exists (not for the scan's first candidate)
+  float best;       // the scan's best (after hook F)
+  bool hookF;
+  float rh, rv, rd;
+};
 template <int T, bool PRE = false>
 __device__ __forceinline__ float eval_one(const GroupCtx& G, float scale, float inv_scale,
                                           CandAcc& A, const float* pre_y = nullptr,
-                                          const f2* pre_xb = nullptr) {
-  A.bits = 0;
-  A.part = 0.0f;
-  A.q.nz = 0;
-  eval_chan<T, 1, PRE, float>(G, scale, inv_scale, A, pre_y);
-  eval_chan<T, kXB, PRE, f2>(G, scale, inv_scale, A, pre_xb);
+                                          const f2* pre_xb = nullptr,
+                                          const Prune* pr = nullptr) {
   // estimate multipliers (== oracle jxo_quantize_block tmul, JXO_TMUL_*)
   constexpr float tm = T == kDCT8 ? 1.0f
                                   : (T == kDCT4X4 ? 1.05f
                                                   : (T == kDCT2X2 ? 1.05f
                                                                   : (T == kIDENTITY ? 1.08f : 1.02f)));
+  A.bits = 0;
+  A.part = 0.0f;
+  A.q.nz = 0;
+  eval_chan<T, 1, PRE, float>(G, scale, inv_scale, A, pre_y);
+  if (pr && pr->on) {
+    float lb = ((float)group_int_sum(A.bits) + 8.0f * group_tree_sum(A.part)) * tm;
+    bool out;
+    if (pr->hookF) {
+      const float avg_r = (pr->rh + pr->rv + pr->rd) / 3.0f;
+      out = avg_r >= 0.0f && hook_f(lb, pr->rh, pr->rv, pr->rd) > pr->best;
+    } else {
+      out = lb > pr->best;
+    }
+    if (__all(out)) return __builtin_nanf("");
+  }
+  eval_chan<T, kXB, PRE, f2>(G, scale, inv_scale, A, pre_xb);
   return ((float)group_int_sum(A.bits) + 8.0f * group_tree_sum(A.part)) * tm;
 }
 
@@ -1129,6 +1157,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
   // ---- phase C: strategy search (FindBest8x8Transform [ext] + hooks) ----
   const int ncand = a.effort >= 5 ? 6 : 1;
   const bool hookF = (a.proposals & 2u) != 0 && ncand > 1;
+#ifndef JXG_FRONT_PRUNE  // (A/B builds: -DJXG_FRONT_PRUNE=0)
+#define JXG_FRONT_PRUNE 1
+#endif
+  const bool prune = JXG_FRONT_PRUNE != 0;
   // hook P target (combined.diff:270-274) is known before the search: it only
   // depends on the homogeneity indices; its coefficients are kept aside
   int pt = kDCT8;
@@ -1160,10 +1192,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
     if (!(ncand > 1 || pt == T)) return;
     CandAcc A;
     float e;
+    const Prune pr{ncand > 1 && prune, beste, hookF, rh, rv, rd};
     if constexpr (T == kDCT8X4) {  // (ncand > 1 here: the fit ran)
-      e = eval_one<T, true>(G, scale, inv_scale, A, rty, rtxb);
+      e = eval_one<T, true>(G, scale, inv_scale, A, rty, rtxb, &pr);
     } else {
-      e = eval_one<T>(G, scale, inv_scale, A);
+      e = eval_one<T>(G, scale, inv_scale, A, nullptr, nullptr, &pr);
     }
     if (ncand > 1) {
       if (hookF) e = hook_f(e, rh, rv, rd);

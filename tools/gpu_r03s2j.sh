@@ -1,0 +1,12 @@
+#!/bin/bash
+# front-kernel scan pruning: parity (the whole GPU suite's front paths), then A/B vs a build without it
+set -e
+export TMPDIR=/tmp
+O=gpurun_out/r03s2j
+mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py tests/test_gpu_filters.py -x -q --timeout 200 --timeout-method thread > $O/parity.log 2>&1
+B="python bench.py --no-cpu-baseline --no-quality --alt-coder 0"
+for r in 1 2; do
+  timeout -k 10 200 $B > $O/prune_r$r.log 2>&1
+  JXG_LIB_PATH=tools/var/libjxg_noprune.so timeout -k 10 200 $B > $O/noprune_r$r.log 2>&1
+done
