@@ -51,6 +51,9 @@ constexpr int kMThreads = 256;
 #ifndef JXG_MERGE_WRITE_WPE
 #define JXG_MERGE_WRITE_WPE 3  // write: 167 VGPRs, no spills
 #endif
+#ifndef JXG_MERGE_PRUNE  // merge_eval's workgroup pruning (A/B builds: -DJXG_MERGE_PRUNE=1)
+#define JXG_MERGE_PRUNE 0
+#endif
 constexpr int kMS = 65;  // LDS row stride (floats)
 constexpr int kMPlane = 64 * kMS;
 
@@ -166,6 +169,7 @@ struct MergeLds {
   int vraw[32];           //               max quant field
   int valid[32];
   float lb[32];           // eval: Y-only lower bound of each varblock's estimate
+  float bent[64];         // eval: the front kernel's estimate of each block of the tile
   uint8_t braw[64];       // front-kernel quant field (raw) of the tile's blocks
   int any;
 };
@@ -678,8 +682,10 @@ __device__ __forceinline__ void setup_varblocks(const MergeArgs& a, const Pass& 
   const int t = threadIdx.x;
   if (t < 64) {
     const int lbx = t & 7, lby = t >> 3;
-    S.braw[t] = lbx < nbx && lby < nby
-                    ? a.qf[(size_t)(P.ty * 8 + lby) * a.bxs + P.tx * 8 + lbx] : 0;
+    const bool in = lbx < nbx && lby < nby;
+    const size_t gb = (size_t)(P.ty * 8 + lby) * a.bxs + P.tx * 8 + lbx;
+    S.braw[t] = in ? a.qf[gb] : 0;
+    if (!WRITE && JXG_MERGE_PRUNE) S.bent[t] = in ? a.ent[gb] : 0.0f;
   }
   if (t < 32) {
     const int v = t;
@@ -746,9 +752,6 @@ void merge_eval_kernel(MergeArgs a) {
   // workgroup's varblocks can be chosen: X and B are skipped and their costs
   // set to +inf, which resolve never picks (its best stays finite).
   const int nbx_t = nbx, nby_t = nby;
-#ifndef JXG_MERGE_PRUNE  // (-DJXG_MERGE_PRUNE=0: A/B builds without it)
-#define JXG_MERGE_PRUNE 0
-#endif
   auto after_y = [&]() -> bool {
     if (!JXG_MERGE_PRUNE) return false;
     const int t = threadIdx.x;
@@ -774,8 +777,7 @@ void merge_eval_kernel(MergeArgs a) {
         bool fin = true;
         for (int iy = 0; iy < sl; iy++)
           for (int ix = 0; ix < sl; ix++) {
-            const float e =
-                a.ent[(size_t)(P.ty * 8 + ry * sl + iy) * a.bxs + P.tx * 8 + rx * sl + ix];
+            const float e = S.bent[(ry * sl + iy) * 8 + rx * sl + ix];
             fin = fin && e >= 0.0f && e < FLT_MAX;
             cur += e;
           }
