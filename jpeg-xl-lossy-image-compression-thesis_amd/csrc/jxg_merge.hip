@@ -629,7 +629,6 @@ __device__ __forceinline__ bool transform_quant(const MergeArgs& a, const Pass& 
       quant_pass<RPC, WRITE, 1>(a, P, S, ty);
     }
     if constexpr (!WRITE) {
-      __syncthreads();  // Y's bits, non-zeros and chunk sums are complete
       if (after_y()) {
         stop = true;
         return;
@@ -753,7 +752,10 @@ void merge_eval_kernel(MergeArgs a) {
   // set to +inf, which resolve never picks (its best stays finite).
   const int nbx_t = nbx, nby_t = nby;
   auto after_y = [&]() -> bool {
-    if (!JXG_MERGE_PRUNE) return false;
+    // (levels 32 and 64 only: with 16 or 32 varblocks a 16-level shape
+    // rarely loses in every region, and the extra barriers would not pay)
+    if (!JXG_MERGE_PRUNE || P.ls < 2) return false;
+    __syncthreads();  // Y's bits, non-zeros and chunk sums are complete
     const int t = threadIdx.x;
     if (t < P.NV() && S.valid[t]) {
       const int nch = P.lcy == 0 ? 1 : P.R() >> 4;
