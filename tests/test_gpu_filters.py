@@ -117,3 +117,22 @@ def test_cli_filter_flags(jxg_mod, oracle, tmp_path):
     assert out.read_bytes() == oracle.encode(img, 2.0, 7, 0, 0, GAB | EPF).bytes
     r = subprocess.run([exe, str(src), str(out), "--epf=2"], capture_output=True, timeout=120)
     assert r.returncode == 1
+
+
+def test_filtered_ans_shards_decode_to_single_image(jxg_mod, decoder):
+    """ANS shards (one HF preset per rank, version-2 payload heads) with both
+    filters: the assembled frame header carries the loop filters, and the
+    codestream decodes (Gaborish + EPF applied) to exactly the single-GPU image."""
+    from test_gpu_shard import _same_image, sharded_encode
+
+    from jxg.synth import natural_rgb8
+
+    img = natural_rgb8(1200, 700, 19)
+    flags = _flags(jxg_mod, GAB | EPF, True)
+    with jxg_mod.Encoder(distance=2.0, effort=7, flags=flags) as enc:
+        ref = enc.encode(img)
+    got = sharded_encode(jxg_mod, img, 3, 2.0, 7, 0, flags=flags)
+    dr, dg = decoder.decode(ref), decoder.decode(got)
+    assert dg.npresets == 3 and dr.npresets == 1
+    assert dg.gab and dr.gab and dg.epf_iters == dr.epf_iters == 2
+    _same_image(dr, dg)
