@@ -16,23 +16,26 @@ codestream of the K steps is in host memory.
 
 N = 1: one 7680x4320 frame per step (BASELINE config 2's frame on one GPU);
 the steps cycle through two distinct synthetic frames.
-N > 1 (launched by torch.distributed.run, backend nccl = RCCL):
+N > 1: one process per GPU.  Launched by torch.distributed.run (RANK /
+LOCAL_RANK / WORLD_SIZE from the environment; WORLD_SIZE must equal --gpus),
+or, with WORLD_SIZE unset, bench.py starts the N ranks itself under
+torch.distributed.run (a child process, before anything touches the GPU) and
+exits with its status.  Backend nccl = RCCL.
   shard   (default) -- BASELINE config 2 as written, strong scaling: every
           step is ONE 7680x4320 frame whose 256x256 pass groups are split over
           the N ranks (whole LF groups per rank, jxg_shard_plan kind 1: no
           per-block records move; one HF preset per rank: no histogram
-          collective), streamed through jxg.dist.HostShardStream -- each rank
+          collective), streamed through jxg.dist.ShardStream -- each rank
           keeps up to jxg_pipeline_depth frames' shards in flight in the
           library's lanes (jxg_shard_submit_device), swaps each frame's payload
           heads with the other ranks through a node-shared /dev/shm region and
           DMAs its sections into the frame's codestream there
           (jxg_shard_next_head / jxg_shard_write_next; rank 0 adds headers +
-          TOC).  value = frames x 7680 x 4320 / time over all ranks.
+          TOC).  value = frames x 7680 x 4320 / time over all ranks.  The
+          /dev/shm exchange replaces an RCCL gather on purpose: the
+          codestream must end in host memory, and every rank DMAs its own
+          sections there over its own PCIe link.
           --scaling weak: one frame of N stacked 8K frames per step instead.
-  shard-native -- the same stream with the per-frame completion in the
-          library (jxg.dist.ShardStream over jxg_shard_stream_*: a completion
-          thread per rank; same bytes, slower in the measurements so far:
-          DESIGN.md §5).
   shard-sync -- the same split one frame at a time (jxg.dist.encode_sharded:
           record exchange + histogram all-reduce when the plan / coder needs
           them, --assembly host|device).
@@ -157,17 +160,43 @@ def load_merge_pmc(workload):
         return None
 
 
-def cpu_threads():
-    """host threads for the CPU baseline: every core this process may run on
-    (its CPU affinity; nproc is reported beside it)"""
+def cpu_quota():
+    """CPUs of this process's cgroup CPU quota (cgroup v2 cpu.max, or v1
+    cfs_quota / cfs_period), None when unlimited.  On the GPU box nproc and the
+    affinity mask show the whole machine (256 CPUs) while the quota is the
+    box's share (16): OpenMP over 256 threads under a 16-CPU quota is
+    throttled (round 3's 8.0 MPix/s on "256 cores" vs 21 on 16)."""
     try:
-        n = len(os.sched_getaffinity(0))
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, int(q) // int(per))
+        return None
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return max(1, q // per) if q > 0 else None
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_affinity():
+    try:
+        return len(os.sched_getaffinity(0))
     except AttributeError:
-        n = os.cpu_count() or 1
-    return max(1, n)
+        return os.cpu_count() or 1
 
 
-def cpu_baseline(img, distance, effort, proposals, coder, gpu_bytes):
+def cpu_threads():
+    """host threads for the CPU baseline: the CPUs this process may actually
+    use -- its affinity, capped by its cgroup CPU quota"""
+    n = cpu_affinity()
+    q = cpu_quota()
+    return max(1, min(n, q) if q else n)
+
+
+def cpu_baseline(img, distance, effort, proposals, coder, gpu_bytes, sweep=None):
     """The oracle/ C restatement (libjxl/cjxl are absent on the box: probe in
     profiles/r02a/probe.txt) timed on the host with OpenMP over
     cpu_threads() threads, on the same frame and settings as the GPU line.
@@ -176,17 +205,31 @@ def cpu_baseline(img, distance, effort, proposals, coder, gpu_bytes):
     import oracle_ffi  # the checker, timed here only as the reported baseline
 
     oracle_ffi.build()
-    n = oracle_ffi.set_threads(cpu_threads())
-    t = time.perf_counter()
-    r = oracle_ffi.encode(img, distance, effort, proposals, coder)
-    dt = time.perf_counter() - t
     h, w, _ = img.shape
-    return {"value": round(w * h / 1e6 / dt, 3), "unit": "MPix/s", "cores": n, "kind": "port",
-            "nproc": os.cpu_count(), "affinity": cpu_threads(),
-            "sample": "one full %dx%d frame (the bench frame), oracle/ C restatement with OpenMP "
-                      "on all %d cores of the process's affinity (nproc %s; libjxl/cjxl absent "
-                      "on the box), %.2f s" % (w, h, n, os.cpu_count(), dt),
-            "bytes_equal_gpu": gpu_bytes is not None and r.bytes == gpu_bytes}
+
+    def timed(threads):
+        n = oracle_ffi.set_threads(threads)
+        t = time.perf_counter()
+        r = oracle_ffi.encode(img, distance, effort, proposals, coder)
+        return n, time.perf_counter() - t, r
+
+    n, dt, r = timed(cpu_threads())
+    res = {"value": round(w * h / 1e6 / dt, 3), "unit": "MPix/s", "cores": n, "kind": "port",
+           "nproc": os.cpu_count(), "affinity": cpu_affinity(), "cgroup_quota_cpus": cpu_quota(),
+           "sample": "one full %dx%d frame (the bench frame), oracle/ C restatement with OpenMP "
+                     "on %d threads = the process's CPU affinity (%d) capped by its cgroup CPU "
+                     "quota (%s; nproc %s; libjxl/cjxl absent on the box), %.2f s"
+                     % (w, h, n, cpu_affinity(), cpu_quota(), os.cpu_count(), dt),
+           "bytes_equal_gpu": gpu_bytes is not None and r.bytes == gpu_bytes}
+    if sweep:
+        # threads vs throughput (one frame each, same bytes)
+        res["sweep"] = {}
+        for th in sweep:
+            n2, dt2, r2 = timed(th)
+            res["sweep"][str(n2)] = round(w * h / 1e6 / dt2, 3)
+            assert r2.bytes == r.bytes
+        oracle_ffi.set_threads(n)
+    return res
 
 
 def quality_probe(enc, img, distance, effort):
@@ -221,6 +264,21 @@ def quality_probe(enc, img, distance, effort):
     return res
 
 
+def spawn_ranks(n, argv):
+    """Run this script as n ranks under torch.distributed.run (one node,
+    rendezvous on 127.0.0.1) in a child process; returns its exit status."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+           str(n), "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -233,14 +291,13 @@ def main():
     ap.add_argument("--distance", type=float, default=1.0)
     ap.add_argument("--effort", type=int, default=7)
     ap.add_argument("--proposals", type=int, default=0)
-    ap.add_argument("--mode", choices=("shard", "shard-native", "shard-sync", "replica"),
+    ap.add_argument("--mode", choices=("shard", "shard-sync", "replica"),
                     default="shard",
                     help="N > 1: shard = every frame's pass groups split over the ranks, "
-                         "streamed (HostShardStream; BASELINE config 2 as written); "
-                         "shard-native = the same with the library's completion thread "
-                         "(ShardStream); shard-sync = the same one frame at a time "
-                         "(encode_sharded); replica = every rank "
-                         "streams its own frames (frame-level data parallelism)")
+                         "streamed (jxg.dist.ShardStream; BASELINE config 2 as written); "
+                         "shard-sync = the same one frame at a time (encode_sharded); "
+                         "replica = every rank streams its own frames (frame-level data "
+                         "parallelism)")
     ap.add_argument("--alt-replica", type=int, default=1,
                     help="shard mode, N > 1: also time frame replicas (reported under "
                          "'replicas')")
@@ -268,11 +325,23 @@ def main():
                     help="also time the workload with the thesis proposals P+F "
                          "(reported under 'thesis_proposals'; 0 = off)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sweep", default="",
+                    help="comma-separated OpenMP thread counts: also time the CPU baseline at "
+                         "each (reported under cpu_baseline.sweep)")
     ap.add_argument("--no-quality", action="store_true",
                     help="skip the untimed decode-PSNR probe")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    # one process per GPU: with WORLD_SIZE unset, --gpus N > 1 starts the N
+    # ranks itself (before this process touches the GPU); a launcher's
+    # WORLD_SIZE must agree with --gpus
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    if env_world is not None and int(env_world) != args.gpus:
+        print("bench.py: WORLD_SIZE=%s but --gpus %d" % (env_world, args.gpus), file=sys.stderr)
+        sys.exit(2)
+    world = int(env_world or "1")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # JXG_DIST_BACKEND=gloo rehearses the multi-rank path with host-staged
@@ -288,7 +357,7 @@ def main():
         else:
             dist.init_process_group(backend)
     name, w, h, nframes = CONFIGS[args.config]
-    sharded_mode = world > 1 and args.mode in ("shard", "shard-native", "shard-sync")
+    sharded_mode = world > 1 and args.mode in ("shard", "shard-sync")
     strong = sharded_mode and args.scaling == "strong"
     fh = h if strong or not sharded_mode else h * world
     # inputs generated on the device (jxg_synth_rgb8_device: the bytes of
@@ -315,8 +384,8 @@ def main():
 
     def run(mode, coder, nstreams=1, proposals=None, pipe=True):
         """Warm up, then time args.steps steps of `mode` ("frames": each rank
-        encodes whole frames -- N = 1 / replicas; "shard": HostShardStream;
-        "shard-native": ShardStream; "shard-sync": encode_sharded)."""
+        encodes whole frames -- N = 1 / replicas; "shard": ShardStream;
+        "shard-sync": encode_sharded)."""
         sharded = mode != "frames"
         per_step, d_imgs = make_frames(sharded)
         nd = len(d_imgs)
@@ -339,9 +408,9 @@ def main():
         ss = None
         host = None
         bufs = {}
-        if mode in ("shard", "shard-native"):
-            from jxg.dist import HostShardStream, ShardStream
-            ss = (HostShardStream if mode == "shard" else ShardStream)(encs[0], w, fh, rank, world)
+        if mode == "shard":
+            from jxg.dist import ShardStream
+            ss = ShardStream(encs[0], w, fh, rank, world)
         elif mode == "shard-sync" and args.assembly == "host":
             from jxg.dist import SharedHostBuffer
             if SharedHostBuffer.single_node():
@@ -395,6 +464,8 @@ def main():
             worker(e, range(max(nw, 16) if (pipe or ss is not None) else args.warmup * per_step))
         for key in ("front_ms", "host_ms", "sizes"):
             rec[key] = []
+        if ss is not None:
+            ss.wait_s = 0.0
 
         total = args.steps * per_step
         share = [list(range(i, total, nstreams)) for i in range(nstreams)]
@@ -412,6 +483,8 @@ def main():
             for t in ths:
                 t.join()
         torch.cuda.synchronize()
+        dt_own = time.perf_counter() - t0  # this rank's own work, before the barrier
+        wait_own = ss.wait_s if ss is not None else 0.0
         if world > 1:
             dist.barrier()
         dt = time.perf_counter() - t0
@@ -420,6 +493,13 @@ def main():
                               device="cpu" if backend == "gloo" else dev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             dt = float(tt.item())
+            # per-rank time and the time it spent waiting for the other ranks
+            # (ShardStream: heads, slots, frames) -> rank 0
+            mine = torch.tensor([dt_own, wait_own], dtype=torch.float64,
+                                device="cpu" if backend == "gloo" else dev)
+            allr = [torch.zeros_like(mine) for _ in range(world)]
+            dist.all_gather(allr, mine)
+            rec["per_rank"] = [(float(x[0]), float(x[1])) for x in allr]
         rec["dt"] = dt
         rec["per_step"] = per_step
         rec["st"] = encs[0].stats()
@@ -427,7 +507,6 @@ def main():
         rec["last"] = last.tobytes() if hasattr(last, "tobytes") else last
         if ss is not None:
             ss.close()
-            rec["ms_wait_ranks"] = getattr(ss, "ms_wait_ranks", None)
         for e in encs[1:]:
             e.close()
         rec["enc"] = encs[0]
@@ -472,7 +551,7 @@ def main():
                         "bytes_per_frame": P["sizes"][-1]}
         P["enc"].close()
     iso = None
-    streamed = mode in ("shard", "shard-native")
+    streamed = mode == "shard"
     if mode == "frames" and pipeline or streamed:
         # the kernels alone on the GPU (one-at-a-time encodes of this rank's
         # frame, same coder): the front kernel's roofline, the rANS chain
@@ -512,9 +591,8 @@ def main():
                         "partition kind %d), %s"
                         % (name, w, fh, distinct, args.distance, args.effort, args.proposals,
                            coder_desc, world, args.scaling, jxg.shard_plan(w, fh, world)[2],
-                           "streamed (jxg.dist.%s, %d frames in flight per rank, heads "
-                           "and sections through /dev/shm)"
-                           % ("HostShardStream" if mode == "shard" else "ShardStream", R["depth"])
+                           "streamed (jxg.dist.ShardStream, %d frames in flight per rank, heads "
+                           "and sections through /dev/shm)" % R["depth"]
                            if streamed else
                            "one frame at a time (encode_sharded), %s assembly" % args.assembly))
             par = "group-shard%d" % world
@@ -602,16 +680,19 @@ def main():
             res["thesis_proposals"] = thesis
         if replicas is not None:
             res["replicas"] = replicas
-        if R.get("ms_wait_ranks") is not None:
-            # rank 0's completion thread: time spent waiting for the other
-            # ranks' heads over warmup + timed frames (their critical path)
-            res["ms_wait_ranks_rank0"] = round(R["ms_wait_ranks"], 2)
+        if R.get("per_rank"):
+            # every rank's own time per step (before the closing barrier) and the
+            # time per step it waited for the other ranks (ShardStream: heads,
+            # slots, frames), over the timed steps
+            res["per_rank_ms_per_step"] = [round(a * 1e3 / args.steps, 3) for a, _ in R["per_rank"]]
+            res["ms_wait_ranks"] = [round(b * 1e3 / args.steps, 3) for _, b in R["per_rank"]]
         if world == 1 and not args.no_quality:
             res["quality"] = quality_probe(R["enc"], img, args.distance, args.effort)
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(img, args.distance, args.effort, args.proposals,
                                                1 if args.coder == "ans" else 0,
-                                               R["last"])
+                                               R["last"],
+                                               [int(x) for x in args.cpu_sweep.split(",") if x])
         print(json.dumps(res), flush=True)
     R["enc"].close()
     if world > 1:

@@ -153,14 +153,7 @@ jxg_status jxg_encode_batch_rgb8_device(void* ctx, const void* const* d_rgbs, ui
  * submitted and not yet received.  A device frame must stay unchanged until
  * its codestream is received; a host frame is copied into pinned staging
  * before jxg_submit_rgb8 returns.  jxg_get_stats after jxg_receive describes
- * the received frame.  On an error every frame in flight is dropped.
- * Two optional modes, same bytes, off by default (measured without gain,
- * DESIGN.md §3.7): JXG_PIPE_BATCH=K (environment, 2..8) -- lane batches for
- * ANS frames of at most 128 pass groups: K frames per lane share its stream
- * and their rANS chains go out as one launch, the depth becomes lanes x K
- * (jxg_pipeline_depth reports it), completion runs on one extra assembly
- * stream; JXG_PIPE_WORKERS=N -- N threads assemble completed frames (layout,
- * concat, codestream D2H) instead of the submitting thread. */
+ * the received frame.  On an error every frame in flight is dropped. */
 jxg_status jxg_submit_rgb8(void* ctx, const uint8_t* rgb, uint32_t xsize, uint32_t ysize,
                            size_t row_stride);
 jxg_status jxg_submit_rgb8_device(void* ctx, const void* d_rgb, uint32_t xsize, uint32_t ysize,
@@ -270,45 +263,8 @@ jxg_status jxg_shard_submit_device(void* ctx, const void* d_rgb, uint32_t xsize,
 jxg_status jxg_shard_next_head(void* ctx, uint32_t* dst, size_t* nwords);
 jxg_status jxg_shard_write_next(void* ctx, const uint32_t* const* heads, const size_t* head_words,
                                 uint32_t n, void* dst, size_t dst_size, size_t* total);
-/* Streaming shards with the per-frame host work in the library (the
- * multi-GPU pipeline as bench.py runs it): the same frames and lanes as
- * above, but a completion thread per context takes each frame in order --
- * waits for its sections, publishes its payload head in `region`, waits for
- * every rank's head of that frame there, DMAs its sections into the frame's
- * codestream slot (rank 0 adds headers + TOC) and marks the frame done.  The
- * ranks synchronise through `region` only (64-bit sequence words, no
- * collective, no caller work per frame).
- *   region: one host mapping shared by all ranks of the node (e.g. a
- *     /dev/shm file), 4096-aligned, jxg_shard_stream_region_size bytes,
- *     page-locked with jxg_host_register in each process; rank 0 passes
- *     init = 1 and must return from begin before the other ranks call it
- *     (any barrier).  slots >= 3 codestream slots of slot_bytes each (a frame
- *     over its slot fails the stream with JXG_ERR_OOM).
- *   submit: this rank's shard of the next frame (device RGB8 of the begin
- *     geometry, ordered by jxg_set_input_stream, unchanged until received);
- *     blocks while jxg_pipeline_depth frames are in flight.
- *   ready: frames receivable without waiting.
- *   receive: the oldest frame (blocking): rank 0 gets the codestream at
- *     region + *offset, *bytes long, valid until its next receive; other
- *     ranks get 0 / 0.  Frame k's slot is reused only after rank 0 has
- *     received frame k - slots + 1, so rank 0 must keep receiving (a rank
- *     submitting more than depth + slots - 2 frames ahead of rank 0's
- *     receives times out with JXG_ERR_INTERNAL after 120 s).
- *   end: stops the completion thread (JXG_ERR_INVALID_ARG if frames were
- *     still pending: they are dropped); *ms_wait_ranks (optional) = time the
- *     completion thread spent waiting for other ranks' heads.
- * While a stream is open every other encode entry point on the context
- * returns JXG_ERR_INVALID_ARG.  world > 1 needs ANS and a partition of kind
- * 0 or 1 (JXG_ERR_UNSUPPORTED otherwise). */
-size_t jxg_shard_stream_region_size(void* ctx, uint32_t xsize, uint32_t ysize, uint32_t world,
-                                    uint32_t slots, size_t slot_bytes);
-jxg_status jxg_shard_stream_begin(void* ctx, void* region, size_t region_size, uint32_t xsize,
-                                  uint32_t ysize, size_t row_stride, uint32_t rank,
-                                  uint32_t world, uint32_t slots, size_t slot_bytes, int init);
-jxg_status jxg_shard_stream_submit(void* ctx, const void* d_rgb);
-jxg_status jxg_shard_stream_ready(void* ctx, uint32_t* n);
-jxg_status jxg_shard_stream_receive(void* ctx, size_t* offset, size_t* bytes);
-jxg_status jxg_shard_stream_end(void* ctx, float* ms_wait_ranks);
+/* page-lock a host range (e.g. the node-shared /dev/shm codestream buffer of
+ * jxg_shard_write_host / jxg_shard_write_next) so the ranks' D2H copies are DMA */
 jxg_status jxg_host_register(void* ptr, size_t size);
 jxg_status jxg_host_unregister(void* ptr);
 

@@ -535,8 +535,7 @@ constexpr int kAnsWaves = JXG_ANS_WAVES;
 __device__ __forceinline__ uint32_t wave_ror1(uint32_t x) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x13C, 0xF, 0xF, false);
 }
-// blk: the chain workgroup's index within its frame (ans_encode_kernel: one
-// frame per launch; ans_encode_multi_kernel: the frames of a chain batch)
+// blk: the chain workgroup's index within its frame
 __device__ __forceinline__ void ans_chain(const AnsArgs& a, uint32_t blk) {
   __shared__ uint32_t sSym[kAnsHists * 128];
   __shared__ uint32_t sInv[kAnsHists * 4096 / 2];  // u16 pairs
@@ -639,22 +638,6 @@ __device__ __forceinline__ void ans_chain(const AnsArgs& a, uint32_t blk) {
 __global__ __launch_bounds__(kAnsWaves * 64) void ans_encode_kernel(AnsArgs a) {
   ans_chain(a, blockIdx.x);
 }
-// A chain batch: the chains of several frames (pipeline lanes) in one launch,
-// so they run side by side and the batch lasts as long as its longest group.
-// wg[b] = frame << 20 | the workgroup's index within that frame.
-__global__ __launch_bounds__(kAnsWaves * 64) void ans_encode_multi_kernel(const AnsArgs* frames,
-                                                                         const uint32_t* wg) {
-  const uint32_t m = __builtin_amdgcn_readfirstlane(wg[blockIdx.x]);
-  const AnsArgs a = frames[m >> 20];
-  ans_chain(a, m & 0xFFFFFu);
-}
-
-__global__ __launch_bounds__(kAnsWaves * 64) void ans_encode_batch_kernel(AnsBatch b) {
-  uint32_t i = 0;
-  while (i + 1 < b.nf && blockIdx.x >= b.wg0[i + 1]) i++;
-  ans_chain(b.f[i], blockIdx.x - b.wg0[i]);
-}
-
 // bit placement: the 32-bit state, then every record's bits, in order; a
 // contiguous record range per wave, coalesced reads, wave scans of the
 // lengths (as ac_emit)
@@ -725,15 +708,6 @@ void launch_ans(const AnsArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(ans_encode_kernel, dim3((n + kAnsWaves - 1) / kAnsWaves), dim3(kAnsWaves * 64),
                      0, s, a);
   hipLaunchKernelGGL(ans_emit_kernel, dim3(n), dim3(kAcThreads), 0, s, a);
-}
-uint32_t ans_chain_wgs(uint32_t ngroups) { return (ngroups + kAnsWaves - 1) / kAnsWaves; }
-void launch_ans_multi(const AnsArgs* d_frames, const uint32_t* d_wg, uint32_t nwg, hipStream_t s) {
-  if (nwg)
-    hipLaunchKernelGGL(ans_encode_multi_kernel, dim3(nwg), dim3(kAnsWaves * 64), 0, s, d_frames, d_wg);
-}
-void launch_ans_batch(const AnsBatch& b, hipStream_t s) {
-  if (b.nf && b.wg0[b.nf])
-    hipLaunchKernelGGL(ans_encode_batch_kernel, dim3(b.wg0[b.nf]), dim3(kAnsWaves * 64), 0, s, b);
 }
 void launch_ans_emit(const AnsArgs& a, hipStream_t s) {
   if (a.n) hipLaunchKernelGGL(ans_emit_kernel, dim3(a.n), dim3(kAcThreads), 0, s, a);

@@ -600,7 +600,10 @@ void write_size(BitWriter& w, uint32_t v) {
 
 uint32_t lf_code(uint32_t flags, float distance) {
   uint32_t c = (flags & JXG_FLAG_GABORISH) ? 1u : 0u;
-  if (flags & JXG_FLAG_EPF) c |= (distance < 1.5f ? 1u : (distance < 4.0f ? 2u : 3u)) << 1;
+  // EPF iterations by distance (cjxl --epf=-1, libjxl's thresholds 0.7 / 1.5 /
+  // 4.0 as recalled [ext, unpinned]): none below d 0.7, then 1 / 2 / 3
+  if (flags & JXG_FLAG_EPF)
+    c |= (distance < 0.7f ? 0u : (distance < 1.5f ? 1u : (distance < 4.0f ? 2u : 3u))) << 1;
   return c;
 }
 

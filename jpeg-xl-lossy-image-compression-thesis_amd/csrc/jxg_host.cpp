@@ -485,11 +485,7 @@ struct CtxDeleter {
 struct Ctx {
   jxg_params params{};
   std::vector<std::unique_ptr<Ctx, CtxDeleter>> lanes;
-  // lane batches (pipe_submit, small frames): D physical lanes x K slots, the
-  // slots of a lane share its leader's stream (blanes_k = K they were built for)
-  std::vector<std::unique_ptr<Ctx, CtxDeleter>> blanes;
-  uint32_t blanes_k = 0;
-  PinBuf<uint8_t> h_stage;  // pinned staging of one host frame (batch lanes)
+  PinBuf<uint8_t> h_stage;  // pinned staging of one host frame (pipeline lanes)
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;  // AC-block concat + D2H (stage_concat_split)
   // ev[6]: AC statistics downloaded (stage_download_ac); ev[7]: AC emission
@@ -564,22 +560,8 @@ struct Ctx {
   hipStream_t in_stream = nullptr;
   hipEvent_t ev_in = nullptr;
   bool owned_lane = false;  // a pipeline / batch lane of another context
-  // streaming pipeline (ANS): the rANS chains go to the pipeline's chain
-  // batcher instead of this context's stream (ev_up: codes uploaded)
-  struct ChainBatcher* batcher = nullptr;
-  hipEvent_t ev_up = nullptr;
-  // lane batches (pipe_submit, small frames): this slot's chain is launched
-  // with the other slots of its physical lane; `stream` may be the lane
-  // leader's (stream_borrowed: not destroyed here); completion (concat + D2H)
-  // runs on the pipeline's assembly stream
-  bool defer_chain = false;
-  bool stream_borrowed = false;
-  hipStream_t asm_stream = nullptr;
-  DevBuf<uint8_t> d_cdesc;  // leader: chain descriptors per slot [AnsArgs K][wg map]
-  PinBuf<uint8_t> h_cdesc;
   std::unique_ptr<struct Job> job;  // sharded encode in flight (begin -> end)
   std::unique_ptr<struct Pipe> pipe;  // streaming encode (jxg_submit_* / jxg_receive)
-  std::unique_ptr<struct SStream> ss; // streaming shards over a shared region (jxg_shard_stream_*)
   std::vector<uint32_t> payload_head;  // last jxg_shard_end: payload head words
   size_t payload_body = 0;             //   and body bytes (in `out`)
 };
@@ -835,9 +817,6 @@ static void build_rows(const Frame& f, const Plan& P, std::vector<LfRow>& rows,
 static float elapsed(hipEvent_t a, hipEvent_t b) {
   float ms = 0.0f;
   (void)hipEventElapsedTime(&ms, a, b);
-#ifdef JXG_PIPE_LEAN
-  (void)hipGetLastError();  // (the unrecorded markers' error)
-#endif
   return ms;
 }
 
@@ -873,188 +852,13 @@ struct Job {
   uint8_t* host_out = nullptr;
   size_t out_bytes = 0;
   float ms_finish_layout = 0.0f;
-  // chain batcher: set once this frame's chains, bit placement and group bit
-  // counts are enqueued (then ev[7] of its context marks them done)
-  std::shared_future<jxg_status> chain;
-  // lane batches (small frames, pipe_submit): stage_emit leaves the rANS
-  // chain to the lane's batch launch (lane_batch_launch), which then places
-  // the bits and downloads the bit counts
-  AnsArgs na{};
-  bool chain_deferred = false, chain_launched = false;
 };
 
-// ---------------------------------------------------------------------------
-// Chain batches (streaming pipeline, ANS).  A frame's rANS chains last as
-// long as its longest pass group's (≈ 5 ms at 256×256 groups, whatever the
-// frame size), so with one chain launch per frame on the frame's own lane a
-// lane is held ≥ 5 ms per frame and small frames (1080p: 40 groups; a rank's
-// 1/8 of an 8K frame: 64) are bound by lanes / latency, not by the GPU.  The
-// pipeline's batcher thread instead launches the chains of every frame whose
-// codes are uploaded as ONE kernel (ans_encode_multi_kernel) on its own
-// stream, each time the previous batch has finished, then each frame's bit
-// placement and group bit counts; the lanes never wait on a chain.
-// ---------------------------------------------------------------------------
-struct ChainEntry {
-  Ctx* lane = nullptr;
-  AnsArgs na{};
-  uint32_t ngroups = 0;
-  std::promise<jxg_status> enq;
-};
-struct ChainBatcher {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  hipEvent_t ev_batch = nullptr;
-  bool have_prev = false;
-  DevBuf<uint8_t> d_desc;  // [AnsArgs frames][u32 workgroup map]
-  PinBuf<uint8_t> h_desc;
-  std::mutex mu;
-  std::condition_variable cv;
-  std::deque<std::unique_ptr<ChainEntry>> pending;
-  bool stop = false;
-  std::thread th;
-  uint64_t batches = 0, frames = 0;  // (profile)
-};
-// Measured slower than per-lane chains at every size tried (1/8 of an 8K
-// frame, 64 x 1080p, 8K; with 12 to 28 lanes, profiles/r03_stream): off
-// unless JXG_CHAIN_BATCH=1.
-static bool chain_batch_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("JXG_CHAIN_BATCH");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-static jxg_status chain_launch(ChainBatcher& B, std::vector<std::unique_ptr<ChainEntry>>& batch) {
-  const size_t nf = batch.size();
-  std::vector<uint32_t> wg;
-  for (size_t i = 0; i < nf; i++)
-    for (uint32_t w = 0; w < ans_chain_wgs(batch[i]->na.n); w++) wg.push_back((uint32_t)i << 20 | w);
-  const size_t fb = (nf * sizeof(AnsArgs) + 255) & ~(size_t)255, total = fb + wg.size() * 4 + 4;
-  // (the previous batch has finished: its descriptors are free)
-  JXG_HIP(B.h_desc.ensure(total));
-  JXG_HIP(B.d_desc.ensure(total));
-  for (size_t i = 0; i < nf; i++)
-    std::memcpy(B.h_desc.p + i * sizeof(AnsArgs), &batch[i]->na, sizeof(AnsArgs));
-  if (!wg.empty()) std::memcpy(B.h_desc.p + fb, wg.data(), wg.size() * 4);
-  JXG_HIP(hipMemcpyAsync(B.d_desc.p, B.h_desc.p, total, hipMemcpyHostToDevice, B.stream));
-  for (auto& e : batch) JXG_HIP(hipStreamWaitEvent(B.stream, e->lane->ev_up, 0));
-  launch_ans_multi(reinterpret_cast<const AnsArgs*>(B.d_desc.p),
-                   reinterpret_cast<const uint32_t*>(B.d_desc.p + fb), (uint32_t)wg.size(), B.stream);
-  JXG_HIP(hipGetLastError());
-  for (auto& e : batch) {
-    launch_ans_emit(e->na, B.stream);
-    JXG_HIP(hipGetLastError());
-    Ctx* L = e->lane;
-    JXG_HIP(hipMemcpyAsync(L->h_gbits.p, L->gbits.p, (size_t)e->ngroups * 4, hipMemcpyDeviceToHost,
-                           B.stream));
-    JXG_HIP(hipEventRecord(L->ev[7], B.stream));
-  }
-  JXG_HIP(hipEventRecord(B.ev_batch, B.stream));
-  B.have_prev = true;
-  B.batches++;
-  B.frames += nf;
-  return JXG_OK;
-}
-static void chain_thread(ChainBatcher* B) {
-  (void)hipSetDevice(B->device);
-  for (;;) {
-    {
-      std::unique_lock<std::mutex> lk(B->mu);
-      B->cv.wait(lk, [&] { return B->stop || !B->pending.empty(); });
-      if (B->pending.empty()) return;  // stopped and drained
-    }
-    // let the running batch finish: the frames that arrive meanwhile join
-    // the next one
-    if (B->have_prev) (void)hipEventSynchronize(B->ev_batch);
-    std::vector<std::unique_ptr<ChainEntry>> batch;
-    {
-      std::lock_guard<std::mutex> lk(B->mu);
-      while (!B->pending.empty()) {
-        batch.push_back(std::move(B->pending.front()));
-        B->pending.pop_front();
-      }
-    }
-    const jxg_status st = chain_launch(*B, batch);
-    for (auto& e : batch) e->enq.set_value(st);
-  }
-}
-static std::unique_ptr<ChainBatcher> chain_batcher_create(int device) {
-  std::unique_ptr<ChainBatcher> B(new (std::nothrow) ChainBatcher());
-  if (!B) return nullptr;
-  B->device = device;
-  if (hipStreamCreateWithFlags(&B->stream, hipStreamNonBlocking) != hipSuccess) return nullptr;
-  if (hipEventCreateWithFlags(&B->ev_batch, hipEventDisableTiming) != hipSuccess) {
-    (void)hipStreamDestroy(B->stream);
-    return nullptr;
-  }
-  try {
-    B->th = std::thread(chain_thread, B.get());
-  } catch (...) {
-    (void)hipEventDestroy(B->ev_batch);
-    (void)hipStreamDestroy(B->stream);
-    return nullptr;
-  }
-  return B;
-}
-// drain (every queued frame's chains are launched) and stop
-static void chain_batcher_destroy(std::unique_ptr<ChainBatcher>& B) {
-  if (!B) return;
-  {
-    std::lock_guard<std::mutex> lk(B->mu);
-    B->stop = true;
-    B->cv.notify_all();
-  }
-  if (B->th.joinable()) B->th.join();
-  (void)hipStreamSynchronize(B->stream);
-  (void)hipEventDestroy(B->ev_batch);
-  (void)hipStreamDestroy(B->stream);
-  if (const char* e = std::getenv("JXG_CHAIN_PROFILE"))
-    if (e[0] == '1' && B->batches)
-      std::fprintf(stderr, "chain batches: %llu, %.2f frames per batch\n",
-                   (unsigned long long)B->batches, (double)B->frames / (double)B->batches);
-  B.reset();
-}
-static std::shared_future<jxg_status> chain_submit(ChainBatcher* B, Ctx* lane, const AnsArgs& na,
-                                                   uint32_t ngroups) {
-  std::unique_ptr<ChainEntry> e(new ChainEntry());
-  e->lane = lane;
-  e->na = na;
-  e->ngroups = ngroups;
-  std::shared_future<jxg_status> f = e->enq.get_future().share();
-  std::lock_guard<std::mutex> lk(B->mu);
-  B->pending.push_back(std::move(e));
-  B->cv.notify_all();
-  return f;
-}
 // the emission of J on c is done and its bit counts are on the host
 static jxg_status wait_emission(Ctx* c, Job& J) {
-  if (J.chain_deferred) {  // a lane-batch slot: its stream carries other slots' work
-    if (!J.chain_launched) return JXG_ERR_INTERNAL;
-    JXG_HIP(hipEventSynchronize(c->ev[3]));
-    return JXG_OK;
-  }
-  if (J.chain.valid()) {
-    const jxg_status st = J.chain.get();
-    J.chain = std::shared_future<jxg_status>();
-    if (st) return st;
-    JXG_HIP(hipEventSynchronize(c->ev[7]));
-  }
+  (void)J;
   JXG_HIP(hipStreamSynchronize(c->stream));
   return JXG_OK;
-}
-// non-blocking: 1 done, 0 not yet, < 0 error
-static int emission_done(Ctx* c, Job& J) {
-  if (J.chain_deferred && !J.chain_launched) return 0;
-  if (J.chain.valid()) {
-    if (J.chain.wait_for(std::chrono::seconds(0)) != std::future_status::ready) return 0;
-    if (J.chain.get()) return -1;
-    const hipError_t q = hipEventQuery(c->ev[7]);
-    if (q == hipErrorNotReady) return 0;
-    if (q != hipSuccess) return -1;
-  }
-  const hipError_t q = hipEventQuery(c->ev[3]);
-  if (q == hipErrorNotReady) return 0;
-  return q == hipSuccess ? 1 : -1;
 }
 
 // ---- stage A: buffers for the frame / plan ----
@@ -1296,9 +1100,7 @@ static jxg_status stage_front(Ctx* c, Job& J) {
   else if (J.plan.world == 1)
     launch_front(fa, f.tiles_x, f.tiles_y, s);
   JXG_HIP(hipGetLastError());
-#ifndef JXG_PIPE_LEAN  // (experiment: no timing markers)
   JXG_HIP(hipEventRecord(c->ev[5], s));  // end of the front kernel alone
-#endif
   if (J.max_s) {
     MergeArgs ma{};
     ma.xyb = c->xyb_tiles.p;
@@ -1636,26 +1438,15 @@ static jxg_status stage_emit(Ctx* c, Job& J, bool sync = true) {
     na.n = J.plan.ng();
     na.glist = J.aa.glist;
     na.order = c->ans_order.p;
-    if (c->defer_chain) {  // the lane batch launches it (lane_batch_launch)
-      J.na = na;
-      J.chain_deferred = true;
-      J.chain_launched = false;
-    } else if (c->batcher) {  // the pipeline's chain batcher (group bit counts: its D2H)
-      if (!c->ev_up) JXG_HIP(hipEventCreateWithFlags(&c->ev_up, hipEventDisableTiming));
-      JXG_HIP(hipEventRecord(c->ev_up, s));
-      J.chain = chain_submit(c->batcher, c, na, f.ngroups);
-    } else {
-      launch_ans(na, s);
-      JXG_HIP(hipGetLastError());
-    }
+    launch_ans(na, s);
+    JXG_HIP(hipGetLastError());
   }
   J.la.scratch = c->lf_scratch;
   if (J.nchunks) launch_lf_bits(J.la, J.nchunks, s);
   launch_lf_scan(J.la, J.nstreams, s);
   if (J.nchunks) launch_lf_emit(J.la, J.nchunks, s);
   JXG_HIP(hipGetLastError());
-  if (J.chain_deferred) return JXG_OK;  // bit counts and ev[3] after the batch's chains
-  if (J.ans && !J.chain.valid()) {  // [gbits | stream_bits]: one copy
+  if (J.ans) {  // [gbits | stream_bits]: one copy
     JXG_HIP(hipMemcpyAsync(c->h_bits.p, c->bits.p, ((size_t)f.ngroups + J.nstreams) * 4,
                            hipMemcpyDeviceToHost, s));
     JXG_HIP(hipEventRecord(c->ev[7], s));
@@ -1681,7 +1472,7 @@ struct Piece {
 static jxg_status stage_concat(Ctx* c, Job& J, bool full, std::vector<uint32_t>* section_ids,
                                std::vector<uint32_t>* section_bytes, uint8_t** host_out,
                                size_t* out_bytes) {
-  hipStream_t s = c->asm_stream ? c->asm_stream : c->stream;  // (lane batches: assembly stream)
+  hipStream_t s = c->stream;
   const Frame& f = J.f;
   std::vector<std::vector<Piece>> sections;
   std::vector<uint32_t> ids;
@@ -1778,9 +1569,7 @@ static jxg_status stage_concat(Ctx* c, Job& J, bool full, std::vector<uint32_t>*
     out_release(ho);
     return JXG_ERR_HIP;
   }
-#ifndef JXG_PIPE_LEAN
   JXG_HIP(hipEventRecord(c->ev[4], s));
-#endif
   if (host_out) *host_out = ho;
   *out_bytes = nbytes;
   if (section_ids) *section_ids = ids;
@@ -1799,11 +1588,6 @@ static jxg_status stage_concat_split(Ctx* c, Job& J, uint8_t** host_out, size_t*
     return JXG_ERR_HIP;  // created on first use: only lone contexts take this path
   hipStream_t s = c->stream, s2 = c->stream2;
   const Frame& f = J.f;
-  if (J.chain.valid()) {  // (a chain batch records ev[7] once it has enqueued this frame)
-    const jxg_status st = J.chain.get();
-    J.chain = std::shared_future<jxg_status>();
-    if (st) return st;
-  }
   JXG_HIP(hipEventSynchronize(c->ev[7]));  // AC emission done, its bit counts on the host
   const uint32_t g0 = J.plan.g0(), ng = J.plan.ng();  // (one context: all groups)
   JXG_HIP(c->h_pieces_ac.ensure(std::max<uint32_t>(ng, 1)));
@@ -1963,13 +1747,9 @@ static jxg_status enc_launch(Ctx* c, Job& J, const uint8_t* d_rgb, uint32_t w, u
   jxg_status st = stage_alloc(c, J);
   if (st) return st;
   J.presets = J.ans && world > 1;
-#ifndef JXG_PIPE_LEAN
   JXG_HIP(hipEventRecord(c->ev[0], s));
-#endif
   if ((st = stage_front(c, J))) return st;
-#ifndef JXG_PIPE_LEAN
   JXG_HIP(hipEventRecord(c->ev[1], s));
-#endif
   if ((st = stage_ac_stats(c, J))) return st;
   if ((st = stage_download_ac(c, J, c->hist_ac.p))) return st;
   if ((st = stage_lf_stats(c, J))) return st;
@@ -2006,7 +1786,7 @@ static jxg_status enc_finish_start(Ctx* c, Job& J, bool split) {
   return JXG_OK;
 }
 static jxg_status enc_finish_end(Ctx* c, Job& J, jxg_buffer* out, Clock::time_point t_call) {
-  hipStream_t s = c->asm_stream ? c->asm_stream : c->stream;
+  hipStream_t s = c->stream;
   const jxg_params& P = c->params;
   const Frame& f = J.f;
   const size_t nb = (size_t)f.bxs * f.bys;
@@ -2078,19 +1858,14 @@ static jxg_status enc_finish(Ctx* c, Job& J, bool split, jxg_buffer* out,
 }
 
 static bool pipe_busy(const Ctx* c);
-static jxg_status lane_batch_launch(Ctx* c, uint32_t lead, bool force);
-// a lane of another context: its own stream, or (borrow) a lane-batch
-// leader's; not counted in g_live_ctx
-static jxg_status ctx_new_lane(const jxg_params& params, hipStream_t borrow, Ctx** out) {
+// a lane of another context (its own stream); not counted in g_live_ctx
+static jxg_status ctx_new_lane(const jxg_params& params, Ctx** out) {
   *out = nullptr;
   Ctx* c = new (std::nothrow) Ctx();
   if (!c) return JXG_ERR_OOM;
   c->params = params;
   c->owned_lane = true;
-  if (borrow) {
-    c->stream = borrow;
-    c->stream_borrowed = true;
-  } else if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return JXG_ERR_HIP;
   }
@@ -2122,42 +1897,22 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
 // streaming encode (jxg_submit_rgb8[_device] / jxg_receive): a software
 // pipeline over D lanes (the caller's context plus lanes it owns, one stream
 // each), driven by the caller's one host thread.  submit(j):
-//   finish the oldest frame if D are in flight (wait for its emission,
-//   assemble, codestream to the host) -> launch frame j's front end, merge
-//   stage and statistics on a free lane; frame j-1's codes (host work:
-//   clustering, ANS / prefix tables, headers, LF-group codes) start on a
-//   helper thread, and the codes of frame j-lag are joined (its emission is
-//   launched by then).
-// So the rANS chains of the D - 2 frames before j (latency-bound waves that use
-// little of their SIMDs; 68 KB of LDS per CU) run while frame j's transform
-// kernels fill the rest of the chip.  A frame's chain lasts as long as its
-// longest pass group's, whatever the frame size, so the depth follows the
-// frame: ~3570 pass groups in flight (8K: 7 lanes, 4 % faster than 5 at 100
-// frames), at least 4, up to kPipeMaxLanes for small frames (a
-// 1080p frame has 40 groups: 40 chain waves on a 1024-SIMD chip).  The lag follows
-// it too: 1 for large frames (the codes of j-1 are joined in submit(j): the
-// GPU is the bound), 3 for small ones, whose host work per frame (0.5 ms of
-// ANS codes, 0.6 ms of launches and assembly) is the bound: three helpers run
-// at once and each has two submit periods (64 x 1080p ANS: lag 1 2.2, lag 2
-// 2.5, lag 3 2.7 GPix/s).  Every lane needs its own
-// hardware queue (GPU_MAX_HW_QUEUES > D, bench.py sets 16).
+//   frame j-1's codes (host work: clustering, ANS / prefix tables, headers,
+//   LF-group codes) start on a helper thread -> finish the oldest frame if D
+//   are in flight (wait for its emission, assemble, codestream to the host)
+//   -> launch frame j's front end, merge stage and statistics on a free lane
+//   -> join the codes of frame j-lag (its emission is launched by then).
+// So the rANS chains of the frames before j (latency-bound waves that use
+// little of their SIMDs) run while frame j's transform kernels fill the rest
+// of the chip.  A frame's chain lasts as long as its longest pass group's,
+// whatever the frame size, so the depth follows the frame: ~3570 pass groups
+// in flight (8K: 7 lanes), at least 4, up to kPipeMaxLanes for small frames.
+// The lag follows it too: 1 for large frames (the GPU is the bound), 3 for
+// small ones, whose host work per frame is the bound.  Every
+// lane needs its own hardware queue (GPU_MAX_HW_QUEUES > D, bench.py sets 16).
 // ---------------------------------------------------------------------------
-#ifndef JXG_PIPE_MAX_LANES  // (experiment builds override them: tools/build_variant.sh)
-#define JXG_PIPE_MAX_LANES 12
-#endif
-#ifndef JXG_PIPE_LAG_SMALL
-#define JXG_PIPE_LAG_SMALL 3
-#endif
-#ifndef JXG_PIPE_LAG_LARGE
-#define JXG_PIPE_LAG_LARGE 1
-#endif
-#ifndef JXG_PIPE_MIN_LANES
-#define JXG_PIPE_MIN_LANES 4
-#endif
-#ifndef JXG_PIPE_CHAIN_GROUPS  // pass groups in flight the depth aims at
-#define JXG_PIPE_CHAIN_GROUPS 3570  // 8K (510 groups): 7 lanes
-#endif
-constexpr uint32_t kPipeMaxLanes = JXG_PIPE_MAX_LANES;
+constexpr uint32_t kPipeMaxLanes = 12, kPipeMinLanes = 4, kPipeChainGroups = 3570;
+constexpr uint32_t kPipeLagSmall = 3, kPipeLagLarge = 1;
 // Hardware queues of this process (GPU_MAX_HW_QUEUES as HIP read it at start
 // up; HIP's default is 4).  Lanes beyond queues - 1 (one is left for the
 // caller's own stream) would share a queue with another lane and serialise
@@ -2170,62 +1925,31 @@ static uint32_t hw_queues() {
   return (uint32_t)std::min<long>(32, std::max<long>(1, q));
 }
 static uint32_t pipe_depth(uint32_t ngroups) {
-  const uint32_t d = (JXG_PIPE_CHAIN_GROUPS + ngroups - 1) / std::max(1u, ngroups);
-  uint32_t maxl = kPipeMaxLanes;
-  if (const char* e = std::getenv("JXG_PIPE_MAX_LANES"))  // (tuning experiments)
-    maxl = std::max(2u, std::min(64u, (uint32_t)std::strtoul(e, nullptr, 10)));
-  const uint32_t want = std::min(maxl, std::max((uint32_t)JXG_PIPE_MIN_LANES, d));
-  const char* qc = std::getenv("JXG_PIPE_QUEUE_CAP");  // 0: lanes may share queues
-  if (qc && qc[0] == '0') return std::max(2u, want);
+  const uint32_t d = (kPipeChainGroups + ngroups - 1) / std::max(1u, ngroups);
+  const uint32_t want = std::min(kPipeMaxLanes, std::max(kPipeMinLanes, d));
   return std::max(2u, std::min(want, hw_queues() - 1));
 }
 static uint32_t pipe_lag(uint32_t ngroups, uint32_t depth) {
-  const uint32_t lag = ngroups >= 256 ? (uint32_t)JXG_PIPE_LAG_LARGE : (uint32_t)JXG_PIPE_LAG_SMALL;
+  const uint32_t lag = ngroups >= 256 ? kPipeLagLarge : kPipeLagSmall;
   return std::max(1u, std::min(lag, depth - 1));
 }
-// JXG_PIPE_PROFILE (experiment builds only): host time per pipeline step,
-// printed by jxg_destroy of the owning context
-#ifdef JXG_PIPE_PROFILE
-struct PipeProf {
-  double complete = 0, finish_wait = 0, launch = 0, join = 0, codes = 0, submit = 0;
-  uint64_t n = 0;
-};
-static PipeProf g_pprof;
-#define PPROF_ADD(field, t0) (g_pprof.field += ms_since(t0))
-#else
-#define PPROF_ADD(field, t0) ((void)0)
-#endif
 struct PipeDone {
   jxg_buffer buf;
   jxg_stats stats;
 };
-// the completion workers' state of a whole frame (under Pipe::cmu)
-struct PipeCompletion {
-  int state = 0;  // 0 not handed over, 1 queued / in progress, 2 completed
-  jxg_status st = JXG_OK;
-  PipeDone res{{nullptr, 0}, {}};
-};
 struct PipeFrame {
   Ctx* lane = nullptr;
-  uint32_t li = 0;  // lane index (lane batches: physical lane li / K, slot li % K)
   Job J;
-  int phase = 1;  // 1: statistics launched; 2: emission launched; 3: assembly enqueued
+  int phase = 1;  // 1: statistics launched; 2: emission launched
   bool shard = false;
   Clock::time_point t0;
   std::future<jxg_status> codes;  // valid while a helper builds the codes
-  // jxg_shard_stream: the codes (a helper's, or the completion thread's own)
-  // waited on by the completion thread and by the submitting thread's lag join
-  std::shared_future<jxg_status> sf;
-  PipeCompletion cw;  // whole frames with completion workers
 };
 // the helper's codes of a frame -> phase 2 (on an error the caller aborts)
 static jxg_status pipe_join_codes(PipeFrame& fr) {
   if (!fr.codes.valid()) return JXG_OK;
   const jxg_status st = fr.codes.get();
   fr.phase = 2;
-#ifdef JXG_PIPE_PROFILE
-  g_pprof.codes += fr.J.ms_codes;
-#endif
   return st;
 }
 struct Pipe {
@@ -2237,44 +1961,17 @@ struct Pipe {
   uint64_t submitted = 0;
   int mode = 0;  // 1 whole frames, 2 shards (while any frame is pending)
   uint32_t depth = 0;
-  std::unique_ptr<ChainBatcher> batcher;  // (ANS; created with the lanes)
-  uint32_t batch_k = 1;                   // lane batches: slots per physical lane (1: off)
-  hipStream_t asm_stream = nullptr;       // lane batches: completion (concat + D2H)
-  // completion workers (whole frames): frames whose emission is launched are
-  // handed over in submission order; a worker assembles one (layout, concat,
-  // codestream D2H, stats) while the submitting thread launches the next
-  std::vector<std::thread> workers;
-  std::mutex cmu;
-  std::condition_variable ccv, dcv;  // work queued / a frame completed
-  std::deque<PipeFrame*> cq;
-  bool cstop = false;
-  int device = 0;
 };
-// the pipeline's chain batcher on every lane (ANS, JXG_CHAIN_BATCH != 0)
-static jxg_status pipe_batcher(Ctx* c) {
-  Pipe& p = *c->pipe;
-  if (!(c->params.flags & JXG_FLAG_ANS) || !chain_batch_enabled()) return JXG_OK;
-  if (!p.batcher) {
-    p.batcher = chain_batcher_create(c->params.device);
-    if (!p.batcher) return JXG_ERR_INTERNAL;
-  }
-  c->batcher = p.batcher.get();
-  for (auto& l : c->lanes) l->batcher = p.batcher.get();
-  return JXG_OK;
-}
 static bool pipe_busy(const Ctx* c) {
-  return c->ss || (c->pipe && (!c->pipe->inflight.empty() || !c->pipe->done.empty() ||
-                               !c->pipe->ready.empty()));
+  return c->pipe && (!c->pipe->inflight.empty() || !c->pipe->done.empty() ||
+                     !c->pipe->ready.empty());
 }
 
 static jxg_status ensure_lanes(Ctx* c, uint32_t extra) {
   while (c->lanes.size() < extra) {
-    void* lc = nullptr;
-    const jxg_status st = jxg_create(&c->params, &lc);
+    Ctx* l = nullptr;
+    const jxg_status st = ctx_new_lane(c->params, &l);
     if (st) return st;
-    Ctx* l = static_cast<Ctx*>(lc);
-    l->owned_lane = true;  // not a caller context (g_live_ctx counts those)
-    g_live_ctx--;
     c->lanes.emplace_back(l);
   }
   return JXG_OK;
@@ -2284,23 +1981,7 @@ static jxg_status ensure_lanes(Ctx* c, uint32_t extra) {
 // lanes' streams
 static void pipe_abort(Ctx* c) {
   Pipe& p = *c->pipe;
-  if (!p.workers.empty()) {  // frames handed to the workers finish first
-    std::unique_lock<std::mutex> lk(p.cmu);
-    p.dcv.wait(lk, [&] {
-      for (auto& q : p.inflight)
-        if (q->cw.state == 1) return false;
-      return true;
-    });
-    for (auto& q : p.inflight)
-      if (q->cw.state == 2 && q->cw.res.buf.data) jxg_buffer_free(&q->cw.res.buf);
-  }
-  for (auto& fr : p.inflight) {
-    (void)pipe_join_codes(*fr);
-    if (fr->sf.valid()) fr->sf.wait();
-    if (fr->J.chain.valid()) fr->J.chain.wait();  // (the batcher launches every queued frame)
-  }
-  if (p.batcher) (void)hipStreamSynchronize(p.batcher->stream);
-  if (p.asm_stream) (void)hipStreamSynchronize(p.asm_stream);
+  for (auto& fr : p.inflight) (void)pipe_join_codes(*fr);
   for (auto& fr : p.inflight) (void)hipStreamSynchronize(fr->lane->stream);
   for (auto& fr : p.ready) (void)hipStreamSynchronize(fr->lane->stream);
   for (auto& fr : p.inflight)  // codestreams of frames whose assembly had started
@@ -2320,7 +2001,7 @@ static void pipe_abort(Ctx* c) {
 //          | section bytes back to back
 constexpr uint32_t kPayloadMagic = 0x5347584Au;  // "JXGS"
 // (sync false: the body may still be in flight on the context's stream; the
-// streaming paths enqueue its D2H behind it -- shard_write_host -- so the head
+// streaming path enqueues its D2H behind it -- shard_write_host -- so the head
 // goes out one GPU round trip earlier)
 static jxg_status shard_finish(Ctx* c, Job& J, size_t* payload_bytes, bool sync = true) {
   hipStream_t s = c->stream;
@@ -2360,9 +2041,6 @@ static jxg_status shard_finish(Ctx* c, Job& J, size_t* payload_bytes, bool sync 
   return JXG_OK;
 }
 
-// oldest frame in flight -> done (a whole frame: assembled, codestream on
-// the host) or ready (a shard: sections emitted, payload head built); on an
-// error the caller aborts the pipe
 // a shard frame's stats (its lane's) once its sections are emitted
 static void shard_frame_stats(PipeFrame& fr, size_t bytes) {
   jxg_stats& S = fr.lane->stats;
@@ -2378,160 +2056,16 @@ static void shard_frame_stats(PipeFrame& fr, size_t bytes) {
   S.ms_host_call = ms_since(fr.t0);
 }
 
-// Non-blocking progress of whole frames in flight, oldest first: codes
-// joined once their helper has finished, assembly (layout, concat, the
-// codestream's D2H) started once the emission is done -- so the blocking
-// completion of the oldest frame later finds its bytes on the way.
-static bool pipe_progress_enabled() {  // (measured slower: off unless JXG_PIPE_PROGRESS=1)
-  static const bool on = [] {
-    const char* e = std::getenv("JXG_PIPE_PROGRESS");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-static jxg_status pipe_progress(Ctx* c) {
-  Pipe& p = *c->pipe;
-  for (auto& up : p.inflight) {
-    PipeFrame& fr = *up;
-    if (fr.shard) break;
-    if (fr.phase == 1) {
-      if (!fr.codes.valid() ||
-          fr.codes.wait_for(std::chrono::seconds(0)) != std::future_status::ready)
-        break;
-      const jxg_status st = pipe_join_codes(fr);
-      if (st) return st;
-    }
-    if (fr.phase == 2) {
-      const int q = emission_done(fr.lane, fr.J);
-      if (q == 0) break;
-      if (q < 0) return JXG_ERR_HIP;
-      const jxg_status st = enc_finish_start(fr.lane, fr.J, false);
-      if (st) return st;
-      fr.phase = 3;
-    }
-  }
-  return JXG_OK;
-}
-
-// ---- completion workers (whole frames) ----
-// The host work of a frame's completion (its layout, the concat launch, the
-// codestream D2H and the wait for it: ≈ 0.45 ms at 1080p, profiles/r03s2_batch)
-// used to run on the submitting thread, which then bounded small frames at
-// ≈ 0.5 ms per frame, it seemed.  JXG_PIPE_WORKERS threads take it over (0:
-// the submitting thread completes).  Measured (profiles/r03s2_batch): no gain
-// at 1080p (1-3 workers ≈ 3.8-4.0 GPix/s, as without), 8K within noise, and
-// two processes on one GPU share the same ≈ 4 GPix/s: the small-frame stream
-// is bound on the GPU side.  Off by default.
-#ifndef JXG_PIPE_WORKERS
-#define JXG_PIPE_WORKERS 0
-#endif
-static uint32_t pipe_workers() {
-  uint32_t n = JXG_PIPE_WORKERS;
-  if (const char* e = std::getenv("JXG_PIPE_WORKERS")) n = (uint32_t)std::strtoul(e, nullptr, 10);
-  return std::min(n, 8u);
-}
-static void pipe_worker(Pipe* p) {
-  (void)hipSetDevice(p->device);
-  for (;;) {
-    PipeFrame* fr = nullptr;
-    {
-      std::unique_lock<std::mutex> lk(p->cmu);
-      p->ccv.wait(lk, [&] { return p->cstop || !p->cq.empty(); });
-      if (p->cq.empty()) return;  // stopped and drained
-      fr = p->cq.front();
-      p->cq.pop_front();
-    }
-    PipeDone d{{nullptr, 0}, {}};
-    jxg_status st = fr->phase < 3 ? enc_finish_start(fr->lane, fr->J, false) : JXG_OK;
-    if (!st) st = enc_finish_end(fr->lane, fr->J, &d.buf, fr->t0);
-    if (!st) d.stats = fr->lane->stats;
-    {
-      std::lock_guard<std::mutex> lk(p->cmu);
-      fr->cw.st = st;
-      fr->cw.res = d;
-      fr->cw.state = 2;
-    }
-    p->dcv.notify_all();
-  }
-}
-static void pipe_workers_start(Ctx* c) {
-  Pipe& p = *c->pipe;
-  if (!p.workers.empty()) return;
-  p.device = c->params.device;
-  const uint32_t n = pipe_workers();
-  for (uint32_t i = 0; i < n; i++) {
-    try {
-      p.workers.emplace_back(pipe_worker, &p);
-    } catch (...) {  // fewer (or no) workers: the submitting thread completes the rest
-      break;
-    }
-  }
-}
-static void pipe_workers_stop(Pipe& p) {
-  {
-    std::lock_guard<std::mutex> lk(p.cmu);
-    p.cstop = true;
-  }
-  p.ccv.notify_all();
-  for (auto& t : p.workers) t.join();
-  p.workers.clear();
-  p.cstop = false;
-}
-// hand over, in submission order, every whole frame whose codes are joined
-// and whose emission is done (a worker then never waits on the GPU for long);
-// oldest: the oldest frame once its emission is launched (the submitting
-// thread waits for it next)
-static void pipe_handoff(Ctx* c, bool oldest = false) {
-  Pipe& p = *c->pipe;
-  if (p.workers.empty()) return;
-  bool any = false;
-  {
-    std::lock_guard<std::mutex> lk(p.cmu);
-    bool first = true;
-    for (auto& q : p.inflight) {
-      PipeFrame& f = *q;
-      if (f.shard) break;
-      const bool forced = oldest && first;
-      first = false;
-      if (f.cw.state) continue;
-      if (f.phase < 2 || f.codes.valid() || (f.J.chain_deferred && !f.J.chain_launched)) break;
-      if (!forced && emission_done(f.lane, f.J) != 1) break;
-      f.cw.state = 1;
-      p.cq.push_back(&f);
-      any = true;
-    }
-  }
-  if (any) p.ccv.notify_all();
-}
-
+// oldest frame in flight -> done (a whole frame: assembled, codestream on
+// the host) or ready (a shard: sections emitted, payload head built); on an
+// error the caller aborts the pipe
 static jxg_status pipe_complete_oldest(Ctx* c) {
   Pipe& p = *c->pipe;
   PipeFrame& fr = *p.inflight.front();
-  // lane batches: a lane whose slots are not all filled (the stream's end,
-  // mixed sizes) launches the chains it has
-  if (p.batch_k > 1 && !fr.shard && !fr.J.chain_launched) {
-    const jxg_status sb = lane_batch_launch(c, fr.li / p.batch_k, true);
-    if (sb) return sb;
-  }
   jxg_status st = pipe_join_codes(fr);
   if (!st && fr.phase == 1) {
     st = enc_codes(fr.lane, fr.J, false);
     fr.phase = 2;
-  }
-  if (!fr.shard && !p.workers.empty()) {  // the workers complete it
-    if (st) return st;
-    pipe_handoff(c, true);
-    {
-      std::unique_lock<std::mutex> lk(p.cmu);
-      if (fr.cw.state == 0) return JXG_ERR_INTERNAL;  // (not handed over: never waited on)
-      p.dcv.wait(lk, [&] { return fr.cw.state == 2; });
-      st = fr.cw.st;
-    }
-    if (st) return st;
-    p.done.push_back(fr.cw.res);
-    fr.cw.res.buf = jxg_buffer{nullptr, 0};
-    p.inflight.erase(p.inflight.begin());
-    return JXG_OK;
   }
   if (fr.shard) {
     size_t bytes = 0;
@@ -2543,18 +2077,7 @@ static jxg_status pipe_complete_oldest(Ctx* c) {
     return JXG_OK;
   }
   PipeDone d{{nullptr, 0}, {}};
-#ifdef JXG_PIPE_PROFILE
-  if (!st) {
-    const Clock::time_point tw = Clock::now();
-    if (fr.J.chain_deferred)  // lane batches: the frame's emission (its stream has other slots' work)
-      (void)hipEventSynchronize(fr.lane->ev[3]);
-    else
-      (void)hipStreamSynchronize(fr.lane->stream);
-    PPROF_ADD(finish_wait, tw);
-  }
-#endif
-  if (!st && fr.phase < 3) st = enc_finish_start(fr.lane, fr.J, false);
-  if (!st) st = enc_finish_end(fr.lane, fr.J, &d.buf, fr.t0);
+  if (!st) st = enc_finish(fr.lane, fr.J, false, &d.buf, fr.t0);
   if (st) return st;
   d.stats = fr.lane->stats;
   p.done.push_back(d);
@@ -2562,136 +2085,7 @@ static jxg_status pipe_complete_oldest(Ctx* c) {
   return JXG_OK;
 }
 
-// ---------------------------------------------------------------------------
-// Lane batches (whole frames, ANS, frames of at most 128 pass groups: 1080p
-// has 40).  A small frame's rANS chains still last as long as its longest
-// group's (≈ 3.5 ms at 1080p), and with one frame per lane the pipeline holds
-// at most as many frames as the process has hardware queues (lanes sharing a
-// queue serialise behind each other's chains), so 64 x 1080p was bound by
-// lanes x frame latency.  With batches a physical lane
-// (one stream, one hardware queue) holds K frames: their transform kernels,
-// statistics and codes go one after the other, and their chains go out as ONE
-// launch (ans_encode_batch_kernel, K x 40 chain waves) once the last slot's
-// codes are joined; each slot then places its bits.  Completion (concat +
-// codestream D2H) runs on one pipeline-wide assembly stream, so it never
-// waits behind the next batch's kernels on the lane's stream.  Bytes are the
-// one-at-a-time bytes (tests/test_gpu_stream.py).
-// ---------------------------------------------------------------------------
-// Measured (profiles/r03s2_batch): no gain -- 64 x 1080p streams at ≈ 4.0
-// GPix/s with 1, 2, 3, 4 or 8 slots (the per-frame latency grows with K), so
-// the stream is not bound by frames in flight: off unless JXG_PIPE_BATCH > 1.
-#ifndef JXG_PIPE_BATCH  // slots per lane (JXG_PIPE_BATCH env overrides; 1: off)
-#define JXG_PIPE_BATCH 1
-#endif
-#ifndef JXG_PIPE_BATCH_MAX_GROUPS
-#define JXG_PIPE_BATCH_MAX_GROUPS 128
-#endif
-static uint32_t batch_slots(uint32_t ngroups, const jxg_params& P) {
-  if (!(P.flags & JXG_FLAG_ANS) || ngroups > JXG_PIPE_BATCH_MAX_GROUPS) return 1;
-  uint32_t k = JXG_PIPE_BATCH;
-  if (const char* e = std::getenv("JXG_PIPE_BATCH")) k = (uint32_t)std::strtoul(e, nullptr, 10);
-  return std::max(1u, std::min<uint32_t>(k, (uint32_t)kAnsBatchMax));
-}
-// frames in flight with lane batches: physical lanes (one hardware queue each
-// beside the caller's stream and the assembly stream) x slots
-static uint32_t batch_depth(uint32_t lanes, uint32_t k) {
-  const uint32_t q = hw_queues();
-  return std::max(1u, std::min(lanes, q > 2 ? q - 2 : 1u)) * k;
-}
-static Ctx* pipe_lane(Ctx* c, uint32_t li) {
-  if (c->pipe->batch_k > 1) return c->blanes[li].get();
-  return li == 0 ? c : c->lanes[li - 1].get();
-}
-// n batch slots of k per physical lane (the caller's context is not one: its
-// stream stays idle), and the assembly stream
-static jxg_status ensure_blanes(Ctx* c, uint32_t n, uint32_t k) {
-  Pipe& p = *c->pipe;
-  if (c->blanes_k != k) {
-    while (!c->blanes.empty()) c->blanes.pop_back();
-    c->blanes_k = k;
-  }
-  if (!p.asm_stream) JXG_HIP(hipStreamCreateWithFlags(&p.asm_stream, hipStreamNonBlocking));
-  while (c->blanes.size() < n) {
-    const size_t li = c->blanes.size();
-    Ctx* l = nullptr;
-    const jxg_status st =
-        ctx_new_lane(c->params, li % k ? c->blanes[li - li % k]->stream : nullptr, &l);
-    if (st) return st;
-    l->defer_chain = true;
-    l->asm_stream = p.asm_stream;
-    c->blanes.emplace_back(l);
-  }
-  return JXG_OK;
-}
-// the deferred chains of physical lane `lead`: every frame in flight on its
-// slots whose chain is not out yet, in one launch on the lane's stream, then
-// each frame's bit placement, bit-count download and emission events.
-// force: now (codes built here where no helper has, helpers waited for);
-// else only once the lane's last slot is taken and every frame's codes are
-// in (no wait)
-static jxg_status lane_batch_launch(Ctx* c, uint32_t lead, bool force) {
-  Pipe& p = *c->pipe;
-  const uint32_t K = p.batch_k;
-  std::vector<PipeFrame*> fr;
-  bool closed = false;
-  for (auto& q : p.inflight)
-    if (!q->shard && q->li / K == lead && !q->J.chain_launched) {
-      fr.push_back(q.get());
-      closed = closed || q->li % K == K - 1;
-    }
-  if (fr.empty()) return JXG_OK;
-  if (fr.size() > (size_t)kAnsBatchMax) return JXG_ERR_INTERNAL;
-  if (!force) {
-    if (!closed) return JXG_OK;
-    for (PipeFrame* f : fr)
-      if (f->phase == 1 && (!f->codes.valid() || f->codes.wait_for(std::chrono::seconds(0)) !=
-                                                         std::future_status::ready))
-        return JXG_OK;
-  }
-  for (PipeFrame* f : fr) {
-    jxg_status st = pipe_join_codes(*f);
-    if (!st && f->phase == 1) {
-      st = enc_codes(f->lane, f->J, false);
-      f->phase = 2;
-    }
-    if (st) return st;
-    if (!f->J.chain_deferred) return JXG_ERR_INTERNAL;
-  }
-  hipStream_t s = fr[0]->lane->stream;
-  AnsBatch b{};
-  uint32_t nwg = 0;
-  for (size_t i = 0; i < fr.size(); i++) {
-    b.f[i] = fr[i]->J.na;
-    b.wg0[i] = nwg;
-    nwg += ans_chain_wgs(fr[i]->J.na.n);
-  }
-  b.wg0[fr.size()] = nwg;
-  b.nf = (uint32_t)fr.size();
-  launch_ans_batch(b, s);
-  JXG_HIP(hipGetLastError());
-  for (PipeFrame* f : fr) {
-    Ctx* L = f->lane;
-    Job& J = f->J;
-    launch_ans_emit(J.na, s);
-    JXG_HIP(hipGetLastError());
-    JXG_HIP(hipMemcpyAsync(L->h_bits.p, L->bits.p, ((size_t)J.f.ngroups + J.nstreams) * 4,
-                           hipMemcpyDeviceToHost, s));
-    JXG_HIP(hipEventRecord(L->ev[7], s));
-    JXG_HIP(hipEventRecord(L->ev[3], s));
-    J.chain_launched = true;
-  }
-  return JXG_OK;
-}
-// every physical lane (see lane_batch_launch for `force`)
-static jxg_status lane_batch_poll(Ctx* c, bool force) {
-  Pipe& p = *c->pipe;
-  const uint32_t nl = (uint32_t)(c->blanes.size() / std::max(1u, p.batch_k));
-  for (uint32_t l = 0; l < nl; l++) {
-    const jxg_status st = lane_batch_launch(c, l, force);
-    if (st) return st;
-  }
-  return JXG_OK;
-}
+static Ctx* pipe_lane(Ctx* c, uint32_t li) { return li == 0 ? c : c->lanes[li - 1].get(); }
 
 // submit one frame (world == 1) or this rank's shard of one frame
 static jxg_status pipe_submit(Ctx* c, const uint8_t* src, bool on_device, uint32_t w,
@@ -2701,7 +2095,6 @@ static jxg_status pipe_submit(Ctx* c, const uint8_t* src, bool on_device, uint32
   if (!c->pipe) return JXG_ERR_OOM;
   Pipe& p = *c->pipe;
   const int mode = shard ? 2 : 1;
-  if (c->ss) return JXG_ERR_INVALID_ARG;  // a jxg_shard_stream owns the lanes
   if (pipe_busy(c) && p.mode != mode) return JXG_ERR_INVALID_ARG;  // one kind at a time
   const Frame f0 = make_frame(w, h, c->params.distance);
   uint32_t ngroups = f0.ngroups;
@@ -2716,15 +2109,10 @@ static jxg_status pipe_submit(Ctx* c, const uint8_t* src, bool on_device, uint32
       return JXG_ERR_UNSUPPORTED;
     ngroups = P.ng();
   }
-  uint32_t depth = pipe_depth(ngroups);
+  const uint32_t depth = pipe_depth(ngroups);
   const uint32_t lag = pipe_lag(ngroups, depth);
-  // lane batches or one frame per lane: chosen when the pipeline is empty
-  if (!pipe_busy(c)) p.batch_k = shard ? 1 : batch_slots(ngroups, c->params);
-  if (p.batch_k > 1) depth = batch_depth(depth, p.batch_k);
-  jxg_status st = p.batch_k > 1 ? ensure_blanes(c, depth, p.batch_k) : ensure_lanes(c, depth - 1);
-  if (!st && p.batch_k == 1) st = pipe_batcher(c);
+  jxg_status st = ensure_lanes(c, depth - 1);
   if (st) return st;
-  if (mode == 1) pipe_workers_start(c);
   const Clock::time_point t0 = Clock::now();
   // a shard frame holds its lane until its sections are written: the caller
   // must take one first (jxg_shard_next_head / jxg_shard_write_next)
@@ -2755,30 +2143,21 @@ static jxg_status pipe_submit(Ctx* c, const uint8_t* src, bool on_device, uint32
     pipe_abort(c);
     return e;
   };
-#ifdef JXG_PIPE_PROFILE
-  const Clock::time_point tc = Clock::now();
-#endif
   while (!p.inflight.empty() && p.inflight.size() + p.ready.size() >= depth)
     if ((st = pipe_complete_oldest(c))) return fail(st);
-  PPROF_ADD(complete, tc);
   // a lane no frame in flight (or ready) uses (the lowest index)
   Ctx* L = nullptr;
-  uint32_t L_li = 0;
   for (uint32_t li = 0; li < depth && !L; li++) {
     Ctx* cand = pipe_lane(c, li);
     bool used = false;
     for (auto& q : p.inflight) used = used || q->lane == cand;
     for (auto& q : p.ready) used = used || q->lane == cand;
-    if (!used) {
-      L = cand;
-      L_li = li;
-    }
+    if (!used) L = cand;
   }
   if (!L) return shard ? JXG_ERR_INVALID_ARG : fail(JXG_ERR_INTERNAL);
   std::unique_ptr<PipeFrame> fr(new (std::nothrow) PipeFrame());
   if (!fr) return fail(JXG_ERR_OOM);
   fr->lane = L;
-  fr->li = L_li;
   fr->t0 = t0;
   fr->shard = shard;
   if (!on_device) {
@@ -2794,53 +2173,27 @@ static jxg_status pipe_submit(Ctx* c, const uint8_t* src, bool on_device, uint32
   } else if ((st = order_input(c, L))) {
     return fail(st);
   }
-#ifdef JXG_PIPE_PROFILE
-  const Clock::time_point tl = Clock::now();
-#endif
   if ((st = enc_launch(L, fr->J, src, w, h, stride, rank, world))) {
     (void)hipStreamSynchronize(L->stream);
     return fail(st);
   }
-  PPROF_ADD(launch, tl);
   p.inflight.push_back(std::move(fr));
   p.submitted++;
   // frame j - lag: codes built, emission launched
-#ifdef JXG_PIPE_PROFILE
-  const Clock::time_point tj = Clock::now();
-#endif
   if (p.inflight.size() > lag) {
     PipeFrame& fj = *p.inflight[p.inflight.size() - 1 - lag];
     st = pipe_join_codes(fj);
     if (st) return fail(st);
   }
-  // lane batches: every lane whose slots are taken and whose codes are in
-  // sends its chains out (checked at every submit, no wait)
-  if (p.batch_k > 1 && (st = lane_batch_poll(c, false))) return fail(st);
-  if (mode == 1) pipe_handoff(c);
-  if (mode == 1 && p.workers.empty() && pipe_progress_enabled() && (st = pipe_progress(c)))
-    return fail(st);
-#ifdef JXG_PIPE_PROFILE
-  PPROF_ADD(join, tj);
-  PPROF_ADD(submit, t0);
-  g_pprof.n++;
-#endif
   return JXG_OK;
 }
 
 static jxg_status pipe_receive(Ctx* c, jxg_buffer* out) {
-  if (c->ss || !c->pipe || c->pipe->mode != 1) return JXG_ERR_INVALID_ARG;
+  if (!c->pipe || c->pipe->mode != 1) return JXG_ERR_INVALID_ARG;
   Pipe& p = *c->pipe;
   if (p.done.empty()) {
     if (p.inflight.empty()) return JXG_ERR_INVALID_ARG;
-    // lane batches: every lane whose slots are taken and whose codes are in
-    // sends its chains out before this thread waits on the oldest (whose
-    // lane, if partly filled, pipe_complete_oldest launches)
-    jxg_status st = p.batch_k > 1 ? lane_batch_poll(c, false) : JXG_OK;
-    if (st) {
-      pipe_abort(c);
-      return st;
-    }
-    st = pipe_complete_oldest(c);
+    const jxg_status st = pipe_complete_oldest(c);
     if (st) {
       pipe_abort(c);
       return st;
@@ -2854,7 +2207,7 @@ static jxg_status pipe_receive(Ctx* c, jxg_buffer* out) {
 
 // streaming shards: the oldest pending shard frame, completed if needed
 static jxg_status pipe_shard_oldest(Ctx* c, PipeFrame** fr) {
-  if (c->ss || !c->pipe || c->pipe->mode != 2) return JXG_ERR_INVALID_ARG;
+  if (!c->pipe || c->pipe->mode != 2) return JXG_ERR_INVALID_ARG;
   Pipe& p = *c->pipe;
   if (p.ready.empty()) {
     if (p.inflight.empty()) return JXG_ERR_INVALID_ARG;
@@ -3287,409 +2640,6 @@ static jxg_status shard_assemble(const uint8_t* const* payloads, const size_t* s
   return JXG_OK;
 }
 
-// ---------------------------------------------------------------------------
-// Streaming shards over a node-shared host region (jxg_shard_stream_*): the
-// multi-GPU pipeline with its per-frame host work off the caller's thread.
-// The caller's thread only submits (launches a frame's shard on a free lane,
-// starts the previous frame's codes on a helper thread); one completion thread
-// per context takes the frames in order: waits for the shard's sections
-// (codes joined, emission done, sections concatenated, payload head built),
-// publishes the head in the region, waits for every rank's head of that
-// frame, DMAs its sections into the frame's codestream slot (rank 0 adds
-// headers + TOC) and marks the frame done.  Ranks synchronise through the
-// region only (64-bit sequence words, lock-free atomics across processes).
-// Region: [header 4 KB][pub: slots x world int64][done: slots x world int64]
-//         [heads: slots x world x hcap u32][pad to 4 KB][data: slots x slot_bytes]
-// ---------------------------------------------------------------------------
-constexpr uint64_t kShmMagic = 0x6a78675348534d31ull;  // "jxgSHSM1"
-struct ShmHeader {
-  uint64_t magic, w, h, world, slots, slot_bytes, hcap, data_off, total;
-  int64_t consumed;  // frames rank 0's caller has received
-};
-static size_t shm_hcap(const Frame& f) {
-  return 7 + 2 * (2 + (size_t)f.nlf + f.ngroups) + 2 + (kAcCtx + 3) / 4 + (size_t)kAnsMaxHists * kAlpha;
-}
-struct ShmLayout {
-  size_t pub, done, heads, data, total;
-};
-static ShmLayout shm_layout(const Frame& f, uint32_t world, uint32_t slots, size_t slot_bytes) {
-  ShmLayout L;
-  L.pub = 4096;
-  L.done = L.pub + 8 * (size_t)slots * world;
-  L.heads = L.done + 8 * (size_t)slots * world;
-  L.data = (L.heads + 4 * (size_t)slots * world * shm_hcap(f) + 4095) & ~(size_t)4095;
-  L.total = L.data + (size_t)slots * slot_bytes;
-  return L;
-}
-static int64_t shm_load(const int64_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
-static void shm_store(int64_t* p, int64_t v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
-
-struct SStream {
-  uint8_t* base = nullptr;
-  ShmHeader* hd = nullptr;
-  int64_t* pub = nullptr;   // [slots][world]: frame whose head rank r published in slot s
-  int64_t* done = nullptr;  // [slots][world]: frame whose sections rank r wrote in slot s
-  uint32_t* heads = nullptr;
-  uint32_t w = 0, h = 0, rank = 0, world = 1, slots = 0, depth = 0, lag = 1;
-  size_t stride = 0, slot_bytes = 0, hcap = 0, data_off = 0;
-  std::thread worker;
-  std::mutex mu;
-  std::condition_variable cv;
-  uint64_t submitted = 0, completed = 0, received = 0;
-  std::deque<size_t> totals;  // codestream bytes of completed, unreceived frames
-  jxg_status err = JXG_OK;
-  std::atomic<bool> stop{false};
-  float ms_wait_ranks = 0.0f;  // completion thread: time spent waiting for other ranks
-  // completion thread profile (JXG_SS_PROFILE=1: printed by end): ms in
-  // codes, finish (sections), slot wait, heads wait, write; frames
-  double prof[5] = {};
-  uint64_t prof_n = 0;
-  double sprof[3] = {};  // submitting thread: lane wait, launch, lag join
-};
-
-// spin (then sleep) until pred(), at most 120 s
-template <class Pred>
-static bool shm_wait(Pred pred, SStream* S) {
-  const Clock::time_point t0 = Clock::now();
-  for (int spin = 0; !pred(); spin++) {
-    if (spin > 256) std::this_thread::sleep_for(std::chrono::microseconds(20));
-    if (S && S->stop) return false;
-    if (ms_since(t0) > 120000.0f) return false;
-  }
-  return true;
-}
-
-static void sstream_fail(SStream& S, jxg_status st) {
-  std::lock_guard<std::mutex> lk(S.mu);
-  if (!S.err) S.err = st;
-  S.cv.notify_all();
-}
-
-// the completion thread: frames in submission order
-static void sstream_worker(Ctx* c) {
-  SStream& S = *c->ss;
-  Pipe& p = *c->pipe;
-  if (hipSetDevice(c->params.device) != hipSuccess) return sstream_fail(S, JXG_ERR_HIP);
-  const uint32_t r = S.rank, W = S.world;
-  // Frame k's sections are DMA'd without waiting; it is marked done (and its
-  // lane freed) after frame k + 1's D2H is queued, or at once when no frame
-  // follows yet: the completion of consecutive frames overlaps.
-  PipeFrame* pend = nullptr;
-  uint64_t pend_k = 0;
-  size_t pend_total = 0;
-  auto flush = [&]() -> bool {
-    if (!pend) return true;
-    if (hipStreamSynchronize(pend->lane->stream) != hipSuccess) {
-      sstream_fail(S, JXG_ERR_HIP);
-      return false;
-    }
-    shm_store(&S.done[(pend_k % S.slots) * W + r], (int64_t)pend_k);
-    std::lock_guard<std::mutex> lk(S.mu);
-    c->stats = pend->lane->stats;
-    p.inflight.erase(p.inflight.begin());  // its lane is free again
-    S.totals.push_back(pend_total);
-    S.completed++;
-    S.cv.notify_all();
-    pend = nullptr;
-    return true;
-  };
-  for (uint64_t k = 0;;) {
-    PipeFrame* fr = nullptr;
-    std::shared_future<jxg_status> codes;
-    std::promise<jxg_status> own;
-    bool mine = false;
-    {
-      std::unique_lock<std::mutex> lk(S.mu);
-      const size_t at = pend ? 1 : 0;  // the frame after the pending one
-      if (!pend) S.cv.wait(lk, [&] { return S.stop || S.err || !p.inflight.empty(); });
-      if (S.err) return;
-      if (p.inflight.size() > at) {
-        fr = p.inflight[at].get();
-        mine = !fr->sf.valid();
-        if (mine) fr->sf = own.get_future().share();  // no helper will start for it now
-        codes = fr->sf;
-      }
-    }
-    if (!fr) {  // nothing behind the pending frame (or stopped and drained)
-      if (!pend) return;
-      if (!flush()) return;
-      continue;
-    }
-    Clock::time_point tp = Clock::now();
-    auto lap = [&](int i) {
-      S.prof[i] += ms_since(tp);
-      tp = Clock::now();
-    };
-    if (mine) own.set_value(enc_codes(fr->lane, fr->J, false));
-    jxg_status st = codes.get();
-    fr->phase = 2;
-    lap(0);
-    size_t bytes = 0;
-    if (!st) st = shard_finish(fr->lane, fr->J, &bytes, false);
-    if (st) return sstream_fail(S, st);
-    shard_frame_stats(*fr, bytes);
-    lap(1);
-    const std::vector<uint32_t>& hw = fr->lane->payload_head;
-    if (hw.size() > S.hcap) return sstream_fail(S, JXG_ERR_INTERNAL);
-    const uint32_t s = (uint32_t)(k % S.slots);
-    const Clock::time_point tw = Clock::now();
-    // slot s held frame k - slots: every rank wrote it and rank 0's caller has
-    // moved past its view (views stay valid until the next receive)
-    const int64_t prev = (int64_t)k - (int64_t)S.slots;
-    if (!shm_wait([&] {
-          for (uint32_t q = 0; q < W; q++)
-            if (shm_load(&S.done[s * W + q]) < prev) return false;
-          return shm_load(&S.hd->consumed) >= prev + 2;
-        }, &S))
-      return sstream_fail(S, JXG_ERR_INTERNAL);
-    lap(2);
-    std::memcpy(S.heads + ((size_t)s * W + r) * S.hcap, hw.data(), hw.size() * 4);
-    shm_store(&S.pub[s * W + r], (int64_t)k);
-    if (!shm_wait([&] {
-          for (uint32_t q = 0; q < W; q++)
-            if (shm_load(&S.pub[s * W + q]) < (int64_t)k) return false;
-          return true;
-        }, &S))
-      return sstream_fail(S, JXG_ERR_INTERNAL);
-    S.ms_wait_ranks += ms_since(tw);
-    lap(3);
-    std::vector<const uint32_t*> hp(W);
-    std::vector<size_t> hwords(W);
-    for (uint32_t q = 0; q < W; q++) {
-      hp[q] = S.heads + ((size_t)s * W + q) * S.hcap;
-      hwords[q] = head_words(hp[q], S.hcap);
-      if (!hwords[q]) return sstream_fail(S, JXG_ERR_INTERNAL);
-    }
-    size_t total = 0;
-    st = shard_write_host(fr->lane, hp.data(), hwords.data(), W,
-                          S.base + S.data_off + (size_t)s * S.slot_bytes, S.slot_bytes, &total,
-                          false);
-    if (st) return sstream_fail(S, st == JXG_ERR_INVALID_ARG && total > S.slot_bytes
-                                        ? JXG_ERR_OOM : st);
-    pend = fr;
-    pend_k = k;
-    pend_total = total;
-    if (!flush()) return;  // (marked done once its copies have landed)
-    lap(4);
-    S.prof_n++;
-    k++;
-  }
-}
-
-static jxg_status sstream_begin(Ctx* c, void* base, size_t size, uint32_t w, uint32_t h,
-                                size_t stride, uint32_t rank, uint32_t world, uint32_t slots,
-                                size_t slot_bytes, int init) {
-  if (c->ss || pipe_busy(c)) return JXG_ERR_INVALID_ARG;
-  if (!base || ((uintptr_t)base & 4095) || world < 1 || rank >= world || slots < 3)
-    return JXG_ERR_INVALID_ARG;
-  const Frame f = make_frame(w, h, c->params.distance);
-  if (f.ngroups < world || (world > 1 && f.ngroups < 2)) return JXG_ERR_INVALID_ARG;
-  const Plan P = make_plan(f, rank, world);
-  if (!P.x.send.empty() || !P.x.recv.empty() || (world > 1 && !(c->params.flags & JXG_FLAG_ANS)))
-    return JXG_ERR_UNSUPPORTED;
-  slot_bytes = (slot_bytes + 4095) & ~(size_t)4095;
-  const ShmLayout L = shm_layout(f, world, slots, slot_bytes);
-  if (size < L.total) return JXG_ERR_INVALID_ARG;
-  ShmHeader* hd = static_cast<ShmHeader*>(base);
-  uint8_t* b = static_cast<uint8_t*>(base);
-  if (init) {
-    std::memset(b, 0, L.data);
-    hd->w = w;
-    hd->h = h;
-    hd->world = world;
-    hd->slots = slots;
-    hd->slot_bytes = slot_bytes;
-    hd->hcap = shm_hcap(f);
-    hd->data_off = L.data;
-    hd->total = L.total;
-    int64_t* pub = reinterpret_cast<int64_t*>(b + L.pub);
-    int64_t* done = reinterpret_cast<int64_t*>(b + L.done);
-    for (size_t i = 0; i < (size_t)slots * world; i++) pub[i] = done[i] = -1;
-    shm_store(&hd->consumed, 0);
-    __atomic_store_n(&hd->magic, kShmMagic, __ATOMIC_RELEASE);
-  } else if (__atomic_load_n(&hd->magic, __ATOMIC_ACQUIRE) != kShmMagic || hd->w != w ||
-             hd->h != h || hd->world != world || hd->slots != slots ||
-             hd->slot_bytes != slot_bytes || hd->total != L.total) {
-    return JXG_ERR_INVALID_ARG;  // not initialised by rank 0 with the same geometry
-  }
-  if (!c->pipe) c->pipe.reset(new (std::nothrow) Pipe());
-  if (!c->pipe) return JXG_ERR_OOM;
-  std::unique_ptr<SStream> S(new (std::nothrow) SStream());
-  if (!S) return JXG_ERR_OOM;
-  S->base = b;
-  S->hd = hd;
-  S->pub = reinterpret_cast<int64_t*>(b + L.pub);
-  S->done = reinterpret_cast<int64_t*>(b + L.done);
-  S->heads = reinterpret_cast<uint32_t*>(b + L.heads);
-  S->w = w;
-  S->h = h;
-  S->stride = stride;
-  S->rank = rank;
-  S->world = world;
-  S->slots = slots;
-  S->slot_bytes = slot_bytes;
-  S->hcap = shm_hcap(f);
-  S->data_off = L.data;
-  S->depth = pipe_depth(P.ng());
-  S->lag = pipe_lag(P.ng(), S->depth);
-  if (const char* e = std::getenv("JXG_SS_DEPTH"))  // (tuning experiments)
-    S->depth = std::max(2u, std::min(S->depth, (uint32_t)std::strtoul(e, nullptr, 10)));
-  if (const char* e = std::getenv("JXG_SS_LAG"))
-    S->lag = std::max(1u, std::min(S->depth - 1, (uint32_t)std::strtoul(e, nullptr, 10)));
-  jxg_status st = ensure_lanes(c, S->depth - 1);
-  if (!st) st = pipe_batcher(c);
-  if (st) return st;
-  c->pipe->mode = 2;
-  c->pipe->depth = S->depth;
-  c->ss = std::move(S);
-  try {
-    c->ss->worker = std::thread(sstream_worker, c);
-  } catch (...) {
-    c->ss.reset();
-    return JXG_ERR_INTERNAL;
-  }
-  return JXG_OK;
-}
-
-static jxg_status sstream_submit(Ctx* c, const uint8_t* d_rgb) {
-  SStream& S = *c->ss;
-  Pipe& p = *c->pipe;
-  Ctx* L = nullptr;
-  std::unique_ptr<PipeFrame> fr(new (std::nothrow) PipeFrame());
-  if (!fr) return JXG_ERR_OOM;
-  const Clock::time_point t_in = Clock::now();
-  {
-    std::unique_lock<std::mutex> lk(S.mu);
-    // (a frame completes only after rank 0's caller receives the one S - 2
-    // frames before it: a caller that never receives times out here)
-    if (!S.cv.wait_for(lk, std::chrono::seconds(120),
-                       [&] { return S.err || p.inflight.size() < S.depth; }))
-      return JXG_ERR_INTERNAL;
-    if (S.err) return S.err;
-    for (uint32_t li = 0; li < S.depth && !L; li++) {
-      Ctx* cand = li == 0 ? c : c->lanes[li - 1].get();
-      bool used = false;
-      for (auto& q : p.inflight) used = used || q->lane == cand;
-      if (!used) L = cand;
-    }
-  }
-  if (!L) return JXG_ERR_INTERNAL;
-  fr->lane = L;
-  fr->t0 = Clock::now();
-  fr->shard = true;
-  S.sprof[0] += ms_since(t_in);
-  const Clock::time_point t_l = Clock::now();
-  jxg_status st = order_input(c, L);
-  if (!st) st = enc_launch(L, fr->J, d_rgb, S.w, S.h, S.stride, S.rank, S.world);
-  S.sprof[1] += ms_since(t_l);
-  if (st) {
-    (void)hipStreamSynchronize(L->stream);
-    sstream_fail(S, st);
-    return st;
-  }
-  std::shared_future<jxg_status> lagged;
-  {
-    std::lock_guard<std::mutex> lk(S.mu);
-    // this frame's codes on a helper thread from now on: it waits for the
-    // statistics download and builds them as soon as they land (the
-    // completion thread builds them itself if no thread can be started)
-    PipeFrame* nf = fr.get();
-    const int dev = c->params.device;
-    try {
-      nf->sf = std::async(std::launch::async, [nf, dev]() {
-                 if (hipSetDevice(dev) != hipSuccess) return JXG_ERR_HIP;
-                 return enc_codes(nf->lane, nf->J, false);
-               }).share();
-    } catch (...) {
-    }
-    p.inflight.push_back(std::move(fr));
-    S.submitted++;
-    S.cv.notify_all();
-    // frame j - lag: codes built, emission launched before this thread
-    // launches frame j + 1 (the pacing of pipe_submit: a chain is queued
-    // before the transform kernels of the frames behind it)
-    if (p.inflight.size() > S.lag) lagged = p.inflight[p.inflight.size() - 1 - S.lag]->sf;
-  }
-  const Clock::time_point t_j = Clock::now();
-  if (lagged.valid() && (st = lagged.get())) {
-    sstream_fail(S, st);
-    return st;
-  }
-  S.sprof[2] += ms_since(t_j);
-  return JXG_OK;
-}
-
-// rank 0: the frame is complete once every rank has written it
-static bool sstream_all_done(SStream& S, uint64_t k) {
-  const uint32_t s = (uint32_t)(k % S.slots);
-  for (uint32_t q = 0; q < S.world; q++)
-    if (shm_load(&S.done[s * S.world + q]) < (int64_t)k) return false;
-  return true;
-}
-
-// frames the caller can receive without waiting (rank 0: written by every rank)
-static uint32_t sstream_ready(Ctx* c) {
-  SStream& S = *c->ss;
-  std::lock_guard<std::mutex> lk(S.mu);
-  uint64_t k = S.received;
-  while (k < S.completed && (S.rank != 0 || sstream_all_done(S, k))) k++;
-  return (uint32_t)(k - S.received);
-}
-
-static jxg_status sstream_receive(Ctx* c, size_t* offset, size_t* bytes) {
-  SStream& S = *c->ss;
-  size_t total = 0;
-  const uint64_t k = S.received;
-  {
-    std::unique_lock<std::mutex> lk(S.mu);
-    if (k >= S.submitted) return JXG_ERR_INVALID_ARG;  // nothing pending
-    if (!S.cv.wait_for(lk, std::chrono::seconds(150), [&] { return S.err || S.completed > k; }))
-      return JXG_ERR_INTERNAL;
-    if (S.err) return S.err;
-    total = S.totals.front();
-  }
-  if (S.rank == 0) {
-    if (!shm_wait([&] { return sstream_all_done(S, k); }, nullptr)) return JXG_ERR_INTERNAL;
-    *offset = S.data_off + (size_t)(k % S.slots) * S.slot_bytes;
-    *bytes = total;
-    shm_store(&S.hd->consumed, (int64_t)k + 1);
-  } else {
-    *offset = 0;
-    *bytes = 0;
-  }
-  std::lock_guard<std::mutex> lk(S.mu);
-  S.totals.pop_front();
-  S.received++;
-  return JXG_OK;
-}
-
-// stop the completion thread (after the frames pending are received, or on
-// an error / destroy: abandon them)
-static void sstream_end(Ctx* c, float* ms_wait_ranks = nullptr) {
-  if (!c->ss) return;
-  SStream& S = *c->ss;
-  {
-    std::lock_guard<std::mutex> lk(S.mu);
-    S.stop = true;
-    S.cv.notify_all();
-  }
-  if (S.worker.joinable()) S.worker.join();
-  if (ms_wait_ranks) *ms_wait_ranks = S.ms_wait_ranks;
-  if (const char* e = std::getenv("JXG_SS_PROFILE"))
-    if (e[0] == '1' && S.prof_n)
-      std::fprintf(stderr,
-                   "shard stream rank %u: %llu frames, ms/frame codes %.3f finish %.3f slot %.3f "
-                   "heads %.3f write %.3f; submit: lane wait %.3f launch %.3f lag join %.3f\n",
-                   S.rank, (unsigned long long)S.prof_n, S.prof[0] / S.prof_n, S.prof[1] / S.prof_n,
-                   S.prof[2] / S.prof_n, S.prof[3] / S.prof_n, S.prof[4] / S.prof_n,
-                   S.sprof[0] / S.prof_n, S.sprof[1] / S.prof_n, S.sprof[2] / S.prof_n);
-  if (c->pipe) {
-    pipe_abort(c);
-    c->pipe->mode = 0;
-  }
-  c->ss.reset();
-}
-
 }  // namespace jxg
 
 using namespace jxg;
@@ -3720,7 +2670,7 @@ jxg_status jxg_create(const jxg_params* params, void** out) {
   if (params->device < 0 || params->device >= ndev) return JXG_ERR_INVALID_ARG;
   if (hipSetDevice(params->device) != hipSuccess) return JXG_ERR_HIP;
   Ctx* c = nullptr;
-  const jxg_status st = ctx_new_lane(*params, nullptr, &c);
+  const jxg_status st = ctx_new_lane(*params, &c);
   if (st) return st;
   c->owned_lane = false;
   g_live_ctx++;
@@ -3731,19 +2681,12 @@ jxg_status jxg_create(const jxg_params* params, void** out) {
 void jxg_destroy(void* ctx) {
   if (!ctx) return;
   Ctx* c = static_cast<Ctx*>(ctx);
-  sstream_end(c);  // a streaming-shard completion thread first
   if (c->pipe) {  // frames still in the pipeline (their lanes are released below)
     pipe_abort(c);
-    chain_batcher_destroy(c->pipe->batcher);
-    c->batcher = nullptr;
-    for (auto& l : c->lanes) l->batcher = nullptr;
-    pipe_workers_stop(*c->pipe);
     for (auto& d : c->pipe->done) jxg_buffer_free(&d.buf);
-    if (c->pipe->asm_stream) (void)hipStreamDestroy(c->pipe->asm_stream);
     c->pipe.reset();
   }
-  c->lanes.clear();  // batch / pipeline lanes (jxg_destroy each)
-  while (!c->blanes.empty()) c->blanes.pop_back();  // slots before the leader whose stream they use
+  c->lanes.clear();  // pipeline lanes (jxg_destroy each)
   (void)hipSetDevice(c->params.device);
   (void)hipStreamSynchronize(c->stream);
   if (c->stream2) (void)hipStreamSynchronize(c->stream2);
@@ -3751,22 +2694,10 @@ void jxg_destroy(void* ctx) {
 #ifdef JXG_MERGE_PROFILE
   dump_merge_profile();
 #endif
-#ifdef JXG_PIPE_PROFILE
-  if (g_pprof.n && !c->lanes.size()) {
-    const double n = (double)g_pprof.n;
-    std::fprintf(stderr,
-                 "pipe profile (ms per submit, %llu submits): submit %.3f = complete %.3f "
-                 "(of which GPU wait %.3f) + launch %.3f + join %.3f; codes (helper) %.3f\n",
-                 (unsigned long long)g_pprof.n, g_pprof.submit / n, g_pprof.complete / n,
-                 g_pprof.finish_wait / n, g_pprof.launch / n, g_pprof.join / n, g_pprof.codes / n);
-    g_pprof = PipeProf{};
-  }
-#endif
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   if (c->ev_in) (void)hipEventDestroy(c->ev_in);
-  if (c->ev_up) (void)hipEventDestroy(c->ev_up);
-  if (c->stream && !c->stream_borrowed) (void)hipStreamDestroy(c->stream);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
   delete c;
 }
@@ -3890,11 +2821,6 @@ jxg_status jxg_receive(void* ctx, jxg_buffer* out) {
 jxg_status jxg_pending(void* ctx, uint32_t* n) {
   if (!ctx || !n) return JXG_ERR_INVALID_ARG;
   Ctx* c = static_cast<Ctx*>(ctx);
-  if (c->ss) {
-    std::lock_guard<std::mutex> lk(c->ss->mu);
-    *n = (uint32_t)(c->ss->submitted - c->ss->received);
-    return JXG_OK;
-  }
   *n = c->pipe ? (uint32_t)(c->pipe->inflight.size() + c->pipe->done.size() +
                             c->pipe->ready.size())
                : 0u;
@@ -3903,13 +2829,7 @@ jxg_status jxg_pending(void* ctx, uint32_t* n) {
 
 jxg_status jxg_get_stats(void* ctx, jxg_stats* stats) {
   if (!ctx || !stats) return JXG_ERR_INVALID_ARG;
-  Ctx* c = static_cast<Ctx*>(ctx);
-  if (c->ss) {  // the completion thread updates them
-    std::lock_guard<std::mutex> lk(c->ss->mu);
-    *stats = c->stats;
-    return JXG_OK;
-  }
-  *stats = c->stats;
+  *stats = static_cast<Ctx*>(ctx)->stats;
   return JXG_OK;
 }
 
@@ -4059,8 +2979,6 @@ jxg_status jxg_pipeline_depth(void* ctx, uint32_t xsize, uint32_t ysize, uint32_
   const Ctx* c = static_cast<Ctx*>(ctx);
   const Frame f = make_frame(xsize, ysize, c->params.distance);
   *depth = pipe_depth(world > 1 ? make_plan(f, rank, world).ng() : f.ngroups);
-  const uint32_t k = world > 1 ? 1 : batch_slots(f.ngroups, c->params);
-  if (k > 1) *depth = batch_depth(*depth, k);  // whole small frames: lane batches
   return JXG_OK;
 }
 
@@ -4104,63 +3022,6 @@ jxg_status jxg_shard_write_next(void* ctx, const uint32_t* const* heads, const s
   if (st) return st;  // (too small a buffer: the frame stays, *total tells the size)
   c->pipe->ready.erase(c->pipe->ready.begin());  // its lane is free again
   return JXG_OK;
-}
-
-size_t jxg_shard_stream_region_size(void* ctx, uint32_t w, uint32_t h, uint32_t world,
-                                    uint32_t slots, size_t slot_bytes) {
-  if (!ctx || w == 0 || h == 0 || w > (1u << 18) || h > (1u << 18) || world == 0 || slots == 0)
-    return 0;
-  const Frame f = make_frame(w, h, static_cast<Ctx*>(ctx)->params.distance);
-  return shm_layout(f, world, slots, (slot_bytes + 4095) & ~(size_t)4095).total;
-}
-
-jxg_status jxg_shard_stream_begin(void* ctx, void* region, size_t region_size, uint32_t w,
-                                  uint32_t h, size_t stride, uint32_t rank, uint32_t world,
-                                  uint32_t slots, size_t slot_bytes, int init) {
-  if (!ctx || w == 0 || h == 0 || w > (1u << 18) || h > (1u << 18) || stride < (size_t)w * 3 ||
-      slot_bytes == 0)
-    return JXG_ERR_INVALID_ARG;
-  Ctx* c = static_cast<Ctx*>(ctx);
-  if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
-  return sstream_begin(c, region, region_size, w, h, stride, rank, world, slots, slot_bytes, init);
-}
-
-jxg_status jxg_shard_stream_submit(void* ctx, const void* d_rgb) {
-  if (!ctx || !d_rgb) return JXG_ERR_INVALID_ARG;
-  Ctx* c = static_cast<Ctx*>(ctx);
-  if (!c->ss) return JXG_ERR_INVALID_ARG;
-  if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
-  return sstream_submit(c, static_cast<const uint8_t*>(d_rgb));
-}
-
-jxg_status jxg_shard_stream_ready(void* ctx, uint32_t* n) {
-  if (!ctx || !n) return JXG_ERR_INVALID_ARG;
-  Ctx* c = static_cast<Ctx*>(ctx);
-  if (!c->ss) return JXG_ERR_INVALID_ARG;
-  *n = sstream_ready(c);
-  std::lock_guard<std::mutex> lk(c->ss->mu);
-  return c->ss->err;
-}
-
-jxg_status jxg_shard_stream_receive(void* ctx, size_t* offset, size_t* bytes) {
-  if (!ctx || !offset || !bytes) return JXG_ERR_INVALID_ARG;
-  Ctx* c = static_cast<Ctx*>(ctx);
-  if (!c->ss) return JXG_ERR_INVALID_ARG;
-  return sstream_receive(c, offset, bytes);
-}
-
-jxg_status jxg_shard_stream_end(void* ctx, float* ms_wait_ranks) {
-  if (!ctx) return JXG_ERR_INVALID_ARG;
-  Ctx* c = static_cast<Ctx*>(ctx);
-  if (!c->ss) return JXG_ERR_INVALID_ARG;
-  jxg_status st;
-  {
-    std::lock_guard<std::mutex> lk(c->ss->mu);
-    st = c->ss->err;
-    if (!st && c->ss->received < c->ss->submitted) st = JXG_ERR_INVALID_ARG;  // frames dropped
-  }
-  sstream_end(c, ms_wait_ranks);
-  return st;
 }
 
 jxg_status jxg_homogeneity_map(void* ctx, const float* xyb, uint32_t xsize, uint32_t ysize,

@@ -136,21 +136,6 @@ struct AnsArgs {
   const uint32_t* order;   // chain order of the n slots (longest group first)
 };
 void launch_ans(const AnsArgs& a, hipStream_t s);
-// chain batches (the streaming pipeline): workgroups per frame, the chains of
-// several frames in one launch (d_wg[b] = frame << 20 | workgroup in frame),
-// then each frame's bit placement
-uint32_t ans_chain_wgs(uint32_t ngroups);
-void launch_ans_multi(const AnsArgs* d_frames, const uint32_t* d_wg, uint32_t nwg, hipStream_t s);
-// lane batches (the streaming pipeline, small frames): the chains of up to
-// kAnsBatchMax frames of one lane in one launch, descriptors passed by value
-// (workgroups [wg0[i], wg0[i+1]) are frame i's)
-constexpr int kAnsBatchMax = 8;
-struct AnsBatch {
-  AnsArgs f[kAnsBatchMax];
-  uint32_t wg0[kAnsBatchMax + 1];
-  uint32_t nf;
-};
-void launch_ans_batch(const AnsBatch& b, hipStream_t s);
 void launch_ans_emit(const AnsArgs& a, hipStream_t s);
 
 // LF-group modular streams: rows of (lf group, stream, channel, y)

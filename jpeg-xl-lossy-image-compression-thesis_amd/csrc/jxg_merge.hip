@@ -51,9 +51,6 @@ constexpr int kMThreads = 256;
 #ifndef JXG_MERGE_WRITE_WPE
 #define JXG_MERGE_WRITE_WPE 3  // write: 167 VGPRs, no spills
 #endif
-#ifndef JXG_MERGE_PRUNE  // merge_eval's workgroup pruning (A/B builds: -DJXG_MERGE_PRUNE=1)
-#define JXG_MERGE_PRUNE 0
-#endif
 constexpr int kMS = 65;  // LDS row stride (floats)
 constexpr int kMPlane = 64 * kMS;
 
@@ -168,8 +165,6 @@ struct MergeLds {
   int vnz[32][3];         //               non-zeros per channel
   int vraw[32];           //               max quant field
   int valid[32];
-  float lb[32];           // eval: Y-only lower bound of each varblock's estimate
-  float bent[64];         // eval: the front kernel's estimate of each block of the tile
   uint8_t braw[64];       // front-kernel quant field (raw) of the tile's blocks
   int any;
 };
@@ -586,12 +581,8 @@ __device__ __forceinline__ void quant_pass(const MergeArgs& a, const Pass& P, Me
 
 // transform + quantize every valid varblock of the pass; leaves per-varblock
 // bits / non-zeros and the chunk sums in LDS
-// after_y (eval): called once Y is quantized (its bits / non-zeros / chunk
-// sums complete in LDS); true stops the pass there (the workgroup's
-// candidates cannot be chosen, merge_eval_kernel)
-template <bool WRITE, class AfterY>
-__device__ __forceinline__ bool transform_quant(const MergeArgs& a, const Pass& P, MergeLds& S,
-                                                AfterY after_y) {
+template <bool WRITE>
+__device__ __forceinline__ void transform_quant(const MergeArgs& a, const Pass& P, MergeLds& S) {
 #ifdef JXG_MERGE_PROFILE
   unsigned long long mprof_t0 = 0;
 #endif
@@ -618,7 +609,6 @@ __device__ __forceinline__ bool transform_quant(const MergeArgs& a, const Pass& 
   // residuals); then X; then B is transformed into X's plane.  Every pass's
   // tables are in flight across the barrier before it.  A lane's X / B items
   // read the Y values its own Y item wrote (same item map).
-  bool stop = false;
   auto quant_yx = [&](auto rpc_tag) {
     constexpr int RPC = decltype(rpc_tag)::value;
     {
@@ -627,12 +617,6 @@ __device__ __forceinline__ bool transform_quant(const MergeArgs& a, const Pass& 
       __syncthreads();
       MPROF_MARK(2);
       quant_pass<RPC, WRITE, 1>(a, P, S, ty);
-    }
-    if constexpr (!WRITE) {
-      if (after_y()) {
-        stop = true;
-        return;
-      }
     }
     QTab<RPC> tx;
     load_qtab<RPC, WRITE, 0>(a, P, tx);
@@ -647,7 +631,6 @@ __device__ __forceinline__ bool transform_quant(const MergeArgs& a, const Pass& 
   };
   if (P.lcy == 0) quant_yx(std::integral_constant<int, 8>());
   else quant_yx(std::integral_constant<int, 16>());
-  if (stop) return true;
   __syncthreads();  // plane 1 (X) fully read
   MPROF_MARK(3);
   transform(std::integral_constant<int, 1>(), 1);  // B -> plane 1
@@ -655,7 +638,6 @@ __device__ __forceinline__ bool transform_quant(const MergeArgs& a, const Pass& 
   else quant_b(std::integral_constant<int, 16>());
   __syncthreads();
   MPROF_MARK(4);
-  return false;
 }
 
 // distortion of varblock v: chunk sums in order per channel, (Y + X) + B
@@ -684,7 +666,6 @@ __device__ __forceinline__ void setup_varblocks(const MergeArgs& a, const Pass& 
     const bool in = lbx < nbx && lby < nby;
     const size_t gb = (size_t)(P.ty * 8 + lby) * a.bxs + P.tx * 8 + lbx;
     S.braw[t] = in ? a.qf[gb] : 0;
-    if (!WRITE && JXG_MERGE_PRUNE) S.bent[t] = in ? a.ent[gb] : 0.0f;
   }
   if (t < 32) {
     const int v = t;
@@ -737,74 +718,7 @@ void merge_eval_kernel(MergeArgs a) {
   setup_varblocks<false>(a, P, S, nbx, nby);
   __syncthreads();
   vraw_pass(a, P, S);
-  // Pruning (no effect on any choice): a varblock's estimate after Y alone
-  // bounds its final one from below (bits and the e*e chunk sums only grow
-  // with X and B; hook F's factor 0.8 avg_r is not negative, a negative or NaN
-  // one disables it).  In merge_resolve a candidate of this shape is compared
-  // against a best that is at most the region's current sum, which merges at
-  // lower levels only lower: so it is at most the sum of the front kernel's
-  // per-block estimates (a.ent) plus float rounding (< 1.2e-5 relative over
-  // three levels of <= 64-term sums; the margin is 2^-12).  When every region
-  // of the tile has (the bound of its candidate, summed over the shape's
-  // halves as resolve sums them) above that sum -- and finite, non-negative
-  // block estimates (NaN ones make resolve accept anything) -- none of this
-  // workgroup's varblocks can be chosen: X and B are skipped and their costs
-  // set to +inf, which resolve never picks (its best stays finite).
-  const int nbx_t = nbx, nby_t = nby;
-  auto after_y = [&]() -> bool {
-    // (levels 32 and 64 only: with 16 or 32 varblocks a 16-level shape
-    // rarely loses in every region, and the extra barriers would not pay)
-    if (!JXG_MERGE_PRUNE || P.ls < 2) return false;
-    __syncthreads();  // Y's bits, non-zeros and chunk sums are complete
-    const int t = threadIdx.x;
-    if (t < P.NV() && S.valid[t]) {
-      const int nch = P.lcy == 0 ? 1 : P.R() >> 4;
-      float pc = S.qsum[0][0][t];
-      for (int ch = 1; ch < nch; ch++) pc = pc + S.qsum[0][ch][t];
-      float lb = ((float)(S.vbits[t] + bitlen_u((uint32_t)S.vnz[t][1])) + 8.0f * pc) * P.tmul;
-      if (a.proposals & 2u) {
-        const float avg_r = (S.vr3[t][0] + S.vr3[t][1] + S.vr3[t][2]) / 3.0f;
-        lb = avg_r >= 0.0f ? hook_f(lb, S.vr3[t][0], S.vr3[t][1], S.vr3[t][2])
-                           : __builtin_nanf("");
-      }
-      S.lb[t] = lb;
-    }
-    __syncthreads();
-    bool ok = true;
-    const int sl = 1 << P.ls, nr = 8 / sl;
-    if (t < nr * nr) {
-      const int rx = t % nr, ry = t / nr;
-      if ((rx + 1) * sl <= nbx_t && (ry + 1) * sl <= nby_t) {
-        float cur = 0.0f;
-        bool fin = true;
-        for (int iy = 0; iy < sl; iy++)
-          for (int ix = 0; ix < sl; ix++) {
-            const float e = S.bent[(ry * sl + iy) * 8 + rx * sl + ix];
-            fin = fin && e >= 0.0f && e < FLT_MAX;
-            cur += e;
-          }
-        const int kind = P.si % 3;  // 0 tall halves, 1 wide halves, 2 full
-        float lbr;
-        if (kind == 2) {
-          lbr = S.lb[ry * nr + rx];
-        } else if (kind == 0) {
-          const int vl = ry * (16 / sl) + 2 * rx;
-          lbr = S.lb[vl] + S.lb[vl + 1];
-        } else {
-          const int vt = (2 * ry) * nr + rx;
-          lbr = S.lb[vt] + S.lb[vt + nr];
-        }
-        ok = fin && cur < FLT_MAX && lbr > cur * (1.0f + 1.0f / 4096.0f);
-      }
-    }
-    return __syncthreads_and(ok) != 0;
-  };
-  if (transform_quant<false>(a, P, S, after_y)) {
-    const int v = threadIdx.x;
-    if (v < P.NV() && S.valid[v])
-      a.cost[((size_t)tile * kNumShapes + si) * 32 + v] = __builtin_inff();
-    return;
-  }
+  transform_quant<false>(a, P, S);
   const int v = threadIdx.x;
   if (v < P.NV() && S.valid[v]) {
     const float dist = varblock_dist(P, S, v);
@@ -928,7 +842,7 @@ __device__ __forceinline__ void write_entry(const MergeArgs& a, int tile, int si
   setup_varblocks<true>(a, P, S, nbx, nby);
   __syncthreads();
   vraw_pass(a, P, S);
-  transform_quant<true>(a, P, S, [] { return false; });
+  transform_quant<true>(a, P, S);
   // per covered block: non-zero counts, quant field, LLF-derived DC
   const int cb = P.cy() * P.cx(), lcb = P.lcy + P.lcx;
   const size_t nb = (size_t)a.bxs * a.bys;

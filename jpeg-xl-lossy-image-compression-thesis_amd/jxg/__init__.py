@@ -87,8 +87,7 @@ EXPORTS = ("jxg_status_str", "jxg_create", "jxg_destroy", "jxg_encode_rgb8",
            "jxg_submit_rgb8", "jxg_submit_rgb8_device", "jxg_receive", "jxg_pending",
            "jxg_set_input_stream", "jxg_pipeline_depth", "jxg_shard_plan",
            "jxg_shard_submit_device", "jxg_shard_next_head", "jxg_shard_write_next",
-           "jxg_shard_stream_region_size", "jxg_shard_stream_begin", "jxg_shard_stream_submit",
-           "jxg_shard_stream_ready", "jxg_shard_stream_receive", "jxg_shard_stream_end")
+)
 
 _lib = None
 
@@ -150,14 +149,6 @@ def load():
     lib.jxg_shard_next_head.argtypes = [vp, vp, ctypes.POINTER(sz)]
     lib.jxg_shard_write_next.argtypes = lib.jxg_shard_write_host.argtypes
     u32 = ctypes.c_uint32
-    lib.jxg_shard_stream_region_size.argtypes = [vp, u32, u32, u32, u32, sz]
-    lib.jxg_shard_stream_region_size.restype = sz
-    lib.jxg_shard_stream_begin.argtypes = [vp, vp, sz, u32, u32, sz, u32, u32, u32, sz,
-                                           ctypes.c_int]
-    lib.jxg_shard_stream_submit.argtypes = [vp, vp]
-    lib.jxg_shard_stream_ready.argtypes = [vp, ctypes.POINTER(u32)]
-    lib.jxg_shard_stream_receive.argtypes = [vp, ctypes.POINTER(sz), ctypes.POINTER(sz)]
-    lib.jxg_shard_stream_end.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
     lib.jxg_host_register.argtypes = [vp, sz]
     lib.jxg_host_unregister.argtypes = [vp]
     cmp_args = [vp, vp, sz, vp, sz, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
@@ -346,44 +337,6 @@ class Encoder:
         released; returns (ok, total) -- ok False when dst_size < total (the
         frame stays pending, nothing written)."""
         return self._write(load().jxg_shard_write_next, heads, dst_ptr, dst_size)
-
-    # streaming shards with the completion in the library (jxg_shard_stream_*):
-    # see jxg.dist.ShardStream
-    def shard_stream_region_size(self, width: int, height: int, world: int, slots: int,
-                                 slot_bytes: int) -> int:
-        n = load().jxg_shard_stream_region_size(self._ctx, width, height, world, slots,
-                                                slot_bytes)
-        if n == 0:
-            raise JxgError("jxg_shard_stream_region_size: invalid geometry")
-        return n
-
-    def shard_stream_begin(self, region_ptr: int, region_size: int, width: int, height: int,
-                           rank: int, world: int, slots: int, slot_bytes: int, init: bool,
-                           row_stride: int | None = None):
-        _check(load().jxg_shard_stream_begin(self._ctx, ctypes.c_void_p(region_ptr), region_size,
-                                             width, height, row_stride or width * 3, rank, world,
-                                             slots, slot_bytes, int(init)))
-
-    def shard_stream_submit(self, ptr: int):
-        _check(load().jxg_shard_stream_submit(self._ctx, ctypes.c_void_p(ptr)))
-
-    def shard_stream_ready(self) -> int:
-        n = ctypes.c_uint32()
-        _check(load().jxg_shard_stream_ready(self._ctx, ctypes.byref(n)))
-        return n.value
-
-    def shard_stream_receive(self) -> tuple:
-        """(offset, bytes) of the oldest frame's codestream in the region
-        (rank 0; other ranks (0, 0)); blocks until it is complete."""
-        off, n = ctypes.c_size_t(), ctypes.c_size_t()
-        _check(load().jxg_shard_stream_receive(self._ctx, ctypes.byref(off), ctypes.byref(n)))
-        return off.value, n.value
-
-    def shard_stream_end(self) -> float:
-        """Close the stream; returns ms the completion thread waited for other ranks."""
-        ms = ctypes.c_float()
-        _check(load().jxg_shard_stream_end(self._ctx, ctypes.byref(ms)))
-        return ms.value
 
     def timings(self) -> tuple:
         """(ms_front_kernel, ms_host_call, ms_host_codes, ms_host_layout) of the

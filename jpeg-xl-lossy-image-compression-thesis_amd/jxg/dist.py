@@ -35,7 +35,10 @@ that needs no record exchange (whole LF groups per rank, jxg_shard_plan kind
 0 / 1) and coded with one HF preset per rank (ANS), so a rank's frames flow
 through the library's lanes with no collective at all; per frame the ranks
 only swap their payload heads through a node-shared /dev/shm region and DMA
-their sections into it.
+their sections into it.  The /dev/shm exchange replaces an RCCL gather on
+purpose: the codestream must end in host memory, so every rank DMAs its own
+sections there over its own PCIe link (nothing crosses xGMI); RCCL is used by
+the one-frame-at-a-time device assembly of :func:`encode_sharded`.
 """
 from __future__ import annotations
 
@@ -294,77 +297,9 @@ def encode_sharded(enc: Encoder, d_rgb: torch.Tensor, width: int, height: int, r
 
 
 class ShardStream:
-    """Streaming group-sharded encode with the per-frame completion in the
-    library (jxg_shard_stream_*, include/jxg.h): every rank submits its shard
-    of the same frames in the same order; a native completion thread per rank
-    takes each frame (sections emitted, payload head published in the
-    node-shared region, every rank's head of the frame read there, its
-    sections DMA'd into the frame's codestream slot).  No collective and no
-    Python work per frame beyond submit / receive.  Rank 0's :meth:`receive`
-    returns a zero-copy view of the oldest frame's codestream, valid until its
-    next receive; other ranks get None.  Rank 0 must keep receiving: keep
-    :meth:`pending` below :attr:`max_pending` (a frame's slot is reused once
-    rank 0 has received the frame slots - 1 after it).  Same bytes as
-    :class:`HostShardStream` (the protocol done in Python)."""
-
-    def __init__(self, enc: Encoder, width: int, height: int, rank: int, world: int,
-                 group=None, slots: int = 6, slot_bytes: int | None = None):
-        self.enc, self.w, self.h, self.rank, self.world = enc, width, height, rank, world
-        self.depth = enc.pipeline_depth(width, height, rank, world)
-        self.slots = slots
-        self.max_pending = self.depth + slots - 2
-        # codestream slot: 12 bpp + 1 MiB (a d1 8K frame is ~2 bpp)
-        self.slot_bytes = slot_bytes or ((width * height * 3 // 2 + (1 << 20) + 4095) & ~4095)
-        self.host = SharedHostBuffer(rank, world, group)
-        need = enc.shard_stream_region_size(width, height, world, slots, self.slot_bytes)
-        self.host.ensure(need)
-        if rank == 0:
-            enc.shard_stream_begin(self.host.addr, self.host.cap, width, height, rank, world,
-                                   slots, self.slot_bytes, True)
-        dist.barrier(group=group)  # the region is initialised
-        if rank != 0:
-            enc.shard_stream_begin(self.host.addr, self.host.cap, width, height, rank, world,
-                                   slots, self.slot_bytes, False)
-        self.submitted = 0
-        self.received = 0
-        self.ms_wait_ranks = 0.0
-
-    def pending(self) -> int:
-        return self.submitted - self.received
-
-    def ready(self) -> int:
-        """Frames :meth:`receive` returns without waiting."""
-        return self.enc.shard_stream_ready()
-
-    def submit(self, ptr: int):
-        """Queue this rank's shard of the next frame (device RGB8, unchanged
-        until the frame is received); blocks while every lane is busy."""
-        self.enc.shard_stream_submit(ptr)
-        self.submitted += 1
-
-    def receive(self):
-        """The oldest frame not yet received (blocking): rank 0 gets a numpy
-        view of its codestream (valid until the next receive), others None."""
-        if self.received >= self.submitted:
-            raise RuntimeError("ShardStream: nothing pending")
-        off, n = self.enc.shard_stream_receive()
-        self.received += 1
-        return self.host.view(n, off) if self.rank == 0 else None
-
-    def close(self):
-        while self.received < self.submitted:
-            self.receive()
-        self.ms_wait_ranks = self.enc.shard_stream_end()
-        dist.barrier(group=self.host.group)
-        self.host.close()
-
-
-class HostShardStream:
     """Streaming group-sharded encode (jxg_shard_submit_device /
-    jxg_shard_next_head / jxg_shard_write_next) with the per-frame protocol in
-    Python -- the same region protocol :class:`ShardStream` runs natively;
-    kept as its cross-check and for callers with their own collective.  Every
-    rank submits its shard
+    jxg_shard_next_head / jxg_shard_write_next), the multi-GPU pipeline
+    bench.py --gpus N times.  Every rank submits its shard
     of the same frames in the same order; frames flow through the library's
     pipeline lanes (front end, merge stage, statistics, codes and rANS chains
     of up to jxg_pipeline_depth frames overlap) with no collective inside a
@@ -409,10 +344,13 @@ class HostShardStream:
         self.written = 0     # frames whose sections this rank has written
         self.received = 0    # frames returned by receive()
         self.totals = {}
+        self.wait_s = 0.0    # seconds spent waiting for the other ranks (heads, slots, frames)
 
     def _wait(self, cond, what):
         t0 = time.perf_counter()
         spins, told = 0, False
+        if cond():
+            return
         while not cond():
             spins += 1
             if spins > 64:
@@ -425,6 +363,7 @@ class HostShardStream:
                 told = True
             if dt > 120:
                 raise RuntimeError("ShardStream: timed out waiting for " + what)
+        self.wait_s += time.perf_counter() - t0
 
     def pending(self) -> int:
         return self.submitted - self.received

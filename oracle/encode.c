@@ -269,7 +269,7 @@ static void lf_group_section(const jxo_frame* f, const jxo_result* r, int lg,
    * unpinned], carried by the EPF leaf's offset (every residual 0) */
   tnode meta[7];
   memcpy(meta, kMetaTree, sizeof(meta));
-  if (filters & JXO_FILTER_EPF) {
+  if ((filters & JXO_FILTER_EPF) && jxo_epf_iters(f->distance) > 0) {
     meta[3].offset = JXO_EPF_SHARPNESS;
     for (size_t i = 0; i < (size_t)bw * bh; i++) ch[3].data[i] = JXO_EPF_SHARPNESS;
   }
@@ -553,16 +553,22 @@ int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h, size_t row_strid
   {
     static _Thread_local uint32_t lh[JXO_MAX_CLUSTERS][JXO_ALPHA];
     memset(lh, 0, sizeof(lh));
+    /* one worst-case token buffer per thread, reused by its groups; each
+     * group keeps an exact-size copy (510 concurrent 1.5 MB allocations per
+     * 8K frame used to serialise the threads on page faults) */
+    actok* scratch = (actok*)malloc(sizeof(actok) * 32 * 32 * 3 * 64);
 #pragma omp for schedule(dynamic)
     for (uint32_t g = 0; g < f.ngroups; g++) {
-      gt[g] = (actok*)malloc(sizeof(actok) * 32 * 32 * 3 * 64);
-      gn[g] = group_tokens(&f, out, (int)g, gt[g], out->ac_tokens + g * 3);
+      gn[g] = group_tokens(&f, out, (int)g, scratch, out->ac_tokens + g * 3);
+      gt[g] = (actok*)malloc(sizeof(actok) * (gn[g] ? gn[g] : 1));
+      memcpy(gt[g], scratch, sizeof(actok) * gn[g]);
       for (size_t i = 0; i < gn[g]; i++) {
         uint32_t tok, nbt, bits;
         jxo_hybrid(gt[g][i].v, &kCfg, &tok, &nbt, &bits);
         lh[jxo_ac_cluster(gt[g][i].ctx)][tok]++;
       }
     }
+    free(scratch);
 #pragma omp critical
     for (int cl = 0; cl < JXO_MAX_CLUSTERS; cl++)
       for (int s = 0; s < JXO_ALPHA; s++) hist[cl][s] += lh[cl][s];

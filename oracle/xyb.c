@@ -92,9 +92,10 @@ void jxo_srgb8_to_xyb(const uint8_t* rgb, uint32_t w, uint32_t h,
 #endif
 
 int jxo_epf_iters(float distance) {
-  /* [ext] cjxl --epf=-1 picks the iterations from the distance; restated:
-   * 1 below d 1.5, 2 below d 4, else 3 (unpinned) */
-  return distance < 1.5f ? 1 : (distance < 4.0f ? 2 : 3);
+  /* [ext] cjxl --epf=-1 picks the iterations from the distance; restated
+   * (libjxl's thresholds 0.7 / 1.5 / 4.0, unpinned): none below d 0.7, then
+   * 1 below d 1.5, 2 below d 4, else 3 */
+  return distance < 0.7f ? 0 : (distance < 1.5f ? 1 : (distance < 4.0f ? 2 : 3));
 }
 
 uint32_t jxo_lf_code(uint32_t filters, float distance) {

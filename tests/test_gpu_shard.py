@@ -274,133 +274,15 @@ def test_stream_shards_equal_one_at_a_time(jxg_mod, decoder, w, h, world, nframe
     _same_image(dr, dg)
 
 
-def native_streamed_shards(jxg_mod, ts, w, h, world, slots=4, d=1.0, e=7, p=0):
-    """Frames ts through `world` contexts' native shard streams
-    (jxg_shard_stream_*: one completion thread per context, heads and sections
-    through one host region); the main thread only submits and receives.
-    Returns the codestreams in order."""
-    import mmap
-
-    import torch
-
-    torch.cuda.synchronize()  # the frames are written (no input stream set)
-    encs = [jxg_mod.Encoder(distance=d, effort=e, proposals=p, flags=jxg_mod.FLAG_ANS)
-            for _ in range(world)]
-    slot_bytes = w * h * 2 + (1 << 20)
-    size = encs[0].shard_stream_region_size(w, h, world, slots, slot_bytes)
-    region = mmap.mmap(-1, size)
-    addr = ctypes.addressof(ctypes.c_char.from_buffer(region))
-    assert jxg_mod.load().jxg_host_register(ctypes.c_void_p(addr), size) == 0
-    outs = []
-    try:
-        for r, enc in enumerate(encs):  # rank 0 initialises the region first
-            enc.shard_stream_begin(addr, size, w, h, r, world, slots, slot_bytes, r == 0)
-        depth = min(enc.pipeline_depth(w, h, r, world) for r, enc in enumerate(encs))
-        max_pending = depth + slots - 2
-        pending = 0
-
-        def take():
-            for r, enc in enumerate(encs):
-                off, n = enc.shard_stream_receive()
-                if r == 0:
-                    outs.append(bytes(region[off:off + n]))
-                else:
-                    assert (off, n) == (0, 0)
-
-        for t in ts:
-            for enc in encs:
-                enc.shard_stream_submit(t.data_ptr())
-            pending += 1
-            while pending >= max_pending or (pending and encs[0].shard_stream_ready()):
-                take()
-                pending -= 1
-        while pending:
-            take()
-            pending -= 1
-        for enc in encs:
-            assert enc.pending() == 0
-            enc.shard_stream_end()
-    finally:
-        for enc in encs:
-            enc.close()
-        jxg_mod.load().jxg_host_unregister(ctypes.c_void_p(addr))
-    return outs
-
-
-@pytest.mark.parametrize("w,h,world,nframes,slots", [(4096, 512, 2, 11, 3), (8192, 2048, 4, 7, 6),
-                                                     (1100, 700, 1, 14, 4)])
-def test_native_stream_equals_host_protocol(jxg_mod, w, h, world, nframes, slots):
-    """jxg_shard_stream_* (native completion threads; 3 slots: every slot
-    reused under the rank-0 receive rule) gives the bytes of the Python
-    protocol over jxg_shard_next_head / write_next for every frame."""
-    from jxg.synth import synth_rgb8_device
-
-    ts = [synth_rgb8_device(w, h, 0x5A17 + 13 * k) for k in range(nframes)]
-    got = native_streamed_shards(jxg_mod, ts, w, h, world, slots=slots)
-    ref = streamed_shards(jxg_mod, ts, w, h, world)
-    assert len(got) == nframes
-    assert [hashlib.sha256(g).hexdigest() for g in got] == \
-        [hashlib.sha256(g).hexdigest() for g in ref]
-
-
-def test_native_stream_8k_over_8(jxg_mod):
-    """The 8K ANS frame over 8 native shard streams (the driver's 8-GPU bench
-    shape, here 8 contexts on one GPU) == the one-at-a-time sharded bytes."""
+def test_stream_8k_over_8(jxg_mod):
+    """The 8K ANS frame over 8 streamed shards (the driver's 8-GPU bench shape,
+    here 8 contexts on one GPU) == the one-at-a-time sharded bytes."""
     from jxg.synth import synth_rgb8_device
 
     ts = [synth_rgb8_device(7680, 4320, 0x4A584C02 + k) for k in range(3)]
-    got = native_streamed_shards(jxg_mod, ts, 7680, 4320, 8, slots=4)
+    got = streamed_shards(jxg_mod, ts, 7680, 4320, 8)
     for k in (0, 2):
         assert got[k] == sharded_encode(jxg_mod, None, 8, flags=jxg_mod.FLAG_ANS, t=ts[k])
-
-
-def test_native_stream_refusals(jxg_mod):
-    """Region checks (alignment, size, a non-zero rank before rank 0's init),
-    the other entry points refused while a stream is open, end with frames
-    pending reports it."""
-    import mmap
-
-    import torch
-
-    w, h, world, slots, sb = 4096, 512, 2, 4, 4096 * 512 * 2
-    small = torch.zeros((h, w, 3), dtype=torch.uint8, device="cuda")
-    with jxg_mod.Encoder(flags=jxg_mod.FLAG_ANS) as e0, jxg_mod.Encoder(flags=jxg_mod.FLAG_ANS) as e1:
-        size = e0.shard_stream_region_size(w, h, world, slots, sb)
-        region = mmap.mmap(-1, size + 4096)
-        addr = ctypes.addressof(ctypes.c_char.from_buffer(region))
-        with pytest.raises(jxg_mod.JxgError, match="invalid"):  # misaligned
-            e0.shard_stream_begin(addr + 8, size, w, h, 0, world, slots, sb, True)
-        with pytest.raises(jxg_mod.JxgError, match="invalid"):  # too small
-            e0.shard_stream_begin(addr, size - 4096, w, h, 0, world, slots, sb, True)
-        with pytest.raises(jxg_mod.JxgError, match="invalid"):  # not initialised
-            e1.shard_stream_begin(addr, size, w, h, 1, world, slots, sb, False)
-        with pytest.raises(jxg_mod.JxgError, match="unsupported"):  # record exchange
-            e0.shard_stream_begin(addr, size, 3840, 2160, 0, 8, slots, sb, True)
-        e0.shard_stream_begin(addr, size, w, h, 0, world, slots, sb, True)
-        with pytest.raises(jxg_mod.JxgError, match="invalid"):  # geometry differs
-            e1.shard_stream_begin(addr, size, w, h, 1, world, slots + 1, sb, False)
-        e1.shard_stream_begin(addr, size, w, h, 1, world, slots, sb, False)
-        for e in (e0, e1):
-            e.shard_stream_submit(small.data_ptr())
-        for call in (lambda: e0.encode_device(small.data_ptr(), w, h),
-                     lambda: e0.shard_submit_device(small.data_ptr(), w, h, 0, world),
-                     lambda: e0.submit_device(small.data_ptr(), w, h),
-                     lambda: e0.shard_stream_begin(addr, size, w, h, 0, world, slots, sb, True)):
-            with pytest.raises(jxg_mod.JxgError, match="invalid"):
-                call()
-        assert e0.pending() == 1
-        off, n = e0.shard_stream_receive()
-        assert e1.shard_stream_receive() == (0, 0)
-        assert n > 0 and bytes(region[off:off + 2]) == b"\xff\x0a"
-        for e in (e0, e1):
-            e.shard_stream_submit(small.data_ptr())
-        e1.shard_stream_receive()
-        with pytest.raises(jxg_mod.JxgError, match="invalid"):  # rank 0's frame dropped
-            e0.shard_stream_end()
-        e1.shard_stream_end()
-        with pytest.raises(jxg_mod.JxgError, match="invalid"):  # no stream open
-            e0.shard_stream_submit(small.data_ptr())
-        assert e0.encode_device(small.data_ptr(), w, h)  # the context works again
 
 
 def test_stream_shards_refusals(jxg_mod):
@@ -558,7 +440,7 @@ def _gloo_stream_rank(rank, world, port, result, nframes):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import jxg
-        from jxg.dist import HostShardStream, SharedHostBuffer, ShardStream, encode_sharded
+        from jxg.dist import SharedHostBuffer, ShardStream, encode_sharded
         from jxg.synth import synth_rgb8_device
 
         w, h = 4096, 512
@@ -576,7 +458,7 @@ def _gloo_stream_rank(rank, world, port, result, nframes):
                 ref = [enc.encode_device(t.data_ptr(), w, h) for t in ts] if rank == 0 else None
             res[ans] = (dev, hst, ref)
         streams = {}
-        for cls in (ShardStream, HostShardStream):
+        for cls in (ShardStream,):
             with jxg.Encoder(flags=jxg.FLAG_ANS) as enc:
                 ss = cls(enc, w, h, rank, world)
                 got = []
@@ -635,7 +517,6 @@ def test_multiprocess_streamed_frames(jxg_mod, decoder):
     dev, hst, ref = res[True]
     assert digests(dev) == digests(hst)
     assert digests(streams["ShardStream"]) == digests(dev)
-    assert digests(streams["HostShardStream"]) == digests(dev)
     got = streams["ShardStream"]
     dr, dg = decoder.decode(ref[3]), decoder.decode(got[3])
     assert dg.npresets == 2

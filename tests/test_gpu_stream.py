@@ -111,22 +111,15 @@ def test_batch_ans_equals_single_and_refuses_pending(jxg_mod):
         assert enc.pending() == 0
 
 
-@pytest.mark.parametrize("k,workers", [("1", "0"), ("1", "2"), ("2", "0"), ("3", "0"), ("3", "2"),
-                                       ("8", "3")])
-def test_lane_batches_equal_single(jxg_mod, monkeypatch, k, workers):
-    """Lane batches (small ANS frames; JXG_PIPE_BATCH slots per physical lane,
-    one chain launch per lane, completion on the assembly stream) and
-    completion workers (JXG_PIPE_WORKERS threads assemble): 41 frames
-    (not a multiple of K or of the depth), host and device inputs, a 4K frame
-    (135 groups) in the middle of a batch-mode stream, receives interleaved,
-    the drain launching partly filled lanes -- every codestream equals the
+def test_mixed_stream_equals_single(jxg_mod):
+    """Small ANS frames of mixed sizes through the pipeline: 41 frames (not a
+    multiple of the depth), host and device inputs, a 4K frame (135 groups)
+    in the middle, receives interleaved -- every codestream equals the
     one-at-a-time encode's."""
     import torch
 
     from jxg.synth import natural_rgb8, synth_rgb8
 
-    monkeypatch.setenv("JXG_PIPE_BATCH", k)
-    monkeypatch.setenv("JXG_PIPE_WORKERS", workers)
     sizes = [(640, 480), (1920, 1080), (333, 250), (800, 600)]
     frames = [(natural_rgb8 if i % 3 else synth_rgb8)(*sizes[i % 4], 900 + i) for i in range(41)]
     frames[17] = synth_rgb8(3840, 2160, 77)

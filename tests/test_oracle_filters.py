@@ -18,16 +18,20 @@ def _psnr(a, b):
 
 
 @pytest.mark.parametrize("filters", [0, GAB, EPF, GAB | EPF])
-@pytest.mark.parametrize("d,iters", [(1.0, 1), (2.0, 2), (6.0, 3)])
+@pytest.mark.parametrize("d,iters", [(0.5, 0), (0.7, 1), (1.0, 1), (2.0, 2), (6.0, 3)])
 def test_header_round_trip(oracle, decoder, filters, d, iters):
+    """EPF iterations by distance (libjxl's 0.7 / 1.5 / 4.0 thresholds as
+    recalled): none below d 0.7 -- the sharpness channel is then
+    not signalled either."""
     img = synth_rgb8(72, 40, 11)
     r = oracle.encode(img, d, 7, 0, 0, filters)
     dec = decoder.decode(r.bytes)
     assert dec.gab == bool(filters & GAB)
-    assert dec.epf_iters == (iters if filters & EPF else 0)
+    epf = iters if filters & EPF else 0
+    assert dec.epf_iters == epf
     assert np.array_equal(dec.ac, r.ac) and np.array_equal(dec.acs, r.acs)
     # the EPF sharpness channel: a constant 4 through the leaf offset
-    assert (dec.sharpness == (4 if filters & EPF else 0)).all()
+    assert (dec.sharpness == (4 if epf else 0)).all()
 
 
 def test_epf_signalling_only_changes_header_and_tree(oracle):
