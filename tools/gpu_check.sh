@@ -1,0 +1,21 @@
+#!/bin/bash
+# One GPU-box pass: GPU tests, smoke, the default bench (CPU baseline with a
+# thread sweep), and a 4-rank gloo rehearsal of bench.py's default sharded
+# path on the box's one GPU (bench.py starts the ranks itself).
+# Usage: bash tools/gpu_check.sh TAG [tests|bench|gloo ...]  (default: all)
+set -e
+export TMPDIR=/tmp
+TAG=${1:-check}; shift || true
+STEPS=${@:-tests bench gloo}
+O=gpurun_out/$TAG
+mkdir -p $O
+for s in $STEPS; do
+  case $s in
+    tests) timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/gpu_tests.log 2>&1
+           timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 ;;
+    bench) timeout -k 10 300 python bench.py --cpu-sweep 16,32,64,128,256 > $O/bench.log 2>&1 ;;
+    bench20) timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-quality > $O/bench20.log 2>&1 ;;
+    gloo) JXG_DIST_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 4 --steps 20 --warmup 3 > $O/bench_gloo4.log 2>&1 ;;
+    cfg) bash tools/gpu_configs.sh $TAG/cfg ;;
+  esac
+done
