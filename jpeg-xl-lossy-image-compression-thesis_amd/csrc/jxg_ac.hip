@@ -78,12 +78,6 @@ __device__ __forceinline__ int nnz_ctx(int n) {
        : n < 33 ? 180 : 206;
 }
 
-__device__ __forceinline__ int predict_nz(const uint8_t* nzc, int bx, int by) {
-  if (bx == 0) return by == 0 ? 32 : nzc[(by - 1) * 32 + bx];
-  if (by == 0) return nzc[by * 32 + bx - 1];
-  return (nzc[(by - 1) * 32 + bx] + nzc[by * 32 + bx - 1] + 1) / 2;
-}
-
 __device__ __forceinline__ int block_ctx_of(int c, int acs) {
   return kDefaultCtxMap[(c < 2 ? c ^ 1 : 2) * 13 + kStrategyOrder[acs]];
 }
@@ -123,19 +117,45 @@ __device__ __forceinline__ void varblock_dims(int type, int& lcb, int& cx, int& 
   }
 }
 
-// One thread per block of the group: slice `sl` of the varblock whose first
-// block is (obx, oby) (group-local; varblocks are aligned to their size).
+// ac_hist runs one 256-thread workgroup per BAND of a pass group: 8 block
+// rows (one row of 64x64 tiles) x 32 block columns.  Varblocks are aligned to
+// their size (<= 8 blocks) inside 64x64 tiles, so a band holds whole
+// varblocks, and the group's token stream (varblocks by first block raster)
+// is the concatenation of its four bands' streams: band j writes its records
+// at [j * kBandTokStride, ...) of the group's record space and its token
+// count to bandtok[g][j]; the coders read the group's stream through
+// rec_index (a 4-entry prefix).  Four workgroups per group give small frames
+// (1080p: 40 groups) 160 workgroups instead of 40.
+constexpr int kBandRows = 8, kBandBlocks = kBandRows * 32, kBands = 32 / kBandRows;
+constexpr int kHistThreads = kBandBlocks;
+static_assert(kBands * kBandTokStride == kGroupTokStride, "band record spaces tile the group's");
+
+// record space index of stream position k of a group whose band counts are bt[4]
+__device__ __forceinline__ uint32_t rec_index(const uint32_t* bt, uint32_t k) {
+  uint32_t j = 0, lo = 0;
+#pragma unroll
+  for (int i = 0; i < kBands - 1; i++) {
+    const bool past = k >= lo + bt[i];
+    lo += past ? bt[i] : 0u;
+    j += past ? 1u : 0u;
+  }
+  return j * (uint32_t)kBandTokStride + (k - lo);
+}
+
+// One thread per block of the band: slice `sl` of the varblock whose first
+// block is (obx, oby) (group-local rows; varblocks are aligned to their size).
 struct SliceTask {
   bool valid;
   int bx, by, obx, oby, sl, lcb, cx, type;
   size_t gb, ogb;
 };
-__device__ __forceinline__ SliceTask slice_task(const AcArgs& a, const GroupGeom& G) {
+__device__ __forceinline__ SliceTask slice_task(const AcArgs& a, const GroupGeom& G, int y0) {
   SliceTask t;
   const int b = threadIdx.x;
-  t.valid = b < G.gw * G.gh;
-  t.bx = t.valid ? b % G.gw : 0;
-  t.by = t.valid ? b / G.gw : 0;
+  t.bx = b & 31;
+  t.by = y0 + (b >> 5);
+  t.valid = t.bx < G.gw && t.by < G.gh;
+  if (!t.valid) t.bx = t.by = 0;
   t.gb = (size_t)(G.by0 + t.by) * a.bxs + G.bx0 + t.bx;
   t.type = t.valid ? (a.acs[t.gb] & 0x7F) : 0;
   int cy;
@@ -146,22 +166,31 @@ __device__ __forceinline__ SliceTask slice_task(const AcArgs& a, const GroupGeom
   t.ogb = (size_t)(G.by0 + t.oby) * a.bxs + G.bx0 + t.obx;
   return t;
 }
-__device__ __forceinline__ int block_of_slice(const SliceTask& t, int j) {
-  return (t.oby + j / t.cx) * 32 + t.obx + j % t.cx;
+// band-local index of slice j of t's varblock
+__device__ __forceinline__ int block_of_slice(const SliceTask& t, int j, int y0) {
+  return (t.oby - y0 + j / t.cx) * 32 + t.obx + j % t.cx;
 }
 
 struct AcLds {
-  uint8_t nz[3][1024];   // predicted-nz image (scaled per covered block)
-  uint8_t snz[3][1024];  // non-zeros of each slice (positions >= cb)
-  uint8_t last[3][1024]; // last coefficient of the slice != 0
-  int8_t lastk[3][1024]; // highest slice-local index >= cb - 64 sl holding a non-zero, or -1
+  uint8_t nz[3][(kBandRows + 1) * 32];  // predicted-nz image, band rows and the row above
+  uint8_t snz[3][kBandBlocks];   // non-zeros of each slice (positions >= cb)
+  uint8_t last[3][kBandBlocks];  // last coefficient of the slice != 0
+  int8_t lastk[3][kBandBlocks];  // highest slice-local index >= cb - 64 sl holding a non-zero, or -1
 };
+// predicted non-zeros of group-local block (bx, by) from the band's nz image
+// (row 0 = the row above the band); neighbours inside the group only
+__device__ __forceinline__ int predict_nz(const uint8_t* nzc, int bx, int by, int y0) {
+  const int r = by - y0 + 1;
+  if (bx == 0) return by == 0 ? 32 : nzc[(r - 1) * 32 + bx];
+  if (by == 0) return nzc[r * 32 + bx - 1];
+  return (nzc[(r - 1) * 32 + bx] + nzc[r * 32 + bx - 1] + 1) / 2;
+}
 
 // tokens of task (t, c) without walking it: the walk runs from the slice's
 // first position >= cb up to the varblock's last non-zero K (1 + K for an
 // 8x8-class block), plus the non-zero count token on slice 0
 __device__ __forceinline__ uint32_t task_token_count(const AcArgs& a, const SliceTask& t,
-                                                     const AcLds& L, int c) {
+                                                     const AcLds& L, int c, int y0) {
   if (t.lcb == 0) {
     uint32_t w[32];
     load_coefs(a.ac + (t.gb * 3 + c) * 64, w);
@@ -173,29 +202,30 @@ __device__ __forceinline__ uint32_t task_token_count(const AcArgs& a, const Slic
   const int cb = 1 << t.lcb;
   int K = -1;
   for (int j = 0; j < cb; j++) {
-    const int lk = L.lastk[c][block_of_slice(t, j)];
+    const int lk = L.lastk[c][block_of_slice(t, j, y0)];
     K = lk >= 0 ? j * 64 + lk : K;
   }
   const int lo = max(t.sl * 64, cb), hi = min(t.sl * 64 + 63, K);
   return (t.sl == 0 ? 1u : 0u) + (hi >= lo ? (uint32_t)(hi - lo + 1) : 0u);
 }
 
-// predicted-nz image and per-slice non-zero counts of the group
+// predicted-nz image (the band and the row above) and per-slice non-zero counts
 __device__ __forceinline__ void fill_slices(const AcArgs& a, const GroupGeom& G,
-                                            const SliceTask& t, AcLds& L) {
+                                            const SliceTask& t, AcLds& L, int y0) {
   const size_t nb = (size_t)a.bxs * a.bys;
-  for (int i = threadIdx.x; i < 3 * 1024; i += blockDim.x) {
-    const int c = i >> 10, by = (i >> 5) & 31, bx = i & 31;
-    if (bx < G.gw && by < G.gh) {
+  for (int i = threadIdx.x; i < 3 * (kBandRows + 1) * 32; i += blockDim.x) {
+    const int c = i / ((kBandRows + 1) * 32), r = (i >> 5) % (kBandRows + 1), bx = i & 31;
+    const int by = y0 - 1 + r;
+    if (bx < G.gw && by >= 0 && by < G.gh) {
       const size_t gb = (size_t)(G.by0 + by) * a.bxs + G.bx0 + bx;
       const int acs = a.acs[gb];
       int l, cx, cy;
       varblock_dims(acs, l, cx, cy);  // covered blocks (flag set) hold scaled counts
-      L.nz[c][by * 32 + bx] = (uint8_t)((a.nz[c * nb + gb] + (1 << l) - 1) >> l);
+      L.nz[c][r * 32 + bx] = (uint8_t)((a.nz[c * nb + gb] + (1 << l) - 1) >> l);
     }
   }
   if (t.valid && t.lcb > 0) {
-    const int cb = 1 << t.lcb;
+    const int cb = 1 << t.lcb, me = threadIdx.x;
 #pragma unroll 1
     for (int c = 0; c < 3; c++) {
       uint32_t w[32];
@@ -207,29 +237,29 @@ __device__ __forceinline__ void fill_slices(const AcArgs& a, const GroupGeom& G,
         n += on;
         lk = on ? kk : lk;
       }
-      L.snz[c][t.by * 32 + t.bx] = (uint8_t)n;
-      L.last[c][t.by * 32 + t.bx] = coef(w, 63) != 0;
-      L.lastk[c][t.by * 32 + t.bx] = (int8_t)lk;
+      L.snz[c][me] = (uint8_t)n;
+      L.last[c][me] = coef(w, 63) != 0;
+      L.lastk[c][me] = (int8_t)lk;
     }
   }
 }
 
 // walk state of task (t, c) at its first coefficient; nz = varblock count
 __device__ __forceinline__ void slice_state(const AcArgs& a, const SliceTask& t, const AcLds& L,
-                                            int c, int& nz, int& left, int& prev) {
+                                            int c, int y0, int& nz, int& left, int& prev) {
   nz = a.nz[c * (size_t)a.bxs * a.bys + t.ogb];
   const int cb = 1 << t.lcb;
   left = nz;
   prev = nz > cb * 4 ? 0 : 1;  // nz > size / 16
   if (t.sl > 0) {
-    for (int j = 0; j < t.sl; j++) left -= L.snz[c][block_of_slice(t, j)];
-    if (t.sl * 64 - 1 >= cb) prev = L.last[c][block_of_slice(t, t.sl - 1)];
+    for (int j = 0; j < t.sl; j++) left -= L.snz[c][block_of_slice(t, j, y0)];
+    if (t.sl * 64 - 1 >= cb) prev = L.last[c][block_of_slice(t, t.sl - 1, y0)];
   }
 }
 
-// workgroup (1024 threads) exclusive scan; *total = sum of all values
-__device__ __forceinline__ uint32_t block_excl_scan1024(uint32_t v, uint32_t* sWave,
-                                                        uint32_t* total) {
+// workgroup (256 threads) exclusive scan; *total = sum of all values
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sWave,
+                                                    uint32_t* total) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t incl = v;
 #pragma unroll
@@ -241,7 +271,7 @@ __device__ __forceinline__ uint32_t block_excl_scan1024(uint32_t v, uint32_t* sW
   __syncthreads();
   uint32_t before = 0, all = 0;
 #pragma unroll
-  for (int i = 0; i < kAcThreads / 64; i++) {
+  for (int i = 0; i < kHistThreads / 64; i++) {
     const uint32_t x = sWave[i];
     before += i < wv ? x : 0u;
     all += x;
@@ -250,21 +280,28 @@ __device__ __forceinline__ uint32_t block_excl_scan1024(uint32_t v, uint32_t* sW
   return before + incl - v;
 }
 
-// 8 waves per SIMD (<= 64 VGPRs): two 1024-thread workgroups per CU, so all
-// pass groups of an 8K frame are resident at once
-__global__ __launch_bounds__(kAcThreads) __attribute__((amdgpu_waves_per_eu(8))) void ac_hist_kernel(AcArgs a) {
-  __shared__ uint32_t sHist[kMaxClusters * kAcTok];
+// The band's clustered histogram in LDS as u16 counts, two bins per word (a
+// band has at most 256 x 3 x 64 = 49152 tokens, so a half never carries)
+__global__ __launch_bounds__(kHistThreads) void ac_hist_kernel(AcArgs a) {
+  constexpr int kHistWords = kMaxClusters * kAcTok / 2;
+  __shared__ uint32_t sHist[kHistWords];
   __shared__ AcLds L;
   __shared__ uint8_t sClu[kAcCtx];
-  __shared__ uint32_t sTask[3][1024];  // tokens per (channel, slice task)
-  __shared__ uint32_t sBase[1024];     // first token of each varblock (first block)
-  __shared__ uint32_t sWave[kAcThreads / 64];
+  __shared__ uint32_t sTask[3][kBandBlocks];  // tokens per (channel, slice task)
+  __shared__ uint32_t sBase[kBandBlocks];     // first token of each varblock (first block)
+  __shared__ uint32_t sWave[kHistThreads / 64];
   __shared__ uint32_t sBound, sNtok[3];
   __shared__ uint16_t sNnzCtx[64];
   __shared__ uint8_t sFreqCtx[64];
-  const int g = (int)slot_group(a.glist, a.g0, blockIdx.x);
+  const uint32_t slot = blockIdx.x / kBands, band = blockIdx.x % kBands;
+  const int g = (int)slot_group(a.glist, a.g0, slot);
   const GroupGeom G = group_geom(a, g);
-  for (int i = threadIdx.x; i < kMaxClusters * kAcTok; i += blockDim.x) sHist[i] = 0;
+  const int y0 = (int)band * kBandRows;
+  if (y0 >= G.gh) {  // below a partial bottom group: an empty band
+    if (threadIdx.x == 0) a.bandtok[g * kBands + band] = 0;
+    return;
+  }
+  for (int i = threadIdx.x; i < kHistWords; i += blockDim.x) sHist[i] = 0;
   if (threadIdx.x < 64) {
     sNnzCtx[threadIdx.x] = (uint16_t)nnz_ctx(threadIdx.x);
     sFreqCtx[threadIdx.x] = (uint8_t)freq_ctx(threadIdx.x);
@@ -272,25 +309,25 @@ __global__ __launch_bounds__(kAcThreads) __attribute__((amdgpu_waves_per_eu(8)))
   for (int i = threadIdx.x; i < kAcCtx; i += blockDim.x) sClu[i] = c_cluster[i];
   if (threadIdx.x < 3) sNtok[threadIdx.x] = 0;
   if (threadIdx.x == 0) sBound = 0;
-  const SliceTask t = slice_task(a, G);
-  fill_slices(a, G, t, L);
+  const SliceTask t = slice_task(a, G, y0);
+  fill_slices(a, G, t, L, y0);
   __syncthreads();
-  const int me = t.by * 32 + t.bx;
+  const int me = threadIdx.x;
   // token counts per task without a walk -> stream positions (varblocks by
   // first block raster, channels Y, X, B, slices): one scan over varblocks
   if (t.valid) {
 #pragma unroll 1
-    for (int ci = 0; ci < 3; ci++) sTask[ci][me] = task_token_count(a, t, L, channel_of(ci));
+    for (int ci = 0; ci < 3; ci++) sTask[ci][me] = task_token_count(a, t, L, channel_of(ci), y0);
   }
   __syncthreads();
   uint32_t vtot = 0;
   const int cb = 1 << t.lcb;
   if (t.valid && t.sl == 0) {
     for (int ci = 0; ci < 3; ci++)
-      for (int j = 0; j < cb; j++) vtot += sTask[ci][block_of_slice(t, j)];
+      for (int j = 0; j < cb; j++) vtot += sTask[ci][block_of_slice(t, j, y0)];
   }
   uint32_t total;
-  const uint32_t off = block_excl_scan1024(vtot, sWave, &total);
+  const uint32_t off = block_excl_scan(vtot, sWave, &total);
   if (t.valid && t.sl == 0) sBase[me] = off;
   __syncthreads();
   // one walk: clustered histogram, bit bound, and every token's 32-bit record
@@ -303,10 +340,14 @@ __global__ __launch_bounds__(kAcThreads) __attribute__((amdgpu_waves_per_eu(8)))
   // token iff left_k > 0 -- the serial walk of block_tokens /
   // varblock_slice_tokens, restated.
   uint32_t bound = 0, nt[3] = {0, 0, 0};
-  uint32_t* rec = a.tokens + (uint64_t)blockIdx.x * kGroupTokStride;
-  uint32_t pos = t.valid ? sBase[t.oby * 32 + t.obx] : 0u;
+  uint32_t* rec = a.tokens + (uint64_t)slot * kGroupTokStride + (uint64_t)band * kBandTokStride;
+  uint32_t pos = t.valid ? sBase[(t.oby - y0) * 32 + t.obx] : 0u;
   const int lane = threadIdx.x & 63;
   const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  auto hist_add = [&](uint32_t clu, uint32_t tok) {
+    const uint32_t bin = clu * kAcTok + tok;
+    atomicAdd(&sHist[bin >> 1], 1u << ((bin & 1u) * 16u));
+  };
 #pragma unroll 1
   for (int ci = 0; ci < 3; ci++) {
     const int c = channel_of(ci);
@@ -314,7 +355,7 @@ __global__ __launch_bounds__(kAcThreads) __attribute__((amdgpu_waves_per_eu(8)))
     if (t.valid) {
       uint32_t before = 0, chan_total = 0;
       for (int j = 0; j < cb; j++) {
-        const uint32_t b = sTask[ci][block_of_slice(t, j)];
+        const uint32_t b = sTask[ci][block_of_slice(t, j, y0)];
         before += j < t.sl ? b : 0u;
         chan_total += b;
       }
@@ -322,17 +363,17 @@ __global__ __launch_bounds__(kAcThreads) __attribute__((amdgpu_waves_per_eu(8)))
       cnt = sTask[ci][me];
       pos += chan_total;
       int nz, left, prev;
-      slice_state(a, t, L, c, nz, left, prev);
+      slice_state(a, t, L, c, y0, nz, left, prev);
       const int bctx = block_ctx_of(c, t.type);
       // info: left (12 bits) | prev << 12 | lcb << 13 | sl << 16 | bctx << 22
       info = (uint32_t)left | ((uint32_t)prev << 12) | ((uint32_t)t.lcb << 13) |
              ((uint32_t)t.sl << 16) | ((uint32_t)bctx << 22);
       if (t.sl == 0) {  // the non-zero count token, written by the task's own thread
-        const int pred = predict_nz(L.nz[c], t.bx, t.by);
+        const int pred = predict_nz(L.nz[c], t.bx, t.by, y0);
         uint32_t tok, nb, bits;
         hybrid420((uint32_t)nz, tok, nb, bits);
         const uint32_t clu = sClu[nz_bucket(pred) * kBlockCtx + bctx];
-        atomicAdd(&sHist[clu * kAcTok + tok], 1u);
+        hist_add(clu, tok);
         bound += 15u + nb;
         tok0 = clu | (tok << 8) | (nb << 14) | (bits << 18);
         rec[idx] = tok0;
@@ -346,10 +387,7 @@ __global__ __launch_bounds__(kAcThreads) __attribute__((amdgpu_waves_per_eu(8)))
     const bool need = t.valid && cnt > (t.sl == 0 ? 1u : 0u);
     const uint32_t qoff = (uint32_t)((t.gb * 3 + c) * 64);
     uint64_t M = __ballot(need);
-#ifndef JXG_AC_BATCH
-#define JXG_AC_BATCH 8
-#endif
-    constexpr int kBatch = JXG_AC_BATCH;
+    constexpr int kBatch = 8;
     while (M) {
       int js[kBatch];
 #pragma unroll
@@ -383,7 +421,7 @@ __global__ __launch_bounds__(kAcThreads) __attribute__((amdgpu_waves_per_eu(8)))
           uint32_t tok, nb, bits;
           hybrid420(pack_signed(v), tok, nb, bits);
           const uint32_t clu = sClu[ctx];
-          atomicAdd(&sHist[clu * kAcTok + tok], 1u);
+          hist_add(clu, tok);
           bound += 15u + nb;
           rec[idxj + (slj == 0 ? 1u : 0u) + (uint32_t)(k - lo)] =
               clu | (tok << 8) | (nb << 14) | (bits << 18);
@@ -396,13 +434,20 @@ __global__ __launch_bounds__(kAcThreads) __attribute__((amdgpu_waves_per_eu(8)))
   atomicAdd(&sNtok[1], nt[1]);
   atomicAdd(&sNtok[2], nt[2]);
   __syncthreads();
-  for (int i = threadIdx.x; i < kMaxClusters * kAcTok; i += blockDim.x)
-    if (sHist[i]) atomicAdd(&a.hist[(i / kAcTok) * kAlpha + (i % kAcTok)], sHist[i]);
+  for (int i = threadIdx.x; i < kHistWords; i += blockDim.x) {
+    const uint32_t w = sHist[i];
+    if (!w) continue;
+    const int bin = 2 * i;
+    if (w & 0xFFFFu) atomicAdd(&a.hist[(bin / kAcTok) * kAlpha + (bin % kAcTok)], w & 0xFFFFu);
+    if (w >> 16) atomicAdd(&a.hist[((bin + 1) / kAcTok) * kAlpha + ((bin + 1) % kAcTok)], w >> 16);
+  }
+  // (bound and ntok: zeroed with the statistics arena; bandtok written here)
   if (threadIdx.x == 0) {
-    a.bound[g] = sBound;
-    a.ntok[g * 3 + 0] = sNtok[0];
-    a.ntok[g * 3 + 1] = sNtok[1];
-    a.ntok[g * 3 + 2] = sNtok[2];
+    atomicAdd(&a.bound[g], sBound);
+    atomicAdd(&a.ntok[g * 3 + 0], sNtok[0]);
+    atomicAdd(&a.ntok[g * 3 + 1], sNtok[1]);
+    atomicAdd(&a.ntok[g * 3 + 2], sNtok[2]);
+    a.bandtok[g * kBands + band] = total;
   }
 }
 
@@ -432,6 +477,9 @@ __global__ __launch_bounds__(kAcThreads) void ac_emit_kernel(AcArgs a) {
     reinterpret_cast<uint4*>(sBits)[i] = make_uint4(0, 0, 0, 0);
   const uint32_t n = a.ntok[g * 3] + a.ntok[g * 3 + 1] + a.ntok[g * 3 + 2];
   const uint32_t* rec = a.tokens + (uint64_t)blockIdx.x * kGroupTokStride;
+  uint32_t bt[kBands];
+#pragma unroll
+  for (int i = 0; i < kBands; i++) bt[i] = a.bandtok[g * kBands + i];
   constexpr int kWaves = kAcThreads / 64;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t chunk = ((n + kWaves * 64 - 1) / (kWaves * 64)) * 64;
@@ -440,7 +488,7 @@ __global__ __launch_bounds__(kAcThreads) void ac_emit_kernel(AcArgs a) {
   auto code_of = [&](uint32_t r) { return sCode[(r & 0xFF) * kAcTok + ((r >> 8) & 63)]; };
   uint32_t tot = 0;
   for (uint32_t k = lo + lane; k < hi; k += 64) {
-    const uint32_t r = rec[k];
+    const uint32_t r = rec[rec_index(bt, k)];
     tot += (code_of(r) >> 16) + ((r >> 14) & 15);
   }
 #pragma unroll
@@ -462,7 +510,7 @@ __global__ __launch_bounds__(kAcThreads) void ac_emit_kernel(AcArgs a) {
     const uint32_t k = k0 + lane;
     uint32_t len = 0, val = 0;
     if (k < hi) {
-      const uint32_t r = rec[k], cl = code_of(r);
+      const uint32_t r = rec[rec_index(bt, k)], cl = code_of(r);
       len = (cl >> 16) + ((r >> 14) & 15);
       // code (<= 15 bits) and raw bits (<= 13): one <= 28-bit value
       val = (cl & 0xFFFFu) | ((r >> 18) << (cl >> 16));
@@ -558,9 +606,12 @@ __device__ __forceinline__ void ans_chain(const AnsArgs& a, uint32_t blk) {
   __builtin_amdgcn_s_setprio(3);
   const int n = (int)(a.ntok[g * 3] + a.ntok[g * 3 + 1] + a.ntok[g * 3 + 2]);
   const uint64_t b = (uint64_t)slot * kGroupTokStride;
+  uint32_t bt[kBands];  // the group's stream = its bands' record spaces, in order
+#pragma unroll
+  for (int i = 0; i < kBands; i++) bt[i] = a.bandtok[g * kBands + i];
   // every lane starts from the initial state x = 0x130000
   uint32_t k = 0x130u, v = 0;
-  uint32_t rec = (int)lane < min(64, n) ? a.tokens[b + n - 1 - lane] : 0u;
+  uint32_t rec = (int)lane < min(64, n) ? a.tokens[b + rec_index(bt, n - 1 - lane)] : 0u;
   for (int hi = n; hi > 0; hi -= 64) {
     const int cnt = min(64, hi);
     // lane L: record hi - 1 - L.  Lanes past cnt get f = 4096 (a valid
@@ -575,7 +626,7 @@ __device__ __forceinline__ void ans_chain(const AnsArgs& a, uint32_t blk) {
     const uint32_t nf2 = (uint32_t)(-(int)(2 * f));
     const double rcp = 1.0 / (double)f, hr = 0.5 * rcp;
     const int hn = hi - 64;
-    const uint32_t nrec = (int)lane < min(64, hn) ? a.tokens[b + hn - 1 - lane] : 0u;
+    const uint32_t nrec = (int)lane < min(64, hn) ? a.tokens[b + rec_index(bt, hn - 1 - lane)] : 0u;
     uint32_t X = 0;     // lane L: the state before record L's step
     uint32_t xin = 0;   // the state handed to the previous step
     auto step = [&](int s) {
@@ -714,7 +765,7 @@ void launch_ans_emit(const AnsArgs& a, hipStream_t s) {
 }
 
 void launch_ac_hist(const AcArgs& a, uint32_t ngroups, hipStream_t s) {
-  if (ngroups) hipLaunchKernelGGL(ac_hist_kernel, dim3(ngroups), dim3(kAcThreads), 0, s, a);
+  if (ngroups) hipLaunchKernelGGL(ac_hist_kernel, dim3(ngroups * kBands), dim3(kHistThreads), 0, s, a);
 }
 void launch_ac_emit(const AcArgs& a, uint32_t ngroups, hipStream_t s) {
   if (ngroups) hipLaunchKernelGGL(ac_emit_kernel, dim3(ngroups), dim3(kAcThreads), 0, s, a);

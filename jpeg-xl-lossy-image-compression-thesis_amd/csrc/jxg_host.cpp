@@ -506,10 +506,10 @@ struct Ctx {
   DevBuf<uint32_t> chunkbits, stream_chunks, scratch, scratch_lf, chunks, out, out_ac;
   DevBuf<uint64_t> chunkoff;
   // Per-frame statistics, zeroed by one memset and downloaded by two copies
-  // (AC part, LF part): [hist_ac | bound | ntok][lfhist | sbound | vcount]
+  // (AC part, LF part): [hist_ac | bound | ntok | bandtok][lfhist | sbound | vcount]
   DevBuf<uint8_t> stat;
   PinBuf<uint8_t> h_stat;
-  View<uint32_t> hist_ac, bound, ntok, lfhist, sbound, vcount;
+  View<uint32_t> hist_ac, bound, ntok, bandtok, lfhist, sbound, vcount;
   View<uint32_t> h_hist_ac, h_bound, h_ntok, h_lfhist, h_sbound, h_vcount;
   size_t stat_lf = 0, stat_bytes = 0;  // byte offset of the LF part, total
   // Per-frame code tables, uploaded by one copy (ANS) or two (prefix codes:
@@ -916,6 +916,8 @@ static jxg_status stage_alloc(Ctx* c, Job& J) {
     o = al(o + (size_t)f.ngroups * 4);
     const size_t o_ntok = o;
     o = al(o + (size_t)f.ngroups * 12);
+    const size_t o_bandtok = o;
+    o = al(o + (size_t)f.ngroups * 16);
     const size_t o_lfhist = o;
     o = al(o + (size_t)ns * 4 * kAlpha * 4);
     const size_t o_sbound = o;
@@ -929,6 +931,7 @@ static jxg_status stage_alloc(Ctx* c, Job& J) {
     c->hist_ac.set(c->stat.p, o_hist, (size_t)kMaxClusters * kAlpha);
     c->bound.set(c->stat.p, o_bound, f.ngroups);
     c->ntok.set(c->stat.p, o_ntok, (size_t)f.ngroups * 3);
+    c->bandtok.set(c->stat.p, o_bandtok, (size_t)f.ngroups * 4);
     c->lfhist.set(c->stat.p, o_lfhist, (size_t)ns * 4 * kAlpha);
     c->sbound.set(c->stat.p, o_sbound, ns);
     c->vcount.set(c->stat.p, o_vcount, f.nlf);
@@ -1025,6 +1028,7 @@ static jxg_status stage_alloc(Ctx* c, Job& J) {
   aa.hist = c->hist_ac.p;
   aa.bound = c->bound.p;
   aa.ntok = c->ntok.p;
+  aa.bandtok = c->bandtok.p;
   aa.codes = c->codes_ac.p;
   aa.base = c->gbase.p;
   aa.bits = c->gbits.p;
@@ -1428,6 +1432,7 @@ static jxg_status stage_emit(Ctx* c, Job& J, bool sync = true) {
     na.val = c->tval.p;
     na.len = c->tlen.p;
     na.ntok = c->ntok.p;
+    na.bandtok = c->bandtok.p;
     na.tab = c->ans_tab.p;
     na.nhist = J.nhist_ans;
     na.state = c->ans_state.p;

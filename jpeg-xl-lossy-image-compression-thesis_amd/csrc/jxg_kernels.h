@@ -103,11 +103,14 @@ struct AcArgs {
   uint32_t* scratch;     // bit buffer (emit pass, zeroed)
   uint32_t* bits;        // [ngroups] exact bits (emit pass)
   uint32_t* tokens;      // token records (cluster | tok << 8 | nbits << 14 | bits << 18),
-                         //   slot i (group glist[i] or g0 + i) at i * kGroupTokStride
-                         //   (hist pass writes them)
+                         //   slot i (group glist[i] or g0 + i) at i * kGroupTokStride,
+                         //   band j of it at + j * kBandTokStride (hist pass writes them)
+  uint32_t* bandtok;     // [ngroups][4] tokens of each 8-block-row band (hist pass)
 };
-// records per pass group: 1024 blocks x 3 channels x <= 64 tokens per slice
+// records per pass group: 1024 blocks x 3 channels x <= 64 tokens per slice;
+// per band (8 of the group's 32 block rows): a quarter of that
 constexpr uint64_t kGroupTokStride = 1024ull * 3 * 64;
+constexpr uint64_t kBandTokStride = 256ull * 3 * 64;
 
 // ANS coding of the pass groups' token records (jxg_ac.hip)
 #ifndef JXG_ANS_HISTS  // (jxg_bitstream.h kAnsMaxHists; experiment builds override it)
@@ -122,6 +125,7 @@ struct AnsArgs {
   uint32_t* val;           // [records] emitted bits: 16-bit chunk (if any) then raw bits
   uint8_t* len;            // [records] number of emitted bits
   const uint32_t* ntok;    // [ngroups][3]
+  const uint32_t* bandtok; // [ngroups][4] tokens per band (the group's stream = its bands')
   const uint8_t* tab;      // table blob (kAnsInvOff / kAnsMapOff):
                            //  u32 [8][128] symbol: f - 1 | cum << 12
                            //  u16 [8][4096] alias inverse: slot of position cum + offset
