@@ -90,14 +90,6 @@ constexpr int kAcTok = 64;
 // 256x256 group, so only near-incompressible groups take the slow path
 // (ac_emit: 96 KiB + 33 KiB of code tables, one 1024-thread workgroup per CU)
 constexpr int kEmitLdsWords = 24576;
-// ans_emit's buffer: 48 KiB (6 bpp over a full group; larger sections take the
-// global-atomics path), so the kernel shares a CU with a resident rANS chain
-// workgroup (68 KB) and a transform workgroup of later frames (80 -> 48 KiB:
-// +2 % pipelined 8K at 100 frames, 8 / 16 / 32 / 48 KiB within 1 %)
-#ifndef JXG_ANS_EMIT_WORDS  // (experiment builds override it: tools/build_variant.sh)
-#define JXG_ANS_EMIT_WORDS 12288
-#endif
-constexpr int kAnsEmitLdsWords = JXG_ANS_EMIT_WORDS;
 
 __device__ __forceinline__ int channel_of(int ci) { return ci == 0 ? 1 : (ci == 1 ? 0 : 2); }
 
@@ -504,6 +496,11 @@ __global__ __launch_bounds__(kAcThreads) void ac_emit_kernel(AcArgs a) {
   }
   const uint64_t base = a.base[g];  // word aligned
   const bool lds = total <= (uint32_t)kEmitLdsWords * 32u;
+  if (!lds) {  // the section's scratch words zeroed before the global ORs (no arena memset)
+    for (uint32_t i = threadIdx.x; i < (total + 31) / 32; i += blockDim.x) a.scratch[(base >> 5) + i] = 0;
+    __threadfence();
+    __syncthreads();
+  }
   uint32_t* buf = lds ? sBits : a.scratch;
   const uint64_t bias = lds ? 0 : base;
   for (uint32_t k0 = lo; k0 < hi; k0 += 64) {
@@ -609,6 +606,12 @@ __device__ __forceinline__ void ans_chain(const AnsArgs& a, uint32_t blk) {
   uint32_t bt[kBands];  // the group's stream = its bands' record spaces, in order
 #pragma unroll
   for (int i = 0; i < kBands; i++) bt[i] = a.bandtok[g * kBands + i];
+  // chunk q (stream order) of the group: the chain's iterations cover
+  // [n - 64 (K - q), n - 64 (K - q - 1)) clipped at 0; their emitted bits go
+  // to csum[q] (ans_emit places every segment from them)
+  const uint32_t K = ((uint32_t)n + 63) / 64;
+  uint32_t* csum = a.csum + (uint64_t)slot * kAnsMaxChunks;
+  uint32_t total = 32;  // the state, then every record's bits
   // every lane starts from the initial state x = 0x130000
   uint32_t k = 0x130u, v = 0;
   uint32_t rec = (int)lane < min(64, n) ? a.tokens[b + rec_index(bt, n - 1 - lane)] : 0u;
@@ -670,13 +673,20 @@ __device__ __forceinline__ void ans_chain(const AnsArgs& a, uint32_t blk) {
         k = kk;
       }
     }
+    uint32_t mylen = 0;
     if ((int)lane < cnt) {
       // emitted bits of the record: [16-bit chunk] then its raw bits
       const bool em = (X >> 20) >= f;
       const uint32_t raw = rec >> 18, nb = (rec >> 14) & 15;
+      mylen = em ? nb + 16 : nb;
       a.val[b + hi - 1 - lane] = em ? (X & 0xFFFFu) | raw << 16 : raw;
-      a.len[b + hi - 1 - lane] = (uint8_t)(em ? nb + 16 : nb);
+      a.len[b + hi - 1 - lane] = (uint8_t)mylen;
     }
+    // the chunk's bits (every lane gets the sum)
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) mylen += __shfl_xor(mylen, d, 64);
+    total += mylen;
+    if (lane == 0) csum[K - 1 - (uint32_t)(n - hi) / 64] = mylen;
     rec = nrec;
     if (hi <= 64) {  // the final state: lane cnt - 1's result
       const uint32_t kf = __builtin_amdgcn_readlane(k, cnt - 1);
@@ -685,72 +695,85 @@ __device__ __forceinline__ void ans_chain(const AnsArgs& a, uint32_t blk) {
     }
   }
   if (n == 0 && lane == 0) a.state[g] = 0x130000u;
+  // the section's bit count, and its scratch words zeroed for ans_emit (which
+  // ORs the words it shares with a neighbouring segment): no arena memset
+  if (lane == 0) a.bits[g] = total;
+  uint32_t* dst = a.scratch + (a.base[g] >> 5);
+  for (uint32_t i = lane; i < (total + 31) / 32; i += 64) dst[i] = 0;
 }
 __global__ __launch_bounds__(kAnsWaves * 64) void ans_encode_kernel(AnsArgs a) {
   ans_chain(a, blockIdx.x);
 }
-// bit placement: the 32-bit state, then every record's bits, in order; a
-// contiguous record range per wave, coalesced reads, wave scans of the
-// lengths (as ac_emit)
-__global__ __launch_bounds__(kAcThreads) void ans_emit_kernel(AnsArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t sBits[kAnsEmitLdsWords];
-  __shared__ uint32_t sWave[kAcThreads / 64];
-  const uint32_t g = slot_group(a.glist, a.g0, blockIdx.x);
+// bit placement: the 32-bit state, then every record's bits, in order.  One
+// 256-thread workgroup per (group, segment of kSegChunks chunks of 64
+// records): the segment's first bit is 32 + the chain's chunk sums before it
+// (no pass over the lengths); each wave places whole chunks (their offsets
+// from the same sums) with a wave scan of the lengths into an LDS image of
+// the segment aligned to the scratch words, then the workgroup stores it --
+// plain stores inside the segment, atomic ORs on the two words it may share
+// with its neighbours (zeroed by the chain).
+constexpr int kSegChunks = 64, kEmitThreads = 256;
+constexpr int kSegWords = (kSegChunks * 64 * 29 + 31) / 32 + 2;  // <= 29 bits per record
+__global__ __launch_bounds__(kEmitThreads) void ans_emit_kernel(AnsArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t sBits[kSegWords];
+  __shared__ uint32_t sCs[kSegChunks + 1];
+  __shared__ uint32_t sPre[kEmitThreads / 64];
+  const uint32_t slot = blockIdx.x, seg = blockIdx.y;
+  const uint32_t g = slot_group(a.glist, a.g0, slot);
   const uint32_t n = a.ntok[g * 3] + a.ntok[g * 3 + 1] + a.ntok[g * 3 + 2];
-  const uint64_t b = (uint64_t)blockIdx.x * kGroupTokStride;
-  constexpr int kWaves = kAcThreads / 64;
+  const uint32_t K = (n + 63) / 64, q0 = seg * kSegChunks;
+  const uint64_t base = a.base[g];  // word aligned
+  if (seg == 0 && threadIdx.x == 0) a.scratch[base >> 5] = a.state[g];
+  if (q0 >= K) return;
+  const uint32_t q1 = min(K, q0 + kSegChunks);
+  const uint32_t* csum = a.csum + (uint64_t)slot * kAnsMaxChunks;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const uint32_t chunk = ((n + kWaves * 64 - 1) / (kWaves * 64)) * 64;
-  const uint32_t lo = min(n, wv * chunk), hi = min(n, lo + chunk);
-  uint32_t tot = 0;
-  for (uint32_t k = lo + lane; k < hi; k += 64) tot += a.len[b + k];
+  // bits before the segment: 32 + sum of the chunks before q0
+  uint32_t pre = 0;
+  for (uint32_t q = threadIdx.x; q < q0; q += kEmitThreads) pre += csum[q];
 #pragma unroll
-  for (int d = 32; d > 0; d >>= 1) tot += __shfl_xor(tot, d, 64);
-  if (lane == 0) sWave[wv] = tot;
+  for (int d = 32; d > 0; d >>= 1) pre += __shfl_xor(pre, d, 64);
+  if (lane == 0) sPre[wv] = pre;
+  if (threadIdx.x <= kSegChunks) sCs[threadIdx.x] = q0 + threadIdx.x < q1 ? csum[q0 + threadIdx.x] : 0u;
+  for (int i = threadIdx.x; i < kSegWords; i += kEmitThreads) sBits[i] = 0;
   __syncthreads();
-  uint32_t run = 32, total = 32;  // the state comes first
-#pragma unroll
-  for (int i = 0; i < kWaves; i++) {
-    const uint32_t x = sWave[i];
-    run += i < wv ? x : 0u;
-    total += x;
-  }
-  const uint64_t base = a.base[g];
-  const bool lds = total <= (uint32_t)kAnsEmitLdsWords * 32u;
-  if (lds) {  // clear only the section's words
-    const uint32_t nq = (total + 127) / 128;
-    for (uint32_t i = threadIdx.x; i < nq; i += blockDim.x)
-      reinterpret_cast<uint4*>(sBits)[i] = make_uint4(0, 0, 0, 0);
-    __syncthreads();
-  }
-  uint32_t* buf = lds ? sBits : a.scratch;
-  const uint64_t bias = lds ? 0 : base;
-  if (threadIdx.x == 0) {
-    // base is word aligned: the state is word 0
-    if (lds) sBits[0] = a.state[g];
-    else a.scratch[base >> 5] = a.state[g];
-  }
-  for (uint32_t k0 = lo; k0 < hi; k0 += 64) {
-    const uint32_t k = k0 + lane;
+  const uint64_t start = base + 32 + sPre[0] + sPre[1] + sPre[2] + sPre[3];  // the segment's first bit
+  const uint32_t sh0 = (uint32_t)(start & 31);
+  uint32_t segbits = 0;
+  for (uint32_t q = 0; q < q1 - q0; q++) segbits += sCs[q];
+  // chunk q's records: [chunk_lo(q), chunk_lo(q + 1)), chunk_lo(K) = n
+  auto chunk_lo = [&](uint32_t q) { return q == 0 ? 0u : n - 64u * (K - q); };
+  const uint64_t b = (uint64_t)slot * kGroupTokStride;
+  constexpr int kPerWave = kSegChunks / (kEmitThreads / 64);
+  uint32_t run = sh0;  // bit offset inside the LDS image
+  for (int i = 0; i < wv * kPerWave; i++) run += sCs[i];
+  for (int i = 0; i < kPerWave; i++) {
+    const uint32_t q = q0 + (uint32_t)(wv * kPerWave + i);
+    if (q >= q1) break;
+    const uint32_t lo = chunk_lo(q), hi = chunk_lo(q + 1);
+    const uint32_t k = lo + (uint32_t)lane;
     const uint32_t len = k < hi ? a.len[b + k] : 0u;
     const uint32_t val = k < hi ? a.val[b + k] : 0u;
     const uint32_t incl = wave_incl_scan(len);
     if (len) {
-      const uint64_t pos = bias + run + incl - len;
-      const uint64_t w = pos >> 5;
-      const uint32_t sh = (uint32_t)(pos & 31);
-      atomicOr(&buf[w], val << sh);
-      if (sh + len > 32) atomicOr(&buf[w + 1], val >> (32 - sh));
+      const uint32_t pos = run + incl - len;
+      const uint32_t w = pos >> 5, sh = pos & 31;
+      atomicOr(&sBits[w], val << sh);
+      if (sh + len > 32) atomicOr(&sBits[w + 1], val >> (32 - sh));
     }
-    run += __shfl(incl, 63, 64);
+    run += sCs[wv * kPerWave + i];
   }
-  if (lds) {
-    __syncthreads();
-    const uint32_t nw = (total + 31) / 32;
-    uint32_t* dst = a.scratch + (base >> 5);
-    for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = sBits[i];
+  __syncthreads();
+  const uint32_t nw = (sh0 + segbits + 31) / 32;
+  uint32_t* dst = a.scratch + (start >> 5);
+  for (uint32_t i = threadIdx.x; i < nw; i += kEmitThreads) {
+    const uint32_t v = sBits[i];
+    if (i == 0 || i == nw - 1) {
+      if (v) atomicOr(&dst[i], v);
+    } else {
+      dst[i] = v;
+    }
   }
-  if (threadIdx.x == 0) a.bits[g] = total;
 }
 
 void launch_ans(const AnsArgs& a, hipStream_t s) {
@@ -758,10 +781,11 @@ void launch_ans(const AnsArgs& a, hipStream_t s) {
   if (!n) return;
   hipLaunchKernelGGL(ans_encode_kernel, dim3((n + kAnsWaves - 1) / kAnsWaves), dim3(kAnsWaves * 64),
                      0, s, a);
-  hipLaunchKernelGGL(ans_emit_kernel, dim3(n), dim3(kAcThreads), 0, s, a);
+  launch_ans_emit(a, s);
 }
 void launch_ans_emit(const AnsArgs& a, hipStream_t s) {
-  if (a.n) hipLaunchKernelGGL(ans_emit_kernel, dim3(a.n), dim3(kAcThreads), 0, s, a);
+  const uint32_t nseg = (a.max_tokens + kSegChunks * 64 - 1) / (kSegChunks * 64);
+  if (a.n && nseg) hipLaunchKernelGGL(ans_emit_kernel, dim3(a.n, nseg), dim3(kEmitThreads), 0, s, a);
 }
 
 void launch_ac_hist(const AcArgs& a, uint32_t ngroups, hipStream_t s) {

@@ -184,6 +184,9 @@ __global__ __launch_bounds__(256) void lf_scan_kernel(LfArgs a) {
     __syncthreads();
   }
   if (threadIdx.x == 0) a.stream_bits[sid] = (uint32_t)(run - start);
+  // the stream's scratch words zeroed for lf_emit's ORs (no arena memset)
+  uint32_t* dst = a.scratch + (start >> 5);
+  for (uint64_t i = threadIdx.x; i < (run - start + 31) / 32; i += blockDim.x) dst[i] = 0;
 }
 
 // workgroup exclusive scan of one value per thread (256 threads)
@@ -235,23 +238,48 @@ __device__ __forceinline__ uint32_t read_bits32(const uint32_t* src, uint64_t bi
   return lo;
 }
 
-__global__ __launch_bounds__(256) void concat_kernel(const ConcatPiece* pieces,
-                                                     const uint32_t* scratch,
-                                                     const uint32_t* chunks,
-                                                     const uint32_t* scratch2, uint32_t* out) {
-  const ConcatPiece p = pieces[blockIdx.y];
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i * 32 >= p.nbits) return;
-  const uint32_t* src = p.arena == 1 ? chunks : (p.arena == 2 ? scratch2 : scratch);
-  const uint64_t nb = p.nbits - i * 32 < 32 ? p.nbits - i * 32 : 32;
-  uint32_t v = read_bits32(src, p.src_bit + i * 32);
-  if (nb < 32) v &= (1u << nb) - 1u;
-  const uint64_t d = p.dst_bit + i * 32;
-  const uint64_t w = d >> 5;
-  const int sh = (int)(d & 31);
-  if (v == 0) return;
-  atomicOr(&out[w], v << sh);
-  if (sh && (uint64_t)sh + nb > 32) atomicOr(&out[w + 1], v >> (32 - sh));
+// One thread per output word: the word's bits from the pieces that overlap
+// it (pieces are sorted by destination and disjoint), one plain store -- so
+// the output needs no zero fill.  The workgroup's first piece is found once
+// (binary search by thread 0); each thread walks on from it.
+constexpr int kConcatThreads = 256;
+__global__ __launch_bounds__(kConcatThreads) void concat_kernel(const ConcatPiece* pieces,
+                                                                uint32_t npieces,
+                                                                const uint32_t* scratch,
+                                                                const uint32_t* chunks,
+                                                                const uint32_t* scratch2,
+                                                                uint32_t* out, uint64_t out_words) {
+  __shared__ uint32_t sFirst;
+  const uint64_t w0 = (uint64_t)blockIdx.x * kConcatThreads;
+  if (threadIdx.x == 0) {
+    // first piece ending after the workgroup's first bit
+    uint32_t lo = 0, hi = npieces;
+    const uint64_t bit0 = w0 * 32;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (pieces[mid].dst_bit + pieces[mid].nbits <= bit0) lo = mid + 1;
+      else hi = mid;
+    }
+    sFirst = lo;
+  }
+  __syncthreads();
+  const uint64_t w = w0 + threadIdx.x;
+  if (w >= out_words) return;
+  const uint64_t b0 = w * 32, b1 = b0 + 32;
+  uint32_t v = 0;
+  for (uint32_t i = sFirst; i < npieces; i++) {
+    const ConcatPiece p = pieces[i];
+    if (p.dst_bit >= b1) break;
+    if (p.dst_bit + p.nbits <= b0) continue;
+    const uint64_t s0 = p.dst_bit > b0 ? p.dst_bit : b0;
+    const uint64_t e0 = p.dst_bit + p.nbits < b1 ? p.dst_bit + p.nbits : b1;
+    const uint32_t* src = p.arena == 1 ? chunks : (p.arena == 2 ? scratch2 : scratch);
+    uint32_t x = read_bits32(src, p.src_bit + (s0 - p.dst_bit));
+    const uint32_t nb = (uint32_t)(e0 - s0);
+    if (nb < 32) x &= (1u << nb) - 1u;
+    v |= x << (uint32_t)(s0 - b0);
+  }
+  out[w] = v;
 }
 
 // ------------------------------- launchers ---------------------------------
@@ -267,13 +295,13 @@ void launch_lf_scan(const LfArgs& a, uint32_t nstreams, hipStream_t s) {
 void launch_lf_emit(const LfArgs& a, uint32_t nchunks, hipStream_t s) {
   hipLaunchKernelGGL(lf_emit_kernel, dim3(nchunks), dim3(256), 0, s, a);
 }
-void launch_concat(const ConcatPiece* pieces, uint32_t npieces, uint64_t max_words,
+void launch_concat(const ConcatPiece* pieces, uint32_t npieces, uint64_t out_words,
                    const uint32_t* scratch, const uint32_t* chunks, const uint32_t* scratch2,
                    uint32_t* out, hipStream_t s) {
-  if (npieces == 0 || max_words == 0) return;
-  const uint32_t gx = (uint32_t)((max_words + 255) / 256);
-  hipLaunchKernelGGL(concat_kernel, dim3(gx, npieces), dim3(256), 0, s, pieces, scratch,
-                     chunks, scratch2, out);
+  if (out_words == 0) return;
+  const uint32_t gx = (uint32_t)((out_words + kConcatThreads - 1) / kConcatThreads);
+  hipLaunchKernelGGL(concat_kernel, dim3(gx), dim3(kConcatThreads), 0, s, pieces, npieces,
+                     scratch, chunks, scratch2, out, out_words);
 }
 
 

@@ -963,6 +963,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
   const int tx = tile_id >= 0 ? tile_id % (int)a.tiles_x : (int)blockIdx.x;
   const int ty = tile_id >= 0 ? tile_id / (int)a.tiles_x : (int)blockIdx.y;
   const int ox = tx * kTile - 1, oy = ty * kTile - 1;
+  if (a.zero) {  // the frame's statistics arena (the statistics kernels add into it)
+    const uint32_t nwg = gridDim.x * gridDim.y, wg = blockIdx.y * gridDim.x + blockIdx.x;
+    const uint32_t per = (a.zero_quads + nwg - 1) / nwg;
+    for (uint32_t i = wg * per + tid; i < min(a.zero_quads, (wg + 1) * per); i += kThreads)
+      a.zero[i] = make_uint4(0, 0, 0, 0);
+  }
   if (tid < 256) {
     sLut[tid] = c_lut[tid];
     sBtab[tid] = c_btab[tid];

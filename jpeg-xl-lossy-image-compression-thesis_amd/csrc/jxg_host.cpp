@@ -527,7 +527,7 @@ struct Ctx {
   View<uint32_t> gbits, stream_bits, h_gbits, h_sbits;
   uint32_t* lf_scratch = nullptr;  // LF-stream bit arena (scratch_lf, or in scratch)
   DevBuf<uint32_t> tile_list, glist;  // shard: tile ids, pass groups (non-contiguous plans)
-  DevBuf<uint32_t> tokens, tval, ans_state;  // ANS coder
+  DevBuf<uint32_t> tokens, tval, ans_state, csum;  // ANS coder
   DevBuf<uint8_t> tlen;
   DevBuf<LfRow> rows;
   DevBuf<LfChunk> lfchunks;
@@ -831,7 +831,7 @@ struct Job {
   bool homog = false;
   bool ans = false;  // ANS instead of prefix codes for the AC stream
   uint32_t lf = 0;   // frame header loop-filter code (lf_code: Gaborish / EPF)
-  uint32_t nhist_ans = 0;
+  uint32_t nhist_ans = 0, max_tokens = 0;
   uint32_t nrows = 0, nchunks = 0, nstreams = 0;
   AcArgs aa{};
   LfArgs la{};
@@ -1099,6 +1099,10 @@ static jxg_status stage_front(Ctx* c, Job& J) {
   fa.tile_list = listed ? c->tile_list.p : nullptr;
   fa.cmap = c->cmap.p;
   fa.ntiles_all = f.tiles_x * f.tiles_y;
+  // the statistics arena (256-byte aligned sections) is zeroed by the front
+  // kernel's workgroups: no memset launch
+  fa.zero = reinterpret_cast<uint4*>(c->stat.p);
+  fa.zero_quads = (uint32_t)(c->stat_bytes / 16);
   if (listed)
     launch_front_list(fa, (uint32_t)J.plan.tiles.size(), s);
   else if (J.plan.world == 1)
@@ -1144,8 +1148,7 @@ static jxg_status stage_front(Ctx* c, Job& J) {
 
 // ---- stage C: AC token statistics of the plan's pass groups ----
 static jxg_status stage_ac_stats(Ctx* c, Job& J) {
-  // the whole statistics arena (AC and LF histograms, bounds) in one memset
-  JXG_HIP(hipMemsetAsync(c->stat.p, 0, c->stat_bytes, c->stream));
+  // (the statistics arena was zeroed by the front kernel)
   launch_ac_hist(J.aa, J.plan.ng(), c->stream);
   JXG_HIP(hipGetLastError());
   return JXG_OK;
@@ -1329,6 +1332,7 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
     JXG_HIP(c->tval.ensure(nrec));
     JXG_HIP(c->tlen.ensure(nrec));
     JXG_HIP(c->ans_state.ensure(f.ngroups));
+    JXG_HIP(c->csum.ensure((uint64_t)std::max(1u, J.plan.ng()) * kAnsMaxChunks));
     JXG_HIP(c->ans_tab.ensure(kAnsTabBytes));
     // chain order: the plan's groups by token count, longest first, so a
     // chain workgroup holds groups of similar length and the workgroups of
@@ -1345,13 +1349,15 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
       const uint32_t gx = gl[x], gy = gl[y];
       return nt[gx * 3] + nt[gx * 3 + 1] + nt[gx * 3 + 2] > nt[gy * 3] + nt[gy * 3 + 1] + nt[gy * 3 + 2];
     });
+    J.max_tokens = 0;
+    for (uint32_t g : J.plan.groups)
+      J.max_tokens = std::max(J.max_tokens, nt[g * 3] + nt[g * 3 + 1] + nt[g * 3 + 2]);
   }
   const float ms_ac_codes = ms_since(t_codes);
   if (!J.ans) {
     // prefix codes: the AC code tables now, so the AC emission runs while the
     // host builds the LF-group codes (ANS: every table in one upload below)
     JXG_HIP(hipMemcpyAsync(c->up.p, c->h_up.p, c->up_ac, hipMemcpyHostToDevice, s));
-    JXG_HIP(hipMemsetAsync(c->scratch.p, 0, ac_words * 4, s));
     J.aa.scratch = c->scratch.p;
     launch_ac_emit(J.aa, J.plan.ng(), s);
     JXG_HIP(hipGetLastError());
@@ -1409,13 +1415,11 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
     J.aa.scratch = c->scratch.p;
     JXG_HIP(hipMemcpyAsync(c->up.p + c->up_gbase, c->h_up.p + c->up_gbase,
                            c->up_bytes - c->up_gbase, hipMemcpyHostToDevice, s));
-    JXG_HIP(hipMemsetAsync(c->scratch.p, 0, (ac_words + lf_words) * 4, s));
   } else {
     JXG_HIP(c->scratch_lf.ensure(lf_words));
     c->lf_scratch = c->scratch_lf.p;
     JXG_HIP(hipMemcpyAsync(c->up.p + c->up_lf, c->h_up.p + c->up_lf, c->up_bytes - c->up_lf,
                            hipMemcpyHostToDevice, s));
-    JXG_HIP(hipMemsetAsync(c->scratch_lf.p, 0, lf_words * 4, s));
   }
   J.ms_codes = ms_ac_codes + ms_since(t_lf);
   return JXG_OK;
@@ -1443,6 +1447,8 @@ static jxg_status stage_emit(Ctx* c, Job& J, bool sync = true) {
     na.n = J.plan.ng();
     na.glist = J.aa.glist;
     na.order = c->ans_order.p;
+    na.csum = c->csum.p;
+    na.max_tokens = J.max_tokens;
     launch_ans(na, s);
     JXG_HIP(hipGetLastError());
   }
@@ -1565,8 +1571,7 @@ static jxg_status stage_concat(Ctx* c, Job& J, bool full, std::vector<uint32_t>*
   if (!cps.empty()) std::memcpy(c->h_cat.p, cps.data(), cps.size() * sizeof(ConcatPiece));
   std::memcpy(c->h_cat.p + pb, chunk_words.data(), wb);
   JXG_HIP(hipMemcpyAsync(c->cat.p, c->h_cat.p, pb + wb, hipMemcpyHostToDevice, s));
-  JXG_HIP(hipMemsetAsync(c->out.p, 0, out_words * 4, s));
-  launch_concat(reinterpret_cast<const ConcatPiece*>(c->cat.p), (uint32_t)cps.size(), max_words,
+  launch_concat(reinterpret_cast<const ConcatPiece*>(c->cat.p), (uint32_t)cps.size(), out_words,
                 c->scratch.p, reinterpret_cast<const uint32_t*>(c->cat.p + pb), c->lf_scratch,
                 c->out.p, s);
   JXG_HIP(hipGetLastError());
@@ -1633,10 +1638,9 @@ static jxg_status stage_concat_split(Ctx* c, Job& J, uint8_t** host_out, size_t*
     return fail(JXG_ERR_HIP);
   if (hipStreamWaitEvent(s2, c->ev[7], 0) != hipSuccess ||
       (np && hipMemcpyAsync(c->pieces_ac.p, c->h_pieces_ac.p, np * sizeof(ConcatPiece),
-                            hipMemcpyHostToDevice, s2) != hipSuccess) ||
-      hipMemsetAsync(c->out_ac.p, 0, ac_words * 4, s2) != hipSuccess)
+                            hipMemcpyHostToDevice, s2) != hipSuccess))
     return fail(JXG_ERR_HIP);
-  launch_concat(c->pieces_ac.p, np, max_words, c->scratch.p, c->chunks.p, nullptr, c->out_ac.p, s2);
+  launch_concat(c->pieces_ac.p, np, ac_words, c->scratch.p, c->chunks.p, nullptr, c->out_ac.p, s2);
   if (hipGetLastError() != hipSuccess ||
       (ac_bytes && hipMemcpyAsync(ho + pmax, c->out_ac.p, ac_bytes, hipMemcpyDeviceToHost, s2) !=
                        hipSuccess) ||
@@ -1705,10 +1709,9 @@ static jxg_status stage_concat_split(Ctx* c, Job& J, uint8_t** host_out, size_t*
   if (hipMemcpyAsync(c->chunks.p, chunk_words.data(), chunk_words.size() * 4,
                      hipMemcpyHostToDevice, s) != hipSuccess ||
       hipMemcpyAsync(c->pieces.p, cps.data(), cps.size() * sizeof(ConcatPiece),
-                     hipMemcpyHostToDevice, s) != hipSuccess ||
-      hipMemsetAsync(c->out.p, 0, out_words * 4, s) != hipSuccess)
+                     hipMemcpyHostToDevice, s) != hipSuccess)
     return fail(JXG_ERR_HIP);
-  launch_concat(c->pieces.p, (uint32_t)cps.size(), max_words, c->scratch.p, c->chunks.p,
+  launch_concat(c->pieces.p, (uint32_t)cps.size(), out_words, c->scratch.p, c->chunks.p,
                 c->lf_scratch, c->out.p, s);
   if (hipGetLastError() != hipSuccess ||
       hipMemcpyAsync(data, c->out.p, pbytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -2517,9 +2520,8 @@ static jxg_status shard_assemble_device(Ctx* c, const uint8_t* d_base, const siz
   if (!ho) return JXG_ERR_OOM;
   JXG_HIP(hipMemcpyAsync(c->chunks.p, chunk_words.data(), chunk_words.size() * 4, hipMemcpyHostToDevice, s));
   JXG_HIP(hipMemcpyAsync(c->pieces.p, cps.data(), cps.size() * sizeof(ConcatPiece), hipMemcpyHostToDevice, s));
-  JXG_HIP(hipMemsetAsync(c->out.p, 0, out_words * 4, s));
   // arena 0 = the payload base (word aligned: offsets are multiples of 4)
-  launch_concat(c->pieces.p, (uint32_t)cps.size(), max_words,
+  launch_concat(c->pieces.p, (uint32_t)cps.size(), out_words,
                 reinterpret_cast<const uint32_t*>(d_base), c->chunks.p, nullptr, c->out.p, s);
   JXG_HIP(hipGetLastError());
   if (hipMemcpyAsync(ho, c->out.p, out_words * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||

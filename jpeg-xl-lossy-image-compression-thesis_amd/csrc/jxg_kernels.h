@@ -32,6 +32,8 @@ struct FrontArgs {
   const uint32_t* tile_list;  // shard: tile ids (ty * tiles_x + tx), 1-D grid; or null
   int8_t* cmap;   // [2][tiles] chroma from luma ytox, ytob per 64x64 tile (out)
   uint32_t ntiles_all;  // tiles_x * tiles_y (cmap plane stride)
+  uint4* zero;          // the frame's statistics arena, zeroed by the workgroups (or null)
+  uint32_t zero_quads;  //   its size in 16-byte units
 };
 
 // merge stage (jxg_merge.hip): weight kinds (stored orientation) and the
@@ -138,7 +140,10 @@ struct AnsArgs {
   uint32_t g0, n;          // slots [0, n): group glist[i], or g0 + i when glist is null
   const uint32_t* glist;
   const uint32_t* order;   // chain order of the n slots (longest group first)
+  uint32_t* csum;          // [slots][kAnsMaxChunks] emitted bits of every 64-record chunk
+  uint32_t max_tokens;     // most tokens of any group (ans_emit's segments per group)
 };
+constexpr uint32_t kAnsMaxChunks = (uint32_t)(kGroupTokStride / 64);
 void launch_ans(const AnsArgs& a, hipStream_t s);
 void launch_ans_emit(const AnsArgs& a, hipStream_t s);
 
@@ -244,7 +249,8 @@ void launch_metrics(const MetricArgs& a, hipStream_t s);
 // synthetic benchmark input (jxg_synth.hip): RGB8 rows of `stride` bytes
 hipError_t launch_synth(uint8_t* out, uint32_t w, uint32_t h, size_t stride, uint64_t seed,
                         hipStream_t s);
-void launch_concat(const ConcatPiece* pieces, uint32_t npieces, uint64_t max_words,
+// every word of out[0, out_words) written once (bits no piece covers: 0)
+void launch_concat(const ConcatPiece* pieces, uint32_t npieces, uint64_t out_words,
                    const uint32_t* scratch, const uint32_t* chunks, const uint32_t* scratch2,
                    uint32_t* out, hipStream_t s);
 

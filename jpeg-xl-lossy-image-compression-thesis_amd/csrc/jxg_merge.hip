@@ -709,6 +709,7 @@ __device__ __forceinline__ int max_level(const MergeArgs& a) {
 __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(JXG_MERGE_WPE)))
 void merge_eval_kernel(MergeArgs a) {
   __shared__ __attribute__((aligned(16))) MergeLds S;
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.work[0] = 0;  // merge_resolve's work-list count
   int tile, si;
   if (!decode_wg(a, tile, si)) return;
   const Pass P = make_pass(a, tile, si);
@@ -997,8 +998,6 @@ hipError_t launch_merge(const MergeArgs& a, hipStream_t s) {
   constexpr uint32_t T = JXG_MERGE_CHUNK;
   const uint32_t nwg = (((a.ntiles + 7) / 8 + T - 1) / T) * T * 8 * kNumShapes;
   hipLaunchKernelGGL(merge_eval_kernel, dim3(nwg), dim3(kMThreads), 0, s, a);
-  const hipError_t e = hipMemsetAsync(a.work, 0, sizeof(uint32_t), s);
-  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(merge_resolve_kernel, dim3((a.ntiles + kResolveWaves - 1) / kResolveWaves),
                      dim3(64 * kResolveWaves), 0, s, a);
   const uint32_t nw = min(a.nwrite, a.ntiles * (uint32_t)kNumShapes);
