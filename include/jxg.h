@@ -67,6 +67,12 @@ typedef enum {
  * unpinned; DESIGN.md §3.8] */
 #define JXG_FLAG_GABORISH 16u
 #define JXG_FLAG_EPF 32u
+/* libjxl-shaped adaptive quantization: the masking-based initial quant field
+ * (InitialQuantField / AdaptiveQuantizationMap [ext]: gamma-weighted local
+ * differences, fuzzy erosion, mask, HF and gamma modulation; restated as
+ * recalled, parity with libjxl unpinned; oracle/aq.c) instead of the
+ * activity heuristic; one extra kernel per frame (csrc/jxg_aq.hip) */
+#define JXG_FLAG_AQ_MASKING 64u
 
 typedef struct {
   float distance;      /* cjxl --distance (butteraugli target), (0, 25] */

@@ -1147,6 +1147,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
   const float qff = a.qf_base * mult;
   int raw = (int)(qff * a.inv_g + 0.5f);
   raw = raw < 1 ? 1 : (raw > 256 ? 256 : raw);
+  if (a.qf_in) raw = (int)a.qf_in[gb] + 1;  // the masking quant field (jxg_aq.hip)
   if (r == 0) {
     const float vy = dc[1] * a.dc_mul[1];
     const int qy = vy >= 0.0f ? (int)(vy + 0.5f) : -(int)(-vy + 0.5f);

@@ -310,6 +310,19 @@ static void quant_weights(float out[5][3][64]) {
   }
 }
 
+// fuzzy-erosion weights of the masking quant field (== oracle/aq.c
+// jxo_aq_erosion_weights, float ops in the same order) [ext, as recalled]
+static void aq_erosion_weights(float distance, float w[4]) {
+  float mul = 0.0f;
+  if (distance < 2.0f) mul = (2.0f - distance) * (1.0f / 2.0f);
+  w[0] = 0.125f + mul * 0.0f;
+  w[1] = 0.10f + mul * -0.10f;
+  w[2] = 0.09f + mul * -0.09f;
+  w[3] = 0.06f + mul * -0.06f;
+  const float norm = 0.29959705784054957f / (((w[0] + w[1]) + w[2]) + w[3]);
+  for (int i = 0; i < 4; i++) w[i] *= norm;
+}
+
 static void srgb_lut(float lut[256]) {
   for (int u = 0; u < 256; u++) {
     const double v = u / 255.0;
@@ -493,7 +506,8 @@ struct Ctx {
   hipEvent_t ev[9] = {};
   bool constants_ready = false;
   // device
-  DevBuf<uint8_t> rgb, acs, qf;
+  DevBuf<uint8_t> rgb, acs, qf, aqf;  // aqf: masking quant field (JXG_FLAG_AQ_MASKING)
+  DevBuf<float> lut;                   // sRGB8 -> linear (the AQ kernel)
   DevBuf<int8_t> cmap;  // [2][tiles] chroma from luma (front kernel)
   DevBuf<uint16_t> nz, mnat;
   DevBuf<float> ent, mwk, msdk, miwy, xyb_tiles, mcost;
@@ -582,6 +596,8 @@ static jxg_status init_constants(Ctx* c) {
   static float wts[5][3][64];
   quant_weights(wts);
   JXG_HIP(set_front_constants(lut, wts, c->stream));
+  JXG_HIP(c->lut.ensure(256));
+  JXG_HIP(hipMemcpyAsync(c->lut.p, lut, sizeof(lut), hipMemcpyHostToDevice, c->stream));
   uint8_t tab[kAcCtx];
   for (int i = 0; i < kAcCtx; i++) tab[i] = (uint8_t)ac_cluster(i);
   JXG_HIP(set_cluster_table(tab, c->stream));
@@ -1103,6 +1119,36 @@ static jxg_status stage_front(Ctx* c, Job& J) {
   // kernel's workgroups: no memset launch
   fa.zero = reinterpret_cast<uint4*>(c->stat.p);
   fa.zero_quads = (uint32_t)(c->stat_bytes / 16);
+  if (P.flags & JXG_FLAG_AQ_MASKING) {
+    // the libjxl-shaped masking quant field of the plan's tiles, before the
+    // front kernel (== oracle/aq.c jxo_aq_masking)
+    JXG_HIP(c->aqf.ensure((size_t)f.bxs * f.bys));
+    AqArgs q{};
+    q.rgb = J.d_rgb;
+    q.w = J.w;
+    q.h = J.h;
+    q.stride = J.stride;
+    q.xp = f.xp;
+    q.yp = f.yp;
+    q.bxs = f.bxs;
+    q.bys = f.bys;
+    q.tiles_x = f.tiles_x;
+    q.lut = c->lut.p;
+    aq_erosion_weights(P.distance, q.ew);
+    float dampen = 1.0f;
+    if (P.distance >= 2.0f) {
+      dampen = 1.0f - ((P.distance - 2.0f) / (14.0f - 2.0f));
+      if (dampen < 0.0f) dampen = 0.0f;
+    }
+    q.mul = f.qf_base * dampen;
+    q.add = (1.0f - dampen) * (0.48f * f.qf_base);
+    q.inv_g = f.inv_g;
+    q.qf = c->aqf.p;
+    q.tile_list = listed ? c->tile_list.p : nullptr;
+    launch_aq(q, listed ? (uint32_t)J.plan.tiles.size() : f.tiles_x * f.tiles_y, s);
+    JXG_HIP(hipGetLastError());
+    fa.qf_in = c->aqf.p;
+  }
   if (listed)
     launch_front_list(fa, (uint32_t)J.plan.tiles.size(), s);
   else if (J.plan.world == 1)

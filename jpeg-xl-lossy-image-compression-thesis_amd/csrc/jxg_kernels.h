@@ -34,7 +34,22 @@ struct FrontArgs {
   uint32_t ntiles_all;  // tiles_x * tiles_y (cmap plane stride)
   uint4* zero;          // the frame's statistics arena, zeroed by the workgroups (or null)
   uint32_t zero_quads;  //   its size in 16-byte units
+  const uint8_t* qf_in; // [nb] raw - 1 of the masking quant field (jxg_aq.hip), or null:
+                        //   the activity heuristic
 };
+// libjxl-shaped masking quant field (jxg_aq.hip, oracle/aq.c)
+struct AqArgs {
+  const uint8_t* rgb;
+  uint32_t w, h;
+  size_t stride;
+  uint32_t xp, yp, bxs, bys, tiles_x;
+  const float* lut;      // [256] sRGB8 -> linear (device)
+  float ew[4];           // fuzzy-erosion weights (aq_erosion_weights)
+  float mul, add, inv_g; // quant field = pow2(...) mul + add; raw = round(qf inv_g)
+  uint8_t* qf;           // [nb] raw - 1 (out)
+  const uint32_t* tile_list;  // shard: tile ids, or null: every tile (1-D grid)
+};
+void launch_aq(const AqArgs& a, uint32_t ntiles, hipStream_t s);
 
 // merge stage (jxg_merge.hip): weight kinds (stored orientation) and the
 // nine merged shapes' pixel-orientation tables, column-major ([kx * R + ky])

@@ -36,6 +36,7 @@ FLAG_ANS = 4
 FLAG_FORCE_ONE_STREAM = 8  # testing: the split assembly's one-stream fallback (same bytes)
 FLAG_GABORISH = 16  # encoder inverse Gaborish + the decoder's Gaborish (cjxl --gaborish=1)
 FLAG_EPF = 32  # the decoder's edge-preserving filter, iterations by distance (cjxl --epf=-1)
+FLAG_AQ_MASKING = 64  # libjxl-shaped masking quant field (oracle/aq.c) instead of the activity AQ
 
 
 class JxgError(RuntimeError):

@@ -18,7 +18,7 @@
 
 int jxo_front_block(const jxo_frame* f, const float px[3][64], const float* homog,
                     int32_t q[3][64], int32_t dcq[3], int* qf_raw, float* ent_out,
-                    const float cfl[2]);
+                    const float cfl[2], int aq_raw);
 
 static const jxo_uintcfg kCfg = {4, 2, 0};
 static const jxo_uintcfg kCfgMap = {8, 0, 0};
@@ -425,12 +425,19 @@ int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h, size_t row_strid
   if (!rgb || w == 0 || h == 0 || w > (1u << 18) || h > (1u << 18)) return -1;
   if (!(p->distance > 0.0f) || p->distance > 25.0f) return -2;
   if (p->coder != 0 && p->coder != 1) return -3;
-  if (p->filters & ~(JXO_FILTER_GAB | JXO_FILTER_EPF)) return -4;
+  if (p->filters & ~(JXO_FILTER_GAB | JXO_FILTER_EPF | JXO_OPT_AQ_MASKING)) return -4;
   jxo_frame f;
   jxo_frame_init(&f, w, h, p);
   const size_t plane = (size_t)f.xp * f.yp, nb = (size_t)f.bxs * f.bys;
   float* xyb = (float*)malloc(sizeof(float) * plane * 3);
   jxo_srgb8_to_xyb(rgb, w, h, row_stride, f.xp, f.yp, xyb);
+  /* the masking quant field on the XYB image before the inverse Gaborish
+   * (libjxl's order [ext]) */
+  uint8_t* aqraw = NULL;
+  if (p->filters & JXO_OPT_AQ_MASKING) {
+    aqraw = (uint8_t*)malloc(nb);
+    jxo_aq_masking(&f, xyb, aqraw);
+  }
   if (p->filters & JXO_FILTER_GAB) jxo_gab_inverse(xyb, f.xp, f.yp);
   out->xsize = w;
   out->ysize = h;
@@ -482,7 +489,7 @@ int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h, size_t row_strid
       float cfl[2];
       jxo_cfl_factors(out->cmap[ti], out->cmap[ntiles + ti], cfl);
       int t = jxo_front_block(&f, px, out->homog ? out->homog + 3 * b : NULL, q,
-                              dcq, &raw, &ent[b], cfl);
+                              dcq, &raw, &ent[b], cfl, aqraw ? (int)aqraw[b] + 1 : 0);
       out->acs[b] = (uint8_t)t;
       out->qf[b] = (uint8_t)(raw - 1);
       raws[b] = raw;
@@ -543,6 +550,7 @@ int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h, size_t row_strid
   free(ent);
   free(raws);
   free(xyb);
+  free(aqraw);
 
   /* ---- AC tokens and clustered histograms ---- */
   actok** gt = (actok**)malloc(sizeof(actok*) * f.ngroups);

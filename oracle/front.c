@@ -498,7 +498,7 @@ void jxo_quant_dc(const jxo_frame* f, const float dc[3], int32_t dcq[3]) {
  * writes qf raw (1..256), quantized AC and DC. */
 int jxo_front_block(const jxo_frame* f, const float px[3][64], const float* homog,
                     int32_t q[3][64], int32_t dcq[3], int* qf_raw, float* ent_out,
-                    const float cfl[2]) {
+                    const float cfl[2], int aq_raw) {
   /* block DC = mean: row partial sums (left to right), then the 8 row sums
    * tree-summed -- the 8-lane order of the GPU path (lane = row) */
   float dc[3];
@@ -535,6 +535,7 @@ int jxo_front_block(const jxo_frame* f, const float px[3][64], const float* homo
   int raw = (int)(qff * f->inv_g + 0.5f);
   if (raw < 1) raw = 1;
   if (raw > 256) raw = 256;
+  if (aq_raw > 0) raw = aq_raw; /* the masking field (aq.c, JXO_OPT_AQ_MASKING) */
   *qf_raw = raw;
   const float scale = (float)f->G * (float)raw / 65536.0f;
 

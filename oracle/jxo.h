@@ -72,6 +72,9 @@ typedef struct {
  * jxo_epf_iters(distance) iterations, constant sharpness JXO_EPF_SHARPNESS */
 #define JXO_FILTER_GAB 1u
 #define JXO_FILTER_EPF 2u
+/* encoder option in the same mask (not a filter): the libjxl-shaped masking
+ * quant field (aq.c) instead of the activity heuristic */
+#define JXO_OPT_AQ_MASKING 4u
 #define JXO_EPF_SHARPNESS 4
 int jxo_epf_iters(float distance);
 /* loop-filter code of the frame header: bit 0 gab, bits 1-2 epf_iters */

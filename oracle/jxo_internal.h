@@ -162,4 +162,15 @@ int jxo_ans_cluster(const uint32_t (*hist)[JXO_ALPHA], int nh, int* assign);
 void jxo_ans_write_stream(jxo_bw* w, const jxo_ans* hists, size_t n, const uint8_t* hist,
                           const uint8_t* sym, const uint8_t* nbits, const uint32_t* bits);
 
+/* libjxl-shaped masking quant field (aq.c): raw - 1 of every block [bys][bxs],
+ * on the block-padded XYB frame before the inverse Gaborish */
+void jxo_aq_masking(const jxo_frame* f, const float* xyb, uint8_t* raw);
+/* its stages (the GPU kernel jxg_aq.hip follows them op for op) */
+float jxo_aq_diff(const float* Y, uint32_t xp, uint32_t yp, int x, int y);
+float jxo_aq_cell(const float* Y, uint32_t xp, uint32_t yp, int cx, int cy);
+void jxo_aq_erosion_weights(float distance, float w[4]);
+float jxo_aq_erode(const float* cells, int ncx, int ncy, int cx, int cy, const float w[4]);
+float jxo_aq_mask(float v);
+float jxo_aq_modulate(const float* X, const float* Y, uint32_t xp, int bx, int by, float v);
+
 #endif

@@ -114,4 +114,4 @@ def test_epf_raises_psnr_at_d2(oracle, decoder):
 
 def test_bad_filters_refused(oracle):
     with pytest.raises(RuntimeError):
-        oracle.encode(synth_rgb8(16, 16, 1), 1.0, 7, 0, 0, 4)
+        oracle.encode(synth_rgb8(16, 16, 1), 1.0, 7, 0, 0, 8)  # (bit 2 is JXO_OPT_AQ_MASKING)
