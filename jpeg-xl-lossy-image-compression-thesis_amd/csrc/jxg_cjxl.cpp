@@ -120,12 +120,16 @@ int main(int argc, char** argv) {
   if (argc < 3) {
     std::fprintf(stderr,
                  "usage: %s INPUT OUTPUT [--distance=D] [--effort=E] "
-                 "[--proposals=none|P|F|PF] [--coder=prefix|ans] [--gaborish=0|1] "
-                 "[--epf=-1|0] [--device=N]\n",
+                 "[--proposals=none|P|F|PF] [--coder=ans|prefix] [--gaborish=1|0] "
+                 "[--epf=-1|0] [--aq=masking|activity] [--device=N]\n"
+                 "defaults: cjxl's (ANS, --gaborish=1, --epf=-1, masking AQ)\n",
                  argv[0]);
     return 1;
   }
-  jxg_params p{1.0f, 7, 0, 1, 0, 0};
+  // `cjxl IN OUT --distance=D --effort=E` with no other flag (the harness's
+  // argv, docker_manager.rs:126-136) gets cjxl's VarDCT defaults [ext]: ANS,
+  // Gaborish on, EPF iterations by distance, the masking quant field
+  jxg_params p{1.0f, 7, 0, 1, JXG_FLAG_ANS | JXG_FLAG_GABORISH | JXG_FLAG_EPF | JXG_FLAG_AQ_MASKING, 0};
   for (int i = 3; i < argc; i++) {
     const char* a = argv[i];
     if (!std::strncmp(a, "--distance=", 11) || !std::strncmp(a, "-d=", 3))
@@ -136,24 +140,31 @@ int main(int argc, char** argv) {
       const char* v = a + 12;
       p.proposals = (std::strchr(v, 'P') ? JXG_PROPOSAL_P : 0u) | (std::strchr(v, 'F') ? JXG_PROPOSAL_F : 0u);
     } else if (!std::strncmp(a, "--coder=", 8)) {
-      if (!std::strcmp(a + 8, "ans"))
-        p.flags |= JXG_FLAG_ANS;
-      else if (std::strcmp(a + 8, "prefix")) {
+      if (!std::strcmp(a + 8, "prefix"))
+        p.flags &= ~JXG_FLAG_ANS;
+      else if (std::strcmp(a + 8, "ans")) {
         std::fprintf(stderr, "unknown coder: %s\n", a + 8);
         return 1;
       }
     } else if (!std::strncmp(a, "--gaborish=", 11)) {  // cjxl --gaborish
-      if (!std::strcmp(a + 11, "1"))
-        p.flags |= JXG_FLAG_GABORISH;
-      else if (std::strcmp(a + 11, "0")) {
+      if (!std::strcmp(a + 11, "0"))
+        p.flags &= ~JXG_FLAG_GABORISH;
+      else if (std::strcmp(a + 11, "1")) {
         std::fprintf(stderr, "unsupported --gaborish: %s\n", a + 11);
         return 1;
       }
     } else if (!std::strncmp(a, "--epf=", 6)) {  // cjxl --epf: -1 = by distance
-      if (!std::strcmp(a + 6, "-1"))
-        p.flags |= JXG_FLAG_EPF;
-      else if (std::strcmp(a + 6, "0")) {
+      if (!std::strcmp(a + 6, "0"))
+        p.flags &= ~JXG_FLAG_EPF;
+      else if (std::strcmp(a + 6, "-1")) {
         std::fprintf(stderr, "unsupported --epf (-1 or 0): %s\n", a + 6);
+        return 1;
+      }
+    } else if (!std::strncmp(a, "--aq=", 5)) {  // the quant field heuristic
+      if (!std::strcmp(a + 5, "activity"))
+        p.flags &= ~JXG_FLAG_AQ_MASKING;
+      else if (std::strcmp(a + 5, "masking")) {
+        std::fprintf(stderr, "unsupported --aq (masking or activity): %s\n", a + 5);
         return 1;
       }
     } else if (!std::strncmp(a, "--device=", 9))

@@ -13,6 +13,9 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
+# oracle filters mask of cjxl's defaults: Gaborish 1 | EPF 2 | masking AQ 4
+CJXL_DEFAULTS = 7
+
 
 def _paeth(a, b, c):
     p = a + b - c
@@ -53,7 +56,8 @@ def test_cjxl_png_success(jxg_mod, oracle, tmp_path, distance, effort):
     ok, msg = jxg_mod.execute_cjxl(str(src), str(out), distance, effort)
     assert ok, msg
     assert out.name == "photo-a-%s-%d.jxl" % (jxg_mod.rust_f64(distance), effort)
-    assert out.read_bytes() == oracle.encode(img, distance, effort, 0).bytes
+    # cjxl's VarDCT defaults: ANS, Gaborish, EPF by distance, masking AQ
+    assert out.read_bytes() == oracle.encode(img, distance, effort, 0, 1, CJXL_DEFAULTS).bytes
 
 
 def test_cjxl_plain_argv(jxg_mod, oracle, tmp_path):
@@ -67,4 +71,26 @@ def test_cjxl_plain_argv(jxg_mod, oracle, tmp_path):
     p = subprocess.run([jxg_mod.CLI_PATH, str(src), str(out), "--distance=1", "--effort=7"],
                        capture_output=True, text=True)
     assert p.returncode == 0, p.stderr
-    assert out.read_bytes() == oracle.encode(img, 1.0, 7, 0).bytes
+    assert out.read_bytes() == oracle.encode(img, 1.0, 7, 0, 1, CJXL_DEFAULTS).bytes
+
+
+def test_cjxl_flags_override_defaults(jxg_mod, oracle, tmp_path):
+    """--coder=prefix --gaborish=0 --epf=0 --aq=activity: the library's
+    default (unfiltered, activity AQ, prefix codes) encode; each flag alone."""
+    from jxg.synth import natural_rgb8
+
+    img = natural_rgb8(200, 136, 0x4A584C09)
+    src = tmp_path / "in.png"
+    write_png(str(src), img)
+    out = tmp_path / "o.jxl"
+    cases = [(["--coder=prefix", "--gaborish=0", "--epf=0", "--aq=activity"], 0, 0),
+             (["--gaborish=0"], 1, CJXL_DEFAULTS & ~1), (["--epf=0"], 1, CJXL_DEFAULTS & ~2),
+             (["--aq=activity"], 1, CJXL_DEFAULTS & ~4)]
+    for extra, coder, filters in cases:
+        p = subprocess.run([jxg_mod.CLI_PATH, str(src), str(out), "--distance=1.5", "--effort=7"]
+                           + extra, capture_output=True, text=True)
+        assert p.returncode == 0, p.stderr
+        assert out.read_bytes() == oracle.encode(img, 1.5, 7, 0, coder, filters).bytes, extra
+    p = subprocess.run([jxg_mod.CLI_PATH, str(src), str(out), "--aq=butteraugli"],
+                       capture_output=True, text=True)
+    assert p.returncode == 1

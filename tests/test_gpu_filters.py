@@ -114,7 +114,8 @@ def test_cli_filter_flags(jxg_mod, oracle, tmp_path):
     r = subprocess.run([exe, str(src), str(out), "--distance=2.0", "--effort=7",
                         "--gaborish=1", "--epf=-1"], capture_output=True, timeout=120)
     assert r.returncode == 0, r.stderr
-    assert out.read_bytes() == oracle.encode(img, 2.0, 7, 0, 0, GAB | EPF).bytes
+    # (the CLI's defaults: ANS and the masking quant field besides the filters)
+    assert out.read_bytes() == oracle.encode(img, 2.0, 7, 0, 1, GAB | EPF | 4).bytes
     r = subprocess.run([exe, str(src), str(out), "--epf=2"], capture_output=True, timeout=120)
     assert r.returncode == 1
 
