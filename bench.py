@@ -232,6 +232,20 @@ def cpu_baseline(img, distance, effort, proposals, coder, gpu_bytes, sweep=None)
     return res
 
 
+def quality_natural(enc):
+    """decoded PSNR / bpp of the photographic-like 1920x1080 frame (untimed)"""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import jxl_decode
+    from jxg.synth import natural_rgb8
+
+    nat = natural_rgb8(1920, 1080, 3)
+    nd = enc.encode(nat)
+    ndec = jxl_decode.decode(nd).rgb
+    return {"frame": "natural_rgb8(1920, 1080, seed 3)",
+            "psnr_db": round(jxg.calculate_psnr(jxg.calculate_mse(nat, ndec)), 3),
+            "bpp": round(len(nd) * 8.0 / (1920 * 1080), 4)}
+
+
 def quality_probe(enc, img, distance, effort):
     """Decoded quality at the bench settings (untimed): the top-left 1920x1080
     crop of the bench frame, encoded on the GPU, decoded by oracle/jxl_decode.py
@@ -324,6 +338,9 @@ def main():
     ap.add_argument("--alt-thesis", type=int, default=1,
                     help="also time the workload with the thesis proposals P+F "
                          "(reported under 'thesis_proposals'; 0 = off)")
+    ap.add_argument("--alt-cjxl", type=int, default=1,
+                    help="also time the workload with cjxl's VarDCT defaults (Gaborish, EPF, "
+                         "masking AQ; reported under 'cjxl_defaults'; 0 = off)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sweep", default="",
                     help="comma-separated OpenMP thread counts: also time the CPU baseline at "
@@ -382,14 +399,14 @@ def main():
         img = synth_rgb8_device(w, h, SEED_BASE + args.config, local).cpu().numpy()
     torch.cuda.synchronize()
 
-    def run(mode, coder, nstreams=1, proposals=None, pipe=True):
+    def run(mode, coder, nstreams=1, proposals=None, pipe=True, extra_flags=0):
         """Warm up, then time args.steps steps of `mode` ("frames": each rank
         encodes whole frames -- N = 1 / replicas; "shard": ShardStream;
         "shard-sync": encode_sharded)."""
         sharded = mode != "frames"
         per_step, d_imgs = make_frames(sharded)
         nd = len(d_imgs)
-        flags = jxg.FLAG_ANS if coder == "ans" else 0
+        flags = (jxg.FLAG_ANS if coder == "ans" else 0) | extra_flags
         props = args.proposals if proposals is None else proposals
         encs = [jxg.Encoder(distance=args.distance, effort=args.effort,
                             proposals=props, device=local, flags=flags)
@@ -571,6 +588,21 @@ def main():
                   "ms_front_kernel": round(sum(T["front_ms"]) / len(T["front_ms"]), 4),
                   "bytes_per_frame": T["sizes"][-1],
                   "bpp": round(T["sizes"][-1] * 8.0 / (w * h), 4)}
+    cjxl = None
+    cjxl_flags = jxg.FLAG_GABORISH | jxg.FLAG_EPF | jxg.FLAG_AQ_MASKING
+    if mode == "frames" and args.alt_cjxl:
+        # the encode `cjxl IN OUT --distance=1 --effort=7` asks for: its VarDCT
+        # defaults (inverse Gaborish, EPF, the masking quant field) on the same
+        # workload and coder -- the headline line is the unfiltered encode
+        C = run("frames", args.coder, nstreams, pipe=pipeline, extra_flags=cjxl_flags)
+        cjxl = {"flags": "gaborish + epf + masking AQ (jxg_cjxl's defaults = cjxl's [ext])",
+                "value": round(px_step * args.steps / C["dt"] / 1e6, 2),
+                "ms_per_step": round(C["dt"] * 1e3 / args.steps, 3),
+                "bytes_per_frame": C["sizes"][-1],
+                "bpp": round(C["sizes"][-1] * 8.0 / (w * h), 4)}
+        if world == 1 and not args.no_quality:
+            cjxl["quality_natural"] = quality_natural(C["enc"])
+        C["enc"].close()
     if rank == 0:
         ms_step = dt * 1e3 / args.steps
         value = px_step * args.steps / dt / 1e6
@@ -678,6 +710,8 @@ def main():
             res["alt_coder"] = alt
         if thesis is not None:
             res["thesis_proposals"] = thesis
+        if cjxl is not None:
+            res["cjxl_defaults"] = cjxl
         if replicas is not None:
             res["replicas"] = replicas
         if R.get("per_rank"):
