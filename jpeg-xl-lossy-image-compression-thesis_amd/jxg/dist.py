@@ -187,6 +187,19 @@ def gather_payloads(payload: bytes, rank: int, world: int, device, group=None):
     return [bytes(b[:s].cpu().numpy().tobytes()) for b, s in zip(bufs, sizes)]
 
 
+def _comm_device(dev, group=None) -> torch.device:
+    """where a collective's tensors live: HBM under nccl (RCCL), host memory
+    under gloo"""
+    return torch.device("cpu") if dist.get_backend(group) == "gloo" else torch.device(dev)
+
+
+def _copy_back(dst: torch.Tensor, src: torch.Tensor):
+    """dst <- src unless they are the same storage (nccl: the collective wrote
+    dst itself)"""
+    if src.data_ptr() != dst.data_ptr() or src.device != dst.device:
+        dst.copy_(src)
+
+
 def encode_sharded(enc: Encoder, d_rgb: torch.Tensor, width: int, height: int, rank: int,
                    world: int, group=None, bufs=None, copy: bool = True,
                    host: SharedHostBuffer | None = None):
@@ -224,30 +237,25 @@ def encode_sharded(enc: Encoder, d_rgb: torch.Tensor, width: int, height: int, r
     enc.shard_begin(d_rgb.data_ptr(), width, height, rank, world, hist.data_ptr(),
                     send.data_ptr())
     ns, nr = sum(snd), sum(rcv)
-    gloo = dist.get_backend(group) == "gloo"
+    # one code path for both backends: under nccl (RCCL) the collectives run on
+    # the HBM tensors themselves (`.to(comm)` returns the same tensor, the
+    # copy-backs are skipped); gloo (the CPU rehearsal, e.g. several ranks on
+    # one device) stages the same tensors through the host
+    comm = _comm_device(dev, group)
     # ANS: one HF preset per rank -- every rank codes its groups
     # with its own histograms, no all-reduce; HfGlobal is built at assembly
     # from the presets in the payload heads.  Prefix codes: one preset from
     # the summed histogram.
     presets = bool(enc.params.flags & FLAG_ANS)
-    if gloo:
-        # host staging (gloo: CPU rehearsal of the exchange, e.g. several ranks
-        # on one device); the nccl (RCCL) path below keeps everything in HBM
-        if not presets:
-            h = hist.cpu()
-            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
-            hist.copy_(h)
-        if bufs["any"]:
-            r_cpu = torch.empty(nr, dtype=torch.uint8)
-            dist.all_to_all_single(r_cpu, send[:ns].cpu(), output_split_sizes=rcv,
-                                   input_split_sizes=snd, group=group)
-            recv[:nr].copy_(r_cpu)
-    else:
-        if not presets:
-            dist.all_reduce(hist, op=dist.ReduceOp.SUM, group=group)
-        if bufs["any"]:
-            dist.all_to_all_single(recv[:nr], send[:ns], output_split_sizes=rcv,
-                                   input_split_sizes=snd, group=group)
+    if not presets:
+        h = hist.to(comm)
+        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+        _copy_back(hist, h)
+    if bufs["any"]:
+        r = recv[:nr] if comm == dev else torch.empty(nr, dtype=torch.uint8, device=comm)
+        dist.all_to_all_single(r, send[:ns].to(comm), output_split_sizes=rcv,
+                               input_split_sizes=snd, group=group)
+        _copy_back(recv[:nr], r)
     torch.cuda.synchronize(dev)  # the library's stream reads what the collectives wrote
     size = enc.shard_end(hist.data_ptr(), recv.data_ptr())
     if host is not None:
@@ -264,7 +272,7 @@ def encode_sharded(enc: Encoder, d_rgb: torch.Tensor, width: int, height: int, r
     # device assembly: payloads gathered into one buffer on rank 0 (RCCL,
     # device to device; the gloo rehearsal stages the same gather through the
     # host), which assembles them with the concat kernel
-    n = torch.tensor([size], dtype=torch.int64, device="cpu" if gloo else dev)
+    n = torch.tensor([size], dtype=torch.int64, device=comm)
     sizes = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(sizes, n, group=group)
     sizes = [int(x.item()) for x in sizes]
@@ -281,14 +289,14 @@ def encode_sharded(enc: Encoder, d_rgb: torch.Tensor, width: int, height: int, r
     enc.shard_payload(psend.data_ptr(), on_device=True)  # returns with the copy complete
     precv = bufs["precv"]
     views = [precv[r * cap:(r + 1) * cap] for r in range(world)] if rank == 0 else None
-    if gloo:
-        parts = [torch.empty(cap, dtype=torch.uint8) for _ in range(world)] if rank == 0 else None
-        dist.gather(psend.cpu(), parts, dst=0, group=group)
-        if rank == 0:
-            for v, part in zip(views, parts):
-                v.copy_(part)
-    else:
-        dist.gather(psend, views, dst=0, group=group)
+    parts = None
+    if rank == 0:
+        parts = views if comm == dev else [torch.empty(cap, dtype=torch.uint8, device=comm)
+                                           for _ in range(world)]
+    dist.gather(psend.to(comm), parts, dst=0, group=group)
+    if rank == 0:
+        for v, part in zip(views, parts):
+            _copy_back(v, part)
     if rank != 0:
         return None
     torch.cuda.synchronize(dev)
