@@ -2,7 +2,8 @@
 # One GPU-box pass: GPU tests, smoke, the default bench (CPU baseline with a
 # thread sweep), and a 4-rank gloo rehearsal of bench.py's default sharded
 # path on the box's one GPU (bench.py starts the ranks itself).
-# Usage: bash tools/gpu_check.sh TAG [tests|bench|gloo ...]  (default: all)
+# Usage: bash tools/gpu_check.sh TAG [tests|bench|bench20|gloo|cfg|small ...]
+# (default: tests bench gloo)
 set -e
 export TMPDIR=/tmp
 TAG=${1:-check}; shift || true
@@ -17,5 +18,12 @@ for s in $STEPS; do
     bench20) timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-quality > $O/bench20.log 2>&1 ;;
     gloo) JXG_DIST_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 4 --steps 20 --warmup 3 > $O/bench_gloo4.log 2>&1 ;;
     cfg) bash tools/gpu_configs.sh $TAG/cfg ;;
+    small) # small-frame streams: config 3's 1080p frames, a 1/8 slice of the
+           # 8K frame (one rank's load), the 8-context emulation; then a
+           # kernel + copy trace of the 1080p stream
+           timeout -k 10 150 python tools/stream_probe.py --mode plain --w 1920 --h 1080 --frames 256 --warmup 32 > $O/probe_1080p.log 2>&1
+           timeout -k 10 150 python tools/stream_probe.py --mode host --world 1 --h 544 --frames 256 --warmup 32 > $O/probe_slice8.log 2>&1
+           timeout -k 10 150 python tools/stream_probe.py --mode host --world 8 --frames 40 > $O/probe_ctx8.log 2>&1
+           timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d $O/prof_1080p -o run -- python3 tools/stream_probe.py --mode plain --w 1920 --h 1080 --frames 64 --warmup 8 > $O/prof_1080p.log 2>&1 ;;
   esac
 done

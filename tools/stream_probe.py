@@ -1,8 +1,11 @@
-"""Throughput of the streamed-shard paths in ONE process (`world` contexts on
-one GPU play the ranks): native (jxg_shard_stream_*, completion threads) vs
-the Python protocol over jxg_shard_next_head / write_next.  For rocprofv3
-(no torch.distributed launcher in between).
-  python tools/stream_probe.py --mode native --world 2 --frames 40"""
+"""Throughput of the streamed paths in ONE process, for rocprofv3 (no
+torch.distributed launcher in between):
+  host   `world` contexts on one GPU play the ranks of the streamed-shard
+         protocol (jxg_shard_submit_device / next_head / write_next), e.g. a
+         1/8 slice: --world 1 --h 544
+  plain  whole frames through jxg_submit_rgb8_device / jxg_receive, e.g.
+         config 3's frames: --w 1920 --h 1080
+  python tools/stream_probe.py --mode host --world 2 --frames 40"""
 import argparse
 import ctypes
 import mmap
@@ -20,19 +23,19 @@ import jxg  # noqa: E402
 from jxg.synth import synth_rgb8_device  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--mode", choices=("native", "host"), default="native")
+ap.add_argument("--mode", choices=("plain", "host"), default="host")
 ap.add_argument("--world", type=int, default=2)
 ap.add_argument("--frames", type=int, default=40)
 ap.add_argument("--warmup", type=int, default=16)
 ap.add_argument("--w", type=int, default=7680)
 ap.add_argument("--h", type=int, default=4320)
-ap.add_argument("--slots", type=int, default=6)
 a = ap.parse_args()
 w, h, W = a.w, a.h, a.world
 ts = [synth_rgb8_device(w, h, 0x4A584C02 + 100 * k) for k in range(2)]
 torch.cuda.synchronize()
 encs = [jxg.Encoder(flags=jxg.FLAG_ANS) for _ in range(W)]
-depth = min(e.pipeline_depth(w, h, r, W) for r, e in enumerate(encs))
+depth = min(e.pipeline_depth(w, h, r, W) for r, e in enumerate(encs)) if a.mode == "host" \
+    else encs[0].pipeline_depth(w, h)
 stamps = []
 sizes = []
 tsub = [0.0]  # main thread: seconds inside submit calls
@@ -43,36 +46,24 @@ def timed_submit(fn, *args):
     fn(*args)
     tsub[0] += time.perf_counter() - t
 
-if a.mode == "native":
-    sb = w * h * 3 // 2 + (1 << 20)
-    size = encs[0].shard_stream_region_size(w, h, W, a.slots, sb)
-    region = mmap.mmap(-1, size)
-    addr = ctypes.addressof(ctypes.c_char.from_buffer(region))
-    assert jxg.load().jxg_host_register(ctypes.c_void_p(addr), size) == 0
-    for r, e in enumerate(encs):
-        e.shard_stream_begin(addr, size, w, h, r, W, a.slots, sb, r == 0)
-    maxp = depth + a.slots - 2
-    pend = 0
+if a.mode == "plain":
+    # whole frames through the one-context streaming pipeline (config 3 shape
+    # with --w 1920 --h 1080): the per-frame kernel sequence under rocprofv3
+    e0 = encs[0]
 
     def take():
-        for r, e in enumerate(encs):
-            off, n = e.shard_stream_receive()
-            if r == 0:
-                sizes.append(n)
+        cs = e0.receive(copy=False)
+        sizes.append(len(cs))
+        cs.release()
         stamps.append(time.perf_counter())
 
     def run(n):
-        global pend
         for k in range(n):
-            for e in encs:
-                timed_submit(e.shard_stream_submit, ts[k % 2].data_ptr())
-            pend += 1
-            while pend >= maxp or (pend and encs[0].shard_stream_ready()):
+            timed_submit(e0.submit_device, ts[k % 2].data_ptr(), w, h)
+            while e0.pending() > max(16, depth):  # bench.py's replica loop
                 take()
-                pend -= 1
-        while pend:
+        while e0.pending():
             take()
-            pend -= 1
 else:
     buf = np.zeros(w * h * 2 + (1 << 20), dtype=np.uint8)
 
@@ -106,8 +97,5 @@ print("mode %s %dx%d world %d depth %d: %.3f ms/frame, %.1f MPix/s, bytes %d; in
       % (a.mode, w, h, W, depth, dt * 1e3 / a.frames, w * h * a.frames / dt / 1e6, sizes[-1],
          tsub[0] * 1e3 / a.frames, np.median(gaps), np.percentile(gaps, 90), gaps.max()),
       flush=True)
-if a.mode == "native":
-    for e in encs:
-        e.shard_stream_end()
 for e in encs:
     e.close()
