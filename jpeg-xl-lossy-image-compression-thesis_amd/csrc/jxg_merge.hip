@@ -929,14 +929,27 @@ __global__ __launch_bounds__(1024) void vb_list_kernel(VbArgs a) {
   const uint32_t n = bw * bh;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint64_t lt = (1ull << lane) - 1ull;
-  auto block_of = [&](uint32_t i) {
-    return (size_t)(by0 + i / bw) * a.bxs + bx0 + i % bw;
+  // (row, column) of element i = k * 1024 + threadIdx.x in the group, stepped
+  // by (1024 / bw, 1024 % bw) with a carry: no integer division per element
+  const uint32_t dq = 1024u / bw, dr = 1024u % bw;
+  const uint32_t y0 = threadIdx.x / bw, x0 = threadIdx.x % bw;
+  auto step = [&](uint32_t& y, uint32_t& x) {
+    x += dr;
+    y += dq;
+    if (x >= bw) {
+      x -= bw;
+      y++;
+    }
   };
   uint64_t fl = 0;  // bit k: block k * 1024 + threadIdx.x starts a varblock
+  {
+    uint32_t y = y0, x = x0;
 #pragma unroll 16
-  for (int k = 0; k < 64; k++) {
-    const uint32_t i = (uint32_t)k * 1024 + threadIdx.x;
-    if (i < n && !(a.acs[block_of(i)] & 0x80)) fl |= 1ull << k;
+    for (int k = 0; k < 64; k++) {
+      const uint32_t i = (uint32_t)k * 1024 + threadIdx.x;
+      if (i < n && !(a.acs[(size_t)(by0 + y) * a.bxs + bx0 + x] & 0x80)) fl |= 1ull << k;
+      step(y, x);
+    }
   }
   for (int k = 0; k < 64; k++) {
     const uint64_t bal = __ballot((fl >> k) & 1);
@@ -960,12 +973,14 @@ __global__ __launch_bounds__(1024) void vb_list_kernel(VbArgs a) {
   }
   sCnt[threadIdx.x] = before + incl - v;
   __syncthreads();
+  uint32_t y = y0, x = x0;
   for (int k = 0; k < 64; k++) {
     const bool f = (fl >> k) & 1;
     const uint64_t bal = __ballot(f);
     if (f)
       a.vb[(size_t)lg * 65536 + sCnt[k * 16 + wv] + (uint32_t)__popcll(bal & lt)] =
-          (uint32_t)block_of((uint32_t)k * 1024 + threadIdx.x);
+          (uint32_t)((size_t)(by0 + y) * a.bxs + bx0 + x);
+    step(y, x);
   }
   if (threadIdx.x == 0) a.count[lg] = total;
 }
