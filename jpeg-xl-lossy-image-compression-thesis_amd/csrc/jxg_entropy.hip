@@ -103,16 +103,23 @@ __device__ __forceinline__ void for_my_samples(const LfArgs& a, const LfChunk& c
   uint32_t seg = 0;
   while (S.start[seg + 1] <= first) seg++;
   uint32_t pos = first;
+  // the row's geometry (two integer divisions) and varblock count only when
+  // the thread's samples cross into the next row
+  LfGeom L = lf_geom(a, S.row[seg].lg);
+  uint32_t nvb = a.vcount[S.row[seg].lg];
 #pragma unroll
   for (uint32_t j = 0; j < kLfPer; j++) {
     if (pos < ch.nsamp) {
-      while (S.start[seg + 1] <= pos) seg++;
+      if (S.start[seg + 1] <= pos) {
+        while (S.start[seg + 1] <= pos) seg++;
+        L = lf_geom(a, S.row[seg].lg);
+        nvb = a.vcount[S.row[seg].lg];
+      }
       const LfRow& r = S.row[seg];
-      const LfGeom L = lf_geom(a, r.lg);
       const uint32_t x = r.x0 + pos - S.start[seg];
       // the strategy/quant-field channel is laid out for bw*bh entries; only
       // the first count (= varblocks) exist
-      if (!(r.stream == 1 && r.chan == 2) || x < a.vcount[r.lg]) {
+      if (!(r.stream == 1 && r.chan == 2) || x < nvb) {
         uint32_t u;
         int leaf;
         lf_residual(a, r, L, (int)x, u, leaf);
