@@ -22,7 +22,9 @@ for s in $STEPS; do
            # 8K frame (one rank's load), the 8-context emulation; then a
            # kernel + copy trace of the 1080p stream
            timeout -k 10 150 python tools/stream_probe.py --mode plain --w 1920 --h 1080 --frames 256 --warmup 32 > $O/probe_1080p.log 2>&1
-           timeout -k 10 150 python tools/stream_probe.py --mode host --world 1 --h 544 --frames 256 --warmup 32 > $O/probe_slice8.log 2>&1
+           for hh in 544 1088 2160 4320; do
+             timeout -k 10 150 python tools/stream_probe.py --mode host --world 1 --h $hh --frames 256 --warmup 32 >> $O/probe_slices.log 2>&1
+           done
            timeout -k 10 150 python tools/stream_probe.py --mode host --world 8 --frames 40 > $O/probe_ctx8.log 2>&1
            timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d $O/prof_1080p -o run -- python3 tools/stream_probe.py --mode plain --w 1920 --h 1080 --frames 64 --warmup 8 > $O/prof_1080p.log 2>&1 ;;
   esac
