@@ -26,6 +26,6 @@ for s in $STEPS; do
              timeout -k 10 150 python tools/stream_probe.py --mode host --world 1 --h $hh --frames 256 --warmup 32 >> $O/probe_slices.log 2>&1
            done
            timeout -k 10 150 python tools/stream_probe.py --mode host --world 8 --frames 40 > $O/probe_ctx8.log 2>&1
-           timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d $O/prof_1080p -o run -- python3 tools/stream_probe.py --mode plain --w 1920 --h 1080 --frames 64 --warmup 8 > $O/prof_1080p.log 2>&1 ;;
+           timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace --hip-trace --stats --output-format csv -d $O/prof_1080p -o run -- python3 tools/stream_probe.py --mode plain --w 1920 --h 1080 --frames 64 --warmup 8 > $O/prof_1080p.log 2>&1 ;;
   esac
 done
