@@ -1839,6 +1839,45 @@ static jxg_status enc_finish_start(Ctx* c, Job& J, bool split) {
   J.ms_finish_layout = split ? J.ms_layout : ms_since(t_layout);
   return JXG_OK;
 }
+// the frame's stats (the lane's jxg_stats); `assembled`: the assembly has
+// completed (ev[4]), else its time is left out
+static void enc_stats(Ctx* c, Job& J, size_t out_bytes, float ms_layout, bool assembled,
+                      const std::vector<int16_t>* m_ac16, Clock::time_point t_call) {
+  const jxg_params& P = c->params;
+  const Frame& f = J.f;
+  const size_t nb = (size_t)f.bxs * f.bys;
+  jxg_stats& S = c->stats;
+  S = jxg_stats{};
+  S.xsize = J.w;
+  S.ysize = J.h;
+  S.xsize_blocks = f.bxs;
+  S.ysize_blocks = f.bys;
+  S.num_groups = f.ngroups;
+  S.num_lf_groups = f.nlf;
+  S.global_scale = f.G;
+  S.quant_dc = f.qdc;
+  S.bytes = out_bytes;
+  c->m_ntok.assign(c->h_ntok.p, c->h_ntok.p + f.ngroups * 3);
+  S.ac_tokens = c->m_ntok.data();
+  if ((P.flags & JXG_FLAG_KEEP_MAPS) && m_ac16) {
+    // coefficients in natural-order slices, widened to int32 for the caller
+    for (size_t i = 0; i < nb * 192; i++) c->m_ac[i] = (*m_ac16)[i];
+    S.ac_strategy = c->m_acs.data();
+    S.quant_field = c->m_qf.data();
+    S.dc = c->m_dc.data();
+    S.ac = c->m_ac.data();
+    S.homogeneity = J.homog ? c->m_homog.data() : nullptr;
+  }
+  S.ms_front = elapsed(c->ev[0], c->ev[1]);
+  S.ms_front_kernel = elapsed(c->ev[0], c->ev[5]);
+  S.ms_histogram = elapsed(c->ev[1], c->ev[2]);
+  S.ms_emit = elapsed(c->ev[2], c->ev[3]);
+  S.ms_assemble = assembled ? elapsed(c->ev[3], c->ev[4]) : 0.0f;
+  S.ms_total = elapsed(c->ev[0], assembled ? c->ev[4] : c->ev[3]);
+  S.ms_host_codes = J.ms_codes;
+  S.ms_host_layout = ms_layout;
+  S.ms_host_call = ms_since(t_call);
+}
 static jxg_status enc_finish_end(Ctx* c, Job& J, jxg_buffer* out, Clock::time_point t_call) {
   hipStream_t s = c->stream;
   const jxg_params& P = c->params;
@@ -1847,7 +1886,6 @@ static jxg_status enc_finish_end(Ctx* c, Job& J, jxg_buffer* out, Clock::time_po
   uint8_t* host_out = J.host_out;
   const size_t out_bytes = J.out_bytes;
   J.host_out = nullptr;
-  const float ms_layout = J.ms_finish_layout;
   std::vector<int16_t> m_ac16_tmp;
   if (P.flags & JXG_FLAG_KEEP_MAPS) {
     c->m_acs.resize(nb);
@@ -1870,39 +1908,7 @@ static jxg_status enc_finish_end(Ctx* c, Job& J, jxg_buffer* out, Clock::time_po
   }
   out->data = host_out;
   out->size = out_bytes;
-
-  // stats
-  jxg_stats& S = c->stats;
-  S = jxg_stats{};
-  S.xsize = J.w;
-  S.ysize = J.h;
-  S.xsize_blocks = f.bxs;
-  S.ysize_blocks = f.bys;
-  S.num_groups = f.ngroups;
-  S.num_lf_groups = f.nlf;
-  S.global_scale = f.G;
-  S.quant_dc = f.qdc;
-  S.bytes = out_bytes;
-  c->m_ntok.assign(c->h_ntok.p, c->h_ntok.p + f.ngroups * 3);
-  S.ac_tokens = c->m_ntok.data();
-  if (P.flags & JXG_FLAG_KEEP_MAPS) {
-    // coefficients in natural-order slices, widened to int32 for the caller
-    for (size_t i = 0; i < nb * 192; i++) c->m_ac[i] = m_ac16_tmp[i];
-    S.ac_strategy = c->m_acs.data();
-    S.quant_field = c->m_qf.data();
-    S.dc = c->m_dc.data();
-    S.ac = c->m_ac.data();
-    S.homogeneity = J.homog ? c->m_homog.data() : nullptr;
-  }
-  S.ms_front = elapsed(c->ev[0], c->ev[1]);
-  S.ms_front_kernel = elapsed(c->ev[0], c->ev[5]);
-  S.ms_histogram = elapsed(c->ev[1], c->ev[2]);
-  S.ms_emit = elapsed(c->ev[2], c->ev[3]);
-  S.ms_assemble = elapsed(c->ev[3], c->ev[4]);
-  S.ms_total = elapsed(c->ev[0], c->ev[4]);
-  S.ms_host_codes = J.ms_codes;
-  S.ms_host_layout = ms_layout;
-  S.ms_host_call = ms_since(t_call);
+  enc_stats(c, J, out_bytes, J.ms_finish_layout, true, &m_ac16_tmp, t_call);
   return JXG_OK;
 }
 static jxg_status enc_finish(Ctx* c, Job& J, bool split, jxg_buffer* out,
@@ -1987,9 +1993,13 @@ static uint32_t pipe_lag(uint32_t ngroups, uint32_t depth) {
   const uint32_t lag = ngroups >= 256 ? kPipeLagLarge : kPipeLagSmall;
   return std::max(1u, std::min(lag, depth - 1));
 }
+// a completed frame: its codestream (pinned host block) and stats; `ev`: the
+// codestream's D2H, still in flight when the frame was completed (deferred
+// finish) -- jxg_receive waits for it
 struct PipeDone {
   jxg_buffer buf;
   jxg_stats stats;
+  hipEvent_t ev;
 };
 struct PipeFrame {
   Ctx* lane = nullptr;
@@ -2009,13 +2019,38 @@ static jxg_status pipe_join_codes(PipeFrame& fr) {
 struct Pipe {
   std::vector<std::unique_ptr<PipeFrame>> inflight;  // submission order
   std::vector<PipeDone> done;                        // submission order
+  std::vector<hipEvent_t> evfree;                    // PipeDone::ev pool
   // shard frames whose sections are emitted and payload head built; each
   // holds its lane (sections in lane->out) until jxg_shard_write_next
   std::vector<std::unique_ptr<PipeFrame>> ready;
   uint64_t submitted = 0;
   int mode = 0;  // 1 whole frames, 2 shards (while any frame is pending)
   uint32_t depth = 0;
+  ~Pipe() {
+    for (auto& d : done)
+      if (d.ev) {
+        (void)hipEventSynchronize(d.ev);  // its D2H writes the codestream block
+        (void)hipEventDestroy(d.ev);
+      }
+    for (hipEvent_t e : evfree) (void)hipEventDestroy(e);
+  }
 };
+// the oldest completed frame's codestream is on the host (its D2H done)
+static jxg_status pipe_done_wait(Pipe& p, PipeDone& d) {
+  if (!d.ev) return JXG_OK;
+  const hipError_t e = hipEventSynchronize(d.ev);
+  p.evfree.push_back(d.ev);
+  d.ev = nullptr;
+  return e == hipSuccess ? JXG_OK : JXG_ERR_HIP;
+}
+// drop every completed frame (their D2H copies finish first)
+static void pipe_drop_done(Pipe& p) {
+  for (auto& d : p.done) {
+    (void)pipe_done_wait(p, d);
+    jxg_buffer_free(&d.buf);
+  }
+  p.done.clear();
+}
 static bool pipe_busy(const Ctx* c) {
   return c->pipe && (!c->pipe->inflight.empty() || !c->pipe->done.empty() ||
                      !c->pipe->ready.empty());
@@ -2130,8 +2165,33 @@ static jxg_status pipe_complete_oldest(Ctx* c) {
     p.inflight.erase(p.inflight.begin());
     return JXG_OK;
   }
-  PipeDone d{{nullptr, 0}, {}};
-  if (!st) st = enc_finish(fr.lane, fr.J, false, &d.buf, fr.t0);
+  PipeDone d{{nullptr, 0}, {}, nullptr};
+  if (fr.lane->params.flags & JXG_FLAG_KEEP_MAPS) {
+    if (!st) st = enc_finish(fr.lane, fr.J, false, &d.buf, fr.t0);
+  } else if (!st) {
+    // deferred finish: layout, concat and the codestream's D2H are enqueued on
+    // the lane's stream and the lane is free at once (the next frame's work
+    // queues behind them); only jxg_receive waits for the D2H.  Saves this
+    // thread one GPU round trip per frame.
+    if (p.evfree.empty()) {
+      hipEvent_t e = nullptr;
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return JXG_ERR_HIP;
+      p.evfree.push_back(e);
+    }
+    st = enc_finish_start(fr.lane, fr.J, false);
+    if (!st && hipEventRecord(p.evfree.back(), fr.lane->stream) != hipSuccess) st = JXG_ERR_HIP;
+    if (st) {
+      (void)hipStreamSynchronize(fr.lane->stream);
+      out_release(fr.J.host_out);
+      fr.J.host_out = nullptr;
+      return st;
+    }
+    d.ev = p.evfree.back();
+    p.evfree.pop_back();
+    d.buf = jxg_buffer{fr.J.host_out, fr.J.out_bytes};
+    fr.J.host_out = nullptr;
+    enc_stats(fr.lane, fr.J, d.buf.size, fr.J.ms_finish_layout, false, nullptr, fr.t0);
+  }
   if (st) return st;
   d.stats = fr.lane->stats;
   p.done.push_back(d);
@@ -2253,6 +2313,8 @@ static jxg_status pipe_receive(Ctx* c, jxg_buffer* out) {
       return st;
     }
   }
+  const jxg_status st = pipe_done_wait(p, p.done.front());
+  if (st) return st;
   *out = p.done.front().buf;
   c->stats = p.done.front().stats;
   p.done.erase(p.done.begin());
@@ -2736,7 +2798,7 @@ void jxg_destroy(void* ctx) {
   Ctx* c = static_cast<Ctx*>(ctx);
   if (c->pipe) {  // frames still in the pipeline (their lanes are released below)
     pipe_abort(c);
-    for (auto& d : c->pipe->done) jxg_buffer_free(&d.buf);
+    pipe_drop_done(*c->pipe);
     c->pipe.reset();
   }
   c->lanes.clear();  // pipeline lanes (jxg_destroy each)
@@ -2804,14 +2866,16 @@ static jxg_status batch_encode(Ctx* c, const uint8_t* const* frames, bool on_dev
   jxg_status st = JXG_OK;
   for (uint32_t i = 0; i < n && !st; i++) {
     st = pipe_submit(c, frames[i], on_device, w, h, stride);
-    while (!st && !c->pipe->done.empty()) st = pipe_receive(c, &outs[got++]);
+    // take completed frames whose codestream copy has landed (or when more
+    // than two are waiting), without waiting on the newest one's
+    while (!st && !c->pipe->done.empty() &&
+           (c->pipe->done.size() > 2 || !c->pipe->done.front().ev ||
+            hipEventQuery(c->pipe->done.front().ev) == hipSuccess))
+      st = pipe_receive(c, &outs[got++]);
   }
   while (!st && got < n) st = pipe_receive(c, &outs[got++]);
   if (st) {  // the pipe is aborted by then; drop what it completed, and ours
-    if (c->pipe) {
-      for (auto& d : c->pipe->done) jxg_buffer_free(&d.buf);
-      c->pipe->done.clear();
-    }
+    if (c->pipe) pipe_drop_done(*c->pipe);
     for (uint32_t i = 0; i < n; i++) jxg_buffer_free(&outs[i]);
   }
   return st;
