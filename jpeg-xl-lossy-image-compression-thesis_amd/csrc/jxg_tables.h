@@ -1,0 +1,25 @@
+// jxg_tables.h -- host-side constant tables of the encoder (built once per
+// process, uploaded to __constant__ / device memory by jxg_host.cpp):
+// default quantization weights, the sRGB8 -> linear table, the masking AQ's
+// erosion weights, and the merge stage's per-shape weight / distortion /
+// natural-order tables and DCT constants.  [ext libjxl quant_weights.cc,
+// coeff_order.cc; == oracle/front.c, oracle/merge.c, oracle/aq.c]
+#pragma once
+#include <cstdint>
+#include <vector>
+
+namespace jxg {
+
+struct MergeTables {
+  std::vector<float> wk, sdk, iwy;
+  std::vector<uint16_t> nat;
+  float lee_c[7][32], lee_s[7][64], llf_p[4][8], llf_ib[4][8][8];
+};
+
+// kinds: 0 DCT8, 1 DCT4X4, 2 DCT4X8 / DCT8X4, 3 IDENTITY, 4 DCT2X2
+void quant_weights(float out[5][3][64]);
+void aq_erosion_weights(float distance, float w[4]);
+void srgb_lut(float lut[256]);
+MergeTables build_merge_tables();
+
+}  // namespace jxg

@@ -15,7 +15,7 @@ for FILE in $FILES; do
 done
 HIPFLAGS="-O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=gfx950 -Wno-unused-function"
 pids=()
-for f in $T/p/csrc/*.hip $T/p/csrc/jxg_host.cpp $T/p/csrc/jxg_bitstream.cpp; do
+for f in $T/p/csrc/*.hip $(ls $T/p/csrc/*.cpp | grep -v jxg_cjxl); do
   b=$(basename $f); /opt/rocm/bin/hipcc $HIPFLAGS -c $f -o $T/${b%.*}.o & pids+=($!)
 done
 for p in ${pids[@]}; do wait $p; done

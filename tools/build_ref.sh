@@ -11,7 +11,7 @@ P=$T/jpeg-xl-lossy-image-compression-thesis_amd
 for f in "$@"; do cp $D/jpeg-xl-lossy-image-compression-thesis_amd/csrc/$f $P/csrc/$f; done
 HIPFLAGS="-O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=gfx950 -Wno-unused-function"
 pids=()
-for f in $P/csrc/*.hip $P/csrc/jxg_host.cpp $P/csrc/jxg_bitstream.cpp; do
+for f in $P/csrc/*.hip $(ls $P/csrc/*.cpp | grep -v jxg_cjxl); do
   b=$(basename $f); /opt/rocm/bin/hipcc $HIPFLAGS -c $f -o $T/${b%.*}.o & pids+=($!)
 done
 for p in ${pids[@]}; do wait $p; done

@@ -9,7 +9,7 @@ O=$D/tools/var/obj_$NAME
 mkdir -p $O
 HIPFLAGS="-O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=gfx950 -Wno-unused-function $FLAGS"
 pids=()
-for f in $P/csrc/*.hip $P/csrc/jxg_host.cpp $P/csrc/jxg_bitstream.cpp; do
+for f in $P/csrc/*.hip $(ls $P/csrc/*.cpp | grep -v jxg_cjxl); do
   b=$(basename $f); /opt/rocm/bin/hipcc $HIPFLAGS -c $f -o $O/${b%.*}.o 2>/dev/null & pids+=($!)
 done
 for p in ${pids[@]}; do wait $p; done
