@@ -3,7 +3,7 @@
 // (pass-group AC kernels: jxg_ac.hip)
 // LF groups (modular streams of quantized DC and AC metadata) are processed
 // in chunks of <= 4096 samples of one stream per workgroup, 16 consecutive
-// samples per thread: lf_hist -> lf_bits -> lf_scan -> lf_emit.
+// samples per thread: lf_hist -> (host codes) -> lf_code.
 // concat  : bit-exact assembly of all sections (device scratch + host chunks)
 //           into the final codestream, one word per lane.
 // Token order, contexts and hybrid-uint split are those of oracle/encode.c
@@ -135,7 +135,10 @@ __global__ __launch_bounds__(256) void lf_hist_kernel(LfArgs a) {
   __shared__ uint32_t sBound;
   __shared__ LfChunkLds S;
   for (int i = threadIdx.x; i < 4 * kAlpha; i += blockDim.x) sHist[i] = 0;
-  if (threadIdx.x == 0) sBound = 0;
+  if (threadIdx.x == 0) {
+    sBound = 0;
+    a.status[blockIdx.x] = 0;  // lf_code's look-back word of this chunk
+  }
   const LfChunk ch = load_chunk(a, S);
   uint32_t bound = 0;
   for_my_samples(a, ch, S, [&](uint32_t, uint32_t u, int leaf) {
@@ -151,52 +154,8 @@ __global__ __launch_bounds__(256) void lf_hist_kernel(LfArgs a) {
   if (threadIdx.x == 0) atomicAdd(&a.sbound[ch.sid], sBound);
 }
 
-// exact bits of each chunk
-__global__ __launch_bounds__(256) void lf_bits_kernel(LfArgs a) {
-  __shared__ uint32_t sSum;
-  __shared__ LfChunkLds S;
-  if (threadIdx.x == 0) sSum = 0;
-  const LfChunk ch = load_chunk(a, S);
-  uint32_t sum = 0;
-  for_my_samples(a, ch, S, [&](uint32_t, uint32_t u, int leaf) {
-    uint32_t tok, nb, bits;
-    hybrid420(u, tok, nb, bits);
-    sum += (a.codes[((size_t)ch.sid * 4 + leaf) * kAlpha + tok] >> 16) + nb;
-  });
-  atomicAdd(&sSum, sum);
-  __syncthreads();
-  if (threadIdx.x == 0) a.chunk_bits[blockIdx.x] = sSum;
-}
-
-// per-stream exclusive scan of chunk bits -> absolute chunk offsets
-__global__ __launch_bounds__(256) void lf_scan_kernel(LfArgs a) {
-  __shared__ uint32_t sScan[256];
-  const uint32_t sid = blockIdx.x;
-  const uint32_t r0 = a.stream_chunks[sid], r1 = a.stream_chunks[sid + 1];
-  uint64_t run = a.stream_base[sid];
-  const uint64_t start = run;
-  for (uint32_t c0 = r0; c0 < r1; c0 += blockDim.x) {
-    const uint32_t r = c0 + threadIdx.x;
-    const uint32_t v = r < r1 ? a.chunk_bits[r] : 0;
-    sScan[threadIdx.x] = v;
-    __syncthreads();
-    for (int d = 1; d < 256; d <<= 1) {
-      uint32_t t = threadIdx.x >= (uint32_t)d ? sScan[threadIdx.x - d] : 0;
-      __syncthreads();
-      sScan[threadIdx.x] += t;
-      __syncthreads();
-    }
-    if (r < r1) a.chunk_off[r] = run + sScan[threadIdx.x] - v;
-    run += sScan[255];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) a.stream_bits[sid] = (uint32_t)(run - start);
-  // the stream's scratch words zeroed for lf_emit's ORs (no arena memset)
-  uint32_t* dst = a.scratch + (start >> 5);
-  for (uint64_t i = threadIdx.x; i < (run - start + 31) / 32; i += blockDim.x) dst[i] = 0;
-}
-
-// workgroup exclusive scan of one value per thread (256 threads)
+// workgroup exclusive scan of one value per thread (256 threads); sWave
+// holds the four wave totals afterwards
 __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* sWave) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t incl = v;
@@ -212,10 +171,33 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* sWa
   return before + incl - v;
 }
 
-__global__ __launch_bounds__(256) void lf_emit_kernel(LfArgs a) {
+// One launch codes the LF streams (chunk = workgroup; a stream's chunks are
+// consecutive workgroups in stream order): every thread codes its samples,
+// a workgroup scan places them in the chunk, a decoupled look-back over the
+// stream's earlier chunks gives the chunk's offset (status word per chunk:
+// aggregate, then inclusive prefix; a chunk only waits on lower-indexed,
+// already dispatched workgroups, and the stream's first chunk publishes its
+// prefix at once), the chunk's bits are assembled in LDS at the word
+// alignment of that offset and stored as whole words.  The two words a chunk
+// shares with its neighbours are merged with an AND then an OR over the
+// chunk's own bits only (disjoint masks commute), so the arena needs no zero
+// fill; the concat kernel masks the bits past a stream's end.  Replaces the
+// lf_bits -> lf_scan -> lf_emit launches (the samples were coded twice).
+constexpr uint64_t kLfAgg = 1ull << 62, kLfPre = 2ull << 62, kLfVal = (1ull << 62) - 1;
+constexpr uint32_t kLfImgWords = (kLfPer * 256 * 31 + 31) / 32 + 2;  // 31 bits per sample at most
+__device__ __forceinline__ uint64_t lf_status_load(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lf_status_store(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__global__ __launch_bounds__(256) void lf_code_kernel(LfArgs a) {
   __shared__ LfChunkLds S;
   __shared__ uint32_t sWave[4];
-  const LfChunk ch = load_chunk(a, S);
+  __shared__ uint32_t sImg[kLfImgWords];
+  __shared__ uint64_t sExcl;
+  for (uint32_t i = threadIdx.x; i < kLfImgWords; i += 256) sImg[i] = 0;
+  const LfChunk ch = load_chunk(a, S);  // (barriers: sImg is clear after it)
   uint32_t val[kLfPer], len[kLfPer];
   uint32_t tot = 0;
 #pragma unroll
@@ -230,10 +212,57 @@ __global__ __launch_bounds__(256) void lf_emit_kernel(LfArgs a) {
     tot += len[j];
   });
   const uint32_t off = block_excl_scan256(tot, sWave);
-  BitSink s{a.scratch, a.chunk_off[blockIdx.x] + off, 0, 0};
+  const uint32_t total = sWave[0] + sWave[1] + sWave[2] + sWave[3];
+  if (threadIdx.x == 0) {
+    const uint32_t r = blockIdx.x, c0 = a.stream_chunks[ch.sid];
+    uint64_t excl = 0;
+    if (r == c0) {
+      lf_status_store(&a.status[r], kLfPre | total);
+    } else {
+      lf_status_store(&a.status[r], kLfAgg | total);
+      for (uint32_t q = r - 1;;) {
+        const uint64_t v = lf_status_load(&a.status[q]);
+        if (!(v >> 62)) {
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        excl += v & kLfVal;
+        if ((v & kLfPre) || q == c0) break;
+        q--;
+      }
+      lf_status_store(&a.status[r], kLfPre | (excl + total));
+    }
+    sExcl = excl;
+    if (r + 1 == a.stream_chunks[ch.sid + 1]) a.stream_bits[ch.sid] = (uint32_t)(excl + total);
+  }
+  __syncthreads();
+  const uint64_t start = a.stream_base[ch.sid] + sExcl;  // absolute bit of the chunk
+  const uint32_t sh = (uint32_t)(start & 31);
+  // this thread's codes into the LDS image (bit 0 = the start word's bit 0)
+  uint32_t pos = sh + off;
 #pragma unroll
-  for (uint32_t j = 0; j < kLfPer; j++) s.put(len[j], val[j]);
-  s.finish();
+  for (uint32_t j = 0; j < kLfPer; j++) {
+    if (len[j]) {
+      const uint32_t w = pos >> 5, b = pos & 31;
+      atomicOr(&sImg[w], val[j] << b);
+      if (b + len[j] > 32) atomicOr(&sImg[w + 1], val[j] >> (32 - b));
+      pos += len[j];
+    }
+  }
+  __syncthreads();
+  const uint64_t w0 = start >> 5;
+  const uint32_t end = sh + total, nw = (end + 31) >> 5;
+  for (uint32_t i = threadIdx.x; i < nw; i += 256) {
+    const uint32_t lo = i == 0 ? sh : 0, hi = min(32u, end - 32 * i);
+    const uint32_t word = sImg[i];
+    if (lo == 0 && hi == 32) {
+      a.scratch[w0 + i] = word;
+    } else {  // shared with a neighbouring chunk: only this chunk's bits
+      const uint32_t m = (hi == 32 ? ~0u : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
+      atomicAnd(&a.scratch[w0 + i], ~m);
+      atomicOr(&a.scratch[w0 + i], word & m);
+    }
+  }
 }
 
 // ------------------------------- concat ------------------------------------
@@ -293,14 +322,8 @@ __global__ __launch_bounds__(kConcatThreads) void concat_kernel(const ConcatPiec
 void launch_lf_hist(const LfArgs& a, uint32_t nchunks, hipStream_t s) {
   hipLaunchKernelGGL(lf_hist_kernel, dim3(nchunks), dim3(256), 0, s, a);
 }
-void launch_lf_bits(const LfArgs& a, uint32_t nchunks, hipStream_t s) {
-  hipLaunchKernelGGL(lf_bits_kernel, dim3(nchunks), dim3(256), 0, s, a);
-}
-void launch_lf_scan(const LfArgs& a, uint32_t nstreams, hipStream_t s) {
-  hipLaunchKernelGGL(lf_scan_kernel, dim3(nstreams), dim3(256), 0, s, a);
-}
-void launch_lf_emit(const LfArgs& a, uint32_t nchunks, hipStream_t s) {
-  hipLaunchKernelGGL(lf_emit_kernel, dim3(nchunks), dim3(256), 0, s, a);
+void launch_lf_code(const LfArgs& a, uint32_t nchunks, hipStream_t s) {
+  hipLaunchKernelGGL(lf_code_kernel, dim3(nchunks), dim3(256), 0, s, a);
 }
 void launch_concat(const ConcatPiece* pieces, uint32_t npieces, uint64_t out_words,
                    const uint32_t* scratch, const uint32_t* chunks, const uint32_t* scratch2,

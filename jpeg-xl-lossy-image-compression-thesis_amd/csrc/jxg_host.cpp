@@ -5,7 +5,7 @@
 //   ac_hist + lf_hist (token statistics)     [jxg_entropy.hip]
 //   -> D2H histograms; host builds prefix codes, LfGlobal/HfGlobal and the
 //      LF-group stream preludes (a few KB of header bits)
-//   ac_emit + lf_bits/lf_scan/lf_emit (bit emission into scratch)
+//   ac_emit or the rANS chain + ans_emit, lf_code (bit emission into scratch)
 //   -> D2H section sizes; host writes headers + TOC and the piece list
 //   concat (bit-exact assembly) -> D2H codestream
 // The byte stream equals the CPU oracle's (oracle/encode.c) bit for bit.
@@ -268,9 +268,9 @@ struct Ctx {
   DevBuf<int16_t> ac;
   DevBuf<float> homog, xyb, r3;
   DevBuf<uint8_t> type;
-  DevBuf<uint32_t> chunkbits, stream_chunks, scratch, scratch_lf, chunks, out, out_ac;
-  DevBuf<uint64_t> chunkoff;
-  // Per-frame statistics, zeroed by one memset and downloaded by two copies
+  DevBuf<uint32_t> stream_chunks, scratch, scratch_lf, chunks, out, out_ac;
+  DevBuf<uint64_t> lfstatus;  // [nchunks] lf_code look-back words
+  // Per-frame statistics, zeroed by the front kernel and downloaded by two copies
   // (AC part, LF part): [hist_ac | bound | ntok | bandtok][lfhist | sbound | vcount]
   DevBuf<uint8_t> stat;
   PinBuf<uint8_t> h_stat;
@@ -762,8 +762,7 @@ static jxg_status stage_alloc(Ctx* c, Job& J) {
   const uint32_t nstreams = J.nstreams;
   JXG_HIP(c->rows.ensure(J.nrows));
   JXG_HIP(c->lfchunks.ensure(J.nchunks));
-  JXG_HIP(c->chunkbits.ensure(J.nchunks));
-  JXG_HIP(c->chunkoff.ensure(J.nchunks));
+  JXG_HIP(c->lfstatus.ensure(J.nchunks));
   JXG_HIP(c->stream_chunks.ensure(nstreams + 1));
   if (new_rows) {
     if (J.nrows)
@@ -819,8 +818,7 @@ static jxg_status stage_alloc(Ctx* c, Job& J) {
   la.hist = c->lfhist.p;
   la.sbound = c->sbound.p;
   la.codes = c->lfcodes.p;
-  la.chunk_bits = c->chunkbits.p;
-  la.chunk_off = c->chunkoff.p;
+  la.status = c->lfstatus.p;
   la.stream_chunks = c->stream_chunks.p;
   la.stream_base = c->stream_base.p;
   la.stream_bits = c->stream_bits.p;
@@ -1205,8 +1203,8 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
   JXG_HIP(c->h_sbase.ensure(J.sbase.size()));
   std::copy(J.sbase.begin(), J.sbase.end(), c->h_sbase.p);
   if (J.ans) {
-    // one arena for the AC and LF bits (one memset) and every table in one
-    // upload
+    // one arena for the AC and LF bits (no fill: the chains clear their
+    // ranges, lf_code stores whole words) and every table in one upload
     JXG_HIP(c->scratch.ensure(ac_words + lf_words));
     c->lf_scratch = c->scratch.p + ac_words;
     J.aa.scratch = c->scratch.p;
@@ -1250,9 +1248,7 @@ static jxg_status stage_emit(Ctx* c, Job& J, bool sync = true) {
     JXG_HIP(hipGetLastError());
   }
   J.la.scratch = c->lf_scratch;
-  if (J.nchunks) launch_lf_bits(J.la, J.nchunks, s);
-  launch_lf_scan(J.la, J.nstreams, s);
-  if (J.nchunks) launch_lf_emit(J.la, J.nchunks, s);
+  if (J.nchunks) launch_lf_code(J.la, J.nchunks, s);
   JXG_HIP(hipGetLastError());
   if (J.ans) {  // [gbits | stream_bits]: one copy
     JXG_HIP(hipMemcpyAsync(c->h_bits.p, c->bits.p, ((size_t)f.ngroups + J.nstreams) * 4,

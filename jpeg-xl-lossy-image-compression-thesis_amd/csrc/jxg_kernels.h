@@ -194,12 +194,11 @@ struct LfArgs {
   uint32_t tiles_x, ntiles_all;
   uint32_t* hist;         // [nstreams][4 leaves][kAlpha]  (hist)
   uint32_t* sbound;       // [nstreams] (hist)
-  const uint32_t* codes;  // [nstreams][4][kAlpha] (emit)
-  uint32_t* chunk_bits;   // [nchunks]
-  uint64_t* chunk_off;    // [nchunks] absolute scratch bit offset (scan -> emit)
+  const uint32_t* codes;  // [nstreams][4][kAlpha] (lf_code)
+  uint64_t* status;       // [nchunks] look-back word (lf_hist clears, lf_code)
   const uint32_t* stream_chunks;  // [nstreams+1] first chunk of each stream
   const uint64_t* stream_base;  // [nstreams] scratch bit offset of each stream
-  uint32_t* stream_bits;        // [nstreams] exact bits (scan)
+  uint32_t* stream_bits;        // [nstreams] exact bits (lf_code)
   uint32_t* scratch;
 };
 
@@ -239,9 +238,7 @@ void launch_homog(const HomogArgs& a, uint32_t tiles_x, uint32_t tiles_y, hipStr
 void launch_ac_hist(const AcArgs& a, uint32_t ngroups, hipStream_t s);
 void launch_ac_emit(const AcArgs& a, uint32_t ngroups, hipStream_t s);
 void launch_lf_hist(const LfArgs& a, uint32_t nchunks, hipStream_t s);
-void launch_lf_bits(const LfArgs& a, uint32_t nchunks, hipStream_t s);
-void launch_lf_scan(const LfArgs& a, uint32_t nstreams, hipStream_t s);
-void launch_lf_emit(const LfArgs& a, uint32_t nchunks, hipStream_t s);
+void launch_lf_code(const LfArgs& a, uint32_t nchunks, hipStream_t s);
 hipError_t set_cluster_table(const uint8_t* tab, hipStream_t s);
 hipError_t set_merge_constants(const float* llf_p /*[4][8]*/, const float* llf_ib /*[4][8][8]*/,
                          hipStream_t s);
