@@ -22,6 +22,9 @@ import math
 import numpy as np
 
 
+LAST_TOC = None  # (byte offsets, sizes) of the last decoded codestream's sections
+
+
 class JxlError(Exception):
     pass
 
@@ -1001,6 +1004,8 @@ def decode(data: bytes, want_pixels: bool = True, groups=None) -> Decoded:
     for s in sizes:
         offs.append(o)
         o += s
+    global LAST_TOC
+    LAST_TOC = (list(offs), list(sizes))  # (diagnostics: tools/diag_sections.py)
 
     def sec(i):
         if nent == 1:
