@@ -123,12 +123,15 @@ constexpr int kHistThreads = kBandBlocks;
 static_assert(kBands * kBandTokStride == kGroupTokStride, "band record spaces tile the group's");
 
 // record space index of stream position k of a group whose band counts are bt[4]
+// (band j holds stream positions [c_j, c_j+1), c_j = bt[0] + ... + bt[j-1];
+// the bounds are cumulative, so k >= c_j holds for a prefix of the bands)
 __device__ __forceinline__ uint32_t rec_index(const uint32_t* bt, uint32_t k) {
-  uint32_t j = 0, lo = 0;
+  uint32_t j = 0, lo = 0, cum = 0;
 #pragma unroll
   for (int i = 0; i < kBands - 1; i++) {
-    const bool past = k >= lo + bt[i];
-    lo += past ? bt[i] : 0u;
+    cum += bt[i];
+    const bool past = k >= cum;
+    lo = past ? cum : lo;
     j += past ? 1u : 0u;
   }
   return j * (uint32_t)kBandTokStride + (k - lo);
