@@ -20,6 +20,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <future>
 #include <memory>
 #include <mutex>
@@ -1763,6 +1764,64 @@ static jxg_status pipe_join_codes(PipeFrame& fr) {
   fr.phase = 2;
   return st;
 }
+// Helper threads of a pipeline: persistent (a std::async thread per frame cost
+// its creation on the submitting thread every frame), HIP device set once.
+class Helpers {
+ public:
+  Helpers(int dev, int n) {
+    try {
+      for (int i = 0; i < n; i++) start(dev);
+    } catch (...) {  // no thread: stop the ones started, the caller builds inline
+      stop_all();
+      throw;
+    }
+  }
+  ~Helpers() { stop_all(); }
+  std::future<jxg_status> run(std::function<jxg_status()> f) {
+    std::packaged_task<jxg_status()> job(std::move(f));
+    std::future<jxg_status> fut = job.get_future();
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      q_.push_back(std::move(job));
+    }
+    cv_.notify_one();
+    return fut;
+  }
+
+ private:
+  void start(int dev) {
+    t_.emplace_back([this, dev]() {
+      (void)hipSetDevice(dev);
+      for (;;) {
+        std::packaged_task<jxg_status()> job;
+        {
+          std::unique_lock<std::mutex> lk(mu_);
+          cv_.wait(lk, [this]() { return stop_ || !q_.empty(); });
+          if (q_.empty()) return;  // stop_, nothing left
+          job = std::move(q_.front());
+          q_.pop_front();
+        }
+        job();
+      }
+    });
+  }
+  void stop_all() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : t_) t.join();
+    t_.clear();
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::packaged_task<jxg_status()>> q_;
+  std::vector<std::thread> t_;
+  bool stop_ = false;
+};
+constexpr int kPipeHelpers = 4;  // >= the small-frame lag (3) + 1
+
 struct Pipe {
   std::vector<std::unique_ptr<PipeFrame>> inflight;  // submission order
   std::vector<PipeDone> done;                        // submission order
@@ -1773,6 +1832,7 @@ struct Pipe {
   uint64_t submitted = 0;
   int mode = 0;  // 1 whole frames, 2 shards (while any frame is pending)
   uint32_t depth = 0;
+  std::unique_ptr<Helpers> helpers;  // created with the first helper task
   ~Pipe() {
     for (auto& d : done)
       if (d.ev) {
@@ -1985,12 +2045,9 @@ static jxg_status pipe_submit(Ctx* c, const uint8_t* src, bool on_device, uint32
   if (!p.inflight.empty()) {
     PipeFrame* prev = p.inflight.back().get();
     if (prev->phase == 1 && !prev->codes.valid()) {
-      const int dev = c->params.device;
       try {
-        prev->codes = std::async(std::launch::async, [prev, dev]() {
-          if (hipSetDevice(dev) != hipSuccess) return JXG_ERR_HIP;
-          return enc_codes(prev->lane, prev->J, false);
-        });
+        if (!p.helpers) p.helpers.reset(new Helpers(c->params.device, kPipeHelpers));
+        prev->codes = p.helpers->run([prev]() { return enc_codes(prev->lane, prev->J, false); });
       } catch (...) {  // no thread: build the codes on this one
         if ((st = enc_codes(prev->lane, prev->J, false))) {
           pipe_abort(c);
