@@ -24,7 +24,7 @@ from jxg.synth import synth_rgb8_device  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--mode", choices=("plain", "host"), default="host")
-ap.add_argument("--world", type=int, default=2)
+ap.add_argument("--world", type=int, default=1)
 ap.add_argument("--frames", type=int, default=40)
 ap.add_argument("--warmup", type=int, default=16)
 ap.add_argument("--w", type=int, default=7680)
