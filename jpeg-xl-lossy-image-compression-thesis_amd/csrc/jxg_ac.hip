@@ -277,7 +277,8 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sWave,
 
 // The band's clustered histogram in LDS as u16 counts, two bins per word (a
 // band has at most 256 x 3 x 64 = 49152 tokens, so a half never carries)
-__global__ __launch_bounds__(kHistThreads) void ac_hist_kernel(AcArgs a) {
+__global__ __launch_bounds__(kHistThreads) void ac_hist_kernel(Batch<AcArgs> bt_) {
+  const AcArgs& a = bt_.a[blockIdx.z];  // the batch's frame
   constexpr int kHistWords = kMaxClusters * kAcTok / 2;
   __shared__ uint32_t sHist[kHistWords];
   __shared__ AcLds L;
@@ -704,8 +705,8 @@ __device__ __forceinline__ void ans_chain(const AnsArgs& a, uint32_t blk) {
   uint32_t* dst = a.scratch + (a.base[g] >> 5);
   for (uint32_t i = lane; i < (total + 31) / 32; i += 64) dst[i] = 0;
 }
-__global__ __launch_bounds__(kAnsWaves * 64) void ans_encode_kernel(AnsArgs a) {
-  ans_chain(a, blockIdx.x);
+__global__ __launch_bounds__(kAnsWaves * 64) void ans_encode_kernel(Batch<AnsArgs> bt_) {
+  ans_chain(bt_.a[blockIdx.z], blockIdx.x);
 }
 // bit placement: the 32-bit state, then every record's bits, in order.  One
 // 256-thread workgroup per (group, segment of kSegChunks chunks of 64
@@ -717,11 +718,13 @@ __global__ __launch_bounds__(kAnsWaves * 64) void ans_encode_kernel(AnsArgs a) {
 // with its neighbours (zeroed by the chain).
 constexpr int kSegChunks = 64, kEmitThreads = 256;
 constexpr int kSegWords = (kSegChunks * 64 * 29 + 31) / 32 + 2;  // <= 29 bits per record
-__global__ __launch_bounds__(kEmitThreads) void ans_emit_kernel(AnsArgs a) {
+__global__ __launch_bounds__(kEmitThreads) void ans_emit_kernel(Batch<AnsArgs> bt_) {
   __shared__ __attribute__((aligned(16))) uint32_t sBits[kSegWords];
   __shared__ uint32_t sCs[kSegChunks + 1];
   __shared__ uint32_t sPre[kEmitThreads / 64];
+  const AnsArgs& a = bt_.a[blockIdx.z];
   const uint32_t slot = blockIdx.x, seg = blockIdx.y;
+  if (slot >= a.n) return;
   const uint32_t g = slot_group(a.glist, a.g0, slot);
   const uint32_t n = a.ntok[g * 3] + a.ntok[g * 3 + 1] + a.ntok[g * 3 + 2];
   const uint32_t K = (n + 63) / 64, q0 = seg * kSegChunks;
@@ -779,20 +782,25 @@ __global__ __launch_bounds__(kEmitThreads) void ans_emit_kernel(AnsArgs a) {
   }
 }
 
-void launch_ans(const AnsArgs& a, hipStream_t s) {
-  const uint32_t n = a.n;
-  if (!n) return;
-  hipLaunchKernelGGL(ans_encode_kernel, dim3((n + kAnsWaves - 1) / kAnsWaves), dim3(kAnsWaves * 64),
-                     0, s, a);
-  launch_ans_emit(a, s);
-}
-void launch_ans_emit(const AnsArgs& a, hipStream_t s) {
-  const uint32_t nseg = (a.max_tokens + kSegChunks * 64 - 1) / (kSegChunks * 64);
-  if (a.n && nseg) hipLaunchKernelGGL(ans_emit_kernel, dim3(a.n, nseg), dim3(kEmitThreads), 0, s, a);
+// the chains, then the bit placement, of k frames (same plan: same group
+// count; the segment grid covers the longest group of any of them)
+void launch_ans(const AnsArgs* a, uint32_t k, hipStream_t s) {
+  if (!k || !a[0].n) return;
+  const Batch<AnsArgs> b = make_batch(a, k);
+  uint32_t n = 0, maxtok = 0;
+  for (uint32_t i = 0; i < k; i++) {
+    n = max(n, a[i].n);
+    maxtok = max(maxtok, a[i].max_tokens);
+  }
+  hipLaunchKernelGGL(ans_encode_kernel, dim3((n + kAnsWaves - 1) / kAnsWaves, 1, k),
+                     dim3(kAnsWaves * 64), 0, s, b);
+  const uint32_t nseg = (maxtok + kSegChunks * 64 - 1) / (kSegChunks * 64);
+  if (nseg) hipLaunchKernelGGL(ans_emit_kernel, dim3(n, nseg, k), dim3(kEmitThreads), 0, s, b);
 }
 
-void launch_ac_hist(const AcArgs& a, uint32_t ngroups, hipStream_t s) {
-  if (ngroups) hipLaunchKernelGGL(ac_hist_kernel, dim3(ngroups * kBands), dim3(kHistThreads), 0, s, a);
+void launch_ac_hist(const AcArgs* a, uint32_t k, uint32_t ngroups, hipStream_t s) {
+  if (ngroups && k)
+    hipLaunchKernelGGL(ac_hist_kernel, dim3(ngroups * kBands, 1, k), dim3(kHistThreads), 0, s, make_batch(a, k));
 }
 void launch_ac_emit(const AcArgs& a, uint32_t ngroups, hipStream_t s) {
   if (ngroups) hipLaunchKernelGGL(ac_emit_kernel, dim3(ngroups), dim3(kAcThreads), 0, s, a);

@@ -100,7 +100,8 @@ __device__ __forceinline__ void store_min4(float v, float& m0, float& m1, float&
   m0 = c0 ? v : m0;
 }
 
-__global__ __launch_bounds__(kAqThreads) void aq_kernel(AqArgs a) {
+__global__ __launch_bounds__(kAqThreads) void aq_kernel(Batch<AqArgs> bt_) {
+  const AqArgs& a = bt_.a[blockIdx.z];
   __shared__ float sY[kAqR * kAqS];  // Y of the tile and its 5 px ring
   __shared__ float sX[64 * 65];      // X of the tile
   __shared__ float sCell[kAqC * kAqC];
@@ -237,8 +238,8 @@ __global__ __launch_bounds__(kAqThreads) void aq_kernel(AqArgs a) {
   }
 }
 
-void launch_aq(const AqArgs& a, uint32_t ntiles, hipStream_t s) {
-  if (ntiles) hipLaunchKernelGGL(aq_kernel, dim3(ntiles), dim3(kAqThreads), 0, s, a);
+void launch_aq(const AqArgs* a, uint32_t k, uint32_t ntiles, hipStream_t s) {
+  if (ntiles && k) hipLaunchKernelGGL(aq_kernel, dim3(ntiles, 1, k), dim3(kAqThreads), 0, s, make_batch(a, k));
 }
 
 }  // namespace jxg

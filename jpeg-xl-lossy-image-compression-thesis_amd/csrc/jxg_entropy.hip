@@ -130,7 +130,8 @@ __device__ __forceinline__ void for_my_samples(const LfArgs& a, const LfChunk& c
   }
 }
 
-__global__ __launch_bounds__(256) void lf_hist_kernel(LfArgs a) {
+__global__ __launch_bounds__(256) void lf_hist_kernel(Batch<LfArgs> bt_) {
+  const LfArgs& a = bt_.a[blockIdx.z];
   __shared__ uint32_t sHist[4 * kAlpha];
   __shared__ uint32_t sBound;
   __shared__ LfChunkLds S;
@@ -191,7 +192,8 @@ __device__ __forceinline__ uint64_t lf_status_load(const uint64_t* p) {
 __device__ __forceinline__ void lf_status_store(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__global__ __launch_bounds__(256) void lf_code_kernel(LfArgs a) {
+__global__ __launch_bounds__(256) void lf_code_kernel(Batch<LfArgs> bt_) {
+  const LfArgs& a = bt_.a[blockIdx.z];
   __shared__ LfChunkLds S;
   __shared__ uint32_t sWave[4];
   __shared__ uint32_t sImg[kLfImgWords];
@@ -319,11 +321,13 @@ __global__ __launch_bounds__(kConcatThreads) void concat_kernel(const ConcatPiec
 }
 
 // ------------------------------- launchers ---------------------------------
-void launch_lf_hist(const LfArgs& a, uint32_t nchunks, hipStream_t s) {
-  hipLaunchKernelGGL(lf_hist_kernel, dim3(nchunks), dim3(256), 0, s, a);
+void launch_lf_hist(const LfArgs* a, uint32_t k, uint32_t nchunks, hipStream_t s) {
+  if (k && nchunks) hipLaunchKernelGGL(lf_hist_kernel, dim3(nchunks, 1, k), dim3(256), 0, s, make_batch(a, k));
 }
-void launch_lf_code(const LfArgs& a, uint32_t nchunks, hipStream_t s) {
-  hipLaunchKernelGGL(lf_code_kernel, dim3(nchunks), dim3(256), 0, s, a);
+// (a frame's chunks are consecutive workgroups of its z slice: the look-back
+// only waits on lower-indexed workgroups)
+void launch_lf_code(const LfArgs* a, uint32_t k, uint32_t nchunks, hipStream_t s) {
+  if (k && nchunks) hipLaunchKernelGGL(lf_code_kernel, dim3(nchunks, 1, k), dim3(256), 0, s, make_batch(a, k));
 }
 void launch_concat(const ConcatPiece* pieces, uint32_t npieces, uint64_t out_words,
                    const uint32_t* scratch, const uint32_t* chunks, const uint32_t* scratch2,

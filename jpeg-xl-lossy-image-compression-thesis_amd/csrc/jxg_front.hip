@@ -940,7 +940,8 @@ __device__ __forceinline__ int cfl_quant(float k) {
 #define JXG_FRONT_WPE 4
 #endif
 template <bool HOOKP>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FRONT_WPE))) void front_kernel(FrontArgs a) {
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FRONT_WPE))) void front_kernel(Batch<FrontArgs> bt_) {
+  const FrontArgs& a = bt_.a[blockIdx.z];  // the batch's frame
   __shared__ __attribute__((aligned(16))) float sPix[3 * kPlane];
   // phase D's zigzag staging [wave][group][64] reuses the bytes of the sRGB
   // LUT (XYB load only) and of the phase-A / CfL scratch sH (a barrier
@@ -1360,18 +1361,22 @@ hipError_t set_front_constants(const float lut[256], const float wts[5][3][64], 
   const hipError_t e2 = hipStreamSynchronize(s);
   return e != hipSuccess ? e : e2;
 }
-void launch_front(const FrontArgs& a, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s) {
-  if (a.proposals & 1u)
-    hipLaunchKernelGGL(front_kernel<true>, dim3(tiles_x, tiles_y), dim3(kThreads), 0, s, a);
+// (the frames of a batch share their size and parameters)
+void launch_front(const FrontArgs* a, uint32_t k, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s) {
+  if (!k) return;
+  const Batch<FrontArgs> b = make_batch(a, k);
+  if (a[0].proposals & 1u)
+    hipLaunchKernelGGL(front_kernel<true>, dim3(tiles_x, tiles_y, k), dim3(kThreads), 0, s, b);
   else
-    hipLaunchKernelGGL(front_kernel<false>, dim3(tiles_x, tiles_y), dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL(front_kernel<false>, dim3(tiles_x, tiles_y, k), dim3(kThreads), 0, s, b);
 }
-void launch_front_list(const FrontArgs& a, uint32_t ntiles, hipStream_t s) {
-  if (!ntiles) return;
-  if (a.proposals & 1u)
-    hipLaunchKernelGGL(front_kernel<true>, dim3(ntiles), dim3(kThreads), 0, s, a);
+void launch_front_list(const FrontArgs* a, uint32_t k, uint32_t ntiles, hipStream_t s) {
+  if (!ntiles || !k) return;
+  const Batch<FrontArgs> b = make_batch(a, k);
+  if (a[0].proposals & 1u)
+    hipLaunchKernelGGL(front_kernel<true>, dim3(ntiles, 1, k), dim3(kThreads), 0, s, b);
   else
-    hipLaunchKernelGGL(front_kernel<false>, dim3(ntiles), dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL(front_kernel<false>, dim3(ntiles, 1, k), dim3(kThreads), 0, s, b);
 }
 void launch_homog(const HomogArgs& a, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s) {
   hipLaunchKernelGGL(homog_kernel, dim3(tiles_x, tiles_y), dim3(kThreads), 0, s, a);

@@ -326,6 +326,10 @@ struct Ctx {
   hipStream_t in_stream = nullptr;
   hipEvent_t ev_in = nullptr;
   bool owned_lane = false;  // a pipeline / batch lane of another context
+  // a pipeline lane's extra slots: contexts with their own buffers that share
+  // this context's stream (super-frames: k frames per batched launch)
+  std::vector<std::unique_ptr<Ctx, CtxDeleter>> slots;
+  bool shared_stream = false;  // `stream` belongs to the lane that owns this slot
   std::unique_ptr<struct Job> job;  // sharded encode in flight (begin -> end)
   std::unique_ptr<struct Pipe> pipe;  // streaming encode (jxg_submit_* / jxg_receive)
   std::vector<uint32_t> payload_head;  // last jxg_shard_end: payload head words
@@ -603,6 +607,14 @@ struct Job {
   uint32_t nrows = 0, nchunks = 0, nstreams = 0;
   AcArgs aa{};
   LfArgs la{};
+  // argument blocks of the front / merge / LF-list stages and the rANS coder
+  // (build_front, build_emit): the batched launches gather them per frame
+  FrontArgs fa{};
+  AqArgs qa{};
+  MergeArgs ma{};
+  VbArgs va{};
+  AnsArgs na{};
+  bool aq = false;  // masking quant field (aq_kernel before the front kernel)
   // host stage results
   std::vector<BitWriter> preA, preB;
   BitWriter lfglobal, hfglobal;
@@ -826,12 +838,13 @@ static jxg_status stage_alloc(Ctx* c, Job& J) {
   return JXG_OK;
 }
 
-// ---- stage B: front end + merge stage over the plan's tiles ----
-static jxg_status stage_front(Ctx* c, Job& J) {
-  hipStream_t s = c->stream;
+// ---- stage B: argument blocks of the front end, merge stage and LF lists
+// over the plan's tiles (launched by launch_stats, batched over frames) ----
+static jxg_status build_front(Ctx* c, Job& J) {
   const jxg_params& P = c->params;
   const Frame& f = J.f;
-  FrontArgs fa{};
+  FrontArgs& fa = J.fa;
+  fa = FrontArgs{};
   fa.rgb = J.d_rgb;
   fa.w = J.w;
   fa.h = J.h;
@@ -873,7 +886,9 @@ static jxg_status stage_front(Ctx* c, Job& J) {
     // the libjxl-shaped masking quant field of the plan's tiles, before the
     // front kernel (== oracle/aq.c jxo_aq_masking)
     JXG_HIP(c->aqf.ensure((size_t)f.bxs * f.bys));
-    AqArgs q{};
+    J.aq = true;
+    AqArgs& q = J.qa;
+    q = AqArgs{};
     q.rgb = J.d_rgb;
     q.w = J.w;
     q.h = J.h;
@@ -895,18 +910,13 @@ static jxg_status stage_front(Ctx* c, Job& J) {
     q.inv_g = f.inv_g;
     q.qf = c->aqf.p;
     q.tile_list = listed ? c->tile_list.p : nullptr;
-    launch_aq(q, listed ? (uint32_t)J.plan.tiles.size() : f.tiles_x * f.tiles_y, s);
-    JXG_HIP(hipGetLastError());
     fa.qf_in = c->aqf.p;
+  } else {
+    J.aq = false;
   }
-  if (listed)
-    launch_front_list(fa, (uint32_t)J.plan.tiles.size(), s);
-  else if (J.plan.world == 1)
-    launch_front(fa, f.tiles_x, f.tiles_y, s);
-  JXG_HIP(hipGetLastError());
-  JXG_HIP(hipEventRecord(c->ev[5], s));  // end of the front kernel alone
   if (J.max_s) {
-    MergeArgs ma{};
+    MergeArgs& ma = J.ma;
+    ma = MergeArgs{};
     ma.xyb = c->xyb_tiles.p;
     ma.bxs = f.bxs;
     ma.bys = f.bys;
@@ -936,29 +946,9 @@ static jxg_status stage_front(Ctx* c, Job& J) {
     ma.nat = c->mnat.p;
     ma.work = c->mwork.p;
     ma.nwrite = 256 * 3 * 4;  // CUs x resident workgroups x 4
-    JXG_HIP(launch_merge(ma, s));
-    JXG_HIP(hipGetLastError());
   }
-  return JXG_OK;
-}
-
-// ---- stage C: AC token statistics of the plan's pass groups ----
-static jxg_status stage_ac_stats(Ctx* c, Job& J) {
-  // (the statistics arena was zeroed by the front kernel)
-  launch_ac_hist(J.aa, J.plan.ng(), c->stream);
-  JXG_HIP(hipGetLastError());
-  return JXG_OK;
-}
-
-// ---- stage D: LF-group statistics (varblock lists, modular histograms) ----
-static jxg_status stage_lf_stats(Ctx* c, Job& J) {
-  hipStream_t s = c->stream;
-  const Frame& f = J.f;
-  VbArgs va{c->acs.p, f.bxs, f.bys, f.lfxs, J.plan.world > 1 ? c->lf_mine.p : nullptr, c->vb.p,
-            c->vcount.p};
-  launch_vb_list(va, f.nlf, s);  // (lfhist, sbound: zeroed by stage_ac_stats)
-  if (J.nchunks) launch_lf_hist(J.la, J.nchunks, s);
-  JXG_HIP(hipGetLastError());
+  J.va = VbArgs{c->acs.p, f.bxs, f.bys, f.lfxs, J.plan.world > 1 ? c->lf_mine.p : nullptr, c->vb.p,
+                c->vcount.p};
   return JXG_OK;
 }
 
@@ -987,6 +977,67 @@ static jxg_status stage_download_lf(Ctx* c, Job& J) {
                          hipMemcpyDeviceToHost, s));
   JXG_HIP(hipEventRecord(c->ev[2], s));
   return JXG_OK;
+}
+
+// ---- stages B-E of k frames of one size and plan whose contexts share one
+// stream (a pipeline lane's slots; k = 1 for one-at-a-time encodes): one
+// launch of each kernel for all of them, each frame's downloads after it ----
+template <class A, class F>
+static std::vector<A> gather(Job* const* js, uint32_t k, F f) {
+  std::vector<A> v(k);
+  for (uint32_t i = 0; i < k; i++) v[i] = f(*js[i]);
+  return v;
+}
+// front end (+ masking quant field), merge stage, AC token statistics
+static jxg_status launch_transform(Ctx* const* cs, Job* const* js, uint32_t k) {
+  hipStream_t s = cs[0]->stream;
+  const Job& J = *js[0];
+  const Frame& f = J.f;
+  const bool listed = !J.plan.tiles.empty();
+  const uint32_t ntiles = listed ? (uint32_t)J.plan.tiles.size() : f.tiles_x * f.tiles_y;
+  for (uint32_t i = 0; i < k; i++) JXG_HIP(hipEventRecord(cs[i]->ev[0], s));
+  if (J.aq) {
+    const auto q = gather<AqArgs>(js, k, [](Job& j) { return j.qa; });
+    launch_aq(q.data(), k, ntiles, s);
+  }
+  const auto fa = gather<FrontArgs>(js, k, [](Job& j) { return j.fa; });
+  if (listed)
+    launch_front_list(fa.data(), k, ntiles, s);
+  else if (J.plan.world == 1)
+    launch_front(fa.data(), k, f.tiles_x, f.tiles_y, s);
+  JXG_HIP(hipGetLastError());
+  for (uint32_t i = 0; i < k; i++) JXG_HIP(hipEventRecord(cs[i]->ev[5], s));  // front kernel alone
+  if (J.max_s) {
+    const auto ma = gather<MergeArgs>(js, k, [](Job& j) { return j.ma; });
+    JXG_HIP(launch_merge(ma.data(), k, s));
+  }
+  for (uint32_t i = 0; i < k; i++) JXG_HIP(hipEventRecord(cs[i]->ev[1], s));
+  // (the statistics arenas were zeroed by the front kernel)
+  const auto aa = gather<AcArgs>(js, k, [](Job& j) { return j.aa; });
+  launch_ac_hist(aa.data(), k, J.plan.ng(), s);
+  JXG_HIP(hipGetLastError());
+  return JXG_OK;
+}
+// varblock lists, LF-stream histograms, and each frame's LF statistics download
+static jxg_status launch_lf_stats(Ctx* const* cs, Job* const* js, uint32_t k) {
+  hipStream_t s = cs[0]->stream;
+  const Job& J = *js[0];
+  const auto va = gather<VbArgs>(js, k, [](Job& j) { return j.va; });
+  launch_vb_list(va.data(), k, J.f.nlf, s);
+  const auto la = gather<LfArgs>(js, k, [](Job& j) { return j.la; });
+  launch_lf_hist(la.data(), k, J.nchunks, s);
+  JXG_HIP(hipGetLastError());
+  for (uint32_t i = 0; i < k; i++) {
+    const jxg_status st = stage_download_lf(cs[i], *js[i]);
+    if (st) return st;
+  }
+  return JXG_OK;
+}
+// all of stages B-E (each frame's own AC histogram)
+static jxg_status launch_stats(Ctx* const* cs, Job* const* js, uint32_t k) {
+  jxg_status st = launch_transform(cs, js, k);
+  for (uint32_t i = 0; i < k && !st; i++) st = stage_download_ac(cs[i], *js[i], cs[i]->hist_ac.p);
+  return st ? st : launch_lf_stats(cs, js, k);
 }
 
 // ---- stage F (host): prefix codes, LF preludes, LfGlobal / HfGlobal,
@@ -1223,47 +1274,64 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
 
 // ---- stage G: rANS coder (the prefix-code AC emission was launched by
 // stage_codes), LF-stream bit emission, bit counts to the host ----
-static jxg_status stage_emit(Ctx* c, Job& J, bool sync = true) {
-  hipStream_t s = c->stream;
-  const Frame& f = J.f;
+static void build_emit(Ctx* c, Job& J) {
+  J.la.scratch = c->lf_scratch;
+  if (!J.ans) return;
+  AnsArgs& na = J.na;
+  na = AnsArgs{};
+  na.tokens = c->tokens.p;
+  na.val = c->tval.p;
+  na.len = c->tlen.p;
+  na.ntok = c->ntok.p;
+  na.bandtok = c->bandtok.p;
+  na.tab = c->ans_tab.p;
+  na.nhist = J.nhist_ans;
+  na.state = c->ans_state.p;
+  na.base = c->gbase.p;
+  na.scratch = c->scratch.p;
+  na.bits = c->gbits.p;
+  na.g0 = J.plan.g0();
+  na.n = J.plan.ng();
+  na.glist = J.aa.glist;
+  na.order = c->ans_order.p;
+  na.csum = c->csum.p;
+  na.max_tokens = J.max_tokens;
+}
+// the emission of k frames sharing a stream (codes built): rANS chains + bit
+// placement and LF streams as one launch each, then each frame's bit counts
+// to the host
+static jxg_status launch_emit(Ctx* const* cs, Job* const* js, uint32_t k) {
+  hipStream_t s = cs[0]->stream;
+  const Job& J = *js[0];
+  for (uint32_t i = 0; i < k; i++) build_emit(cs[i], *js[i]);
   if (J.ans) {
-    AnsArgs na{};
-    na.tokens = c->tokens.p;
-    na.val = c->tval.p;
-    na.len = c->tlen.p;
-    na.ntok = c->ntok.p;
-    na.bandtok = c->bandtok.p;
-    na.tab = c->ans_tab.p;
-    na.nhist = J.nhist_ans;
-    na.state = c->ans_state.p;
-    na.base = c->gbase.p;
-    na.scratch = c->scratch.p;
-    na.bits = c->gbits.p;
-    na.g0 = J.plan.g0();
-    na.n = J.plan.ng();
-    na.glist = J.aa.glist;
-    na.order = c->ans_order.p;
-    na.csum = c->csum.p;
-    na.max_tokens = J.max_tokens;
-    launch_ans(na, s);
+    const auto na = gather<AnsArgs>(js, k, [](Job& j) { return j.na; });
+    launch_ans(na.data(), k, s);
     JXG_HIP(hipGetLastError());
   }
-  J.la.scratch = c->lf_scratch;
-  if (J.nchunks) launch_lf_code(J.la, J.nchunks, s);
+  const auto la = gather<LfArgs>(js, k, [](Job& j) { return j.la; });
+  launch_lf_code(la.data(), k, J.nchunks, s);
   JXG_HIP(hipGetLastError());
-  if (J.ans) {  // [gbits | stream_bits]: one copy
-    JXG_HIP(hipMemcpyAsync(c->h_bits.p, c->bits.p, ((size_t)f.ngroups + J.nstreams) * 4,
-                           hipMemcpyDeviceToHost, s));
-    JXG_HIP(hipEventRecord(c->ev[7], s));
-  } else {
-    JXG_HIP(hipMemcpyAsync(c->h_sbits.p, c->stream_bits.p, J.nstreams * 4, hipMemcpyDeviceToHost, s));
-  }
-  JXG_HIP(hipEventRecord(c->ev[3], s));
-  if (sync) {
-    jxg_status st = wait_emission(c, J);
-    if (st) return st;
+  for (uint32_t i = 0; i < k; i++) {
+    Ctx* c = cs[i];
+    const Frame& f = js[i]->f;
+    if (J.ans) {  // [gbits | stream_bits]: one copy
+      JXG_HIP(hipMemcpyAsync(c->h_bits.p, c->bits.p, ((size_t)f.ngroups + js[i]->nstreams) * 4,
+                             hipMemcpyDeviceToHost, s));
+      JXG_HIP(hipEventRecord(c->ev[7], s));
+    } else {
+      JXG_HIP(hipMemcpyAsync(c->h_sbits.p, c->stream_bits.p, js[i]->nstreams * 4,
+                             hipMemcpyDeviceToHost, s));
+    }
+    JXG_HIP(hipEventRecord(c->ev[3], s));
   }
   return JXG_OK;
+}
+static jxg_status stage_emit(Ctx* c, Job& J, bool sync = true) {
+  Job* jp = &J;
+  jxg_status st = launch_emit(&c, &jp, 1);
+  if (!st && sync) st = wait_emission(c, J);
+  return st;
 }
 
 // ---- stage H: concatenation.  Sections are bit-exact piece lists (host
@@ -1537,9 +1605,9 @@ static jxg_status order_input(Ctx* owner, Ctx* lane) {
 // downloads, all launched asynchronously on the context's stream
 // (rank, world): a shard of a frame whose plan needs no record exchange and,
 // with world > 1, ANS (one HF preset per rank): no collective before assembly
-static jxg_status enc_launch(Ctx* c, Job& J, const uint8_t* d_rgb, uint32_t w, uint32_t h,
-                             size_t stride, uint32_t rank = 0, uint32_t world = 1) {
-  hipStream_t s = c->stream;
+// the frame's plan, buffers and argument blocks (nothing launched)
+static jxg_status enc_prepare(Ctx* c, Job& J, const uint8_t* d_rgb, uint32_t w, uint32_t h,
+                              size_t stride, uint32_t rank, uint32_t world) {
   J.f = make_frame(w, h, c->params.distance);
   J.plan = make_plan(J.f, rank, world);
   J.w = w;
@@ -1549,13 +1617,14 @@ static jxg_status enc_launch(Ctx* c, Job& J, const uint8_t* d_rgb, uint32_t w, u
   jxg_status st = stage_alloc(c, J);
   if (st) return st;
   J.presets = J.ans && world > 1;
-  JXG_HIP(hipEventRecord(c->ev[0], s));
-  if ((st = stage_front(c, J))) return st;
-  JXG_HIP(hipEventRecord(c->ev[1], s));
-  if ((st = stage_ac_stats(c, J))) return st;
-  if ((st = stage_download_ac(c, J, c->hist_ac.p))) return st;
-  if ((st = stage_lf_stats(c, J))) return st;
-  return stage_download_lf(c, J);
+  return build_front(c, J);
+}
+static jxg_status enc_launch(Ctx* c, Job& J, const uint8_t* d_rgb, uint32_t w, uint32_t h,
+                             size_t stride, uint32_t rank = 0, uint32_t world = 1) {
+  jxg_status st = enc_prepare(c, J, d_rgb, w, h, stride, rank, world);
+  if (st) return st;
+  Job* jp = &J;
+  return launch_stats(&c, &jp, 1);
 }
 
 // phase 2: (host, after the statistics arrive) codes and headers; AC / LF
@@ -1703,24 +1772,28 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
 
 // ---------------------------------------------------------------------------
 // streaming encode (jxg_submit_rgb8[_device] / jxg_receive): a software
-// pipeline over D lanes (the caller's context plus lanes it owns, one stream
-// each), driven by the caller's one host thread.  submit(j):
-//   frame j-1's codes (host work: clustering, ANS / prefix tables, headers,
-//   LF-group codes) start on a helper thread -> finish the oldest frame if D
-//   are in flight (wait for its emission, assemble, codestream to the host)
-//   -> launch frame j's front end, merge stage and statistics on a free lane
-//   -> join the codes of frame j-lag (its emission is launched by then).
-// So the rANS chains of the frames before j (latency-bound waves that use
-// little of their SIMDs) run while frame j's transform kernels fill the rest
-// of the chip.  A frame's chain lasts as long as its longest pass group's,
-// whatever the frame size, so the depth follows the frame: ~3570 pass groups
-// in flight (8K: 7 lanes), at least 4, up to kPipeMaxLanes for small frames.
-// The lag follows it too: 1 for large frames (the GPU is the bound), 3 for
-// small ones, whose host work per frame is the bound.  Every
-// lane needs its own hardware queue (GPU_MAX_HW_QUEUES > D, bench.py sets 16).
+// pipeline over lanes (the caller's context plus lanes it owns, one stream
+// each), driven by the caller's one host thread.  A frame's rANS chains last
+// as long as its longest pass group's whatever the frame size, and a lane's
+// stream is held by a frame from its front end to its assembly, so the
+// frames in flight -- not the GPU's throughput -- bound small frames
+// (profiles/r04f: ms per 1080p frame falls as 1 / lanes up to the 12 lanes
+// the hardware queues allow).  So a lane carries a SUPER-FRAME: up to
+// kMaxBatch frames of one size in slots (contexts with their own buffers
+// sharing the lane's stream) that go through every per-frame kernel as one
+// batched launch (blockIdx.z = the frame): front end, merge stage,
+// statistics, then -- once a helper thread has built the codes of every
+// frame of the batch -- rANS chains + bit placement and LF streams.  submit:
+//   the frame joins the open batch (a free lane's next slot; completing the
+//   oldest frames frees one) -> a full batch (or one of another size) is
+//   launched, its codes queued on the helper threads; the last helper to
+//   finish launches the batch's emission.
+// Frames complete in submission order (deferred finish: layout, concat and
+// the codestream's D2H enqueued; jxg_receive waits for the copy).  ~3570 pass
+// groups in flight: 8K 7 lanes x 1, 1080p 12 lanes x 4.  Every lane needs
+// its own hardware queue (GPU_MAX_HW_QUEUES > lanes, bench.py sets 16).
 // ---------------------------------------------------------------------------
 constexpr uint32_t kPipeMaxLanes = 12, kPipeMinLanes = 4, kPipeChainGroups = 3570;
-constexpr uint32_t kPipeLagSmall = 3, kPipeLagLarge = 1;
 // Hardware queues of this process (GPU_MAX_HW_QUEUES as HIP read it at start
 // up; HIP's default is 4).  Lanes beyond queues - 1 (one is left for the
 // caller's own stream) would share a queue with another lane and serialise
@@ -1732,14 +1805,17 @@ static uint32_t hw_queues() {
   const long q = e && *e ? std::strtol(e, nullptr, 10) : 4;
   return (uint32_t)std::min<long>(32, std::max<long>(1, q));
 }
-static uint32_t pipe_depth(uint32_t ngroups) {
-  const uint32_t d = (kPipeChainGroups + ngroups - 1) / std::max(1u, ngroups);
-  const uint32_t want = std::min(kPipeMaxLanes, std::max(kPipeMinLanes, d));
-  return std::max(2u, std::min(want, hw_queues() - 1));
-}
-static uint32_t pipe_lag(uint32_t ngroups, uint32_t depth) {
-  const uint32_t lag = ngroups >= 256 ? kPipeLagLarge : kPipeLagSmall;
-  return std::max(1u, std::min(lag, depth - 1));
+// lanes and frames per lane (batch) for a frame / shard of `ngroups` groups
+struct PipeShape {
+  uint32_t lanes, batch;
+  uint32_t frames() const { return lanes * batch; }
+};
+static PipeShape pipe_shape(uint32_t ngroups) {
+  const uint32_t want = (kPipeChainGroups + ngroups - 1) / std::max(1u, ngroups);  // frames
+  const uint32_t lmax = std::max(2u, std::min(kPipeMaxLanes, hw_queues() - 1));
+  const uint32_t k = std::min(kMaxBatch, std::max(1u, (want + lmax - 1) / lmax));
+  const uint32_t lanes = std::min(lmax, std::max(std::min(kPipeMinLanes, lmax), (want + k - 1) / k));
+  return PipeShape{lanes, k};
 }
 // a completed frame: its codestream (pinned host block) and stats; `ev`: the
 // codestream's D2H, still in flight when the frame was completed (deferred
@@ -1749,19 +1825,56 @@ struct PipeDone {
   jxg_stats stats;
   hipEvent_t ev;
 };
+struct PipeBatch;
 struct PipeFrame {
-  Ctx* lane = nullptr;
+  Ctx* lane = nullptr;   // the frame's slot (its buffers; the lane's stream)
+  Ctx* owner = nullptr;  // the lane
+  std::shared_ptr<PipeBatch> batch;
   Job J;
-  int phase = 1;  // 1: statistics launched; 2: emission launched
+  int phase = 0;  // 0: in the open batch; 1: statistics launched; 2: emission launched
   bool shard = false;
   Clock::time_point t0;
+  const uint8_t* src = nullptr;  // the device input (phase 0)
+  uint32_t w = 0, h = 0, rank = 0, world = 1;
+  size_t stride = 0;
   std::future<jxg_status> codes;  // valid while a helper builds the codes
 };
+// frames launched together on one lane; the last of their codes launches the
+// batch's emission
+struct PipeBatch {
+  Ctx* owner = nullptr;
+  uint32_t w = 0, h = 0, rank = 0, world = 1;
+  bool shard = false;
+  std::vector<PipeFrame*> frames;
+  std::atomic<int> left{0};         // codes not yet built
+  std::atomic<int> err{JXG_OK};     // a frame's codes or the emission failed
+};
+// the codes of frame fr of its batch (a helper thread, or inline); the
+// batch's last one launches the emission of all its frames
+static jxg_status pipe_codes(PipeFrame* fr) {
+  PipeBatch& B = *fr->batch;
+  jxg_status st = stage_codes(fr->lane, fr->J);
+  if (st) B.err.store(st);
+  if (B.left.fetch_sub(1) == 1 && !B.err.load()) {
+    std::vector<Ctx*> cs;
+    std::vector<Job*> js;
+    for (PipeFrame* q : B.frames) {
+      cs.push_back(q->lane);
+      js.push_back(&q->J);
+    }
+    const jxg_status e = launch_emit(cs.data(), js.data(), (uint32_t)cs.size());
+    if (e) B.err.store(e);
+  }
+  return st;
+}
 // the helper's codes of a frame -> phase 2 (on an error the caller aborts)
 static jxg_status pipe_join_codes(PipeFrame& fr) {
-  if (!fr.codes.valid()) return JXG_OK;
-  const jxg_status st = fr.codes.get();
-  fr.phase = 2;
+  jxg_status st = JXG_OK;
+  if (fr.codes.valid()) {
+    st = fr.codes.get();
+    fr.phase = 2;
+  }
+  if (!st && fr.batch) st = (jxg_status)fr.batch->err.load();
   return st;
 }
 // Helper threads of a pipeline: persistent (a std::async thread per frame cost
@@ -1820,7 +1933,7 @@ class Helpers {
   std::vector<std::thread> t_;
   bool stop_ = false;
 };
-constexpr int kPipeHelpers = 4;  // >= the small-frame lag (3) + 1
+constexpr int kPipeHelpers = 6;  // codes of a batch (<= kMaxBatch) and the next one's in parallel
 
 struct Pipe {
   std::vector<std::unique_ptr<PipeFrame>> inflight;  // submission order
@@ -1831,7 +1944,8 @@ struct Pipe {
   std::vector<std::unique_ptr<PipeFrame>> ready;
   uint64_t submitted = 0;
   int mode = 0;  // 1 whole frames, 2 shards (while any frame is pending)
-  uint32_t depth = 0;
+  uint32_t depth = 0;  // frames in flight (lanes x batch)
+  std::shared_ptr<PipeBatch> open;   // frames submitted, not yet launched
   std::unique_ptr<Helpers> helpers;  // created with the first helper task
   ~Pipe() {
     for (auto& d : done)
@@ -1872,11 +1986,28 @@ static jxg_status ensure_lanes(Ctx* c, uint32_t extra) {
   }
   return JXG_OK;
 }
+// slot i of lane L (0: the lane itself; others share its stream)
+static jxg_status ensure_slots(Ctx* L, uint32_t k) {
+  while (L->slots.size() + 1 < k) {
+    Ctx* q = new (std::nothrow) Ctx();
+    if (!q) return JXG_ERR_OOM;
+    q->params = L->params;
+    q->owned_lane = true;
+    q->shared_stream = true;
+    q->stream = L->stream;
+    L->slots.emplace_back(q);
+    for (auto& e : q->ev)
+      if (hipEventCreate(&e) != hipSuccess) return JXG_ERR_HIP;
+  }
+  return JXG_OK;
+}
+static Ctx* lane_slot(Ctx* L, uint32_t i) { return i == 0 ? L : L->slots[i - 1].get(); }
 
 // drop every frame in flight (after an error): wait for the helpers and the
 // lanes' streams
 static void pipe_abort(Ctx* c) {
   Pipe& p = *c->pipe;
+  p.open.reset();
   for (auto& fr : p.inflight) (void)pipe_join_codes(*fr);
   for (auto& fr : p.inflight) (void)hipStreamSynchronize(fr->lane->stream);
   for (auto& fr : p.ready) (void)hipStreamSynchronize(fr->lane->stream);
@@ -1952,16 +2083,54 @@ static void shard_frame_stats(PipeFrame& fr, size_t bytes) {
   S.ms_host_call = ms_since(fr.t0);
 }
 
+// the open batch -> launched: every frame's plan and buffers, the batched
+// front end / merge / statistics kernels, the frames' codes queued on the
+// helper threads (inline without threads: codes, then the emission)
+static jxg_status pipe_launch_open(Ctx* c) {
+  Pipe& p = *c->pipe;
+  std::shared_ptr<PipeBatch> B = std::move(p.open);
+  p.open.reset();
+  if (!B || B->frames.empty()) return JXG_OK;
+  const uint32_t k = (uint32_t)B->frames.size();
+  std::vector<Ctx*> cs;
+  std::vector<Job*> js;
+  for (PipeFrame* fr : B->frames) {
+    const jxg_status st = enc_prepare(fr->lane, fr->J, fr->src, fr->w, fr->h, fr->stride,
+                                      fr->rank, fr->world);
+    if (st) return st;
+    cs.push_back(fr->lane);
+    js.push_back(&fr->J);
+  }
+  jxg_status st = launch_stats(cs.data(), js.data(), k);
+  if (st) return st;
+  B->left.store((int)k);
+  for (PipeFrame* fr : B->frames) fr->phase = 1;
+  try {
+    if (!p.helpers) p.helpers.reset(new Helpers(c->params.device, kPipeHelpers));
+    for (PipeFrame* fr : B->frames) fr->codes = p.helpers->run([fr]() { return pipe_codes(fr); });
+  } catch (...) {  // no thread: the codes (and the emission) on this one
+    for (PipeFrame* fr : B->frames) {
+      if (fr->codes.valid()) continue;
+      if ((st = pipe_codes(fr))) return st;
+      fr->phase = 2;
+    }
+  }
+  return JXG_OK;
+}
+
 // oldest frame in flight -> done (a whole frame: assembled, codestream on
 // the host) or ready (a shard: sections emitted, payload head built); on an
 // error the caller aborts the pipe
 static jxg_status pipe_complete_oldest(Ctx* c) {
   Pipe& p = *c->pipe;
+  jxg_status st = JXG_OK;
+  if (p.inflight.front()->phase == 0 && (st = pipe_launch_open(c))) return st;
   PipeFrame& fr = *p.inflight.front();
-  jxg_status st = pipe_join_codes(fr);
-  if (!st && fr.phase == 1) {
-    st = enc_codes(fr.lane, fr.J, false);
-    fr.phase = 2;
+  // every frame of its batch: the last codes launch the batch's emission
+  // (the batch's frames are the oldest in flight, consecutive)
+  for (size_t i = 0; i < p.inflight.size() && p.inflight[i]->batch == fr.batch; i++) {
+    const jxg_status e = pipe_join_codes(*p.inflight[i]);
+    if (!st) st = e;
   }
   if (fr.shard) {
     size_t bytes = 0;
@@ -2030,79 +2199,81 @@ static jxg_status pipe_submit(Ctx* c, const uint8_t* src, bool on_device, uint32
       return JXG_ERR_UNSUPPORTED;
     ngroups = P.ng();
   }
-  const uint32_t depth = pipe_depth(ngroups);
-  const uint32_t lag = pipe_lag(ngroups, depth);
-  jxg_status st = ensure_lanes(c, depth - 1);
+  const PipeShape shape = pipe_shape(ngroups);
+  jxg_status st = ensure_lanes(c, shape.lanes - 1);
   if (st) return st;
   const Clock::time_point t0 = Clock::now();
-  // a shard frame holds its lane until its sections are written: the caller
+  // a shard frame holds its slot until its sections are written: the caller
   // must take one first (jxg_shard_next_head / jxg_shard_write_next)
-  if (shard && p.ready.size() >= depth) return JXG_ERR_INVALID_ARG;
+  if (shard && p.ready.size() >= shape.frames()) return JXG_ERR_INVALID_ARG;
   p.mode = mode;
-  p.depth = depth;
-  // the newest frame's codes on a helper thread, while this thread finishes
-  // the oldest frame and launches frame j on another lane
-  if (!p.inflight.empty()) {
-    PipeFrame* prev = p.inflight.back().get();
-    if (prev->phase == 1 && !prev->codes.valid()) {
-      try {
-        if (!p.helpers) p.helpers.reset(new Helpers(c->params.device, kPipeHelpers));
-        prev->codes = p.helpers->run([prev]() { return enc_codes(prev->lane, prev->J, false); });
-      } catch (...) {  // no thread: build the codes on this one
-        if ((st = enc_codes(prev->lane, prev->J, false))) {
-          pipe_abort(c);
-          return st;
-        }
-        prev->phase = 2;
-      }
-    }
-  }
+  p.depth = shape.frames();
   auto fail = [&](jxg_status e) {
     pipe_abort(c);
     return e;
   };
-  while (!p.inflight.empty() && p.inflight.size() + p.ready.size() >= depth)
-    if ((st = pipe_complete_oldest(c))) return fail(st);
-  // a lane no frame in flight (or ready) uses (the lowest index)
-  Ctx* L = nullptr;
-  for (uint32_t li = 0; li < depth && !L; li++) {
-    Ctx* cand = pipe_lane(c, li);
-    bool used = false;
-    for (auto& q : p.inflight) used = used || q->lane == cand;
-    for (auto& q : p.ready) used = used || q->lane == cand;
-    if (!used) L = cand;
+  // an open batch of another size / plan, or a full one, goes out first
+  if (p.open && (p.open->w != w || p.open->h != h || p.open->rank != rank ||
+                 p.open->world != world || p.open->frames.size() >= shape.batch))
+    if ((st = pipe_launch_open(c))) return fail(st);
+  if (!p.open) {
+    // a free lane (no frame in flight or ready on it): complete the oldest
+    // frames until one is
+    Ctx* L = nullptr;
+    for (;;) {
+      for (uint32_t li = 0; li < shape.lanes && !L; li++) {
+        Ctx* cand = pipe_lane(c, li);
+        bool used = false;
+        for (auto& q : p.inflight) used = used || q->owner == cand;
+        for (auto& q : p.ready) used = used || q->owner == cand;
+        if (!used) L = cand;
+      }
+      if (L) break;
+      if (p.inflight.empty()) return shard ? JXG_ERR_INVALID_ARG : fail(JXG_ERR_INTERNAL);
+      if ((st = pipe_complete_oldest(c))) return fail(st);
+    }
+    if ((st = ensure_slots(L, shape.batch))) return fail(st);
+    p.open = std::make_shared<PipeBatch>();
+    PipeBatch& B = *p.open;
+    B.owner = L;
+    B.w = w;
+    B.h = h;
+    B.rank = rank;
+    B.world = world;
+    B.shard = shard;
   }
-  if (!L) return shard ? JXG_ERR_INVALID_ARG : fail(JXG_ERR_INTERNAL);
+  PipeBatch& B = *p.open;
   std::unique_ptr<PipeFrame> fr(new (std::nothrow) PipeFrame());
   if (!fr) return fail(JXG_ERR_OOM);
-  fr->lane = L;
+  Ctx* S = lane_slot(B.owner, (uint32_t)B.frames.size());
+  fr->lane = S;
+  fr->owner = B.owner;
+  fr->batch = p.open;
   fr->t0 = t0;
   fr->shard = shard;
+  fr->w = w;
+  fr->h = h;
+  fr->stride = stride;
+  fr->rank = rank;
+  fr->world = world;
   if (!on_device) {
-    // the lane's previous frame has completed, so its staging is free
+    // the slot's previous frame has completed, so its staging is free
     const size_t bytes = stride * (h - 1) + (size_t)w * 3;
-    if (L->h_stage.ensure(bytes) != hipSuccess || L->rgb.ensure(bytes) != hipSuccess)
+    if (S->h_stage.ensure(bytes) != hipSuccess || S->rgb.ensure(bytes) != hipSuccess)
       return fail(JXG_ERR_OOM);
-    std::memcpy(L->h_stage.p, src, bytes);
-    if (hipMemcpyAsync(L->rgb.p, L->h_stage.p, bytes, hipMemcpyHostToDevice, L->stream) !=
+    std::memcpy(S->h_stage.p, src, bytes);
+    if (hipMemcpyAsync(S->rgb.p, S->h_stage.p, bytes, hipMemcpyHostToDevice, S->stream) !=
         hipSuccess)
       return fail(JXG_ERR_HIP);
-    src = L->rgb.p;
-  } else if ((st = order_input(c, L))) {
+    src = S->rgb.p;
+  } else if ((st = order_input(c, S))) {
     return fail(st);
   }
-  if ((st = enc_launch(L, fr->J, src, w, h, stride, rank, world))) {
-    (void)hipStreamSynchronize(L->stream);
-    return fail(st);
-  }
+  fr->src = src;
+  B.frames.push_back(fr.get());
   p.inflight.push_back(std::move(fr));
   p.submitted++;
-  // frame j - lag: codes built, emission launched
-  if (p.inflight.size() > lag) {
-    PipeFrame& fj = *p.inflight[p.inflight.size() - 1 - lag];
-    st = pipe_join_codes(fj);
-    if (st) return fail(st);
-  }
+  if (B.frames.size() >= shape.batch && (st = pipe_launch_open(c))) return fail(st);
   return JXG_OK;
 }
 
@@ -2166,9 +2337,9 @@ static jxg_status shard_begin(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32_t
   // histogram (N x 132 clusters would not fit one context map).
   J.presets = J.ans && world > 1;
   if ((st = order_input(c, c))) return st;
-  JXG_HIP(hipEventRecord(c->ev[0], s));
-  if ((st = stage_front(c, J))) return st;
-  if ((st = stage_ac_stats(c, J))) return st;
+  if ((st = build_front(c, J))) return st;
+  Job* jp = &J;
+  if ((st = launch_transform(&c, &jp, 1))) return st;
   JXG_HIP(hipMemcpyAsync(d_hist, c->hist_ac.p, kMaxClusters * kAlpha * 4, hipMemcpyDeviceToDevice, s));
   // the send list (then the receive list) of the record exchange
   const Exchange& X = J.plan.x;
@@ -2201,8 +2372,8 @@ static jxg_status shard_end(Ctx* c, const uint32_t* d_hist, const uint8_t* d_xbu
   JXG_HIP(hipGetLastError());
   jxg_status st;
   if ((st = stage_download_ac(c, J, d_hist))) return st;
-  if ((st = stage_lf_stats(c, J))) return st;
-  if ((st = stage_download_lf(c, J))) return st;
+  Job* jp = &J;
+  if ((st = launch_lf_stats(&c, &jp, 1))) return st;
   if ((st = stage_codes(c, J))) return st;
   if ((st = stage_emit(c, J))) return st;
   if ((st = shard_finish(c, J, payload_bytes))) return st;
@@ -2606,6 +2777,7 @@ void jxg_destroy(void* ctx) {
     c->pipe.reset();
   }
   c->lanes.clear();  // pipeline lanes (jxg_destroy each)
+  c->slots.clear();  // their extra slots (sharing this context's stream)
   (void)hipSetDevice(c->params.device);
   (void)hipStreamSynchronize(c->stream);
   if (c->stream2) (void)hipStreamSynchronize(c->stream2);
@@ -2616,7 +2788,7 @@ void jxg_destroy(void* ctx) {
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   if (c->ev_in) (void)hipEventDestroy(c->ev_in);
-  if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->stream && !c->shared_stream) (void)hipStreamDestroy(c->stream);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
   delete c;
 }
@@ -2899,7 +3071,7 @@ jxg_status jxg_pipeline_depth(void* ctx, uint32_t xsize, uint32_t ysize, uint32_
     return JXG_ERR_INVALID_ARG;
   const Ctx* c = static_cast<Ctx*>(ctx);
   const Frame f = make_frame(xsize, ysize, c->params.distance);
-  *depth = pipe_depth(world > 1 ? make_plan(f, rank, world).ng() : f.ngroups);
+  *depth = pipe_shape(world > 1 ? make_plan(f, rank, world).ng() : f.ngroups).frames();
   return JXG_OK;
 }
 

@@ -8,6 +8,22 @@
 
 namespace jxg {
 
+// Batched launches (the streaming pipeline's super-frames): up
+// to kMaxBatch frames of one size go through each per-frame kernel as ONE
+// launch -- the argument blocks of all of them in the kernel arguments,
+// blockIdx.z = the frame.  One-at-a-time encodes launch batches of one.
+constexpr uint32_t kMaxBatch = 4;
+template <class A>
+struct Batch {
+  A a[kMaxBatch];
+};
+template <class A>
+inline Batch<A> make_batch(const A* a, uint32_t k) {
+  Batch<A> b{};
+  for (uint32_t i = 0; i < k && i < kMaxBatch; i++) b.a[i] = a[i];
+  return b;
+}
+
 struct FrontArgs {
   const uint8_t* rgb;
   uint32_t w, h;
@@ -49,7 +65,7 @@ struct AqArgs {
   uint8_t* qf;           // [nb] raw - 1 (out)
   const uint32_t* tile_list;  // shard: tile ids, or null: every tile (1-D grid)
 };
-void launch_aq(const AqArgs& a, uint32_t ntiles, hipStream_t s);
+void launch_aq(const AqArgs* a, uint32_t k, uint32_t ntiles, hipStream_t s);
 
 // merge stage (jxg_merge.hip): weight kinds (stored orientation) and the
 // nine merged shapes' pixel-orientation tables, column-major ([kx * R + ky])
@@ -159,8 +175,8 @@ struct AnsArgs {
   uint32_t max_tokens;     // most tokens of any group (ans_emit's segments per group)
 };
 constexpr uint32_t kAnsMaxChunks = (uint32_t)(kGroupTokStride / 64);
-void launch_ans(const AnsArgs& a, hipStream_t s);
-void launch_ans_emit(const AnsArgs& a, hipStream_t s);
+// rANS chains + bit placement of k frames (same plan)
+void launch_ans(const AnsArgs* a, uint32_t k, hipStream_t s);
 
 // LF-group modular streams: rows of (lf group, stream, channel, y)
 // One segment of <= kLfSeg samples of a channel row (long rows -- the
@@ -218,8 +234,8 @@ inline float dist_weight(int c, int area, float w) {
   return (float)(std::sqrt((double)area / 64.0) * ((double)kW0[c] / (double)w));
 }
 hipError_t set_front_constants(const float lut[256], const float wts[5][3][64], hipStream_t s);
-void launch_front(const FrontArgs& a, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s);
-void launch_front_list(const FrontArgs& a, uint32_t ntiles, hipStream_t s);
+void launch_front(const FrontArgs* a, uint32_t k, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s);
+void launch_front_list(const FrontArgs* a, uint32_t k, uint32_t ntiles, hipStream_t s);
 // shard exchange: per-group block records (acs, qf, dc) <-> frame arrays
 struct PackArgs {
   uint8_t* acs;
@@ -235,16 +251,16 @@ struct PackArgs {
 void launch_pack(const PackArgs& a, hipStream_t s);    // frame arrays -> records
 void launch_unpack(const PackArgs& a, hipStream_t s);  // records -> frame arrays
 void launch_homog(const HomogArgs& a, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s);
-void launch_ac_hist(const AcArgs& a, uint32_t ngroups, hipStream_t s);
+void launch_ac_hist(const AcArgs* a, uint32_t k, uint32_t ngroups, hipStream_t s);
 void launch_ac_emit(const AcArgs& a, uint32_t ngroups, hipStream_t s);
-void launch_lf_hist(const LfArgs& a, uint32_t nchunks, hipStream_t s);
-void launch_lf_code(const LfArgs& a, uint32_t nchunks, hipStream_t s);
+void launch_lf_hist(const LfArgs* a, uint32_t k, uint32_t nchunks, hipStream_t s);
+void launch_lf_code(const LfArgs* a, uint32_t k, uint32_t nchunks, hipStream_t s);
 hipError_t set_cluster_table(const uint8_t* tab, hipStream_t s);
 hipError_t set_merge_constants(const float* llf_p /*[4][8]*/, const float* llf_ib /*[4][8][8]*/,
                          hipStream_t s);
-hipError_t launch_merge(const MergeArgs& a, hipStream_t s);
+hipError_t launch_merge(const MergeArgs* a, uint32_t k, hipStream_t s);
 void dump_merge_profile();  // JXG_MERGE_PROFILE experiment builds; no-op otherwise
-void launch_vb_list(const VbArgs& a, uint32_t nlf, hipStream_t s);
+void launch_vb_list(const VbArgs* a, uint32_t k, uint32_t nlf, hipStream_t s);
 // decode-side quality (jxg_metrics.hip): orig / comp RGB8 interleaved rows
 struct MetricArgs {
   const uint8_t* orig;

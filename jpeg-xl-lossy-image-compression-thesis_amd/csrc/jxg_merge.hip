@@ -707,7 +707,8 @@ __device__ __forceinline__ int max_level(const MergeArgs& a) {
 }
 
 __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(JXG_MERGE_WPE)))
-void merge_eval_kernel(MergeArgs a) {
+void merge_eval_kernel(Batch<MergeArgs> bt_) {
+  const MergeArgs& a = bt_.a[blockIdx.z];  // the batch's frame
   __shared__ __attribute__((aligned(16))) MergeLds S;
   if (blockIdx.x == 0 && threadIdx.x == 0) a.work[0] = 0;  // merge_resolve's work-list count
   int tile, si;
@@ -739,7 +740,8 @@ __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
 }
-__global__ __launch_bounds__(64 * kResolveWaves) void merge_resolve_kernel(MergeArgs a) {
+__global__ __launch_bounds__(64 * kResolveWaves) void merge_resolve_kernel(Batch<MergeArgs> bt_) {
+  const MergeArgs& a = bt_.a[blockIdx.z];
   __shared__ float sEntW[kResolveWaves][64];
   __shared__ uint8_t sAcsW[kResolveWaves][64];
   __shared__ uint32_t sCnt[kResolveWaves];
@@ -901,7 +903,8 @@ __device__ __forceinline__ void write_entry(const MergeArgs& a, int tile, int si
 // persistent workgroups over the (tile, shape) entries the resolve kernel
 // listed: only (tile, shape) pairs holding a chosen varblock cost anything
 __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(JXG_MERGE_WRITE_WPE)))
-void merge_write_kernel(MergeArgs a) {
+void merge_write_kernel(Batch<MergeArgs> bt_) {
+  const MergeArgs& a = bt_.a[blockIdx.z];
   __shared__ __attribute__((aligned(16))) MergeLds S;
   const uint32_t n = __builtin_amdgcn_readfirstlane(*(volatile uint32_t*)a.work);
   for (uint32_t w = blockIdx.x; w < n; w += gridDim.x) {
@@ -919,7 +922,8 @@ void merge_write_kernel(MergeArgs a) {
 // varblock's first block, in raster order inside the LF group.  Thread t
 // holds the first-block flags of blocks t, t + 1024, ... (all 64 loads in
 // flight at once); per-(chunk, wave) counts -> one workgroup scan -> stores.
-__global__ __launch_bounds__(1024) void vb_list_kernel(VbArgs a) {
+__global__ __launch_bounds__(1024) void vb_list_kernel(Batch<VbArgs> bt_) {
+  const VbArgs& a = bt_.a[blockIdx.z];
   __shared__ uint32_t sCnt[64 * 16];
   __shared__ uint32_t sWave[16];
   const uint32_t lg = blockIdx.x;
@@ -1008,19 +1012,23 @@ hipError_t set_merge_constants(const float* llf_p, const float* llf_ib, hipStrea
   const hipError_t e2 = hipStreamSynchronize(s);
   return e != hipSuccess ? e : e2;
 }
-hipError_t launch_merge(const MergeArgs& a, hipStream_t s) {
-  if (!a.ntiles) return hipSuccess;
+// k frames of one size (same tile count): one launch of each kernel
+hipError_t launch_merge(const MergeArgs* a, uint32_t k, hipStream_t s) {
+  if (!k || !a[0].ntiles) return hipSuccess;
+  const Batch<MergeArgs> b = make_batch(a, k);
+  const uint32_t ntiles = a[0].ntiles;
   constexpr uint32_t T = JXG_MERGE_CHUNK;
-  const uint32_t nwg = (((a.ntiles + 7) / 8 + T - 1) / T) * T * 8 * kNumShapes;
-  hipLaunchKernelGGL(merge_eval_kernel, dim3(nwg), dim3(kMThreads), 0, s, a);
-  hipLaunchKernelGGL(merge_resolve_kernel, dim3((a.ntiles + kResolveWaves - 1) / kResolveWaves),
-                     dim3(64 * kResolveWaves), 0, s, a);
-  const uint32_t nw = min(a.nwrite, a.ntiles * (uint32_t)kNumShapes);
-  hipLaunchKernelGGL(merge_write_kernel, dim3(nw), dim3(kMThreads), 0, s, a);
+  const uint32_t nwg = (((ntiles + 7) / 8 + T - 1) / T) * T * 8 * kNumShapes;
+  hipLaunchKernelGGL(merge_eval_kernel, dim3(nwg, 1, k), dim3(kMThreads), 0, s, b);
+  hipLaunchKernelGGL(merge_resolve_kernel, dim3((ntiles + kResolveWaves - 1) / kResolveWaves, 1, k),
+                     dim3(64 * kResolveWaves), 0, s, b);
+  // the persistent write workgroups: nwrite over the whole launch
+  const uint32_t nw = max(1u, min(a[0].nwrite / k, ntiles * (uint32_t)kNumShapes));
+  hipLaunchKernelGGL(merge_write_kernel, dim3(nw, 1, k), dim3(kMThreads), 0, s, b);
   return hipGetLastError();
 }
-void launch_vb_list(const VbArgs& a, uint32_t nlf, hipStream_t s) {
-  hipLaunchKernelGGL(vb_list_kernel, dim3(nlf), dim3(1024), 0, s, a);
+void launch_vb_list(const VbArgs* a, uint32_t k, uint32_t nlf, hipStream_t s) {
+  if (k) hipLaunchKernelGGL(vb_list_kernel, dim3(nlf, 1, k), dim3(1024), 0, s, make_batch(a, k));
 }
 
 }  // namespace jxg

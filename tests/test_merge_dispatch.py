@@ -54,4 +54,4 @@ def test_source_matches_restatement():
     text = open(SRC).read()
     assert "const int r = q % (kNumShapes * T);" in text
     assert "tile = ((q / (kNumShapes * T)) * T + r % T) * 8 + x;" in text
-    assert "(((a.ntiles + 7) / 8 + T - 1) / T) * T * 8 * kNumShapes" in text
+    assert "(((ntiles + 7) / 8 + T - 1) / T) * T * 8 * kNumShapes" in text
