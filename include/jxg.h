@@ -166,8 +166,10 @@ jxg_status jxg_submit_rgb8_device(void* ctx, const void* d_rgb, uint32_t xsize, 
                                   size_t row_stride);
 jxg_status jxg_receive(void* ctx, jxg_buffer* out);
 jxg_status jxg_pending(void* ctx, uint32_t* n);
-/* lanes of the streaming pipeline for frames of this size (world == 1) or for
- * this rank's shard of them (jxg_shard_submit_device) */
+/* frames the streaming pipeline keeps in flight for frames of this size
+ * (world == 1) or for this rank's shard of them (jxg_shard_submit_device):
+ * lanes x frames per lane (one batched launch per lane), less what keeps a
+ * lane free for the next submit -- (lanes - 1) x batch + 1 */
 jxg_status jxg_pipeline_depth(void* ctx, uint32_t xsize, uint32_t ysize, uint32_t rank,
                               uint32_t world, uint32_t* depth);
 jxg_status jxg_get_stats(void* ctx, jxg_stats* stats);

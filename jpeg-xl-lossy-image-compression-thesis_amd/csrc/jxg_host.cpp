@@ -3071,7 +3071,11 @@ jxg_status jxg_pipeline_depth(void* ctx, uint32_t xsize, uint32_t ysize, uint32_
     return JXG_ERR_INVALID_ARG;
   const Ctx* c = static_cast<Ctx*>(ctx);
   const Frame f = make_frame(xsize, ysize, c->params.distance);
-  *depth = pipe_shape(world > 1 ? make_plan(f, rank, world).ng() : f.ngroups).frames();
+  // frames that may be pending with a submit always accepted: a lane is
+  // free while the unwritten frames fill at most lanes - 1 batches (written
+  // oldest first, so only the oldest batch is partly written)
+  const PipeShape sh = pipe_shape(world > 1 ? make_plan(f, rank, world).ng() : f.ngroups);
+  *depth = (sh.lanes - 1) * sh.batch + 1;
   return JXG_OK;
 }
 
