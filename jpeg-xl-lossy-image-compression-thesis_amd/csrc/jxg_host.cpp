@@ -1805,15 +1805,22 @@ static uint32_t hw_queues() {
   const long q = e && *e ? std::strtol(e, nullptr, 10) : 4;
   return (uint32_t)std::min<long>(32, std::max<long>(1, q));
 }
-// lanes and frames per lane (batch) for a frame / shard of `ngroups` groups
+// lanes and frames per lane (batch) for a frame / shard of `ngroups` pass
+// groups and `ntiles` 64x64 tiles.  Batches only for frames whose front end
+// does not fill the chip (< kPipeBatchTiles tiles: 1080p 510 -> 4 frames):
+// a frame that fills it gains nothing from sharing a launch and its lane's
+// latency grows with every frame in the batch (4K in batches of 3: 8.1 ->
+// 4.8 GPix/s, profiles/r04h).
+constexpr uint32_t kPipeBatchTiles = 2048;
 struct PipeShape {
   uint32_t lanes, batch;
   uint32_t frames() const { return lanes * batch; }
 };
-static PipeShape pipe_shape(uint32_t ngroups) {
+static PipeShape pipe_shape(uint32_t ngroups, uint32_t ntiles) {
   const uint32_t want = (kPipeChainGroups + ngroups - 1) / std::max(1u, ngroups);  // frames
   const uint32_t lmax = std::max(2u, std::min(kPipeMaxLanes, hw_queues() - 1));
-  const uint32_t k = std::min(kMaxBatch, std::max(1u, (want + lmax - 1) / lmax));
+  const uint32_t kt = std::min(kMaxBatch, std::max(1u, kPipeBatchTiles / std::max(1u, ntiles)));
+  const uint32_t k = std::min(kt, std::max(1u, (want + lmax - 1) / lmax));
   const uint32_t lanes = std::min(lmax, std::max(std::min(kPipeMinLanes, lmax), (want + k - 1) / k));
   return PipeShape{lanes, k};
 }
@@ -2187,7 +2194,7 @@ static jxg_status pipe_submit(Ctx* c, const uint8_t* src, bool on_device, uint32
   const int mode = shard ? 2 : 1;
   if (pipe_busy(c) && p.mode != mode) return JXG_ERR_INVALID_ARG;  // one kind at a time
   const Frame f0 = make_frame(w, h, c->params.distance);
-  uint32_t ngroups = f0.ngroups;
+  uint32_t ngroups = f0.ngroups, ntiles = f0.tiles_x * f0.tiles_y;
   if (shard) {
     if (world < 1 || rank >= world || f0.ngroups < world || (world > 1 && f0.ngroups < 2))
       return JXG_ERR_INVALID_ARG;
@@ -2198,8 +2205,9 @@ static jxg_status pipe_submit(Ctx* c, const uint8_t* src, bool on_device, uint32
         (world > 1 && !(c->params.flags & JXG_FLAG_ANS)))
       return JXG_ERR_UNSUPPORTED;
     ngroups = P.ng();
+    if (!P.tiles.empty()) ntiles = (uint32_t)P.tiles.size();
   }
-  const PipeShape shape = pipe_shape(ngroups);
+  const PipeShape shape = pipe_shape(ngroups, ntiles);
   jxg_status st = ensure_lanes(c, shape.lanes - 1);
   if (st) return st;
   const Clock::time_point t0 = Clock::now();
@@ -3074,7 +3082,9 @@ jxg_status jxg_pipeline_depth(void* ctx, uint32_t xsize, uint32_t ysize, uint32_
   // frames that may be pending with a submit always accepted: a lane is
   // free while the unwritten frames fill at most lanes - 1 batches (written
   // oldest first, so only the oldest batch is partly written)
-  const PipeShape sh = pipe_shape(world > 1 ? make_plan(f, rank, world).ng() : f.ngroups);
+  const Plan P = make_plan(f, rank, world);
+  const uint32_t nt = P.tiles.empty() ? f.tiles_x * f.tiles_y : (uint32_t)P.tiles.size();
+  const PipeShape sh = pipe_shape(world > 1 ? P.ng() : f.ngroups, nt);
   *depth = (sh.lanes - 1) * sh.batch + 1;
   return JXG_OK;
 }
