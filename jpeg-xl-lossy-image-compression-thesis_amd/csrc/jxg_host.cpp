@@ -1811,7 +1811,10 @@ static uint32_t hw_queues() {
 // a frame that fills it gains nothing from sharing a launch and its lane's
 // latency grows with every frame in the batch (4K in batches of 3: 8.1 ->
 // 4.8 GPix/s, profiles/r04h).
-constexpr uint32_t kPipeBatchTiles = 2048;
+#ifndef JXG_PIPE_BATCH_TILES  // (experiment builds override it: tools/build_variant.sh)
+#define JXG_PIPE_BATCH_TILES 2048
+#endif
+constexpr uint32_t kPipeBatchTiles = JXG_PIPE_BATCH_TILES;
 struct PipeShape {
   uint32_t lanes, batch;
   uint32_t frames() const { return lanes * batch; }

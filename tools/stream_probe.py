@@ -67,12 +67,19 @@ if a.mode == "plain":
 else:
     buf = np.zeros(w * h * 2 + (1 << 20), dtype=np.uint8)
 
+    ttake = [0.0, 0.0]  # seconds in next_head, in write_next
+
     def take():
+        t = time.perf_counter()
         heads = [e.shard_next_head() for e in encs]
+        t1 = time.perf_counter()
         for e in encs:
-            ok, t = e.shard_write_next(heads, buf.ctypes.data, buf.size)
-        sizes.append(t)
-        stamps.append(time.perf_counter())
+            ok, tot = e.shard_write_next(heads, buf.ctypes.data, buf.size)
+        t2 = time.perf_counter()
+        ttake[0] += t1 - t
+        ttake[1] += t2 - t1
+        sizes.append(tot)
+        stamps.append(t2)
 
     def run(n):
         for k in range(n):
@@ -87,6 +94,8 @@ run(a.warmup)
 torch.cuda.synchronize()
 stamps.clear()
 tsub[0] = 0.0
+if a.mode == "host":
+    ttake[0] = ttake[1] = 0.0
 t0 = time.perf_counter()
 run(a.frames)
 torch.cuda.synchronize()
@@ -97,5 +106,8 @@ print("mode %s %dx%d world %d depth %d: %.3f ms/frame, %.1f MPix/s, bytes %d; in
       % (a.mode, w, h, W, depth, dt * 1e3 / a.frames, w * h * a.frames / dt / 1e6, sizes[-1],
          tsub[0] * 1e3 / a.frames, np.median(gaps), np.percentile(gaps, 90), gaps.max()),
       flush=True)
+if a.mode == "host":
+    print("  in next_head %.3f ms/frame, in write_next %.3f ms/frame"
+          % (ttake[0] * 1e3 / a.frames, ttake[1] * 1e3 / a.frames), flush=True)
 for e in encs:
     e.close()
