@@ -1794,6 +1794,9 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
 // its own hardware queue (GPU_MAX_HW_QUEUES > lanes, bench.py sets 16).
 // ---------------------------------------------------------------------------
 constexpr uint32_t kPipeMaxLanes = 12, kPipeMinLanes = 4, kPipeChainGroups = 3570;
+#ifndef JXG_PIPE_LAG_JOIN
+#define JXG_PIPE_LAG_JOIN 0
+#endif
 // Hardware queues of this process (GPU_MAX_HW_QUEUES as HIP read it at start
 // up; HIP's default is 4).  Lanes beyond queues - 1 (one is left for the
 // caller's own stream) would share a queue with another lane and serialise
@@ -2285,6 +2288,20 @@ static jxg_status pipe_submit(Ctx* c, const uint8_t* src, bool on_device, uint32
   p.inflight.push_back(std::move(fr));
   p.submitted++;
   if (B.frames.size() >= shape.batch && (st = pipe_launch_open(c))) return fail(st);
+#if JXG_PIPE_LAG_JOIN
+  // (experiment) pace the submitting thread: wait for the codes of the frame
+  // JXG_PIPE_LAG_JOIN batches back
+  {
+    size_t i = p.inflight.size();
+    uint32_t nb = 0;
+    while (i > 0 && nb <= JXG_PIPE_LAG_JOIN) {
+      i--;
+      if (i + 1 < p.inflight.size() && p.inflight[i]->batch != p.inflight[i + 1]->batch) nb++;
+    }
+    if (nb > JXG_PIPE_LAG_JOIN && p.inflight[i]->phase >= 1 && (st = pipe_join_codes(*p.inflight[i])))
+      return fail(st);
+  }
+#endif
   return JXG_OK;
 }
 

@@ -66,6 +66,8 @@ if a.mode == "plain":
             take()
 else:
     buf = np.zeros(w * h * 2 + (1 << 20), dtype=np.uint8)
+    # page-locked like ShardStream's shared buffer (the writes are DMA)
+    assert jxg.load().jxg_host_register(ctypes.c_void_p(buf.ctypes.data), buf.nbytes) == 0
 
     ttake = [0.0, 0.0]  # seconds in next_head, in write_next
 
