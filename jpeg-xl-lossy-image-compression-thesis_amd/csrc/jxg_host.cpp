@@ -325,6 +325,7 @@ struct Ctx {
   // whose work so far every device-input entry point orders itself after
   hipStream_t in_stream = nullptr;
   hipEvent_t ev_in = nullptr;
+  hipEvent_t ev_write = nullptr;  // jxg_shard_write_next: this slot's section copies
   bool owned_lane = false;  // a pipeline / batch lane of another context
   // a pipeline lane's extra slots: contexts with their own buffers that share
   // this context's stream (super-frames: k frames per batched launch)
@@ -1794,9 +1795,6 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
 // its own hardware queue (GPU_MAX_HW_QUEUES > lanes, bench.py sets 16).
 // ---------------------------------------------------------------------------
 constexpr uint32_t kPipeMaxLanes = 12, kPipeMinLanes = 4, kPipeChainGroups = 3570;
-#ifndef JXG_PIPE_LAG_JOIN
-#define JXG_PIPE_LAG_JOIN 0
-#endif
 // Hardware queues of this process (GPU_MAX_HW_QUEUES as HIP read it at start
 // up; HIP's default is 4).  Lanes beyond queues - 1 (one is left for the
 // caller's own stream) would share a queue with another lane and serialise
@@ -1959,6 +1957,7 @@ struct Pipe {
   int mode = 0;  // 1 whole frames, 2 shards (while any frame is pending)
   uint32_t depth = 0;  // frames in flight (lanes x batch)
   std::shared_ptr<PipeBatch> open;   // frames submitted, not yet launched
+  hipEvent_t write_ev = nullptr;     // the last jxg_shard_write_next's copies (in flight)
   std::unique_ptr<Helpers> helpers;  // created with the first helper task
   ~Pipe() {
     for (auto& d : done)
@@ -2288,20 +2287,17 @@ static jxg_status pipe_submit(Ctx* c, const uint8_t* src, bool on_device, uint32
   p.inflight.push_back(std::move(fr));
   p.submitted++;
   if (B.frames.size() >= shape.batch && (st = pipe_launch_open(c))) return fail(st);
-#if JXG_PIPE_LAG_JOIN
-  // (experiment) pace the submitting thread: wait for the codes of the frame
-  // JXG_PIPE_LAG_JOIN batches back
-  {
-    size_t i = p.inflight.size();
-    uint32_t nb = 0;
-    while (i > 0 && nb <= JXG_PIPE_LAG_JOIN) {
-      i--;
-      if (i + 1 < p.inflight.size() && p.inflight[i]->batch != p.inflight[i + 1]->batch) nb++;
+  // frames one per lane: this thread waits for the codes of frame j - lag
+  // (their emission launched), which paces the launches by the codes and
+  // rANS chains instead of filling every lane with transform work at once
+  // (8K: +4 %, profiles/r04j); batched small frames are paced by their lanes
+  if (shape.batch == 1) {
+    const size_t lag = ngroups >= 256 ? 1 : 3;
+    if (p.inflight.size() > lag) {
+      PipeFrame& fj = *p.inflight[p.inflight.size() - 1 - lag];
+      if (fj.phase >= 1 && (st = pipe_join_codes(fj))) return fail(st);
     }
-    if (nb > JXG_PIPE_LAG_JOIN && p.inflight[i]->phase >= 1 && (st = pipe_join_codes(*p.inflight[i])))
-      return fail(st);
   }
-#endif
   return JXG_OK;
 }
 
@@ -2816,6 +2812,7 @@ void jxg_destroy(void* ctx) {
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   if (c->ev_in) (void)hipEventDestroy(c->ev_in);
+  if (c->ev_write) (void)hipEventDestroy(c->ev_write);
   if (c->stream && !c->shared_stream) (void)hipStreamDestroy(c->stream);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
   delete c;
@@ -3145,9 +3142,30 @@ jxg_status jxg_shard_write_next(void* ctx, const uint32_t* const* heads, const s
   PipeFrame* fr = nullptr;
   jxg_status st = pipe_shard_oldest(c, &fr);
   if (st) return st;
-  st = shard_write_host(fr->lane, heads, head_words, n, static_cast<uint8_t*>(dst), dst_size, total);
+  Ctx* S = fr->lane;
+  // the copies are enqueued, not waited for: this call returns once the
+  // PREVIOUS frame's copies have landed (jxg_shard_write_flush: the last one's)
+  st = shard_write_host(S, heads, head_words, n, static_cast<uint8_t*>(dst), dst_size, total, false);
   if (st) return st;  // (too small a buffer: the frame stays, *total tells the size)
-  c->pipe->ready.erase(c->pipe->ready.begin());  // its lane is free again
+  if (!S->ev_write && hipEventCreateWithFlags(&S->ev_write, hipEventDisableTiming) != hipSuccess)
+    return JXG_ERR_HIP;
+  JXG_HIP(hipEventRecord(S->ev_write, S->stream));
+  Pipe& p = *c->pipe;
+  hipEvent_t prev = p.write_ev;
+  p.write_ev = S->ev_write;
+  p.ready.erase(p.ready.begin());  // its slot is free again (later work queues behind the copies)
+  if (prev) JXG_HIP(hipEventSynchronize(prev));  // (the same slot twice: covers both)
+  return JXG_OK;
+}
+jxg_status jxg_shard_write_flush(void* ctx) {
+  if (!ctx) return JXG_ERR_INVALID_ARG;
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
+  if (c->pipe && c->pipe->write_ev) {
+    const hipEvent_t e = c->pipe->write_ev;
+    c->pipe->write_ev = nullptr;
+    JXG_HIP(hipEventSynchronize(e));
+  }
   return JXG_OK;
 }
 

@@ -88,6 +88,7 @@ EXPORTS = ("jxg_status_str", "jxg_create", "jxg_destroy", "jxg_encode_rgb8",
            "jxg_submit_rgb8", "jxg_submit_rgb8_device", "jxg_receive", "jxg_pending",
            "jxg_set_input_stream", "jxg_pipeline_depth", "jxg_shard_plan",
            "jxg_shard_submit_device", "jxg_shard_next_head", "jxg_shard_write_next",
+           "jxg_shard_write_flush",
 )
 
 _lib = None
@@ -149,6 +150,7 @@ def load():
                                             ctypes.c_uint32, ctypes.c_uint32]
     lib.jxg_shard_next_head.argtypes = [vp, vp, ctypes.POINTER(sz)]
     lib.jxg_shard_write_next.argtypes = lib.jxg_shard_write_host.argtypes
+    lib.jxg_shard_write_flush.argtypes = [vp]
     u32 = ctypes.c_uint32
     lib.jxg_host_register.argtypes = [vp, sz]
     lib.jxg_host_unregister.argtypes = [vp]
@@ -336,8 +338,14 @@ class Encoder:
     def shard_write_next(self, heads, dst_ptr: int, dst_size: int):
         """jxg_shard_write_host for the oldest pending shard frame, which is then
         released; returns (ok, total) -- ok False when dst_size < total (the
-        frame stays pending, nothing written)."""
+        frame stays pending, nothing written).  The copies are enqueued: the
+        PREVIOUS frame's are complete on return (:meth:`shard_write_flush`:
+        the last one's)."""
         return self._write(load().jxg_shard_write_next, heads, dst_ptr, dst_size)
+
+    def shard_write_flush(self):
+        """Wait for the last shard_write_next's copies."""
+        _check(load().jxg_shard_write_flush(self._ctx))
 
     def timings(self) -> tuple:
         """(ms_front_kernel, ms_host_call, ms_host_codes, ms_host_layout) of the

@@ -317,7 +317,8 @@ class ShardStream:
          reads the other ranks' heads there (a sequence word per rank and
          slot: spin until every rank has published frame k),
       3. DMAs its sections into frame k's codestream slot (rank 0 adds headers
-         + TOC) and marks frame k done.
+         + TOC) -- the copies run on while it goes on; it marks frame k done
+         once write_next of frame k + 1 (or a flush) has returned.
     Rank 0's :meth:`receive` returns a zero-copy view of frame k's codestream
     once every rank has marked it done (valid for the next S - 1 receives);
     other ranks get None.  All ranks must run on one node (the shared
@@ -351,6 +352,7 @@ class ShardStream:
         self.submitted = 0   # frames submitted
         self.written = 0     # frames whose sections this rank has written
         self.received = 0    # frames returned by receive()
+        self.unmarked = None  # the last frame written: its copies may be in flight (not done yet)
         self.totals = {}
         self.wait_s = 0.0    # seconds spent waiting for the other ranks (heads, slots, frames)
 
@@ -409,8 +411,18 @@ class ShardStream:
             raise RuntimeError("codestream of %d bytes over the %d-byte slot" % (total,
                                                                                self.slot_bytes))
         self.totals[k] = total
-        self.done[s, r] = k
+        # write_next returned once the previous frame's copies had landed
+        if self.unmarked is not None:
+            self.done[self.unmarked % self.slots, r] = self.unmarked
+        self.unmarked = k
         self.written += 1
+
+    def _mark(self):
+        """This rank's part of the last frame written is in place (flush)."""
+        if self.unmarked is not None:
+            self.enc.shard_write_flush()
+            self.done[self.unmarked % self.slots, self.rank] = self.unmarked
+            self.unmarked = None
 
     def receive(self):
         """The oldest frame not yet received: rank 0 gets a numpy view of its
@@ -420,6 +432,8 @@ class ShardStream:
             raise RuntimeError("ShardStream: nothing pending")
         while self.written <= k:
             self._write_one()
+        if self.unmarked is not None and self.unmarked <= k:
+            self._mark()
         self.received += 1
         total = self.totals.pop(k)
         if self.rank != 0:

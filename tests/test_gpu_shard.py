@@ -235,6 +235,8 @@ def streamed_shards(jxg_mod, ts, w, h, world, d=1.0, e=7, p=0, flags=None):
             ok, t = enc.shard_write_next(heads, buf.ctypes.data, buf.size)
             assert ok and (total is None or t == total)
             total = t
+        for enc in encs:  # write_next enqueues the copies: wait for them
+            enc.shard_write_flush()
         outs.append(buf[:total].tobytes())
 
     for t in ts:

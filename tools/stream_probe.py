@@ -100,6 +100,9 @@ if a.mode == "host":
     ttake[0] = ttake[1] = 0.0
 t0 = time.perf_counter()
 run(a.frames)
+if a.mode == "host":
+    for e in encs:
+        e.shard_write_flush()
 torch.cuda.synchronize()
 dt = time.perf_counter() - t0
 gaps = np.diff(np.array([t0] + stamps)) * 1e3
