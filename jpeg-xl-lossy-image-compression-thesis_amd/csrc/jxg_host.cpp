@@ -1819,6 +1819,11 @@ constexpr uint32_t kPipeBatchTiles = JXG_PIPE_BATCH_TILES;
 struct PipeShape {
   uint32_t lanes, batch;
   uint32_t frames() const { return lanes * batch; }
+  // shard frames that may be pending with the next submit always accepted:
+  // unwritten frames (written oldest first, so only the oldest batch is
+  // partly written) leave a lane free while they fill at most lanes - 1
+  // batches -- jxg_pipeline_depth
+  uint32_t pending() const { return (lanes - 1) * batch + 1; }
 };
 static PipeShape pipe_shape(uint32_t ngroups, uint32_t ntiles) {
   const uint32_t want = (kPipeChainGroups + ngroups - 1) / std::max(1u, ngroups);  // frames
@@ -2218,7 +2223,7 @@ static jxg_status pipe_submit(Ctx* c, const uint8_t* src, bool on_device, uint32
   const Clock::time_point t0 = Clock::now();
   // a shard frame holds its slot until its sections are written: the caller
   // must take one first (jxg_shard_next_head / jxg_shard_write_next)
-  if (shard && p.ready.size() >= shape.frames()) return JXG_ERR_INVALID_ARG;
+  if (shard && p.inflight.size() + p.ready.size() >= shape.pending()) return JXG_ERR_INVALID_ARG;
   p.mode = mode;
   p.depth = shape.frames();
   auto fail = [&](jxg_status e) {
@@ -3096,13 +3101,9 @@ jxg_status jxg_pipeline_depth(void* ctx, uint32_t xsize, uint32_t ysize, uint32_
     return JXG_ERR_INVALID_ARG;
   const Ctx* c = static_cast<Ctx*>(ctx);
   const Frame f = make_frame(xsize, ysize, c->params.distance);
-  // frames that may be pending with a submit always accepted: a lane is
-  // free while the unwritten frames fill at most lanes - 1 batches (written
-  // oldest first, so only the oldest batch is partly written)
   const Plan P = make_plan(f, rank, world);
   const uint32_t nt = P.tiles.empty() ? f.tiles_x * f.tiles_y : (uint32_t)P.tiles.size();
-  const PipeShape sh = pipe_shape(world > 1 ? P.ng() : f.ngroups, nt);
-  *depth = (sh.lanes - 1) * sh.batch + 1;
+  *depth = pipe_shape(world > 1 ? P.ng() : f.ngroups, nt).pending();
   return JXG_OK;
 }
 
