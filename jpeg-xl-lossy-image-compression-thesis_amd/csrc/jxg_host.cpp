@@ -1807,13 +1807,14 @@ static uint32_t hw_queues() {
   return (uint32_t)std::min<long>(32, std::max<long>(1, q));
 }
 // lanes and frames per lane (batch) for a frame / shard of `ngroups` pass
-// groups and `ntiles` 64x64 tiles.  Batches only for frames whose front end
-// does not fill the chip (< kPipeBatchTiles tiles: 1080p 510 -> 4 frames):
-// a frame that fills it gains nothing from sharing a launch and its lane's
-// latency grows with every frame in the batch (4K in batches of 3: 8.1 ->
-// 4.8 GPix/s, profiles/r04h).
+// groups and `ntiles` 64x64 tiles.  Batches only for frames of at most
+// kPipeBatchTiles tiles (1080p: 510, a rank's eighth of 8K: 1080): 4K in
+// batches of 3 fell from 8.1 to 4.8 GPix/s (profiles/r04h) -- a frame that
+// fills the chip gains nothing from sharing a launch and its lane's latency
+// grows with every frame in the batch; the 8K eighth gains 0.63 -> 0.56 ms
+// per frame, a quarter (2160 tiles) nothing (profiles/r04k).
 #ifndef JXG_PIPE_BATCH_TILES  // (experiment builds override it: tools/build_variant.sh)
-#define JXG_PIPE_BATCH_TILES 2048
+#define JXG_PIPE_BATCH_TILES 1280
 #endif
 constexpr uint32_t kPipeBatchTiles = JXG_PIPE_BATCH_TILES;
 struct PipeShape {
@@ -1828,7 +1829,7 @@ struct PipeShape {
 static PipeShape pipe_shape(uint32_t ngroups, uint32_t ntiles) {
   const uint32_t want = (kPipeChainGroups + ngroups - 1) / std::max(1u, ngroups);  // frames
   const uint32_t lmax = std::max(2u, std::min(kPipeMaxLanes, hw_queues() - 1));
-  const uint32_t kt = std::min(kMaxBatch, std::max(1u, kPipeBatchTiles / std::max(1u, ntiles)));
+  const uint32_t kt = ntiles <= kPipeBatchTiles ? kMaxBatch : 1u;
   const uint32_t k = std::min(kt, std::max(1u, (want + lmax - 1) / lmax));
   const uint32_t lanes = std::min(lmax, std::max(std::min(kPipeMinLanes, lmax), (want + k - 1) / k));
   return PipeShape{lanes, k};
