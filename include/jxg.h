@@ -261,10 +261,11 @@ jxg_status jxg_shard_write_host(void* ctx, const uint32_t* const* heads, const s
  *   jxg_shard_write_next: as jxg_shard_write_host for that frame (its
  *     sections D2H into the shared host buffer at their codestream offsets,
  *     rank 0 adds headers + TOC), then releases its slot.  The copies are
- *     enqueued and NOT waited for: the call returns once the PREVIOUS
- *     frame's copies have landed (this rank's part of frame k is in place
- *     when write_next of frame k + 1 returns, or after jxg_shard_write_flush);
- *   jxg_shard_write_flush: waits for the last write's copies.
+ *     enqueued and NOT waited for: the call returns once the copies of the
+ *     write JXG_SHARD_WRITE_LAG calls back have landed (this rank's part of
+ *     frame k is in place when write_next of frame k + JXG_SHARD_WRITE_LAG
+ *     returns, or after jxg_shard_write_flush);
+ *   jxg_shard_write_flush: waits for every write's copies.
  * A frame's codestream is complete once every rank's part is in place.  At
  * most jxg_pipeline_depth frames may be pending (submit returns
  * JXG_ERR_INVALID_ARG when full; JXG_ERR_UNSUPPORTED for a plan needing the
@@ -275,6 +276,7 @@ jxg_status jxg_shard_submit_device(void* ctx, const void* d_rgb, uint32_t xsize,
 jxg_status jxg_shard_next_head(void* ctx, uint32_t* dst, size_t* nwords);
 jxg_status jxg_shard_write_next(void* ctx, const uint32_t* const* heads, const size_t* head_words,
                                 uint32_t n, void* dst, size_t dst_size, size_t* total);
+#define JXG_SHARD_WRITE_LAG 2
 jxg_status jxg_shard_write_flush(void* ctx);
 /* page-lock a host range (e.g. the node-shared /dev/shm codestream buffer of
  * jxg_shard_write_host / jxg_shard_write_next) so the ranks' D2H copies are DMA */

@@ -1963,7 +1963,7 @@ struct Pipe {
   int mode = 0;  // 1 whole frames, 2 shards (while any frame is pending)
   uint32_t depth = 0;  // frames in flight (lanes x batch)
   std::shared_ptr<PipeBatch> open;   // frames submitted, not yet launched
-  hipEvent_t write_ev = nullptr;     // the last jxg_shard_write_next's copies (in flight)
+  std::deque<hipEvent_t> writes;    // jxg_shard_write_next copies in flight, oldest first
   std::unique_ptr<Helpers> helpers;  // created with the first helper task
   ~Pipe() {
     for (auto& d : done)
@@ -3153,21 +3153,32 @@ jxg_status jxg_shard_write_next(void* ctx, const uint32_t* const* heads, const s
     return JXG_ERR_HIP;
   JXG_HIP(hipEventRecord(S->ev_write, S->stream));
   Pipe& p = *c->pipe;
-  hipEvent_t prev = p.write_ev;
-  p.write_ev = S->ev_write;
   p.ready.erase(p.ready.begin());  // its slot is free again (later work queues behind the copies)
-  if (prev) JXG_HIP(hipEventSynchronize(prev));  // (the same slot twice: covers both)
+  // the copies of the write JXG_SHARD_WRITE_LAG calls back have landed on return
+  // (copy kernels queue behind the other lanes' kernels: waiting for the
+  // previous frame's held this thread ~0.27 ms per frame, profiles/r04l)
+  for (hipEvent_t& e : p.writes)
+    if (e == S->ev_write) {  // re-recorded below: covered by its new record
+      e = nullptr;
+    }
+  p.writes.push_back(S->ev_write);
+  while (p.writes.size() > JXG_SHARD_WRITE_LAG) {
+    const hipEvent_t e = p.writes.front();
+    p.writes.pop_front();
+    if (e) JXG_HIP(hipEventSynchronize(e));
+  }
   return JXG_OK;
 }
 jxg_status jxg_shard_write_flush(void* ctx) {
   if (!ctx) return JXG_ERR_INVALID_ARG;
   Ctx* c = static_cast<Ctx*>(ctx);
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
-  if (c->pipe && c->pipe->write_ev) {
-    const hipEvent_t e = c->pipe->write_ev;
-    c->pipe->write_ev = nullptr;
-    JXG_HIP(hipEventSynchronize(e));
-  }
+  if (c->pipe)
+    while (!c->pipe->writes.empty()) {
+      const hipEvent_t e = c->pipe->writes.front();
+      c->pipe->writes.pop_front();
+      if (e) JXG_HIP(hipEventSynchronize(e));
+    }
   return JXG_OK;
 }
 

@@ -130,6 +130,7 @@ class SharedHostBuffer:
 
 AC_CONTEXTS = 7425   # AC contexts of one HF preset (15 block contexts x 495)
 ANS_MAX_HISTS = 8    # histograms per preset (csrc/jxg_bitstream.h kAnsMaxHists)
+WRITE_LAG = 2        # include/jxg.h JXG_SHARD_WRITE_LAG
 ALPHA = 128
 
 
@@ -318,7 +319,7 @@ class ShardStream:
          slot: spin until every rank has published frame k),
       3. DMAs its sections into frame k's codestream slot (rank 0 adds headers
          + TOC) -- the copies run on while it goes on; it marks frame k done
-         once write_next of frame k + 1 (or a flush) has returned.
+         once write_next of frame k + WRITE_LAG (or a flush) has returned.
     Rank 0's :meth:`receive` returns a zero-copy view of frame k's codestream
     once every rank has marked it done (valid for the next S - 1 receives);
     other ranks get None.  All ranks must run on one node (the shared
@@ -326,7 +327,7 @@ class ShardStream:
     be ANS when world > 1 (jxg_shard_submit_device refuses otherwise)."""
 
     def __init__(self, enc: Encoder, width: int, height: int, rank: int, world: int,
-                 group=None, slots: int = 4, slot_bytes: int | None = None):
+                 group=None, slots: int = 6, slot_bytes: int | None = None):
         self.enc, self.w, self.h, self.rank, self.world = enc, width, height, rank, world
         self.depth = enc.pipeline_depth(width, height, rank, world)
         self.slots = slots
@@ -352,7 +353,7 @@ class ShardStream:
         self.submitted = 0   # frames submitted
         self.written = 0     # frames whose sections this rank has written
         self.received = 0    # frames returned by receive()
-        self.unmarked = None  # the last frame written: its copies may be in flight (not done yet)
+        self.unmarked = []   # frames written whose copies may be in flight (not done yet)
         self.totals = {}
         self.wait_s = 0.0    # seconds spent waiting for the other ranks (heads, slots, frames)
 
@@ -411,18 +412,21 @@ class ShardStream:
             raise RuntimeError("codestream of %d bytes over the %d-byte slot" % (total,
                                                                                self.slot_bytes))
         self.totals[k] = total
-        # write_next returned once the previous frame's copies had landed
-        if self.unmarked is not None:
-            self.done[self.unmarked % self.slots, r] = self.unmarked
-        self.unmarked = k
+        # write_next returned once the copies of the frame WRITE_LAG writes
+        # back had landed (include/jxg.h JXG_SHARD_WRITE_LAG)
+        self.unmarked.append(k)
+        while len(self.unmarked) > WRITE_LAG:
+            j = self.unmarked.pop(0)
+            self.done[j % self.slots, r] = j
         self.written += 1
 
     def _mark(self):
-        """This rank's part of the last frame written is in place (flush)."""
-        if self.unmarked is not None:
+        """This rank's parts of the frames written are in place (flush)."""
+        if self.unmarked:
             self.enc.shard_write_flush()
-            self.done[self.unmarked % self.slots, self.rank] = self.unmarked
-            self.unmarked = None
+            for j in self.unmarked:
+                self.done[j % self.slots, self.rank] = j
+            self.unmarked = []
 
     def receive(self):
         """The oldest frame not yet received: rank 0 gets a numpy view of its
@@ -432,7 +436,7 @@ class ShardStream:
             raise RuntimeError("ShardStream: nothing pending")
         while self.written <= k:
             self._write_one()
-        if self.unmarked is not None and self.unmarked <= k:
+        if self.unmarked and self.unmarked[0] <= k:
             self._mark()
         self.received += 1
         total = self.totals.pop(k)
