@@ -5,7 +5,10 @@ means and the derived figures DESIGN.md quotes:
   wait_frac       = SQ_WAIT_ANY / SQ_WAVE_CYCLES
   lds_bank_conflict_frac = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
   hbm_bytes_per_launch   = FETCH_SIZE x 2 (gfx950 half-count) + WRITE_SIZE, KiB -> B
-Usage: python3 tools/pmc_reduce.py PMC_DIR KERNEL_SUBSTR OUT_JSON [note]"""
+Usage: python3 tools/pmc_reduce.py PMC_DIR KERNEL_SUBSTR OUT_JSON [note]
+FIRST=N keeps the first N dispatches of each counter in each pass (the timed
+default-bench encodes; later dispatches of a run with side rows are other
+configurations, e.g. the filtered cjxl-defaults row)."""
 import csv
 import glob
 import json
@@ -15,12 +18,17 @@ from collections import defaultdict
 
 d, kern, out = sys.argv[1], sys.argv[2], sys.argv[3]
 note = sys.argv[4] if len(sys.argv) > 4 else ""
+first = int(os.environ.get("FIRST", "0"))
 vals = defaultdict(list)
 for p in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+    per = defaultdict(list)
     with open(p) as f:
         for r in csv.DictReader(f):
             if kern in r["Kernel_Name"]:
-                vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+                per[r["Counter_Name"]].append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
+    for k, v in per.items():
+        v.sort()
+        vals[k] += [x for _, x in (v[:first] if first else v)]
 m = {k: sum(v) / len(v) for k, v in vals.items()}
 res = {"kernel": kern, "workload": "8k", "note": note}
 res.update({k: m[k] for k in sorted(m)})
