@@ -72,7 +72,8 @@ import time
 # taken by torch's stream), and two lanes sharing a queue serialise their
 # kernels.  Must be set before HIP initialises (JXG_BENCH_HW_QUEUES overrides
 # it for experiments; at most 32).
-os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, int(os.environ.get("JXG_BENCH_HW_QUEUES", "16"))))
+HW_QUEUES = min(32, int(os.environ.get("JXG_BENCH_HW_QUEUES", "16")))
+os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "jpeg-xl-lossy-image-compression-thesis_amd"))
@@ -364,8 +365,12 @@ def main():
     # JXG_DIST_BACKEND=gloo rehearses the multi-rank path with host-staged
     # collectives (several ranks may then share one device)
     backend = os.environ.get("JXG_DIST_BACKEND", "nccl")
+    ranks_on_device = 1
     if backend == "gloo":
-        local = local % max(1, torch.cuda.device_count())
+        ndev = max(1, torch.cuda.device_count())
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", env_world or "1"))
+        ranks_on_device = (local_world + ndev - 1) // ndev
+        local = local % ndev
     dev = torch.device("cuda", local)
     if world > 1:
         torch.cuda.set_device(local)
@@ -426,8 +431,9 @@ def main():
         host = None
         bufs = {}
         if mode == "shard":
-            from jxg.dist import ShardStream
-            ss = ShardStream(encs[0], w, fh, rank, world)
+            from jxg.dist import ShardStream, shared_gpu_lanes
+            ss = ShardStream(encs[0], w, fh, rank, world,
+                             lanes=shared_gpu_lanes(ranks_on_device, HW_QUEUES))
         elif mode == "shard-sync" and args.assembly == "host":
             from jxg.dist import SharedHostBuffer
             if SharedHostBuffer.single_node():

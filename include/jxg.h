@@ -172,6 +172,12 @@ jxg_status jxg_pending(void* ctx, uint32_t* n);
  * lane free for the next submit -- (lanes - 1) x batch + 1 */
 jxg_status jxg_pipeline_depth(void* ctx, uint32_t xsize, uint32_t ysize, uint32_t rank,
                               uint32_t world, uint32_t* depth);
+/* at most `lanes` pipeline lanes (1..12; 0: the default, GPU_MAX_HW_QUEUES - 1)
+ * for this context's later streams -- for several contexts streaming on ONE
+ * GPU (ranks rehearsed on a shared device), which would otherwise put up to
+ * 12 lanes each on the same hardware queues.  JXG_ERR_INVALID_ARG while
+ * frames are pending.  jxg_pipeline_depth reflects the cap. */
+jxg_status jxg_set_pipeline_lanes(void* ctx, uint32_t lanes);
 jxg_status jxg_get_stats(void* ctx, jxg_stats* stats);
 void jxg_buffer_free(jxg_buffer* buf);
 

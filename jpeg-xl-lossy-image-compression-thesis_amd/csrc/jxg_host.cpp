@@ -32,6 +32,7 @@
 #include "jxg_bitstream.h"
 #include "jxg_device.h"
 #include "jxg_kernels.h"
+#include "jxg_payload.h"
 #include "jxg_tables.h"
 
 namespace jxg {
@@ -326,6 +327,7 @@ struct Ctx {
   hipStream_t in_stream = nullptr;
   hipEvent_t ev_in = nullptr;
   hipEvent_t ev_write = nullptr;  // jxg_shard_write_next: this slot's section copies
+  uint32_t lane_cap = 0;          // jxg_set_pipeline_lanes (0: the queues' limit)
   bool owned_lane = false;  // a pipeline / batch lane of another context
   // a pipeline lane's extra slots: contexts with their own buffers that share
   // this context's stream (super-frames: k frames per batched launch)
@@ -1826,9 +1828,11 @@ struct PipeShape {
   // batches -- jxg_pipeline_depth
   uint32_t pending() const { return (lanes - 1) * batch + 1; }
 };
-static PipeShape pipe_shape(uint32_t ngroups, uint32_t ntiles) {
+// (cap: jxg_set_pipeline_lanes, 0 = none)
+static PipeShape pipe_shape(uint32_t ngroups, uint32_t ntiles, uint32_t cap) {
   const uint32_t want = (kPipeChainGroups + ngroups - 1) / std::max(1u, ngroups);  // frames
-  const uint32_t lmax = std::max(2u, std::min(kPipeMaxLanes, hw_queues() - 1));
+  uint32_t lmax = std::max(2u, std::min(kPipeMaxLanes, hw_queues() - 1));
+  if (cap) lmax = std::min(lmax, cap);
   const uint32_t kt = ntiles <= kPipeBatchTiles ? kMaxBatch : 1u;
   const uint32_t k = std::min(kt, std::max(1u, (want + lmax - 1) / lmax));
   const uint32_t lanes = std::min(lmax, std::max(std::min(kPipeMinLanes, lmax), (want + k - 1) / k));
@@ -2044,7 +2048,6 @@ static void pipe_abort(Ctx* c) {
 // payload: "JXGS" | version | rank (| loop-filter code << 16) | world | xsize | ysize | nsections |
 //          nsections x (TOC index, bytes) [| version 2: the rank's HF preset]
 //          | section bytes back to back
-constexpr uint32_t kPayloadMagic = 0x5347584Au;  // "JXGS"
 // (sync false: the body may still be in flight on the context's stream; the
 // streaming path enqueues its D2H behind it -- shard_write_host -- so the head
 // goes out one GPU round trip earlier)
@@ -2218,7 +2221,7 @@ static jxg_status pipe_submit(Ctx* c, const uint8_t* src, bool on_device, uint32
     ngroups = P.ng();
     if (!P.tiles.empty()) ntiles = (uint32_t)P.tiles.size();
   }
-  const PipeShape shape = pipe_shape(ngroups, ntiles);
+  const PipeShape shape = pipe_shape(ngroups, ntiles, c->lane_cap);
   jxg_status st = ensure_lanes(c, shape.lanes - 1);
   if (st) return st;
   const Clock::time_point t0 = Clock::now();
@@ -2436,131 +2439,6 @@ static jxg_status shard_payload(Ctx* c, void* dst, bool on_device) {
   }
   JXG_HIP(hipStreamSynchronize(s));
   return JXG_OK;
-}
-
-// Parse payload heads (host copies) into the section table of the frame:
-// for each TOC index, (payload, byte offset inside it, size)
-struct SectionRef {
-  uint32_t payload;
-  uint64_t off;
-  uint32_t size;
-};
-// words of a payload head from its first words (avail of them; 0: malformed
-// or more words needed to tell -- version 2 needs 7 + 2 nsections + 1)
-static size_t head_words(const uint32_t* hw, size_t avail) {
-  if (avail < 7 || hw[0] != kPayloadMagic) return 0;
-  const size_t base = 7 + 2 * (size_t)hw[6];
-  if (hw[1] == 1) return base;
-  if (hw[1] != 2 || avail < base + 1) return 0;
-  return base + 1 + hw[base];
-}
-
-// HfGlobal of a frame sharded with one HF preset per rank (payload heads of
-// version 2): num_hf_presets = ranks, one context map over every preset's
-// contexts (rank r's clusters after those of ranks < r), every rank's ANS
-// histograms rebuilt from its clustered counts [ext HfGlobal / HfPass]
-static jxg_status build_hf_presets(const std::vector<std::vector<uint32_t>>& heads,
-                                   const Frame& f, BitWriter& hf) {
-  const uint32_t n = (uint32_t)heads.size();
-  const size_t cw = (kAcCtx + 3) / 4;
-  std::vector<uint8_t> ctxmap((size_t)n * kAcCtx);
-  std::vector<AnsTable> tables;
-  uint32_t off = 0;
-  for (uint32_t r = 0; r < n; r++) {
-    const std::vector<uint32_t>& hw = heads[r];
-    const size_t base = 7 + 2 * (size_t)hw[6];
-    if (hw[1] != 2 || hw.size() < base + 2) return JXG_ERR_INVALID_ARG;
-    const uint32_t B = hw[base], nh = hw[base + 1];
-    if (nh < 1 || nh > (uint32_t)kAnsMaxHists || B != 1 + cw + nh * kAlpha ||
-        hw.size() != base + 1 + B)
-      return JXG_ERR_INVALID_ARG;
-    const uint8_t* cm = reinterpret_cast<const uint8_t*>(hw.data() + base + 2);
-    for (int k = 0; k < kAcCtx; k++) {
-      if (cm[k] >= nh) return JXG_ERR_INVALID_ARG;
-      ctxmap[(size_t)r * kAcCtx + k] = (uint8_t)(off + cm[k]);
-    }
-    const uint32_t* cnt = hw.data() + base + 2 + cw;
-    for (uint32_t h = 0; h < nh; h++) tables.push_back(build_ans_table(cnt + (size_t)h * kAlpha));
-    off += nh;
-  }
-  if (off > 255 || n - 1 >= (1u << ceil_log2(f.ngroups))) return JXG_ERR_INVALID_ARG;
-  hf.put(1, 1);                            // DequantMatrices all_default
-  hf.put(ceil_log2(f.ngroups), n - 1);     // num_hf_presets - 1
-  write_u32_sel(hf, 2, 0, 0);              // used_orders = 0
-  write_ans_histograms(hf, ctxmap, (int)off, tables, kCfg420, nullptr);
-  return JXG_OK;
-}
-
-// hf: with version-2 heads, the generated HfGlobal (section 1 + nlf, whose
-// SectionRef then names payload n = "generated")
-static jxg_status parse_payload_heads(const std::vector<std::vector<uint32_t>>& heads,
-                                      const std::vector<size_t>& psizes, uint32_t* w,
-                                      uint32_t* h, std::vector<SectionRef>& secs,
-                                      std::vector<uint8_t>& hf, uint32_t* lf) {
-  const uint32_t n = (uint32_t)heads.size();
-  secs.clear();
-  hf.clear();
-  std::vector<bool> seen;
-  for (uint32_t i = 0; i < n; i++) {
-    const std::vector<uint32_t>& hw = heads[i];
-    if (hw.size() < 7 || hw[0] != kPayloadMagic || (hw[1] != 1 && hw[1] != 2) ||
-        hw[1] != heads[0][1] || hw[3] != n)
-      return JXG_ERR_INVALID_ARG;
-    if (i == 0) {
-      *w = hw[4];
-      *h = hw[5];
-      *lf = hw[2] >> 16;  // loop-filter code (shard_finish)
-    } else if (hw[4] != *w || hw[5] != *h || (hw[2] >> 16) != *lf) {
-      return JXG_ERR_INVALID_ARG;
-    }
-    const size_t hwords = head_words(hw.data(), hw.size());
-    if (!hwords || hw.size() != hwords) return JXG_ERR_INVALID_ARG;
-    uint64_t off = 4 * (uint64_t)hwords;  // the body follows the whole head
-    for (uint32_t k = 0; k < hw[6]; k++) {
-      const uint32_t id = hw[7 + 2 * k], sz = hw[8 + 2 * k];
-      if (off + sz > psizes[i]) return JXG_ERR_INVALID_ARG;
-      if (id >= secs.size()) {
-        secs.resize(id + 1, SectionRef{0, 0, 0});
-        seen.resize(id + 1, false);
-      }
-      if (seen[id]) return JXG_ERR_INVALID_ARG;  // section twice
-      seen[id] = true;
-      secs[id] = SectionRef{i, off, sz};
-      off += sz;
-    }
-  }
-  if (*w == 0 || *h == 0 || *lf > 7) return JXG_ERR_INVALID_ARG;
-  const Frame f = make_frame(*w, *h, 1.0f);
-  if (secs.size() != 2 + f.nlf + f.ngroups) return JXG_ERR_INVALID_ARG;
-  if (heads[0][1] == 2) {  // per-rank presets: HfGlobal from the heads
-    const uint32_t id = 1 + f.nlf;
-    if (seen[id]) return JXG_ERR_INVALID_ARG;
-    BitWriter bw;
-    const jxg_status st = build_hf_presets(heads, f, bw);
-    if (st) return st;
-    hf = bw.bytes();
-    secs[id] = SectionRef{n, 0, (uint32_t)hf.size()};
-    seen[id] = true;
-  }
-  for (size_t i = 0; i < secs.size(); i++)
-    if (!seen[i]) return JXG_ERR_INVALID_ARG;  // section missing
-  return JXG_OK;
-}
-
-static std::vector<uint32_t> read_head(const uint8_t* p, size_t size) {
-  if (size < 28) return {};
-  std::vector<uint32_t> hw(7);
-  std::memcpy(hw.data(), p, 28);
-  const size_t base = 7 + 2 * (size_t)hw[6];
-  if (hw[1] == 2 && size >= (base + 1) * 4) {  // version 2: the preset block's length
-    hw.resize(base + 1);
-    std::memcpy(hw.data(), p, (base + 1) * 4);
-  }
-  const size_t words = head_words(hw.data(), hw.size());
-  if (!words || size < words * 4) return {};
-  hw.resize(words);
-  std::memcpy(hw.data(), p, words * 4);
-  return hw;
 }
 
 // device-resident payloads (payload i at d_base + offsets[i]) -> codestream in
@@ -3104,7 +2982,15 @@ jxg_status jxg_pipeline_depth(void* ctx, uint32_t xsize, uint32_t ysize, uint32_
   const Frame f = make_frame(xsize, ysize, c->params.distance);
   const Plan P = make_plan(f, rank, world);
   const uint32_t nt = P.tiles.empty() ? f.tiles_x * f.tiles_y : (uint32_t)P.tiles.size();
-  *depth = pipe_shape(world > 1 ? P.ng() : f.ngroups, nt).pending();
+  *depth = pipe_shape(world > 1 ? P.ng() : f.ngroups, nt, c->lane_cap).pending();
+  return JXG_OK;
+}
+
+jxg_status jxg_set_pipeline_lanes(void* ctx, uint32_t lanes) {
+  if (!ctx || lanes > kPipeMaxLanes) return JXG_ERR_INVALID_ARG;
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (pipe_busy(c)) return JXG_ERR_INVALID_ARG;
+  c->lane_cap = lanes;
   return JXG_OK;
 }
 

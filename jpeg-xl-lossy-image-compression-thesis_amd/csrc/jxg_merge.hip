@@ -201,10 +201,13 @@ struct Pass {
 // chunk, so the workgroups resident on a CU at a time mostly run one shape's
 // code (the kernel is 53 KB of code; interleaved shapes, chunk 1, took 1.595
 // ms at 8K, chunk 64 1.545 ms: profiles/r02s4_merge_chunk) while a chunk's
-// tiles (64 x 48 KB) are still re-read from the XCD's L2 / the MALL.
+// tiles are still in the XCD's L2: chunk 32 (1.5 MB of XYB per XCD) fetches
+// 448 MB per 8K launch, chunk 64 650 MB (the nine shape passes no longer
+// find the tiles in L2), at the same merge-stage time (1.81 ms;
+// chunk 16: 435 MB, 1.84 ms -- profiles/r04p/merge_chunk).
 // (a shard's tiles come through a list: tile = list[index])
 #ifndef JXG_MERGE_CHUNK
-#define JXG_MERGE_CHUNK 64
+#define JXG_MERGE_CHUNK 32
 #endif
 __device__ __forceinline__ bool decode_wg(const MergeArgs& a, int& tile, int& si) {
   constexpr int T = JXG_MERGE_CHUNK;

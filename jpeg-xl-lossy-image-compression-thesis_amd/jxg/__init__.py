@@ -88,7 +88,7 @@ EXPORTS = ("jxg_status_str", "jxg_create", "jxg_destroy", "jxg_encode_rgb8",
            "jxg_submit_rgb8", "jxg_submit_rgb8_device", "jxg_receive", "jxg_pending",
            "jxg_set_input_stream", "jxg_pipeline_depth", "jxg_shard_plan",
            "jxg_shard_submit_device", "jxg_shard_next_head", "jxg_shard_write_next",
-           "jxg_shard_write_flush",
+           "jxg_shard_write_flush", "jxg_set_pipeline_lanes",
 )
 
 _lib = None
@@ -151,6 +151,7 @@ def load():
     lib.jxg_shard_next_head.argtypes = [vp, vp, ctypes.POINTER(sz)]
     lib.jxg_shard_write_next.argtypes = lib.jxg_shard_write_host.argtypes
     lib.jxg_shard_write_flush.argtypes = [vp]
+    lib.jxg_set_pipeline_lanes.argtypes = [vp, ctypes.c_uint32]
     u32 = ctypes.c_uint32
     lib.jxg_host_register.argtypes = [vp, sz]
     lib.jxg_host_unregister.argtypes = [vp]
@@ -312,6 +313,11 @@ class Encoder:
         n = ctypes.c_uint32()
         _check(load().jxg_pipeline_depth(self._ctx, width, height, rank, world, ctypes.byref(n)))
         return n.value
+
+    def set_pipeline_lanes(self, lanes: int) -> None:
+        """Cap this context's pipeline lanes (0: default) -- several contexts
+        streaming on one GPU share its hardware queues (include/jxg.h)."""
+        _check(load().jxg_set_pipeline_lanes(self._ctx, lanes))
 
     def set_input_stream(self, stream) -> None:
         """Order every later device-input call after the work submitted so far

@@ -305,6 +305,15 @@ def encode_sharded(enc: Encoder, d_rgb: torch.Tensor, width: int, height: int, r
                                      copy=copy)
 
 
+def shared_gpu_lanes(ranks_on_device: int, queues: int = 16) -> int | None:
+    """Lane cap for each of `ranks_on_device` ranks streaming on one GPU: the
+    process-wide hardware queues (GPU_MAX_HW_QUEUES, bench.py 16) less one,
+    split between them (None: a rank has its GPU to itself)."""
+    if ranks_on_device <= 1:
+        return None
+    return max(1, (queues - 1) // ranks_on_device)
+
+
 class ShardStream:
     """Streaming group-sharded encode (jxg_shard_submit_device /
     jxg_shard_next_head / jxg_shard_write_next), the multi-GPU pipeline
@@ -324,11 +333,16 @@ class ShardStream:
     once every rank has marked it done (valid for the next S - 1 receives);
     other ranks get None.  All ranks must run on one node (the shared
     mapping); the partition must need no record exchange and the coder must
-    be ANS when world > 1 (jxg_shard_submit_device refuses otherwise)."""
+    be ANS when world > 1 (jxg_shard_submit_device refuses otherwise).
+    `lanes` caps the rank's pipeline lanes (jxg_set_pipeline_lanes): for
+    ranks sharing one GPU, :func:`shared_gpu_lanes`."""
 
     def __init__(self, enc: Encoder, width: int, height: int, rank: int, world: int,
-                 group=None, slots: int = 6, slot_bytes: int | None = None):
+                 group=None, slots: int = 6, slot_bytes: int | None = None,
+                 lanes: int | None = None):
         self.enc, self.w, self.h, self.rank, self.world = enc, width, height, rank, world
+        if lanes is not None:  # ranks sharing one GPU split its hardware queues
+            enc.set_pipeline_lanes(lanes)
         self.depth = enc.pipeline_depth(width, height, rank, world)
         self.slots = slots
         self.hcap = _head_cap(width, height)

@@ -214,15 +214,19 @@ def test_sharded_8k_strong(jxg_mod, world):
 # streaming shards (jxg_shard_submit_device / next_head / write_next): the
 # multi-GPU pipeline, `world` contexts of one process playing the ranks
 # ---------------------------------------------------------------------------
-def streamed_shards(jxg_mod, ts, w, h, world, d=1.0, e=7, p=0, flags=None):
+def streamed_shards(jxg_mod, ts, w, h, world, d=1.0, e=7, p=0, flags=None, lanes=None):
     """Frames ts (device tensors) through `world` contexts' streaming shard
     pipelines; heads swapped in-process, sections written into one host
-    buffer per frame.  Returns the codestreams in order."""
+    buffer per frame.  Returns the codestreams in order.  lanes: each
+    context's lane cap (jxg_set_pipeline_lanes)."""
     import torch
 
     flags = jxg_mod.FLAG_ANS if flags is None else flags
     torch.cuda.synchronize()  # the frames are written (no input stream set)
     encs = [jxg_mod.Encoder(distance=d, effort=e, proposals=p, flags=flags) for _ in range(world)]
+    if lanes is not None:
+        for enc in encs:
+            enc.set_pipeline_lanes(lanes)
     depth = min(enc.pipeline_depth(w, h, r, world) for r, enc in enumerate(encs))
     outs = []
     buf = np.zeros(w * h * 2 + (1 << 20), dtype=np.uint8)
@@ -282,9 +286,39 @@ def test_stream_8k_over_8(jxg_mod):
     from jxg.synth import synth_rgb8_device
 
     ts = [synth_rgb8_device(7680, 4320, 0x4A584C02 + k) for k in range(3)]
-    got = streamed_shards(jxg_mod, ts, 7680, 4320, 8)
+    got = streamed_shards(jxg_mod, ts, 7680, 4320, 8, lanes=2)
     for k in (0, 2):
         assert got[k] == sharded_encode(jxg_mod, None, 8, flags=jxg_mod.FLAG_ANS, t=ts[k])
+
+
+def test_stream_shards_lane_cap(jxg_mod):
+    """jxg_set_pipeline_lanes (ranks sharing one GPU): the depth follows the
+    cap, (lanes - 1) x batch + 1; the bytes do not change with it; the cap
+    is refused while frames are pending and above 12 lanes."""
+    from jxg.dist import shared_gpu_lanes
+    from jxg.synth import synth_rgb8_device
+
+    assert shared_gpu_lanes(1) is None and shared_gpu_lanes(8) == 1 and shared_gpu_lanes(4) == 3
+    w, h, world = 4096, 512, 2
+    ts = [synth_rgb8_device(w, h, 0x4A60 + 7 * k) for k in range(7)]
+    ref = streamed_shards(jxg_mod, ts, w, h, world)
+    with jxg_mod.Encoder(flags=jxg_mod.FLAG_ANS) as enc:
+        full = enc.pipeline_depth(w, h, 0, world)
+        batch = (full - 1) // 11  # 12 lanes at the default 16 queues
+        for cap in (1, 2, 3):
+            enc.set_pipeline_lanes(cap)
+            assert enc.pipeline_depth(w, h, 0, world) == (cap - 1) * batch + 1
+        enc.set_pipeline_lanes(0)
+        assert enc.pipeline_depth(w, h, 0, world) == full
+        with pytest.raises(jxg_mod.JxgError, match="invalid"):
+            enc.set_pipeline_lanes(13)
+        enc.set_pipeline_lanes(2)
+        enc.shard_submit_device(ts[0].data_ptr(), w, h, 0, world)
+        with pytest.raises(jxg_mod.JxgError, match="invalid"):  # a frame is pending
+            enc.set_pipeline_lanes(3)
+        enc.shard_next_head()
+    for cap in (1, 2):
+        assert streamed_shards(jxg_mod, ts, w, h, world, lanes=cap) == ref
 
 
 def test_stream_shards_refusals(jxg_mod):

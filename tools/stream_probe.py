@@ -29,11 +29,18 @@ ap.add_argument("--frames", type=int, default=40)
 ap.add_argument("--warmup", type=int, default=16)
 ap.add_argument("--w", type=int, default=7680)
 ap.add_argument("--h", type=int, default=4320)
+ap.add_argument("--lanes", type=int, default=-1,
+                help="lane cap per context (-1: jxg.dist.shared_gpu_lanes(world), 0: none)")
 a = ap.parse_args()
 w, h, W = a.w, a.h, a.world
 ts = [synth_rgb8_device(w, h, 0x4A584C02 + 100 * k) for k in range(2)]
 torch.cuda.synchronize()
 encs = [jxg.Encoder(flags=jxg.FLAG_ANS) for _ in range(W)]
+if a.lanes < 0:
+    from jxg.dist import shared_gpu_lanes
+    a.lanes = shared_gpu_lanes(W, int(os.environ["GPU_MAX_HW_QUEUES"])) or 0
+for e in encs:
+    e.set_pipeline_lanes(a.lanes)
 depth = min(e.pipeline_depth(w, h, r, W) for r, e in enumerate(encs)) if a.mode == "host" \
     else encs[0].pipeline_depth(w, h)
 stamps = []
@@ -106,9 +113,9 @@ if a.mode == "host":
 torch.cuda.synchronize()
 dt = time.perf_counter() - t0
 gaps = np.diff(np.array([t0] + stamps)) * 1e3
-print("mode %s %dx%d world %d depth %d: %.3f ms/frame, %.1f MPix/s, bytes %d; in submit "
+print("mode %s %dx%d world %d lanes cap %d depth %d: %.3f ms/frame, %.1f MPix/s, bytes %d; in submit "
       "%.3f ms/frame; receive gaps ms p50 %.3f p90 %.3f max %.3f"
-      % (a.mode, w, h, W, depth, dt * 1e3 / a.frames, w * h * a.frames / dt / 1e6, sizes[-1],
+      % (a.mode, w, h, W, a.lanes, depth, dt * 1e3 / a.frames, w * h * a.frames / dt / 1e6, sizes[-1],
          tsub[0] * 1e3 / a.frames, np.median(gaps), np.percentile(gaps, 90), gaps.max()),
       flush=True)
 if a.mode == "host":
