@@ -308,10 +308,12 @@ def encode_sharded(enc: Encoder, d_rgb: torch.Tensor, width: int, height: int, r
 def shared_gpu_lanes(ranks_on_device: int, queues: int = 16) -> int | None:
     """Lane cap for each of `ranks_on_device` ranks streaming on one GPU: the
     process-wide hardware queues (GPU_MAX_HW_QUEUES, bench.py 16) less one,
-    split between them (None: a rank has its GPU to itself)."""
+    split between them, at least two (one lane per rank serialises its frames:
+    8 contexts 0.69 GPix/s at 1 lane, 3.9 at 2, 4.0 at 3, profiles/r04q);
+    None: a rank has its GPU to itself."""
     if ranks_on_device <= 1:
         return None
-    return max(1, (queues - 1) // ranks_on_device)
+    return max(2, (queues - 1) // ranks_on_device)
 
 
 class ShardStream:

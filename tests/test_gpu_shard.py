@@ -298,7 +298,7 @@ def test_stream_shards_lane_cap(jxg_mod):
     from jxg.dist import shared_gpu_lanes
     from jxg.synth import synth_rgb8_device
 
-    assert shared_gpu_lanes(1) is None and shared_gpu_lanes(8) == 1 and shared_gpu_lanes(4) == 3
+    assert shared_gpu_lanes(1) is None and shared_gpu_lanes(8) == 2 and shared_gpu_lanes(4) == 3
     w, h, world = 4096, 512, 2
     ts = [synth_rgb8_device(w, h, 0x4A60 + 7 * k) for k in range(7)]
     ref = streamed_shards(jxg_mod, ts, w, h, world)
