@@ -190,13 +190,6 @@ static void out_release(uint8_t* data) {
 }
 
 using Clock = std::chrono::steady_clock;
-#ifdef JXG_WRITE_PROFILE  // experiment builds: where a shard frame's host time goes
-static double g_wprof[8];  // write_host, write wait, next_head, join codes, wait_emission, concat
-static long g_wprof_n;
-#define WPROF_ADD(i, t0) (g_wprof[i] += ms_since(t0))
-#else
-#define WPROF_ADD(i, t0) ((void)0)
-#endif
 static float ms_since(Clock::time_point t0) {
   return std::chrono::duration<float, std::milli>(Clock::now() - t0).count();
 }
@@ -2005,16 +1998,12 @@ static void pipe_abort(Ctx* c) {
 // goes out one GPU round trip earlier)
 static jxg_status shard_finish(Ctx* c, Job& J, size_t* payload_bytes, bool sync = true) {
   hipStream_t s = c->stream;
-  const Clock::time_point te0 = Clock::now();
   jxg_status st0 = wait_emission(c, J);  // the emission's bit counts on the host
   if (st0) return st0;
-  WPROF_ADD(4, te0);
   std::vector<uint32_t> ids, sizes;
   size_t nbytes = 0;
   jxg_status st;
-  const Clock::time_point tc0 = Clock::now();
   if ((st = stage_concat(c, J, false, &ids, &sizes, nullptr, &nbytes))) return st;
-  WPROF_ADD(5, tc0);
   std::vector<uint32_t>& hw = c->payload_head;
   hw.assign(7 + 2 * ids.size(), 0);
   hw[0] = kPayloadMagic;
@@ -2105,12 +2094,10 @@ static jxg_status pipe_complete_oldest(Ctx* c) {
   PipeFrame& fr = *p.inflight.front();
   // every frame of its batch: the last codes launch the batch's emission
   // (the batch's frames are the oldest in flight, consecutive)
-  const Clock::time_point tj0 = Clock::now();
   for (size_t i = 0; i < p.inflight.size() && p.inflight[i]->batch == fr.batch; i++) {
     const jxg_status e = pipe_join_codes(*p.inflight[i]);
     if (!st) st = e;
   }
-  WPROF_ADD(3, tj0);
   if (fr.shard) {
     size_t bytes = 0;
     if (!st) st = shard_finish(fr.lane, fr.J, &bytes, false);
@@ -2651,16 +2638,6 @@ void jxg_destroy(void* ctx) {
 #ifdef JXG_MERGE_PROFILE
   dump_merge_profile();
 #endif
-#ifdef JXG_WRITE_PROFILE
-  if (!c->owned_lane && g_wprof_n) {
-    std::fprintf(stderr, "shard host ms per write (%ld): write_host %.4f wait %.4f | next_head %.4f = "
-                 "join %.4f + wait_emission %.4f + concat %.4f + ...\n", g_wprof_n,
-                 g_wprof[0] / g_wprof_n, g_wprof[1] / g_wprof_n, g_wprof[2] / g_wprof_n,
-                 g_wprof[3] / g_wprof_n, g_wprof[4] / g_wprof_n, g_wprof[5] / g_wprof_n);
-    for (double& x : g_wprof) x = 0;
-    g_wprof_n = 0;
-  }
-#endif
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   if (c->ev_in) (void)hipEventDestroy(c->ev_in);
@@ -2977,10 +2954,8 @@ jxg_status jxg_shard_next_head(void* ctx, uint32_t* dst, size_t* nwords) {
   Ctx* c = static_cast<Ctx*>(ctx);
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
   PipeFrame* fr = nullptr;
-  const Clock::time_point th0 = Clock::now();
   const jxg_status st = pipe_shard_oldest(c, &fr);
   if (st) return st;
-  WPROF_ADD(2, th0);
   const std::vector<uint32_t>& hw = fr->lane->payload_head;
   if (dst) {
     if (*nwords < hw.size()) return JXG_ERR_INVALID_ARG;
@@ -3003,10 +2978,8 @@ jxg_status jxg_shard_write_next(void* ctx, const uint32_t* const* heads, const s
   Ctx* S = fr->lane;
   // the copies are enqueued, not waited for: this call returns once the
   // PREVIOUS frame's copies have landed (jxg_shard_write_flush: the last one's)
-  const Clock::time_point tw0 = Clock::now();
   st = shard_write_host(S, heads, head_words, n, static_cast<uint8_t*>(dst), dst_size, total, false);
   if (st) return st;  // (too small a buffer: the frame stays, *total tells the size)
-  WPROF_ADD(0, tw0);
   if (!S->ev_write && hipEventCreateWithFlags(&S->ev_write, hipEventDisableTiming) != hipSuccess)
     return JXG_ERR_HIP;
   JXG_HIP(hipEventRecord(S->ev_write, S->stream));
@@ -3020,16 +2993,11 @@ jxg_status jxg_shard_write_next(void* ctx, const uint32_t* const* heads, const s
       e = nullptr;
     }
   p.writes.push_back(S->ev_write);
-  const Clock::time_point tw1 = Clock::now();
   while (p.writes.size() > JXG_SHARD_WRITE_LAG) {
     const hipEvent_t e = p.writes.front();
     p.writes.pop_front();
     if (e) JXG_HIP(hipEventSynchronize(e));
   }
-  WPROF_ADD(1, tw1);
-#ifdef JXG_WRITE_PROFILE
-  g_wprof_n++;
-#endif
   return JXG_OK;
 }
 jxg_status jxg_shard_write_flush(void* ctx) {

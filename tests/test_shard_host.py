@@ -252,3 +252,13 @@ def test_assemble_v2_presets(jxg_mod):
     for pl in bad:
         with pytest.raises(jxg_mod.JxgError):
             jxg_mod.shard_assemble(pl)
+
+
+def test_shared_gpu_lanes_split():
+    """Ranks rehearsed on one GPU split its hardware queues (GPU_MAX_HW_QUEUES
+    - 1), at least two lanes each; a rank alone on its GPU is not capped."""
+    from jxg.dist import shared_gpu_lanes
+
+    assert shared_gpu_lanes(1) is None and shared_gpu_lanes(0) is None
+    assert [shared_gpu_lanes(k) for k in (2, 3, 4, 5, 8, 16)] == [7, 5, 3, 3, 2, 2]
+    assert shared_gpu_lanes(2, queues=32) == 15
