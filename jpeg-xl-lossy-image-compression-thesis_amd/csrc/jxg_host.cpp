@@ -2629,11 +2629,12 @@ void jxg_destroy(void* ctx) {
     pipe_drop_done(*c->pipe);
     c->pipe.reset();
   }
-  c->lanes.clear();  // pipeline lanes (jxg_destroy each)
-  c->slots.clear();  // their extra slots (sharing this context's stream)
   (void)hipSetDevice(c->params.device);
+  // written shard frames' section copies may still read a slot's buffers
   (void)hipStreamSynchronize(c->stream);
   if (c->stream2) (void)hipStreamSynchronize(c->stream2);
+  c->lanes.clear();  // pipeline lanes (jxg_destroy each)
+  c->slots.clear();  // their extra slots (sharing this context's stream)
   if (!c->owned_lane) g_live_ctx--;
 #ifdef JXG_MERGE_PROFILE
   dump_merge_profile();
