@@ -992,8 +992,23 @@ static std::vector<A> gather(Job* const* js, uint32_t k, F f) {
   for (uint32_t i = 0; i < k; i++) v[i] = f(*js[i]);
   return v;
 }
+// a batched launch sizes its grid from frame 0 and indexes the argument
+// blocks by blockIdx.z: 1..kMaxBatch frames of one geometry and plan, one stream
+static bool batch_ok(Ctx* const* cs, Job* const* js, uint32_t k) {
+  if (k < 1 || k > kMaxBatch) return false;
+  const Job& A = *js[0];
+  for (uint32_t i = 1; i < k; i++) {
+    const Job& B = *js[i];
+    if (cs[i]->stream != cs[0]->stream || B.w != A.w || B.h != A.h || B.plan.rank != A.plan.rank ||
+        B.plan.world != A.plan.world || B.plan.tiles.size() != A.plan.tiles.size() ||
+        B.plan.ng() != A.plan.ng() || B.nchunks != A.nchunks || B.max_s != A.max_s || B.aq != A.aq)
+      return false;
+  }
+  return true;
+}
 // front end (+ masking quant field), merge stage, AC token statistics
 static jxg_status launch_transform(Ctx* const* cs, Job* const* js, uint32_t k) {
+  if (!batch_ok(cs, js, k)) return JXG_ERR_INTERNAL;
   hipStream_t s = cs[0]->stream;
   const Job& J = *js[0];
   const Frame& f = J.f;
@@ -1024,6 +1039,7 @@ static jxg_status launch_transform(Ctx* const* cs, Job* const* js, uint32_t k) {
 }
 // varblock lists, LF-stream histograms, and each frame's LF statistics download
 static jxg_status launch_lf_stats(Ctx* const* cs, Job* const* js, uint32_t k) {
+  if (!batch_ok(cs, js, k)) return JXG_ERR_INTERNAL;
   hipStream_t s = cs[0]->stream;
   const Job& J = *js[0];
   const auto va = gather<VbArgs>(js, k, [](Job& j) { return j.va; });
@@ -1305,6 +1321,7 @@ static void build_emit(Ctx* c, Job& J) {
 // placement and LF streams as one launch each, then each frame's bit counts
 // to the host
 static jxg_status launch_emit(Ctx* const* cs, Job* const* js, uint32_t k) {
+  if (!batch_ok(cs, js, k)) return JXG_ERR_INTERNAL;
   hipStream_t s = cs[0]->stream;
   const Job& J = *js[0];
   for (uint32_t i = 0; i < k; i++) build_emit(cs[i], *js[i]);
