@@ -6,9 +6,12 @@ metric), device-resident RGB8 in HBM -> complete .jxl bytes in host memory.
                   [--scaling strong|weak] [--coder prefix|ans] [--config C]
 
 One step = one full encode (front end + merge stage, token statistics, entropy
-codes, bit emission, assembly, D2H of the codestream).  The AC stream is
-ANS-coded by default (libjxl's e7 entropy coder; --coder prefix for prefix
-codes).  Single-GPU and replica steps go through the library's streaming entry
+codes, bit emission, assembly, D2H of the codestream).  The encode is the one
+the reference's harness gets from `cjxl IN OUT --distance=1 --effort=7`
+(docker_manager.rs:126-136): JXG_FLAGS_CJXL_DEFAULTS -- ANS, inverse
+Gaborish, EPF by distance, the masking quant field (--preset cjxl, the
+default); --preset plain is the unfiltered activity-AQ encode of rounds 1-4
+(reported beside it as `filters_off`).  --coder prefix swaps the AC coder.  Single-GPU and replica steps go through the library's streaming entry
 points (jxg_submit_rgb8_device / jxg_receive: a one-thread software pipeline
 inside the library in which the rANS chains of earlier frames run under the
 transform kernels of later ones); the timed region ends when the last
@@ -54,6 +57,10 @@ The JSON line also carries:
                   the encoder's stream) vs 8.0 TB/s; the design's own bytes
                   and the PMC-measured HBM traffic (profiles/) beside it;
   alt_coder    -- the same workload with the other AC entropy coder;
+  filters_off  -- (--preset cjxl) the unfiltered activity-AQ encode (the
+                  rounds 1-4 headline), same pipeline;
+  roofline_e4  -- the front kernel at effort 4 (DCT8 only: the literal fused
+                  XYB + DCT + quant of SURVEY §8(d)), a labelled secondary line;
   quality      -- decoded PSNR / bpp of a 1920x1080 crop of the bench frame and
                   of a 1920x1080 photographic-like frame (untimed);
   cpu_baseline -- the oracle/ C restatement with OpenMP on the host's cores
@@ -197,7 +204,7 @@ def cpu_threads():
     return max(1, min(n, q) if q else n)
 
 
-def cpu_baseline(img, distance, effort, proposals, coder, gpu_bytes, sweep=None):
+def cpu_baseline(img, distance, effort, proposals, coder, filters, gpu_bytes, sweep=None):
     """The oracle/ C restatement (libjxl/cjxl are absent on the box: probe in
     profiles/r02a/probe.txt) timed on the host with OpenMP over
     cpu_threads() threads, on the same frame and settings as the GPU line.
@@ -211,7 +218,7 @@ def cpu_baseline(img, distance, effort, proposals, coder, gpu_bytes, sweep=None)
     def timed(threads):
         n = oracle_ffi.set_threads(threads)
         t = time.perf_counter()
-        r = oracle_ffi.encode(img, distance, effort, proposals, coder)
+        r = oracle_ffi.encode(img, distance, effort, proposals, coder, filters)
         return n, time.perf_counter() - t, r
 
     n, dt, r = timed(cpu_threads())
@@ -219,8 +226,9 @@ def cpu_baseline(img, distance, effort, proposals, coder, gpu_bytes, sweep=None)
            "nproc": os.cpu_count(), "affinity": cpu_affinity(), "cgroup_quota_cpus": cpu_quota(),
            "sample": "one full %dx%d frame (the bench frame), oracle/ C restatement with OpenMP "
                      "on %d threads = the process's CPU affinity (%d) capped by its cgroup CPU "
-                     "quota (%s; nproc %s; libjxl/cjxl absent on the box), %.2f s"
-                     % (w, h, n, cpu_affinity(), cpu_quota(), os.cpu_count(), dt),
+                     "quota (%s; nproc %s; libjxl/cjxl absent on the box), same flags as the GPU "
+                     "line (oracle filters mask %d), %.2f s"
+                     % (w, h, n, cpu_affinity(), cpu_quota(), os.cpu_count(), filters, dt),
            "bytes_equal_gpu": gpu_bytes is not None and r.bytes == gpu_bytes}
     if sweep:
         # threads vs throughput (one frame each, same bytes)
@@ -339,9 +347,16 @@ def main():
     ap.add_argument("--alt-thesis", type=int, default=1,
                     help="also time the workload with the thesis proposals P+F "
                          "(reported under 'thesis_proposals'; 0 = off)")
-    ap.add_argument("--alt-cjxl", type=int, default=1,
-                    help="also time the workload with cjxl's VarDCT defaults (Gaborish, EPF, "
-                         "masking AQ; reported under 'cjxl_defaults'; 0 = off)")
+    ap.add_argument("--preset", choices=("cjxl", "plain"), default="cjxl",
+                    help="cjxl = JXG_FLAGS_CJXL_DEFAULTS (Gaborish + EPF + masking AQ: what "
+                         "`cjxl IN OUT --distance=1 --effort=7` encodes, the headline); plain = "
+                         "no restoration filters, activity AQ")
+    ap.add_argument("--alt-preset", "--alt-cjxl", dest="alt_preset", type=int, default=1,
+                    help="also time the other preset (reported under 'filters_off' or "
+                         "'cjxl_defaults'; 0 = off)")
+    ap.add_argument("--alt-e4", type=int, default=1,
+                    help="also report the effort-4 (DCT8-only) front kernel's roofline "
+                         "('roofline_e4'; 0 = off)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sweep", default="",
                     help="comma-separated OpenMP thread counts: also time the CPU baseline at "
@@ -404,24 +419,29 @@ def main():
         img = synth_rgb8_device(w, h, SEED_BASE + args.config, local).cpu().numpy()
     torch.cuda.synchronize()
 
-    def run(mode, coder, nstreams=1, proposals=None, pipe=True, extra_flags=0):
+    preset_flags = {"cjxl": jxg.FLAGS_CJXL_DEFAULTS & ~jxg.FLAG_ANS, "plain": 0}
+    pflags = preset_flags[args.preset]
+
+    def run(mode, coder, nstreams=1, proposals=None, pipe=True, extra_flags=None, effort=None):
         """Warm up, then time args.steps steps of `mode` ("frames": each rank
         encodes whole frames -- N = 1 / replicas; "shard": ShardStream;
         "shard-sync": encode_sharded)."""
         sharded = mode != "frames"
         per_step, d_imgs = make_frames(sharded)
         nd = len(d_imgs)
-        flags = (jxg.FLAG_ANS if coder == "ans" else 0) | extra_flags
+        flags = (jxg.FLAG_ANS if coder == "ans" else 0) | (
+            pflags if extra_flags is None else extra_flags)
         props = args.proposals if proposals is None else proposals
-        encs = [jxg.Encoder(distance=args.distance, effort=args.effort,
+        encs = [jxg.Encoder(distance=args.distance, effort=args.effort if effort is None else effort,
                             proposals=props, device=local, flags=flags)
                 for _ in range(nstreams)]
-        rec = {"front_ms": [], "host_ms": [], "sizes": [], "last": None}
+        rec = {"front_ms": [], "host_ms": [], "aq_ms": [], "sizes": [], "last": None}
 
         def took(e, k, out):
             t = e.timings()
             rec["front_ms"].append(t[0])
-            rec["host_ms"].append(t[1:])
+            rec["host_ms"].append(t[1:4])
+            rec["aq_ms"].append(t[4])
             rec["sizes"].append(len(out) if out is not None else 0)
             if k % nd == 0:
                 # shared-memory views (ShardStream) are recycled: keep a copy
@@ -485,7 +505,7 @@ def main():
             # which must not land in the timed region
             nw = max(args.warmup, 1) * per_step
             worker(e, range(max(nw, 16) if (pipe or ss is not None) else args.warmup * per_step))
-        for key in ("front_ms", "host_ms", "sizes"):
+        for key in ("front_ms", "host_ms", "aq_ms", "sizes"):
             rec[key] = []
         if ss is not None:
             ss.wait_s = 0.0
@@ -594,21 +614,31 @@ def main():
                   "ms_front_kernel": round(sum(T["front_ms"]) / len(T["front_ms"]), 4),
                   "bytes_per_frame": T["sizes"][-1],
                   "bpp": round(T["sizes"][-1] * 8.0 / (w * h), 4)}
-    cjxl = None
-    cjxl_flags = jxg.FLAG_GABORISH | jxg.FLAG_EPF | jxg.FLAG_AQ_MASKING
-    if mode == "frames" and args.alt_cjxl:
-        # the encode `cjxl IN OUT --distance=1 --effort=7` asks for: its VarDCT
-        # defaults (inverse Gaborish, EPF, the masking quant field) on the same
-        # workload and coder -- the headline line is the unfiltered encode
-        C = run("frames", args.coder, nstreams, pipe=pipeline, extra_flags=cjxl_flags)
-        cjxl = {"flags": "gaborish + epf + masking AQ (jxg_cjxl's defaults = cjxl's [ext])",
-                "value": round(px_step * args.steps / C["dt"] / 1e6, 2),
-                "ms_per_step": round(C["dt"] * 1e3 / args.steps, 3),
-                "bytes_per_frame": C["sizes"][-1],
-                "bpp": round(C["sizes"][-1] * 8.0 / (w * h), 4)}
+    alt_preset = None
+    other_preset = "plain" if args.preset == "cjxl" else "cjxl"
+    if mode == "frames" and args.alt_preset:
+        # the other preset on the same workload and coder: with the cjxl
+        # headline, the unfiltered activity-AQ encode of rounds 1-4
+        C = run("frames", args.coder, nstreams, pipe=pipeline,
+                extra_flags=preset_flags[other_preset])
+        alt_preset = {"preset": other_preset,
+                      "flags": ("gaborish + epf + masking AQ (JXG_FLAGS_CJXL_DEFAULTS)"
+                                if other_preset == "cjxl" else
+                                "no Gaborish, no EPF, activity AQ"),
+                      "value": round(px_step * args.steps / C["dt"] / 1e6, 2),
+                      "ms_per_step": round(C["dt"] * 1e3 / args.steps, 3),
+                      "bytes_per_frame": C["sizes"][-1],
+                      "bpp": round(C["sizes"][-1] * 8.0 / (w * h), 4)}
         if world == 1 and not args.no_quality:
-            cjxl["quality_natural"] = quality_natural(C["enc"])
+            alt_preset["quality_natural"] = quality_natural(C["enc"])
         C["enc"].close()
+    e4 = None
+    if mode == "frames" and args.alt_e4 and world == 1:
+        # the front kernel at effort 4 (DCT8 only, no merge stage): the fused
+        # XYB + DCT + quant of SURVEY §8(d) taken literally, one frame at a time
+        E = run("frames", args.coder, 1, pipe=False, effort=4)
+        E["enc"].close()
+        e4 = sum(E["front_ms"]) / len(E["front_ms"])
     if rank == 0:
         ms_step = dt * 1e3 / args.steps
         value = px_step * args.steps / dt / 1e6
@@ -622,12 +652,17 @@ def main():
             fb = front_bytes_survey(w, fh) / world  # this rank's share of the frame
         achieved = fb / (fms * 1e-3) / 1e9 if fms > 0 else 0.0
         coder_desc = "%s-coded" % args.coder
+        # PMC figures (profiles/front_pmc_<key>.json) are per preset
+        pmc_key = name + ("_cjxl" if args.preset == "cjxl" else "")
+        preset_desc = ("cjxl defaults (JXG_FLAGS_CJXL_DEFAULTS: Gaborish + EPF + masking AQ)"
+                       if args.preset == "cjxl" else "no filters, activity AQ")
         distinct = max(1, args.distinct) if per_step == 1 else per_step
         if mode != "frames":
             workload = ("%s: %dx%d RGB8 (synth_rgb8, %d distinct frames cycled), VarDCT d%g e%d, "
-                        "proposals=%d, %s, 256x256 groups sharded over %d ranks (%s scaling; "
+                        "%s, proposals=%d, %s, 256x256 groups sharded over %d ranks (%s scaling; "
                         "partition kind %d), %s"
-                        % (name, w, fh, distinct, args.distance, args.effort, args.proposals,
+                        % (name, w, fh, distinct, args.distance, args.effort, preset_desc,
+                           args.proposals,
                            coder_desc, world, args.scaling, jxg.shard_plan(w, fh, world)[2],
                            "streamed (jxg.dist.ShardStream, %d frames in flight per rank, heads "
                            "and sections through /dev/shm)" % R["depth"]
@@ -635,9 +670,10 @@ def main():
                            "one frame at a time (encode_sharded), %s assembly" % args.assembly))
             par = "group-shard%d" % world
         else:
-            workload = ("%s %dx%d RGB8 (synth_rgb8), VarDCT d%g e%d, proposals=%d, %s, "
+            workload = ("%s %dx%d RGB8 (synth_rgb8), VarDCT d%g e%d, %s, proposals=%d, %s, "
                         "%d frame(s) per step, %d distinct frames cycled, %s"
-                        % (name, w, h, args.distance, args.effort, args.proposals, coder_desc,
+                        % (name, w, h, args.distance, args.effort, preset_desc, args.proposals,
+                           coder_desc,
                            per_step, distinct, "streaming entry points (jxg_submit_rgb8_device / "
                            "jxg_receive, one host thread)" if pipeline else
                            "%d concurrent encoder stream(s) per rank" % nstreams))
@@ -674,17 +710,19 @@ def main():
             "roofline": {"kernel": "front_kernel", "bound": "hbm",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": load_pmc_traffic(name),
+                         "traffic": load_pmc_traffic(pmc_key),
                          "algorithmic_bytes": int(fb),
                          "bytes_per_px": SURVEY_BYTES_PER_PX,
                          "design_bytes": front_bytes_design(fw, fhh, args.effort),
                          "avg_ms": round(fms, 4),
+                         "aq_kernel_ms": round(sum(iso["aq_ms"]) / len(iso["aq_ms"]), 4)
+                         if iso else None,
                          # the kernel is VALU-bound (the six-candidate 8x8 search):
                          # its PMC VALU issue rate beside the HBM fraction
-                         "valu_issue_frac_pmc": load_front_valu(name),
+                         "valu_issue_frac_pmc": load_front_valu(pmc_key),
                          # the bound that applies: VALU issue (the HBM fraction
                          # cannot pass ~0.17 while the kernel runs at this floor)
-                         "valu_floor": load_front_valu_floor(name, fms),
+                         "valu_floor": load_front_valu_floor(pmc_key, fms),
                          "measured": ("one-at-a-time encodes of a whole frame (the kernel alone "
                                       "on the GPU, HIP events on its stream); in the timed run "
                                       "(sharing the GPU with rANS chains%s): %.4f ms"
@@ -698,7 +736,7 @@ def main():
                             "bound": "latency",
                             "avg_ms": round((iso["st"] if iso else st)["ms_front"] -
                                             (iso["st"] if iso else st)["ms_front_kernel"], 4),
-                            "valu_issue_frac_pmc": load_merge_pmc(name)},
+                            "valu_issue_frac_pmc": load_merge_pmc(pmc_key)},
         }
         if iso is not None and args.coder == "ans":
             # the rANS chain: one serial state recurrence per pass group (the
@@ -716,8 +754,18 @@ def main():
             res["alt_coder"] = alt
         if thesis is not None:
             res["thesis_proposals"] = thesis
-        if cjxl is not None:
-            res["cjxl_defaults"] = cjxl
+        if alt_preset is not None:
+            res["filters_off" if other_preset == "plain" else "cjxl_defaults"] = alt_preset
+        if e4 is not None:
+            fb4 = front_bytes_survey(w, h)
+            a4 = fb4 / (e4 * 1e-3) / 1e9
+            res["roofline_e4"] = {"kernel": "front_kernel (effort 4: XYB + DC/AQ + DCT8 + quant, "
+                                            "no 8x8 search, no merge stage)",
+                                  "bound": "hbm", "achieved": round(a4, 1), "peak": HBM_PEAK_GBS,
+                                  "unit": "GB/s", "frac": round(a4 / HBM_PEAK_GBS, 4),
+                                  "algorithmic_bytes": int(fb4), "avg_ms": round(e4, 4),
+                                  "measured": "one-at-a-time encodes at effort 4, HIP events on "
+                                              "the encoder's stream"}
         if replicas is not None:
             res["replicas"] = replicas
         if R.get("per_rank"):
@@ -731,6 +779,8 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(img, args.distance, args.effort, args.proposals,
                                                1 if args.coder == "ans" else 0,
+                                               jxg.ORACLE_FILTERS_CJXL_DEFAULTS
+                                               if args.preset == "cjxl" else 0,
                                                R["last"],
                                                [int(x) for x in args.cpu_sweep.split(",") if x])
         print(json.dumps(res), flush=True)

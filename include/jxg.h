@@ -73,6 +73,17 @@ typedef enum {
  * recalled, parity with libjxl unpinned; oracle/aq.c) instead of the
  * activity heuristic; one extra kernel per frame (csrc/jxg_aq.hip) */
 #define JXG_FLAG_AQ_MASKING 64u
+/* What `cjxl IN OUT --distance=D --effort=E` with no other flag encodes (the
+ * harness's argv, benchmark-jpegxl/src/docker_manager.rs:126-136): cjxl's
+ * VarDCT defaults [ext] -- ANS, Gaborish, EPF iterations by distance, the
+ * masking quant field.  jxg_cjxl starts from this set, INTEGRATION.md's
+ * execute_cjxl over the C ABI passes it, and bench.py's headline value is
+ * measured with it; the same (image, distance, effort, proposals) give the
+ * same bytes through either route (tests/test_gpu_cli.py). */
+#define JXG_FLAGS_CJXL_DEFAULTS (JXG_FLAG_ANS | JXG_FLAG_GABORISH | JXG_FLAG_EPF | JXG_FLAG_AQ_MASKING)
+
+/* opaque encoder context (one HIP device, its streams and buffers) */
+typedef struct jxg_ctx jxg_ctx;
 
 typedef struct {
   float distance;      /* cjxl --distance (butteraugli target), (0, 25] */
@@ -105,22 +116,24 @@ typedef struct {
   /* host wall clock of the whole call and of the host-side code/header work */
   float ms_host_call, ms_host_codes, ms_host_layout;
   /* device time of the fused front kernel alone (XYB + ACS + DCT + quant);
-   * ms_front also covers the merge stage */
+   * ms_front also covers the masking quant field and the merge stage */
   float ms_front_kernel;
+  /* device time of the masking quant field kernel (JXG_FLAG_AQ_MASKING; 0 otherwise) */
+  float ms_aq;
 } jxg_stats;
 
 const char* jxg_status_str(jxg_status s);
-jxg_status jxg_create(const jxg_params* params, void** ctx);
-void jxg_destroy(void* ctx);
+jxg_status jxg_create(const jxg_params* params, jxg_ctx** ctx);
+void jxg_destroy(jxg_ctx* ctx);
 /* the caller's stream (hipStream_t) that produces device inputs; NULL: none
  * (writes complete before each call) -- see the conventions above */
-jxg_status jxg_set_input_stream(void* ctx, void* stream);
+jxg_status jxg_set_input_stream(jxg_ctx* ctx, void* stream);
 
 /* host RGB8 (interleaved, row_stride bytes per row) -> codestream */
-jxg_status jxg_encode_rgb8(void* ctx, const uint8_t* rgb, uint32_t xsize, uint32_t ysize,
+jxg_status jxg_encode_rgb8(jxg_ctx* ctx, const uint8_t* rgb, uint32_t xsize, uint32_t ysize,
                            size_t row_stride, jxg_buffer* out);
 /* device-resident RGB8 (same layout, device pointer) -> codestream */
-jxg_status jxg_encode_rgb8_device(void* ctx, const void* d_rgb, uint32_t xsize,
+jxg_status jxg_encode_rgb8_device(jxg_ctx* ctx, const void* d_rgb, uint32_t xsize,
                                   uint32_t ysize, size_t row_stride, jxg_buffer* out);
 /* n frames of equal size (benchmark config 3: 64 x 1080p; the reference's
  * caller encodes every image at 10 distances x 5 efforts, benchmark.rs:
@@ -131,11 +144,11 @@ jxg_status jxg_encode_rgb8_device(void* ctx, const void* d_rgb, uint32_t xsize,
  * jxg_encode_rgb8 of that frame); on error every output is released.  The
  * context must have no streamed frames pending (JXG_ERR_INVALID_ARG
  * otherwise).  jxg_get_stats then describes the last frame. */
-jxg_status jxg_encode_batch_rgb8(void* ctx, const uint8_t* const* rgbs, uint32_t n,
+jxg_status jxg_encode_batch_rgb8(jxg_ctx* ctx, const uint8_t* const* rgbs, uint32_t n,
                                  uint32_t xsize, uint32_t ysize, size_t row_stride,
                                  jxg_buffer* outs);
 /* the same with device-resident frames */
-jxg_status jxg_encode_batch_rgb8_device(void* ctx, const void* const* d_rgbs, uint32_t n,
+jxg_status jxg_encode_batch_rgb8_device(jxg_ctx* ctx, const void* const* d_rgbs, uint32_t n,
                                         uint32_t xsize, uint32_t ysize, size_t row_stride,
                                         jxg_buffer* outs);
 /* Streaming encode, one host thread: frames are submitted in order and their
@@ -160,25 +173,25 @@ jxg_status jxg_encode_batch_rgb8_device(void* ctx, const void* const* d_rgbs, ui
  * its codestream is received; a host frame is copied into pinned staging
  * before jxg_submit_rgb8 returns.  jxg_get_stats after jxg_receive describes
  * the received frame.  On an error every frame in flight is dropped. */
-jxg_status jxg_submit_rgb8(void* ctx, const uint8_t* rgb, uint32_t xsize, uint32_t ysize,
+jxg_status jxg_submit_rgb8(jxg_ctx* ctx, const uint8_t* rgb, uint32_t xsize, uint32_t ysize,
                            size_t row_stride);
-jxg_status jxg_submit_rgb8_device(void* ctx, const void* d_rgb, uint32_t xsize, uint32_t ysize,
+jxg_status jxg_submit_rgb8_device(jxg_ctx* ctx, const void* d_rgb, uint32_t xsize, uint32_t ysize,
                                   size_t row_stride);
-jxg_status jxg_receive(void* ctx, jxg_buffer* out);
-jxg_status jxg_pending(void* ctx, uint32_t* n);
+jxg_status jxg_receive(jxg_ctx* ctx, jxg_buffer* out);
+jxg_status jxg_pending(jxg_ctx* ctx, uint32_t* n);
 /* frames the streaming pipeline keeps in flight for frames of this size
  * (world == 1) or for this rank's shard of them (jxg_shard_submit_device):
  * lanes x frames per lane (one batched launch per lane), less what keeps a
  * lane free for the next submit -- (lanes - 1) x batch + 1 */
-jxg_status jxg_pipeline_depth(void* ctx, uint32_t xsize, uint32_t ysize, uint32_t rank,
+jxg_status jxg_pipeline_depth(jxg_ctx* ctx, uint32_t xsize, uint32_t ysize, uint32_t rank,
                               uint32_t world, uint32_t* depth);
 /* at most `lanes` pipeline lanes (1..12; 0: the default, GPU_MAX_HW_QUEUES - 1)
  * for this context's later streams -- for several contexts streaming on ONE
  * GPU (ranks rehearsed on a shared device), which would otherwise put up to
  * 12 lanes each on the same hardware queues.  JXG_ERR_INVALID_ARG while
  * frames are pending.  jxg_pipeline_depth reflects the cap. */
-jxg_status jxg_set_pipeline_lanes(void* ctx, uint32_t lanes);
-jxg_status jxg_get_stats(void* ctx, jxg_stats* stats);
+jxg_status jxg_set_pipeline_lanes(jxg_ctx* ctx, uint32_t lanes);
+jxg_status jxg_get_stats(jxg_ctx* ctx, jxg_stats* stats);
 void jxg_buffer_free(jxg_buffer* buf);
 
 /* ---- multi-GPU group sharding (one context per rank) ----
@@ -230,13 +243,13 @@ jxg_status jxg_shard_plan(uint32_t xsize, uint32_t ysize, uint32_t world, uint32
                           uint32_t* lf_owner, int* kind);
 jxg_status jxg_shard_exchange(uint32_t xsize, uint32_t ysize, uint32_t world, uint32_t rank,
                               size_t* send_bytes /* [world] */, size_t* recv_bytes /* [world] */);
-jxg_status jxg_shard_begin(void* ctx, const void* d_rgb, uint32_t xsize, uint32_t ysize,
+jxg_status jxg_shard_begin(jxg_ctx* ctx, const void* d_rgb, uint32_t xsize, uint32_t ysize,
                            size_t row_stride, uint32_t rank, uint32_t world, uint32_t* d_hist,
                            void* d_xbuf);
-jxg_status jxg_shard_end(void* ctx, const uint32_t* d_hist, const void* d_xbuf,
+jxg_status jxg_shard_end(jxg_ctx* ctx, const uint32_t* d_hist, const void* d_xbuf,
                          size_t* payload_bytes);
-jxg_status jxg_shard_payload(void* ctx, void* dst, int dst_on_device);
-jxg_status jxg_shard_assemble_device(void* ctx, const void* d_payloads, const size_t* offsets,
+jxg_status jxg_shard_payload(jxg_ctx* ctx, void* dst, int dst_on_device);
+jxg_status jxg_shard_assemble_device(jxg_ctx* ctx, const void* d_payloads, const size_t* offsets,
                                      const size_t* sizes, uint32_t n, jxg_buffer* out);
 jxg_status jxg_shard_assemble(const uint8_t* const* payloads, const size_t* sizes, uint32_t n,
                               jxg_buffer* out);
@@ -252,8 +265,8 @@ jxg_status jxg_shard_assemble(const uint8_t* const* payloads, const size_t* size
  * bytes (also returned with JXG_ERR_INVALID_ARG when dst_size is too small).
  * Once every rank has returned (a barrier), dst[0, total) holds the
  * codestream, byte-identical to jxg_shard_assemble_device. */
-jxg_status jxg_shard_head(void* ctx, uint32_t* dst, size_t* nwords);
-jxg_status jxg_shard_write_host(void* ctx, const uint32_t* const* heads, const size_t* head_words,
+jxg_status jxg_shard_head(jxg_ctx* ctx, uint32_t* dst, size_t* nwords);
+jxg_status jxg_shard_write_host(jxg_ctx* ctx, const uint32_t* const* heads, const size_t* head_words,
                                 uint32_t n, void* dst, size_t dst_size, size_t* total);
 /* Streaming sharded encode (the multi-GPU pipeline; kinds 0 / 1 with ANS, or
  * world == 1): every rank submits its shard of consecutive frames, in the
@@ -277,13 +290,13 @@ jxg_status jxg_shard_write_host(void* ctx, const uint32_t* const* heads, const s
  * JXG_ERR_INVALID_ARG when full; JXG_ERR_UNSUPPORTED for a plan needing the
  * record exchange or, with world > 1, for prefix codes).  The frame's device
  * RGB8 must stay unchanged until its write. */
-jxg_status jxg_shard_submit_device(void* ctx, const void* d_rgb, uint32_t xsize, uint32_t ysize,
+jxg_status jxg_shard_submit_device(jxg_ctx* ctx, const void* d_rgb, uint32_t xsize, uint32_t ysize,
                                    size_t row_stride, uint32_t rank, uint32_t world);
-jxg_status jxg_shard_next_head(void* ctx, uint32_t* dst, size_t* nwords);
-jxg_status jxg_shard_write_next(void* ctx, const uint32_t* const* heads, const size_t* head_words,
+jxg_status jxg_shard_next_head(jxg_ctx* ctx, uint32_t* dst, size_t* nwords);
+jxg_status jxg_shard_write_next(jxg_ctx* ctx, const uint32_t* const* heads, const size_t* head_words,
                                 uint32_t n, void* dst, size_t dst_size, size_t* total);
 #define JXG_SHARD_WRITE_LAG 2
-jxg_status jxg_shard_write_flush(void* ctx);
+jxg_status jxg_shard_write_flush(jxg_ctx* ctx);
 /* page-lock a host range (e.g. the node-shared /dev/shm codestream buffer of
  * jxg_shard_write_host / jxg_shard_write_next) so the ranks' D2H copies are DMA */
 jxg_status jxg_host_register(void* ptr, size_t size);
@@ -292,7 +305,7 @@ jxg_status jxg_host_unregister(void* ptr);
 /* thesis selector alone over a host XYB frame [3][ysize][xsize] (xsize, ysize
  * multiples of 8): r3 = (r_h, r_v, r_d) per block, type = raw strategy
  * (combined.diff:183-235) */
-jxg_status jxg_homogeneity_map(void* ctx, const float* xyb, uint32_t xsize, uint32_t ysize,
+jxg_status jxg_homogeneity_map(jxg_ctx* ctx, const float* xyb, uint32_t xsize, uint32_t ysize,
                                float distance, uint32_t flags, float* r3, uint8_t* type);
 
 /* ---- decode-side quality: the harness's metrics on the GPU ----
@@ -312,10 +325,10 @@ typedef struct {
   double ssim;      /* NaN when not requested or the image is under 11x11 */
 } jxg_quality;
 
-jxg_status jxg_compare_rgb8(void* ctx, const uint8_t* orig, size_t orig_stride,
+jxg_status jxg_compare_rgb8(jxg_ctx* ctx, const uint8_t* orig, size_t orig_stride,
                             const uint8_t* comp, size_t comp_stride, uint32_t xsize,
                             uint32_t ysize, int want_ssim, jxg_quality* out);
-jxg_status jxg_compare_rgb8_device(void* ctx, const void* d_orig, size_t orig_stride,
+jxg_status jxg_compare_rgb8_device(jxg_ctx* ctx, const void* d_orig, size_t orig_stride,
                                    const void* d_comp, size_t comp_stride, uint32_t xsize,
                                    uint32_t ysize, int want_ssim, jxg_quality* out);
 
@@ -325,7 +338,7 @@ jxg_status jxg_compare_rgb8_device(void* ctx, const void* d_orig, size_t orig_st
  * hashes, seed 0x4A584C00 + config index), written into device memory
  * d_out (row_stride bytes per row) on the context's stream; returns when it
  * is complete.  Same bytes as jxg/synth.py synth_rgb8. */
-jxg_status jxg_synth_rgb8_device(void* ctx, void* d_out, uint32_t xsize, uint32_t ysize,
+jxg_status jxg_synth_rgb8_device(jxg_ctx* ctx, void* d_out, uint32_t xsize, uint32_t ysize,
                                  size_t row_stride, uint64_t seed);
 
 #ifdef __cplusplus

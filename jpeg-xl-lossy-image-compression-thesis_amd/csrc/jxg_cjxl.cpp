@@ -129,7 +129,7 @@ int main(int argc, char** argv) {
   // `cjxl IN OUT --distance=D --effort=E` with no other flag (the harness's
   // argv, docker_manager.rs:126-136) gets cjxl's VarDCT defaults [ext]: ANS,
   // Gaborish on, EPF iterations by distance, the masking quant field
-  jxg_params p{1.0f, 7, 0, 1, JXG_FLAG_ANS | JXG_FLAG_GABORISH | JXG_FLAG_EPF | JXG_FLAG_AQ_MASKING, 0};
+  jxg_params p{1.0f, 7, 0, 1, JXG_FLAGS_CJXL_DEFAULTS, 0};
   for (int i = 3; i < argc; i++) {
     const char* a = argv[i];
     if (!std::strncmp(a, "--distance=", 11) || !std::strncmp(a, "-d=", 3))
@@ -188,7 +188,7 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "%s: %s\n", argv[1], err.c_str());
     return 1;
   }
-  void* ctx = nullptr;
+  jxg_ctx* ctx = nullptr;
   jxg_status st = jxg_create(&p, &ctx);
   if (st != JXG_OK) {
     std::fprintf(stderr, "jxg_create: %s\n", jxg_status_str(st));

@@ -256,8 +256,9 @@ struct Ctx {
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;  // AC-block concat + D2H (stage_concat_split)
   // ev[6]: AC statistics downloaded (stage_download_ac); ev[7]: AC emission
-  // done and its bit counts on the host; ev[8]: AC block in host memory
-  hipEvent_t ev[9] = {};
+  // done and its bit counts on the host; ev[8]: AC block in host memory;
+  // ev[9]: masking quant field done (front kernel start)
+  hipEvent_t ev[10] = {};
   bool constants_ready = false;
   // device
   DevBuf<uint8_t> rgb, acs, qf, aqf;  // aqf: masking quant field (JXG_FLAG_AQ_MASKING)
@@ -340,7 +341,7 @@ struct Ctx {
   size_t payload_body = 0;             //   and body bytes (in `out`)
 };
 
-void CtxDeleter::operator()(Ctx* c) const { jxg_destroy(c); }
+void CtxDeleter::operator()(Ctx* c) const { jxg_destroy(reinterpret_cast<jxg_ctx*>(c)); }
 
 static std::mutex g_const_mu;  // device __constant__ tables are shared by all contexts
 // Live contexts of the process.  A HIP process has 4 hardware queues
@@ -1019,6 +1020,7 @@ static jxg_status launch_transform(Ctx* const* cs, Job* const* js, uint32_t k) {
     const auto q = gather<AqArgs>(js, k, [](Job& j) { return j.qa; });
     launch_aq(q.data(), k, ntiles, s);
   }
+  for (uint32_t i = 0; i < k; i++) JXG_HIP(hipEventRecord(cs[i]->ev[9], s));
   const auto fa = gather<FrontArgs>(js, k, [](Job& j) { return j.fa; });
   if (listed)
     launch_front_list(fa.data(), k, ntiles, s);
@@ -1707,7 +1709,8 @@ static void enc_stats(Ctx* c, Job& J, size_t out_bytes, float ms_layout, bool as
     S.homogeneity = J.homog ? c->m_homog.data() : nullptr;
   }
   S.ms_front = elapsed(c->ev[0], c->ev[1]);
-  S.ms_front_kernel = elapsed(c->ev[0], c->ev[5]);
+  S.ms_front_kernel = elapsed(c->ev[9], c->ev[5]);
+  S.ms_aq = elapsed(c->ev[0], c->ev[9]);
   S.ms_histogram = elapsed(c->ev[1], c->ev[2]);
   S.ms_emit = elapsed(c->ev[2], c->ev[3]);
   S.ms_assemble = assembled ? elapsed(c->ev[3], c->ev[4]) : 0.0f;
@@ -1769,7 +1772,7 @@ static jxg_status ctx_new_lane(const jxg_params& params, Ctx** out) {
   }
   for (auto& e : c->ev)
     if (hipEventCreate(&e) != hipSuccess) {
-      jxg_destroy(c);
+      jxg_destroy(reinterpret_cast<jxg_ctx*>(c));
       return JXG_ERR_HIP;
     }
   *out = c;
@@ -2060,7 +2063,8 @@ static void shard_frame_stats(PipeFrame& fr, size_t bytes) {
   S.num_groups = fr.J.f.ngroups;
   S.num_lf_groups = fr.J.f.nlf;
   S.bytes = bytes;
-  S.ms_front_kernel = elapsed(fr.lane->ev[0], fr.lane->ev[5]);
+  S.ms_front_kernel = elapsed(fr.lane->ev[9], fr.lane->ev[5]);
+  S.ms_aq = elapsed(fr.lane->ev[0], fr.lane->ev[9]);
   S.ms_front = elapsed(fr.lane->ev[0], fr.lane->ev[1]);
   S.ms_host_codes = fr.J.ms_codes;
   S.ms_host_call = ms_since(fr.t0);
@@ -2379,7 +2383,8 @@ static jxg_status shard_end(Ctx* c, const uint32_t* d_hist, const uint8_t* d_xbu
   c->stats.num_lf_groups = J.f.nlf;
   c->stats.bytes = *payload_bytes;
   c->stats.ms_front = elapsed(c->ev[0], c->ev[1]);
-  c->stats.ms_front_kernel = elapsed(c->ev[0], c->ev[5]);
+  c->stats.ms_front_kernel = elapsed(c->ev[9], c->ev[5]);
+  c->stats.ms_aq = elapsed(c->ev[0], c->ev[9]);
   c->stats.ms_total = elapsed(c->ev[0], c->ev[4]);
   c->stats.ms_host_call = ms_since(t_call);
   c->job.reset();
@@ -2619,7 +2624,7 @@ const char* jxg_status_str(jxg_status s) {
 }
 
 
-jxg_status jxg_create(const jxg_params* params, void** out) {
+jxg_status jxg_create(const jxg_params* params, jxg_ctx** out) {
   if (!params || !out) return JXG_ERR_INVALID_ARG;
   *out = nullptr;
   if (!(params->distance > 0.0f) || params->distance > 25.0f) return JXG_ERR_INVALID_ARG;
@@ -2634,13 +2639,13 @@ jxg_status jxg_create(const jxg_params* params, void** out) {
   if (st) return st;
   c->owned_lane = false;
   g_live_ctx++;
-  *out = c;
+  *out = reinterpret_cast<jxg_ctx*>(c);
   return JXG_OK;
 }
 
-void jxg_destroy(void* ctx) {
+void jxg_destroy(jxg_ctx* ctx) {
   if (!ctx) return;
-  Ctx* c = static_cast<Ctx*>(ctx);
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (c->pipe) {  // frames still in the pipeline (their lanes are released below)
     pipe_abort(c);
     pipe_drop_done(*c->pipe);
@@ -2665,12 +2670,12 @@ void jxg_destroy(void* ctx) {
   delete c;
 }
 
-jxg_status jxg_encode_rgb8_device(void* ctx, const void* d_rgb, uint32_t w, uint32_t h,
+jxg_status jxg_encode_rgb8_device(jxg_ctx* ctx, const void* d_rgb, uint32_t w, uint32_t h,
                                   size_t stride, jxg_buffer* out) {
   if (!ctx || !d_rgb || !out || w == 0 || h == 0 || w > (1u << 18) || h > (1u << 18) ||
       stride < (size_t)w * 3)
     return JXG_ERR_INVALID_ARG;
-  Ctx* c = static_cast<Ctx*>(ctx);
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
   const Clock::time_point t0 = Clock::now();
   out->data = nullptr;
   out->size = 0;
@@ -2681,13 +2686,13 @@ jxg_status jxg_encode_rgb8_device(void* ctx, const void* d_rgb, uint32_t w, uint
   return encode_device(c, static_cast<const uint8_t*>(d_rgb), w, h, stride, out, t0);
 }
 
-jxg_status jxg_encode_rgb8(void* ctx, const uint8_t* rgb, uint32_t w, uint32_t h, size_t stride,
+jxg_status jxg_encode_rgb8(jxg_ctx* ctx, const uint8_t* rgb, uint32_t w, uint32_t h, size_t stride,
                            jxg_buffer* out) {
   if (!ctx || !rgb || !out || w == 0 || h == 0 || w > (1u << 18) || h > (1u << 18) ||
       stride < (size_t)w * 3)
     return JXG_ERR_INVALID_ARG;
   const Clock::time_point t0 = Clock::now();
-  Ctx* c = static_cast<Ctx*>(ctx);
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
   if (pipe_busy(c)) return JXG_ERR_INVALID_ARG;  // c->rgb may be an in-flight lane's input
   const size_t bytes = stride * (h - 1) + (size_t)w * 3;
@@ -2729,19 +2734,19 @@ static jxg_status batch_encode(Ctx* c, const uint8_t* const* frames, bool on_dev
   return st;
 }
 
-jxg_status jxg_encode_batch_rgb8(void* ctx, const uint8_t* const* rgbs, uint32_t n, uint32_t w,
+jxg_status jxg_encode_batch_rgb8(jxg_ctx* ctx, const uint8_t* const* rgbs, uint32_t n, uint32_t w,
                                  uint32_t h, size_t stride, jxg_buffer* outs) {
   if (!ctx || !rgbs || !outs || w == 0 || h == 0 || w > (1u << 18) || h > (1u << 18) ||
       stride < (size_t)w * 3)
     return JXG_ERR_INVALID_ARG;
   for (uint32_t i = 0; i < n; i++)
     if (!rgbs[i]) return JXG_ERR_INVALID_ARG;
-  Ctx* c = static_cast<Ctx*>(ctx);
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
   return batch_encode(c, rgbs, false, n, w, h, stride, outs);
 }
 
-jxg_status jxg_encode_batch_rgb8_device(void* ctx, const void* const* d_rgbs, uint32_t n,
+jxg_status jxg_encode_batch_rgb8_device(jxg_ctx* ctx, const void* const* d_rgbs, uint32_t n,
                                         uint32_t w, uint32_t h, size_t stride,
                                         jxg_buffer* outs) {
   if (!ctx || !d_rgbs || !outs || w == 0 || h == 0 || w > (1u << 18) || h > (1u << 18) ||
@@ -2749,52 +2754,52 @@ jxg_status jxg_encode_batch_rgb8_device(void* ctx, const void* const* d_rgbs, ui
     return JXG_ERR_INVALID_ARG;
   for (uint32_t i = 0; i < n; i++)
     if (!d_rgbs[i]) return JXG_ERR_INVALID_ARG;
-  Ctx* c = static_cast<Ctx*>(ctx);
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
   return batch_encode(c, reinterpret_cast<const uint8_t* const*>(d_rgbs), true, n, w, h, stride,
                       outs);
 }
 
-jxg_status jxg_submit_rgb8_device(void* ctx, const void* d_rgb, uint32_t w, uint32_t h,
+jxg_status jxg_submit_rgb8_device(jxg_ctx* ctx, const void* d_rgb, uint32_t w, uint32_t h,
                                   size_t stride) {
   if (!ctx || !d_rgb || w == 0 || h == 0 || w > (1u << 18) || h > (1u << 18) ||
       stride < (size_t)w * 3)
     return JXG_ERR_INVALID_ARG;
-  Ctx* c = static_cast<Ctx*>(ctx);
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
   return pipe_submit(c, static_cast<const uint8_t*>(d_rgb), true, w, h, stride);
 }
 
-jxg_status jxg_submit_rgb8(void* ctx, const uint8_t* rgb, uint32_t w, uint32_t h, size_t stride) {
+jxg_status jxg_submit_rgb8(jxg_ctx* ctx, const uint8_t* rgb, uint32_t w, uint32_t h, size_t stride) {
   if (!ctx || !rgb || w == 0 || h == 0 || w > (1u << 18) || h > (1u << 18) ||
       stride < (size_t)w * 3)
     return JXG_ERR_INVALID_ARG;
-  Ctx* c = static_cast<Ctx*>(ctx);
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
   return pipe_submit(c, rgb, false, w, h, stride);
 }
 
-jxg_status jxg_receive(void* ctx, jxg_buffer* out) {
+jxg_status jxg_receive(jxg_ctx* ctx, jxg_buffer* out) {
   if (!ctx || !out) return JXG_ERR_INVALID_ARG;
   out->data = nullptr;
   out->size = 0;
-  Ctx* c = static_cast<Ctx*>(ctx);
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
   return pipe_receive(c, out);
 }
 
-jxg_status jxg_pending(void* ctx, uint32_t* n) {
+jxg_status jxg_pending(jxg_ctx* ctx, uint32_t* n) {
   if (!ctx || !n) return JXG_ERR_INVALID_ARG;
-  Ctx* c = static_cast<Ctx*>(ctx);
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
   *n = c->pipe ? (uint32_t)(c->pipe->inflight.size() + c->pipe->done.size() +
                             c->pipe->ready.size())
                : 0u;
   return JXG_OK;
 }
 
-jxg_status jxg_get_stats(void* ctx, jxg_stats* stats) {
+jxg_status jxg_get_stats(jxg_ctx* ctx, jxg_stats* stats) {
   if (!ctx || !stats) return JXG_ERR_INVALID_ARG;
-  *stats = static_cast<Ctx*>(ctx)->stats;
+  *stats = reinterpret_cast<Ctx*>(ctx)->stats;
   return JXG_OK;
 }
 
@@ -2835,42 +2840,42 @@ jxg_status jxg_shard_exchange(uint32_t xsize, uint32_t ysize, uint32_t world, ui
   return JXG_OK;
 }
 
-jxg_status jxg_shard_begin(void* ctx, const void* d_rgb, uint32_t w, uint32_t h, size_t stride,
+jxg_status jxg_shard_begin(jxg_ctx* ctx, const void* d_rgb, uint32_t w, uint32_t h, size_t stride,
                            uint32_t rank, uint32_t world, uint32_t* d_hist, void* d_xbuf) {
   if (!ctx || !d_rgb || !d_hist || !d_xbuf || w == 0 || h == 0 || w > (1u << 18) ||
       h > (1u << 18) || stride < (size_t)w * 3)
     return JXG_ERR_INVALID_ARG;
-  Ctx* c = static_cast<Ctx*>(ctx);
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
   if (pipe_busy(c)) return JXG_ERR_INVALID_ARG;
   return shard_begin(c, static_cast<const uint8_t*>(d_rgb), w, h, stride, rank, world, d_hist,
                      static_cast<uint8_t*>(d_xbuf));
 }
 
-jxg_status jxg_shard_end(void* ctx, const uint32_t* d_hist, const void* d_xbuf,
+jxg_status jxg_shard_end(jxg_ctx* ctx, const uint32_t* d_hist, const void* d_xbuf,
                          size_t* payload_bytes) {
   if (!ctx || !d_hist || !d_xbuf || !payload_bytes) return JXG_ERR_INVALID_ARG;
-  Ctx* c = static_cast<Ctx*>(ctx);
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
   *payload_bytes = 0;
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
   if (pipe_busy(c)) return JXG_ERR_INVALID_ARG;
   return shard_end(c, d_hist, static_cast<const uint8_t*>(d_xbuf), payload_bytes);
 }
 
-jxg_status jxg_shard_payload(void* ctx, void* dst, int dst_on_device) {
+jxg_status jxg_shard_payload(jxg_ctx* ctx, void* dst, int dst_on_device) {
   if (!ctx || !dst) return JXG_ERR_INVALID_ARG;
-  Ctx* c = static_cast<Ctx*>(ctx);
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
   if (pipe_busy(c)) return JXG_ERR_INVALID_ARG;
   return shard_payload(c, dst, dst_on_device != 0);
 }
 
-jxg_status jxg_shard_assemble_device(void* ctx, const void* d_payloads, const size_t* offsets,
+jxg_status jxg_shard_assemble_device(jxg_ctx* ctx, const void* d_payloads, const size_t* offsets,
                                      const size_t* sizes, uint32_t n, jxg_buffer* out) {
   if (!ctx || !d_payloads || !offsets || !sizes || !out || n == 0) return JXG_ERR_INVALID_ARG;
   for (uint32_t i = 0; i < n; i++)
     if (offsets[i] % 4) return JXG_ERR_INVALID_ARG;
-  Ctx* c = static_cast<Ctx*>(ctx);
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
   out->data = nullptr;
   out->size = 0;
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
@@ -2878,9 +2883,9 @@ jxg_status jxg_shard_assemble_device(void* ctx, const void* d_payloads, const si
   return shard_assemble_device(c, static_cast<const uint8_t*>(d_payloads), offsets, sizes, n, out);
 }
 
-jxg_status jxg_shard_head(void* ctx, uint32_t* dst, size_t* nwords) {
+jxg_status jxg_shard_head(jxg_ctx* ctx, uint32_t* dst, size_t* nwords) {
   if (!ctx || !nwords) return JXG_ERR_INVALID_ARG;
-  Ctx* c = static_cast<Ctx*>(ctx);
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
   const size_t n = c->payload_head.size();
   if (n == 0) return JXG_ERR_INVALID_ARG;
   if (dst) {
@@ -2891,11 +2896,11 @@ jxg_status jxg_shard_head(void* ctx, uint32_t* dst, size_t* nwords) {
   return JXG_OK;
 }
 
-jxg_status jxg_shard_write_host(void* ctx, const uint32_t* const* heads, const size_t* head_words,
+jxg_status jxg_shard_write_host(jxg_ctx* ctx, const uint32_t* const* heads, const size_t* head_words,
                                 uint32_t n, void* dst, size_t dst_size, size_t* total) {
   if (!ctx || !heads || !head_words || !total || n == 0) return JXG_ERR_INVALID_ARG;
   *total = 0;
-  Ctx* c = static_cast<Ctx*>(ctx);
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
   if (pipe_busy(c)) return JXG_ERR_INVALID_ARG;
   return shard_write_host(c, heads, head_words, n, static_cast<uint8_t*>(dst), dst_size, total);
@@ -2931,17 +2936,17 @@ jxg_status jxg_shard_plan(uint32_t xsize, uint32_t ysize, uint32_t world, uint32
   return JXG_OK;
 }
 
-jxg_status jxg_set_input_stream(void* ctx, void* stream) {
+jxg_status jxg_set_input_stream(jxg_ctx* ctx, void* stream) {
   if (!ctx) return JXG_ERR_INVALID_ARG;
-  static_cast<Ctx*>(ctx)->in_stream = static_cast<hipStream_t>(stream);
+  reinterpret_cast<Ctx*>(ctx)->in_stream = static_cast<hipStream_t>(stream);
   return JXG_OK;
 }
 
-jxg_status jxg_pipeline_depth(void* ctx, uint32_t xsize, uint32_t ysize, uint32_t rank,
+jxg_status jxg_pipeline_depth(jxg_ctx* ctx, uint32_t xsize, uint32_t ysize, uint32_t rank,
                               uint32_t world, uint32_t* depth) {
   if (!ctx || !depth || xsize == 0 || ysize == 0 || world == 0 || rank >= world)
     return JXG_ERR_INVALID_ARG;
-  const Ctx* c = static_cast<Ctx*>(ctx);
+  const Ctx* c = reinterpret_cast<Ctx*>(ctx);
   const Frame f = make_frame(xsize, ysize, c->params.distance);
   const Plan P = make_plan(f, rank, world);
   const uint32_t nt = P.tiles.empty() ? f.tiles_x * f.tiles_y : (uint32_t)P.tiles.size();
@@ -2949,27 +2954,27 @@ jxg_status jxg_pipeline_depth(void* ctx, uint32_t xsize, uint32_t ysize, uint32_
   return JXG_OK;
 }
 
-jxg_status jxg_set_pipeline_lanes(void* ctx, uint32_t lanes) {
+jxg_status jxg_set_pipeline_lanes(jxg_ctx* ctx, uint32_t lanes) {
   if (!ctx || lanes > kPipeMaxLanes) return JXG_ERR_INVALID_ARG;
-  Ctx* c = static_cast<Ctx*>(ctx);
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (pipe_busy(c)) return JXG_ERR_INVALID_ARG;
   c->lane_cap = lanes;
   return JXG_OK;
 }
 
-jxg_status jxg_shard_submit_device(void* ctx, const void* d_rgb, uint32_t w, uint32_t h,
+jxg_status jxg_shard_submit_device(jxg_ctx* ctx, const void* d_rgb, uint32_t w, uint32_t h,
                                    size_t stride, uint32_t rank, uint32_t world) {
   if (!ctx || !d_rgb || w == 0 || h == 0 || w > (1u << 18) || h > (1u << 18) ||
       stride < (size_t)w * 3)
     return JXG_ERR_INVALID_ARG;
-  Ctx* c = static_cast<Ctx*>(ctx);
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
   return pipe_submit(c, static_cast<const uint8_t*>(d_rgb), true, w, h, stride, rank, world, true);
 }
 
-jxg_status jxg_shard_next_head(void* ctx, uint32_t* dst, size_t* nwords) {
+jxg_status jxg_shard_next_head(jxg_ctx* ctx, uint32_t* dst, size_t* nwords) {
   if (!ctx || !nwords) return JXG_ERR_INVALID_ARG;
-  Ctx* c = static_cast<Ctx*>(ctx);
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
   PipeFrame* fr = nullptr;
   const jxg_status st = pipe_shard_oldest(c, &fr);
@@ -2984,11 +2989,11 @@ jxg_status jxg_shard_next_head(void* ctx, uint32_t* dst, size_t* nwords) {
   return JXG_OK;
 }
 
-jxg_status jxg_shard_write_next(void* ctx, const uint32_t* const* heads, const size_t* head_words,
+jxg_status jxg_shard_write_next(jxg_ctx* ctx, const uint32_t* const* heads, const size_t* head_words,
                                 uint32_t n, void* dst, size_t dst_size, size_t* total) {
   if (!ctx || !heads || !head_words || !total || n == 0) return JXG_ERR_INVALID_ARG;
   *total = 0;
-  Ctx* c = static_cast<Ctx*>(ctx);
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
   PipeFrame* fr = nullptr;
   jxg_status st = pipe_shard_oldest(c, &fr);
@@ -3018,9 +3023,9 @@ jxg_status jxg_shard_write_next(void* ctx, const uint32_t* const* heads, const s
   }
   return JXG_OK;
 }
-jxg_status jxg_shard_write_flush(void* ctx) {
+jxg_status jxg_shard_write_flush(jxg_ctx* ctx) {
   if (!ctx) return JXG_ERR_INVALID_ARG;
-  Ctx* c = static_cast<Ctx*>(ctx);
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
   if (c->pipe)
     while (!c->pipe->writes.empty()) {
@@ -3031,11 +3036,11 @@ jxg_status jxg_shard_write_flush(void* ctx) {
   return JXG_OK;
 }
 
-jxg_status jxg_homogeneity_map(void* ctx, const float* xyb, uint32_t xsize, uint32_t ysize,
+jxg_status jxg_homogeneity_map(jxg_ctx* ctx, const float* xyb, uint32_t xsize, uint32_t ysize,
                                float distance, uint32_t flags, float* r3, uint8_t* type) {
   if (!ctx || !xyb || !r3 || !type || xsize == 0 || ysize == 0 || xsize % 8 || ysize % 8)
     return JXG_ERR_INVALID_ARG;
-  Ctx* c = static_cast<Ctx*>(ctx);
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
   if (pipe_busy(c)) return JXG_ERR_INVALID_ARG;
   const size_t plane = (size_t)xsize * ysize, nb = plane / 64;
@@ -3102,13 +3107,13 @@ static jxg_status compare_device(Ctx* c, const uint8_t* d_orig, size_t so, const
   return JXG_OK;
 }
 
-jxg_status jxg_compare_rgb8_device(void* ctx, const void* d_orig, size_t orig_stride,
+jxg_status jxg_compare_rgb8_device(jxg_ctx* ctx, const void* d_orig, size_t orig_stride,
                                    const void* d_comp, size_t comp_stride, uint32_t xsize,
                                    uint32_t ysize, int want_ssim, jxg_quality* out) {
   if (!ctx || !d_orig || !d_comp || !out || xsize == 0 || ysize == 0 ||
       orig_stride < (size_t)xsize * 3 || comp_stride < (size_t)xsize * 3)
     return JXG_ERR_INVALID_ARG;
-  Ctx* c = static_cast<Ctx*>(ctx);
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
   if (pipe_busy(c)) return JXG_ERR_INVALID_ARG;
   const jxg_status st = order_input(c, c);
@@ -3118,13 +3123,13 @@ jxg_status jxg_compare_rgb8_device(void* ctx, const void* d_orig, size_t orig_st
                         out);
 }
 
-jxg_status jxg_compare_rgb8(void* ctx, const uint8_t* orig, size_t orig_stride,
+jxg_status jxg_compare_rgb8(jxg_ctx* ctx, const uint8_t* orig, size_t orig_stride,
                             const uint8_t* comp, size_t comp_stride, uint32_t xsize,
                             uint32_t ysize, int want_ssim, jxg_quality* out) {
   if (!ctx || !orig || !comp || !out || xsize == 0 || ysize == 0 ||
       orig_stride < (size_t)xsize * 3 || comp_stride < (size_t)xsize * 3)
     return JXG_ERR_INVALID_ARG;
-  Ctx* c = static_cast<Ctx*>(ctx);
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
   if (pipe_busy(c)) return JXG_ERR_INVALID_ARG;
   const size_t row = (size_t)xsize * 3, n = row * ysize;
@@ -3138,11 +3143,11 @@ jxg_status jxg_compare_rgb8(void* ctx, const uint8_t* orig, size_t orig_stride,
   return compare_device(c, c->q_orig.p, row, c->q_comp.p, row, xsize, ysize, want_ssim, out);
 }
 
-jxg_status jxg_synth_rgb8_device(void* ctx, void* d_out, uint32_t xsize, uint32_t ysize,
+jxg_status jxg_synth_rgb8_device(jxg_ctx* ctx, void* d_out, uint32_t xsize, uint32_t ysize,
                                  size_t row_stride, uint64_t seed) {
   if (!ctx || !d_out || xsize == 0 || ysize == 0 || row_stride < (size_t)xsize * 3)
     return JXG_ERR_INVALID_ARG;
-  Ctx* c = static_cast<Ctx*>(ctx);
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
   JXG_HIP(launch_synth(static_cast<uint8_t*>(d_out), xsize, ysize, row_stride, seed, c->stream));
   JXG_HIP(hipStreamSynchronize(c->stream));

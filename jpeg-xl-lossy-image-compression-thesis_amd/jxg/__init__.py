@@ -37,6 +37,11 @@ FLAG_FORCE_ONE_STREAM = 8  # testing: the split assembly's one-stream fallback (
 FLAG_GABORISH = 16  # encoder inverse Gaborish + the decoder's Gaborish (cjxl --gaborish=1)
 FLAG_EPF = 32  # the decoder's edge-preserving filter, iterations by distance (cjxl --epf=-1)
 FLAG_AQ_MASKING = 64  # libjxl-shaped masking quant field (oracle/aq.c) instead of the activity AQ
+# JXG_FLAGS_CJXL_DEFAULTS: what `cjxl IN OUT --distance=D --effort=E` encodes
+# (docker_manager.rs:126-136) -- jxg_cjxl's defaults, bench.py's headline
+FLAGS_CJXL_DEFAULTS = FLAG_ANS | FLAG_GABORISH | FLAG_EPF | FLAG_AQ_MASKING
+# the same set as the oracle's filters mask (oracle/jxo.h: GAB 1 | EPF 2 | AQ_MASKING 4; coder 1)
+ORACLE_FILTERS_CJXL_DEFAULTS = 7
 
 
 class JxgError(RuntimeError):
@@ -69,7 +74,7 @@ class _Stats(ctypes.Structure):
                 ("ms_emit", ctypes.c_float), ("ms_assemble", ctypes.c_float),
                 ("ms_total", ctypes.c_float), ("ms_host_call", ctypes.c_float),
                 ("ms_host_codes", ctypes.c_float), ("ms_host_layout", ctypes.c_float),
-                ("ms_front_kernel", ctypes.c_float)]
+                ("ms_front_kernel", ctypes.c_float), ("ms_aq", ctypes.c_float)]
 
 
 class _Quality(ctypes.Structure):
@@ -354,11 +359,12 @@ class Encoder:
         _check(load().jxg_shard_write_flush(self._ctx))
 
     def timings(self) -> tuple:
-        """(ms_front_kernel, ms_host_call, ms_host_codes, ms_host_layout) of the
-        last encode -- the per-frame subset of :meth:`stats` without its copies."""
+        """(ms_front_kernel, ms_host_call, ms_host_codes, ms_host_layout, ms_aq)
+        of the last encode -- the per-frame subset of :meth:`stats` without its
+        copies."""
         s = _Stats()
         _check(load().jxg_get_stats(self._ctx, ctypes.byref(s)))
-        return s.ms_front_kernel, s.ms_host_call, s.ms_host_codes, s.ms_host_layout
+        return s.ms_front_kernel, s.ms_host_call, s.ms_host_codes, s.ms_host_layout, s.ms_aq
 
     def stats(self) -> dict:
         s = _Stats()
@@ -369,7 +375,7 @@ class Encoder:
                                           "quant_dc", "bytes", "ms_front", "ms_histogram",
                                           "ms_emit", "ms_assemble", "ms_total",
                                           "ms_host_call", "ms_host_codes",
-                                          "ms_host_layout", "ms_front_kernel")}
+                                          "ms_host_layout", "ms_front_kernel", "ms_aq")}
         if s.ac_tokens:
             out["ac_tokens"] = np.ctypeslib.as_array(s.ac_tokens, (s.num_groups * 3,)).reshape(-1, 3).copy()
         if s.ac_strategy:

@@ -24,7 +24,9 @@ import numpy as np  # noqa: E402
 import oracle_ffi  # noqa: E402
 
 SEED_BASE = 0x4A584C00
-# (name, config index, frame, width, height, distance, effort, proposals, coder)
+# (name, config index, frame, width, height, distance, effort, proposals, coder[,
+#  filters]) -- filters: the oracle's mask (oracle/jxo.h), 7 = cjxl's defaults
+#  (Gaborish | EPF | masking AQ, = JXG_FLAGS_CJXL_DEFAULTS with coder 1)
 CASES = [
     ("cpu512_d1", 0, 0, 512, 512, 1.0, 7, 0, 0),
     ("4k_d1", 1, 0, 3840, 2160, 1.0, 7, 0, 0),
@@ -38,6 +40,12 @@ CASES = [
     ("1080p_f1_d1", 3, 1, 1920, 1080, 1.0, 7, 0, 0),
     ("1080p_f1_d2", 3, 1, 1920, 1080, 2.0, 7, 0, 0),
     ("16k_d1_pf", 4, 0, 16384, 16384, 1.0, 7, 3, 0),
+    # round 5: the encode the harness's argv gets (bench.py's headline preset)
+    ("cpu512_d1_cjxl", 0, 0, 512, 512, 1.0, 7, 0, 1, 7),
+    ("4k_d1_cjxl", 1, 0, 3840, 2160, 1.0, 7, 0, 1, 7),
+    ("8k_d1_cjxl", 2, 0, 7680, 4320, 1.0, 7, 0, 1, 7),
+    ("8k_d1_cjxl_pf", 2, 0, 7680, 4320, 1.0, 7, 3, 1, 7),
+    ("8k_d1_cjxl_f100", 2, 100, 7680, 4320, 1.0, 7, 0, 1, 7),
 ]
 
 
@@ -45,10 +53,14 @@ def seed_of(case):
     return SEED_BASE + case[1] + case[2]
 
 
+def filters_of(case):
+    return case[9] if len(case) > 9 else 0
+
+
 def fingerprint_of(case, img, r):
-    name, cfg, fr, w, h, d, e, p, coder = case
+    name, cfg, fr, w, h, d, e, p, coder = case[:9]
     tok = np.ascontiguousarray(r.ac_tokens.astype("<u4"))
-    return {
+    out = {
         "name": name, "config": cfg, "frame": fr, "width": w, "height": h, "distance": d,
         "effort": e, "proposals": p, "coder": coder, "seed": seed_of(case),
         "input_sha256": hashlib.sha256(img.tobytes()).hexdigest(),
@@ -58,6 +70,9 @@ def fingerprint_of(case, img, r):
         "ac_tokens_total": [int(x) for x in tok.sum(axis=0)],
         "acs_hist": {str(k): int(v) for k, v in zip(*np.unique(r.acs, return_counts=True))},
     }
+    if filters_of(case):
+        out["filters"] = filters_of(case)
+    return out
 
 
 if __name__ == "__main__":
@@ -70,7 +85,7 @@ if __name__ == "__main__":
             imgs.clear()
             imgs[key] = oracle_ffi.synth_rgb8(case[3], case[4], seed_of(case))
         img = imgs[key]
-        r = oracle_ffi.encode(img, case[5], case[6], case[7], case[8])
+        r = oracle_ffi.encode(img, case[5], case[6], case[7], case[8], filters_of(case))
         out.append(fingerprint_of(case, img, r))
         print(case[0], out[-1]["bytes"], flush=True)
     with open(os.path.join(HERE, "config_golden.json"), "w") as f:

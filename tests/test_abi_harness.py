@@ -47,6 +47,25 @@ def test_flag_constants_match_header(jxg_mod):
         assert getattr(jxg_mod, name) == int(val), name
 
 
+def test_cjxl_defaults_flag_set(jxg_mod):
+    """JXG_FLAGS_CJXL_DEFAULTS (include/jxg.h) is ANS | Gaborish | EPF | masking
+    AQ, the Python mirror has the same value, and jxg_cjxl starts from it (one
+    named set for both drop-in routes)."""
+    src = open(os.path.join(ROOT, "include", "jxg.h")).read()
+    m = re.search(r"#define JXG_FLAGS_CJXL_DEFAULTS \(([^)]*)\)", src)
+    assert m
+    names = [t.strip() for t in m.group(1).split("|")]
+    assert sorted(names) == sorted(["JXG_FLAG_ANS", "JXG_FLAG_GABORISH", "JXG_FLAG_EPF",
+                                    "JXG_FLAG_AQ_MASKING"])
+    val = 0
+    for n in names:
+        val |= getattr(jxg_mod, n[len("JXG_"):])
+    assert jxg_mod.FLAGS_CJXL_DEFAULTS == val
+    cli = open(os.path.join(ROOT, "jpeg-xl-lossy-image-compression-thesis_amd", "csrc",
+                            "jxg_cjxl.cpp")).read()
+    assert "jxg_params p{1.0f, 7, 0, 1, JXG_FLAGS_CJXL_DEFAULTS, 0};" in cli
+
+
 def test_status_strings(jxg_mod):
     lib = jxg_mod.load()
     assert lib.jxg_status_str(0) == b"ok"

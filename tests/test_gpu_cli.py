@@ -94,3 +94,28 @@ def test_cjxl_flags_override_defaults(jxg_mod, oracle, tmp_path):
     p = subprocess.run([jxg_mod.CLI_PATH, str(src), str(out), "--aq=butteraugli"],
                        capture_output=True, text=True)
     assert p.returncode == 1
+
+
+@pytest.mark.parametrize("distance,effort,proposals", [(1.0, 7, "none"), (2.0, 5, "PF"),
+                                                       (0.5, 7, "F")])
+def test_cli_and_c_abi_give_the_same_bytes(jxg_mod, oracle, tmp_path, distance, effort, proposals):
+    """The two drop-in routes agree: the same PNG through
+    `jxg_cjxl IN OUT --distance=D --effort=E [--proposals=..]` and through the
+    C ABI (jxg_create with JXG_FLAGS_CJXL_DEFAULTS, jxg_encode_rgb8 -- what
+    INTEGRATION.md's Rust execute_cjxl does) give identical bytes, equal to the
+    oracle's encode of cjxl's defaults."""
+    from jxg.synth import natural_rgb8
+
+    img = natural_rgb8(419, 263, 11)
+    src = tmp_path / "in.png"
+    write_png(str(src), img)
+    out = tmp_path / "cli.jxl"
+    ok, msg = jxg_mod.execute_cjxl(str(src), str(out), distance, effort, proposals=proposals)
+    assert ok, msg
+    props = {"none": 0, "P": 1, "F": 2, "PF": 3}[proposals]
+    with jxg_mod.Encoder(distance=distance, effort=effort, proposals=props,
+                         flags=jxg_mod.FLAGS_CJXL_DEFAULTS) as enc:
+        lib_bytes = enc.encode(img)
+    assert out.read_bytes() == lib_bytes
+    assert lib_bytes == oracle.encode(img, distance, effort, props, 1,
+                                      jxg_mod.ORACLE_FILTERS_CJXL_DEFAULTS).bytes

@@ -2,6 +2,7 @@
 oracle's committed fingerprints (tests/golden/config_golden.json, made by
 tests/golden/make_config_golden.py): codestream bytes (sha256), per-group AC
 token counts (sha256) and, where the maps are kept, the AC-strategy histogram.
+The *_cjxl cases encode with JXG_FLAGS_CJXL_DEFAULTS (bench.py's headline).
 Inputs are generated on the device (jxg_synth_rgb8_device) and their bytes are
 checked against the fixture's input hash first.  The 1080p frames go through
 the batch entry point (jxg_encode_batch_rgb8) at d0.5 / d1 / d2."""
@@ -41,6 +42,9 @@ def test_config_matches_oracle(jxg_mod, name):
     t = _device_frame(jxg_mod, g)
     flags = (jxg_mod.FLAG_ANS if g["coder"] else 0) | (
         jxg_mod.FLAG_KEEP_MAPS if g["width"] * g["height"] <= 8294400 else 0)
+    if g.get("filters"):  # cjxl's defaults (the bench headline's preset)
+        assert g["filters"] == jxg_mod.ORACLE_FILTERS_CJXL_DEFAULTS and g["coder"] == 1
+        flags |= jxg_mod.FLAGS_CJXL_DEFAULTS
     with jxg_mod.Encoder(distance=g["distance"], effort=g["effort"], proposals=g["proposals"],
                          flags=flags) as enc:
         data = enc.encode_device(t.data_ptr(), g["width"], g["height"])

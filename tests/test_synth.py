@@ -39,7 +39,7 @@ def test_config_fixture_small_encodes(oracle):
         if case[3] * case[4] > 1920 * 1080:
             continue
         img = oracle.synth_rgb8(case[3], case[4], mk.seed_of(case))
-        r = oracle.encode(img, case[5], case[6], case[7], case[8])
+        r = oracle.encode(img, case[5], case[6], case[7], case[8], mk.filters_of(case))
         want = [g for g in json.load(open(os.path.join(HERE, "golden", "config_golden.json")))
                 if g["name"] == case[0]][0]
         assert mk.fingerprint_of(case, img, r) == want, case[0]

@@ -14,6 +14,7 @@ for s in $STEPS; do
   case $s in
     tests) timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/gpu_tests.log 2>&1
            timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 ;;
+    tcjxl) timeout -k 10 400 python -u -m pytest tests/test_gpu_cli.py tests/test_gpu_configs.py -m gpu -x -v -k "cjxl or cli or c_abi" --timeout 200 --timeout-method thread > $O/gpu_tests_cjxl.log 2>&1 ;;
     bench) timeout -k 10 300 python bench.py --cpu-sweep 16,32,64,128,256 > $O/bench.log 2>&1 ;;
     bench20) timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-quality > $O/bench20.log 2>&1 ;;
     gloo) JXG_DIST_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 4 --steps 20 --warmup 3 > $O/bench_gloo4.log 2>&1 ;;
