@@ -79,7 +79,27 @@ import time
 # taken by torch's stream), and two lanes sharing a queue serialise their
 # kernels.  Must be set before HIP initialises (JXG_BENCH_HW_QUEUES overrides
 # it for experiments; at most 32).
-HW_QUEUES = min(32, int(os.environ.get("JXG_BENCH_HW_QUEUES", "16")))
+#
+# Several ranks on ONE device (the JXG_DIST_BACKEND=gloo rehearsal of the
+# multi-GPU path on a one-GPU box): every process has its own
+# GPU_MAX_HW_QUEUES queues, so 4 ranks x 16 = 64 queues oversubscribe the
+# device's hardware queue slots and the scheduler time-slices the processes
+# (round 4's 4-rank rehearsal: 49 ms per frame, 367 ms latency,
+# profiles/r04m/bench_gloo4.log).  The rehearsal splits the 16 queues between
+# the ranks sharing the device instead (each rank's pipeline lanes follow:
+# queues - 1).  A rank alone on its GPU (the driver's N-GPU run) keeps 16.
+def _ranks_sharing_device():
+    if os.environ.get("JXG_DIST_BACKEND", "nccl") != "gloo":
+        return 1
+    lw = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
+    vis = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("ROCR_VISIBLE_DEVICES")
+    ndev = len(vis.split(",")) if vis else int(os.environ.get("JXG_BENCH_DEVICES", "1"))
+    return max(1, (lw + ndev - 1) // ndev)
+
+
+RANKS_PER_DEVICE = _ranks_sharing_device()
+HW_QUEUES = min(32, int(os.environ.get("JXG_BENCH_HW_QUEUES",
+                                       str(max(3, 16 // RANKS_PER_DEVICE)))))
 os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -380,12 +400,8 @@ def main():
     # JXG_DIST_BACKEND=gloo rehearses the multi-rank path with host-staged
     # collectives (several ranks may then share one device)
     backend = os.environ.get("JXG_DIST_BACKEND", "nccl")
-    ranks_on_device = 1
     if backend == "gloo":
-        ndev = max(1, torch.cuda.device_count())
-        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", env_world or "1"))
-        ranks_on_device = (local_world + ndev - 1) // ndev
-        local = local % ndev
+        local = local % max(1, torch.cuda.device_count())
     dev = torch.device("cuda", local)
     if world > 1:
         torch.cuda.set_device(local)
@@ -451,9 +467,10 @@ def main():
         host = None
         bufs = {}
         if mode == "shard":
-            from jxg.dist import ShardStream, shared_gpu_lanes
-            ss = ShardStream(encs[0], w, fh, rank, world,
-                             lanes=shared_gpu_lanes(ranks_on_device, HW_QUEUES))
+            from jxg.dist import ShardStream
+            # (each process has its own HW_QUEUES queues, split above when
+            # ranks share a device: its lanes follow them, no cap needed)
+            ss = ShardStream(encs[0], w, fh, rank, world)
         elif mode == "shard-sync" and args.assembly == "host":
             from jxg.dist import SharedHostBuffer
             if SharedHostBuffer.single_node():
@@ -698,6 +715,8 @@ def main():
                        "global_batch": per_step * (1 if mode != "frames" else world),
                        "parallelism": par},
             "streams_per_gpu": nstreams,
+            "hw_queues_per_process": HW_QUEUES,
+            "ranks_per_device": RANKS_PER_DEVICE,
             "pipeline": pipeline or streamed,
             "ms_latency": round(sum(x[0] for x in host_ms) / len(host_ms), 3),
             "bytes_per_frame": nbytes,

@@ -610,12 +610,6 @@ __device__ __forceinline__ void ans_chain(const AnsArgs& a, uint32_t blk) {
   uint32_t bt[kBands];  // the group's stream = its bands' record spaces, in order
 #pragma unroll
   for (int i = 0; i < kBands; i++) bt[i] = a.bandtok[g * kBands + i];
-  // chunk q (stream order) of the group: the chain's iterations cover
-  // [n - 64 (K - q), n - 64 (K - q - 1)) clipped at 0; their emitted bits go
-  // to csum[q] (ans_emit places every segment from them)
-  const uint32_t K = ((uint32_t)n + 63) / 64;
-  uint32_t* csum = a.csum + (uint64_t)slot * kAnsMaxChunks;
-  uint32_t total = 32;  // the state, then every record's bits
   // every lane starts from the initial state x = 0x130000
   uint32_t k = 0x130u, v = 0;
   uint32_t rec = (int)lane < min(64, n) ? a.tokens[b + rec_index(bt, n - 1 - lane)] : 0u;
@@ -631,25 +625,35 @@ __device__ __forceinline__ void ans_chain(const AnsArgs& a, uint32_t blk) {
     }
     const uint32_t Fq = f << 8;  // emit iff k >= Fq
     const uint32_t nf2 = (uint32_t)(-(int)(2 * f));
+    // quotient floor(xs / f) = floor(x / (f << sh)) = trunc((x + .5) * rcp(f)
+    // * 2^-sh): the shift is folded into the multiplier (exact: one rounding,
+    // < 2^-20 / (f << sh), while (x + .5) / (f << sh) stays >= .5 / (f << sh)
+    // from an integer), so it leaves the quotient's path
     const double rcp = 1.0 / (double)f, hr = 0.5 * rcp;
+    const double rcp16 = rcp * (1.0 / 65536.0), hr16 = hr * (1.0 / 65536.0);
     const int hn = hi - 64;
     const uint32_t nrec = (int)lane < min(64, hn) ? a.tokens[b + rec_index(bt, hn - 1 - lane)] : 0u;
     uint32_t X = 0;     // lane L: the state before record L's step
     uint32_t xin = 0;   // the state handed to the previous step
     auto step = [&](int s) {
-      // shadow: emission (a shift of 16 drops v: (k << 12 | v) >> 16 = k >> 4),
-      // and the previous step's input state into its lane
+      // shadow: k from lane L-1, emission (a shift of 16), the multiplier it
+      // selects, and the previous step's input state into its lane
       const uint32_t kin = wave_ror1(k);
-      const uint32_t sh = kin >= Fq ? 16u : 0u;
+      const bool em = kin >= Fq;
+      const uint32_t sh = em ? 16u : 0u;
+      const double rs = em ? rcp16 : rcp, hs = em ? hr16 : hr;
+      uint32_t t = kin << 12;
+      asm volatile("" : "+v"(t));  // opaque: t + v below stays a plain add
       if (s > 0)
         asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(X) : "v"(X), "v"(xin), "s"(1ull << (s - 1)));
       __builtin_amdgcn_sched_barrier(0);
-      // critical path: v -> x -> xs -> quotient -> address -> next read
-      const uint32_t vin = wave_ror1(v);
-      const uint32_t x = (kin << 12) + vin;
-      const uint32_t xs = x >> sh;
-      const uint32_t kk = (uint32_t)__builtin_fma((double)xs, rcp, hr);
-      const uint32_t x2 = (xs << 1) + base2;
+      // critical path: v (lane L-1, DPP folded into the add) -> x -> quotient
+      // -> address -> next read
+      uint32_t x;
+      asm("v_add_u32_dpp %0, %1, %2 wave_ror:1 row_mask:0xf bank_mask:0xf"
+          : "=v"(x) : "v"(v), "v"(t));
+      const uint32_t kk = (uint32_t)__builtin_fma((double)x, rs, hs);
+      const uint32_t x2 = ((x >> sh) << 1) + base2;
       uint32_t addr;
       asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(addr) : "v"(kk), "v"(nf2), "v"(x2));
       v = *reinterpret_cast<const uint16_t*>(inv + addr);
@@ -677,20 +681,14 @@ __device__ __forceinline__ void ans_chain(const AnsArgs& a, uint32_t blk) {
         k = kk;
       }
     }
-    uint32_t mylen = 0;
     if ((int)lane < cnt) {
-      // emitted bits of the record: [16-bit chunk] then its raw bits
+      // emitted bits of the record: [16-bit chunk] then its raw bits (their
+      // sums per chunk: ans_sums, off the chain)
       const bool em = (X >> 20) >= f;
       const uint32_t raw = rec >> 18, nb = (rec >> 14) & 15;
-      mylen = em ? nb + 16 : nb;
       a.val[b + hi - 1 - lane] = em ? (X & 0xFFFFu) | raw << 16 : raw;
-      a.len[b + hi - 1 - lane] = (uint8_t)mylen;
+      a.len[b + hi - 1 - lane] = (uint8_t)(em ? nb + 16 : nb);
     }
-    // the chunk's bits (every lane gets the sum)
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) mylen += __shfl_xor(mylen, d, 64);
-    total += mylen;
-    if (lane == 0) csum[K - 1 - (uint32_t)(n - hi) / 64] = mylen;
     rec = nrec;
     if (hi <= 64) {  // the final state: lane cnt - 1's result
       const uint32_t kf = __builtin_amdgcn_readlane(k, cnt - 1);
@@ -699,14 +697,47 @@ __device__ __forceinline__ void ans_chain(const AnsArgs& a, uint32_t blk) {
     }
   }
   if (n == 0 && lane == 0) a.state[g] = 0x130000u;
-  // the section's bit count, and its scratch words zeroed for ans_emit (which
-  // ORs the words it shares with a neighbouring segment): no arena memset
-  if (lane == 0) a.bits[g] = total;
-  uint32_t* dst = a.scratch + (a.base[g] >> 5);
-  for (uint32_t i = lane; i < (total + 31) / 32; i += 64) dst[i] = 0;
 }
 __global__ __launch_bounds__(kAnsWaves * 64) void ans_encode_kernel(Batch<AnsArgs> bt_) {
   ans_chain(bt_.a[blockIdx.z], blockIdx.x);
+}
+// After the chains, one 256-thread workgroup per group: the emitted bits of
+// every 64-record chunk q (stream order; records [n - 64 (K - q), n - 64 (K -
+// q - 1)) clipped at 0) into csum[q], from which ans_emit places its
+// segments; the section's bit count (the 32-bit state, then every record's
+// bits); and the section's scratch words zeroed (ans_emit ORs the two words a
+// segment shares with its neighbours; no arena memset).  Round 4 did this
+// bookkeeping inside the chain, on its serial path.
+constexpr int kSumThreads = 256;
+__global__ __launch_bounds__(kSumThreads) void ans_sums_kernel(Batch<AnsArgs> bt_) {
+  __shared__ uint32_t sTot[kSumThreads / 64];
+  const AnsArgs& a = bt_.a[blockIdx.z];
+  const uint32_t slot = blockIdx.x;
+  if (slot >= a.n) return;
+  const uint32_t g = slot_group(a.glist, a.g0, slot);
+  const uint32_t n = a.ntok[g * 3] + a.ntok[g * 3 + 1] + a.ntok[g * 3 + 2];
+  const uint32_t K = (n + 63) / 64;
+  const uint64_t b = (uint64_t)slot * kGroupTokStride;
+  uint32_t* csum = a.csum + (uint64_t)slot * kAnsMaxChunks;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t tot = 0;
+  for (uint32_t q = (uint32_t)wv; q < K; q += kSumThreads / 64) {
+    const uint32_t lo = q == 0 ? 0u : n - 64u * (K - q), hi = n - 64u * (K - q - 1);
+    const uint32_t k = lo + (uint32_t)lane;
+    uint32_t l = k < hi ? (uint32_t)a.len[b + k] : 0u;
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) l += __shfl_xor(l, d, 64);
+    if (lane == 0) csum[q] = l;
+    tot += l;
+  }
+  if (lane == 0) sTot[wv] = tot;
+  __syncthreads();
+  uint32_t total = 32;
+#pragma unroll
+  for (int i = 0; i < kSumThreads / 64; i++) total += sTot[i];
+  if (threadIdx.x == 0) a.bits[g] = total;
+  uint32_t* dst = a.scratch + (a.base[g] >> 5);
+  for (uint32_t i = threadIdx.x; i < (total + 31) / 32; i += kSumThreads) dst[i] = 0;
 }
 // bit placement: the 32-bit state, then every record's bits, in order.  One
 // 256-thread workgroup per (group, segment of kSegChunks chunks of 64
@@ -794,6 +825,7 @@ void launch_ans(const AnsArgs* a, uint32_t k, hipStream_t s) {
   }
   hipLaunchKernelGGL(ans_encode_kernel, dim3((n + kAnsWaves - 1) / kAnsWaves, 1, k),
                      dim3(kAnsWaves * 64), 0, s, b);
+  hipLaunchKernelGGL(ans_sums_kernel, dim3(n, 1, k), dim3(kSumThreads), 0, s, b);
   const uint32_t nseg = (maxtok + kSegChunks * 64 - 1) / (kSegChunks * 64);
   if (nseg) hipLaunchKernelGGL(ans_emit_kernel, dim3(n, nseg, k), dim3(kEmitThreads), 0, s, b);
 }

@@ -881,10 +881,11 @@ __device__ __forceinline__ float gab_src(const float* P, const float* R, int lx,
   if (lx >= 0 && lx < 66 && ly >= 0 && ly < 66) return P[lds_at(lx, ly)];
   return R[ring_index(lx, ly)];
 }
-// In-place sweep: thread = (row half, channel, column), 396 threads; a 3 x 3
-// window in registers, one new row per step, one barrier per step before the
-// step's store (every thread has read the rows it still needs by then; the
-// first half reads row 33 up front, which the second half overwrites first).
+// Sweep: thread = (row half, channel, column), 396 threads; a 3 x 3 window in
+// registers, one new row per step, the 33 outputs of its column half kept in
+// registers until every thread has read its inputs (one barrier), then
+// stored in place.  (Round 4 stored each row after a barrier of its own: 33
+// barriers per tile.)
 __device__ __forceinline__ void gab_sweep(const FrontArgs& a, float* sPix, const float* ring,
                                           int ox, int oy) {
   const int t = threadIdx.x;
@@ -895,33 +896,34 @@ __device__ __forceinline__ void gab_sweep(const FrontArgs& a, float* sPix, const
   float* P = sPix + c * kPlane;
   const float* R = ring + c * kRing;
   const bool colin = ox + lx >= 0 && ox + lx < xp;
-  float n[3], m[3], sn[3], ex[3];
+  float out[33];
   if (act) {
+    float n[3], m[3], sn[3];
 #pragma unroll
     for (int k = 0; k < 3; k++) {
       n[k] = gab_src(P, R, lx + k - 1, y0 - 1, ox, oy, xp, yp);
       m[k] = gab_src(P, R, lx + k - 1, y0, ox, oy, xp, yp);
-      ex[k] = half == 0 ? gab_src(P, R, lx + k - 1, 33, ox, oy, xp, yp) : 0.0f;
     }
-  }
-#pragma unroll 1
-  for (int st = 0; st < 33; st++) {
-    const int ly = y0 + st;
-    float o = 0.0f;
-    if (act) {
 #pragma unroll
-      for (int k = 0; k < 3; k++)
-        sn[k] = (half == 0 && st == 32) ? ex[k] : gab_src(P, R, lx + k - 1, ly + 1, ox, oy, xp, yp);
+    for (int st = 0; st < 33; st++) {
+#pragma unroll
+      for (int k = 0; k < 3; k++) sn[k] = gab_src(P, R, lx + k - 1, y0 + st + 1, ox, oy, xp, yp);
       const float s1 = (n[1] + sn[1]) + (m[0] + m[2]);
       const float s2 = (n[0] + n[2]) + (sn[0] + sn[2]);
-      o = (m[1] * kGabK0 + s1 * kGabK1) + s2 * kGabK2;
-    }
-    __syncthreads();
-    if (act && colin && oy + ly >= 0 && oy + ly < yp) P[lds_at(lx, ly)] = o;
+      out[st] = (m[1] * kGabK0 + s1 * kGabK1) + s2 * kGabK2;
 #pragma unroll
-    for (int k = 0; k < 3; k++) {
-      n[k] = m[k];
-      m[k] = sn[k];
+      for (int k = 0; k < 3; k++) {
+        n[k] = m[k];
+        m[k] = sn[k];
+      }
+    }
+  }
+  __syncthreads();
+  if (act && colin) {
+#pragma unroll
+    for (int st = 0; st < 33; st++) {
+      const int ly = y0 + st;
+      if (oy + ly >= 0 && oy + ly < yp) P[lds_at(lx, ly)] = out[st];
     }
   }
 }

@@ -3005,16 +3005,23 @@ jxg_status jxg_shard_write_next(jxg_ctx* ctx, const uint32_t* const* heads, cons
   if (st) return st;  // (too small a buffer: the frame stays, *total tells the size)
   if (!S->ev_write && hipEventCreateWithFlags(&S->ev_write, hipEventDisableTiming) != hipSuccess)
     return JXG_ERR_HIP;
-  JXG_HIP(hipEventRecord(S->ev_write, S->stream));
   Pipe& p = *c->pipe;
+  // this slot's event may still be queued for an older write of the slot:
+  // wait for that write's copies before its record is replaced, so the
+  // promise below never rests on an incidental earlier synchronisation
+  for (auto it = p.writes.begin(); it != p.writes.end();) {
+    if (*it == S->ev_write) {
+      JXG_HIP(hipEventSynchronize(*it));
+      it = p.writes.erase(it);
+    } else {
+      ++it;
+    }
+  }
+  JXG_HIP(hipEventRecord(S->ev_write, S->stream));
   p.ready.erase(p.ready.begin());  // its slot is free again (later work queues behind the copies)
   // the copies of the write JXG_SHARD_WRITE_LAG calls back have landed on return
   // (copy kernels queue behind the other lanes' kernels: waiting for the
   // previous frame's held this thread ~0.27 ms per frame, profiles/r04l)
-  for (hipEvent_t& e : p.writes)
-    if (e == S->ev_write) {  // re-recorded below: covered by its new record
-      e = nullptr;
-    }
   p.writes.push_back(S->ev_write);
   while (p.writes.size() > JXG_SHARD_WRITE_LAG) {
     const hipEvent_t e = p.writes.front();

@@ -343,6 +343,11 @@ class ShardStream:
                  group=None, slots: int = 6, slot_bytes: int | None = None,
                  lanes: int | None = None):
         self.enc, self.w, self.h, self.rank, self.world = enc, width, height, rank, world
+        if slots <= WRITE_LAG:
+            # a rank marks frame k done only after writing frame k + WRITE_LAG,
+            # and writing frame k waits for slot k % slots (frame k - slots) to
+            # be done on every rank, its own included
+            raise ValueError("ShardStream needs slots > %d (got %d)" % (WRITE_LAG, slots))
         if lanes is not None:  # ranks sharing one GPU split its hardware queues
             enc.set_pipeline_lanes(lanes)
         self.depth = enc.pipeline_depth(width, height, rank, world)
@@ -417,6 +422,9 @@ class ShardStream:
         if head.size > self.hcap:
             raise RuntimeError("payload head of %d words over %d" % (head.size, self.hcap))
         # slot s was last used by frame k - S: every rank must be done with it
+        # (this rank's own part: flushed here if it is still unmarked)
+        if self.unmarked and self.unmarked[0] <= k - self.slots:
+            self._mark()
         self._wait(lambda: bool((self.done[s] >= k - self.slots).all()), "slot %d" % s)
         self.heads[s, r, :head.size] = head
         self.published[s, r] = k          # (x86: the head's stores are visible first)

@@ -262,3 +262,17 @@ def test_shared_gpu_lanes_split():
     assert shared_gpu_lanes(1) is None and shared_gpu_lanes(0) is None
     assert [shared_gpu_lanes(k) for k in (2, 3, 4, 5, 8, 16)] == [7, 5, 3, 3, 2, 2]
     assert shared_gpu_lanes(2, queues=32) == 15
+
+
+def test_shard_stream_rejects_too_few_slots(jxg_mod):
+    """a rank marks frame k done after writing frame
+    k + WRITE_LAG and writing frame k waits for frame k - slots on every rank,
+    so slots <= WRITE_LAG would wait on itself; the constructor refuses it
+    before touching the encoder or the shared region."""
+    import pytest
+
+    from jxg import dist as jd
+
+    for slots in range(0, jd.WRITE_LAG + 1):
+        with pytest.raises(ValueError):
+            jd.ShardStream(None, 64, 64, 0, 1, slots=slots)

@@ -2,7 +2,7 @@
 # One GPU-box pass: GPU tests, smoke, the default bench (CPU baseline with a
 # thread sweep), and a 4-rank gloo rehearsal of bench.py's default sharded
 # path on the box's one GPU (bench.py starts the ranks itself).
-# Usage: bash tools/gpu_check.sh TAG [tests|bench|bench20|gloo|cfg|small|wide ...]
+# Usage: bash tools/gpu_check.sh TAG [tests|tcjxl|bench|bench20|gloo|rank8|chainab|cfg|small ...]
 # (default: tests bench gloo)
 set -e
 export TMPDIR=/tmp
@@ -18,14 +18,15 @@ for s in $STEPS; do
     bench) timeout -k 10 300 python bench.py --cpu-sweep 16,32,64,128,256 > $O/bench.log 2>&1 ;;
     bench20) timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-quality > $O/bench20.log 2>&1 ;;
     gloo) JXG_DIST_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 4 --steps 20 --warmup 3 > $O/bench_gloo4.log 2>&1 ;;
+    rank8) # rank 7's real kind-1 shard of an 8K frame over 8 ranks, one context
+           for pr in cjxl plain; do
+             timeout -k 10 150 python tools/stream_probe.py --mode rank --world 8 --preset $pr --frames 200 --warmup 32 >> $O/probe_rank8.log 2>&1
+           done ;;
+    chainab) # same-box A/B of tools/ab builds (tools/build_lib_variant.sh): stage times
+           for r in 1 2; do for v in $AB; do
+             JXG_LIB_PATH=$PWD/tools/ab/libjxg_$v.so timeout -k 10 120 python tools/chain_probe.py >> $O/chain_ab.log 2>&1
+           done; done ;;
     cfg) bash tools/gpu_configs.sh $TAG/cfg ;;
-    wide) # tools/patches/merge_wide_transforms.patch built as tools/ab/libjxg_wide.so
-          # (tools/ab/libjxg_base.so: the same tree without it): parity, then merge-stage A/B
-          JXG_LIB_PATH=$PWD/tools/ab/libjxg_wide.so timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_gpu_parity.py tests/test_gpu_configs.py tests/test_gpu_stream.py > $O/wide_tests.log 2>&1
-          for r in 1 2; do for v in base wide; do
-            echo "== $v round $r" >> $O/merge_ab.log
-            JXG_LIB_PATH=$PWD/tools/ab/libjxg_$v.so timeout -k 10 120 python tools/merge_probe.py >> $O/merge_ab.log 2>&1
-          done; done ;;
     small) # small-frame streams: config 3's 1080p frames, a 1/8 slice of the
            # 8K frame (one rank's load), the 8-context emulation; then a
            # kernel + copy trace of the 1080p stream

@@ -5,6 +5,10 @@ torch.distributed launcher in between):
          1/8 slice: --world 1 --h 544
   plain  whole frames through jxg_submit_rgb8_device / jxg_receive, e.g.
          config 3's frames: --w 1920 --h 1080
+  rank   ONE context streams rank --rank's real shard of a --world split
+         (jxg_shard_plan's partition, e.g. rank 7 of 8: kind 1, whole LF
+         groups) through the same protocol; the other ranks' payload heads
+         are taken from one streamed encode of each distinct frame beforehand
   python tools/stream_probe.py --mode host --world 2 --frames 40"""
 import argparse
 import ctypes
@@ -23,7 +27,10 @@ import jxg  # noqa: E402
 from jxg.synth import synth_rgb8_device  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--mode", choices=("plain", "host"), default="host")
+ap.add_argument("--mode", choices=("plain", "host", "rank"), default="host")
+ap.add_argument("--rank", type=int, default=-1, help="rank mode: the rank (-1: world - 1)")
+ap.add_argument("--preset", choices=("cjxl", "plain"), default="cjxl",
+                help="cjxl = JXG_FLAGS_CJXL_DEFAULTS (bench.py's headline), plain = ANS only")
 ap.add_argument("--world", type=int, default=1)
 ap.add_argument("--frames", type=int, default=40)
 ap.add_argument("--warmup", type=int, default=16)
@@ -35,14 +42,17 @@ a = ap.parse_args()
 w, h, W = a.w, a.h, a.world
 ts = [synth_rgb8_device(w, h, 0x4A584C02 + 100 * k) for k in range(2)]
 torch.cuda.synchronize()
-encs = [jxg.Encoder(flags=jxg.FLAG_ANS) for _ in range(W)]
+FLAGS = jxg.FLAGS_CJXL_DEFAULTS if a.preset == "cjxl" else jxg.FLAG_ANS
+R = a.rank if a.rank >= 0 else W - 1
+encs = [jxg.Encoder(flags=FLAGS) for _ in range(W if a.mode == "host" else 1)]
 if a.lanes < 0:
     from jxg.dist import shared_gpu_lanes
-    a.lanes = shared_gpu_lanes(W, int(os.environ["GPU_MAX_HW_QUEUES"])) or 0
+    a.lanes = shared_gpu_lanes(len(encs), int(os.environ["GPU_MAX_HW_QUEUES"])) or 0
 for e in encs:
     e.set_pipeline_lanes(a.lanes)
-depth = min(e.pipeline_depth(w, h, r, W) for r, e in enumerate(encs)) if a.mode == "host" \
-    else encs[0].pipeline_depth(w, h)
+depth = (min(e.pipeline_depth(w, h, r, W) for r, e in enumerate(encs)) if a.mode == "host"
+         else encs[0].pipeline_depth(w, h, R, W) if a.mode == "rank"
+         else encs[0].pipeline_depth(w, h))
 stamps = []
 sizes = []
 tsub = [0.0]  # main thread: seconds inside submit calls
@@ -73,6 +83,23 @@ if a.mode == "plain":
             take()
 else:
     buf = np.zeros(w * h * 2 + (1 << 20), dtype=np.uint8)
+    cache = []  # rank mode: every rank's payload head of each distinct frame
+    if a.mode == "rank":
+        tmp = [jxg.Encoder(flags=FLAGS) for _ in range(W)]
+        for e in tmp:
+            e.set_pipeline_lanes(2)
+        for t in ts:
+            for r, e in enumerate(tmp):
+                e.shard_submit_device(t.data_ptr(), w, h, r, W)
+            hs = [e.shard_next_head() for e in tmp]
+            for e in tmp:
+                e.shard_write_next(hs, buf.ctypes.data, buf.size)
+                e.shard_write_flush()
+            cache.append(hs)
+        for e in tmp:
+            e.close()
+        torch.cuda.synchronize()
+    taken = [0]
     # page-locked like ShardStream's shared buffer (the writes are DMA)
     assert jxg.load().jxg_host_register(ctypes.c_void_p(buf.ctypes.data), buf.nbytes) == 0
 
@@ -80,7 +107,12 @@ else:
 
     def take():
         t = time.perf_counter()
-        heads = [e.shard_next_head() for e in encs]
+        if a.mode == "rank":
+            heads = list(cache[taken[0] % 2])
+            heads[R] = encs[0].shard_next_head()
+        else:
+            heads = [e.shard_next_head() for e in encs]
+        taken[0] += 1
         t1 = time.perf_counter()
         for e in encs:
             ok, tot = e.shard_write_next(heads, buf.ctypes.data, buf.size)
@@ -93,7 +125,8 @@ else:
     def run(n):
         for k in range(n):
             for r, e in enumerate(encs):
-                timed_submit(e.shard_submit_device, ts[k % 2].data_ptr(), w, h, r, W)
+                timed_submit(e.shard_submit_device, ts[k % 2].data_ptr(), w, h,
+                             R if a.mode == "rank" else r, W)
             if encs[0].pending() >= depth:
                 take()
         while encs[0].pending():
@@ -103,22 +136,22 @@ run(a.warmup)
 torch.cuda.synchronize()
 stamps.clear()
 tsub[0] = 0.0
-if a.mode == "host":
+if a.mode != "plain":
     ttake[0] = ttake[1] = 0.0
 t0 = time.perf_counter()
 run(a.frames)
-if a.mode == "host":
+if a.mode != "plain":
     for e in encs:
         e.shard_write_flush()
 torch.cuda.synchronize()
 dt = time.perf_counter() - t0
 gaps = np.diff(np.array([t0] + stamps)) * 1e3
-print("mode %s %dx%d world %d lanes cap %d depth %d: %.3f ms/frame, %.1f MPix/s, bytes %d; in submit "
+print("mode %s%s %s %dx%d world %d lanes cap %d depth %d: %.3f ms/frame, %.1f MPix/s, bytes %d; in submit "
       "%.3f ms/frame; receive gaps ms p50 %.3f p90 %.3f max %.3f"
-      % (a.mode, w, h, W, a.lanes, depth, dt * 1e3 / a.frames, w * h * a.frames / dt / 1e6, sizes[-1],
+      % (a.mode, " rank %d" % R if a.mode == "rank" else "", a.preset, w, h, W, a.lanes, depth, dt * 1e3 / a.frames, w * h * a.frames / dt / 1e6, sizes[-1],
          tsub[0] * 1e3 / a.frames, np.median(gaps), np.percentile(gaps, 90), gaps.max()),
       flush=True)
-if a.mode == "host":
+if a.mode != "plain":
     print("  in next_head %.3f ms/frame, in write_next %.3f ms/frame"
           % (ttake[0] * 1e3 / a.frames, ttake[1] * 1e3 / a.frames), flush=True)
 for e in encs:
