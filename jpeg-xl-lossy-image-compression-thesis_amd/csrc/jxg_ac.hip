@@ -625,35 +625,25 @@ __device__ __forceinline__ void ans_chain(const AnsArgs& a, uint32_t blk) {
     }
     const uint32_t Fq = f << 8;  // emit iff k >= Fq
     const uint32_t nf2 = (uint32_t)(-(int)(2 * f));
-    // quotient floor(xs / f) = floor(x / (f << sh)) = trunc((x + .5) * rcp(f)
-    // * 2^-sh): the shift is folded into the multiplier (exact: one rounding,
-    // < 2^-20 / (f << sh), while (x + .5) / (f << sh) stays >= .5 / (f << sh)
-    // from an integer), so it leaves the quotient's path
     const double rcp = 1.0 / (double)f, hr = 0.5 * rcp;
-    const double rcp16 = rcp * (1.0 / 65536.0), hr16 = hr * (1.0 / 65536.0);
     const int hn = hi - 64;
     const uint32_t nrec = (int)lane < min(64, hn) ? a.tokens[b + rec_index(bt, hn - 1 - lane)] : 0u;
     uint32_t X = 0;     // lane L: the state before record L's step
     uint32_t xin = 0;   // the state handed to the previous step
     auto step = [&](int s) {
-      // shadow: k from lane L-1, emission (a shift of 16), the multiplier it
-      // selects, and the previous step's input state into its lane
+      // shadow: emission (a shift of 16 drops v: (k << 12 | v) >> 16 = k >> 4),
+      // and the previous step's input state into its lane
       const uint32_t kin = wave_ror1(k);
-      const bool em = kin >= Fq;
-      const uint32_t sh = em ? 16u : 0u;
-      const double rs = em ? rcp16 : rcp, hs = em ? hr16 : hr;
-      uint32_t t = kin << 12;
-      asm volatile("" : "+v"(t));  // opaque: t + v below stays a plain add
+      const uint32_t sh = kin >= Fq ? 16u : 0u;
       if (s > 0)
         asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(X) : "v"(X), "v"(xin), "s"(1ull << (s - 1)));
       __builtin_amdgcn_sched_barrier(0);
-      // critical path: v (lane L-1, DPP folded into the add) -> x -> quotient
-      // -> address -> next read
-      uint32_t x;
-      asm("v_add_u32_dpp %0, %1, %2 wave_ror:1 row_mask:0xf bank_mask:0xf"
-          : "=v"(x) : "v"(v), "v"(t));
-      const uint32_t kk = (uint32_t)__builtin_fma((double)x, rs, hs);
-      const uint32_t x2 = ((x >> sh) << 1) + base2;
+      // critical path: v -> x -> xs -> quotient -> address -> next read
+      const uint32_t vin = wave_ror1(v);
+      const uint32_t x = (kin << 12) + vin;
+      const uint32_t xs = x >> sh;
+      const uint32_t kk = (uint32_t)__builtin_fma((double)xs, rcp, hr);
+      const uint32_t x2 = (xs << 1) + base2;
       uint32_t addr;
       asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(addr) : "v"(kk), "v"(nf2), "v"(x2));
       v = *reinterpret_cast<const uint16_t*>(inv + addr);
