@@ -521,6 +521,11 @@ def main():
             # pipeline (up to 12) allocates its buffers on its first frame,
             # which must not land in the timed region
             nw = max(args.warmup, 1) * per_step
+            if ss is not None:
+                # every lane slot of the rank's pipeline (up to 12 lanes x 4
+                # frames) allocates its buffers on its first frames: all of
+                # them run before the timed region
+                nw = max(nw, 2 * ss.depth + 8)
             worker(e, range(max(nw, 16) if (pipe or ss is not None) else args.warmup * per_step))
         for key in ("front_ms", "host_ms", "aq_ms", "sizes"):
             rec[key] = []

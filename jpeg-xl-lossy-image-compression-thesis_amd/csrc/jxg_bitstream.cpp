@@ -222,7 +222,39 @@ void write_context_map(BitWriter& w, const std::vector<uint8_t>& map, int nhist)
   for (uint8_t v : map) counts[v]++;
   std::vector<PrefixCode> code{build_prefix_code(counts, 256)};
   write_histograms(w, std::vector<uint8_t>{0}, 1, code, kCfgMap);
-  for (uint8_t v : map) write_token(w, code[0], kCfgMap, v);
+  // every entry's token code + raw bits as one put (a per-rank-preset map of a
+  // sharded frame has ranks x 7425 entries, written by every rank each frame)
+  uint32_t len[256];
+  uint64_t val[256];
+  for (int v = 0; v < 256; v++) {
+    if (!counts[v]) continue;
+    uint32_t tok, nb, bits;
+    hybrid_encode((uint32_t)v, kCfgMap, &tok, &nb, &bits);
+    len[v] = code[0].len[tok] + nb;
+    val[v] = (uint64_t)code[0].code[tok] | ((uint64_t)bits << code[0].len[tok]);
+  }
+  if (w.count_only()) {
+    uint64_t nbits = 0;
+    for (int v = 0; v < 256; v++)
+      if (counts[v]) nbits += (uint64_t)counts[v] * len[v];
+    w.skip(nbits);
+    return;
+  }
+  uint64_t acc = 0;  // (entries gathered 64 bits at a time)
+  uint32_t na = 0;
+  for (uint8_t v : map) {
+    const uint32_t l = len[v];
+    acc |= val[v] << na;
+    if (na + l >= 64) {
+      w.put(64, acc);
+      const uint32_t used = 64 - na;  // bits of this entry that went out
+      acc = used < 64 ? val[v] >> used : 0;
+      na = na + l - 64;
+    } else {
+      na += l;
+    }
+  }
+  w.put(na, acc);
 }
 
 void write_histograms(BitWriter& w, const std::vector<uint8_t>& ctxmap, int nhist,
@@ -352,7 +384,7 @@ int cluster_ans_histograms(const uint32_t* hist, int nh, int* assign) {
   return ncl;
 }
 
-AnsTable build_ans_table(const uint32_t* counts) {
+AnsTable build_ans_table(const uint32_t* counts, bool with_inverse) {
   constexpr int kAlpha = 128, kTab = 4096, kEntry = kTab / kAlpha;
   AnsTable t;
   uint64_t total = 0;
@@ -393,6 +425,7 @@ AnsTable build_ans_table(const uint32_t* counts) {
     }
     t.freq[omit] = (uint16_t)rem;
   }
+  if (!with_inverse) return t;  // (the histogram writers need the frequencies only)
   // alias table of the decoder, then its inverse
   int cutoff[kAlpha], right[kAlpha], offset[kAlpha], cut[kAlpha];
   int nz = 0, only = 0;

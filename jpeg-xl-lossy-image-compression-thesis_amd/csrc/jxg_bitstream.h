@@ -14,7 +14,19 @@ namespace jxg {
 
 class BitWriter {
  public:
+  // a counting writer: put() only advances bits() (sizes without the bytes)
+  static BitWriter counter() {
+    BitWriter w;
+    w.count_only_ = true;
+    return w;
+  }
+  bool count_only() const { return count_only_; }
+  void skip(size_t nbits) { bits_ += nbits; }  // (count-only writers)
   void put(uint32_t nbits, uint64_t v) {
+    if (count_only_) {
+      bits_ += nbits;
+      return;
+    }
     if (nbits == 0) return;
     if (nbits < 64) v &= (1ull << nbits) - 1;
     const size_t word = bits_ >> 6;
@@ -47,6 +59,7 @@ class BitWriter {
  private:
   std::vector<uint64_t> words_;
   size_t bits_ = 0;
+  bool count_only_ = false;
 };
 
 struct UintCfg {
@@ -90,7 +103,9 @@ struct AnsTable {
   std::vector<uint16_t> inv;  // [cum[s] + off] -> alias-table position (4096)
   int nused = 0, omit = 0, omit_code = 0;
 };
-AnsTable build_ans_table(const uint32_t* counts /* [128] */);
+// with_inverse false: the normalized frequencies only (enough to write the
+// histogram; the encoder's alias inverse is left empty)
+AnsTable build_ans_table(const uint32_t* counts /* [128] */, bool with_inverse = true);
 // ANS histogram clustering (oracle/ans.c jxo_ans_cluster): hist[nh][128] ->
 // assign[nh] (centre id, -1 for an empty histogram); returns the centre count
 // (<= kAnsMaxHists: their alias inverses fill 64 KB of LDS in the encoder, so

@@ -51,12 +51,17 @@ template <class T>
 struct DevBuf {
   T* p = nullptr;
   size_t n = 0;
+  bool n_grow = false;  // allocated before
   hipError_t ensure(size_t count) {
     if (count <= n && p) return hipSuccess;
     if (p) (void)hipFree(p);
     p = nullptr;
     n = 0;
-    size_t want = std::max<size_t>(count, 1);
+    // a regrowth gets 1/8 headroom: per-frame sizes (bit scratch, output)
+    // vary a little between frames, and a reallocation in a streamed frame
+    // costs ~0.1 ms of host time (hipFree + hipMalloc)
+    size_t want = n_grow ? std::max<size_t>(count + count / 8, 1) : std::max<size_t>(count, 1);
+    n_grow = true;
     hipError_t e = hipMalloc((void**)&p, want * sizeof(T));
     if (e == hipSuccess) n = want;
     return e;
@@ -2519,7 +2524,9 @@ static jxg_status shard_write_host(Ctx* c, const uint32_t* const* heads_in, cons
   std::vector<SectionRef> secs;
   std::vector<uint8_t> hf;
   uint32_t lf = 0;
-  jxg_status st = parse_payload_heads(heads, ps, &w, &h, secs, hf, &lf);
+  // a generated HfGlobal (per-rank presets) is written by rank 0; the others
+  // need its size only
+  jxg_status st = parse_payload_heads(heads, ps, &w, &h, secs, hf, &lf, me == 0);
   if (st) return st;
   std::vector<uint32_t> sec_size(secs.size());
   for (size_t i = 0; i < secs.size(); i++) sec_size[i] = secs[i].size;
@@ -2537,24 +2544,42 @@ static jxg_status shard_write_host(Ctx* c, const uint32_t* const* heads_in, cons
   if (!dst || pos > dst_size) return JXG_ERR_INVALID_ARG;  // *total tells the size needed
   hipStream_t s = c->stream;
   const std::vector<uint32_t>& hw = c->payload_head;
-  uint64_t body = 0, run_src = 0, run_dst = 0, run_len = 0;
+  // runs of consecutive sections (payload body -> codestream offsets)
+  std::vector<ScatterPiece> runs;
+  uint64_t body = 0;
   for (uint32_t k = 0; k < hw[6]; k++) {
     const uint32_t id = hw[7 + 2 * k], sz = hw[8 + 2 * k];
-    if (run_len && run_src + run_len == body && run_dst + run_len == out_off[id]) {
-      run_len += sz;
-    } else {
-      if (run_len)
-        JXG_HIP(hipMemcpyAsync(dst + run_dst, reinterpret_cast<const uint8_t*>(c->out.p) + run_src,
-                               run_len, hipMemcpyDeviceToHost, s));
-      run_src = body;
-      run_dst = out_off[id];
-      run_len = sz;
-    }
+    ScatterPiece* r = runs.empty() ? nullptr : &runs.back();
+    if (r && r->src + r->len == body && r->dst + r->len == out_off[id])
+      r->len += sz;
+    else if (sz)
+      runs.push_back({body, out_off[id], sz, 0});
     body += sz;
   }
-  if (run_len)
-    JXG_HIP(hipMemcpyAsync(dst + run_dst, reinterpret_cast<const uint8_t*>(c->out.p) + run_src,
-                           run_len, hipMemcpyDeviceToHost, s));
+  // one scatter launch through the buffer's device mapping (page-locked with
+  // jxg_host_register); D2H copies per run otherwise
+  void* dmap = nullptr;
+  if (!runs.empty() && runs.size() <= (size_t)kMaxScatterPieces &&
+      hipHostGetDevicePointer(&dmap, dst, 0) == hipSuccess && dmap) {
+    ScatterArgs sa{};
+    sa.src = reinterpret_cast<const uint8_t*>(c->out.p);
+    sa.dst = static_cast<uint8_t*>(dmap);
+    sa.n = (uint32_t)runs.size();
+    uint32_t nwg = 0;
+    for (size_t i = 0; i < runs.size(); i++) {
+      sa.p[i] = runs[i];
+      sa.p[i].wg0 = nwg;
+      const uint64_t w0 = runs[i].dst >> 2, w1 = (runs[i].dst + runs[i].len + 3) >> 2;
+      nwg += (uint32_t)((w1 - w0 + 1023) / 1024);
+    }
+    launch_scatter(sa, nwg, s);
+    JXG_HIP(hipGetLastError());
+  } else {
+    (void)hipGetLastError();  // (an unmapped buffer: hipHostGetDevicePointer failed)
+    for (const ScatterPiece& r : runs)
+      JXG_HIP(hipMemcpyAsync(dst + r.dst, reinterpret_cast<const uint8_t*>(c->out.p) + r.src, r.len,
+                             hipMemcpyDeviceToHost, s));
+  }
   if (me == 0) {
     std::memcpy(dst, hb.data(), hb.size());
     for (size_t i = 0; i < secs.size(); i++)  // a generated HfGlobal (per-rank presets)

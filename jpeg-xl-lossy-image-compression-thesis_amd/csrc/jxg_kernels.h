@@ -249,6 +249,21 @@ struct PackArgs {
   uint32_t n;
 };
 void launch_pack(const PackArgs& a, hipStream_t s);    // frame arrays -> records
+// a rank's sections (runs of consecutive section bytes of its payload body)
+// -> their codestream offsets in mapped host memory; piece i takes workgroups
+// [wg0, next wg0) of 1024 destination dwords each
+struct ScatterPiece {
+  uint64_t src, dst;
+  uint32_t len, wg0;
+};
+constexpr int kMaxScatterPieces = 64;
+struct ScatterArgs {
+  const uint8_t* src;
+  uint8_t* dst;
+  uint32_t n;
+  ScatterPiece p[kMaxScatterPieces];
+};
+void launch_scatter(const ScatterArgs& a, uint32_t nwg, hipStream_t s);
 void launch_unpack(const PackArgs& a, hipStream_t s);  // records -> frame arrays
 void launch_homog(const HomogArgs& a, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s);
 void launch_ac_hist(const AcArgs* a, uint32_t k, uint32_t ngroups, hipStream_t s);

@@ -41,7 +41,7 @@ static jxg_status build_hf_presets(const std::vector<std::vector<uint32_t>>& hea
       ctxmap[(size_t)r * kAcCtx + k] = (uint8_t)(off + cm[k]);
     }
     const uint32_t* cnt = hw.data() + base + 2 + cw;
-    for (uint32_t h = 0; h < nh; h++) tables.push_back(build_ans_table(cnt + (size_t)h * kAlpha));
+    for (uint32_t h = 0; h < nh; h++) tables.push_back(build_ans_table(cnt + (size_t)h * kAlpha, false));
     off += nh;
   }
   if (off > 255 || n - 1 >= (1u << ceil_log2(ngroups))) return JXG_ERR_INVALID_ARG;
@@ -57,7 +57,7 @@ static jxg_status build_hf_presets(const std::vector<std::vector<uint32_t>>& hea
 jxg_status parse_payload_heads(const std::vector<std::vector<uint32_t>>& heads,
                                       const std::vector<size_t>& psizes, uint32_t* w,
                                       uint32_t* h, std::vector<SectionRef>& secs,
-                                      std::vector<uint8_t>& hf, uint32_t* lf) {
+                                      std::vector<uint8_t>& hf, uint32_t* lf, bool hf_bytes) {
   const uint32_t n = (uint32_t)heads.size();
   secs.clear();
   hf.clear();
@@ -97,11 +97,12 @@ jxg_status parse_payload_heads(const std::vector<std::vector<uint32_t>>& heads,
   if (heads[0][1] == 2) {  // per-rank presets: HfGlobal from the heads
     const uint32_t id = 1 + nlf;
     if (seen[id]) return JXG_ERR_INVALID_ARG;
-    BitWriter bw;
+    // (a rank that does not write HfGlobal needs its size only)
+    BitWriter bw = hf_bytes ? BitWriter() : BitWriter::counter();
     const jxg_status st = build_hf_presets(heads, ngroups, bw);
     if (st) return st;
-    hf = bw.bytes();
-    secs[id] = SectionRef{n, 0, (uint32_t)hf.size()};
+    if (hf_bytes) hf = bw.bytes();
+    secs[id] = SectionRef{n, 0, (uint32_t)((bw.bits() + 7) / 8)};
     seen[id] = true;
   }
   for (size_t i = 0; i < secs.size(); i++)

@@ -28,11 +28,12 @@ struct SectionRef {
 size_t head_words(const uint32_t* hw, size_t avail);
 // every rank's head (psizes: whole payload bytes) -> frame size, loop-filter
 // code, section table; with version-2 heads also the generated HfGlobal
-// (`hf`; its SectionRef names payload n = "generated")
+// (`hf`; its SectionRef names payload n = "generated"; hf_bytes false: its
+// size only, `hf` left empty)
 jxg_status parse_payload_heads(const std::vector<std::vector<uint32_t>>& heads,
                                const std::vector<size_t>& psizes, uint32_t* w, uint32_t* h,
                                std::vector<SectionRef>& secs, std::vector<uint8_t>& hf,
-                               uint32_t* lf);
+                               uint32_t* lf, bool hf_bytes = true);
 // the head at the start of a payload in host memory (empty: malformed)
 std::vector<uint32_t> read_head(const uint8_t* p, size_t size);
 

@@ -54,6 +54,41 @@ __global__ __launch_bounds__(1024) void unpack_kernel(PackArgs a) {
   group_record(a, a.list[blockIdx.x], a.xbuf + blockIdx.x * kGroupRecord, false);
 }
 
+// A rank's sections -> their codestream offsets in the node-shared host buffer
+// (jxg_shard_write_host / jxg_shard_write_next), one launch instead of one
+// D2H copy per run of consecutive sections (a kind-1 shard of an 8K frame has
+// ~12 runs: its LF groups' sections and one per pass-group row; ~20 us of host
+// time per copy call).  The buffer is page-locked host memory the device
+// writes through its mapping (jxg_host_register).  Thread = one destination
+// dword: a dword inside the piece is one store, a dword the piece shares with
+// a neighbouring section (another rank's, written concurrently) takes byte
+// stores of the piece's bytes only.
+__global__ __launch_bounds__(256) void scatter_kernel(ScatterArgs a) {
+  uint32_t i = 0;
+  while (i + 1 < a.n && blockIdx.x >= a.p[i + 1].wg0) i++;
+  const ScatterPiece P = a.p[i];
+  const uint64_t lo = P.dst, hi = P.dst + P.len;
+  const uint64_t w0 = (lo >> 2) + (uint64_t)(blockIdx.x - P.wg0) * 1024, w1 = (hi + 3) >> 2;
+#pragma unroll
+  for (int it = 0; it < 4; it++) {
+    const uint64_t w = w0 + (uint64_t)it * 256 + threadIdx.x;
+    if (w >= w1) break;
+    const uint64_t b0 = w << 2;
+    if (b0 >= lo && b0 + 4 <= hi) {
+      const uint8_t* q = a.src + P.src + (b0 - lo);
+      reinterpret_cast<uint32_t*>(a.dst)[w] =
+          (uint32_t)q[0] | (uint32_t)q[1] << 8 | (uint32_t)q[2] << 16 | (uint32_t)q[3] << 24;
+    } else {
+      for (uint64_t b = b0; b < b0 + 4; b++)
+        if (b >= lo && b < hi) a.dst[b] = a.src[P.src + (b - lo)];
+    }
+  }
+  __threadfence_system();
+}
+void launch_scatter(const ScatterArgs& a, uint32_t nwg, hipStream_t s) {
+  if (a.n && nwg) hipLaunchKernelGGL(scatter_kernel, dim3(nwg), dim3(256), 0, s, a);
+}
+
 void launch_pack(const PackArgs& a, hipStream_t s) {
   if (a.n) hipLaunchKernelGGL(pack_kernel, dim3(a.n), dim3(1024), 0, s, a);
 }

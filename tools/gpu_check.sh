@@ -26,6 +26,9 @@ for s in $STEPS; do
            for r in 1 2; do for v in $AB; do
              JXG_LIB_PATH=$PWD/tools/ab/libjxg_$v.so timeout -k 10 120 python tools/chain_probe.py >> $O/chain_ab.log 2>&1
            done; done ;;
+    rankprof) # API + kernel + copy trace of rank 7's shard stream and of the 7680x544 slice
+           timeout -k 10 200 rocprofv3 --hip-trace --kernel-trace --memory-copy-trace --stats --output-format csv -d $O/prof_rank7 -o run -- python3 tools/stream_probe.py --mode rank --world 8 --preset plain --frames 100 --warmup 16 > $O/prof_rank7.log 2>&1
+           timeout -k 10 200 rocprofv3 --hip-trace --kernel-trace --memory-copy-trace --stats --output-format csv -d $O/prof_slice -o run -- python3 tools/stream_probe.py --mode host --world 1 --h 544 --preset plain --frames 100 --warmup 16 > $O/prof_slice.log 2>&1 ;;
     cfg) bash tools/gpu_configs.sh $TAG/cfg ;;
     small) # small-frame streams: config 3's 1080p frames, a 1/8 slice of the
            # 8K frame (one rank's load), the 8-context emulation; then a
