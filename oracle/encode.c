@@ -502,6 +502,7 @@ int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h, size_t row_strid
   /* ---- merge stage: 16x8 ... 64x64 varblocks (effort >= 5) ---- */
   if (p->effort >= 5) {
     const int max_s = p->effort >= 6 ? 8 : 4;
+    /* effort >= 8: also levels 128 / 256 px (raw ids 21-26) */
     const uint32_t tx_n = (f.bxs + 7) / 8, ty_n = (f.bys + 7) / 8;
 #pragma omp parallel for schedule(dynamic) collapse(2)
     for (uint32_t ty = 0; ty < ty_n; ty++)
@@ -511,11 +512,14 @@ int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h, size_t row_strid
         jxo_cfl_factors(out->cmap[ti], out->cmap[ntiles + ti], cfl);
         jxo_merge_tile(&f, xyb, out->homog, (int)tx, (int)ty, max_s, ent, raws, out->acs, cfl);
       }
+    if (p->effort >= 8)
+      for (int s = 16; s <= 32; s *= 2)
+        jxo_merge_big(&f, xyb, out->homog, s, ent, raws, out->acs, out->cmap, tiles_x, ntiles);
 #pragma omp parallel for schedule(dynamic)
     for (uint32_t by = 0; by < f.bys; by++)
       for (uint32_t bx = 0; bx < f.bxs; bx++) {
-        static _Thread_local int32_t vq[3 * 4096];
-        float llf[3 * 64];
+        static _Thread_local int32_t vq[3 * 65536];
+        static _Thread_local float llf[3 * JXO_LLF_DIM * JXO_LLF_DIM];
         const size_t b = (size_t)by * f.bxs + bx;
         const int si = jxo_shape_of(out->acs[b]);
         if (si < 0) continue; /* 8x8 class or covered */
@@ -539,7 +543,7 @@ int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h, size_t row_strid
             int32_t dcq[3];
             for (int c = 0; c < 3; c++) {
               memcpy(out->ac + (bi * 3 + c) * 64, vq + c * RC + slice * 64, sizeof(int32_t) * 64);
-              dcv[c] = jxo_llf_dc(sh, llf + c * 64, iy, ix);
+              dcv[c] = jxo_llf_dc(sh, llf + c * JXO_LLF_DIM * JXO_LLF_DIM, iy, ix);
             }
             jxo_quant_dc(&f, dcv, dcq);
             for (int c = 0; c < 3; c++) out->dc[c * nb + bi] = dcq[c];

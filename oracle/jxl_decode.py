@@ -733,9 +733,12 @@ _I8, _I4 = _idct_mat(8), _idct_mat(4)
 
 # merged varblocks [ext AcStrategy]: raw id -> (blocks down, blocks across, kind)
 SHAPES = {6: (2, 1, 0), 7: (1, 2, 0), 4: (2, 2, 1), 10: (4, 2, 2), 11: (2, 4, 2), 5: (4, 4, 3),
-          19: (8, 4, 4), 20: (4, 8, 4), 18: (8, 8, 5)}
+          19: (8, 4, 4), 20: (4, 8, 4), 18: (8, 8, 5),
+          22: (16, 8, 6), 23: (8, 16, 6), 21: (16, 16, 7), 25: (32, 16, 8), 26: (16, 32, 8),
+          24: (32, 32, 9)}
 # default weight bands per kind [ext quant_weights.cc]; stored dims rows x cols
-KIND_DIM = [(8, 16), (16, 16), (16, 32), (32, 32), (32, 64), (64, 64)]
+KIND_DIM = [(8, 16), (16, 16), (16, 32), (32, 32), (32, 64), (64, 64), (64, 128), (128, 128),
+            (128, 256), (256, 256)]
 KIND_BANDS = [
     [[7240.7734393502, -0.7, -0.7, -0.2, -0.2, -0.2, -0.5],
      [1448.15468787004, -0.5, -0.5, -0.5, -0.2, -0.2, -0.2],
@@ -765,6 +768,28 @@ KIND_BANDS = [
      [0.9 * 9311.3238710010046, -0.3041958212306401, -0.3633036457487539, -0.35660379990111464,
       -0.3443074455424403, -0.33699592683512467, -0.30180866526242109, -0.27321683125358037],
      [0.9 * 4992.2486445538634, -1.2, -1.2, -0.8, -0.7, -0.7, -0.4, -0.5]],
+    # DCT128X64, DCT128X128, DCT256X128, DCT256X256 (the encoder's restated
+    # defaults, oracle/merge.c; parity with libjxl unpinned)
+    [[1.3 * 23629.073922049845, -1.025, -0.78, -0.65012, -0.19041574084286472, -0.20819395464,
+      -0.421064, -0.32733845535848671],
+     [1.3 * 8611.3238710010046, -0.3041958212306401, -0.3633036457487539, -0.35660379990111464,
+      -0.3443074455424403, -0.33699592683512467, -0.30180866526242109, -0.27321683125358037],
+     [1.3 * 4492.2486445538634, -1.2, -1.2, -0.8, -0.7, -0.7, -0.4, -0.5]],
+    [[1.7 * 26629.073922049845, -1.025, -0.78, -0.65012, -0.19041574084286472, -0.20819395464,
+      -0.421064, -0.32733845535848671],
+     [1.7 * 9311.3238710010046, -0.3041958212306401, -0.3633036457487539, -0.35660379990111464,
+      -0.3443074455424403, -0.33699592683512467, -0.30180866526242109, -0.27321683125358037],
+     [1.7 * 4992.2486445538634, -1.2, -1.2, -0.8, -0.7, -0.7, -0.4, -0.5]],
+    [[2.2 * 23629.073922049845, -1.025, -0.78, -0.65012, -0.19041574084286472, -0.20819395464,
+      -0.421064, -0.32733845535848671],
+     [2.2 * 8611.3238710010046, -0.3041958212306401, -0.3633036457487539, -0.35660379990111464,
+      -0.3443074455424403, -0.33699592683512467, -0.30180866526242109, -0.27321683125358037],
+     [2.2 * 4492.2486445538634, -1.2, -1.2, -0.8, -0.7, -0.7, -0.4, -0.5]],
+    [[3.0 * 26629.073922049845, -1.025, -0.78, -0.65012, -0.19041574084286472, -0.20819395464,
+      -0.421064, -0.32733845535848671],
+     [3.0 * 9311.3238710010046, -0.3041958212306401, -0.3633036457487539, -0.35660379990111464,
+      -0.3443074455424403, -0.33699592683512467, -0.30180866526242109, -0.27321683125358037],
+     [3.0 * 4992.2486445538634, -1.2, -1.2, -0.8, -0.7, -0.7, -0.4, -0.5]],
 ]
 
 

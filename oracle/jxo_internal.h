@@ -71,12 +71,16 @@ extern const uint16_t jxo_nnz_ctx[64];
 
 /* merged varblocks (merge.c) [ext AcStrategy / quant_weights / coeff_order] */
 enum { JXO_VK_16X8 = 0, JXO_VK_16, JXO_VK_32X16, JXO_VK_32, JXO_VK_64X32, JXO_VK_64,
-       JXO_NVKINDS };
+       JXO_VK_128X64, JXO_VK_128, JXO_VK_256X128, JXO_VK_256, JXO_NVKINDS };
 typedef struct {
   uint8_t type, cy, cx, kind; /* raw id, blocks down, blocks across, weight kind */
   float tmul;                 /* cost multiplier of the search */
 } jxo_shape;
-#define JXO_NSHAPES 9
+/* shapes by level L (16, 32, 64, 128, 256 px): tall 3L, wide 3L + 1, full
+ * 3L + 2; levels 128 / 256 (raw ids 21-26) are searched at effort >= 8 */
+#define JXO_NSHAPES 15
+#define JXO_NTILE_SHAPES 9 /* levels <= 64: inside one 64x64 tile */
+#define JXO_LLF_DIM 32     /* LLF buffers: [3][32][32] (a 256x256 varblock's) */
 extern const jxo_shape jxo_shapes[JXO_NSHAPES];
 typedef struct {
   int rows, cols; /* stored orientation: rows = 8 min(cy,cx), cols = 8 max(cy,cx) */
@@ -87,11 +91,17 @@ typedef struct {
 const jxo_vkind* jxo_vkinds(void);
 int jxo_shape_of(int type); /* shape index of a merged raw id, -1 otherwise */
 float jxo_varblock(const jxo_frame* f, const jxo_shape* s, const float* xyb, int px0, int py0,
-                   int raw, int32_t* q /* [3][R*C] natural order */, float* llf /* [3][8][8] */,
+                   int raw, int32_t* q /* [3][R*C] natural order */, float* llf /* [3][32][32] */,
                    int* nz /* [3] */, const float cfl[2] /* chroma-from-luma kx, kb */);
 float jxo_llf_dc(const jxo_shape* s, const float* llf_c, int by, int bx);
 void jxo_merge_tile(const jxo_frame* f, const float* xyb, const float* homog, int tx, int ty,
                     int max_s, float* ent, const int* raw, uint8_t* acs, const float cfl[2]);
+/* levels 128 / 256 px (s = 16 / 32 blocks) over the whole frame, after every
+ * tile's merge (regions span tiles; a candidate's chroma-from-luma factors
+ * are those of its top-left block's tile, as the decoder applies them) */
+void jxo_merge_big(const jxo_frame* f, const float* xyb, const float* homog, int s, float* ent,
+                   const int* raw, uint8_t* acs, const int8_t* cmap, uint32_t tiles_x,
+                   size_t ntiles);
 /* chroma from luma (front.c): the tile's int8 factors, and kx, kb from them */
 void jxo_cfl_tile(const jxo_frame* f, const float* xyb, int tx, int ty, int8_t* ytox,
                   int8_t* ytob);

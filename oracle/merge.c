@@ -46,6 +46,13 @@ const jxo_shape jxo_shapes[JXO_NSHAPES] = {
     {19, 8, 4, JXO_VK_64X32, 1.05f}, /* DCT64X32                  */
     {20, 4, 8, JXO_VK_64X32, 1.05f}, /* DCT32X64                  */
     {18, 8, 8, JXO_VK_64, 1.05f},   /* DCT64X64                   */
+    /* levels 128 / 256 (effort >= 8; cost multipliers extend the series) */
+    {22, 16, 8, JXO_VK_128X64, 1.07f},  /* DCT128X64                */
+    {23, 8, 16, JXO_VK_128X64, 1.07f},  /* DCT64X128                */
+    {21, 16, 16, JXO_VK_128, 1.07f},    /* DCT128X128               */
+    {25, 32, 16, JXO_VK_256X128, 1.09f}, /* DCT256X128              */
+    {26, 16, 32, JXO_VK_256X128, 1.09f}, /* DCT128X256              */
+    {24, 32, 32, JXO_VK_256, 1.09f},    /* DCT256X256               */
 };
 
 int jxo_shape_of(int type) {
@@ -55,10 +62,10 @@ int jxo_shape_of(int type) {
 }
 
 /* ---------------- tables (built once, double -> float) ---------------- */
-static float g_lee_c[7][32]; /* [log2 N][i], N = 2..64 */
-static float g_lee_s[7][64]; /* [log2 N][k], N = 1..64 */
-static float g_llf_p[4][8];  /* [log2 M][k]  M = 1..8 blocks */
-static float g_llf_ib[4][8][8]; /* [log2 M][n][k] inverse basis */
+static float g_lee_c[9][128]; /* [log2 N][i], N = 2..256 */
+static float g_lee_s[9][256]; /* [log2 N][k], N = 1..256 */
+static float g_llf_p[6][32];  /* [log2 M][k]  M = 1..32 blocks */
+static float g_llf_ib[6][32][32]; /* [log2 M][n][k] inverse basis */
 static jxo_vkind g_kinds[JXO_NVKINDS];
 static int g_init = 0;
 
@@ -99,10 +106,33 @@ static const double kBands[JXO_NVKINDS][3][8] = {
      {0.9 * 9311.3238710010046, -0.3041958212306401, -0.3633036457487539, -0.35660379990111464,
       -0.3443074455424403, -0.33699592683512467, -0.30180866526242109, -0.27321683125358037},
      {0.9 * 4992.2486445538634, -1.2, -1.2, -0.8, -0.7, -0.7, -0.4, -0.5}},
+    /* DCT128X64, DCT128X128, DCT256X128, DCT256X256: the bands of DCT64X32 /
+     * DCT64X64 with the first band scaled up with the transform size -- as
+     * recalled, parity with libjxl's defaults unpinned */
+    {{1.3 * 23629.073922049845, -1.025, -0.78, -0.65012, -0.19041574084286472, -0.20819395464,
+      -0.421064, -0.32733845535848671},
+     {1.3 * 8611.3238710010046, -0.3041958212306401, -0.3633036457487539, -0.35660379990111464,
+      -0.3443074455424403, -0.33699592683512467, -0.30180866526242109, -0.27321683125358037},
+     {1.3 * 4492.2486445538634, -1.2, -1.2, -0.8, -0.7, -0.7, -0.4, -0.5}},
+    {{1.7 * 26629.073922049845, -1.025, -0.78, -0.65012, -0.19041574084286472, -0.20819395464,
+      -0.421064, -0.32733845535848671},
+     {1.7 * 9311.3238710010046, -0.3041958212306401, -0.3633036457487539, -0.35660379990111464,
+      -0.3443074455424403, -0.33699592683512467, -0.30180866526242109, -0.27321683125358037},
+     {1.7 * 4992.2486445538634, -1.2, -1.2, -0.8, -0.7, -0.7, -0.4, -0.5}},
+    {{2.2 * 23629.073922049845, -1.025, -0.78, -0.65012, -0.19041574084286472, -0.20819395464,
+      -0.421064, -0.32733845535848671},
+     {2.2 * 8611.3238710010046, -0.3041958212306401, -0.3633036457487539, -0.35660379990111464,
+      -0.3443074455424403, -0.33699592683512467, -0.30180866526242109, -0.27321683125358037},
+     {2.2 * 4492.2486445538634, -1.2, -1.2, -0.8, -0.7, -0.7, -0.4, -0.5}},
+    {{3.0 * 26629.073922049845, -1.025, -0.78, -0.65012, -0.19041574084286472, -0.20819395464,
+      -0.421064, -0.32733845535848671},
+     {3.0 * 9311.3238710010046, -0.3041958212306401, -0.3633036457487539, -0.35660379990111464,
+      -0.3443074455424403, -0.33699592683512467, -0.30180866526242109, -0.27321683125358037},
+     {3.0 * 4992.2486445538634, -1.2, -1.2, -0.8, -0.7, -0.7, -0.4, -0.5}},
 };
-static const int kNumBands[JXO_NVKINDS] = {7, 7, 8, 8, 8, 8};
-static const int kKindDim[JXO_NVKINDS][2] = {{8, 16}, {16, 16}, {16, 32},
-                                             {32, 32}, {32, 64}, {64, 64}};
+static const int kNumBands[JXO_NVKINDS] = {7, 7, 8, 8, 8, 8, 8, 8, 8, 8};
+static const int kKindDim[JXO_NVKINDS][2] = {{8, 16},  {16, 16},  {16, 32},   {32, 32},  {32, 64},
+                                             {64, 64}, {64, 128}, {128, 128}, {128, 256}, {256, 256}};
 
 /* GetQuantWeights [ext]: bands -> weights over a rows x cols table */
 static void kind_weights(int kind, float* out3[3]) {
@@ -170,12 +200,12 @@ static void kind_order(int kind, uint16_t* nat /* [stored idx] -> position */) {
 static void init_tables(void) {
   if (g_init) return;
   const double pi = 3.14159265358979323846;
-  for (int l = 0; l < 7; l++) {
+  for (int l = 0; l < 9; l++) {
     const int N = 1 << l;
     for (int i = 0; i < N / 2; i++) g_lee_c[l][i] = (float)(1.0 / (2.0 * cos(pi * (2 * i + 1) / (2.0 * N))));
     for (int k = 0; k < N; k++) g_lee_s[l][k] = (float)(k ? sqrt(2.0) / N : 1.0 / N);
   }
-  for (int l = 0; l < 4; l++) {
+  for (int l = 0; l < 6; l++) {
     const int M = 1 << l;
     for (int k = 0; k < M; k++)
       g_llf_p[l][k] = (float)(cos(pi * k / (16.0 * M)) * cos(pi * k / (8.0 * M)) *
@@ -204,9 +234,12 @@ const jxo_vkind* jxo_vkinds(void) {
   init_tables();
   return g_kinds;
 }
-const float* jxo_lee_consts(void) { /* [7][32] then [7][64] (for the product's tables test) */
+const float* jxo_lee_consts(void) { /* [9][128] then [9][256] (for the product's tables test) */
   init_tables();
-  return &g_lee_c[0][0];
+  static float out[9 * 128 + 9 * 256];
+  memcpy(out, g_lee_c, sizeof(g_lee_c));
+  memcpy(out + 9 * 128, g_lee_s, sizeof(g_lee_s));
+  return out;
 }
 
 static int ilog2(int n) {
@@ -219,7 +252,7 @@ static int ilog2(int n) {
 static void lee(float* x, int N) {
   if (N == 1) return;
   const int h = N / 2, l = ilog2(N);
-  float a[32], b[32];
+  float a[128], b[128];
   for (int i = 0; i < h; i++) {
     a[i] = x[i] + x[N - 1 - i];
     b[i] = (x[i] - x[N - 1 - i]) * g_lee_c[l][i];
@@ -278,8 +311,8 @@ float jxo_varblock(const jxo_frame* f, const jxo_shape* s, const float* xyb, int
   const int R = 8 * s->cy, C = 8 * s->cx;
   const jxo_vkind* K = &g_kinds[s->kind];
   const size_t plane = (size_t)f->xp * f->yp;
-  static _Thread_local float F[3][64 * 64];
-  float tmp[64];
+  static _Thread_local float F[3][256 * 256];
+  float tmp[256];
   for (int c = 0; c < 3; c++) {
     const float* P = xyb + c * plane;
     for (int y = 0; y < R; y++) {
@@ -302,12 +335,12 @@ float jxo_varblock(const jxo_frame* f, const jxo_shape* s, const float* xyb, int
   int bits = 0, nz[3] = {0, 0, 0};
   static const int corder[3] = {1, 0, 2};
   const int rows_per_chunk = R < 16 ? R : 16;
-  static _Thread_local float yd[64 * 64];
+  static _Thread_local float yd[256 * 256];
   float pc[3] = {0.0f, 0.0f, 0.0f};
   for (int ci = 0; ci < 3; ci++) {
     const int c = corder[ci];
     for (int ch = 0; ch * rows_per_chunk < R; ch++) {
-      float part[64];
+      float part[256];
       for (int x = 0; x < C; x++) {
         float cp = 0.0f;
         for (int ky = ch * rows_per_chunk; ky < (ch + 1) * rows_per_chunk; ky++) {
@@ -346,21 +379,22 @@ float jxo_varblock(const jxo_frame* f, const jxo_shape* s, const float* xyb, int
   if (llf)
     for (int c = 0; c < 3; c++)
       for (int ky = 0; ky < s->cy; ky++)
-        for (int kx = 0; kx < s->cx; kx++) llf[(c * 8 + ky) * 8 + kx] = F[c][ky * C + kx];
+        for (int kx = 0; kx < s->cx; kx++)
+          llf[(c * JXO_LLF_DIM + ky) * JXO_LLF_DIM + kx] = F[c][ky * C + kx];
   return ((float)bits + 8.0f * dist) * s->tmul;
 }
 
 /* DC of covered block (by, bx) from the LLF [ext DCFromLowestFrequencies]:
  * t = (F * P_cy[ky]) * P_cx[kx]; u[ky] = sum_kx fmaf(t, IB_cx[bx][kx]);
  * dc = sum_ky fmaf(u[ky], IB_cy[by][ky]) */
-float jxo_llf_dc(const jxo_shape* s, const float* llf_c /* [8][8] */, int by, int bx) {
+float jxo_llf_dc(const jxo_shape* s, const float* llf_c /* [32][32] */, int by, int bx) {
   init_tables();
   const int ly = ilog2(s->cy), lx = ilog2(s->cx);
   float acc = 0.0f;
   for (int ky = 0; ky < s->cy; ky++) {
     float u = 0.0f;
     for (int kx = 0; kx < s->cx; kx++) {
-      const float t = (llf_c[ky * 8 + kx] * g_llf_p[ly][ky]) * g_llf_p[lx][kx];
+      const float t = (llf_c[ky * JXO_LLF_DIM + kx] * g_llf_p[ly][ky]) * g_llf_p[lx][kx];
       u = fmaf(t, g_llf_ib[lx][bx][kx], u);
     }
     acc = fmaf(u, g_llf_ib[ly][by][ky], acc);
@@ -373,9 +407,8 @@ float jxo_llf_dc(const jxo_shape* s, const float* llf_c /* [8][8] */, int by, in
 void jxo_merge_tile(const jxo_frame* f, const float* xyb, const float* homog, int tx, int ty,
                     int max_s, float* ent, const int* raw, uint8_t* acs, const float cfl[2]) {
   for (int s = 2; s <= max_s; s *= 2) {
-    const int full = s == 2 ? 2 : (s == 4 ? 5 : 8);      /* shape index */
-    const int tall = s == 2 ? 0 : (s == 4 ? 3 : 6);
-    const int wide = tall + 1;
+    const int L = s == 2 ? 0 : (s == 4 ? 1 : 2);
+    const int tall = 3 * L, wide = 3 * L + 1, full = 3 * L + 2; /* shape index */
     for (int ry = 0; ry < 8 / s; ry++)
       for (int rx = 0; rx < 8 / s; rx++) {
         const int bx0 = tx * 8 + rx * s, by0 = ty * 8 + ry * s;
@@ -431,6 +464,75 @@ void jxo_merge_tile(const jxo_frame* f, const float* xyb, const float* homog, in
             }
         }
       }
+  }
+}
+
+/* levels 128 / 256 px: every s x s region (s = 16 / 32 blocks) inside the
+ * frame -- the TryMergeAcs comparison of jxo_merge_tile over the decisions of
+ * the levels below (ent: the estimate of each varblock at its first block,
+ * 0 at covered blocks).  Regions are independent of each other within a
+ * level. */
+void jxo_merge_big(const jxo_frame* f, const float* xyb, const float* homog, int s, float* ent,
+                   const int* raw, uint8_t* acs, const int8_t* cmap, uint32_t tiles_x,
+                   size_t ntiles) {
+  const int L = s == 16 ? 3 : 4;
+  const int tall = 3 * L, wide = 3 * L + 1, full = 3 * L + 2;
+  const int nry = (int)f->bys / s, nrx = (int)f->bxs / s;
+#pragma omp parallel for schedule(dynamic)
+  for (int r = 0; r < nry * nrx; r++) {
+    const int bx0 = (r % nrx) * s, by0 = (r / nrx) * s;
+    float cur = 0.0f;
+    for (int iy = 0; iy < s; iy++)
+      for (int ix = 0; ix < s; ix++) cur += ent[(size_t)(by0 + iy) * f->bxs + bx0 + ix];
+    float e[5];
+    const int vs[5] = {full, tall, tall, wide, wide};
+    const int vx[5] = {0, 0, s / 2, 0, 0}, vy[5] = {0, 0, 0, 0, s / 2};
+    for (int i = 0; i < 5; i++) {
+      const jxo_shape* sh = &jxo_shapes[vs[i]];
+      const int bx = bx0 + vx[i], by = by0 + vy[i];
+      int rr = 0;
+      for (int iy = 0; iy < sh->cy; iy++)
+        for (int ix = 0; ix < sh->cx; ix++) {
+          const int v = raw[(size_t)(by + iy) * f->bxs + bx + ix];
+          rr = v > rr ? v : rr;
+        }
+      const size_t ti = (size_t)(by / 8) * tiles_x + bx / 8;
+      float cfl[2];
+      jxo_cfl_factors(cmap[ti], cmap[ntiles + ti], cfl);
+      e[i] = jxo_varblock(f, sh, xyb, bx * 8, by * 8, rr, NULL, NULL, NULL, cfl);
+      if (f->proposals & 2) {
+        const float* h = homog + 3 * ((size_t)by * f->bxs + bx);
+        e[i] = jxo_hook_f(e[i], h[0], h[1], h[2]);
+      }
+    }
+    const float et = e[1] + e[2], ew = e[3] + e[4];
+    float best = cur;
+    int choice = 0;
+    if (!(e[0] >= best)) {
+      best = e[0];
+      choice = 1;
+    }
+    if (!(et >= best)) {
+      best = et;
+      choice = 2;
+    }
+    if (!(ew >= best)) {
+      best = ew;
+      choice = 3;
+    }
+    if (!choice) continue;
+    const int first = choice == 1 ? 0 : (choice == 2 ? 1 : 3);
+    const int nv = choice == 1 ? 1 : 2;
+    for (int i = first; i < first + nv; i++) {
+      const jxo_shape* sh = &jxo_shapes[vs[i]];
+      const int bx = bx0 + vx[i], by = by0 + vy[i];
+      for (int iy = 0; iy < sh->cy; iy++)
+        for (int ix = 0; ix < sh->cx; ix++) {
+          const size_t b = (size_t)(by + iy) * f->bxs + bx + ix;
+          acs[b] = (uint8_t)(sh->type | ((iy | ix) ? 0x80 : 0));
+          ent[b] = (iy | ix) ? 0.0f : e[i];
+        }
+    }
   }
 }
 

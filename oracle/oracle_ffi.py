@@ -167,7 +167,8 @@ def srgb8_to_xyb(rgb: np.ndarray) -> np.ndarray:
     return out
 
 
-KIND_DIMS = [(8, 16), (16, 16), (16, 32), (32, 32), (32, 64), (64, 64)]
+KIND_DIMS = [(8, 16), (16, 16), (16, 32), (32, 32), (32, 64), (64, 64), (64, 128), (128, 128),
+             (128, 256), (256, 256)]
 
 
 def kind_tables(kind: int):

@@ -27,7 +27,7 @@ def smooth_rgb8(w, h, seed):
     return np.clip(img, 0, 255).astype(np.uint8)
 
 
-@pytest.mark.parametrize("n", [1, 2, 4, 8, 16, 32, 64])
+@pytest.mark.parametrize("n", [1, 2, 4, 8, 16, 32, 64, 128, 256])
 def test_lee_dct_matches_float64(oracle, n):
     rng = np.random.default_rng(n)
     x = rng.uniform(-1, 1, n).astype(np.float32)
@@ -38,7 +38,7 @@ def test_lee_dct_matches_float64(oracle, n):
     assert np.allclose(got, ref, atol=2e-6 * max(1, n / 8)), (got, ref)
 
 
-@pytest.mark.parametrize("kind", range(6))
+@pytest.mark.parametrize("kind", range(10))
 def test_kind_tables_match_decoder(oracle, decoder, kind):
     w, nat = oracle.kind_tables(kind)
     iw, order = decoder.kind_tables(kind)
@@ -116,3 +116,45 @@ def test_hook_f_nan_estimates_merge(oracle):
     assert np.isnan(rf.homog).all()
     assert rf.acs[0, 0] == 20 and rf.acs[4, 0] == 20
     assert ((rf.acs & 0x7F) == 20).all()
+
+
+def _gradient_rgb8(w, h, seed):
+    rng = np.random.default_rng(seed)
+    y, x = np.mgrid[0:h, 0:w].astype(np.float64)
+    img = np.stack([128 + 60 * np.sin(x / rng.uniform(150, 400) + y / rng.uniform(150, 400) + c)
+                    for c in range(3)], -1)
+    return np.clip(img, 0, 255).astype(np.uint8)
+
+
+@pytest.mark.parametrize("w,h,d", [(512, 512, 1.0), (768, 520, 2.0)])
+def test_big_varblocks_roundtrip(oracle, decoder, w, h, d):
+    """Effort 8 adds the 128 / 256 px levels (DCT128X128 / 128X64 / 64X128 /
+    256X256 / 256X128 / 128X256, raw ids 21-26; north_star's "2x2...256x256"):
+    on smooth content they are chosen, the decoder recovers every integer of
+    the codestream, and the RD note of DESIGN.md §3.10 holds (fewer bytes than
+    effort 7, PSNR within 0.5 dB)."""
+    import jxg
+
+    img = _gradient_rgb8(w, h, w + h)
+    r7 = oracle.encode(img, d, 7, 0, 1)
+    r8 = oracle.encode(img, d, 8, 0, 1)
+    first = r8.acs[(r8.acs & 0x80) == 0]
+    assert np.isin(first, [21, 22, 23, 24, 25, 26]).any()
+    assert not np.isin(r7.acs & 0x7F, [21, 22, 23, 24, 25, 26]).any()
+    dec = decoder.decode(r8.bytes)
+    for k in ("acs", "dc", "ac", "ac_tokens"):
+        assert np.array_equal(getattr(dec, k), getattr(r8, k)), k
+    p7 = jxg.calculate_psnr(jxg.calculate_mse(img, decoder.decode(r7.bytes).rgb))
+    p8 = jxg.calculate_psnr(jxg.calculate_mse(img, dec.rgb))
+    assert len(r8.bytes) < len(r7.bytes)
+    assert p8 > p7 - 0.5
+
+
+def test_every_big_shape_is_decodable(oracle, decoder):
+    """All six 128 / 256 px shapes appear across these frames and decode."""
+    seen = set()
+    for (w, h, d) in [(512, 512, 1.0), (768, 520, 2.0)]:
+        r = oracle.encode(_gradient_rgb8(w, h, w + h), d, 8, 0, 1)
+        seen |= set(int(t) for t in np.unique(r.acs[(r.acs & 0x80) == 0]))
+        assert np.array_equal(decoder.decode(r.bytes).ac, r.ac)
+    assert {21, 22, 23, 24, 25, 26} <= seen
