@@ -105,21 +105,28 @@ __device__ __forceinline__ void varblock_dims(int type, int& lcb, int& cx, int& 
     case 19: lcb = 5, cx = 4, cy = 8; break;  // 64x32
     case 20: lcb = 5, cx = 8, cy = 4; break;  // 32x64
     case 18: lcb = 6, cx = 8, cy = 8; break;  // 64x64
+    case 22: lcb = 7, cx = 8, cy = 16; break;   // 128x64 (effort >= 8)
+    case 23: lcb = 7, cx = 16, cy = 8; break;   // 64x128
+    case 21: lcb = 8, cx = 16, cy = 16; break;  // 128x128
+    case 25: lcb = 9, cx = 16, cy = 32; break;  // 256x128
+    case 26: lcb = 9, cx = 32, cy = 16; break;  // 128x256
+    case 24: lcb = 10, cx = 32, cy = 32; break; // 256x256
     default: lcb = 0, cx = 1, cy = 1; break;  // 8x8 class
   }
 }
 
 // ac_hist runs one 256-thread workgroup per BAND of a pass group: 8 block
-// rows (one row of 64x64 tiles) x 32 block columns.  Varblocks are aligned to
-// their size (<= 8 blocks) inside 64x64 tiles, so a band holds whole
+// rows (one row of 64x64 tiles) x 32 block columns.  Varblocks up to 64x64
+// are aligned to their size inside 64x64 tiles, so a band holds whole
 // varblocks, and the group's token stream (varblocks by first block raster)
 // is the concatenation of its four bands' streams: band j writes its records
 // at [j * kBandTokStride, ...) of the group's record space and its token
 // count to bandtok[g][j]; the coders read the group's stream through
 // rec_index (a 4-entry prefix).  Four workgroups per group give small frames
-// (1080p: 40 groups) 160 workgroups instead of 40.
-constexpr int kBandRows = 8, kBandBlocks = kBandRows * 32, kBands = 32 / kBandRows;
-constexpr int kHistThreads = kBandBlocks;
+// (1080p: 40 groups) 160 workgroups instead of 40.  At effort >= 8 varblocks
+// of 128 / 256 px span bands: the kernel then runs with BR = 32 (one
+// 1024-thread workgroup = one band = the whole group; bands 1-3 empty).
+constexpr int kBands = 4;  // bandtok entries per group (the coders' view)
 static_assert(kBands * kBandTokStride == kGroupTokStride, "band record spaces tile the group's");
 
 // record space index of stream position k of a group whose band counts are bt[4]
@@ -144,6 +151,7 @@ struct SliceTask {
   int bx, by, obx, oby, sl, lcb, cx, type;
   size_t gb, ogb;
 };
+// (BR: the band's block rows, 8 or 32; thread = block of the band)
 __device__ __forceinline__ SliceTask slice_task(const AcArgs& a, const GroupGeom& G, int y0) {
   SliceTask t;
   const int b = threadIdx.x;
@@ -166,11 +174,12 @@ __device__ __forceinline__ int block_of_slice(const SliceTask& t, int j, int y0)
   return (t.oby - y0 + j / t.cx) * 32 + t.obx + j % t.cx;
 }
 
+template <int BR>
 struct AcLds {
-  uint8_t nz[3][(kBandRows + 1) * 32];  // predicted-nz image, band rows and the row above
-  uint8_t snz[3][kBandBlocks];   // non-zeros of each slice (positions >= cb)
-  uint8_t last[3][kBandBlocks];  // last coefficient of the slice != 0
-  int8_t lastk[3][kBandBlocks];  // highest slice-local index >= cb - 64 sl holding a non-zero, or -1
+  uint8_t nz[3][(BR + 1) * 32];  // predicted-nz image, band rows and the row above
+  uint8_t snz[3][BR * 32];   // non-zeros of each slice (positions >= cb)
+  uint8_t last[3][BR * 32];  // last coefficient of the slice != 0
+  int8_t lastk[3][BR * 32];  // highest slice-local index >= cb - 64 sl holding a non-zero, or -1
 };
 // predicted non-zeros of group-local block (bx, by) from the band's nz image
 // (row 0 = the row above the band); neighbours inside the group only
@@ -184,8 +193,9 @@ __device__ __forceinline__ int predict_nz(const uint8_t* nzc, int bx, int by, in
 // tokens of task (t, c) without walking it: the walk runs from the slice's
 // first position >= cb up to the varblock's last non-zero K (1 + K for an
 // 8x8-class block), plus the non-zero count token on slice 0
+template <int BR>
 __device__ __forceinline__ uint32_t task_token_count(const AcArgs& a, const SliceTask& t,
-                                                     const AcLds& L, int c, int y0) {
+                                                     const AcLds<BR>& L, int c, int y0) {
   if (t.lcb == 0) {
     uint32_t w[32];
     load_coefs(a.ac + (t.gb * 3 + c) * 64, w);
@@ -205,11 +215,12 @@ __device__ __forceinline__ uint32_t task_token_count(const AcArgs& a, const Slic
 }
 
 // predicted-nz image (the band and the row above) and per-slice non-zero counts
+template <int BR>
 __device__ __forceinline__ void fill_slices(const AcArgs& a, const GroupGeom& G,
-                                            const SliceTask& t, AcLds& L, int y0) {
+                                            const SliceTask& t, AcLds<BR>& L, int y0) {
   const size_t nb = (size_t)a.bxs * a.bys;
-  for (int i = threadIdx.x; i < 3 * (kBandRows + 1) * 32; i += blockDim.x) {
-    const int c = i / ((kBandRows + 1) * 32), r = (i >> 5) % (kBandRows + 1), bx = i & 31;
+  for (int i = threadIdx.x; i < 3 * (BR + 1) * 32; i += blockDim.x) {
+    const int c = i / ((BR + 1) * 32), r = (i >> 5) % (BR + 1), bx = i & 31;
     const int by = y0 - 1 + r;
     if (bx < G.gw && by >= 0 && by < G.gh) {
       const size_t gb = (size_t)(G.by0 + by) * a.bxs + G.bx0 + bx;
@@ -240,8 +251,10 @@ __device__ __forceinline__ void fill_slices(const AcArgs& a, const GroupGeom& G,
 }
 
 // walk state of task (t, c) at its first coefficient; nz = varblock count
-__device__ __forceinline__ void slice_state(const AcArgs& a, const SliceTask& t, const AcLds& L,
-                                            int c, int y0, int& nz, int& left, int& prev) {
+template <int BR>
+__device__ __forceinline__ void slice_state(const AcArgs& a, const SliceTask& t,
+                                            const AcLds<BR>& L, int c, int y0, int& nz, int& left,
+                                            int& prev) {
   nz = a.nz[c * (size_t)a.bxs * a.bys + t.ogb];
   const int cb = 1 << t.lcb;
   left = nz;
@@ -252,7 +265,8 @@ __device__ __forceinline__ void slice_state(const AcArgs& a, const SliceTask& t,
   }
 }
 
-// workgroup (256 threads) exclusive scan; *total = sum of all values
+// workgroup (NT threads) exclusive scan; *total = sum of all values
+template <int NT>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sWave,
                                                     uint32_t* total) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -266,7 +280,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sWave,
   __syncthreads();
   uint32_t before = 0, all = 0;
 #pragma unroll
-  for (int i = 0; i < kHistThreads / 64; i++) {
+  for (int i = 0; i < NT / 64; i++) {
     const uint32_t x = sWave[i];
     before += i < wv ? x : 0u;
     all += x;
@@ -277,11 +291,13 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sWave,
 
 // The band's clustered histogram in LDS as u16 counts, two bins per word (a
 // band has at most 256 x 3 x 64 = 49152 tokens, so a half never carries)
-__global__ __launch_bounds__(kHistThreads) void ac_hist_kernel(Batch<AcArgs> bt_) {
+template <int BR>
+__global__ __launch_bounds__(BR * 32) void ac_hist_kernel(Batch<AcArgs> bt_) {
+  constexpr int kBandBlocks = BR * 32, kHistThreads = kBandBlocks, kWgBands = 32 / BR;
   const AcArgs& a = bt_.a[blockIdx.z];  // the batch's frame
   constexpr int kHistWords = kMaxClusters * kAcTok / 2;
   __shared__ uint32_t sHist[kHistWords];
-  __shared__ AcLds L;
+  __shared__ AcLds<BR> L;
   __shared__ uint8_t sClu[kAcCtx];
   __shared__ uint32_t sTask[3][kBandBlocks];  // tokens per (channel, slice task)
   __shared__ uint32_t sBase[kBandBlocks];     // first token of each varblock (first block)
@@ -289,10 +305,12 @@ __global__ __launch_bounds__(kHistThreads) void ac_hist_kernel(Batch<AcArgs> bt_
   __shared__ uint32_t sBound, sNtok[3];
   __shared__ uint16_t sNnzCtx[64];
   __shared__ uint8_t sFreqCtx[64];
-  const uint32_t slot = blockIdx.x / kBands, band = blockIdx.x % kBands;
+  const uint32_t slot = blockIdx.x / kWgBands, band = blockIdx.x % kWgBands;
   const int g = (int)slot_group(a.glist, a.g0, slot);
   const GroupGeom G = group_geom(a, g);
-  const int y0 = (int)band * kBandRows;
+  const int y0 = (int)band * BR;
+  if (BR == 32 && threadIdx.x > 0 && threadIdx.x < kBands)
+    a.bandtok[g * kBands + threadIdx.x] = 0;  // one band holds the whole group's stream
   if (y0 >= G.gh) {  // below a partial bottom group: an empty band
     if (threadIdx.x == 0) a.bandtok[g * kBands + band] = 0;
     return;
@@ -323,7 +341,7 @@ __global__ __launch_bounds__(kHistThreads) void ac_hist_kernel(Batch<AcArgs> bt_
       for (int j = 0; j < cb; j++) vtot += sTask[ci][block_of_slice(t, j, y0)];
   }
   uint32_t total;
-  const uint32_t off = block_excl_scan(vtot, sWave, &total);
+  const uint32_t off = block_excl_scan<kHistThreads>(vtot, sWave, &total);
   if (t.valid && t.sl == 0) sBase[me] = off;
   __syncthreads();
   // one walk: clustered histogram, bit bound, and every token's 32-bit record
@@ -347,7 +365,7 @@ __global__ __launch_bounds__(kHistThreads) void ac_hist_kernel(Batch<AcArgs> bt_
 #pragma unroll 1
   for (int ci = 0; ci < 3; ci++) {
     const int c = channel_of(ci);
-    uint32_t idx = 0, cnt = 0, info = 0, tok0 = 0;
+    uint32_t idx = 0, cnt = 0, info = 0, info2 = 0, tok0 = 0;
     if (t.valid) {
       uint32_t before = 0, chan_total = 0;
       for (int j = 0; j < cb; j++) {
@@ -361,9 +379,11 @@ __global__ __launch_bounds__(kHistThreads) void ac_hist_kernel(Batch<AcArgs> bt_
       int nz, left, prev;
       slice_state(a, t, L, c, y0, nz, left, prev);
       const int bctx = block_ctx_of(c, t.type);
-      // info: left (12 bits) | prev << 12 | lcb << 13 | sl << 16 | bctx << 22
-      info = (uint32_t)left | ((uint32_t)prev << 12) | ((uint32_t)t.lcb << 13) |
-             ((uint32_t)t.sl << 16) | ((uint32_t)bctx << 22);
+      // info: left (16 bits) | prev << 16 | lcb << 17 (4 bits) | bctx << 21;
+      // info2: the slice index (varblocks of up to 1024 blocks)
+      info = (uint32_t)left | ((uint32_t)prev << 16) | ((uint32_t)t.lcb << 17) |
+             ((uint32_t)bctx << 21);
+      info2 = (uint32_t)t.sl;
       if (t.sl == 0) {  // the non-zero count token, written by the task's own thread
         const int pred = predict_nz(L.nz[c], t.bx, t.by, y0);
         uint32_t tok, nb, bits;
@@ -401,8 +421,8 @@ __global__ __launch_bounds__(kHistThreads) void ac_hist_kernel(Batch<AcArgs> bt_
         const int j = js[u];
         const uint32_t ij = (uint32_t)__builtin_amdgcn_readlane((int)info, j);
         const uint32_t idxj = (uint32_t)__builtin_amdgcn_readlane((int)idx, j);
-        const int slj = (ij >> 16) & 63, lcbj = (ij >> 13) & 7;
-        const int leftj = ij & 4095, prevj = (ij >> 12) & 1, bctxj = ij >> 22;
+        const int slj = __builtin_amdgcn_readlane((int)info2, j), lcbj = (ij >> 17) & 15;
+        const int leftj = ij & 0xFFFF, prevj = (ij >> 16) & 1, bctxj = ij >> 21;
         const int cbj = 1 << lcbj;
         const int k = slj * 64 + lane;
         const int lo = max(slj * 64, cbj);
@@ -820,9 +840,12 @@ void launch_ans(const AnsArgs* a, uint32_t k, hipStream_t s) {
   if (nseg) hipLaunchKernelGGL(ans_emit_kernel, dim3(n, nseg, k), dim3(kEmitThreads), 0, s, b);
 }
 
-void launch_ac_hist(const AcArgs* a, uint32_t k, uint32_t ngroups, hipStream_t s) {
-  if (ngroups && k)
-    hipLaunchKernelGGL(ac_hist_kernel, dim3(ngroups * kBands, 1, k), dim3(kHistThreads), 0, s, make_batch(a, k));
+void launch_ac_hist(const AcArgs* a, uint32_t k, uint32_t ngroups, hipStream_t s, bool whole_group) {
+  if (!ngroups || !k) return;
+  if (whole_group)  // varblocks of 128 / 256 px (effort >= 8) span bands
+    hipLaunchKernelGGL(ac_hist_kernel<32>, dim3(ngroups, 1, k), dim3(1024), 0, s, make_batch(a, k));
+  else
+    hipLaunchKernelGGL(ac_hist_kernel<8>, dim3(ngroups * kBands, 1, k), dim3(256), 0, s, make_batch(a, k));
 }
 void launch_ac_emit(const AcArgs& a, uint32_t ngroups, hipStream_t s) {
   if (ngroups) hipLaunchKernelGGL(ac_emit_kernel, dim3(ngroups), dim3(kAcThreads), 0, s, a);

@@ -271,6 +271,12 @@ struct Ctx {
   DevBuf<int8_t> cmap;  // [2][tiles] chroma from luma (front kernel)
   DevBuf<uint16_t> nz, mnat;
   DevBuf<float> ent, mwk, msdk, miwy, xyb_tiles, mcost;
+  // merge levels 128 / 256 px (effort >= 8): tables (uploaded once), scratch
+  // planes of the persistent workgroups, candidate estimates, chosen list
+  DevBuf<float> big_tab, big_scratch, big_cost;
+  DevBuf<uint16_t> big_nat;
+  DevBuf<uint32_t> big_work;
+  bool big_ready = false;
   DevBuf<uint32_t> vb, mwork, xlist;
   DevBuf<uint8_t> lf_mine;  // shard: [nlf] owned LF groups (vb_list)
   DevBuf<int32_t> dc;
@@ -622,6 +628,8 @@ struct Job {
   FrontArgs fa{};
   AqArgs qa{};
   MergeArgs ma{};
+  BigArgs ba{};
+  bool big = false;  // merge levels 128 / 256 px (effort >= 8)
   VbArgs va{};
   AnsArgs na{};
   bool aq = false;  // masking quant field (aq_kernel before the front kernel)
@@ -957,6 +965,36 @@ static jxg_status build_front(Ctx* c, Job& J) {
     ma.work = c->mwork.p;
     ma.nwrite = 256 * 3 * 4;  // CUs x resident workgroups x 4
   }
+  // effort >= 8: the 128 / 256 px levels over the plan's pass groups
+  J.big = J.max_s && P.effort >= 8;
+  if (J.big) {
+    if (!c->big_ready) {
+      static const BigTables bt = build_big_tables();
+      JXG_HIP(c->big_tab.ensure(bt.tab.size()));
+      JXG_HIP(c->big_nat.ensure(bt.nat.size()));
+      JXG_HIP(hipMemcpyAsync(c->big_tab.p, bt.tab.data(), bt.tab.size() * 4, hipMemcpyHostToDevice, c->stream));
+      JXG_HIP(hipMemcpyAsync(c->big_nat.p, bt.nat.data(), bt.nat.size() * 2, hipMemcpyHostToDevice, c->stream));
+      c->big_ready = true;
+    }
+    const uint32_t ng = std::max(1u, J.plan.ng());
+    constexpr uint32_t kBigSlots = 256;  // persistent workgroups (one per CU)
+    JXG_HIP(c->big_scratch.ensure((size_t)kBigSlots * 2 * 65536));
+    JXG_HIP(c->big_cost.ensure((size_t)ng * 25));
+    JXG_HIP(c->big_work.ensure(1 + (size_t)ng * 16));
+    BigArgs& ba = J.ba;
+    ba = BigArgs{};
+    ba.m = J.ma;
+    ba.tab = c->big_tab.p;
+    ba.nat = c->big_nat.p;
+    ba.scratch = c->big_scratch.p;
+    ba.slots = kBigSlots;
+    ba.cost = c->big_cost.p;
+    ba.work = c->big_work.p;
+    ba.glist = J.plan.contiguous ? nullptr : c->glist.p;
+    ba.g0 = J.plan.g0();
+    ba.ng = J.plan.ng();
+    ba.gxs = f.gxs;
+  }
   J.va = VbArgs{c->acs.p, f.bxs, f.bys, f.lfxs, J.plan.world > 1 ? c->lf_mine.p : nullptr, c->vb.p,
                 c->vcount.p};
   return JXG_OK;
@@ -1036,11 +1074,25 @@ static jxg_status launch_transform(Ctx* const* cs, Job* const* js, uint32_t k) {
   if (J.max_s) {
     const auto ma = gather<MergeArgs>(js, k, [](Job& j) { return j.ma; });
     JXG_HIP(launch_merge(ma.data(), k, s));
+    if (J.big) {  // levels 128 / 256 px (effort >= 8)
+      const auto ba = gather<BigArgs>(js, k, [](Job& j) { return j.ba; });
+      JXG_HIP(launch_big(ba.data(), k, s));
+      // test hook: JXG_DEBUG_BIGCOST=path writes frame 0's candidate estimates
+      if (const char* dbg = std::getenv("JXG_DEBUG_BIGCOST")) {
+        std::vector<float> h((size_t)std::max(1u, J.plan.ng()) * 25);
+        JXG_HIP(hipMemcpyAsync(h.data(), ba[0].cost, h.size() * 4, hipMemcpyDeviceToHost, s));
+        JXG_HIP(hipStreamSynchronize(s));
+        if (FILE* fp = std::fopen(dbg, "wb")) {
+          std::fwrite(h.data(), 4, h.size(), fp);
+          std::fclose(fp);
+        }
+      }
+    }
   }
   for (uint32_t i = 0; i < k; i++) JXG_HIP(hipEventRecord(cs[i]->ev[1], s));
   // (the statistics arenas were zeroed by the front kernel)
   const auto aa = gather<AcArgs>(js, k, [](Job& j) { return j.aa; });
-  launch_ac_hist(aa.data(), k, J.plan.ng(), s);
+  launch_ac_hist(aa.data(), k, J.plan.ng(), s, J.big);
   JXG_HIP(hipGetLastError());
   return JXG_OK;
 }

@@ -100,6 +100,29 @@ struct MergeArgs {
   const int8_t* cmap;   // [2][tiles_all] chroma from luma (front kernel)
   uint32_t ntiles_all;
 };
+// merge levels 128 / 256 px (effort >= 8; jxg_bigvb.hip): kinds 64x128,
+// 128x128, 128x256, 256x256 (stored orientation rows <= cols), and the
+// layout of their table blob (floats): weights [3][n], distortion weights
+// [3][n], 1 / Y weight [n], Lee constants [9][128] / scales [9][256], LLF
+// scales [6][32] and inverse basis [6][32][32]; natural orders separately
+constexpr int kBigKindOff[5] = {0, 8192, 24576, 57344, 122880};
+constexpr size_t kBigTabW = 0, kBigTabSd = 3 * 122880, kBigTabIw = 6 * 122880,
+                 kBigTabLeeC = 7 * 122880, kBigTabLeeS = kBigTabLeeC + 9 * 128,
+                 kBigTabLlfP = kBigTabLeeS + 9 * 256, kBigTabLlfIb = kBigTabLlfP + 6 * 32,
+                 kBigTabFloats = kBigTabLlfIb + 6 * 32 * 32;
+struct BigArgs {
+  MergeArgs m;             // the frame's merge arguments (xyb tiles, maps, outputs)
+  const float* tab;        // kBigTab* blob
+  const uint16_t* nat;     // [kBigKindOff[4]] natural-order position per stored index
+  float* scratch;          // [slots][2][65536] coefficient planes (Y / dequantized Y, X then B)
+  uint32_t slots;          // persistent workgroups (one scratch slot each)
+  float* cost;             // [ng][25] candidate estimates (level 128: 4 x 5, level 256: 5)
+  uint32_t* work;          // [1 + ng * 16]: count, then first blocks of the chosen varblocks
+  const uint32_t* glist;   // the plan's pass groups: glist[i], or g0 + i
+  uint32_t g0, ng, gxs;
+};
+hipError_t launch_big(const BigArgs* a, uint32_t k, hipStream_t s);
+
 // per-LF-group varblock lists (AC metadata channel)
 struct VbArgs {
   const uint8_t* acs;
@@ -266,7 +289,10 @@ struct ScatterArgs {
 void launch_scatter(const ScatterArgs& a, uint32_t nwg, hipStream_t s);
 void launch_unpack(const PackArgs& a, hipStream_t s);  // records -> frame arrays
 void launch_homog(const HomogArgs& a, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s);
-void launch_ac_hist(const AcArgs* a, uint32_t k, uint32_t ngroups, hipStream_t s);
+// whole_group: one 1024-thread workgroup per group (varblocks of 128 / 256 px
+// span the 8-row bands; effort >= 8)
+void launch_ac_hist(const AcArgs* a, uint32_t k, uint32_t ngroups, hipStream_t s,
+                    bool whole_group = false);
 void launch_ac_emit(const AcArgs& a, uint32_t ngroups, hipStream_t s);
 void launch_lf_hist(const LfArgs* a, uint32_t k, uint32_t nchunks, hipStream_t s);
 void launch_lf_code(const LfArgs* a, uint32_t k, uint32_t nchunks, hipStream_t s);

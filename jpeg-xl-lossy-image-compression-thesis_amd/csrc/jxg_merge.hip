@@ -818,7 +818,10 @@ __global__ __launch_bounds__(64 * kResolveWaves) void merge_resolve_kernel(Batch
       }
       wave_sync_lds();
     }
-    if (in) a.acs[gb] = sAcs[t];
+    if (in) {
+      a.acs[gb] = sAcs[t];
+      a.ent[gb] = sEnt[t];  // the decisions' estimates: the 128 / 256 px levels' "current"
+    }
     // the shapes chosen somewhere in this tile
     if (in && !(sAcs[t] & 0x80)) {
 #pragma unroll

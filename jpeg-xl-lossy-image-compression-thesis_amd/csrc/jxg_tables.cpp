@@ -253,4 +253,94 @@ MergeTables build_merge_tables() {
   return T;
 }
 
+// DCT128X64, DCT128X128, DCT256X128, DCT256X256: the bands of DCT64X32 /
+// DCT64X64 with the first band scaled up with the size (== oracle/merge.c;
+// as recalled, parity with libjxl unpinned)
+BigTables build_big_tables() {
+  static const double kY32[3] = {23629.073922049845, 8611.3238710010046, 4492.2486445538634};
+  static const double kY64[3] = {26629.073922049845, 9311.3238710010046, 4992.2486445538634};
+  static const double kRest[3][7] = {
+      {-1.025, -0.78, -0.65012, -0.19041574084286472, -0.20819395464, -0.421064,
+       -0.32733845535848671},
+      {-0.3041958212306401, -0.3633036457487539, -0.35660379990111464, -0.3443074455424403,
+       -0.33699592683512467, -0.30180866526242109, -0.27321683125358037},
+      {-1.2, -1.2, -0.8, -0.7, -0.7, -0.4, -0.5}};
+  static const double kScale[4] = {1.3, 1.7, 2.2, 3.0};
+  static const int kDims[4][2] = {{64, 128}, {128, 128}, {128, 256}, {256, 256}};
+  BigTables T;
+  const size_t n = kBigKindOff[4];
+  T.tab.assign(kBigTabFloats, 0.0f);
+  T.nat.assign(n, 0);
+  for (int k = 0; k < 4; k++) {
+    const int rows = kDims[k][0], cols = kDims[k][1], nb = 8, off = kBigKindOff[k];
+    for (int c = 0; c < 3; c++) {
+      double bands[8];
+      bands[0] = kScale[k] * ((k & 1) ? kY64[c] : kY32[c]);
+      for (int i = 1; i < nb; i++) {
+        const double v = kRest[c][i - 1];
+        bands[i] = bands[i - 1] * (v > 0 ? 1.0 + v : 1.0 / (1.0 - v));
+      }
+      const double scale = (nb - 1) / (1.4142135623730951 + 1e-6);
+      const double rc = scale / (cols - 1), rr = scale / (rows - 1);
+      for (int y = 0; y < rows; y++)
+        for (int x = 0; x < cols; x++) {
+          const double dx = x * rc, dy = y * rr;
+          const double pos = std::sqrt(dx * dx + dy * dy);
+          int idx = (int)pos;
+          if (idx > nb - 2) idx = nb - 2;
+          const double frac = pos - idx;
+          const double a = bands[idx], b = bands[idx + 1];
+          const float w = (float)(a * std::pow(b / a, frac));
+          T.tab[kBigTabW + (size_t)c * n + off + y * cols + x] = w;
+          T.tab[kBigTabSd + (size_t)c * n + off + y * cols + x] = dist_weight(c, rows * cols, w);
+          if (c == 1) T.tab[kBigTabIw + off + y * cols + x] = 1.0f / w;
+        }
+    }
+    uint16_t* nat = &T.nat[off];
+    const int cs = rows / 8, cl = cols / 8, xf = cols / rows;
+    int cur = 0;
+    for (int y = 0; y < cs; y++)
+      for (int x = 0; x < cl; x++) nat[y * cols + x] = (uint16_t)cur++;
+    auto visit = [&](int x, int y, bool skip_llf) {
+      if (y % xf) return;
+      y /= xf;
+      if (skip_llf && x < cl && y < cs) return;
+      nat[y * cols + x] = (uint16_t)cur++;
+    };
+    for (int i = 0; i < cols; i++)
+      for (int j = 0; j <= i; j++) {
+        const bool odd = i & 1;
+        visit(odd ? i - j : j, odd ? j : i - j, true);
+      }
+    for (int ip = cols - 1; ip > 0; ip--) {
+      const int i = ip - 1;
+      for (int j = 0; j <= i; j++) {
+        const int x = cols - 1 - (i - j), y = cols - 1 - j;
+        const bool odd = i & 1;
+        visit(odd ? y : x, odd ? x : y, false);
+      }
+    }
+  }
+  const double pi = 3.14159265358979323846;
+  for (int l = 0; l < 9; l++) {
+    const int N = 1 << l;
+    for (int i = 0; i < N / 2; i++)
+      T.tab[kBigTabLeeC + l * 128 + i] = (float)(1.0 / (2.0 * std::cos(pi * (2 * i + 1) / (2.0 * N))));
+    for (int k = 0; k < N; k++)
+      T.tab[kBigTabLeeS + l * 256 + k] = (float)(k ? std::sqrt(2.0) / N : 1.0 / N);
+  }
+  for (int l = 0; l < 6; l++) {
+    const int M = 1 << l;
+    for (int k = 0; k < M; k++)
+      T.tab[kBigTabLlfP + l * 32 + k] = (float)(std::cos(pi * k / (16.0 * M)) *
+                                                std::cos(pi * k / (8.0 * M)) *
+                                                std::cos(pi * k / (4.0 * M)));
+    for (int nn = 0; nn < M; nn++)
+      for (int k = 0; k < M; k++)
+        T.tab[kBigTabLlfIb + (l * 32 + nn) * 32 + k] =
+            (float)(k ? std::sqrt(2.0) * std::cos(pi * (2 * nn + 1) * k / (2.0 * M)) : 1.0);
+  }
+  return T;
+}
+
 }  // namespace jxg

@@ -21,5 +21,12 @@ void quant_weights(float out[5][3][64]);
 void aq_erosion_weights(float distance, float w[4]);
 void srgb_lut(float lut[256]);
 MergeTables build_merge_tables();
+// the 128 / 256 px levels' tables (kBigTab* layout, jxg_kernels.h) and their
+// natural orders (== oracle/merge.c kinds 6-9)
+struct BigTables {
+  std::vector<float> tab;
+  std::vector<uint16_t> nat;
+};
+BigTables build_big_tables();
 
 }  // namespace jxg

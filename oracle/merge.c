@@ -472,6 +472,12 @@ void jxo_merge_tile(const jxo_frame* f, const float* xyb, const float* homog, in
  * the levels below (ent: the estimate of each varblock at its first block,
  * 0 at covered blocks).  Regions are independent of each other within a
  * level. */
+/* test hook: when set, every candidate estimate of the 128 / 256 px levels
+ * is stored at [group][25] (level 128: region r x 5 + candidate, level 256: 20
+ * + candidate), the layout of the product's big_cost arena */
+float* jxo_debug_big_cost = NULL;
+void jxo_set_debug_big_cost(float* p) { jxo_debug_big_cost = p; }
+
 void jxo_merge_big(const jxo_frame* f, const float* xyb, const float* homog, int s, float* ent,
                    const int* raw, uint8_t* acs, const int8_t* cmap, uint32_t tiles_x,
                    size_t ntiles) {
@@ -504,6 +510,11 @@ void jxo_merge_big(const jxo_frame* f, const float* xyb, const float* homog, int
         const float* h = homog + 3 * ((size_t)by * f->bxs + bx);
         e[i] = jxo_hook_f(e[i], h[0], h[1], h[2]);
       }
+    }
+    if (jxo_debug_big_cost) {
+      const size_t g = (size_t)(by0 / 32) * f->gxs + bx0 / 32;
+      const int o = s == 16 ? ((by0 % 32) / 16 * 2 + (bx0 % 32) / 16) * 5 : 20;
+      for (int i = 0; i < 5; i++) jxo_debug_big_cost[g * 25 + o + i] = e[i];
     }
     const float et = e[1] + e[2], ew = e[3] + e[4];
     float best = cur;

@@ -76,6 +76,8 @@ def lib():
         _lib.jxo_export_kind.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         _lib.jxo_export_kind.restype = ctypes.c_int
         _lib.jxo_export_dct.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        _lib.jxo_set_debug_big_cost.argtypes = [ctypes.c_void_p]
+        _lib.jxo_set_debug_big_cost.restype = None
         _lib.jxo_synth_rgb8.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,
                                         ctypes.c_void_p]
         _lib.jxo_set_threads.argtypes = [ctypes.c_int]
@@ -186,3 +188,17 @@ def dct(x: np.ndarray) -> np.ndarray:
     v = np.ascontiguousarray(x, dtype=np.float32).copy()
     lib().jxo_export_dct(v.ctypes.data, len(v))
     return v
+
+
+def debug_big_costs(rgb: np.ndarray, distance=1.0, effort=8, proposals=0, coder=0, filters=0):
+    """(result, [groups][25] candidate estimates of the 128 / 256 px levels)
+    -- the layout of the product's JXG_DEBUG_BIGCOST dump (test hook)"""
+    h, w, _ = rgb.shape
+    ng = ((w + 255) // 256) * ((h + 255) // 256)
+    buf = np.full(ng * 25, np.nan, dtype=np.float32)
+    lib().jxo_set_debug_big_cost(buf.ctypes.data)
+    try:
+        r = encode(rgb, distance, effort, proposals, coder, filters)
+    finally:
+        lib().jxo_set_debug_big_cost(None)
+    return r, buf.reshape(ng, 25)
