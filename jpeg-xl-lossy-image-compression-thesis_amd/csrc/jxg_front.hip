@@ -886,8 +886,79 @@ __device__ __forceinline__ float gab_src(const float* P, const float* R, int lx,
 // registers until every thread has read its inputs (one barrier), then
 // stored in place.  (Round 4 stored each row after a barrier of its own: 33
 // barriers per tile.)
+//
+// Interior tiles (every sample of the 68 x 68 window inside the padded frame:
+// 96 % of an 8K frame's tiles) take a clamp-free form of the same sweep: each
+// source column is one LDS column at a per-thread base (row offsets become
+// immediates), the two ring columns are read beside it and selected, and only
+// the first row (half 0) and the last row (half 1) come from the ring rows.
+__device__ __forceinline__ void gab_sweep_interior(float* sPix, const float* ring) {
+  const int t = threadIdx.x;
+  const bool act = t < 396;
+  const int half = t >= 198 ? 1 : 0, c = (t - 198 * half) / 66, lx = t % 66;
+  const int y0 = 33 * half;
+  float* P = sPix + c * kPlane;
+  const float* R = ring + c * kRing;
+  float out[33];
+  if (act) {
+    const bool ringL = lx == 0, ringR = lx == 65;
+    // column bases at row y0 (LDS) and the ring columns' bases at row y0
+    const int bL = (ringL ? 0 : lds_at(lx - 1, 0)) + y0 * kS, bM = lds_at(lx, 0) + y0 * kS;
+    const int bR = (ringR ? 0 : lds_at(lx + 1, 0)) + y0 * kS;
+    const int cL = 136 + y0, cR = 202 + y0;
+    // sample of column k at row y0 + d (d in [0, 33] for half 0, [-1, 32] for half 1)
+#define GAB_L(d) (ringL ? R[cL + (d)] : P[bL + (d) * kS])
+#define GAB_M(d) (P[bM + (d) * kS])
+#define GAB_R(d) (ringR ? R[cR + (d)] : P[bR + (d) * kS])
+    float n[3], m[3], sn[3];
+    if (half == 0) {  // row -1: the ring's top row
+      n[0] = R[lx];
+      n[1] = R[lx + 1];
+      n[2] = R[lx + 2];
+    } else {
+      n[0] = GAB_L(-1);
+      n[1] = GAB_M(-1);
+      n[2] = GAB_R(-1);
+    }
+    m[0] = GAB_L(0);
+    m[1] = GAB_M(0);
+    m[2] = GAB_R(0);
+#pragma unroll
+    for (int st = 0; st < 33; st++) {
+      if (st == 32 && half == 1) {  // row 66: the ring's bottom row
+        sn[0] = R[68 + lx];
+        sn[1] = R[69 + lx];
+        sn[2] = R[70 + lx];
+      } else {
+        sn[0] = GAB_L(st + 1);
+        sn[1] = GAB_M(st + 1);
+        sn[2] = GAB_R(st + 1);
+      }
+      const float s1 = (n[1] + sn[1]) + (m[0] + m[2]);
+      const float s2 = (n[0] + n[2]) + (sn[0] + sn[2]);
+      out[st] = (m[1] * kGabK0 + s1 * kGabK1) + s2 * kGabK2;
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        n[k] = m[k];
+        m[k] = sn[k];
+      }
+    }
+#undef GAB_L
+#undef GAB_M
+#undef GAB_R
+  }
+  __syncthreads();
+  if (act) {
+#pragma unroll
+    for (int st = 0; st < 33; st++) P[lds_at(lx, y0 + st)] = out[st];
+  }
+}
 __device__ __forceinline__ void gab_sweep(const FrontArgs& a, float* sPix, const float* ring,
                                           int ox, int oy) {
+  if (ox >= 1 && oy >= 1 && ox + 67 <= (int)a.xp && oy + 67 <= (int)a.yp) {  // (uniform)
+    gab_sweep_interior(sPix, ring);
+    return;
+  }
   const int t = threadIdx.x;
   const bool act = t < 396;
   const int half = t >= 198 ? 1 : 0, c = (t - 198 * half) / 66, lx = t % 66;

@@ -20,7 +20,11 @@ n = int(os.environ.get("N", "12"))
 t = synth_rgb8_device(7680, 4320, 0x4A584C02)
 torch.cuda.synchronize()
 lib = os.path.basename(os.environ.get("JXG_LIB_PATH", "") or "libjxg.so")
-for preset, flags in (("cjxl", jxg.FLAGS_CJXL_DEFAULTS), ("plain", jxg.FLAG_ANS)):
+ALL = {"cjxl": jxg.FLAGS_CJXL_DEFAULTS, "plain": jxg.FLAG_ANS,
+       "gab": jxg.FLAG_ANS | jxg.FLAG_GABORISH, "epf": jxg.FLAG_ANS | jxg.FLAG_EPF,
+       "aqm": jxg.FLAG_ANS | jxg.FLAG_AQ_MASKING}
+for preset in os.environ.get("PRESETS", "cjxl,plain").split(","):
+    flags = ALL[preset]
     with jxg.Encoder(distance=1.0, effort=7, flags=flags) as enc:
         rows, shas = [], set()
         for i in range(n + 2):
