@@ -10,7 +10,8 @@
 //   1. RGB8 -> X, Y (two cube roots; B is not needed) of the tile and a 5 px
 //      ring, coordinates clamped to the padded frame, into LDS;
 //   2. the pre-erosion cells (4x4) of the tile and a one-cell ring: thread =
-//      cell, its 16 gamma-weighted, masked neighbour differences;
+//      (cell, pixel column), its 4 gamma-weighted, masked neighbour
+//      differences, then a thread per cell sums the 4 columns;
 //   3. fuzzy erosion, thread = cell: the 4 smallest of the clamped 3 x 3
 //      neighbourhood, weighted;
 //   4. per block, 8 lanes = its pixel columns: HF and gamma sums over the
@@ -105,6 +106,7 @@ __global__ __launch_bounds__(kAqThreads) void aq_kernel(Batch<AqArgs> bt_) {
   __shared__ float sY[kAqR * kAqS];  // Y of the tile and its 5 px ring
   __shared__ float sX[64 * 65];      // X of the tile
   __shared__ float sCell[kAqC * kAqC];
+  __shared__ float sCol[kAqC * kAqC * 4];  // per cell: its 4 column sums
   __shared__ float sEro[16 * 16];
   __shared__ float sLut[256];
   const int tid = threadIdx.x;
@@ -148,20 +150,48 @@ __global__ __launch_bounds__(kAqThreads) void aq_kernel(Batch<AqArgs> bt_) {
     if (d >= 0.2f) d = 0.2f;
     return aq_masking_sqrt(d);
   };
-  // 2. pre-erosion cells: local (ci, cj) = global cell (16 tx - 1 + ci, 16 ty - 1 + cj)
+  // 2. pre-erosion cells: local (ci, cj) = global cell (16 tx - 1 + ci, 16 ty - 1 + cj);
+  // item = (cell, pixel column j): the column's 4 diffs from a vertical window
+  // (the sums in the oracle's order), then one thread per cell adds its columns.
+  // Tiles whose cells and their 1 px ring lie inside the padded frame read the
+  // region without clamps.
   const int ncx = xp / 4, ncy = yp / 4, cx0 = 16 * tx - 1, cy0 = 16 * ty - 1;
-  for (int i = tid; i < kAqC * kAqC; i += kAqThreads) {
-    const int gcx = cx0 + i % kAqC, gcy = cy0 + i / kAqC;
+  const bool inner = tx >= 1 && ty >= 1 && 16 * tx + 17 <= ncx && 16 * ty + 17 <= ncy &&
+                     64 * tx + 69 <= xp && 64 * ty + 69 <= yp;
+  for (int i = tid; i < kAqC * kAqC * 4; i += kAqThreads) {
+    const int cell = i >> 2, j = i & 3;
+    const int gcx = cx0 + cell % kAqC, gcy = cy0 + cell / kAqC;
     if (gcx < 0 || gcy < 0 || gcx >= ncx || gcy >= ncy) continue;
-    float col[4];
+    const int x = 4 * gcx + j, y = 4 * gcy;
+    float s;
+    if (inner) {  // (uniform) region-local rows y - 1 .. y + 4 of column x
+      const float* c0 = sY + (y - (oy - kAqRing)) * kAqS + x - (ox - kAqRing);
+      float up = c0[-kAqS], cc = c0[0];
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-      float s = diff(4 * gcx + j, 4 * gcy);
+      for (int r = 0; r < 4; r++) {
+        const float* cr = c0 + r * kAqS;
+        const float dn = cr[kAqS];
+        const float base = 0.25f * (((dn + up) + cr[-1]) + cr[1]);
+        const float gammac = aq_ratio<false>(cc + 0.019f);
+        float d = gammac * (cc - base);
+        d = d * d;
+        if (d >= 0.2f) d = 0.2f;
+        const float dv = aq_masking_sqrt(d);
+        s = r == 0 ? dv : s + dv;
+        up = cc;
+        cc = dn;
+      }
+    } else {
+      s = diff(x, y);
 #pragma unroll
-      for (int r = 1; r < 4; r++) s += diff(4 * gcx + j, 4 * gcy + r);
-      col[j] = s;
+      for (int r = 1; r < 4; r++) s += diff(x, y + r);
     }
-    sCell[i] = (((col[0] + col[1]) + col[2]) + col[3]) * 0.25f;
+    sCol[i] = s;
+  }
+  __syncthreads();
+  for (int i = tid; i < kAqC * kAqC; i += kAqThreads) {
+    const float* c = sCol + 4 * i;
+    sCell[i] = (((c[0] + c[1]) + c[2]) + c[3]) * 0.25f;
   }
   __syncthreads();
   // 3. fuzzy erosion of the tile's cells (neighbours clamped to the cell grid)
