@@ -332,8 +332,12 @@ class ShardStream:
          + TOC) -- the copies run on while it goes on; it marks frame k done
          once write_next of frame k + WRITE_LAG (or a flush) has returned.
     Rank 0's :meth:`receive` returns a zero-copy view of frame k's codestream
-    once every rank has marked it done (valid for the next S - 1 receives);
-    other ranks get None.  All ranks must run on one node (the shared
+    once every rank has marked it done; other ranks get None.  The view is
+    valid until the next receive -- for the next S - 1 receives while at most
+    jxg_pipeline_depth frames are kept pending (then every write happens in
+    receive).  A frame is written into slot k % S only once rank 0 has
+    released frame k - S (called receive for a later frame), so at most
+    depth + S - 2 frames may be pending: :meth:`submit` raises beyond.  All ranks must run on one node (the shared
     mapping); the partition must need no record exchange and the coder must
     be ANS when world > 1 (jxg_shard_submit_device refuses otherwise).
     `lanes` caps the rank's pipeline lanes (jxg_set_pipeline_lanes): for
@@ -356,7 +360,8 @@ class ShardStream:
         # codestream slot: 12 bpp + 1 MiB (a d1 8K frame is ~2 bpp); a frame
         # over it raises (pass slot_bytes)
         self.slot_bytes = slot_bytes or ((width * height * 3 // 2 + (1 << 20) + 4095) & ~4095)
-        self.meta_words = 2 * slots * world          # int64: published[S][W], done[S][W]
+        # int64: published[S][W], done[S][W], released (frames rank 0 is done with)
+        self.meta_words = 2 * slots * world + 1
         self.heads_off = 8 * self.meta_words
         self.data_off = (self.heads_off + 4 * slots * world * self.hcap + 4095) & ~4095
         self.host = SharedHostBuffer(rank, world, group)
@@ -364,13 +369,15 @@ class ShardStream:
         self.meta = np.frombuffer(self.host.mm, dtype=np.int64, count=self.meta_words)
         if rank == 0:
             self.meta[:] = -1
+            self.meta[-1] = 0
         dist.barrier(group=group)
         self.published = self.meta[:slots * world].reshape(slots, world)
-        self.done = self.meta[slots * world:].reshape(slots, world)
+        self.done = self.meta[slots * world:2 * slots * world].reshape(slots, world)
         self.heads = np.frombuffer(self.host.mm, dtype=np.uint32,
                                    count=slots * world * self.hcap,
                                    offset=self.heads_off).reshape(slots, world, self.hcap)
         self.max_pending = self.depth  # (more pending: submit writes the oldest out)
+        self.max_ahead = self.depth + slots - 2  # pending frames submit accepts
         self.submitted = 0   # frames submitted
         self.written = 0     # frames whose sections this rank has written
         self.received = 0    # frames returned by receive()
@@ -410,6 +417,9 @@ class ShardStream:
         until the frame is received).  When the library's lanes are all busy
         the oldest frame is written out first (its codestream is then taken by
         a later :meth:`receive`)."""
+        if self.submitted - self.received >= self.max_ahead:
+            raise RuntimeError("ShardStream: %d frames pending (at most depth + slots - 2 = "
+                               "%d): receive first" % (self.pending(), self.max_ahead))
         if self.submitted - self.written >= self.depth:
             self._write_one()
         self.enc.shard_submit_device(ptr, self.w, self.h, self.rank, self.world)
@@ -426,6 +436,9 @@ class ShardStream:
         if self.unmarked and self.unmarked[0] <= k - self.slots:
             self._mark()
         self._wait(lambda: bool((self.done[s] >= k - self.slots).all()), "slot %d" % s)
+        # ... and rank 0 must have released the frame it held (receive of a
+        # later frame): on rank 0 itself the submit bound guarantees it
+        self._wait(lambda: int(self.meta[-1]) > k - self.slots, "release of frame %d" % (k - self.slots))
         self.heads[s, r, :head.size] = head
         self.published[s, r] = k          # (x86: the head's stores are visible first)
         self._wait(lambda: bool((self.published[s] >= k).all()), "heads of frame %d" % k)
@@ -458,6 +471,8 @@ class ShardStream:
         k = self.received
         if k >= self.submitted:
             raise RuntimeError("ShardStream: nothing pending")
+        if self.rank == 0:
+            self.meta[-1] = k  # frames < k released (the view of k - 1 ends here)
         while self.written <= k:
             self._write_one()
         if self.unmarked and self.unmarked[0] <= k:

@@ -256,6 +256,57 @@ def streamed_shards(jxg_mod, ts, w, h, world, d=1.0, e=7, p=0, flags=None, lanes
     return outs
 
 
+def test_stream_shards_write_lag(jxg_mod):
+    """the JXG_SHARD_WRITE_LAG promise with no flush -- each
+    frame has its own host buffer, nothing is flushed until the end, and
+    frame k's buffer is checked as soon as write_next of frame k + LAG has
+    returned on every context (two contexts, two lanes each, so lane slots
+    and their write events are re-used)."""
+    import torch
+
+    from jxg.synth import synth_rgb8_device
+
+    w, h, world, n = 4096, 512, 2, 9
+    lag = 2  # include/jxg.h JXG_SHARD_WRITE_LAG
+    ts = [synth_rgb8_device(w, h, 0x1A6 + k) for k in range(n)]
+    ref = streamed_shards(jxg_mod, ts, w, h, world, lanes=2)
+    torch.cuda.synchronize()
+    encs = [jxg_mod.Encoder(flags=jxg_mod.FLAG_ANS) for _ in range(world)]
+    for enc in encs:
+        enc.set_pipeline_lanes(2)
+    depth = min(enc.pipeline_depth(w, h, r, world) for r, enc in enumerate(encs))
+    bufs, totals, checked = [], [], []
+
+    def take():
+        k = len(bufs)
+        heads = [enc.shard_next_head() for enc in encs]
+        buf = np.full(w * h * 2 + (1 << 20), 0xCD, dtype=np.uint8)
+        total = None
+        for enc in encs:
+            ok, t = enc.shard_write_next(heads, buf.ctypes.data, buf.size)
+            assert ok and (total is None or t == total)
+            total = t
+        bufs.append(buf)
+        totals.append(total)
+        if k >= lag:  # frame k - lag has landed on every context
+            j = k - lag
+            assert bufs[j][:totals[j]].tobytes() == ref[j], "frame %d not in place" % j
+            checked.append(j)
+
+    for t in ts:
+        for r, enc in enumerate(encs):
+            enc.shard_submit_device(t.data_ptr(), w, h, r, world)
+        if encs[0].pending() >= depth:
+            take()
+    while encs[0].pending():
+        take()
+    for enc in encs:
+        enc.shard_write_flush()
+        enc.close()
+    assert checked == list(range(n - lag))
+    assert [b[:t].tobytes() for b, t in zip(bufs, totals)] == ref
+
+
 @pytest.mark.parametrize("w,h,world,nframes", [(4096, 512, 2, 9), (8192, 512, 4, 5), (1100, 700, 1, 14)])
 def test_stream_shards_equal_one_at_a_time(jxg_mod, decoder, w, h, world, nframes):
     """Streamed shards (several frames in flight per rank, more than the
@@ -494,9 +545,12 @@ def _gloo_stream_rank(rank, world, port, result, nframes):
                 ref = [enc.encode_device(t.data_ptr(), w, h) for t in ts] if rank == 0 else None
             res[ans] = (dev, hst, ref)
         streams = {}
-        for cls in (ShardStream,):
+        for name, slots, ahead in (("ShardStream", 6, False), ("ahead", 3, True)):
+            # ahead: slots = 3 and frames submitted up to depth + slots - 2
+            # before each receive, so submit writes frames out (the write lag
+            # and the slot release between ranks on the path)
             with jxg.Encoder(flags=jxg.FLAG_ANS) as enc:
-                ss = cls(enc, w, h, rank, world)
+                ss = ShardStream(enc, w, h, rank, world, slots=slots, lanes=2 if ahead else None)
                 got = []
 
                 def take():  # a view is valid until the next receive: copy now
@@ -504,13 +558,20 @@ def _gloo_stream_rank(rank, world, port, result, nframes):
                     got.append(None if g is None else g.tobytes())
 
                 for t in ts:
+                    if ahead:
+                        if ss.pending() >= ss.max_ahead:
+                            take()
+                        ss.submit(t.data_ptr())
+                        continue
                     ss.submit(t.data_ptr())
                     while ss.pending() >= ss.max_pending or (ss.pending() and ss.ready()):
                         take()
+                if ahead:
+                    assert ss.written > ss.received  # submit wrote ahead of receive
                 while ss.pending():
                     take()
                 ss.close()
-            streams[cls.__name__] = got
+            streams[name] = got
         if rank == 0:
             result.put((res, streams))
     finally:
@@ -553,6 +614,7 @@ def test_multiprocess_streamed_frames(jxg_mod, decoder):
     dev, hst, ref = res[True]
     assert digests(dev) == digests(hst)
     assert digests(streams["ShardStream"]) == digests(dev)
+    assert digests(streams["ahead"]) == digests(dev)
     got = streams["ShardStream"]
     dr, dg = decoder.decode(ref[3]), decoder.decode(got[3])
     assert dg.npresets == 2

@@ -276,3 +276,82 @@ def test_shard_stream_rejects_too_few_slots(jxg_mod):
     for slots in range(0, jd.WRITE_LAG + 1):
         with pytest.raises(ValueError):
             jd.ShardStream(None, 64, 64, 0, 1, slots=slots)
+
+
+class _FakeShardEnc:
+    """Stands in for jxg.Encoder in ShardStream's protocol tests (no GPU):
+    frame k's codestream is 100 bytes of value k & 255, written synchronously
+    into the slot; the head is an empty version-1 head."""
+
+    def __init__(self, depth):
+        self.depth, self.sub, self.wrote = depth, 0, 0
+
+    def pipeline_depth(self, w, h, rank=0, world=1):
+        return self.depth
+
+    def shard_submit_device(self, ptr, w, h, rank, world):
+        assert self.sub - self.wrote < self.depth, "the library's lanes are full"
+        self.sub += 1
+
+    def shard_next_head(self):
+        h = np.zeros(7, dtype=np.uint32)
+        h[1] = 1
+        return h
+
+    def shard_write_next(self, heads, base, size):
+        import ctypes
+
+        ctypes.memmove(base, bytes([self.wrote & 255]) * 100, 100)
+        self.wrote += 1
+        return True, 100
+
+    def shard_write_flush(self):
+        pass
+
+
+def test_shard_stream_slot_release(jxg_mod, monkeypatch):
+    """Writing ahead of receive (submit past the library's depth): a frame
+    goes into slot k % slots only once rank 0 released frame k - slots, and
+    submit refuses more than depth + slots - 2 pending frames -- so a frame
+    whose codestream has not been received is never overwritten.  slots = 3
+    (the smallest accepted), depth 2, world 1 (gloo)."""
+    import socket
+
+    import pytest
+    import torch.distributed as dist
+
+    from jxg import dist as jd
+
+    class _NoPin:  # page-locking needs a HIP device: not part of the protocol
+        @staticmethod
+        def jxg_host_register(addr, size):
+            return 0
+
+        @staticmethod
+        def jxg_host_unregister(addr):
+            return 0
+
+    monkeypatch.setattr(jd, "load", lambda: _NoPin)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1)
+    try:
+        enc = _FakeShardEnc(depth=2)
+        ss = jd.ShardStream(enc, 64, 64, 0, 1, slots=3)
+        assert ss.max_ahead == 3
+        got = []
+        for k in range(3):  # frame 0 is written from submit (lanes full at 2)
+            ss.submit(0)
+        assert ss.written == 1 and ss.pending() == 3
+        with pytest.raises(RuntimeError, match="receive first"):
+            ss.submit(0)
+        for k in range(3, 12):
+            got.append(bytes(ss.receive()))
+            ss.submit(0)  # writes ahead: frame k - 1 while k - 2 is received
+        while ss.pending():
+            got.append(bytes(ss.receive()))
+        assert got == [bytes([k]) * 100 for k in range(12)]
+        ss.close()
+    finally:
+        dist.destroy_process_group()
