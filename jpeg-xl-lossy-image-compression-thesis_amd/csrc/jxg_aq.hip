@@ -110,8 +110,20 @@ __global__ __launch_bounds__(kAqThreads) void aq_kernel(Batch<AqArgs> bt_) {
   __shared__ float sEro[16 * 16];
   __shared__ float sLut[256];
   const int tid = threadIdx.x;
-  const int tile = a.tile_list ? (int)a.tile_list[blockIdx.x] : (int)blockIdx.x;
-  const int tx = tile % (int)a.tiles_x, ty = tile / (int)a.tiles_x;
+  // a whole frame: the front kernel's XCD-aware order (XCD x = workgroup % 8
+  // takes the column run [x run, (x + 1) run) of every tile row), so the
+  // lines of RGB8 rows neighbouring tiles share are L2 hits
+  int tx, ty;
+  if (a.tile_list) {
+    const int tile = (int)a.tile_list[blockIdx.x];
+    tx = tile % (int)a.tiles_x;
+    ty = tile / (int)a.tiles_x;
+  } else {
+    const int run = ((int)a.tiles_x + 7) >> 3, j = (int)(blockIdx.x >> 3);
+    ty = j / run;
+    tx = (int)(blockIdx.x & 7) * run + (j - ty * run);
+    if (tx >= (int)a.tiles_x) return;
+  }
   const int ox = tx * 64, oy = ty * 64;  // padded-frame coordinate of tile-local (0, 0)
   const int xp = (int)a.xp, yp = (int)a.yp;
   sLut[tid] = a.lut[tid];
@@ -269,7 +281,11 @@ __global__ __launch_bounds__(kAqThreads) void aq_kernel(Batch<AqArgs> bt_) {
 }
 
 void launch_aq(const AqArgs* a, uint32_t k, uint32_t ntiles, hipStream_t s) {
-  if (ntiles && k) hipLaunchKernelGGL(aq_kernel, dim3(ntiles, 1, k), dim3(kAqThreads), 0, s, make_batch(a, k));
+  if (!ntiles || !k) return;
+  // a list: one workgroup per listed tile; a whole frame: the XCD-aware grid
+  const uint32_t tiles_y = (a[0].bys + 7) / 8;
+  const uint32_t nwg = a[0].tile_list ? ntiles : 8 * ((a[0].tiles_x + 7) / 8) * tiles_y;
+  hipLaunchKernelGGL(aq_kernel, dim3(nwg, 1, k), dim3(kAqThreads), 0, s, make_batch(a, k));
 }
 
 }  // namespace jxg

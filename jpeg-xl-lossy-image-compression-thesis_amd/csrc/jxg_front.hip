@@ -1033,16 +1033,31 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
   __shared__ uint64_t sLapBits[64];
   const int tid = threadIdx.x;
   // a shard launches its own tiles through a list (1-D grid)
-  const int tile_id = a.tile_list ? (int)a.tile_list[blockIdx.x] : -1;
-  const int tx = tile_id >= 0 ? tile_id % (int)a.tiles_x : (int)blockIdx.x;
-  const int ty = tile_id >= 0 ? tile_id / (int)a.tiles_x : (int)blockIdx.y;
+  // A whole frame's tiles go in an XCD-aware order (1-D grid of 8 x run x
+  // tiles_y workgroups; workgroup w runs on XCD w % 8): XCD x takes the
+  // column run [x run, (x + 1) run) of every tile row, rows in order, so the
+  // 128-byte lines a tile's RGB8 rows share with its left / right / upper
+  // neighbours are L2 hits on the same XCD instead of fetches by another.
+  int tx, ty;
+  bool idle = false;
+  if (a.tile_list) {
+    const int tile_id = (int)a.tile_list[blockIdx.x];
+    tx = tile_id % (int)a.tiles_x;
+    ty = tile_id / (int)a.tiles_x;
+  } else {
+    const int run = ((int)a.tiles_x + 7) >> 3, j = (int)(blockIdx.x >> 3);
+    ty = j / run;
+    tx = (int)(blockIdx.x & 7) * run + (j - ty * run);
+    idle = tx >= (int)a.tiles_x;  // (the run of the last XCDs past the frame)
+  }
   const int ox = tx * kTile - 1, oy = ty * kTile - 1;
   if (a.zero) {  // the frame's statistics arena (the statistics kernels add into it)
-    const uint32_t nwg = gridDim.x * gridDim.y, wg = blockIdx.y * gridDim.x + blockIdx.x;
+    const uint32_t nwg = gridDim.x, wg = blockIdx.x;
     const uint32_t per = (a.zero_quads + nwg - 1) / nwg;
     for (uint32_t i = wg * per + tid; i < min(a.zero_quads, (wg + 1) * per); i += kThreads)
       a.zero[i] = make_uint4(0, 0, 0, 0);
   }
+  if (idle) return;
   if (tid < 256) {
     sLut[tid] = c_lut[tid];
     sBtab[tid] = c_btab[tid];
@@ -1438,10 +1453,11 @@ hipError_t set_front_constants(const float lut[256], const float wts[5][3][64], 
 void launch_front(const FrontArgs* a, uint32_t k, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s) {
   if (!k) return;
   const Batch<FrontArgs> b = make_batch(a, k);
+  const uint32_t nwg = 8 * ((tiles_x + 7) / 8) * tiles_y;  // XCD-aware order (front_kernel)
   if (a[0].proposals & 1u)
-    hipLaunchKernelGGL(front_kernel<true>, dim3(tiles_x, tiles_y, k), dim3(kThreads), 0, s, b);
+    hipLaunchKernelGGL(front_kernel<true>, dim3(nwg, 1, k), dim3(kThreads), 0, s, b);
   else
-    hipLaunchKernelGGL(front_kernel<false>, dim3(tiles_x, tiles_y, k), dim3(kThreads), 0, s, b);
+    hipLaunchKernelGGL(front_kernel<false>, dim3(nwg, 1, k), dim3(kThreads), 0, s, b);
 }
 void launch_front_list(const FrontArgs* a, uint32_t k, uint32_t ntiles, hipStream_t s) {
   if (!ntiles || !k) return;
