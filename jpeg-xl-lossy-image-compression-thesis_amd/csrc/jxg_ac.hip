@@ -718,8 +718,9 @@ __global__ __launch_bounds__(kAnsWaves * 64) void ans_encode_kernel(Batch<AnsArg
 // bits); and the section's scratch words zeroed (ans_emit ORs the two words a
 // segment shares with its neighbours; no arena memset).  Round 4 did this
 // bookkeeping inside the chain, on its serial path.
-constexpr int kSumThreads = 256;
+constexpr int kSumThreads = 1024;
 __global__ __launch_bounds__(kSumThreads) void ans_sums_kernel(Batch<AnsArgs> bt_) {
+  __shared__ uint32_t sC[kAnsMaxChunks];
   __shared__ uint32_t sTot[kSumThreads / 64];
   const AnsArgs& a = bt_.a[blockIdx.z];
   const uint32_t slot = blockIdx.x;
@@ -728,18 +729,39 @@ __global__ __launch_bounds__(kSumThreads) void ans_sums_kernel(Batch<AnsArgs> bt
   const uint32_t n = a.ntok[g * 3] + a.ntok[g * 3 + 1] + a.ntok[g * 3 + 2];
   const uint32_t K = (n + 63) / 64;
   const uint64_t b = (uint64_t)slot * kGroupTokStride;
-  uint32_t* csum = a.csum + (uint64_t)slot * kAnsMaxChunks;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint32_t tot = 0;
-  for (uint32_t q = (uint32_t)wv; q < K; q += kSumThreads / 64) {
-    const uint32_t lo = q == 0 ? 0u : n - 64u * (K - q), hi = n - 64u * (K - q - 1);
-    const uint32_t k = lo + (uint32_t)lane;
-    uint32_t l = k < hi ? (uint32_t)a.len[b + k] : 0u;
+  for (uint32_t q = threadIdx.x; q < K; q += kSumThreads) sC[q] = 0;
+  __syncthreads();
+  // chunk q = records [64 q - off, 64 q + 64 - off) clipped at 0 (chunks end
+  // at n); 16-byte words of the lengths: a chunk boundary can only fall at
+  // byte r = n % 16 of a word (n - 64 (K - q) = r mod 16), so a word's bytes
+  // below r go to one chunk and the rest to one chunk (LDS adds)
+  const uint32_t off = (64u - (n & 63u)) & 63u, r = n & 15u;
+  const uint4* L = reinterpret_cast<const uint4*>(a.len + b);
+  for (uint32_t w = threadIdx.x; w < (n + 15) / 16; w += kSumThreads) {
+    const uint4 v = L[w];
+    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+    const uint32_t valid = min(16u, n - 16u * w);
+    uint32_t lo = 0, hi = 0;
 #pragma unroll
-    for (int d = 32; d > 0; d >>= 1) l += __shfl_xor(l, d, 64);
-    if (lane == 0) csum[q] = l;
-    tot += l;
+    for (uint32_t j = 0; j < 16; j++) {
+      const uint32_t x = j < valid ? (d[j >> 2] >> (8 * (j & 3))) & 0xFFu : 0u;
+      if (j < r) lo += x;
+      else hi += x;
+    }
+    if (lo) atomicAdd(&sC[(16u * w + off) >> 6], lo);
+    if (hi) atomicAdd(&sC[(16u * w + r + off) >> 6], hi);
   }
+  __syncthreads();
+  uint32_t* csum = a.csum + (uint64_t)slot * kAnsMaxChunks;
+  uint32_t tot = 0;
+  for (uint32_t q = threadIdx.x; q < K; q += kSumThreads) {
+    const uint32_t c = sC[q];
+    csum[q] = c;
+    tot += c;
+  }
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) tot += __shfl_xor(tot, m, 64);
   if (lane == 0) sTot[wv] = tot;
   __syncthreads();
   uint32_t total = 32;

@@ -32,11 +32,11 @@
 
 #include "jxg_device.h"
 #include "jxg_kernels.h"
+#include "jxg_lee_tables.h"
 
 namespace jxg {
 
-constexpr int kBT = 1024;      // threads per workgroup
-constexpr int kLeeBuf = 2048;  // floats per Lee ping-pong buffer (a batch of rows / columns)
+constexpr int kBT = 512;  // threads per workgroup (two per CU)
 
 // shape index = level * 3 + {0 tall, 1 wide, 2 full}; level 0 = 128 px, 1 = 256 px
 struct BigShape {
@@ -47,95 +47,174 @@ constexpr BigShape kBig[6] = {{22, 4, 3, 0, 1.07f}, {23, 3, 4, 0, 1.07f}, {21, 4
                               {25, 5, 4, 2, 1.09f}, {26, 4, 5, 2, 1.09f}, {24, 5, 5, 3, 1.09f}};
 
 struct BigLds {
-  float buf[2][kLeeBuf];  // Lee ping-pong
   float part[4096];       // quantization: [chunk][column] partials
   float llf[3][32 * 32];  // write: the LLF (cy x cx) of each channel
+  float lee_c[9 * 128];   // the Lee tables (kBigTabLeeC / kBigTabLeeS), copied once per workgroup
+  float lee_s[9 * 256];
   float pc[3];
   int bits, nz[3], raw;
 };
 
 __device__ __forceinline__ int ilog2i(int n) { return 31 - __clz(n); }
 
-// Lee's DCT-II of `nrows` vectors of N (2..256) held in S.buf[0], breadth-
-// first; returns the buffer holding the unnormalized result
-__device__ __forceinline__ float* lee_batch(BigLds& S, int nrows, int N, const float* lee_c) {
-  const int L = ilog2i(N);
-  float* src = S.buf[0];
-  float* dst = S.buf[1];
-  for (int d = 0; d < L; d++) {  // split: segment n -> (sums | scaled differences)
-    const int n = N >> d, h = n >> 1, l = L - d;
-    const int half = N >> 1;
-    for (int t = threadIdx.x; t < nrows * half; t += kBT) {
-      const int row = t / half, i = t - row * half;
-      const int seg = i / h, j = i - seg * h;
-      const int s0 = row * N + seg * n;
-      const float x = src[s0 + j], y = src[s0 + n - 1 - j];
-      dst[s0 + j] = x + y;
-      dst[s0 + h + j] = (x - y) * lee_c[l * 128 + j];
+// unnormalized DCT-II in registers, Lee's recursive even/odd split (== the
+// oracle's lee; constants of jxg_lee_tables.h)
+template <int N>
+__device__ __forceinline__ void lee_reg(float* x) {
+  if constexpr (N > 1) {
+    constexpr int h = N / 2, l = N == 2 ? 1 : (N == 4 ? 2 : (N == 8 ? 3 : (N == 16 ? 4 : (N == 32 ? 5 : 6))));
+    float a[h], b[h];
+#pragma unroll
+    for (int i = 0; i < h; i++) {
+      a[i] = x[i] + x[N - 1 - i];
+      b[i] = (x[i] - x[N - 1 - i]) * kLeeC[l][i];
     }
-    __syncthreads();
-    float* tt = src;
-    src = dst;
-    dst = tt;
+    lee_reg<h>(a);
+    lee_reg<h>(b);
+#pragma unroll
+    for (int k = 0; k < h; k++) x[2 * k] = a[k];
+#pragma unroll
+    for (int k = 0; k < h - 1; k++) x[2 * k + 1] = b[k] + b[k + 1];
+    x[N - 1] = b[h - 1];
   }
-  for (int d = L - 2; d >= 0; d--) {  // recombine (segments of 2 are already in place)
-    const int n = N >> d, h = n >> 1;
-    for (int t = threadIdx.x; t < nrows * N; t += kBT) {
-      const int row = t / N, o = t - row * N;
-      const int seg = o / n, k = o - seg * n;
-      const int s0 = row * N + seg * n;
-      float out;
-      if (!(k & 1)) out = src[s0 + (k >> 1)];
-      else if (k < n - 1) out = src[s0 + h + (k >> 1)] + src[s0 + h + (k >> 1) + 1];
-      else out = src[s0 + n - 1];
-      dst[s0 + k] = out;
-    }
-    __syncthreads();
-    float* tt = src;
-    src = dst;
-    dst = tt;
-  }
-  return src;
 }
 
-// the candidate's channel ch (0 X, 1 Y, 2 B) from the tile-major XYB copy
-// into plane P (R x C, row-major): rows, then columns
-__device__ __forceinline__ void vb_transform(const MergeArgs& a, const float* tab, const BigShape& sh, int bx,
-                             int by, int ch, float* P, BigLds& S) {
+// One N-point transform (N = 64, 128, 256) of a vector, element p = ld(p),
+// spread over NP = N / 32 adjacent lanes (D = log2 NP split levels).  Lane
+// r of the group (bit d - 1 of r: s_d, the branch taken at split level d,
+// 0 the sums, 1 the scaled differences) evaluates its 32-point sub-vector
+// v_D[j] straight from the elements (each node u0 + u1 or (u0 - u1) c, the
+// recursion's float ops), runs Lee's 32-point DCT in registers, then the
+// recombinations upward: at the 64-point level the lane alone (odd outputs
+// b[k] + b[k + 1]); at the higher levels the b-child's values are spread
+// over the lanes r + 2^d (same k) and, for the last of them, r - 2^d rho_max
+// (k + 1): DPP-free shuffles (ds_bpermute).  Output k of lane r lands at
+// position k NP + r.
+template <int NN, int d, class Ld>
+__device__ __forceinline__ float vb_node(Ld ld, int i, int r, const BigLds& S) {
+  // v_d[i] of the sub-vector chosen by the low d bits of r (v_0 = x)
+  if constexpr (d == 0) {
+    return ld(i);
+  } else {
+    constexpr int n = NN >> (d - 1), l = n == 64 ? 6 : (n == 128 ? 7 : 8);
+    const float u0 = vb_node<NN, d - 1>(ld, i, r, S), u1 = vb_node<NN, d - 1>(ld, n - 1 - i, r, S);
+    const float c = l == 6 ? kLeeC[6][i] : S.lee_c[l * 128 + i];
+    return ((r >> (d - 1)) & 1) ? (u0 - u1) * c : u0 + u1;
+  }
+}
+template <int N, class Ld>
+__device__ __forceinline__ void vb_vec(Ld ld, int r, float* o, const BigLds& S) {
+  constexpr int NP = N / 32, D = NP == 2 ? 1 : (NP == 4 ? 2 : 3);
+#pragma unroll
+  for (int j = 0; j < 32; j++) {
+    o[j] = vb_node<N, D>(ld, j, r, S);
+    // (the scheduler keeps at most four vectors' leaves in flight: hoisting
+    // all 32 x NP leaf loads would spill)
+    if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+  }
+  lee_reg<32>(o);
+  // level D (64 points of v_{D-1}): the b-lanes' odd outputs, in-lane
+  const bool bD = (r >> (D - 1)) & 1;
+#pragma unroll
+  for (int k = 0; k < 31; k++) o[k] = bD ? o[k] + o[k + 1] : o[k];
+  // levels D - 1 .. 1: the b-child spread over 2^(D - d) lanes
+#pragma unroll
+  for (int d = D - 1; d >= 1; d--) {
+    const int lane = (int)(threadIdx.x & 63);
+    const int rho = r >> d, rmax = (1 << (D - d)) - 1;
+    const int src_same = lane + (1 << d);                 // rho + 1, same k
+    const int src_next = lane - (rho << d);               // rho 0, k + 1
+    const bool bl = (r >> (d - 1)) & 1;
+#pragma unroll
+    for (int k = 0; k < 32; k++) {
+      const float qs = __shfl(o[k], rho < rmax ? src_same : lane, 64);
+      const float qn = __shfl(o[k < 31 ? k + 1 : 31], src_next, 64);
+      // (selects, no branches: the last value of the last lane stays alone)
+      const float sum = o[k] + (rho < rmax ? qs : qn);
+      o[k] = bl && (rho < rmax || k < 31) ? sum : o[k];
+    }
+  }
+}
+
+// item i of a pass over the three channels' nv vectors -> (channel c, vector
+// v, lane r of its NP-lane group)
+template <int NP>
+__device__ __forceinline__ void pass_item(int i, int nv, int& c, int& v, int& r) {
+  r = i & (NP - 1);
+  const int u = i / NP;
+  c = u / nv;
+  v = u - c * nv;
+}
+
+// rows: the candidate's rows of the three channels from the tile-major XYB
+// copy into their planes (R x C, row-major; pl[c]: X, Y, B)
+template <int C>
+__device__ __forceinline__ void rows_pass(const MergeArgs& a, int bx, int by, int R, float* pl,
+                                          const BigLds& S) {
+  constexpr int NP = C / 32, L = C == 64 ? 6 : (C == 128 ? 7 : 8);
+  const int n = 3 * R * NP;
+  for (int base = 0; base < n; base += kBT) {
+    const int i = base + (int)threadIdx.x;
+    const bool act = i < n;
+    int c, y, r;
+    pass_item<NP>(act ? i : (i & (NP - 1)), R, c, y, r);  // (idle lanes: a valid row, not stored)
+    // pixel x of the row: tile (Y >> 6, (bx >> 3) + (x >> 6)), column x & 63
+    // (varblocks start on the 64-px grid); 32-bit offsets from the frame's XYB base
+    const int Y = by * 8 + y;
+    const uint32_t row0 = ((uint32_t)(Y >> 6) * a.tiles_x + (uint32_t)(bx >> 3)) * (3u * 4096u) +
+                          (uint32_t)(c * 4096 + (Y & 63) * 64);
+    const float* xyb = a.xyb;
+    float o[32];
+    vb_vec<C>([&](int x) { return xyb[row0 + (uint32_t)((x >> 6) * (3 * 4096) + (x & 63))]; }, r, o, S);
+    if (act) {  // column-major planes: coefficient (row y, column pos) at pos R + y
+      const uint32_t d0 = (uint32_t)c * 65536u + (uint32_t)y;
+#pragma unroll
+      for (int k = 0; k < 32; k++) {
+        const int pos = k * NP + r;
+        pl[d0 + (uint32_t)(pos * R)] = o[k] * S.lee_s[L * 256 + pos];
+      }
+    }
+  }
+}
+// columns, in place: every lane of a round computes before any stores
+template <int R>
+__device__ __forceinline__ void cols_pass(int C, float* pl, const BigLds& S) {
+  constexpr int NP = R / 32, L = R == 64 ? 6 : (R == 128 ? 7 : 8);
+  const int n = 3 * C * NP;
+  for (int base = 0; base < n; base += kBT) {
+    const int i = base + (int)threadIdx.x;
+    const bool act = i < n;
+    int c, x, r;
+    pass_item<NP>(act ? i : (i & (NP - 1)), C, c, x, r);
+    const uint32_t c0 = (uint32_t)c * 65536u + (uint32_t)(x * R);  // column x: R contiguous floats
+    float o[32];
+    vb_vec<R>([&](int p) { return pl[c0 + (uint32_t)p]; }, r, o, S);
+    __syncthreads();
+    if (act) {
+#pragma unroll
+      for (int k = 0; k < 32; k++) {
+        const int pos = k * NP + r;
+        pl[c0 + (uint32_t)pos] = o[k] * S.lee_s[L * 256 + pos];
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void vb_transform(const MergeArgs& a, const BigShape& sh, int bx, int by,
+                                             float* pl, const BigLds& S) {
   const int R = 8 << sh.lcy, C = 8 << sh.lcx;
-  const float* lee_c = tab + kBigTabLeeC;
-  const float* lee_s = tab + kBigTabLeeS;
-  const int lR = ilog2i(R), lC = ilog2i(C);
-  const int RB = kLeeBuf / C;
-  for (int y0 = 0; y0 < R; y0 += RB) {
-    for (int e = threadIdx.x; e < RB * C; e += kBT) {
-      const int r = e >> lC, x = e & (C - 1);
-      const int X = bx * 8 + x, Y = by * 8 + y0 + r;
-      const size_t tile = (size_t)(Y >> 6) * a.tiles_x + (X >> 6);
-      S.buf[0][e] = a.xyb[tile * (3 * 4096) + ch * 4096 + (Y & 63) * 64 + (X & 63)];
-    }
-    __syncthreads();
-    const float* o = lee_batch(S, RB, C, lee_c);
-    for (int e = threadIdx.x; e < RB * C; e += kBT) {
-      const int x = e & (C - 1);
-      P[(size_t)(y0 + (e >> lC)) * C + x] = o[e] * lee_s[lC * 256 + x];
-    }
-    __syncthreads();
+  switch (sh.lcx) {
+    case 3: rows_pass<64>(a, bx, by, R, pl, S); break;
+    case 4: rows_pass<128>(a, bx, by, R, pl, S); break;
+    default: rows_pass<256>(a, bx, by, R, pl, S); break;
   }
-  const int CB = kLeeBuf / R;
-  for (int x0 = 0; x0 < C; x0 += CB) {
-    for (int e = threadIdx.x; e < R * CB; e += kBT) {
-      const int y = e / CB, j = e - y * CB;
-      S.buf[0][j * R + y] = P[(size_t)y * C + x0 + j];
-    }
-    __syncthreads();
-    const float* o = lee_batch(S, CB, R, lee_c);
-    for (int e = threadIdx.x; e < R * CB; e += kBT) {
-      const int y = e / CB, j = e - y * CB;
-      P[(size_t)y * C + x0 + j] = o[j * R + y] * lee_s[lR * 256 + y];
-    }
-    __syncthreads();
+  __syncthreads();
+  switch (sh.lcy) {
+    case 3: cols_pass<64>(C, pl, S); break;
+    case 4: cols_pass<128>(C, pl, S); break;
+    default: cols_pass<256>(C, pl, S); break;
   }
+  __syncthreads();
 }
 
 // quantization of channel ch of the candidate (jxo_varblock's loop): S.bits,
@@ -157,21 +236,37 @@ __device__ __forceinline__ void vb_quant(const MergeArgs& a, const float* tab, c
   const uint16_t* NAT = natt + koff;
   const float inv_scale = 1.0f / scale;
   const int nch = R >> 4;
+  float* part = S.part;
   int bits = 0, nzc = 0;
   const size_t nb = (size_t)a.bxs * a.bys;
   for (int t = threadIdx.x; t < nch * C; t += kBT) {
     const int chunk = t >> lC, x = t & (C - 1);
     float cp = 0.0f;
-    for (int ky = chunk * 16; ky < chunk * 16 + 16; ky++) {
+    // the chunk's 16 coefficients, Y's dequantized values (X / B) or the
+    // inverse weights (Y) and the tables, loaded before the first use
+    for (int hh = 0; hh < 16; hh += 8) {
+    float pv[8], yv[8], wv[8], sdv[8];
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+      const int ky = chunk * 16 + hh + r;
+      const int si = C >= R ? ky * C + x : x * R + ky;
+      pv[r] = P[(size_t)x * R + ky];  // column-major planes
+      yv[r] = ch != 1 ? Yp[(size_t)x * R + ky] : IW[si];  // Y: the inverse weight
+      wv[r] = W[si];
+      sdv[r] = SD[si];
+    }
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+      const int ky = chunk * 16 + hh + r;
       const int si = C >= R ? ky * C + x : x * R + ky;
       float qq_f = 0.0f;
       bool neg = false;
       if (ky < cy && x < cx) {  // LLF: carried by the DC image
-        if (WRITE) S.llf[ch][ky * 32 + x] = P[(size_t)ky * C + x];
+        if (WRITE) S.llf[ch][ky * 32 + x] = pv[r];
       } else {
-        const float w = W[si];
-        float rv = P[(size_t)ky * C + x];
-        if (ch != 1) rv = rv - kc * Yp[(size_t)ky * C + x];
+        const float w = wv[r];
+        float rv = pv[r];
+        if (ch != 1) rv = rv - kc * yv[r];
         const float v = rv * (w * scale);
         const float av = fabsf(v);
         const float qf = av < 0.58f ? 0.0f : floorf(fminf(av, 32767.0f) + 0.5f);
@@ -179,9 +274,9 @@ __device__ __forceinline__ void vb_quant(const MergeArgs& a, const float* tab, c
         if (ch == 1) {
           float adj = qa == 0 ? 0.0f : (qa == 1 ? kBias1 : qf - 0.145f / qf);
           if (v < 0.0f) adj = -adj;
-          P[(size_t)ky * C + x] = adj * (IW[si] * inv_scale);
+          P[(size_t)x * R + ky] = adj * (yv[r] * inv_scale);
         }
-        const float e = (av - qf) * SD[si];
+        const float e = (av - qf) * sdv[r];
         cp = fmaf(e, e, cp);
         if (qa) {
           bits += 2 + 2 * (32 - __clz((uint32_t)qa));
@@ -198,34 +293,35 @@ __device__ __forceinline__ void vb_quant(const MergeArgs& a, const float* tab, c
         a.ac[(gb * 3 + ch) * 64 + (p & 63)] = (int16_t)q;
       }
     }
-    S.part[t] = cp;
+    }
+    part[t] = cp;
   }
   (void)nb;
   if (bits) atomicAdd(&S.bits, bits);
   if (nzc) atomicAdd(&S.nz[ch], nzc);
   __syncthreads();
   // a chunk's column partials: pairwise tree over its C columns (tree_sum)
-  for (int st = 1; st < C; st <<= 1) {
-    const int per = C / (2 * st);
-    for (int t = threadIdx.x; t < nch * per; t += kBT) {
-      const int chunk = t / per, i = chunk * C + (t - chunk * per) * 2 * st;
-      S.part[i] = S.part[i] + S.part[i + st];
+  for (int ls = 0; ls < lC; ls++) {
+    const int st = 1 << ls, lper = lC - 1 - ls;  // per = C / (2 st) pairs per chunk
+    for (int t = threadIdx.x; t < (nch << lper); t += kBT) {
+      const int chunk = t >> lper, i = (chunk << lC) + ((t & ((1 << lper) - 1)) << (ls + 1));
+      part[i] = part[i] + part[i + st];
     }
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    float pc = S.part[0];
-    for (int k = 1; k < nch; k++) pc = pc + S.part[k * C];
+    float pc = part[0];
+    for (int k = 1; k < nch; k++) pc = pc + part[k * C];
     S.pc[ch] = pc;
   }
   __syncthreads();
 }
 
-// transform + quantization of one candidate (scratch slot: planes Yp, Xp);
+// transform + quantization of one candidate (scratch slot: planes X, Y, B);
 // returns the estimate (thread 0's value is the one used)
 template <bool WRITE>
 __device__ __forceinline__ float vb_eval(const BigArgs& b, const BigShape& sh, int bx, int by, BigLds& S,
-                         float* Yp, float* Xp) {
+                                         float* pl) {
   const MergeArgs& a = b.m;
   const int cy = 1 << sh.lcy, cx = 1 << sh.lcx;
   if (threadIdx.x == 0) {
@@ -239,18 +335,16 @@ __device__ __forceinline__ float vb_eval(const BigArgs& b, const BigShape& sh, i
   for (int i = threadIdx.x; i < cy * cx; i += kBT)
     r = max(r, (int)a.qf[(size_t)(by + (i >> sh.lcx)) * a.bxs + bx + (i & (cx - 1))] + 1);
   if (r) atomicMax(&S.raw, r);
-  __syncthreads();
+  vb_transform(a, sh, bx, by, pl, S);  // (ends with a barrier)
   const float scale = (float)a.G * (float)S.raw / 65536.0f;
   // chroma from luma of the top-left block's tile (as the decoder applies it)
   const size_t tile = (size_t)(by >> 3) * a.tiles_x + (bx >> 3);
   const float kx = (float)a.cmap[tile] * (1.0f / 84.0f);
   const float kb = 1.0f + (float)a.cmap[a.ntiles_all + tile] * (1.0f / 84.0f);
-  vb_transform(a, b.tab, sh, bx, by, 1, Yp, S);
+  float* Yp = pl + 65536;  // planes: X, Y, B
   vb_quant<WRITE>(a, b.tab, b.nat, sh, bx, by, 1, Yp, Yp, scale, 0.0f, S);
-  vb_transform(a, b.tab, sh, bx, by, 0, Xp, S);
-  vb_quant<WRITE>(a, b.tab, b.nat, sh, bx, by, 0, Xp, Yp, scale, kx, S);
-  vb_transform(a, b.tab, sh, bx, by, 2, Xp, S);
-  vb_quant<WRITE>(a, b.tab, b.nat, sh, bx, by, 2, Xp, Yp, scale, kb, S);
+  vb_quant<WRITE>(a, b.tab, b.nat, sh, bx, by, 0, pl, Yp, scale, kx, S);
+  vb_quant<WRITE>(a, b.tab, b.nat, sh, bx, by, 2, pl + 2 * 65536, Yp, scale, kb, S);
   const float dist = (S.pc[1] + S.pc[0]) + S.pc[2];
   const int tb = S.bits + (32 - __clz((uint32_t)S.nz[0])) + (32 - __clz((uint32_t)S.nz[1])) +
                  (32 - __clz((uint32_t)S.nz[2]));
@@ -282,14 +376,22 @@ __device__ __forceinline__ const BigShape& big_cand(int L, int j, int bx0, int b
 }
 constexpr int kBigCost = 25;  // per group slot: level 128 (4 regions x 5), level 256 (5)
 
-__global__ __launch_bounds__(kBT) void big_eval_kernel(Batch<BigArgs> bt_, int L) {
+// the Lee tables into LDS (once per workgroup; the transforms read them per
+// element and stage)
+__device__ __forceinline__ void load_lee_tables(const float* tab, BigLds& S) {
+  for (int i = threadIdx.x; i < 9 * 128; i += kBT) S.lee_c[i] = tab[kBigTabLeeC + i];
+  for (int i = threadIdx.x; i < 9 * 256; i += kBT) S.lee_s[i] = tab[kBigTabLeeS + i];
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(4))) void big_eval_kernel(Batch<BigArgs> bt_, int L) {
   const BigArgs& b = bt_.a[blockIdx.z];
   __shared__ BigLds S;
   if (L == 0 && blockIdx.x == 0 && threadIdx.x == 0) b.work[0] = 0;  // big_list's count
   const int nreg = L == 0 ? 4 : 1;
   const uint32_t total = b.ng * (uint32_t)nreg * 5u;
-  float* Yp = b.scratch + (size_t)blockIdx.x * 2 * 65536;
-  float* Xp = Yp + 65536;
+  float* const pl = b.scratch + (size_t)blockIdx.x * kBigPlanes;  // X, Y, B planes
+  load_lee_tables(b.tab, S);
   for (uint32_t w = blockIdx.x; w < total; w += gridDim.x) {
     const uint32_t gi = w / (nreg * 5), rem = w - gi * (nreg * 5);
     const int r = (int)rem / 5, j = (int)rem % 5;
@@ -297,7 +399,7 @@ __global__ __launch_bounds__(kBT) void big_eval_kernel(Batch<BigArgs> bt_, int L
     if (!big_region(b, L, gi, r, bx0, by0)) continue;  // (uniform)
     int bx, by;
     const BigShape& sh = big_cand(L, j, bx0, by0, bx, by);
-    const float e = vb_eval<false>(b, sh, bx, by, S, Yp, Xp);
+    const float e = vb_eval<false>(b, sh, bx, by, S, pl);
     if (threadIdx.x == 0) b.cost[(size_t)gi * kBigCost + (L == 0 ? r * 5 + j : 20 + j)] = e;
     __syncthreads();
   }
@@ -364,14 +466,14 @@ __global__ __launch_bounds__(64) void big_list_kernel(Batch<BigArgs> bt_) {
   if (t >= 21 && t <= 26) b.work[1 + atomicAdd(b.work, 1u)] = gb;
 }
 
-__global__ __launch_bounds__(kBT) void big_write_kernel(Batch<BigArgs> bt_) {
+__global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(4))) void big_write_kernel(Batch<BigArgs> bt_) {
   const BigArgs& b = bt_.a[blockIdx.z];
   const MergeArgs& a = b.m;
   __shared__ BigLds S;
-  float* Yp = b.scratch + (size_t)blockIdx.x * 2 * 65536;
-  float* Xp = Yp + 65536;
+  float* const pl = b.scratch + (size_t)blockIdx.x * kBigPlanes;  // X, Y, B planes
   const uint32_t n = __builtin_amdgcn_readfirstlane(*(volatile uint32_t*)b.work);
   const size_t nb = (size_t)a.bxs * a.bys;
+  if (blockIdx.x < n) load_lee_tables(b.tab, S);
   for (uint32_t w = blockIdx.x; w < n; w += gridDim.x) {
     const uint32_t gb0 = b.work[1 + w];
     const int bx = (int)(gb0 % a.bxs), by = (int)(gb0 / a.bxs);
@@ -379,7 +481,7 @@ __global__ __launch_bounds__(kBT) void big_write_kernel(Batch<BigArgs> bt_) {
     int si = 0;
     for (int i = 0; i < 6; i++) si = kBig[i].type == t ? i : si;
     const BigShape& sh = kBig[si];
-    (void)vb_eval<true>(b, sh, bx, by, S, Yp, Xp);
+    (void)vb_eval<true>(b, sh, bx, by, S, pl);
     // per covered block: non-zero counts, quant field, DC from the LLF
     const int lcy = sh.lcy, lcx = sh.lcx, cy = 1 << lcy, cx = 1 << lcx, lcb = lcy + lcx;
     const float* llf_p = b.tab + kBigTabLlfP;

@@ -977,8 +977,7 @@ static jxg_status build_front(Ctx* c, Job& J) {
       c->big_ready = true;
     }
     const uint32_t ng = std::max(1u, J.plan.ng());
-    constexpr uint32_t kBigSlots = 256;  // persistent workgroups (one per CU)
-    JXG_HIP(c->big_scratch.ensure((size_t)kBigSlots * 2 * 65536));
+    JXG_HIP(c->big_scratch.ensure((size_t)kBigSlots * kBigPlanes));
     JXG_HIP(c->big_cost.ensure((size_t)ng * 25));
     JXG_HIP(c->big_work.ensure(1 + (size_t)ng * 16));
     BigArgs& ba = J.ba;

@@ -106,6 +106,8 @@ struct MergeArgs {
 // [3][n], 1 / Y weight [n], Lee constants [9][128] / scales [9][256], LLF
 // scales [6][32] and inverse basis [6][32][32]; natural orders separately
 constexpr int kBigKindOff[5] = {0, 8192, 24576, 57344, 122880};
+constexpr uint32_t kBigSlots = 512;          // persistent workgroups of the 128 / 256 px levels (two per CU)
+constexpr size_t kBigPlanes = 3 * 65536;     // floats of a slot's scratch: X, Y, B planes of up to 256 x 256
 constexpr size_t kBigTabW = 0, kBigTabSd = 3 * 122880, kBigTabIw = 6 * 122880,
                  kBigTabLeeC = 7 * 122880, kBigTabLeeS = kBigTabLeeC + 9 * 128,
                  kBigTabLlfP = kBigTabLeeS + 9 * 256, kBigTabLlfIb = kBigTabLlfP + 6 * 32,

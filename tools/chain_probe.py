@@ -25,7 +25,7 @@ ALL = {"cjxl": jxg.FLAGS_CJXL_DEFAULTS, "plain": jxg.FLAG_ANS,
        "aqm": jxg.FLAG_ANS | jxg.FLAG_AQ_MASKING}
 for preset in os.environ.get("PRESETS", "cjxl,plain").split(","):
     flags = ALL[preset]
-    with jxg.Encoder(distance=1.0, effort=7, flags=flags) as enc:
+    with jxg.Encoder(distance=1.0, effort=int(os.environ.get("EFFORT", "7")), flags=flags) as enc:
         rows, shas = [], set()
         for i in range(n + 2):
             b = enc.encode_device(t.data_ptr(), 7680, 4320)
