@@ -14,20 +14,24 @@
 //
 // A varblock of up to 256 x 256 coefficients per channel does not fit the
 // LDS image the tile kernels use, so the planes live in a per-workgroup
-// global scratch slot (persistent workgroups, L2-resident for the 128 level):
-//   transform  rows, then columns, in batches through LDS: Lee's recursive
-//              DCT evaluated breadth-first (every split stage over all rows
-//              of the batch, then every recombination stage) -- the same
-//              float ops as the recursion, in another order, so bit-identical;
-//   quantize   Y first (its dequantized values replace its coefficients for
-//              the X / B residuals), then X, then B transformed into X's
-//              plane; item = (16-row chunk, column): fmaf(e, e) over the
-//              chunk's rows ascending, the chunk's column partials tree-summed
-//              pairwise, chunks in order, dist = (Y + X) + B.
-// Kernels: big_eval (one candidate varblock per task), big_resolve (one
-// thread per region), big_list (the chosen big varblocks), big_write
-// (transform + quantization + coefficients / non-zero counts / quant field /
-// LLF-derived DC of every covered block).
+// global scratch slot (512 persistent workgroups, three column-major planes):
+//   transform  Y first, then X and B: rows from the tile-major XYB copy, then
+//              columns in place, one 32-point Lee DCT per lane in registers
+//              (a vector of 64 / 128 / 256 points over 2 / 4 / 8 adjacent
+//              lanes: the first splits evaluated from the elements, the upper
+//              recombinations by lane shuffles) -- the recursion's float ops;
+//   quantize   Y (its dequantized values replace its coefficients for the X
+//              / B residuals), then X and B; item = (16-row chunk, column):
+//              fmaf(e, e) over the chunk's rows ascending, the chunk's column
+//              partials tree-summed pairwise, chunks in order,
+//              dist = (Y + X) + B;
+//   prune      a candidate whose estimate after Y alone reaches its region's
+//              current sum cannot be chosen (exact: every later term only
+//              adds), so its X / B half is skipped and it reads +inf.
+// Kernels: big_cur (each region's current sum), big_eval (one candidate
+// varblock per task), big_resolve (one thread per region), big_list (the
+// chosen big varblocks), big_write (transform + quantization + coefficients /
+// non-zero counts / quant field / LLF-derived DC of every covered block).
 #include <float.h>
 
 #include "jxg_device.h"
@@ -150,14 +154,15 @@ __device__ __forceinline__ void pass_item(int i, int nv, int& c, int& v, int& r)
 // copy into their planes (R x C, row-major; pl[c]: X, Y, B)
 template <int C>
 __device__ __forceinline__ void rows_pass(const MergeArgs& a, int bx, int by, int R, float* pl,
-                                          const BigLds& S) {
+                                          int nch, int c0, int cstep, const BigLds& S) {
   constexpr int NP = C / 32, L = C == 64 ? 6 : (C == 128 ? 7 : 8);
-  const int n = 3 * R * NP;
+  const int n = nch * R * NP;
   for (int base = 0; base < n; base += kBT) {
     const int i = base + (int)threadIdx.x;
     const bool act = i < n;
     int c, y, r;
     pass_item<NP>(act ? i : (i & (NP - 1)), R, c, y, r);  // (idle lanes: a valid row, not stored)
+    c = c0 + c * cstep;  // the pass's channel list
     // pixel x of the row: tile (Y >> 6, (bx >> 3) + (x >> 6)), column x & 63
     // (varblocks start on the 64-px grid); 32-bit offsets from the frame's XYB base
     const int Y = by * 8 + y;
@@ -178,14 +183,15 @@ __device__ __forceinline__ void rows_pass(const MergeArgs& a, int bx, int by, in
 }
 // columns, in place: every lane of a round computes before any stores
 template <int R>
-__device__ __forceinline__ void cols_pass(int C, float* pl, const BigLds& S) {
+__device__ __forceinline__ void cols_pass(int C, float* pl, int nch, int c0, int cstep, const BigLds& S) {
   constexpr int NP = R / 32, L = R == 64 ? 6 : (R == 128 ? 7 : 8);
-  const int n = 3 * C * NP;
+  const int n = nch * C * NP;
   for (int base = 0; base < n; base += kBT) {
     const int i = base + (int)threadIdx.x;
     const bool act = i < n;
     int c, x, r;
     pass_item<NP>(act ? i : (i & (NP - 1)), C, c, x, r);
+    c = c0 + c * cstep;
     const uint32_t c0 = (uint32_t)c * 65536u + (uint32_t)(x * R);  // column x: R contiguous floats
     float o[32];
     vb_vec<R>([&](int p) { return pl[c0 + (uint32_t)p]; }, r, o, S);
@@ -200,19 +206,20 @@ __device__ __forceinline__ void cols_pass(int C, float* pl, const BigLds& S) {
   }
 }
 
+// channels c0, c0 + cstep, ... (nch of them)
 __device__ __forceinline__ void vb_transform(const MergeArgs& a, const BigShape& sh, int bx, int by,
-                                             float* pl, const BigLds& S) {
+                                             float* pl, int nch, int c0, int cstep, const BigLds& S) {
   const int R = 8 << sh.lcy, C = 8 << sh.lcx;
   switch (sh.lcx) {
-    case 3: rows_pass<64>(a, bx, by, R, pl, S); break;
-    case 4: rows_pass<128>(a, bx, by, R, pl, S); break;
-    default: rows_pass<256>(a, bx, by, R, pl, S); break;
+    case 3: rows_pass<64>(a, bx, by, R, pl, nch, c0, cstep, S); break;
+    case 4: rows_pass<128>(a, bx, by, R, pl, nch, c0, cstep, S); break;
+    default: rows_pass<256>(a, bx, by, R, pl, nch, c0, cstep, S); break;
   }
   __syncthreads();
   switch (sh.lcy) {
-    case 3: cols_pass<64>(C, pl, S); break;
-    case 4: cols_pass<128>(C, pl, S); break;
-    default: cols_pass<256>(C, pl, S); break;
+    case 3: cols_pass<64>(C, pl, nch, c0, cstep, S); break;
+    case 4: cols_pass<128>(C, pl, nch, c0, cstep, S); break;
+    default: cols_pass<256>(C, pl, nch, c0, cstep, S); break;
   }
   __syncthreads();
 }
@@ -318,10 +325,16 @@ __device__ __forceinline__ void vb_quant(const MergeArgs& a, const float* tab, c
 }
 
 // transform + quantization of one candidate (scratch slot: planes X, Y, B);
-// returns the estimate (thread 0's value is the one used)
+// returns the estimate (thread 0's value is the one used).  cur: the region's
+// current sum (eval) -- the candidate is dropped (+inf) when its estimate
+// after Y alone already reaches it (the bits and the distortion sums only
+// grow with X and B, every float op on them is monotone, so the final
+// estimate would be >= cur >= the resolve's best and never chosen, alone or
+// in a pair; hook F off -- its factor may be negative or NaN).  NaN cur or
+// WRITE: no pruning.
 template <bool WRITE>
 __device__ __forceinline__ float vb_eval(const BigArgs& b, const BigShape& sh, int bx, int by, BigLds& S,
-                                         float* pl) {
+                                         float* pl, float cur) {
   const MergeArgs& a = b.m;
   const int cy = 1 << sh.lcy, cx = 1 << sh.lcx;
   if (threadIdx.x == 0) {
@@ -335,7 +348,7 @@ __device__ __forceinline__ float vb_eval(const BigArgs& b, const BigShape& sh, i
   for (int i = threadIdx.x; i < cy * cx; i += kBT)
     r = max(r, (int)a.qf[(size_t)(by + (i >> sh.lcx)) * a.bxs + bx + (i & (cx - 1))] + 1);
   if (r) atomicMax(&S.raw, r);
-  vb_transform(a, sh, bx, by, pl, S);  // (ends with a barrier)
+  vb_transform(a, sh, bx, by, pl, 1, 1, 0, S);  // Y (ends with a barrier)
   const float scale = (float)a.G * (float)S.raw / 65536.0f;
   // chroma from luma of the top-left block's tile (as the decoder applies it)
   const size_t tile = (size_t)(by >> 3) * a.tiles_x + (bx >> 3);
@@ -343,6 +356,11 @@ __device__ __forceinline__ float vb_eval(const BigArgs& b, const BigShape& sh, i
   const float kb = 1.0f + (float)a.cmap[a.ntiles_all + tile] * (1.0f / 84.0f);
   float* Yp = pl + 65536;  // planes: X, Y, B
   vb_quant<WRITE>(a, b.tab, b.nat, sh, bx, by, 1, Yp, Yp, scale, 0.0f, S);
+  if (!WRITE && !(a.proposals & 2u)) {
+    const float lb = ((float)(S.bits + (32 - __clz((uint32_t)S.nz[1]))) + 8.0f * S.pc[1]) * sh.tmul;
+    if (lb >= cur) return __builtin_inff();  // (uniform: every thread reads the same LDS values)
+  }
+  vb_transform(a, sh, bx, by, pl, 2, 0, 2, S);  // X and B
   vb_quant<WRITE>(a, b.tab, b.nat, sh, bx, by, 0, pl, Yp, scale, kx, S);
   vb_quant<WRITE>(a, b.tab, b.nat, sh, bx, by, 2, pl + 2 * 65536, Yp, scale, kb, S);
   const float dist = (S.pc[1] + S.pc[0]) + S.pc[2];
@@ -374,7 +392,31 @@ __device__ __forceinline__ const BigShape& big_cand(int L, int j, int bx0, int b
   by = by0 + (j == 4 ? s / 2 : 0);
   return kBig[L * 3 + (j == 0 ? 2 : (j <= 2 ? 0 : 1))];
 }
-constexpr int kBigCost = 25;  // per group slot: level 128 (4 regions x 5), level 256 (5)
+// per group slot: level 128 (4 regions x 5), level 256 (5), then the regions'
+// current sums (4 + 1, big_cur_kernel)
+constexpr int kBigCost = 30;
+__device__ __forceinline__ size_t cur_index(uint32_t gi, int L, int r) {
+  return (size_t)gi * kBigCost + 25 + (L == 0 ? r : 4);
+}
+
+// one thread per region of level L: the sum of the decisions below in raster
+// order (each varblock's estimate at its first block, 0 at covered blocks),
+// which the eval kernel prunes against and the resolve kernel compares with
+__global__ __launch_bounds__(256) void big_cur_kernel(Batch<BigArgs> bt_, int L) {
+  const BigArgs& b = bt_.a[blockIdx.z];
+  const MergeArgs& a = b.m;
+  const int nreg = L == 0 ? 4 : 1, s = 16 << L;
+  const uint32_t idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= b.ng * (uint32_t)nreg) return;
+  const uint32_t gi = idx / nreg;
+  const int r = (int)(idx - gi * nreg);
+  int bx0, by0;
+  if (!big_region(b, L, gi, r, bx0, by0)) return;
+  float cur = 0.0f;
+  for (int iy = 0; iy < s; iy++)
+    for (int ix = 0; ix < s; ix++) cur += a.ent[(size_t)(by0 + iy) * a.bxs + bx0 + ix];
+  b.cost[cur_index(gi, L, r)] = cur;
+}
 
 // the Lee tables into LDS (once per workgroup; the transforms read them per
 // element and stage)
@@ -399,7 +441,7 @@ __global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(4))) void b
     if (!big_region(b, L, gi, r, bx0, by0)) continue;  // (uniform)
     int bx, by;
     const BigShape& sh = big_cand(L, j, bx0, by0, bx, by);
-    const float e = vb_eval<false>(b, sh, bx, by, S, pl);
+    const float e = vb_eval<false>(b, sh, bx, by, S, pl, b.cost[cur_index(gi, L, r)]);
     if (threadIdx.x == 0) b.cost[(size_t)gi * kBigCost + (L == 0 ? r * 5 + j : 20 + j)] = e;
     __syncthreads();
   }
@@ -411,16 +453,14 @@ __global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(4))) void b
 __global__ __launch_bounds__(256) void big_resolve_kernel(Batch<BigArgs> bt_, int L) {
   const BigArgs& b = bt_.a[blockIdx.z];
   const MergeArgs& a = b.m;
-  const int nreg = L == 0 ? 4 : 1, s = 16 << L;
+  const int nreg = L == 0 ? 4 : 1;
   const uint32_t idx = blockIdx.x * 256 + threadIdx.x;
   if (idx >= b.ng * (uint32_t)nreg) return;
   const uint32_t gi = idx / nreg;
   const int r = (int)(idx - gi * nreg);
   int bx0, by0;
   if (!big_region(b, L, gi, r, bx0, by0)) return;
-  float cur = 0.0f;
-  for (int iy = 0; iy < s; iy++)
-    for (int ix = 0; ix < s; ix++) cur += a.ent[(size_t)(by0 + iy) * a.bxs + bx0 + ix];
+  const float cur = b.cost[cur_index(gi, L, r)];
   const float* cost = b.cost + (size_t)gi * kBigCost + (L == 0 ? r * 5 : 20);
   const float e0 = cost[0], et = cost[1] + cost[2], ew = cost[3] + cost[4];
   float best = cur;
@@ -481,7 +521,7 @@ __global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(4))) void b
     int si = 0;
     for (int i = 0; i < 6; i++) si = kBig[i].type == t ? i : si;
     const BigShape& sh = kBig[si];
-    (void)vb_eval<true>(b, sh, bx, by, S, pl);
+    (void)vb_eval<true>(b, sh, bx, by, S, pl, __builtin_nanf(""));
     // per covered block: non-zero counts, quant field, DC from the LLF
     const int lcy = sh.lcy, lcx = sh.lcx, cy = 1 << lcy, cx = 1 << lcx, lcb = lcy + lcx;
     const float* llf_p = b.tab + kBigTabLlfP;
@@ -525,6 +565,8 @@ hipError_t launch_big(const BigArgs* a, uint32_t k, hipStream_t s) {
   const uint32_t ng = a[0].ng;
   for (int L = 0; L < 2; L++) {
     const uint32_t tasks = ng * (L == 0 ? 20u : 5u);
+    const uint32_t nreg0 = ng * (L == 0 ? 4u : 1u);
+    hipLaunchKernelGGL(big_cur_kernel, dim3((nreg0 + 255) / 256, 1, k), dim3(256), 0, s, bt, L);
     hipLaunchKernelGGL(big_eval_kernel, dim3(min(tasks, a[0].slots), 1, k), dim3(kBT), 0, s, bt, L);
     const uint32_t nreg = ng * (L == 0 ? 4u : 1u);
     hipLaunchKernelGGL(big_resolve_kernel, dim3((nreg + 255) / 256, 1, k), dim3(256), 0, s, bt, L);

@@ -978,7 +978,7 @@ static jxg_status build_front(Ctx* c, Job& J) {
     }
     const uint32_t ng = std::max(1u, J.plan.ng());
     JXG_HIP(c->big_scratch.ensure((size_t)kBigSlots * kBigPlanes));
-    JXG_HIP(c->big_cost.ensure((size_t)ng * 25));
+    JXG_HIP(c->big_cost.ensure((size_t)ng * 30));  // [group][25 estimates + 5 current sums]
     JXG_HIP(c->big_work.ensure(1 + (size_t)ng * 16));
     BigArgs& ba = J.ba;
     ba = BigArgs{};
@@ -1078,11 +1078,12 @@ static jxg_status launch_transform(Ctx* const* cs, Job* const* js, uint32_t k) {
       JXG_HIP(launch_big(ba.data(), k, s));
       // test hook: JXG_DEBUG_BIGCOST=path writes frame 0's candidate estimates
       if (const char* dbg = std::getenv("JXG_DEBUG_BIGCOST")) {
-        std::vector<float> h((size_t)std::max(1u, J.plan.ng()) * 25);
+        const size_t ngc = std::max(1u, J.plan.ng());
+        std::vector<float> h(ngc * 30);
         JXG_HIP(hipMemcpyAsync(h.data(), ba[0].cost, h.size() * 4, hipMemcpyDeviceToHost, s));
         JXG_HIP(hipStreamSynchronize(s));
-        if (FILE* fp = std::fopen(dbg, "wb")) {
-          std::fwrite(h.data(), 4, h.size(), fp);
+        if (FILE* fp = std::fopen(dbg, "wb")) {  // the 25 estimates of every group
+          for (size_t g = 0; g < ngc; g++) std::fwrite(h.data() + g * 30, 4, 25, fp);
           std::fclose(fp);
         }
       }

@@ -116,9 +116,9 @@ struct BigArgs {
   MergeArgs m;             // the frame's merge arguments (xyb tiles, maps, outputs)
   const float* tab;        // kBigTab* blob
   const uint16_t* nat;     // [kBigKindOff[4]] natural-order position per stored index
-  float* scratch;          // [slots][2][65536] coefficient planes (Y / dequantized Y, X then B)
+  float* scratch;          // [slots][3][65536] column-major planes X, Y (dequantized after its quantization), B
   uint32_t slots;          // persistent workgroups (one scratch slot each)
-  float* cost;             // [ng][25] candidate estimates (level 128: 4 x 5, level 256: 5)
+  float* cost;             // [ng][30] candidate estimates (level 128: 4 x 5, level 256: 5), the regions' current sums (4 + 1)
   uint32_t* work;          // [1 + ng * 16]: count, then first blocks of the chosen varblocks
   const uint32_t* glist;   // the plan's pass groups: glist[i], or g0 + i
   uint32_t g0, ng, gxs;

@@ -1,14 +1,14 @@
-"""The lane protocol of the rANS chain kernels (csrc/jxg_ac.hip ans_chain /
-ans_chain2) restated over 64 model lanes and checked against a sequential
-encoder on random record streams: the diagonal hand-over by a whole-wave
-rotation, the pre-step state each lane captures, the final state of a stream
-(lane 63 / 31 after a full batch, else the state the lane past the last record
-captured) and, for two chains per wave, the swap of lanes 31 and 63 at a batch
-boundary.  The step itself is a toy rANS (the kernels' arithmetic is checked
-on the GPU against the oracle); what this pins is which lane holds which state
-when, for every stream length class: empty, shorter than a batch, exactly a
-batch, batch + 1, several batches, and an odd number of chains (an empty
-partner half)."""
+"""The lane protocol of the rANS chain kernel (csrc/jxg_ac.hip ans_chain)
+restated over 64 model lanes and checked against a sequential encoder on
+random record streams: the diagonal hand-over by a whole-wave rotation, the
+pre-step state each lane captures, and the final state of a stream (the lane
+of the last record after its batch's last step).  The step itself is a toy
+rANS (the kernel's arithmetic is checked on the GPU against the oracle); what
+this pins is which lane holds which state when, for every stream length
+class: empty, shorter than a batch, exactly a batch, batch + 1, several
+batches.  (Round 5 also ran two chains per wave, lanes 0-31 / 32-63 with a
+carry swap at the batch boundary: bit-exact on the GPU, but slower alone and
+no faster pipelined, DESIGN.md §3.5, so it was removed.)"""
 import random
 
 import pytest
@@ -69,34 +69,6 @@ def single_chain(recs):
     return final, outs
 
 
-def paired_chain(ra, rb):
-    """ans_chain2: stream A on lanes 0-31, stream B (None: no group) on 32-63"""
-    streams = [ra, rb if rb is not None else []]
-    x = [INIT] * 64
-    outs = [[None] * len(s) for s in streams]
-    finals = [INIT, INIT]
-    hi = [len(streams[0]), len(streams[1])]
-    while hi[0] > 0 or hi[1] > 0:
-        c = [min(32, max(h, 0)) for h in hi]
-        rec = []
-        for lane in range(64):
-            h, hl = lane >> 5, lane & 31
-            rec.append(streams[h][hi[h] - 1 - hl] if hl < c[h] else DUMMY)
-        X = [0] * 64
-        for s in range(32):  # always 32 steps (both halves)
-            xin = rotate(x)
-            X[s], X[32 + s] = xin[s], xin[32 + s]
-            x = [step(xin[l], rec[l])[0] for l in range(64)]
-        for h in range(2):
-            for hl in range(c[h]):
-                outs[h][hi[h] - 1 - hl] = emitted(X[32 * h + hl], rec[32 * h + hl])
-            if 0 < hi[h] <= 32:
-                finals[h] = x[32 * h + 31] if c[h] == 32 else X[32 * h + c[h]]
-        x[31], x[63] = x[63], x[31]  # the carry swap
-        hi = [hi[0] - c[0], hi[1] - c[1]]
-    return finals, outs
-
-
 def rand_stream(rng, n):
     out = []
     for _ in range(n):
@@ -113,15 +85,3 @@ def test_single_chain_protocol(n):
     rng = random.Random(n)
     recs = rand_stream(rng, n)
     assert single_chain(recs) == sequential(recs)
-
-
-def test_paired_chain_protocol():
-    rng = random.Random(7)
-    for na in LENGTHS:
-        for nb in LENGTHS + [None]:
-            ra = rand_stream(rng, na)
-            rb = None if nb is None else rand_stream(rng, nb)
-            (fa, fb), (oa, ob) = paired_chain(ra, rb)
-            assert (fa, oa) == sequential(ra), (na, nb)
-            if rb is not None:
-                assert (fb, ob) == sequential(rb), (na, nb)

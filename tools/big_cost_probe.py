@@ -1,5 +1,7 @@
 """Debug probe: the GPU's 128 / 256 px candidate estimates (JXG_DEBUG_BIGCOST
-dump) beside the oracle's (jxo_set_debug_big_cost), per group and candidate."""
+dump) beside the oracle's (jxo_set_debug_big_cost), per group and candidate.
+The GPU drops candidates whose estimate after Y alone reaches the region's
+current sum (hook F off): those read +inf here."""
 import os
 import sys
 
