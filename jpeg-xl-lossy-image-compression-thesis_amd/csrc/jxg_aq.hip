@@ -111,7 +111,7 @@ __global__ __launch_bounds__(kAqThreads) void aq_kernel(Batch<AqArgs> bt_) {
   __shared__ float sLut[256];
   const int tid = threadIdx.x;
   // a whole frame: the front kernel's XCD-aware order (XCD x = workgroup % 8
-  // takes the column run [x run, (x + 1) run) of every tile row), so the
+  // takes the chunk [x chunk, (x + 1) chunk) of the raster tile order), so the
   // lines of RGB8 rows neighbouring tiles share are L2 hits
   int tx, ty;
   if (a.tile_list) {
@@ -119,10 +119,11 @@ __global__ __launch_bounds__(kAqThreads) void aq_kernel(Batch<AqArgs> bt_) {
     tx = tile % (int)a.tiles_x;
     ty = tile / (int)a.tiles_x;
   } else {
-    const int run = ((int)a.tiles_x + 7) >> 3, j = (int)(blockIdx.x >> 3);
-    ty = j / run;
-    tx = (int)(blockIdx.x & 7) * run + (j - ty * run);
-    if (tx >= (int)a.tiles_x) return;
+    const int ntiles = (int)a.tiles_x * (((int)a.bys + 7) >> 3), chunk = (ntiles + 7) >> 3;
+    const int j = (int)(blockIdx.x >> 3), tile = (int)(blockIdx.x & 7) * chunk + j;
+    if (j >= chunk || tile >= ntiles) return;
+    tx = tile % (int)a.tiles_x;
+    ty = tile / (int)a.tiles_x;
   }
   const int ox = tx * 64, oy = ty * 64;  // padded-frame coordinate of tile-local (0, 0)
   const int xp = (int)a.xp, yp = (int)a.yp;
@@ -284,7 +285,7 @@ void launch_aq(const AqArgs* a, uint32_t k, uint32_t ntiles, hipStream_t s) {
   if (!ntiles || !k) return;
   // a list: one workgroup per listed tile; a whole frame: the XCD-aware grid
   const uint32_t tiles_y = (a[0].bys + 7) / 8;
-  const uint32_t nwg = a[0].tile_list ? ntiles : 8 * ((a[0].tiles_x + 7) / 8) * tiles_y;
+  const uint32_t nwg = a[0].tile_list ? ntiles : 8 * ((a[0].tiles_x * tiles_y + 7) / 8);
   hipLaunchKernelGGL(aq_kernel, dim3(nwg, 1, k), dim3(kAqThreads), 0, s, make_batch(a, k));
 }
 

@@ -1033,11 +1033,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
   __shared__ uint64_t sLapBits[64];
   const int tid = threadIdx.x;
   // a shard launches its own tiles through a list (1-D grid)
-  // A whole frame's tiles go in an XCD-aware order (1-D grid of 8 x run x
-  // tiles_y workgroups; workgroup w runs on XCD w % 8): XCD x takes the
-  // column run [x run, (x + 1) run) of every tile row, rows in order, so the
-  // 128-byte lines a tile's RGB8 rows share with its left / right / upper
-  // neighbours are L2 hits on the same XCD instead of fetches by another.
+  // A whole frame's tiles go in an XCD-aware order (1-D grid of 8 x chunk
+  // workgroups; workgroup w runs on XCD w % 8): XCD x takes the chunk
+  // [x chunk, (x + 1) chunk) of the raster tile order, so the 128-byte lines
+  // a tile's RGB8 rows share with its left / right / upper neighbours are L2
+  // hits on the same XCD instead of fetches by another, and every XCD gets
+  // the same number of tiles (a column-strip split left a 1080p frame's 510
+  // tiles 68 per XCD on 64 workgroup slots: two rounds instead of one).
   int tx, ty;
   bool idle = false;
   if (a.tile_list) {
@@ -1045,10 +1047,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
     tx = tile_id % (int)a.tiles_x;
     ty = tile_id / (int)a.tiles_x;
   } else {
-    const int run = ((int)a.tiles_x + 7) >> 3, j = (int)(blockIdx.x >> 3);
-    ty = j / run;
-    tx = (int)(blockIdx.x & 7) * run + (j - ty * run);
-    idle = tx >= (int)a.tiles_x;  // (the run of the last XCDs past the frame)
+    const int ntiles = (int)a.ntiles_all, chunk = (ntiles + 7) >> 3;
+    const int j = (int)(blockIdx.x >> 3), tile = (int)(blockIdx.x & 7) * chunk + j;
+    idle = j >= chunk || tile >= ntiles;  // (the last XCD's chunk past the frame)
+    tx = tile % (int)a.tiles_x;
+    ty = tile / (int)a.tiles_x;
   }
   const int ox = tx * kTile - 1, oy = ty * kTile - 1;
   if (a.zero) {  // the frame's statistics arena (the statistics kernels add into it)
@@ -1453,7 +1456,7 @@ hipError_t set_front_constants(const float lut[256], const float wts[5][3][64], 
 void launch_front(const FrontArgs* a, uint32_t k, uint32_t tiles_x, uint32_t tiles_y, hipStream_t s) {
   if (!k) return;
   const Batch<FrontArgs> b = make_batch(a, k);
-  const uint32_t nwg = 8 * ((tiles_x + 7) / 8) * tiles_y;  // XCD-aware order (front_kernel)
+  const uint32_t nwg = 8 * ((tiles_x * tiles_y + 7) / 8);  // XCD-aware order (front_kernel)
   if (a[0].proposals & 1u)
     hipLaunchKernelGGL(front_kernel<true>, dim3(nwg, 1, k), dim3(kThreads), 0, s, b);
   else
