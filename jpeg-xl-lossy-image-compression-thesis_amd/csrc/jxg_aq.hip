@@ -131,21 +131,35 @@ __global__ __launch_bounds__(kAqThreads) void aq_kernel(Batch<AqArgs> bt_) {
   __syncthreads();
   // 1. X, Y of the region (padded-frame coordinates clamped; the padded
   // frame replicates the image's last column / row)
+  // (pixel pairs of a row -- 74 is even -- through packed float ops,
+  // cbrt_det2: the same values as one pixel at a time)
   const float cb = cbrt_det(kOpsinBias);
-  for (int i = tid; i < kAqR * kAqR; i += kAqThreads) {
-    const int lx = i % kAqR, ly = i / kAqR;
-    const int gx = min(max(ox - kAqRing + lx, 0), xp - 1);
+  const pf2 cb2 = {cb, cb};
+  for (int i = tid; i < kAqR * kAqR / 2; i += kAqThreads) {
+    const int ly = (2 * i) / kAqR, lx0 = 2 * i - ly * kAqR;
     const int gy = min(max(oy - kAqRing + ly, 0), yp - 1);
-    const uint8_t* q =
-        a.rgb + (size_t)min(gy, (int)a.h - 1) * a.stride + 3 * (size_t)min(gx, (int)a.w - 1);
-    const float r = sLut[q[0]], g = sLut[q[1]], b = sLut[q[2]];
-    float m0 = ((kM00 * r + kM01 * g) + kM02 * b) + kOpsinBias;
-    float m1 = ((kM10 * r + kM11 * g) + kM12 * b) + kOpsinBias;
-    m0 = cbrt_det(m0) - cb;
-    m1 = cbrt_det(m1) - cb;
-    sY[ly * kAqS + lx] = 0.5f * (m0 + m1);
-    const int tlx = lx - kAqRing, tly = ly - kAqRing;
-    if (tlx >= 0 && tlx < 64 && tly >= 0 && tly < 64) sX[tly * 65 + tlx] = 0.5f * (m0 - m1);
+    const uint8_t* row = a.rgb + (size_t)min(gy, (int)a.h - 1) * a.stride;
+    pf2 r, g, b;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int gx = min(max(ox - kAqRing + lx0 + h, 0), xp - 1);
+      const uint8_t* q = row + 3 * (size_t)min(gx, (int)a.w - 1);
+      r[h] = sLut[q[0]];
+      g[h] = sLut[q[1]];
+      b[h] = sLut[q[2]];
+    }
+    pf2 m0, m1, m2;
+    opsin2(r, g, b, m0, m1, m2);
+    m0 = cbrt_det2(m0) - cb2;
+    m1 = cbrt_det2(m1) - cb2;
+    const pf2 Y = 0.5f * (m0 + m1), X = 0.5f * (m0 - m1);
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int lx = lx0 + h;
+      sY[ly * kAqS + lx] = Y[h];
+      const int tlx = lx - kAqRing, tly = ly - kAqRing;
+      if (tlx >= 0 && tlx < 64 && tly >= 0 && tly < 64) sX[tly * 65 + tlx] = X[h];
+    }
   }
   __syncthreads();
   // Y at padded-frame coordinate (gx, gy), clamped to the frame (inside the region)

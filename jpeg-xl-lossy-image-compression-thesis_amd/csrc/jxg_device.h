@@ -53,6 +53,50 @@ __device__ __forceinline__ void pixel_xyb(const float* lut, float cb, uint32_t r
   B = m2;
 }
 
+// Two pixels at once: every float multiply / add / fma is one packed op
+// (v_pk_mul_f32 / v_pk_add_f32 / v_pk_fma_f32), each half exactly the scalar
+// op, so the results are cbrt_det's / pixel_xyb's bit for bit at about half
+// the float instructions.  A half whose input is not > 0 runs the iterations
+// on a meaningless seed and is replaced by 0 at the end (no traps on the GPU).
+typedef float pf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ pf2 cbrt_det2(pf2 x) {
+  pf2 r = {__uint_as_float(0x54a2fa8cu - __float_as_uint(x.x) / 3u),
+           __uint_as_float(0x54a2fa8cu - __float_as_uint(x.y) / 3u)};
+  const pf2 one = {1.0f, 1.0f}, third = {0x1.555556p-2f, 0x1.555556p-2f};
+#pragma unroll
+  for (int it = 0; it < 3; it++) {
+    const pf2 r3 = (r * r) * r;
+    const pf2 e = __builtin_elementwise_fma(-x, r3, one);
+    r = __builtin_elementwise_fma(r * e, third, r);
+  }
+  pf2 y = (x * r) * r;
+  y.x = x.x > 0.0f ? y.x : 0.0f;
+  y.y = x.y > 0.0f ? y.y : 0.0f;
+  return y;
+}
+// linear RGB of two pixels -> opsin (m0, m1, m2) before the cube roots
+__device__ __forceinline__ void opsin2(pf2 r, pf2 g, pf2 b, pf2& m0, pf2& m1, pf2& m2) {
+  const pf2 bias = {kOpsinBias, kOpsinBias};
+  m0 = ((kM00 * r + kM01 * g) + kM02 * b) + bias;
+  m1 = ((kM10 * r + kM11 * g) + kM12 * b) + bias;
+  m2 = ((kM20 * r + kM21 * g) + kM22 * b) + bias;
+}
+__device__ __forceinline__ void pixel_xyb2(const float* lut, float cb, const uint32_t* r8,
+                                           const uint32_t* g8, const uint32_t* b8, pf2& X,
+                                           pf2& Y, pf2& B) {
+  const pf2 r = {lut[r8[0]], lut[r8[1]]}, g = {lut[g8[0]], lut[g8[1]]},
+            b = {lut[b8[0]], lut[b8[1]]};
+  pf2 m0, m1, m2;
+  opsin2(r, g, b, m0, m1, m2);
+  const pf2 cb2 = {cb, cb};
+  m0 = cbrt_det2(m0) - cb2;
+  m1 = cbrt_det2(m1) - cb2;
+  m2 = cbrt_det2(m2) - cb2;
+  X = 0.5f * (m0 - m1);
+  Y = 0.5f * (m0 + m1);
+  B = m2;
+}
+
 // thesis hook F (combined.diff:247-253): ret * 0.8 * avg_r in double, stored
 // to float
 __device__ __forceinline__ float hook_f(float ret, float rh, float rv, float rd) {

@@ -514,6 +514,19 @@ __device__ __forceinline__ void haar_lane(const GroupCtx& G, V* v) {
   }
 }
 
+// The signed quantized value of a coefficient: qf is the integer-valued
+// magnitude (0 .. 32767), vq the scaled coefficient; (vq < 0 ? -(int)qf :
+// (int)qf) as one sign insert and one conversion (vq = -0 has qf = 0 and
+// converts to 0 either way).  Two of them go into one word as int16 lo / hi
+// (v_cvt_pk_i16_i32; its saturation never applies at |q| <= 32767).
+__device__ __forceinline__ int signed_q(float qf, float vq) {
+  return (int)__builtin_copysignf(qf, vq);
+}
+__device__ __forceinline__ uint32_t pack_q(int lo, int hi) {
+  const auto p = __builtin_amdgcn_cvt_pk_i16(lo, hi);
+  return __builtin_bit_cast(uint32_t, p);
+}
+
 // Quantization of lane r's 8 values of channel C (0 X, 1 Y, 2 B) under
 // strategy T: accumulate e*e (fmaf), rate bits and the non-zero count; Y
 // records its dequantized values for the X / B residuals.  Float op order ==
@@ -585,16 +598,14 @@ __device__ __forceinline__ void quant_lane(const GroupCtx& G, float* v, float sc
     A.part = fmaf(e.y, e.y, A.part);
     ebits += (__float_as_uint(qf.x) >> 23) + (__float_as_uint(qf.y) >> 23);
     nz += (qf.x != 0.0f) + (qf.y != 0.0f);
-    const int q0 = (int)qf.x, q1 = (int)qf.y;
-    qs[k] = vq.x < 0.0f ? -q0 : q0;
-    qs[k + 1] = vq.y < 0.0f ? -q1 : q1;
+    qs[k] = signed_q(qf.x, vq.x);
+    qs[k + 1] = signed_q(qf.y, vq.y);
   }
   // sum over k of [qa != 0] (2 + 2 bitlen) = 2 E-sum - 250 nz
   A.bits += 2 * (int)ebits - 250 * nz;
   uint32_t pk[4];
 #pragma unroll
-  for (int i = 0; i < 4; i++)
-    pk[i] = ((uint32_t)qs[2 * i] & 0xFFFFu) | ((uint32_t)qs[2 * i + 1] << 16);
+  for (int i = 0; i < 4; i++) pk[i] = pack_q(qs[2 * i], qs[2 * i + 1]);
   const int nzc = group_int_sum(nz);
   A.bits += G.r == 0 ? bitlen((uint32_t)nzc) : 0;
   constexpr int slot = C == 1 ? 4 : (C == 0 ? 0 : 8);
@@ -624,7 +635,7 @@ __device__ __forceinline__ void quant_xb(const GroupCtx& G, f2* v, float scale, 
   int nzx = 0, nzb = 0;
   uint32_t ebits = 0;
   float eb[8];
-  uint32_t pkx[4], pkb[4];
+  int sx[8], sb[8];
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     const f2 ws = wk[k] * sc2;
@@ -640,16 +651,8 @@ __device__ __forceinline__ void quant_xb(const GroupCtx& G, f2* v, float scale, 
     ebits += (__float_as_uint(qf.x) >> 23) + (__float_as_uint(qf.y) >> 23);
     nzx += qf.x != 0.0f;
     nzb += qf.y != 0.0f;
-    const int q0 = (int)qf.x, q1 = (int)qf.y;
-    const uint32_t sx = (uint32_t)(vq.x < 0.0f ? -q0 : q0) & 0xFFFFu;
-    const uint32_t sb = (uint32_t)(vq.y < 0.0f ? -q1 : q1) & 0xFFFFu;
-    if (k & 1) {
-      pkx[k >> 1] |= sx << 16;
-      pkb[k >> 1] |= sb << 16;
-    } else {
-      pkx[k >> 1] = sx;
-      pkb[k >> 1] = sb;
-    }
+    sx[k] = signed_q(qf.x, vq.x);
+    sb[k] = signed_q(qf.y, vq.y);
   }
 #pragma unroll
   for (int k = 0; k < 8; k++) A.part = fmaf(eb[k], eb[k], A.part);  // then B's
@@ -658,8 +661,8 @@ __device__ __forceinline__ void quant_xb(const GroupCtx& G, f2* v, float scale, 
   A.bits += G.r == 0 ? bitlen((uint32_t)nzcx) + bitlen((uint32_t)nzcb) : 0;
 #pragma unroll
   for (int i = 0; i < 4; i++) {
-    A.q.w[i] = pkx[i];
-    A.q.w[8 + i] = pkb[i];
+    A.q.w[i] = pack_q(sx[2 * i], sx[2 * i + 1]);
+    A.q.w[8 + i] = pack_q(sb[2 * i], sb[2 * i + 1]);
   }
   A.q.nz |= (uint32_t)nzcx | ((uint32_t)nzcb << 16);
 }
