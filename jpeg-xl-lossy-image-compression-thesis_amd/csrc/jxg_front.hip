@@ -516,12 +516,19 @@ __device__ __forceinline__ void haar_lane(const GroupCtx& G, V* v) {
 
 // The signed quantized value of a coefficient: qf is the integer-valued
 // magnitude (0 .. 32767), vq the scaled coefficient; (vq < 0 ? -(int)qf :
-// (int)qf) as one sign insert and one conversion (vq = -0 has qf = 0 and
-// converts to 0 either way).  Two of them go into one word as int16 lo / hi
+// (int)qf) is (int)sq, sq = copysign(qf, vq): one sign insert and one
+// conversion (vq = -0 has qf = 0 and converts to 0 either way).  Two of them go into one word as int16 lo / hi
 // (v_cvt_pk_i16_i32; its saturation never applies at |q| <= 32767).
-__device__ __forceinline__ int signed_q(float qf, float vq) {
-  return (int)__builtin_copysignf(qf, vq);
-}
+// signed_err: the quantization error is taken on the signed values, (vq -
+// sq) with sq = copysign(qf, vq): for vq < 0 that is (-|vq|) - (-qf) = -(|vq| -
+// qf) exactly (round to nearest is symmetric in sign), for vq = +-0 it is +0,
+// so e * e -- the only use of e -- is the oracle's (|vq| - qf)^2 bit for bit,
+// with no |vq| pair to build for the packed subtraction.
+// Non-zero count of eight quantized magnitudes from the sum of their biased
+// exponents: a zero has E = 0, a non-zero qf in [1, 32767] has E = 127 + d
+// with d = floor(log2 qf) in [0, 14], so the sum is 127 nz + (sum of d) with
+// the second term at most 8 x 14 = 112 < 127: nz = sum / 127 exactly.
+__device__ __forceinline__ int nz_of_esum(uint32_t esum) { return (int)(esum / 127u); }
 __device__ __forceinline__ uint32_t pack_q(int lo, int hi) {
   const auto p = __builtin_amdgcn_cvt_pk_i16(lo, hi);
   return __builtin_bit_cast(uint32_t, p);
@@ -556,7 +563,6 @@ __device__ __forceinline__ void quant_lane(const GroupCtx& G, float* v, float sc
     iwk2[3] = f2{i1.z, i1.w};
   }
   const f2 sc2 = f2{scale, scale}, isc2 = f2{inv_scale, inv_scale};
-  int nz = 0;
   uint32_t ebits = 0;
   int qs[8];
 #pragma unroll
@@ -567,10 +573,10 @@ __device__ __forceinline__ void quant_lane(const GroupCtx& G, float* v, float sc
     if (C == 0) rv = rv - f2{G.kx, G.kx} * f2{A.yd[k], A.yd[k + 1]};
     if (C == 2) rv = rv - f2{G.kb, G.kb} * f2{A.yd[k], A.yd[k + 1]};
     const f2 vq = rv * ws;
-    const f2 a = f2{fabsf(vq.x), fabsf(vq.y)};
     f2 qf;
-    qf.x = a.x < 0.58f ? 0.0f : floorf(fminf(a.x, 32767.0f) + 0.5f);
-    qf.y = a.y < 0.58f ? 0.0f : floorf(fminf(a.y, 32767.0f) + 0.5f);
+    qf.x = fabsf(vq.x) < 0.58f ? 0.0f : floorf(fminf(fabsf(vq.x), 32767.0f) + 0.5f);
+    qf.y = fabsf(vq.y) < 0.58f ? 0.0f : floorf(fminf(fabsf(vq.y), 32767.0f) + 0.5f);
+    const f2 sq = f2{__builtin_copysignf(qf.x, vq.x), __builtin_copysignf(qf.y, vq.y)};
     if (C == 1) {
       f2 adj;
 #pragma unroll
@@ -592,16 +598,17 @@ __device__ __forceinline__ void quant_lane(const GroupCtx& G, float* v, float sc
     }
     // quantization error in steps, times the distortion weight: the
     // coefficient's pixel-domain error (oracle jxo_dist_weight)
+    // (signed_err: (vq - sq) sd = +-(|vq| - qf) sd exactly, same square)
     const float2 sd = sdp[kp];
-    const f2 e = (a - qf) * f2{sd.x, sd.y};
+    const f2 e = (vq - sq) * f2{sd.x, sd.y};
     A.part = fmaf(e.x, e.x, A.part);
     A.part = fmaf(e.y, e.y, A.part);
     ebits += (__float_as_uint(qf.x) >> 23) + (__float_as_uint(qf.y) >> 23);
-    nz += (qf.x != 0.0f) + (qf.y != 0.0f);
-    qs[k] = signed_q(qf.x, vq.x);
-    qs[k + 1] = signed_q(qf.y, vq.y);
+    qs[k] = (int)sq.x;
+    qs[k + 1] = (int)sq.y;
   }
   // sum over k of [qa != 0] (2 + 2 bitlen) = 2 E-sum - 250 nz
+  const int nz = nz_of_esum(ebits);
   A.bits += 2 * (int)ebits - 250 * nz;
   uint32_t pk[4];
 #pragma unroll
@@ -632,8 +639,7 @@ __device__ __forceinline__ void quant_xb(const GroupCtx& G, f2* v, float scale, 
   const f2 wk[8] = {f2{wx0.x, wb0.x}, f2{wx0.y, wb0.y}, f2{wx0.z, wb0.z}, f2{wx0.w, wb0.w},
                     f2{wx1.x, wb1.x}, f2{wx1.y, wb1.y}, f2{wx1.z, wb1.z}, f2{wx1.w, wb1.w}};
   const f2 sc2 = f2{scale, scale}, kxb = f2{G.kx, G.kb};
-  int nzx = 0, nzb = 0;
-  uint32_t ebits = 0;
+  uint32_t ebx = 0, ebb = 0;  // exponent sums of X's and of B's eight values
   float eb[8];
   int sx[8], sb[8];
 #pragma unroll
@@ -641,22 +647,22 @@ __device__ __forceinline__ void quant_xb(const GroupCtx& G, f2* v, float scale, 
     const f2 ws = wk[k] * sc2;
     const f2 rv = v[k] - kxb * f2{A.yd[k], A.yd[k]};
     const f2 vq = rv * ws;
-    const f2 a = f2{fabsf(vq.x), fabsf(vq.y)};
     f2 qf;
-    qf.x = a.x < 0.58f ? 0.0f : floorf(fminf(a.x, 32767.0f) + 0.5f);
-    qf.y = a.y < 0.58f ? 0.0f : floorf(fminf(a.y, 32767.0f) + 0.5f);
-    const f2 e = (a - qf) * f2{sxp[k], sbp[k]};
+    qf.x = fabsf(vq.x) < 0.58f ? 0.0f : floorf(fminf(fabsf(vq.x), 32767.0f) + 0.5f);
+    qf.y = fabsf(vq.y) < 0.58f ? 0.0f : floorf(fminf(fabsf(vq.y), 32767.0f) + 0.5f);
+    const f2 sq = f2{__builtin_copysignf(qf.x, vq.x), __builtin_copysignf(qf.y, vq.y)};
+    const f2 e = (vq - sq) * f2{sxp[k], sbp[k]};  // (signed_err)
     A.part = fmaf(e.x, e.x, A.part);  // X's chain
     eb[k] = e.y;
-    ebits += (__float_as_uint(qf.x) >> 23) + (__float_as_uint(qf.y) >> 23);
-    nzx += qf.x != 0.0f;
-    nzb += qf.y != 0.0f;
-    sx[k] = signed_q(qf.x, vq.x);
-    sb[k] = signed_q(qf.y, vq.y);
+    ebx += __float_as_uint(qf.x) >> 23;
+    ebb += __float_as_uint(qf.y) >> 23;
+    sx[k] = (int)sq.x;
+    sb[k] = (int)sq.y;
   }
 #pragma unroll
   for (int k = 0; k < 8; k++) A.part = fmaf(eb[k], eb[k], A.part);  // then B's
-  A.bits += 2 * (int)ebits - 250 * (nzx + nzb);
+  const int nzx = nz_of_esum(ebx), nzb = nz_of_esum(ebb);
+  A.bits += 2 * (int)(ebx + ebb) - 250 * (nzx + nzb);
   const int nzcx = group_int_sum(nzx), nzcb = group_int_sum(nzb);
   A.bits += G.r == 0 ? bitlen((uint32_t)nzcx) + bitlen((uint32_t)nzcb) : 0;
 #pragma unroll
