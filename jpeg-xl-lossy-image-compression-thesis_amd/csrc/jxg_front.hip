@@ -31,7 +31,7 @@ constexpr int kNT = 6;
 __constant__ float c_wperm[kNT * 3 * 64];  // [T][c][lane r][row k] = w[qkind(T)][c][co_index(T,k,r)]
 __constant__ float c_iwperm[kNT * 64];     // [T][r][k] = 1.0f / (Y weight) at the same slot
 __constant__ float c_sdperm[kNT * 3 * 64]; // [T][c][r][k] distortion weight at the same slot
-__constant__ float c_btab[256];            // [q] = 0.145f / q (AdjustQuantBias, |q| >= 2)
+__constant__ float c_btab[256];            // [q] = the bias-adjusted magnitude of q (adj_of)
 __constant__ uint8_t c_zz[kNT * 64];       // [T][r][k] = zigzag index of co_index(T,k,r)
 
 constexpr int kTile = 64;
@@ -344,7 +344,7 @@ struct GroupCtx {
   int r;
   const float* wperm;  // LDS [kNT T][3 c][8 r][8 k] weights per lane
   const float* iwperm; // LDS [kNT T][8 r][8 k] Y inverse weights per lane
-  const float* btab;   // LDS [256] 0.145f / q
+  const float* btab;   // LDS [256] adj_of(q), q < 256
   const float* sdperm; // LDS [kNT T][3 c][8 r][8 k] distortion weights per lane
   float kx, kb;        // chroma from luma of the tile: X - kx Yd, B - kb Yd
 };
@@ -547,7 +547,6 @@ template <int T, int C>
 __device__ __forceinline__ void quant_lane(const GroupCtx& G, float* v, float scale,
                                            float inv_scale, CandAcc& A) {
   constexpr int ti = tindex<T>();
-  constexpr float kBias1 = 1.0f - 0.07005449891748593f;
   if (G.r == 0) v[0] = 0.0f;  // DC slot: quantizes to 0, contributes nothing
   const float4* wp = reinterpret_cast<const float4*>(G.wperm + ((ti * 3 + C) * 8 + G.r) * 8);
   const float4 w0 = wp[0], w1 = wp[1];
@@ -583,11 +582,10 @@ __device__ __forceinline__ void quant_lane(const GroupCtx& G, float* v, float sc
       for (int h = 0; h < 2; h++) {
         const float q = h ? qf.y : qf.x;
         const int qa = (int)q;
-        float bq = G.btab[qa < 255 ? qa : 255];
+        float ad = G.btab[qa < 255 ? qa : 255];  // adj_of(qa) below 256
         if (__any(qa >= 256)) {
-          if (qa >= 256) bq = 0.145f / q;
+          if (qa >= 256) ad = q - 0.145f / q;
         }
-        float ad = qa == 0 ? 0.0f : (qa == 1 ? kBias1 : q - bq);
         if ((h ? vq.y : vq.x) < 0.0f) ad = -ad;
         if (h) adj.y = ad;
         else adj.x = ad;
@@ -1439,8 +1437,13 @@ hipError_t set_front_constants(const float lut[256], const float wts[5][3][64], 
         zz[(ti * 8 + r) * 8 + k] = (uint8_t)c_inv_order_h(co);
       }
   }
-  btab[0] = btab[1] = 0.0f;
-  for (int q = 2; q < 256; q++) btab[q] = 0.145f / (float)q;
+  // AdjustQuantBias of a magnitude q: 0 -> 0, 1 -> kBias1, else q - 0.145 / q
+  // (the same single-precision division and subtraction the kernel did per
+  // coefficient before round 5; SSE rounds them as the GPU does, no
+  // contraction is involved)
+  btab[0] = 0.0f;
+  btab[1] = 1.0f - 0.07005449891748593f;
+  for (int q = 2; q < 256; q++) btab[q] = (float)q - 0.145f / (float)q;
   hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_lut), lut, sizeof(float) * 256, 0,
                                         hipMemcpyHostToDevice, s);
   if (e == hipSuccess)

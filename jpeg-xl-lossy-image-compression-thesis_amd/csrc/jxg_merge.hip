@@ -159,7 +159,7 @@ struct MergeLds {
   float co[2 * kMPlane];  // coefficient image of the tile's varblocks
   float llf[3][64];       // write mode: the LLF of covered block b, per channel
   float qsum[3][4][32];   // [Y, X, B][chunk][varblock]: column-tree chunk sums
-  float btab[256];        // 0.145f / q (AdjustQuantBias), q < 256
+  float btab[256];        // AdjustQuantBias of a magnitude q < 256 (setup_varblocks)
   float vr3[32][3];       // hook F: similarity indices of each top-left block
   int vbits[32];          // per varblock: rate bits
   int vnz[32][3];         //               non-zeros per channel
@@ -466,7 +466,6 @@ __device__ __forceinline__ void load_qtab(const MergeArgs& a, const Pass& P, QTa
 template <int RPC, bool WRITE, int CH>
 __device__ __forceinline__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S, const QTab<RPC>& T) {
   constexpr int cidx = CH == 1 ? 0 : (CH == 0 ? 1 : 2);  // 0 Y, 1 X, 2 B
-  constexpr float kBias1 = 1.0f - 0.07005449891748593f;
   const int C = P.C(), NV = P.NV();
   // chroma from luma of the tile (front kernel): X - kx Yd, B - kb Yd
   float kc = 0.0f;
@@ -505,8 +504,9 @@ __device__ __forceinline__ void quant_pass(const MergeArgs& a, const Pass& P, Me
     // the LLF (first cy rows x cx columns) only occurs in chunk 0
     const bool llf_col = ch == 0 && x < P.cx();
     float cp = 0.0f;
-    uint32_t ebits = 0;
-    int nzc = 0;
+    // exponent sums of the rows below 8 and from 8 on: non-zeros from each
+    // (nz = sum / 127, exact for eight values: jxg_front.hip nz_of_esum)
+    uint32_t eb8[2] = {0u, 0u};
     // rows in pairs: the float multiplies / adds of the two rows are one
     // packed op each (f2, no contraction: each half is the scalar op order);
     // the distortion chain stays in row order
@@ -523,7 +523,7 @@ __device__ __forceinline__ void quant_pass(const MergeArgs& a, const Pass& P, Me
       // LLF positions carry weight 0 (host tables): vq = +-0 quantizes to 0
       // and contributes nothing
       const f2 vq = rv * (f2{w[kk], w[kk + 1]} * f2{scale, scale});
-      float avs[2], qfs[2];
+      float sqs[2];
 #pragma unroll
       for (int h = 0; h < 2; h++) {
         const float vqh = h ? vq.y : vq.x;
@@ -532,25 +532,21 @@ __device__ __forceinline__ void quant_pass(const MergeArgs& a, const Pass& P, Me
         // truncation of a positive value is its floor): no conversions
         // needed for the error and the rate
         const float qf = av < 0.58f ? 0.0f : floorf(fminf(av, 32767.0f) + 0.5f);
-        avs[h] = av;
-        qfs[h] = qf;
+        sqs[h] = __builtin_copysignf(qf, vqh);
         if (CH == 1) {
           const int qa = (int)qf;
-          float bq = S.btab[min(qa, 255)];
+          float adj = S.btab[min(qa, 255)];
           if (__builtin_expect(__any(qa >= 256), 0)) {
-            if (qa >= 256) bq = 0.145f / qf;
+            if (qa >= 256) adj = qf - 0.145f / qf;
           }
-          float adj = qa == 0 ? 0.0f : (qa == 1 ? kBias1 : qf - bq);
           if (vqh < 0.0f) adj = -adj;
           cplane[(ky + h) * kMS] = adj * iw[kk + h];  // LLF: 0 (its value lives in llf_at)
         }
         // 2 + 2 bitlen(qa) per non-zero = 2 E - 250, E = biased exponent of
         // qf (qf = 0 has E = 0 and is not counted in nzc)
-        ebits += __float_as_uint(qf) >> 23;
-        nzc += qf != 0.0f;
+        eb8[kk >= 8] += __float_as_uint(qf) >> 23;
         if (WRITE) {
-          const int qa = (int)qf;
-          const int qq = vqh < 0.0f ? -qa : qa;
+          const int qq = (int)sqs[h];  // (vq < 0 ? -qa : qa)
           const int p = nat[kk + h];
           const int sl = p >> 6;
           const int lbx = bx0 + (sl & (P.cx() - 1)), lby = by0 + (sl >> P.lcx);
@@ -560,13 +556,16 @@ __device__ __forceinline__ void quant_pass(const MergeArgs& a, const Pass& P, Me
       }
       // error in steps times the distortion weight (oracle jxo_dist_weight);
       // the write pass needs no estimate
+      // (the signed error: (vq - sq) sd = +-(|vq| - qf) sd exactly, the same
+      // square; jxg_front.hip signed_err)
       if (!WRITE) {
-        const f2 e = (f2{avs[0], avs[1]} - f2{qfs[0], qfs[1]}) * f2{sd[kk], sd[kk + 1]};
+        const f2 e = (vq - f2{sqs[0], sqs[1]}) * f2{sd[kk], sd[kk + 1]};
         cp = fmaf(e.x, e.x, cp);
         cp = fmaf(e.y, e.y, cp);
       }
     }
-    const int bits = 2 * (int)ebits - 250 * nzc;
+    const int nzc = (int)(eb8[0] / 127u) + (int)(eb8[1] / 127u);
+    const int bits = 2 * (int)(eb8[0] + eb8[1]) - 250 * nzc;
     // the chunk's column partials, tree-summed over the varblock's C lanes
     // (an aligned group inside one wave); bits | non-zeros << 20 likewise
     int packed = bits | nzc << 20;
@@ -691,7 +690,10 @@ __device__ __forceinline__ void setup_varblocks(const MergeArgs& a, const Pass& 
     S.vbits[v] = 0;
     S.vnz[v][0] = S.vnz[v][1] = S.vnz[v][2] = 0;
   }
-  for (int i = t; i < 256; i += kMThreads) S.btab[i] = i < 2 ? 0.0f : 0.145f / (float)i;
+  // AdjustQuantBias of q: 0 -> 0, 1 -> 1 - 0.0700..., else q - 0.145 / q (the
+  // per-coefficient expression, tabulated)
+  for (int i = t; i < 256; i += kMThreads)
+    S.btab[i] = i == 0 ? 0.0f : (i == 1 ? 1.0f - 0.07005449891748593f : (float)i - 0.145f / (float)i);
 }
 // varblock quant field = max raw over its covered blocks (after a barrier)
 __device__ __forceinline__ void vraw_pass(const MergeArgs& a, const Pass& P, MergeLds& S) {
