@@ -31,7 +31,7 @@ constexpr int kNT = 6;
 __constant__ float c_wperm[kNT * 3 * 64];  // [T][c][lane r][row k] = w[qkind(T)][c][co_index(T,k,r)]
 __constant__ float c_iwperm[kNT * 64];     // [T][r][k] = 1.0f / (Y weight) at the same slot
 __constant__ float c_sdperm[kNT * 3 * 64]; // [T][c][r][k] distortion weight at the same slot
-__constant__ float c_btab[256];            // [q] = the bias-adjusted magnitude of q (adj_of)
+__constant__ float c_btab[256];            // [q] = AdjustQuantBias of a magnitude q < 256 (host table: 0, 1 - 0.0700..., q - 0.145 / q)
 __constant__ uint8_t c_zz[kNT * 64];       // [T][r][k] = zigzag index of co_index(T,k,r)
 
 constexpr int kTile = 64;
@@ -344,7 +344,7 @@ struct GroupCtx {
   int r;
   const float* wperm;  // LDS [kNT T][3 c][8 r][8 k] weights per lane
   const float* iwperm; // LDS [kNT T][8 r][8 k] Y inverse weights per lane
-  const float* btab;   // LDS [256] adj_of(q), q < 256
+  const float* btab;   // LDS [256] AdjustQuantBias of a magnitude q < 256 (c_btab)
   const float* sdperm; // LDS [kNT T][3 c][8 r][8 k] distortion weights per lane
   float kx, kb;        // chroma from luma of the tile: X - kx Yd, B - kb Yd
 };
@@ -582,7 +582,7 @@ __device__ __forceinline__ void quant_lane(const GroupCtx& G, float* v, float sc
       for (int h = 0; h < 2; h++) {
         const float q = h ? qf.y : qf.x;
         const int qa = (int)q;
-        float ad = G.btab[qa < 255 ? qa : 255];  // adj_of(qa) below 256
+        float ad = G.btab[qa < 255 ? qa : 255];  // the tabulated bias below 256
         if (__any(qa >= 256)) {
           if (qa >= 256) ad = q - 0.145f / q;
         }
