@@ -564,6 +564,7 @@ __device__ __forceinline__ void quant_lane(const GroupCtx& G, float* v, float sc
   const f2 sc2 = f2{scale, scale}, isc2 = f2{inv_scale, inv_scale};
   uint32_t ebits = 0;
   int qs[8];
+  int qmax = 0;  // (Y) magnitudes >= 256 take the division after the loop
 #pragma unroll
   for (int kp = 0; kp < 4; kp++) {
     const int k = 2 * kp;
@@ -583,9 +584,7 @@ __device__ __forceinline__ void quant_lane(const GroupCtx& G, float* v, float sc
         const float q = h ? qf.y : qf.x;
         const int qa = (int)q;
         float ad = G.btab[qa < 255 ? qa : 255];  // the tabulated bias below 256
-        if (__any(qa >= 256)) {
-          if (qa >= 256) ad = q - 0.145f / q;
-        }
+        qmax = max(qmax, qa);
         if ((h ? vq.y : vq.x) < 0.0f) ad = -ad;
         if (h) adj.y = ad;
         else adj.x = ad;
@@ -604,6 +603,20 @@ __device__ __forceinline__ void quant_lane(const GroupCtx& G, float* v, float sc
     ebits += (__float_as_uint(qf.x) >> 23) + (__float_as_uint(qf.y) >> 23);
     qs[k] = (int)sq.x;
     qs[k + 1] = (int)sq.y;
+  }
+  if (C == 1 && __any(qmax >= 256)) {
+    // the bias of a magnitude >= 256, q - 0.145 / q (the table stops at 255),
+    // and its dequantized value: the same float ops as below 256
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int qa = qs[k] < 0 ? -qs[k] : qs[k];
+      if (qa >= 256) {
+        const float q = (float)qa;
+        float ad = q - 0.145f / q;
+        if (qs[k] < 0) ad = -ad;
+        A.yd[k] = ad * (((k & 1) ? iwk2[k >> 1].y : iwk2[k >> 1].x) * inv_scale);
+      }
+    }
   }
   // sum over k of [qa != 0] (2 + 2 bitlen) = 2 E-sum - 250 nz
   const int nz = nz_of_esum(ebits);
