@@ -585,7 +585,10 @@ __device__ __forceinline__ void quant_lane(const GroupCtx& G, float* v, float sc
         const int qa = (int)q;
         float ad = G.btab[qa < 255 ? qa : 255];  // the tabulated bias below 256
         qmax = max(qmax, qa);
-        if ((h ? vq.y : vq.x) < 0.0f) ad = -ad;
+        // vq < 0 ? -ad : ad as one sign insert; at vq = -0 (ad = 0) it gives
+        // -0, a dequantized Y of -0 whose only uses (the X / B residuals, every
+        // quantity derived from them) see the same values for +-0
+        ad = __builtin_copysignf(ad, h ? vq.y : vq.x);
         if (h) adj.y = ad;
         else adj.x = ad;
       }
