@@ -539,7 +539,7 @@ __device__ __forceinline__ void quant_pass(const MergeArgs& a, const Pass& P, Me
           if (__builtin_expect(__any(qa >= 256), 0)) {
             if (qa >= 256) adj = qf - 0.145f / qf;
           }
-          if (vqh < 0.0f) adj = -adj;
+          adj = __builtin_copysignf(adj, vqh);  // (vq = -0: a -0 that no result sees; jxg_front.hip)
           cplane[(ky + h) * kMS] = adj * iw[kk + h];  // LLF: 0 (its value lives in llf_at)
         }
         // 2 + 2 bitlen(qa) per non-zero = 2 E - 250, E = biased exponent of
