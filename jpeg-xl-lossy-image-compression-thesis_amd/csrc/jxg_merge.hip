@@ -49,7 +49,10 @@ constexpr int kMThreads = 256;
 #define JXG_MERGE_WPE 4  // waves per SIMD the eval kernel is register-capped for (4 WGs / CU)
 #endif
 #ifndef JXG_MERGE_WRITE_WPE
-#define JXG_MERGE_WRITE_WPE 3  // write: 167 VGPRs, no spills
+// write: 168 VGPRs and 52 B of scratch per lane at 3 waves / SIMD; 2 (195
+// VGPRs, no scratch) measured slower: merge stage 1.85 vs 1.94 ms at 8K
+// (profiles/r05zp); 4 spills 204 B
+#define JXG_MERGE_WRITE_WPE 3
 #endif
 constexpr int kMS = 65;  // LDS row stride (floats)
 constexpr int kMPlane = 64 * kMS;
