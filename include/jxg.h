@@ -205,8 +205,10 @@ void jxg_buffer_free(jxg_buffer* buf);
  *           2 / 4 / 8): no per-block records move;
  *   kind 2: else the ranges of kind 0 with the record exchange below.
  * The owner of an LF group encodes its LF-group stream.  Per rank:
- *   1. jxg_shard_sizes: words of the AC histogram and the byte capacity of
- *      the record send / receive buffers (the largest of any rank);
+ *   1. jxg_shard_sizes: words of the AC histogram (132 x 128 counts, then
+ *      the rank's varblock count per 128 / 256 px kind, whose sum decides
+ *      which quant tables HfGlobal carries) and the byte capacity of the
+ *      record send / receive buffers (the largest of any rank);
  *      jxg_shard_exchange: this rank's send and receive bytes per peer;
  *   2. jxg_shard_begin: front end + merge stage + AC token statistics of the
  *      rank's groups; writes the rank's AC histogram to d_hist (u32, device)

@@ -289,13 +289,19 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sWave,
   return before + incl - v;
 }
 
-// The band's clustered histogram in LDS as u16 counts, two bins per word (a
-// band has at most 256 x 3 x 64 = 49152 tokens, so a half never carries)
+// The band's clustered histogram in LDS.  An 8-row band (BR = 8) has at most
+// 256 x 3 x 64 + 768 = 49920 tokens, so its counts are u16, two bins per word,
+// and a half never carries.  The whole-group form (BR = 32, effort >= 8) walks
+// up to 1024 x 3 x 64 + 3072 tokens, and one bin can pass 65535 (a DCT256X256
+// whose X and B hold only their last coefficient puts ~129 K zero tokens into
+// one cluster; tests/test_gpu_bigvb.py::test_whole_group_histogram_bin_above_u16):
+// u32 bins there (67.6 KB of LDS for the histogram).
 template <int BR>
 __global__ __launch_bounds__(BR * 32) void ac_hist_kernel(Batch<AcArgs> bt_) {
   constexpr int kBandBlocks = BR * 32, kHistThreads = kBandBlocks, kWgBands = 32 / BR;
   const AcArgs& a = bt_.a[blockIdx.z];  // the batch's frame
-  constexpr int kHistWords = kMaxClusters * kAcTok / 2;
+  constexpr bool kWide = BR == 32;  // u32 bins
+  constexpr int kHistWords = kWide ? kMaxClusters * kAcTok : kMaxClusters * kAcTok / 2;
   __shared__ uint32_t sHist[kHistWords];
   __shared__ AcLds<BR> L;
   __shared__ uint8_t sClu[kAcCtx];
@@ -360,7 +366,10 @@ __global__ __launch_bounds__(BR * 32) void ac_hist_kernel(Batch<AcArgs> bt_) {
   const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
   auto hist_add = [&](uint32_t clu, uint32_t tok) {
     const uint32_t bin = clu * kAcTok + tok;
-    atomicAdd(&sHist[bin >> 1], 1u << ((bin & 1u) * 16u));
+    if (kWide)
+      atomicAdd(&sHist[bin], 1u);
+    else
+      atomicAdd(&sHist[bin >> 1], 1u << ((bin & 1u) * 16u));
   };
 #pragma unroll 1
   for (int ci = 0; ci < 3; ci++) {
@@ -453,6 +462,10 @@ __global__ __launch_bounds__(BR * 32) void ac_hist_kernel(Batch<AcArgs> bt_) {
   for (int i = threadIdx.x; i < kHistWords; i += blockDim.x) {
     const uint32_t w = sHist[i];
     if (!w) continue;
+    if (kWide) {
+      atomicAdd(&a.hist[(i / kAcTok) * kAlpha + (i % kAcTok)], w);
+      continue;
+    }
     const int bin = 2 * i;
     if (w & 0xFFFFu) atomicAdd(&a.hist[(bin / kAcTok) * kAlpha + (bin % kAcTok)], w & 0xFFFFu);
     if (w >> 16) atomicAdd(&a.hist[((bin + 1) / kAcTok) * kAlpha + ((bin + 1) % kAcTok)], w >> 16);

@@ -503,7 +503,12 @@ __global__ __launch_bounds__(64) void big_list_kernel(Batch<BigArgs> bt_) {
   if (bx >= a.bxs || by >= a.bys) return;
   const uint32_t gb = by * a.bxs + bx;
   const uint8_t t = a.acs[gb];
-  if (t >= 21 && t <= 26) b.work[1 + atomicAdd(b.work, 1u)] = gb;
+  if (t >= 21 && t <= 26) {
+    b.work[1 + atomicAdd(b.work, 1u)] = gb;
+    // kind 0 128X64 (22, 23), 1 128X128 (21), 2 256X128 (25, 26), 3 256X256 (24)
+    const uint32_t k = t == 21 ? 1u : (t == 24 ? 3u : (t <= 23 ? 0u : 2u));
+    atomicAdd(b.kinds + k, 1u);
+  }
 }
 
 __global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(4))) void big_write_kernel(Batch<BigArgs> bt_) {

@@ -286,11 +286,11 @@ struct Ctx {
   DevBuf<uint32_t> stream_chunks, scratch, scratch_lf, chunks, out, out_ac;
   DevBuf<uint64_t> lfstatus;  // [nchunks] lf_code look-back words
   // Per-frame statistics, zeroed by the front kernel and downloaded by two copies
-  // (AC part, LF part): [hist_ac | bound | ntok | bandtok][lfhist | sbound | vcount]
+  // (AC part, LF part): [hist_ac | bound | ntok | bandtok | bigcount][lfhist | sbound | vcount]
   DevBuf<uint8_t> stat;
   PinBuf<uint8_t> h_stat;
-  View<uint32_t> hist_ac, bound, ntok, bandtok, lfhist, sbound, vcount;
-  View<uint32_t> h_hist_ac, h_bound, h_ntok, h_lfhist, h_sbound, h_vcount;
+  View<uint32_t> hist_ac, bound, ntok, bandtok, bigcount, lfhist, sbound, vcount;
+  View<uint32_t> h_hist_ac, h_bound, h_ntok, h_bigcount, h_lfhist, h_sbound, h_vcount;
   size_t stat_lf = 0, stat_bytes = 0;  // byte offset of the LF part, total
   // Per-frame code tables, uploaded by one copy (ANS) or two (prefix codes:
   // the AC part ahead of the AC emission): [codes_ac | gbase | ans_order |
@@ -716,6 +716,8 @@ static jxg_status stage_alloc(Ctx* c, Job& J) {
     o = al(o + (size_t)f.ngroups * 12);
     const size_t o_bandtok = o;
     o = al(o + (size_t)f.ngroups * 16);
+    const size_t o_bigcount = o;  // varblocks per big kind (big_list_kernel)
+    o = al(o + 16);
     const size_t o_lfhist = o;
     o = al(o + (size_t)ns * 4 * kAlpha * 4);
     const size_t o_sbound = o;
@@ -730,6 +732,8 @@ static jxg_status stage_alloc(Ctx* c, Job& J) {
     c->bound.set(c->stat.p, o_bound, f.ngroups);
     c->ntok.set(c->stat.p, o_ntok, (size_t)f.ngroups * 3);
     c->bandtok.set(c->stat.p, o_bandtok, (size_t)f.ngroups * 4);
+    c->bigcount.set(c->stat.p, o_bigcount, 4);
+    c->h_bigcount.set(c->h_stat.p, o_bigcount, 4);
     c->lfhist.set(c->stat.p, o_lfhist, (size_t)ns * 4 * kAlpha);
     c->sbound.set(c->stat.p, o_sbound, ns);
     c->vcount.set(c->stat.p, o_vcount, f.nlf);
@@ -977,7 +981,11 @@ static jxg_status build_front(Ctx* c, Job& J) {
       c->big_ready = true;
     }
     const uint32_t ng = std::max(1u, J.plan.ng());
-    JXG_HIP(c->big_scratch.ensure((size_t)kBigSlots * kBigPlanes));
+    // one scratch slot per persistent workgroup; a frame of ng groups has at
+    // most 20 ng tasks per level launch (a 512 x 512 frame needs 20
+    // slots, not the 512 of an 8K one -- 402 MB per context otherwise)
+    const uint32_t slots = std::min<uint32_t>(ng * 20u, kBigSlots);
+    JXG_HIP(c->big_scratch.ensure((size_t)slots * kBigPlanes));
     JXG_HIP(c->big_cost.ensure((size_t)ng * 30));  // [group][25 estimates + 5 current sums]
     JXG_HIP(c->big_work.ensure(1 + (size_t)ng * 16));
     BigArgs& ba = J.ba;
@@ -986,9 +994,10 @@ static jxg_status build_front(Ctx* c, Job& J) {
     ba.tab = c->big_tab.p;
     ba.nat = c->big_nat.p;
     ba.scratch = c->big_scratch.p;
-    ba.slots = kBigSlots;
+    ba.slots = slots;
     ba.cost = c->big_cost.p;
     ba.work = c->big_work.p;
+    ba.kinds = c->bigcount.p;
     ba.glist = J.plan.contiguous ? nullptr : c->glist.p;
     ba.g0 = J.plan.g0();
     ba.ng = J.plan.ng();
@@ -997,6 +1006,14 @@ static jxg_status build_front(Ctx* c, Job& J) {
   J.va = VbArgs{c->acs.p, f.bxs, f.bys, f.lfxs, J.plan.world > 1 ? c->lf_mine.p : nullptr, c->vb.p,
                 c->vcount.p};
   return JXG_OK;
+}
+
+// bit k: the frame (or with a caller's summed histogram, the whole sharded
+// frame) holds a varblock of big kind k
+static uint32_t big_mask(const uint32_t* count) {
+  uint32_t m = 0;
+  for (int k = 0; k < 4; k++) m |= (count[k] != 0 ? 1u : 0u) << k;
+  return m;
 }
 
 // ---- stage E: statistics to the host (AC histogram from `hist`) ----
@@ -1012,6 +1029,9 @@ static jxg_status stage_download_ac(Ctx* c, Job& J, const uint32_t* hist) {
     const size_t hb = (size_t)kMaxClusters * kAlpha * 4, ob = (uint8_t*)c->bound.p - c->stat.p;
     JXG_HIP(hipMemcpyAsync(c->h_hist_ac.p, hist, hb, hipMemcpyDeviceToHost, s));
     JXG_HIP(hipMemcpyAsync(c->h_stat.p + ob, c->stat.p + ob, c->stat_lf - ob, hipMemcpyDeviceToHost, s));
+    // the big-kind counts summed with it (jxg_shard_sizes: after the histogram)
+    JXG_HIP(hipMemcpyAsync(c->h_bigcount.p, hist + (size_t)kMaxClusters * kAlpha, 16,
+                           hipMemcpyDeviceToHost, s));
   }
   JXG_HIP(hipEventRecord(c->ev[6], s));
   return JXG_OK;
@@ -1218,7 +1238,8 @@ static jxg_status stage_codes(Ctx* c, Job& J) {
     lfglobal.put(1, 1);  // colour correlation default
     lfglobal.put(1, 0);  // GlobalModular: no tree, no channels
     if (!J.presets) {  // (per-rank presets: HfGlobal at assembly, build_hf_presets)
-      hfglobal.put(1, 1);  // DequantMatrices all_default
+      // the quant tables of the 128 / 256 px kinds the frame uses (e >= 8)
+      write_dequant_matrices(hfglobal, J.big ? big_mask(c->h_bigcount.p) : 0u);
       hfglobal.put(ceil_log2(f.ngroups), 0);  // num_hf_presets - 1
       write_u32_sel(hfglobal, 2, 0, 0);        // used_orders = 0
       if (nhist != c->cm_nhist || ctxmap != c->cm_last) {
@@ -2085,7 +2106,9 @@ static jxg_status shard_finish(Ctx* c, Job& J, size_t* payload_bytes, bool sync 
   hw.assign(7 + 2 * ids.size(), 0);
   hw[0] = kPayloadMagic;
   hw[1] = J.presets ? 2 : 1;
-  hw[2] = J.plan.rank | J.lf << 16;  // the rank, the frame's loop-filter code
+  // the rank, the frame's loop-filter code, the 128 / 256 px kinds the rank's
+  // groups use (their quant tables go into HfGlobal, effort >= 8)
+  hw[2] = J.plan.rank | J.lf << 16 | (J.big ? big_mask(c->h_bigcount.p) : 0u) << 24;
   hw[3] = J.plan.world;
   hw[4] = J.w;
   hw[5] = J.h;
@@ -2397,6 +2420,8 @@ static jxg_status shard_begin(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32_t
   Job* jp = &J;
   if ((st = launch_transform(&c, &jp, 1))) return st;
   JXG_HIP(hipMemcpyAsync(d_hist, c->hist_ac.p, kMaxClusters * kAlpha * 4, hipMemcpyDeviceToDevice, s));
+  JXG_HIP(hipMemcpyAsync(d_hist + (size_t)kMaxClusters * kAlpha, c->bigcount.p, 16,
+                         hipMemcpyDeviceToDevice, s));
   // the send list (then the receive list) of the record exchange
   const Exchange& X = J.plan.x;
   JXG_HIP(c->xlist.ensure(X.send.size() + X.recv.size() + 1));
@@ -2892,7 +2917,7 @@ jxg_status jxg_shard_sizes(uint32_t xsize, uint32_t ysize, uint32_t world, size_
   if (!hist_words || !slot_bytes || xsize == 0 || ysize == 0 || world == 0)
     return JXG_ERR_INVALID_ARG;
   const Frame f = make_frame(xsize, ysize, 1.0f);
-  *hist_words = (size_t)kMaxClusters * kAlpha;
+  *hist_words = (size_t)kMaxClusters * kAlpha + 4;  // + the varblocks per big kind
   // the largest send or receive buffer of any rank
   const Partition part = make_partition(f, world);
   size_t most = 1;

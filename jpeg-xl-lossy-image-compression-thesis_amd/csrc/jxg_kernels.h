@@ -120,6 +120,7 @@ struct BigArgs {
   uint32_t slots;          // persistent workgroups (one scratch slot each)
   float* cost;             // [ng][30] candidate estimates (level 128: 4 x 5, level 256: 5), the regions' current sums (4 + 1)
   uint32_t* work;          // [1 + ng * 16]: count, then first blocks of the chosen varblocks
+  uint32_t* kinds;         // [4] varblocks chosen per big kind (statistics arena; the host writes the used kinds' quant tables)
   const uint32_t* glist;   // the plan's pass groups: glist[i], or g0 + i
   uint32_t g0, ng, gxs;
 };

@@ -5,6 +5,7 @@
 
 #include "jxg_bitstream.h"
 #include "jxg_device.h"
+#include "jxg_tables.h"
 
 namespace jxg {
 
@@ -21,7 +22,7 @@ size_t head_words(const uint32_t* hw, size_t avail) {
 // contexts (rank r's clusters after those of ranks < r), every rank's ANS
 // histograms rebuilt from its clustered counts [ext HfGlobal / HfPass]
 static jxg_status build_hf_presets(const std::vector<std::vector<uint32_t>>& heads,
-                                   uint32_t ngroups, BitWriter& hf) {
+                                   uint32_t ngroups, uint32_t big, BitWriter& hf) {
   const uint32_t n = (uint32_t)heads.size();
   const size_t cw = (kAcCtx + 3) / 4;
   std::vector<uint8_t> ctxmap((size_t)n * kAcCtx);
@@ -45,7 +46,7 @@ static jxg_status build_hf_presets(const std::vector<std::vector<uint32_t>>& hea
     off += nh;
   }
   if (off > 255 || n - 1 >= (1u << ceil_log2(ngroups))) return JXG_ERR_INVALID_ARG;
-  hf.put(1, 1);                            // DequantMatrices all_default
+  write_dequant_matrices(hf, big);         // DequantMatrices
   hf.put(ceil_log2(ngroups), n - 1);     // num_hf_presets - 1
   write_u32_sel(hf, 2, 0, 0);              // used_orders = 0
   write_ans_histograms(hf, ctxmap, (int)off, tables, kCfg420, nullptr);
@@ -67,11 +68,13 @@ jxg_status parse_payload_heads(const std::vector<std::vector<uint32_t>>& heads,
     if (hw.size() < 7 || hw[0] != kPayloadMagic || (hw[1] != 1 && hw[1] != 2) ||
         hw[1] != heads[0][1] || hw[3] != n)
       return JXG_ERR_INVALID_ARG;
+    // bits 16-23: loop-filter code (equal over the ranks), bits 24-27: the
+    // big kinds of the rank's groups (shard_finish; their union is written)
     if (i == 0) {
       *w = hw[4];
       *h = hw[5];
-      *lf = hw[2] >> 16;  // loop-filter code (shard_finish)
-    } else if (hw[4] != *w || hw[5] != *h || (hw[2] >> 16) != *lf) {
+      *lf = (hw[2] >> 16) & 0xFFu;
+    } else if (hw[4] != *w || hw[5] != *h || ((hw[2] >> 16) & 0xFFu) != *lf) {
       return JXG_ERR_INVALID_ARG;
     }
     const size_t hwords = head_words(hw.data(), hw.size());
@@ -90,6 +93,11 @@ jxg_status parse_payload_heads(const std::vector<std::vector<uint32_t>>& heads,
       off += sz;
     }
   }
+  uint32_t big = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    if (heads[i][2] >> 28) return JXG_ERR_INVALID_ARG;
+    big |= heads[i][2] >> 24;
+  }
   if (*w == 0 || *h == 0 || *lf > 7) return JXG_ERR_INVALID_ARG;
   const uint32_t ngroups = ((*w + 255) / 256) * ((*h + 255) / 256);
   const uint32_t nlf = ((*w + 2047) / 2048) * ((*h + 2047) / 2048);
@@ -99,7 +107,7 @@ jxg_status parse_payload_heads(const std::vector<std::vector<uint32_t>>& heads,
     if (seen[id]) return JXG_ERR_INVALID_ARG;
     // (a rank that does not write HfGlobal needs its size only)
     BitWriter bw = hf_bytes ? BitWriter() : BitWriter::counter();
-    const jxg_status st = build_hf_presets(heads, ngroups, bw);
+    const jxg_status st = build_hf_presets(heads, ngroups, big, bw);
     if (st) return st;
     if (hf_bytes) hf = bw.bytes();
     secs[id] = SectionRef{n, 0, (uint32_t)((bw.bits() + 7) / 8)};

@@ -4,6 +4,7 @@
 #include <cmath>
 #include <cstring>
 
+#include "jxg_bitstream.h"
 #include "jxg_kernels.h"
 
 namespace jxg {
@@ -253,19 +254,74 @@ MergeTables build_merge_tables() {
   return T;
 }
 
+double f16_round(double v) {
+  const double a = std::fabs(v);
+  if (a == 0.0) return 0.0;
+  int e;
+  (void)std::frexp(a, &e);  // a = m * 2^e, m in [0.5, 1)
+  int ue = e - 11;          // ulp exponent of an 11-bit significand
+  if (ue < -24) ue = -24;   // subnormal spacing
+  const double q = std::ldexp(std::nearbyint(std::ldexp(a, -ue)), ue);
+  return v < 0 ? -q : q;
+}
+uint32_t f16_bits(double v) {
+  const uint32_t sign = v < 0 ? 0x8000u : 0u;
+  const double a = std::fabs(v);
+  if (a == 0.0) return sign;
+  if (a < std::ldexp(1.0, -14)) return sign | (uint32_t)std::ldexp(a, 24);
+  int e;
+  const double m = std::frexp(a, &e);
+  return sign | (uint32_t)(e - 1 + 15) << 10 | (uint32_t)std::ldexp(2.0 * m - 1.0, 10);
+}
+
 // DCT128X64, DCT128X128, DCT256X128, DCT256X256: the bands of DCT64X32 /
-// DCT64X64 with the first band scaled up with the size (== oracle/merge.c;
-// as recalled, parity with libjxl unpinned)
+// DCT64X64 with the first band scaled up with the size (== oracle/merge.c),
+// rounded to the binary16 parameters the stream carries for them
+// (write_dequant_matrices): the first band 64 * f16(band / 64), the others
+// f16(v)
+static const double kBigY32[3] = {23629.073922049845, 8611.3238710010046, 4492.2486445538634};
+static const double kBigY64[3] = {26629.073922049845, 9311.3238710010046, 4992.2486445538634};
+static const double kBigRest[3][7] = {
+    {-1.025, -0.78, -0.65012, -0.19041574084286472, -0.20819395464, -0.421064,
+     -0.32733845535848671},
+    {-0.3041958212306401, -0.3633036457487539, -0.35660379990111464, -0.3443074455424403,
+     -0.33699592683512467, -0.30180866526242109, -0.27321683125358037},
+    {-1.2, -1.2, -0.8, -0.7, -0.7, -0.4, -0.5}};
+static const double kBigScale[4] = {1.3, 1.7, 2.2, 3.0};
+static double big_param(int k, int c, int i) {
+  if (i) return f16_round(kBigRest[c][i - 1]);
+  return 64.0 * f16_round(kBigScale[k] * ((k & 1) ? kBigY64[c] : kBigY32[c]) / 64.0);
+}
+
+void write_dequant_matrices(BitWriter& w, uint32_t mask) {
+  if (!mask) {
+    w.put(1, 1);  // all_default
+    return;
+  }
+  // quant table order DCT, IDENTITY, DCT2X2, DCT4X4, DCT16X16, DCT32X32,
+  // DCT16X8, DCT32X8, DCT32X16, DCT64X64, DCT64X32, DCT4X8, AFV0, DCT128X128,
+  // DCT128X64, DCT256X256, DCT256X128 -> big kind (0 128X64, 1 128X128,
+  // 2 256X128, 3 256X256) or -1 (Library)
+  static const int kTableBig[17] = {-1, -1, -1, -1, -1, -1, -1, -1, -1,
+                                    -1, -1, -1, -1, 1,  0,  3,  2};
+  w.put(1, 0);
+  for (int t = 0; t < 17; t++) {
+    const int k = kTableBig[t];
+    if (k < 0 || !(mask >> k & 1)) {
+      w.put(3, 0);  // Library
+      continue;
+    }
+    w.put(3, 6);      // DCT
+    w.put(4, 8 - 1);  // bands
+    for (int c = 0; c < 3; c++)
+      for (int i = 0; i < 8; i++) {
+        const double v = big_param(k, c, i);
+        w.put(16, f16_bits(i ? v : v / 64.0));
+      }
+  }
+}
+
 BigTables build_big_tables() {
-  static const double kY32[3] = {23629.073922049845, 8611.3238710010046, 4492.2486445538634};
-  static const double kY64[3] = {26629.073922049845, 9311.3238710010046, 4992.2486445538634};
-  static const double kRest[3][7] = {
-      {-1.025, -0.78, -0.65012, -0.19041574084286472, -0.20819395464, -0.421064,
-       -0.32733845535848671},
-      {-0.3041958212306401, -0.3633036457487539, -0.35660379990111464, -0.3443074455424403,
-       -0.33699592683512467, -0.30180866526242109, -0.27321683125358037},
-      {-1.2, -1.2, -0.8, -0.7, -0.7, -0.4, -0.5}};
-  static const double kScale[4] = {1.3, 1.7, 2.2, 3.0};
   static const int kDims[4][2] = {{64, 128}, {128, 128}, {128, 256}, {256, 256}};
   BigTables T;
   const size_t n = kBigKindOff[4];
@@ -275,9 +331,9 @@ BigTables build_big_tables() {
     const int rows = kDims[k][0], cols = kDims[k][1], nb = 8, off = kBigKindOff[k];
     for (int c = 0; c < 3; c++) {
       double bands[8];
-      bands[0] = kScale[k] * ((k & 1) ? kY64[c] : kY32[c]);
+      bands[0] = big_param(k, c, 0);
       for (int i = 1; i < nb; i++) {
-        const double v = kRest[c][i - 1];
+        const double v = big_param(k, c, i);
         bands[i] = bands[i - 1] * (v > 0 ? 1.0 + v : 1.0 / (1.0 - v));
       }
       const double scale = (nb - 1) / (1.4142135623730951 + 1e-6);

@@ -29,4 +29,16 @@ struct BigTables {
 };
 BigTables build_big_tables();
 
+// DequantMatrices of HfGlobal [ext quant_weights.cc]: all_default when mask is
+// 0, else Library for every table but those of the big kinds in mask (bit 0
+// 128X64, 1 128X128, 2 256X128, 3 256X256: the kinds the frame uses, effort
+// >= 8), which are written in mode DCT with the binary16 parameters
+// build_big_tables quantizes with (== oracle/encode.c put_dequant_matrices),
+// so no decoder default is involved for them
+class BitWriter;
+void write_dequant_matrices(BitWriter& w, uint32_t mask);
+// the binary16 value nearest v (ties to even) and its bits (== oracle/merge.c)
+double f16_round(double v);
+uint32_t f16_bits(double v);
+
 }  // namespace jxg

@@ -21,6 +21,9 @@ int jxo_front_block(const jxo_frame* f, const float px[3][64], const float* homo
                     const float cfl[2], int aq_raw);
 
 static const jxo_uintcfg kCfg = {4, 2, 0};
+
+uint32_t* jxo_debug_group_bins = NULL; /* tests: see the AC token loop */
+void jxo_set_debug_group_bins(uint32_t* p) { jxo_debug_group_bins = p; }
 static const jxo_uintcfg kCfgMap = {8, 0, 0};
 
 static uint32_t ceil_log2(uint32_t x) { /* CeilLog2Nonzero */
@@ -61,6 +64,51 @@ static void put_token(jxo_bw* w, const jxo_prefix* p, const jxo_uintcfg* c,
   jxo_hybrid(v, c, &tok, &nb, &bits);
   jxo_bw_put(w, p->len[tok], p->code[tok]);
   jxo_bw_put(w, nb, bits);
+}
+
+/* DequantMatrices [ext quant_weights.cc DequantMatrices::Decode]: all_default,
+ * else one encoding per quant table in the format's table order (DCT,
+ * IDENTITY, DCT2X2, DCT4X4, DCT16X16, DCT32X32, DCT16X8, DCT32X8, DCT32X16,
+ * DCT64X64, DCT64X32, DCT4X8, AFV0, DCT128X128, DCT128X64, DCT256X256,
+ * DCT256X128): 3-bit mode, 0 = Library (the decoder's defaults), 6 = DCT
+ * (4-bit band count - 1, then per channel the bands as binary16, the first one
+ * divided by 64).  The tables of the 128 / 256 px kinds a frame uses (effort
+ * >= 8) are written (merge.c jxo_kind_param) -- the stream then does not
+ * depend on the decoder's defaults for them; a frame without such a
+ * varblock keeps all_default. */
+static const int kQuantTableKind[17] = {-1, -1, -1, -1, JXO_VK_16, JXO_VK_32, JXO_VK_16X8, -1,
+                                        JXO_VK_32X16, JXO_VK_64, JXO_VK_64X32, -1, -1,
+                                        JXO_VK_128, JXO_VK_128X64, JXO_VK_256, JXO_VK_256X128};
+/* mask: bit k - JXO_VK_128X64 set when the frame holds a varblock of kind k */
+static uint32_t big_kind_mask(const uint8_t* acs, size_t nb) {
+  uint32_t m = 0;
+  for (size_t i = 0; i < nb; i++) {
+    const int t = acs[i];
+    if (t >= 21 && t <= 26) m |= 1u << (jxo_shapes[jxo_shape_of(t)].kind - JXO_VK_128X64);
+  }
+  return m;
+}
+static void put_dequant_matrices(jxo_bw* w, uint32_t mask) {
+  if (!mask) {
+    jxo_bw_put(w, 1, 1); /* all_default */
+    return;
+  }
+  jxo_bw_put(w, 1, 0);
+  for (int t = 0; t < 17; t++) {
+    const int k = kQuantTableKind[t];
+    if (k < JXO_VK_128X64 || !(mask >> (k - JXO_VK_128X64) & 1)) {
+      jxo_bw_put(w, 3, 0); /* Library */
+      continue;
+    }
+    const int nb = jxo_kind_num_bands(k);
+    jxo_bw_put(w, 3, 6); /* DCT */
+    jxo_bw_put(w, 4, (uint32_t)(nb - 1));
+    for (int c = 0; c < 3; c++)
+      for (int i = 0; i < nb; i++) {
+        const double v = jxo_kind_param(k, c, i);
+        jxo_bw_put(w, 16, jxo_f16_bits(i ? v : v / 64.0));
+      }
+  }
 }
 
 /* Entropy-code header (DecodeHistograms): lz77 off, context map, prefix
@@ -557,6 +605,9 @@ int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h, size_t row_strid
   free(aqraw);
 
   /* ---- AC tokens and clustered histograms ---- */
+  /* (debug: the largest count of one (static cluster, token) bin inside one
+   * pass group -- what a group's LDS histogram on the GPU must hold) */
+  uint32_t dbg_max_bin = 0;
   actok** gt = (actok**)malloc(sizeof(actok*) * f.ngroups);
   size_t* gn = (size_t*)malloc(sizeof(size_t) * f.ngroups);
   static uint32_t hist[JXO_MAX_CLUSTERS][JXO_ALPHA];
@@ -579,12 +630,26 @@ int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h, size_t row_strid
         jxo_hybrid(gt[g][i].v, &kCfg, &tok, &nbt, &bits);
         lh[jxo_ac_cluster(gt[g][i].ctx)][tok]++;
       }
+      if (jxo_debug_group_bins) {
+        uint32_t* gh = (uint32_t*)calloc(JXO_MAX_CLUSTERS * JXO_ALPHA, 4);
+        uint32_t mx = 0;
+        for (size_t i = 0; i < gn[g]; i++) {
+          uint32_t tok, nbt, bits;
+          jxo_hybrid(gt[g][i].v, &kCfg, &tok, &nbt, &bits);
+          const uint32_t v = ++gh[jxo_ac_cluster(gt[g][i].ctx) * JXO_ALPHA + tok];
+          mx = v > mx ? v : mx;
+        }
+        free(gh);
+#pragma omp critical
+        dbg_max_bin = mx > dbg_max_bin ? mx : dbg_max_bin;
+      }
     }
     free(scratch);
 #pragma omp critical
     for (int cl = 0; cl < JXO_MAX_CLUSTERS; cl++)
       for (int s = 0; s < JXO_ALPHA; s++) hist[cl][s] += lh[cl][s];
   }
+  if (jxo_debug_group_bins) *jxo_debug_group_bins = dbg_max_bin;
   /* prefix codes: one histogram per static cluster.  ANS: the static
    * clusters are clustered again into <= JXO_ANS_MAX_HISTS centres
    * (jxo_ans_cluster).  Dense ids in order of first appearance over contexts. */
@@ -647,7 +712,7 @@ int jxo_encode_rgb8(const uint8_t* rgb, uint32_t w, uint32_t h, size_t row_strid
   for (uint32_t lg = 0; lg < f.nlf; lg++) lf_group_section(&f, out, (int)lg, p->filters, &sec[1 + lg]);
   {
     jxo_bw* s = &sec[1 + f.nlf];
-    jxo_bw_put(s, 1, 1); /* DequantMatrices all_default */
+    put_dequant_matrices(s, big_kind_mask(out->acs, (size_t)f.bxs * f.bys));
     jxo_bw_put(s, ceil_log2(f.ngroups), 0); /* num_hf_presets - 1 */
     put_u32_sel(s, 2, 0, 0);                /* used_orders = 0 */
     if (!ans) {

@@ -825,14 +825,59 @@ def natural_order(rows, cols):
 
 _KIND_CACHE = {}
 
+# DequantMatrices [ext quant_weights.cc]: quant table index (the format's
+# order DCT, IDENTITY, DCT2X2, DCT4X4, DCT16X16, DCT32X32, DCT16X8, DCT32X8,
+# DCT32X16, DCT64X64, DCT64X32, DCT4X8, AFV0, DCT128X128, DCT128X64,
+# DCT256X256, DCT256X128) -> merged-varblock kind (None: an 8x8-class table)
+QUANT_TABLE_KIND = [None, None, None, None, 1, 3, 0, None, 2, 5, 4, None, None, 7, 6, 9, 8]
+QM_LIBRARY, QM_DCT = 0, 6
 
-def kind_tables(kind):
-    """(inverse weights (3, rows*cols) stored raster, natural order)"""
-    if kind not in _KIND_CACHE:
+
+def f16_value(bits):
+    """binary16 bits -> float [ext F16Coder::Read]; inf / NaN are invalid"""
+    sign, exp, mant = bits >> 15, (bits >> 10) & 31, bits & 1023
+    if exp == 31:
+        raise JxlError("binary16 inf / NaN in a header")
+    v = mant * 2.0 ** -24 if exp == 0 else (1024 + mant) * 2.0 ** (exp - 25)
+    return -v if sign else v
+
+
+def read_dequant_matrices(br):
+    """-> {kind: bands (3 x nb)} of the tables a stream writes in DCT mode;
+    kinds absent from the dict use the decoder's defaults (KIND_BANDS)."""
+    if br.bool():  # all_default
+        return {}
+    params = {}
+    for t, kind in enumerate(QUANT_TABLE_KIND):
+        mode = br.read(3)
+        if mode == QM_LIBRARY:
+            br.read(0)  # one predefined table set: zero bits
+            continue
+        if mode != QM_DCT or kind is None:
+            raise JxlError("quant table %d: mode %d not produced" % (t, mode))
+        nb = br.read(4) + 1
+        bands = []
+        for c in range(3):
+            row = [f16_value(br.read(16)) for _ in range(nb)]
+            if row[0] < 1e-8:
+                raise JxlError("quant table %d: first band ~0" % t)
+            row[0] *= 64.0
+            bands.append(row)
+        params[kind] = bands
+    return params
+
+
+def kind_tables(kind, bands=None):
+    """(inverse weights (3, rows*cols) stored raster, natural order); bands:
+    the stream's parameters for the kind (read_dequant_matrices), else the
+    library defaults"""
+    key = (kind, None if bands is None else tuple(tuple(r) for r in bands))
+    if key not in _KIND_CACHE:
         r, c = KIND_DIM[kind]
-        w = _weights(r, c, KIND_BANDS[kind], len(KIND_BANDS[kind][0]))
-        _KIND_CACHE[kind] = (1.0 / w, natural_order(r, c))
-    return _KIND_CACHE[kind]
+        src = KIND_BANDS[kind] if bands is None else bands
+        w = _weights(r, c, src, len(src[0]))
+        _KIND_CACHE[key] = (1.0 / w, natural_order(r, c))
+    return _KIND_CACHE[key]
 
 
 def _llf_scale(M):
@@ -1115,8 +1160,7 @@ def decode(data: bytes, want_pixels: bool = True, groups=None) -> Decoded:
             raise JxlError("varblock count mismatch")
     # HfGlobal
     s = sec(1 + nlf)
-    if not s.bool():
-        raise JxlError("custom dequant matrices not produced")
+    d.qm_params = read_dequant_matrices(s)
     npresets = s.read(ceil_log2(ng)) + 1
     used_orders = s.u32(("v", 0x5F), ("v", 0x13), ("v", 0), ("b", 13, 0))
     if used_orders:
@@ -1191,6 +1235,7 @@ def decode(data: bytes, want_pixels: bool = True, groups=None) -> Decoded:
 
 def reconstruct(d: Decoded) -> np.ndarray:
     deq = default_dequant()
+    qm = getattr(d, "qm_params", {})
     inv_gs = 65536.0 / d.global_scale
     x_mul = 1.25 ** (2 - d.x_qm)  # scale 2 -> 1.0
     b_mul = 1.25 ** (2 - d.b_qm)
@@ -1220,7 +1265,7 @@ def reconstruct(d: Decoded) -> np.ndarray:
             if t in SHAPES:
                 ccy, ccx, kind = SHAPES[t]
                 R, C = 8 * ccy, 8 * ccx
-                iw, nat = kind_tables(kind)
+                iw, nat = kind_tables(kind, qm.get(kind))
                 nat = np.array(nat)
                 cols_s = KIND_DIM[kind][1]
                 sy, sx = nat // cols_s, nat % cols_s

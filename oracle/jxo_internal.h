@@ -89,6 +89,13 @@ typedef struct {
   uint16_t* nat;  /* stored raster index -> natural order position */
 } jxo_vkind;
 const jxo_vkind* jxo_vkinds(void);
+/* weight parameters of a kind as the stream carries them (merge.c): kinds
+ * 128X64 ... 256X256 rounded through binary16 (written explicitly into
+ * DequantMatrices), the others the library defaults */
+double jxo_kind_param(int kind, int c, int i);
+int jxo_kind_num_bands(int kind);
+double jxo_f16_round(double v);
+uint32_t jxo_f16_bits(double v);
 int jxo_shape_of(int type); /* shape index of a merged raw id, -1 otherwise */
 float jxo_varblock(const jxo_frame* f, const jxo_shape* s, const float* xyb, int px0, int py0,
                    int raw, int32_t* q /* [3][R*C] natural order */, float* llf /* [3][32][32] */,

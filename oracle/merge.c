@@ -134,14 +134,51 @@ static const int kNumBands[JXO_NVKINDS] = {7, 7, 8, 8, 8, 8, 8, 8, 8, 8};
 static const int kKindDim[JXO_NVKINDS][2] = {{8, 16},  {16, 16},  {16, 32},   {32, 32},  {32, 64},
                                              {64, 64}, {64, 128}, {128, 128}, {128, 256}, {256, 256}};
 
+/* nearest binary16 value (ties to even) of v, as a double [ext F16Coder] */
+double jxo_f16_round(double v) {
+  const double a = fabs(v);
+  if (a == 0.0) return 0.0;
+  int e;
+  (void)frexp(a, &e); /* a = m * 2^e, m in [0.5, 1) */
+  int ue = e - 11;    /* ulp exponent of an 11-bit significand */
+  if (ue < -24) ue = -24; /* subnormal spacing */
+  const double q = ldexp(nearbyint(ldexp(a, -ue)), ue);
+  return v < 0 ? -q : q;
+}
+/* binary16 bits of a value that jxo_f16_round leaves unchanged */
+uint32_t jxo_f16_bits(double v) {
+  const uint32_t sign = v < 0 ? 0x8000u : 0u;
+  const double a = fabs(v);
+  if (a == 0.0) return sign;
+  if (a < ldexp(1.0, -14)) return sign | (uint32_t)ldexp(a, 24); /* subnormal */
+  int e;
+  const double m = frexp(a, &e); /* a = 2m * 2^(e-1), 2m in [1, 2) */
+  const uint32_t mant = (uint32_t)ldexp(2.0 * m - 1.0, 10);
+  return sign | (uint32_t)(e - 1 + 15) << 10 | mant;
+}
+
+/* The quantization tables of kinds 128X64 ... 256X256 are written into the
+ * stream (DequantMatrices, mode DCT: per channel the first band / 64 and the
+ * band ratios as binary16, put_dequant_matrices in encode.c), so the encoder
+ * quantizes with the parameters as the decoder reads them: the first band
+ * 64 * f16(band / 64), the others f16(v) [ext quant_weights.cc
+ * DecodeDctParams].  Kinds below 128 keep the library's defaults (mode
+ * Library) and are used as restated. */
+double jxo_kind_param(int kind, int c, int i) {
+  const double v = kBands[kind][c][i];
+  if (kind < JXO_VK_128X64) return v;
+  return i ? jxo_f16_round(v) : 64.0 * jxo_f16_round(v / 64.0);
+}
+int jxo_kind_num_bands(int kind) { return kNumBands[kind]; }
+
 /* GetQuantWeights [ext]: bands -> weights over a rows x cols table */
 static void kind_weights(int kind, float* out3[3]) {
   const int rows = kKindDim[kind][0], cols = kKindDim[kind][1], nb = kNumBands[kind];
   for (int c = 0; c < 3; c++) {
     double bands[8];
-    bands[0] = kBands[kind][c][0];
+    bands[0] = jxo_kind_param(kind, c, 0);
     for (int i = 1; i < nb; i++) {
-      const double v = kBands[kind][c][i];
+      const double v = jxo_kind_param(kind, c, i);
       bands[i] = bands[i - 1] * (v > 0 ? 1.0 + v : 1.0 / (1.0 - v));
     }
     const double scale = (nb - 1) / (1.4142135623730951 + 1e-6);

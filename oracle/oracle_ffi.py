@@ -78,6 +78,8 @@ def lib():
         _lib.jxo_export_dct.argtypes = [ctypes.c_void_p, ctypes.c_int]
         _lib.jxo_set_debug_big_cost.argtypes = [ctypes.c_void_p]
         _lib.jxo_set_debug_big_cost.restype = None
+        _lib.jxo_set_debug_group_bins.argtypes = [ctypes.c_void_p]
+        _lib.jxo_set_debug_group_bins.restype = None
         _lib.jxo_synth_rgb8.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,
                                         ctypes.c_void_p]
         _lib.jxo_set_threads.argtypes = [ctypes.c_int]
@@ -202,3 +204,16 @@ def debug_big_costs(rgb: np.ndarray, distance=1.0, effort=8, proposals=0, coder=
     finally:
         lib().jxo_set_debug_big_cost(None)
     return r, buf.reshape(ng, 25)
+
+
+def max_group_bin(rgb: np.ndarray, distance=1.0, effort=7, proposals=0, coder=0, filters=0):
+    """(result, the largest count of one (static cluster, token) bin inside one
+    pass group) -- what the product's per-group LDS histogram must hold (test
+    hook)"""
+    buf = np.zeros(1, dtype=np.uint32)
+    lib().jxo_set_debug_group_bins(buf.ctypes.data)
+    try:
+        r = encode(rgb, distance, effort, proposals, coder, filters)
+    finally:
+        lib().jxo_set_debug_group_bins(None)
+    return r, int(buf[0])

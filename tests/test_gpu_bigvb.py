@@ -88,3 +88,42 @@ def test_effort8_sharded_matches_single(jxg_mod):
         single = enc.encode(img)
     for world in (2, 3):
         assert sharded_encode(jxg_mod, img, world, 1.0, 8, 0) == single
+
+
+def chroma_checker_rgb8(w, h):
+    """red / blue one-pixel checkerboard: at d1 e8 a 256x256 group becomes one
+    DCT256X256 whose X and B carry little but their last coefficient, so ~129 K
+    zero tokens land in one (cluster, token) bin of the group"""
+    y, x = np.mgrid[0:h, 0:w]
+    m = ((x + y) % 2).astype(bool)[..., None]
+    return np.where(m, np.array([255, 0, 0]), np.array([0, 60, 255])).astype(np.uint8)
+
+
+@pytest.mark.parametrize("coder", [0, 1])
+def test_whole_group_histogram_bin_above_u16(jxg_mod, oracle, coder):
+    """the whole-group ac_hist_kernel (BR = 32, effort >= 8) counted
+    in u16 LDS halves; a bin past 65535 carried into its neighbour.  The oracle
+    shows this frame's largest per-group bin above 65535, and the GPU bytes
+    (histogram -> codes) equal the oracle's."""
+    img = chroma_checker_rgb8(512, 256)
+    ref, mx = oracle.max_group_bin(img, 1.0, 8, 0, coder)
+    assert mx > 65535, mx
+    flags = jxg_mod.FLAG_ANS if coder else 0
+    with jxg_mod.Encoder(distance=1.0, effort=8, flags=flags) as enc:
+        assert enc.encode(img) == ref.bytes
+
+
+def test_effort8_sharded_ans_decodes_to_single(jxg_mod, decoder):
+    """ANS sharded at effort 8 (one HF preset per rank; the big kinds' quant
+    tables of every rank's groups in HfGlobal): decodes to the single-context
+    image, with the same explicit tables"""
+    from test_gpu_shard import sharded_encode
+
+    img = gradient_rgb8(1024, 768, 11)
+    with jxg_mod.Encoder(distance=1.0, effort=8, flags=jxg_mod.FLAG_ANS) as enc:
+        single = decoder.decode(enc.encode(img))
+    assert single.qm_params
+    for world in (2, 3):
+        got = decoder.decode(sharded_encode(jxg_mod, img, world, 1.0, 8, 0, jxg_mod.FLAG_ANS))
+        assert sorted(got.qm_params) == sorted(single.qm_params)
+        assert np.array_equal(got.rgb, single.rgb)

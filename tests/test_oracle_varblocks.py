@@ -41,7 +41,11 @@ def test_lee_dct_matches_float64(oracle, n):
 @pytest.mark.parametrize("kind", range(10))
 def test_kind_tables_match_decoder(oracle, decoder, kind):
     w, nat = oracle.kind_tables(kind)
-    iw, order = decoder.kind_tables(kind)
+    bands = None
+    if kind >= 6:  # written into DequantMatrices: binary16 parameters
+        bands = [[64.0 * float(np.float16(r[0] / 64.0))] + [float(np.float16(v)) for v in r[1:]]
+                 for r in decoder.KIND_BANDS[kind]]
+    iw, order = decoder.kind_tables(kind, bands)
     rows, cols = decoder.KIND_DIM[kind]
     # natural order: a permutation, LLF (rows/8 x cols/8) first in raster order
     assert sorted(nat.tolist()) == list(range(rows * cols))
@@ -158,3 +162,46 @@ def test_every_big_shape_is_decodable(oracle, decoder):
         seen |= set(int(t) for t in np.unique(r.acs[(r.acs & 0x80) == 0]))
         assert np.array_equal(decoder.decode(r.bytes).ac, r.ac)
     assert {21, 22, 23, 24, 25, 26} <= seen
+
+
+def test_big_quant_tables_travel_in_the_stream(oracle, decoder, monkeypatch):
+    """Effort >= 8 streams carry the quant tables of the 128 / 256 px kinds
+    (HfGlobal DequantMatrices not all_default: Library for the other 13 tables,
+    mode DCT with binary16 band parameters for those of DCT128X128 / 128X64 /
+    256X256 / 256X128 the frame uses), so they decode to the same pixels whatever the decoder's built-in
+    defaults for those kinds are; effort 7 streams still signal all_default."""
+    img = _gradient_rgb8(512, 512, 1024)
+    r8 = oracle.encode(img, 1.0, 8, 0, 1)
+    assert np.isin(r8.acs[(r8.acs & 0x80) == 0], [21, 22, 23, 24, 25, 26]).any()
+    ref = decoder.decode(r8.bytes)
+    kind_of = {22: 6, 23: 6, 21: 7, 25: 8, 26: 8, 24: 9}
+    used = {kind_of[int(t)] for t in np.unique(r8.acs) if int(t) in kind_of}
+    assert sorted(ref.qm_params) == sorted(used) and len(used) >= 2
+    # perturb the decoder's built-in tables of every big kind (and its cache)
+    bad = [list(b) for b in decoder.KIND_BANDS]
+    for k in (6, 7, 8, 9):
+        bad[k] = [[r[0] * 0.37] + [v * 1.9 for v in r[1:]] for r in decoder.KIND_BANDS[k]]
+    monkeypatch.setattr(decoder, "KIND_BANDS", bad)
+    monkeypatch.setattr(decoder, "_KIND_CACHE", {})
+    got = decoder.decode(r8.bytes)
+    assert np.array_equal(got.rgb, ref.rgb)
+    # ... whereas a stream that relies on the defaults would change: e7 keeps
+    # all_default, and perturbing a kind it uses (DCT64X64) moves its pixels
+    r7 = oracle.encode(img, 1.0, 7, 0, 1)
+    assert decoder.decode(r7.bytes).qm_params == {}
+    ok7 = decoder.decode(r7.bytes).rgb
+    bad[5] = [[r[0] * 0.37] + list(r[1:]) for r in decoder.KIND_BANDS[5]]
+    monkeypatch.setattr(decoder, "_KIND_CACHE", {})
+    assert np.isin(r7.acs & 0x7F, [18]).any()
+    assert not np.array_equal(decoder.decode(r7.bytes).rgb, ok7)
+
+
+def test_whole_group_bin_can_pass_u16(oracle):
+    """the premise of tests/test_gpu_bigvb.py::test_whole_group_histogram_bin_above_u16
+    (ADVICE r5): one pass group of this frame puts more than 65535 tokens into
+    one (static cluster, token) bin at effort 8"""
+    y, x = np.mgrid[0:256, 0:512]
+    m = ((x + y) % 2).astype(bool)[..., None]
+    img = np.where(m, np.array([255, 0, 0]), np.array([0, 60, 255])).astype(np.uint8)
+    r, mx = oracle.max_group_bin(img, 1.0, 8, 0, 0)
+    assert mx > 65535 and (r.acs == 24).any()
