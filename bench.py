@@ -307,6 +307,104 @@ def quality_probe(enc, img, distance, effort):
     return res
 
 
+def write_png(path, img):
+    """8-bit RGB PNG, filter 0, zlib level 1 (the harness's input format)"""
+    import struct
+    import zlib
+
+    h, w, _ = img.shape
+    raw = np.zeros((h, w * 3 + 1), dtype=np.uint8)
+    raw[:, 1:] = img.reshape(h, w * 3)
+
+    def chunk(t, b):
+        return struct.pack(">I", len(b)) + t + b + struct.pack(">I", zlib.crc32(t + b) & 0xFFFFFFFF)
+
+    with open(path, "wb") as f:
+        f.write(b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, 8, 2, 0, 0, 0)) +
+                chunk(b"IDAT", zlib.compress(raw.tobytes(), 1)) + chunk(b"IEND", b""))
+
+
+def single_image_probe(img, distance, effort, headline_bytes, device, runs=3):
+    """What one image costs a caller that encodes images one at a time -- the
+    harness's pattern (execute_cjxl runs one encoder process per (image,
+    distance, effort), docker_manager.rs:126-136, benchmark.rs:641-660):
+    * cli: `jxg_cjxl IN.png OUT.jxl --distance=D --effort=E` wall time, process
+      start to exit (HIP runtime init, PNG decode, jxg_create, encode, write,
+      jxg_destroy), and the phases the tool reports (JXG_CJXL_TIMING);
+    * encode_rgb8: one-at-a-time jxg_encode_rgb8 from host RGB8 on a warm
+      context (H2D included);
+    * create_destroy: jxg_create + jxg_destroy, and the first encode of a new
+      context (its buffers and tables) against a warm one."""
+    import subprocess
+    import tempfile
+
+    h, w, _ = img.shape
+    out = {"image": "%dx%d synth_rgb8 frame (bench frame 0) as PNG" % (w, h)}
+    flags = jxg.FLAGS_CJXL_DEFAULTS
+    with tempfile.TemporaryDirectory() as td:
+        src = os.path.join(td, "frame.png")
+        t0 = time.perf_counter()
+        write_png(src, img)
+        out["png_bytes"] = os.path.getsize(src)
+        walls, phases, same = [], [], True
+        env = dict(os.environ, JXG_CJXL_TIMING="1")
+        for i in range(runs):
+            dst = os.path.join(td, "frame-%g-%d.jxl" % (distance, effort))
+            t0 = time.perf_counter()
+            p = subprocess.run([jxg.CLI_PATH, src, dst, "--distance=%g" % distance,
+                                "--effort=%d" % effort, "--device=%d" % device],
+                               capture_output=True, text=True, env=env)
+            walls.append((time.perf_counter() - t0) * 1e3)
+            if p.returncode != 0:
+                out["cli_error"] = p.stderr.strip()[-300:]
+                break
+            line = [l for l in p.stderr.splitlines() if l.startswith("{")]
+            if line:
+                phases.append(json.loads(line[-1]))
+            with open(dst, "rb") as f:
+                same = same and (headline_bytes is None or f.read() == headline_bytes)
+        if walls:
+            out["cli"] = {"argv": "jxg_cjxl IN.png OUT.jxl --distance=%g --effort=%d" % (distance, effort),
+                          "ms_wall": [round(x, 1) for x in walls],
+                          "ms_wall_best": round(min(walls), 1),
+                          "mpix_s_wall_best": round(w * h / (min(walls) * 1e3), 1),
+                          "bytes_equal_headline": same}
+            if phases:
+                best = min(range(len(phases)), key=lambda i: walls[i])
+                ph = {k: round(v, 2) for k, v in phases[best].items()}
+                ph["ms_process_and_runtime"] = round(walls[best] - sum(phases[best].values()), 1)
+                out["cli"]["phases_best_run"] = ph
+    # one-at-a-time jxg_encode_rgb8 from host memory, warm context
+    host = np.ascontiguousarray(img)
+    t0 = time.perf_counter()
+    enc = jxg.Encoder(distance=distance, effort=effort, device=device, flags=flags)
+    t_create = (time.perf_counter() - t0) * 1e3
+    t0 = time.perf_counter()
+    first = enc.encode(host)
+    t_first = (time.perf_counter() - t0) * 1e3
+    ts = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        enc.encode(host)
+        ts.append((time.perf_counter() - t0) * 1e3)
+    t0 = time.perf_counter()
+    enc.close()
+    t_destroy = (time.perf_counter() - t0) * 1e3
+    cd = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        jxg.Encoder(distance=distance, effort=effort, device=device, flags=flags).close()
+        cd.append((time.perf_counter() - t0) * 1e3)
+    out["encode_rgb8"] = {"ms": [round(x, 2) for x in ts], "ms_median": round(float(np.median(ts)), 2),
+                          "mpix_s": round(w * h / (float(np.median(ts)) * 1e3), 1),
+                          "bytes_equal_headline": headline_bytes is None or first == headline_bytes}
+    out["create_destroy"] = {"ms_first_create": round(t_create, 2),
+                             "ms_first_encode_new_context": round(t_first, 2),
+                             "ms_destroy": round(t_destroy, 2),
+                             "ms_create_destroy": [round(x, 2) for x in cd]}
+    return out
+
+
 def spawn_ranks(n, argv):
     """Run this script as n ranks under torch.distributed.run (one node,
     rendezvous on 127.0.0.1) in a child process; returns its exit status."""
@@ -383,6 +481,8 @@ def main():
                          "each (reported under cpu_baseline.sweep)")
     ap.add_argument("--no-quality", action="store_true",
                     help="skip the untimed decode-PSNR probe")
+    ap.add_argument("--no-single", action="store_true",
+                    help="skip the untimed one-image-at-a-time probe (single_image)")
     args = ap.parse_args()
 
     # one process per GPU: with WORLD_SIZE unset, --gpus N > 1 starts the N
@@ -800,6 +900,11 @@ def main():
             res["ms_wait_ranks"] = [round(b * 1e3 / args.steps, 3) for _, b in R["per_rank"]]
         if world == 1 and not args.no_quality:
             res["quality"] = quality_probe(R["enc"], img, args.distance, args.effort)
+        if world == 1 and not args.no_single and args.preset == "cjxl" and args.coder == "ans":
+            # the drop-in's per-call cost (untimed: after the timed region)
+            res["single_image"] = single_image_probe(img, args.distance, args.effort,
+                                                     R["last"] if args.proposals == 0 else None,
+                                                     local)
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(img, args.distance, args.effort, args.proposals,
                                                1 if args.coder == "ans" else 0,

@@ -334,6 +334,13 @@ jxg_status jxg_compare_rgb8_device(jxg_ctx* ctx, const void* d_orig, size_t orig
                                    const void* d_comp, size_t comp_stride, uint32_t xsize,
                                    uint32_t ysize, int want_ssim, jxg_quality* out);
 
+/* Prepares the context for frames of xsize x ysize before the first one
+ * arrives: encodes one synthetic frame of that size (device-generated, result
+ * discarded), which allocates the size's device buffers and loads every
+ * kernel.  Optional -- a caller that creates a context per image (the
+ * harness's execute_cjxl pattern, docker_manager.rs:126-136) runs it beside
+ * its image decode; jxg_cjxl does.  Not while streamed frames are pending. */
+jxg_status jxg_warmup(jxg_ctx* ctx, uint32_t xsize, uint32_t ysize);
 /* ---- benchmark input ----
  * The deterministic synthetic RGB8 frame of SURVEY.md §8(d) (64x64 tiles of
  * flat / gradient / stripe / checker / edge / noise content, splitmix64

@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/jxg.h"
@@ -35,13 +36,48 @@ bool read_file(const char* path, std::vector<uint8_t>& out) {
 
 uint32_t be32(const uint8_t* p) { return (uint32_t)p[0] << 24 | p[1] << 16 | p[2] << 8 | p[3]; }
 
+// PNG: the IDAT stream is inflated in 1 MB pieces and every completed row is
+// unfiltered straight into the RGB output (one switch per row, the filter's
+// own loop; no whole-image inflate buffer), so the pass over the pixels runs
+// while the data is still in cache.  (The first form inflated the whole
+// image, then unfiltered byte by byte through a switch: 275 ms of an 8K
+// frame's 496 ms process wall time, bench.py single_image, round 6.)
+bool unfilter_row(uint8_t ft, const uint8_t* src, const uint8_t* prev, uint8_t* row,
+                  size_t stride, int ch) {
+  switch (ft) {
+    case 0:
+      std::memcpy(row, src, stride);
+      return true;
+    case 1:
+      for (size_t x = 0; x < stride; x++) row[x] = (uint8_t)(src[x] + (x >= (size_t)ch ? row[x - ch] : 0));
+      return true;
+    case 2:
+      for (size_t x = 0; x < stride; x++) row[x] = (uint8_t)(src[x] + prev[x]);
+      return true;
+    case 3:
+      for (size_t x = 0; x < stride; x++)
+        row[x] = (uint8_t)(src[x] + ((x >= (size_t)ch ? row[x - ch] : 0) + prev[x]) / 2);
+      return true;
+    case 4:
+      for (size_t x = 0; x < stride; x++) {
+        const int a = x >= (size_t)ch ? row[x - ch] : 0, b = prev[x],
+                  c = x >= (size_t)ch ? prev[x - ch] : 0;
+        const int pp = a + b - c, pa = std::abs(pp - a), pb = std::abs(pp - b), pc = std::abs(pp - c);
+        row[x] = (uint8_t)(src[x] + ((pa <= pb && pa <= pc) ? a : (pb <= pc ? b : c)));
+      }
+      return true;
+    default:
+      return false;
+  }
+}
+
 bool decode_png(const std::vector<uint8_t>& d, std::vector<uint8_t>& rgb, uint32_t& w,
                 uint32_t& h, std::string& err) {
   static const uint8_t sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
   if (d.size() < 8 || std::memcmp(d.data(), sig, 8)) return err = "not a PNG", false;
   size_t p = 8;
   int depth = 0, ctype = -1, interlace = 0;
-  std::vector<uint8_t> idat;
+  std::vector<std::pair<const uint8_t*, size_t>> idat;  // the IDAT pieces in place
   while (p + 12 <= d.size()) {
     const uint32_t len = be32(&d[p]);
     const char* type = (const char*)&d[p + 4];
@@ -54,7 +90,7 @@ bool decode_png(const std::vector<uint8_t>& d, std::vector<uint8_t>& rgb, uint32
       ctype = body[9];
       interlace = body[12];
     } else if (!std::memcmp(type, "IDAT", 4)) {
-      idat.insert(idat.end(), body, body + len);
+      idat.emplace_back(body, (size_t)len);
     } else if (!std::memcmp(type, "IEND", 4)) {
       break;
     }
@@ -62,41 +98,71 @@ bool decode_png(const std::vector<uint8_t>& d, std::vector<uint8_t>& rgb, uint32
   }
   if (depth != 8 || interlace || !(ctype == 0 || ctype == 2 || ctype == 4 || ctype == 6))
     return err = "unsupported PNG (need 8-bit, non-interlaced gray/RGB[A])", false;
+  if (w == 0 || h == 0 || w > (1u << 20) || h > (1u << 20)) return err = "bad PNG size", false;
   const int ch = ctype == 0 ? 1 : ctype == 2 ? 3 : ctype == 4 ? 2 : 4;
-  const size_t stride = (size_t)w * ch;
-  std::vector<uint8_t> raw((stride + 1) * h);
-  uLongf rawlen = raw.size();
-  if (uncompress(raw.data(), &rawlen, idat.data(), idat.size()) != Z_OK || rawlen != raw.size())
-    return err = "PNG inflate failed", false;
-  std::vector<uint8_t> img(stride * h), prev(stride, 0);
-  for (uint32_t y = 0; y < h; y++) {
-    const uint8_t ft = raw[y * (stride + 1)];
-    const uint8_t* src = &raw[y * (stride + 1) + 1];
-    uint8_t* row = &img[y * stride];
-    for (size_t x = 0; x < stride; x++) {
-      const int a = x >= (size_t)ch ? row[x - ch] : 0, b = prev[x],
-                c = x >= (size_t)ch ? prev[x - ch] : 0;
-      int v = src[x];
-      switch (ft) {
-        case 0: break;
-        case 1: v += a; break;
-        case 2: v += b; break;
-        case 3: v += (a + b) / 2; break;
-        case 4: {
-          const int pp = a + b - c, pa = std::abs(pp - a), pb = std::abs(pp - b), pc = std::abs(pp - c);
-          v += (pa <= pb && pa <= pc) ? a : (pb <= pc ? b : c);
-          break;
-        }
-        default: return err = "bad PNG filter", false;
-      }
-      row[x] = (uint8_t)v;
-    }
-    std::memcpy(prev.data(), row, stride);
-  }
+  const size_t stride = (size_t)w * ch, rowbytes = stride + 1;
   rgb.resize((size_t)w * h * 3);
-  for (size_t i = 0; i < (size_t)w * h; i++)
-    for (int c = 0; c < 3; c++) rgb[i * 3 + c] = img[i * ch + (ch >= 3 ? c : 0)];
+  // RGB rows are unfiltered in place in the output; other layouts go through
+  // a two-row buffer and are converted per row
+  std::vector<uint8_t> tmp(ch == 3 ? 0 : 2 * stride, 0), zero(stride, 0);
+  std::vector<uint8_t> buf((size_t)1 << 20);
+  if (buf.size() < 2 * rowbytes) buf.resize(2 * rowbytes);
+  z_stream zs{};
+  if (inflateInit(&zs) != Z_OK) return err = "PNG inflate failed", false;
+  size_t have = 0, piece = 0;
+  uint32_t y = 0;
+  int zr = Z_OK;
+  while (y < h) {
+    if (zs.avail_in == 0 && piece < idat.size()) {
+      zs.next_in = const_cast<Bytef*>(idat[piece].first);
+      zs.avail_in = (uInt)idat[piece].second;
+      piece++;
+    }
+    zs.next_out = buf.data() + have;
+    zs.avail_out = (uInt)(buf.size() - have);
+    zr = inflate(&zs, Z_NO_FLUSH);
+    if (zr != Z_OK && zr != Z_STREAM_END && !(zr == Z_BUF_ERROR && zs.avail_in == 0)) break;
+    have = buf.size() - zs.avail_out;
+    size_t used = 0;
+    while (y < h && have - used >= rowbytes) {
+      const uint8_t* src = buf.data() + used;
+      uint8_t* row = ch == 3 ? &rgb[(size_t)y * stride] : &tmp[(y & 1) * stride];
+      const uint8_t* prev = y == 0 ? zero.data() : (ch == 3 ? row - stride : &tmp[((y + 1) & 1) * stride]);
+      if (!unfilter_row(src[0], src + 1, prev, row, stride, ch)) {
+        inflateEnd(&zs);
+        return err = "bad PNG filter", false;
+      }
+      if (ch != 3) {
+        uint8_t* o = &rgb[(size_t)y * w * 3];
+        for (uint32_t x = 0; x < w; x++)
+          for (int c = 0; c < 3; c++) o[x * 3 + c] = row[x * ch + (ch >= 3 ? c : 0)];
+      }
+      used += rowbytes;
+      y++;
+    }
+    std::memmove(buf.data(), buf.data() + used, have - used);
+    have -= used;
+    if (zr == Z_STREAM_END || (zs.avail_in == 0 && piece == idat.size() && zs.avail_out != 0))
+      if (y < h && have < rowbytes) break;
+  }
+  inflateEnd(&zs);
+  if (y != h) return err = "PNG inflate failed", false;
   return true;
+}
+
+// the image size from the PNG IHDR / PPM header (0 x 0 if unknown)
+void probe_dims(const std::vector<uint8_t>& d, uint32_t& w, uint32_t& h) {
+  static const uint8_t sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
+  w = h = 0;
+  if (d.size() >= 24 && !std::memcmp(d.data(), sig, 8) && !std::memcmp(&d[12], "IHDR", 4)) {
+    w = be32(&d[16]);
+    h = be32(&d[20]);
+  } else if (d.size() >= 2 && d[0] == 'P' && d[1] == '6') {
+    std::string s(d.begin(), d.begin() + std::min<size_t>(d.size(), 64));
+    unsigned W = 0, H = 0;
+    if (std::sscanf(s.c_str(), "P6 %u %u", &W, &H) == 2) w = W, h = H;
+  }
+  if (w > (1u << 18) || h > (1u << 18)) w = h = 0;
 }
 
 bool decode_ppm(const std::vector<uint8_t>& d, std::vector<uint8_t>& rgb, uint32_t& w,
@@ -174,10 +240,43 @@ int main(int argc, char** argv) {
       return 1;
     }
   }
+  // JXG_CJXL_TIMING=1: the phases of this call as one JSON line on stderr
+  // (bench.py's single_image probe: where a per-image process spends its time)
+  using Clk = std::chrono::steady_clock;
+  const auto ms = [](Clk::time_point a, Clk::time_point b) {
+    return std::chrono::duration<double, std::milli>(b - a).count();
+  };
+  const bool timing = std::getenv("JXG_CJXL_TIMING") != nullptr;
+  const auto t_start = Clk::now();
+  jxg_ctx* ctx = nullptr;
+  jxg_status st = JXG_OK;
+  double ms_create = 0.0;
+  // JXG_CJXL_DECODE_ONLY=1 (tests, no GPU): write the decoded image as a
+  // binary PPM to OUTPUT instead of encoding it
+  const bool decode_only = std::getenv("JXG_CJXL_DECODE_ONLY") != nullptr;
+  std::thread maker;
+  auto fail = [&](int code) {
+    if (maker.joinable()) maker.join();
+    if (ctx) jxg_destroy(ctx);
+    return code;
+  };
   std::vector<uint8_t> file, rgb;
   if (!read_file(argv[1], file)) {
     std::fprintf(stderr, "cannot read %s\n", argv[1]);
     return 1;
+  }
+  // the context (HIP runtime initialisation, device buffers for the image's
+  // size, every kernel's code object: jxg_create + jxg_warmup) is made on a
+  // second thread while this one decodes the image
+  uint32_t pw = 0, ph = 0;
+  if (!decode_only) {
+    probe_dims(file, pw, ph);
+    maker = std::thread([&] {
+      const auto t = Clk::now();
+      st = jxg_create(&p, &ctx);
+      if (st == JXG_OK && pw && ph) (void)jxg_warmup(ctx, pw, ph);  // (best effort)
+      ms_create = ms(t, Clk::now());
+    });
   }
   uint32_t w = 0, h = 0;
   std::string err;
@@ -186,10 +285,20 @@ int main(int argc, char** argv) {
                       : decode_png(file, rgb, w, h, err);
   if (!ok) {
     std::fprintf(stderr, "%s: %s\n", argv[1], err.c_str());
-    return 1;
+    return fail(1);
   }
-  jxg_ctx* ctx = nullptr;
-  jxg_status st = jxg_create(&p, &ctx);
+  const auto t_read = Clk::now();
+  if (decode_only) {
+    FILE* f = std::fopen(argv[2], "wb");
+    const bool wr = f && std::fprintf(f, "P6\n%u %u\n255\n", w, h) > 0 &&
+                    std::fwrite(rgb.data(), 1, rgb.size(), f) == rgb.size();
+    if (f) std::fclose(f);
+    if (timing) std::fprintf(stderr, "{\"ms_read_decode\": %.3f}\n", ms(t_start, t_read));
+    if (!wr) std::fprintf(stderr, "cannot write %s\n", argv[2]);
+    return wr ? 0 : 1;
+  }
+  maker.join();
+  const auto t_create = Clk::now();  // (the wait for the context, if any)
   if (st != JXG_OK) {
     std::fprintf(stderr, "jxg_create: %s\n", jxg_status_str(st));
     return 1;
@@ -197,7 +306,8 @@ int main(int argc, char** argv) {
   jxg_buffer out{};
   const auto t0 = std::chrono::steady_clock::now();
   st = jxg_encode_rgb8(ctx, rgb.data(), w, h, (size_t)w * 3, &out);
-  const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  const auto t_enc = Clk::now();
+  const double sec = std::chrono::duration<double>(t_enc - t0).count();
   if (st != JXG_OK) {
     std::fprintf(stderr, "encode failed: %s\n", jxg_status_str(st));
     jxg_destroy(ctx);
@@ -212,10 +322,19 @@ int main(int argc, char** argv) {
     return 1;
   }
   std::fclose(f);
+  const auto t_write = Clk::now();
   std::printf("Encoding [VarDCT, d%.3f, effort: %d], %u x %u, %zu bytes, %.3f bpp, %.2f MP/s\n",
               p.distance, p.effort, w, h, out.size, out.size * 8.0 / ((double)w * h),
               (double)w * h / 1e6 / sec);
   jxg_buffer_free(&out);
   jxg_destroy(ctx);
+  if (timing) {
+    const auto t_end = Clk::now();
+    std::fprintf(stderr,
+                 "{\"ms_read_decode\": %.3f, \"ms_create_wait\": %.3f, \"ms_encode\": %.3f, "
+                 "\"ms_write\": %.3f, \"ms_destroy\": %.3f, \"ms_create_overlapped\": %.3f}\n",
+                 ms(t_start, t_read), ms(t_read, t_create), sec * 1e3,
+                 ms(t_enc, t_write), ms(t_write, t_end), ms_create);
+  }
   return 0;
 }

@@ -173,18 +173,15 @@ __device__ __forceinline__ float homogeneity(const Tile& t, const uint64_t* lbit
 // region r of CalculateHomogeneitySimilarityIndices (combined.diff:189-204):
 // 0 h1(8,4,0,0) 1 h2(8,4,0,4) 2 v1(4,8,0,0) 3 v2(4,8,4,0)
 // 4 (4,4,0,0) 5 (4,4,4,4) 6 (4,4,0,4) 7 (4,4,4,0)
+// (one instantiation per region shape, the offsets at run time: r is
+// wave-uniform, and eight inlined copies cost 9 KB of instruction cache)
 __device__ __forceinline__ float homog_region(const Tile& t, const uint64_t* lb, int r, int x, int y,
                                               float dist, int ysize, int h1) {
-  switch (r) {
-    case 0: return homogeneity<8, 4>(t, lb, x, y, 0, 0, dist, ysize, h1);
-    case 1: return homogeneity<8, 4>(t, lb, x, y, 0, 4, dist, ysize, h1);
-    case 2: return homogeneity<4, 8>(t, lb, x, y, 0, 0, dist, ysize, h1);
-    case 3: return homogeneity<4, 8>(t, lb, x, y, 4, 0, dist, ysize, h1);
-    case 4: return homogeneity<4, 4>(t, lb, x, y, 0, 0, dist, ysize, h1);
-    case 5: return homogeneity<4, 4>(t, lb, x, y, 4, 4, dist, ysize, h1);
-    case 6: return homogeneity<4, 4>(t, lb, x, y, 0, 4, dist, ysize, h1);
-    default: return homogeneity<4, 4>(t, lb, x, y, 4, 0, dist, ysize, h1);
-  }
+  const int bx = (r == 3 || r == 5 || r == 7) ? 4 : 0;
+  const int by = (r == 1 || r == 5 || r == 6) ? 4 : 0;
+  if (r < 2) return homogeneity<8, 4>(t, lb, x, y, bx, by, dist, ysize, h1);
+  if (r < 4) return homogeneity<4, 8>(t, lb, x, y, bx, by, dist, ysize, h1);
+  return homogeneity<4, 4>(t, lb, x, y, bx, by, dist, ysize, h1);
 }
 
 __device__ __forceinline__ float fmax_std(float a, float b) { return (a < b) ? b : a; }
@@ -543,10 +540,9 @@ __device__ __forceinline__ uint32_t pack_q(int lo, int hi) {
 // qa is kept as an integer-valued float qf (the truncation of a positive value
 // is its floor): the error needs no conversion, and the rate 2 + 2 bitlen(qa)
 // of a non-zero is 2 E - 250, E = the biased exponent of qf.
-template <int T, int C>
-__device__ __forceinline__ void quant_lane(const GroupCtx& G, float* v, float scale,
+template <int C>
+__device__ __forceinline__ void quant_lane(const GroupCtx& G, int ti, float* v, float scale,
                                            float inv_scale, CandAcc& A) {
-  constexpr int ti = tindex<T>();
   if (G.r == 0) v[0] = 0.0f;  // DC slot: quantizes to 0, contributes nothing
   const float4* wp = reinterpret_cast<const float4*>(G.wperm + ((ti * 3 + C) * 8 + G.r) * 8);
   const float4 w0 = wp[0], w1 = wp[1];
@@ -640,9 +636,7 @@ __device__ __forceinline__ void quant_lane(const GroupCtx& G, float* v, float sc
 // coefficient k), each channel with its own weights, chroma-from-luma factor
 // and distortion weights: every float op of the pair is one packed op.  The
 // e*e chain keeps the scalar order (X's k = 0..7, then B's).
-template <int T>
-__device__ __forceinline__ void quant_xb(const GroupCtx& G, f2* v, float scale, CandAcc& A) {
-  constexpr int ti = tindex<T>();
+__device__ __forceinline__ void quant_xb(const GroupCtx& G, int ti, f2* v, float scale, CandAcc& A) {
   if (G.r == 0) v[0] = f2{0.0f, 0.0f};  // DC slots quantize to 0
   const float* wxp = G.wperm + ((ti * 3 + 0) * 8 + G.r) * 8;
   const float* wbp = G.wperm + ((ti * 3 + 2) * 8 + G.r) * 8;
@@ -687,34 +681,18 @@ __device__ __forceinline__ void quant_xb(const GroupCtx& G, f2* v, float scale, 
   A.q.nz |= (uint32_t)nzcx | ((uint32_t)nzcb << 16);
 }
 
-// one channel of one candidate (C = kXB: X and B together): transform (row
-// pass + transpose + column transform, or the Haar steps) and quantization.
-// PRE: the row pass and its transpose were already done and are shared by
-// the two candidates with the same row transform (DCT8 / DCT8X4: 8-point rows,
-// from the chroma-from-luma fit of phase B0; DCT4X4 / DCT4X8: 4-point rows):
-// only the column transform is left.
-template <int T, int C, bool PRE = false, class V>
-__device__ __forceinline__ void eval_chan(const GroupCtx& G, float scale, float inv_scale,
-                                          CandAcc& A, const V* pre = nullptr) {
-  V v[8];
-  if constexpr (PRE) {
-    static_assert(T != kDCT2X2 && T != kIDENTITY, "DCT candidates only");
-#pragma unroll
-    for (int k = 0; k < 8; k++) v[k] = pre[k];
-    col_transform<T>(G, v);
-  } else if constexpr (T == kDCT2X2 || T == kIDENTITY) {
-    haar_lane<T, C>(G, v);
-  } else {
-    row_pass_t<T == kDCT8 || T == kDCT8X4, C>(G, v);
-    col_transform<T>(G, v);
-  }
-  if constexpr (C == kXB) quant_xb<T>(G, v, scale, A);
-  else quant_lane<T, C>(G, v, scale, inv_scale, A);
-}
-
-// One candidate: Y, then X and B together (f2); only one candidate's state is
-// live at a time, which keeps the kernel inside 128 VGPRs.  PRE (DCT8,
-// DCT8X4): the fit's transposed 8-point row passes, y[k] and xb[k] = (X, B).
+// One candidate T (run-time, wave-uniform): Y, then X and B together (f2);
+// only one candidate's state is live at a time, which keeps the kernel inside
+// 128 VGPRs.  Round 6: the candidates share one transform dispatch and one
+// quantization body per channel (the kernel evaluates them in two rolled
+// loops, phase C) instead of six fully inlined instantiations -- 130 KB of
+// machine code, twice the instruction cache a CU pair shares, and 31 % of the
+// waves' cycles waiting on instruction fetch (profiles/r05zr/attr_front.json).
+// The float ops of every candidate are unchanged.
+// PRE (DCT8, DCT8X4): the fit's transposed 8-point row passes, y[k] and
+// xb[k] = (X, B), are given; only the column transform is left.  Without PRE
+// (DCT4X4, DCT4X8: 4-point rows; DCT2X2 / IDENTITY: Haar steps; hook P's
+// re-evaluation of DCT8X4: 8-point rows) the transform starts from the pixels.
 // Scan pruning (no effect on any result): the estimate's bits and e*e sum
 // only grow from channel to channel (every non-zero adds 2 + 2 bitlen > 0,
 // bitlen(nz) >= 0; fmaf(e, e, acc) >= acc and the tree sum of non-negative
@@ -731,32 +709,62 @@ struct Prune {
   bool hookF;
   float rh, rv, rd;
 };
-template <int T, bool PRE = false>
-__device__ __forceinline__ float eval_one(const GroupCtx& G, float scale, float inv_scale,
-                                          CandAcc& A, const float* pre_y = nullptr,
-                                          const f2* pre_xb = nullptr,
-                                          const Prune* pr = nullptr) {
+template <bool PRE, int C, class V>
+__device__ __forceinline__ void cand_transform(const GroupCtx& G, int T, V* v, const V* pre) {
+  if constexpr (PRE) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[k] = pre[k];
+    if (T == kDCT8) col_transform<kDCT8>(G, v);
+    else col_transform<kDCT8X4>(G, v);
+  } else {
+    if (T == kDCT4X4 || T == kDCT4X8) {
+      row_pass_t<false, C>(G, v);
+      if (T == kDCT4X4) col_transform<kDCT4X4>(G, v);
+      else col_transform<kDCT4X8>(G, v);
+    } else if (T == kDCT2X2) {
+      haar_lane<kDCT2X2, C>(G, v);
+    } else if (T == kIDENTITY) {
+      haar_lane<kIDENTITY, C>(G, v);
+    } else {  // kDCT8X4 without the fit's rows (hook P's re-evaluation)
+      row_pass_t<true, C>(G, v);
+      col_transform<kDCT8X4>(G, v);
+    }
+  }
+}
+template <bool PRE>
+__device__ __forceinline__ float eval_cand(const GroupCtx& G, int T, float scale, float inv_scale,
+                                           CandAcc& A, const float* pre_y, const f2* pre_xb,
+                                           const Prune& pr) {
   // estimate multipliers (== oracle jxo_quantize_block tmul, JXO_TMUL_*)
-  constexpr float tm = T == kDCT8 ? 1.0f
-                                  : (T == kDCT4X4 ? 1.05f
-                                                  : (T == kDCT2X2 ? 1.05f
-                                                                  : (T == kIDENTITY ? 1.08f : 1.02f)));
+  const float tm = T == kDCT8 ? 1.0f
+                              : (T == kDCT4X4 ? 1.05f
+                                              : (T == kDCT2X2 ? 1.05f
+                                                              : (T == kIDENTITY ? 1.08f : 1.02f)));
+  const int ti = tindex_rt(T);
   A.bits = 0;
   A.part = 0.0f;
   A.q.nz = 0;
-  eval_chan<T, 1, PRE, float>(G, scale, inv_scale, A, pre_y);
-  if (pr && pr->on) {
+  {
+    float v[8];
+    cand_transform<PRE, 1>(G, T, v, pre_y);
+    quant_lane<1>(G, ti, v, scale, inv_scale, A);
+  }
+  if (pr.on) {
     float lb = ((float)group_int_sum(A.bits) + 8.0f * group_tree_sum(A.part)) * tm;
     bool out;
-    if (pr->hookF) {
-      const float avg_r = (pr->rh + pr->rv + pr->rd) / 3.0f;
-      out = avg_r >= 0.0f && hook_f(lb, pr->rh, pr->rv, pr->rd) > pr->best;
+    if (pr.hookF) {
+      const float avg_r = (pr.rh + pr.rv + pr.rd) / 3.0f;
+      out = avg_r >= 0.0f && hook_f(lb, pr.rh, pr.rv, pr.rd) > pr.best;
     } else {
-      out = lb > pr->best;
+      out = lb > pr.best;
     }
     if (__all(out)) return __builtin_nanf("");
   }
-  eval_chan<T, kXB, PRE, f2>(G, scale, inv_scale, A, pre_xb);
+  {
+    f2 v[8];
+    cand_transform<PRE, kXB>(G, T, v, pre_xb);
+    quant_xb(G, ti, v, scale, A);
+  }
   return ((float)group_int_sum(A.bits) + 8.0f * group_tree_sum(A.part)) * tm;
 }
 
@@ -788,63 +796,88 @@ __device__ __forceinline__ bool beats(float ea, int ia, float eb, int ib) {
 constexpr int kChunksX = 18;
 constexpr int kChunks = kRows * kChunksX;
 constexpr int kChunkIters = (kChunks + kThreads - 1) / kThreads;
-__device__ __forceinline__ void load_xyb_tile(const FrontArgs& a, const float* lut, float* sPix,
-                                              int ox, int oy) {
-  const bool al = ((a.stride | (size_t)a.rgb) & 3) == 0;
-  uint32_t d[kChunkIters][3];
-#pragma unroll
-  for (int k = 0; k < kChunkIters; k++) {
-    const int i = min(threadIdx.x + k * kThreads, kChunks - 1);
-    const int ly = i / kChunksX, cx = i - ly * kChunksX;
-    const int gy = oy + ly, gx0 = ox - 3 + 4 * cx;
-    const int sy = min(max(gy, 0), (int)a.h - 1);
-    const uint8_t* row = a.rgb + (size_t)sy * a.stride;
-    if (al && gx0 >= 0 && gx0 + 4 <= (int)a.w) {
-      const uint32_t* p = reinterpret_cast<const uint32_t*>(row + 3 * (size_t)gx0);
-      d[k][0] = p[0];
-      d[k][1] = p[1];
-      d[k][2] = p[2];
-    } else {
-      uint32_t by[12];
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const int sx = min(max(gx0 + j, 0), (int)a.w - 1);
-        const uint8_t* q = row + 3 * (size_t)sx;
-        by[3 * j] = q[0];
-        by[3 * j + 1] = q[1];
-        by[3 * j + 2] = q[2];
-      }
-#pragma unroll
-      for (int w = 0; w < 3; w++)
-        d[k][w] = by[4 * w] | by[4 * w + 1] << 8 | by[4 * w + 2] << 16 | by[4 * w + 3] << 24;
-    }
-  }
-  const float cb = cbrt_det(kOpsinBias);
-#pragma unroll
-  for (int k = 0; k < kChunkIters; k++) {
-    const int i = threadIdx.x + k * kThreads;
-    if (i >= kChunks) continue;
-    const int ly = i / kChunksX, cx = i - ly * kChunksX;
-    const int gy = oy + ly, gx0 = ox - 3 + 4 * cx;
+// chunk i's 12 bytes (4 pixels), clamped to the image
+__device__ __forceinline__ void load_chunk(const FrontArgs& a, bool al, int i, int ox, int oy,
+                                           uint32_t d[3]) {
+  const int ly = i / kChunksX, cx = i - ly * kChunksX;
+  const int gy = oy + ly, gx0 = ox - 3 + 4 * cx;
+  const int sy = min(max(gy, 0), (int)a.h - 1);
+  const uint8_t* row = a.rgb + (size_t)sy * a.stride;
+  if (al && gx0 >= 0 && gx0 + 4 <= (int)a.w) {
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(row + 3 * (size_t)gx0);
+    d[0] = p[0];
+    d[1] = p[1];
+    d[2] = p[2];
+  } else {
+    uint32_t by[12];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      const int lx = 4 * cx - 3 + j;
-      if (lx < 0 || lx >= 66) continue;
-      const int gx = gx0 + j;
-      const bool inside = gx >= 0 && gy >= 0 && gx < (int)a.xp && gy < (int)a.yp;
-      float X = 0.0f, Y = 0.0f, B = 0.0f;
-      if (inside) {
-        const int b0 = 3 * j;
-        const uint32_t r8 = (d[k][b0 >> 2] >> ((b0 & 3) * 8)) & 0xFF;
-        const uint32_t g8 = (d[k][(b0 + 1) >> 2] >> (((b0 + 1) & 3) * 8)) & 0xFF;
-        const uint32_t b8 = (d[k][(b0 + 2) >> 2] >> (((b0 + 2) & 3) * 8)) & 0xFF;
-        pixel_xyb(lut, cb, r8, g8, b8, X, Y, B);
-      }
-      const int o = lds_at(lx, ly);
-      sPix[o] = X;
-      sPix[kPlane + o] = Y;
-      sPix[2 * kPlane + o] = B;
+      const int sx = min(max(gx0 + j, 0), (int)a.w - 1);
+      const uint8_t* q = row + 3 * (size_t)sx;
+      by[3 * j] = q[0];
+      by[3 * j + 1] = q[1];
+      by[3 * j + 2] = q[2];
     }
+#pragma unroll
+    for (int w = 0; w < 3; w++)
+      d[w] = by[4 * w] | by[4 * w + 1] << 8 | by[4 * w + 2] << 16 | by[4 * w + 3] << 24;
+  }
+}
+// rep (Gaborish): samples outside the block-padded frame hold the clamped
+// image sample too (the inverse Gaborish reads every source at coordinates
+// clamped to the padded frame, i.e. the image sample at coordinates clamped to
+// the image); they are zeroed again after the sweep (zero_outside).
+// The chunks go through a rolled loop with the next chunk's loads issued
+// before the current one's conversion: four inlined conversions instead of
+// twelve (round 6: the kernel's instruction-cache footprint).
+__device__ __forceinline__ void load_xyb_tile(const FrontArgs& a, const float* lut, float* sPix,
+                                              int ox, int oy, bool rep) {
+  const bool al = ((a.stride | (size_t)a.rgb) & 3) == 0;
+  const float cb = cbrt_det(kOpsinBias);
+  uint32_t d[3];
+  load_chunk(a, al, min((int)threadIdx.x, kChunks - 1), ox, oy, d);
+#pragma unroll 1
+  for (int k = 0; k < kChunkIters; k++) {
+    const int i = threadIdx.x + k * kThreads;
+    uint32_t nx[3] = {0u, 0u, 0u};
+    if (k + 1 < kChunkIters) load_chunk(a, al, min(i + kThreads, kChunks - 1), ox, oy, nx);
+    if (i < kChunks) {
+      const int ly = i / kChunksX, cx = i - ly * kChunksX;
+      const int gy = oy + ly, gx0 = ox - 3 + 4 * cx;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int lx = 4 * cx - 3 + j;
+        if (lx < 0 || lx >= 66) continue;
+        const int gx = gx0 + j;
+        const bool inside = rep || (gx >= 0 && gy >= 0 && gx < (int)a.xp && gy < (int)a.yp);
+        float X = 0.0f, Y = 0.0f, B = 0.0f;
+        if (inside) {
+          const int b0 = 3 * j;
+          const uint32_t r8 = (d[b0 >> 2] >> ((b0 & 3) * 8)) & 0xFF;
+          const uint32_t g8 = (d[(b0 + 1) >> 2] >> (((b0 + 1) & 3) * 8)) & 0xFF;
+          const uint32_t b8 = (d[(b0 + 2) >> 2] >> (((b0 + 2) & 3) * 8)) & 0xFF;
+          pixel_xyb(lut, cb, r8, g8, b8, X, Y, B);
+        }
+        const int o = lds_at(lx, ly);
+        sPix[o] = X;
+        sPix[kPlane + o] = Y;
+        sPix[2 * kPlane + o] = B;
+      }
+    }
+#pragma unroll
+    for (int w = 0; w < 3; w++) d[w] = nx[w];
+  }
+}
+// samples outside the block-padded frame back to 0 (H2) after the sweep
+__device__ __forceinline__ void zero_outside(const FrontArgs& a, float* sPix, int ox, int oy) {
+  for (int i = threadIdx.x; i < 66 * 66; i += kThreads) {
+    const int ly = i / 66, lx = i - ly * 66;
+    const int gx = ox + lx, gy = oy + ly;
+    if (gx >= 0 && gy >= 0 && gx < (int)a.xp && gy < (int)a.yp) continue;
+    const int o = lds_at(lx, ly);
+    sPix[o] = 0.0f;
+    sPix[kPlane + o] = 0.0f;
+    sPix[2 * kPlane + o] = 0.0f;
   }
 }
 
@@ -895,27 +928,23 @@ __device__ __forceinline__ void gab_ring(const FrontArgs& a, const float* lut, f
     ring[2 * kRing + i] = B;
   }
 }
-// the unfiltered sample at tile-local (lx, ly) in [-1, 66]^2, clamped to the
-// padded frame
-__device__ __forceinline__ float gab_src(const float* P, const float* R, int lx, int ly, int ox,
-                                         int oy, int xp, int yp) {
-  lx = min(max(lx, -ox), xp - 1 - ox);
-  ly = min(max(ly, -oy), yp - 1 - oy);
-  if (lx >= 0 && lx < 66 && ly >= 0 && ly < 66) return P[lds_at(lx, ly)];
-  return R[ring_index(lx, ly)];
-}
 // Sweep: thread = (row half, channel, column), 396 threads; a 3 x 3 window in
 // registers, one new row per step, the 33 outputs of its column half kept in
 // registers until every thread has read its inputs (one barrier), then
 // stored in place.  (Round 4 stored each row after a barrier of its own: 33
-// barriers per tile.)
+// barriers per tile.)  Each source column is one LDS column at a per-thread
+// base (row offsets become immediates), the two ring columns are read beside
+// it and selected, and only the first row (half 0) and the last row (half 1)
+// come from the ring rows.
 //
-// Interior tiles (every sample of the 68 x 68 window inside the padded frame:
-// 96 % of an 8K frame's tiles) take a clamp-free form of the same sweep: each
-// source column is one LDS column at a per-thread base (row offsets become
-// immediates), the two ring columns are read beside it and selected, and only
-// the first row (half 0) and the last row (half 1) come from the ring rows.
-__device__ __forceinline__ void gab_sweep_interior(float* sPix, const float* ring) {
+// Round 6: every tile takes this form.  The edge tiles' clamped sweep (a
+// second 33-step body with a clamp per sample: 28 KB of the kernel's code)
+// is gone: an edge tile's LDS tile and ring hold the clamped image sample at
+// every position (load_xyb_tile rep; gab_ring clamps to the image), which is
+// what the clamped sweep read, so every in-frame output is the same float
+// expression of the same values; the positions outside the padded frame are
+// zeroed after it (zero_outside).
+__device__ __forceinline__ void gab_sweep(float* sPix, const float* ring) {
   const int t = threadIdx.x;
   const bool act = t < 396;
   const int half = t >= 198 ? 1 : 0, c = (t - 198 * half) / 66, lx = t % 66;
@@ -976,52 +1005,6 @@ __device__ __forceinline__ void gab_sweep_interior(float* sPix, const float* rin
     for (int st = 0; st < 33; st++) P[lds_at(lx, y0 + st)] = out[st];
   }
 }
-__device__ __forceinline__ void gab_sweep(const FrontArgs& a, float* sPix, const float* ring,
-                                          int ox, int oy) {
-  if (ox >= 1 && oy >= 1 && ox + 67 <= (int)a.xp && oy + 67 <= (int)a.yp) {  // (uniform)
-    gab_sweep_interior(sPix, ring);
-    return;
-  }
-  const int t = threadIdx.x;
-  const bool act = t < 396;
-  const int half = t >= 198 ? 1 : 0, c = (t - 198 * half) / 66, lx = t % 66;
-  const int y0 = 33 * half;
-  const int xp = (int)a.xp, yp = (int)a.yp;
-  float* P = sPix + c * kPlane;
-  const float* R = ring + c * kRing;
-  const bool colin = ox + lx >= 0 && ox + lx < xp;
-  float out[33];
-  if (act) {
-    float n[3], m[3], sn[3];
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      n[k] = gab_src(P, R, lx + k - 1, y0 - 1, ox, oy, xp, yp);
-      m[k] = gab_src(P, R, lx + k - 1, y0, ox, oy, xp, yp);
-    }
-#pragma unroll
-    for (int st = 0; st < 33; st++) {
-#pragma unroll
-      for (int k = 0; k < 3; k++) sn[k] = gab_src(P, R, lx + k - 1, y0 + st + 1, ox, oy, xp, yp);
-      const float s1 = (n[1] + sn[1]) + (m[0] + m[2]);
-      const float s2 = (n[0] + n[2]) + (sn[0] + sn[2]);
-      out[st] = (m[1] * kGabK0 + s1 * kGabK1) + s2 * kGabK2;
-#pragma unroll
-      for (int k = 0; k < 3; k++) {
-        n[k] = m[k];
-        m[k] = sn[k];
-      }
-    }
-  }
-  __syncthreads();
-  if (act && colin) {
-#pragma unroll
-    for (int st = 0; st < 33; st++) {
-      const int ly = y0 + st;
-      if (oy + ly >= 0 && oy + ly < yp) P[lds_at(lx, ly)] = out[st];
-    }
-  }
-}
-
 // chroma-from-luma factor as an int8 multiple of 1/84 (oracle cfl_quant)
 __device__ __forceinline__ int cfl_quant(float k) {
   float v = k * 84.0f;
@@ -1097,12 +1080,16 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
     sSdperm[i] = c_sdperm[i];
   }
   __syncthreads();
-  load_xyb_tile(a, sLut, sPix, ox, oy);
+  load_xyb_tile(a, sLut, sPix, ox, oy, a.gab);
   if (a.gab) {  // (uniform) the ring beside the tile, then the in-place sweep
     float* ring = sUnion + 256;  // 3 x 268 floats, before phase A's sH
     gab_ring(a, sLut, ring, ox, oy);
     __syncthreads();
-    gab_sweep(a, sPix, ring, ox, oy);
+    gab_sweep(sPix, ring);
+    if (!(ox >= 0 && oy >= 0 && ox + 66 <= (int)a.xp && oy + 66 <= (int)a.yp)) {  // (uniform)
+      __syncthreads();
+      zero_outside(a, sPix, ox, oy);
+    }
   }
   __syncthreads();
   if (a.xyb_out) {
@@ -1224,10 +1211,17 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
       a.cmap[t] = (int8_t)ytox;
       a.cmap[a.ntiles_all + t] = (int8_t)ytob;
     }
-  } else if (tid == 0 && a.cmap) {
-    const size_t t = (size_t)ty * a.tiles_x + tx;
-    a.cmap[t] = 0;
-    a.cmap[a.ntiles_all + t] = 0;
+  } else {
+    if (tid == 0 && a.cmap) {
+      const size_t t = (size_t)ty * a.tiles_x + tx;
+      a.cmap[t] = 0;
+      a.cmap[a.ntiles_all + t] = 0;
+    }
+    // (no fit below effort 5: the DCT8 candidate's row passes alone)
+    const GroupCtx G0{sPix, lby * 8 + 1, lbx * 8 + 1, r, sWperm, sIwperm, sBtab, sSdperm,
+                      0.0f, 1.0f};
+    row_pass_t<true, 1>(G0, rty);
+    row_pass_t<true, kXB>(G0, rtxb);
   }
   if (lbx >= nbx || lby >= nby) return;  // whole groups leave; no barrier follows
   // block index (recomputed where used: keeps a 64-bit value out of the
@@ -1295,59 +1289,69 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
   // hook P lives in FindBest8x8Transform, which libjxl does not run below
   // effort 5 (all-DCT8 speed tiers [ext]): no override there either
   if (HOOKP && (a.proposals & 1u) && ncand > 1) pt = partition_of(rh, rv, rd, a.distance);
-  // scan indices: DCT8 0, DCT4X4 1, DCT2X2 2, DCT4X8 3, DCT8X4 4, IDENTITY 5
+  // scan indices: DCT8 0, DCT4X4 1, DCT2X2 2, DCT4X8 3, DCT8X4 4, IDENTITY 5.
+  // `beats` is a strict total order on (estimate, scan index) in which every
+  // estimate that is not below FLT_MAX ranks after the finite ones, so any
+  // evaluation order finds the scan's winner.  Round 6: DCT8X4 and DCT8 first
+  // (the fit's 8-point row passes, which die after them; DCT8X4 before DCT8
+  // so that no winner's coefficients are held during the first evaluation),
+  // then the others from the pixels in one rolled loop -- one transform
+  // dispatch and one quantization body (eval_cand) for four candidates.
+  // The best estimate is normalised to FLT_MAX when it is not finite, as the
+  // scan's first candidate always was; pruning needs a finite best (then a
+  // pruned candidate's NaN cannot win; with a non-finite best it could, by
+  // its scan index).
   QVals best;
   int bt = kDCT8, bi = 0;
   float beste = FLT_MAX;
-  // candidates one at a time; `beats` is a strict total order on (estimate,
-  // scan index), so this finds the scan's winner
-  {
+  if (ncand > 1) {
     CandAcc A;
-    float e = ncand > 1 ? eval_one<kDCT8, true>(G, scale, inv_scale, A, rty, rtxb)
-                        : eval_one<kDCT8>(G, scale, inv_scale, A);
+    const Prune pr{false, beste, hookF, rh, rv, rd};
+    float e = eval_cand<true>(G, kDCT8X4, scale, inv_scale, A, rty, rtxb, pr);
     if (hookF) e = hook_f(e, rh, rv, rd);
     copy_q(best, A.q, true);
-    if (ncand > 1) beste = e < FLT_MAX ? e : FLT_MAX;
+    bt = kDCT8X4;
+    bi = 4;
+    beste = e < FLT_MAX ? e : FLT_MAX;
   }
-  auto cand = [&](auto tag, int idx) {
-    constexpr int T = decltype(tag)::value;
-    if (!(ncand > 1 || pt == T)) return;
+  {
     CandAcc A;
-    float e;
-    const Prune pr{ncand > 1 && prune, beste, hookF, rh, rv, rd};
-    if constexpr (T == kDCT8X4) {  // (ncand > 1 here: the fit ran)
-      e = eval_one<T, true>(G, scale, inv_scale, A, rty, rtxb, &pr);
-    } else {
-      e = eval_one<T>(G, scale, inv_scale, A, nullptr, nullptr, &pr);
+    const Prune pr{ncand > 1 && prune && beste < FLT_MAX, beste, hookF, rh, rv, rd};
+    float e = eval_cand<true>(G, kDCT8, scale, inv_scale, A, rty, rtxb, pr);
+    if (hookF) e = hook_f(e, rh, rv, rd);
+    if (ncand == 1 || beats(e, 0, beste, bi)) {
+      copy_q(best, A.q, true);
+      bt = kDCT8;
+      bi = 0;
+      beste = ncand > 1 && e < FLT_MAX ? e : FLT_MAX;
     }
-    if (ncand > 1) {
-      if (hookF) e = hook_f(e, rh, rv, rd);
-      if (beats(e, idx, beste, bi)) {
-        copy_q(best, A.q, true);
-        bt = T;
-        bi = idx;
-        beste = e;
-      }
-    }
-  };
-  cand(std::integral_constant<int, kDCT8X4>(), 4);
-  // (DCT4X4 / DCT4X8 could share their 4-point row passes the same way, but
-  // holding them through DCT4X4's evaluation spills: 115+ VGPRs at 128)
-  cand(std::integral_constant<int, kDCT4X4>(), 1);
-  cand(std::integral_constant<int, kDCT4X8>(), 3);
-  if (ncand > 1) {
-    cand(std::integral_constant<int, kDCT2X2>(), 2);
-    cand(std::integral_constant<int, kIDENTITY>(), 5);
   }
-  if (HOOKP && bt == kDCT8 && pt != kDCT8) {
-    // hook P's override: its candidate is evaluated again (keeping it aside
-    // through the search would hold 13 more VGPRs); same inputs, same values
+  // DCT4X4, DCT4X8, DCT2X2, IDENTITY; then (HOOKP) hook P's override
+  // (combined.diff:270-274): when the scan kept DCT8, the partition's
+  // candidate is evaluated again (keeping it aside through the search would
+  // hold 13 more VGPRs; same inputs, same values) and replaces it
+  const int n1 = ncand > 1 ? 4 : 0;
+#pragma unroll 1
+  for (int idx = 0;; idx++) {
+    const bool over = HOOKP && idx == n1;
+    if (idx > n1 || (over && !(bt == kDCT8 && pt != kDCT8))) break;
+    const int T = over ? pt : (idx == 0 ? kDCT4X4 : (idx == 1 ? kDCT4X8 : (idx == 2 ? kDCT2X2 : kIDENTITY)));
+    const int si = idx == 0 ? 1 : (idx == 1 ? 3 : (idx == 2 ? 2 : 5));
     CandAcc A;
-    if (pt == kDCT4X4) (void)eval_one<kDCT4X4>(G, scale, inv_scale, A);
-    else if (pt == kDCT8X4) (void)eval_one<kDCT8X4>(G, scale, inv_scale, A);
-    else (void)eval_one<kDCT4X8>(G, scale, inv_scale, A);
-    bt = pt;
-    copy_q(best, A.q, true);
+    const Prune pr{!over && prune && beste < FLT_MAX, beste, hookF, rh, rv, rd};
+    float e = eval_cand<false>(G, T, scale, inv_scale, A, nullptr, nullptr, pr);
+    if (over) {
+      bt = pt;
+      copy_q(best, A.q, true);
+      break;
+    }
+    if (hookF) e = hook_f(e, rh, rv, rd);
+    if (beats(e, si, beste, bi)) {
+      copy_q(best, A.q, true);
+      bt = T;
+      bi = si;
+      beste = e;
+    }
   }
   gb = gblock();
   if (r == 0) {

@@ -3252,6 +3252,27 @@ jxg_status jxg_compare_rgb8(jxg_ctx* ctx, const uint8_t* orig, size_t orig_strid
   return compare_device(c, c->q_orig.p, row, c->q_comp.p, row, xsize, ysize, want_ssim, out);
 }
 
+// one synthetic frame of the caller's size through the one-at-a-time path:
+// the context's buffers for that size are allocated and every kernel's code
+// object is loaded before the caller's first frame (jxg_cjxl runs it beside
+// the PNG decode: a new context's first 8K encode took 35 ms against 12 ms)
+jxg_status jxg_warmup(jxg_ctx* ctx, uint32_t xsize, uint32_t ysize) {
+  if (!ctx || xsize == 0 || ysize == 0 || xsize > (1u << 18) || ysize > (1u << 18))
+    return JXG_ERR_INVALID_ARG;
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (hipSetDevice(c->params.device) != hipSuccess) return JXG_ERR_HIP;
+  if (pipe_busy(c)) return JXG_ERR_INVALID_ARG;
+  const size_t stride = (size_t)xsize * 3;
+  if (c->rgb.ensure(stride * ysize) != hipSuccess) return JXG_ERR_OOM;  // jxg_encode_rgb8's upload buffer
+  JXG_HIP(launch_synth(c->rgb.p, xsize, ysize, stride, 0x5741524Dull, c->stream));
+  jxg_buffer out{nullptr, 0};
+  jxg_status st = order_input(c, c);
+  if (!st) st = encode_device(c, c->rgb.p, xsize, ysize, stride, &out, Clock::now());
+  jxg_buffer_free(&out);
+  c->stats = jxg_stats{};
+  return st;
+}
+
 jxg_status jxg_synth_rgb8_device(jxg_ctx* ctx, void* d_out, uint32_t xsize, uint32_t ysize,
                                  size_t row_stride, uint64_t seed) {
   if (!ctx || !d_out || xsize == 0 || ysize == 0 || row_stride < (size_t)xsize * 3)

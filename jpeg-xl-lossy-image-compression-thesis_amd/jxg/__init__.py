@@ -93,7 +93,7 @@ EXPORTS = ("jxg_status_str", "jxg_create", "jxg_destroy", "jxg_encode_rgb8",
            "jxg_submit_rgb8", "jxg_submit_rgb8_device", "jxg_receive", "jxg_pending",
            "jxg_set_input_stream", "jxg_pipeline_depth", "jxg_shard_plan",
            "jxg_shard_submit_device", "jxg_shard_next_head", "jxg_shard_write_next",
-           "jxg_shard_write_flush", "jxg_set_pipeline_lanes",
+           "jxg_shard_write_flush", "jxg_set_pipeline_lanes", "jxg_warmup",
 )
 
 _lib = None
@@ -166,6 +166,7 @@ def load():
     lib.jxg_compare_rgb8_device.argtypes = cmp_args
     lib.jxg_synth_rgb8_device.argtypes = [vp, vp, ctypes.c_uint32, ctypes.c_uint32, sz,
                                           ctypes.c_uint64]
+    lib.jxg_warmup.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32]
     _lib = lib
     return lib
 
@@ -460,6 +461,11 @@ class Encoder:
         _check(load().jxg_homogeneity_map(self._ctx, xyb.ctypes.data, xs, ys, distance, flags,
                                           r3.ctypes.data, t.ctypes.data))
         return r3, t
+
+    def warmup(self, width: int, height: int):
+        """jxg_warmup: allocate this context's buffers for width x height and
+        load every kernel (one synthetic frame, result discarded)."""
+        _check(load().jxg_warmup(self._ctx, width, height))
 
     def synth_device(self, ptr: int, width: int, height: int, seed: int,
                      row_stride: int | None = None):

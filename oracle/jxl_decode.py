@@ -990,7 +990,7 @@ class Decoded:
     pass
 
 
-def decode(data: bytes, want_pixels: bool = True, groups=None) -> Decoded:
+def decode(data: bytes, want_pixels: bool = True, groups=None, toc_only: bool = False) -> Decoded:
     """groups: decode only these pass groups (and the LF groups holding them;
     every other block stays zero, no pixels) -- for spot checks of large
     frames, whose full decode takes minutes in Python."""
@@ -1089,6 +1089,8 @@ def decode(data: bytes, want_pixels: bool = True, groups=None) -> Decoded:
     d.sharpness = np.zeros((bys, bxs), dtype=np.int32)
     d.section_sizes = sizes
     d.section_offsets = offs
+    if toc_only:  # headers and TOC only (section comparisons of large frames)
+        return d
     # LfGlobal
     s = sec(0)
     if not s.bool():

@@ -46,6 +46,14 @@ CASES = [
     ("8k_d1_cjxl", 2, 0, 7680, 4320, 1.0, 7, 0, 1, 7),
     ("8k_d1_cjxl_pf", 2, 0, 7680, 4320, 1.0, 7, 3, 1, 7),
     ("8k_d1_cjxl_f100", 2, 100, 7680, 4320, 1.0, 7, 0, 1, 7),
+    # round 6: configs 3 and 4 at the headline preset too
+    ("1080p_f0_d0.5_cjxl", 3, 0, 1920, 1080, 0.5, 7, 0, 1, 7),
+    ("1080p_f0_d1_cjxl", 3, 0, 1920, 1080, 1.0, 7, 0, 1, 7),
+    ("1080p_f0_d2_cjxl", 3, 0, 1920, 1080, 2.0, 7, 0, 1, 7),
+    ("1080p_f1_d0.5_cjxl", 3, 1, 1920, 1080, 0.5, 7, 0, 1, 7),
+    ("1080p_f1_d1_cjxl", 3, 1, 1920, 1080, 1.0, 7, 0, 1, 7),
+    ("1080p_f1_d2_cjxl", 3, 1, 1920, 1080, 2.0, 7, 0, 1, 7),
+    ("16k_d1_cjxl_pf", 4, 0, 16384, 16384, 1.0, 7, 3, 1, 7),
 ]
 
 

@@ -58,15 +58,22 @@ def test_config_matches_oracle(jxg_mod, name):
     assert hashlib.sha256(data).hexdigest() == g["sha256"], "codestream differs from the oracle"
 
 
+@pytest.mark.parametrize("preset", ["plain", "cjxl"])
 @pytest.mark.parametrize("distance", [0.5, 1.0, 2.0])
-def test_batch_1080p_matches_oracle(jxg_mod, distance):
+def test_batch_1080p_matches_oracle(jxg_mod, distance, preset):
+    """config 3 (1080p frames through jxg_encode_batch_rgb8) with no flags and
+    at cjxl's defaults (the preset bench.py's config-3 line times)"""
     from jxg.synth import synth_rgb8_device
 
-    gs = [g for g in GOLD if g["config"] == 3 and g["distance"] == distance]
+    cjxl = preset == "cjxl"
+    gs = [g for g in GOLD if g["config"] == 3 and g["distance"] == distance
+          and bool(g.get("filters")) == cjxl]
+    assert len(gs) == 2
     frames = [synth_rgb8_device(g["width"], g["height"], g["seed"]).cpu().numpy() for g in gs]
     for f, g in zip(frames, gs):
         assert hashlib.sha256(f.tobytes()).hexdigest() == g["input_sha256"]
-    with jxg_mod.Encoder(distance=distance, effort=7) as enc:
+    flags = jxg_mod.FLAGS_CJXL_DEFAULTS if cjxl else 0
+    with jxg_mod.Encoder(distance=distance, effort=7, flags=flags) as enc:
         outs = enc.encode_batch(frames)
     for data, g in zip(outs, gs):
         assert len(data) == g["bytes"] and hashlib.sha256(data).hexdigest() == g["sha256"], g["name"]

@@ -495,6 +495,80 @@ def test_sharded_8k_ans_over_8(jxg_mod, decoder):
     assert streamed_shards(jxg_mod, [t], w, h, world)[0] == got
 
 
+def _sharded_ans_matches_single(jxg_mod, decoder, w, h, seed, world, p, flags, rows):
+    """ANS over `world` contexts (one HF preset per rank) against the
+    one-context encode: LfGlobal and every LF-group section byte-identical, the
+    pass groups of block-group rows `rows` decoded to the single encode's
+    coefficients, strategies and token counts, each group on its rank's preset"""
+    from jxg.synth import synth_rgb8_device
+
+    t = synth_rgb8_device(w, h, seed)
+    keep = jxg_mod.FLAG_KEEP_MAPS
+    with jxg_mod.Encoder(distance=1.0, effort=7, proposals=p, flags=flags | keep) as enc:
+        ref = enc.encode_device(t.data_ptr(), w, h)
+        st = enc.stats()
+    got = sharded_encode(jxg_mod, None, world, p=p, flags=flags, t=t)
+    del t
+    go, lo, kind = jxg_mod.shard_plan(w, h, world)
+    nlf = len(lo)
+    dr = decoder.decode(ref, groups=[])
+    gxs = -(-w // 256)
+    sel = [gy * gxs + gx for gy in rows for gx in range(gxs)]
+    dg = decoder.decode(got, groups=sel)
+    assert (dg.gab, dg.epf_iters) == (dr.gab, dr.epf_iters)  # filters signalled alike
+    for i in range(1 + nlf):  # LfGlobal + LF groups: byte-identical sections
+        a = ref[dr.section_offsets[i]:dr.section_offsets[i] + dr.section_sizes[i]]
+        b = got[dg.section_offsets[i]:dg.section_offsets[i] + dg.section_sizes[i]]
+        assert a == b, i
+    assert dg.npresets == world
+    assert [int(dg.group_presets[g]) for g in sel] == [go[g] for g in sel]
+    for gy in rows:
+        r = slice(32 * gy, min(32 * gy + 32, dg.bys))
+        assert np.array_equal(dg.ac[r], st["ac"][r])
+        assert np.array_equal(dg.acs[r], st["acs"][r].astype(np.int32))
+    assert np.array_equal(dg.ac_tokens[sel], st["ac_tokens"][sel])
+    return kind
+
+
+def test_sharded_8k_cjxl_over_8(jxg_mod, decoder):
+    """config 2 at the headline preset (JXG_FLAGS_CJXL_DEFAULTS: Gaborish,
+    EPF, masking AQ, ANS) over 8 contexts.  The inverse Gaborish and the AQ
+    neighbourhood read across shard edges; every rank reads its halo from the
+    whole frame, so the LF sections (quant field, strategies, DC) equal the
+    single-GPU encode's and the decoded group rows at rank seams (block-group
+    rows 7, 8, 16) hold the single-GPU coefficients."""
+    kind = _sharded_ans_matches_single(jxg_mod, decoder, 7680, 4320, 0x4A584C02, 8, 0,
+                                       jxg_mod.FLAGS_CJXL_DEFAULTS, [7, 8, 16])
+    assert kind == 1
+
+
+def test_sharded_16k_cjxl_pf_over_8(jxg_mod, decoder):
+    """config 4 at the headline preset: 16384^2, P+F, cjxl defaults, over 8
+    contexts (the single-context encode equals the oracle fingerprint
+    16k_d1_cjxl_pf in test_gpu_configs).  LfGlobal and all 64 LF-group sections
+    (DC, quant field, strategies, CfL: everything the AQ halo and the inverse
+    Gaborish decide across rank seams) equal the single encode's byte for
+    byte; the frame signals the same filters and one HF preset per rank."""
+    from jxg.synth import synth_rgb8_device
+
+    w = h = 16384
+    t = synth_rgb8_device(w, h, 0x4A584C04)
+    flags = jxg_mod.FLAGS_CJXL_DEFAULTS
+    with jxg_mod.Encoder(distance=1.0, effort=7, proposals=3, flags=flags) as enc:
+        ref = enc.encode_device(t.data_ptr(), w, h)
+    got = sharded_encode(jxg_mod, None, 8, p=3, flags=flags, t=t)
+    del t
+    go, lo, kind = jxg_mod.shard_plan(w, h, 8)
+    assert kind == 0 and len(lo) == 64
+    dr = decoder.decode(ref, toc_only=True)
+    dg = decoder.decode(got, toc_only=True)
+    assert (dg.gab, dg.epf_iters) == (dr.gab, dr.epf_iters) == (True, 1)
+    for i in range(1 + len(lo)):
+        a = ref[dr.section_offsets[i]:dr.section_offsets[i] + dr.section_sizes[i]]
+        b = got[dg.section_offsets[i]:dg.section_offsets[i] + dg.section_sizes[i]]
+        assert a == b, i
+
+
 def test_sharded_16k_pf_over_8(jxg_mod):
     """BASELINE config 4 as written: 16384^2, proposals P+F, over 8 contexts
     (LF-group rows aligned with the ranks: no record moves); prefix codes ->
