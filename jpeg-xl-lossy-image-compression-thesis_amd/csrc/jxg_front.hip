@@ -1333,8 +1333,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
   const int n1 = ncand > 1 ? 4 : 0;
 #pragma unroll 1
   for (int idx = 0;; idx++) {
-    const bool over = HOOKP && idx == n1;
-    if (idx > n1 || (over && !(bt == kDCT8 && pt != kDCT8))) break;
+    const bool over = idx == n1;  // past the scan: hook P's override, if any
+    if (over && !(HOOKP && bt == kDCT8 && pt != kDCT8)) break;
     const int T = over ? pt : (idx == 0 ? kDCT4X4 : (idx == 1 ? kDCT4X8 : (idx == 2 ? kDCT2X2 : kIDENTITY)));
     const int si = idx == 0 ? 1 : (idx == 1 ? 3 : (idx == 2 ? 2 : 5));
     CandAcc A;

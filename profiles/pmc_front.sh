@@ -7,7 +7,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 R=$PWD
 # one-at-a-time encodes (each kernel alone on the GPU), no side measurements
-BARGS=${BENCH_ARGS:---steps 2 --warmup 1 --no-cpu-baseline --no-quality --alt-coder 0 --alt-thesis 0 --alt-cjxl 0 --no-pipeline}
+BARGS=${BENCH_ARGS:---steps 2 --warmup 1 --no-cpu-baseline --no-quality --no-single --alt-coder 0 --alt-thesis 0 --alt-cjxl 0 --alt-e4 0 --no-pipeline}
 run() { timeout -k 10 300 rocprofv3 --pmc $2 --kernel-include-regex "$3" -d $R/$OUT/$1 -o run --output-format csv -- python3 $R/bench.py $BARGS > $R/$OUT/$1.log 2>&1; }
 K=${KERNEL:-front_kernel}
 run p1 "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY" "$K"
