@@ -351,16 +351,23 @@ def single_image_probe(img, distance, effort, headline_bytes, device, runs=3):
         for i in range(runs):
             dst = os.path.join(td, "frame-%g-%d.jxl" % (distance, effort))
             t0 = time.perf_counter()
+            u0 = time.time() * 1e3
             p = subprocess.run([jxg.CLI_PATH, src, dst, "--distance=%g" % distance,
                                 "--effort=%d" % effort, "--device=%d" % device],
                                capture_output=True, text=True, env=env)
             walls.append((time.perf_counter() - t0) * 1e3)
+            u1 = time.time() * 1e3
             if p.returncode != 0:
                 out["cli_error"] = p.stderr.strip()[-300:]
                 break
             line = [l for l in p.stderr.splitlines() if l.startswith("{")]
             if line:
-                phases.append(json.loads(line[-1]))
+                ph = json.loads(line[-1])
+                um = ph.pop("unix_ms_main", None)
+                if um:  # process start (exec, dynamic loading) / exit (teardown)
+                    ph["ms_before_main"] = um[0] - u0
+                    ph["ms_after_main"] = u1 - um[1]
+                phases.append(ph)
             with open(dst, "rb") as f:
                 same = same and (headline_bytes is None or f.read() == headline_bytes)
         if walls:
@@ -372,7 +379,9 @@ def single_image_probe(img, distance, effort, headline_bytes, device, runs=3):
             if phases:
                 best = min(range(len(phases)), key=lambda i: walls[i])
                 ph = {k: round(v, 2) for k, v in phases[best].items()}
-                ph["ms_process_and_runtime"] = round(walls[best] - sum(phases[best].values()), 1)
+                # (ms_create_overlapped runs on a second thread beside the decode)
+                ph["ms_unaccounted"] = round(walls[best] - sum(
+                    v for k, v in phases[best].items() if k != "ms_create_overlapped"), 1)
                 out["cli"]["phases_best_run"] = ph
     # one-at-a-time jxg_encode_rgb8 from host memory, warm context
     host = np.ascontiguousarray(img)
@@ -888,6 +897,9 @@ def main():
                                   "bound": "hbm", "achieved": round(a4, 1), "peak": HBM_PEAK_GBS,
                                   "unit": "GB/s", "frac": round(a4 / HBM_PEAK_GBS, 4),
                                   "algorithmic_bytes": int(fb4), "avg_ms": round(e4, 4),
+                                  # PMC HBM bytes per launch (profiles/front_pmc_<cfg>_e4.json)
+                                  "traffic": load_pmc_traffic(name + "_e4"),
+                                  "valu_floor": load_front_valu_floor(name + "_e4", e4),
                                   "measured": "one-at-a-time encodes at effort 4, HIP events on "
                                               "the encoder's stream"}
         if replicas is not None:

@@ -248,6 +248,12 @@ int main(int argc, char** argv) {
   };
   const bool timing = std::getenv("JXG_CJXL_TIMING") != nullptr;
   const auto t_start = Clk::now();
+  const auto unix_ms = [] {
+    return std::chrono::duration<double, std::milli>(
+               std::chrono::system_clock::now().time_since_epoch())
+        .count();
+  };
+  const double u_start = unix_ms();  // (the caller's clock brackets main with these)
   jxg_ctx* ctx = nullptr;
   jxg_status st = JXG_OK;
   double ms_create = 0.0;
@@ -332,9 +338,10 @@ int main(int argc, char** argv) {
     const auto t_end = Clk::now();
     std::fprintf(stderr,
                  "{\"ms_read_decode\": %.3f, \"ms_create_wait\": %.3f, \"ms_encode\": %.3f, "
-                 "\"ms_write\": %.3f, \"ms_destroy\": %.3f, \"ms_create_overlapped\": %.3f}\n",
+                 "\"ms_write\": %.3f, \"ms_destroy\": %.3f, \"ms_create_overlapped\": %.3f, "
+                 "\"unix_ms_main\": [%.3f, %.3f]}\n",
                  ms(t_start, t_read), ms(t_read, t_create), sec * 1e3,
-                 ms(t_enc, t_write), ms(t_write, t_end), ms_create);
+                 ms(t_enc, t_write), ms(t_write, t_end), ms_create, u_start, unix_ms());
   }
   return 0;
 }

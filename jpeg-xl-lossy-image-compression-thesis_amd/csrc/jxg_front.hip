@@ -17,6 +17,8 @@
 // (nearly) bank-conflict free.  Float op order == oracle/front.c.
 #include <float.h>
 
+#include <cstdio>
+
 #include <type_traits>
 
 #include "jxg_device.h"
@@ -796,6 +798,7 @@ __device__ __forceinline__ bool beats(float ea, int ia, float eb, int ib) {
 constexpr int kChunksX = 18;
 constexpr int kChunks = kRows * kChunksX;
 constexpr int kChunkIters = (kChunks + kThreads - 1) / kThreads;
+constexpr int kRing = 2 * 68 + 2 * 66;  // Gaborish ring: tile-local rows / columns -1 and 66
 // chunk i's 12 bytes (4 pixels), clamped to the image
 __device__ __forceinline__ void load_chunk(const FrontArgs& a, bool al, int i, int ox, int oy,
                                            uint32_t d[3]) {
@@ -823,24 +826,44 @@ __device__ __forceinline__ void load_chunk(const FrontArgs& a, bool al, int i, i
       d[w] = by[4 * w] | by[4 * w + 1] << 8 | by[4 * w + 2] << 16 | by[4 * w + 3] << 24;
   }
 }
+// The tile's global loads, issued all at once at the workgroup's start (before
+// the table copies and their barrier): a thread's three chunks (12 bytes each)
+// and, with Gaborish, its ring pixel.  Round 6: the per-phase clock profile
+// (JXG_FRONT_PROFILE, profiles/r06p) put 29 % of an e7 workgroup's time (42 %
+// at e4) in the tile load, which waited for one chunk's loads per iteration
+// and then for the ring's: every wait a full memory latency.
+struct TileLoads {
+  uint32_t d[kChunkIters][3];  // chunks threadIdx.x + k * kThreads
+  uint32_t ring;               // ring pixel threadIdx.x: r | g << 8 | b << 16
+};
+__device__ __forceinline__ int ring_x(int i) { return i < 68 ? i - 1 : (i < 136 ? i - 69 : (i < 202 ? -1 : 66)); }
+__device__ __forceinline__ int ring_y(int i) { return i < 68 ? -1 : (i < 136 ? 66 : (i < 202 ? i - 136 : i - 202)); }
+__device__ __forceinline__ void issue_tile_loads(const FrontArgs& a, int ox, int oy, bool gab,
+                                                 TileLoads& L) {
+  const bool al = ((a.stride | (size_t)a.rgb) & 3) == 0;
+#pragma unroll
+  for (int k = 0; k < kChunkIters; k++)
+    load_chunk(a, al, min((int)threadIdx.x + k * kThreads, kChunks - 1), ox, oy, L.d[k]);
+  L.ring = 0;
+  if (gab && threadIdx.x < (unsigned)kRing) {  // (the ring's pixels: gab_ring's clamping)
+    const int i = threadIdx.x, lx = ring_x(i), ly = ring_y(i);
+    const int sx = min(max(ox + lx, 0), (int)a.w - 1), sy = min(max(oy + ly, 0), (int)a.h - 1);
+    const uint8_t* q = a.rgb + (size_t)sy * a.stride + 3 * (size_t)sx;
+    L.ring = (uint32_t)q[0] | (uint32_t)q[1] << 8 | (uint32_t)q[2] << 16;
+  }
+}
 // rep (Gaborish): samples outside the block-padded frame hold the clamped
 // image sample too (the inverse Gaborish reads every source at coordinates
 // clamped to the padded frame, i.e. the image sample at coordinates clamped to
 // the image); they are zeroed again after the sweep (zero_outside).
-// The chunks go through a rolled loop with the next chunk's loads issued
-// before the current one's conversion: four inlined conversions instead of
-// twelve (round 6: the kernel's instruction-cache footprint).
+// The chunks are converted in a rolled loop (four inlined conversions; the
+// chunk registers rotate, so every index stays static).
 __device__ __forceinline__ void load_xyb_tile(const FrontArgs& a, const float* lut, float* sPix,
-                                              int ox, int oy, bool rep) {
-  const bool al = ((a.stride | (size_t)a.rgb) & 3) == 0;
+                                              int ox, int oy, bool rep, TileLoads& L) {
   const float cb = cbrt_det(kOpsinBias);
-  uint32_t d[3];
-  load_chunk(a, al, min((int)threadIdx.x, kChunks - 1), ox, oy, d);
 #pragma unroll 1
   for (int k = 0; k < kChunkIters; k++) {
     const int i = threadIdx.x + k * kThreads;
-    uint32_t nx[3] = {0u, 0u, 0u};
-    if (k + 1 < kChunkIters) load_chunk(a, al, min(i + kThreads, kChunks - 1), ox, oy, nx);
     if (i < kChunks) {
       const int ly = i / kChunksX, cx = i - ly * kChunksX;
       const int gy = oy + ly, gx0 = ox - 3 + 4 * cx;
@@ -853,9 +876,9 @@ __device__ __forceinline__ void load_xyb_tile(const FrontArgs& a, const float* l
         float X = 0.0f, Y = 0.0f, B = 0.0f;
         if (inside) {
           const int b0 = 3 * j;
-          const uint32_t r8 = (d[b0 >> 2] >> ((b0 & 3) * 8)) & 0xFF;
-          const uint32_t g8 = (d[(b0 + 1) >> 2] >> (((b0 + 1) & 3) * 8)) & 0xFF;
-          const uint32_t b8 = (d[(b0 + 2) >> 2] >> (((b0 + 2) & 3) * 8)) & 0xFF;
+          const uint32_t r8 = (L.d[0][b0 >> 2] >> ((b0 & 3) * 8)) & 0xFF;
+          const uint32_t g8 = (L.d[0][(b0 + 1) >> 2] >> (((b0 + 1) & 3) * 8)) & 0xFF;
+          const uint32_t b8 = (L.d[0][(b0 + 2) >> 2] >> (((b0 + 2) & 3) * 8)) & 0xFF;
           pixel_xyb(lut, cb, r8, g8, b8, X, Y, B);
         }
         const int o = lds_at(lx, ly);
@@ -865,7 +888,9 @@ __device__ __forceinline__ void load_xyb_tile(const FrontArgs& a, const float* l
       }
     }
 #pragma unroll
-    for (int w = 0; w < 3; w++) d[w] = nx[w];
+    for (int q = 0; q + 1 < kChunkIters; q++)
+#pragma unroll
+      for (int w = 0; w < 3; w++) L.d[q][w] = L.d[q + 1][w];
   }
 }
 // samples outside the block-padded frame back to 0 (H2) after the sweep
@@ -893,36 +918,20 @@ __device__ __forceinline__ void zero_outside(const FrontArgs& a, float* sPix, in
 constexpr float kGabK0 = 1.8012209f;
 constexpr float kGabK1 = -0.15485205f;
 constexpr float kGabK2 = -0.04545318f;
-constexpr int kRing = 2 * 68 + 2 * 66;
 __device__ __forceinline__ int ring_index(int lx, int ly) {  // (lx, ly) on the ring
   if (ly == -1) return lx + 1;
   if (ly == 66) return 69 + lx;
   if (lx == -1) return 136 + ly;
   return 202 + ly;
 }
-// RGB8 -> XYB of the ring pixels (the tile load's replication rule)
-__device__ __forceinline__ void gab_ring(const FrontArgs& a, const float* lut, float* ring, int ox,
-                                         int oy) {
+// RGB8 -> XYB of the ring pixels (the tile load's replication rule), from the
+// pixel issue_tile_loads fetched
+__device__ __forceinline__ void gab_ring(const float* lut, float* ring, const TileLoads& L) {
   const float cb = cbrt_det(kOpsinBias);
-  for (int i = threadIdx.x; i < kRing; i += kThreads) {
-    int lx, ly;
-    if (i < 68) {
-      lx = i - 1;
-      ly = -1;
-    } else if (i < 136) {
-      lx = i - 69;
-      ly = 66;
-    } else if (i < 202) {
-      lx = -1;
-      ly = i - 136;
-    } else {
-      lx = 66;
-      ly = i - 202;
-    }
-    const int sx = min(max(ox + lx, 0), (int)a.w - 1), sy = min(max(oy + ly, 0), (int)a.h - 1);
-    const uint8_t* q = a.rgb + (size_t)sy * a.stride + 3 * (size_t)sx;
+  const int i = threadIdx.x;
+  if (i < kRing) {
     float X, Y, B;
-    pixel_xyb(lut, cb, q[0], q[1], q[2], X, Y, B);
+    pixel_xyb(lut, cb, L.ring & 0xFF, (L.ring >> 8) & 0xFF, (L.ring >> 16) & 0xFF, X, Y, B);
     ring[i] = X;
     ring[kRing + i] = Y;
     ring[2 * kRing + i] = B;
@@ -1013,6 +1022,26 @@ __device__ __forceinline__ int cfl_quant(float k) {
   return q > 127 ? 127 : (q < -128 ? -128 : q);
 }
 
+// JXG_FRONT_PROFILE (experiment builds only): per-phase shader-clock sums of
+// thread 0 of every workgroup (wave 0's view; the phases up to B end at
+// workgroup barriers), printed by dump_front_profile() at context destroy
+#ifdef JXG_FRONT_PROFILE
+__device__ unsigned long long g_fprof[12];
+#define FPROF(k)                                                     \
+  do {                                                               \
+    if (threadIdx.x == 0) {                                          \
+      const unsigned long long now_ = __builtin_readcyclecounter();  \
+      if ((k) > 0) atomicAdd(&g_fprof[(k)], now_ - fprof_t0);       \
+      else atomicAdd(&g_fprof[0], 1ull);                             \
+      fprof_t0 = now_;                                               \
+    }                                                                \
+  } while (0)
+#else
+#define FPROF(k) \
+  do {           \
+  } while (0)
+#endif
+
 // HOOKP: hook P compiled in (proposals bit 0); without it the kernel keeps
 // no hook-P candidate aside (fewer live registers)
 #ifndef JXG_FRONT_WPE  // (experiment builds override it: tools/build_variant.sh)
@@ -1067,6 +1096,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
       a.zero[i] = make_uint4(0, 0, 0, 0);
   }
   if (idle) return;
+#ifdef JXG_FRONT_PROFILE
+  unsigned long long fprof_t0 = 0;
+#endif
+  FPROF(0);
+  TileLoads TL;
+  issue_tile_loads(a, ox, oy, a.gab, TL);  // in flight through the table copies
   if (tid < 256) {
     sLut[tid] = c_lut[tid];
     sBtab[tid] = c_btab[tid];
@@ -1080,11 +1115,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
     sSdperm[i] = c_sdperm[i];
   }
   __syncthreads();
-  load_xyb_tile(a, sLut, sPix, ox, oy, a.gab);
+  FPROF(1);  // tables
+  load_xyb_tile(a, sLut, sPix, ox, oy, a.gab, TL);
   if (a.gab) {  // (uniform) the ring beside the tile, then the in-place sweep
     float* ring = sUnion + 256;  // 3 x 268 floats, before phase A's sH
-    gab_ring(a, sLut, ring, ox, oy);
+    gab_ring(sLut, ring, TL);
     __syncthreads();
+    FPROF(2);  // tile + ring load
     gab_sweep(sPix, ring);
     if (!(ox >= 0 && oy >= 0 && ox + 66 <= (int)a.xp && oy + 66 <= (int)a.yp)) {  // (uniform)
       __syncthreads();
@@ -1092,6 +1129,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
     }
   }
   __syncthreads();
+  FPROF(3);  // (Gaborish sweep; without it: the tile load)
   if (a.xyb_out) {
     // tile-major XYB copy for the merge stage: [tile][X, Y, B][64][64]
     float* dst = a.xyb_out + (size_t)(ty * a.tiles_x + tx) * (3 * 4096);
@@ -1103,6 +1141,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
       reinterpret_cast<float4*>(dst)[i] = make_float4(q[0], q[1], q[2], q[3]);
     }
   }
+  FPROF(4);  // XYB tile copy
   const int nbx = min(8, (int)a.bxs - tx * 8), nby = min(8, (int)a.bys - ty * 8);
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const size_t nb = (size_t)a.bxs * a.bys;
@@ -1134,6 +1173,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
     }
     __syncthreads();
   }
+  FPROF(5);  // phase A
   // ---- phase B: wave w = block row, 8-lane group g = block column ----
   const int g = lane >> 3, r = lane & 7;
   const int lbx = g, lby = wave;
@@ -1223,6 +1263,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
     row_pass_t<true, 1>(G0, rty);
     row_pass_t<true, kXB>(G0, rtxb);
   }
+  FPROF(6);  // phase B (CfL fit / row passes)
   if (lbx >= nbx || lby >= nby) return;  // whole groups leave; no barrier follows
   // block index (recomputed where used: keeps a 64-bit value out of the
   // candidate search's live registers)
@@ -1270,6 +1311,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
   if (r == 0) a.qf[gb] = (uint8_t)(raw - 1);
   const float scale = (float)a.G * (float)raw / 65536.0f;
   const float inv_scale = 1.0f / scale;
+  FPROF(7);  // DC + AQ
   // ---- phase C: strategy search (FindBest8x8Transform [ext] + hooks) ----
   const int ncand = a.effort >= 5 ? 6 : 1;
   const bool hookF = (a.proposals & 2u) != 0 && ncand > 1;
@@ -1361,6 +1403,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
     if (a.ent) a.ent[gb] = beste;
   }
   if (r < 3) a.nz[r * nb + gb] = (uint16_t)((best.nz >> (8 * r)) & 0xFFu);
+  FPROF(8);  // phase C (the candidates)
   // ---- phase D: zigzag scatter through LDS, 16-byte stores ----
   const int bti = tindex_rt(bt);
   const uint2 zz2 = *reinterpret_cast<const uint2*>(sZz + bti * 64 + r * 8);
@@ -1379,6 +1422,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
         *reinterpret_cast<const uint4*>(stage + 8 * r);
     wave_lds_sync();
   }
+  FPROF(9);  // phase D
 }
 
 
@@ -1425,6 +1469,21 @@ __global__ __launch_bounds__(kThreads) void homog_kernel(HomogArgs a) {
     a.type[b] = partition_of(rh, rv, rd, a.distance);
   }
 }
+
+#ifdef JXG_FRONT_PROFILE
+void dump_front_profile() {
+  unsigned long long h[12];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_fprof), sizeof(h)) != hipSuccess) return;
+  static const char* kNames[10] = {"workgroups", "tables", "tile+ring load", "gab sweep",
+                                   "xyb copy", "phase A", "phase B", "dc+aq", "phase C",
+                                   "phase D"};
+  std::fprintf(stderr, "front_kernel thread-0 shader cycles (Mcycles summed over workgroups):\n");
+  for (int k = 0; k < 10; k++)
+    std::fprintf(stderr, "  %-16s %12.3f\n", kNames[k], k ? h[k] / 1e6 : (double)h[0]);
+}
+#else
+void dump_front_profile() {}
+#endif
 
 hipError_t set_front_constants(const float lut[256], const float wts[5][3][64], hipStream_t s) {
   static float wperm[kNT * 3 * 64], iwperm[kNT * 64], btab[256], sdperm[kNT * 3 * 64];

@@ -2763,6 +2763,9 @@ void jxg_destroy(jxg_ctx* ctx) {
 #ifdef JXG_MERGE_PROFILE
   dump_merge_profile();
 #endif
+#ifdef JXG_FRONT_PROFILE
+  dump_front_profile();
+#endif
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   if (c->ev_in) (void)hipEventDestroy(c->ev_in);

@@ -332,10 +332,11 @@ class ShardStream:
          + TOC) -- the copies run on while it goes on; it marks frame k done
          once write_next of frame k + WRITE_LAG (or a flush) has returned.
     Rank 0's :meth:`receive` returns a zero-copy view of frame k's codestream
-    once every rank has marked it done; other ranks get None.  The view is
-    valid until the next receive -- for the next S - 1 receives while at most
-    jxg_pipeline_depth frames are kept pending (then every write happens in
-    receive).  A frame is written into slot k % S only once rank 0 has
+    once every rank has marked it done; other ranks get None.  **The view is
+    valid only until the next receive** (receive(k + 1) releases frame k's slot
+    to the writers; round 5 changed this from "the next S - 1 receives"):
+    keep a copy (``receive(copy=True)`` or ``bytes(view)``) to hold a frame
+    longer.  A frame is written into slot k % S only once rank 0 has
     released frame k - S (called receive for a later frame), so at most
     depth + S - 2 frames may be pending: :meth:`submit` raises beyond.  All ranks must run on one node (the shared
     mapping); the partition must need no record exchange and the coder must
@@ -465,9 +466,10 @@ class ShardStream:
                 self.done[j % self.slots, self.rank] = j
             self.unmarked = []
 
-    def receive(self):
+    def receive(self, copy: bool = False):
         """The oldest frame not yet received: rank 0 gets a numpy view of its
-        codestream (valid for the next slots - 1 receives), other ranks None."""
+        codestream, valid until the next receive (which releases its slot), or
+        with copy=True its bytes; other ranks None."""
         k = self.received
         if k >= self.submitted:
             raise RuntimeError("ShardStream: nothing pending")
@@ -483,7 +485,8 @@ class ShardStream:
             return None
         s = k % self.slots
         self._wait(lambda: bool((self.done[s] >= k).all()), "frame %d" % k)
-        return self.host.view(total, self.data_off + s * self.slot_bytes)
+        v = self.host.view(total, self.data_off + s * self.slot_bytes)
+        return v.tobytes() if copy else v
 
     def close(self):
         while self.received < self.submitted:
