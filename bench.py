@@ -70,6 +70,7 @@ The JSON line also carries:
 import argparse
 import json
 import os
+import resource
 import sys
 import time
 
@@ -646,6 +647,7 @@ def main():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
+        ru0 = resource.getrusage(resource.RUSAGE_SELF)  # this process's CPU (all threads)
         t0 = time.perf_counter()
         if nstreams == 1:
             worker(encs[0], range(total))
@@ -658,6 +660,8 @@ def main():
                 t.join()
         torch.cuda.synchronize()
         dt_own = time.perf_counter() - t0  # this rank's own work, before the barrier
+        ru1 = resource.getrusage(resource.RUSAGE_SELF)
+        cpu_own = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
         wait_own = ss.wait_s if ss is not None else 0.0
         if world > 1:
             dist.barrier()
@@ -669,12 +673,14 @@ def main():
             dt = float(tt.item())
             # per-rank time and the time it spent waiting for the other ranks
             # (ShardStream: heads, slots, frames) -> rank 0
-            mine = torch.tensor([dt_own, wait_own], dtype=torch.float64,
+            mine = torch.tensor([dt_own, wait_own, cpu_own], dtype=torch.float64,
                                 device="cpu" if backend == "gloo" else dev)
             allr = [torch.zeros_like(mine) for _ in range(world)]
             dist.all_gather(allr, mine)
             rec["per_rank"] = [(float(x[0]), float(x[1])) for x in allr]
+            rec["cpu_per_rank"] = [float(x[2]) for x in allr]
         rec["dt"] = dt
+        rec["cpu_s"] = cpu_own
         rec["per_step"] = per_step
         rec["st"] = encs[0].stats()
         last = rec["last"]
@@ -910,6 +916,14 @@ def main():
             # slots, frames), over the timed steps
             res["per_rank_ms_per_step"] = [round(a * 1e3 / args.steps, 3) for a, _ in R["per_rank"]]
             res["ms_wait_ranks"] = [round(b * 1e3 / args.steps, 3) for _, b in R["per_rank"]]
+        # host CPU the ranks used over the timed region (getrusage of each rank's
+        # process, every thread: submit / ShardStream thread + the library's
+        # helper pool), as busy CPUs = CPU seconds / wall seconds, against the
+        # cgroup quota the box grants (8 ranks on a 16-CPU share)
+        cpus = R.get("cpu_per_rank") or [R["cpu_s"]]
+        res["host_cpu"] = {"busy_cpus_per_rank": [round(c / dt, 2) for c in cpus],
+                           "busy_cpus_total": round(sum(cpus) / dt, 2),
+                           "cgroup_quota_cpus": cpu_quota()}
         if world == 1 and not args.no_quality:
             res["quality"] = quality_probe(R["enc"], img, args.distance, args.effort)
         if world == 1 and not args.no_single and args.preset == "cjxl" and args.coder == "ans":
