@@ -44,6 +44,10 @@ constexpr int kThreads = 512;
 
 // LDS offset of tile-local pixel (lx, ly), lx/ly in [0, 66): one dword of
 // skew per interior 8-pixel block column
+// (round 6 measured a stride-67 layout without the skew, which the bank
+// model gives conflict-free row reads: front kernel -1 %, e4 -0.6 %, but the
+// lane = block reads of the thesis homogeneity phase become 8-way conflicted:
+// not kept, profiles/r06h)
 __device__ __forceinline__ int lds_at(int lx, int ly) { return ly * kS + lx + ((lx + 7) >> 3); }
 
 // ---------------------------------------------------------------------------
@@ -834,8 +838,12 @@ __device__ __forceinline__ void load_chunk(const FrontArgs& a, bool al, int i, i
 // and then for the ring's: every wait a full memory latency.
 struct TileLoads {
   uint32_t d[kChunkIters][3];  // chunks threadIdx.x + k * kThreads
-  uint32_t ring;               // ring pixel threadIdx.x: r | g << 8 | b << 16
+  uint32_t ring;               // ring pixel threadIdx.x - kRingT0: r | g << 8 | b << 16
 };
+// the ring's pixels go to the threads the last chunk round leaves idle
+// (threads kRingT0 .. kRingT0 + 267), so the ring costs no pass of its own
+constexpr int kRingT0 = kChunks - (kChunkIters - 1) * kThreads;
+static_assert(kRingT0 + kRing <= kThreads, "the ring fits the last round's idle threads");
 __device__ __forceinline__ int ring_x(int i) { return i < 68 ? i - 1 : (i < 136 ? i - 69 : (i < 202 ? -1 : 66)); }
 __device__ __forceinline__ int ring_y(int i) { return i < 68 ? -1 : (i < 136 ? 66 : (i < 202 ? i - 136 : i - 202)); }
 __device__ __forceinline__ void issue_tile_loads(const FrontArgs& a, int ox, int oy, bool gab,
@@ -845,8 +853,9 @@ __device__ __forceinline__ void issue_tile_loads(const FrontArgs& a, int ox, int
   for (int k = 0; k < kChunkIters; k++)
     load_chunk(a, al, min((int)threadIdx.x + k * kThreads, kChunks - 1), ox, oy, L.d[k]);
   L.ring = 0;
-  if (gab && threadIdx.x < (unsigned)kRing) {  // (the ring's pixels: gab_ring's clamping)
-    const int i = threadIdx.x, lx = ring_x(i), ly = ring_y(i);
+  const int ri = (int)threadIdx.x - kRingT0;
+  if (gab && ri >= 0 && ri < kRing) {  // (the ring's pixels, clamped to the image)
+    const int i = ri, lx = ring_x(i), ly = ring_y(i);
     const int sx = min(max(ox + lx, 0), (int)a.w - 1), sy = min(max(oy + ly, 0), (int)a.h - 1);
     const uint8_t* q = a.rgb + (size_t)sy * a.stride + 3 * (size_t)sx;
     L.ring = (uint32_t)q[0] | (uint32_t)q[1] << 8 | (uint32_t)q[2] << 16;
@@ -859,12 +868,22 @@ __device__ __forceinline__ void issue_tile_loads(const FrontArgs& a, int ox, int
 // The chunks are converted in a rolled loop (four inlined conversions; the
 // chunk registers rotate, so every index stays static).
 __device__ __forceinline__ void load_xyb_tile(const FrontArgs& a, const float* lut, float* sPix,
-                                              int ox, int oy, bool rep, TileLoads& L) {
+                                              int ox, int oy, bool rep, TileLoads& L,
+                                              float* ring) {
   const float cb = cbrt_det(kOpsinBias);
 #pragma unroll 1
   for (int k = 0; k < kChunkIters; k++) {
     const int i = threadIdx.x + k * kThreads;
-    if (i < kChunks) {
+    if (i >= kChunks) {  // (last round) the Gaborish ring's pixel instead
+      const int ri = (int)threadIdx.x - kRingT0;
+      if (ring && ri >= 0 && ri < kRing) {
+        float X, Y, B;
+        pixel_xyb(lut, cb, L.ring & 0xFF, (L.ring >> 8) & 0xFF, (L.ring >> 16) & 0xFF, X, Y, B);
+        ring[ri] = X;
+        ring[kRing + ri] = Y;
+        ring[2 * kRing + ri] = B;
+      }
+    } else {
       const int ly = i / kChunksX, cx = i - ly * kChunksX;
       const int gy = oy + ly, gx0 = ox - 3 + 4 * cx;
 #pragma unroll
@@ -924,19 +943,6 @@ __device__ __forceinline__ int ring_index(int lx, int ly) {  // (lx, ly) on the 
   if (lx == -1) return 136 + ly;
   return 202 + ly;
 }
-// RGB8 -> XYB of the ring pixels (the tile load's replication rule), from the
-// pixel issue_tile_loads fetched
-__device__ __forceinline__ void gab_ring(const float* lut, float* ring, const TileLoads& L) {
-  const float cb = cbrt_det(kOpsinBias);
-  const int i = threadIdx.x;
-  if (i < kRing) {
-    float X, Y, B;
-    pixel_xyb(lut, cb, L.ring & 0xFF, (L.ring >> 8) & 0xFF, (L.ring >> 16) & 0xFF, X, Y, B);
-    ring[i] = X;
-    ring[kRing + i] = Y;
-    ring[2 * kRing + i] = B;
-  }
-}
 // Sweep: thread = (row half, channel, column), 396 threads; a 3 x 3 window in
 // registers, one new row per step, the 33 outputs of its column half kept in
 // registers until every thread has read its inputs (one barrier), then
@@ -949,7 +955,7 @@ __device__ __forceinline__ void gab_ring(const float* lut, float* ring, const Ti
 // Round 6: every tile takes this form.  The edge tiles' clamped sweep (a
 // second 33-step body with a clamp per sample: 28 KB of the kernel's code)
 // is gone: an edge tile's LDS tile and ring hold the clamped image sample at
-// every position (load_xyb_tile rep; gab_ring clamps to the image), which is
+// every position (load_xyb_tile rep; the ring pixels are clamped to the image), which is
 // what the clamped sweep read, so every in-frame output is the same float
 // expression of the same values; the positions outside the padded frame are
 // zeroed after it (zero_outside).
@@ -1100,26 +1106,46 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
   unsigned long long fprof_t0 = 0;
 #endif
   FPROF(0);
+  // the table loads first, then the tile's (HBM) loads: a wave's loads
+  // complete in order, so the table stores below wait for the tables (L2
+  // hits) only, and the tile's loads stay in flight through them (round 6;
+  // the other order made the table copy wait a memory latency)
+  constexpr int kTabIt = (kNT * 3 * 64 + kThreads - 1) / kThreads;
+  const bool t256 = tid < 256, t384 = tid < kNT * 64;
+  const float lut_v = t256 ? c_lut[tid] : 0.0f, btab_v = t256 ? c_btab[tid] : 0.0f;
+  const float iw_v = t384 ? c_iwperm[tid] : 0.0f;
+  const uint8_t zz_v = t384 ? c_zz[tid] : 0;
+  float w_v[kTabIt], sd_v[kTabIt];
+#pragma unroll
+  for (int k = 0; k < kTabIt; k++) {
+    const int i = tid + k * kThreads;
+    w_v[k] = i < kNT * 3 * 64 ? c_wperm[i] : 0.0f;
+    sd_v[k] = i < kNT * 3 * 64 ? c_sdperm[i] : 0.0f;
+  }
   TileLoads TL;
   issue_tile_loads(a, ox, oy, a.gab, TL);  // in flight through the table copies
-  if (tid < 256) {
-    sLut[tid] = c_lut[tid];
-    sBtab[tid] = c_btab[tid];
+  if (t256) {
+    sLut[tid] = lut_v;
+    sBtab[tid] = btab_v;
   }
-  for (int i = tid; i < kNT * 64; i += kThreads) {
-    sIwperm[i] = c_iwperm[i];
-    sZz[i] = c_zz[i];
+  if (t384) {
+    sIwperm[tid] = iw_v;
+    sZz[tid] = zz_v;
   }
-  for (int i = tid; i < kNT * 3 * 64; i += kThreads) {
-    sWperm[i] = c_wperm[i];
-    sSdperm[i] = c_sdperm[i];
+#pragma unroll
+  for (int k = 0; k < kTabIt; k++) {
+    const int i = tid + k * kThreads;
+    if (i < kNT * 3 * 64) {
+      sWperm[i] = w_v[k];
+      sSdperm[i] = sd_v[k];
+    }
   }
   __syncthreads();
   FPROF(1);  // tables
-  load_xyb_tile(a, sLut, sPix, ox, oy, a.gab, TL);
-  if (a.gab) {  // (uniform) the ring beside the tile, then the in-place sweep
-    float* ring = sUnion + 256;  // 3 x 268 floats, before phase A's sH
-    gab_ring(sLut, ring, TL);
+  // (Gaborish: the ring beside the tile, 3 x 268 floats before phase A's sH)
+  float* const ring = a.gab ? sUnion + 256 : nullptr;
+  load_xyb_tile(a, sLut, sPix, ox, oy, a.gab, TL, ring);
+  if (a.gab) {  // (uniform) the in-place sweep
     __syncthreads();
     FPROF(2);  // tile + ring load
     gab_sweep(sPix, ring);
@@ -1234,9 +1260,28 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
     }
     __syncthreads();
     if (tid < 4) {
+      // the tile's sum in raster order, the same float adds; the partials come
+      // in 16-byte loads, 16 at a time (a dependent LDS read per add before:
+      // round 6), and a block outside a partial tile adds +0 instead of being
+      // skipped -- the same sum: T starts at +0 and a sum is -0 only when both
+      // of its terms are, so T + 0 = T at every step
       float T = 0.0f;
-      for (int bb = 0; bb < 64; bb++)
-        if ((bb & 7) < nbx && (bb >> 3) < nby) T = T + cs[tid * 64 + bb];
+      const float4* row = reinterpret_cast<const float4*>(cs + tid * 64);
+#pragma unroll
+      for (int q0 = 0; q0 < 16; q0 += 4) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) v[u] = row[q0 + u];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const float e[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            const int bb = (q0 + u) * 4 + j;
+            T = T + (((bb & 7) < nbx && (bb >> 3) < nby) ? e[j] : 0.0f);
+          }
+        }
+      }
       cs[256 + tid] = T;
     }
     __syncthreads();

@@ -602,6 +602,19 @@ static void build_rows(const Frame& f, const Plan& P, std::vector<LfRow>& rows,
   schunks.push_back((uint32_t)chunks.size());
 }
 
+// Host waits on the library's events (helper threads waiting for statistics,
+// emission, codestream copies): JXG_EVENT_BLOCKING=1 makes them blocking-sync
+// events (the waiting thread sleeps until the GPU signals) instead of the
+// runtime's default active wait -- an A/B switch for the host-CPU budget of
+// several ranks per node
+static hipError_t make_event(hipEvent_t* e, unsigned flags) {
+  static const bool blocking = [] {
+    const char* v = std::getenv("JXG_EVENT_BLOCKING");
+    return v && v[0] == '1';
+  }();
+  return hipEventCreateWithFlags(e, flags | (blocking ? hipEventBlockingSync : 0u));
+}
+
 static float elapsed(hipEvent_t a, hipEvent_t b) {
   float ms = 0.0f;
   (void)hipEventElapsedTime(&ms, a, b);
@@ -1693,7 +1706,7 @@ static jxg_status stage_concat_split(Ctx* c, Job& J, uint8_t** host_out, size_t*
 // stream the caller's writes must be complete before the call (include/jxg.h).
 static jxg_status order_input(Ctx* owner, Ctx* lane) {
   if (!owner->in_stream) return JXG_OK;
-  if (!lane->ev_in && hipEventCreateWithFlags(&lane->ev_in, hipEventDisableTiming) != hipSuccess)
+  if (!lane->ev_in && make_event(&lane->ev_in, hipEventDisableTiming) != hipSuccess)
     return JXG_ERR_HIP;
   JXG_HIP(hipEventRecord(lane->ev_in, owner->in_stream));
   JXG_HIP(hipStreamWaitEvent(lane->stream, lane->ev_in, 0));
@@ -1849,7 +1862,7 @@ static jxg_status ctx_new_lane(const jxg_params& params, Ctx** out) {
     return JXG_ERR_HIP;
   }
   for (auto& e : c->ev)
-    if (hipEventCreate(&e) != hipSuccess) {
+    if (make_event(&e, 0) != hipSuccess) {
       jxg_destroy(reinterpret_cast<jxg_ctx*>(c));
       return JXG_ERR_HIP;
     }
@@ -2062,7 +2075,7 @@ static jxg_status ensure_slots(Ctx* L, uint32_t k) {
     q->stream = L->stream;
     L->slots.emplace_back(q);
     for (auto& e : q->ev)
-      if (hipEventCreate(&e) != hipSuccess) return JXG_ERR_HIP;
+      if (make_event(&e, 0) != hipSuccess) return JXG_ERR_HIP;
   }
   return JXG_OK;
 }
@@ -2218,7 +2231,7 @@ static jxg_status pipe_complete_oldest(Ctx* c) {
     // thread one GPU round trip per frame.
     if (p.evfree.empty()) {
       hipEvent_t e = nullptr;
-      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return JXG_ERR_HIP;
+      if (make_event(&e, hipEventDisableTiming) != hipSuccess) return JXG_ERR_HIP;
       p.evfree.push_back(e);
     }
     st = enc_finish_start(fr.lane, fr.J, false);
@@ -3108,7 +3121,7 @@ jxg_status jxg_shard_write_next(jxg_ctx* ctx, const uint32_t* const* heads, cons
   // PREVIOUS frame's copies have landed (jxg_shard_write_flush: the last one's)
   st = shard_write_host(S, heads, head_words, n, static_cast<uint8_t*>(dst), dst_size, total, false);
   if (st) return st;  // (too small a buffer: the frame stays, *total tells the size)
-  if (!S->ev_write && hipEventCreateWithFlags(&S->ev_write, hipEventDisableTiming) != hipSuccess)
+  if (!S->ev_write && make_event(&S->ev_write, hipEventDisableTiming) != hipSuccess)
     return JXG_ERR_HIP;
   Pipe& p = *c->pipe;
   // this slot's event may still be queued for an older write of the slot:

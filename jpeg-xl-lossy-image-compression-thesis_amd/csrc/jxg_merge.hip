@@ -690,6 +690,7 @@ __device__ __forceinline__ void setup_varblocks(const MergeArgs& a, const Pass& 
       }
     }
     S.valid[v] = ok;
+    S.vraw[v] = 0;  // (vraw_pass: atomic max over the covered blocks)
     S.vbits[v] = 0;
     S.vnz[v][0] = S.vnz[v][1] = S.vnz[v][2] = 0;
   }
@@ -698,15 +699,18 @@ __device__ __forceinline__ void setup_varblocks(const MergeArgs& a, const Pass& 
   for (int i = t; i < 256; i += kMThreads)
     S.btab[i] = i == 0 ? 0.0f : (i == 1 ? 1.0f - 0.07005449891748593f : (float)i - 0.145f / (float)i);
 }
-// varblock quant field = max raw over its covered blocks (after a barrier)
+// varblock quant field = max raw over its covered blocks (after a barrier):
+// one thread per block, an LDS atomic max into its varblock (round 6: one
+// thread per varblock walked up to 64 blocks in a row of dependent LDS reads
+// while its wave's row pass waited; max is order-free, so the result is the
+// same); visible to the quantization after the row pass's barrier
 __device__ __forceinline__ void vraw_pass(const MergeArgs& a, const Pass& P, MergeLds& S) {
-  const int v = threadIdx.x;
-  if (v < P.NV() && S.valid[v]) {
-    const int bx0 = P.bx0(v), by0 = P.by0(v);
-    int raw = 0;
-    for (int iy = 0; iy < P.cy(); iy++)
-      for (int ix = 0; ix < P.cx(); ix++) raw = max(raw, (int)S.braw[(by0 + iy) * 8 + bx0 + ix] + 1);
-    S.vraw[v] = raw;
+  (void)a;
+  const int b = threadIdx.x;
+  if (b < 64) {
+    const int lbx = b & 7, lby = b >> 3;
+    const int v = ((lby >> P.lcy) << P.lGX()) | (lbx >> P.lcx);
+    if (v < P.NV() && S.valid[v]) atomicMax(&S.vraw[v], (int)S.braw[b] + 1);
   }
 }
 
@@ -725,9 +729,15 @@ void merge_eval_kernel(Batch<MergeArgs> bt_) {
   if (P.ls > max_level(a)) return;  // level not searched at this effort
   const int nbx = min(8, (int)a.bxs - P.tx * 8), nby = min(8, (int)a.bys - P.ty * 8);
   if ((1 << P.ls) > nbx || (1 << P.ls) > nby) return;  // no region of this level fits
+#ifdef JXG_MERGE_PROFILE
+  const unsigned long long t_setup = __builtin_readcyclecounter();
+#endif
   setup_varblocks<false>(a, P, S, nbx, nby);
   __syncthreads();
   vraw_pass(a, P, S);
+#ifdef JXG_MERGE_PROFILE
+  if (threadIdx.x == 0) atomicAdd(&g_mprof[P.si][5], __builtin_readcyclecounter() - t_setup);
+#endif
   transform_quant<false>(a, P, S);
   const int v = threadIdx.x;
   if (v < P.NV() && S.valid[v]) {
@@ -1004,11 +1014,12 @@ __global__ __launch_bounds__(1024) void vb_list_kernel(Batch<VbArgs> bt_) {
 void dump_merge_profile() {
   unsigned long long h[16][8];
   if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_mprof), sizeof(h)) != hipSuccess) return;
-  std::fprintf(stderr, "merge_eval cycles (thread 0 sums, Mcycles): shape rows cols quantY quantXB\n");
+  std::fprintf(stderr, "merge_eval cycles (thread 0 sums, Mcycles): shape setup rows+cols(Y,X) "
+                       "qtab quantY+X B(rows,cols,quant)\n");
   for (int si = 0; si < kNumShapes; si++)
-    std::fprintf(stderr, "  %dx%d %8.1f %8.1f %8.1f %8.1f\n", 8 << kShapes[si].lcy,
-                 8 << kShapes[si].lcx, h[si][1] / 1e6, h[si][2] / 1e6, h[si][3] / 1e6,
-                 h[si][4] / 1e6);
+    std::fprintf(stderr, "  %dx%d %8.1f %8.1f %8.1f %8.1f %8.1f\n", 8 << kShapes[si].lcy,
+                 8 << kShapes[si].lcx, h[si][5] / 1e6, h[si][1] / 1e6, h[si][2] / 1e6,
+                 h[si][3] / 1e6, h[si][4] / 1e6);
 }
 #else
 void dump_merge_profile() {}
