@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 TAG=${1:-cfg}
 O=gpurun_out/$TAG
 mkdir -p $O
-B="python bench.py --no-cpu-baseline --no-quality --alt-thesis 0"
+B="python bench.py --no-cpu-baseline --no-quality --no-single --alt-thesis 0"
 timeout -k 10 200 $B --config 1 > $O/cfg_4k.log 2>&1
 for d in 0.5 1.0 2.0; do
   timeout -k 10 200 $B --config 3 --steps 6 --warmup 3 --distance $d --alt-coder 0 > $O/cfg_batch_d$d.log 2>&1
