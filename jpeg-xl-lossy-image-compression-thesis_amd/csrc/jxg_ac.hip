@@ -31,7 +31,10 @@
 
 namespace jxg {
 
-__constant__ uint8_t c_cluster[kAcCtx];  // context -> static cluster id
+// context -> static cluster id (padded to whole 16-byte words: ac_hist copies
+// it to LDS with 16-byte loads; the pad stays 0)
+constexpr int kAcCtxPad = (kAcCtx + 15) & ~15;
+__constant__ __attribute__((aligned(16))) uint8_t c_cluster[kAcCtxPad];
 
 constexpr int kAcThreads = 1024;
 
@@ -214,21 +217,35 @@ __device__ __forceinline__ uint32_t task_token_count(const AcArgs& a, const Slic
   return (t.sl == 0 ? 1u : 0u) + (hi >= lo ? (uint32_t)(hi - lo + 1) : 0u);
 }
 
-// predicted-nz image (the band and the row above) and per-slice non-zero counts
+// predicted-nz image (the band and the row above) and per-slice non-zero counts.
+// Round 6: every position's loads (its strategy byte, three counts) are
+// issued before the first LDS store -- the strided loop waited a memory
+// latency per position and channel (the phase clock put ~90 K cycles per band
+// workgroup here, a third of its time).
 template <int BR>
 __device__ __forceinline__ void fill_slices(const AcArgs& a, const GroupGeom& G,
                                             const SliceTask& t, AcLds<BR>& L, int y0) {
   const size_t nb = (size_t)a.bxs * a.bys;
-  for (int i = threadIdx.x; i < 3 * (BR + 1) * 32; i += blockDim.x) {
-    const int c = i / ((BR + 1) * 32), r = (i >> 5) % (BR + 1), bx = i & 31;
-    const int by = y0 - 1 + r;
-    if (bx < G.gw && by >= 0 && by < G.gh) {
-      const size_t gb = (size_t)(G.by0 + by) * a.bxs + G.bx0 + bx;
-      const int acs = a.acs[gb];
-      int l, cx, cy;
-      varblock_dims(acs, l, cx, cy);  // covered blocks (flag set) hold scaled counts
-      L.nz[c][r * 32 + bx] = (uint8_t)((a.nz[c * nb + gb] + (1 << l) - 1) >> l);
-    }
+  constexpr int kPos = (BR + 1) * 32, kNT = BR * 32, kIt = (kPos + kNT - 1) / kNT;
+  uint32_t acsv[kIt], nzv[kIt][3];
+  bool in[kIt];
+#pragma unroll
+  for (int it = 0; it < kIt; it++) {
+    const int i = threadIdx.x + it * kNT, r = i >> 5, bx = i & 31, by = y0 - 1 + r;
+    in[it] = i < kPos && bx < G.gw && by >= 0 && by < G.gh;
+    const size_t gb = in[it] ? (size_t)(G.by0 + by) * a.bxs + G.bx0 + bx : 0;
+    acsv[it] = in[it] ? a.acs[gb] : 0u;
+#pragma unroll
+    for (int c = 0; c < 3; c++) nzv[it][c] = in[it] ? a.nz[c * nb + gb] : 0u;
+  }
+#pragma unroll
+  for (int it = 0; it < kIt; it++) {
+    if (!in[it]) continue;
+    const int i = threadIdx.x + it * kNT;
+    int l, cx, cy;
+    varblock_dims((int)acsv[it], l, cx, cy);  // covered blocks (flag set) hold scaled counts
+#pragma unroll
+    for (int c = 0; c < 3; c++) L.nz[c][i] = (uint8_t)((nzv[it][c] + (1u << l) - 1) >> l);
   }
   if (t.valid && t.lcb > 0) {
     const int cb = 1 << t.lcb, me = threadIdx.x;
@@ -252,10 +269,8 @@ __device__ __forceinline__ void fill_slices(const AcArgs& a, const GroupGeom& G,
 
 // walk state of task (t, c) at its first coefficient; nz = varblock count
 template <int BR>
-__device__ __forceinline__ void slice_state(const AcArgs& a, const SliceTask& t,
-                                            const AcLds<BR>& L, int c, int y0, int& nz, int& left,
-                                            int& prev) {
-  nz = a.nz[c * (size_t)a.bxs * a.bys + t.ogb];
+__device__ __forceinline__ void slice_state(const SliceTask& t, const AcLds<BR>& L, int c, int y0,
+                                            int nz, int& left, int& prev) {
   const int cb = 1 << t.lcb;
   left = nz;
   prev = nz > cb * 4 ? 0 : 1;  // nz > size / 16
@@ -289,6 +304,32 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sWave,
   return before + incl - v;
 }
 
+// JXG_FRONT_PROFILE (experiment builds only): ac_hist phase clock sums of
+// thread 0 of every band workgroup, printed by dump_hist_profile()
+#ifdef JXG_FRONT_PROFILE
+__device__ unsigned long long g_hprof[8];
+#define HPROF(k)                                                     \
+  do {                                                               \
+    if (threadIdx.x == 0) {                                          \
+      const unsigned long long now_ = __builtin_readcyclecounter();  \
+      if ((k) > 0) atomicAdd(&g_hprof[(k)], now_ - hprof_t0);       \
+      else atomicAdd(&g_hprof[0], 1ull);                             \
+      hprof_t0 = now_;                                               \
+    }                                                                \
+  } while (0)
+void dump_hist_profile() {
+  unsigned long long h[8];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_hprof), sizeof(h)) != hipSuccess) return;
+  static const char* kNames[6] = {"workgroups", "fill slices", "token counts", "scan", "walk", "flush"};
+  std::fprintf(stderr, "ac_hist thread-0 shader cycles (Mcycles summed over workgroups):\n");
+  for (int k = 0; k < 6; k++) std::fprintf(stderr, "  %-16s %12.3f\n", kNames[k], k ? h[k] / 1e6 : (double)h[0]);
+}
+#else
+#define HPROF(k) \
+  do {           \
+  } while (0)
+void dump_hist_profile() {}
+#endif
 // The band's clustered histogram in LDS.  An 8-row band (BR = 8) has at most
 // 256 x 3 x 64 + 768 = 49920 tokens, so its counts are u16, two bins per word,
 // and a half never carries.  The whole-group form (BR = 32, effort >= 8) walks
@@ -304,7 +345,7 @@ __global__ __launch_bounds__(BR * 32) void ac_hist_kernel(Batch<AcArgs> bt_) {
   constexpr int kHistWords = kWide ? kMaxClusters * kAcTok : kMaxClusters * kAcTok / 2;
   __shared__ uint32_t sHist[kHistWords];
   __shared__ AcLds<BR> L;
-  __shared__ uint8_t sClu[kAcCtx];
+  __shared__ __attribute__((aligned(16))) uint8_t sClu[kAcCtxPad];
   __shared__ uint32_t sTask[3][kBandBlocks];  // tokens per (channel, slice task)
   __shared__ uint32_t sBase[kBandBlocks];     // first token of each varblock (first block)
   __shared__ uint32_t sWave[kHistThreads / 64];
@@ -321,17 +362,38 @@ __global__ __launch_bounds__(BR * 32) void ac_hist_kernel(Batch<AcArgs> bt_) {
     if (threadIdx.x == 0) a.bandtok[g * kBands + band] = 0;
     return;
   }
+#ifdef JXG_FRONT_PROFILE
+  unsigned long long hprof_t0 = 0;
+#endif
+  HPROF(0);
   for (int i = threadIdx.x; i < kHistWords; i += blockDim.x) sHist[i] = 0;
   if (threadIdx.x < 64) {
     sNnzCtx[threadIdx.x] = (uint16_t)nnz_ctx(threadIdx.x);
     sFreqCtx[threadIdx.x] = (uint8_t)freq_ctx(threadIdx.x);
   }
-  for (int i = threadIdx.x; i < kAcCtx; i += blockDim.x) sClu[i] = c_cluster[i];
+  {  // the cluster map: 16-byte loads, all issued before the stores
+    constexpr int kQ = kAcCtxPad / 16, kQIt = (kQ + kHistThreads - 1) / kHistThreads;
+    uint4 q[kQIt];
+#pragma unroll
+    for (int it = 0; it < kQIt; it++) {
+      const int i = threadIdx.x + it * kHistThreads;
+      q[it] = i < kQ ? reinterpret_cast<const uint4*>(c_cluster)[i] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int it = 0; it < kQIt; it++) {
+      const int i = threadIdx.x + it * kHistThreads;
+      if (i < kQ) reinterpret_cast<uint4*>(sClu)[i] = q[it];
+    }
+  }
   if (threadIdx.x < 3) sNtok[threadIdx.x] = 0;
   if (threadIdx.x == 0) sBound = 0;
   const SliceTask t = slice_task(a, G, y0);
+  uint32_t nzo[3];  // the varblock's non-zero counts (the walk's start state)
+#pragma unroll
+  for (int c = 0; c < 3; c++) nzo[c] = t.valid ? a.nz[c * (size_t)a.bxs * a.bys + t.ogb] : 0u;
   fill_slices(a, G, t, L, y0);
   __syncthreads();
+  HPROF(1);
   const int me = threadIdx.x;
   // token counts per task without a walk -> stream positions (varblocks by
   // first block raster, channels Y, X, B, slices): one scan over varblocks
@@ -340,6 +402,7 @@ __global__ __launch_bounds__(BR * 32) void ac_hist_kernel(Batch<AcArgs> bt_) {
     for (int ci = 0; ci < 3; ci++) sTask[ci][me] = task_token_count(a, t, L, channel_of(ci), y0);
   }
   __syncthreads();
+  HPROF(2);
   uint32_t vtot = 0;
   const int cb = 1 << t.lcb;
   if (t.valid && t.sl == 0) {
@@ -350,6 +413,7 @@ __global__ __launch_bounds__(BR * 32) void ac_hist_kernel(Batch<AcArgs> bt_) {
   const uint32_t off = block_excl_scan<kHistThreads>(vtot, sWave, &total);
   if (t.valid && t.sl == 0) sBase[me] = off;
   __syncthreads();
+  HPROF(3);
   // one walk: clustered histogram, bit bound, and every token's 32-bit record
   // at its stream position.  Wave-parallel: each thread derives the walk state
   // of its own task (slice, channel); the wave then takes its 64 tasks one at
@@ -385,8 +449,9 @@ __global__ __launch_bounds__(BR * 32) void ac_hist_kernel(Batch<AcArgs> bt_) {
       idx = pos + before;
       cnt = sTask[ci][me];
       pos += chan_total;
-      int nz, left, prev;
-      slice_state(a, t, L, c, y0, nz, left, prev);
+      const int nz = (int)nzo[c];
+      int left, prev;
+      slice_state(t, L, c, y0, nz, left, prev);
       const int bctx = block_ctx_of(c, t.type);
       // info: left (16 bits) | prev << 16 | lcb << 17 (4 bits) | bctx << 21;
       // info2: the slice index (varblocks of up to 1024 blocks)
@@ -412,7 +477,10 @@ __global__ __launch_bounds__(BR * 32) void ac_hist_kernel(Batch<AcArgs> bt_) {
     const bool need = t.valid && cnt > (t.sl == 0 ? 1u : 0u);
     const uint32_t qoff = (uint32_t)((t.gb * 3 + c) * 64);
     uint64_t M = __ballot(need);
-    constexpr int kBatch = 8;
+#ifndef JXG_AC_BATCH
+#define JXG_AC_BATCH 8
+#endif
+    constexpr int kBatch = JXG_AC_BATCH;
     while (M) {
       int js[kBatch];
 #pragma unroll
@@ -459,6 +527,7 @@ __global__ __launch_bounds__(BR * 32) void ac_hist_kernel(Batch<AcArgs> bt_) {
   atomicAdd(&sNtok[1], nt[1]);
   atomicAdd(&sNtok[2], nt[2]);
   __syncthreads();
+  HPROF(4);
   for (int i = threadIdx.x; i < kHistWords; i += blockDim.x) {
     const uint32_t w = sHist[i];
     if (!w) continue;
@@ -478,6 +547,7 @@ __global__ __launch_bounds__(BR * 32) void ac_hist_kernel(Batch<AcArgs> bt_) {
     atomicAdd(&a.ntok[g * 3 + 2], sNtok[2]);
     a.bandtok[g * kBands + band] = total;
   }
+  HPROF(5);
 }
 
 // prefix-code emission from the group's token records (no coefficient walk):

@@ -848,6 +848,15 @@ __device__ __forceinline__ int ring_x(int i) { return i < 68 ? i - 1 : (i < 136 
 __device__ __forceinline__ int ring_y(int i) { return i < 68 ? -1 : (i < 136 ? 66 : (i < 202 ? i - 136 : i - 202)); }
 __device__ __forceinline__ void issue_tile_loads(const FrontArgs& a, int ox, int oy, bool gab,
                                                  TileLoads& L) {
+#ifdef JXG_EXP_NOLOAD  // (timing experiment only: no tile loads, hashed bytes)
+#pragma unroll
+  for (int k = 0; k < kChunkIters; k++)
+#pragma unroll
+    for (int w = 0; w < 3; w++)
+      L.d[k][w] = ((uint32_t)threadIdx.x * 2654435761u + (uint32_t)(ox * 7919 + oy * 104729) + k * 31 + w) * 2246822519u;
+  L.ring = ((uint32_t)threadIdx.x * 2246822519u + (uint32_t)(ox + oy)) & 0xFFFFFF;
+  return;
+#endif
   const bool al = ((a.stride | (size_t)a.rgb) & 3) == 0;
 #pragma unroll
   for (int k = 0; k < kChunkIters; k++)
@@ -1119,8 +1128,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(JXG_FR
 #pragma unroll
   for (int k = 0; k < kTabIt; k++) {
     const int i = tid + k * kThreads;
+#ifdef JXG_EXP_NOTAB  // (timing experiment only: no per-workgroup weight-table loads)
+    w_v[k] = 0.25f + (float)(i & 63) * (1.0f / 64.0f);
+    sd_v[k] = 1.0f + (float)(i & 31) * (1.0f / 32.0f);
+#else
     w_v[k] = i < kNT * 3 * 64 ? c_wperm[i] : 0.0f;
     sd_v[k] = i < kNT * 3 * 64 ? c_sdperm[i] : 0.0f;
+#endif
   }
   TileLoads TL;
   issue_tile_loads(a, ox, oy, a.gab, TL);  // in flight through the table copies

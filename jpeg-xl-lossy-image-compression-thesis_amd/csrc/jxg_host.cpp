@@ -2778,6 +2778,7 @@ void jxg_destroy(jxg_ctx* ctx) {
 #endif
 #ifdef JXG_FRONT_PROFILE
   dump_front_profile();
+  dump_hist_profile();
 #endif
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);

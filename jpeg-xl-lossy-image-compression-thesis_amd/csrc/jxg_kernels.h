@@ -305,6 +305,7 @@ hipError_t set_merge_constants(const float* llf_p /*[4][8]*/, const float* llf_i
 hipError_t launch_merge(const MergeArgs* a, uint32_t k, hipStream_t s);
 void dump_merge_profile();  // JXG_MERGE_PROFILE experiment builds; no-op otherwise
 void dump_front_profile();  // JXG_FRONT_PROFILE experiment builds; no-op otherwise
+void dump_hist_profile();   // (the same builds: ac_hist's phase clock)
 void launch_vb_list(const VbArgs* a, uint32_t k, uint32_t nlf, hipStream_t s);
 // decode-side quality (jxg_metrics.hip): orig / comp RGB8 interleaved rows
 struct MetricArgs {

@@ -22,9 +22,15 @@ torch.cuda.synchronize()
 enc = jxg.Encoder(distance=1.0, effort=e, flags=flags)
 enc.encode_device(t.data_ptr(), w, h)  # warm (counted too)
 fk = []
+mk = []
 for _ in range(n):
     enc.encode_device(t.data_ptr(), w, h)
     fk.append(enc.timings()[0])
+    if os.environ.get("PROBE_MERGE"):
+        st = enc.stats()
+        mk.append(st["ms_front"] - st["ms_front_kernel"])
 print("effort %d preset %s: front kernel ms per launch %s (the profile sums %d launches)"
       % (e, preset, [round(x, 4) for x in fk], n + 1), flush=True)
+if mk:
+    print("effort %d preset %s: merge stage ms per encode %s" % (e, preset, [round(x, 4) for x in mk]), flush=True)
 enc.close()
