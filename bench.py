@@ -433,10 +433,11 @@ def spawn_ranks(n, argv):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # 100 frames by default: the timed region of a streaming run includes one
-    # pipeline fill + drain (about one frame's latency, ~22 ms at 8K ANS), which
-    # costs 16 % of a 20-frame run and 3 % of a 100-frame one
-    ap.add_argument("--steps", type=int, default=100)
+    # 300 frames by default: the timed region of a streaming run includes one
+    # pipeline fill + drain (about one frame's latency, ~25 ms at 8K ANS), which
+    # costs 16 % of a 20-frame run, 2-3 % of a 100-frame one and < 1 % of 300
+    # (1.1 s of timed encodes at 8K)
+    ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=2, help="BASELINE config index (2 = 8K)")
     ap.add_argument("--distance", type=float, default=1.0)
