@@ -135,30 +135,57 @@ __global__ __launch_bounds__(kAqThreads) void aq_kernel(Batch<AqArgs> bt_) {
   // cbrt_det2: the same values as one pixel at a time)
   const float cb = cbrt_det(kOpsinBias);
   const pf2 cb2 = {cb, cb};
-  for (int i = tid; i < kAqR * kAqR / 2; i += kAqThreads) {
-    const int ly = (2 * i) / kAqR, lx0 = 2 * i - ly * kAqR;
-    const int gy = min(max(oy - kAqRing + ly, 0), yp - 1);
-    const uint8_t* row = a.rgb + (size_t)min(gy, (int)a.h - 1) * a.stride;
-    pf2 r, g, b;
+  // Round 6: the pairs go kAqBatch at a time, every byte load of a batch
+  // issued before its first conversion (the strided loop waited one memory
+  // latency per pair); a pair index past the region is clamped for the loads
+  // and its stores skipped.
+#ifndef JXG_AQ_BATCH
+#define JXG_AQ_BATCH 4
+#endif
+  constexpr int kPairs = kAqR * kAqR / 2, kAqBatch = JXG_AQ_BATCH;
+  constexpr int kPairIt = (kPairs + kAqThreads - 1) / kAqThreads;
+#pragma unroll 1
+  for (int it0 = 0; it0 < kPairIt; it0 += kAqBatch) {
+    uint32_t px[kAqBatch][2][3];
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const int gx = min(max(ox - kAqRing + lx0 + h, 0), xp - 1);
-      const uint8_t* q = row + 3 * (size_t)min(gx, (int)a.w - 1);
-      r[h] = sLut[q[0]];
-      g[h] = sLut[q[1]];
-      b[h] = sLut[q[2]];
+    for (int u = 0; u < kAqBatch; u++) {
+      const int i = min(tid + (it0 + u) * kAqThreads, kPairs - 1);
+      const int ly = (2 * i) / kAqR, lx0 = 2 * i - ly * kAqR;
+      const int gy = min(max(oy - kAqRing + ly, 0), yp - 1);
+      const uint8_t* row = a.rgb + (size_t)min(gy, (int)a.h - 1) * a.stride;
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const int gx = min(max(ox - kAqRing + lx0 + h, 0), xp - 1);
+        const uint8_t* q = row + 3 * (size_t)min(gx, (int)a.w - 1);
+        px[u][h][0] = q[0];
+        px[u][h][1] = q[1];
+        px[u][h][2] = q[2];
+      }
     }
-    pf2 m0, m1, m2;
-    opsin2(r, g, b, m0, m1, m2);
-    m0 = cbrt_det2(m0) - cb2;
-    m1 = cbrt_det2(m1) - cb2;
-    const pf2 Y = 0.5f * (m0 + m1), X = 0.5f * (m0 - m1);
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const int lx = lx0 + h;
-      sY[ly * kAqS + lx] = Y[h];
-      const int tlx = lx - kAqRing, tly = ly - kAqRing;
-      if (tlx >= 0 && tlx < 64 && tly >= 0 && tly < 64) sX[tly * 65 + tlx] = X[h];
+    for (int u = 0; u < kAqBatch; u++) {
+      const int i = tid + (it0 + u) * kAqThreads;
+      if (it0 + u >= kPairIt || i >= kPairs) break;  // (i grows with u)
+      const int ly = (2 * i) / kAqR, lx0 = 2 * i - ly * kAqR;
+      pf2 r, g, b;
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        r[h] = sLut[px[u][h][0]];
+        g[h] = sLut[px[u][h][1]];
+        b[h] = sLut[px[u][h][2]];
+      }
+      pf2 m0, m1, m2;
+      opsin2(r, g, b, m0, m1, m2);
+      m0 = cbrt_det2(m0) - cb2;
+      m1 = cbrt_det2(m1) - cb2;
+      const pf2 Y = 0.5f * (m0 + m1), X = 0.5f * (m0 - m1);
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const int lx = lx0 + h;
+        sY[ly * kAqS + lx] = Y[h];
+        const int tlx = lx - kAqRing, tly = ly - kAqRing;
+        if (tlx >= 0 && tlx < 64 && tly >= 0 && tly < 64) sX[tly * 65 + tlx] = X[h];
+      }
     }
   }
   __syncthreads();
