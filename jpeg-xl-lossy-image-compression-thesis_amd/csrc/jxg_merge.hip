@@ -466,6 +466,48 @@ __device__ __forceinline__ void load_qtab(const MergeArgs& a, const Pass& P, QTa
     }
   }
 }
+// All-reduce over an aligned group of C lanes (C = 8 .. 64, the group fully
+// active) as the XOR butterfly v += v(lane ^ m), m = 1, 2, 4, ...: every
+// step's partner value comes from DPP / ds_swizzle / readlane instead of a
+// ds_bpermute chain (round 6).  Exactness: each step adds the partner's
+// value, which is what lane ^ m holds -- xor 1 / 2 / 4 are exact lane
+// permutations (quad_perm, quad_perm + row_half_mirror), xor 8 is
+// row_half_mirror + row_mirror ((i ^ 7) ^ 15 = i ^ 8), xor 16 a ds_swizzle
+// xor mask; for xor 32 the two 32-lane halves are uniform by then, so the
+// partner is the other half's lane 0 / 32, and a + b = b + a.
+template <int M>
+__device__ __forceinline__ uint32_t grp_xor(uint32_t v) {
+  if constexpr (M == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+  if constexpr (M == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+  if constexpr (M == 4) {
+    const int t = __builtin_amdgcn_mov_dpp((int)v, 0x1B, 0xF, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_mov_dpp(t, 0x141, 0xF, 0xF, false);
+  }
+  if constexpr (M == 8) {
+    const int t = __builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_mov_dpp(t, 0x140, 0xF, 0xF, false);
+  }
+  if constexpr (M == 16) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F);
+  if constexpr (M == 32) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)v, 32);
+    return (threadIdx.x & 32) ? lo : hi;
+  }
+}
+template <int M>
+__device__ __forceinline__ void grp_step(float& cp, int& packed) {
+  cp += __uint_as_float(grp_xor<M>(__float_as_uint(cp)));
+  packed += (int)grp_xor<M>((uint32_t)packed);
+}
+__device__ __forceinline__ void group_all_reduce(float& cp, int& packed, int C) {
+  grp_step<1>(cp, packed);
+  grp_step<2>(cp, packed);
+  grp_step<4>(cp, packed);
+  if (C > 8) grp_step<8>(cp, packed);
+  if (C > 16) grp_step<16>(cp, packed);
+  if (C > 32) grp_step<32>(cp, packed);
+}
+
 template <int RPC, bool WRITE, int CH>
 __device__ __forceinline__ void quant_pass(const MergeArgs& a, const Pass& P, MergeLds& S, const QTab<RPC>& T) {
   constexpr int cidx = CH == 1 ? 0 : (CH == 0 ? 1 : 2);  // 0 Y, 1 X, 2 B
@@ -572,10 +614,7 @@ __device__ __forceinline__ void quant_pass(const MergeArgs& a, const Pass& P, Me
     // the chunk's column partials, tree-summed over the varblock's C lanes
     // (an aligned group inside one wave); bits | non-zeros << 20 likewise
     int packed = bits | nzc << 20;
-    for (int msk = 1; msk < C; msk <<= 1) {
-      cp += __shfl_xor(cp, msk, 64);
-      packed += __shfl_xor(packed, msk, 64);
-    }
+    group_all_reduce(cp, packed, C);
     if (x == 0) {
       S.qsum[cidx][ch][v] = cp;
       if (packed & 0xFFFFF) atomicAdd(&S.vbits[v], packed & 0xFFFFF);
