@@ -99,27 +99,36 @@ __device__ __forceinline__ void dct_from(const float* src, int st, float* x) {
 #pragma unroll
   for (int k = 0; k < N; k++) x[k] = x[k] * kLeeS[l][k];
 }
-// half h of the normalized 64-point DCT (Lee's first split: h = 0 the even
+// half h of the normalized N-point DCT (Lee's first split: h = 0 the even
 // outputs 2k from the sums, h = 1 the odd outputs 2k+1 from the scaled
-// differences) -- the same float ops as lee<64>, spread over two lanes.
-// dct64_first: t[i] from x[i] and its mirror x[63 - i]; dct64_rest: the
-// 32-point transform of t and the output scaling, out(k, value) for output
+// differences) -- the same float ops as lee<N>, spread over two lanes.
+// dctN_first: t[i] from x[i] and its mirror x[N - 1 - i]; dctN_rest: the
+// N/2-point transform of t and the output scaling, out(k, value) for output
 // 2k + h.  T = f2: two independent rows / columns with the same h.
+template <int N, class T>
+__device__ __forceinline__ T dctN_first(T xi, T xm, int i, int h) {
+  return h == 0 ? xi + xm : (xi - xm) * kLeeC[ilog2c<N>()][i];
+}
+template <int N, class T, class Out>
+__device__ __forceinline__ void dctN_rest(T* t, int h, Out out) {
+  constexpr int l = ilog2c<N>(), H = N / 2;
+  lee<H>(t);
+  if (h == 0) {
+#pragma unroll
+    for (int k = 0; k < H; k++) out(k, t[k] * kLeeS[l][2 * k]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < H - 1; k++) out(k, (t[k] + t[k + 1]) * kLeeS[l][2 * k + 1]);
+    out(H - 1, t[H - 1] * kLeeS[l][N - 1]);
+  }
+}
 template <class T>
 __device__ __forceinline__ T dct64_first(T xi, T xm, int i, int h) {
-  return h == 0 ? xi + xm : (xi - xm) * kLeeC[6][i];
+  return dctN_first<64>(xi, xm, i, h);
 }
 template <class T, class Out>
 __device__ __forceinline__ void dct64_rest(T* t, int h, Out out) {
-  lee<32>(t);
-  if (h == 0) {
-#pragma unroll
-    for (int k = 0; k < 32; k++) out(k, t[k] * kLeeS[6][2 * k]);
-  } else {
-#pragma unroll
-    for (int k = 0; k < 31; k++) out(k, (t[k] + t[k + 1]) * kLeeS[6][2 * k + 1]);
-    out(31, t[31] * kLeeS[6][63]);
-  }
+  dctN_rest<64>(t, h, out);
 }
 
 // JXG_MERGE_PROFILE (experiment builds only): per (shape, phase) cycle sums
@@ -367,8 +376,14 @@ __device__ __forceinline__ void col_pass(const Pass& P, MergeLds& S, int pass) {
     okA = S.valid[(band << lGX) | (X >> lC)];
     okB = S.valid[(band << lGX) | ((X + 32) >> lC)];
   };
-  if constexpr (R == 64) {
-    // 96 pairs x 2 halves; h wave-uniform (waves alternate h over 64 pairs)
+  // Two lanes per column pair (Lee halves, h wave-uniform: waves alternate h
+  // over 64 pairs) for 64-point columns, and (round 6) for 16 / 32-point
+  // columns whenever one lane per pair would leave threads idle (<= 128
+  // pairs: R = 32, and the B pass at R = 16) -- each lane then runs half the
+  // transform, every thread busy; a barrier separates the column reads from
+  // the in-place writes.
+  if constexpr (R == 64 || (R >= 16 && npairs <= kMThreads / 2)) {
+    constexpr int H = R / 2;
     constexpr int n = ((npairs + 63) >> 6) << 7;
     for (int i0 = 0; i0 < n; i0 += kMThreads) {
       const int i = i0 + threadIdx.x;
@@ -377,20 +392,20 @@ __device__ __forceinline__ void col_pass(const Pass& P, MergeLds& S, int pass) {
       bool okA = false, okB = false;
       if (p < npairs) col_of(p, off, okA, okB);
       const bool act = okA || okB;
-      f2 o[32];
+      f2 o[H];
       if (act) {
         const float* q0 = S.co + off;
-        f2 t[32];
+        f2 t[H];
 #pragma unroll
-        for (int j = 0; j < 32; j++)
-          t[j] = dct64_first(f2{q0[j * kMS], q0[j * kMS + 32]},
-                             f2{q0[(63 - j) * kMS], q0[(63 - j) * kMS + 32]}, j, h);
-        dct64_rest(t, h, [&](int k, f2 u) { o[k] = u; });
+        for (int j = 0; j < H; j++)
+          t[j] = dctN_first<R>(f2{q0[j * kMS], q0[j * kMS + 32]},
+                               f2{q0[(R - 1 - j) * kMS], q0[(R - 1 - j) * kMS + 32]}, j, h);
+        dctN_rest<R>(t, h, [&](int k, f2 u) { o[k] = u; });
       }
       __syncthreads();
       if (act) {
 #pragma unroll
-        for (int k = 0; k < 32; k++) {
+        for (int k = 0; k < H; k++) {
           if (okA) S.co[off + (2 * k + h) * kMS] = o[k].x;
           if (okB) S.co[off + 32 + (2 * k + h) * kMS] = o[k].y;
         }
