@@ -49,10 +49,11 @@ constexpr int kMThreads = 256;
 #define JXG_MERGE_WPE 4  // waves per SIMD the eval kernel is register-capped for (4 WGs / CU)
 #endif
 #ifndef JXG_MERGE_WRITE_WPE
-// write: 168 VGPRs and 52 B of scratch per lane at 3 waves / SIMD; 2 (195
-// VGPRs, no scratch) measured slower: merge stage 1.85 vs 1.94 ms at 8K
-// (profiles/r05zp); 4 spills 204 B
-#define JXG_MERGE_WRITE_WPE 3
+// write: round 5 ran 3 waves / SIMD (168 VGPRs, 52 B of scratch; 2: 195
+// VGPRs, no scratch, merge stage 1.94 vs 1.85 ms, profiles/r05zp; 4: 204 B of
+// scratch).  Round 6 (the column halves): 3 -> 168 VGPRs + 8 B, 4 -> 128
+// VGPRs + 120 B, and 4 is the faster: 0.308 -> 0.301 ms (profiles/r06mw)
+#define JXG_MERGE_WRITE_WPE 4
 #endif
 constexpr int kMS = 65;  // LDS row stride (floats)
 constexpr int kMPlane = 64 * kMS;
