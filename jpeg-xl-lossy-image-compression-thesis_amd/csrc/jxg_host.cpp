@@ -980,7 +980,7 @@ static jxg_status build_front(Ctx* c, Job& J) {
     ma.iwy = c->miwy.p;
     ma.nat = c->mnat.p;
     ma.work = c->mwork.p;
-    ma.nwrite = 256 * 4 * 3;  // CUs x resident workgroups (4) x 3 rounds
+    ma.nwrite = 256 * 3 * 4;  // CUs x resident workgroups (3) x 4 rounds
   }
   // effort >= 8: the 128 / 256 px levels over the plan's pass groups
   J.big = J.max_s && P.effort >= 8;

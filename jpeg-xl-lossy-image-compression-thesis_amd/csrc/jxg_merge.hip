@@ -49,11 +49,12 @@ constexpr int kMThreads = 256;
 #define JXG_MERGE_WPE 4  // waves per SIMD the eval kernel is register-capped for (4 WGs / CU)
 #endif
 #ifndef JXG_MERGE_WRITE_WPE
-// write: round 5 ran 3 waves / SIMD (168 VGPRs, 52 B of scratch; 2: 195
-// VGPRs, no scratch, merge stage 1.94 vs 1.85 ms, profiles/r05zp; 4: 204 B of
-// scratch).  Round 6 (the column halves): 3 -> 168 VGPRs + 8 B, 4 -> 128
-// VGPRs + 120 B, and 4 is the faster: 0.308 -> 0.301 ms (profiles/r06mw)
-#define JXG_MERGE_WRITE_WPE 4
+// write: 3 waves / SIMD (168 VGPRs, 8 B of scratch since round 6's column
+// halves; 2: 195 VGPRs, no scratch, merge stage 1.94 vs 1.85 ms in round 5,
+// profiles/r05zp).  4 (128 VGPRs, 120 B = 39 spilled VGPRs, past
+// tests/test_isa_lint.py's 32) ran 0.301 vs 0.308 ms (profiles/r06mw): not
+// worth the spill traffic it hides
+#define JXG_MERGE_WRITE_WPE 3
 #endif
 constexpr int kMS = 65;  // LDS row stride (floats)
 constexpr int kMPlane = 64 * kMS;
