@@ -1908,7 +1908,10 @@ static jxg_status encode_device(Ctx* c, const uint8_t* d_rgb, uint32_t w, uint32
 // groups in flight: 8K 7 lanes x 1, 1080p 12 lanes x 4.  Every lane needs
 // its own hardware queue (GPU_MAX_HW_QUEUES > lanes, bench.py sets 16).
 // ---------------------------------------------------------------------------
-constexpr uint32_t kPipeMaxLanes = 12, kPipeMinLanes = 4, kPipeChainGroups = 3570;
+#ifndef JXG_PIPE_CHAIN_GROUPS  // (experiment builds override it: tools/build_variant.sh)
+#define JXG_PIPE_CHAIN_GROUPS 3570
+#endif
+constexpr uint32_t kPipeMaxLanes = 12, kPipeMinLanes = 4, kPipeChainGroups = JXG_PIPE_CHAIN_GROUPS;
 // Hardware queues of this process (GPU_MAX_HW_QUEUES as HIP read it at start
 // up; HIP's default is 4).  Lanes beyond queues - 1 (one is left for the
 // caller's own stream) would share a queue with another lane and serialise
