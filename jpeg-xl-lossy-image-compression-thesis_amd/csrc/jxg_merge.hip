@@ -585,7 +585,7 @@ __device__ __forceinline__ void quant_pass(const MergeArgs& a, const Pass& P, Me
       // LLF positions carry weight 0 (host tables): vq = +-0 quantizes to 0
       // and contributes nothing
       const f2 vq = rv * (f2{w[kk], w[kk + 1]} * f2{scale, scale});
-      float sqs[2];
+      float sqs[2], qfs[2];
 #pragma unroll
       for (int h = 0; h < 2; h++) {
         const float vqh = h ? vq.y : vq.x;
@@ -593,17 +593,30 @@ __device__ __forceinline__ void quant_pass(const MergeArgs& a, const Pass& P, Me
         // qa = (int)(min(av, 32767) + 0.5) as an integer-valued float (the
         // truncation of a positive value is its floor): no conversions
         // needed for the error and the rate
-        const float qf = av < 0.58f ? 0.0f : floorf(fminf(av, 32767.0f) + 0.5f);
-        sqs[h] = __builtin_copysignf(qf, vqh);
-        if (CH == 1) {
-          const int qa = (int)qf;
-          float adj = S.btab[min(qa, 255)];
-          if (__builtin_expect(__any(qa >= 256), 0)) {
-            if (qa >= 256) adj = qf - 0.145f / qf;
-          }
-          adj = __builtin_copysignf(adj, vqh);  // (vq = -0: a -0 that no result sees; jxg_front.hip)
-          cplane[(ky + h) * kMS] = adj * iw[kk + h];  // LLF: 0 (its value lives in llf_at)
+        qfs[h] = av < 0.58f ? 0.0f : floorf(fminf(av, 32767.0f) + 0.5f);
+        sqs[h] = __builtin_copysignf(qfs[h], vqh);
+      }
+      if (CH == 1) {
+        // AdjustQuantBias from the table below 256; one wave vote per row pair
+        // for the (rare) larger magnitudes
+        float adj[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) adj[h] = S.btab[min((int)qfs[h], 255)];
+        if (__builtin_expect(__any(fmaxf(qfs[0], qfs[1]) >= 256.0f), 0)) {
+#pragma unroll
+          for (int h = 0; h < 2; h++)
+            if (qfs[h] >= 256.0f) adj[h] = qfs[h] - 0.145f / qfs[h];
         }
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          // (vq = -0: a -0 that no result sees; jxg_front.hip)
+          const float a1 = __builtin_copysignf(adj[h], h ? vq.y : vq.x);
+          cplane[(ky + h) * kMS] = a1 * iw[kk + h];  // LLF: 0 (its value lives in llf_at)
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const float qf = qfs[h];
         // 2 + 2 bitlen(qa) per non-zero = 2 E - 250, E = biased exponent of
         // qf (qf = 0 has E = 0 and is not counted in nzc)
         eb8[kk >= 8] += __float_as_uint(qf) >> 23;
